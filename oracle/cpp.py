@@ -1,0 +1,120 @@
+"""ctypes wrapper of oracle/trie_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ (parity checker) and bench.py's cpu_baseline leg.  Build with
+``make -C oracle`` (done by ``__graft_entry__.build()``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            raise RuntimeError("oracle not built: run `make -C oracle`")
+        L = ctypes.CDLL(_LIB)
+        vp, u64p, u32p, u8p = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p
+        L.orc_create.restype = vp
+        L.orc_create.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_destroy.argtypes = [vp]
+        L.orc_add.argtypes = [vp, u8p, u64p, ctypes.c_uint64, u32p]
+        L.orc_delete.argtypes = [vp, u8p, u64p, ctypes.c_uint64]
+        L.orc_freeze.argtypes = [vp]
+        L.orc_num_keys.restype = ctypes.c_uint64
+        L.orc_num_keys.argtypes = [vp]
+        L.orc_match.restype = ctypes.c_uint64
+        L.orc_match.argtypes = [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                u32p, u32p, ctypes.c_uint32]
+        L.orc_evals.argtypes = [vp, u8p, u64p, ctypes.c_uint64, u64p]
+        L.orc_topic_match.restype = ctypes.c_int
+        L.orc_topic_match.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64]
+        _lib = L
+    return _lib
+
+
+def pack(strs: Sequence[bytes]):
+    """bytes list -> (uint8 buffer, uint64 offsets[n+1])."""
+    offs = np.zeros(len(strs) + 1, dtype=np.uint64)
+    if strs:
+        offs[1:] = np.cumsum([len(s) for s in strs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(strs), dtype=np.uint8) if strs else np.zeros(1, np.uint8)
+    if buf.size == 0:
+        buf = np.zeros(1, np.uint8)
+    return np.ascontiguousarray(buf), offs
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+MODE_ROUTES = 0
+MODE_TRIE = 1
+
+
+class CppOracle:
+    """compact: broker.perf.trie_compaction; trie_all: insert exact filters into the
+    trie too (emqx_trie_SUITE style) instead of the router's wildcard-only trie."""
+
+    def __init__(self, compact: bool = True, trie_all: bool = False):
+        self.h = lib().orc_create(int(compact), int(trie_all))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    def add_packed(self, buf, offs):
+        n = len(offs) - 1
+        ids = np.zeros(max(n, 1), dtype=np.uint32)
+        lib().orc_add(self.h, _p(buf), _p(offs), n, _p(ids))
+        return ids[:n]
+
+    def add(self, filters: Sequence[bytes]):
+        return self.add_packed(*pack(list(filters)))
+
+    def delete(self, filters: Sequence[bytes]):
+        buf, offs = pack(list(filters))
+        lib().orc_delete(self.h, _p(buf), _p(offs), len(filters))
+
+    def freeze(self):
+        lib().orc_freeze(self.h)
+
+    def num_keys(self) -> int:
+        return int(lib().orc_num_keys(self.h))
+
+    def match_packed(self, buf, offs, mode=MODE_ROUTES, threads=1, stride=64, want_ids=True):
+        n = len(offs) - 1
+        counts = np.zeros(max(n, 1), dtype=np.uint32)
+        ids = np.zeros(max(n * stride, 1), dtype=np.uint32) if want_ids else None
+        lookups = lib().orc_match(self.h, _p(buf), _p(offs), n, mode, threads, _p(counts),
+                                  _p(ids) if want_ids else None, stride)
+        return counts[:n], (ids[: n * stride].reshape(n, stride) if want_ids else None), int(lookups)
+
+    def match_lists(self, topics: Sequence[bytes], mode=MODE_ROUTES, threads=1, stride=256):
+        buf, offs = pack(list(topics))
+        counts, ids, _ = self.match_packed(buf, offs, mode, threads, stride)
+        if counts.size and int(counts.max(initial=0)) > stride:
+            return self.match_lists(topics, mode, threads, int(counts.max()) + 1)
+        return [ids[i, : counts[i]].tolist() for i in range(len(topics))]
+
+    def evals_packed(self, buf, offs):
+        n = len(offs) - 1
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        lib().orc_evals(self.h, _p(buf), _p(offs), n, _p(out))
+        return out[:n]
+
+
+def topic_match(name: bytes, filt: bytes) -> bool:
+    nb = np.frombuffer(name or b"\0", np.uint8)
+    fb = np.frombuffer(filt or b"\0", np.uint8)
+    return bool(lib().orc_topic_match(_p(nb), len(name), _p(fb), len(filt)))
