@@ -1,0 +1,198 @@
+"""Benchmark: published topics matched/s (and match evals/s) at 10M subscriptions.
+
+Workload (BASELINE.json configs[1], SURVEY §8 d config B): 10M distinct mixed exact/'+'/'#'
+filters (depth 4-8, Zipf vocab), batches of 1M published topics (depth 4-8, 50% instantiated
+from filters).  A step = one batched match (emqx_match_batch_device) of one batch already
+resident in HBM -> CSR of matching filter ids in HBM (kernels, scan, scatter, the per-call
+host readback included).
+
+Multi-GPU (``torchrun --nproc-per-node N``): the table is REPLICATED on every GPU (10M
+filters = a few GB, SURVEY §8 e) and each rank matches its own batch — weak scaling, no
+collective on the data path; one barrier + a MAX of the per-rank time brackets the timed
+region.
+
+Prints ONE JSON line (rank 0).  Extra keys: evals_per_s, roofline (HBM, algorithmic bytes of
+the fused match kernel per launch ÷ its HIP-event duration), cpu_baseline (the oracle's C++
+restatement of emqx_trie's compact DFS, timed on host cores on a bounded topic sample).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-filters", type=int, default=10_000_000)
+    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--mode", type=int, default=0, help="0 routes, 1 trie, 2 trie_wildcard")
+    ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics in the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per kernel launch from PMC (rocprofv3 FETCH_SIZE/WRITE_SIZE)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+
+    t0 = time.time()
+    # every rank replicates the table (seed 2); each rank draws its own topic stream (weak scaling)
+    wl = W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
+                    topic_seed=None if rank == 0 else 1000 + rank)
+    log(f"[rank {rank}] workload: {wl.n_filters} filters, {wl.n_topics} topics ({time.time() - t0:.1f}s)")
+
+    t0 = time.time()
+    eng = Engine(local)
+    eng.insert_packed(*wl.filters)
+    eng.commit()
+    st = eng.stats()
+    log(f"[rank {rank}] table: {st['n_nodes']} nodes, {st['n_slots']} slots, {st['n_words']} words, "
+        f"{st['table_bytes'] / 1e9:.2f} GB, build {st['last_build_ms'] / 1e3:.1f}s ({time.time() - t0:.1f}s)")
+
+    tb = torch.from_numpy(wl.topics[0]).to(dev)
+    to = torch.from_numpy(wl.topics[1].view(np.int64)).to(dev)
+    n = wl.n_topics
+    d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    cap = max(64 * n, 1 << 20)
+    d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        return eng.match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
+                                mode=args.mode, stream=stream)
+
+    nout = 0
+    for _ in range(args.warmup):
+        nout = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern_ms, call_ms = [], []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        nout = step()
+        s = eng.stats()
+        kern_ms.append(s["last_kernel_ms"])
+        call_ms.append(s["last_match_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    evals = eng.stats()["last_evals"]
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = torch.tensor([float(evals), float(nout)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        evals_all, nout_all = float(tot[0].item()), float(tot[1].item())
+    else:
+        evals_all, nout_all = float(evals), float(nout)
+
+    topics_total = float(n) * world * args.steps
+    value = topics_total / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # roofline of the fused match kernel (rank 0's launch): algorithmic bytes / kernel time
+    offs = wl.topics[1].astype(np.int64)
+    tbytes = int(offs[-1] - offs[0])
+    levels = int(np.count_nonzero(wl.topics[0][: tbytes] == ord("/"))) + n
+    alg_bytes = tbytes + 64 * levels + 64 * evals + 4 * (nout + n)
+    kms = float(np.mean(kern_ms)) if kern_ms else float("nan")
+    achieved = alg_bytes / (kms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": args.traffic_bytes, "kernel": "match_fast_kernel",
+                "kernel_ms_avg": round(kms, 4), "alg_bytes_per_launch": alg_bytes,
+                "alg_bytes_model": "len(T) + 64*L(T) + 64*evals(T) + 4*(|M(T)|+1) per topic (SURVEY §8 d)"}
+
+    result = {
+        "metric": "published topics matched/sec (and match evals/sec) at 10M subs; % of HBM BW",
+        "value": round(value, 1),
+        "unit": "topics/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "B: 10M mixed exact/'+'/'#' subscriptions, 1xMI355X, batched topics of depth 4-8",
+                   "n_filters": wl.n_filters, "batch_topics_per_gpu": n, "mode": ["routes", "trie", "trie_wildcard"][args.mode],
+                   "parallelism": f"replicated table, topic stream split x{world}"},
+        "evals_per_s": round(evals_all * args.steps / elapsed, 1),
+        "matches_per_topic": round(nout_all / (n * world), 3),
+        "evals_per_topic": round(evals_all / (n * world), 3),
+        "call_ms_avg": round(float(np.mean(call_ms)), 4),
+        "roofline": roofline,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(wl, args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(wl, args):
+    """emqx_trie compact-mode DFS (oracle/trie_oracle.cpp) + emqx_router exact union, timed on
+    a bounded sample of the same batch with one thread per core (kind "port": Erlang is absent
+    on the GPU box)."""
+    from emqx_amd import workloads as W
+    from oracle import cpp as C
+    t0 = time.time()
+    o = C.CppOracle(True)
+    o.add_packed(*wl.filters)
+    o.freeze()
+    build_s = time.time() - t0
+    sample = min(args.cpu_sample, wl.n_topics)
+    s = W.take(wl.topics, np.arange(sample))
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    counts, _, lookups = o.match_packed(*s, mode=args.mode, threads=threads, want_ids=False)
+    dt = time.perf_counter() - t0
+    log(f"cpu baseline: {sample} topics in {dt:.2f}s on {threads} threads (table build {build_s:.1f}s)")
+    return {"value": round(sample / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
+            "sample": f"first {sample} topics of the batch vs the full {wl.n_filters}-filter table",
+            "ets_lookups_per_topic": round(lookups / sample, 2),
+            "matches_per_topic": round(float(np.mean(counts)), 3)}
+
+
+if __name__ == "__main__":
+    main()

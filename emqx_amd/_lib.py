@@ -1,0 +1,112 @@
+"""Loader for the engine's C ABI (include/emqx_match.h -> emqx_amd/_build/libemqxmatch.so).
+
+The library is built in-tree (``make -C emqx_amd/csrc`` / ``__graft_entry__.build()``).
+There is no fallback: if the library is missing this raises, and every match call runs
+on the HIP device or fails with ``EngineError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libemqxmatch.so")
+
+EMQX_OK = 0
+EMQX_EINVAL = -1
+EMQX_ENOMEM = -2
+EMQX_EDEVICE = -3
+EMQX_EOVERFLOW = -4
+EMQX_ENOTFOUND = -5
+EMQX_ETOODEEP = -6
+
+MODE_ROUTES = 0
+MODE_TRIE = 1
+MODE_TRIE_WILDCARD = 2
+
+# Every symbol include/emqx_match.h declares (checked by tests/test_abi_cpu.py).
+EXPORTS = (
+    "emqx_engine_create", "emqx_engine_destroy", "emqx_insert_filters", "emqx_delete_filters",
+    "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
+    "emqx_match_batch_device", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
+    "emqx_strerror", "emqx_version",
+)
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = lib().emqx_strerror(code).decode(errors="replace")
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+class EngineOpts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("n_filters", ctypes.c_uint64), ("n_ids", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64),
+        ("n_slots", ctypes.c_uint64), ("n_words", ctypes.c_uint64), ("table_bytes", ctypes.c_uint64),
+        ("epoch", ctypes.c_uint64), ("last_evals", ctypes.c_uint64), ("last_deferred", ctypes.c_uint64),
+        ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double),
+        ("last_kernel_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Loads libemqxmatch.so (once).  If torch is already imported its HIP runtime
+    (same soname) is reused, so device pointers from torch tensors are valid here."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not built; run `make -C emqx_amd/csrc` or __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "emqx_engine_create": (i32, [ctypes.POINTER(EngineOpts), ctypes.POINTER(vp)]),
+        "emqx_engine_destroy": (i32, [vp]),
+        "emqx_insert_filters": (i32, [vp, vp, vp, u64, vp]),
+        "emqx_delete_filters": (i32, [vp, vp, u64]),
+        "emqx_lookup_filter": (i32, [vp, vp, u64, ctypes.POINTER(u32)]),
+        "emqx_filter_name": (i32, [vp, u32, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_commit": (i32, [vp]),
+        "emqx_match_batch": (i32, [vp, u32, vp, vp, u64, vp, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_match_batch_device": (i32, [vp, u32, vp, vp, u64, vp, vp, u64, ctypes.POINTER(u64), vp]),
+        "emqx_stats_get": (i32, [vp, ctypes.POINTER(Stats)]),
+        "emqx_topic_match": (i32, [vp, u64, vp, u64]),
+        "emqx_topic_wildcard": (i32, [vp, u64]),
+        "emqx_strerror": (ctypes.c_char_p, [i32]),
+        "emqx_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> int:
+    if rc != EMQX_OK:
+        raise EngineError(rc, what)
+    return rc
+
+
+def loaded_path() -> str:
+    return LIB_PATH if _lib is not None else ""
+
+
+if __name__ == "__main__":  # pragma: no cover
+    print(lib().emqx_version().decode())
+    sys.exit(0)

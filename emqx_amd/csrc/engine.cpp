@@ -1,0 +1,592 @@
+// C ABI implementation (include/emqx_match.h): filter store, snapshot build/upload with an
+// RCU-style epoch swap, per-call workspaces, and the match pipeline
+//   fast kernel -> deep kernel -> scan -> [one small D2H readback] -> scatter.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/emqx_match.h"
+#include "kernels.h"
+#include "tables.h"
+
+using namespace emqx;
+
+namespace {
+
+#define HIP_TRY(expr)                    \
+  do {                                   \
+    hipError_t _e = (expr);              \
+    if (_e != hipSuccess) {              \
+      set_last_error(hipGetErrorString(_e)); \
+      return EMQX_EDEVICE;               \
+    }                                    \
+  } while (0)
+
+thread_local std::string g_last_error;
+void set_last_error(const char* s) { g_last_error = s ? s : ""; }
+
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+template <class T>
+hipError_t dalloc(T*& p, uint64_t count) {
+  dfree(p);
+  return hipMalloc(reinterpret_cast<void**>(&p), std::max<uint64_t>(count, 1) * sizeof(T));
+}
+
+struct Snapshot {
+  int device = 0;
+  EdgeSlot* edges = nullptr;
+  NodeFids* fids = nullptr;
+  VocabSlot* vocab = nullptr;
+  uint8_t* arena = nullptr;
+  TableView tv{};
+  uint64_t n_nodes = 0, n_slots = 0, n_words = 0, bytes = 0;
+  uint32_t max_depth = 0;
+  ~Snapshot() {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    dfree(edges);
+    dfree(fids);
+    dfree(vocab);
+    dfree(arena);
+    (void)hipSetDevice(cur);
+  }
+};
+
+constexpr uint32_t DEEP_WAVES = 32;
+
+struct Workspace {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evk = nullptr;
+  uint64_t cap_n = 0, cap_tiles = 0, cap_partials = 0, cap_slab = 0;
+  uint32_t slab_per_tile = 256;
+  uint32_t* counts = nullptr;
+  uint32_t* deferred = nullptr;
+  uint32_t* deep_rank = nullptr;
+  uint64_t* slab = nullptr;
+  uint32_t* tile_fill = nullptr;
+  uint64_t* tile_defer = nullptr;
+  uint32_t* tile_evals = nullptr;
+  uint64_t* partials = nullptr;
+  uint32_t* ctrl = nullptr;         // CTRL_WORDS u32 + 2 u64 (evals) -> 8 u32 words + 2 u64
+  uint64_t* evals = nullptr;        // [0] total evals (device reduction)
+  uint32_t* deep_wids = nullptr;
+  uint4* deep_stack = nullptr;
+  uint32_t deep_stack_cap = 1u << 16;
+  uint64_t* deep_slab = nullptr;
+  uint32_t deep_slab_cap = 1u << 20;
+  uint32_t* deep_evals = nullptr;
+  // host-API staging
+  uint8_t* d_tbytes = nullptr;
+  uint64_t cap_tbytes = 0;
+  uint64_t* d_toffs = nullptr;
+  uint64_t cap_toffs = 0;
+  uint64_t* d_out_off = nullptr;
+  uint64_t cap_out_off = 0;
+  uint32_t* d_out_ids = nullptr;
+  uint64_t cap_out_ids = 0;
+  uint64_t* h_rb = nullptr;         // pinned readback: [0..3] ctrl (as u64), [4] total, [5] evals
+  bool deep_ready = false;
+
+  ~Workspace() {
+    (void)hipSetDevice(device);
+    dfree(counts); dfree(deferred); dfree(deep_rank); dfree(slab); dfree(tile_fill);
+    dfree(tile_defer); dfree(tile_evals); dfree(partials); dfree(ctrl); dfree(evals);
+    dfree(deep_wids); dfree(deep_stack); dfree(deep_slab); dfree(deep_evals);
+    dfree(d_tbytes); dfree(d_toffs); dfree(d_out_off); dfree(d_out_ids);
+    if (h_rb) (void)hipHostFree(h_rb);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (evk) (void)hipEventDestroy(evk);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+uint64_t round_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+struct emqx_engine {
+  int device = 0;
+  std::mutex writer;
+  FilterStore store;
+  uint64_t epoch = 0;
+  double last_build_ms = 0;
+  std::mutex snap_mu;
+  std::shared_ptr<Snapshot> snap;
+  std::mutex ws_mu;
+  std::vector<std::unique_ptr<Workspace>> all_ws;
+  std::vector<Workspace*> free_ws;
+  std::atomic<uint64_t> last_evals{0}, last_deferred{0};
+  std::atomic<double> last_match_ms{0};
+  std::atomic<double> last_kernel_ms{0};
+};
+
+namespace {
+
+int upload(emqx_engine* e, const HostTables& ht, std::shared_ptr<Snapshot>* out) {
+  auto s = std::make_shared<Snapshot>();
+  s->device = e->device;
+  HIP_TRY(dalloc(s->edges, ht.edges.size()));
+  HIP_TRY(dalloc(s->fids, ht.fids.size()));
+  HIP_TRY(dalloc(s->vocab, ht.vocab.size()));
+  HIP_TRY(dalloc(s->arena, ht.arena.size() + 16));
+  HIP_TRY(hipMemcpy(s->edges, ht.edges.data(), ht.edges.size() * sizeof(EdgeSlot), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->fids, ht.fids.data(), ht.fids.size() * sizeof(NodeFids), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
+  s->tv.edges = s->edges;
+  s->tv.fids = s->fids;
+  s->tv.vocab = s->vocab;
+  s->tv.arena = s->arena;
+  s->tv.vocab_mask = ht.vocab_mask;
+  s->tv.root_base = ht.root_base;
+  s->tv.root_meta = ht.root_meta;
+  s->tv.root_node = 0;
+  s->n_nodes = ht.n_nodes;
+  s->n_slots = ht.edges.size();
+  s->n_words = ht.n_words;
+  s->max_depth = ht.max_depth;
+  s->bytes = ht.edges.size() * sizeof(EdgeSlot) + ht.fids.size() * sizeof(NodeFids) +
+             ht.vocab.size() * sizeof(VocabSlot) + ht.arena.size();
+  *out = std::move(s);
+  return EMQX_OK;
+}
+
+int commit_locked(emqx_engine* e) {
+  auto t0 = std::chrono::steady_clock::now();
+  HostTables ht;
+  std::string err;
+  if (!build_tables(e->store, ht, &err)) {
+    set_last_error(err.c_str());
+    return EMQX_ENOMEM;
+  }
+  std::shared_ptr<Snapshot> s;
+  int rc = upload(e, ht, &s);
+  if (rc != EMQX_OK) return rc;
+  {
+    std::lock_guard<std::mutex> g(e->snap_mu);
+    e->snap = std::move(s);  // old snapshot freed when its last reader returns
+  }
+  e->epoch += 1;
+  e->last_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return EMQX_OK;
+}
+
+Workspace* acquire_ws(emqx_engine* e) {
+  std::lock_guard<std::mutex> g(e->ws_mu);
+  if (!e->free_ws.empty()) {
+    Workspace* w = e->free_ws.back();
+    e->free_ws.pop_back();
+    return w;
+  }
+  auto w = std::make_unique<Workspace>();
+  w->device = e->device;
+  Workspace* p = w.get();
+  e->all_ws.push_back(std::move(w));
+  return p;
+}
+
+void release_ws(emqx_engine* e, Workspace* w) {
+  std::lock_guard<std::mutex> g(e->ws_mu);
+  e->free_ws.push_back(w);
+}
+
+int ensure_ws(Workspace* w, uint64_t n) {
+  if (!w->stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&w->ev0));
+    HIP_TRY(hipEventCreate(&w->ev1));
+    HIP_TRY(hipEventCreate(&w->evk));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_rb), 16 * sizeof(uint64_t), hipHostMallocDefault));
+    HIP_TRY(dalloc(w->ctrl, 16));
+    HIP_TRY(dalloc(w->evals, 2));
+  }
+  if (!w->deep_ready) {
+    HIP_TRY(dalloc(w->deep_wids, uint64_t(DEEP_WAVES) * DEEP_MAX_LEVELS));
+    HIP_TRY(dalloc(w->deep_stack, uint64_t(DEEP_WAVES) * w->deep_stack_cap));
+    HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
+    HIP_TRY(dalloc(w->deep_evals, 4));
+    w->deep_ready = true;
+  }
+  if (n > w->cap_n) {
+    const uint64_t cap = round_pow2(std::max<uint64_t>(n, 1024));
+    HIP_TRY(dalloc(w->counts, cap));
+    HIP_TRY(dalloc(w->deferred, cap));
+    HIP_TRY(dalloc(w->deep_rank, cap));
+    w->cap_n = cap;
+  }
+  const uint64_t ntiles = (n + TILE_TOPICS - 1) / TILE_TOPICS;
+  if (ntiles > w->cap_tiles || w->cap_tiles == 0) {
+    const uint64_t cap = round_pow2(std::max<uint64_t>(ntiles, 64));
+    HIP_TRY(dalloc(w->tile_fill, cap));
+    HIP_TRY(dalloc(w->tile_defer, cap));
+    HIP_TRY(dalloc(w->tile_evals, cap));
+    w->cap_tiles = cap;
+  }
+  const uint64_t need_slab = std::max<uint64_t>(ntiles, 1) * w->slab_per_tile;
+  if (need_slab > w->cap_slab) {
+    const uint64_t cap = round_pow2(need_slab);
+    HIP_TRY(dalloc(w->slab, cap));
+    w->cap_slab = cap;
+  }
+  const uint64_t np = scan_partials(n);
+  if (np > w->cap_partials) {
+    const uint64_t cap = round_pow2(std::max<uint64_t>(np, 64));
+    HIP_TRY(dalloc(w->partials, cap));
+    w->cap_partials = cap;
+  }
+  return EMQX_OK;
+}
+
+__global__ void reduce_evals_kernel(const uint32_t* tile_evals, uint64_t ntiles, const uint32_t* deep_evals,
+                                    uint64_t* out) {
+  uint64_t s = 0;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntiles; i += uint64_t(gridDim.x) * blockDim.x)
+    s += tile_evals[i];
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(s), d, 64);
+    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(s >> 32), d, 64);
+    s += (uint64_t(hi) << 32) | lo;
+  }
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(out), static_cast<unsigned long long>(s));
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out), static_cast<unsigned long long>(*deep_evals));
+}
+
+// The pipeline on device buffers.  All inputs/outputs are device pointers.
+int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode, const uint8_t* d_tbytes,
+              const uint64_t* d_toffs, uint64_t n, uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap,
+              uint64_t* n_out, hipStream_t s) {
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    int rc = ensure_ws(w, n);
+    if (rc != EMQX_OK) return rc;
+    MatchArgs a{};
+    a.tv = snap.tv;
+    a.tbytes = d_tbytes;
+    a.toffs = d_toffs;
+    a.n = n;
+    a.mode = mode;
+    a.slab_cap = w->slab_per_tile;
+    a.counts = w->counts;
+    a.slab = w->slab;
+    a.tile_fill = w->tile_fill;
+    a.tile_defer = w->tile_defer;
+    a.tile_evals = w->tile_evals;
+    a.ctrl = w->ctrl;
+    a.deferred = w->deferred;
+    a.deep_wids = w->deep_wids;
+    a.deep_stack = w->deep_stack;
+    a.deep_stack_cap = w->deep_stack_cap;
+    a.deep_waves = DEEP_WAVES;
+    a.deep_slab = w->deep_slab;
+    a.deep_slab_cap = w->deep_slab_cap;
+    a.deep_evals = w->deep_evals;
+
+    HIP_TRY(hipMemsetAsync(w->ctrl, 0, 16 * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(w->evals, 0, 2 * sizeof(uint64_t), s));
+    HIP_TRY(hipMemsetAsync(w->deep_evals, 0, 4 * sizeof(uint32_t), s));
+    HIP_TRY(hipEventRecord(w->ev0, s));
+    const FastVariant v = snap.max_depth > 14 ? FAST_STACK_2K : FAST_STACK_1K;
+    HIP_TRY(launch_match_fast(a, v, s));
+    HIP_TRY(hipEventRecord(w->evk, s));
+    HIP_TRY(launch_match_deep(a, s));
+    HIP_TRY(launch_scan(w->counts, n, d_out_off, w->partials, s));
+    const uint64_t ntiles = (n + TILE_TOPICS - 1) / TILE_TOPICS;
+    hipLaunchKernelGGL(reduce_evals_kernel, dim3(64), dim3(256), 0, s, w->tile_evals, ntiles, w->deep_evals, w->evals);
+    HIP_TRY(hipGetLastError());
+    // one small readback: ctrl words, total, evals
+    HIP_TRY(hipMemcpyAsync(w->h_rb, w->ctrl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(w->h_rb + 4, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(w->h_rb + 5, w->evals, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(w->h_rb);
+    const uint32_t ndef = c32[CTRL_DEFERRED], need_slab = c32[CTRL_NEED_SLAB], err = c32[CTRL_ERROR];
+    const uint32_t deep_fill = c32[CTRL_DEEP_FILL];
+    if (err & CTRL_ERR_TOO_LONG) {
+      set_last_error("topic longer than 65535 bytes on the deep path");
+      return EMQX_EINVAL;
+    }
+    bool retry = false;
+    if (need_slab > w->slab_per_tile) {
+      w->slab_per_tile = static_cast<uint32_t>(round_pow2(need_slab));
+      retry = true;
+    }
+    if (err & CTRL_ERR_DEEP_SLAB) {
+      w->deep_slab_cap = static_cast<uint32_t>(std::min<uint64_t>(round_pow2(uint64_t(deep_fill) + 1), 1u << 30));
+      HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
+      retry = true;
+    }
+    if (err & CTRL_ERR_TOO_DEEP) {
+      if (w->deep_stack_cap >= (1u << 22)) {
+        set_last_error("topic frontier exceeds the deep path's stack");
+        return EMQX_ETOODEEP;
+      }
+      w->deep_stack_cap <<= 2;
+      HIP_TRY(dalloc(w->deep_stack, uint64_t(DEEP_WAVES) * w->deep_stack_cap));
+      retry = true;
+    }
+    if (retry) continue;
+    {
+      float kms = 0;
+      if (hipEventElapsedTime(&kms, w->ev0, w->evk) == hipSuccess) e->last_kernel_ms.store(kms);
+    }
+    e->last_deferred.store(ndef);
+    e->last_evals.store(w->h_rb[5]);
+    float ms = 0;
+    (void)hipEventRecord(w->ev1, s);
+    const uint64_t total = w->h_rb[4];
+    *n_out = total;
+    if (total > cap) return EMQX_EOVERFLOW;
+    HIP_TRY(launch_scatter(a, d_out_off, d_out_ids, w->deep_rank, s));
+    HIP_TRY(hipEventRecord(w->ev1, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (hipEventElapsedTime(&ms, w->ev0, w->ev1) == hipSuccess) e->last_match_ms.store(ms);
+    return EMQX_OK;
+  }
+  set_last_error("match did not converge");
+  return EMQX_EDEVICE;
+}
+
+std::shared_ptr<Snapshot> current(emqx_engine* e) {
+  std::lock_guard<std::mutex> g(e->snap_mu);
+  return e->snap;
+}
+
+bool offsets_ok(const uint64_t* offs, uint64_t n) {
+  if (!offs) return n == 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (offs[i + 1] < offs[i]) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int emqx_engine_create(const emqx_engine_opts* opts, emqx_engine** out) {
+  if (!out) return EMQX_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_last_error("no HIP device");
+    return EMQX_EDEVICE;
+  }
+  int dev = 0;
+  if (opts && opts->device >= 0) dev = opts->device;
+  else (void)hipGetDevice(&dev);
+  if (dev >= ndev) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(dev));
+  auto* e = new (std::nothrow) emqx_engine();
+  if (!e) return EMQX_ENOMEM;
+  e->device = dev;
+  int rc = commit_locked(e);  // empty snapshot
+  if (rc != EMQX_OK) {
+    delete e;
+    return rc;
+  }
+  e->epoch = 0;
+  *out = e;
+  return EMQX_OK;
+}
+
+int emqx_engine_destroy(emqx_engine* e) {
+  if (!e) return EMQX_EINVAL;
+  (void)hipSetDevice(e->device);
+  delete e;
+  return EMQX_OK;
+}
+
+int emqx_insert_filters(emqx_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                        uint32_t* ids_out) {
+  if (!e || (n && (!offsets || (!bytes && offsets[n] != offsets[0])))) return EMQX_EINVAL;
+  if (!offsets_ok(offsets, n)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(e->writer);
+  for (uint64_t i = 0; i < n; ++i) {
+    bool created = false;
+    const uint32_t id = e->store.insert(bytes + offsets[i], offsets[i + 1] - offsets[i], &created);
+    if (ids_out) ids_out[i] = id;
+  }
+  return EMQX_OK;
+}
+
+int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n) {
+  if (!e || (n && !ids)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(e->writer);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (ids[i] >= e->store.n_ids()) return EMQX_ENOTFOUND;
+    if (e->store.live[ids[i]]) {
+      e->store.live[ids[i]] = 0;
+      e->store.n_live -= 1;
+    }
+  }
+  return EMQX_OK;
+}
+
+int emqx_lookup_filter(emqx_engine* e, const uint8_t* bytes, uint64_t len, uint32_t* id_out) {
+  if (!e || !id_out || (len && !bytes)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(e->writer);
+  const uint32_t id = e->store.find(bytes, len);
+  if (id == WID_NONE || !e->store.live[id]) return EMQX_ENOTFOUND;
+  *id_out = id;
+  return EMQX_OK;
+}
+
+int emqx_filter_name(emqx_engine* e, uint32_t id, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+  if (!e || !len_out) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(e->writer);
+  if (id >= e->store.n_ids()) return EMQX_ENOTFOUND;
+  const uint64_t len = e->store.off[id + 1] - e->store.off[id];
+  *len_out = len;
+  if (buf && cap) std::memcpy(buf, e->store.bytes.data() + e->store.off[id], std::min(len, cap));
+  return EMQX_OK;
+}
+
+int emqx_commit(emqx_engine* e) {
+  if (!e) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  std::lock_guard<std::mutex> g(e->writer);
+  return commit_locked(e);
+}
+
+int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topic_bytes,
+                            const uint64_t* d_topic_offsets, uint64_t n, uint64_t* d_out_offsets,
+                            uint32_t* d_out_ids, uint64_t cap, uint64_t* n_out, void* stream) {
+  if (!e || !n_out || mode > EMQX_MODE_TRIE_WILDCARD) return EMQX_EINVAL;
+  if (n && (!d_topic_bytes || !d_topic_offsets)) return EMQX_EINVAL;
+  if (!d_out_offsets) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  auto snap = current(e);
+  Workspace* w = acquire_ws(e);
+  int rc = ensure_ws(w, n);
+  if (rc == EMQX_OK) {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
+    rc = run_match(e, *snap, w, mode, d_topic_bytes, d_topic_offsets, n, d_out_offsets, d_out_ids, cap, n_out, s);
+  }
+  release_ws(e, w);
+  return rc;
+}
+
+int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, const uint64_t* topic_offsets,
+                     uint64_t n, uint64_t* out_offsets, uint32_t* out_ids, uint64_t cap, uint64_t* n_out) {
+  if (!e || !n_out || !out_offsets || mode > EMQX_MODE_TRIE_WILDCARD) return EMQX_EINVAL;
+  if (n && !topic_offsets) return EMQX_EINVAL;
+  if (!offsets_ok(topic_offsets, n)) return EMQX_EINVAL;
+  const uint64_t b0 = n ? topic_offsets[0] : 0, b1 = n ? topic_offsets[n] : 0;
+  if (b1 > b0 && !topic_bytes) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  auto snap = current(e);
+  Workspace* w = acquire_ws(e);
+  int rc = ensure_ws(w, n);
+  if (rc != EMQX_OK) {
+    release_ws(e, w);
+    return rc;
+  }
+  // stage inputs (bytes rebased to 0, padded)
+  const uint64_t nbytes = b1 - b0;
+  if (nbytes + 16 > w->cap_tbytes) {
+    w->cap_tbytes = round_pow2(nbytes + 16);
+    if (dalloc(w->d_tbytes, w->cap_tbytes) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
+  }
+  if (n + 1 > w->cap_toffs) {
+    w->cap_toffs = round_pow2(n + 1);
+    if (dalloc(w->d_toffs, w->cap_toffs) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
+  }
+  if (n + 1 > w->cap_out_off) {
+    w->cap_out_off = round_pow2(n + 1);
+    if (dalloc(w->d_out_off, w->cap_out_off) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
+  }
+  std::vector<uint64_t> rebased(n + 1);
+  for (uint64_t i = 0; i <= n; ++i) rebased[i] = n ? topic_offsets[i] - b0 : 0;
+  hipStream_t s = w->stream;
+  auto fail = [&](hipError_t err) {
+    set_last_error(hipGetErrorString(err));
+    release_ws(e, w);
+    return EMQX_EDEVICE;
+  };
+  hipError_t he;
+  if (nbytes && (he = hipMemcpyAsync(w->d_tbytes, topic_bytes + b0, nbytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+    return fail(he);
+  if ((he = hipMemcpyAsync(w->d_toffs, rebased.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s)) != hipSuccess)
+    return fail(he);
+  // results: size the id buffer lazily (first pass learns the total)
+  uint64_t total = 0;
+  uint32_t* d_ids = w->d_out_ids;
+  uint64_t dcap = w->cap_out_ids;
+  rc = run_match(e, *snap, w, mode, w->d_tbytes, w->d_toffs, n, w->d_out_off, d_ids, dcap, &total, s);
+  if (rc == EMQX_EOVERFLOW && total <= cap) {
+    w->cap_out_ids = round_pow2(total + 1);
+    if (dalloc(w->d_out_ids, w->cap_out_ids) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
+    rc = run_match(e, *snap, w, mode, w->d_tbytes, w->d_toffs, n, w->d_out_off, w->d_out_ids, w->cap_out_ids,
+                   &total, s);
+  }
+  *n_out = total;
+  if (rc == EMQX_OK && total > cap) rc = EMQX_EOVERFLOW;
+  if (rc == EMQX_OK) {
+    if ((he = hipMemcpyAsync(out_offsets, w->d_out_off, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return fail(he);
+    if (total && out_ids &&
+        (he = hipMemcpyAsync(out_ids, w->d_out_ids, total * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return fail(he);
+    if ((he = hipStreamSynchronize(s)) != hipSuccess) return fail(he);
+  }
+  release_ws(e, w);
+  return rc;
+}
+
+int emqx_stats_get(emqx_engine* e, emqx_stats* out) {
+  if (!e || !out) return EMQX_EINVAL;
+  std::memset(out, 0, sizeof(*out));
+  {
+    std::lock_guard<std::mutex> g(e->writer);
+    out->n_filters = e->store.n_live;
+    out->n_ids = e->store.n_ids();
+    out->epoch = e->epoch;
+    out->last_build_ms = e->last_build_ms;
+  }
+  auto s = current(e);
+  if (s) {
+    out->n_nodes = s->n_nodes;
+    out->n_slots = s->n_slots;
+    out->n_words = s->n_words;
+    out->table_bytes = s->bytes;
+  }
+  out->last_evals = e->last_evals.load();
+  out->last_deferred = e->last_deferred.load();
+  out->last_match_ms = e->last_match_ms.load();
+  out->last_kernel_ms = e->last_kernel_ms.load();
+  return EMQX_OK;
+}
+
+const char* emqx_strerror(int code) {
+  switch (code) {
+    case EMQX_OK: return "ok";
+    case EMQX_EINVAL: return "invalid argument";
+    case EMQX_ENOMEM: return "out of memory";
+    case EMQX_EDEVICE: return g_last_error.empty() ? "device error" : g_last_error.c_str();
+    case EMQX_EOVERFLOW: return "output capacity too small";
+    case EMQX_ENOTFOUND: return "not found";
+    case EMQX_ETOODEEP: return "topic frontier too deep";
+    default: return "unknown error";
+  }
+}
+
+const char* emqx_version(void) { return "emqx-match-mi355x 0.1.0 (gfx950)"; }
+
+}  // extern "C"

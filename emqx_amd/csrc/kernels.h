@@ -1,0 +1,62 @@
+// Launch interface of the HIP kernels (match_kernels.hip), used by engine.cpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "layout.h"
+
+namespace emqx {
+
+// ctrl[] words (zeroed before every call)
+enum Ctrl : uint32_t {
+  CTRL_DEFERRED = 0,    // number of topics handed to the deep path
+  CTRL_NEED_SLAB = 1,   // max entries any tile needed (> slab_cap => rerun)
+  CTRL_ERROR = 2,       // error bits (CTRL_ERR_*)
+  CTRL_DEEP_FILL = 3,   // entries the deep path emitted
+  CTRL_WORDS = 4
+};
+constexpr uint32_t CTRL_ERR_TOO_LONG = 1u;   // deferred topic longer than 65535 bytes
+constexpr uint32_t CTRL_ERR_TOO_DEEP = 2u;   // deep-path frontier exceeded its stack
+constexpr uint32_t CTRL_ERR_DEEP_SLAB = 4u;  // deep-path slab overflow
+
+constexpr int TILE_TOPICS = 64;        // topics per wave (one per lane during tokenizing)
+constexpr uint32_t DEEP_MAX_LEVELS = 65536;
+
+struct MatchArgs {
+  TableView tv;
+  const uint8_t* tbytes;
+  const uint64_t* toffs;
+  uint64_t n;
+  uint32_t mode;
+  uint32_t slab_cap;       // entries per tile
+  uint32_t* counts;        // [n]
+  uint64_t* slab;          // [ntiles * slab_cap]  (topic_local << 32) | fid
+  uint32_t* tile_fill;     // [ntiles]
+  uint64_t* tile_defer;    // [ntiles]
+  uint32_t* tile_evals;    // [ntiles]
+  uint32_t* ctrl;          // [CTRL_WORDS]
+  uint32_t* deferred;      // [n]
+  // deep path
+  uint32_t* deep_wids;     // [deep_waves * DEEP_MAX_LEVELS]
+  uint4* deep_stack;       // [deep_waves * deep_stack_cap]
+  uint32_t deep_stack_cap;
+  uint32_t deep_waves;
+  uint64_t* deep_slab;     // [deep_slab_cap]  (deferred_slot << 32) | fid
+  uint32_t deep_slab_cap;
+  uint32_t* deep_evals;    // [1] (atomic)
+};
+
+// Which fast-kernel variant: stack capacity (items per wave).
+enum FastVariant { FAST_STACK_1K = 0, FAST_STACK_2K = 1 };
+
+hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);
+hipError_t launch_match_deep(const MatchArgs& a, hipStream_t s);
+// counts[n] -> offsets[n+1] (exclusive); partials: scratch of >= scan_partials(n) u64.
+uint64_t scan_partials(uint64_t n);
+hipError_t launch_scan(const uint32_t* counts, uint64_t n, uint64_t* offsets, uint64_t* partials,
+                       hipStream_t s);
+hipError_t launch_scatter(const MatchArgs& a, const uint64_t* offsets, uint32_t* out_ids,
+                          uint32_t* deep_rank, hipStream_t s);
+
+}  // namespace emqx

@@ -1,0 +1,91 @@
+// Device-resident table layout shared by the host builder (tables.cpp) and the HIP
+// kernels (match_kernels.hip).  See DESIGN.md §2 for the HBM layout.
+//
+// The reference stores its trie as an ETS ordered_set of joined-string keys
+// {Prefix,0}/{Topic,1} (apps/emqx/src/emqx_trie.erl:53-77) and matches by probing that
+// set once per visited prefix (emqx_trie.erl:315-334).  Here the same filter set is a
+// *level trie over interned words*:
+//
+//   * vocab:  open-addressed table  word bytes -> 32-bit word id (exact byte check)
+//   * nodes:  one per distinct filter prefix (all filters, exact and wildcard)
+//   * edges:  each node owns a power-of-two slice of one global slot array, open-
+//             addressed by word id; '+' is the reserved word WID_PLUS, a non-final '#'
+//             the reserved word WID_HASH; a final '#' is the parent's hash filter.
+//   * fids:   per node {filter "<path>/#", filter "<path>"} ids, read only on a hit.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define EMQX_HD __host__ __device__ __forceinline__
+#else
+#define EMQX_HD inline
+#endif
+
+namespace emqx {
+
+constexpr uint32_t WID_NONE = 0xFFFFFFFFu;  // unknown word / empty edge slot
+constexpr uint32_t WID_PLUS = 0xFFFFFFFEu;  // '+' level
+constexpr uint32_t WID_HASH = 0xFFFFFFFDu;  // '#' level (edge only when not final)
+constexpr uint32_t FID_NONE = 0xFFFFFFFFu;
+
+// EdgeSlot.meta bits (describe the CHILD the slot points to).
+constexpr uint32_t META_CAPLOG2_MASK = 0x1Fu;   // child's edge-array size = 1 << caplog2
+constexpr uint32_t META_HAS_PLUS = 1u << 5;     // child has a '+' edge
+constexpr uint32_t META_HAS_EDGES = 1u << 6;    // child has any edge (literal/'+'/'#')
+constexpr uint32_t META_HAS_HASH = 1u << 7;     // filter "<child path>/#" exists
+constexpr uint32_t META_HAS_TERM = 1u << 8;     // filter "<child path>" exists
+constexpr uint32_t META_TERM_WILD = 1u << 9;    // ... and that filter is a wildcard filter
+
+// 16-byte edge slot: one global_load_dwordx4 per probe, 4 slots per 64-B line.
+struct alignas(16) EdgeSlot {
+  uint32_t wid;         // key (WID_NONE = empty)
+  uint32_t child_base;  // first slot of the child's edge array
+  uint32_t meta;        // META_* of the child
+  uint32_t child;       // child node id
+};
+static_assert(sizeof(EdgeSlot) == 16, "EdgeSlot must be 16 bytes");
+
+// 32-byte vocab slot; words up to 16 bytes are verified from `inl` without a second load.
+struct alignas(16) VocabSlot {
+  uint32_t hash;   // fnv1a32 of the word bytes
+  uint32_t len;    // word length in bytes
+  uint32_t wid;    // word id (WID_NONE = empty slot)
+  uint32_t off;    // offset of the bytes in the arena
+  uint32_t inl[4]; // first 16 bytes, little-endian, zero padded
+};
+static_assert(sizeof(VocabSlot) == 32, "VocabSlot must be 32 bytes");
+
+struct NodeFids {
+  uint32_t hash_fid;  // id of "<path>/#" or FID_NONE
+  uint32_t term_fid;  // id of "<path>"   or FID_NONE
+};
+
+// Kernel-argument view of one committed snapshot.
+struct TableView {
+  const EdgeSlot* edges;
+  const NodeFids* fids;
+  const VocabSlot* vocab;
+  const uint8_t* arena;
+  uint32_t vocab_mask;
+  uint32_t root_base;
+  uint32_t root_meta;
+  uint32_t root_node;
+};
+
+EMQX_HD uint32_t fnv1a_step(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }
+constexpr uint32_t FNV_BASIS = 2166136261u;
+
+// murmur3 fmix32: spreads word ids inside a node's edge array.
+EMQX_HD uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+EMQX_HD uint32_t vocab_slot0(uint32_t hash) { return mix32(hash ^ 0x9e3779b9u); }
+
+}  // namespace emqx

@@ -1,0 +1,786 @@
+// HIP kernels for gfx950 (MI355X): batched topic -> filter-id matching.
+//
+// Replaces the reference's per-topic DFS over ETS prefix keys
+// (apps/emqx/src/emqx_trie.erl:272-334) and the exact-route union of
+// emqx_router:match_routes/1 (apps/emqx/src/emqx_router.erl:128-133).
+//
+// Structure:
+//   match_fast_kernel  one wavefront per tile of 64 published topics.
+//     phase A  the tile's topic bytes are staged into LDS with coalesced dword loads; each
+//              lane splits its topic on '/', hashes every level (FNV-1a) and interns it in
+//              the vocab table (exact byte check) -> word ids in LDS.
+//     phase B  the frontier of all 64 topics is pooled in one LDS work stack.  Each step
+//              pops up to 64 (topic, node, level) items — one per lane — probes the node's
+//              literal edge and its '+' edge (16-B slots, linear probing), emits the
+//              children's '#' and terminal filters, and pushes the children; pushes and
+//              emissions are stream-compacted with wave ballots + popcount prefix sums.
+//              The stack is LIFO, which bounds it by ~64 x levels regardless of the
+//              frontier width.  No MFMA: this is pointer chasing.
+//     phase C  per-topic counts + a per-tile slab of (topic, filter id) entries.
+//   match_deep_kernel  topics that did not fit the fast path's LDS budget (very deep
+//              topics, or a frontier that overflowed the stack): one wavefront per topic,
+//              word ids and stack in global scratch.
+//   scan / scatter     counts -> CSR offsets; slab entries -> out_ids.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace emqx {
+
+namespace {
+
+constexpr uint32_t MODE_ROUTES = 0, MODE_TRIE = 1;  // MODE_TRIE_WILDCARD = 2 is the default branch of term_ok
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
+
+// Exclusive prefix of a small per-lane value (0..7) across the wave; *total = wave sum.
+__device__ __forceinline__ uint32_t wave_prefix_small(uint32_t v, uint32_t lane, uint32_t* total) {
+  const uint64_t b0 = __ballot(v & 1u), b1 = __ballot(v & 2u), b2 = __ballot(v & 4u);
+  const uint64_t lt = lanemask_lt(lane);
+  *total = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
+  return __popcll(b0 & lt) + 2u * __popcll(b1 & lt) + 4u * __popcll(b2 & lt);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), d, 64);
+    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), d, 64);
+    v |= (static_cast<uint64_t>(hi) << 32) | lo;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint4 load_slot(const EdgeSlot* p) {
+  return *reinterpret_cast<const uint4*>(p);
+}
+
+// Term-filter emission rule per mode (see include/emqx_match.h):
+//  ROUTES          every filter ending here (exact ∪ wildcard), emqx_router.erl:128-133
+//  TRIE_WILDCARD   wildcard filters only (the router's trie), emqx_router.erl:117-123
+//  TRIE            wildcard filters, plus the one-level '$x' exact filter quirk of
+//                  emqx_trie.erl:276-277 (lookup_topic/2 without the wildcard gate)
+__device__ __forceinline__ bool term_ok(uint32_t meta, uint32_t mode, bool dollar_root_literal) {
+  if (!(meta & META_HAS_TERM)) return false;
+  if (mode == MODE_ROUTES) return true;
+  if (meta & META_TERM_WILD) return true;
+  return mode == MODE_TRIE && dollar_root_literal;
+}
+
+// Vocab lookup with exact byte verification.  w0..w3 hold the first 16 bytes of the word;
+// longer words compare the tail against the arena.  Returns WID_NONE if absent.
+template <class ByteAt>
+__device__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, uint32_t w0,
+                                uint32_t w1, uint32_t w2, uint32_t w3, uint64_t wstart,
+                                ByteAt byte_at) {
+  uint32_t i = vocab_slot0(h) & tv.vocab_mask;
+  for (uint32_t k = 0; k <= tv.vocab_mask; ++k) {
+    const uint4* vp = reinterpret_cast<const uint4*>(tv.vocab + i);
+    const uint4 hd = vp[0];  // hash, len, wid, off
+    if (hd.z == WID_NONE) return WID_NONE;
+    if (hd.x == h && hd.y == len) {
+      const uint4 in = vp[1];
+      bool eq = in.x == w0 && in.y == w1 && in.z == w2 && in.w == w3;
+      if (eq && len > 16) {
+        for (uint32_t b = 16; b < len && eq; ++b) eq = tv.arena[hd.w + b] == byte_at(wstart + b);
+      }
+      if (eq) return hd.z;
+    }
+    i = (i + 1) & tv.vocab_mask;
+  }
+  return WID_NONE;
+}
+
+// Probe one node's edge array for `wid` (bounded linear probing).
+__device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t caplog, uint32_t wid, uint4* out) {
+  const uint32_t mask = (1u << caplog) - 1u;
+  uint32_t i = mix32(wid) & mask;
+  for (uint32_t k = 0; k <= mask; ++k) {
+    const uint4 s = load_slot(arr + i);
+    if (s.x == wid) {
+      *out = s;
+      return true;
+    }
+    if (s.x == WID_NONE) return false;
+    i = (i + 1) & mask;
+  }
+  return false;
+}
+
+// Byte-identical lookup of a wildcard "topic" for match_routes (emqx_router.erl:130):
+// walks literal/'+'/'#' edges; a final '#' is the node's hash filter.  Returns the fid or
+// FID_NONE.
+template <class WidAt>
+__device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at) {
+  uint32_t base = tv.root_base, meta = tv.root_meta, node = tv.root_node;
+  for (uint32_t k = 0; k < nlev; ++k) {
+    const uint32_t w = wid_at(k);
+    if (w == WID_HASH && k + 1 == nlev) {
+      return (meta & META_HAS_HASH) ? tv.fids[node].hash_fid : FID_NONE;
+    }
+    if (w == WID_NONE || !(meta & META_HAS_EDGES)) return FID_NONE;
+    uint4 s;
+    if (!probe_one(tv.edges + base, meta & META_CAPLOG2_MASK, w, &s)) return FID_NONE;
+    base = s.y;
+    meta = s.z;
+    node = s.w;
+  }
+  return (meta & META_HAS_TERM) ? tv.fids[node].term_fid : FID_NONE;
+}
+
+// Item (8 B):  x = edge-array base of the node
+//              y = caplog2 (5) | has_plus (1) | dollar_root (1) | - (1) | topic (6) | - (2) | widx (16)
+constexpr uint32_t ITEM_DROOT = 1u << 6;
+
+__device__ __forceinline__ uint2 make_item(uint32_t base, uint32_t meta, bool droot, uint32_t tl,
+                                           uint32_t widx) {
+  return make_uint2(base, (meta & (META_CAPLOG2_MASK | META_HAS_PLUS)) | (droot ? ITEM_DROOT : 0u) |
+                              (tl << 8) | (widx << 16));
+}
+
+// One frontier step for one lane: probes literal + '+' edges of the item's node.
+struct StepOut {
+  uint4 s0, s1;  // found children (literal, plus)
+  bool f0, f1;
+};
+
+__device__ __forceinline__ void probe_pair(const EdgeSlot* arr, uint32_t caplog, bool need0,
+                                           uint32_t wid, bool need1, StepOut* o) {
+  const uint32_t mask = (1u << caplog) - 1u;
+  uint32_t i0 = mix32(wid) & mask;
+  uint32_t i1 = mix32(WID_PLUS) & mask;
+  o->f0 = o->f1 = false;
+  o->s0 = o->s1 = make_uint4(WID_NONE, 0, 0, 0);
+  for (uint32_t k = 0;; ++k) {
+    uint4 a = make_uint4(WID_NONE, 0, 0, 0), b = make_uint4(WID_NONE, 0, 0, 0);
+    if (need0) a = load_slot(arr + i0);
+    if (need1) b = load_slot(arr + i1);
+    if (need0) {
+      if (a.x == wid) {
+        o->s0 = a;
+        o->f0 = true;
+        need0 = false;
+      } else if (a.x == WID_NONE || k >= mask) {
+        need0 = false;
+      } else {
+        i0 = (i0 + 1) & mask;
+      }
+    }
+    if (need1) {
+      if (b.x == WID_PLUS) {
+        o->s1 = b;
+        o->f1 = true;
+        need1 = false;
+      } else if (b.x == WID_NONE || k >= mask) {
+        need1 = false;
+      } else {
+        i1 = (i1 + 1) & mask;
+      }
+    }
+    if (!__any(need0 || need1)) break;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// Fast path
+// ------------------------------------------------------------------------------------
+template <int WAVES, int STACK_CAP, int WID_CAP>
+__global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
+  struct WaveLds {
+    uint2 stack[STACK_CAP];  // phase A: staged topic bytes; phase B: work stack
+    uint32_t wids[WID_CAP];
+    uint32_t wend[64];
+    uint32_t cnt[64];
+  };
+  __shared__ WaveLds lds_all[WAVES];
+
+  const uint32_t lane = lane_id();
+  const uint32_t wv = threadIdx.x >> 6;
+  WaveLds& L = lds_all[wv];
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * WAVES + wv;
+  const uint64_t t0 = tile * TILE_TOPICS;
+  if (t0 >= a.n) return;  // wave-uniform; the kernel uses no block-wide barrier
+
+  const TableView& tv = a.tv;
+  const uint32_t tcount = static_cast<uint32_t>(min<uint64_t>(TILE_TOPICS, a.n - t0));
+  const bool valid = lane < tcount;
+  const uint64_t t = t0 + lane;
+  const uint64_t b0 = a.toffs[t0];
+  const uint64_t b1 = a.toffs[t0 + tcount];
+  uint64_t start = 0, end = 0;
+  if (valid) {
+    start = a.toffs[t];
+    end = a.toffs[t + 1];
+  }
+
+  // ---- phase A: stage bytes, tokenize, intern -------------------------------------
+  uint8_t* sbytes = reinterpret_cast<uint8_t*>(L.stack);
+  const uint64_t a0 = b0 & ~3ull;
+  const bool staged = ((reinterpret_cast<uintptr_t>(a.tbytes) & 3u) == 0) &&
+                      (b1 - a0) <= static_cast<uint64_t>(STACK_CAP) * 8u;
+  if (staged) {
+    const uint64_t nfull = (b1 - a0) >> 2;
+    const uint32_t* src32 = reinterpret_cast<const uint32_t*>(a.tbytes + a0);
+    uint32_t* dst32 = reinterpret_cast<uint32_t*>(sbytes);
+    for (uint64_t i = lane; i < nfull; i += 64) dst32[i] = src32[i];
+    for (uint64_t i = a0 + nfull * 4 + lane; i < b1; i += 64) sbytes[i - a0] = a.tbytes[i];
+  }
+  wave_sync();
+  auto byte_at = [&](uint64_t i) -> uint32_t {
+    return staged ? static_cast<uint32_t>(sbytes[i - a0]) : static_cast<uint32_t>(a.tbytes[i]);
+  };
+
+  uint32_t nlev = 0;
+  bool wild = false, dollar = false;
+  if (valid) {
+    nlev = 1;
+    uint32_t llen = 0, first = 0;
+    for (uint64_t i = start; i < end; ++i) {
+      const uint32_t c = byte_at(i);
+      if (c == '/') {
+        if (llen == 1 && (first == '+' || first == '#')) wild = true;
+        ++nlev;
+        llen = 0;
+      } else {
+        if (llen == 0) first = c;
+        ++llen;
+      }
+    }
+    if (llen == 1 && (first == '+' || first == '#')) wild = true;
+    dollar = end > start && byte_at(start) == '$';
+  }
+  bool defer = valid && nlev > static_cast<uint32_t>(WID_CAP / 8);
+  const uint32_t need = (valid && !defer) ? nlev : 0u;
+  const uint32_t incl = wave_incl_scan(need, lane);
+  const uint32_t wbase = incl - need;
+  if (valid && !defer && incl > static_cast<uint32_t>(WID_CAP)) defer = true;
+  uint64_t defer_mask = __ballot(defer);
+
+  if (valid && !defer) {
+    uint32_t k = 0, h = FNV_BASIS, len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    uint64_t ws = start;
+    for (uint64_t i = start; i <= end; ++i) {
+      const uint32_t c = (i < end) ? byte_at(i) : static_cast<uint32_t>('/');
+      if (c != '/') {
+        h = fnv1a_step(h, c);
+        if (len < 16) {
+          const uint32_t v = c << (8u * (len & 3u));
+          const uint32_t q = len >> 2;
+          w0 |= q == 0 ? v : 0u;
+          w1 |= q == 1 ? v : 0u;
+          w2 |= q == 2 ? v : 0u;
+          w3 |= q == 3 ? v : 0u;
+        }
+        ++len;
+      } else {
+        uint32_t wid;
+        if (len == 1 && w0 == '+') wid = WID_PLUS;
+        else if (len == 1 && w0 == '#') wid = WID_HASH;
+        else wid = intern_word(tv, h, len, w0, w1, w2, w3, ws, byte_at);
+        L.wids[wbase + k] = wid;
+        ++k;
+        h = FNV_BASIS;
+        len = 0;
+        w0 = w1 = w2 = w3 = 0;
+        ws = i + 1;
+      }
+    }
+    L.wend[lane] = wbase + nlev;
+  }
+  L.cnt[lane] = 0;
+  wave_sync();
+
+  // ---- phase B: pooled frontier walk ------------------------------------------------
+  uint64_t* slab = a.slab + tile * a.slab_cap;
+  const uint32_t cap = a.slab_cap;
+  const uint32_t mode = a.mode;
+  uint32_t cursor = 0;  // wave-uniform
+  uint32_t top = 0;     // wave-uniform
+  uint32_t evals = 0;   // per lane
+
+  auto emit = [&](uint32_t tl, bool e0, uint32_t g0, bool e1, uint32_t g1, bool e2, uint32_t g2,
+                  bool e3, uint32_t g3) {
+    const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u) + (e2 ? 1u : 0u) + (e3 ? 1u : 0u);
+    uint32_t tot;
+    uint32_t pos = cursor + wave_prefix_small(c, lane, &tot);
+    const uint64_t tag = static_cast<uint64_t>(tl) << 32;
+    if (e0) { if (pos < cap) slab[pos] = tag | g0; ++pos; }
+    if (e1) { if (pos < cap) slab[pos] = tag | g1; ++pos; }
+    if (e2) { if (pos < cap) slab[pos] = tag | g2; ++pos; }
+    if (e3) { if (pos < cap) slab[pos] = tag | g3; ++pos; }
+    if (c) atomicAdd(&L.cnt[tl], c);
+    cursor += tot;
+  };
+
+  {
+    bool e0 = false, e1 = false, push = false;
+    uint32_t g0 = 0, g1 = 0;
+    uint2 it = make_uint2(0, 0);
+    if (valid && !defer) {
+      if (wild) {
+        if (mode == MODE_ROUTES) {
+          const uint32_t f = exact_walk(tv, nlev, [&](uint32_t k) { return L.wids[wbase + k]; });
+          if (f != FID_NONE) {
+            e1 = true;
+            g1 = f;
+          }
+        }
+      } else {
+        evals = 1;  // the root visit, F_0
+        if (!dollar && (tv.root_meta & META_HAS_HASH)) {
+          e0 = true;  // filter '#'
+          g0 = tv.fids[tv.root_node].hash_fid;
+        }
+        if (tv.root_meta & META_HAS_EDGES) {
+          push = true;
+          // '$' rule (emqx_trie.erl:272-279): no root-level '+' or '#' for '$' topics
+          const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
+          it = make_item(tv.root_base, rmeta, dollar, lane, wbase);
+        }
+      }
+    }
+    emit(lane, e0, g0, e1, g1, false, 0, false, 0);
+    uint32_t ptot;
+    const uint32_t ppos = wave_prefix_small(push ? 1u : 0u, lane, &ptot);
+    if (push) L.stack[ppos] = it;
+    top = ptot;
+    wave_sync();
+  }
+
+  while (true) {
+    top = __builtin_amdgcn_readfirstlane(top);
+    if (top == 0) break;
+    const uint32_t room = static_cast<uint32_t>(STACK_CAP) - top;
+    const uint32_t nb = min(64u, min(top, room));
+    if (nb == 0) {
+      // Stack full: hand every topic still on the stack to the deep path.
+      uint64_t m = 0;
+      for (uint32_t i0 = 0; i0 < top; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        if (i < top) m |= 1ull << ((L.stack[i].y >> 8) & 63u);
+      }
+      defer_mask |= wave_or64(m);
+      top = 0;
+      break;
+    }
+    const bool act = lane < nb;
+    uint2 it = make_uint2(0, 0);
+    if (act) it = L.stack[top - nb + lane];
+    top -= nb;
+    wave_sync();
+
+    const uint32_t caplog = it.y & META_CAPLOG2_MASK;
+    const bool hp = (it.y & META_HAS_PLUS) != 0;
+    const bool droot = (it.y & ITEM_DROOT) != 0;
+    const uint32_t tl = (it.y >> 8) & 63u;
+    const uint32_t widx = it.y >> 16;
+    uint32_t wid = WID_NONE;
+    bool leaf = false;
+    if (act) {
+      wid = L.wids[widx];
+      leaf = (widx + 1 == L.wend[tl]);
+    }
+    StepOut so;
+    probe_pair(tv.edges + it.x, caplog, act && wid != WID_NONE, wid, act && hp, &so);
+    evals += (so.f0 ? 1u : 0u) + (so.f1 ? 1u : 0u);
+
+    const uint32_t m0 = so.s0.z, m1 = so.s1.z;
+    const bool eh0 = so.f0 && (m0 & META_HAS_HASH);
+    const bool et0 = so.f0 && leaf && term_ok(m0, mode, droot);
+    const bool eh1 = so.f1 && (m1 & META_HAS_HASH);
+    const bool et1 = so.f1 && leaf && term_ok(m1, mode, false);
+    NodeFids fd0{FID_NONE, FID_NONE}, fd1{FID_NONE, FID_NONE};
+    if (eh0 || et0) fd0 = tv.fids[so.s0.w];
+    if (eh1 || et1) fd1 = tv.fids[so.s1.w];
+    emit(tl, eh0, fd0.hash_fid, et0, fd0.term_fid, eh1, fd1.hash_fid, et1, fd1.term_fid);
+
+    const bool p0 = so.f0 && !leaf && (m0 & META_HAS_EDGES);
+    const bool p1 = so.f1 && !leaf && (m1 & META_HAS_EDGES);
+    uint32_t ptot;
+    const uint32_t ppos = wave_prefix_small((p0 ? 1u : 0u) + (p1 ? 1u : 0u), lane, &ptot);
+    if (p0) L.stack[top + ppos] = make_item(so.s0.y, m0, false, tl, widx + 1);
+    if (p1) L.stack[top + ppos + (p0 ? 1u : 0u)] = make_item(so.s1.y, m1, false, tl, widx + 1);
+    top += ptot;
+    wave_sync();
+  }
+
+  // ---- phase C: per-topic counts, tile bookkeeping ---------------------------------
+  wave_sync();
+  if (valid) a.counts[t] = ((defer_mask >> lane) & 1ull) ? 0u : L.cnt[lane];
+  const uint32_t ev = wave_sum(evals);
+  if (lane == 0) {
+    a.tile_fill[tile] = cursor;
+    a.tile_defer[tile] = defer_mask;
+    a.tile_evals[tile] = ev;
+    if (cursor > cap) atomicMax(&a.ctrl[CTRL_NEED_SLAB], cursor);
+  }
+  if (defer_mask) {
+    uint32_t pos0 = 0;
+    if (lane == 0) pos0 = atomicAdd(&a.ctrl[CTRL_DEFERRED], static_cast<uint32_t>(__popcll(defer_mask)));
+    pos0 = __shfl(pos0, 0, 64);
+    if ((defer_mask >> lane) & 1ull)
+      a.deferred[pos0 + __popcll(defer_mask & lanemask_lt(lane))] = static_cast<uint32_t>(t);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Deep path: one wavefront per deferred topic; word ids and stack in global scratch.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
+  const uint32_t lane = lane_id();
+  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (gw >= a.deep_waves) return;
+  const TableView& tv = a.tv;
+  const uint32_t ndef = __hip_atomic_load(&a.ctrl[CTRL_DEFERRED], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t* wids = a.deep_wids + static_cast<uint64_t>(gw) * DEEP_MAX_LEVELS;
+  uint4* stack = a.deep_stack + static_cast<uint64_t>(gw) * a.deep_stack_cap;
+  const uint32_t scap = a.deep_stack_cap;
+  const uint32_t mode = a.mode;
+
+  for (uint32_t j = gw; j < ndef; j += a.deep_waves) {
+    const uint32_t t = a.deferred[j];
+    const uint64_t start = a.toffs[t], end = a.toffs[t + 1];
+    if (end - start > 65535u) {
+      if (lane == 0) {
+        atomicOr(&a.ctrl[CTRL_ERROR], CTRL_ERR_TOO_LONG);
+        a.counts[t] = 0;
+      }
+      continue;
+    }
+    auto byte_at = [&](uint64_t i) -> uint32_t { return a.tbytes[i]; };
+    // tokenize + intern (lane 0; rare path)
+    uint32_t nlev = 0, wild = 0, dollar = 0;
+    if (lane == 0) {
+      uint32_t k = 0, h = FNV_BASIS, len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+      uint64_t ws = start;
+      for (uint64_t i = start; i <= end; ++i) {
+        const uint32_t c = (i < end) ? byte_at(i) : static_cast<uint32_t>('/');
+        if (c != '/') {
+          h = fnv1a_step(h, c);
+          if (len < 16) {
+            const uint32_t v = c << (8u * (len & 3u));
+            const uint32_t q = len >> 2;
+            w0 |= q == 0 ? v : 0u;
+            w1 |= q == 1 ? v : 0u;
+            w2 |= q == 2 ? v : 0u;
+            w3 |= q == 3 ? v : 0u;
+          }
+          ++len;
+        } else {
+          uint32_t wid;
+          if (len == 1 && w0 == '+') { wid = WID_PLUS; wild = 1; }
+          else if (len == 1 && w0 == '#') { wid = WID_HASH; wild = 1; }
+          else wid = intern_word(tv, h, len, w0, w1, w2, w3, ws, byte_at);
+          wids[k++] = wid;
+          h = FNV_BASIS;
+          len = 0;
+          w0 = w1 = w2 = w3 = 0;
+          ws = i + 1;
+        }
+      }
+      nlev = k;
+      dollar = (end > start && byte_at(start) == '$') ? 1u : 0u;
+    }
+    __threadfence_block();
+    nlev = __shfl(nlev, 0, 64);
+    wild = __shfl(wild, 0, 64);
+    dollar = __shfl(dollar, 0, 64);
+    uint32_t count = 0, evals = 0;  // wave-uniform / per-lane
+
+    auto emit = [&](bool e0, uint32_t g0, bool e1, uint32_t g1, bool e2, uint32_t g2, bool e3, uint32_t g3) {
+      const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u) + (e2 ? 1u : 0u) + (e3 ? 1u : 0u);
+      uint32_t tot;
+      const uint32_t rel = wave_prefix_small(c, lane, &tot);
+      if (tot == 0) return;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&a.ctrl[CTRL_DEEP_FILL], tot);
+      base = __shfl(base, 0, 64);
+      uint32_t pos = base + rel;
+      const uint64_t tag = static_cast<uint64_t>(j) << 32;
+      bool over = false;
+      if (e0) { if (pos < a.deep_slab_cap) a.deep_slab[pos] = tag | g0; else over = true; ++pos; }
+      if (e1) { if (pos < a.deep_slab_cap) a.deep_slab[pos] = tag | g1; else over = true; ++pos; }
+      if (e2) { if (pos < a.deep_slab_cap) a.deep_slab[pos] = tag | g2; else over = true; ++pos; }
+      if (e3) { if (pos < a.deep_slab_cap) a.deep_slab[pos] = tag | g3; else over = true; ++pos; }
+      if (over) atomicOr(&a.ctrl[CTRL_ERROR], CTRL_ERR_DEEP_SLAB);
+      count += tot;
+    };
+
+    uint32_t top = 0;
+    if (wild) {
+      if (mode == MODE_ROUTES) {
+        uint32_t f = FID_NONE;
+        if (lane == 0) f = exact_walk(tv, nlev, [&](uint32_t k) { return wids[k]; });
+        f = __shfl(f, 0, 64);
+        emit(lane == 0 && f != FID_NONE, f, false, 0, false, 0, false, 0);
+      }
+    } else {
+      if (lane == 0) evals = 1;
+      const bool eh = lane == 0 && !dollar && (tv.root_meta & META_HAS_HASH);
+      emit(eh, eh ? tv.fids[tv.root_node].hash_fid : 0u, false, 0, false, 0, false, 0);
+      if (tv.root_meta & META_HAS_EDGES) {
+        const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
+        if (lane == 0)
+          stack[0] = make_uint4(tv.root_base, (rmeta & (META_CAPLOG2_MASK | META_HAS_PLUS)) | (dollar ? ITEM_DROOT : 0u), 0u, 0u);
+        top = 1;
+      }
+    }
+    __threadfence_block();
+
+    while (top > 0) {
+      const uint32_t nb = min(64u, min(top, scap - top));
+      if (nb == 0) {
+        if (lane == 0) atomicOr(&a.ctrl[CTRL_ERROR], CTRL_ERR_TOO_DEEP);
+        break;
+      }
+      const bool act = lane < nb;
+      uint4 it = make_uint4(0, 0, 0, 0);
+      if (act) it = stack[top - nb + lane];
+      top -= nb;
+      __threadfence_block();
+      const uint32_t caplog = it.y & META_CAPLOG2_MASK;
+      const bool hp = (it.y & META_HAS_PLUS) != 0;
+      const bool droot = (it.y & ITEM_DROOT) != 0;
+      const uint32_t widx = it.z;
+      uint32_t wid = WID_NONE;
+      bool leaf = false;
+      if (act) {
+        wid = wids[widx];
+        leaf = widx + 1 == nlev;
+      }
+      StepOut so;
+      probe_pair(tv.edges + it.x, caplog, act && wid != WID_NONE, wid, act && hp, &so);
+      evals += (so.f0 ? 1u : 0u) + (so.f1 ? 1u : 0u);
+      const uint32_t m0 = so.s0.z, m1 = so.s1.z;
+      const bool eh0 = so.f0 && (m0 & META_HAS_HASH);
+      const bool et0 = so.f0 && leaf && term_ok(m0, mode, droot);
+      const bool eh1 = so.f1 && (m1 & META_HAS_HASH);
+      const bool et1 = so.f1 && leaf && term_ok(m1, mode, false);
+      NodeFids fd0{FID_NONE, FID_NONE}, fd1{FID_NONE, FID_NONE};
+      if (eh0 || et0) fd0 = tv.fids[so.s0.w];
+      if (eh1 || et1) fd1 = tv.fids[so.s1.w];
+      emit(eh0, fd0.hash_fid, et0, fd0.term_fid, eh1, fd1.hash_fid, et1, fd1.term_fid);
+      const bool p0 = so.f0 && !leaf && (m0 & META_HAS_EDGES);
+      const bool p1 = so.f1 && !leaf && (m1 & META_HAS_EDGES);
+      uint32_t ptot;
+      const uint32_t ppos = wave_prefix_small((p0 ? 1u : 0u) + (p1 ? 1u : 0u), lane, &ptot);
+      if (p0) stack[top + ppos] = make_uint4(so.s0.y, m0 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
+      if (p1) stack[top + ppos + (p0 ? 1u : 0u)] = make_uint4(so.s1.y, m1 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
+      top += ptot;
+      __threadfence_block();
+    }
+    const uint32_t ev = wave_sum(evals);
+    if (lane == 0) {
+      a.counts[t] = count;
+      atomicAdd(&a.deep_evals[0], ev);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Scan: counts[n] (u32) -> offsets[n+1] (u64, exclusive)
+// ------------------------------------------------------------------------------------
+namespace {
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t lo = __shfl_up(static_cast<uint32_t>(v), d, 64);
+    const uint32_t hi = __shfl_up(static_cast<uint32_t>(v >> 32), d, 64);
+    if (lane >= d) v += (static_cast<uint64_t>(hi) << 32) | lo;
+  }
+  return v;
+}
+
+// Block-wide exclusive scan of one u64 per thread (SCAN_THREADS threads).
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t wsum[SCAN_THREADS / 64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t incl = wave_incl_scan64(v, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  for (uint32_t k = 0; k < SCAN_THREADS / 64; ++k) {
+    if (k < w) before += wsum[k];
+    all += wsum[k];
+  }
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
+}  // namespace
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const uint32_t* counts, uint64_t n,
+                                                                   uint64_t* partials) {
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * SCAN_TILE;
+  uint64_t s = 0;
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + static_cast<uint64_t>(k) * SCAN_THREADS + threadIdx.x;
+    if (i < n) s += counts[i];
+  }
+  uint64_t tot;
+  block_excl_scan(s, &tot);
+  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_partials_kernel(uint64_t* partials, uint64_t nb,
+                                                                     uint64_t* offsets, uint64_t n) {
+  uint64_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nb; b0 += SCAN_THREADS) {
+    const uint64_t i = b0 + threadIdx.x;
+    const uint64_t v = i < nb ? partials[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(v, &tot);
+    if (i < nb) partials[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) offsets[n] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_final_kernel(const uint32_t* counts, uint64_t n,
+                                                                  const uint64_t* partials,
+                                                                  uint64_t* offsets) {
+  // thread-contiguous items: thread k owns [base + k*ITEMS, base + (k+1)*ITEMS)
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * SCAN_TILE + static_cast<uint64_t>(threadIdx.x) * SCAN_ITEMS;
+  uint32_t v[SCAN_ITEMS];
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    v[k] = i < n ? counts[i] : 0u;
+    s += v[k];
+  }
+  uint64_t tot;
+  uint64_t run = partials[blockIdx.x] + block_excl_scan(s, &tot);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    if (i < n) offsets[i] = run;
+    run += v[k];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Scatter: slab entries -> CSR out_ids
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a, const uint64_t* offsets,
+                                                           uint32_t* out_ids) {
+  __shared__ uint32_t rank[4][64];
+  const uint32_t lane = lane_id();
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4 + wv;
+  const uint64_t t0 = tile * TILE_TOPICS;
+  if (t0 >= a.n) return;
+  rank[wv][lane] = 0;
+  wave_sync();
+  const uint32_t fill = min(a.tile_fill[tile], a.slab_cap);
+  const uint64_t dmask = a.tile_defer[tile];
+  const uint64_t* slab = a.slab + tile * a.slab_cap;
+  for (uint32_t i = lane; i < fill; i += 64) {
+    const uint64_t e = slab[i];
+    const uint32_t tl = static_cast<uint32_t>(e >> 32);
+    if ((dmask >> tl) & 1ull) continue;
+    const uint32_t r = atomicAdd(&rank[wv][tl], 1u);
+    out_ids[offsets[t0 + tl] + r] = static_cast<uint32_t>(e);
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a, const uint64_t* offsets,
+                                                           uint32_t* out_ids, uint32_t* deep_rank) {
+  const uint32_t fill = min(a.ctrl[CTRL_DEEP_FILL], a.deep_slab_cap);
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < fill;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t e = a.deep_slab[i];
+    const uint32_t j = static_cast<uint32_t>(e >> 32);
+    const uint32_t t = a.deferred[j];
+    const uint32_t r = atomicAdd(&deep_rank[j], 1u);
+    out_ids[offsets[t] + r] = static_cast<uint32_t>(e);
+  }
+}
+
+__global__ void zero_u32_kernel(uint32_t* p, const uint32_t* count) {
+  const uint32_t n = *count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0;
+}
+
+// ------------------------------------------------------------------------------------
+// Launch wrappers
+// ------------------------------------------------------------------------------------
+hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
+  const uint64_t ntiles = (a.n + TILE_TOPICS - 1) / TILE_TOPICS;
+  if (ntiles == 0) return hipSuccess;
+  if (v == FAST_STACK_2K) {
+    constexpr int W = 2;
+    const uint64_t grid = (ntiles + W - 1) / W;
+    hipLaunchKernelGGL((match_fast_kernel<W, 2048, 1024>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+  } else {
+    constexpr int W = 4;
+    const uint64_t grid = (ntiles + W - 1) / W;
+    hipLaunchKernelGGL((match_fast_kernel<W, 1024, 1024>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_match_deep(const MatchArgs& a, hipStream_t s) {
+  const uint32_t blocks = (a.deep_waves * 64 + 255) / 256;
+  hipLaunchKernelGGL(match_deep_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+uint64_t scan_partials(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
+
+hipError_t launch_scan(const uint32_t* counts, uint64_t n, uint64_t* offsets, uint64_t* partials,
+                       hipStream_t s) {
+  const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (nb == 0) {
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, partials, 0, offsets, n);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3(static_cast<uint32_t>(nb)), dim3(SCAN_THREADS), 0, s, counts, n, partials);
+  hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, partials, nb, offsets, n);
+  hipLaunchKernelGGL(scan_final_kernel, dim3(static_cast<uint32_t>(nb)), dim3(SCAN_THREADS), 0, s, counts, n, partials, offsets);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(const MatchArgs& a, const uint64_t* offsets, uint32_t* out_ids,
+                          uint32_t* deep_rank, hipStream_t s) {
+  const uint64_t ntiles = (a.n + TILE_TOPICS - 1) / TILE_TOPICS;
+  if (ntiles) {
+    hipLaunchKernelGGL(scatter_fast_kernel, dim3(static_cast<uint32_t>((ntiles + 3) / 4)), dim3(256), 0, s, a,
+                       offsets, out_ids);
+  }
+  hipLaunchKernelGGL(zero_u32_kernel, dim3(64), dim3(256), 0, s, deep_rank, a.ctrl + CTRL_DEFERRED);
+  hipLaunchKernelGGL(scatter_deep_kernel, dim3(256), dim3(256), 0, s, a, offsets, out_ids, deep_rank);
+  return hipGetLastError();
+}
+
+}  // namespace emqx

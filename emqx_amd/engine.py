@@ -1,0 +1,134 @@
+"""Python handle on one device engine (a committed level-trie snapshot on one MI355X).
+
+Thin wrapper over the C ABI: packing, capacity retries and CSR -> list conversion.  All
+matching runs in the HIP kernels of ``emqx_amd/csrc/match_kernels.hip``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import MODE_ROUTES, MODE_TRIE, MODE_TRIE_WILDCARD, EngineError, check
+
+__all__ = ["Engine", "pack", "MODE_ROUTES", "MODE_TRIE", "MODE_TRIE_WILDCARD", "EngineError"]
+
+
+def pack(items: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    """bytes items -> (uint8 buffer, uint64 offsets[n+1])."""
+    n = len(items)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(np.fromiter((len(s) for s in items), dtype=np.uint64, count=n))
+    joined = b"".join(items)
+    buf = np.frombuffer(joined, dtype=np.uint8) if joined else np.zeros(1, dtype=np.uint8)
+    return np.ascontiguousarray(buf), offs
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Engine:
+    """One device table.  ``device=-1`` uses the current HIP device."""
+
+    def __init__(self, device: int = -1):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        opts = _lib.EngineOpts(device, 0)
+        check(L.emqx_engine_create(ctypes.byref(opts), ctypes.byref(h)), "emqx_engine_create")
+        self._h = h
+        self._cap_hint = 1 << 16
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().emqx_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- mutations ---------------------------------------------------------------
+    def insert_packed(self, buf: np.ndarray, offs: np.ndarray) -> np.ndarray:
+        n = len(offs) - 1
+        ids = np.zeros(max(n, 1), dtype=np.uint32)
+        check(_lib.lib().emqx_insert_filters(self._h, _ptr(buf), _ptr(offs), n, _ptr(ids)),
+              "emqx_insert_filters")
+        return ids[:n]
+
+    def insert(self, filters: Sequence[bytes]) -> np.ndarray:
+        return self.insert_packed(*pack(list(filters)))
+
+    def delete(self, ids) -> None:
+        a = np.ascontiguousarray(np.asarray(ids, dtype=np.uint32).reshape(-1))
+        check(_lib.lib().emqx_delete_filters(self._h, _ptr(a), a.size), "emqx_delete_filters")
+
+    def lookup(self, filt: bytes) -> Optional[int]:
+        b = np.frombuffer(filt or b"\0", dtype=np.uint8)
+        out = ctypes.c_uint32()
+        rc = _lib.lib().emqx_lookup_filter(self._h, _ptr(b), len(filt), ctypes.byref(out))
+        if rc == _lib.EMQX_ENOTFOUND:
+            return None
+        check(rc, "emqx_lookup_filter")
+        return int(out.value)
+
+    def name(self, fid: int) -> bytes:
+        n = ctypes.c_uint64()
+        check(_lib.lib().emqx_filter_name(self._h, fid, None, 0, ctypes.byref(n)), "emqx_filter_name")
+        buf = ctypes.create_string_buffer(max(n.value, 1))
+        check(_lib.lib().emqx_filter_name(self._h, fid, buf, n.value, ctypes.byref(n)), "emqx_filter_name")
+        return buf.raw[: n.value]
+
+    def commit(self) -> None:
+        check(_lib.lib().emqx_commit(self._h), "emqx_commit")
+
+    def stats(self) -> dict:
+        s = _lib.Stats()
+        check(_lib.lib().emqx_stats_get(self._h, ctypes.byref(s)), "emqx_stats_get")
+        return s.as_dict()
+
+    # ---- matching ------------------------------------------------------------------
+    def match_packed(self, buf: np.ndarray, offs: np.ndarray, mode: int = MODE_ROUTES):
+        """-> (offsets[n+1] uint64, ids uint32) CSR."""
+        n = len(offs) - 1
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        cap = self._cap_hint
+        while True:
+            ids = np.zeros(max(cap, 1), dtype=np.uint32)
+            total = ctypes.c_uint64()
+            rc = _lib.lib().emqx_match_batch(self._h, mode, _ptr(buf), _ptr(offs), n, _ptr(out_off),
+                                              _ptr(ids), cap, ctypes.byref(total))
+            if rc == _lib.EMQX_EOVERFLOW:
+                cap = int(total.value) + 1
+                self._cap_hint = max(self._cap_hint, cap)
+                continue
+            check(rc, "emqx_match_batch")
+            return out_off, ids[: int(total.value)]
+
+    def match(self, topics: Sequence[bytes], mode: int = MODE_ROUTES) -> List[List[int]]:
+        """Per-topic lists of matching filter ids (sorted)."""
+        off, ids = self.match_packed(*pack(list(topics)), mode=mode)
+        return [sorted(ids[off[i]:off[i + 1]].tolist()) for i in range(len(topics))]
+
+    def match_device(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, d_out_off_ptr: int,
+                     d_out_ids_ptr: int, cap: int, mode: int = MODE_ROUTES, stream: int = 0) -> int:
+        """Device-resident batch (raw HIP pointers, e.g. ``tensor.data_ptr()``).  Returns the
+        number of ids written; raises EngineError(EMQX_EOVERFLOW) with ``.needed`` set when
+        ``cap`` is too small."""
+        total = ctypes.c_uint64()
+        rc = _lib.lib().emqx_match_batch_device(
+            self._h, mode, ctypes.c_void_p(d_bytes_ptr), ctypes.c_void_p(d_offs_ptr), n,
+            ctypes.c_void_p(d_out_off_ptr), ctypes.c_void_p(d_out_ids_ptr), cap, ctypes.byref(total),
+            ctypes.c_void_p(stream) if stream else None)
+        if rc == _lib.EMQX_EOVERFLOW:
+            err = EngineError(rc, "emqx_match_batch_device")
+            err.needed = int(total.value)
+            raise err
+        check(rc, "emqx_match_batch_device")
+        return int(total.value)

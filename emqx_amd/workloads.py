@@ -1,0 +1,319 @@
+"""Synthetic subscription tables and topic streams for the BASELINE configs (SURVEY §8 d).
+
+Everything is generated with numpy PCG64 at fixed seeds and returned PACKED:
+``(uint8 bytes, uint64 offsets[n+1])`` — the engine's batch format — so 10M-filter tables
+never become Python lists.  Filter ids are 0-based indices in the returned (deduplicated,
+generation-ordered) filter list.
+
+Level codes used while composing: >= 0 word id in that level's vocabulary, PLUS_CODE = '+',
+HASH_CODE = '#', ABSENT = level not present.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+PLUS_CODE = -1
+HASH_CODE = -2
+ABSENT = -3
+
+B_VOCAB = [64, 1024, 4096, 65536, 65536, 1024, 256, 64]
+B_PREFIX = [b"region", b"site", b"bldg", b"dev", b"sensor", b"metric", b"unit", b"q"]
+
+
+@dataclass
+class Workload:
+    name: str
+    filters: Tuple[np.ndarray, np.ndarray]   # packed filters
+    topics: Tuple[np.ndarray, np.ndarray]    # packed topics
+
+    @property
+    def n_filters(self) -> int:
+        return len(self.filters[1]) - 1
+
+    @property
+    def n_topics(self) -> int:
+        return len(self.topics[1]) - 1
+
+
+# ---------------------------------------------------------------------------------------
+# packing helpers
+# ---------------------------------------------------------------------------------------
+
+def vocab_table(words: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    offs = np.zeros(len(words) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(w) for w in words])
+    buf = np.frombuffer(b"".join(words), dtype=np.uint8).copy() if offs[-1] else np.zeros(0, np.uint8)
+    return buf, offs
+
+
+PAD = 0xFF  # never a byte of a generated word
+
+
+def _padded(vb: np.ndarray, vo: np.ndarray) -> np.ndarray:
+    """(bytes, offsets) vocabulary -> [V, maxlen] uint8 table padded with PAD."""
+    lens = np.diff(vo)
+    V, W = len(lens), int(lens.max(initial=0))
+    t = np.full((V, max(W, 1)), PAD, dtype=np.uint8)
+    for k in range(V):
+        t[k, : lens[k]] = vb[vo[k]:vo[k + 1]]
+    return t
+
+
+def compose(codes: np.ndarray, level_vocabs: List[Tuple[np.ndarray, np.ndarray]],
+            chunk: int = 1 << 20) -> Tuple[np.ndarray, np.ndarray]:
+    """codes[N, D] level codes -> packed '/'-joined strings.  Levels must be contiguous from
+    level 0 (ABSENT only as a suffix).  level_vocabs[l] = (bytes, offsets) of level l.
+
+    Each chunk is laid out as a fixed-width byte matrix (padded words + separators) and
+    compacted with one boolean mask, which keeps the 10M-filter tables to a few seconds."""
+    N, D = codes.shape
+    tables = []
+    for l in range(D):
+        vb, vo = level_vocabs[min(l, len(level_vocabs) - 1)]
+        t = _padded(vb, vo)
+        W = max(t.shape[1], 1)
+        extra = np.full((3, W), PAD, dtype=np.uint8)   # rows: '+', '#', absent
+        extra[0, 0] = ord("+")
+        extra[1, 0] = ord("#")
+        tables.append(np.concatenate([t, extra]))
+    out_bufs, out_lens = [], []
+    for c0 in range(0, N, chunk):
+        c = codes[c0:c0 + chunk]
+        n = c.shape[0]
+        cols = []
+        for l in range(D):
+            tb = tables[l]
+            V = tb.shape[0] - 3
+            col = c[:, l]
+            idx = np.where(col >= 0, col, np.where(col == PLUS_CODE, V, np.where(col == HASH_CODE, V + 1, V + 2)))
+            if l > 0:
+                sep = np.where(col != ABSENT, ord("/"), PAD).astype(np.uint8)[:, None]
+                cols.append(sep)
+            cols.append(tb[idx])
+        mat = np.concatenate(cols, axis=1)
+        keep = mat != PAD
+        out_lens.append(keep.sum(1))
+        out_bufs.append(mat[keep])
+    lens = np.concatenate(out_lens) if out_lens else np.zeros(0, np.int64)
+    offs = np.zeros(N + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    buf = np.concatenate(out_bufs) if out_bufs else np.zeros(0, np.uint8)
+    if buf.size == 0:
+        buf = np.zeros(1, np.uint8)
+    return np.ascontiguousarray(buf), offs
+
+
+def unpack(packed: Tuple[np.ndarray, np.ndarray], idx=None) -> List[bytes]:
+    buf, offs = packed
+    raw = buf.tobytes()
+    n = len(offs) - 1
+    it = range(n) if idx is None else idx
+    return [raw[int(offs[i]):int(offs[i + 1])] for i in it]
+
+
+def take(packed: Tuple[np.ndarray, np.ndarray], idx: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Sub-batch of a packed list (vectorized gather)."""
+    buf, offs = packed
+    idx = np.asarray(idx, dtype=np.int64)
+    s = offs[:-1].astype(np.int64)[idx]
+    ln = (offs[1:].astype(np.int64) - offs[:-1].astype(np.int64))[idx]
+    o = np.zeros(len(idx) + 1, dtype=np.uint64)
+    o[1:] = np.cumsum(ln)
+    tot = int(o[-1])
+    within = np.arange(tot, dtype=np.int64) - np.repeat(np.cumsum(ln) - ln, ln)
+    nb = buf[np.repeat(s, ln) + within] if tot else np.zeros(1, np.uint8)
+    return np.ascontiguousarray(nb), o
+
+
+def dedupe_rows(codes: np.ndarray) -> np.ndarray:
+    """Unique rows in first-occurrence order.  Rows are keyed by a 64-bit hash: a collision
+    can only drop a distinct row, which the generators replace by drawing more rows."""
+    c = codes.astype(np.uint64)
+    h = np.full(c.shape[0], 0x9E3779B97F4A7C15, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for j in range(c.shape[1]):
+            h ^= c[:, j] + np.uint64(0x632BE59BD9B4E019) + (h << np.uint64(6)) + (h >> np.uint64(2))
+            h *= np.uint64(0xff51afd7ed558ccd)
+            h ^= h >> np.uint64(29)
+    _, first = np.unique(h, return_index=True)
+    return codes[np.sort(first)]
+
+
+def zipf_sampler(rng: np.random.Generator, vsize: int, s: float = 1.1):
+    p = 1.0 / np.arange(1, vsize + 1, dtype=np.float64) ** s
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    return lambda n: np.minimum(np.searchsorted(cdf, rng.random(n)), vsize - 1).astype(np.int32)
+
+
+def level_vocabs(prefixes: Sequence[bytes], sizes: Sequence[int]):
+    return [vocab_table([p + b"%d" % k for k in range(v)]) for p, v in zip(prefixes, sizes)]
+
+
+# ---------------------------------------------------------------------------------------
+# Config A (CPU reference config) and A' (emqx_broker_bench run1 shape)
+# ---------------------------------------------------------------------------------------
+
+def config_a(n_filters: int = 100_000, n_topics: int = 1_000_000, seed: int = 1) -> Workload:
+    """100k filters site{i mod 1000}/+/dev{i div 1000}/#; topics
+    site{U[0,1000)}/gw{U[0,64)}/dev{U[0,128)}/m{U[0,8)} (SURVEY §8 d)."""
+    i = np.arange(n_filters)
+    vs = [vocab_table([b"site%d" % k for k in range(1000)]), vocab_table([b"gw%d" % k for k in range(64)]),
+          vocab_table([b"dev%d" % k for k in range(max(128, n_filters // 1000 + 1))]),
+          vocab_table([b"m%d" % k for k in range(8)])]
+    fc = np.stack([i % 1000, np.full(n_filters, PLUS_CODE), i // 1000, np.full(n_filters, HASH_CODE)], 1)
+    filters = compose(fc, vs)
+    rng = np.random.default_rng(seed)
+    tc = np.stack([rng.integers(0, 1000, n_topics), rng.integers(0, 64, n_topics),
+                   rng.integers(0, 128, n_topics), rng.integers(0, 8, n_topics)], 1)
+    topics = compose(tc, vs)
+    return Workload("A", filters, topics)
+
+
+def config_a_prime(subscribers: int = 80, sub_ops: int = 1000, publishers: int = 80) -> Workload:
+    """emqx_broker_bench run1 (apps/emqx/src/emqx_broker_bench.erl:25-34,146-162): filters
+    device/{id}/+/{num}/#, one topic per publisher device/{id rem subs + 1}/foo/1/bar/1/2/3/4/5."""
+    ids = np.repeat(np.arange(1, subscribers + 1), sub_ops)
+    nums = np.tile(np.arange(1, sub_ops + 1), subscribers)
+    V = max(subscribers, sub_ops) + 2
+    num_v = vocab_table([b"%d" % k for k in range(V)])
+    vs = [vocab_table([b"device"]), num_v, vocab_table([b"foo"]), num_v, vocab_table([b"bar"])] + [num_v] * 5
+    fc = np.stack([np.zeros_like(ids), ids, np.full_like(ids, PLUS_CODE), nums, np.full_like(ids, HASH_CODE)], 1)
+    fc = np.concatenate([fc, np.full((len(ids), 5), ABSENT)], 1)
+    filters = compose(fc, vs)
+    pid = np.arange(1, publishers + 1)
+    tc = np.stack([np.zeros_like(pid), pid % subscribers + 1, np.zeros_like(pid), np.ones_like(pid),
+                   np.zeros_like(pid)] + [np.full_like(pid, k) for k in (1, 2, 3, 4, 5)], 1)
+    topics = compose(tc, vs)
+    return Workload("A'", filters, topics)
+
+
+# ---------------------------------------------------------------------------------------
+# Config B (1 x MI355X headline) — also C at larger scale
+# ---------------------------------------------------------------------------------------
+
+def _b_filter_codes(rng, n, vocab_sizes, samplers):
+    D = len(vocab_sizes)
+    d = rng.integers(4, D + 1, n)  # U{4..8}
+    words = np.stack([samplers[l](n) for l in range(D)], 1).astype(np.int32)
+    lvl = np.arange(D)[None, :]
+    codes = np.where(lvl < d[:, None], words, ABSENT).astype(np.int32)
+    cls = rng.random(n)
+    plus_cls = (cls >= 0.5) & (cls < 0.8)
+    hash_cls = cls >= 0.8
+    # '+' class: each level '+' w.p. 0.25, at least one
+    pm = (rng.random((n, D)) < 0.25) & (lvl < d[:, None])
+    none = plus_cls & ~pm.any(1)
+    force = rng.integers(0, d)  # one level in [0, d)
+    pm[np.nonzero(none)[0], force[none]] = True
+    codes = np.where(plus_cls[:, None] & pm, PLUS_CODE, codes)
+    # '#' class: keep t = U{1..d} literal levels, then '#'
+    t = rng.integers(1, d + 1)
+    hrows = np.nonzero(hash_cls)[0]
+    hc = codes[hrows].copy()
+    hc[lvl.repeat(len(hrows), 0) >= t[hrows, None]] = ABSENT
+    codes9 = np.full((n, D + 1), ABSENT, dtype=np.int32)
+    codes9[:, :D] = codes
+    hc9 = np.full((len(hrows), D + 1), ABSENT, dtype=np.int32)
+    hc9[:, :D] = hc
+    hc9[np.arange(len(hrows)), t[hrows]] = HASH_CODE
+    codes9[hrows] = hc9
+    return codes9
+
+
+def config_b(n_filters: int = 10_000_000, n_topics: int = 1_000_000, seed: int = 2,
+             vocab_scale: int = 1, prefixes=B_PREFIX, topic_seed=None) -> Workload:
+    """10M mixed exact/'+'/'#' filters, depth U{4..8}, Zipf(1.1) per-level vocab
+    [64,1024,4096,65536,65536,1024,256,64]; 50% exact / 30% '+' / 20% '#'.  Topics depth
+    U{4..8}: 50% instantiated from a random filter ('+' -> random word, '#' -> 0-3 words),
+    50% random (SURVEY §8 d)."""
+    rng = np.random.default_rng(seed)
+    sizes = [v * vocab_scale for v in B_VOCAB]
+    samplers = [zipf_sampler(rng, v) for v in sizes]
+    vs = level_vocabs(prefixes, sizes)
+    vs.append(vocab_table([b"x"]))  # level 8 only ever holds '#' or instantiated words
+    got = np.zeros((0, 9), dtype=np.int32)
+    want = n_filters
+    while got.shape[0] < n_filters:
+        extra = int((want - got.shape[0]) * 1.15) + 1024
+        got = dedupe_rows(np.concatenate([got, _b_filter_codes(rng, extra, sizes, samplers)]))
+    fcodes = got[:n_filters]
+    filters = compose(fcodes, vs)
+    if topic_seed is not None:  # an independent topic stream over the same table
+        rng = np.random.default_rng(topic_seed)
+        samplers = [zipf_sampler(rng, v) for v in sizes]
+
+    # topics (levels up to 8 + 3 for '#' expansion => pad to 11)
+    TD = 11
+    half = n_topics // 2
+    src = fcodes[rng.integers(0, n_filters, half)]
+    tcodes = np.full((n_topics, TD), ABSENT, dtype=np.int32)
+    rand_words = np.stack([samplers[min(l, 7)](half) for l in range(TD)], 1)
+    inst = np.full((half, TD), ABSENT, dtype=np.int32)
+    inst[:, :9] = np.where(src == PLUS_CODE, rand_words[:, :9], src)
+    # '#': replace by 0-3 random words at its position
+    hpos = np.argmax(src == HASH_CODE, axis=1)
+    has_h = (src == HASH_CODE).any(1)
+    k = rng.integers(0, 4, half)
+    lvl = np.arange(TD)[None, :]
+    exp = has_h[:, None] & (lvl >= hpos[:, None]) & (lvl < (hpos + k)[:, None])
+    inst = np.where(exp, rand_words, inst)
+    inst = np.where(has_h[:, None] & (lvl >= (hpos + k)[:, None]), ABSENT, inst)
+    # a '#' with zero expansion at position 0 would leave an empty topic: keep >= 1 level
+    empty = inst[:, 0] == ABSENT
+    inst[empty, 0] = rand_words[empty, 0]
+    tcodes[:half] = inst
+    nr = n_topics - half
+    d = rng.integers(4, 9, nr)
+    rw = np.stack([samplers[min(l, 7)](nr) for l in range(TD)], 1)
+    tcodes[half:] = np.where(lvl < d[:, None], rw, ABSENT)
+    perm = rng.permutation(n_topics)
+    tcodes = tcodes[perm]
+    # levels >= 8 use level-7 vocab words (instantiated '#' expansions)
+    tv = vs[:8] + [vs[7]] * 3
+    topics = compose(tcodes, tv)
+    return Workload("B", filters, topics)
+
+
+# ---------------------------------------------------------------------------------------
+# Config D (adversarial)
+# ---------------------------------------------------------------------------------------
+
+def config_d(n_filters: int = 1_000_000, n_topics: int = 100_000, seed: int = 4, depth: int = 16,
+             vocab: int = 4) -> Workload:
+    """Depth-16 templates over 4 words/level, each level '+' w.p. 0.5, 30% '#'-terminated,
+    plus '#', '+/#', '+/+/#'; topics exactly 16 levels from the same vocab."""
+    rng = np.random.default_rng(seed)
+    got = np.zeros((0, depth + 1), dtype=np.int32)
+    while got.shape[0] < n_filters:
+        n = int((n_filters - got.shape[0]) * 1.1) + 64
+        c = rng.integers(0, vocab, (n, depth)).astype(np.int32)
+        c = np.where(rng.random((n, depth)) < 0.5, PLUS_CODE, c)
+        c17 = np.full((n, depth + 1), ABSENT, dtype=np.int32)
+        c17[:, :depth] = c
+        hrows = np.nonzero(rng.random(n) < 0.3)[0]
+        t = rng.integers(1, depth + 1, len(hrows))
+        lvl = np.arange(depth + 1)[None, :]
+        sub = c17[hrows]
+        sub = np.where(lvl >= t[:, None], ABSENT, sub)
+        sub[np.arange(len(hrows)), t] = HASH_CODE
+        c17[hrows] = sub
+        got = dedupe_rows(np.concatenate([got, c17]))
+    special = np.full((3, depth + 1), ABSENT, dtype=np.int32)
+    special[0, 0] = HASH_CODE
+    special[1, :2] = [PLUS_CODE, HASH_CODE]
+    special[2, :3] = [PLUS_CODE, PLUS_CODE, HASH_CODE]
+    fcodes = dedupe_rows(np.concatenate([special, got]))[:n_filters]
+    vs = [vocab_table([b"l%dw%d" % (l, k) for k in range(vocab)]) for l in range(depth + 1)]
+    filters = compose(fcodes, vs)
+    tcodes = rng.integers(0, vocab, (n_topics, depth)).astype(np.int32)
+    topics = compose(tcodes, vs[:depth])
+    return Workload("D", filters, topics)
+
+
+def config_by_name(name: str, **kw) -> Workload:
+    return {"A": config_a, "A'": config_a_prime, "B": config_b, "D": config_d}[name](**kw)

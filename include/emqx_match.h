@@ -1,0 +1,133 @@
+/*
+ * emqx_match.h — C ABI of the MI355X-native EMQX route-lookup engine (libemqxmatch.so).
+ *
+ * This is the drop-in boundary for EMQX's publish-side route lookup.  A thin Erlang NIF
+ * (emqx_amd/csrc/nif/emqx_match_nif.c) binds these entry points so
+ * that the Erlang call shapes stay unchanged.  Paths are relative to the reference
+ * checkout (xiongzhenhai-zh/emqx, EMQX 5.0.0-beta.3):
+ *
+ *   emqx_trie:insert/1, emqx_trie:delete/1   apps/emqx/src/emqx_trie.erl:106-137
+ *       -> emqx_insert_filters / emqx_delete_filters (+ emqx_commit: batched rebuild,
+ *          epoch swap; the reference applies each mutation in a mria transaction,
+ *          apps/emqx/src/emqx_router_utils.erl:33-70,97-125)
+ *   emqx_trie:match/1                        apps/emqx/src/emqx_trie.erl:139-162
+ *       -> emqx_match_batch(mode = EMQX_MODE_TRIE)
+ *   emqx_router:match_trie/1 (private)       apps/emqx/src/emqx_router.erl:136-140
+ *       -> emqx_match_batch(mode = EMQX_MODE_TRIE_WILDCARD)
+ *   emqx_router:match_routes/1               apps/emqx/src/emqx_router.erl:127-133
+ *       -> emqx_match_batch(mode = EMQX_MODE_ROUTES): filter ids whose routes the
+ *          reference returns; the NIF maps ids to the #route{} records it keeps.
+ *   emqx_trie:empty/0                        apps/emqx/src/emqx_trie.erl:164-171
+ *       -> emqx_stats(...).n_filters == 0
+ *   emqx_topic:match/2                       apps/emqx/src/emqx_topic.erl:65-87
+ *       -> emqx_topic_match (CPU; per-pair callers such as authz stay on the CPU)
+ *
+ * Conventions: plain C, no exceptions cross the ABI, every entry point returns an int
+ * status (EMQX_OK = 0, negative = error) unless documented otherwise.  Topic/filter
+ * batches are packed byte buffers plus uint64 offsets[n+1] (item i = bytes[offsets[i] ..
+ * offsets[i+1])).  Match results are CSR: out_offsets[n+1] and out_ids[out_offsets[n]].
+ *
+ * Threading: any number of threads may call emqx_match_batch* concurrently; each call
+ * reads an immutable table snapshot.  Mutations (insert/delete/commit) must come from one
+ * writer at a time (the reference serialises route mutations per topic through
+ * router_pool, apps/emqx/src/emqx_router.erl:184-188); emqx_commit publishes a new
+ * snapshot RCU-style — in-flight matches keep the old one until they return.
+ *
+ * Ownership: the caller owns every buffer it passes for the duration of the call; the
+ * engine owns device tables, staging and workspaces, all released by
+ * emqx_engine_destroy.
+ */
+#ifndef EMQX_MATCH_H
+#define EMQX_MATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------------- */
+#define EMQX_OK 0
+#define EMQX_EINVAL -1        /* bad argument (null handle, bad mode, bad offsets)          */
+#define EMQX_ENOMEM -2        /* host or device allocation failed                            */
+#define EMQX_EDEVICE -3       /* HIP runtime / kernel error (no device, launch failure)      */
+#define EMQX_EOVERFLOW -4     /* out_ids too small: *n_out holds the required capacity       */
+#define EMQX_ENOTFOUND -5     /* unknown filter id / name                                     */
+#define EMQX_ETOODEEP -6      /* a topic exceeded the engine's frontier capacity             */
+
+/* ---- match modes --------------------------------------------------------------- */
+#define EMQX_MODE_ROUTES 0          /* emqx_router:match_routes/1 — exact ∪ wildcard    */
+#define EMQX_MODE_TRIE 1            /* emqx_trie:match/1, trie holding every inserted
+                                       filter (emqx_trie_SUITE usage)                  */
+#define EMQX_MODE_TRIE_WILDCARD 2   /* emqx_router:match_trie/1 — wildcard filters only */
+
+typedef struct emqx_engine emqx_engine; /* opaque */
+
+typedef struct emqx_engine_opts {
+  int32_t device;        /* HIP device ordinal (-1: current device)                        */
+  uint32_t flags;        /* reserved, must be 0                                             */
+} emqx_engine_opts;
+
+typedef struct emqx_stats {
+  uint64_t n_filters;        /* live filters                                                 */
+  uint64_t n_ids;            /* ids ever assigned (ids are never reused)                    */
+  uint64_t n_nodes;          /* level-trie nodes in the committed snapshot (root included)  */
+  uint64_t n_slots;          /* edge-array slots                                             */
+  uint64_t n_words;          /* interned literal words                                       */
+  uint64_t table_bytes;      /* device bytes held by the committed snapshot                  */
+  uint64_t epoch;            /* number of commits                                            */
+  uint64_t last_evals;       /* node visits (SURVEY §8 d) of the last match call             */
+  uint64_t last_deferred;    /* topics that took the deep-topic path in the last call        */
+  double last_build_ms;      /* host build time of the last commit                           */
+  double last_match_ms;      /* device time of the last match call (hipEvent)                */
+  double last_kernel_ms;     /* device time of its fused match kernel alone (hipEvent)       */
+} emqx_stats;
+
+/* Lifecycle. */
+int emqx_engine_create(const emqx_engine_opts* opts, emqx_engine** out);
+int emqx_engine_destroy(emqx_engine* e);
+
+/* Mutations (applied to the device snapshot by emqx_commit).
+ * insert: ids_out[i] = id of filter i; an already-live filter keeps its id (emqx_trie:insert/2
+ *         is idempotent, emqx_trie.erl:115-120); a deleted filter re-inserted gets its old id. */
+int emqx_insert_filters(emqx_engine* e, const uint8_t* bytes, const uint64_t* offsets,
+                        uint64_t n, uint32_t* ids_out);
+int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n);
+int emqx_lookup_filter(emqx_engine* e, const uint8_t* bytes, uint64_t len, uint32_t* id_out);
+/* Copies the bytes of filter `id` into buf (cap bytes); *len_out = its length. */
+int emqx_filter_name(emqx_engine* e, uint32_t id, uint8_t* buf, uint64_t cap, uint64_t* len_out);
+/* Rebuilds the device tables from the live filter set and publishes them (epoch swap). */
+int emqx_commit(emqx_engine* e);
+
+/* Batched match, host buffers.  out_offsets has n+1 entries.  On EMQX_EOVERFLOW nothing
+ * is written to out_ids and *n_out is the capacity required. */
+int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes,
+                     const uint64_t* topic_offsets, uint64_t n, uint64_t* out_offsets,
+                     uint32_t* out_ids, uint64_t cap, uint64_t* n_out);
+
+/* Batched match, DEVICE buffers already resident in HBM (d_* pointers), ordered on the
+ * given hipStream_t (NULL: the engine's own stream).  Same contract as above; *n_out is a
+ * host pointer.  Returns after the results are complete on `stream`. */
+int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topic_bytes,
+                            const uint64_t* d_topic_offsets, uint64_t n,
+                            uint64_t* d_out_offsets, uint32_t* d_out_ids, uint64_t cap,
+                            uint64_t* n_out, void* stream);
+
+int emqx_stats_get(emqx_engine* e, emqx_stats* out);
+
+/* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */
+int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filter,
+                     uint64_t filter_len);
+/* emqx_topic:wildcard/1 (emqx_topic.erl:53-62): 1 if some level is exactly '+' or '#'. */
+int emqx_topic_wildcard(const uint8_t* topic, uint64_t len);
+
+const char* emqx_strerror(int code);
+/* Library version string. */
+const char* emqx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EMQX_MATCH_H */

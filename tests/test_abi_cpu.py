@@ -1,0 +1,108 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library builds, loads and exports every
+symbol include/emqx_match.h declares; its CPU entry points (emqx_topic:match/2, wildcard/1)
+agree with the reference KATs; without a GPU the engine fails loudly (no CPU fallback)."""
+
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    lib_path = os.path.join(ROOT, "emqx_amd", "_build", "libemqxmatch.so")
+    if not os.path.exists(lib_path):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "emqx_amd", "csrc"), "-j4"], check=True,
+                       capture_output=True)
+    from emqx_amd import _lib
+    return _lib.lib()
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "emqx_match.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(emqx_[a-z_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol(L):
+    from emqx_amd import _lib
+    declared = header_functions()
+    assert len(declared) >= 14
+    assert sorted(_lib.EXPORTS) == declared
+    for name in declared:
+        assert hasattr(L, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared:
+        assert re.search(r"\bT %s\b" % name, nm), name
+
+
+def test_version_and_strerror(L):
+    assert b"gfx950" in L.emqx_version()
+    assert L.emqx_strerror(-4) == b"output capacity too small"
+
+
+def test_topic_match_kats(L, kats):
+    from emqx_amd import topic
+    for name, filt, expect in kats["topic_match"]:
+        assert topic.match(name.encode(), filt.encode()) is expect, (name, filt)
+
+
+def test_topic_match_fuzz_vs_oracle(L):
+    import random
+    from emqx_amd import topic
+    from oracle import emqx_ref as R
+    from tests.test_oracle_fuzz import rand_filter, rand_topic
+    rng = random.Random(3)
+    for _ in range(4000):
+        f, t = rand_filter(rng), rand_topic(rng)
+        assert topic.match(t, f) == R.match(t, f), (t, f)
+        assert topic.wildcard(t) == R.wildcard(t)
+
+
+def test_topic_misc_kats(L, kats):
+    from emqx_amd import topic as T
+    m = kats["topic_misc"]
+    for t, expect in m["wildcard"]["cases"]:
+        assert T.wildcard(t.encode()) is expect
+    for kind, t in m["validate_ok"]["cases"]:
+        assert T.validate((kind, t.encode()))
+    for kind, t, err in m["validate_err"]["cases"]:
+        if isinstance(t, dict):
+            t = "".join("%d/" % i for i in range(66667))
+        with pytest.raises(T.TopicError) as ei:
+            T.validate((kind, t.encode()))
+        assert ei.value.reason == err
+    for tf, opts, etf, eopts in m["parse_ok"]["cases"]:
+        got = T.parse(tf.encode(), {k: v.encode() if isinstance(v, str) else v for k, v in opts.items()})
+        assert got == (etf.encode(), {k: v.encode() if isinstance(v, str) else v for k, v in eopts.items()})
+    for tf, opts in m["parse_err"]["cases"]:
+        with pytest.raises(T.TopicError):
+            T.parse(tf.encode(), {k: v.encode() for k, v in opts.items()})
+
+
+def test_engine_without_gpu_fails_loudly(L):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from emqx_amd.engine import Engine, EngineError
+    with pytest.raises(EngineError) as ei:
+        Engine()
+    assert ei.value.code == -3   # EMQX_EDEVICE
+
+
+def test_workloads_shapes():
+    from emqx_amd import workloads as W
+    a = W.config_a(n_topics=2000)
+    assert a.n_filters == 100_000
+    assert W.unpack(a.filters, [0])[0] == b"site0/+/dev0/#"
+    ap = W.config_a_prime(subscribers=4, sub_ops=10, publishers=8)
+    assert W.unpack(ap.topics, [0])[0] == b"device/2/foo/1/bar/1/2/3/4/5"
+    b = W.config_b(n_filters=50_000, n_topics=4000)
+    fl = W.unpack(b.filters)
+    assert len(set(fl)) == len(fl) == 50_000
+    d = W.config_d(n_filters=5000, n_topics=100)
+    assert d.n_filters == 5000
+    assert all(t.count(b"/") == 15 for t in W.unpack(d.topics))

@@ -1,0 +1,269 @@
+"""Parity of the HIP engine with the oracle (GPU).
+
+Every result is compared bit-exactly as sorted filter-id sets against the
+oracle: the reference KATs (tests/golden/kats.json), fuzzed tables in all three modes, the
+BASELINE configs at sizes the oracle finishes in seconds, and the edge cases the reference
+tests (empty levels, '$' topics, wildcard topics, 26-level topics, deletes) plus the engine's
+own capacity paths (deep topics, slab overflow, long words, unknown words)."""
+
+import random
+
+import numpy as np
+import pytest
+
+from oracle import cpp as C
+from oracle import emqx_ref as R
+from tests.test_oracle_fuzz import rand_filter, rand_topic
+
+pytestmark = pytest.mark.gpu
+
+MODES = {"routes": 0, "trie": 1, "trie_wildcard": 2}
+
+
+@pytest.fixture(scope="module")
+def Engine():
+    import torch  # noqa: F401  (shares the HIP runtime with the engine)
+    from emqx_amd.engine import Engine as E
+    from emqx_amd import _lib
+    _lib.lib()
+    return E
+
+
+def engine_with(Engine, filters):
+    e = Engine()
+    ids = e.insert(filters)
+    assert list(ids) == list(range(len(filters)))
+    e.commit()
+    return e
+
+
+def expected(filters, topics, mode):
+    if mode == 0:
+        return [R.brute_force_routes(filters, t) for t in topics]
+    if mode == 1:
+        return [R.brute_force_trie(filters, t) for t in topics]
+    wild = [f if R.wildcard(f) else b"\x00never" for f in filters]
+    return [R.brute_force_trie(wild, t) for t in topics]
+
+
+def test_trie_suite_kats(Engine, kats):
+    for case in kats["trie_cases"]:
+        e = Engine()
+        names = {}
+        for op, arg in case["ops"]:
+            if op == "insert":
+                fid = int(e.insert([arg.encode()])[0])
+                names[fid] = arg.encode()
+            elif op == "delete":
+                fid = e.lookup(arg.encode())
+                if fid is not None:
+                    e.delete([fid])
+            elif op == "assert_empty":
+                assert (e.stats()["n_filters"] == 0) == arg
+        e.commit()
+        for topic, exp in case["queries"]:
+            got = sorted(names[i] for i in e.match([topic.encode()], mode=1)[0])
+            assert got == sorted(x.encode() for x in exp), (case["name"], topic)
+        for topic, n in case.get("len_queries", []):
+            assert len(e.match([topic.encode()], mode=1)[0]) == n
+
+
+def test_router_and_client_kats(Engine, kats):
+    from emqx_amd.router import Router
+    for case in kats["router_cases"]:
+        r = Router()
+        for t in case["add"]:
+            r.add_route(t.encode())
+        for topic, exp in case["queries"]:
+            assert sorted(x.topic for x in r.match_routes(topic.encode())) == sorted(e.encode() for e in exp)
+        for t in case["add"]:
+            r.delete_route(t.encode())
+        for topic, exp in case["then_delete_all"]:
+            assert r.match_routes(topic.encode()) == []
+    c = kats["client"]
+    for key in ("overlapping", "dollar"):
+        r = Router()
+        for s in c[key]["subs"]:
+            r.add_route(s.encode())
+        got = sorted(x.topic for x in r.match_routes(c[key]["topic"].encode()))
+        assert got == sorted(e.encode() for e in c[key]["expect"])
+
+
+def test_topic_match_pairs_on_device(Engine, kats):
+    """emqx_topic:match/2 KATs as one-filter tables (valid names only; the device implements
+    the trie/router semantics, which equal match/2 for non-wildcard names)."""
+    for name, filt, exp in kats["topic_match"]:
+        if R.wildcard(name.encode()):
+            continue
+        e = engine_with(Engine, [filt.encode()])
+        got = e.match([name.encode()], mode=0)[0]
+        assert (got == [0]) is exp, (name, filt)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_fuzz_parity(Engine, seed, mode):
+    rng = random.Random(9000 + seed)
+    filters = sorted({rand_filter(rng) for _ in range(rng.randint(20, 400))})
+    topics = [rand_topic(rng) for _ in range(600)] + [b"", b"/", b"$", b"$/x", b"+", b"#", b"a/#/b"]
+    e = engine_with(Engine, filters)
+    got = e.match(topics, mode=mode)
+    exp = expected(filters, topics, mode)
+    for t, g, x in zip(topics, got, exp):
+        assert g == x, (mode, t, g, x)
+
+
+def test_deletes_and_recommit(Engine):
+    rng = random.Random(77)
+    filters = sorted({rand_filter(rng) for _ in range(300)})
+    e = engine_with(Engine, filters)
+    gone = set(rng.sample(range(len(filters)), 100))
+    e.delete(sorted(gone))
+    e.commit()
+    live = [f if i not in gone else b"\x00dead" for i, f in enumerate(filters)]
+    topics = [rand_topic(rng) for _ in range(500)]
+    for t, g in zip(topics, e.match(topics, mode=0)):
+        assert g == R.brute_force_routes(live, t)
+    # re-insert keeps the old ids
+    back = sorted(gone)[:10]
+    ids = e.insert([filters[i] for i in back])
+    assert list(ids) == back
+
+
+def oracle_ids(filters_packed, topics_packed, mode=C.MODE_ROUTES, threads=8):
+    o = C.CppOracle(True, trie_all=(mode == C.MODE_TRIE))
+    o.add_packed(*filters_packed)
+    counts, ids, _ = o.match_packed(*topics_packed, mode=mode, threads=threads, stride=512)
+    return counts, ids
+
+
+def csr_equal(off, ids, counts, oids):
+    n = len(counts)
+    assert off[-1] == ids.size
+    got_counts = np.diff(off.astype(np.int64))
+    bad = np.nonzero(got_counts != counts.astype(np.int64))[0]
+    assert bad.size == 0, f"count mismatch at topics {bad[:10]}"
+    for i in range(n):
+        g = np.sort(ids[off[i]:off[i + 1]])
+        x = oids[i, :counts[i]]
+        assert np.array_equal(g, x), (i, g, x)
+
+
+def test_config_a_sample(Engine):
+    from emqx_amd import workloads as W
+    a = W.config_a(n_topics=50_000)
+    e = Engine()
+    e.insert_packed(*a.filters)
+    e.commit()
+    off, ids = e.match_packed(*a.topics, mode=0)
+    counts, oids = oracle_ids(a.filters, a.topics)
+    csr_equal(off, ids, counts, oids)
+    assert 0.7 < float(np.mean(counts == 1)) < 0.85   # ≈78% hit exactly one filter (SURVEY §8 d)
+
+
+def test_config_a_prime_one_route(Engine):
+    """emqx_broker_bench.erl:161-162: every publisher topic matches exactly one route."""
+    from emqx_amd import workloads as W
+    ap = W.config_a_prime()
+    e = Engine()
+    e.insert_packed(*ap.filters)
+    e.commit()
+    off, ids = e.match_packed(*ap.topics, mode=0)
+    assert np.all(np.diff(off.astype(np.int64)) == 1)
+
+
+def test_config_b_reduced(Engine):
+    from emqx_amd import workloads as W
+    b = W.config_b(n_filters=300_000, n_topics=40_000)
+    e = Engine()
+    e.insert_packed(*b.filters)
+    e.commit()
+    for mode in (0, 2):
+        off, ids = e.match_packed(*b.topics, mode=mode)
+        counts, oids = oracle_ids(b.filters, b.topics, mode=mode)
+        csr_equal(off, ids, counts, oids)
+    # evals: the engine's node-visit count equals the oracle's cost model
+    o = C.CppOracle(True)
+    o.add_packed(*b.filters)
+    e.match_packed(*b.topics, mode=0)
+    assert e.stats()["last_evals"] == int(o.evals_packed(*b.topics).sum())
+
+
+def test_config_d_reduced(Engine):
+    from emqx_amd import workloads as W
+    d = W.config_d(n_filters=30_000, n_topics=3000)
+    e = Engine()
+    e.insert_packed(*d.filters)
+    e.commit()
+    off, ids = e.match_packed(*d.topics, mode=0)
+    counts, oids = oracle_ids(d.filters, d.topics)
+    csr_equal(off, ids, counts, oids)
+    assert counts.mean() > 3
+
+
+def test_deep_topics_take_deep_path(Engine):
+    """Topics beyond the fast path's LDS budget (WID_CAP/8 levels) run on the deep path."""
+    rng = random.Random(5)
+    deep = b"/".join(b"w%d" % (i % 7) for i in range(300))
+    filters = [b"#", b"w0/#", b"+/+/#", deep, deep + b"/#", b"/".join([b"+"] * 300),
+               b"/".join([b"+"] * 150) + b"/#", b"w0/w1/+/w3/#"]
+    topics = [deep, deep + b"/x", b"/".join([b"w0"] * 400), b"a/b"] + [rand_topic(rng) for _ in range(100)]
+    e = engine_with(Engine, filters)
+    for mode in (0, 1, 2):
+        got = e.match(topics, mode=mode)
+        for t, g, x in zip(topics, got, expected(filters, topics, mode)):
+            assert g == x, (mode, t[:40])
+    assert e.stats()["last_deferred"] >= 3
+
+
+def test_many_matches_slab_growth(Engine):
+    """One topic matched by thousands of filters: the per-tile slab grows and reruns."""
+    filters = [b"a/b/c/d"] + [b"a/%s#" % (b"+/" * k) for k in range(3)]
+    filters += [b"a/b/c/d/%d/#" % i for i in range(3000)] + [b"+/b/+/d"]
+    filters += [b"a/+/c/d"] + [b"+/+/+/+"]
+    topics = [b"a/b/c/d"] * 70 + [b"a/b/c/d/%d" % i for i in range(50)]
+    e = engine_with(Engine, filters)
+    got = e.match(topics, mode=0)
+    for t, g, x in zip(topics, got, expected(filters, topics, 0)):
+        assert g == x
+
+
+def test_long_and_unknown_words(Engine):
+    long_w = b"x" * 40
+    filters = [long_w + b"/+", b"+/" + long_w, long_w + b"y/#", long_w[:-1] + b"/#", b"\xe4\xbd\xa0/+"]
+    topics = [long_w + b"/a", b"q/" + long_w, long_w + b"y", long_w + b"z/k", b"\xe4\xbd\xa0/1",
+              b"nope/nope", long_w[:-1]]
+    e = engine_with(Engine, filters)
+    got = e.match(topics, mode=0)
+    assert got == expected(filters, topics, 0)
+
+
+def test_empty_table_and_empty_batch(Engine):
+    e = Engine()
+    e.commit()
+    assert e.match([b"a/b", b""], mode=0) == [[], []]
+    e2 = engine_with(Engine, [b"#"])
+    assert e2.match([], mode=0) == []
+
+
+def test_device_api_matches_host_api(Engine):
+    import torch
+    from emqx_amd import workloads as W
+    b = W.config_b(n_filters=100_000, n_topics=20_000)
+    e = Engine()
+    e.insert_packed(*b.filters)
+    e.commit()
+    off_h, ids_h = e.match_packed(*b.topics, mode=0)
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(b.topics[0]).to(dev)
+    to = torch.from_numpy(b.topics[1].view(np.int64)).to(dev)
+    d_off = torch.empty(len(b.topics[1]), dtype=torch.int64, device=dev)
+    d_ids = torch.empty(ids_h.size + 16, dtype=torch.int32, device=dev)
+    n = e.match_device(tb.data_ptr(), to.data_ptr(), len(b.topics[1]) - 1, d_off.data_ptr(), d_ids.data_ptr(),
+                       d_ids.numel(), mode=0, stream=torch.cuda.current_stream().cuda_stream)
+    assert n == ids_h.size
+    off_d = d_off.cpu().numpy().view(np.uint64)
+    ids_d = d_ids[:n].cpu().numpy().view(np.uint32)
+    assert np.array_equal(off_d, off_h)
+    for i in range(0, len(off_h) - 1, 97):
+        assert np.array_equal(np.sort(ids_d[off_d[i]:off_d[i + 1]]), np.sort(ids_h[off_h[i]:off_h[i + 1]]))
