@@ -47,6 +47,10 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics in the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ab", type=str, default=None,
+                    help="comma list of fast-kernel variants: interleaved A/B rounds in this process, "
+                         "prints per-variant kernel/call times instead of the bench line")
+    ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per kernel launch from PMC (rocprofv3 FETCH_SIZE/WRITE_SIZE)")
     args = ap.parse_args()
@@ -90,6 +94,9 @@ def main():
     def step():
         return eng.match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
                                 mode=args.mode, stream=stream)
+
+    if args.ab:
+        return ab_variants(eng, step, args, wl)
 
     nout = 0
     for _ in range(args.warmup):
@@ -168,6 +175,39 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def ab_variants(eng, step, args, wl):
+    """Interleaved rounds of every variant in one process (cdna_hip_programming.md §5.4
+    rule 24): median/min of the fused kernel's HIP-event time and of the whole call."""
+    import torch
+    variants = [int(v) for v in args.ab.split(",")]
+    res = {v: {"kernel_ms": [], "call_ms": [], "nout": None, "deferred": 0, "max_stack": 0} for v in variants}
+    for v in variants:  # warm each variant once
+        eng.set_tuning("fast_variant", v)
+        step()
+    for _ in range(args.ab_rounds):
+        for v in variants:
+            eng.set_tuning("fast_variant", v)
+            for _ in range(max(1, args.steps // args.ab_rounds)):
+                nout = step()
+                st = eng.stats()
+                r = res[v]
+                r["kernel_ms"].append(st["last_kernel_ms"])
+                r["call_ms"].append(st["last_match_ms"])
+                r["nout"] = nout
+                r["deferred"] = max(r["deferred"], st["last_deferred"])
+                r["max_stack"] = max(r["max_stack"], st["last_max_stack"])
+    torch.cuda.synchronize()
+    out = {}
+    for v, r in res.items():
+        out[v] = {"kernel_ms_median": round(float(np.median(r["kernel_ms"])), 4),
+                  "kernel_ms_min": round(float(np.min(r["kernel_ms"])), 4),
+                  "call_ms_median": round(float(np.median(r["call_ms"])), 4),
+                  "topics_per_s_call": round(wl.n_topics / (float(np.median(r["call_ms"])) * 1e-3), 1),
+                  "nout": r["nout"], "deferred": r["deferred"], "max_stack": r["max_stack"]}
+    eng.set_tuning("fast_variant", -1)
+    print(json.dumps({"ab": out, "n_filters": wl.n_filters, "batch": wl.n_topics}), flush=True)
 
 
 def cpu_baseline(wl, args):

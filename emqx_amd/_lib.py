@@ -31,7 +31,7 @@ EXPORTS = (
     "emqx_engine_create", "emqx_engine_destroy", "emqx_insert_filters", "emqx_delete_filters",
     "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
     "emqx_match_batch_device", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
-    "emqx_strerror", "emqx_version",
+    "emqx_set_tuning", "emqx_strerror", "emqx_version",
 )
 
 
@@ -51,6 +51,7 @@ class Stats(ctypes.Structure):
         ("n_filters", ctypes.c_uint64), ("n_ids", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64),
         ("n_slots", ctypes.c_uint64), ("n_words", ctypes.c_uint64), ("table_bytes", ctypes.c_uint64),
         ("epoch", ctypes.c_uint64), ("last_evals", ctypes.c_uint64), ("last_deferred", ctypes.c_uint64),
+        ("last_max_stack", ctypes.c_uint64),
         ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double),
         ("last_kernel_ms", ctypes.c_double),
     ]
@@ -86,6 +87,7 @@ def lib():
         "emqx_stats_get": (i32, [vp, ctypes.POINTER(Stats)]),
         "emqx_topic_match": (i32, [vp, u64, vp, u64]),
         "emqx_topic_wildcard": (i32, [vp, u64]),
+        "emqx_set_tuning": (i32, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "emqx_strerror": (ctypes.c_char_p, [i32]),
         "emqx_version": (ctypes.c_char_p, []),
     }

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -47,7 +48,6 @@ hipError_t dalloc(T*& p, uint64_t count) {
 struct Snapshot {
   int device = 0;
   EdgeSlot* edges = nullptr;
-  NodeFids* fids = nullptr;
   VocabSlot* vocab = nullptr;
   uint8_t* arena = nullptr;
   TableView tv{};
@@ -58,7 +58,6 @@ struct Snapshot {
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
     dfree(edges);
-    dfree(fids);
     dfree(vocab);
     dfree(arena);
     (void)hipSetDevice(cur);
@@ -79,7 +78,9 @@ struct Workspace {
   uint64_t* slab = nullptr;
   uint32_t* tile_fill = nullptr;
   uint64_t* tile_defer = nullptr;
-  uint32_t* tile_evals = nullptr;
+  uint2* tile_stats = nullptr;
+  uint2* spill = nullptr;
+  uint32_t spill_cap = 2048;  // items per tile
   uint64_t* partials = nullptr;
   uint32_t* ctrl = nullptr;         // CTRL_WORDS u32 + 2 u64 (evals) -> 8 u32 words + 2 u64
   uint64_t* evals = nullptr;        // [0] total evals (device reduction)
@@ -104,7 +105,7 @@ struct Workspace {
   ~Workspace() {
     (void)hipSetDevice(device);
     dfree(counts); dfree(deferred); dfree(deep_rank); dfree(slab); dfree(tile_fill);
-    dfree(tile_defer); dfree(tile_evals); dfree(partials); dfree(ctrl); dfree(evals);
+    dfree(tile_defer); dfree(tile_stats); dfree(spill); dfree(partials); dfree(ctrl); dfree(evals);
     dfree(deep_wids); dfree(deep_stack); dfree(deep_slab); dfree(deep_evals);
     dfree(d_tbytes); dfree(d_toffs); dfree(d_out_off); dfree(d_out_ids);
     if (h_rb) (void)hipHostFree(h_rb);
@@ -134,9 +135,10 @@ struct emqx_engine {
   std::mutex ws_mu;
   std::vector<std::unique_ptr<Workspace>> all_ws;
   std::vector<Workspace*> free_ws;
-  std::atomic<uint64_t> last_evals{0}, last_deferred{0};
+  std::atomic<uint64_t> last_evals{0}, last_deferred{0}, last_max_stack{0};
   std::atomic<double> last_match_ms{0};
   std::atomic<double> last_kernel_ms{0};
+  std::atomic<int> forced_variant{-1};
 };
 
 namespace {
@@ -145,26 +147,23 @@ int upload(emqx_engine* e, const HostTables& ht, std::shared_ptr<Snapshot>* out)
   auto s = std::make_shared<Snapshot>();
   s->device = e->device;
   HIP_TRY(dalloc(s->edges, ht.edges.size()));
-  HIP_TRY(dalloc(s->fids, ht.fids.size()));
   HIP_TRY(dalloc(s->vocab, ht.vocab.size()));
   HIP_TRY(dalloc(s->arena, ht.arena.size() + 16));
   HIP_TRY(hipMemcpy(s->edges, ht.edges.data(), ht.edges.size() * sizeof(EdgeSlot), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s->fids, ht.fids.data(), ht.fids.size() * sizeof(NodeFids), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
   s->tv.edges = s->edges;
-  s->tv.fids = s->fids;
   s->tv.vocab = s->vocab;
   s->tv.arena = s->arena;
   s->tv.vocab_mask = ht.vocab_mask;
   s->tv.root_base = ht.root_base;
   s->tv.root_meta = ht.root_meta;
-  s->tv.root_node = 0;
+  s->tv.root_hash_fid = ht.root_hash_fid;
   s->n_nodes = ht.n_nodes;
   s->n_slots = ht.edges.size();
   s->n_words = ht.n_words;
   s->max_depth = ht.max_depth;
-  s->bytes = ht.edges.size() * sizeof(EdgeSlot) + ht.fids.size() * sizeof(NodeFids) +
+  s->bytes = ht.edges.size() * sizeof(EdgeSlot) +
              ht.vocab.size() * sizeof(VocabSlot) + ht.arena.size();
   *out = std::move(s);
   return EMQX_OK;
@@ -238,7 +237,8 @@ int ensure_ws(Workspace* w, uint64_t n) {
     const uint64_t cap = round_pow2(std::max<uint64_t>(ntiles, 64));
     HIP_TRY(dalloc(w->tile_fill, cap));
     HIP_TRY(dalloc(w->tile_defer, cap));
-    HIP_TRY(dalloc(w->tile_evals, cap));
+    HIP_TRY(dalloc(w->tile_stats, cap));
+    HIP_TRY(dalloc(w->spill, cap * w->spill_cap));
     w->cap_tiles = cap;
   }
   const uint64_t need_slab = std::max<uint64_t>(ntiles, 1) * w->slab_per_tile;
@@ -256,18 +256,41 @@ int ensure_ws(Workspace* w, uint64_t n) {
   return EMQX_OK;
 }
 
-__global__ void reduce_evals_kernel(const uint32_t* tile_evals, uint64_t ntiles, const uint32_t* deep_evals,
+// Sums per-tile node visits (+ the deep path's) into out[0] and takes the max stack depth
+// into out[1].
+__global__ void reduce_stats_kernel(const uint2* tile_stats, uint64_t ntiles, const uint32_t* deep_evals,
                                     uint64_t* out) {
   uint64_t s = 0;
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntiles; i += uint64_t(gridDim.x) * blockDim.x)
-    s += tile_evals[i];
+  uint32_t m = 0;
+  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntiles; i += uint64_t(gridDim.x) * blockDim.x) {
+    const uint2 v = tile_stats[i];
+    s += v.x;
+    m = max(m, v.y);
+  }
   for (int d = 32; d >= 1; d >>= 1) {
     const uint32_t lo = __shfl_xor(static_cast<uint32_t>(s), d, 64);
     const uint32_t hi = __shfl_xor(static_cast<uint32_t>(s >> 32), d, 64);
     s += (uint64_t(hi) << 32) | lo;
+    m = max(m, static_cast<uint32_t>(__shfl_xor(m, d, 64)));
   }
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(out), static_cast<unsigned long long>(s));
+  if ((threadIdx.x & 63) == 0) {
+    if (s) atomicAdd(reinterpret_cast<unsigned long long*>(out), static_cast<unsigned long long>(s));
+    if (m) atomicMax(reinterpret_cast<unsigned long long*>(out + 1), static_cast<unsigned long long>(m));
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out), static_cast<unsigned long long>(*deep_evals));
+}
+
+// Fast-kernel variant: EMQX_FAST_VARIANT overrides (A/B runs); otherwise deep tables get
+// the 2K-item stack and everything else the 1K stack with two items per lane.
+FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
+  static const int env_forced = [] {
+    const char* v = getenv("EMQX_FAST_VARIANT");
+    return v ? atoi(v) : -1;
+  }();
+  const int fv = e->forced_variant.load();
+  const int forced = fv >= 0 ? fv : env_forced;
+  if (forced >= 0 && forced < FAST_NVARIANTS) return static_cast<FastVariant>(forced);
+  return snap.max_depth > 12 ? FAST_K2_S2K : FAST_K1_S256;
 }
 
 // The pipeline on device buffers.  All inputs/outputs are device pointers.
@@ -288,7 +311,9 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
     a.slab = w->slab;
     a.tile_fill = w->tile_fill;
     a.tile_defer = w->tile_defer;
-    a.tile_evals = w->tile_evals;
+    a.tile_stats = w->tile_stats;
+    a.spill = w->spill;
+    a.spill_cap = w->spill_cap;
     a.ctrl = w->ctrl;
     a.deferred = w->deferred;
     a.deep_wids = w->deep_wids;
@@ -303,18 +328,18 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
     HIP_TRY(hipMemsetAsync(w->evals, 0, 2 * sizeof(uint64_t), s));
     HIP_TRY(hipMemsetAsync(w->deep_evals, 0, 4 * sizeof(uint32_t), s));
     HIP_TRY(hipEventRecord(w->ev0, s));
-    const FastVariant v = snap.max_depth > 14 ? FAST_STACK_2K : FAST_STACK_1K;
+    const FastVariant v = pick_variant(e, snap);
     HIP_TRY(launch_match_fast(a, v, s));
     HIP_TRY(hipEventRecord(w->evk, s));
     HIP_TRY(launch_match_deep(a, s));
     HIP_TRY(launch_scan(w->counts, n, d_out_off, w->partials, s));
     const uint64_t ntiles = (n + TILE_TOPICS - 1) / TILE_TOPICS;
-    hipLaunchKernelGGL(reduce_evals_kernel, dim3(64), dim3(256), 0, s, w->tile_evals, ntiles, w->deep_evals, w->evals);
+    hipLaunchKernelGGL(reduce_stats_kernel, dim3(64), dim3(256), 0, s, w->tile_stats, ntiles, w->deep_evals, w->evals);
     HIP_TRY(hipGetLastError());
     // one small readback: ctrl words, total, evals
     HIP_TRY(hipMemcpyAsync(w->h_rb, w->ctrl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(w->h_rb + 4, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(w->h_rb + 5, w->evals, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(w->h_rb + 5, w->evals, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(w->h_rb);
     const uint32_t ndef = c32[CTRL_DEFERRED], need_slab = c32[CTRL_NEED_SLAB], err = c32[CTRL_ERROR];
@@ -349,6 +374,7 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
     }
     e->last_deferred.store(ndef);
     e->last_evals.store(w->h_rb[5]);
+    e->last_max_stack.store(w->h_rb[6]);
     float ms = 0;
     (void)hipEventRecord(w->ev1, s);
     const uint64_t total = w->h_rb[4];
@@ -569,6 +595,7 @@ int emqx_stats_get(emqx_engine* e, emqx_stats* out) {
   }
   out->last_evals = e->last_evals.load();
   out->last_deferred = e->last_deferred.load();
+  out->last_max_stack = e->last_max_stack.load();
   out->last_match_ms = e->last_match_ms.load();
   out->last_kernel_ms = e->last_kernel_ms.load();
   return EMQX_OK;
@@ -585,6 +612,16 @@ const char* emqx_strerror(int code) {
     case EMQX_ETOODEEP: return "topic frontier too deep";
     default: return "unknown error";
   }
+}
+
+int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
+  if (!e || !key) return EMQX_EINVAL;
+  if (std::strcmp(key, "fast_variant") == 0) {
+    if (value < -1 || value >= FAST_NVARIANTS) return EMQX_EINVAL;
+    e->forced_variant.store(static_cast<int>(value));
+    return EMQX_OK;
+  }
+  return EMQX_ENOTFOUND;
 }
 
 const char* emqx_version(void) { return "emqx-match-mi355x 0.1.0 (gfx950)"; }

@@ -34,9 +34,11 @@ struct MatchArgs {
   uint64_t* slab;          // [ntiles * slab_cap]  (topic_local << 32) | fid
   uint32_t* tile_fill;     // [ntiles]
   uint64_t* tile_defer;    // [ntiles]
-  uint32_t* tile_evals;    // [ntiles]
+  uint2* tile_stats;       // [ntiles] {node visits, max stack depth}
   uint32_t* ctrl;          // [CTRL_WORDS]
   uint32_t* deferred;      // [n]
+  uint2* spill;            // [ntiles * spill_cap] HBM overflow of the per-wave LDS stack
+  uint32_t spill_cap;
   // deep path
   uint32_t* deep_wids;     // [deep_waves * DEEP_MAX_LEVELS]
   uint4* deep_stack;       // [deep_waves * deep_stack_cap]
@@ -47,8 +49,18 @@ struct MatchArgs {
   uint32_t* deep_evals;    // [1] (atomic)
 };
 
-// Which fast-kernel variant: stack capacity (items per wave).
-enum FastVariant { FAST_STACK_1K = 0, FAST_STACK_2K = 1 };
+// Fast-kernel variants: K items per lane per step, LDS stack / word-id capacity per wave.
+enum FastVariant {
+  FAST_K1_S1K = 0,   // 4 waves/block, stack 1024, K=1
+  FAST_K2_S1K = 1,   // 4 waves/block, stack 1024, K=2
+  FAST_K2_S2K = 2,   // 2 waves/block, stack 2048, K=2 (deep tables)
+  FAST_K2_S768 = 3,  // 4 waves/block, stack 768, K=2 (shallow tables, more waves per CU)
+  FAST_K4_S2K = 4,   // 2 waves/block, stack 2048, K=4
+  FAST_K1_S256 = 5,  // 4 waves/block, stack 256 (+HBM spill), 640 word ids: 32 waves/CU
+  FAST_K2_S512 = 6,  // 4 waves/block, stack 512 (+HBM spill), 640 word ids
+  FAST_K1_S384 = 7,  // 4 waves/block, stack 384 (+HBM spill), 640 word ids
+  FAST_NVARIANTS = 8
+};
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);
 hipError_t launch_match_deep(const MatchArgs& a, hipStream_t s);

@@ -11,7 +11,8 @@
 //   * edges:  each node owns a power-of-two slice of one global slot array, open-
 //             addressed by word id; '+' is the reserved word WID_PLUS, a non-final '#'
 //             the reserved word WID_HASH; a final '#' is the parent's hash filter.
-//   * fids:   per node {filter "<path>/#", filter "<path>"} ids, read only on a hit.
+//   * fids:   each slot carries its child's {filter "<path>/#", filter "<path>"} ids; the
+//             root's '#' filter is a table-view field.
 #pragma once
 
 #include <stdint.h>
@@ -37,14 +38,21 @@ constexpr uint32_t META_HAS_HASH = 1u << 7;     // filter "<child path>/#" exist
 constexpr uint32_t META_HAS_TERM = 1u << 8;     // filter "<child path>" exists
 constexpr uint32_t META_TERM_WILD = 1u << 9;    // ... and that filter is a wildcard filter
 
-// 16-byte edge slot: one global_load_dwordx4 per probe, 4 slots per 64-B line.
-struct alignas(16) EdgeSlot {
+// 32-byte edge slot: the child's record travels with the edge, so one probe (a dwordx4 +
+// a dwordx2 load of the same 32-B sector) yields everything the next level needs, including
+// the filter ids to emit — no dependent load on a hit.  A node's '+' edge, when present,
+// always sits in slot 0 of its array (no probing); literal edges are linear-probed by
+// mix32(wid).
+struct alignas(32) EdgeSlot {
   uint32_t wid;         // key (WID_NONE = empty)
   uint32_t child_base;  // first slot of the child's edge array
   uint32_t meta;        // META_* of the child
-  uint32_t child;       // child node id
+  uint32_t child;       // child node id (BFS order)
+  uint32_t hash_fid;    // filter "<child path>/#" or FID_NONE
+  uint32_t term_fid;    // filter "<child path>"   or FID_NONE
+  uint32_t pad0, pad1;
 };
-static_assert(sizeof(EdgeSlot) == 16, "EdgeSlot must be 16 bytes");
+static_assert(sizeof(EdgeSlot) == 32, "EdgeSlot must be 32 bytes");
 
 // 32-byte vocab slot; words up to 16 bytes are verified from `inl` without a second load.
 struct alignas(16) VocabSlot {
@@ -56,21 +64,15 @@ struct alignas(16) VocabSlot {
 };
 static_assert(sizeof(VocabSlot) == 32, "VocabSlot must be 32 bytes");
 
-struct NodeFids {
-  uint32_t hash_fid;  // id of "<path>/#" or FID_NONE
-  uint32_t term_fid;  // id of "<path>"   or FID_NONE
-};
-
 // Kernel-argument view of one committed snapshot.
 struct TableView {
   const EdgeSlot* edges;
-  const NodeFids* fids;
   const VocabSlot* vocab;
   const uint8_t* arena;
   uint32_t vocab_mask;
-  uint32_t root_base;
-  uint32_t root_meta;
-  uint32_t root_node;
+  uint32_t root_base;      // root's edge array
+  uint32_t root_meta;      // META_* of the root
+  uint32_t root_hash_fid;  // filter '#' or FID_NONE
 };
 
 EMQX_HD uint32_t fnv1a_step(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }

@@ -10,12 +10,13 @@
 //              lane splits its topic on '/', hashes every level (FNV-1a) and interns it in
 //              the vocab table (exact byte check) -> word ids in LDS.
 //     phase B  the frontier of all 64 topics is pooled in one LDS work stack.  Each step
-//              pops up to 64 (topic, node, level) items — one per lane — probes the node's
-//              literal edge and its '+' edge (16-B slots, linear probing), emits the
-//              children's '#' and terminal filters, and pushes the children; pushes and
-//              emissions are stream-compacted with wave ballots + popcount prefix sums.
-//              The stack is LIFO, which bounds it by ~64 x levels regardless of the
-//              frontier width.  No MFMA: this is pointer chasing.
+//              pops up to 64*K (topic, node, level) items — K per lane, all their loads in
+//              flight together — probes each node's '+' edge (slot 0, no search) and its
+//              literal edge (linear probing), emits the children's '#' and terminal filter
+//              ids (carried in the slot: no dependent load) and pushes the children; pushes
+//              and emissions are stream-compacted with wave ballots + popcount prefix sums.
+//              The stack is LIFO, which bounds it by ~64*K x levels whatever the frontier
+//              width.  No MFMA: this is pointer chasing.
 //     phase C  per-topic counts + a per-tile slab of (topic, filter id) entries.
 //   match_deep_kernel  topics that did not fit the fast path's LDS budget (very deep
 //              topics, or a frontier that overflowed the stack): one wavefront per topic,
@@ -29,7 +30,7 @@ namespace emqx {
 
 namespace {
 
-constexpr uint32_t MODE_ROUTES = 0, MODE_TRIE = 1;  // MODE_TRIE_WILDCARD = 2 is the default branch of term_ok
+constexpr uint32_t MODE_ROUTES = 0, MODE_TRIE = 1;  // MODE_TRIE_WILDCARD = 2: default branch
 
 __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -42,12 +43,19 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
-// Exclusive prefix of a small per-lane value (0..7) across the wave; *total = wave sum.
-__device__ __forceinline__ uint32_t wave_prefix_small(uint32_t v, uint32_t lane, uint32_t* total) {
-  const uint64_t b0 = __ballot(v & 1u), b1 = __ballot(v & 2u), b2 = __ballot(v & 4u);
+// Exclusive prefix of a small per-lane value (< 2^BITS) across the wave; *total = wave sum.
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t lane, uint32_t* total) {
   const uint64_t lt = lanemask_lt(lane);
-  *total = __popcll(b0) + 2u * __popcll(b1) + 4u * __popcll(b2);
-  return __popcll(b0 & lt) + 2u * __popcll(b1 & lt) + 4u * __popcll(b2 & lt);
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const uint64_t m = __ballot((v >> b) & 1u);
+    pre += static_cast<uint32_t>(__popcll(m & lt)) << b;
+    tot += static_cast<uint32_t>(__popcll(m)) << b;
+  }
+  *total = tot;
+  return pre;
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
@@ -65,6 +73,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+
 __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
 #pragma unroll
   for (uint32_t d = 32; d >= 1; d >>= 1) {
@@ -75,8 +84,17 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
   return v;
 }
 
-__device__ __forceinline__ uint4 load_slot(const EdgeSlot* p) {
-  return *reinterpret_cast<const uint4*>(p);
+// One edge slot = key/child record (16 B) + the child's filter ids (8 B).
+struct Slot {
+  uint4 a;  // wid, child_base, meta, child
+  uint2 f;  // hash_fid, term_fid
+};
+
+__device__ __forceinline__ Slot load_slot(const EdgeSlot* p) {
+  Slot s;
+  s.a = *reinterpret_cast<const uint4*>(p);
+  s.f = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p) + 16);
+  return s;
 }
 
 // Term-filter emission rule per mode (see include/emqx_match.h):
@@ -93,10 +111,9 @@ __device__ __forceinline__ bool term_ok(uint32_t meta, uint32_t mode, bool dolla
 
 // Vocab lookup with exact byte verification.  w0..w3 hold the first 16 bytes of the word;
 // longer words compare the tail against the arena.  Returns WID_NONE if absent.
-template <class ByteAt>
 __device__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, uint32_t w0,
-                                uint32_t w1, uint32_t w2, uint32_t w3, uint64_t wstart,
-                                ByteAt byte_at) {
+                                uint32_t w1, uint32_t w2, uint32_t w3, const uint8_t* tbytes,
+                                uint64_t wstart) {
   uint32_t i = vocab_slot0(h) & tv.vocab_mask;
   for (uint32_t k = 0; k <= tv.vocab_mask; ++k) {
     const uint4* vp = reinterpret_cast<const uint4*>(tv.vocab + i);
@@ -106,7 +123,7 @@ __device__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, u
       const uint4 in = vp[1];
       bool eq = in.x == w0 && in.y == w1 && in.z == w2 && in.w == w3;
       if (eq && len > 16) {
-        for (uint32_t b = 16; b < len && eq; ++b) eq = tv.arena[hd.w + b] == byte_at(wstart + b);
+        for (uint32_t b = 16; b < len && eq; ++b) eq = tv.arena[hd.w + b] == tbytes[wstart + b];
       }
       if (eq) return hd.z;
     }
@@ -115,17 +132,21 @@ __device__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, u
   return WID_NONE;
 }
 
-// Probe one node's edge array for `wid` (bounded linear probing).
-__device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t caplog, uint32_t wid, uint4* out) {
+// Probe one node's edge array for `wid` ('+' sits in slot 0; literals linear-probed).
+__device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t caplog, uint32_t wid, Slot* out) {
+  if (wid == WID_PLUS) {
+    *out = load_slot(arr);
+    return out->a.x == WID_PLUS;
+  }
   const uint32_t mask = (1u << caplog) - 1u;
   uint32_t i = mix32(wid) & mask;
   for (uint32_t k = 0; k <= mask; ++k) {
-    const uint4 s = load_slot(arr + i);
-    if (s.x == wid) {
+    const Slot s = load_slot(arr + i);
+    if (s.a.x == wid) {
       *out = s;
       return true;
     }
-    if (s.x == WID_NONE) return false;
+    if (s.a.x == WID_NONE) return false;
     i = (i + 1) & mask;
   }
   return false;
@@ -136,20 +157,19 @@ __device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t caplog, 
 // FID_NONE.
 template <class WidAt>
 __device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at) {
-  uint32_t base = tv.root_base, meta = tv.root_meta, node = tv.root_node;
+  uint32_t base = tv.root_base, meta = tv.root_meta, hash_fid = tv.root_hash_fid, term_fid = FID_NONE;
   for (uint32_t k = 0; k < nlev; ++k) {
     const uint32_t w = wid_at(k);
-    if (w == WID_HASH && k + 1 == nlev) {
-      return (meta & META_HAS_HASH) ? tv.fids[node].hash_fid : FID_NONE;
-    }
+    if (w == WID_HASH && k + 1 == nlev) return (meta & META_HAS_HASH) ? hash_fid : FID_NONE;
     if (w == WID_NONE || !(meta & META_HAS_EDGES)) return FID_NONE;
-    uint4 s;
+    Slot s;
     if (!probe_one(tv.edges + base, meta & META_CAPLOG2_MASK, w, &s)) return FID_NONE;
-    base = s.y;
-    meta = s.z;
-    node = s.w;
+    base = s.a.y;
+    meta = s.a.z;
+    hash_fid = s.f.x;
+    term_fid = s.f.y;
   }
-  return (meta & META_HAS_TERM) ? tv.fids[node].term_fid : FID_NONE;
+  return (meta & META_HAS_TERM) ? term_fid : FID_NONE;
 }
 
 // Item (8 B):  x = edge-array base of the node
@@ -162,46 +182,51 @@ __device__ __forceinline__ uint2 make_item(uint32_t base, uint32_t meta, bool dr
                               (tl << 8) | (widx << 16));
 }
 
-// One frontier step for one lane: probes literal + '+' edges of the item's node.
-struct StepOut {
-  uint4 s0, s1;  // found children (literal, plus)
-  bool f0, f1;
-};
-
-__device__ __forceinline__ void probe_pair(const EdgeSlot* arr, uint32_t caplog, bool need0,
-                                           uint32_t wid, bool need1, StepOut* o) {
-  const uint32_t mask = (1u << caplog) - 1u;
-  uint32_t i0 = mix32(wid) & mask;
-  uint32_t i1 = mix32(WID_PLUS) & mask;
-  o->f0 = o->f1 = false;
-  o->s0 = o->s1 = make_uint4(WID_NONE, 0, 0, 0);
-  for (uint32_t k = 0;; ++k) {
-    uint4 a = make_uint4(WID_NONE, 0, 0, 0), b = make_uint4(WID_NONE, 0, 0, 0);
-    if (need0) a = load_slot(arr + i0);
-    if (need1) b = load_slot(arr + i1);
-    if (need0) {
-      if (a.x == wid) {
-        o->s0 = a;
-        o->f0 = true;
-        need0 = false;
-      } else if (a.x == WID_NONE || k >= mask) {
-        need0 = false;
+// Probe the '+' edge (slot 0) and the literal edge of K nodes at once.  All first loads are
+// issued before any result is consumed; literal misses then walk their probe sequences.
+template <int K>
+__device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, const uint2 (&it)[K],
+                                            const bool (&needL0)[K], const uint32_t (&wid)[K],
+                                            const bool (&needP)[K], Slot (&lit)[K], bool (&fL)[K],
+                                            Slot (&pls)[K], bool (&fP)[K]) {
+  uint32_t li[K], lm[K], np[K];
+  bool needL[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const EdgeSlot* arr = edges + it[k].x;
+    lm[k] = (1u << (it[k].y & META_CAPLOG2_MASK)) - 1u;
+    li[k] = mix32(wid[k]) & lm[k];
+    np[k] = 0;
+    needL[k] = needL0[k];
+    fL[k] = false;
+    pls[k].a = make_uint4(WID_NONE, 0, 0, 0);
+    pls[k].f = make_uint2(FID_NONE, FID_NONE);
+    lit[k] = pls[k];
+    if (needP[k]) pls[k] = load_slot(arr);
+    if (needL[k]) lit[k] = load_slot(arr + li[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) fP[k] = needP[k] && pls[k].a.x == WID_PLUS;
+  while (true) {
+    bool more = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!needL[k]) continue;
+      if (lit[k].a.x == wid[k]) {
+        fL[k] = true;
+        needL[k] = false;
+      } else if (lit[k].a.x == WID_NONE || np[k] >= lm[k]) {
+        needL[k] = false;
       } else {
-        i0 = (i0 + 1) & mask;
+        li[k] = (li[k] + 1) & lm[k];
+        ++np[k];
+        more = true;
       }
     }
-    if (need1) {
-      if (b.x == WID_PLUS) {
-        o->s1 = b;
-        o->f1 = true;
-        need1 = false;
-      } else if (b.x == WID_NONE || k >= mask) {
-        need1 = false;
-      } else {
-        i1 = (i1 + 1) & mask;
-      }
-    }
-    if (!__any(need0 || need1)) break;
+    if (!__any(more)) break;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (needL[k]) lit[k] = load_slot(edges + it[k].x + li[k]);
   }
 }
 
@@ -210,13 +235,54 @@ __device__ __forceinline__ void probe_pair(const EdgeSlot* arr, uint32_t caplog,
 // ------------------------------------------------------------------------------------
 // Fast path
 // ------------------------------------------------------------------------------------
-template <int WAVES, int STACK_CAP, int WID_CAP>
+
+// Per-lane byte reader over the packed topic buffer: 16-B aligned register windows (one
+// dwordx4 load per window; the last window of the buffer is filled bytewise).
+struct ByteWin {
+  const uint8_t* p;
+  uint64_t lim;  // bytes [0, lim) are readable
+  bool vec_ok;   // p is 16-B aligned
+  uint64_t wbase;
+  uint4 w;
+  __device__ __forceinline__ ByteWin(const uint8_t* p_, uint64_t lim_)
+      : p(p_), lim(lim_), vec_ok((reinterpret_cast<uintptr_t>(p_) & 15u) == 0), wbase(~0ull),
+        w(make_uint4(0, 0, 0, 0)) {}
+  __device__ __forceinline__ uint32_t operator()(uint64_t i) {
+    const uint64_t b = i & ~15ull;
+    if (b != wbase) {
+      wbase = b;
+      if (vec_ok && b + 16 <= lim) {
+        w = *reinterpret_cast<const uint4*>(p + b);
+      } else {
+        uint64_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (b + k < lim) lo |= static_cast<uint64_t>(p[b + k]) << (8 * k);
+          if (b + 8 + k < lim) hi |= static_cast<uint64_t>(p[b + 8 + k]) << (8 * k);
+        }
+        w = make_uint4(static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32), static_cast<uint32_t>(hi),
+                       static_cast<uint32_t>(hi >> 32));
+      }
+    }
+    // value selects + shifts (a select between members would become a scratch load)
+    const uint32_t j = static_cast<uint32_t>(i & 15u);
+    const uint64_t lo = (static_cast<uint64_t>(w.y) << 32) | w.x;
+    const uint64_t hi = (static_cast<uint64_t>(w.w) << 32) | w.z;
+    const uint64_t q = (j & 8u) ? hi : lo;
+    return static_cast<uint32_t>(q >> (8u * (j & 7u))) & 0xFFu;
+  }
+};
+
+constexpr int ceil_log2(int v) { return v <= 1 ? 0 : 1 + ceil_log2((v + 1) / 2); }
+
+template <int WAVES, int STACK_CAP, int WID_CAP, int K>
 __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
+  static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
   struct WaveLds {
-    uint2 stack[STACK_CAP];  // phase A: staged topic bytes; phase B: work stack
-    uint32_t wids[WID_CAP];
-    uint32_t wend[64];
-    uint32_t cnt[64];
+    uint2 stack[STACK_CAP];  // work stack (LIFO); overflow spills its bottom half to HBM
+    uint32_t wids[WID_CAP];  // word ids of the tile's topics, topic after topic
+    uint32_t wend[64];       // per topic: end index of its word ids
+    uint32_t cnt[64];        // per topic: emitted filter ids
   };
   __shared__ WaveLds lds_all[WAVES];
 
@@ -231,31 +297,14 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   const uint32_t tcount = static_cast<uint32_t>(min<uint64_t>(TILE_TOPICS, a.n - t0));
   const bool valid = lane < tcount;
   const uint64_t t = t0 + lane;
-  const uint64_t b0 = a.toffs[t0];
-  const uint64_t b1 = a.toffs[t0 + tcount];
   uint64_t start = 0, end = 0;
   if (valid) {
     start = a.toffs[t];
     end = a.toffs[t + 1];
   }
 
-  // ---- phase A: stage bytes, tokenize, intern -------------------------------------
-  uint8_t* sbytes = reinterpret_cast<uint8_t*>(L.stack);
-  const uint64_t a0 = b0 & ~3ull;
-  const bool staged = ((reinterpret_cast<uintptr_t>(a.tbytes) & 3u) == 0) &&
-                      (b1 - a0) <= static_cast<uint64_t>(STACK_CAP) * 8u;
-  if (staged) {
-    const uint64_t nfull = (b1 - a0) >> 2;
-    const uint32_t* src32 = reinterpret_cast<const uint32_t*>(a.tbytes + a0);
-    uint32_t* dst32 = reinterpret_cast<uint32_t*>(sbytes);
-    for (uint64_t i = lane; i < nfull; i += 64) dst32[i] = src32[i];
-    for (uint64_t i = a0 + nfull * 4 + lane; i < b1; i += 64) sbytes[i - a0] = a.tbytes[i];
-  }
-  wave_sync();
-  auto byte_at = [&](uint64_t i) -> uint32_t {
-    return staged ? static_cast<uint32_t>(sbytes[i - a0]) : static_cast<uint32_t>(a.tbytes[i]);
-  };
-
+  // ---- phase A: tokenize + intern (one topic per lane) -----------------------------
+  ByteWin byte_at(a.tbytes, a.toffs[a.n]);  // bytes [0, toffs[n]) are readable
   uint32_t nlev = 0;
   bool wild = false, dollar = false;
   if (valid) {
@@ -302,7 +351,7 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
         uint32_t wid;
         if (len == 1 && w0 == '+') wid = WID_PLUS;
         else if (len == 1 && w0 == '#') wid = WID_HASH;
-        else wid = intern_word(tv, h, len, w0, w1, w2, w3, ws, byte_at);
+        else wid = intern_word(tv, h, len, w0, w1, w2, w3, a.tbytes, ws);
         L.wids[wbase + k] = wid;
         ++k;
         h = FNV_BASIS;
@@ -318,26 +367,16 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
 
   // ---- phase B: pooled frontier walk ------------------------------------------------
   uint64_t* slab = a.slab + tile * a.slab_cap;
+  uint2* spill = a.spill + tile * a.spill_cap;
   const uint32_t cap = a.slab_cap;
   const uint32_t mode = a.mode;
-  uint32_t cursor = 0;  // wave-uniform
-  uint32_t top = 0;     // wave-uniform
-  uint32_t evals = 0;   // per lane
+  uint32_t cursor = 0;    // wave-uniform
+  uint32_t top = 0;       // wave-uniform
+  uint32_t stop = 0;      // wave-uniform: items in the HBM spill
+  uint32_t maxtop = 0;    // wave-uniform (LDS + spill)
+  uint32_t evals = 0;     // per lane
 
-  auto emit = [&](uint32_t tl, bool e0, uint32_t g0, bool e1, uint32_t g1, bool e2, uint32_t g2,
-                  bool e3, uint32_t g3) {
-    const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u) + (e2 ? 1u : 0u) + (e3 ? 1u : 0u);
-    uint32_t tot;
-    uint32_t pos = cursor + wave_prefix_small(c, lane, &tot);
-    const uint64_t tag = static_cast<uint64_t>(tl) << 32;
-    if (e0) { if (pos < cap) slab[pos] = tag | g0; ++pos; }
-    if (e1) { if (pos < cap) slab[pos] = tag | g1; ++pos; }
-    if (e2) { if (pos < cap) slab[pos] = tag | g2; ++pos; }
-    if (e3) { if (pos < cap) slab[pos] = tag | g3; ++pos; }
-    if (c) atomicAdd(&L.cnt[tl], c);
-    cursor += tot;
-  };
-
+  // root: '#' emission, exact walk of wildcard topics, the root item
   {
     bool e0 = false, e1 = false, push = false;
     uint32_t g0 = 0, g1 = 0;
@@ -345,17 +384,14 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
     if (valid && !defer) {
       if (wild) {
         if (mode == MODE_ROUTES) {
-          const uint32_t f = exact_walk(tv, nlev, [&](uint32_t k) { return L.wids[wbase + k]; });
-          if (f != FID_NONE) {
-            e1 = true;
-            g1 = f;
-          }
+          g1 = exact_walk(tv, nlev, [&](uint32_t k) { return L.wids[wbase + k]; });
+          e1 = g1 != FID_NONE;
         }
       } else {
         evals = 1;  // the root visit, F_0
         if (!dollar && (tv.root_meta & META_HAS_HASH)) {
           e0 = true;  // filter '#'
-          g0 = tv.fids[tv.root_node].hash_fid;
+          g0 = tv.root_hash_fid;
         }
         if (tv.root_meta & META_HAS_EDGES) {
           push = true;
@@ -365,68 +401,128 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
         }
       }
     }
-    emit(lane, e0, g0, e1, g1, false, 0, false, 0);
+    const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u);
+    uint32_t tot;
+    uint32_t pos = wave_prefix<2>(c, lane, &tot);
+    const uint64_t tag = static_cast<uint64_t>(lane) << 32;
+    if (e0) { if (pos < cap) slab[pos] = tag | g0; ++pos; }
+    if (e1) { if (pos < cap) slab[pos] = tag | g1; ++pos; }
+    if (c) L.cnt[lane] = c;
+    cursor = tot;
     uint32_t ptot;
-    const uint32_t ppos = wave_prefix_small(push ? 1u : 0u, lane, &ptot);
+    const uint32_t ppos = wave_prefix<1>(push ? 1u : 0u, lane, &ptot);
     if (push) L.stack[ppos] = it;
     top = ptot;
+    maxtop = top;
     wave_sync();
   }
 
+  constexpr uint32_t POP = 64u * K;
+  constexpr uint32_t HALF = STACK_CAP / 2;
   while (true) {
     top = __builtin_amdgcn_readfirstlane(top);
+    stop = __builtin_amdgcn_readfirstlane(stop);
+    if (top < POP && stop > 0) {
+      // refill from the HBM spill (its newest items first)
+      const uint32_t r = min(stop, HALF - (top < HALF ? top : HALF));
+      for (uint32_t i = lane; i < r; i += 64) L.stack[top + i] = spill[stop - r + i];
+      top += r;
+      stop -= r;
+      wave_sync();
+    }
     if (top == 0) break;
-    const uint32_t room = static_cast<uint32_t>(STACK_CAP) - top;
-    const uint32_t nb = min(64u, min(top, room));
-    if (nb == 0) {
-      // Stack full: hand every topic still on the stack to the deep path.
-      uint64_t m = 0;
-      for (uint32_t i0 = 0; i0 < top; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        if (i < top) m |= 1ull << ((L.stack[i].y >> 8) & 63u);
+    if (top + POP > static_cast<uint32_t>(STACK_CAP)) {
+      if (stop + HALF <= a.spill_cap) {
+        // spill the bottom half of the LDS stack to HBM, slide the rest down
+        for (uint32_t i = lane; i < HALF; i += 64) spill[stop + i] = L.stack[i];
+        for (uint32_t i0 = 0; i0 < top - HALF; i0 += 64) {
+          const uint32_t i = i0 + lane;
+          uint2 v = make_uint2(0, 0);
+          if (i < top - HALF) v = L.stack[HALF + i];
+          wave_sync();
+          if (i < top - HALF) L.stack[i] = v;
+          wave_sync();
+        }
+        stop += HALF;
+        top -= HALF;
+      } else {
+        // spill full: hand every topic still pending to the deep path
+        uint64_t m = 0;
+        for (uint32_t i = lane; i < top; i += 64) m |= 1ull << ((L.stack[i].y >> 8) & 63u);
+        for (uint32_t i = lane; i < stop; i += 64) m |= 1ull << ((spill[i].y >> 8) & 63u);
+        defer_mask |= wave_or64(m);
+        top = 0;
+        stop = 0;
+        break;
       }
-      defer_mask |= wave_or64(m);
-      top = 0;
-      break;
     }
-    const bool act = lane < nb;
-    uint2 it = make_uint2(0, 0);
-    if (act) it = L.stack[top - nb + lane];
+    const uint32_t nb = min(POP, top);
+    uint2 it[K];
+    bool act[K], needL[K], needP[K], leaf[K], droot[K];
+    uint32_t wid[K], tl[K], widx[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t idx = lane + 64u * k;
+      act[k] = idx < nb;
+      it[k] = act[k] ? L.stack[top - nb + idx] : make_uint2(0, 0);
+    }
     top -= nb;
-    wave_sync();
-
-    const uint32_t caplog = it.y & META_CAPLOG2_MASK;
-    const bool hp = (it.y & META_HAS_PLUS) != 0;
-    const bool droot = (it.y & ITEM_DROOT) != 0;
-    const uint32_t tl = (it.y >> 8) & 63u;
-    const uint32_t widx = it.y >> 16;
-    uint32_t wid = WID_NONE;
-    bool leaf = false;
-    if (act) {
-      wid = L.wids[widx];
-      leaf = (widx + 1 == L.wend[tl]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      tl[k] = (it[k].y >> 8) & 63u;
+      widx[k] = it[k].y >> 16;
+      droot[k] = (it[k].y & ITEM_DROOT) != 0;
+      wid[k] = act[k] ? L.wids[widx[k]] : WID_NONE;
+      leaf[k] = act[k] && (widx[k] + 1 == L.wend[tl[k]]);
+      needL[k] = act[k] && wid[k] != WID_NONE;
+      needP[k] = act[k] && (it[k].y & META_HAS_PLUS);
     }
-    StepOut so;
-    probe_pair(tv.edges + it.x, caplog, act && wid != WID_NONE, wid, act && hp, &so);
-    evals += (so.f0 ? 1u : 0u) + (so.f1 ? 1u : 0u);
+    wave_sync();
+    Slot lit[K], pls[K];
+    bool fL[K], fP[K];
+    probe_items<K>(tv.edges, it, needL, wid, needP, lit, fL, pls, fP);
 
-    const uint32_t m0 = so.s0.z, m1 = so.s1.z;
-    const bool eh0 = so.f0 && (m0 & META_HAS_HASH);
-    const bool et0 = so.f0 && leaf && term_ok(m0, mode, droot);
-    const bool eh1 = so.f1 && (m1 & META_HAS_HASH);
-    const bool et1 = so.f1 && leaf && term_ok(m1, mode, false);
-    NodeFids fd0{FID_NONE, FID_NONE}, fd1{FID_NONE, FID_NONE};
-    if (eh0 || et0) fd0 = tv.fids[so.s0.w];
-    if (eh1 || et1) fd1 = tv.fids[so.s1.w];
-    emit(tl, eh0, fd0.hash_fid, et0, fd0.term_fid, eh1, fd1.hash_fid, et1, fd1.term_fid);
-
-    const bool p0 = so.f0 && !leaf && (m0 & META_HAS_EDGES);
-    const bool p1 = so.f1 && !leaf && (m1 & META_HAS_EDGES);
-    uint32_t ptot;
-    const uint32_t ppos = wave_prefix_small((p0 ? 1u : 0u) + (p1 ? 1u : 0u), lane, &ptot);
-    if (p0) L.stack[top + ppos] = make_item(so.s0.y, m0, false, tl, widx + 1);
-    if (p1) L.stack[top + ppos + (p0 ? 1u : 0u)] = make_item(so.s1.y, m1, false, tl, widx + 1);
-    top += ptot;
+    // emissions: per item ('#' and terminal filter of each found child)
+    bool eLh[K], eLt[K], ePh[K], ePt[K], pL[K], pP[K];
+    uint32_t ce[K], ecount = 0, pcount = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      evals += (fL[k] ? 1u : 0u) + (fP[k] ? 1u : 0u);
+      eLh[k] = fL[k] && (lit[k].a.z & META_HAS_HASH);
+      eLt[k] = fL[k] && leaf[k] && term_ok(lit[k].a.z, mode, droot[k]);
+      ePh[k] = fP[k] && (pls[k].a.z & META_HAS_HASH);
+      ePt[k] = fP[k] && leaf[k] && term_ok(pls[k].a.z, mode, false);
+      pL[k] = fL[k] && !leaf[k] && (lit[k].a.z & META_HAS_EDGES);
+      pP[k] = fP[k] && !leaf[k] && (pls[k].a.z & META_HAS_EDGES);
+      ce[k] = (eLh[k] ? 1u : 0u) + (eLt[k] ? 1u : 0u) + (ePh[k] ? 1u : 0u) + (ePt[k] ? 1u : 0u);
+      ecount += ce[k];
+      pcount += (pL[k] ? 1u : 0u) + (pP[k] ? 1u : 0u);
+    }
+    {
+      uint32_t tot;
+      uint32_t pos = cursor + wave_prefix<ceil_log2(4 * K + 1)>(ecount, lane, &tot);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t tag = static_cast<uint64_t>(tl[k]) << 32;
+        if (eLh[k]) { if (pos < cap) slab[pos] = tag | lit[k].f.x; ++pos; }
+        if (eLt[k]) { if (pos < cap) slab[pos] = tag | lit[k].f.y; ++pos; }
+        if (ePh[k]) { if (pos < cap) slab[pos] = tag | pls[k].f.x; ++pos; }
+        if (ePt[k]) { if (pos < cap) slab[pos] = tag | pls[k].f.y; ++pos; }
+        if (ce[k]) atomicAdd(&L.cnt[tl[k]], ce[k]);
+      }
+      cursor += tot;
+    }
+    {
+      uint32_t ptot;
+      uint32_t pos = top + wave_prefix<ceil_log2(2 * K + 1)>(pcount, lane, &ptot);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (pL[k]) L.stack[pos++] = make_item(lit[k].a.y, lit[k].a.z, false, tl[k], widx[k] + 1);
+        if (pP[k]) L.stack[pos++] = make_item(pls[k].a.y, pls[k].a.z, false, tl[k], widx[k] + 1);
+      }
+      top += ptot;
+      maxtop = max(maxtop, top + stop);
+    }
     wave_sync();
   }
 
@@ -437,7 +533,7 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   if (lane == 0) {
     a.tile_fill[tile] = cursor;
     a.tile_defer[tile] = defer_mask;
-    a.tile_evals[tile] = ev;
+    a.tile_stats[tile] = make_uint2(ev, maxtop);
     if (cursor > cap) atomicMax(&a.ctrl[CTRL_NEED_SLAB], cursor);
   }
   if (defer_mask) {
@@ -496,7 +592,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
           uint32_t wid;
           if (len == 1 && w0 == '+') { wid = WID_PLUS; wild = 1; }
           else if (len == 1 && w0 == '#') { wid = WID_HASH; wild = 1; }
-          else wid = intern_word(tv, h, len, w0, w1, w2, w3, ws, byte_at);
+          else wid = intern_word(tv, h, len, w0, w1, w2, w3, a.tbytes, ws);
           wids[k++] = wid;
           h = FNV_BASIS;
           len = 0;
@@ -516,7 +612,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     auto emit = [&](bool e0, uint32_t g0, bool e1, uint32_t g1, bool e2, uint32_t g2, bool e3, uint32_t g3) {
       const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u) + (e2 ? 1u : 0u) + (e3 ? 1u : 0u);
       uint32_t tot;
-      const uint32_t rel = wave_prefix_small(c, lane, &tot);
+      const uint32_t rel = wave_prefix<3>(c, lane, &tot);
       if (tot == 0) return;
       uint32_t base = 0;
       if (lane == 0) base = atomicAdd(&a.ctrl[CTRL_DEEP_FILL], tot);
@@ -543,7 +639,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     } else {
       if (lane == 0) evals = 1;
       const bool eh = lane == 0 && !dollar && (tv.root_meta & META_HAS_HASH);
-      emit(eh, eh ? tv.fids[tv.root_node].hash_fid : 0u, false, 0, false, 0, false, 0);
+      emit(eh, tv.root_hash_fid, false, 0, false, 0, false, 0);
       if (tv.root_meta & META_HAS_EDGES) {
         const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
         if (lane == 0)
@@ -560,38 +656,30 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
         break;
       }
       const bool act = lane < nb;
-      uint4 it = make_uint4(0, 0, 0, 0);
-      if (act) it = stack[top - nb + lane];
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if (act) q = stack[top - nb + lane];
       top -= nb;
       __threadfence_block();
-      const uint32_t caplog = it.y & META_CAPLOG2_MASK;
-      const bool hp = (it.y & META_HAS_PLUS) != 0;
-      const bool droot = (it.y & ITEM_DROOT) != 0;
-      const uint32_t widx = it.z;
-      uint32_t wid = WID_NONE;
-      bool leaf = false;
-      if (act) {
-        wid = wids[widx];
-        leaf = widx + 1 == nlev;
-      }
-      StepOut so;
-      probe_pair(tv.edges + it.x, caplog, act && wid != WID_NONE, wid, act && hp, &so);
-      evals += (so.f0 ? 1u : 0u) + (so.f1 ? 1u : 0u);
-      const uint32_t m0 = so.s0.z, m1 = so.s1.z;
-      const bool eh0 = so.f0 && (m0 & META_HAS_HASH);
-      const bool et0 = so.f0 && leaf && term_ok(m0, mode, droot);
-      const bool eh1 = so.f1 && (m1 & META_HAS_HASH);
-      const bool et1 = so.f1 && leaf && term_ok(m1, mode, false);
-      NodeFids fd0{FID_NONE, FID_NONE}, fd1{FID_NONE, FID_NONE};
-      if (eh0 || et0) fd0 = tv.fids[so.s0.w];
-      if (eh1 || et1) fd1 = tv.fids[so.s1.w];
-      emit(eh0, fd0.hash_fid, et0, fd0.term_fid, eh1, fd1.hash_fid, et1, fd1.term_fid);
-      const bool p0 = so.f0 && !leaf && (m0 & META_HAS_EDGES);
-      const bool p1 = so.f1 && !leaf && (m1 & META_HAS_EDGES);
+      const uint2 it[1] = {make_uint2(q.x, q.y)};
+      const bool droot = (q.y & ITEM_DROOT) != 0;
+      const uint32_t widx = q.z;
+      const uint32_t w[1] = {act ? wids[widx] : WID_NONE};
+      const bool leaf = act && widx + 1 == nlev;
+      const bool nL[1] = {act && w[0] != WID_NONE};
+      const bool nP[1] = {act && (q.y & META_HAS_PLUS) != 0};
+      Slot lit[1], pls[1];
+      bool fL[1], fP[1];
+      probe_items<1>(tv.edges, it, nL, w, nP, lit, fL, pls, fP);
+      evals += (fL[0] ? 1u : 0u) + (fP[0] ? 1u : 0u);
+      const uint32_t m0 = lit[0].a.z, m1 = pls[0].a.z;
+      emit(fL[0] && (m0 & META_HAS_HASH), lit[0].f.x, fL[0] && leaf && term_ok(m0, mode, droot), lit[0].f.y,
+           fP[0] && (m1 & META_HAS_HASH), pls[0].f.x, fP[0] && leaf && term_ok(m1, mode, false), pls[0].f.y);
+      const bool p0 = fL[0] && !leaf && (m0 & META_HAS_EDGES);
+      const bool p1 = fP[0] && !leaf && (m1 & META_HAS_EDGES);
       uint32_t ptot;
-      const uint32_t ppos = wave_prefix_small((p0 ? 1u : 0u) + (p1 ? 1u : 0u), lane, &ptot);
-      if (p0) stack[top + ppos] = make_uint4(so.s0.y, m0 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
-      if (p1) stack[top + ppos + (p0 ? 1u : 0u)] = make_uint4(so.s1.y, m1 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
+      const uint32_t ppos = wave_prefix<2>((p0 ? 1u : 0u) + (p1 ? 1u : 0u), lane, &ptot);
+      if (p0) stack[top + ppos] = make_uint4(lit[0].a.y, m0 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
+      if (p1) stack[top + ppos + (p0 ? 1u : 0u)] = make_uint4(pls[0].a.y, m1 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
       top += ptot;
       __threadfence_block();
     }
@@ -735,17 +823,25 @@ __global__ void zero_u32_kernel(uint32_t* p, const uint32_t* count) {
 // ------------------------------------------------------------------------------------
 // Launch wrappers
 // ------------------------------------------------------------------------------------
+template <int W, int S, int WC, int K>
+static void launch_fast_t(const MatchArgs& a, uint64_t ntiles, hipStream_t s) {
+  const uint64_t grid = (ntiles + W - 1) / W;
+  hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+}
+
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
   const uint64_t ntiles = (a.n + TILE_TOPICS - 1) / TILE_TOPICS;
   if (ntiles == 0) return hipSuccess;
-  if (v == FAST_STACK_2K) {
-    constexpr int W = 2;
-    const uint64_t grid = (ntiles + W - 1) / W;
-    hipLaunchKernelGGL((match_fast_kernel<W, 2048, 1024>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
-  } else {
-    constexpr int W = 4;
-    const uint64_t grid = (ntiles + W - 1) / W;
-    hipLaunchKernelGGL((match_fast_kernel<W, 1024, 1024>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+  switch (v) {
+    case FAST_K1_S1K: launch_fast_t<4, 1024, 1024, 1>(a, ntiles, s); break;
+    case FAST_K2_S1K: launch_fast_t<4, 1024, 1024, 2>(a, ntiles, s); break;
+    case FAST_K2_S2K: launch_fast_t<2, 2048, 1024, 2>(a, ntiles, s); break;
+    case FAST_K2_S768: launch_fast_t<4, 768, 768, 2>(a, ntiles, s); break;
+    case FAST_K4_S2K: launch_fast_t<2, 2048, 1024, 4>(a, ntiles, s); break;
+    case FAST_K1_S256: launch_fast_t<4, 256, 640, 1>(a, ntiles, s); break;
+    case FAST_K2_S512: launch_fast_t<4, 512, 640, 2>(a, ntiles, s); break;
+    case FAST_K1_S384: launch_fast_t<4, 384, 640, 1>(a, ntiles, s); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

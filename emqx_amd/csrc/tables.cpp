@@ -313,21 +313,29 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     return m;
   };
 
-  out.edges.assign(std::max<uint64_t>(total_slots, 1), EdgeSlot{WID_NONE, 0, 0, 0});
-  em.for_each([&](uint64_t key, uint32_t child) {
-    const uint32_t parent = static_cast<uint32_t>(key >> 32);
-    const uint32_t wid = static_cast<uint32_t>(key);
+  out.edges.assign(std::max<uint64_t>(total_slots, 1),
+                   EdgeSlot{WID_NONE, 0, 0, 0, FID_NONE, FID_NONE, 0, 0});
+  auto fill = [&](uint32_t parent, uint32_t wid, uint32_t child) {
     const uint32_t mask = (1u << caplog[parent]) - 1;
-    uint32_t i = mix32(wid) & mask;
+    uint32_t i = (wid == WID_PLUS) ? 0u : (mix32(wid) & mask);  // '+' pinned at slot 0
     while (out.edges[base[parent] + i].wid != WID_NONE) i = (i + 1) & mask;
     EdgeSlot& s = out.edges[base[parent] + i];
     s.wid = wid;
     s.child_base = base[child];
     s.meta = meta_of(child);
     s.child = new_id[child];
+    s.hash_fid = hash_fid[child];
+    s.term_fid = term_fid[child];
+  };
+  // '+' edges first so that each one lands in slot 0 of its parent's array
+  em.for_each([&](uint64_t key, uint32_t child) {
+    if (static_cast<uint32_t>(key) == WID_PLUS) fill(static_cast<uint32_t>(key >> 32), WID_PLUS, child);
   });
-  out.fids.resize(n_nodes);
-  for (uint64_t v = 0; v < n_nodes; ++v) out.fids[new_id[v]] = NodeFids{hash_fid[v], term_fid[v]};
+  em.for_each([&](uint64_t key, uint32_t child) {
+    const uint32_t wid = static_cast<uint32_t>(key);
+    if (wid != WID_PLUS) fill(static_cast<uint32_t>(key >> 32), wid, child);
+  });
+  out.root_hash_fid = hash_fid[0];
   out.root_base = base[0];
   out.root_meta = meta_of(0);
   out.n_nodes = n_nodes;

@@ -64,12 +64,12 @@ struct FilterStore {
 
 struct HostTables {
   std::vector<EdgeSlot> edges;
-  std::vector<NodeFids> fids;
   std::vector<VocabSlot> vocab;
   std::vector<uint8_t> arena;
   uint32_t vocab_mask = 0;
   uint32_t root_base = 0;
   uint32_t root_meta = 0;
+  uint32_t root_hash_fid = FID_NONE;
   uint64_t n_nodes = 0;
   uint64_t n_words = 0;
   uint32_t max_depth = 0;

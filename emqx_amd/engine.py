@@ -85,6 +85,9 @@ class Engine:
         check(_lib.lib().emqx_filter_name(self._h, fid, buf, n.value, ctypes.byref(n)), "emqx_filter_name")
         return buf.raw[: n.value]
 
+    def set_tuning(self, key: str, value: int) -> None:
+        check(_lib.lib().emqx_set_tuning(self._h, key.encode(), int(value)), "emqx_set_tuning")
+
     def commit(self) -> None:
         check(_lib.lib().emqx_commit(self._h), "emqx_commit")
 

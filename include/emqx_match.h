@@ -79,6 +79,7 @@ typedef struct emqx_stats {
   uint64_t epoch;            /* number of commits                                            */
   uint64_t last_evals;       /* node visits (SURVEY §8 d) of the last match call             */
   uint64_t last_deferred;    /* topics that took the deep-topic path in the last call        */
+  uint64_t last_max_stack;   /* deepest per-wave work stack of the last call (items)         */
   double last_build_ms;      /* host build time of the last commit                           */
   double last_match_ms;      /* device time of the last match call (hipEvent)                */
   double last_kernel_ms;     /* device time of its fused match kernel alone (hipEvent)       */
@@ -121,6 +122,10 @@ int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filt
                      uint64_t filter_len);
 /* emqx_topic:wildcard/1 (emqx_topic.erl:53-62): 1 if some level is exactly '+' or '#'. */
 int emqx_topic_wildcard(const uint8_t* topic, uint64_t len);
+
+/* Tuning hook (benchmarks / A-B runs).  Keys: "fast_variant" (-1 = automatic, 0..4 = a
+ * fixed kernel variant, see emqx_amd/csrc/kernels.h).  EMQX_ENOTFOUND for unknown keys. */
+int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value);
 
 const char* emqx_strerror(int code);
 /* Library version string. */
