@@ -47,10 +47,13 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics in the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cache", type=str, default=None,
+                    help="npz path: reuse the generated workload across runs (profiling passes)")
     ap.add_argument("--ab", type=str, default=None,
                     help="comma list of fast-kernel variants: interleaved A/B rounds in this process, "
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
+    ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per kernel launch from PMC (rocprofv3 FETCH_SIZE/WRITE_SIZE)")
     args = ap.parse_args()
@@ -71,8 +74,8 @@ def main():
 
     t0 = time.time()
     # every rank replicates the table (seed 2); each rank draws its own topic stream (weak scaling)
-    wl = W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
-                    topic_seed=None if rank == 0 else 1000 + rank)
+    wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
+                                                     topic_seed=None if rank == 0 else 1000 + rank))
     log(f"[rank {rank}] workload: {wl.n_filters} filters, {wl.n_topics} topics ({time.time() - t0:.1f}s)")
 
     t0 = time.time()
@@ -168,6 +171,15 @@ def main():
         "roofline": roofline,
     }
 
+    if args.diag:
+        eng.set_tuning("diag", 1)
+        eng.diag(reset=True)
+        step()
+        d = eng.diag(reset=True)
+        eng.set_tuning("diag", 0)
+        result["diag_per_topic"] = {k: round(v / n, 3) for k, v in d.items()}
+        result["diag_per_topic"]["kernel_ms_diag_call"] = round(eng.stats()["last_kernel_ms"], 4)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(wl, args)
     if rank == 0:
@@ -175,6 +187,18 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def load_or_make(args, rank, make):
+    from emqx_amd.workloads import Workload
+    path = f"{args.cache}.{rank}.npz" if args.cache else None
+    if path and os.path.exists(path):
+        z = np.load(path)
+        return Workload("B", (z["fb"], z["fo"]), (z["tb"], z["to"]))
+    wl = make()
+    if path:
+        np.savez(path, fb=wl.filters[0], fo=wl.filters[1], tb=wl.topics[0], to=wl.topics[1])
+    return wl
 
 
 def ab_variants(eng, step, args, wl):

@@ -31,7 +31,7 @@ EXPORTS = (
     "emqx_engine_create", "emqx_engine_destroy", "emqx_insert_filters", "emqx_delete_filters",
     "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
     "emqx_match_batch_device", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
-    "emqx_set_tuning", "emqx_strerror", "emqx_version",
+    "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_strerror", "emqx_version",
 )
 
 
@@ -88,6 +88,8 @@ def lib():
         "emqx_topic_match": (i32, [vp, u64, vp, u64]),
         "emqx_topic_wildcard": (i32, [vp, u64]),
         "emqx_set_tuning": (i32, [vp, ctypes.c_char_p, ctypes.c_int64]),
+        "emqx_diag_read": (i32, [vp, vp, u32, i32]),
+        "emqx_build_check": (i32, [vp, vp, u64, vp, ctypes.c_char_p, u64]),
         "emqx_strerror": (ctypes.c_char_p, [i32]),
         "emqx_version": (ctypes.c_char_p, []),
     }

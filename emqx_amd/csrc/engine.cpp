@@ -80,6 +80,7 @@ struct Workspace {
   uint64_t* tile_defer = nullptr;
   uint2* tile_stats = nullptr;
   uint2* spill = nullptr;
+  uint64_t* diag = nullptr;
   uint32_t spill_cap = 2048;  // items per tile
   uint64_t* partials = nullptr;
   uint32_t* ctrl = nullptr;         // CTRL_WORDS u32 + 2 u64 (evals) -> 8 u32 words + 2 u64
@@ -105,7 +106,7 @@ struct Workspace {
   ~Workspace() {
     (void)hipSetDevice(device);
     dfree(counts); dfree(deferred); dfree(deep_rank); dfree(slab); dfree(tile_fill);
-    dfree(tile_defer); dfree(tile_stats); dfree(spill); dfree(partials); dfree(ctrl); dfree(evals);
+    dfree(tile_defer); dfree(tile_stats); dfree(spill); dfree(diag); dfree(partials); dfree(ctrl); dfree(evals);
     dfree(deep_wids); dfree(deep_stack); dfree(deep_slab); dfree(deep_evals);
     dfree(d_tbytes); dfree(d_toffs); dfree(d_out_off); dfree(d_out_ids);
     if (h_rb) (void)hipHostFree(h_rb);
@@ -139,6 +140,7 @@ struct emqx_engine {
   std::atomic<double> last_match_ms{0};
   std::atomic<double> last_kernel_ms{0};
   std::atomic<int> forced_variant{-1};
+  std::atomic<bool> diag_on{false};
 };
 
 namespace {
@@ -217,6 +219,8 @@ int ensure_ws(Workspace* w, uint64_t n) {
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_rb), 16 * sizeof(uint64_t), hipHostMallocDefault));
     HIP_TRY(dalloc(w->ctrl, 16));
     HIP_TRY(dalloc(w->evals, 2));
+    HIP_TRY(dalloc(w->diag, DIAG_WORDS));
+    HIP_TRY(hipMemset(w->diag, 0, DIAG_WORDS * sizeof(uint64_t)));
   }
   if (!w->deep_ready) {
     HIP_TRY(dalloc(w->deep_wids, uint64_t(DEEP_WAVES) * DEEP_MAX_LEVELS));
@@ -313,6 +317,7 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
     a.tile_defer = w->tile_defer;
     a.tile_stats = w->tile_stats;
     a.spill = w->spill;
+    a.diag = e->diag_on.load() ? w->diag : nullptr;
     a.spill_cap = w->spill_cap;
     a.ctrl = w->ctrl;
     a.deferred = w->deferred;
@@ -621,7 +626,26 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
     e->forced_variant.store(static_cast<int>(value));
     return EMQX_OK;
   }
+  if (std::strcmp(key, "diag") == 0) {
+    e->diag_on.store(value != 0);
+    return EMQX_OK;
+  }
   return EMQX_ENOTFOUND;
+}
+
+int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset) {
+  if (!e || !out) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  std::vector<uint64_t> acc(DIAG_WORDS, 0), tmp(DIAG_WORDS);
+  std::lock_guard<std::mutex> g(e->ws_mu);
+  for (auto& w : e->all_ws) {
+    if (!w->diag) continue;
+    HIP_TRY(hipMemcpy(tmp.data(), w->diag, DIAG_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < DIAG_WORDS; ++i) acc[i] += tmp[i];
+    if (reset) HIP_TRY(hipMemset(w->diag, 0, DIAG_WORDS * sizeof(uint64_t)));
+  }
+  for (uint32_t i = 0; i < n && i < DIAG_WORDS; ++i) out[i] = acc[i];
+  return EMQX_OK;
 }
 
 const char* emqx_version(void) { return "emqx-match-mi355x 0.1.0 (gfx950)"; }

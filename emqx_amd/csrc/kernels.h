@@ -20,7 +20,21 @@ constexpr uint32_t CTRL_ERR_TOO_LONG = 1u;   // deferred topic longer than 65535
 constexpr uint32_t CTRL_ERR_TOO_DEEP = 2u;   // deep-path frontier exceeded its stack
 constexpr uint32_t CTRL_ERR_DEEP_SLAB = 4u;  // deep-path slab overflow
 
-constexpr int TILE_TOPICS = 64;        // topics per wave (one per lane during tokenizing)
+constexpr int TILE_TOPICS = 64;
+
+// Diagnostic counters (emqx_set_tuning("diag", 1); read with emqx_diag_read).
+enum Diag : uint32_t {
+  DIAG_STEPS = 0,        // frontier steps (wave iterations)
+  DIAG_ITEMS = 1,        // items popped
+  DIAG_LIT_PROBES = 2,   // literal lookups started
+  DIAG_LIT_HITS = 3,     // literal lookups that found the child
+  DIAG_LIT_EXTRA = 4,    // extra slot loads beyond the first (linear probing)
+  DIAG_PLUS_PROBES = 5,  // '+' slot loads
+  DIAG_PLUS_HITS = 6,
+  DIAG_EMITS = 7,        // filter ids emitted
+  DIAG_SPILLS = 8,       // stack spills to HBM
+  DIAG_WORDS = 16
+};        // topics per wave (one per lane during tokenizing)
 constexpr uint32_t DEEP_MAX_LEVELS = 65536;
 
 struct MatchArgs {
@@ -37,6 +51,7 @@ struct MatchArgs {
   uint2* tile_stats;       // [ntiles] {node visits, max stack depth}
   uint32_t* ctrl;          // [CTRL_WORDS]
   uint32_t* deferred;      // [n]
+  uint64_t* diag;          // optional [DIAG_WORDS] counters (nullptr = off)
   uint2* spill;            // [ntiles * spill_cap] HBM overflow of the per-wave LDS stack
   uint32_t spill_cap;
   // deep path

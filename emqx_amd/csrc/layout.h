@@ -37,20 +37,28 @@ constexpr uint32_t META_HAS_EDGES = 1u << 6;    // child has any edge (literal/'
 constexpr uint32_t META_HAS_HASH = 1u << 7;     // filter "<child path>/#" exists
 constexpr uint32_t META_HAS_TERM = 1u << 8;     // filter "<child path>" exists
 constexpr uint32_t META_TERM_WILD = 1u << 9;    // ... and that filter is a wildcard filter
+constexpr uint32_t META_PH = 1u << 10;          // literal edges perfect-hashed (seed below); else 2-choice cuckoo
+constexpr uint32_t META_LITF_EXACT = 1u << 11;  // lit_lo = the child's only literal edge word
+constexpr uint32_t META_LITF_NONE = 1u << 12;   // the child has no literal edge at all
+constexpr uint32_t META_SEED_SHIFT = 16;        // 8-bit perfect-hash seed
+constexpr uint32_t PH_MAX_CAPLOG = 15;
 
-// 32-byte edge slot: the child's record travels with the edge, so one probe (a dwordx4 +
-// a dwordx2 load of the same 32-B sector) yields everything the next level needs, including
-// the filter ids to emit — no dependent load on a hit.  A node's '+' edge, when present,
-// always sits in slot 0 of its array (no probing); literal edges are linear-probed by
-// mix32(wid).
+// 32-byte edge slot: the child's record travels with the edge, so one probe (two dwordx4
+// loads of one 32-B sector) yields everything the next level needs: the filter ids to emit
+// and a filter over the child's literal edges, tested against the topic's next word before
+// the child is even pushed.  A node's '+' edge, when present, always sits in slot 0 of its
+// array; literal edges are perfect-hashed by a per-node seed found at build time (one load
+// per lookup, hit or miss), or — in the few wide nodes where no seed fits — cuckoo-hashed
+// over two candidate slots that are loaded together (still one dependent round trip).
 struct alignas(32) EdgeSlot {
   uint32_t wid;         // key (WID_NONE = empty)
   uint32_t child_base;  // first slot of the child's edge array
-  uint32_t meta;        // META_* of the child
+  uint32_t meta;        // META_* (+ seed) of the child
   uint32_t child;       // child node id (BFS order)
   uint32_t hash_fid;    // filter "<child path>/#" or FID_NONE
   uint32_t term_fid;    // filter "<child path>"   or FID_NONE
-  uint32_t pad0, pad1;
+  uint32_t lit_lo;      // literal-edge filter of the child: the word (LITF_EXACT) or a
+  uint32_t lit_hi;      //   2-probe 64-bit Bloom mask (all ones when the child is wide)
 };
 static_assert(sizeof(EdgeSlot) == 32, "EdgeSlot must be 32 bytes");
 
@@ -89,5 +97,38 @@ EMQX_HD uint32_t mix32(uint32_t x) {
 }
 
 EMQX_HD uint32_t vocab_slot0(uint32_t hash) { return mix32(hash ^ 0x9e3779b9u); }
+
+// Slot of literal word `wid` in a perfect-hashed node's array (mask = cap - 1).
+EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask) {
+  return mix32(wid ^ (seed * 0x9E3779B1u + 0x7F4A7C15u)) & mask;
+}
+
+// The two candidate slots of `wid` in a cuckoo-hashed (wide) node's array, both in
+// [1, cap) — slot 0 belongs to '+' (mask = cap - 1 >= 2).
+EMQX_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return static_cast<uint32_t>((static_cast<uint64_t>(a) * b) >> 32);
+}
+// `seed` (7 bits) is re-drawn by the builder until every word of the node fits.
+EMQX_HD uint32_t cuckoo_slot1(uint32_t wid, uint32_t seed, uint32_t mask) {
+  return 1u + mulhi32(mix32(wid ^ (0x3C6EF372u + seed * 0x9E3779B9u)), mask);
+}
+EMQX_HD uint32_t cuckoo_slot2(uint32_t wid, uint32_t seed, uint32_t mask) {
+  const uint32_t a = cuckoo_slot1(wid, seed, mask);
+  const uint32_t b = 1u + mulhi32(mix32(wid ^ (0xDAA66D2Bu + seed * 0x7F4A7C15u)), mask);
+  return b != a ? b : (a == mask ? 1u : a + 1u);
+}
+constexpr uint32_t CUCKOO_SEEDS = 128;
+
+EMQX_HD uint32_t litf_hash(uint32_t wid) { return mix32(wid ^ 0xA5A5A5A5u); }
+
+// May the child (meta, lit_lo, lit_hi) have a literal edge for `wid`?  No false negatives.
+EMQX_HD bool litf_may_contain(uint32_t meta, uint32_t lo, uint32_t hi, uint32_t wid) {
+  if (meta & META_LITF_NONE) return false;
+  if (meta & META_LITF_EXACT) return lo == wid;
+  const uint32_t h = litf_hash(wid);
+  const uint32_t b1 = h & 63u, b2 = (h >> 6) & 63u;
+  const uint32_t w1 = b1 < 32 ? lo : hi, w2 = b2 < 32 ? lo : hi;
+  return ((w1 >> (b1 & 31u)) & 1u) && ((w2 >> (b2 & 31u)) & 1u);
+}
 
 }  // namespace emqx

@@ -84,16 +84,23 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
   return v;
 }
 
-// One edge slot = key/child record (16 B) + the child's filter ids (8 B).
+// One edge slot: key/child record + the child's filter ids and literal-edge filter.
 struct Slot {
   uint4 a;  // wid, child_base, meta, child
-  uint2 f;  // hash_fid, term_fid
+  uint4 f;  // hash_fid, term_fid, lit_lo, lit_hi
 };
 
 __device__ __forceinline__ Slot load_slot(const EdgeSlot* p) {
   Slot s;
   s.a = *reinterpret_cast<const uint4*>(p);
-  s.f = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p) + 16);
+  s.f = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(p) + 16);
+  return s;
+}
+
+__device__ __forceinline__ Slot empty_slot() {
+  Slot s;
+  s.a = make_uint4(WID_NONE, 0, 0, 0);
+  s.f = make_uint4(FID_NONE, FID_NONE, 0, 0);
   return s;
 }
 
@@ -132,24 +139,27 @@ __device__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, u
   return WID_NONE;
 }
 
-// Probe one node's edge array for `wid` ('+' sits in slot 0; literals linear-probed).
-__device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t caplog, uint32_t wid, Slot* out) {
+// Probe one node's edge array for `wid` ('+' sits in slot 0; literals perfect-hashed, or
+// cuckoo-hashed over two candidate slots, according to the node's meta).
+__device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t meta, uint32_t wid, Slot* out) {
   if (wid == WID_PLUS) {
     *out = load_slot(arr);
     return out->a.x == WID_PLUS;
   }
-  const uint32_t mask = (1u << caplog) - 1u;
-  uint32_t i = mix32(wid) & mask;
-  for (uint32_t k = 0; k <= mask; ++k) {
-    const Slot s = load_slot(arr + i);
-    if (s.a.x == wid) {
-      *out = s;
-      return true;
-    }
-    if (s.a.x == WID_NONE) return false;
-    i = (i + 1) & mask;
+  const uint32_t mask = (1u << (meta & META_CAPLOG2_MASK)) - 1u;
+  if (meta & META_PH) {
+    *out = load_slot(arr + lit_slot(wid, (meta >> META_SEED_SHIFT) & 255u, mask));
+    return out->a.x == wid;
   }
-  return false;
+  const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
+  const Slot s1 = load_slot(arr + cuckoo_slot1(wid, sd, mask));
+  const Slot s2 = load_slot(arr + cuckoo_slot2(wid, sd, mask));
+  if (s1.a.x == wid) {
+    *out = s1;
+    return true;
+  }
+  *out = s2;
+  return s2.a.x == wid;
 }
 
 // Byte-identical lookup of a wildcard "topic" for match_routes (emqx_router.erl:130):
@@ -163,7 +173,7 @@ __device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at)
     if (w == WID_HASH && k + 1 == nlev) return (meta & META_HAS_HASH) ? hash_fid : FID_NONE;
     if (w == WID_NONE || !(meta & META_HAS_EDGES)) return FID_NONE;
     Slot s;
-    if (!probe_one(tv.edges + base, meta & META_CAPLOG2_MASK, w, &s)) return FID_NONE;
+    if (!probe_one(tv.edges + base, meta, w, &s)) return FID_NONE;
     base = s.a.y;
     meta = s.a.z;
     hash_fid = s.f.x;
@@ -173,60 +183,65 @@ __device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at)
 }
 
 // Item (8 B):  x = edge-array base of the node
-//              y = caplog2 (5) | has_plus (1) | dollar_root (1) | - (1) | topic (6) | - (2) | widx (16)
-constexpr uint32_t ITEM_DROOT = 1u << 6;
+//   y = widx (10) | topic (6) | dollar_root (1) | has_plus (1) | no_literal (1) | ph (1) |
+//       hashing (12): ph ? caplog (4) | seed (8) << 4 : caplog (5) | cuckoo seed (7) << 5
+constexpr uint32_t IT_TOPIC_SHIFT = 10;
+constexpr uint32_t IT_DROOT = 1u << 16;
+constexpr uint32_t IT_PLUS = 1u << 17;
+constexpr uint32_t IT_NOLIT = 1u << 18;
+constexpr uint32_t IT_PH = 1u << 19;
+constexpr uint32_t IT_HASH_SHIFT = 20;
 
-__device__ __forceinline__ uint2 make_item(uint32_t base, uint32_t meta, bool droot, uint32_t tl,
+__device__ __forceinline__ uint2 make_item(uint32_t base, uint32_t meta, bool droot, bool nolit, uint32_t tl,
                                            uint32_t widx) {
-  return make_uint2(base, (meta & (META_CAPLOG2_MASK | META_HAS_PLUS)) | (droot ? ITEM_DROOT : 0u) |
-                              (tl << 8) | (widx << 16));
+  const bool ph = (meta & META_PH) != 0;
+  const uint32_t caplog = meta & META_CAPLOG2_MASK;
+  const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
+  const uint32_t hp = ph ? (caplog | (sd << 4)) : (caplog | (sd << 5));
+  return make_uint2(base, widx | (tl << IT_TOPIC_SHIFT) | (droot ? IT_DROOT : 0u) |
+                              ((meta & META_HAS_PLUS) ? IT_PLUS : 0u) | (nolit ? IT_NOLIT : 0u) |
+                              (ph ? IT_PH : 0u) | (hp << IT_HASH_SHIFT));
 }
 
-// Probe the '+' edge (slot 0) and the literal edge of K nodes at once.  All first loads are
-// issued before any result is consumed; literal misses then walk their probe sequences.
+__device__ __forceinline__ uint32_t item_topic(uint2 it) { return (it.y >> IT_TOPIC_SHIFT) & 63u; }
+
+// Probe the '+' edge (slot 0) and the literal edge of K nodes at once: every load is issued
+// before any result is consumed, so a step costs one dependent round trip.  Perfect-hashed
+// nodes answer in one slot load; cuckoo-hashed (wide) nodes load both candidate slots.
 template <int K>
-__device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, const uint2 (&it)[K],
-                                            const bool (&needL0)[K], const uint32_t (&wid)[K],
+__device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, const uint32_t (&base)[K],
+                                            const uint32_t (&hparams)[K], const bool (&isph)[K],
+                                            const bool (&needL)[K], const uint32_t (&wid)[K],
                                             const bool (&needP)[K], Slot (&lit)[K], bool (&fL)[K],
-                                            Slot (&pls)[K], bool (&fP)[K]) {
-  uint32_t li[K], lm[K], np[K];
-  bool needL[K];
+                                            Slot (&pls)[K], bool (&fP)[K], uint32_t& extra) {
+  Slot alt[K];
+  bool need2[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const EdgeSlot* arr = edges + it[k].x;
-    lm[k] = (1u << (it[k].y & META_CAPLOG2_MASK)) - 1u;
-    li[k] = mix32(wid[k]) & lm[k];
-    np[k] = 0;
-    needL[k] = needL0[k];
-    fL[k] = false;
-    pls[k].a = make_uint4(WID_NONE, 0, 0, 0);
-    pls[k].f = make_uint2(FID_NONE, FID_NONE);
+    const EdgeSlot* arr = edges + base[k];
+    const uint32_t caplog = isph[k] ? (hparams[k] & 15u) : (hparams[k] & 31u);
+    const uint32_t sd = isph[k] ? (hparams[k] >> 4) : (hparams[k] >> 5);
+    const uint32_t mask = (1u << caplog) - 1u;
+    const uint32_t i1 = isph[k] ? lit_slot(wid[k], sd, mask) : cuckoo_slot1(wid[k], sd, mask);
+    need2[k] = needL[k] && !isph[k];
+    pls[k] = empty_slot();
     lit[k] = pls[k];
+    alt[k] = pls[k];
     if (needP[k]) pls[k] = load_slot(arr);
-    if (needL[k]) lit[k] = load_slot(arr + li[k]);
+    if (needL[k]) lit[k] = load_slot(arr + i1);
+    if (need2[k]) {
+      alt[k] = load_slot(arr + cuckoo_slot2(wid[k], sd, mask));
+      ++extra;
+    }
   }
 #pragma unroll
-  for (int k = 0; k < K; ++k) fP[k] = needP[k] && pls[k].a.x == WID_PLUS;
-  while (true) {
-    bool more = false;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (!needL[k]) continue;
-      if (lit[k].a.x == wid[k]) {
-        fL[k] = true;
-        needL[k] = false;
-      } else if (lit[k].a.x == WID_NONE || np[k] >= lm[k]) {
-        needL[k] = false;
-      } else {
-        li[k] = (li[k] + 1) & lm[k];
-        ++np[k];
-        more = true;
-      }
+  for (int k = 0; k < K; ++k) {
+    fP[k] = needP[k] && pls[k].a.x == WID_PLUS;
+    fL[k] = needL[k] && lit[k].a.x == wid[k];
+    if (need2[k] && !fL[k] && alt[k].a.x == wid[k]) {
+      lit[k] = alt[k];
+      fL[k] = true;
     }
-    if (!__any(more)) break;
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      if (needL[k]) lit[k] = load_slot(edges + it[k].x + li[k]);
   }
 }
 
@@ -275,9 +290,10 @@ struct ByteWin {
 
 constexpr int ceil_log2(int v) { return v <= 1 ? 0 : 1 + ceil_log2((v + 1) / 2); }
 
-template <int WAVES, int STACK_CAP, int WID_CAP, int K>
+template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG>
 __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
+  static_assert(WID_CAP <= 1024, "item word index is 10 bits");
   struct WaveLds {
     uint2 stack[STACK_CAP];  // work stack (LIFO); overflow spills its bottom half to HBM
     uint32_t wids[WID_CAP];  // word ids of the tile's topics, topic after topic
@@ -375,6 +391,7 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   uint32_t stop = 0;      // wave-uniform: items in the HBM spill
   uint32_t maxtop = 0;    // wave-uniform (LDS + spill)
   uint32_t evals = 0;     // per lane
+  uint32_t dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // diagnostic counters (per lane)
 
   // root: '#' emission, exact walk of wildcard topics, the root item
   {
@@ -397,7 +414,7 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
           push = true;
           // '$' rule (emqx_trie.erl:272-279): no root-level '+' or '#' for '$' topics
           const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
-          it = make_item(tv.root_base, rmeta, dollar, lane, wbase);
+          it = make_item(tv.root_base, rmeta, dollar, false, lane, wbase);
         }
       }
     }
@@ -445,11 +462,12 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
         }
         stop += HALF;
         top -= HALF;
+        if (DIAG) dg[8] += lane == 0 ? 1u : 0u;
       } else {
         // spill full: hand every topic still pending to the deep path
         uint64_t m = 0;
-        for (uint32_t i = lane; i < top; i += 64) m |= 1ull << ((L.stack[i].y >> 8) & 63u);
-        for (uint32_t i = lane; i < stop; i += 64) m |= 1ull << ((spill[i].y >> 8) & 63u);
+        for (uint32_t i = lane; i < top; i += 64) m |= 1ull << item_topic(L.stack[i]);
+        for (uint32_t i = lane; i < stop; i += 64) m |= 1ull << item_topic(spill[i]);
         defer_mask |= wave_or64(m);
         top = 0;
         stop = 0;
@@ -458,8 +476,8 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
     }
     const uint32_t nb = min(POP, top);
     uint2 it[K];
-    bool act[K], needL[K], needP[K], leaf[K], droot[K];
-    uint32_t wid[K], tl[K], widx[K];
+    bool act[K], needL[K], needP[K], leaf[K], droot[K], isph[K];
+    uint32_t wid[K], tl[K], widx[K], ibase[K], hpar[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const uint32_t idx = lane + 64u * k;
@@ -469,22 +487,36 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
     top -= nb;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      tl[k] = (it[k].y >> 8) & 63u;
-      widx[k] = it[k].y >> 16;
-      droot[k] = (it[k].y & ITEM_DROOT) != 0;
+      tl[k] = item_topic(it[k]);
+      widx[k] = it[k].y & 1023u;
+      droot[k] = (it[k].y & IT_DROOT) != 0;
+      isph[k] = (it[k].y & IT_PH) != 0;
+      hpar[k] = it[k].y >> IT_HASH_SHIFT;
+      ibase[k] = it[k].x;
       wid[k] = act[k] ? L.wids[widx[k]] : WID_NONE;
       leaf[k] = act[k] && (widx[k] + 1 == L.wend[tl[k]]);
-      needL[k] = act[k] && wid[k] != WID_NONE;
-      needP[k] = act[k] && (it[k].y & META_HAS_PLUS);
+      needL[k] = act[k] && wid[k] != WID_NONE && !(it[k].y & IT_NOLIT);
+      needP[k] = act[k] && (it[k].y & IT_PLUS);
     }
     wave_sync();
     Slot lit[K], pls[K];
     bool fL[K], fP[K];
-    probe_items<K>(tv.edges, it, needL, wid, needP, lit, fL, pls, fP);
+    probe_items<K>(tv.edges, ibase, hpar, isph, needL, wid, needP, lit, fL, pls, fP, dg[4]);
+    if (DIAG) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        dg[1] += act[k] ? 1u : 0u;
+        dg[2] += needL[k] ? 1u : 0u;
+        dg[3] += fL[k] ? 1u : 0u;
+        dg[5] += needP[k] ? 1u : 0u;
+        dg[6] += fP[k] ? 1u : 0u;
+      }
+      dg[0] += 1;
+    }
 
     // emissions: per item ('#' and terminal filter of each found child)
-    bool eLh[K], eLt[K], ePh[K], ePt[K], pL[K], pP[K];
-    uint32_t ce[K], ecount = 0, pcount = 0;
+    bool eLh[K], eLt[K], ePh[K], ePt[K], pL[K], pP[K], nlL[K], nlP[K];
+    uint32_t ce[K], nwid[K], ecount = 0, pcount = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       evals += (fL[k] ? 1u : 0u) + (fP[k] ? 1u : 0u);
@@ -494,6 +526,13 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
       ePt[k] = fP[k] && leaf[k] && term_ok(pls[k].a.z, mode, false);
       pL[k] = fL[k] && !leaf[k] && (lit[k].a.z & META_HAS_EDGES);
       pP[k] = fP[k] && !leaf[k] && (pls[k].a.z & META_HAS_EDGES);
+      // the topic's next word decides whether a child's literal edges can matter at all;
+      // a child with nothing left to probe is not pushed
+      nwid[k] = (pL[k] || pP[k]) ? L.wids[widx[k] + 1] : WID_NONE;
+      nlL[k] = nwid[k] == WID_NONE || !litf_may_contain(lit[k].a.z, lit[k].f.z, lit[k].f.w, nwid[k]);
+      nlP[k] = nwid[k] == WID_NONE || !litf_may_contain(pls[k].a.z, pls[k].f.z, pls[k].f.w, nwid[k]);
+      pL[k] = pL[k] && !(nlL[k] && !(lit[k].a.z & META_HAS_PLUS));
+      pP[k] = pP[k] && !(nlP[k] && !(pls[k].a.z & META_HAS_PLUS));
       ce[k] = (eLh[k] ? 1u : 0u) + (eLt[k] ? 1u : 0u) + (ePh[k] ? 1u : 0u) + (ePt[k] ? 1u : 0u);
       ecount += ce[k];
       pcount += (pL[k] ? 1u : 0u) + (pP[k] ? 1u : 0u);
@@ -511,14 +550,15 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
         if (ce[k]) atomicAdd(&L.cnt[tl[k]], ce[k]);
       }
       cursor += tot;
+      if (DIAG) dg[7] += ecount;
     }
     {
       uint32_t ptot;
       uint32_t pos = top + wave_prefix<ceil_log2(2 * K + 1)>(pcount, lane, &ptot);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        if (pL[k]) L.stack[pos++] = make_item(lit[k].a.y, lit[k].a.z, false, tl[k], widx[k] + 1);
-        if (pP[k]) L.stack[pos++] = make_item(pls[k].a.y, pls[k].a.z, false, tl[k], widx[k] + 1);
+        if (pL[k]) L.stack[pos++] = make_item(lit[k].a.y, lit[k].a.z, false, nlL[k], tl[k], widx[k] + 1);
+        if (pP[k]) L.stack[pos++] = make_item(pls[k].a.y, pls[k].a.z, false, nlP[k], tl[k], widx[k] + 1);
       }
       top += ptot;
       maxtop = max(maxtop, top + stop);
@@ -528,6 +568,14 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
 
   // ---- phase C: per-topic counts, tile bookkeeping ---------------------------------
   wave_sync();
+  if (DIAG && a.diag) {
+    dg[0] = lane == 0 ? dg[0] : 0u;  // steps are wave-uniform
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const uint32_t v = wave_sum(dg[i]);
+      if (lane == 0 && v) atomicAdd(reinterpret_cast<unsigned long long*>(a.diag + i), static_cast<unsigned long long>(v));
+    }
+  }
   if (valid) a.counts[t] = ((defer_mask >> lane) & 1ull) ? 0u : L.cnt[lane];
   const uint32_t ev = wave_sum(evals);
   if (lane == 0) {
@@ -643,7 +691,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       if (tv.root_meta & META_HAS_EDGES) {
         const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
         if (lane == 0)
-          stack[0] = make_uint4(tv.root_base, (rmeta & (META_CAPLOG2_MASK | META_HAS_PLUS)) | (dollar ? ITEM_DROOT : 0u), 0u, 0u);
+          stack[0] = make_uint4(tv.root_base, rmeta, 0u, dollar ? 1u : 0u);  // {base, meta, widx, droot}
         top = 1;
       }
     }
@@ -660,16 +708,20 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       if (act) q = stack[top - nb + lane];
       top -= nb;
       __threadfence_block();
-      const uint2 it[1] = {make_uint2(q.x, q.y)};
-      const bool droot = (q.y & ITEM_DROOT) != 0;
+      const bool droot = (q.w & 1u) != 0;
       const uint32_t widx = q.z;
+      const uint32_t qbase[1] = {q.x};
+      const bool qph[1] = {(q.y & META_PH) != 0};
+      const uint32_t qsd = (q.y >> META_SEED_SHIFT) & 255u;
+      const uint32_t qhp[1] = {qph[0] ? ((q.y & 15u) | (qsd << 4)) : ((q.y & META_CAPLOG2_MASK) | (qsd << 5))};
       const uint32_t w[1] = {act ? wids[widx] : WID_NONE};
       const bool leaf = act && widx + 1 == nlev;
       const bool nL[1] = {act && w[0] != WID_NONE};
       const bool nP[1] = {act && (q.y & META_HAS_PLUS) != 0};
       Slot lit[1], pls[1];
       bool fL[1], fP[1];
-      probe_items<1>(tv.edges, it, nL, w, nP, lit, fL, pls, fP);
+      uint32_t extra = 0;
+      probe_items<1>(tv.edges, qbase, qhp, qph, nL, w, nP, lit, fL, pls, fP, extra);
       evals += (fL[0] ? 1u : 0u) + (fP[0] ? 1u : 0u);
       const uint32_t m0 = lit[0].a.z, m1 = pls[0].a.z;
       emit(fL[0] && (m0 & META_HAS_HASH), lit[0].f.x, fL[0] && leaf && term_ok(m0, mode, droot), lit[0].f.y,
@@ -678,8 +730,8 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       const bool p1 = fP[0] && !leaf && (m1 & META_HAS_EDGES);
       uint32_t ptot;
       const uint32_t ppos = wave_prefix<2>((p0 ? 1u : 0u) + (p1 ? 1u : 0u), lane, &ptot);
-      if (p0) stack[top + ppos] = make_uint4(lit[0].a.y, m0 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
-      if (p1) stack[top + ppos + (p0 ? 1u : 0u)] = make_uint4(pls[0].a.y, m1 & (META_CAPLOG2_MASK | META_HAS_PLUS), widx + 1, 0u);
+      if (p0) stack[top + ppos] = make_uint4(lit[0].a.y, m0, widx + 1, 0u);
+      if (p1) stack[top + ppos + (p0 ? 1u : 0u)] = make_uint4(pls[0].a.y, m1, widx + 1, 0u);
       top += ptot;
       __threadfence_block();
     }
@@ -826,7 +878,10 @@ __global__ void zero_u32_kernel(uint32_t* p, const uint32_t* count) {
 template <int W, int S, int WC, int K>
 static void launch_fast_t(const MatchArgs& a, uint64_t ntiles, hipStream_t s) {
   const uint64_t grid = (ntiles + W - 1) / W;
-  hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+  if (a.diag)
+    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, true>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, false>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
 }
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {

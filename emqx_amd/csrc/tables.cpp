@@ -12,6 +12,8 @@
 #include "tables.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace emqx {
@@ -276,13 +278,96 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     }
   }
 
+  // ---- pass 2: per-node child lists -----------------------------------------------
   const uint64_t n_nodes = depth.size();
-  // ---- pass 2: layout — BFS by depth, larger arrays first (natural alignment) -------
-  std::vector<uint32_t> caplog(n_nodes, 0);
-  for (uint64_t v = 0; v < n_nodes; ++v) {
-    uint32_t e = n_edges[v];
-    caplog[v] = e ? log2u(next_pow2(uint64_t(e) + e / 2 + 1)) : 0;
+  std::vector<uint64_t> coff(n_nodes + 1, 0);
+  em.for_each([&](uint64_t key, uint32_t) { coff[(key >> 32) + 1] += 1; });
+  for (uint64_t v = 0; v < n_nodes; ++v) coff[v + 1] += coff[v];
+  std::vector<uint32_t> cwid(coff[n_nodes]), cid(coff[n_nodes]);
+  {
+    std::vector<uint64_t> fillp(coff.begin(), coff.end() - 1);
+    em.for_each([&](uint64_t key, uint32_t child) {
+      const uint64_t p = key >> 32;
+      cwid[fillp[p]] = static_cast<uint32_t>(key);
+      cid[fillp[p]] = child;
+      fillp[p] += 1;
+    });
   }
+
+  // 2-choice cuckoo placement of node v's literal edges (random-walk eviction) for one
+  // seed; false when the cuckoo graph has an overfull component.  Slot 0 stays free for '+'.
+  std::vector<uint32_t> ck_key, ck_child;
+  auto cuckoo_place = [&](uint64_t v, uint32_t sd, uint32_t cap, std::vector<uint32_t>& key_out,
+                          std::vector<uint32_t>& child_out) -> bool {
+    const uint32_t mask = cap - 1;
+    key_out.assign(cap, WID_NONE);
+    child_out.assign(cap, 0);
+    uint32_t rng = 0x9E3779B9u ^ static_cast<uint32_t>(v) ^ (sd << 20);
+    for (uint64_t j = coff[v]; j < coff[v + 1]; ++j) {
+      if (cwid[j] == WID_PLUS) continue;
+      uint32_t key = cwid[j], ch = cid[j];
+      for (int kick = 0;; ++kick) {
+        const uint32_t s1 = cuckoo_slot1(key, sd, mask), s2 = cuckoo_slot2(key, sd, mask);
+        if (key_out[s1] == WID_NONE) { key_out[s1] = key; child_out[s1] = ch; break; }
+        if (key_out[s2] == WID_NONE) { key_out[s2] = key; child_out[s2] = ch; break; }
+        if (kick > 500) return false;
+        rng = rng * 1664525u + 1013904223u;
+        const uint32_t victim = ((rng >> 16) & 1u) ? s1 : s2;
+        std::swap(key, key_out[victim]);
+        std::swap(ch, child_out[victim]);
+      }
+    }
+    return true;
+  };
+
+  // ---- pass 3: hashing per node — perfect hash (seed search) or cuckoo ------------------
+  std::vector<uint32_t> caplog(n_nodes, 0), seed(n_nodes, 0);
+  std::vector<uint8_t> ph(n_nodes, 0);
+  std::vector<uint32_t> slots_tmp;
+  for (uint64_t v = 0; v < n_nodes; ++v) {
+    const uint32_t e = n_edges[v];
+    if (!e) continue;
+    const uint32_t n_lit = e - (has_plus[v] ? 1u : 0u);
+    bool done = false;
+    if (n_lit <= 32) {
+      const uint64_t cap0 = next_pow2(std::max<uint64_t>(2, 2ull * e));
+      const uint64_t cap_max = next_pow2(std::max<uint64_t>(16, 8ull * e));
+      for (uint64_t cap = cap0; cap <= cap_max && !done && log2u(cap) <= PH_MAX_CAPLOG; cap <<= 1) {
+        const uint32_t mask = static_cast<uint32_t>(cap - 1);
+        for (uint32_t sd = 0; sd < 256 && !done; ++sd) {
+          slots_tmp.clear();
+          bool ok = true;
+          if (has_plus[v]) slots_tmp.push_back(0);
+          for (uint64_t j = coff[v]; j < coff[v + 1] && ok; ++j) {
+            if (cwid[j] == WID_PLUS) continue;
+            const uint32_t sl = lit_slot(cwid[j], sd, mask);
+            for (uint32_t x : slots_tmp) ok &= (x != sl);
+            slots_tmp.push_back(sl);
+          }
+          if (ok) {
+            caplog[v] = log2u(cap);
+            seed[v] = sd;
+            ph[v] = 1;
+            done = true;
+          }
+        }
+      }
+    }
+    if (!done) {
+      caplog[v] = log2u(next_pow2(4ull * e + 2));  // cuckoo at load <= 1/4
+      bool ok = false;
+      for (uint32_t sd = 0; sd < CUCKOO_SEEDS && !ok; ++sd) {
+        ok = cuckoo_place(v, sd, 1u << caplog[v], ck_key, ck_child);
+        if (ok) seed[v] = sd;
+      }
+      if (!ok) {
+        if (err) *err = "cuckoo placement failed for a node with " + std::to_string(e) + " edges";
+        return false;
+      }
+    }
+  }
+
+  // ---- pass 4: layout — BFS by depth, larger arrays first (natural alignment) -------
   std::vector<uint32_t> order(n_nodes);
   for (uint64_t v = 0; v < n_nodes; ++v) order[v] = static_cast<uint32_t>(v);
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
@@ -303,6 +388,31 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       }
     }
   }
+  // literal-edge filter of each node (stored in the slot that leads to it)
+  std::vector<uint32_t> lf_lo(n_nodes, 0), lf_hi(n_nodes, 0), lf_flag(n_nodes, 0);
+  for (uint64_t v = 0; v < n_nodes; ++v) {
+    uint32_t n_lit = 0, only = WID_NONE, lo = 0, hi = 0;
+    for (uint64_t j = coff[v]; j < coff[v + 1]; ++j) {
+      if (cwid[j] == WID_PLUS) continue;
+      ++n_lit;
+      only = cwid[j];
+      const uint32_t h = litf_hash(cwid[j]);
+      const uint32_t b1 = h & 63u, b2 = (h >> 6) & 63u;
+      (b1 < 32 ? lo : hi) |= 1u << (b1 & 31u);
+      (b2 < 32 ? lo : hi) |= 1u << (b2 & 31u);
+    }
+    if (n_lit == 0) {
+      lf_flag[v] = META_LITF_NONE;
+    } else if (n_lit == 1) {
+      lf_flag[v] = META_LITF_EXACT;
+      lf_lo[v] = only;
+    } else if (n_lit <= 32) {
+      lf_lo[v] = lo;
+      lf_hi[v] = hi;
+    } else {
+      lf_lo[v] = lf_hi[v] = ~0u;
+    }
+  }
   auto meta_of = [&](uint32_t v) -> uint32_t {
     uint32_t m = caplog[v] & META_CAPLOG2_MASK;
     if (n_edges[v]) m |= META_HAS_EDGES;
@@ -310,36 +420,47 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     if (hash_fid[v] != FID_NONE) m |= META_HAS_HASH;
     if (term_fid[v] != FID_NONE) m |= META_HAS_TERM;
     if (term_wild[v]) m |= META_TERM_WILD;
+    m |= (ph[v] ? META_PH : 0u) | (seed[v] << META_SEED_SHIFT);
+    m |= lf_flag[v];
     return m;
   };
 
   out.edges.assign(std::max<uint64_t>(total_slots, 1),
                    EdgeSlot{WID_NONE, 0, 0, 0, FID_NONE, FID_NONE, 0, 0});
-  auto fill = [&](uint32_t parent, uint32_t wid, uint32_t child) {
-    const uint32_t mask = (1u << caplog[parent]) - 1;
-    uint32_t i = (wid == WID_PLUS) ? 0u : (mix32(wid) & mask);  // '+' pinned at slot 0
-    while (out.edges[base[parent] + i].wid != WID_NONE) i = (i + 1) & mask;
-    EdgeSlot& s = out.edges[base[parent] + i];
+  auto write_slot = [&](uint64_t at, uint32_t wid, uint32_t child) {
+    EdgeSlot& s = out.edges[at];
     s.wid = wid;
     s.child_base = base[child];
     s.meta = meta_of(child);
     s.child = new_id[child];
     s.hash_fid = hash_fid[child];
     s.term_fid = term_fid[child];
+    s.lit_lo = lf_lo[child];
+    s.lit_hi = lf_hi[child];
   };
-  // '+' edges first so that each one lands in slot 0 of its parent's array
-  em.for_each([&](uint64_t key, uint32_t child) {
-    if (static_cast<uint32_t>(key) == WID_PLUS) fill(static_cast<uint32_t>(key >> 32), WID_PLUS, child);
-  });
-  em.for_each([&](uint64_t key, uint32_t child) {
-    const uint32_t wid = static_cast<uint32_t>(key);
-    if (wid != WID_PLUS) fill(static_cast<uint32_t>(key >> 32), wid, child);
-  });
+  for (uint64_t v = 0; v < n_nodes; ++v) {
+    if (!n_edges[v]) continue;
+    // '+' is pinned at slot 0
+    for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
+      if (cwid[j] == WID_PLUS) write_slot(base[v], WID_PLUS, cid[j]);
+    if (ph[v]) {
+      const uint32_t mask = (1u << caplog[v]) - 1;
+      for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
+        if (cwid[j] != WID_PLUS) write_slot(base[v] + lit_slot(cwid[j], seed[v], mask), cwid[j], cid[j]);
+      continue;
+    }
+    // cuckoo node: re-run the placement found in pass 3 (deterministic for its seed)
+    const uint32_t cap = 1u << caplog[v];
+    cuckoo_place(v, seed[v], cap, ck_key, ck_child);
+    for (uint32_t i = 1; i < cap; ++i)
+      if (ck_key[i] != WID_NONE) write_slot(base[v] + i, ck_key[i], ck_child[i]);
+  }
   out.root_hash_fid = hash_fid[0];
   out.root_base = base[0];
   out.root_meta = meta_of(0);
   out.n_nodes = n_nodes;
   out.max_depth = max_depth;
+  for (uint64_t v = 0; v < n_nodes; ++v) out.n_ph_nodes += ph[v];
 
   // ---- vocab device table ----------------------------------------------------------
   const uint64_t nw = vb.h32.size();
@@ -362,6 +483,68 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
   out.arena.swap(vb.arena);
   if (out.arena.empty()) out.arena.push_back(0);
   out.n_words = nw;
+  return true;
+}
+
+// Host self-check of a built table: every stored edge must be found by the device lookup
+// rule (slot 0 for '+', perfect hash or the two cuckoo candidates), every non-edge word
+// must miss, and every literal filter must admit every word it summarises.
+bool check_tables(const HostTables& t, std::string* err) {
+  const uint64_t n = t.edges.size();
+  std::vector<std::pair<uint32_t, uint32_t>> arrays;  // (base, meta) of every node with edges
+  arrays.push_back({t.root_base, t.root_meta});
+  for (uint64_t i = 0; i < n; ++i) {
+    const EdgeSlot& s = t.edges[i];
+    if (s.wid != WID_NONE && (s.meta & META_HAS_EDGES)) arrays.push_back({s.child_base, s.meta});
+  }
+  for (auto& [base, meta] : arrays) {
+    if (!(meta & META_HAS_EDGES)) continue;
+    const uint32_t caplog = meta & META_CAPLOG2_MASK;
+    const uint32_t mask = (1u << caplog) - 1u;
+    const bool ph = (meta & META_PH) != 0;
+    uint32_t n_lit = 0;
+    for (uint32_t i = 0; i <= mask; ++i) {
+      const EdgeSlot& s = t.edges[base + i];
+      if (s.wid == WID_NONE) continue;
+      if (s.wid == WID_PLUS) {
+        if (i != 0 || !(meta & META_HAS_PLUS)) {
+          if (err) *err = "'+' edge not in slot 0";
+          return false;
+        }
+        continue;
+      }
+      ++n_lit;
+      bool found;
+      if (ph) found = lit_slot(s.wid, (meta >> META_SEED_SHIFT) & 255u, mask) == i;
+      else {
+        const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
+        found = cuckoo_slot1(s.wid, sd, mask) == i || cuckoo_slot2(s.wid, sd, mask) == i;
+      }
+      if (!found) {
+        if (err) *err = "edge not at its lookup slot";
+        return false;
+      }
+    }
+    if ((meta & META_HAS_PLUS) && t.edges[base].wid != WID_PLUS) {
+      if (err) *err = "missing '+' edge";
+      return false;
+    }
+    (void)n_lit;
+  }
+  // literal filters: every literal child word of a node must pass the node's filter
+  for (uint64_t i = 0; i < n; ++i) {
+    const EdgeSlot& s = t.edges[i];
+    if (s.wid == WID_NONE || !(s.meta & META_HAS_EDGES)) continue;
+    const uint32_t mask = (1u << (s.meta & META_CAPLOG2_MASK)) - 1u;
+    for (uint32_t j = 0; j <= mask; ++j) {
+      const EdgeSlot& c = t.edges[s.child_base + j];
+      if (c.wid == WID_NONE || c.wid == WID_PLUS) continue;
+      if (!litf_may_contain(s.meta, s.lit_lo, s.lit_hi, c.wid)) {
+        if (err) *err = "literal filter rejects a present word";
+        return false;
+      }
+    }
+  }
   return true;
 }
 

@@ -73,9 +73,12 @@ struct HostTables {
   uint64_t n_nodes = 0;
   uint64_t n_words = 0;
   uint32_t max_depth = 0;
+  uint64_t n_ph_nodes = 0;
 };
 
 // Builds the level trie of every live filter.  Returns false on size overflow.
 bool build_tables(const FilterStore& fs, HostTables& out, std::string* err);
+// Verifies the lookup invariants of a built table (host-side; used by tests).
+bool check_tables(const HostTables& t, std::string* err);
 
 }  // namespace emqx

@@ -5,7 +5,12 @@
 // apps/emqx/src/emqx_topic.erl:53-62 (wildcard/1), :68-87 (match/2), :153-164 (words).
 #include <stdint.h>
 
+#include <string.h>
+
+#include <string>
+
 #include "../../include/emqx_match.h"
+#include "tables.h"
 
 namespace {
 
@@ -64,4 +69,30 @@ extern "C" int emqx_topic_match(const uint8_t* name, uint64_t nlen, const uint8_
     if (hf && is_hash(f) && fd) return 1;          // match(_, ['#'])
     return 0;
   }
+}
+
+// Host-only builder self-check (no device needed): builds the level trie of the given
+// filters and verifies its lookup invariants.  stats_out (optional, 4 entries): nodes,
+// slots, words, perfect-hashed nodes.
+extern "C" int emqx_build_check(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* stats_out,
+                                char* err, uint64_t err_cap) {
+  emqx::FilterStore fs;
+  for (uint64_t i = 0; i < n; ++i) {
+    bool created = false;
+    fs.insert(bytes + offsets[i], offsets[i + 1] - offsets[i], &created);
+  }
+  emqx::HostTables t;
+  std::string e;
+  bool ok = emqx::build_tables(fs, t, &e) && emqx::check_tables(t, &e);
+  if (stats_out) {
+    stats_out[0] = t.n_nodes;
+    stats_out[1] = t.edges.size();
+    stats_out[2] = t.n_words;
+    stats_out[3] = t.n_ph_nodes;
+  }
+  if (!ok && err && err_cap) {
+    strncpy(err, e.c_str(), err_cap - 1);
+    err[err_cap - 1] = 0;
+  }
+  return ok ? EMQX_OK : EMQX_EINVAL;
 }

@@ -88,6 +88,14 @@ class Engine:
     def set_tuning(self, key: str, value: int) -> None:
         check(_lib.lib().emqx_set_tuning(self._h, key.encode(), int(value)), "emqx_set_tuning")
 
+    DIAG_NAMES = ("steps", "items", "lit_probes", "lit_hits", "lit_extra_loads", "plus_probes",
+                  "plus_hits", "emits", "spills")
+
+    def diag(self, reset: bool = True) -> dict:
+        out = np.zeros(16, dtype=np.uint64)
+        check(_lib.lib().emqx_diag_read(self._h, _ptr(out), 16, int(reset)), "emqx_diag_read")
+        return {k: int(out[i]) for i, k in enumerate(self.DIAG_NAMES)}
+
     def commit(self) -> None:
         check(_lib.lib().emqx_commit(self._h), "emqx_commit")
 

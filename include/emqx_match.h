@@ -123,9 +123,18 @@ int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filt
 /* emqx_topic:wildcard/1 (emqx_topic.erl:53-62): 1 if some level is exactly '+' or '#'. */
 int emqx_topic_wildcard(const uint8_t* topic, uint64_t len);
 
-/* Tuning hook (benchmarks / A-B runs).  Keys: "fast_variant" (-1 = automatic, 0..4 = a
- * fixed kernel variant, see emqx_amd/csrc/kernels.h).  EMQX_ENOTFOUND for unknown keys. */
+/* Tuning hook (benchmarks / A-B runs).  Keys: "fast_variant" (-1 = automatic, otherwise a
+ * fixed kernel variant, see emqx_amd/csrc/kernels.h), "diag" (1 = accumulate the kernel's
+ * diagnostic counters).  EMQX_ENOTFOUND for unknown keys. */
 int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value);
+/* Reads (and optionally resets) the accumulated diagnostic counters (DIAG_* order). */
+int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset);
+
+/* Host-only self-check of the table builder (no device needed): builds the level trie of
+ * the given filters and verifies its lookup invariants.  stats_out (4 entries, optional):
+ * nodes, slots, interned words, perfect-hashed nodes.  err receives the failure reason. */
+int emqx_build_check(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* stats_out,
+                     char* err, uint64_t err_cap);
 
 const char* emqx_strerror(int code);
 /* Library version string. */

@@ -106,3 +106,40 @@ def test_workloads_shapes():
     d = W.config_d(n_filters=5000, n_topics=100)
     assert d.n_filters == 5000
     assert all(t.count(b"/") == 15 for t in W.unpack(d.topics))
+
+
+def build_check(packed):
+    import ctypes
+    import numpy as np
+    from emqx_amd import _lib
+    buf, offs = packed
+    st = np.zeros(4, np.uint64)
+    err = ctypes.create_string_buffer(256)
+    rc = _lib.lib().emqx_build_check(buf.ctypes.data_as(ctypes.c_void_p), offs.ctypes.data_as(ctypes.c_void_p),
+                                     len(offs) - 1, st.ctypes.data_as(ctypes.c_void_p), err, 256)
+    return rc, err.value.decode(), st
+
+
+@pytest.mark.parametrize("cfg", ["A", "B", "D", "fuzz", "kats"])
+def test_builder_invariants(L, cfg, kats):
+    """Host table builder (no device): every edge sits at its perfect-hash / cuckoo slot,
+    '+' in slot 0, literal filters admit every present word."""
+    import random
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import pack
+    from tests.test_oracle_fuzz import rand_filter
+    if cfg == "A":
+        packed = W.config_a(n_topics=10).filters
+    elif cfg == "B":
+        packed = W.config_b(n_filters=400_000, n_topics=10).filters
+    elif cfg == "D":
+        packed = W.config_d(n_filters=100_000, n_topics=10).filters
+    elif cfg == "fuzz":
+        rng = random.Random(11)
+        packed = pack(sorted({rand_filter(rng, 9) for _ in range(20000)}))
+    else:
+        fl = sorted({op[1].encode() for c in kats["trie_cases"] for op in c["ops"] if op[0] == "insert"})
+        packed = pack(fl + [b"a/#/b", b"+", b"#", b"", b"/"])
+    rc, err, st = build_check(packed)
+    assert rc == 0, err
+    assert st[0] >= 1 and st[1] >= 1

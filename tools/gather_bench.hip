@@ -1,0 +1,118 @@
+// Random-access ceiling for the match kernel's access pattern on MI355X (gfx950):
+// 32-byte records (one dwordx4 + one dwordx2 load per lane) at random addresses of a table
+// that is larger than the Infinity Cache.  Two shapes:
+//   indep  every lane issues R independent random record loads (throughput ceiling)
+//   chase  every lane follows its own chain of R dependent loads (latency x concurrency)
+// Prints one JSON line per (shape, table size, waves per CU).  Used to price the roofline of
+// match_fast_kernel against random-access HBM rather than the streaming 8 TB/s figure.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/_build/gather_bench tools/gather_bench.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e = (x);                                                       \
+    if (e != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+struct alignas(32) Rec {
+  uint32_t next, a, b, c, d, e, f, g;
+};
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__global__ void init_kernel(Rec* t, uint32_t n, uint32_t stride) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    Rec r;
+    r.next = (uint32_t)(((uint64_t)i * stride + 1) % n);  // stride coprime with n: one long cycle
+    r.a = i; r.b = i ^ 1; r.c = i ^ 2; r.d = i ^ 3; r.e = i ^ 4; r.f = 0; r.g = 0;
+    t[i] = r;
+  }
+}
+
+__global__ void indep_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t iters, uint32_t* out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  uint32_t h = mix(gid * 0x9e3779b9u + 12345u);
+  for (uint32_t k = 0; k < iters; ++k) {
+    h = mix(h + k);
+    const Rec* p = t + (h % n);
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    const uint2 y = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p) + 16);
+    acc ^= x.x + x.y + x.z + x.w + y.x + y.y;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+__global__ void chase_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t iters, uint32_t* out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t i = mix(gid * 0x9e3779b9u + 777u) % n;
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < iters; ++k) {
+    const Rec* p = t + i;
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    const uint2 y = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p) + 16);
+    acc ^= x.y + y.x;
+    i = x.x;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+int main(int argc, char** argv) {
+  const uint64_t sizes_mb[] = {64, 2048};
+  const int wpc[] = {8, 16, 32};
+  uint32_t* out;
+  CK(hipMalloc(&out, 64));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (uint64_t mb : sizes_mb) {
+    const uint32_t n = (uint32_t)(mb * 1024 * 1024 / sizeof(Rec));
+    Rec* t;
+    CK(hipMalloc(&t, (uint64_t)n * sizeof(Rec)));
+    hipLaunchKernelGGL(init_kernel, dim3(4096), dim3(256), 0, 0, t, n, 2654435761u % n | 1u);
+    CK(hipDeviceSynchronize());
+    for (int shape = 0; shape < 2; ++shape) {
+      for (int w : wpc) {
+        const uint32_t blocks = 256u * w / 4u;  // 256 threads = 4 waves per block
+        const uint32_t iters = shape == 0 ? 256 : 128;
+        for (int rep = 0; rep < 2; ++rep) {  // rep 0 = warm-up
+          CK(hipEventRecord(e0));
+          if (shape == 0)
+            hipLaunchKernelGGL(indep_kernel, dim3(blocks), dim3(256), 0, 0, t, n, iters, out);
+          else
+            hipLaunchKernelGGL(chase_kernel, dim3(blocks), dim3(256), 0, 0, t, n, iters, out);
+          CK(hipEventRecord(e1));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          if (rep == 1) {
+            const double loads = (double)blocks * 256 * iters;
+            printf("{\"shape\": \"%s\", \"table_mb\": %llu, \"waves_per_cu\": %d, \"ms\": %.4f, "
+                   "\"records_per_s\": %.4g, \"gb_per_s_32B\": %.1f, \"gb_per_s_64B_lines\": %.1f, "
+                   "\"ns_per_dependent_load\": %.1f}\n",
+                   shape == 0 ? "indep" : "chase", (unsigned long long)mb, w, ms, loads / (ms * 1e-3),
+                   loads * 32 / (ms * 1e-3) / 1e9, loads * 64 / (ms * 1e-3) / 1e9,
+                   shape == 1 ? ms * 1e6 / iters : 0.0);
+          }
+        }
+      }
+    }
+    CK(hipFree(t));
+  }
+  return 0;
+}
