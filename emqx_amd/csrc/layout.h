@@ -37,7 +37,7 @@ constexpr uint32_t META_HAS_EDGES = 1u << 6;    // child has any edge (literal/'
 constexpr uint32_t META_HAS_HASH = 1u << 7;     // filter "<child path>/#" exists
 constexpr uint32_t META_HAS_TERM = 1u << 8;     // filter "<child path>" exists
 constexpr uint32_t META_TERM_WILD = 1u << 9;    // ... and that filter is a wildcard filter
-constexpr uint32_t META_PH = 1u << 10;          // literal edges perfect-hashed (seed below); else 2-choice cuckoo
+constexpr uint32_t META_PH = 1u << 10;          // literal edges perfect-hashed (seed below); else 2-slot buckets
 constexpr uint32_t META_LITF_EXACT = 1u << 11;  // lit_lo = the child's only literal edge word
 constexpr uint32_t META_LITF_NONE = 1u << 12;   // the child has no literal edge at all
 constexpr uint32_t META_SEED_SHIFT = 16;        // 8-bit perfect-hash seed
@@ -48,13 +48,14 @@ constexpr uint32_t PH_MAX_CAPLOG = 15;
 // and a filter over the child's literal edges, tested against the topic's next word before
 // the child is even pushed.  A node's '+' edge, when present, always sits in slot 0 of its
 // array; literal edges are perfect-hashed by a per-node seed found at build time (one load
-// per lookup, hit or miss), or — in the few wide nodes where no seed fits — cuckoo-hashed
-// over two candidate slots that are loaded together (still one dependent round trip).
+// per lookup, hit or miss), or — in wide nodes, where no seed fits — hashed into 2-slot
+// buckets of one 64-B sector each (one sector per lookup, a second one for ~1% of words).
 struct alignas(32) EdgeSlot {
   uint32_t wid;         // key (WID_NONE = empty)
   uint32_t child_base;  // first slot of the child's edge array
   uint32_t meta;        // META_* (+ seed) of the child
-  uint32_t child;       // child node id (BFS order)
+  uint32_t aux;         // bit 0 (first slot of a 2-slot bucket of a wide node): some word
+                        // whose primary bucket this is lives in its secondary bucket
   uint32_t hash_fid;    // filter "<child path>/#" or FID_NONE
   uint32_t term_fid;    // filter "<child path>"   or FID_NONE
   uint32_t lit_lo;      // literal-edge filter of the child: the word (LITF_EXACT) or a
@@ -103,19 +104,17 @@ EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask) {
   return mix32(wid ^ (seed * 0x9E3779B1u + 0x7F4A7C15u)) & mask;
 }
 
-// The two candidate slots of `wid` in a cuckoo-hashed (wide) node's array, both in
-// [1, cap) — slot 0 belongs to '+' (mask = cap - 1 >= 2).
-EMQX_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
-  return static_cast<uint32_t>((static_cast<uint64_t>(a) * b) >> 32);
+// Wide (non-perfect-hashed) nodes use 2-slot buckets = one 64-B sector: a word lives in its
+// primary bucket, or — rarely, flagged by AUX_OVERFLOW on the primary bucket's first slot —
+// in its secondary bucket.  Bucket 0's slot 0 is '+'.  `seed` (7 bits) is re-drawn by the
+// builder until every word fits.
+constexpr uint32_t AUX_OVERFLOW = 1u;
+EMQX_HD uint32_t bucket1(uint32_t wid, uint32_t seed, uint32_t nbmask) {
+  return mix32(wid ^ (0x3C6EF372u + seed * 0x9E3779B9u)) & nbmask;
 }
-// `seed` (7 bits) is re-drawn by the builder until every word of the node fits.
-EMQX_HD uint32_t cuckoo_slot1(uint32_t wid, uint32_t seed, uint32_t mask) {
-  return 1u + mulhi32(mix32(wid ^ (0x3C6EF372u + seed * 0x9E3779B9u)), mask);
-}
-EMQX_HD uint32_t cuckoo_slot2(uint32_t wid, uint32_t seed, uint32_t mask) {
-  const uint32_t a = cuckoo_slot1(wid, seed, mask);
-  const uint32_t b = 1u + mulhi32(mix32(wid ^ (0xDAA66D2Bu + seed * 0x7F4A7C15u)), mask);
-  return b != a ? b : (a == mask ? 1u : a + 1u);
+EMQX_HD uint32_t bucket2(uint32_t wid, uint32_t seed, uint32_t nbmask) {
+  const uint32_t a = bucket1(wid, seed, nbmask), b = mix32(wid ^ (0xDAA66D2Bu + seed * 0x7F4A7C15u)) & nbmask;
+  return b != a ? b : ((a + 1) & nbmask);
 }
 constexpr uint32_t CUCKOO_SEEDS = 128;
 

@@ -140,26 +140,29 @@ __device__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, u
 }
 
 // Probe one node's edge array for `wid` ('+' sits in slot 0; literals perfect-hashed, or
-// cuckoo-hashed over two candidate slots, according to the node's meta).
+// bucketed in 2-slot sectors, according to the node's meta).
 __device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t meta, uint32_t wid, Slot* out) {
   if (wid == WID_PLUS) {
     *out = load_slot(arr);
     return out->a.x == WID_PLUS;
   }
   const uint32_t mask = (1u << (meta & META_CAPLOG2_MASK)) - 1u;
+  const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
   if (meta & META_PH) {
-    *out = load_slot(arr + lit_slot(wid, (meta >> META_SEED_SHIFT) & 255u, mask));
+    *out = load_slot(arr + lit_slot(wid, sd, mask));
     return out->a.x == wid;
   }
-  const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
-  const Slot s1 = load_slot(arr + cuckoo_slot1(wid, sd, mask));
-  const Slot s2 = load_slot(arr + cuckoo_slot2(wid, sd, mask));
-  if (s1.a.x == wid) {
-    *out = s1;
-    return true;
-  }
-  *out = s2;
-  return s2.a.x == wid;
+  const uint32_t nbm = mask >> 1;
+  const uint32_t b1 = bucket1(wid, sd, nbm);
+  const Slot x = load_slot(arr + 2 * b1), y = load_slot(arr + 2 * b1 + 1);
+  if (x.a.x == wid) { *out = x; return true; }
+  if (y.a.x == wid) { *out = y; return true; }
+  if (!(x.a.w & AUX_OVERFLOW)) return false;
+  const uint32_t b2 = bucket2(wid, sd, nbm);
+  const Slot u = load_slot(arr + 2 * b2), v = load_slot(arr + 2 * b2 + 1);
+  if (u.a.x == wid) { *out = u; return true; }
+  if (v.a.x == wid) { *out = v; return true; }
+  return false;
 }
 
 // Byte-identical lookup of a wildcard "topic" for match_routes (emqx_router.erl:130):
@@ -206,8 +209,9 @@ __device__ __forceinline__ uint2 make_item(uint32_t base, uint32_t meta, bool dr
 __device__ __forceinline__ uint32_t item_topic(uint2 it) { return (it.y >> IT_TOPIC_SHIFT) & 63u; }
 
 // Probe the '+' edge (slot 0) and the literal edge of K nodes at once: every load is issued
-// before any result is consumed, so a step costs one dependent round trip.  Perfect-hashed
-// nodes answer in one slot load; cuckoo-hashed (wide) nodes load both candidate slots.
+// before any result is consumed, so a step costs one dependent round trip (plus one more for
+// the ~1% of wide-node words displaced to their secondary bucket).  Perfect-hashed nodes
+// answer in one slot load; wide nodes load their word's 2-slot bucket (one 64-B sector).
 template <int K>
 __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, const uint32_t (&base)[K],
                                             const uint32_t (&hparams)[K], const bool (&isph)[K],
@@ -215,32 +219,45 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
                                             const bool (&needP)[K], Slot (&lit)[K], bool (&fL)[K],
                                             Slot (&pls)[K], bool (&fP)[K], uint32_t& extra) {
   Slot alt[K];
-  bool need2[K];
+  bool wide[K], again[K];
+  uint32_t sdk[K], nbm[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const EdgeSlot* arr = edges + base[k];
     const uint32_t caplog = isph[k] ? (hparams[k] & 15u) : (hparams[k] & 31u);
-    const uint32_t sd = isph[k] ? (hparams[k] >> 4) : (hparams[k] >> 5);
+    sdk[k] = isph[k] ? (hparams[k] >> 4) : (hparams[k] >> 5);
     const uint32_t mask = (1u << caplog) - 1u;
-    const uint32_t i1 = isph[k] ? lit_slot(wid[k], sd, mask) : cuckoo_slot1(wid[k], sd, mask);
-    need2[k] = needL[k] && !isph[k];
+    nbm[k] = mask >> 1;
+    wide[k] = needL[k] && !isph[k];
+    const uint32_t i1 = isph[k] ? lit_slot(wid[k], sdk[k], mask) : 2u * bucket1(wid[k], sdk[k], nbm[k]);
     pls[k] = empty_slot();
     lit[k] = pls[k];
     alt[k] = pls[k];
     if (needP[k]) pls[k] = load_slot(arr);
     if (needL[k]) lit[k] = load_slot(arr + i1);
-    if (need2[k]) {
-      alt[k] = load_slot(arr + cuckoo_slot2(wid[k], sd, mask));
-      ++extra;
-    }
+    if (wide[k]) alt[k] = load_slot(arr + i1 + 1);  // same 64-B sector
   }
+  bool any_again = false;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     fP[k] = needP[k] && pls[k].a.x == WID_PLUS;
     fL[k] = needL[k] && lit[k].a.x == wid[k];
-    if (need2[k] && !fL[k] && alt[k].a.x == wid[k]) {
+    if (wide[k] && !fL[k] && alt[k].a.x == wid[k]) {
       lit[k] = alt[k];
       fL[k] = true;
+    }
+    again[k] = wide[k] && !fL[k] && (lit[k].a.w & AUX_OVERFLOW);
+    any_again |= again[k];
+  }
+  if (__any(any_again)) {  // secondary buckets (rare): one more dependent round trip
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!again[k]) continue;
+      const uint32_t i2 = 2u * bucket2(wid[k], sdk[k], nbm[k]);
+      const Slot u = load_slot(edges + base[k] + i2), v = load_slot(edges + base[k] + i2 + 1);
+      ++extra;
+      if (u.a.x == wid[k]) { lit[k] = u; fL[k] = true; }
+      else if (v.a.x == wid[k]) { lit[k] = v; fL[k] = true; }
     }
   }
 }

@@ -294,25 +294,36 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     });
   }
 
-  // 2-choice cuckoo placement of node v's literal edges (random-walk eviction) for one
-  // seed; false when the cuckoo graph has an overfull component.  Slot 0 stays free for '+'.
+  // Bucketed placement of node v's literal edges (2-slot buckets, two candidate buckets,
+  // random-walk eviction) for one seed; false when some word cannot be placed.  Slot 0
+  // stays free for '+'.  Afterwards every word outside its primary bucket flags that bucket.
   std::vector<uint32_t> ck_key, ck_child;
-  auto cuckoo_place = [&](uint64_t v, uint32_t sd, uint32_t cap, std::vector<uint32_t>& key_out,
+  auto bucket_place = [&](uint64_t v, uint32_t sd, uint32_t cap, std::vector<uint32_t>& key_out,
                           std::vector<uint32_t>& child_out) -> bool {
-    const uint32_t mask = cap - 1;
+    const uint32_t nbm = cap / 2 - 1;
     key_out.assign(cap, WID_NONE);
     child_out.assign(cap, 0);
+    if (has_plus[v]) key_out[0] = WID_PLUS;
     uint32_t rng = 0x9E3779B9u ^ static_cast<uint32_t>(v) ^ (sd << 20);
     for (uint64_t j = coff[v]; j < coff[v + 1]; ++j) {
       if (cwid[j] == WID_PLUS) continue;
       uint32_t key = cwid[j], ch = cid[j];
       for (int kick = 0;; ++kick) {
-        const uint32_t s1 = cuckoo_slot1(key, sd, mask), s2 = cuckoo_slot2(key, sd, mask);
-        if (key_out[s1] == WID_NONE) { key_out[s1] = key; child_out[s1] = ch; break; }
-        if (key_out[s2] == WID_NONE) { key_out[s2] = key; child_out[s2] = ch; break; }
+        const uint32_t b1 = bucket1(key, sd, nbm), b2 = bucket2(key, sd, nbm);
+        const uint32_t cand[4] = {2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1};
+        bool placed = false;
+        for (uint32_t c : cand)
+          if (key_out[c] == WID_NONE) {
+            key_out[c] = key;
+            child_out[c] = ch;
+            placed = true;
+            break;
+          }
+        if (placed) break;
         if (kick > 500) return false;
         rng = rng * 1664525u + 1013904223u;
-        const uint32_t victim = ((rng >> 16) & 1u) ? s1 : s2;
+        const uint32_t victim = cand[(rng >> 16) & 3u];
+        if (key_out[victim] == WID_PLUS) continue;
         std::swap(key, key_out[victim]);
         std::swap(ch, child_out[victim]);
       }
@@ -320,7 +331,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     return true;
   };
 
-  // ---- pass 3: hashing per node — perfect hash (seed search) or cuckoo ------------------
+  // ---- pass 3: hashing per node — perfect hash (seed search) or 2-slot buckets ---------
   std::vector<uint32_t> caplog(n_nodes, 0), seed(n_nodes, 0);
   std::vector<uint8_t> ph(n_nodes, 0);
   std::vector<uint32_t> slots_tmp;
@@ -330,7 +341,8 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     const uint32_t n_lit = e - (has_plus[v] ? 1u : 0u);
     bool done = false;
     if (n_lit <= 32) {
-      const uint64_t cap0 = next_pow2(std::max<uint64_t>(2, 2ull * e));
+      // smallest cap first: small nodes (plus + a literal or two) stay inside one 64-B line
+      const uint64_t cap0 = next_pow2(std::max<uint64_t>(2, e));
       const uint64_t cap_max = next_pow2(std::max<uint64_t>(16, 8ull * e));
       for (uint64_t cap = cap0; cap <= cap_max && !done && log2u(cap) <= PH_MAX_CAPLOG; cap <<= 1) {
         const uint32_t mask = static_cast<uint32_t>(cap - 1);
@@ -354,14 +366,14 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       }
     }
     if (!done) {
-      caplog[v] = log2u(next_pow2(4ull * e + 2));  // cuckoo at load <= 1/4
+      caplog[v] = log2u(next_pow2(4ull * e + 4));  // 2-slot buckets at load <= 1/4
       bool ok = false;
       for (uint32_t sd = 0; sd < CUCKOO_SEEDS && !ok; ++sd) {
-        ok = cuckoo_place(v, sd, 1u << caplog[v], ck_key, ck_child);
+        ok = bucket_place(v, sd, 1u << caplog[v], ck_key, ck_child);
         if (ok) seed[v] = sd;
       }
       if (!ok) {
-        if (err) *err = "cuckoo placement failed for a node with " + std::to_string(e) + " edges";
+        if (err) *err = "bucket placement failed for a node with " + std::to_string(e) + " edges";
         return false;
       }
     }
@@ -432,7 +444,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     s.wid = wid;
     s.child_base = base[child];
     s.meta = meta_of(child);
-    s.child = new_id[child];
+    s.aux = 0;
     s.hash_fid = hash_fid[child];
     s.term_fid = term_fid[child];
     s.lit_lo = lf_lo[child];
@@ -449,11 +461,18 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
         if (cwid[j] != WID_PLUS) write_slot(base[v] + lit_slot(cwid[j], seed[v], mask), cwid[j], cid[j]);
       continue;
     }
-    // cuckoo node: re-run the placement found in pass 3 (deterministic for its seed)
-    const uint32_t cap = 1u << caplog[v];
-    cuckoo_place(v, seed[v], cap, ck_key, ck_child);
-    for (uint32_t i = 1; i < cap; ++i)
-      if (ck_key[i] != WID_NONE) write_slot(base[v] + i, ck_key[i], ck_child[i]);
+    // wide node: re-run the placement found in pass 3 (deterministic for its seed), then
+    // flag every primary bucket that overflowed
+    const uint32_t cap = 1u << caplog[v], nbm = cap / 2 - 1;
+    bucket_place(v, seed[v], cap, ck_key, ck_child);
+    for (uint32_t i = 0; i < cap; ++i)
+      if (ck_key[i] != WID_NONE && ck_key[i] != WID_PLUS) write_slot(base[v] + i, ck_key[i], ck_child[i]);
+    for (uint32_t i = 0; i < cap; ++i) {
+      const uint32_t key = ck_key[i];
+      if (key == WID_NONE || key == WID_PLUS) continue;
+      const uint32_t b1 = bucket1(key, seed[v], nbm);
+      if (i / 2 != b1) out.edges[base[v] + 2 * b1].aux |= AUX_OVERFLOW;
+    }
   }
   out.root_hash_fid = hash_fid[0];
   out.root_base = base[0];
@@ -487,7 +506,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
 }
 
 // Host self-check of a built table: every stored edge must be found by the device lookup
-// rule (slot 0 for '+', perfect hash or the two cuckoo candidates), every non-edge word
+// rule (slot 0 for '+', perfect hash, or primary / flagged secondary bucket), every non-edge word
 // must miss, and every literal filter must admit every word it summarises.
 bool check_tables(const HostTables& t, std::string* err) {
   const uint64_t n = t.edges.size();
@@ -517,8 +536,9 @@ bool check_tables(const HostTables& t, std::string* err) {
       bool found;
       if (ph) found = lit_slot(s.wid, (meta >> META_SEED_SHIFT) & 255u, mask) == i;
       else {
-        const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
-        found = cuckoo_slot1(s.wid, sd, mask) == i || cuckoo_slot2(s.wid, sd, mask) == i;
+        const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u, nbm = mask / 2;
+        const uint32_t b1 = bucket1(s.wid, sd, nbm), b2 = bucket2(s.wid, sd, nbm);
+        found = i / 2 == b1 || (i / 2 == b2 && (t.edges[base + 2 * b1].aux & AUX_OVERFLOW));
       }
       if (!found) {
         if (err) *err = "edge not at its lookup slot";
