@@ -28,7 +28,8 @@ MODE_TRIE_WILDCARD = 2
 
 # Every symbol include/emqx_match.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
-    "emqx_engine_create", "emqx_engine_destroy", "emqx_insert_filters", "emqx_delete_filters",
+    "emqx_engine_create", "emqx_engine_destroy", "emqx_insert_filters", "emqx_insert_filters_ext",
+    "emqx_delete_filters",
     "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
     "emqx_match_batch_device", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
     "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_strerror", "emqx_version",
@@ -78,6 +79,7 @@ def lib():
         "emqx_engine_create": (i32, [ctypes.POINTER(EngineOpts), ctypes.POINTER(vp)]),
         "emqx_engine_destroy": (i32, [vp]),
         "emqx_insert_filters": (i32, [vp, vp, vp, u64, vp]),
+        "emqx_insert_filters_ext": (i32, [vp, vp, vp, u64, vp, vp]),
         "emqx_delete_filters": (i32, [vp, vp, u64]),
         "emqx_lookup_filter": (i32, [vp, vp, u64, ctypes.POINTER(u32)]),
         "emqx_filter_name": (i32, [vp, u32, vp, u64, ctypes.POINTER(u64)]),

@@ -457,6 +457,20 @@ int emqx_insert_filters(emqx_engine* e, const uint8_t* bytes, const uint64_t* of
   return EMQX_OK;
 }
 
+int emqx_insert_filters_ext(emqx_engine* e, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                            const uint32_t* ext_ids, uint32_t* ids_out) {
+  if (!e || !ext_ids || (n && (!offsets || (!bytes && offsets[n] != offsets[0])))) return EMQX_EINVAL;
+  if (!offsets_ok(offsets, n)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(e->writer);
+  for (uint64_t i = 0; i < n; ++i) {
+    bool created = false;
+    const uint32_t id = e->store.insert(bytes + offsets[i], offsets[i + 1] - offsets[i], &created);
+    e->store.ext[id] = ext_ids[i];
+    if (ids_out) ids_out[i] = id;
+  }
+  return EMQX_OK;
+}
+
 int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n) {
   if (!e || (n && !ids)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(e->writer);

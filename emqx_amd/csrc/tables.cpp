@@ -198,6 +198,7 @@ uint32_t FilterStore::insert(const uint8_t* p, uint64_t n, bool* created) {
   bytes.insert(bytes.end(), p, p + n);
   off.push_back(bytes.size());
   live.push_back(1);
+  ext.push_back(id);
   ++n_live;
   index.insert_new(h, id);
   *created = true;
@@ -242,7 +243,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
         wid = WID_PLUS;
       } else if (len == 1 && p[s] == '#') {
         if (i == n) {  // final '#': the parent level's hash filter
-          hash_fid[node] = static_cast<uint32_t>(id);
+          hash_fid[node] = fs.ext[id];
           ended_hash = true;
           break;
         }
@@ -273,7 +274,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       s = i + 1;
     }
     if (!ended_hash) {
-      term_fid[node] = static_cast<uint32_t>(id);
+      term_fid[node] = fs.ext[id];
       term_wild[node] = wild ? 1 : 0;
     }
   }

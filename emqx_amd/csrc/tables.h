@@ -53,6 +53,7 @@ struct FilterStore {
   std::vector<uint8_t> bytes;
   std::vector<uint64_t> off{0};  // id -> [off[id], off[id+1])
   std::vector<uint8_t> live;
+  std::vector<uint32_t> ext;     // id -> the id reported by matches (default: the id itself)
   uint64_t n_live = 0;
   StrIdMap index;
 

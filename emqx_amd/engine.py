@@ -62,6 +62,16 @@ class Engine:
               "emqx_insert_filters")
         return ids[:n]
 
+    def insert_packed_ext(self, buf: np.ndarray, offs: np.ndarray, ext_ids: np.ndarray) -> np.ndarray:
+        """Insert filters whose matches report ``ext_ids`` (e.g. global ids of a shard)."""
+        n = len(offs) - 1
+        ext = np.ascontiguousarray(np.asarray(ext_ids, dtype=np.uint32))
+        assert ext.size == n
+        ids = np.zeros(max(n, 1), dtype=np.uint32)
+        check(_lib.lib().emqx_insert_filters_ext(self._h, _ptr(buf), _ptr(offs), n, _ptr(ext), _ptr(ids)),
+              "emqx_insert_filters_ext")
+        return ids[:n]
+
     def insert(self, filters: Sequence[bytes]) -> np.ndarray:
         return self.insert_packed(*pack(list(filters)))
 

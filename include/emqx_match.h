@@ -94,6 +94,11 @@ int emqx_engine_destroy(emqx_engine* e);
  *         is idempotent, emqx_trie.erl:115-120); a deleted filter re-inserted gets its old id. */
 int emqx_insert_filters(emqx_engine* e, const uint8_t* bytes, const uint64_t* offsets,
                         uint64_t n, uint32_t* ids_out);
+/* As emqx_insert_filters, but matches report ext_ids[i] for filter i instead of the engine's
+ * own id (filter-sharded tables report global ids; a NIF may report its route-table keys).
+ * Deletion and lookup keep using the engine's ids (ids_out). */
+int emqx_insert_filters_ext(emqx_engine* e, const uint8_t* bytes, const uint64_t* offsets,
+                            uint64_t n, const uint32_t* ext_ids, uint32_t* ids_out);
 int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n);
 int emqx_lookup_filter(emqx_engine* e, const uint8_t* bytes, uint64_t len, uint32_t* id_out);
 /* Copies the bytes of filter `id` into buf (cap bytes); *len_out = its length. */

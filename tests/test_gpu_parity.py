@@ -267,3 +267,27 @@ def test_device_api_matches_host_api(Engine):
     assert np.array_equal(off_d, off_h)
     for i in range(0, len(off_h) - 1, 97):
         assert np.array_equal(np.sort(ids_d[off_d[i]:off_d[i + 1]]), np.sort(ids_h[off_h[i]:off_h[i + 1]]))
+
+
+def test_sharded_matcher_world1_rccl(Engine):
+    """The filter-sharded path end to end on one GPU over RCCL (world size 1): broadcast,
+    global-id shard table, gather and concatenation give the single-engine result."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import workloads as W
+    from emqx_amd.dist import ShardedMatcher
+    wl = W.config_b(n_filters=120_000, n_topics=5000, seed=9)
+    dev = torch.device("cuda:0")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29541")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        sm = ShardedMatcher(wl.filters, device=dev)
+        topics = (torch.from_numpy(wl.topics[0]).to(dev), torch.from_numpy(wl.topics[1].view(np.int64)).to(dev))
+        off, ids = sm.match(topics)
+        off, ids = off.cpu().numpy(), ids.cpu().numpy().view(np.uint32)
+    finally:
+        dist.destroy_process_group()
+    counts, oids = oracle_ids(wl.filters, wl.topics)
+    csr_equal(off.astype(np.uint64), ids, counts, oids)
