@@ -32,7 +32,8 @@ EXPORTS = (
     "emqx_delete_filters",
     "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
     "emqx_match_batch_device", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
-    "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_strerror", "emqx_version",
+    "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_batcher_create",
+    "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_strerror", "emqx_version",
 )
 
 
@@ -60,6 +61,8 @@ class Stats(ctypes.Structure):
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
+
+BATCH_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64)
 
 _lib = None
 
@@ -92,6 +95,10 @@ def lib():
         "emqx_set_tuning": (i32, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "emqx_diag_read": (i32, [vp, vp, u32, i32]),
         "emqx_build_check": (i32, [vp, vp, u64, vp, ctypes.c_char_p, u64]),
+        "emqx_batcher_create": (i32, [vp, u32, u32, u32, BATCH_CB, ctypes.POINTER(vp)]),
+        "emqx_batcher_submit": (i32, [vp, vp, u64, vp]),
+        "emqx_batcher_destroy": (i32, [vp]),
+        "emqx_batcher_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "emqx_strerror": (ctypes.c_char_p, [i32]),
         "emqx_version": (ctypes.c_char_p, []),
     }

@@ -122,6 +122,20 @@ int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topi
 
 int emqx_stats_get(emqx_engine* e, emqx_stats* out);
 
+/* Cross-caller batcher: coalesces concurrent single-topic matches (emqx_router:match_routes/1
+ * is called once per PUBLISH from each publisher process, apps/emqx/src/emqx_broker.erl:213)
+ * into one device batch.  submit() returns at once; a worker thread runs a batch when
+ * max_batch topics are queued or max_wait_us after the oldest submission, then calls
+ * cb(ctx, status, ids, n) once per submission from that thread (ids valid during the call).
+ * destroy() drains pending submissions.  The NIF's cb enif_send()s the ids to the caller. */
+typedef struct emqx_batcher emqx_batcher;
+typedef void (*emqx_batch_cb)(void* ctx, int status, const uint32_t* ids, uint64_t n);
+int emqx_batcher_create(emqx_engine* e, uint32_t mode, uint32_t max_batch, uint32_t max_wait_us,
+                        emqx_batch_cb cb, emqx_batcher** out);
+int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, void* ctx);
+int emqx_batcher_destroy(emqx_batcher* b);
+int emqx_batcher_stats(emqx_batcher* b, uint64_t* n_batches, uint64_t* n_topics);
+
 /* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */
 int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filter,
                      uint64_t filter_len);

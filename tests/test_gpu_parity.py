@@ -291,3 +291,34 @@ def test_sharded_matcher_world1_rccl(Engine):
         dist.destroy_process_group()
     counts, oids = oracle_ids(wl.filters, wl.topics)
     csr_equal(off.astype(np.uint64), ids, counts, oids)
+
+
+def test_batcher_coalesces_concurrent_callers(Engine):
+    """Concurrent single-topic callers (one PUBLISH each, as emqx_broker:publish/1 calls
+    match_routes/1) get exactly their own results, in batches larger than one."""
+    import threading
+    from emqx_amd import workloads as W
+    from emqx_amd.batcher import Batcher
+    wl = W.config_b(n_filters=50_000, n_topics=2000, seed=13)
+    e = Engine()
+    e.insert_packed(*wl.filters)
+    e.commit()
+    topics = W.unpack(wl.topics)
+    expect = e.match(topics, mode=0)
+    b = Batcher(e, mode=0, max_batch=512, max_wait_us=2000)
+    got = [None] * len(topics)
+
+    def worker(k):
+        for i in range(k, len(topics), 32):
+            got[i] = sorted(b.match(topics[i]))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(32)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    st = b.stats()
+    b.close()
+    assert got == expect
+    assert st["topics"] == len(topics)
+    assert st["batches"] < len(topics) // 4
