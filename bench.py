@@ -149,9 +149,12 @@ def main():
     alg_bytes = tbytes + 64 * levels + 64 * evals + 4 * (nout + n)
     kms = float(np.mean(kern_ms)) if kern_ms else float("nan")
     achieved = alg_bytes / (kms * 1e-3) / 1e9
+    traffic, traffic_src = args.traffic_bytes, "--traffic-bytes"
+    if traffic is None:
+        traffic, traffic_src = measured_traffic(n, args)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": args.traffic_bytes, "kernel": "match_fast_kernel",
+                "traffic": traffic, "traffic_source": traffic_src, "kernel": "match_fast_kernel",
                 "kernel_ms_avg": round(kms, 4), "alg_bytes_per_launch": alg_bytes,
                 "alg_bytes_model": "len(T) + 64*L(T) + 64*evals(T) + 4*(|M(T)|+1) per topic (SURVEY §8 d)"}
 
@@ -248,6 +251,19 @@ def sharded_bench(args, rank, world, dev):
         }), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def measured_traffic(n, args):
+    """HBM bytes per launch of the fused match kernel from the committed rocprofv3 PMC passes
+    (profiles/pmc_match_fast.json, written from tools/gpu_round.sh's counter runs on the same
+    workload), scaled to this batch.  None when the file is absent or the workload differs."""
+    path = os.path.join(ROOT, "profiles", "pmc_match_fast.json")
+    if not os.path.exists(path) or args.n_filters != 10_000_000 or args.mode != 0 or args.vocab_scale != 1:
+        return None, None
+    with open(path) as f:
+        p = json.load(f)
+    per_topic = p["traffic_bytes_per_launch"] / p["batch_topics"]
+    return round(per_topic * n), "profiles/pmc_match_fast.json (%s; %s)" % (p["traffic_rule"], p["source"])
 
 
 def load_or_make(args, rank, make):
