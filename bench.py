@@ -54,6 +54,10 @@ def main():
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
+    ap.add_argument("--workload", type=str, default="B", choices=["B", "E"],
+                    help="E = publish fan-out (SURVEY §8 d config E): match + fan-out per step")
+    ap.add_argument("--strategy", type=str, default="hash_clientid",
+                    help="$share strategy for --workload E")
     ap.add_argument("--sharded", action="store_true",
                     help="filter-sharded table (filter i on rank i mod N): rank 0's batch is broadcast over "
                          "RCCL, matched on every shard, gathered and concatenated on rank 0 (strong scaling)")
@@ -80,6 +84,8 @@ def main():
     # every rank replicates the table (seed 2); each rank draws its own topic stream (weak scaling)
     if args.sharded:
         return sharded_bench(args, rank, world, dev)
+    if args.workload == "E":
+        return fanout_bench(args, rank, world, dev)
     wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
                                                      vocab_scale=args.vocab_scale,
                                                      topic_seed=None if rank == 0 else 1000 + rank))
@@ -264,6 +270,133 @@ def measured_traffic(n, args):
         p = json.load(f)
     per_topic = p["traffic_bytes_per_launch"] / p["batch_topics"]
     return round(per_topic * n), "profiles/pmc_match_fast.json (%s; %s)" % (p["traffic_rule"], p["source"])
+
+
+def fanout_bench(args, rank, world, dev):
+    """Config E: 10M subscriptions (1M subscribers x 10 filters over a 2M-filter config-B table,
+    10% in $share groups of 2-16 members).  A step = match (emqx_match_batch_device) + fan-out
+    (emqx_fanout_batch_device) of one 1M-topic batch resident in HBM -> per-topic CSR of
+    (subscriber, filter) deliveries in HBM.  Replicated tables, weak scaling over ranks."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    from emqx_amd.fanout import SubTable
+    t0 = time.time()
+    fw = W.config_e(n_topics=args.batch)
+    log(f"[rank {rank}] config E: {fw.wl.n_filters} filters, {fw.n_subscriptions} subscriptions ({time.time() - t0:.1f}s)")
+    eng = Engine(dev.index)
+    eng.insert_packed(*fw.wl.filters)
+    eng.commit()
+    st = SubTable(dev.index)
+    st.add(fw.sub_filter, fw.sub_id, fw.sub_group)
+    st.commit()
+    log(f"[rank {rank}] subtab {st.stats()}")
+    n = fw.wl.n_topics
+    tb = torch.from_numpy(fw.wl.topics[0]).to(dev)
+    to = torch.from_numpy(fw.wl.topics[1].view(np.int64)).to(dev)
+    keys = torch.from_numpy(fw.keys.view(np.int32)).to(dev)
+    moff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    mcap = 32 * n
+    mids = torch.empty(mcap, dtype=torch.int32, device=dev)
+    ooff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ocap = 128 * n
+    osubs = torch.empty(ocap, dtype=torch.int32, device=dev)
+    ofil = torch.empty(ocap, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fo_ms = []
+
+    def step():
+        nm = eng.match_device(tb.data_ptr(), to.data_ptr(), n, moff.data_ptr(), mids.data_ptr(), mcap, mode=0,
+                              stream=stream)
+        ev[0].record()
+        nd = st.fanout_device(args.strategy, moff.data_ptr(), mids.data_ptr(), n, keys.data_ptr(), ooff.data_ptr(),
+                              osubs.data_ptr(), ofil.data_ptr(), ocap, stream=stream)
+        ev[1].record()
+        return nm, nd
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    kern = []
+    for _ in range(args.steps):
+        nm, nd = step()
+        ev[1].synchronize()
+        fo_ms.append(ev[0].elapsed_time(ev[1]))
+        kern.append(eng.stats()["last_match_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    fo = float(np.median(fo_ms))
+    alg = 32 * nm + 12 * nd  # per match entry: id, filter record, offsets, topic; per delivery: read + 2 writes
+    res = {
+        "metric": "published topics matched and fanned out/sec (config E, 10M subscriptions)",
+        "value": round(n * world * args.steps / elapsed, 1), "unit": "topics/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "E: end-to-end publish fan-out, match -> subscriber ids incl. $share, 10M subs",
+                   "n_filters": fw.wl.n_filters, "subscriptions": fw.n_subscriptions, "batch_topics_per_gpu": n,
+                   "strategy": args.strategy, "parallelism": f"replicated tables, topic stream split x{world}"},
+        "deliveries_per_s": round(nd * world * args.steps / elapsed, 1),
+        "matches_per_topic": round(nm / n, 3), "deliveries_per_topic": round(nd / n, 3),
+        "match_call_ms": round(float(np.median(kern)), 4), "fanout_call_ms": round(fo, 4),
+        "fanout_roofline": {"bound": "hbm", "achieved": round(alg / (fo * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(alg / (fo * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "alg_bytes_per_call": alg,
+                            "alg_bytes_model": "32 B per match entry + 12 B per delivery; call time incl. "
+                                               "count/scan/offsets, one D2H of the total and the write kernel"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = fanout_cpu_baseline(fw, args)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def fanout_cpu_baseline(fw, args):
+    """Host restatement of publish/1's lookup + dispatch on a bounded sample: the C++ port of
+    emqx_trie's DFS (oracle) for the match, then per matched filter a dictionary read of its
+    subscribers and one pick per $share group (like the ?SUBSCRIBER / shared-sub ETS reads)."""
+    from emqx_amd import workloads as W
+    from oracle import cpp as C
+    o = C.CppOracle(True)
+    o.add_packed(*fw.wl.filters)
+    o.freeze()
+    plain, groups = {}, {}
+    for f, s_, g in zip(fw.sub_filter.tolist(), fw.sub_id.tolist(), fw.sub_group.tolist()):
+        if g == W.NO_GROUP:
+            plain.setdefault(f, []).append(s_)
+        else:
+            groups.setdefault(f, {}).setdefault(g, []).append(s_)
+    sample = min(20_000, fw.wl.n_topics)
+    s = W.take(fw.wl.topics, np.arange(sample))
+    t0 = time.perf_counter()
+    counts, ids, _ = o.match_packed(*s, mode=0, threads=1, stride=256)
+    nd = 0
+    keys = fw.keys
+    for i in range(sample):
+        for f in ids[i, :counts[i]].tolist():
+            out = list(plain.get(f, ()))
+            for mem in groups.get(f, {}).values():
+                out.append(mem[keys[i] % len(mem)])
+            nd += len(out)
+    dt = time.perf_counter() - t0
+    return {"value": round(sample / dt, 1), "unit": "topics/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample} topics; C++ DFS match + Python dict fan-out, one thread",
+            "deliveries_per_topic": round(nd / sample, 3)}
 
 
 def load_or_make(args, rank, make):

@@ -34,7 +34,13 @@ EXPORTS = (
     "emqx_match_batch_device", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
     "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_batcher_create",
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_strerror", "emqx_version",
+    "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
+    "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_publish_batch",
 )
+
+NO_GROUP = 0xFFFFFFFF
+FANOUT_SHARED_BIT = 0x80000000
+SHARE_RANDOM, SHARE_ROUND_ROBIN, SHARE_STICKY, SHARE_HASH_CLIENTID, SHARE_HASH_TOPIC = 0, 1, 2, 3, 4
 
 
 class EngineError(RuntimeError):
@@ -99,6 +105,14 @@ def lib():
         "emqx_batcher_submit": (i32, [vp, vp, u64, vp]),
         "emqx_batcher_destroy": (i32, [vp]),
         "emqx_batcher_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "emqx_subtab_create": (i32, [ctypes.c_int32, ctypes.POINTER(vp)]),
+        "emqx_subtab_destroy": (i32, [vp]),
+        "emqx_subtab_add": (i32, [vp, vp, vp, vp, u64]),
+        "emqx_subtab_remove": (i32, [vp, vp, vp, vp, u64]),
+        "emqx_subtab_commit": (i32, [vp]),
+        "emqx_subtab_stats": (i32, [vp, vp]),
+        "emqx_fanout_batch_device": (i32, [vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
+        "emqx_publish_batch": (i32, [vp, vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]),
         "emqx_strerror": (ctypes.c_char_p, [i32]),
         "emqx_version": (ctypes.c_char_p, []),
     }

@@ -315,5 +315,68 @@ def config_d(n_filters: int = 1_000_000, n_topics: int = 100_000, seed: int = 4,
     return Workload("D", filters, topics)
 
 
+# ---------------------------------------------------------------------------------------
+# Config E (publish fan-out)
+# ---------------------------------------------------------------------------------------
+
+NO_GROUP = 0xFFFFFFFF
+
+
+@dataclass
+class FanoutWorkload:
+    wl: Workload              # route table (filters) + topic stream
+    sub_filter: np.ndarray    # uint32 filter id per subscription
+    sub_id: np.ndarray        # uint32 subscriber id
+    sub_group: np.ndarray     # uint32 $share group id, NO_GROUP for plain subscriptions
+    keys: np.ndarray          # uint32 per-topic pick key (stands in for erlang:phash2, < 2^27)
+
+    @property
+    def n_subscriptions(self) -> int:
+        return len(self.sub_id)
+
+
+def config_e(n_filters: int = 2_000_000, n_subscribers: int = 1_000_000, per_sub: int = 10,
+             shared_frac: float = 0.1, n_topics: int = 1_000_000, seed: int = 5, groups: int = 8,
+             min_group: int = 2, max_group: int = 16) -> FanoutWorkload:
+    """SURVEY §8 d config E: n_subscribers x per_sub subscriptions over config B's generator
+    table of n_filters; shared_frac of them in $share groups g0..g7 of U{2..16} members
+    (one group instance = (filter, group, members)), the rest plain (deduplicated
+    (filter, subscriber) pairs); topics from config B's topic generator."""
+    wl = config_b(n_filters=n_filters, n_topics=n_topics, seed=seed)
+    rng = np.random.default_rng(seed + 1000)
+    total = n_subscribers * per_sub
+    n_shared = int(total * shared_frac)
+    # plain
+    n_plain = total - n_shared
+    ps = (np.arange(n_plain, dtype=np.uint64) % np.uint64(n_subscribers))
+    pf = rng.integers(0, n_filters, n_plain).astype(np.uint64)
+    key = np.unique((pf << np.uint64(32)) | ps)
+    pf, ps = (key >> np.uint64(32)).astype(np.uint32), (key & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    # shared group instances until n_shared memberships
+    sizes = []
+    acc = 0
+    while acc < n_shared:
+        k = int(rng.integers(min_group, max_group + 1))
+        sizes.append(k)
+        acc += k
+    sizes = np.array(sizes, dtype=np.int64)
+    ng = len(sizes)
+    gf = rng.integers(0, n_filters, ng).astype(np.uint64)
+    gg = rng.integers(0, groups, ng).astype(np.uint64)
+    gkey, first = np.unique((gf << np.uint64(3)) | gg, return_index=True)  # one instance per (filter, group)
+    sizes, gf, gg = sizes[first], gf[first], gg[first]
+    sf = np.repeat(gf, sizes).astype(np.uint32)
+    sg = np.repeat(gg, sizes).astype(np.uint32)
+    ss = rng.integers(0, n_subscribers, int(sizes.sum())).astype(np.uint32)
+    # members of one instance are distinct subscribers (duplicates dropped, order kept)
+    mk = (sf.astype(np.uint64) << np.uint64(35)) | (sg.astype(np.uint64) << np.uint64(32)) | ss.astype(np.uint64)
+    _, keep = np.unique(mk, return_index=True)
+    keep.sort()
+    sf, sg, ss = sf[keep], sg[keep], ss[keep]
+    keys = rng.integers(0, 1 << 27, n_topics).astype(np.uint32)
+    return FanoutWorkload(wl, np.concatenate([pf, sf]), np.concatenate([ps, ss]),
+                          np.concatenate([np.full(len(pf), NO_GROUP, np.uint32), sg]), keys)
+
+
 def config_by_name(name: str, **kw) -> Workload:
     return {"A": config_a, "A'": config_a_prime, "B": config_b, "D": config_d}[name](**kw)

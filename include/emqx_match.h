@@ -136,6 +136,63 @@ int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, voi
 int emqx_batcher_destroy(emqx_batcher* b);
 int emqx_batcher_stats(emqx_batcher* b, uint64_t* n_batches, uint64_t* n_topics);
 
+/* ---- publish fan-out ------------------------------------------------------------
+ * A subscription table maps the filter ids reported by a match (engine ids, or the ext ids of
+ * emqx_insert_filters_ext) to subscribers.  It replaces the broker's ETS tables
+ *   ?SUBSCRIBER  Topic -> SubPid | {shard, I}      apps/emqx/src/emqx_broker.erl:96-108,146-158
+ *   emqx_shared_subscription {Group, Topic, SubPid} apps/emqx/src/emqx_shared_sub.erl:78-91,300-314
+ * and the dispatch that follows match_routes/1 in emqx_broker:publish/1:
+ *   route/2 + aggre/1 + do_dispatch/2,3            apps/emqx/src/emqx_broker.erl:244-272,500-524
+ *   emqx_shared_sub:dispatch/3, pick/6, do_pick/6  apps/emqx/src/emqx_shared_sub.erl:113-126,251-288
+ * Subscriber ids and group ids are the caller's uint32 handles (the NIF maps pids and group
+ * names to them).  Filter ids must be < 2^31.  A delivery is (subscriber id, filter id); the
+ * filter id has EMQX_FANOUT_SHARED_BIT set when the delivery is a $share pick ({share, To, ...}
+ * in publish_result(), emqx_types.erl:201-206).  Fan-out calls on one table are serialised
+ * (the round_robin and sticky strategies update per-group state). */
+#define EMQX_NO_GROUP 0xFFFFFFFFu
+#define EMQX_FANOUT_SHARED_BIT 0x80000000u
+
+/* broker.shared_subscription_strategy (emqx_shared_sub.erl:60-65) */
+#define EMQX_SHARE_RANDOM 0          /* rand:uniform(N)                               */
+#define EMQX_SHARE_ROUND_ROBIN 1     /* per-group counter                              */
+#define EMQX_SHARE_STICKY 2          /* first pick random, then kept while subscribed  */
+#define EMQX_SHARE_HASH_CLIENTID 3   /* 1 + Key rem N, Key = erlang:phash2(ClientId)   */
+#define EMQX_SHARE_HASH_TOPIC 4      /* 1 + Key rem N, Key = erlang:phash2(Topic)      */
+
+typedef struct emqx_subtab emqx_subtab; /* opaque */
+
+int emqx_subtab_create(int32_t device, emqx_subtab** out);
+int emqx_subtab_destroy(emqx_subtab* s);
+/* emqx_broker:subscribe/3 (emqx_broker.erl:124-163): subscriber sub_ids[i] subscribes to
+ * filter_ids[i], plainly (group_ids NULL or EMQX_NO_GROUP) or in $share group group_ids[i].
+ * Idempotent: re-subscribing keeps the member's place in its group (ETS bag semantics). */
+int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids,
+                    const uint32_t* group_ids, uint64_t n);
+/* emqx_broker:unsubscribe/1 (emqx_broker.erl:169-195); absent pairs are ignored. */
+int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids,
+                       const uint32_t* group_ids, uint64_t n);
+/* Publishes the mutations to the device (sticky picks of members that left are dropped). */
+int emqx_subtab_commit(emqx_subtab* s);
+/* counts[0..3] = live plain subscriptions, live shared memberships, groups with members,
+ * device bytes */
+int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4);
+
+/* Fan-out of a match CSR already in HBM (d_match_offsets[n+1], d_match_ids): per-topic CSR of
+ * deliveries d_out_offsets[n+1], d_out_subs[], d_out_filters[] (optional, may be NULL).
+ * d_pick_keys[n] (device) is required for the hash strategies.  On EMQX_EOVERFLOW nothing is
+ * written to the id arrays and *n_out is the capacity required. */
+int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
+                             const uint32_t* d_match_ids, uint64_t n, const uint32_t* d_pick_keys,
+                             uint64_t* d_out_offsets, uint32_t* d_out_subs, uint32_t* d_out_filters,
+                             uint64_t cap, uint64_t* n_out, void* stream);
+/* emqx_broker:publish/1's lookup + fan-out for a batch of topics (host buffers): match
+ * (mode EMQX_MODE_ROUTES) and fan-out run back to back on the device; the match CSR never
+ * leaves HBM.  pick_keys[n] (host) as above. */
+int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const uint8_t* topic_bytes,
+                       const uint64_t* topic_offsets, uint64_t n, const uint32_t* pick_keys,
+                       uint64_t* out_offsets, uint32_t* out_subs, uint32_t* out_filters, uint64_t cap,
+                       uint64_t* n_out);
+
 /* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */
 int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filter,
                      uint64_t filter_len);

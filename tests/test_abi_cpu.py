@@ -93,6 +93,32 @@ def test_engine_without_gpu_fails_loudly(L):
     assert ei.value.code == -3   # EMQX_EDEVICE
 
 
+def test_subtab_without_gpu_fails_loudly(L):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from emqx_amd.fanout import SubTable
+    from emqx_amd.engine import EngineError
+    with pytest.raises(EngineError) as ei:
+        SubTable()
+    assert ei.value.code == -3
+
+
+def test_config_e_shapes():
+    import numpy as np
+    from emqx_amd import workloads as W
+    e = W.config_e(n_filters=20_000, n_subscribers=10_000, n_topics=500)
+    shared = e.sub_group != W.NO_GROUP
+    assert abs(int(shared.sum()) - 10_000) < 200          # 10% of 100k subscriptions
+    assert e.n_subscriptions > 98_000 and e.keys.max() < (1 << 27)
+    assert int(e.sub_filter.max()) < 20_000 and int(e.sub_group[shared].max()) < 8
+    rows = np.stack([e.sub_filter, e.sub_group, e.sub_id], 1)
+    assert len(np.unique(rows, axis=0)) == len(rows)        # no duplicate subscription
+    gk = (e.sub_filter[shared].astype(np.uint64) << np.uint64(3)) | e.sub_group[shared].astype(np.uint64)
+    sizes = np.unique(gk, return_counts=True)[1]
+    assert sizes.max() <= 16 and np.median(sizes) >= 2
+
+
 def test_workloads_shapes():
     from emqx_amd import workloads as W
     a = W.config_a(n_topics=2000)

@@ -1,0 +1,101 @@
+"""The fan-out oracle (oracle/broker_ref.py) against the reference's own scenarios.
+
+Scenarios transcribed from apps/emqx/test/emqx_shared_sub_SUITE.erl (test_two_messages/2
+:315-355, t_hash_topic :181-218, t_not_so_sticky :220-243, t_dispatch :297-309) and the
+aggre/route rules of apps/emqx/src/emqx_broker.erl:244-272.  erlang:phash2 values are passed
+in as keys (the suite only asserts phash2(T1) rem 2 =/= phash2(T2) rem 2, :192).
+"""
+
+import pytest
+
+from oracle import broker_ref as B
+
+NODE = B.NODE
+
+
+def two_member_broker():
+    b = B.Broker()
+    b.subscribe(b"foo/bar", "ConnPid1", group=b"group1")
+    b.subscribe(b"foo/bar", "ConnPid2", group=b"group1")
+    return b
+
+
+def picked(deliveries):
+    assert len(deliveries) == 1 and deliveries[0][2]
+    return deliveries[0][1]
+
+
+@pytest.mark.parametrize("strategy", [B.HASH_CLIENTID])
+def test_two_messages_hash_same_client_same_member(strategy):
+    b = two_member_broker()
+    key = 12345  # phash2(<<"ClientId1">>) stand-in: both messages come from ClientId1
+    p1 = picked(b.publish(b"foo/bar", key, strategy))
+    p2 = picked(b.publish(b"foo/bar", key, strategy))
+    assert p1 == p2
+
+
+def test_two_messages_round_robin_alternates():
+    b = two_member_broker()
+    p1 = picked(b.publish(b"foo/bar", 0, B.ROUND_ROBIN))
+    p2 = picked(b.publish(b"foo/bar", 0, B.ROUND_ROBIN))
+    assert p1 != p2
+    assert picked(b.publish(b"foo/bar", 0, B.ROUND_ROBIN)) == p1
+
+
+def test_hash_topic_different_parity_different_member():
+    b = B.Broker()
+    b.subscribe(b"foo/#", "ConnPid1", group=b"group1")
+    b.subscribe(b"foo/#", "ConnPid2", group=b"group1")
+    k1, k2 = 7, 10  # phash2(Topic1) rem 2 =/= phash2(Topic2) rem 2
+    assert picked(b.publish(b"foo/bar1", k1, B.HASH_TOPIC)) != picked(b.publish(b"foo/bar2", k2, B.HASH_TOPIC))
+    # lists:nth(1 + Key rem N, Subs) with Subs in subscription order
+    assert picked(b.publish(b"foo/bar1", 7, B.HASH_TOPIC)) == "ConnPid2"
+    assert picked(b.publish(b"foo/bar1", 10, B.HASH_TOPIC)) == "ConnPid1"
+
+
+def test_not_so_sticky_follows_resubscription():
+    b = B.Broker()
+    b.subscribe(b"foo/bar", "C1", group=b"group1")
+    assert b.publish(b"foo/bar", 0, B.HASH_CLIENTID) == [(b"foo/bar", "C1", True)]
+    b.unsubscribe(b"foo/bar", "C1", group=b"group1")
+    assert b.router.lookup_routes(b"foo/bar") == []  # last member gone: route deleted
+    b.subscribe(b"foo/#", "C1", group=b"group1")
+    assert b.publish(b"foo/bar", 0, B.HASH_CLIENTID) == [(b"foo/#", "C1", True)]
+
+
+def test_dispatch_no_subscribers_then_one():
+    b = B.Broker()
+    assert b.publish(b"foo", 0) == []
+    b.subscribe(b"foo", "S", group=b"group1")
+    assert b.publish(b"foo", 0) == [(b"foo", "S", True)]
+
+
+def test_plain_and_shared_on_overlapping_filters():
+    b = B.Broker()
+    b.subscribe(b"a/b", "p1")
+    b.subscribe(b"a/+", "p1")          # same subscriber, second filter: delivered twice
+    b.subscribe(b"a/#", "p2")
+    b.subscribe(b"a/#", "g1", group=b"g")
+    b.subscribe(b"a/#", "g2", group=b"g")
+    b.subscribe(b"a/#", "h1", group=b"h")
+    got = sorted(b.publish(b"a/b", 1, B.HASH_CLIENTID), key=repr)
+    assert got == sorted([(b"a/b", "p1", False), (b"a/+", "p1", False), (b"a/#", "p2", False),
+                          (b"a/#", "g2", True), (b"a/#", "h1", True)], key=repr)
+    b.subscribe(b"a/b", "p1")          # idempotent
+    assert len(b.publish(b"a/b", 1, B.HASH_CLIENTID)) == 5
+
+
+def test_aggre_dedups_group_routes_across_nodes():
+    routes = [(b"t", "n1@h"), (b"t", (b"g", "n1@h")), (b"t", (b"g", "n2@h"))]
+    assert sorted(B.Broker.aggre(routes), key=repr) == sorted([(b"t", "n1@h"), (b"t", b"g")], key=repr)
+    assert B.Broker.aggre([(b"t", (b"g", "n1@h"))]) == [(b"t", b"g")]
+    assert B.Broker.aggre([]) == []
+
+
+def test_dollar_and_wildcard_topics_follow_match_routes():
+    b = B.Broker()
+    b.subscribe(b"#", "all")
+    b.subscribe(b"$SYS/#", "sys")
+    b.subscribe(b"a/+", "exact-wild")  # a wildcard *topic* publish hits only the identical filter
+    assert b.publish(b"$SYS/x", 0) == [(b"$SYS/#", "sys", False)]
+    assert sorted(b.publish(b"a/+", 0), key=repr) == [(b"a/+", "exact-wild", False)]

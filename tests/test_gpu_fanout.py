@@ -1,0 +1,207 @@
+"""GPU parity of the publish fan-out (emqx_amd/csrc/fanout_kernels.hip) against the fan-out
+oracle (oracle/broker_ref.py) and a direct restatement of the dispatch rules on config E.
+
+Deliveries are compared per topic as sorted multisets of (filter, subscriber, shared).
+Hash strategies are exact (keys = the caller's phash2 values); round_robin / sticky / random
+are checked by their invariants (the reference's are per-process and randomly seeded)."""
+
+import collections
+import random
+
+import numpy as np
+import pytest
+
+from oracle import broker_ref as B
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def F():
+    import torch
+    assert torch.cuda.is_available()
+    from emqx_amd import fanout
+    return fanout
+
+
+def scenario_ops(seed, n_filters=60, n_subs=40, n_ops=600):
+    rng = random.Random(seed)
+    words = [b"a", b"b", b"c", b"", b"$SYS"]
+    filters = set()
+    while len(filters) < n_filters:
+        d = rng.randint(1, 4)
+        lv = [rng.choice(words + [b"+"]) for _ in range(d)]
+        if rng.random() < 0.3:
+            lv.append(b"#")
+        filters.add(b"/".join(lv))
+    filters = sorted(filters)
+    ops = []
+    for _ in range(n_ops):
+        f = rng.choice(filters)
+        s = "s%d" % rng.randrange(n_subs)
+        g = rng.choice([None, None, b"g1", b"g2"])
+        ops.append(("sub" if rng.random() < 0.85 else "unsub", f, s, g))
+    topics = []
+    for _ in range(300):
+        d = rng.randint(1, 5)
+        topics.append(b"/".join(rng.choice(words) for _ in range(d)))
+    topics += [b"a/+", b"#", b"$SYS/a"]
+    return ops, topics
+
+
+def canon(rows):
+    return sorted((f, str(s), sh) for f, s, sh in rows)
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("strategy", [B.HASH_CLIENTID, B.HASH_TOPIC])
+def test_broker_hash_strategies_exact(F, seed, strategy):
+    ops, topics = scenario_ops(seed)
+    ref = B.Broker()
+    dev = F.Broker(0, node=B.NODE, strategy=strategy)
+    for op, f, s, g in ops:
+        getattr(ref, "subscribe" if op == "sub" else "unsubscribe")(f, s, g)
+        getattr(dev, "subscribe" if op == "sub" else "unsubscribe")(f, s, g)
+    keys = [random.Random(seed * 7 + i).randrange(1 << 27) for i in range(len(topics))]
+    got = dev.publish_batch(topics, keys)
+    for t, k, row in zip(topics, keys, got):
+        assert canon(row) == canon(ref.publish(t, k, strategy)), t
+
+
+def test_two_messages_scenarios(F):
+    """emqx_shared_sub_SUITE test_two_messages/2 on the device for every strategy."""
+    for name in ["random", "round_robin", "sticky", "hash", "hash_clientid"]:
+        b = F.Broker(0, strategy=name)
+        b.subscribe(b"foo/bar", "ConnPid1", share=b"group1")
+        b.subscribe(b"foo/bar", "ConnPid2", share=b"group1")
+        r1 = b.publish(b"foo/bar", key=99)
+        r2 = b.publish(b"foo/bar", key=99)
+        assert len(r1) == len(r2) == 1 and r1[0][2] and r2[0][2]
+        if name == "sticky" or name.startswith("hash"):
+            assert r1[0][1] == r2[0][1], name
+        if name == "round_robin":
+            assert r1[0][1] != r2[0][1]
+
+
+def test_not_so_sticky_and_dispatch(F):
+    b = F.Broker(0, strategy="sticky")
+    assert b.publish(b"foo/bar") == []
+    b.subscribe(b"foo/bar", "C1", share=b"group1")
+    assert b.publish(b"foo/bar") == [(b"foo/bar", "C1", True)]
+    b.unsubscribe(b"foo/bar", "C1", share=b"group1")
+    b.subscribe(b"foo/#", "C1", share=b"group1")
+    assert b.publish(b"foo/bar") == [(b"foo/#", "C1", True)]
+    # a sticky member that leaves is replaced by one still subscribed
+    b.subscribe(b"foo/#", "C2", share=b"group1")
+    first = b.publish(b"foo/bar")[0][1]
+    b.unsubscribe(b"foo/#", first, share=b"group1")
+    other = "C2" if first == "C1" else "C1"
+    assert [b.publish(b"foo/bar")[0][1] for _ in range(3)] == [other] * 3
+
+
+def test_round_robin_and_random_invariants(F):
+    b = F.Broker(0, strategy="round_robin")
+    members = ["m%d" % i for i in range(5)]
+    for m in members:
+        b.subscribe(b"x/+", m, share=b"g")
+    b.subscribe(b"x/+", "lone", share=b"solo")
+    topics = [b"x/%d" % i for i in range(1000)]
+    rows = b.publish_batch(topics)
+    picks = collections.Counter(r[1] for row in rows for r in row if r[0] == b"x/+" and r[1] != "lone")
+    assert sum(picks.values()) == 1000 and set(picks) == set(members)
+    assert all(v == 200 for v in picks.values())  # 1000 consecutive counter values, 5 members
+    assert all(sum(1 for r in row if r[1] == "lone") == 1 for row in rows)
+    rows = b.publish_batch(topics, strategy="random")
+    picks = collections.Counter(r[1] for row in rows for r in row if r[1] != "lone")
+    assert set(picks) == set(members) and min(picks.values()) > 120
+
+
+def expected_fanout(moff, mids, fw, keys, lo, hi):
+    """Per-topic sorted (sub, filter|shared_bit) pairs for topics [lo, hi) with hash picks:
+    plain subscribers of each matched filter, plus lists:nth(1 + key rem N, Members) for each
+    group (members in subscription order)."""
+    from emqx_amd.workloads import NO_GROUP
+    plain = collections.defaultdict(list)
+    groups = collections.defaultdict(dict)
+    for f, s, g in zip(fw.sub_filter.tolist(), fw.sub_id.tolist(), fw.sub_group.tolist()):
+        if g == NO_GROUP:
+            plain[f].append(s)
+        else:
+            groups[f].setdefault(g, []).append(s)
+    out = []
+    for t in range(lo, hi):
+        row = []
+        for f in mids[moff[t]:moff[t + 1]].tolist():
+            row += [(s, f) for s in plain.get(f, [])]
+            for g, mem in groups.get(f, {}).items():
+                row.append((mem[keys[t] % len(mem)], f | 0x80000000))
+        out.append(sorted(row))
+    return out
+
+
+def test_config_e_reduced_device_pipeline(F):
+    """Config E generator at reduced scale through the device-pointer API: match CSR in HBM ->
+    emqx_fanout_batch_device -> compared with the dispatch rules applied to the same CSR."""
+    import torch
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    fw = W.config_e(n_filters=200_000, n_subscribers=100_000, n_topics=50_000, seed=5)
+    eng = Engine(0)
+    eng.insert_packed(*fw.wl.filters)
+    eng.commit()
+    st = F.SubTable(0)
+    st.add(fw.sub_filter, fw.sub_id, fw.sub_group)
+    st.commit()
+    stats = st.stats()
+    assert stats["plain"] + stats["shared_members"] == fw.n_subscriptions
+    dev = torch.device("cuda", 0)
+    tb = torch.from_numpy(fw.wl.topics[0]).to(dev)
+    to = torch.from_numpy(fw.wl.topics[1].view(np.int64)).to(dev)
+    n = fw.wl.n_topics
+    moff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    mids = torch.empty(64 * n, dtype=torch.int32, device=dev)
+    nm = eng.match_device(tb.data_ptr(), to.data_ptr(), n, moff.data_ptr(), mids.data_ptr(), 64 * n)
+    keys = torch.from_numpy(fw.keys.view(np.int32)).to(dev)
+    ooff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    with pytest.raises(Exception) as ei:
+        st.fanout_device("hash_clientid", moff.data_ptr(), mids.data_ptr(), n, keys.data_ptr(), ooff.data_ptr(),
+                         0, 0, 0)
+    need = ei.value.needed
+    osubs = torch.empty(need, dtype=torch.int32, device=dev)
+    ofil = torch.empty(need, dtype=torch.int32, device=dev)
+    tot = st.fanout_device("hash_clientid", moff.data_ptr(), mids.data_ptr(), n, keys.data_ptr(), ooff.data_ptr(),
+                           osubs.data_ptr(), ofil.data_ptr(), need)
+    torch.cuda.synchronize()
+    assert tot == need
+    mo, mi = moff.cpu().numpy(), mids[:nm].cpu().numpy().view(np.uint32)
+    oo, os_, of = ooff.cpu().numpy(), osubs.cpu().numpy().view(np.uint32), ofil.cpu().numpy().view(np.uint32)
+    assert oo[0] == 0 and oo[-1] == tot and np.all(np.diff(oo) >= 0)
+    exp = expected_fanout(mo, mi, fw, fw.keys, 0, 4000)
+    for t in range(4000):
+        got = sorted(zip(os_[oo[t]:oo[t + 1]].tolist(), of[oo[t]:oo[t + 1]].tolist()))
+        assert got == exp[t], t
+    # whole batch: per-topic delivery counts
+    from emqx_amd.workloads import NO_GROUP
+    per_f = np.zeros(fw.wl.n_filters, dtype=np.int64)
+    np.add.at(per_f, fw.sub_filter[fw.sub_group == NO_GROUP].astype(np.int64), 1)
+    gk = np.unique((fw.sub_filter[fw.sub_group != NO_GROUP].astype(np.uint64) << np.uint64(8))
+                   | fw.sub_group[fw.sub_group != NO_GROUP].astype(np.uint64))
+    np.add.at(per_f, (gk >> np.uint64(8)).astype(np.int64), 1)
+    cnt = np.add.reduceat(per_f[mi.astype(np.int64)], mo[:-1].astype(np.int64)) if nm else np.zeros(n)
+    cnt = np.where(np.diff(mo) > 0, cnt, 0)
+    assert np.array_equal(np.diff(oo), cnt)
+
+
+def test_empty_batches_and_tables(F):
+    from emqx_amd.engine import Engine
+    eng = Engine(0)
+    st = F.SubTable(0)
+    off, subs, fils = F.publish_packed(eng, st, "round_robin", np.zeros(1, np.uint8), np.zeros(1, np.uint64))
+    assert len(off) == 1 and off[0] == 0 and subs.size == 0
+    eng.insert([b"a/#"])
+    eng.commit()
+    from emqx_amd.engine import pack
+    off, subs, fils = F.publish_packed(eng, st, "round_robin", *pack([b"a/b", b"a"]))
+    assert list(off) == [0, 0, 0]
+    with pytest.raises(Exception):  # hash strategies need keys
+        F.publish_packed(eng, st, "hash_topic", *pack([b"a/b"]))
