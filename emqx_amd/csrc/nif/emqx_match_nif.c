@@ -1,0 +1,433 @@
+/*
+ * emqx_match_nif.c — thin Erlang NIF over the engine's C ABI (include/emqx_match.h).
+ *
+ * This is the reference-side binding: EMQX's Erlang modules keep their call shapes and call
+ * these NIFs (see INTEGRATION.md for the Erlang stubs and the edits to emqx_trie.erl,
+ * emqx_router.erl and emqx_broker.erl).  Built only where OTP's erl_nif.h exists
+ * (`make -C emqx_amd/csrc/nif ERL_INCLUDE=...`); this image has no Erlang/OTP,
+ * so the C ABI underneath is what the repo's tests exercise directly.
+ *
+ * Scheduling: every call that touches the device runs on a DIRTY CPU scheduler.  The
+ * per-PUBLISH lookup (emqx_router:match_routes/1, apps/emqx/src/emqx_router.erl:127-133, called
+ * from each publisher process, emqx_broker.erl:213) goes through the cross-caller batcher:
+ * match_async/3 returns at once and the engine's worker thread enif_send()s {Ref, Ids} to the
+ * caller when its batch completes, so many publisher processes share one kernel launch.
+ *
+ * Errors: {error, Atom} with Atom in einval | enomem | device_error | overflow | not_found |
+ * too_deep; non-binary topics raise badarg (the reference's `when is_binary(Topic)` guards).
+ */
+#include <erl_nif.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/emqx_match.h"
+
+static ErlNifResourceType* RES_ENGINE;
+static ErlNifResourceType* RES_SUBTAB;
+static ErlNifResourceType* RES_BATCHER;
+
+typedef struct { emqx_engine* e; } engine_res;
+typedef struct { emqx_subtab* s; } subtab_res;
+typedef struct { emqx_batcher* b; engine_res* owner; } batcher_res;
+
+static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_EINVAL, ATOM_ENOMEM, ATOM_DEVICE,
+    ATOM_OVERFLOW, ATOM_NOTFOUND, ATOM_TOODEEP, ATOM_UNKNOWN;
+
+static ERL_NIF_TERM err_term(ErlNifEnv* env, int rc) {
+  ERL_NIF_TERM a;
+  switch (rc) {
+    case EMQX_EINVAL: a = ATOM_EINVAL; break;
+    case EMQX_ENOMEM: a = ATOM_ENOMEM; break;
+    case EMQX_EDEVICE: a = ATOM_DEVICE; break;
+    case EMQX_EOVERFLOW: a = ATOM_OVERFLOW; break;
+    case EMQX_ENOTFOUND: a = ATOM_NOTFOUND; break;
+    case EMQX_ETOODEEP: a = ATOM_TOODEEP; break;
+    default: a = ATOM_UNKNOWN; break;
+  }
+  return enif_make_tuple2(env, ATOM_ERROR, a);
+}
+
+static void engine_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  engine_res* r = (engine_res*)obj;
+  if (r->e) emqx_engine_destroy(r->e);
+  r->e = NULL;
+}
+
+static void subtab_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  subtab_res* r = (subtab_res*)obj;
+  if (r->s) emqx_subtab_destroy(r->s);
+  r->s = NULL;
+}
+
+static void batcher_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  batcher_res* r = (batcher_res*)obj;
+  if (r->b) emqx_batcher_destroy(r->b); /* drains pending submissions */
+  r->b = NULL;
+  if (r->owner) enif_release_resource(r->owner);
+  r->owner = NULL;
+}
+
+/* Packs a list of binaries into one buffer + offsets (malloc'd; caller frees). */
+static int pack_binaries(ErlNifEnv* env, ERL_NIF_TERM list, uint8_t** bytes, uint64_t** offs, unsigned* n_out) {
+  unsigned n;
+  if (!enif_get_list_length(env, list, &n)) return 0;
+  *offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  size_t total = 0;
+  ERL_NIF_TERM head, tail = list;
+  ErlNifBinary bin;
+  for (unsigned i = 0; i < n; ++i) {
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_inspect_binary(env, head, &bin)) {
+      free(*offs);
+      return 0;
+    }
+    total += bin.size;
+  }
+  *bytes = (uint8_t*)malloc(total ? total : 1);
+  (*offs)[0] = 0;
+  tail = list;
+  for (unsigned i = 0; i < n; ++i) {
+    enif_get_list_cell(env, tail, &head, &tail);
+    enif_inspect_binary(env, head, &bin);
+    memcpy(*bytes + (*offs)[i], bin.data, bin.size);
+    (*offs)[i + 1] = (*offs)[i] + bin.size;
+  }
+  *n_out = n;
+  return 1;
+}
+
+static ERL_NIF_TERM u32_list(ErlNifEnv* env, const uint32_t* v, uint64_t n) {
+  ERL_NIF_TERM l = enif_make_list(env, 0);
+  for (uint64_t i = n; i > 0; --i) l = enif_make_list_cell(env, enif_make_uint(env, v[i - 1]), l);
+  return l;
+}
+
+/* new_engine(Device) -> {ok, Ref} | {error, Reason} */
+static ERL_NIF_TERM nif_new_engine(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  int dev;
+  (void)argc;
+  if (!enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
+  emqx_engine_opts o = {dev, 0};
+  engine_res* r = (engine_res*)enif_alloc_resource(RES_ENGINE, sizeof(engine_res));
+  int rc = emqx_engine_create(&o, &r->e);
+  if (rc != EMQX_OK) {
+    r->e = NULL;
+    enif_release_resource(r);
+    return err_term(env, rc);
+  }
+  ERL_NIF_TERM t = enif_make_resource(env, r);
+  enif_release_resource(r);
+  return enif_make_tuple2(env, ATOM_OK, t);
+}
+
+/* insert(Eng, [Filter]) -> {ok, [Id]}  (emqx_trie:insert/1, emqx_router:do_add_route/2) */
+static ERL_NIF_TERM nif_insert(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* r;
+  uint8_t* bytes;
+  uint64_t* offs;
+  unsigned n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !pack_binaries(env, argv[1], &bytes, &offs, &n))
+    return enif_make_badarg(env);
+  uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  int rc = emqx_insert_filters(r->e, bytes, offs, n, ids);
+  ERL_NIF_TERM out = rc == EMQX_OK ? enif_make_tuple2(env, ATOM_OK, u32_list(env, ids, n)) : err_term(env, rc);
+  free(ids);
+  free(bytes);
+  free(offs);
+  return out;
+}
+
+/* delete(Eng, [Id]) -> ok  (emqx_trie:delete/1) */
+static ERL_NIF_TERM nif_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* r;
+  unsigned n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
+    return enif_make_badarg(env);
+  uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  ERL_NIF_TERM head, tail = argv[1];
+  for (unsigned i = 0; i < n; ++i) {
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_uint(env, head, &ids[i])) {
+      free(ids);
+      return enif_make_badarg(env);
+    }
+  }
+  int rc = emqx_delete_filters(r->e, ids, n);
+  free(ids);
+  return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
+}
+
+/* commit(Eng) -> ok  (rebuild + epoch swap; dirty CPU, seconds at 10M filters) */
+static ERL_NIF_TERM nif_commit(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* r;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r)) return enif_make_badarg(env);
+  int rc = emqx_commit(r->e);
+  return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
+}
+
+/* empty(Eng) -> boolean()  (emqx_trie:empty/0) */
+static ERL_NIF_TERM nif_empty(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* r;
+  emqx_stats st;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r)) return enif_make_badarg(env);
+  if (emqx_stats_get(r->e, &st) != EMQX_OK) return enif_make_badarg(env);
+  return st.n_filters == 0 ? ATOM_TRUE : ATOM_FALSE;
+}
+
+/* match_batch(Eng, Mode, [Topic]) -> {ok, [[Id]]}  (batched emqx_trie:match/1 and
+ * emqx_router:match_routes/1; dirty CPU) */
+static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* r;
+  unsigned mode, n;
+  uint8_t* bytes;
+  uint64_t* offs;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !enif_get_uint(env, argv[1], &mode) ||
+      !pack_binaries(env, argv[2], &bytes, &offs, &n))
+    return enif_make_badarg(env);
+  uint64_t* out_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  uint64_t cap = 16 * (uint64_t)n + 64, total = 0;
+  uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+  int rc = emqx_match_batch(r->e, mode, bytes, offs, n, out_off, ids, cap, &total);
+  if (rc == EMQX_EOVERFLOW) {
+    free(ids);
+    cap = total;
+    ids = (uint32_t*)malloc(sizeof(uint32_t) * (cap ? cap : 1));
+    rc = emqx_match_batch(r->e, mode, bytes, offs, n, out_off, ids, cap, &total);
+  }
+  ERL_NIF_TERM out;
+  if (rc == EMQX_OK) {
+    ERL_NIF_TERM l = enif_make_list(env, 0);
+    for (unsigned i = n; i > 0; --i)
+      l = enif_make_list_cell(env, u32_list(env, ids + out_off[i - 1], out_off[i] - out_off[i - 1]), l);
+    out = enif_make_tuple2(env, ATOM_OK, l);
+  } else {
+    out = err_term(env, rc);
+  }
+  free(ids);
+  free(out_off);
+  free(bytes);
+  free(offs);
+  return out;
+}
+
+/* ---- cross-caller batcher ------------------------------------------------------ */
+typedef struct {
+  ErlNifPid pid;
+  ErlNifEnv* env;
+  ERL_NIF_TERM ref;
+} waiter;
+
+static void batch_done(void* ctx, int status, const uint32_t* ids, uint64_t n) {
+  waiter* w = (waiter*)ctx;
+  ERL_NIF_TERM res = status == EMQX_OK ? enif_make_tuple2(w->env, ATOM_OK, u32_list(w->env, ids, n))
+                                       : err_term(w->env, status);
+  enif_send(NULL, &w->pid, w->env, enif_make_tuple2(w->env, w->ref, res));
+  enif_free_env(w->env);
+  enif_free(w);
+}
+
+/* new_batcher(Eng, Mode, MaxBatch, MaxWaitUs) -> {ok, Ref} */
+static ERL_NIF_TERM nif_new_batcher(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* r;
+  unsigned mode, max_batch, max_wait;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !enif_get_uint(env, argv[1], &mode) ||
+      !enif_get_uint(env, argv[2], &max_batch) || !enif_get_uint(env, argv[3], &max_wait))
+    return enif_make_badarg(env);
+  batcher_res* b = (batcher_res*)enif_alloc_resource(RES_BATCHER, sizeof(batcher_res));
+  b->owner = NULL;
+  int rc = emqx_batcher_create(r->e, mode, max_batch, max_wait, batch_done, &b->b);
+  if (rc != EMQX_OK) {
+    b->b = NULL;
+    enif_release_resource(b);
+    return err_term(env, rc);
+  }
+  enif_keep_resource(r); /* the engine outlives its batcher */
+  b->owner = r;
+  ERL_NIF_TERM t = enif_make_resource(env, b);
+  enif_release_resource(b);
+  return enif_make_tuple2(env, ATOM_OK, t);
+}
+
+/* match_async(Batcher, Topic, Ref) -> ok; the caller then receives {Ref, {ok, [Id]}} */
+static ERL_NIF_TERM nif_match_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  batcher_res* b;
+  ErlNifBinary bin;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_BATCHER, (void**)&b) || !enif_inspect_binary(env, argv[1], &bin))
+    return enif_make_badarg(env);
+  waiter* w = (waiter*)enif_alloc(sizeof(waiter));
+  enif_self(env, &w->pid);
+  w->env = enif_alloc_env();
+  w->ref = enif_make_copy(w->env, argv[2]);
+  int rc = emqx_batcher_submit(b->b, bin.data, bin.size, w);
+  if (rc != EMQX_OK) {
+    enif_free_env(w->env);
+    enif_free(w);
+    return err_term(env, rc);
+  }
+  return ATOM_OK;
+}
+
+/* ---- fan-out ------------------------------------------------------------------- */
+/* new_subtab(Device) -> {ok, Ref} */
+static ERL_NIF_TERM nif_new_subtab(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  int dev;
+  (void)argc;
+  if (!enif_get_int(env, argv[0], &dev)) return enif_make_badarg(env);
+  subtab_res* r = (subtab_res*)enif_alloc_resource(RES_SUBTAB, sizeof(subtab_res));
+  int rc = emqx_subtab_create(dev, &r->s);
+  if (rc != EMQX_OK) {
+    r->s = NULL;
+    enif_release_resource(r);
+    return err_term(env, rc);
+  }
+  ERL_NIF_TERM t = enif_make_resource(env, r);
+  enif_release_resource(r);
+  return enif_make_tuple2(env, ATOM_OK, t);
+}
+
+/* subscribe(Subtab, [{FilterId, SubId, GroupId | none}], Add :: boolean()) -> ok */
+static ERL_NIF_TERM nif_subscribe(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  subtab_res* r;
+  unsigned n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_SUBTAB, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
+    return enif_make_badarg(env);
+  uint32_t* f = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1) * 3);
+  uint32_t *s = f + n, *g = f + 2 * n;
+  ERL_NIF_TERM head, tail = argv[1];
+  for (unsigned i = 0; i < n; ++i) {
+    const ERL_NIF_TERM* tup;
+    int arity;
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_tuple(env, head, &arity, &tup) || arity != 3 ||
+        !enif_get_uint(env, tup[0], &f[i]) || !enif_get_uint(env, tup[1], &s[i])) {
+      free(f);
+      return enif_make_badarg(env);
+    }
+    if (!enif_get_uint(env, tup[2], &g[i])) g[i] = EMQX_NO_GROUP; /* 'none' */
+  }
+  int rc = enif_is_identical(argv[2], ATOM_TRUE) ? emqx_subtab_add(r->s, f, s, g, n)
+                                                 : emqx_subtab_remove(r->s, f, s, g, n);
+  if (rc == EMQX_OK) rc = emqx_subtab_commit(r->s);
+  free(f);
+  return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
+}
+
+/* publish_batch(Eng, Subtab, Strategy, [{Topic, Key}]) ->
+ *   {ok, [[{SubId, FilterId, Shared :: boolean()}]]}
+ * Key = erlang:phash2(ClientId) or erlang:phash2(Topic) computed by the caller (hash
+ * strategies); any integer otherwise.  Dirty CPU. */
+static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* er;
+  subtab_res* sr;
+  unsigned strategy, n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&er) ||
+      !enif_get_resource(env, argv[1], RES_SUBTAB, (void**)&sr) || !enif_get_uint(env, argv[2], &strategy) ||
+      !enif_get_list_length(env, argv[3], &n))
+    return enif_make_badarg(env);
+  uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  ErlNifBinary* bins = (ErlNifBinary*)malloc(sizeof(ErlNifBinary) * (n ? n : 1));
+  ERL_NIF_TERM head, tail = argv[3];
+  offs[0] = 0;
+  for (unsigned i = 0; i < n; ++i) {
+    const ERL_NIF_TERM* tup;
+    int arity;
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_tuple(env, head, &arity, &tup) || arity != 2 ||
+        !enif_inspect_binary(env, tup[0], &bins[i]) || !enif_get_uint(env, tup[1], &keys[i])) {
+      free(offs);
+      free(keys);
+      free(bins);
+      return enif_make_badarg(env);
+    }
+    offs[i + 1] = offs[i] + bins[i].size;
+  }
+  uint8_t* bytes = (uint8_t*)malloc(offs[n] ? offs[n] : 1);
+  for (unsigned i = 0; i < n; ++i) memcpy(bytes + offs[i], bins[i].data, bins[i].size);
+  uint64_t* out_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  uint64_t cap = 64 * (uint64_t)n + 64, total = 0;
+  uint32_t* subs = (uint32_t*)malloc(sizeof(uint32_t) * cap * 2);
+  int rc = emqx_publish_batch(er->e, sr->s, strategy, bytes, offs, n, keys, out_off, subs, subs + cap, cap, &total);
+  if (rc == EMQX_OK) {
+    ERL_NIF_TERM rows = enif_make_list(env, 0);
+    for (unsigned i = n; i > 0; --i) {
+      ERL_NIF_TERM row = enif_make_list(env, 0);
+      for (uint64_t j = out_off[i]; j > out_off[i - 1]; --j) {
+        const uint32_t fl = subs[cap + j - 1];
+        ERL_NIF_TERM d = enif_make_tuple3(env, enif_make_uint(env, subs[j - 1]),
+                                          enif_make_uint(env, fl & ~EMQX_FANOUT_SHARED_BIT),
+                                          (fl & EMQX_FANOUT_SHARED_BIT) ? ATOM_TRUE : ATOM_FALSE);
+        row = enif_make_list_cell(env, d, row);
+      }
+      rows = enif_make_list_cell(env, row, rows);
+    }
+    free(subs);
+    free(out_off);
+    free(bytes);
+    free(bins);
+    free(keys);
+    free(offs);
+    return enif_make_tuple2(env, ATOM_OK, rows);
+  }
+  free(subs);
+  free(out_off);
+  free(bytes);
+  free(bins);
+  free(keys);
+  free(offs);
+  return err_term(env, rc); /* overflow: the Erlang side splits the batch and retries */
+}
+
+/* topic_match(Name, Filter) -> boolean()  (emqx_topic:match/2 on binaries; normal scheduler) */
+static ERL_NIF_TERM nif_topic_match(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  ErlNifBinary a, b;
+  (void)argc;
+  if (!enif_inspect_binary(env, argv[0], &a) || !enif_inspect_binary(env, argv[1], &b)) return enif_make_badarg(env);
+  return emqx_topic_match(a.data, a.size, b.data, b.size) ? ATOM_TRUE : ATOM_FALSE;
+}
+
+static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
+  (void)priv;
+  (void)info;
+  const ErlNifResourceFlags fl = ERL_NIF_RT_CREATE | ERL_NIF_RT_TAKEOVER;
+  RES_ENGINE = enif_open_resource_type(env, NULL, "emqx_match_engine", engine_dtor, fl, NULL);
+  RES_SUBTAB = enif_open_resource_type(env, NULL, "emqx_match_subtab", subtab_dtor, fl, NULL);
+  RES_BATCHER = enif_open_resource_type(env, NULL, "emqx_match_batcher", batcher_dtor, fl, NULL);
+  ATOM_OK = enif_make_atom(env, "ok");
+  ATOM_ERROR = enif_make_atom(env, "error");
+  ATOM_TRUE = enif_make_atom(env, "true");
+  ATOM_FALSE = enif_make_atom(env, "false");
+  ATOM_EINVAL = enif_make_atom(env, "einval");
+  ATOM_ENOMEM = enif_make_atom(env, "enomem");
+  ATOM_DEVICE = enif_make_atom(env, "device_error");
+  ATOM_OVERFLOW = enif_make_atom(env, "overflow");
+  ATOM_NOTFOUND = enif_make_atom(env, "not_found");
+  ATOM_TOODEEP = enif_make_atom(env, "too_deep");
+  ATOM_UNKNOWN = enif_make_atom(env, "unknown");
+  return RES_ENGINE && RES_SUBTAB && RES_BATCHER ? 0 : 1;
+}
+
+static ErlNifFunc nif_funcs[] = {
+    {"new_engine", 1, nif_new_engine, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"insert", 2, nif_insert, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"delete", 2, nif_delete, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"commit", 1, nif_commit, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"empty", 1, nif_empty, 0},
+    {"match_batch", 3, nif_match_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"new_batcher", 4, nif_new_batcher, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"match_async", 3, nif_match_async, 0},
+    {"new_subtab", 1, nif_new_subtab, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"subscribe", 3, nif_subscribe, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"publish_batch", 4, nif_publish_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"topic_match", 2, nif_topic_match, 0},
+};
+
+ERL_NIF_INIT(emqx_match_nif, nif_funcs, load, NULL, NULL, NULL)
