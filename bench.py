@@ -193,7 +193,11 @@ def main():
         step()
         d = eng.diag(reset=True)
         eng.set_tuning("diag", 0)
-        result["diag_per_topic"] = {k: round(v / n, 3) for k, v in d.items()}
+        result["diag_per_topic"] = {k: round(v / n, 3) for k, v in d.items() if not k.startswith(("ticks", "waves"))}
+        w = max(d.get("waves", 0), 1)
+        result["diag_per_wave"] = {"phase_a_us": round(d["ticks_a"] / w / 100.0, 3),  # 100 MHz wall clock
+                                   "phase_b_us": round(d["ticks_b"] / w / 100.0, 3),
+                                   "steps": round(d["steps"] / w, 2), "waves": d.get("waves", 0)}
         result["diag_per_topic"]["kernel_ms_diag_call"] = round(eng.stats()["last_kernel_ms"], 4)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

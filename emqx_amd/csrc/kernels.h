@@ -33,6 +33,9 @@ enum Diag : uint32_t {
   DIAG_PLUS_HITS = 6,
   DIAG_EMITS = 7,        // filter ids emitted
   DIAG_SPILLS = 8,       // stack spills to HBM
+  DIAG_TICKS_A = 9,      // wall-clock ticks (100 MHz) in phase A (tokenize + intern), summed over waves
+  DIAG_TICKS_B = 10,     // ... in phase B (frontier walk)
+  DIAG_WAVES = 11,       // waves (tiles) counted
   DIAG_WORDS = 16
 };        // topics per wave (one per lane during tokenizing)
 constexpr uint32_t DEEP_MAX_LEVELS = 65536;

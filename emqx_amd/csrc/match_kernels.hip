@@ -118,7 +118,7 @@ __device__ __forceinline__ bool term_ok(uint32_t meta, uint32_t mode, bool dolla
 
 // Vocab lookup with exact byte verification.  w0..w3 hold the first 16 bytes of the word;
 // longer words compare the tail against the arena.  Returns WID_NONE if absent.
-__device__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, uint32_t w0,
+__device__ __forceinline__ uint32_t intern_word(const TableView& tv, uint32_t h, uint32_t len, uint32_t w0,
                                 uint32_t w1, uint32_t w2, uint32_t w3, const uint8_t* tbytes,
                                 uint64_t wstart) {
   uint32_t i = vocab_slot0(h) & tv.vocab_mask;
@@ -305,12 +305,74 @@ struct ByteWin {
   }
 };
 
+// Per-lane 64-B register chunk over the packed topic buffer: four 16-B aligned windows
+// loaded together (one round trip); bytes [0, lim) are readable, the rest reads as 0.
+struct Chunk64 {
+  const uint8_t* p;
+  uint64_t lim;
+  bool vec_ok;  // p is 16-B aligned
+  uint64_t cb;  // chunk base, ~0 = empty
+  uint4 w0, w1, w2, w3;
+  __device__ __forceinline__ Chunk64(const uint8_t* p_, uint64_t lim_)
+      : p(p_), lim(lim_), vec_ok((reinterpret_cast<uintptr_t>(p_) & 15u) == 0), cb(~0ull) {}
+  __device__ __forceinline__ static uint4 win(const uint8_t* p, uint64_t lim, bool vec_ok, uint64_t b) {
+    if (vec_ok && b + 16 <= lim) return *reinterpret_cast<const uint4*>(p + b);
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+      if (b + k < lim) v[k >> 2] |= static_cast<uint32_t>(p[b + k]) << (8u * (k & 3u));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  // the aligned dword at i (i % 4 == 0)
+  __device__ __forceinline__ uint32_t dword(uint64_t i) {
+    if (i < cb || i >= cb + 64) {
+      cb = i & ~15ull;
+      w0 = win(p, lim, vec_ok, cb);
+      w1 = win(p, lim, vec_ok, cb + 16);
+      w2 = win(p, lim, vec_ok, cb + 32);
+      w3 = win(p, lim, vec_ok, cb + 48);
+    }
+    // component-wise value selects (an aggregate select becomes a scratch access)
+    const uint32_t r = static_cast<uint32_t>(i - cb);
+    const uint32_t q = r >> 4, d = (r >> 2) & 3u;
+    return pick4(d, pick4(q, w0.x, w1.x, w2.x, w3.x), pick4(q, w0.y, w1.y, w2.y, w3.y),
+                 pick4(q, w0.z, w1.z, w2.z, w3.z), pick4(q, w0.w, w1.w, w2.w, w3.w));
+  }
+  __device__ __forceinline__ static uint32_t pick4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return (q & 2u) ? ((q & 1u) ? d : c) : ((q & 1u) ? b : a);
+  }
+};
+
+__device__ __forceinline__ uint32_t sel8(uint4 a, uint4 b, uint32_t i) {
+  const uint32_t lo = Chunk64::pick4(i & 3u, a.x, a.y, a.z, a.w), hi = Chunk64::pick4(i & 3u, b.x, b.y, b.z, b.w);
+  return (i & 4u) ? hi : lo;
+}
+
+// First 16 bytes of a word (zero padded past its length), given the two aligned windows
+// that cover [ws, ws + 16) and sh = ws % 16 — the layout of VocabSlot::inl.
+__device__ __forceinline__ void word_head(uint4 wa, uint4 wb, uint32_t sh, uint32_t len, uint32_t (&w)[4]) {
+#pragma unroll
+  for (uint32_t o = 0; o < 4; ++o) {
+    const uint32_t i = (sh >> 2) + o;
+    const uint32_t v = __builtin_amdgcn_alignbyte(sel8(wa, wb, i + 1), sel8(wa, wb, i), sh & 3u);
+    const uint32_t nb = len > 4 * o ? min(len - 4 * o, 4u) : 0u;
+    w[o] = nb >= 4 ? v : (v & ((1u << (8 * nb)) - 1u));
+  }
+}
+
+// aux[] word records of phase A: offset from the tile's first byte | length << 20
+constexpr uint32_t AUX_DONE = 0xFFFFFFFFu;  // word already resolved ('+' / '#')
+constexpr uint32_t AUX_LEN_SHIFT = 20;
+constexpr uint64_t AUX_OFF_LIM = 1ull << AUX_LEN_SHIFT;
+constexpr uint32_t AUX_LEN_MAX = 4095;      // longer levels go to the deep path
+
 constexpr int ceil_log2(int v) { return v <= 1 ? 0 : 1 + ceil_log2((v + 1) / 2); }
 
 template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG>
-__global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
+__global__ __launch_bounds__(WAVES * 64, 8) void match_fast_kernel(MatchArgs a) {
   static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
   static_assert(WID_CAP <= 1024, "item word index is 10 bits");
+  static_assert(WID_CAP <= 2 * STACK_CAP, "phase A keeps one aux word per word id in the stack area");
   struct WaveLds {
     uint2 stack[STACK_CAP];  // work stack (LIFO); overflow spills its bottom half to HBM
     uint32_t wids[WID_CAP];  // word ids of the tile's topics, topic after topic
@@ -325,6 +387,7 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * WAVES + wv;
   const uint64_t t0 = tile * TILE_TOPICS;
   if (t0 >= a.n) return;  // wave-uniform; the kernel uses no block-wide barrier
+  const uint64_t clk0 = DIAG ? wall_clock64() : 0;
 
   const TableView& tv = a.tv;
   const uint32_t tcount = static_cast<uint32_t>(min<uint64_t>(TILE_TOPICS, a.n - t0));
@@ -336,28 +399,43 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
     end = a.toffs[t + 1];
   }
 
-  // ---- phase A: tokenize + intern (one topic per lane) -----------------------------
-  ByteWin byte_at(a.tbytes, a.toffs[a.n]);  // bytes [0, toffs[n]) are readable
+  // ---- phase A1: tokenize (one topic per lane, bytes from a 64-B register chunk) ------
+  // Pass 1 counts levels and finds wildcard / '$' topics; after a wave scan of the level
+  // counts, pass 2 (same registers, no reload for topics of <= 48 B) writes each word's
+  // FNV-1a hash to wids[] and its (offset, length) to aux[] — the stack area, idle until
+  // phase B.  '+' and '#' levels are resolved here.
+  uint32_t* aux = reinterpret_cast<uint32_t*>(L.stack);
+  const uint64_t lim = a.toffs[a.n];   // bytes [0, lim) are readable
+  const uint64_t tbase = a.toffs[t0];  // tile's first byte
+  Chunk64 C(a.tbytes, lim);
   uint32_t nlev = 0;
-  bool wild = false, dollar = false;
+  bool wild = false, dollar = false, longw = false;
   if (valid) {
     nlev = 1;
     uint32_t llen = 0, first = 0;
-    for (uint64_t i = start; i < end; ++i) {
-      const uint32_t c = byte_at(i);
-      if (c == '/') {
-        if (llen == 1 && (first == '+' || first == '#')) wild = true;
-        ++nlev;
-        llen = 0;
-      } else {
-        if (llen == 0) first = c;
-        ++llen;
+    for (uint64_t i = start & ~3ull; i < end; i += 4) {
+      const uint32_t d = C.dword(i);
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint64_t pos = i + b;
+        if (pos < start || pos >= end) continue;
+        const uint32_t c = (d >> (8u * b)) & 0xFFu;
+        if (pos == start) dollar = c == '$';
+        if (c == '/') {
+          if (llen == 1 && (first == '+' || first == '#')) wild = true;
+          longw |= llen >= AUX_LEN_MAX;
+          ++nlev;
+          llen = 0;
+        } else {
+          if (llen == 0) first = c;
+          ++llen;
+        }
       }
     }
     if (llen == 1 && (first == '+' || first == '#')) wild = true;
-    dollar = end > start && byte_at(start) == '$';
+    longw |= llen >= AUX_LEN_MAX;
   }
-  bool defer = valid && nlev > static_cast<uint32_t>(WID_CAP / 8);
+  bool defer = valid && (nlev > static_cast<uint32_t>(WID_CAP / 8) || longw || end - tbase >= AUX_OFF_LIM);
   const uint32_t need = (valid && !defer) ? nlev : 0u;
   const uint32_t incl = wave_incl_scan(need, lane);
   const uint32_t wbase = incl - need;
@@ -365,38 +443,92 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   uint64_t defer_mask = __ballot(defer);
 
   if (valid && !defer) {
-    uint32_t k = 0, h = FNV_BASIS, len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    uint32_t k = 0, h = FNV_BASIS, len = 0, first = 0;
     uint64_t ws = start;
-    for (uint64_t i = start; i <= end; ++i) {
-      const uint32_t c = (i < end) ? byte_at(i) : static_cast<uint32_t>('/');
-      if (c != '/') {
-        h = fnv1a_step(h, c);
-        if (len < 16) {
-          const uint32_t v = c << (8u * (len & 3u));
-          const uint32_t q = len >> 2;
-          w0 |= q == 0 ? v : 0u;
-          w1 |= q == 1 ? v : 0u;
-          w2 |= q == 2 ? v : 0u;
-          w3 |= q == 3 ? v : 0u;
-        }
-        ++len;
+    auto put = [&]() {
+      const uint32_t j = wbase + k++;
+      if (len == 1 && (first == '+' || first == '#')) {
+        L.wids[j] = first == '+' ? WID_PLUS : WID_HASH;
+        aux[j] = AUX_DONE;
       } else {
-        uint32_t wid;
-        if (len == 1 && w0 == '+') wid = WID_PLUS;
-        else if (len == 1 && w0 == '#') wid = WID_HASH;
-        else wid = intern_word(tv, h, len, w0, w1, w2, w3, a.tbytes, ws);
-        L.wids[wbase + k] = wid;
-        ++k;
-        h = FNV_BASIS;
-        len = 0;
-        w0 = w1 = w2 = w3 = 0;
-        ws = i + 1;
+        L.wids[j] = h;
+        aux[j] = static_cast<uint32_t>(ws - tbase) | (len << AUX_LEN_SHIFT);
+      }
+    };
+    for (uint64_t i = start & ~3ull; i < end; i += 4) {
+      const uint32_t d = C.dword(i);
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint64_t pos = i + b;
+        if (pos < start || pos >= end) continue;
+        const uint32_t c = (d >> (8u * b)) & 0xFFu;
+        if (c == '/') {
+          put();
+          h = FNV_BASIS;
+          len = 0;
+          ws = pos + 1;
+        } else {
+          h = fnv1a_step(h, c);
+          if (len == 0) first = c;
+          ++len;
+        }
       }
     }
+    put();
     L.wend[lane] = wbase + nlev;
+  }
+  // words of the tile: entries [0, nwords) of wids/aux belong to topics kept on the fast path
+  uint32_t nwords = (valid && !defer) ? incl : 0u;
+#pragma unroll
+  for (uint32_t dd = 32; dd >= 1; dd >>= 1) nwords = max(nwords, static_cast<uint32_t>(__shfl_xor(nwords, dd, 64)));
+  wave_sync();
+
+  // ---- phase A2: intern every word of the tile, word-parallel ------------------------
+  // Each lane takes IW words per round and issues all their loads (the word's bytes and
+  // its first vocab slot) before consuming any, so a round costs one dependent trip.
+  constexpr uint32_t IW = 1;
+  for (uint32_t j0 = 0; j0 < nwords; j0 += 64u * IW) {
+    uint32_t jj[IW], hh[IW], ln[IW], sh[IW];
+    uint64_t wsa[IW];
+    bool act[IW];
+    uint4 wa[IW], wb[IW], hd[IW], in[IW];
+#pragma unroll
+    for (uint32_t u = 0; u < IW; ++u) {
+      jj[u] = j0 + lane + 64u * u;
+      const uint32_t ax = jj[u] < nwords ? aux[jj[u]] : AUX_DONE;
+      act[u] = ax != AUX_DONE;
+      hh[u] = act[u] ? L.wids[jj[u]] : 0u;
+      ln[u] = ax >> AUX_LEN_SHIFT;
+      wsa[u] = tbase + (ax & (AUX_OFF_LIM - 1));
+      sh[u] = static_cast<uint32_t>(wsa[u] & 15u);
+      const uint64_t w0 = wsa[u] & ~15ull;
+      wa[u] = (act[u] && ln[u]) ? Chunk64::win(a.tbytes, lim, C.vec_ok, w0) : make_uint4(0, 0, 0, 0);
+      wb[u] = (act[u] && sh[u] + min(ln[u], 16u) > 16u) ? Chunk64::win(a.tbytes, lim, C.vec_ok, w0 + 16)
+                                                         : make_uint4(0, 0, 0, 0);
+      const uint4* vp = reinterpret_cast<const uint4*>(tv.vocab + (vocab_slot0(hh[u]) & tv.vocab_mask));
+      hd[u] = act[u] ? vp[0] : make_uint4(0, 0, WID_NONE, 0);
+      in[u] = act[u] ? vp[1] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < IW; ++u) {
+      if (!act[u]) continue;
+      uint32_t w[4];
+      word_head(wa[u], wb[u], sh[u], ln[u], w);
+      uint32_t wid;
+      if (hd[u].z == WID_NONE) {
+        wid = WID_NONE;
+      } else if (hd[u].x == hh[u] && hd[u].y == ln[u] && ln[u] <= 16 && in[u].x == w[0] && in[u].y == w[1] &&
+                 in[u].z == w[2] && in[u].w == w[3]) {
+        wid = hd[u].z;
+      } else {  // long word or a probe chain: the full lookup (rare)
+        wid = intern_word(tv, hh[u], ln[u], w[0], w[1], w[2], w[3], a.tbytes, wsa[u]);
+      }
+      L.wids[jj[u]] = wid;
+    }
   }
   L.cnt[lane] = 0;
   wave_sync();
+  const uint64_t clk1 = DIAG ? wall_clock64() : 0;
 
   // ---- phase B: pooled frontier walk ------------------------------------------------
   uint64_t* slab = a.slab + tile * a.slab_cap;
@@ -408,7 +540,7 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   uint32_t stop = 0;      // wave-uniform: items in the HBM spill
   uint32_t maxtop = 0;    // wave-uniform (LDS + spill)
   uint32_t evals = 0;     // per lane
-  uint32_t dg[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // diagnostic counters (per lane)
+  uint32_t dg[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // diagnostic counters (per lane)
 
   // root: '#' emission, exact walk of wildcard topics, the root item
   {
@@ -587,8 +719,13 @@ __global__ __launch_bounds__(WAVES * 64) void match_fast_kernel(MatchArgs a) {
   wave_sync();
   if (DIAG && a.diag) {
     dg[0] = lane == 0 ? dg[0] : 0u;  // steps are wave-uniform
+    dg[8] = lane == 0 ? dg[8] : 0u;
+    const uint64_t clk2 = wall_clock64();  // 100 MHz constant clock
+    dg[9] = lane == 0 ? static_cast<uint32_t>(clk1 - clk0) : 0u;
+    dg[10] = lane == 0 ? static_cast<uint32_t>(clk2 - clk1) : 0u;
+    dg[11] = lane == 0 ? 1u : 0u;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < 12; ++i) {
       const uint32_t v = wave_sum(dg[i]);
       if (lane == 0 && v) atomicAdd(reinterpret_cast<unsigned long long*>(a.diag + i), static_cast<unsigned long long>(v));
     }
@@ -910,7 +1047,7 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K2_S2K: launch_fast_t<2, 2048, 1024, 2>(a, ntiles, s); break;
     case FAST_K2_S768: launch_fast_t<4, 768, 768, 2>(a, ntiles, s); break;
     case FAST_K4_S2K: launch_fast_t<2, 2048, 1024, 4>(a, ntiles, s); break;
-    case FAST_K1_S256: launch_fast_t<4, 256, 640, 1>(a, ntiles, s); break;
+    case FAST_K1_S256: launch_fast_t<4, 256, 512, 1>(a, ntiles, s); break;
     case FAST_K2_S512: launch_fast_t<4, 512, 640, 2>(a, ntiles, s); break;
     case FAST_K1_S384: launch_fast_t<4, 384, 640, 1>(a, ntiles, s); break;
     default: return hipErrorInvalidValue;

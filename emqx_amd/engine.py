@@ -99,7 +99,7 @@ class Engine:
         check(_lib.lib().emqx_set_tuning(self._h, key.encode(), int(value)), "emqx_set_tuning")
 
     DIAG_NAMES = ("steps", "items", "lit_probes", "lit_hits", "lit_extra_loads", "plus_probes",
-                  "plus_hits", "emits", "spills")
+                  "plus_hits", "emits", "spills", "ticks_a", "ticks_b", "waves")
 
     def diag(self, reset: bool = True) -> dict:
         out = np.zeros(16, dtype=np.uint64)
