@@ -285,7 +285,7 @@ __global__ void reduce_stats_kernel(const uint2* tile_stats, uint64_t ntiles, co
 }
 
 // Fast-kernel variant: EMQX_FAST_VARIANT overrides (A/B runs); otherwise deep tables get
-// the 2K-item stack and everything else the 1K stack with two items per lane.
+// the 2K-item stack and everything else the 512-item stack with two items per lane.
 FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
   static const int env_forced = [] {
     const char* v = getenv("EMQX_FAST_VARIANT");
@@ -294,7 +294,7 @@ FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
   const int fv = e->forced_variant.load();
   const int forced = fv >= 0 ? fv : env_forced;
   if (forced >= 0 && forced < FAST_NVARIANTS) return static_cast<FastVariant>(forced);
-  return snap.max_depth > 12 ? FAST_K2_S2K : FAST_K1_S256;
+  return snap.max_depth > 12 ? FAST_K2_S2K : FAST_K2_S512;
 }
 
 // The pipeline on device buffers.  All inputs/outputs are device pointers.

@@ -65,7 +65,7 @@ static_assert(sizeof(EdgeSlot) == 32, "EdgeSlot must be 32 bytes");
 
 // 32-byte vocab slot; words up to 16 bytes are verified from `inl` without a second load.
 struct alignas(16) VocabSlot {
-  uint32_t hash;   // fnv1a32 of the word bytes
+  uint32_t hash;   // word_hash_bytes() of the word
   uint32_t len;    // word length in bytes
   uint32_t wid;    // word id (WID_NONE = empty slot)
   uint32_t off;    // offset of the bytes in the arena
@@ -84,9 +84,6 @@ struct TableView {
   uint32_t root_hash_fid;  // filter '#' or FID_NONE
 };
 
-EMQX_HD uint32_t fnv1a_step(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }
-constexpr uint32_t FNV_BASIS = 2166136261u;
-
 // murmur3 fmix32: spreads word ids inside a node's edge array.
 EMQX_HD uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
@@ -97,7 +94,32 @@ EMQX_HD uint32_t mix32(uint32_t x) {
   return x;
 }
 
-EMQX_HD uint32_t vocab_slot0(uint32_t hash) { return mix32(hash ^ 0x9e3779b9u); }
+// Vocab word hash: a multiply-rotate chain over the word's bytes read as little-endian
+// dwords (zero padded, at least four dwords), seeded by the length, then fmix32.  A word of
+// at most 16 bytes hashes from the four head dwords the kernels already hold for the exact
+// byte check (VocabSlot::inl), so interning needs no per-byte loop.
+EMQX_HD uint32_t whash_init(uint32_t len) { return len * 0x9E3779B1u + 0x7F4A7C15u; }
+EMQX_HD uint32_t whash_step(uint32_t h, uint32_t d) {
+  h = (h ^ d) * 0x85EBCA77u;
+  return (h << 13) | (h >> 19);
+}
+EMQX_HD uint32_t word_hash16(uint32_t len, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  return mix32(whash_step(whash_step(whash_step(whash_step(whash_init(len), w0), w1), w2), w3));
+}
+// Any length; p[0, n) are the word's bytes.
+EMQX_HD uint32_t word_hash_bytes(const uint8_t* p, uint32_t n) {
+  uint32_t h = whash_init(n);
+  const uint32_t nd = n > 16 ? (n + 3) / 4 : 4;
+  for (uint32_t i = 0; i < nd; ++i) {
+    uint32_t d = 0;
+    for (uint32_t b = 0; b < 4; ++b)
+      if (4 * i + b < n) d |= static_cast<uint32_t>(p[4 * i + b]) << (8 * b);
+    h = whash_step(h, d);
+  }
+  return mix32(h);
+}
+
+EMQX_HD uint32_t vocab_slot0(uint32_t hash) { return hash; }
 
 // Slot of literal word `wid` in a perfect-hashed node's array (mask = cap - 1).
 EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask) {

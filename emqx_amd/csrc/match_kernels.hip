@@ -360,19 +360,47 @@ __device__ __forceinline__ void word_head(uint4 wa, uint4 wb, uint32_t sh, uint3
   }
 }
 
-// aux[] word records of phase A: offset from the tile's first byte | length << 20
-constexpr uint32_t AUX_DONE = 0xFFFFFFFFu;  // word already resolved ('+' / '#')
+// Phase A keeps a word record in wids[] until the word is interned: its offset from the
+// tile's 16-B aligned first byte | its length << 20.  Values >= WID_RESOLVED are word ids
+// already ('+' / '#' levels, or WID_NONE for a topic handed to the deep path).
 constexpr uint32_t AUX_LEN_SHIFT = 20;
 constexpr uint64_t AUX_OFF_LIM = 1ull << AUX_LEN_SHIFT;
-constexpr uint32_t AUX_LEN_MAX = 4095;      // longer levels go to the deep path
+constexpr uint32_t AUX_LEN_MAX = 4095;  // longer levels go to the deep path
+constexpr uint32_t WID_RESOLVED = 0xFFFFFFF0u;
+
+// 4-bit mask of the bytes of x equal to the byte replicated in pat (exact: no carry
+// crosses a byte, and the gather multiply's partial products never overlap).
+__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t x, uint32_t pat) {
+  const uint32_t y = x ^ pat;
+  const uint32_t z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+  return (((z >> 7) * 0x204081u) >> 21) & 0xFu;
+}
+
+// Level map of one aligned 16-B chunk: bit b = byte b is '/', bit 16 + b = byte b is '+' or '#'.
+__device__ __forceinline__ uint32_t chunk_levelmap(uint4 v) {
+  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    m |= byte_eq_mask(d[i], 0x2F2F2F2Fu) << (4 * i);
+    m |= (byte_eq_mask(d[i], 0x2B2B2B2Bu) | byte_eq_mask(d[i], 0x23232323u)) << (16 + 4 * i);
+  }
+  return m;
+}
+
+// Bits of chunk k (bytes [16k, 16k + 16)) that fall inside [lo, hi); requires hi > 16k.
+__device__ __forceinline__ uint32_t span_mask(uint32_t k, uint32_t lo, uint32_t hi) {
+  const uint32_t c = 16u * k;
+  const uint32_t b0 = lo > c ? lo - c : 0u, b1 = min(hi - c, 16u);
+  return ((1u << b1) - 1u) & ~((1u << b0) - 1u);
+}
 
 constexpr int ceil_log2(int v) { return v <= 1 ? 0 : 1 + ceil_log2((v + 1) / 2); }
 
 template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG>
-__global__ __launch_bounds__(WAVES * 64, 8) void match_fast_kernel(MatchArgs a) {
+__global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(MatchArgs a) {
   static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
   static_assert(WID_CAP <= 1024, "item word index is 10 bits");
-  static_assert(WID_CAP <= 2 * STACK_CAP, "phase A keeps one aux word per word id in the stack area");
   struct WaveLds {
     uint2 stack[STACK_CAP];  // work stack (LIFO); overflow spills its bottom half to HBM
     uint32_t wids[WID_CAP];  // word ids of the tile's topics, topic after topic
@@ -399,18 +427,47 @@ __global__ __launch_bounds__(WAVES * 64, 8) void match_fast_kernel(MatchArgs a) 
     end = a.toffs[t + 1];
   }
 
-  // ---- phase A1: tokenize (one topic per lane, bytes from a 64-B register chunk) ------
-  // Pass 1 counts levels and finds wildcard / '$' topics; after a wave scan of the level
-  // counts, pass 2 (same registers, no reload for topics of <= 48 B) writes each word's
-  // FNV-1a hash to wids[] and its (offset, length) to aux[] — the stack area, idle until
-  // phase B.  '+' and '#' levels are resolved here.
-  uint32_t* aux = reinterpret_cast<uint32_t*>(L.stack);
-  const uint64_t lim = a.toffs[a.n];   // bytes [0, lim) are readable
-  const uint64_t tbase = a.toffs[t0];  // tile's first byte
+  // ---- phase A1: tokenize ----------------------------------------------------------
+  // The tile's topics are one contiguous byte range.  The wave reads it with coalesced
+  // 16-B loads and writes a level map (chunk_levelmap) to the stack area, idle until
+  // phase B; then each lane counts its topic's levels with popcounts, and after a wave scan
+  // of the counts writes one record per level to wids[].  A tile whose bytes exceed the
+  // map falls back to a per-lane byte loop over 64-B register chunks.
+  const uint64_t lim = a.toffs[a.n];  // bytes [0, lim) are readable
+  const uint64_t A0 = a.toffs[t0] & ~15ull;
+  const uint64_t tend = a.toffs[t0 + tcount];
+  const bool vec_ok = (reinterpret_cast<uintptr_t>(a.tbytes) & 15u) == 0;
+  constexpr uint32_t MAP_CHUNKS = 2 * STACK_CAP;  // one dword per 16-B chunk
+  const bool use_map = tend - A0 <= 16ull * MAP_CHUNKS;  // wave-uniform
+  uint32_t* lmap = reinterpret_cast<uint32_t*>(L.stack);
+  const uint32_t lo = static_cast<uint32_t>(start - A0), hi = static_cast<uint32_t>(end - A0);  // map path only
   Chunk64 C(a.tbytes, lim);
   uint32_t nlev = 0;
   bool wild = false, dollar = false, longw = false;
-  if (valid) {
+  if (use_map) {
+    const uint32_t first = (valid && end > start) ? a.tbytes[start] : 0u;
+    const uint32_t nch = static_cast<uint32_t>((tend - A0 + 15) >> 4);
+    for (uint32_t c0 = 0; c0 < nch; c0 += 256) {
+      uint4 v[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t c = c0 + lane + 64u * u;
+        v[u] = c < nch ? Chunk64::win(a.tbytes, lim, vec_ok, A0 + 16ull * c) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t c = c0 + lane + 64u * u;
+        if (c < nch) lmap[c] = chunk_levelmap(v[u]);
+      }
+    }
+    dollar = first == '$';
+    wave_sync();
+    if (valid) {
+      uint32_t cnt = 0;
+      for (uint32_t k = lo >> 4; 16u * k < hi; ++k) cnt += __popc(lmap[k] & span_mask(k, lo, hi));
+      nlev = cnt + 1;
+    }
+  } else if (valid) {
     nlev = 1;
     uint32_t llen = 0, first = 0;
     for (uint64_t i = start & ~3ull; i < end; i += 4) {
@@ -422,7 +479,6 @@ __global__ __launch_bounds__(WAVES * 64, 8) void match_fast_kernel(MatchArgs a) 
         const uint32_t c = (d >> (8u * b)) & 0xFFu;
         if (pos == start) dollar = c == '$';
         if (c == '/') {
-          if (llen == 1 && (first == '+' || first == '#')) wild = true;
           longw |= llen >= AUX_LEN_MAX;
           ++nlev;
           llen = 0;
@@ -432,79 +488,99 @@ __global__ __launch_bounds__(WAVES * 64, 8) void match_fast_kernel(MatchArgs a) 
         }
       }
     }
-    if (llen == 1 && (first == '+' || first == '#')) wild = true;
     longw |= llen >= AUX_LEN_MAX;
   }
-  bool defer = valid && (nlev > static_cast<uint32_t>(WID_CAP / 8) || longw || end - tbase >= AUX_OFF_LIM);
+  bool defer = valid && (nlev > static_cast<uint32_t>(WID_CAP / 8) || longw || end - A0 >= AUX_OFF_LIM);
   const uint32_t need = (valid && !defer) ? nlev : 0u;
   const uint32_t incl = wave_incl_scan(need, lane);
   const uint32_t wbase = incl - need;
   if (valid && !defer && incl > static_cast<uint32_t>(WID_CAP)) defer = true;
-  uint64_t defer_mask = __ballot(defer);
 
   if (valid && !defer) {
-    uint32_t k = 0, h = FNV_BASIS, len = 0, first = 0;
-    uint64_t ws = start;
-    auto put = [&]() {
-      const uint32_t j = wbase + k++;
-      if (len == 1 && (first == '+' || first == '#')) {
-        L.wids[j] = first == '+' ? WID_PLUS : WID_HASH;
-        aux[j] = AUX_DONE;
-      } else {
-        L.wids[j] = h;
-        aux[j] = static_cast<uint32_t>(ws - tbase) | (len << AUX_LEN_SHIFT);
+    uint32_t j = wbase;
+    uint64_t ws = start;  // first byte of the current level
+    // one record per level; '+' / '#' levels resolve here, over-long ones defer the topic
+    auto put = [&](uint64_t wend_) {
+      const uint32_t len = static_cast<uint32_t>(wend_ - ws);
+      uint32_t v = static_cast<uint32_t>(ws - A0) | (len << AUX_LEN_SHIFT);
+      if (len == 1) {
+        const bool maybe = !use_map || ((lmap[(ws - A0) >> 4] >> (16u + ((ws - A0) & 15u))) & 1u);
+        const uint32_t c = maybe ? static_cast<uint32_t>(a.tbytes[ws]) : 0u;
+        v = c == '+' ? WID_PLUS : c == '#' ? WID_HASH : v;
       }
+      v = len >= AUX_LEN_MAX ? WID_NONE : v;
+      L.wids[j++] = v;
+      return v;
     };
-    for (uint64_t i = start & ~3ull; i < end; i += 4) {
-      const uint32_t d = C.dword(i);
-#pragma unroll
-      for (uint32_t b = 0; b < 4; ++b) {
-        const uint64_t pos = i + b;
-        if (pos < start || pos >= end) continue;
-        const uint32_t c = (d >> (8u * b)) & 0xFFu;
-        if (c == '/') {
-          put();
-          h = FNV_BASIS;
-          len = 0;
+    uint32_t seen = 0;  // OR of the records' flags: bit 0 wildcard level, bit 1 over-long level
+    auto note = [](uint32_t v) -> uint32_t {
+      return (v == WID_PLUS || v == WID_HASH ? 1u : 0u) | (v == WID_NONE ? 2u : 0u);
+    };
+    if (use_map) {
+      for (uint32_t k = lo >> 4; 16u * k < hi; ++k) {
+        uint32_t m = lmap[k] & span_mask(k, lo, hi);
+        while (m) {
+          const uint64_t pos = A0 + 16u * k + static_cast<uint32_t>(__builtin_ctz(m));
+          m &= m - 1u;
+          seen |= note(put(pos));
           ws = pos + 1;
-        } else {
-          h = fnv1a_step(h, c);
-          if (len == 0) first = c;
-          ++len;
+        }
+      }
+    } else {
+      for (uint64_t i = start & ~3ull; i < end; i += 4) {
+        const uint32_t d = C.dword(i);
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+          const uint64_t pos = i + b;
+          if (pos < start || pos >= end) continue;
+          if (((d >> (8u * b)) & 0xFFu) == '/') {
+            seen |= note(put(pos));
+            ws = pos + 1;
+          }
         }
       }
     }
-    put();
+    seen |= note(put(end));
+    wild = (seen & 1u) != 0;
+    longw = (seen & 2u) != 0;
     L.wend[lane] = wbase + nlev;
   }
-  // words of the tile: entries [0, nwords) of wids/aux belong to topics kept on the fast path
+  // words of the tile: entries [0, nwords) of wids belong to topics kept on the fast path
   uint32_t nwords = (valid && !defer) ? incl : 0u;
 #pragma unroll
   for (uint32_t dd = 32; dd >= 1; dd >>= 1) nwords = max(nwords, static_cast<uint32_t>(__shfl_xor(nwords, dd, 64)));
+  defer |= longw;
+  uint64_t defer_mask = __ballot(defer);
   wave_sync();
 
   // ---- phase A2: intern every word of the tile, word-parallel ------------------------
-  // Each lane takes IW words per round and issues all their loads (the word's bytes and
-  // its first vocab slot) before consuming any, so a round costs one dependent trip.
-  constexpr uint32_t IW = 1;
+  // Each lane takes IW words per round: it loads their bytes (16-B windows, mostly L1/L2
+  // hits after A1), hashes the head dwords (word_hash16) and loads their first vocab slot;
+  // the exact byte check uses the same head dwords.
+  constexpr uint32_t IW = K > 2 ? 2 : K;
   for (uint32_t j0 = 0; j0 < nwords; j0 += 64u * IW) {
-    uint32_t jj[IW], hh[IW], ln[IW], sh[IW];
+    uint32_t jj[IW], ln[IW], sh[IW], hh[IW], w[IW][4];
     uint64_t wsa[IW];
     bool act[IW];
     uint4 wa[IW], wb[IW], hd[IW], in[IW];
 #pragma unroll
     for (uint32_t u = 0; u < IW; ++u) {
       jj[u] = j0 + lane + 64u * u;
-      const uint32_t ax = jj[u] < nwords ? aux[jj[u]] : AUX_DONE;
-      act[u] = ax != AUX_DONE;
-      hh[u] = act[u] ? L.wids[jj[u]] : 0u;
-      ln[u] = ax >> AUX_LEN_SHIFT;
-      wsa[u] = tbase + (ax & (AUX_OFF_LIM - 1));
+      const uint32_t v = jj[u] < nwords ? L.wids[jj[u]] : WID_NONE;
+      act[u] = v < WID_RESOLVED;
+      ln[u] = v >> AUX_LEN_SHIFT;
+      wsa[u] = A0 + (v & (AUX_OFF_LIM - 1));
       sh[u] = static_cast<uint32_t>(wsa[u] & 15u);
       const uint64_t w0 = wsa[u] & ~15ull;
-      wa[u] = (act[u] && ln[u]) ? Chunk64::win(a.tbytes, lim, C.vec_ok, w0) : make_uint4(0, 0, 0, 0);
-      wb[u] = (act[u] && sh[u] + min(ln[u], 16u) > 16u) ? Chunk64::win(a.tbytes, lim, C.vec_ok, w0 + 16)
+      wa[u] = (act[u] && ln[u]) ? Chunk64::win(a.tbytes, lim, vec_ok, w0) : make_uint4(0, 0, 0, 0);
+      wb[u] = (act[u] && sh[u] + min(ln[u], 16u) > 16u) ? Chunk64::win(a.tbytes, lim, vec_ok, w0 + 16)
                                                          : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < IW; ++u) {
+      word_head(wa[u], wb[u], sh[u], ln[u], w[u]);
+      hh[u] = !act[u] ? 0u : ln[u] <= 16 ? word_hash16(ln[u], w[u][0], w[u][1], w[u][2], w[u][3])
+                          : word_hash_bytes(a.tbytes + wsa[u], ln[u]);
       const uint4* vp = reinterpret_cast<const uint4*>(tv.vocab + (vocab_slot0(hh[u]) & tv.vocab_mask));
       hd[u] = act[u] ? vp[0] : make_uint4(0, 0, WID_NONE, 0);
       in[u] = act[u] ? vp[1] : make_uint4(0, 0, 0, 0);
@@ -512,16 +588,14 @@ __global__ __launch_bounds__(WAVES * 64, 8) void match_fast_kernel(MatchArgs a) 
 #pragma unroll
     for (uint32_t u = 0; u < IW; ++u) {
       if (!act[u]) continue;
-      uint32_t w[4];
-      word_head(wa[u], wb[u], sh[u], ln[u], w);
       uint32_t wid;
       if (hd[u].z == WID_NONE) {
         wid = WID_NONE;
-      } else if (hd[u].x == hh[u] && hd[u].y == ln[u] && ln[u] <= 16 && in[u].x == w[0] && in[u].y == w[1] &&
-                 in[u].z == w[2] && in[u].w == w[3]) {
+      } else if (hd[u].x == hh[u] && hd[u].y == ln[u] && ln[u] <= 16 && in[u].x == w[u][0] &&
+                 in[u].y == w[u][1] && in[u].z == w[u][2] && in[u].w == w[u][3]) {
         wid = hd[u].z;
       } else {  // long word or a probe chain: the full lookup (rare)
-        wid = intern_word(tv, hh[u], ln[u], w[0], w[1], w[2], w[3], a.tbytes, wsa[u]);
+        wid = intern_word(tv, hh[u], ln[u], w[u][0], w[u][1], w[u][2], w[u][3], a.tbytes, wsa[u]);
       }
       L.wids[jj[u]] = wid;
     }
@@ -775,12 +849,11 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     // tokenize + intern (lane 0; rare path)
     uint32_t nlev = 0, wild = 0, dollar = 0;
     if (lane == 0) {
-      uint32_t k = 0, h = FNV_BASIS, len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+      uint32_t k = 0, len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
       uint64_t ws = start;
       for (uint64_t i = start; i <= end; ++i) {
         const uint32_t c = (i < end) ? byte_at(i) : static_cast<uint32_t>('/');
         if (c != '/') {
-          h = fnv1a_step(h, c);
           if (len < 16) {
             const uint32_t v = c << (8u * (len & 3u));
             const uint32_t q = len >> 2;
@@ -794,9 +867,11 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
           uint32_t wid;
           if (len == 1 && w0 == '+') { wid = WID_PLUS; wild = 1; }
           else if (len == 1 && w0 == '#') { wid = WID_HASH; wild = 1; }
-          else wid = intern_word(tv, h, len, w0, w1, w2, w3, a.tbytes, ws);
+          else {
+            const uint32_t h = len <= 16 ? word_hash16(len, w0, w1, w2, w3) : word_hash_bytes(a.tbytes + ws, len);
+            wid = intern_word(tv, h, len, w0, w1, w2, w3, a.tbytes, ws);
+          }
           wids[k++] = wid;
-          h = FNV_BASIS;
           len = 0;
           w0 = w1 = w2 = w3 = 0;
           ws = i + 1;

@@ -119,9 +119,7 @@ struct VocabBuilder {
     id = static_cast<uint32_t>(h32.size());
     arena.insert(arena.end(), p, p + n);
     off.push_back(static_cast<uint32_t>(arena.size()));
-    uint32_t f = FNV_BASIS;
-    for (uint64_t i = 0; i < n; ++i) f = fnv1a_step(f, p[i]);
-    h32.push_back(f);
+    h32.push_back(word_hash_bytes(p, static_cast<uint32_t>(n)));
     map.insert_new(h, id);
     return id;
   }
