@@ -48,6 +48,7 @@ hipError_t dalloc(T*& p, uint64_t count) {
 struct Snapshot {
   int device = 0;
   EdgeSlot* edges = nullptr;
+  uint32_t* fids = nullptr;
   VocabSlot* vocab = nullptr;
   uint8_t* arena = nullptr;
   TableView tv{};
@@ -58,6 +59,7 @@ struct Snapshot {
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
     dfree(edges);
+    dfree(fids);
     dfree(vocab);
     dfree(arena);
     (void)hipSetDevice(cur);
@@ -149,23 +151,27 @@ int upload(emqx_engine* e, const HostTables& ht, std::shared_ptr<Snapshot>* out)
   auto s = std::make_shared<Snapshot>();
   s->device = e->device;
   HIP_TRY(dalloc(s->edges, ht.edges.size()));
+  HIP_TRY(dalloc(s->fids, ht.fids.size()));
   HIP_TRY(dalloc(s->vocab, ht.vocab.size()));
   HIP_TRY(dalloc(s->arena, ht.arena.size() + 16));
   HIP_TRY(hipMemcpy(s->edges, ht.edges.data(), ht.edges.size() * sizeof(EdgeSlot), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
   s->tv.edges = s->edges;
+  s->tv.fids = s->fids;
   s->tv.vocab = s->vocab;
   s->tv.arena = s->arena;
   s->tv.vocab_mask = ht.vocab_mask;
   s->tv.root_base = ht.root_base;
   s->tv.root_meta = ht.root_meta;
   s->tv.root_hash_fid = ht.root_hash_fid;
+  s->tv.root_hash_ref = ht.root_hash_ref;
   s->n_nodes = ht.n_nodes;
   s->n_slots = ht.edges.size();
   s->n_words = ht.n_words;
   s->max_depth = ht.max_depth;
-  s->bytes = ht.edges.size() * sizeof(EdgeSlot) +
+  s->bytes = ht.edges.size() * sizeof(EdgeSlot) + ht.fids.size() * sizeof(uint32_t) +
              ht.vocab.size() * sizeof(VocabSlot) + ht.arena.size();
   *out = std::move(s);
   return EMQX_OK;
@@ -285,7 +291,7 @@ __global__ void reduce_stats_kernel(const uint2* tile_stats, uint64_t ntiles, co
 }
 
 // Fast-kernel variant: EMQX_FAST_VARIANT overrides (A/B runs); otherwise deep tables get
-// the 2K-item stack and everything else the 512-item stack with two items per lane.
+// the 2K-item stack and everything else the 384-item stack, one item per lane (26 waves/CU).
 FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
   static const int env_forced = [] {
     const char* v = getenv("EMQX_FAST_VARIANT");
@@ -294,7 +300,7 @@ FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
   const int fv = e->forced_variant.load();
   const int forced = fv >= 0 ? fv : env_forced;
   if (forced >= 0 && forced < FAST_NVARIANTS) return static_cast<FastVariant>(forced);
-  return snap.max_depth > 12 ? FAST_K2_S2K : FAST_K2_S512;
+  return snap.max_depth > 12 ? FAST_K2_S2K : FAST_K1_S384;
 }
 
 // The pipeline on device buffers.  All inputs/outputs are device pointers.

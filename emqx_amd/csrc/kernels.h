@@ -36,7 +36,11 @@ enum Diag : uint32_t {
   DIAG_TICKS_A = 9,      // wall-clock ticks (100 MHz) in phase A (tokenize + intern), summed over waves
   DIAG_TICKS_B = 10,     // ... in phase B (frontier walk)
   DIAG_WAVES = 11,       // waves (tiles) counted
-  DIAG_WORDS = 16
+  DIAG_LEVEL0 = 12,      // items popped at topic level 0..7 (12..19; 19 = level >= 7)
+  DIAG_SMALL = 20,       // items whose node array has <= 8 slots (one 128-B line)
+  DIAG_WIDE = 21,        // items whose node array is larger
+  DIAG_NCOUNT = 22,
+  DIAG_WORDS = 32
 };        // topics per wave (one per lane during tokenizing)
 constexpr uint32_t DEEP_MAX_LEVELS = 65536;
 
@@ -77,7 +81,8 @@ enum FastVariant {
   FAST_K1_S256 = 5,  // 4 waves/block, stack 256 (+HBM spill), 640 word ids: 32 waves/CU
   FAST_K2_S512 = 6,  // 4 waves/block, stack 512 (+HBM spill), 640 word ids
   FAST_K1_S384 = 7,  // 4 waves/block, stack 384 (+HBM spill), 640 word ids
-  FAST_NVARIANTS = 8
+  FAST_K2_S512W = 8, // 4 waves/block, stack 512 (+HBM spill), 512 word ids: 24 waves/CU
+  FAST_NVARIANTS = 9
 };
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);

@@ -11,8 +11,8 @@
 //   * edges:  each node owns a power-of-two slice of one global slot array, open-
 //             addressed by word id; '+' is the reserved word WID_PLUS, a non-final '#'
 //             the reserved word WID_HASH; a final '#' is the parent's hash filter.
-//   * fids:   each slot carries its child's {filter "<path>/#", filter "<path>"} ids; the
-//             root's '#' filter is a table-view field.
+//   * fids:   per slot, its child's {filter "<path>/#", filter "<path>"} ids, resolved
+//             after the walk; the root's '#' filter follows the last slot's pair.
 #pragma once
 
 #include <stdint.h>
@@ -38,30 +38,34 @@ constexpr uint32_t META_HAS_HASH = 1u << 7;     // filter "<child path>/#" exist
 constexpr uint32_t META_HAS_TERM = 1u << 8;     // filter "<child path>" exists
 constexpr uint32_t META_TERM_WILD = 1u << 9;    // ... and that filter is a wildcard filter
 constexpr uint32_t META_PH = 1u << 10;          // literal edges perfect-hashed (seed below); else 2-slot buckets
-constexpr uint32_t META_LITF_EXACT = 1u << 11;  // lit_lo = the child's only literal edge word
+constexpr uint32_t META_LITF_EXACT = 1u << 11;  // litf = the child's only literal edge word
 constexpr uint32_t META_LITF_NONE = 1u << 12;   // the child has no literal edge at all
+constexpr uint32_t META_BUCKET_OVF = 1u << 13;  // (slot position, wide nodes) first slot of a 2-slot
+                                                // bucket some word of which lives in its secondary bucket
 constexpr uint32_t META_SEED_SHIFT = 16;        // 8-bit perfect-hash seed
 constexpr uint32_t PH_MAX_CAPLOG = 15;
 
-// 32-byte edge slot: the child's record travels with the edge, so one probe (two dwordx4
-// loads of one 32-B sector) yields everything the next level needs: the filter ids to emit
-// and a filter over the child's literal edges, tested against the topic's next word before
-// the child is even pushed.  A node's '+' edge, when present, always sits in slot 0 of its
-// array; literal edges are perfect-hashed by a per-node seed found at build time (one load
-// per lookup, hit or miss), or — in wide nodes, where no seed fits — hashed into 2-slot
-// buckets of one 64-B sector each (one sector per lookup, a second one for ~1% of words).
-struct alignas(32) EdgeSlot {
+// 16-byte edge slot: the child's record travels with the edge, so one probe (one dwordx4
+// load per lane) yields everything the next level's walk needs: the child's edge array and
+// meta, and a filter over the child's literal edges, tested against the topic's next word
+// before the child is even pushed.  A node's '+' edge, when present, always sits in slot 0 of
+// its array; literal edges are perfect-hashed by a per-node seed found at build time (one
+// load per lookup, hit or miss), or — in wide nodes, where no seed fits — hashed into 2-slot
+// buckets (two loads per lookup, two more for ~1% of words).
+//
+// The filter ids of the child reached through slot i live apart, in `fids[2i]` ("<child>/#")
+// and `fids[2i + 1]` ("<child>"): the walk emits the reference 2i + kind and the scatter
+// kernel resolves it, so a probe moves 16 B instead of 32 and the walk never waits on a fid.
+// `fids[2 * n_slots]` holds the root's '#' filter (REF of the root hash filter).
+struct alignas(16) EdgeSlot {
   uint32_t wid;         // key (WID_NONE = empty)
   uint32_t child_base;  // first slot of the child's edge array
-  uint32_t meta;        // META_* (+ seed) of the child
-  uint32_t aux;         // bit 0 (first slot of a 2-slot bucket of a wide node): some word
-                        // whose primary bucket this is lives in its secondary bucket
-  uint32_t hash_fid;    // filter "<child path>/#" or FID_NONE
-  uint32_t term_fid;    // filter "<child path>"   or FID_NONE
-  uint32_t lit_lo;      // literal-edge filter of the child: the word (LITF_EXACT) or a
-  uint32_t lit_hi;      //   2-probe 64-bit Bloom mask (all ones when the child is wide)
+  uint32_t meta;        // META_* (+ seed) of the child; META_BUCKET_OVF belongs to this slot
+  uint32_t litf;        // literal-edge filter of the child: its only literal word (LITF_EXACT)
+                        //   or a 2-probe 32-bit Bloom mask (all ones when the child is wide)
 };
-static_assert(sizeof(EdgeSlot) == 32, "EdgeSlot must be 32 bytes");
+static_assert(sizeof(EdgeSlot) == 16, "EdgeSlot must be 16 bytes");
+constexpr uint64_t MAX_SLOTS = (1ull << 31) - 1;  // fid references 2i + kind fit 32 bits
 
 // 32-byte vocab slot; words up to 16 bytes are verified from `inl` without a second load.
 struct alignas(16) VocabSlot {
@@ -76,12 +80,14 @@ static_assert(sizeof(VocabSlot) == 32, "VocabSlot must be 32 bytes");
 // Kernel-argument view of one committed snapshot.
 struct TableView {
   const EdgeSlot* edges;
+  const uint32_t* fids;  // 2 * n_slots + 1 filter ids (see EdgeSlot)
   const VocabSlot* vocab;
   const uint8_t* arena;
   uint32_t vocab_mask;
   uint32_t root_base;      // root's edge array
   uint32_t root_meta;      // META_* of the root
   uint32_t root_hash_fid;  // filter '#' or FID_NONE
+  uint32_t root_hash_ref;  // 2 * n_slots: fids[] index of the root's '#' filter
 };
 
 // murmur3 fmix32: spreads word ids inside a node's edge array.
@@ -126,11 +132,10 @@ EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask) {
   return mix32(wid ^ (seed * 0x9E3779B1u + 0x7F4A7C15u)) & mask;
 }
 
-// Wide (non-perfect-hashed) nodes use 2-slot buckets = one 64-B sector: a word lives in its
-// primary bucket, or — rarely, flagged by AUX_OVERFLOW on the primary bucket's first slot —
+// Wide (non-perfect-hashed) nodes use 2-slot buckets: a word lives in its primary bucket,
+// or — rarely, flagged by META_BUCKET_OVF on the primary bucket's first slot —
 // in its secondary bucket.  Bucket 0's slot 0 is '+'.  `seed` (7 bits) is re-drawn by the
 // builder until every word fits.
-constexpr uint32_t AUX_OVERFLOW = 1u;
 EMQX_HD uint32_t bucket1(uint32_t wid, uint32_t seed, uint32_t nbmask) {
   return mix32(wid ^ (0x3C6EF372u + seed * 0x9E3779B9u)) & nbmask;
 }
@@ -142,14 +147,13 @@ constexpr uint32_t CUCKOO_SEEDS = 128;
 
 EMQX_HD uint32_t litf_hash(uint32_t wid) { return mix32(wid ^ 0xA5A5A5A5u); }
 
-// May the child (meta, lit_lo, lit_hi) have a literal edge for `wid`?  No false negatives.
-EMQX_HD bool litf_may_contain(uint32_t meta, uint32_t lo, uint32_t hi, uint32_t wid) {
+// May the child (meta, litf) have a literal edge for `wid`?  No false negatives.
+EMQX_HD bool litf_may_contain(uint32_t meta, uint32_t litf, uint32_t wid) {
   if (meta & META_LITF_NONE) return false;
-  if (meta & META_LITF_EXACT) return lo == wid;
+  if (meta & META_LITF_EXACT) return litf == wid;
   const uint32_t h = litf_hash(wid);
-  const uint32_t b1 = h & 63u, b2 = (h >> 6) & 63u;
-  const uint32_t w1 = b1 < 32 ? lo : hi, w2 = b2 < 32 ? lo : hi;
-  return ((w1 >> (b1 & 31u)) & 1u) && ((w2 >> (b2 & 31u)) & 1u);
+  return ((litf >> (h & 31u)) & (litf >> ((h >> 5) & 31u)) & 1u) != 0;
 }
+constexpr uint32_t LITF_BLOOM_MAX = 16;  // wider children get an all-ones filter
 
 }  // namespace emqx

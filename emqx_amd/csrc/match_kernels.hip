@@ -6,22 +6,24 @@
 //
 // Structure:
 //   match_fast_kernel  one wavefront per tile of 64 published topics.
-//     phase A  the tile's topic bytes are staged into LDS with coalesced dword loads; each
-//              lane splits its topic on '/', hashes every level (FNV-1a) and interns it in
-//              the vocab table (exact byte check) -> word ids in LDS.
+//     phase A  the tile's topic bytes are read with coalesced 16-B loads into an LDS level
+//              map ('/' and wildcard bytes); each lane splits its topic from the map, then
+//              every word of the tile is hashed and interned word-parallel in the vocab
+//              table (exact byte check) -> word ids in LDS.
 //     phase B  the frontier of all 64 topics is pooled in one LDS work stack.  Each step
 //              pops up to 64*K (topic, node, level) items — K per lane, all their loads in
 //              flight together — probes each node's '+' edge (slot 0, no search) and its
-//              literal edge (linear probing), emits the children's '#' and terminal filter
-//              ids (carried in the slot: no dependent load) and pushes the children; pushes
-//              and emissions are stream-compacted with wave ballots + popcount prefix sums.
+//              literal edge (perfect hash or 2-slot bucket), emits references to the
+//              children's '#' and terminal filter ids (slot index * 2 + kind: no fid load on
+//              the walk) and pushes the children; pushes and emissions are stream-compacted
+//              with wave ballots + popcount prefix sums.
 //              The stack is LIFO, which bounds it by ~64*K x levels whatever the frontier
 //              width.  No MFMA: this is pointer chasing.
-//     phase C  per-topic counts + a per-tile slab of (topic, filter id) entries.
+//     phase C  per-topic counts + a per-tile slab of (topic, fid reference) entries.
 //   match_deep_kernel  topics that did not fit the fast path's LDS budget (very deep
 //              topics, or a frontier that overflowed the stack): one wavefront per topic,
 //              word ids and stack in global scratch.
-//   scan / scatter     counts -> CSR offsets; slab entries -> out_ids.
+//   scan / scatter     counts -> CSR offsets; slab entries -> fids[ref] -> out_ids.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -84,25 +86,29 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
   return v;
 }
 
-// One edge slot: key/child record + the child's filter ids and literal-edge filter.
+// One edge slot (wid, child_base, child meta, child literal filter) and its index, which
+// names the child's filter ids: fids[2 * idx] ('#') and fids[2 * idx + 1] (terminal).
 struct Slot {
-  uint4 a;  // wid, child_base, meta, child
-  uint4 f;  // hash_fid, term_fid, lit_lo, lit_hi
+  uint4 a;
+  uint32_t idx;
 };
 
-__device__ __forceinline__ Slot load_slot(const EdgeSlot* p) {
+__device__ __forceinline__ Slot load_slot(const EdgeSlot* edges, uint32_t i) {
   Slot s;
-  s.a = *reinterpret_cast<const uint4*>(p);
-  s.f = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(p) + 16);
+  s.a = *reinterpret_cast<const uint4*>(edges + i);
+  s.idx = i;
   return s;
 }
 
 __device__ __forceinline__ Slot empty_slot() {
   Slot s;
   s.a = make_uint4(WID_NONE, 0, 0, 0);
-  s.f = make_uint4(FID_NONE, FID_NONE, 0, 0);
+  s.idx = 0;
   return s;
 }
+
+__device__ __forceinline__ uint32_t hash_ref(const Slot& s) { return 2u * s.idx; }
+__device__ __forceinline__ uint32_t term_ref(const Slot& s) { return 2u * s.idx + 1u; }
 
 // Term-filter emission rule per mode (see include/emqx_match.h):
 //  ROUTES          every filter ending here (exact ∪ wildcard), emqx_router.erl:128-133
@@ -139,50 +145,51 @@ __device__ __forceinline__ uint32_t intern_word(const TableView& tv, uint32_t h,
   return WID_NONE;
 }
 
-// Probe one node's edge array for `wid` ('+' sits in slot 0; literals perfect-hashed, or
-// bucketed in 2-slot sectors, according to the node's meta).
-__device__ __forceinline__ bool probe_one(const EdgeSlot* arr, uint32_t meta, uint32_t wid, Slot* out) {
+// Probe one node's edge array (slots [base, base + cap)) for `wid` ('+' sits in slot 0;
+// literals perfect-hashed, or in 2-slot buckets, according to the node's meta).
+__device__ __forceinline__ bool probe_one(const EdgeSlot* edges, uint32_t base, uint32_t meta, uint32_t wid,
+                                          Slot* out) {
   if (wid == WID_PLUS) {
-    *out = load_slot(arr);
+    *out = load_slot(edges, base);
     return out->a.x == WID_PLUS;
   }
   const uint32_t mask = (1u << (meta & META_CAPLOG2_MASK)) - 1u;
   const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
   if (meta & META_PH) {
-    *out = load_slot(arr + lit_slot(wid, sd, mask));
+    *out = load_slot(edges, base + lit_slot(wid, sd, mask));
     return out->a.x == wid;
   }
   const uint32_t nbm = mask >> 1;
   const uint32_t b1 = bucket1(wid, sd, nbm);
-  const Slot x = load_slot(arr + 2 * b1), y = load_slot(arr + 2 * b1 + 1);
+  const Slot x = load_slot(edges, base + 2 * b1), y = load_slot(edges, base + 2 * b1 + 1);
   if (x.a.x == wid) { *out = x; return true; }
   if (y.a.x == wid) { *out = y; return true; }
-  if (!(x.a.w & AUX_OVERFLOW)) return false;
+  if (!(x.a.z & META_BUCKET_OVF)) return false;
   const uint32_t b2 = bucket2(wid, sd, nbm);
-  const Slot u = load_slot(arr + 2 * b2), v = load_slot(arr + 2 * b2 + 1);
+  const Slot u = load_slot(edges, base + 2 * b2), v = load_slot(edges, base + 2 * b2 + 1);
   if (u.a.x == wid) { *out = u; return true; }
   if (v.a.x == wid) { *out = v; return true; }
   return false;
 }
 
 // Byte-identical lookup of a wildcard "topic" for match_routes (emqx_router.erl:130):
-// walks literal/'+'/'#' edges; a final '#' is the node's hash filter.  Returns the fid or
-// FID_NONE.
+// walks literal/'+'/'#' edges; a final '#' is the node's hash filter.  Returns the filter's
+// fids[] reference or FID_NONE.
 template <class WidAt>
 __device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at) {
-  uint32_t base = tv.root_base, meta = tv.root_meta, hash_fid = tv.root_hash_fid, term_fid = FID_NONE;
+  uint32_t base = tv.root_base, meta = tv.root_meta, href = tv.root_hash_ref, tref = FID_NONE;
   for (uint32_t k = 0; k < nlev; ++k) {
     const uint32_t w = wid_at(k);
-    if (w == WID_HASH && k + 1 == nlev) return (meta & META_HAS_HASH) ? hash_fid : FID_NONE;
+    if (w == WID_HASH && k + 1 == nlev) return (meta & META_HAS_HASH) ? href : FID_NONE;
     if (w == WID_NONE || !(meta & META_HAS_EDGES)) return FID_NONE;
     Slot s;
-    if (!probe_one(tv.edges + base, meta, w, &s)) return FID_NONE;
+    if (!probe_one(tv.edges, base, meta, w, &s)) return FID_NONE;
     base = s.a.y;
     meta = s.a.z;
-    hash_fid = s.f.x;
-    term_fid = s.f.y;
+    href = hash_ref(s);
+    tref = term_ref(s);
   }
-  return (meta & META_HAS_TERM) ? term_fid : FID_NONE;
+  return (meta & META_HAS_TERM) ? tref : FID_NONE;
 }
 
 // Item (8 B):  x = edge-array base of the node
@@ -208,10 +215,10 @@ __device__ __forceinline__ uint2 make_item(uint32_t base, uint32_t meta, bool dr
 
 __device__ __forceinline__ uint32_t item_topic(uint2 it) { return (it.y >> IT_TOPIC_SHIFT) & 63u; }
 
-// Probe the '+' edge (slot 0) and the literal edge of K nodes at once: every load is issued
+// Probe the '+' edge and the literal edge of K nodes at once: every load is issued
 // before any result is consumed, so a step costs one dependent round trip (plus one more for
 // the ~1% of wide-node words displaced to their secondary bucket).  Perfect-hashed nodes
-// answer in one slot load; wide nodes load their word's 2-slot bucket (one 64-B sector).
+// answer in one slot load; wide nodes load their word's 2-slot bucket (one 32-B pair).
 template <int K>
 __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, const uint32_t (&base)[K],
                                             const uint32_t (&hparams)[K], const bool (&isph)[K],
@@ -223,7 +230,6 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
   uint32_t sdk[K], nbm[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const EdgeSlot* arr = edges + base[k];
     const uint32_t caplog = isph[k] ? (hparams[k] & 15u) : (hparams[k] & 31u);
     sdk[k] = isph[k] ? (hparams[k] >> 4) : (hparams[k] >> 5);
     const uint32_t mask = (1u << caplog) - 1u;
@@ -233,9 +239,9 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
     pls[k] = empty_slot();
     lit[k] = pls[k];
     alt[k] = pls[k];
-    if (needP[k]) pls[k] = load_slot(arr);
-    if (needL[k]) lit[k] = load_slot(arr + i1);
-    if (wide[k]) alt[k] = load_slot(arr + i1 + 1);  // same 64-B sector
+    if (needP[k]) pls[k] = load_slot(edges, base[k]);
+    if (needL[k]) lit[k] = load_slot(edges, base[k] + i1);
+    if (wide[k]) alt[k] = load_slot(edges, base[k] + i1 + 1);  // same 32-B bucket
   }
   bool any_again = false;
 #pragma unroll
@@ -246,7 +252,7 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
       lit[k] = alt[k];
       fL[k] = true;
     }
-    again[k] = wide[k] && !fL[k] && (lit[k].a.w & AUX_OVERFLOW);
+    again[k] = wide[k] && !fL[k] && (lit[k].a.z & META_BUCKET_OVF);
     any_again |= again[k];
   }
   if (__any(any_again)) {  // secondary buckets (rare): one more dependent round trip
@@ -254,7 +260,7 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
     for (int k = 0; k < K; ++k) {
       if (!again[k]) continue;
       const uint32_t i2 = 2u * bucket2(wid[k], sdk[k], nbm[k]);
-      const Slot u = load_slot(edges + base[k] + i2), v = load_slot(edges + base[k] + i2 + 1);
+      const Slot u = load_slot(edges, base[k] + i2), v = load_slot(edges, base[k] + i2 + 1);
       ++extra;
       if (u.a.x == wid[k]) { lit[k] = u; fL[k] = true; }
       else if (v.a.x == wid[k]) { lit[k] = v; fL[k] = true; }
@@ -495,6 +501,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   const uint32_t incl = wave_incl_scan(need, lane);
   const uint32_t wbase = incl - need;
   if (valid && !defer && incl > static_cast<uint32_t>(WID_CAP)) defer = true;
+  L.wend[lane] = incl;  // end of the topic's word ids (= the next topic's first)
 
   if (valid && !defer) {
     uint32_t j = wbase;
@@ -543,7 +550,6 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     seen |= note(put(end));
     wild = (seen & 1u) != 0;
     longw = (seen & 2u) != 0;
-    L.wend[lane] = wbase + nlev;
   }
   // words of the tile: entries [0, nwords) of wids belong to topics kept on the fast path
   uint32_t nwords = (valid && !defer) ? incl : 0u;
@@ -614,7 +620,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   uint32_t stop = 0;      // wave-uniform: items in the HBM spill
   uint32_t maxtop = 0;    // wave-uniform (LDS + spill)
   uint32_t evals = 0;     // per lane
-  uint32_t dg[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // diagnostic counters (per lane)
+  uint32_t dg[DIAG_NCOUNT] = {};  // diagnostic counters (per lane)
 
   // root: '#' emission, exact walk of wildcard topics, the root item
   {
@@ -631,7 +637,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
         evals = 1;  // the root visit, F_0
         if (!dollar && (tv.root_meta & META_HAS_HASH)) {
           e0 = true;  // filter '#'
-          g0 = tv.root_hash_fid;
+          g0 = tv.root_hash_ref;
         }
         if (tv.root_meta & META_HAS_EDGES) {
           push = true;
@@ -733,6 +739,14 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
         dg[3] += fL[k] ? 1u : 0u;
         dg[5] += needP[k] ? 1u : 0u;
         dg[6] += fP[k] ? 1u : 0u;
+        if (act[k]) {
+          const uint32_t lvl = widx[k] - (tl[k] ? L.wend[tl[k] - 1] : 0u);
+#pragma unroll
+          for (uint32_t q = 0; q < 8; ++q) dg[DIAG_LEVEL0 + q] += (lvl == q || (q == 7 && lvl > 7)) ? 1u : 0u;
+          const uint32_t cl = isph[k] ? (hpar[k] & 15u) : (hpar[k] & 31u);
+          dg[DIAG_SMALL] += cl <= 3 ? 1u : 0u;
+          dg[DIAG_WIDE] += cl > 3 ? 1u : 0u;
+        }
       }
       dg[0] += 1;
     }
@@ -752,8 +766,8 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
       // the topic's next word decides whether a child's literal edges can matter at all;
       // a child with nothing left to probe is not pushed
       nwid[k] = (pL[k] || pP[k]) ? L.wids[widx[k] + 1] : WID_NONE;
-      nlL[k] = nwid[k] == WID_NONE || !litf_may_contain(lit[k].a.z, lit[k].f.z, lit[k].f.w, nwid[k]);
-      nlP[k] = nwid[k] == WID_NONE || !litf_may_contain(pls[k].a.z, pls[k].f.z, pls[k].f.w, nwid[k]);
+      nlL[k] = nwid[k] == WID_NONE || !litf_may_contain(lit[k].a.z, lit[k].a.w, nwid[k]);
+      nlP[k] = nwid[k] == WID_NONE || !litf_may_contain(pls[k].a.z, pls[k].a.w, nwid[k]);
       pL[k] = pL[k] && !(nlL[k] && !(lit[k].a.z & META_HAS_PLUS));
       pP[k] = pP[k] && !(nlP[k] && !(pls[k].a.z & META_HAS_PLUS));
       ce[k] = (eLh[k] ? 1u : 0u) + (eLt[k] ? 1u : 0u) + (ePh[k] ? 1u : 0u) + (ePt[k] ? 1u : 0u);
@@ -766,10 +780,10 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const uint64_t tag = static_cast<uint64_t>(tl[k]) << 32;
-        if (eLh[k]) { if (pos < cap) slab[pos] = tag | lit[k].f.x; ++pos; }
-        if (eLt[k]) { if (pos < cap) slab[pos] = tag | lit[k].f.y; ++pos; }
-        if (ePh[k]) { if (pos < cap) slab[pos] = tag | pls[k].f.x; ++pos; }
-        if (ePt[k]) { if (pos < cap) slab[pos] = tag | pls[k].f.y; ++pos; }
+        if (eLh[k]) { if (pos < cap) slab[pos] = tag | hash_ref(lit[k]); ++pos; }
+        if (eLt[k]) { if (pos < cap) slab[pos] = tag | term_ref(lit[k]); ++pos; }
+        if (ePh[k]) { if (pos < cap) slab[pos] = tag | hash_ref(pls[k]); ++pos; }
+        if (ePt[k]) { if (pos < cap) slab[pos] = tag | term_ref(pls[k]); ++pos; }
         if (ce[k]) atomicAdd(&L.cnt[tl[k]], ce[k]);
       }
       cursor += tot;
@@ -799,7 +813,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     dg[10] = lane == 0 ? static_cast<uint32_t>(clk2 - clk1) : 0u;
     dg[11] = lane == 0 ? 1u : 0u;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
+    for (int i = 0; i < DIAG_NCOUNT; ++i) {
       const uint32_t v = wave_sum(dg[i]);
       if (lane == 0 && v) atomicAdd(reinterpret_cast<unsigned long long*>(a.diag + i), static_cast<unsigned long long>(v));
     }
@@ -916,7 +930,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     } else {
       if (lane == 0) evals = 1;
       const bool eh = lane == 0 && !dollar && (tv.root_meta & META_HAS_HASH);
-      emit(eh, tv.root_hash_fid, false, 0, false, 0, false, 0);
+      emit(eh, tv.root_hash_ref, false, 0, false, 0, false, 0);
       if (tv.root_meta & META_HAS_EDGES) {
         const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
         if (lane == 0)
@@ -953,8 +967,9 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       probe_items<1>(tv.edges, qbase, qhp, qph, nL, w, nP, lit, fL, pls, fP, extra);
       evals += (fL[0] ? 1u : 0u) + (fP[0] ? 1u : 0u);
       const uint32_t m0 = lit[0].a.z, m1 = pls[0].a.z;
-      emit(fL[0] && (m0 & META_HAS_HASH), lit[0].f.x, fL[0] && leaf && term_ok(m0, mode, droot), lit[0].f.y,
-           fP[0] && (m1 & META_HAS_HASH), pls[0].f.x, fP[0] && leaf && term_ok(m1, mode, false), pls[0].f.y);
+      emit(fL[0] && (m0 & META_HAS_HASH), hash_ref(lit[0]), fL[0] && leaf && term_ok(m0, mode, droot),
+           term_ref(lit[0]), fP[0] && (m1 & META_HAS_HASH), hash_ref(pls[0]),
+           fP[0] && leaf && term_ok(m1, mode, false), term_ref(pls[0]));
       const bool p0 = fL[0] && !leaf && (m0 & META_HAS_EDGES);
       const bool p1 = fP[0] && !leaf && (m1 & META_HAS_EDGES);
       uint32_t ptot;
@@ -1079,7 +1094,7 @@ __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a, const ui
     const uint32_t tl = static_cast<uint32_t>(e >> 32);
     if ((dmask >> tl) & 1ull) continue;
     const uint32_t r = atomicAdd(&rank[wv][tl], 1u);
-    out_ids[offsets[t0 + tl] + r] = static_cast<uint32_t>(e);
+    out_ids[offsets[t0 + tl] + r] = a.tv.fids[static_cast<uint32_t>(e)];
   }
 }
 
@@ -1092,7 +1107,7 @@ __global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a, const ui
     const uint32_t j = static_cast<uint32_t>(e >> 32);
     const uint32_t t = a.deferred[j];
     const uint32_t r = atomicAdd(&deep_rank[j], 1u);
-    out_ids[offsets[t] + r] = static_cast<uint32_t>(e);
+    out_ids[offsets[t] + r] = a.tv.fids[static_cast<uint32_t>(e)];
   }
 }
 
@@ -1125,6 +1140,7 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K1_S256: launch_fast_t<4, 256, 512, 1>(a, ntiles, s); break;
     case FAST_K2_S512: launch_fast_t<4, 512, 640, 2>(a, ntiles, s); break;
     case FAST_K1_S384: launch_fast_t<4, 384, 640, 1>(a, ntiles, s); break;
+    case FAST_K2_S512W: launch_fast_t<4, 512, 512, 2>(a, ntiles, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -293,16 +293,23 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     });
   }
 
+  // A node with a '+' edge keeps it in slot 0.  (Replicating it at the head of every 128-B
+  // line of a wide array, so that '+' and the literal probe share a line, cut L2 misses by
+  // 12% but made the kernel 6% slower: the walk is bound by per-lane access issue, not by
+  // line fetches — DESIGN.md §4.)
+  auto plus_slot = [&](uint64_t v, uint64_t /*cap*/, uint32_t i) -> bool { return has_plus[v] && i == 0; };
+
   // Bucketed placement of node v's literal edges (2-slot buckets, two candidate buckets,
-  // random-walk eviction) for one seed; false when some word cannot be placed.  Slot 0
-  // stays free for '+'.  Afterwards every word outside its primary bucket flags that bucket.
+  // random-walk eviction) for one seed; false when some word cannot be placed.  The '+'
+  // slots stay free.  Afterwards every word outside its primary bucket flags that bucket.
   std::vector<uint32_t> ck_key, ck_child;
   auto bucket_place = [&](uint64_t v, uint32_t sd, uint32_t cap, std::vector<uint32_t>& key_out,
                           std::vector<uint32_t>& child_out) -> bool {
     const uint32_t nbm = cap / 2 - 1;
     key_out.assign(cap, WID_NONE);
     child_out.assign(cap, 0);
-    if (has_plus[v]) key_out[0] = WID_PLUS;
+    for (uint32_t i = 0; i < cap; ++i)
+      if (plus_slot(v, cap, i)) key_out[i] = WID_PLUS;
     uint32_t rng = 0x9E3779B9u ^ static_cast<uint32_t>(v) ^ (sd << 20);
     for (uint64_t j = coff[v]; j < coff[v + 1]; ++j) {
       if (cwid[j] == WID_PLUS) continue;
@@ -348,10 +355,10 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
         for (uint32_t sd = 0; sd < 256 && !done; ++sd) {
           slots_tmp.clear();
           bool ok = true;
-          if (has_plus[v]) slots_tmp.push_back(0);
           for (uint64_t j = coff[v]; j < coff[v + 1] && ok; ++j) {
             if (cwid[j] == WID_PLUS) continue;
             const uint32_t sl = lit_slot(cwid[j], sd, mask);
+            ok &= !plus_slot(v, cap, sl);
             for (uint32_t x : slots_tmp) ok &= (x != sl);
             slots_tmp.push_back(sl);
           }
@@ -378,50 +385,92 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     }
   }
 
-  // ---- pass 4: layout — BFS by depth, larger arrays first (natural alignment) -------
-  std::vector<uint32_t> order(n_nodes);
-  for (uint64_t v = 0; v < n_nodes; ++v) order[v] = static_cast<uint32_t>(v);
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-    if (depth[a] != depth[b]) return depth[a] < depth[b];
-    return caplog[a] > caplog[b];
-  });
-  std::vector<uint32_t> new_id(n_nodes), base(n_nodes, 0);
+  // ---- pass 4: layout — line-packed preorder ----------------------------------------
+  // An L2 miss fetches a 128-B line (8 slots) while a probe uses one 16-B slot, so the
+  // layout packs walks into lines: when a node is visited, the arrays of all its children
+  // are placed right behind it, first-fit into the currently open line (an array of c <= 8
+  // slots is aligned to c, so it never straddles a line; larger arrays start on a line);
+  // then the children are visited in order.  A chain of small nodes — the deep tail of
+  // most filters — shares one line across several levels, so its walk misses once.
+  std::vector<uint32_t> base(n_nodes, 0);
   uint64_t total_slots = 0;
-  for (uint64_t k = 0; k < n_nodes; ++k) {
-    const uint32_t v = order[k];
-    new_id[v] = static_cast<uint32_t>(k);
-    if (n_edges[v]) {
-      base[v] = static_cast<uint32_t>(total_slots);
-      total_slots += 1ull << caplog[v];
-      if (total_slots >= 0xFFFFFFF0ull) {
-        if (err) *err = "edge slot array exceeds 2^32 slots";
+  {
+    constexpr uint64_t LINE = 8;
+    uint64_t line = 0;  // open line (slot index, multiple of LINE)
+    uint32_t used = 0xFFu;  // its occupied slots (bit mask); all ones = no open line
+    auto place = [&](uint32_t caplg) -> uint64_t {
+      const uint64_t c = 1ull << caplg;
+      if (c >= LINE) {
+        const uint64_t at = (total_slots + LINE - 1) & ~(LINE - 1);
+        total_slots = at + c;
+        used = 0xFFu;
+        return at;
+      }
+      const uint32_t want = (1u << c) - 1u;
+      for (uint32_t o = 0; o < LINE; o += static_cast<uint32_t>(c))
+        if (!(used & (want << o))) {
+          used |= want << o;
+          return line + o;
+        }
+      line = (total_slots + LINE - 1) & ~(LINE - 1);
+      total_slots = line + LINE;
+      used = want;
+      return line;
+    };
+    // EMQX_LAYOUT=bfs (A/B runs only): breadth-first by depth, larger arrays first
+    static const bool bfs = [] {
+      const char* v = getenv("EMQX_LAYOUT");
+      return v && std::strcmp(v, "bfs") == 0;
+    }();
+    if (bfs) {
+      std::vector<uint32_t> order(n_nodes);
+      for (uint64_t v = 0; v < n_nodes; ++v) order[v] = static_cast<uint32_t>(v);
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return depth[a] != depth[b] ? depth[a] < depth[b] : caplog[a] > caplog[b];
+      });
+      for (uint32_t v : order)
+        if (n_edges[v]) base[v] = static_cast<uint32_t>(place(caplog[v]));
+      if (total_slots > MAX_SLOTS) {
+        if (err) *err = "edge slot array exceeds 2^31 slots";
         return false;
       }
     }
+    std::vector<uint32_t> stack;
+    if (n_edges[0] && !bfs) {
+      base[0] = static_cast<uint32_t>(place(caplog[0]));
+      stack.push_back(0);
+    }
+    while (!stack.empty()) {
+      const uint32_t v = stack.back();
+      stack.pop_back();
+      for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
+        if (n_edges[cid[j]]) base[cid[j]] = static_cast<uint32_t>(place(caplog[cid[j]]));
+      if (total_slots > MAX_SLOTS) {
+        if (err) *err = "edge slot array exceeds 2^31 slots";
+        return false;
+      }
+      for (uint64_t j = coff[v + 1]; j-- > coff[v];)
+        if (n_edges[cid[j]]) stack.push_back(cid[j]);
+    }
   }
   // literal-edge filter of each node (stored in the slot that leads to it)
-  std::vector<uint32_t> lf_lo(n_nodes, 0), lf_hi(n_nodes, 0), lf_flag(n_nodes, 0);
+  std::vector<uint32_t> lf(n_nodes, 0), lf_flag(n_nodes, 0);
   for (uint64_t v = 0; v < n_nodes; ++v) {
-    uint32_t n_lit = 0, only = WID_NONE, lo = 0, hi = 0;
+    uint32_t n_lit = 0, only = WID_NONE, bloom = 0;
     for (uint64_t j = coff[v]; j < coff[v + 1]; ++j) {
       if (cwid[j] == WID_PLUS) continue;
       ++n_lit;
       only = cwid[j];
       const uint32_t h = litf_hash(cwid[j]);
-      const uint32_t b1 = h & 63u, b2 = (h >> 6) & 63u;
-      (b1 < 32 ? lo : hi) |= 1u << (b1 & 31u);
-      (b2 < 32 ? lo : hi) |= 1u << (b2 & 31u);
+      bloom |= (1u << (h & 31u)) | (1u << ((h >> 5) & 31u));
     }
     if (n_lit == 0) {
       lf_flag[v] = META_LITF_NONE;
     } else if (n_lit == 1) {
       lf_flag[v] = META_LITF_EXACT;
-      lf_lo[v] = only;
-    } else if (n_lit <= 32) {
-      lf_lo[v] = lo;
-      lf_hi[v] = hi;
+      lf[v] = only;
     } else {
-      lf_lo[v] = lf_hi[v] = ~0u;
+      lf[v] = n_lit <= LITF_BLOOM_MAX ? bloom : ~0u;
     }
   }
   auto meta_of = [&](uint32_t v) -> uint32_t {
@@ -436,24 +485,25 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     return m;
   };
 
-  out.edges.assign(std::max<uint64_t>(total_slots, 1),
-                   EdgeSlot{WID_NONE, 0, 0, 0, FID_NONE, FID_NONE, 0, 0});
+  const uint64_t n_slots = std::max<uint64_t>(total_slots, 1);
+  out.edges.assign(n_slots, EdgeSlot{WID_NONE, 0, 0, 0});
+  out.fids.assign(2 * n_slots + 1, FID_NONE);
   auto write_slot = [&](uint64_t at, uint32_t wid, uint32_t child) {
     EdgeSlot& s = out.edges[at];
     s.wid = wid;
     s.child_base = base[child];
-    s.meta = meta_of(child);
-    s.aux = 0;
-    s.hash_fid = hash_fid[child];
-    s.term_fid = term_fid[child];
-    s.lit_lo = lf_lo[child];
-    s.lit_hi = lf_hi[child];
+    s.meta = meta_of(child) | (s.meta & META_BUCKET_OVF);
+    s.litf = lf[child];
+    out.fids[2 * at] = hash_fid[child];
+    out.fids[2 * at + 1] = term_fid[child];
   };
   for (uint64_t v = 0; v < n_nodes; ++v) {
     if (!n_edges[v]) continue;
     // '+' is pinned at slot 0
     for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
-      if (cwid[j] == WID_PLUS) write_slot(base[v], WID_PLUS, cid[j]);
+      if (cwid[j] == WID_PLUS)
+        for (uint32_t i = 0; i < (1u << caplog[v]); ++i)
+          if (plus_slot(v, 1ull << caplog[v], i)) write_slot(base[v] + i, WID_PLUS, cid[j]);
     if (ph[v]) {
       const uint32_t mask = (1u << caplog[v]) - 1;
       for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
@@ -470,10 +520,12 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       const uint32_t key = ck_key[i];
       if (key == WID_NONE || key == WID_PLUS) continue;
       const uint32_t b1 = bucket1(key, seed[v], nbm);
-      if (i / 2 != b1) out.edges[base[v] + 2 * b1].aux |= AUX_OVERFLOW;
+      if (i / 2 != b1) out.edges[base[v] + 2 * b1].meta |= META_BUCKET_OVF;
     }
   }
   out.root_hash_fid = hash_fid[0];
+  out.root_hash_ref = static_cast<uint32_t>(2 * n_slots);
+  out.fids[2 * n_slots] = hash_fid[0];
   out.root_base = base[0];
   out.root_meta = meta_of(0);
   out.n_nodes = n_nodes;
@@ -526,7 +578,7 @@ bool check_tables(const HostTables& t, std::string* err) {
       if (s.wid == WID_NONE) continue;
       if (s.wid == WID_PLUS) {
         if (i != 0 || !(meta & META_HAS_PLUS)) {
-          if (err) *err = "'+' edge not in slot 0";
+          if (err) *err = "'+' edge outside its slots";
           return false;
         }
         continue;
@@ -537,7 +589,7 @@ bool check_tables(const HostTables& t, std::string* err) {
       else {
         const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u, nbm = mask / 2;
         const uint32_t b1 = bucket1(s.wid, sd, nbm), b2 = bucket2(s.wid, sd, nbm);
-        found = i / 2 == b1 || (i / 2 == b2 && (t.edges[base + 2 * b1].aux & AUX_OVERFLOW));
+        found = i / 2 == b1 || (i / 2 == b2 && (t.edges[base + 2 * b1].meta & META_BUCKET_OVF));
       }
       if (!found) {
         if (err) *err = "edge not at its lookup slot";
@@ -550,6 +602,20 @@ bool check_tables(const HostTables& t, std::string* err) {
     }
     (void)n_lit;
   }
+  // filter ids: a slot's pair agrees with its child's meta
+  for (uint64_t i = 0; i < n; ++i) {
+    const EdgeSlot& s = t.edges[i];
+    if (s.wid == WID_NONE) continue;
+    if ((t.fids[2 * i] != FID_NONE) != ((s.meta & META_HAS_HASH) != 0) ||
+        (t.fids[2 * i + 1] != FID_NONE) != ((s.meta & META_HAS_TERM) != 0)) {
+      if (err) *err = "filter ids disagree with the child's meta";
+      return false;
+    }
+  }
+  if (t.fids.size() != 2 * n + 1 || t.fids[t.root_hash_ref] != t.root_hash_fid) {
+    if (err) *err = "root '#' filter reference";
+    return false;
+  }
   // literal filters: every literal child word of a node must pass the node's filter
   for (uint64_t i = 0; i < n; ++i) {
     const EdgeSlot& s = t.edges[i];
@@ -558,7 +624,7 @@ bool check_tables(const HostTables& t, std::string* err) {
     for (uint32_t j = 0; j <= mask; ++j) {
       const EdgeSlot& c = t.edges[s.child_base + j];
       if (c.wid == WID_NONE || c.wid == WID_PLUS) continue;
-      if (!litf_may_contain(s.meta, s.lit_lo, s.lit_hi, c.wid)) {
+      if (!litf_may_contain(s.meta, s.litf, c.wid)) {
         if (err) *err = "literal filter rejects a present word";
         return false;
       }

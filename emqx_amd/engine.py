@@ -99,11 +99,12 @@ class Engine:
         check(_lib.lib().emqx_set_tuning(self._h, key.encode(), int(value)), "emqx_set_tuning")
 
     DIAG_NAMES = ("steps", "items", "lit_probes", "lit_hits", "lit_extra_loads", "plus_probes",
-                  "plus_hits", "emits", "spills", "ticks_a", "ticks_b", "waves")
+                  "plus_hits", "emits", "spills", "ticks_a", "ticks_b", "waves",
+                  "lvl0", "lvl1", "lvl2", "lvl3", "lvl4", "lvl5", "lvl6", "lvl7+", "small_arrays", "wide_arrays")
 
     def diag(self, reset: bool = True) -> dict:
-        out = np.zeros(16, dtype=np.uint64)
-        check(_lib.lib().emqx_diag_read(self._h, _ptr(out), 16, int(reset)), "emqx_diag_read")
+        out = np.zeros(32, dtype=np.uint64)
+        check(_lib.lib().emqx_diag_read(self._h, _ptr(out), 32, int(reset)), "emqx_diag_read")
         return {k: int(out[i]) for i, k in enumerate(self.DIAG_NAMES)}
 
     def commit(self) -> None:

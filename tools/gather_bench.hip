@@ -1,6 +1,6 @@
 // Random-access ceiling for the match kernel's access pattern on MI355X (gfx950):
-// 32-byte records (one dwordx4 + one dwordx2 load per lane) at random addresses of a table
-// that is larger than the Infinity Cache.  Two shapes:
+// 16-byte records (one dwordx4 load per lane, the EdgeSlot size) at random addresses of a
+// table from L2-resident to far larger than the Infinity Cache.  Two shapes:
 //   indep  every lane issues R independent random record loads (throughput ceiling)
 //   chase  every lane follows its own chain of R dependent loads (latency x concurrency)
 // Prints one JSON line per (shape, table size, waves per CU).  Used to price the roofline of
@@ -22,8 +22,8 @@
     }                                                                         \
   } while (0)
 
-struct alignas(32) Rec {
-  uint32_t next, a, b, c, d, e, f, g;
+struct alignas(16) Rec {
+  uint32_t next, a, b, c;
 };
 
 __device__ __forceinline__ uint32_t mix(uint32_t x) {
@@ -39,7 +39,7 @@ __global__ void init_kernel(Rec* t, uint32_t n, uint32_t stride) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     Rec r;
     r.next = (uint32_t)(((uint64_t)i * stride + 1) % n);  // stride coprime with n: one long cycle
-    r.a = i; r.b = i ^ 1; r.c = i ^ 2; r.d = i ^ 3; r.e = i ^ 4; r.f = 0; r.g = 0;
+    r.a = i; r.b = i ^ 1; r.c = i ^ 2;
     t[i] = r;
   }
 }
@@ -52,8 +52,7 @@ __global__ void indep_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t ite
     h = mix(h + k);
     const Rec* p = t + (h % n);
     const uint4 x = *reinterpret_cast<const uint4*>(p);
-    const uint2 y = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p) + 16);
-    acc ^= x.x + x.y + x.z + x.w + y.x + y.y;
+    acc ^= x.x + x.y + x.z + x.w;
   }
   if (acc == 0x12345678u) out[0] = acc;
 }
@@ -65,16 +64,15 @@ __global__ void chase_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t ite
   for (uint32_t k = 0; k < iters; ++k) {
     const Rec* p = t + i;
     const uint4 x = *reinterpret_cast<const uint4*>(p);
-    const uint2 y = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p) + 16);
-    acc ^= x.y + y.x;
+    acc ^= x.y + x.w;
     i = x.x;
   }
   if (acc == 0x12345678u) out[0] = acc;
 }
 
 int main(int argc, char** argv) {
-  const uint64_t sizes_mb[] = {64, 2048};
-  const int wpc[] = {8, 16, 32};
+  const uint64_t sizes_mb[] = {2, 64, 1024};
+  const int wpc[] = {8, 16, 24, 32};
   uint32_t* out;
   CK(hipMalloc(&out, 64));
   hipEvent_t e0, e1;
@@ -103,10 +101,10 @@ int main(int argc, char** argv) {
           if (rep == 1) {
             const double loads = (double)blocks * 256 * iters;
             printf("{\"shape\": \"%s\", \"table_mb\": %llu, \"waves_per_cu\": %d, \"ms\": %.4f, "
-                   "\"records_per_s\": %.4g, \"gb_per_s_32B\": %.1f, \"gb_per_s_64B_lines\": %.1f, "
+                   "\"records_per_s\": %.4g, \"gb_per_s_16B\": %.1f, \"gb_per_s_128B_lines\": %.1f, "
                    "\"ns_per_dependent_load\": %.1f}\n",
                    shape == 0 ? "indep" : "chase", (unsigned long long)mb, w, ms, loads / (ms * 1e-3),
-                   loads * 32 / (ms * 1e-3) / 1e9, loads * 64 / (ms * 1e-3) / 1e9,
+                   loads * 16 / (ms * 1e-3) / 1e9, loads * 128 / (ms * 1e-3) / 1e9,
                    shape == 1 ? ms * 1e6 / iters : 0.0);
           }
         }
