@@ -166,7 +166,6 @@ int upload(emqx_engine* e, const HostTables& ht, std::shared_ptr<Snapshot>* out)
   s->tv.root_base = ht.root_base;
   s->tv.root_meta = ht.root_meta;
   s->tv.root_hash_fid = ht.root_hash_fid;
-  s->tv.root_hash_ref = ht.root_hash_ref;
   s->n_nodes = ht.n_nodes;
   s->n_slots = ht.edges.size();
   s->n_words = ht.n_words;

@@ -11,8 +11,8 @@
 //   * edges:  each node owns a power-of-two slice of one global slot array, open-
 //             addressed by word id; '+' is the reserved word WID_PLUS, a non-final '#'
 //             the reserved word WID_HASH; a final '#' is the parent's hash filter.
-//   * fids:   per slot, its child's {filter "<path>/#", filter "<path>"} ids, resolved
-//             after the walk; the root's '#' filter follows the last slot's pair.
+//   * fids:   per slot, its child's {filter "<path>/#", filter "<path>"} ids (inline in
+//             the slot for an edgeless child); the root's '#' filter is a table-view field.
 #pragma once
 
 #include <stdint.h>
@@ -52,20 +52,21 @@ constexpr uint32_t PH_MAX_CAPLOG = 15;
 // its array; literal edges are perfect-hashed by a per-node seed found at build time (one
 // load per lookup, hit or miss), or — in wide nodes, where no seed fits — hashed into 2-slot
 // buckets (two loads per lookup, two more for ~1% of words).
-//
-// The filter ids of the child reached through slot i live apart, in `fids[2i]` ("<child>/#")
-// and `fids[2i + 1]` ("<child>"): the walk emits the reference 2i + kind and the scatter
-// kernel resolves it, so a probe moves 16 B instead of 32 and the walk never waits on a fid.
-// `fids[2 * n_slots]` holds the root's '#' filter (REF of the root hash filter).
+// The filter ids of the child behind slot i live apart, in `fids[2i]` ("<child>/#") and
+// `fids[2i + 1]` ("<child>"), except for a child without edges (no META_HAS_EDGES: it is
+// never pushed), which carries them in place of child_base and litf — the common leaf
+// emission needs no second load.  For the others the walk emits the reference 2i + kind
+// and the scatter kernel resolves it, so a probe moves 16 B and the walk never waits on an id.
 struct alignas(16) EdgeSlot {
   uint32_t wid;         // key (WID_NONE = empty)
-  uint32_t child_base;  // first slot of the child's edge array
+  uint32_t child_base;  // first slot of the child's edge array  | edgeless child: hash_fid
   uint32_t meta;        // META_* (+ seed) of the child; META_BUCKET_OVF belongs to this slot
   uint32_t litf;        // literal-edge filter of the child: its only literal word (LITF_EXACT)
                         //   or a 2-probe 32-bit Bloom mask (all ones when the child is wide)
+                        //   | edgeless child: term_fid
 };
 static_assert(sizeof(EdgeSlot) == 16, "EdgeSlot must be 16 bytes");
-constexpr uint64_t MAX_SLOTS = (1ull << 31) - 1;  // fid references 2i + kind fit 32 bits
+constexpr uint64_t MAX_SLOTS = (1ull << 31) - 1;  // references 2i + kind fit 32 bits
 
 // 32-byte vocab slot; words up to 16 bytes are verified from `inl` without a second load.
 struct alignas(16) VocabSlot {
@@ -80,14 +81,13 @@ static_assert(sizeof(VocabSlot) == 32, "VocabSlot must be 32 bytes");
 // Kernel-argument view of one committed snapshot.
 struct TableView {
   const EdgeSlot* edges;
-  const uint32_t* fids;  // 2 * n_slots + 1 filter ids (see EdgeSlot)
+  const uint32_t* fids;  // 2 * n_slots filter ids (see EdgeSlot)
   const VocabSlot* vocab;
   const uint8_t* arena;
   uint32_t vocab_mask;
   uint32_t root_base;      // root's edge array
   uint32_t root_meta;      // META_* of the root
   uint32_t root_hash_fid;  // filter '#' or FID_NONE
-  uint32_t root_hash_ref;  // 2 * n_slots: fids[] index of the root's '#' filter
 };
 
 // murmur3 fmix32: spreads word ids inside a node's edge array.

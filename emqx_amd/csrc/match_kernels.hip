@@ -13,17 +13,18 @@
 //     phase B  the frontier of all 64 topics is pooled in one LDS work stack.  Each step
 //              pops up to 64*K (topic, node, level) items — K per lane, all their loads in
 //              flight together — probes each node's '+' edge (slot 0, no search) and its
-//              literal edge (perfect hash or 2-slot bucket), emits references to the
-//              children's '#' and terminal filter ids (slot index * 2 + kind: no fid load on
-//              the walk) and pushes the children; pushes and emissions are stream-compacted
-//              with wave ballots + popcount prefix sums.
+//              literal edge (perfect hash or 2-slot bucket), pushes the children and emits
+//              the found children's '#' and terminal filter ids (inline in the slot of an
+//              edgeless child, else a fids[] reference the scatter resolves: the walk never
+//              waits on an id); pushes and emissions are stream-compacted with wave ballots
+//              + popcount prefix sums.
 //              The stack is LIFO, which bounds it by ~64*K x levels whatever the frontier
 //              width.  No MFMA: this is pointer chasing.
-//     phase C  per-topic counts + a per-tile slab of (topic, fid reference) entries.
+//     phase C  per-topic counts + a per-tile slab of (topic, filter id or reference) entries.
 //   match_deep_kernel  topics that did not fit the fast path's LDS budget (very deep
 //              topics, or a frontier that overflowed the stack): one wavefront per topic,
 //              word ids and stack in global scratch.
-//   scan / scatter     counts -> CSR offsets; slab entries -> fids[ref] -> out_ids.
+//   scan / scatter     counts -> CSR offsets; slab entries (references resolved) -> out_ids.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -87,7 +88,7 @@ __device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
 }
 
 // One edge slot (wid, child_base, child meta, child literal filter) and its index, which
-// names the child's filter ids: fids[2 * idx] ('#') and fids[2 * idx + 1] (terminal).
+// names the child's filter ids fids[2 * idx + kind] (see EdgeSlot).
 struct Slot {
   uint4 a;
   uint32_t idx;
@@ -100,6 +101,21 @@ __device__ __forceinline__ Slot load_slot(const EdgeSlot* edges, uint32_t i) {
   return s;
 }
 
+// Slab / deep-slab entry: owner << 32 | value.  The value is a filter id, or — with
+// ENTRY_REF set — a fids[] reference the scatter kernels resolve.
+constexpr uint64_t ENTRY_REF = 1ull << 63;
+
+// Emission value of a found child's '#' (kind 0) or terminal (kind 1) filter: the id itself
+// when the child is edgeless (inline in the slot), else a reference.
+__device__ __forceinline__ uint64_t emit_value(const Slot& s, uint32_t kind) {
+  if (!(s.a.z & META_HAS_EDGES)) return kind ? s.a.w : s.a.y;
+  return ENTRY_REF | (2u * s.idx + kind);
+}
+
+__device__ __forceinline__ uint32_t resolve_entry(const TableView& tv, uint64_t e) {
+  return (e & ENTRY_REF) ? tv.fids[static_cast<uint32_t>(e)] : static_cast<uint32_t>(e);
+}
+
 __device__ __forceinline__ Slot empty_slot() {
   Slot s;
   s.a = make_uint4(WID_NONE, 0, 0, 0);
@@ -107,8 +123,6 @@ __device__ __forceinline__ Slot empty_slot() {
   return s;
 }
 
-__device__ __forceinline__ uint32_t hash_ref(const Slot& s) { return 2u * s.idx; }
-__device__ __forceinline__ uint32_t term_ref(const Slot& s) { return 2u * s.idx + 1u; }
 
 // Term-filter emission rule per mode (see include/emqx_match.h):
 //  ROUTES          every filter ending here (exact ∪ wildcard), emqx_router.erl:128-133
@@ -173,23 +187,30 @@ __device__ __forceinline__ bool probe_one(const EdgeSlot* edges, uint32_t base, 
 }
 
 // Byte-identical lookup of a wildcard "topic" for match_routes (emqx_router.erl:130):
-// walks literal/'+'/'#' edges; a final '#' is the node's hash filter.  Returns the filter's
-// fids[] reference or FID_NONE.
+// walks literal/'+'/'#' edges; a final '#' is the node's hash filter.  Returns the fid or
+// FID_NONE.
 template <class WidAt>
 __device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at) {
-  uint32_t base = tv.root_base, meta = tv.root_meta, href = tv.root_hash_ref, tref = FID_NONE;
+  uint32_t base = tv.root_base, meta = tv.root_meta, at = 0, term_inline = FID_NONE;
+  bool root = true;
   for (uint32_t k = 0; k < nlev; ++k) {
     const uint32_t w = wid_at(k);
-    if (w == WID_HASH && k + 1 == nlev) return (meta & META_HAS_HASH) ? href : FID_NONE;
+    if (w == WID_HASH && k + 1 == nlev) {
+      if (!(meta & META_HAS_HASH)) return FID_NONE;
+      if (root) return tv.root_hash_fid;
+      return (meta & META_HAS_EDGES) ? tv.fids[2u * at] : base;  // edgeless: inline in child_base
+    }
     if (w == WID_NONE || !(meta & META_HAS_EDGES)) return FID_NONE;
     Slot s;
     if (!probe_one(tv.edges, base, meta, w, &s)) return FID_NONE;
     base = s.a.y;
     meta = s.a.z;
-    href = hash_ref(s);
-    tref = term_ref(s);
+    term_inline = s.a.w;
+    at = s.idx;
+    root = false;
   }
-  return (meta & META_HAS_TERM) ? tref : FID_NONE;
+  if (root || !(meta & META_HAS_TERM)) return FID_NONE;
+  return (meta & META_HAS_EDGES) ? tv.fids[2u * at + 1u] : term_inline;
 }
 
 // Item (8 B):  x = edge-array base of the node
@@ -637,7 +658,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
         evals = 1;  // the root visit, F_0
         if (!dollar && (tv.root_meta & META_HAS_HASH)) {
           e0 = true;  // filter '#'
-          g0 = tv.root_hash_ref;
+          g0 = tv.root_hash_fid;
         }
         if (tv.root_meta & META_HAS_EDGES) {
           push = true;
@@ -775,21 +796,6 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
       pcount += (pL[k] ? 1u : 0u) + (pP[k] ? 1u : 0u);
     }
     {
-      uint32_t tot;
-      uint32_t pos = cursor + wave_prefix<ceil_log2(4 * K + 1)>(ecount, lane, &tot);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const uint64_t tag = static_cast<uint64_t>(tl[k]) << 32;
-        if (eLh[k]) { if (pos < cap) slab[pos] = tag | hash_ref(lit[k]); ++pos; }
-        if (eLt[k]) { if (pos < cap) slab[pos] = tag | term_ref(lit[k]); ++pos; }
-        if (ePh[k]) { if (pos < cap) slab[pos] = tag | hash_ref(pls[k]); ++pos; }
-        if (ePt[k]) { if (pos < cap) slab[pos] = tag | term_ref(pls[k]); ++pos; }
-        if (ce[k]) atomicAdd(&L.cnt[tl[k]], ce[k]);
-      }
-      cursor += tot;
-      if (DIAG) dg[7] += ecount;
-    }
-    {
       uint32_t ptot;
       uint32_t pos = top + wave_prefix<ceil_log2(2 * K + 1)>(pcount, lane, &ptot);
 #pragma unroll
@@ -799,6 +805,21 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
       }
       top += ptot;
       maxtop = max(maxtop, top + stop);
+    }
+    {
+      uint32_t tot;
+      uint32_t pos = cursor + wave_prefix<ceil_log2(4 * K + 1)>(ecount, lane, &tot);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint64_t tag = static_cast<uint64_t>(tl[k]) << 32;
+        if (eLh[k]) { if (pos < cap) slab[pos] = tag | emit_value(lit[k], 0); ++pos; }
+        if (eLt[k]) { if (pos < cap) slab[pos] = tag | emit_value(lit[k], 1); ++pos; }
+        if (ePh[k]) { if (pos < cap) slab[pos] = tag | emit_value(pls[k], 0); ++pos; }
+        if (ePt[k]) { if (pos < cap) slab[pos] = tag | emit_value(pls[k], 1); ++pos; }
+        if (ce[k]) atomicAdd(&L.cnt[tl[k]], ce[k]);
+      }
+      cursor += tot;
+      if (DIAG) dg[7] += ecount;
     }
     wave_sync();
   }
@@ -900,7 +921,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     dollar = __shfl(dollar, 0, 64);
     uint32_t count = 0, evals = 0;  // wave-uniform / per-lane
 
-    auto emit = [&](bool e0, uint32_t g0, bool e1, uint32_t g1, bool e2, uint32_t g2, bool e3, uint32_t g3) {
+    auto emit = [&](bool e0, uint64_t g0, bool e1, uint64_t g1, bool e2, uint64_t g2, bool e3, uint64_t g3) {
       const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u) + (e2 ? 1u : 0u) + (e3 ? 1u : 0u);
       uint32_t tot;
       const uint32_t rel = wave_prefix<3>(c, lane, &tot);
@@ -930,7 +951,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     } else {
       if (lane == 0) evals = 1;
       const bool eh = lane == 0 && !dollar && (tv.root_meta & META_HAS_HASH);
-      emit(eh, tv.root_hash_ref, false, 0, false, 0, false, 0);
+      emit(eh, tv.root_hash_fid, false, 0, false, 0, false, 0);
       if (tv.root_meta & META_HAS_EDGES) {
         const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
         if (lane == 0)
@@ -967,9 +988,10 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       probe_items<1>(tv.edges, qbase, qhp, qph, nL, w, nP, lit, fL, pls, fP, extra);
       evals += (fL[0] ? 1u : 0u) + (fP[0] ? 1u : 0u);
       const uint32_t m0 = lit[0].a.z, m1 = pls[0].a.z;
-      emit(fL[0] && (m0 & META_HAS_HASH), hash_ref(lit[0]), fL[0] && leaf && term_ok(m0, mode, droot),
-           term_ref(lit[0]), fP[0] && (m1 & META_HAS_HASH), hash_ref(pls[0]),
-           fP[0] && leaf && term_ok(m1, mode, false), term_ref(pls[0]));
+      const bool e0 = fL[0] && (m0 & META_HAS_HASH), e1 = fL[0] && leaf && term_ok(m0, mode, droot);
+      const bool e2 = fP[0] && (m1 & META_HAS_HASH), e3 = fP[0] && leaf && term_ok(m1, mode, false);
+      emit(e0, emit_value(lit[0], 0), e1, emit_value(lit[0], 1), e2, emit_value(pls[0], 0), e3,
+           emit_value(pls[0], 1));
       const bool p0 = fL[0] && !leaf && (m0 & META_HAS_EDGES);
       const bool p1 = fP[0] && !leaf && (m1 & META_HAS_EDGES);
       uint32_t ptot;
@@ -1091,10 +1113,10 @@ __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a, const ui
   const uint64_t* slab = a.slab + tile * a.slab_cap;
   for (uint32_t i = lane; i < fill; i += 64) {
     const uint64_t e = slab[i];
-    const uint32_t tl = static_cast<uint32_t>(e >> 32);
+    const uint32_t tl = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
     if ((dmask >> tl) & 1ull) continue;
     const uint32_t r = atomicAdd(&rank[wv][tl], 1u);
-    out_ids[offsets[t0 + tl] + r] = a.tv.fids[static_cast<uint32_t>(e)];
+    out_ids[offsets[t0 + tl] + r] = resolve_entry(a.tv, e);
   }
 }
 
@@ -1104,10 +1126,10 @@ __global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a, const ui
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < fill;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint64_t e = a.deep_slab[i];
-    const uint32_t j = static_cast<uint32_t>(e >> 32);
+    const uint32_t j = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
     const uint32_t t = a.deferred[j];
     const uint32_t r = atomicAdd(&deep_rank[j], 1u);
-    out_ids[offsets[t] + r] = a.tv.fids[static_cast<uint32_t>(e)];
+    out_ids[offsets[t] + r] = resolve_entry(a.tv, e);
   }
 }
 

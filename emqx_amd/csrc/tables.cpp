@@ -386,24 +386,25 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
   }
 
   // ---- pass 4: layout — line-packed preorder ----------------------------------------
-  // An L2 miss fetches a 128-B line (8 slots) while a probe uses one 16-B slot, so the
-  // layout packs walks into lines: when a node is visited, the arrays of all its children
-  // are placed right behind it, first-fit into the currently open line (an array of c <= 8
-  // slots is aligned to c, so it never straddles a line; larger arrays start on a line);
+  // An L2 miss fetches a 128-B line (8 slots) while a probe uses one, so the layout packs
+  // walks into lines: when a node is visited, the arrays of all its children are placed
+  // right behind it, first-fit into the currently open line (an array of c <= 8 slots is
+  // aligned to c, so it never straddles a line; larger arrays start on a line);
   // then the children are visited in order.  A chain of small nodes — the deep tail of
   // most filters — shares one line across several levels, so its walk misses once.
   std::vector<uint32_t> base(n_nodes, 0);
   uint64_t total_slots = 0;
   {
-    constexpr uint64_t LINE = 8;
-    uint64_t line = 0;  // open line (slot index, multiple of LINE)
-    uint32_t used = 0xFFu;  // its occupied slots (bit mask); all ones = no open line
+    constexpr uint64_t LINE = 128 / sizeof(EdgeSlot);
+    constexpr uint32_t FULL = (1u << LINE) - 1u;
+    uint64_t line = 0;       // open line (slot index, multiple of LINE)
+    uint32_t used = FULL;    // its occupied slots (bit mask); FULL = no open line
     auto place = [&](uint32_t caplg) -> uint64_t {
       const uint64_t c = 1ull << caplg;
       if (c >= LINE) {
         const uint64_t at = (total_slots + LINE - 1) & ~(LINE - 1);
         total_slots = at + c;
-        used = 0xFFu;
+        used = FULL;
         return at;
       }
       const uint32_t want = (1u << c) - 1u;
@@ -487,13 +488,14 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
 
   const uint64_t n_slots = std::max<uint64_t>(total_slots, 1);
   out.edges.assign(n_slots, EdgeSlot{WID_NONE, 0, 0, 0});
-  out.fids.assign(2 * n_slots + 1, FID_NONE);
+  out.fids.assign(2 * n_slots, FID_NONE);
   auto write_slot = [&](uint64_t at, uint32_t wid, uint32_t child) {
-    EdgeSlot& s = out.edges[at];
-    s.wid = wid;
-    s.child_base = base[child];
-    s.meta = meta_of(child) | (s.meta & META_BUCKET_OVF);
-    s.litf = lf[child];
+    EdgeSlot& r = out.edges[at];
+    r.wid = wid;
+    const bool leaf = n_edges[child] == 0;
+    r.child_base = leaf ? hash_fid[child] : base[child];
+    r.meta = meta_of(child) | (r.meta & META_BUCKET_OVF);
+    r.litf = leaf ? term_fid[child] : lf[child];
     out.fids[2 * at] = hash_fid[child];
     out.fids[2 * at + 1] = term_fid[child];
   };
@@ -524,8 +526,6 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     }
   }
   out.root_hash_fid = hash_fid[0];
-  out.root_hash_ref = static_cast<uint32_t>(2 * n_slots);
-  out.fids[2 * n_slots] = hash_fid[0];
   out.root_base = base[0];
   out.root_meta = meta_of(0);
   out.n_nodes = n_nodes;
@@ -607,14 +607,11 @@ bool check_tables(const HostTables& t, std::string* err) {
     const EdgeSlot& s = t.edges[i];
     if (s.wid == WID_NONE) continue;
     if ((t.fids[2 * i] != FID_NONE) != ((s.meta & META_HAS_HASH) != 0) ||
-        (t.fids[2 * i + 1] != FID_NONE) != ((s.meta & META_HAS_TERM) != 0)) {
+        (t.fids[2 * i + 1] != FID_NONE) != ((s.meta & META_HAS_TERM) != 0) ||
+        (!(s.meta & META_HAS_EDGES) && (s.child_base != t.fids[2 * i] || s.litf != t.fids[2 * i + 1]))) {
       if (err) *err = "filter ids disagree with the child's meta";
       return false;
     }
-  }
-  if (t.fids.size() != 2 * n + 1 || t.fids[t.root_hash_ref] != t.root_hash_fid) {
-    if (err) *err = "root '#' filter reference";
-    return false;
   }
   // literal filters: every literal child word of a node must pass the node's filter
   for (uint64_t i = 0; i < n; ++i) {

@@ -65,14 +65,13 @@ struct FilterStore {
 
 struct HostTables {
   std::vector<EdgeSlot> edges;
-  std::vector<uint32_t> fids;  // 2 * edges.size() + 1 (see EdgeSlot)
+  std::vector<uint32_t> fids;  // 2 * edges.size() (see EdgeSlot)
   std::vector<VocabSlot> vocab;
   std::vector<uint8_t> arena;
   uint32_t vocab_mask = 0;
   uint32_t root_base = 0;
   uint32_t root_meta = 0;
   uint32_t root_hash_fid = FID_NONE;
-  uint32_t root_hash_ref = 0;
   uint64_t n_nodes = 0;
   uint64_t n_words = 0;
   uint32_t max_depth = 0;
