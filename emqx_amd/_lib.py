@@ -31,7 +31,7 @@ EXPORTS = (
     "emqx_engine_create", "emqx_engine_destroy", "emqx_insert_filters", "emqx_insert_filters_ext",
     "emqx_delete_filters",
     "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
-    "emqx_match_batch_device", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
+    "emqx_match_batch_device", "emqx_match_batch_device_async", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
     "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_batcher_create",
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
@@ -95,6 +95,7 @@ def lib():
         "emqx_commit": (i32, [vp]),
         "emqx_match_batch": (i32, [vp, u32, vp, vp, u64, vp, vp, u64, ctypes.POINTER(u64)]),
         "emqx_match_batch_device": (i32, [vp, u32, vp, vp, u64, vp, vp, u64, ctypes.POINTER(u64), vp]),
+        "emqx_match_batch_device_async": (i32, [vp, u32, vp, vp, u64, vp, vp, u64, vp, vp]),
         "emqx_stats_get": (i32, [vp, ctypes.POINTER(Stats)]),
         "emqx_topic_match": (i32, [vp, u64, vp, u64]),
         "emqx_topic_wildcard": (i32, [vp, u64]),

@@ -58,6 +58,7 @@ struct Snapshot {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();  // an async call may still read this snapshot
     dfree(edges);
     dfree(fids);
     dfree(vocab);
@@ -72,7 +73,7 @@ struct Workspace {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evk = nullptr;
-  uint64_t cap_n = 0, cap_tiles = 0, cap_partials = 0, cap_slab = 0;
+  uint64_t cap_n = 0, cap_tiles = 0, cap_slab = 0;
   uint32_t slab_per_tile = 256;
   uint32_t* counts = nullptr;
   uint32_t* deferred = nullptr;
@@ -84,15 +85,16 @@ struct Workspace {
   uint2* spill = nullptr;
   uint64_t* diag = nullptr;
   uint32_t spill_cap = 2048;  // items per tile
-  uint64_t* partials = nullptr;
-  uint32_t* ctrl = nullptr;         // CTRL_WORDS u32 + 2 u64 (evals) -> 8 u32 words + 2 u64
-  uint64_t* evals = nullptr;        // [0] total evals (device reduction)
+  uint32_t* ctrl = nullptr;         // [16]: CTRL_* words, then deep_evals (one memset per call)
+  uint64_t* tile_sum = nullptr;
+  uint64_t* tile_off = nullptr;
+  hipEvent_t done = nullptr;        // end of the last call enqueued with this workspace
+  std::shared_ptr<Snapshot> inflight;  // table of the last async call (kept alive for it)
   uint32_t* deep_wids = nullptr;
   uint4* deep_stack = nullptr;
   uint32_t deep_stack_cap = 1u << 16;
   uint64_t* deep_slab = nullptr;
   uint32_t deep_slab_cap = 1u << 20;
-  uint32_t* deep_evals = nullptr;
   // host-API staging
   uint8_t* d_tbytes = nullptr;
   uint64_t cap_tbytes = 0;
@@ -102,19 +104,20 @@ struct Workspace {
   uint64_t cap_out_off = 0;
   uint32_t* d_out_ids = nullptr;
   uint64_t cap_out_ids = 0;
-  uint64_t* h_rb = nullptr;         // pinned readback: [0..3] ctrl (as u64), [4] total, [5] evals
+  uint64_t* h_rb = nullptr;         // pinned call summary (SUM_WORDS), written by tile_scan_kernel
   bool deep_ready = false;
 
   ~Workspace() {
     (void)hipSetDevice(device);
     dfree(counts); dfree(deferred); dfree(deep_rank); dfree(slab); dfree(tile_fill);
-    dfree(tile_defer); dfree(tile_stats); dfree(spill); dfree(diag); dfree(partials); dfree(ctrl); dfree(evals);
-    dfree(deep_wids); dfree(deep_stack); dfree(deep_slab); dfree(deep_evals);
+    dfree(tile_defer); dfree(tile_stats); dfree(spill); dfree(diag); dfree(ctrl); dfree(tile_sum);
+    dfree(tile_off); dfree(deep_wids); dfree(deep_stack); dfree(deep_slab);
     dfree(d_tbytes); dfree(d_toffs); dfree(d_out_off); dfree(d_out_ids);
     if (h_rb) (void)hipHostFree(h_rb);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (evk) (void)hipEventDestroy(evk);
+    if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -221,9 +224,9 @@ int ensure_ws(Workspace* w, uint64_t n) {
     HIP_TRY(hipEventCreate(&w->ev0));
     HIP_TRY(hipEventCreate(&w->ev1));
     HIP_TRY(hipEventCreate(&w->evk));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_rb), 16 * sizeof(uint64_t), hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_rb), SUM_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     HIP_TRY(dalloc(w->ctrl, 16));
-    HIP_TRY(dalloc(w->evals, 2));
     HIP_TRY(dalloc(w->diag, DIAG_WORDS));
     HIP_TRY(hipMemset(w->diag, 0, DIAG_WORDS * sizeof(uint64_t)));
   }
@@ -231,7 +234,6 @@ int ensure_ws(Workspace* w, uint64_t n) {
     HIP_TRY(dalloc(w->deep_wids, uint64_t(DEEP_WAVES) * DEEP_MAX_LEVELS));
     HIP_TRY(dalloc(w->deep_stack, uint64_t(DEEP_WAVES) * w->deep_stack_cap));
     HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
-    HIP_TRY(dalloc(w->deep_evals, 4));
     w->deep_ready = true;
   }
   if (n > w->cap_n) {
@@ -247,6 +249,8 @@ int ensure_ws(Workspace* w, uint64_t n) {
     HIP_TRY(dalloc(w->tile_fill, cap));
     HIP_TRY(dalloc(w->tile_defer, cap));
     HIP_TRY(dalloc(w->tile_stats, cap));
+    HIP_TRY(dalloc(w->tile_sum, cap));
+    HIP_TRY(dalloc(w->tile_off, cap));
     HIP_TRY(dalloc(w->spill, cap * w->spill_cap));
     w->cap_tiles = cap;
   }
@@ -256,37 +260,7 @@ int ensure_ws(Workspace* w, uint64_t n) {
     HIP_TRY(dalloc(w->slab, cap));
     w->cap_slab = cap;
   }
-  const uint64_t np = scan_partials(n);
-  if (np > w->cap_partials) {
-    const uint64_t cap = round_pow2(std::max<uint64_t>(np, 64));
-    HIP_TRY(dalloc(w->partials, cap));
-    w->cap_partials = cap;
-  }
   return EMQX_OK;
-}
-
-// Sums per-tile node visits (+ the deep path's) into out[0] and takes the max stack depth
-// into out[1].
-__global__ void reduce_stats_kernel(const uint2* tile_stats, uint64_t ntiles, const uint32_t* deep_evals,
-                                    uint64_t* out) {
-  uint64_t s = 0;
-  uint32_t m = 0;
-  for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < ntiles; i += uint64_t(gridDim.x) * blockDim.x) {
-    const uint2 v = tile_stats[i];
-    s += v.x;
-    m = max(m, v.y);
-  }
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(s), d, 64);
-    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(s >> 32), d, 64);
-    s += (uint64_t(hi) << 32) | lo;
-    m = max(m, static_cast<uint32_t>(__shfl_xor(m, d, 64)));
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (s) atomicAdd(reinterpret_cast<unsigned long long*>(out), static_cast<unsigned long long>(s));
-    if (m) atomicMax(reinterpret_cast<unsigned long long*>(out + 1), static_cast<unsigned long long>(m));
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out), static_cast<unsigned long long>(*deep_evals));
 }
 
 // Fast-kernel variant: EMQX_FAST_VARIANT overrides (A/B runs); otherwise deep tables get
@@ -302,99 +276,100 @@ FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
   return snap.max_depth > 12 ? FAST_K2_S2K : FAST_K1_S384;
 }
 
-// The pipeline on device buffers.  All inputs/outputs are device pointers.
+// Enqueue one match call on stream s (no host synchronisation): memset of the control
+// words, fast kernel, deep kernel, tile scan (+ summary into `summary`), scatter.  A call on
+// a workspace last used from another stream first waits for that call to drain.
+int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode, const uint8_t* d_tbytes,
+                  const uint64_t* d_toffs, uint64_t n, uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap,
+                  uint64_t* summary, hipStream_t s) {
+  int rc = ensure_ws(w, n);
+  if (rc != EMQX_OK) return rc;
+  MatchArgs a{};
+  a.tv = snap.tv;
+  a.tbytes = d_tbytes;
+  a.toffs = d_toffs;
+  a.n = n;
+  a.mode = mode;
+  a.slab_cap = w->slab_per_tile;
+  a.counts = w->counts;
+  a.slab = w->slab;
+  a.tile_fill = w->tile_fill;
+  a.tile_defer = w->tile_defer;
+  a.tile_stats = w->tile_stats;
+  a.spill = w->spill;
+  a.diag = e->diag_on.load() ? w->diag : nullptr;
+  a.spill_cap = w->spill_cap;
+  a.ctrl = w->ctrl;
+  a.deferred = w->deferred;
+  a.deep_wids = w->deep_wids;
+  a.deep_stack = w->deep_stack;
+  a.deep_stack_cap = w->deep_stack_cap;
+  a.deep_waves = DEEP_WAVES;
+  a.deep_slab = w->deep_slab;
+  a.deep_slab_cap = w->deep_slab_cap;
+  a.deep_evals = w->ctrl + 8;
+  a.tile_sum = w->tile_sum;
+  a.tile_off = w->tile_off;
+  a.deep_rank = w->deep_rank;
+  a.out_off = d_out_off;
+  a.out_ids = d_out_ids;
+  a.out_cap = d_out_ids ? cap : 0;
+  a.summary = summary;
+
+  HIP_TRY(hipStreamWaitEvent(s, w->done, 0));
+  HIP_TRY(hipMemsetAsync(w->ctrl, 0, 16 * sizeof(uint32_t), s));
+  HIP_TRY(hipEventRecord(w->ev0, s));
+  HIP_TRY(launch_match_fast(a, pick_variant(e, snap), s));
+  HIP_TRY(hipEventRecord(w->evk, s));
+  HIP_TRY(launch_match_deep(a, s));
+  HIP_TRY(launch_assemble(a, s));
+  HIP_TRY(hipEventRecord(w->ev1, s));
+  HIP_TRY(hipEventRecord(w->done, s));
+  return EMQX_OK;
+}
+
+// The pipeline on device buffers, synchronous: enqueue, drain, read the summary, rerun with
+// larger scratch areas if one overflowed (learnt once per workspace).
 int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode, const uint8_t* d_tbytes,
               const uint64_t* d_toffs, uint64_t n, uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap,
               uint64_t* n_out, hipStream_t s) {
+  uint64_t* sum_dev = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&sum_dev), w->h_rb, 0));
   for (int attempt = 0; attempt < 8; ++attempt) {
-    int rc = ensure_ws(w, n);
+    int rc = enqueue_match(e, snap, w, mode, d_tbytes, d_toffs, n, d_out_off, d_out_ids, cap, sum_dev, s);
     if (rc != EMQX_OK) return rc;
-    MatchArgs a{};
-    a.tv = snap.tv;
-    a.tbytes = d_tbytes;
-    a.toffs = d_toffs;
-    a.n = n;
-    a.mode = mode;
-    a.slab_cap = w->slab_per_tile;
-    a.counts = w->counts;
-    a.slab = w->slab;
-    a.tile_fill = w->tile_fill;
-    a.tile_defer = w->tile_defer;
-    a.tile_stats = w->tile_stats;
-    a.spill = w->spill;
-    a.diag = e->diag_on.load() ? w->diag : nullptr;
-    a.spill_cap = w->spill_cap;
-    a.ctrl = w->ctrl;
-    a.deferred = w->deferred;
-    a.deep_wids = w->deep_wids;
-    a.deep_stack = w->deep_stack;
-    a.deep_stack_cap = w->deep_stack_cap;
-    a.deep_waves = DEEP_WAVES;
-    a.deep_slab = w->deep_slab;
-    a.deep_slab_cap = w->deep_slab_cap;
-    a.deep_evals = w->deep_evals;
-
-    HIP_TRY(hipMemsetAsync(w->ctrl, 0, 16 * sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(w->evals, 0, 2 * sizeof(uint64_t), s));
-    HIP_TRY(hipMemsetAsync(w->deep_evals, 0, 4 * sizeof(uint32_t), s));
-    HIP_TRY(hipEventRecord(w->ev0, s));
-    const FastVariant v = pick_variant(e, snap);
-    HIP_TRY(launch_match_fast(a, v, s));
-    HIP_TRY(hipEventRecord(w->evk, s));
-    HIP_TRY(launch_match_deep(a, s));
-    HIP_TRY(launch_scan(w->counts, n, d_out_off, w->partials, s));
-    const uint64_t ntiles = (n + TILE_TOPICS - 1) / TILE_TOPICS;
-    hipLaunchKernelGGL(reduce_stats_kernel, dim3(64), dim3(256), 0, s, w->tile_stats, ntiles, w->deep_evals, w->evals);
-    HIP_TRY(hipGetLastError());
-    // one small readback: ctrl words, total, evals
-    HIP_TRY(hipMemcpyAsync(w->h_rb, w->ctrl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(w->h_rb + 4, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(w->h_rb + 5, w->evals, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(w->h_rb);
-    const uint32_t ndef = c32[CTRL_DEFERRED], need_slab = c32[CTRL_NEED_SLAB], err = c32[CTRL_ERROR];
-    const uint32_t deep_fill = c32[CTRL_DEEP_FILL];
-    if (err & CTRL_ERR_TOO_LONG) {
+    const uint64_t* sm = w->h_rb;
+    const uint64_t flags = sm[SUM_FLAGS];
+    const uint32_t err = static_cast<uint32_t>(sm[SUM_ERROR]);
+    if (flags & SUM_F_ERROR) {
       set_last_error("topic longer than 65535 bytes on the deep path");
       return EMQX_EINVAL;
     }
-    bool retry = false;
-    if (need_slab > w->slab_per_tile) {
-      w->slab_per_tile = static_cast<uint32_t>(round_pow2(need_slab));
-      retry = true;
-    }
-    if (err & CTRL_ERR_DEEP_SLAB) {
-      w->deep_slab_cap = static_cast<uint32_t>(std::min<uint64_t>(round_pow2(uint64_t(deep_fill) + 1), 1u << 30));
-      HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
-      retry = true;
-    }
-    if (err & CTRL_ERR_TOO_DEEP) {
-      if (w->deep_stack_cap >= (1u << 22)) {
-        set_last_error("topic frontier exceeds the deep path's stack");
-        return EMQX_ETOODEEP;
+    if (flags & SUM_F_RETRY) {
+      if (sm[SUM_NEED_SLAB] > w->slab_per_tile) w->slab_per_tile = static_cast<uint32_t>(round_pow2(sm[SUM_NEED_SLAB]));
+      if (err & CTRL_ERR_DEEP_SLAB) {
+        w->deep_slab_cap = static_cast<uint32_t>(std::min<uint64_t>(round_pow2(sm[SUM_DEEP_FILL] + 1), 1u << 30));
+        HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
       }
-      w->deep_stack_cap <<= 2;
-      HIP_TRY(dalloc(w->deep_stack, uint64_t(DEEP_WAVES) * w->deep_stack_cap));
-      retry = true;
+      if (err & CTRL_ERR_TOO_DEEP) {
+        if (w->deep_stack_cap >= (1u << 22)) {
+          set_last_error("topic frontier exceeds the deep path's stack");
+          return EMQX_ETOODEEP;
+        }
+        w->deep_stack_cap <<= 2;
+        HIP_TRY(dalloc(w->deep_stack, uint64_t(DEEP_WAVES) * w->deep_stack_cap));
+      }
+      continue;
     }
-    if (retry) continue;
-    {
-      float kms = 0;
-      if (hipEventElapsedTime(&kms, w->ev0, w->evk) == hipSuccess) e->last_kernel_ms.store(kms);
-    }
-    e->last_deferred.store(ndef);
-    e->last_evals.store(w->h_rb[5]);
-    e->last_max_stack.store(w->h_rb[6]);
-    float ms = 0;
-    (void)hipEventRecord(w->ev1, s);
-    const uint64_t total = w->h_rb[4];
-    *n_out = total;
-    if (total > cap) return EMQX_EOVERFLOW;
-    HIP_TRY(launch_scatter(a, d_out_off, d_out_ids, w->deep_rank, s));
-    HIP_TRY(hipEventRecord(w->ev1, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    float kms = 0, ms = 0;
+    if (hipEventElapsedTime(&kms, w->ev0, w->evk) == hipSuccess) e->last_kernel_ms.store(kms);
     if (hipEventElapsedTime(&ms, w->ev0, w->ev1) == hipSuccess) e->last_match_ms.store(ms);
-    return EMQX_OK;
+    e->last_deferred.store(sm[SUM_DEFERRED]);
+    e->last_evals.store(sm[SUM_EVALS]);
+    e->last_max_stack.store(sm[SUM_MAXSTACK]);
+    *n_out = sm[SUM_TOTAL];
+    return (flags & SUM_F_OVERFLOW) ? EMQX_EOVERFLOW : EMQX_OK;
   }
   set_last_error("match did not converge");
   return EMQX_EDEVICE;
@@ -528,6 +503,26 @@ int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topi
   if (rc == EMQX_OK) {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
     rc = run_match(e, *snap, w, mode, d_topic_bytes, d_topic_offsets, n, d_out_offsets, d_out_ids, cap, n_out, s);
+  }
+  release_ws(e, w);
+  return rc;
+}
+
+int emqx_match_batch_device_async(emqx_engine* e, uint32_t mode, const uint8_t* d_topic_bytes,
+                                  const uint64_t* d_topic_offsets, uint64_t n, uint64_t* d_out_offsets,
+                                  uint32_t* d_out_ids, uint64_t cap, uint64_t* summary, void* stream) {
+  if (!e || !summary || mode > EMQX_MODE_TRIE_WILDCARD) return EMQX_EINVAL;
+  if (n && (!d_topic_bytes || !d_topic_offsets)) return EMQX_EINVAL;
+  if (!d_out_offsets) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  auto snap = current(e);
+  Workspace* w = acquire_ws(e);
+  int rc = ensure_ws(w, n);
+  if (rc == EMQX_OK) {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
+    rc = enqueue_match(e, *snap, w, mode, d_topic_bytes, d_topic_offsets, n, d_out_offsets, d_out_ids, cap,
+                       summary, s);
+    w->inflight = snap;  // released when the workspace is next used (its stream has moved on)
   }
   release_ws(e, w);
   return rc;

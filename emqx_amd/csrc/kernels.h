@@ -44,6 +44,23 @@ enum Diag : uint32_t {
 };        // topics per wave (one per lane during tokenizing)
 constexpr uint32_t DEEP_MAX_LEVELS = 65536;
 
+// Call summary written by tile_scan_kernel (u64 words), read by the host after the stream
+// drains (sync calls) or by the caller of the async entry point.
+enum Summary : uint32_t {
+  SUM_FLAGS = 0,      // SUM_F_* bits; 0 = the call's output is complete
+  SUM_TOTAL = 1,      // matched filter ids over the batch (= out_offsets[n])
+  SUM_EVALS = 2,      // node visits (fast + deep path)
+  SUM_MAXSTACK = 3,   // max frontier stack depth of any tile
+  SUM_DEFERRED = 4,   // topics handed to the deep path
+  SUM_NEED_SLAB = 5,  // max slab entries any tile needed
+  SUM_DEEP_FILL = 6,  // deep-path slab entries
+  SUM_ERROR = 7,      // CTRL_ERR_* bits
+  SUM_WORDS = 8
+};
+constexpr uint64_t SUM_F_RETRY = 1;     // a scratch area overflowed: rerun with larger buffers
+constexpr uint64_t SUM_F_OVERFLOW = 2;  // total > out_cap: out_ids truncated
+constexpr uint64_t SUM_F_ERROR = 4;     // a topic the engine cannot match (see SUM_ERROR)
+
 struct MatchArgs {
   TableView tv;
   const uint8_t* tbytes;
@@ -69,6 +86,14 @@ struct MatchArgs {
   uint64_t* deep_slab;     // [deep_slab_cap]  (deferred_slot << 32) | fid
   uint32_t deep_slab_cap;
   uint32_t* deep_evals;    // [1] (atomic)
+  // output assembly
+  uint64_t* tile_sum;      // [ntiles] filter ids per tile (fast path + deep path's atomics)
+  uint64_t* tile_off;      // [ntiles] exclusive scan of tile_sum
+  uint32_t* deep_rank;     // [n] per deferred slot: ids placed so far
+  uint64_t* out_off;       // [n + 1] CSR offsets (caller's)
+  uint32_t* out_ids;       // [out_cap] CSR ids (caller's)
+  uint64_t out_cap;
+  uint64_t* summary;       // [SUM_WORDS] (device or host-pinned memory)
 };
 
 // Fast-kernel variants: K items per lane per step, LDS stack / word-id capacity per wave.
@@ -87,11 +112,12 @@ enum FastVariant {
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);
 hipError_t launch_match_deep(const MatchArgs& a, hipStream_t s);
-// counts[n] -> offsets[n+1] (exclusive); partials: scratch of >= scan_partials(n) u64.
+// tile scan -> out_off[n] and the summary; then per-tile offsets + ids (fast, then deep)
+hipError_t launch_assemble(const MatchArgs& a, hipStream_t s);
+// counts[n] -> offsets[n+1] (exclusive); partials: scratch of >= scan_partials(n) u64
+// (fan-out's entry scan).
 uint64_t scan_partials(uint64_t n);
 hipError_t launch_scan(const uint32_t* counts, uint64_t n, uint64_t* offsets, uint64_t* partials,
                        hipStream_t s);
-hipError_t launch_scatter(const MatchArgs& a, const uint64_t* offsets, uint32_t* out_ids,
-                          uint32_t* deep_rank, hipStream_t s);
 
 }  // namespace emqx

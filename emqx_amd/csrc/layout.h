@@ -42,6 +42,11 @@ constexpr uint32_t META_LITF_EXACT = 1u << 11;  // litf = the child's only liter
 constexpr uint32_t META_LITF_NONE = 1u << 12;   // the child has no literal edge at all
 constexpr uint32_t META_BUCKET_OVF = 1u << 13;  // (slot position, wide nodes) first slot of a 2-slot
                                                 // bucket some word of which lives in its secondary bucket
+constexpr uint32_t META_XFID = 1u << 14;        // litf holds the child's one filter id; the literal
+                                                // filter shrinks to 8 bits in meta[31:24]
+constexpr uint32_t META_XFID_TERM = 1u << 15;   // ... which is its terminal filter (else its '#' filter)
+constexpr uint32_t META_F8_SHIFT = 24;          // XFID: fingerprint of the only literal (LITF_EXACT)
+                                                // or an 8-bit Bloom mask of the literals
 constexpr uint32_t META_SEED_SHIFT = 16;        // 8-bit perfect-hash seed
 constexpr uint32_t PH_MAX_CAPLOG = 15;
 
@@ -53,10 +58,13 @@ constexpr uint32_t PH_MAX_CAPLOG = 15;
 // load per lookup, hit or miss), or — in wide nodes, where no seed fits — hashed into 2-slot
 // buckets (two loads per lookup, two more for ~1% of words).
 // The filter ids of the child behind slot i live apart, in `fids[2i]` ("<child>/#") and
-// `fids[2i + 1]` ("<child>"), except for a child without edges (no META_HAS_EDGES: it is
-// never pushed), which carries them in place of child_base and litf — the common leaf
-// emission needs no second load.  For the others the walk emits the reference 2i + kind
-// and the scatter kernel resolves it, so a probe moves 16 B and the walk never waits on an id.
+// `fids[2i + 1]` ("<child>"), except
+//   * for a child without edges (no META_HAS_EDGES: it is never pushed), which carries them
+//     in place of child_base and litf — the common leaf emission needs no second load;
+//   * for a child with edges and one filter id (META_XFID), which carries it in litf; its
+//     literal filter shrinks to an 8-bit fingerprint / Bloom mask in the meta's top byte.
+// For the others the walk emits the reference 2i + kind and the scatter kernel resolves it,
+// so a probe moves 16 B and the walk never waits on an id.
 struct alignas(16) EdgeSlot {
   uint32_t wid;         // key (WID_NONE = empty)
   uint32_t child_base;  // first slot of the child's edge array  | edgeless child: hash_fid
@@ -150,6 +158,11 @@ EMQX_HD uint32_t litf_hash(uint32_t wid) { return mix32(wid ^ 0xA5A5A5A5u); }
 // May the child (meta, litf) have a literal edge for `wid`?  No false negatives.
 EMQX_HD bool litf_may_contain(uint32_t meta, uint32_t litf, uint32_t wid) {
   if (meta & META_LITF_NONE) return false;
+  if (meta & META_XFID) {
+    const uint32_t f8 = meta >> META_F8_SHIFT, h = litf_hash(wid);
+    if (meta & META_LITF_EXACT) return (h >> 24) == f8;
+    return ((f8 >> (h & 7u)) & 1u) != 0;
+  }
   if (meta & META_LITF_EXACT) return litf == wid;
   const uint32_t h = litf_hash(wid);
   return ((litf >> (h & 31u)) & (litf >> ((h >> 5) & 31u)) & 1u) != 0;

@@ -70,6 +70,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
   return v;
 }
 
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t lo = __shfl_up(static_cast<uint32_t>(v), d, 64);
+    const uint32_t hi = __shfl_up(static_cast<uint32_t>(v >> 32), d, 64);
+    if (lane >= d) v += (static_cast<uint64_t>(hi) << 32) | lo;
+  }
+  return v;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -106,9 +116,10 @@ __device__ __forceinline__ Slot load_slot(const EdgeSlot* edges, uint32_t i) {
 constexpr uint64_t ENTRY_REF = 1ull << 63;
 
 // Emission value of a found child's '#' (kind 0) or terminal (kind 1) filter: the id itself
-// when the child is edgeless (inline in the slot), else a reference.
+// when the slot carries it (edgeless child, or META_XFID), else a reference.
 __device__ __forceinline__ uint64_t emit_value(const Slot& s, uint32_t kind) {
   if (!(s.a.z & META_HAS_EDGES)) return kind ? s.a.w : s.a.y;
+  if (s.a.z & META_XFID) return s.a.w;  // the child's only filter id: the one asked for
   return ENTRY_REF | (2u * s.idx + kind);
 }
 
@@ -839,9 +850,12 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
       if (lane == 0 && v) atomicAdd(reinterpret_cast<unsigned long long*>(a.diag + i), static_cast<unsigned long long>(v));
     }
   }
-  if (valid) a.counts[t] = ((defer_mask >> lane) & 1ull) ? 0u : L.cnt[lane];
+  const uint32_t mine = (valid && !((defer_mask >> lane) & 1ull)) ? L.cnt[lane] : 0u;
+  if (valid) a.counts[t] = mine;
   const uint32_t ev = wave_sum(evals);
+  const uint32_t tsum = wave_sum(mine);
   if (lane == 0) {
+    a.tile_sum[tile] = tsum;  // the deep path adds its topics' counts
     a.tile_fill[tile] = cursor;
     a.tile_defer[tile] = defer_mask;
     a.tile_stats[tile] = make_uint2(ev, maxtop);
@@ -872,6 +886,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
 
   for (uint32_t j = gw; j < ndef; j += a.deep_waves) {
     const uint32_t t = a.deferred[j];
+    if (lane == 0) a.deep_rank[j] = 0;
     const uint64_t start = a.toffs[t], end = a.toffs[t + 1];
     if (end - start > 65535u) {
       if (lane == 0) {
@@ -1004,6 +1019,8 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     const uint32_t ev = wave_sum(evals);
     if (lane == 0) {
       a.counts[t] = count;
+      if (count) atomicAdd(reinterpret_cast<unsigned long long*>(a.tile_sum + t / TILE_TOPICS),
+                           static_cast<unsigned long long>(count));
       atomicAdd(&a.deep_evals[0], ev);
     }
   }
@@ -1016,16 +1033,6 @@ namespace {
 constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
-
-__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, uint32_t lane) {
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t lo = __shfl_up(static_cast<uint32_t>(v), d, 64);
-    const uint32_t hi = __shfl_up(static_cast<uint32_t>(v >> 32), d, 64);
-    if (lane >= d) v += (static_cast<uint64_t>(hi) << 32) | lo;
-  }
-  return v;
-}
 
 // Block-wide exclusive scan of one u64 per thread (SCAN_THREADS threads).
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* total) {
@@ -1096,46 +1103,149 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_final_kernel(const uint32_t
 }
 
 // ------------------------------------------------------------------------------------
-// Scatter: slab entries -> CSR out_ids
+// Output assembly: tile scan -> per-tile offsets; scatter: slab entries -> CSR out_ids
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a, const uint64_t* offsets,
-                                                           uint32_t* out_ids) {
-  __shared__ uint32_t rank[4][64];
+constexpr int TSCAN_THREADS = 1024;
+
+// One block: exclusive scan of tile_sum -> tile_off, out_off[n] = total, and the call
+// summary (ctrl words are final: the fast and deep kernels have drained).  Each thread owns a
+// run of consecutive tiles: sum it, one block scan of the run totals, then write the run.
+__global__ __launch_bounds__(TSCAN_THREADS) void tile_scan_kernel(MatchArgs a, uint64_t ntiles) {
+  __shared__ uint64_t wsum[TSCAN_THREADS / 64];
+  __shared__ uint32_t wmax[TSCAN_THREADS / 64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t per = (ntiles + TSCAN_THREADS - 1) / TSCAN_THREADS;
+  const uint64_t b = min<uint64_t>(per * threadIdx.x, ntiles), e = min<uint64_t>(b + per, ntiles);
+  constexpr uint32_t R = 16;  // loads in flight per thread (one block: latency is the cost)
+  uint64_t mine = 0, evals = 0;
+  uint32_t maxtop = 0;
+  for (uint64_t c0 = b; c0 < e; c0 += R) {
+    uint64_t v[R];
+    uint2 st[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      v[k] = c0 + k < e ? a.tile_sum[c0 + k] : 0;
+      st[k] = c0 + k < e ? a.tile_stats[c0 + k] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      mine += v[k];
+      evals += st[k].x;
+      maxtop = max(maxtop, st[k].y);
+    }
+  }
+  const uint64_t incl = wave_incl_scan64(mine, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint64_t carry = incl - mine, all = 0;
+  for (uint32_t k = 0; k < TSCAN_THREADS / 64; ++k) {
+    carry += k < w ? wsum[k] : 0;
+    all += wsum[k];
+  }
+  for (uint64_t c0 = b; c0 < e; c0 += R) {
+    uint64_t v[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) v[k] = c0 + k < e ? a.tile_sum[c0 + k] : 0;
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      if (c0 + k < e) a.tile_off[c0 + k] = carry;
+      carry += v[k];
+    }
+  }
+  carry = all;
+  __syncthreads();
+  // evals / max stack: block reductions
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    evals += (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(evals >> 32), d, 64)) << 32) |
+             __shfl_xor(static_cast<uint32_t>(evals), d, 64);
+    maxtop = max(maxtop, static_cast<uint32_t>(__shfl_xor(maxtop, d, 64)));
+  }
+  if (lane == 0) {
+    wsum[w] = evals;
+    wmax[w] = maxtop;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < TSCAN_THREADS / 64; ++k) {
+      evals += wsum[k];
+      maxtop = max(maxtop, wmax[k]);
+    }
+    const uint32_t ndef = a.ctrl[CTRL_DEFERRED], need = a.ctrl[CTRL_NEED_SLAB], err = a.ctrl[CTRL_ERROR];
+    const uint32_t fill = a.ctrl[CTRL_DEEP_FILL];
+    uint64_t flags = 0;
+    if (need > a.slab_cap || (err & (CTRL_ERR_DEEP_SLAB | CTRL_ERR_TOO_DEEP))) flags |= SUM_F_RETRY;
+    if (carry > a.out_cap) flags |= SUM_F_OVERFLOW;
+    if (err & CTRL_ERR_TOO_LONG) flags |= SUM_F_ERROR;
+    a.out_off[a.n] = carry;
+    uint64_t* sm = a.summary;
+    sm[SUM_TOTAL] = carry;
+    sm[SUM_EVALS] = evals + *a.deep_evals;
+    sm[SUM_MAXSTACK] = maxtop;
+    sm[SUM_DEFERRED] = ndef;
+    sm[SUM_NEED_SLAB] = need;
+    sm[SUM_DEEP_FILL] = fill;
+    sm[SUM_ERROR] = err;
+    sm[SUM_FLAGS] = flags;
+    __threadfence_system();
+  }
+}
+
+// One wave per tile: the tile's CSR offsets (wave scan of its 64 counts on top of the tile
+// offset), then its slab entries, 64 at a time: lanes holding the same topic find each other
+// with six ballots (one per bit of the topic index), take ranks by popcount and the group's
+// first lane advances the topic's running count — no atomics.  Ids beyond out_cap are
+// dropped (the summary reports the overflow).
+__global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
+  __shared__ uint32_t run[4][64];
+  __shared__ uint64_t base[4][64];
   const uint32_t lane = lane_id();
   const uint32_t wv = threadIdx.x >> 6;
   const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4 + wv;
   const uint64_t t0 = tile * TILE_TOPICS;
   if (t0 >= a.n) return;
-  rank[wv][lane] = 0;
+  const uint64_t t = t0 + lane;
+  const uint64_t c = t < a.n ? a.counts[t] : 0;
+  const uint64_t off = a.tile_off[tile] + wave_incl_scan64(c, lane) - c;
+  if (t < a.n) a.out_off[t] = off;
+  base[wv][lane] = off;
+  run[wv][lane] = 0;
   wave_sync();
   const uint32_t fill = min(a.tile_fill[tile], a.slab_cap);
   const uint64_t dmask = a.tile_defer[tile];
   const uint64_t* slab = a.slab + tile * a.slab_cap;
-  for (uint32_t i = lane; i < fill; i += 64) {
-    const uint64_t e = slab[i];
-    const uint32_t tl = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
-    if ((dmask >> tl) & 1ull) continue;
-    const uint32_t r = atomicAdd(&rank[wv][tl], 1u);
-    out_ids[offsets[t0 + tl] + r] = resolve_entry(a.tv, e);
+  const uint64_t lt = lanemask_lt(lane);
+  for (uint32_t i0 = 0; i0 < fill; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint64_t e = i < fill ? slab[i] : 0;
+    const uint32_t tl = static_cast<uint32_t>(e >> 32) & 63u;
+    const bool keep = i < fill && !((dmask >> tl) & 1ull);
+    uint64_t peers = __ballot(keep);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 6; ++bit) {
+      const uint64_t m = __ballot(keep && ((tl >> bit) & 1u));
+      peers &= ((tl >> bit) & 1u) ? m : ~m;
+    }
+    const uint32_t rk = static_cast<uint32_t>(__popcll(peers & lt));
+    if (keep) {
+      const uint64_t p = base[wv][tl] + run[wv][tl] + rk;
+      if (p < a.out_cap) a.out_ids[p] = resolve_entry(a.tv, e);
+    }
+    wave_sync();
+    if (keep && rk == 0) run[wv][tl] += static_cast<uint32_t>(__popcll(peers));
+    wave_sync();
   }
 }
 
-__global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a, const uint64_t* offsets,
-                                                           uint32_t* out_ids, uint32_t* deep_rank) {
+__global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a) {
   const uint32_t fill = min(a.ctrl[CTRL_DEEP_FILL], a.deep_slab_cap);
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < fill;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint64_t e = a.deep_slab[i];
     const uint32_t j = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
     const uint32_t t = a.deferred[j];
-    const uint32_t r = atomicAdd(&deep_rank[j], 1u);
-    out_ids[offsets[t] + r] = resolve_entry(a.tv, e);
+    const uint64_t p = a.out_off[t] + atomicAdd(&a.deep_rank[j], 1u);
+    if (p < a.out_cap) a.out_ids[p] = resolve_entry(a.tv, e);
   }
-}
-
-__global__ void zero_u32_kernel(uint32_t* p, const uint32_t* count) {
-  const uint32_t n = *count;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1189,15 +1299,11 @@ hipError_t launch_scan(const uint32_t* counts, uint64_t n, uint64_t* offsets, ui
   return hipGetLastError();
 }
 
-hipError_t launch_scatter(const MatchArgs& a, const uint64_t* offsets, uint32_t* out_ids,
-                          uint32_t* deep_rank, hipStream_t s) {
+hipError_t launch_assemble(const MatchArgs& a, hipStream_t s) {
   const uint64_t ntiles = (a.n + TILE_TOPICS - 1) / TILE_TOPICS;
-  if (ntiles) {
-    hipLaunchKernelGGL(scatter_fast_kernel, dim3(static_cast<uint32_t>((ntiles + 3) / 4)), dim3(256), 0, s, a,
-                       offsets, out_ids);
-  }
-  hipLaunchKernelGGL(zero_u32_kernel, dim3(64), dim3(256), 0, s, deep_rank, a.ctrl + CTRL_DEFERRED);
-  hipLaunchKernelGGL(scatter_deep_kernel, dim3(256), dim3(256), 0, s, a, offsets, out_ids, deep_rank);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(TSCAN_THREADS), 0, s, a, ntiles);
+  if (ntiles) hipLaunchKernelGGL(scatter_fast_kernel, dim3(static_cast<uint32_t>((ntiles + 3) / 4)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(scatter_deep_kernel, dim3(64), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -474,6 +474,37 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       lf[v] = n_lit <= LITF_BLOOM_MAX ? bloom : ~0u;
     }
   }
+  // A child with edges and exactly one filter id carries it in litf (META_XFID), so its
+  // emission needs no fids[] reference; its literal filter moves to 8 bits of the meta: the
+  // fingerprint of its only literal word, or an 8-bit Bloom mask.  (EMQX_XFID=0, A/B runs:
+  // only children without literal edges, which lose no filter.)
+  {
+    static const bool xfid_off = [] {
+      const char* v = getenv("EMQX_XFID");
+      return v && std::strcmp(v, "0") == 0;
+    }();
+    for (uint64_t v = 1; v < n_nodes; ++v) {
+      if (!n_edges[v]) continue;
+      const bool h = hash_fid[v] != FID_NONE, t = term_fid[v] != FID_NONE;
+      if (h == t) continue;
+      const bool none = (lf_flag[v] & META_LITF_NONE) != 0, exact = (lf_flag[v] & META_LITF_EXACT) != 0;
+      if (!none && xfid_off) continue;
+      uint32_t f8 = 0;
+      if (exact) {
+        f8 = litf_hash(lf[v]) >> 24;
+      } else if (!none) {
+        uint32_t n_lit = 0;
+        for (uint64_t j = coff[v]; j < coff[v + 1]; ++j) {
+          if (cwid[j] == WID_PLUS) continue;
+          ++n_lit;
+          f8 |= 1u << (litf_hash(cwid[j]) & 7u);
+        }
+        if (n_lit > LITF_BLOOM_MAX) f8 = 0xFFu;
+      }
+      lf_flag[v] |= META_XFID | (t ? META_XFID_TERM : 0u) | (f8 << META_F8_SHIFT);
+      lf[v] = t ? term_fid[v] : hash_fid[v];
+    }
+  }
   auto meta_of = [&](uint32_t v) -> uint32_t {
     uint32_t m = caplog[v] & META_CAPLOG2_MASK;
     if (n_edges[v]) m |= META_HAS_EDGES;
@@ -608,7 +639,9 @@ bool check_tables(const HostTables& t, std::string* err) {
     if (s.wid == WID_NONE) continue;
     if ((t.fids[2 * i] != FID_NONE) != ((s.meta & META_HAS_HASH) != 0) ||
         (t.fids[2 * i + 1] != FID_NONE) != ((s.meta & META_HAS_TERM) != 0) ||
-        (!(s.meta & META_HAS_EDGES) && (s.child_base != t.fids[2 * i] || s.litf != t.fids[2 * i + 1]))) {
+        (!(s.meta & META_HAS_EDGES) && (s.child_base != t.fids[2 * i] || s.litf != t.fids[2 * i + 1])) ||
+        ((s.meta & META_HAS_EDGES) && (s.meta & META_XFID) &&
+         s.litf != t.fids[2 * i + ((s.meta & META_XFID_TERM) ? 1 : 0)])) {
       if (err) *err = "filter ids disagree with the child's meta";
       return false;
     }

@@ -154,3 +154,16 @@ class Engine:
             raise err
         check(rc, "emqx_match_batch_device")
         return int(total.value)
+
+    SUMMARY_WORDS = 8  # flags, total, evals, max stack, deferred, need_slab, deep_fill, error
+
+    def match_device_async(self, d_bytes_ptr: int, d_offs_ptr: int, n: int, d_out_off_ptr: int,
+                           d_out_ids_ptr: int, cap: int, d_summary_ptr: int, mode: int = MODE_ROUTES,
+                           stream: int = 0) -> None:
+        """Enqueue a device-resident batch and return at once; ``d_summary_ptr`` (8 uint64,
+        device or pinned memory) receives the call summary when the stream reaches it:
+        word 0 == 0 means the output is complete (see include/emqx_match.h)."""
+        check(_lib.lib().emqx_match_batch_device_async(
+            self._h, mode, ctypes.c_void_p(d_bytes_ptr), ctypes.c_void_p(d_offs_ptr), n,
+            ctypes.c_void_p(d_out_off_ptr), ctypes.c_void_p(d_out_ids_ptr), cap, ctypes.c_void_p(d_summary_ptr),
+            ctypes.c_void_p(stream) if stream else None), "emqx_match_batch_device_async")

@@ -113,12 +113,26 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes,
                      uint32_t* out_ids, uint64_t cap, uint64_t* n_out);
 
 /* Batched match, DEVICE buffers already resident in HBM (d_* pointers), ordered on the
- * given hipStream_t (NULL: the engine's own stream).  Same contract as above; *n_out is a
- * host pointer.  Returns after the results are complete on `stream`. */
+ * given hipStream_t (NULL: the engine's own stream).  Same contract as above, except that on
+ * EMQX_EOVERFLOW d_out_offsets are complete and d_out_ids holds the first cap ids; *n_out is
+ * a host pointer.  Returns after the results are complete on `stream`. */
 int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topic_bytes,
                             const uint64_t* d_topic_offsets, uint64_t n,
                             uint64_t* d_out_offsets, uint32_t* d_out_ids, uint64_t cap,
                             uint64_t* n_out, void* stream);
+
+/* Asynchronous emqx_match_batch_device for pipelined callers (a batcher double-buffering
+ * device batches): enqueues the call on `stream` and returns at once.  `summary` (>= 8
+ * uint64_t, device or host-pinned memory) receives, when the stream reaches it:
+ *   [0] flags: 0 = complete; 1 = a scratch area overflowed (redo the batch with
+ *       emqx_match_batch_device, which grows it once for the engine); 2 = more than cap ids
+ *       (d_out_offsets complete, d_out_ids truncated); 4 = a topic over 65535 bytes;
+ *   [1] total ids; [2] trie node visits; [3] max frontier depth; [4] deep-path topics.
+ * The table snapshot the call reads stays alive until the call has drained. */
+int emqx_match_batch_device_async(emqx_engine* e, uint32_t mode, const uint8_t* d_topic_bytes,
+                                  const uint64_t* d_topic_offsets, uint64_t n,
+                                  uint64_t* d_out_offsets, uint32_t* d_out_ids, uint64_t cap,
+                                  uint64_t* summary, void* stream);
 
 int emqx_stats_get(emqx_engine* e, emqx_stats* out);
 

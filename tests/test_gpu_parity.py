@@ -269,6 +269,77 @@ def test_device_api_matches_host_api(Engine):
         assert np.array_equal(np.sort(ids_d[off_d[i]:off_d[i + 1]]), np.sort(ids_h[off_h[i]:off_h[i + 1]]))
 
 
+def test_async_device_api(Engine):
+    """emqx_match_batch_device_async: pipelined calls on one stream give the synchronous
+    call's CSR, each writes its summary, and the flags report a too-small id buffer and a
+    slab that must grow (the synchronous call then sizes it)."""
+    import torch
+    from emqx_amd import workloads as W
+    b = W.config_b(n_filters=100_000, n_topics=20_000)
+    e = Engine()
+    e.insert_packed(*b.filters)
+    e.commit()
+    off_h, ids_h = e.match_packed(*b.topics, mode=0)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    tb = torch.from_numpy(b.topics[0]).to(dev)
+    to = torch.from_numpy(b.topics[1].view(np.int64)).to(dev)
+    n = len(b.topics[1]) - 1
+    summ = torch.zeros((4, Engine.SUMMARY_WORDS), dtype=torch.int64, device=dev)
+    outs = []
+    for k in range(3):
+        d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_ids = torch.empty(ids_h.size + 16, dtype=torch.int32, device=dev)
+        e.match_device_async(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), d_ids.numel(),
+                             summ[k].data_ptr(), mode=0, stream=s)
+        outs.append((d_off, d_ids))
+    small = torch.empty(8, dtype=torch.int32, device=dev)
+    d_off_s = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    e.match_device_async(tb.data_ptr(), to.data_ptr(), n, d_off_s.data_ptr(), small.data_ptr(), small.numel(),
+                         summ[3].data_ptr(), mode=0, stream=s)
+    torch.cuda.synchronize()
+    sm = summ.cpu().numpy()
+    assert (sm[:3, 0] == 0).all() and (sm[:, 1] == ids_h.size).all()
+    assert sm[3, 0] == 2  # overflow: offsets complete, ids truncated
+    assert np.array_equal(d_off_s.cpu().numpy().view(np.uint64), off_h)
+    for d_off, d_ids in outs:
+        off_d = d_off.cpu().numpy().view(np.uint64)
+        ids_d = d_ids[:ids_h.size].cpu().numpy().view(np.uint32)
+        assert np.array_equal(off_d, off_h)
+        for i in range(0, n, 89):
+            assert np.array_equal(np.sort(ids_d[off_d[i]:off_d[i + 1]]), np.sort(ids_h[off_h[i]:off_h[i + 1]]))
+    # a fresh engine's first async call on a hot topic overflows its slab: flag 1, then the
+    # synchronous call grows it and the async call completes.  The topic has 10 levels; the
+    # filters are every literal/'+' pattern of it and every such prefix + '#' (3071 matches).
+    from emqx_amd.engine import pack
+    words = [b"w%d" % i for i in range(10)]
+    pats = []
+    for L in range(11):
+        for m in range(1 << L):
+            lv = [b"+" if (m >> i) & 1 else words[i] for i in range(L)]
+            pats.append(b"/".join(lv + [b"#"]) if L < 10 else b"/".join(lv))
+    e2 = engine_with(Engine, pats)
+    hot = pack([b"/".join(words)] * 64)
+    want = len(expected(pats, [b"/".join(words)], 0)[0])
+    htb = torch.from_numpy(hot[0]).to(dev)
+    hto = torch.from_numpy(hot[1].view(np.int64)).to(dev)
+    d_off = torch.empty(65, dtype=torch.int64, device=dev)
+    d_ids = torch.empty(64 * want + 16, dtype=torch.int32, device=dev)
+    s2 = torch.zeros(Engine.SUMMARY_WORDS, dtype=torch.int64, device=dev)
+    e2.match_device_async(htb.data_ptr(), hto.data_ptr(), 64, d_off.data_ptr(), d_ids.data_ptr(), d_ids.numel(),
+                          s2.data_ptr(), mode=0, stream=s)
+    torch.cuda.synchronize()
+    assert int(s2[0]) & 1
+    assert e2.match_device(htb.data_ptr(), hto.data_ptr(), 64, d_off.data_ptr(), d_ids.data_ptr(), d_ids.numel(),
+                           mode=0, stream=s) == 64 * want
+    e2.match_device_async(htb.data_ptr(), hto.data_ptr(), 64, d_off.data_ptr(), d_ids.data_ptr(), d_ids.numel(),
+                          s2.data_ptr(), mode=0, stream=s)
+    torch.cuda.synchronize()
+    assert int(s2[0]) == 0 and int(s2[1]) == 64 * want
+    got = d_ids[:want].cpu().numpy().view(np.uint32)
+    assert sorted(got.tolist()) == expected(pats, [b"/".join(words)], 0)[0]
+
+
 def test_sharded_matcher_world1_rccl(Engine):
     """The filter-sharded path end to end on one GPU over RCCL (world size 1): broadcast,
     global-id shard table, gather and concatenation give the single-engine result."""
