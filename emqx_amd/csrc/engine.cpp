@@ -81,13 +81,14 @@ struct Workspace {
   uint64_t* slab = nullptr;
   uint32_t* tile_fill = nullptr;
   uint64_t* tile_defer = nullptr;
-  uint2* tile_stats = nullptr;
   uint2* spill = nullptr;
   uint64_t* diag = nullptr;
   uint32_t spill_cap = 2048;  // items per tile
-  uint32_t* ctrl = nullptr;         // [16]: CTRL_* words, then deep_evals (one memset per call)
+  uint32_t* ctrl = nullptr;         // CTRL_WORDS words (one memset per call)
   uint64_t* tile_sum = nullptr;
-  uint64_t* tile_off = nullptr;
+  uint2* tile_stats = nullptr;
+  uint64_t* group_sum = nullptr;
+  uint2* group_stats = nullptr;
   hipEvent_t done = nullptr;        // end of the last call enqueued with this workspace
   std::shared_ptr<Snapshot> inflight;  // table of the last async call (kept alive for it)
   uint32_t* deep_wids = nullptr;
@@ -110,8 +111,9 @@ struct Workspace {
   ~Workspace() {
     (void)hipSetDevice(device);
     dfree(counts); dfree(deferred); dfree(deep_rank); dfree(slab); dfree(tile_fill);
-    dfree(tile_defer); dfree(tile_stats); dfree(spill); dfree(diag); dfree(ctrl); dfree(tile_sum);
-    dfree(tile_off); dfree(deep_wids); dfree(deep_stack); dfree(deep_slab);
+    dfree(tile_defer); dfree(spill); dfree(diag); dfree(ctrl); dfree(tile_sum); dfree(tile_stats);
+    dfree(group_sum); dfree(group_stats);
+    dfree(deep_wids); dfree(deep_stack); dfree(deep_slab);
     dfree(d_tbytes); dfree(d_toffs); dfree(d_out_off); dfree(d_out_ids);
     if (h_rb) (void)hipHostFree(h_rb);
     if (ev0) (void)hipEventDestroy(ev0);
@@ -226,7 +228,7 @@ int ensure_ws(Workspace* w, uint64_t n) {
     HIP_TRY(hipEventCreate(&w->evk));
     HIP_TRY(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_rb), SUM_WORDS * sizeof(uint64_t), hipHostMallocDefault));
-    HIP_TRY(dalloc(w->ctrl, 16));
+    HIP_TRY(dalloc(w->ctrl, CTRL_WORDS));
     HIP_TRY(dalloc(w->diag, DIAG_WORDS));
     HIP_TRY(hipMemset(w->diag, 0, DIAG_WORDS * sizeof(uint64_t)));
   }
@@ -248,9 +250,10 @@ int ensure_ws(Workspace* w, uint64_t n) {
     const uint64_t cap = round_pow2(std::max<uint64_t>(ntiles, 64));
     HIP_TRY(dalloc(w->tile_fill, cap));
     HIP_TRY(dalloc(w->tile_defer, cap));
-    HIP_TRY(dalloc(w->tile_stats, cap));
     HIP_TRY(dalloc(w->tile_sum, cap));
-    HIP_TRY(dalloc(w->tile_off, cap));
+    HIP_TRY(dalloc(w->tile_stats, cap));
+    HIP_TRY(dalloc(w->group_sum, cap / GROUP_TILES + 1));
+    HIP_TRY(dalloc(w->group_stats, cap / GROUP_TILES + 1));
     HIP_TRY(dalloc(w->spill, cap * w->spill_cap));
     w->cap_tiles = cap;
   }
@@ -295,7 +298,6 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.slab = w->slab;
   a.tile_fill = w->tile_fill;
   a.tile_defer = w->tile_defer;
-  a.tile_stats = w->tile_stats;
   a.spill = w->spill;
   a.diag = e->diag_on.load() ? w->diag : nullptr;
   a.spill_cap = w->spill_cap;
@@ -307,9 +309,11 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.deep_waves = DEEP_WAVES;
   a.deep_slab = w->deep_slab;
   a.deep_slab_cap = w->deep_slab_cap;
-  a.deep_evals = w->ctrl + 8;
   a.tile_sum = w->tile_sum;
-  a.tile_off = w->tile_off;
+  a.tile_stats = w->tile_stats;
+  a.group_sum = w->group_sum;
+  a.group_stats = w->group_stats;
+  a.ngroups = static_cast<uint32_t>((n + TILE_TOPICS * GROUP_TILES - 1) / (TILE_TOPICS * GROUP_TILES));
   a.deep_rank = w->deep_rank;
   a.out_off = d_out_off;
   a.out_ids = d_out_ids;
@@ -317,7 +321,7 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.summary = summary;
 
   HIP_TRY(hipStreamWaitEvent(s, w->done, 0));
-  HIP_TRY(hipMemsetAsync(w->ctrl, 0, 16 * sizeof(uint32_t), s));
+  HIP_TRY(hipMemsetAsync(w->ctrl, 0, CTRL_WORDS * sizeof(uint32_t), s));
   HIP_TRY(hipEventRecord(w->ev0, s));
   HIP_TRY(launch_match_fast(a, pick_variant(e, snap), s));
   HIP_TRY(hipEventRecord(w->evk, s));

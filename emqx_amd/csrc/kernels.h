@@ -14,8 +14,10 @@ enum Ctrl : uint32_t {
   CTRL_NEED_SLAB = 1,   // max entries any tile needed (> slab_cap => rerun)
   CTRL_ERROR = 2,       // error bits (CTRL_ERR_*)
   CTRL_DEEP_FILL = 3,   // entries the deep path emitted
-  CTRL_WORDS = 4
+  CTRL_DEEP_EVALS = 4,  // node visits of the deep path
+  CTRL_WORDS = 8
 };
+constexpr uint32_t GROUP_TILES = 256;  // tiles per group sum (two-level output offsets)
 constexpr uint32_t CTRL_ERR_TOO_LONG = 1u;   // deferred topic longer than 65535 bytes
 constexpr uint32_t CTRL_ERR_TOO_DEEP = 2u;   // deep-path frontier exceeded its stack
 constexpr uint32_t CTRL_ERR_DEEP_SLAB = 4u;  // deep-path slab overflow
@@ -72,7 +74,6 @@ struct MatchArgs {
   uint64_t* slab;          // [ntiles * slab_cap]  (topic_local << 32) | fid
   uint32_t* tile_fill;     // [ntiles]
   uint64_t* tile_defer;    // [ntiles]
-  uint2* tile_stats;       // [ntiles] {node visits, max stack depth}
   uint32_t* ctrl;          // [CTRL_WORDS]
   uint32_t* deferred;      // [n]
   uint64_t* diag;          // optional [DIAG_WORDS] counters (nullptr = off)
@@ -85,10 +86,12 @@ struct MatchArgs {
   uint32_t deep_waves;
   uint64_t* deep_slab;     // [deep_slab_cap]  (deferred_slot << 32) | fid
   uint32_t deep_slab_cap;
-  uint32_t* deep_evals;    // [1] (atomic)
   // output assembly
   uint64_t* tile_sum;      // [ntiles] filter ids per tile (fast path + deep path's atomics)
-  uint64_t* tile_off;      // [ntiles] exclusive scan of tile_sum
+  uint2* tile_stats;       // [ntiles] {node visits, max stack depth}
+  uint64_t* group_sum;     // [ngroups] filter ids per GROUP_TILES tiles
+  uint2* group_stats;      // [ngroups] {node visits, max stack depth}
+  uint32_t ngroups;
   uint32_t* deep_rank;     // [n] per deferred slot: ids placed so far
   uint64_t* out_off;       // [n + 1] CSR offsets (caller's)
   uint32_t* out_ids;       // [out_cap] CSR ids (caller's)
@@ -112,7 +115,8 @@ enum FastVariant {
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);
 hipError_t launch_match_deep(const MatchArgs& a, hipStream_t s);
-// tile scan -> out_off[n] and the summary; then per-tile offsets + ids (fast, then deep)
+// group sums -> per-tile offsets + ids (fast path), the deep path's ids, then out_off[n]
+// and the call summary
 hipError_t launch_assemble(const MatchArgs& a, hipStream_t s);
 // counts[n] -> offsets[n+1] (exclusive); partials: scratch of >= scan_partials(n) u64
 // (fan-out's entry scan).

@@ -856,9 +856,9 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   const uint32_t tsum = wave_sum(mine);
   if (lane == 0) {
     a.tile_sum[tile] = tsum;  // the deep path adds its topics' counts
+    a.tile_stats[tile] = make_uint2(ev, maxtop);
     a.tile_fill[tile] = cursor;
     a.tile_defer[tile] = defer_mask;
-    a.tile_stats[tile] = make_uint2(ev, maxtop);
     if (cursor > cap) atomicMax(&a.ctrl[CTRL_NEED_SLAB], cursor);
   }
   if (defer_mask) {
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       a.counts[t] = count;
       if (count) atomicAdd(reinterpret_cast<unsigned long long*>(a.tile_sum + t / TILE_TOPICS),
                            static_cast<unsigned long long>(count));
-      atomicAdd(&a.deep_evals[0], ev);
+      atomicAdd(a.ctrl + CTRL_DEEP_EVALS, ev);
     }
   }
 }
@@ -1105,96 +1105,57 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_final_kernel(const uint32_t
 // ------------------------------------------------------------------------------------
 // Output assembly: tile scan -> per-tile offsets; scatter: slab entries -> CSR out_ids
 // ------------------------------------------------------------------------------------
-constexpr int TSCAN_THREADS = 1024;
+// Sum of v over lanes (u64).
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1)
+    v += (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(v >> 32), d, 64)) << 32) |
+         __shfl_xor(static_cast<uint32_t>(v), d, 64);
+  return v;
+}
 
-// One block: exclusive scan of tile_sum -> tile_off, out_off[n] = total, and the call
-// summary (ctrl words are final: the fast and deep kernels have drained).  Each thread owns a
-// run of consecutive tiles: sum it, one block scan of the run totals, then write the run.
-__global__ __launch_bounds__(TSCAN_THREADS) void tile_scan_kernel(MatchArgs a, uint64_t ntiles) {
-  __shared__ uint64_t wsum[TSCAN_THREADS / 64];
-  __shared__ uint32_t wmax[TSCAN_THREADS / 64];
+// One block per group of GROUP_TILES tiles: its id total and its node visits / max stack
+// (coalesced; no atomics — same-address atomics serialise at L2, ~50 ns each).
+__global__ __launch_bounds__(GROUP_TILES) void group_reduce_kernel(MatchArgs a, uint64_t ntiles) {
+  __shared__ uint64_t ws[GROUP_TILES / 64], we[GROUP_TILES / 64];
+  __shared__ uint32_t wm[GROUP_TILES / 64];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t per = (ntiles + TSCAN_THREADS - 1) / TSCAN_THREADS;
-  const uint64_t b = min<uint64_t>(per * threadIdx.x, ntiles), e = min<uint64_t>(b + per, ntiles);
-  constexpr uint32_t R = 16;  // loads in flight per thread (one block: latency is the cost)
-  uint64_t mine = 0, evals = 0;
-  uint32_t maxtop = 0;
-  for (uint64_t c0 = b; c0 < e; c0 += R) {
-    uint64_t v[R];
-    uint2 st[R];
-#pragma unroll
-    for (uint32_t k = 0; k < R; ++k) {
-      v[k] = c0 + k < e ? a.tile_sum[c0 + k] : 0;
-      st[k] = c0 + k < e ? a.tile_stats[c0 + k] : make_uint2(0, 0);
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < R; ++k) {
-      mine += v[k];
-      evals += st[k].x;
-      maxtop = max(maxtop, st[k].y);
-    }
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * GROUP_TILES + threadIdx.x;
+  uint64_t v = 0, ev = 0;
+  uint32_t mx = 0;
+  if (i < ntiles) {
+    v = a.tile_sum[i];
+    const uint2 st = a.tile_stats[i];
+    ev = st.x;
+    mx = st.y;
   }
-  const uint64_t incl = wave_incl_scan64(mine, lane);
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint64_t carry = incl - mine, all = 0;
-  for (uint32_t k = 0; k < TSCAN_THREADS / 64; ++k) {
-    carry += k < w ? wsum[k] : 0;
-    all += wsum[k];
-  }
-  for (uint64_t c0 = b; c0 < e; c0 += R) {
-    uint64_t v[R];
-#pragma unroll
-    for (uint32_t k = 0; k < R; ++k) v[k] = c0 + k < e ? a.tile_sum[c0 + k] : 0;
-#pragma unroll
-    for (uint32_t k = 0; k < R; ++k) {
-      if (c0 + k < e) a.tile_off[c0 + k] = carry;
-      carry += v[k];
-    }
-  }
-  carry = all;
-  __syncthreads();
-  // evals / max stack: block reductions
-  for (uint32_t d = 32; d >= 1; d >>= 1) {
-    evals += (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(evals >> 32), d, 64)) << 32) |
-             __shfl_xor(static_cast<uint32_t>(evals), d, 64);
-    maxtop = max(maxtop, static_cast<uint32_t>(__shfl_xor(maxtop, d, 64)));
-  }
+  v = wave_sum64(v);
+  ev = wave_sum64(ev);
+  for (uint32_t d = 32; d >= 1; d >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, d, 64)));
   if (lane == 0) {
-    wsum[w] = evals;
-    wmax[w] = maxtop;
+    ws[w] = v;
+    we[w] = ev;
+    wm[w] = mx;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (uint32_t k = 1; k < TSCAN_THREADS / 64; ++k) {
-      evals += wsum[k];
-      maxtop = max(maxtop, wmax[k]);
+    uint64_t sv = 0, se = 0;
+    uint32_t sm = 0;
+    for (uint32_t k = 0; k < GROUP_TILES / 64; ++k) {
+      sv += ws[k];
+      se += we[k];
+      sm = max(sm, wm[k]);
     }
-    const uint32_t ndef = a.ctrl[CTRL_DEFERRED], need = a.ctrl[CTRL_NEED_SLAB], err = a.ctrl[CTRL_ERROR];
-    const uint32_t fill = a.ctrl[CTRL_DEEP_FILL];
-    uint64_t flags = 0;
-    if (need > a.slab_cap || (err & (CTRL_ERR_DEEP_SLAB | CTRL_ERR_TOO_DEEP))) flags |= SUM_F_RETRY;
-    if (carry > a.out_cap) flags |= SUM_F_OVERFLOW;
-    if (err & CTRL_ERR_TOO_LONG) flags |= SUM_F_ERROR;
-    a.out_off[a.n] = carry;
-    uint64_t* sm = a.summary;
-    sm[SUM_TOTAL] = carry;
-    sm[SUM_EVALS] = evals + *a.deep_evals;
-    sm[SUM_MAXSTACK] = maxtop;
-    sm[SUM_DEFERRED] = ndef;
-    sm[SUM_NEED_SLAB] = need;
-    sm[SUM_DEEP_FILL] = fill;
-    sm[SUM_ERROR] = err;
-    sm[SUM_FLAGS] = flags;
-    __threadfence_system();
+    a.group_sum[blockIdx.x] = sv;
+    a.group_stats[blockIdx.x] = make_uint2(static_cast<uint32_t>(min<uint64_t>(se, 0xFFFFFFFFull)), sm);
   }
 }
 
-// One wave per tile: the tile's CSR offsets (wave scan of its 64 counts on top of the tile
-// offset), then its slab entries, 64 at a time: lanes holding the same topic find each other
-// with six ballots (one per bit of the topic index), take ranks by popcount and the group's
-// first lane advances the topic's running count — no atomics.  Ids beyond out_cap are
-// dropped (the summary reports the overflow).
+// One wave per tile.  The tile's first output position is two short sums — the group sums
+// before its group and its group's tile sums before it — plus a wave scan of its 64 counts.
+// Then its slab entries, 64 at a time: lanes holding the same topic find each other with six
+// ballots (one per bit of the topic index), take ranks by popcount and the group's first
+// lane advances the topic's running count — no atomics.  Ids beyond out_cap are dropped.
 __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
   __shared__ uint32_t run[4][64];
   __shared__ uint64_t base[4][64];
@@ -1203,9 +1164,14 @@ __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
   const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4 + wv;
   const uint64_t t0 = tile * TILE_TOPICS;
   if (t0 >= a.n) return;
+  const uint64_t g = tile / GROUP_TILES, g0 = g * GROUP_TILES;
+  uint64_t before = 0;
+  for (uint64_t k = lane; k < g; k += 64) before += a.group_sum[k];
+  for (uint64_t j = g0 + lane; j < tile; j += 64) before += a.tile_sum[j];
+  before = wave_sum64(before);
   const uint64_t t = t0 + lane;
   const uint64_t c = t < a.n ? a.counts[t] : 0;
-  const uint64_t off = a.tile_off[tile] + wave_incl_scan64(c, lane) - c;
+  const uint64_t off = before + wave_incl_scan64(c, lane) - c;
   if (t < a.n) a.out_off[t] = off;
   base[wv][lane] = off;
   run[wv][lane] = 0;
@@ -1233,6 +1199,41 @@ __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
     wave_sync();
     if (keep && rk == 0) run[wv][tl] += static_cast<uint32_t>(__popcll(peers));
     wave_sync();
+  }
+}
+
+// One wave: out_off[n] and the call summary from the group sums and the ctrl words.
+__global__ __launch_bounds__(64) void summary_kernel(MatchArgs a) {
+  const uint32_t lane = lane_id();
+  uint64_t tot = 0, ev = 0;
+  uint32_t mx = 0;
+  for (uint32_t k = lane; k < a.ngroups; k += 64) {
+    tot += a.group_sum[k];
+    const uint2 st = a.group_stats[k];
+    ev += st.x;
+    mx = max(mx, st.y);
+  }
+  tot = wave_sum64(tot);
+  ev = wave_sum64(ev);
+  for (uint32_t d = 32; d >= 1; d >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, d, 64)));
+  if (lane == 0) {
+    const uint32_t* c = a.ctrl;
+    const uint32_t need = c[CTRL_NEED_SLAB], err = c[CTRL_ERROR];
+    uint64_t flags = 0;
+    if (need > a.slab_cap || (err & (CTRL_ERR_DEEP_SLAB | CTRL_ERR_TOO_DEEP))) flags |= SUM_F_RETRY;
+    if (tot > a.out_cap) flags |= SUM_F_OVERFLOW;
+    if (err & CTRL_ERR_TOO_LONG) flags |= SUM_F_ERROR;
+    a.out_off[a.n] = tot;
+    uint64_t* sm = a.summary;
+    sm[SUM_TOTAL] = tot;
+    sm[SUM_EVALS] = ev + c[CTRL_DEEP_EVALS];
+    sm[SUM_MAXSTACK] = mx;
+    sm[SUM_DEFERRED] = c[CTRL_DEFERRED];
+    sm[SUM_NEED_SLAB] = need;
+    sm[SUM_DEEP_FILL] = c[CTRL_DEEP_FILL];
+    sm[SUM_ERROR] = err;
+    sm[SUM_FLAGS] = flags;
+    __threadfence_system();
   }
 }
 
@@ -1301,9 +1302,12 @@ hipError_t launch_scan(const uint32_t* counts, uint64_t n, uint64_t* offsets, ui
 
 hipError_t launch_assemble(const MatchArgs& a, hipStream_t s) {
   const uint64_t ntiles = (a.n + TILE_TOPICS - 1) / TILE_TOPICS;
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(TSCAN_THREADS), 0, s, a, ntiles);
-  if (ntiles) hipLaunchKernelGGL(scatter_fast_kernel, dim3(static_cast<uint32_t>((ntiles + 3) / 4)), dim3(256), 0, s, a);
+  if (ntiles) {
+    hipLaunchKernelGGL(group_reduce_kernel, dim3(a.ngroups), dim3(GROUP_TILES), 0, s, a, ntiles);
+    hipLaunchKernelGGL(scatter_fast_kernel, dim3(static_cast<uint32_t>((ntiles + 3) / 4)), dim3(256), 0, s, a);
+  }
   hipLaunchKernelGGL(scatter_deep_kernel, dim3(64), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -30,4 +30,10 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_s
   rc=$?; cd "$ROOT"; echo "pmc pass $i ($grp) rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python tools/pmc_summary.py --dir "$OUT" --kernel match_fast_kernel | tee "$OUT/pmc_summary.json"
+echo "== FETCH_SIZE calibration on random 16-B gathers (tools/gather_bench.hip)"; date
+if [ -x tools/_build/gather_bench ]; then
+  cd /tmp
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TCC_MISS_sum --kernel-include-regex indep_kernel --output-format csv -d "$ROOT/$OUT/cal" -o cal -- "$ROOT/tools/_build/gather_bench" > "$ROOT/$OUT/cal.log" 2>&1
+  rc=$?; cd "$ROOT"; echo "calibration rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
 echo "== done"; date
