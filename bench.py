@@ -36,6 +36,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+WORKLOAD_NAMES = {
+    "A": "A: 100k filters site{i%1000}/+/dev{i/1000}/#, 1M-topic stream (configs[0] table on 1xMI355X)",
+    "B": "B: 10M mixed exact/'+'/'#' subscriptions, 1xMI355X, batched topics of depth 4-8",
+    "D": "D: adversarial '#'/'+'-rich table, 1M filters, depth-16 topics, 1xMI355X",
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,8 +61,10 @@ def main():
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
-    ap.add_argument("--workload", type=str, default="B", choices=["B", "E"],
-                    help="E = publish fan-out (SURVEY §8 d config E): match + fan-out per step")
+    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E"],
+                    help="B = the headline (BASELINE configs[1]); A = configs[0]'s 100k-filter table, "
+                         "D = the adversarial depth-16 table (configs[3], 100k-topic batches), "
+                         "E = publish fan-out (configs[4]): match + fan-out per step")
     ap.add_argument("--strategy", type=str, default="hash_clientid",
                     help="$share strategy for --workload E")
     ap.add_argument("--sharded", action="store_true",
@@ -78,7 +87,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from emqx_amd import workloads as W
-    from emqx_amd.engine import Engine
+    from emqx_amd.engine import Engine, EngineError
 
     t0 = time.time()
     # every rank replicates the table (seed 2); each rank draws its own topic stream (weak scaling)
@@ -86,9 +95,16 @@ def main():
         return sharded_bench(args, rank, world, dev)
     if args.workload == "E":
         return fanout_bench(args, rank, world, dev)
-    wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
-                                                     vocab_scale=args.vocab_scale,
-                                                     topic_seed=None if rank == 0 else 1000 + rank))
+    if args.workload == "A":
+        wl = load_or_make(args, rank, lambda: W.config_a(n_topics=args.batch, seed=1 if rank == 0 else 1000 + rank))
+    elif args.workload == "D":
+        if args.batch == 1_000_000:
+            args.batch = 100_000  # ~1000 node visits per topic: a 100k batch is ~0.1 G visits
+        wl = load_or_make(args, rank, lambda: W.config_d(n_topics=args.batch, seed=4))
+    else:
+        wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
+                                                         vocab_scale=args.vocab_scale,
+                                                         topic_seed=None if rank == 0 else 1000 + rank))
     log(f"[rank {rank}] workload: {wl.n_filters} filters, {wl.n_topics} topics ({time.time() - t0:.1f}s)")
 
     t0 = time.time()
@@ -116,7 +132,14 @@ def main():
 
     nout = 0
     for _ in range(max(args.warmup, 1)):  # synchronous calls: size the scratch areas once
-        nout = step()
+        try:
+            nout = step()
+        except EngineError as err:  # id buffer too small for this workload: size it and redo
+            if getattr(err, "needed", None) is None:
+                raise
+            cap = int(err.needed * 1.25) + 1024
+            d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+            nout = step()
     # Timed steps are enqueued with emqx_match_batch_device_async, as a pipelined caller
     # would: every step runs the whole pipeline (fast + deep kernels, scan, scatter) and
     # writes its own summary; nothing is skipped, only the host no longer blocks per batch.
@@ -189,7 +212,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": "B: 10M mixed exact/'+'/'#' subscriptions, 1xMI355X, batched topics of depth 4-8",
+        "config": {"workload": WORKLOAD_NAMES[args.workload],
                    "n_filters": wl.n_filters, "batch_topics_per_gpu": n, "mode": ["routes", "trie", "trie_wildcard"][args.mode],
                    "parallelism": f"replicated table, topic stream split x{world}"},
         "evals_per_s": round(evals_all * args.steps / elapsed, 1),
@@ -280,7 +303,8 @@ def measured_traffic(n, args):
     (profiles/pmc_match_fast.json, written from tools/gpu_round.sh's counter runs on the same
     workload), scaled to this batch.  None when the file is absent or the workload differs."""
     path = os.path.join(ROOT, "profiles", "pmc_match_fast.json")
-    if not os.path.exists(path) or args.n_filters != 10_000_000 or args.mode != 0 or args.vocab_scale != 1:
+    if (not os.path.exists(path) or args.workload != "B" or args.n_filters != 10_000_000 or args.mode != 0
+            or args.vocab_scale != 1):
         return None, None
     with open(path) as f:
         p = json.load(f)
