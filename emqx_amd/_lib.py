@@ -62,6 +62,7 @@ class Stats(ctypes.Structure):
         ("last_max_stack", ctypes.c_uint64),
         ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double),
         ("last_kernel_ms", ctypes.c_double),
+        ("delta_filters", ctypes.c_uint64), ("last_commit_kind", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -1,6 +1,6 @@
-// C ABI implementation (include/emqx_match.h): filter store, snapshot build/upload with an
-// RCU-style epoch swap, per-call workspaces, and the match pipeline
-//   fast kernel -> deep kernel -> scan -> [one small D2H readback] -> scatter.
+// C ABI implementation (include/emqx_match.h): filter store, full and incremental commits
+// with an RCU-style snapshot swap, per-call workspaces, and the match pipeline
+//   fast kernel -> deep kernel -> group reduce -> scatter -> summary (one sync per call).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -11,6 +11,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/emqx_match.h"
@@ -45,26 +46,63 @@ hipError_t dalloc(T*& p, uint64_t count) {
   return hipMalloc(reinterpret_cast<void**>(&p), std::max<uint64_t>(count, 1) * sizeof(T));
 }
 
-struct Snapshot {
+// Device buffers of one full build, with headroom for incremental commits: two delta-trie
+// regions behind the base slots (alternating per commit), vocab slots to fill, arena bytes to
+// append.  Shared by every snapshot published from that build; freed (after draining the
+// device: an async call may still read it) when the last one goes.
+struct DeviceTables {
   int device = 0;
-  EdgeSlot* edges = nullptr;
-  uint32_t* fids = nullptr;
+  EdgeSlot* edges = nullptr;  // cap_slots
+  uint32_t* fids = nullptr;   // 2 * cap_slots
   VocabSlot* vocab = nullptr;
   uint8_t* arena = nullptr;
-  TableView tv{};
-  uint64_t n_nodes = 0, n_slots = 0, n_words = 0, bytes = 0;
-  uint32_t max_depth = 0;
-  ~Snapshot() {
+  uint64_t cap_slots = 0, n_vocab = 0, cap_arena = 0;
+  uint64_t bytes() const {
+    return cap_slots * (sizeof(EdgeSlot) + 2 * sizeof(uint32_t)) + n_vocab * sizeof(VocabSlot) + cap_arena;
+  }
+  ~DeviceTables() {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
-    (void)hipDeviceSynchronize();  // an async call may still read this snapshot
+    (void)hipDeviceSynchronize();
     dfree(edges);
     dfree(fids);
     dfree(vocab);
     dfree(arena);
     (void)hipSetDevice(cur);
   }
+};
+
+// Lease on one delta region: a snapshot holds it while its walks may read the region; a
+// delta commit rewrites a region only when no snapshot but the writer's holds it.
+struct RegionLease {};
+
+struct Snapshot {
+  std::shared_ptr<DeviceTables> dt;
+  std::shared_ptr<RegionLease> region;  // the delta region tv.delta_* points into (or null)
+  TableView tv{};
+  uint64_t n_nodes = 0, n_slots = 0, n_words = 0, bytes = 0;
+  uint32_t max_depth = 0;
+};
+
+// Writer-side state of incremental commits (under emqx_engine::writer).  A filter is either
+// in the base trie (fixed at the last full build; deleting / re-inserting it flips its meta
+// flag in place) or in the delta trie (filters created after the build, rebuilt on every
+// commit into the delta region not in use).
+struct DeltaState {
+  bool valid = false;
+  std::shared_ptr<DeviceTables> dt;
+  std::unique_ptr<VocabState> vocab;
+  uint64_t base_slots = 0, region_slots = 0, base_n_ids = 0, base_nodes = 0, base_live = 0;
+  uint32_t base_depth = 0;
+  std::vector<uint64_t> loc;    // per id < base_n_ids: FIDLOC of its filter in the base
+  std::vector<uint8_t> on;      // ... whose flag is set on the device
+  std::vector<uint8_t> cand_flag;
+  std::vector<uint32_t> cand;   // ids that may live in the delta trie
+  std::shared_ptr<RegionLease> lease[2];
+  int next_region = 0;
+  uint32_t root_meta = 0;       // the base root's meta, '#' flag included
+  uint64_t delta_filters = 0;
 };
 
 constexpr uint32_t DEEP_WAVES = 32;
@@ -148,54 +186,221 @@ struct emqx_engine {
   std::atomic<double> last_kernel_ms{0};
   std::atomic<int> forced_variant{-1};
   std::atomic<bool> diag_on{false};
+  // incremental commits (under `writer`)
+  DeltaState ds;
+  std::vector<uint32_t> dirty;  // ids inserted / deleted since the last commit
+  bool incremental = true;      // emqx_set_tuning("incremental", 0|1)
+  int64_t delta_max = -1;       // emqx_set_tuning("delta_max", n): delta filters before a full
+                                // rebuild (-1: max(min(65536, base / 4), base / 16))
+  uint64_t last_commit_kind = 0;
 };
 
 namespace {
 
-int upload(emqx_engine* e, const HostTables& ht, std::shared_ptr<Snapshot>* out) {
+constexpr int EMQX_NEED_FULL = 1;  // internal: the incremental path cannot take this commit
+
+void publish(emqx_engine* e, std::shared_ptr<Snapshot> s) {
+  std::lock_guard<std::mutex> g(e->snap_mu);
+  e->snap = std::move(s);  // the old snapshot goes when its last reader returns
+}
+
+// Full rebuild: every live filter into a fresh base trie, uploaded into new device tables
+// with delta headroom; the old tables stay alive until their last reader returns.
+int full_commit(emqx_engine* e) {
+  auto vs = std::make_unique<VocabState>();
+  std::vector<uint64_t> loc;
+  BuildOpts o;
+  o.vocab = vs.get();
+  o.fid_loc = &loc;
+  HostTables ht;
+  std::string err;
+  if (!build_tables(e->store, o, ht, &err)) {
+    set_last_error(err.c_str());
+    return EMQX_ENOMEM;
+  }
+  const uint64_t n_slots = ht.edges.size();
+  const uint64_t region = std::max<uint64_t>(1u << 16, n_slots / 8);
+  auto dt = std::make_shared<DeviceTables>();
+  dt->device = e->device;
+  dt->cap_slots = std::min<uint64_t>(n_slots + 2 * region, MAX_SLOTS);
+  dt->n_vocab = ht.vocab.size();
+  dt->cap_arena = ht.arena.size() + std::max<uint64_t>(1u << 20, ht.arena.size() / 4) + 16;
+  HIP_TRY(dalloc(dt->edges, dt->cap_slots));
+  HIP_TRY(dalloc(dt->fids, 2 * dt->cap_slots));
+  HIP_TRY(dalloc(dt->vocab, dt->n_vocab));
+  HIP_TRY(dalloc(dt->arena, dt->cap_arena));
+  HIP_TRY(hipMemcpy(dt->edges, ht.edges.data(), n_slots * sizeof(EdgeSlot), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dt->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dt->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dt->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
+
   auto s = std::make_shared<Snapshot>();
-  s->device = e->device;
-  HIP_TRY(dalloc(s->edges, ht.edges.size()));
-  HIP_TRY(dalloc(s->fids, ht.fids.size()));
-  HIP_TRY(dalloc(s->vocab, ht.vocab.size()));
-  HIP_TRY(dalloc(s->arena, ht.arena.size() + 16));
-  HIP_TRY(hipMemcpy(s->edges, ht.edges.data(), ht.edges.size() * sizeof(EdgeSlot), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
-  s->tv.edges = s->edges;
-  s->tv.fids = s->fids;
-  s->tv.vocab = s->vocab;
-  s->tv.arena = s->arena;
+  s->dt = dt;
+  s->tv.edges = dt->edges;
+  s->tv.fids = dt->fids;
+  s->tv.vocab = dt->vocab;
+  s->tv.arena = dt->arena;
   s->tv.vocab_mask = ht.vocab_mask;
   s->tv.root_base = ht.root_base;
   s->tv.root_meta = ht.root_meta;
   s->tv.root_hash_fid = ht.root_hash_fid;
+  s->tv.delta_base = 0;
+  s->tv.delta_meta = 0;
+  s->tv.delta_hash_fid = FID_NONE;
   s->n_nodes = ht.n_nodes;
-  s->n_slots = ht.edges.size();
+  s->n_slots = n_slots;
   s->n_words = ht.n_words;
   s->max_depth = ht.max_depth;
-  s->bytes = ht.edges.size() * sizeof(EdgeSlot) + ht.fids.size() * sizeof(uint32_t) +
-             ht.vocab.size() * sizeof(VocabSlot) + ht.arena.size();
-  *out = std::move(s);
+  s->bytes = dt->bytes();
+
+  DeltaState& d = e->ds;
+  d.valid = dt->cap_slots == n_slots + 2 * region;
+  d.dt = dt;
+  d.vocab = std::move(vs);
+  d.base_slots = n_slots;
+  d.region_slots = region;
+  d.base_n_ids = e->store.n_ids();
+  d.base_live = e->store.n_live;
+  d.base_nodes = ht.n_nodes;
+  d.base_depth = ht.max_depth;
+  d.loc = std::move(loc);
+  d.on.assign(d.base_n_ids, 0);
+  for (uint64_t id = 0; id < d.base_n_ids; ++id) d.on[id] = d.loc[id] != FIDLOC_NONE;
+  d.cand_flag.assign(d.base_n_ids, 0);
+  d.cand.clear();
+  d.lease[0] = std::make_shared<RegionLease>();
+  d.lease[1] = std::make_shared<RegionLease>();
+  d.next_region = 0;
+  d.root_meta = ht.root_meta;
+  d.delta_filters = 0;
+  e->dirty.clear();
+  publish(e, std::move(s));
+  e->last_commit_kind = 0;
+  return EMQX_OK;
+}
+
+// Incremental commit: flips the meta flags of base filters deleted / re-inserted since the
+// last commit and rebuilds the (small) delta trie of the filters created since the last full
+// build into the delta region no reader holds.  EMQX_NEED_FULL when the delta outgrows its
+// region, the vocab or the arena headroom, or e->delta_max.
+int delta_commit(emqx_engine* e) {
+  DeltaState& d = e->ds;
+  const FilterStore& fs = e->store;
+  const uint64_t n_ids = fs.n_ids();
+  if (d.cand_flag.size() < n_ids) d.cand_flag.resize(n_ids, 0);
+  std::vector<uint2> patches;
+  uint32_t root_meta = d.root_meta;
+  std::vector<uint8_t> base_on = d.on;  // staged: committed only on success
+  for (uint32_t id : e->dirty) {
+    if (id < d.base_n_ids && d.loc[id] != FIDLOC_NONE) {
+      const uint8_t want = fs.live[id];
+      if (want == base_on[id]) continue;
+      base_on[id] = want;
+      const uint64_t l = d.loc[id];
+      if (l == FIDLOC_ROOT_HASH) {
+        root_meta = want ? (root_meta | META_HAS_HASH) : (root_meta & ~META_HAS_HASH);
+        continue;
+      }
+      const uint32_t bit = (l & 3) == FIDLOC_HASH ? META_HAS_HASH : META_HAS_TERM;
+      patches.push_back(make_uint2(static_cast<uint32_t>(l >> 2), bit | (want ? 0u : META_PATCH_CLEAR)));
+    } else if (!d.cand_flag[id]) {
+      d.cand_flag[id] = 1;
+      d.cand.push_back(id);
+    }
+  }
+  std::vector<uint32_t> ids;
+  for (uint32_t id : d.cand)
+    if (fs.live[id]) ids.push_back(id);
+  // default: a quarter of the base up to 64k filters, 1/16 of it beyond (an empty base always
+  // takes a full build: walks then start at one root)
+  const uint64_t cap = e->delta_max >= 0
+                           ? static_cast<uint64_t>(e->delta_max)
+                           : std::max<uint64_t>(std::min<uint64_t>(65536, d.base_live / 4), d.base_live / 16);
+  if (ids.size() > cap) return EMQX_NEED_FULL;
+
+  // the delta trie, into the region no published snapshot but the current one may hold
+  const int r = d.next_region;
+  const uint64_t nw0 = d.vocab->n_words(), arena0 = d.vocab->arena.size();
+  HostTables dh;
+  if (!ids.empty()) {
+    BuildOpts o;
+    o.ids = &ids;
+    o.slot_offset = d.base_slots + r * d.region_slots;
+    o.vocab = d.vocab.get();
+    o.vocab_table = false;
+    std::string err;
+    if (!build_tables(fs, o, dh, &err) || dh.edges.size() > d.region_slots) return EMQX_NEED_FULL;
+  }
+  std::vector<uint32_t> vdirty;
+  if (!d.vocab->insert_table(nw0, &vdirty) || d.vocab->arena.size() + 16 > d.dt->cap_arena) return EMQX_NEED_FULL;
+
+  // readers of region r (snapshots two commits old) must be gone, and their device work:
+  // drain the device, drop the async-call references idle workspaces keep, wait for the rest
+  HIP_TRY(hipDeviceSynchronize());
+  {
+    std::lock_guard<std::mutex> g(e->ws_mu);
+    for (Workspace* w : e->free_ws) w->inflight.reset();
+  }
+  while (d.lease[r].use_count() > 1) std::this_thread::yield();
+  HIP_TRY(hipDeviceSynchronize());
+  if (!ids.empty()) {
+    const uint64_t at = d.base_slots + r * d.region_slots;
+    HIP_TRY(hipMemcpy(d.dt->edges + at, dh.edges.data(), dh.edges.size() * sizeof(EdgeSlot), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d.dt->fids + 2 * at, dh.fids.data(), dh.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  if (d.vocab->arena.size() > arena0)
+    HIP_TRY(hipMemcpy(d.dt->arena + arena0, d.vocab->arena.data() + arena0, d.vocab->arena.size() - arena0,
+                      hipMemcpyHostToDevice));
+  for (uint32_t v : vdirty)
+    HIP_TRY(hipMemcpy(d.dt->vocab + v, &d.vocab->table[v], sizeof(VocabSlot), hipMemcpyHostToDevice));
+  if (!patches.empty()) {
+    uint2* dp = nullptr;
+    HIP_TRY(dalloc(dp, patches.size()));
+    HIP_TRY(hipMemcpy(dp, patches.data(), patches.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    HIP_TRY(launch_meta_patches(d.dt->edges, dp, static_cast<uint32_t>(patches.size()), nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+    dfree(dp);
+  }
+  HIP_TRY(hipDeviceSynchronize());
+
+  std::shared_ptr<Snapshot> cur;
+  {
+    std::lock_guard<std::mutex> g(e->snap_mu);
+    cur = e->snap;
+  }
+  auto s = std::make_shared<Snapshot>(*cur);
+  s->tv.root_meta = root_meta;
+  if (ids.empty()) {
+    s->region = nullptr;
+    s->tv.delta_base = 0;
+    s->tv.delta_meta = 0;
+    s->tv.delta_hash_fid = FID_NONE;
+  } else {
+    s->region = d.lease[r];
+    s->tv.delta_base = dh.root_base;
+    s->tv.delta_meta = dh.root_meta;
+    s->tv.delta_hash_fid = dh.root_hash_fid;
+  }
+  s->n_nodes = d.base_nodes + (ids.empty() ? 0 : dh.n_nodes);
+  s->n_slots = d.base_slots + dh.edges.size();
+  s->n_words = d.vocab->n_words();
+  s->max_depth = std::max(d.base_depth, dh.max_depth);
+  d.on.swap(base_on);
+  d.root_meta = root_meta;
+  d.delta_filters = ids.size();
+  d.next_region = 1 - r;
+  e->dirty.clear();
+  publish(e, std::move(s));
+  e->last_commit_kind = 1;
   return EMQX_OK;
 }
 
 int commit_locked(emqx_engine* e) {
   auto t0 = std::chrono::steady_clock::now();
-  HostTables ht;
-  std::string err;
-  if (!build_tables(e->store, ht, &err)) {
-    set_last_error(err.c_str());
-    return EMQX_ENOMEM;
-  }
-  std::shared_ptr<Snapshot> s;
-  int rc = upload(e, ht, &s);
+  int rc = EMQX_NEED_FULL;
+  if (e->incremental && e->ds.valid && e->snap) rc = delta_commit(e);
+  if (rc == EMQX_NEED_FULL) rc = full_commit(e);
   if (rc != EMQX_OK) return rc;
-  {
-    std::lock_guard<std::mutex> g(e->snap_mu);
-    e->snap = std::move(s);  // old snapshot freed when its last reader returns
-  }
   e->epoch += 1;
   e->last_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return EMQX_OK;
@@ -436,6 +641,7 @@ int emqx_insert_filters(emqx_engine* e, const uint8_t* bytes, const uint64_t* of
   for (uint64_t i = 0; i < n; ++i) {
     bool created = false;
     const uint32_t id = e->store.insert(bytes + offsets[i], offsets[i + 1] - offsets[i], &created);
+    e->dirty.push_back(id);
     if (ids_out) ids_out[i] = id;
   }
   return EMQX_OK;
@@ -449,7 +655,9 @@ int emqx_insert_filters_ext(emqx_engine* e, const uint8_t* bytes, const uint64_t
   for (uint64_t i = 0; i < n; ++i) {
     bool created = false;
     const uint32_t id = e->store.insert(bytes + offsets[i], offsets[i + 1] - offsets[i], &created);
+    if (e->store.ext[id] != ext_ids[i]) e->ds.valid = false;  // a changed report id: rebuild
     e->store.ext[id] = ext_ids[i];
+    e->dirty.push_back(id);
     if (ids_out) ids_out[i] = id;
   }
   return EMQX_OK;
@@ -463,6 +671,7 @@ int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n) {
     if (e->store.live[ids[i]]) {
       e->store.live[ids[i]] = 0;
       e->store.n_live -= 1;
+      e->dirty.push_back(ids[i]);
     }
   }
   return EMQX_OK;
@@ -608,6 +817,8 @@ int emqx_stats_get(emqx_engine* e, emqx_stats* out) {
     out->n_ids = e->store.n_ids();
     out->epoch = e->epoch;
     out->last_build_ms = e->last_build_ms;
+    out->delta_filters = e->ds.delta_filters;
+    out->last_commit_kind = e->last_commit_kind;
   }
   auto s = current(e);
   if (s) {
@@ -646,6 +857,16 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
   }
   if (std::strcmp(key, "diag") == 0) {
     e->diag_on.store(value != 0);
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "incremental") == 0) {
+    std::lock_guard<std::mutex> g(e->writer);
+    e->incremental = value != 0;
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "delta_max") == 0) {
+    std::lock_guard<std::mutex> g(e->writer);
+    e->delta_max = value;
     return EMQX_OK;
   }
   return EMQX_ENOTFOUND;

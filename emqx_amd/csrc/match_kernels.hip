@@ -27,6 +27,8 @@
 //   scan / scatter     counts -> CSR offsets; slab entries (references resolved) -> out_ids.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace emqx {
@@ -201,14 +203,15 @@ __device__ __forceinline__ bool probe_one(const EdgeSlot* edges, uint32_t base, 
 // walks literal/'+'/'#' edges; a final '#' is the node's hash filter.  Returns the fid or
 // FID_NONE.
 template <class WidAt>
-__device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at) {
-  uint32_t base = tv.root_base, meta = tv.root_meta, at = 0, term_inline = FID_NONE;
+__device__ uint32_t exact_walk1(const TableView& tv, uint32_t root_base, uint32_t root_meta, uint32_t root_hash_fid,
+                                uint32_t nlev, WidAt wid_at) {
+  uint32_t base = root_base, meta = root_meta, at = 0, term_inline = FID_NONE;
   bool root = true;
   for (uint32_t k = 0; k < nlev; ++k) {
     const uint32_t w = wid_at(k);
     if (w == WID_HASH && k + 1 == nlev) {
       if (!(meta & META_HAS_HASH)) return FID_NONE;
-      if (root) return tv.root_hash_fid;
+      if (root) return root_hash_fid;
       return (meta & META_HAS_EDGES) ? tv.fids[2u * at] : base;  // edgeless: inline in child_base
     }
     if (w == WID_NONE || !(meta & META_HAS_EDGES)) return FID_NONE;
@@ -222,6 +225,14 @@ __device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at)
   }
   if (root || !(meta & META_HAS_TERM)) return FID_NONE;
   return (meta & META_HAS_EDGES) ? tv.fids[2u * at + 1u] : term_inline;
+}
+
+// ... in the base trie, then in the delta trie (a live filter is in exactly one of them)
+template <class WidAt>
+__device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at) {
+  const uint32_t f = exact_walk1(tv, tv.root_base, tv.root_meta, tv.root_hash_fid, nlev, wid_at);
+  if (f != FID_NONE || !tv.delta_meta) return f;
+  return exact_walk1(tv, tv.delta_base, tv.delta_meta, tv.delta_hash_fid, nlev, wid_at);
 }
 
 // Item (8 B):  x = edge-array base of the node
@@ -654,11 +665,12 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   uint32_t evals = 0;     // per lane
   uint32_t dg[DIAG_NCOUNT] = {};  // diagnostic counters (per lane)
 
-  // root: '#' emission, exact walk of wildcard topics, the root item
+  // roots (the base trie's and, after incremental commits, the delta trie's): '#' emission,
+  // exact walk of wildcard topics, the root items
   {
-    bool e0 = false, e1 = false, push = false;
-    uint32_t g0 = 0, g1 = 0;
-    uint2 it = make_uint2(0, 0);
+    bool e0 = false, e1 = false, e2 = false, push = false, push2 = false;
+    uint32_t g1 = 0;
+    uint2 it = make_uint2(0, 0), it2 = make_uint2(0, 0);
     if (valid && !defer) {
       if (wild) {
         if (mode == MODE_ROUTES) {
@@ -667,29 +679,34 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
         }
       } else {
         evals = 1;  // the root visit, F_0
-        if (!dollar && (tv.root_meta & META_HAS_HASH)) {
-          e0 = true;  // filter '#'
-          g0 = tv.root_hash_fid;
-        }
+        // filter '#'; '$' rule (emqx_trie.erl:272-279): no root-level '+' or '#' for '$' topics
+        e0 = !dollar && (tv.root_meta & META_HAS_HASH);
+        e2 = !dollar && (tv.delta_meta & META_HAS_HASH);
         if (tv.root_meta & META_HAS_EDGES) {
           push = true;
-          // '$' rule (emqx_trie.erl:272-279): no root-level '+' or '#' for '$' topics
           const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
           it = make_item(tv.root_base, rmeta, dollar, false, lane, wbase);
         }
+        if (tv.delta_meta & META_HAS_EDGES) {
+          push2 = true;
+          const uint32_t dmeta = dollar ? (tv.delta_meta & ~META_HAS_PLUS) : tv.delta_meta;
+          it2 = make_item(tv.delta_base, dmeta, dollar, false, lane, wbase);
+        }
       }
     }
-    const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u);
+    const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u) + (e2 ? 1u : 0u);
     uint32_t tot;
     uint32_t pos = wave_prefix<2>(c, lane, &tot);
     const uint64_t tag = static_cast<uint64_t>(lane) << 32;
-    if (e0) { if (pos < cap) slab[pos] = tag | g0; ++pos; }
+    if (e0) { if (pos < cap) slab[pos] = tag | tv.root_hash_fid; ++pos; }
     if (e1) { if (pos < cap) slab[pos] = tag | g1; ++pos; }
+    if (e2) { if (pos < cap) slab[pos] = tag | tv.delta_hash_fid; ++pos; }
     if (c) L.cnt[lane] = c;
     cursor = tot;
     uint32_t ptot;
-    const uint32_t ppos = wave_prefix<1>(push ? 1u : 0u, lane, &ptot);
-    if (push) L.stack[ppos] = it;
+    uint32_t ppos = wave_prefix<2>((push ? 1u : 0u) + (push2 ? 1u : 0u), lane, &ptot);
+    if (push) L.stack[ppos++] = it;
+    if (push2) L.stack[ppos] = it2;
     top = ptot;
     maxtop = top;
     wave_sync();
@@ -966,12 +983,18 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     } else {
       if (lane == 0) evals = 1;
       const bool eh = lane == 0 && !dollar && (tv.root_meta & META_HAS_HASH);
-      emit(eh, tv.root_hash_fid, false, 0, false, 0, false, 0);
+      const bool dh = lane == 0 && !dollar && (tv.delta_meta & META_HAS_HASH);
+      emit(eh, tv.root_hash_fid, dh, tv.delta_hash_fid, false, 0, false, 0);
       if (tv.root_meta & META_HAS_EDGES) {
         const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
         if (lane == 0)
-          stack[0] = make_uint4(tv.root_base, rmeta, 0u, dollar ? 1u : 0u);  // {base, meta, widx, droot}
-        top = 1;
+          stack[top] = make_uint4(tv.root_base, rmeta, 0u, dollar ? 1u : 0u);  // {base, meta, widx, droot}
+        top += 1;
+      }
+      if (tv.delta_meta & META_HAS_EDGES) {
+        const uint32_t dmeta = dollar ? (tv.delta_meta & ~META_HAS_PLUS) : tv.delta_meta;
+        if (lane == 0) stack[top] = make_uint4(tv.delta_base, dmeta, 0u, dollar ? 1u : 0u);
+        top += 1;
       }
     }
     __threadfence_block();
@@ -1249,6 +1272,18 @@ __global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a) {
   }
 }
 
+// Incremental commits: set (bit 31 clear) or clear (bit 31 set) meta flag bits of slots —
+// tombstones and revivals of filters in the base trie.  One 32-bit atomic per patch, so a
+// concurrent walk sees each filter present or absent, never a torn slot.
+__global__ void meta_patch_kernel(EdgeSlot* edges, const uint2* patches, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint2 p = patches[i];
+    uint32_t* m = &edges[p.x].meta;
+    if (p.y & META_PATCH_CLEAR) atomicAnd(m, ~(p.y & ~META_PATCH_CLEAR));
+    else atomicOr(m, p.y);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Launch wrappers
 // ------------------------------------------------------------------------------------
@@ -1308,6 +1343,11 @@ hipError_t launch_assemble(const MatchArgs& a, hipStream_t s) {
   }
   hipLaunchKernelGGL(scatter_deep_kernel, dim3(64), dim3(256), 0, s, a);
   hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_meta_patches(EdgeSlot* edges, const uint2* patches, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(meta_patch_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 1024)), dim3(256), 0, s, edges, patches, n);
   return hipGetLastError();
 }
 

@@ -102,29 +102,6 @@ class EdgeMap {
   uint64_t size_ = 0;
 };
 
-struct VocabBuilder {
-  std::vector<uint8_t> arena;
-  std::vector<uint32_t> off{0};
-  std::vector<uint32_t> h32;
-  StrIdMap map;
-
-  uint32_t intern(const uint8_t* p, uint64_t n) {
-    uint64_t h = hash64_bytes(p, n);
-    auto res = [this](uint32_t id, const uint8_t*& q, uint64_t& m) {
-      q = arena.data() + off[id];
-      m = off[id + 1] - off[id];
-    };
-    uint32_t id = map.find(p, n, h, res);
-    if (id != WID_NONE) return id;
-    id = static_cast<uint32_t>(h32.size());
-    arena.insert(arena.end(), p, p + n);
-    off.push_back(static_cast<uint32_t>(arena.size()));
-    h32.push_back(word_hash_bytes(p, static_cast<uint32_t>(n)));
-    map.insert_new(h, id);
-    return id;
-  }
-};
-
 }  // namespace
 
 uint64_t hash64_bytes(const uint8_t* p, uint64_t n) {
@@ -168,6 +145,57 @@ void StrIdMap::insert_new(uint64_t h, uint32_t id) {
   ++size_;
 }
 
+uint32_t VocabState::intern(const uint8_t* p, uint64_t n) {
+  uint64_t h = hash64_bytes(p, n);
+  auto res = [this](uint32_t id, const uint8_t*& q, uint64_t& m) {
+    q = arena.data() + off[id];
+    m = off[id + 1] - off[id];
+  };
+  uint32_t id = map.find(p, n, h, res);
+  if (id != WID_NONE) return id;
+  id = static_cast<uint32_t>(h32.size());
+  arena.insert(arena.end(), p, p + n);
+  off.push_back(static_cast<uint32_t>(arena.size()));
+  h32.push_back(word_hash_bytes(p, static_cast<uint32_t>(n)));
+  map.insert_new(h, id);
+  return id;
+}
+
+namespace {
+void vocab_put(VocabState& v, uint64_t w, uint32_t* at) {
+  uint32_t i = vocab_slot0(v.h32[w]) & v.mask;
+  while (v.table[i].wid != WID_NONE) i = (i + 1) & v.mask;
+  VocabSlot& s = v.table[i];
+  s.hash = v.h32[w];
+  s.off = v.off[w];
+  s.len = v.off[w + 1] - v.off[w];
+  s.wid = static_cast<uint32_t>(w);
+  uint8_t tmp[16] = {0};
+  std::memcpy(tmp, v.arena.data() + s.off, std::min<uint32_t>(s.len, 16));
+  std::memcpy(s.inl, tmp, 16);
+  *at = i;
+}
+}  // namespace
+
+void VocabState::build_table() {
+  const uint64_t nw = n_words();
+  const uint64_t vcap = next_pow2(std::max<uint64_t>(nw * 3, 1024));  // load <= 1/3: room to grow
+  table.assign(vcap, VocabSlot{0, 0, WID_NONE, 0, {0, 0, 0, 0}});
+  mask = static_cast<uint32_t>(vcap - 1);
+  uint32_t at;
+  for (uint64_t w = 0; w < nw; ++w) vocab_put(*this, w, &at);
+}
+
+bool VocabState::insert_table(uint64_t from, std::vector<uint32_t>* dirty) {
+  if (n_words() * 2 > table.size()) return false;
+  uint32_t at;
+  for (uint64_t w = from; w < n_words(); ++w) {
+    vocab_put(*this, w, &at);
+    if (dirty) dirty->push_back(at);
+  }
+  return true;
+}
+
 uint32_t FilterStore::find(const uint8_t* p, uint64_t n) const {
   uint64_t h = hash64_bytes(p, n);
   auto res = [this](uint32_t id, const uint8_t*& q, uint64_t& m) {
@@ -203,20 +231,25 @@ uint32_t FilterStore::insert(const uint8_t* p, uint64_t n, bool* created) {
   return id;
 }
 
-bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
+bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out, std::string* err) {
   // ---- pass 1: intern words, build the level trie (old node ids) -----------------
-  VocabBuilder vb;
+  VocabState own;
+  VocabState& vb = opts.vocab ? *opts.vocab : own;
   vb.map.reserve(1024);
   EdgeMap em;
-  em.reserve(fs.n_live * 2 + 16);
+  const uint64_t n_sel = opts.ids ? opts.ids->size() : fs.n_live;
+  em.reserve(n_sel * 2 + 16);
   std::vector<uint32_t> depth{0}, n_edges{0};
   std::vector<uint8_t> has_plus{0}, term_wild{0};
   std::vector<uint32_t> hash_fid{FID_NONE}, term_fid{FID_NONE};
+  std::vector<uint32_t> hash_id{WID_NONE}, term_id{WID_NONE};  // engine ids (fid_loc)
   uint32_t max_depth = 0;
 
   const uint64_t n_ids = fs.n_ids();
-  for (uint64_t id = 0; id < n_ids; ++id) {
-    if (!fs.live[id]) continue;
+  const uint64_t n_iter = opts.ids ? opts.ids->size() : n_ids;
+  for (uint64_t k = 0; k < n_iter; ++k) {
+    const uint64_t id = opts.ids ? (*opts.ids)[k] : k;
+    if (id >= n_ids || !fs.live[id]) continue;
     const uint8_t* p = fs.bytes.data() + fs.off[id];
     const uint64_t n = fs.off[id + 1] - fs.off[id];
     // wildcard? (emqx_topic:wildcard/1)
@@ -242,6 +275,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       } else if (len == 1 && p[s] == '#') {
         if (i == n) {  // final '#': the parent level's hash filter
           hash_fid[node] = fs.ext[id];
+          hash_id[node] = static_cast<uint32_t>(id);
           ended_hash = true;
           break;
         }
@@ -265,6 +299,8 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
         term_wild.push_back(0);
         hash_fid.push_back(FID_NONE);
         term_fid.push_back(FID_NONE);
+        hash_id.push_back(WID_NONE);
+        term_id.push_back(WID_NONE);
         n_edges[node] += 1;
         if (wid == WID_PLUS) has_plus[node] = 1;
       }
@@ -273,6 +309,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     }
     if (!ended_hash) {
       term_fid[node] = fs.ext[id];
+      term_id[node] = static_cast<uint32_t>(id);
       term_wild[node] = wild ? 1 : 0;
     }
   }
@@ -431,7 +468,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       });
       for (uint32_t v : order)
         if (n_edges[v]) base[v] = static_cast<uint32_t>(place(caplog[v]));
-      if (total_slots > MAX_SLOTS) {
+      if (total_slots + opts.slot_offset > MAX_SLOTS) {
         if (err) *err = "edge slot array exceeds 2^31 slots";
         return false;
       }
@@ -446,7 +483,7 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
       stack.pop_back();
       for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
         if (n_edges[cid[j]]) base[cid[j]] = static_cast<uint32_t>(place(caplog[cid[j]]));
-      if (total_slots > MAX_SLOTS) {
+      if (total_slots + opts.slot_offset > MAX_SLOTS) {
         if (err) *err = "edge slot array exceeds 2^31 slots";
         return false;
       }
@@ -520,11 +557,18 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
   const uint64_t n_slots = std::max<uint64_t>(total_slots, 1);
   out.edges.assign(n_slots, EdgeSlot{WID_NONE, 0, 0, 0});
   out.fids.assign(2 * n_slots, FID_NONE);
+  const uint32_t off0 = static_cast<uint32_t>(opts.slot_offset);
+  if (opts.fid_loc) opts.fid_loc->assign(n_ids, FIDLOC_NONE);
   auto write_slot = [&](uint64_t at, uint32_t wid, uint32_t child) {
     EdgeSlot& r = out.edges[at];
     r.wid = wid;
     const bool leaf = n_edges[child] == 0;
-    r.child_base = leaf ? hash_fid[child] : base[child];
+    r.child_base = leaf ? hash_fid[child] : off0 + base[child];
+    if (opts.fid_loc) {
+      const uint64_t abs = opts.slot_offset + at;
+      if (hash_id[child] != WID_NONE) (*opts.fid_loc)[hash_id[child]] = abs << 2 | FIDLOC_HASH;
+      if (term_id[child] != WID_NONE) (*opts.fid_loc)[term_id[child]] = abs << 2 | FIDLOC_TERM;
+    }
     r.meta = meta_of(child) | (r.meta & META_BUCKET_OVF);
     r.litf = leaf ? term_fid[child] : lf[child];
     out.fids[2 * at] = hash_fid[child];
@@ -557,33 +601,23 @@ bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
     }
   }
   out.root_hash_fid = hash_fid[0];
-  out.root_base = base[0];
+  if (opts.fid_loc && hash_id[0] != WID_NONE) (*opts.fid_loc)[hash_id[0]] = FIDLOC_ROOT_HASH;
+  out.root_base = off0 + base[0];
+  out.slot_offset = opts.slot_offset;
   out.root_meta = meta_of(0);
   out.n_nodes = n_nodes;
   out.max_depth = max_depth;
   for (uint64_t v = 0; v < n_nodes; ++v) out.n_ph_nodes += ph[v];
 
   // ---- vocab device table ----------------------------------------------------------
-  const uint64_t nw = vb.h32.size();
-  const uint64_t vcap = next_pow2(std::max<uint64_t>(nw * 2, 2));
-  out.vocab.assign(vcap, VocabSlot{0, 0, WID_NONE, 0, {0, 0, 0, 0}});
-  out.vocab_mask = static_cast<uint32_t>(vcap - 1);
-  for (uint64_t w = 0; w < nw; ++w) {
-    const uint32_t h = vb.h32[w];
-    uint32_t i = vocab_slot0(h) & out.vocab_mask;
-    while (out.vocab[i].wid != WID_NONE) i = (i + 1) & out.vocab_mask;
-    VocabSlot& s = out.vocab[i];
-    s.hash = h;
-    s.off = vb.off[w];
-    s.len = vb.off[w + 1] - vb.off[w];
-    s.wid = static_cast<uint32_t>(w);
-    uint8_t tmp[16] = {0};
-    std::memcpy(tmp, vb.arena.data() + s.off, std::min<uint32_t>(s.len, 16));
-    std::memcpy(s.inl, tmp, 16);
+  out.n_words = vb.n_words();
+  if (opts.vocab_table) {
+    vb.build_table();
+    out.vocab = vb.table;
+    out.vocab_mask = vb.mask;
+    out.arena = vb.arena;
+    if (out.arena.empty()) out.arena.push_back(0);
   }
-  out.arena.swap(vb.arena);
-  if (out.arena.empty()) out.arena.push_back(0);
-  out.n_words = nw;
   return true;
 }
 
@@ -605,7 +639,7 @@ bool check_tables(const HostTables& t, std::string* err) {
     const bool ph = (meta & META_PH) != 0;
     uint32_t n_lit = 0;
     for (uint32_t i = 0; i <= mask; ++i) {
-      const EdgeSlot& s = t.edges[base + i];
+      const EdgeSlot& s = t.edges[base - t.slot_offset + i];
       if (s.wid == WID_NONE) continue;
       if (s.wid == WID_PLUS) {
         if (i != 0 || !(meta & META_HAS_PLUS)) {
@@ -620,14 +654,14 @@ bool check_tables(const HostTables& t, std::string* err) {
       else {
         const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u, nbm = mask / 2;
         const uint32_t b1 = bucket1(s.wid, sd, nbm), b2 = bucket2(s.wid, sd, nbm);
-        found = i / 2 == b1 || (i / 2 == b2 && (t.edges[base + 2 * b1].meta & META_BUCKET_OVF));
+        found = i / 2 == b1 || (i / 2 == b2 && (t.edges[base - t.slot_offset + 2 * b1].meta & META_BUCKET_OVF));
       }
       if (!found) {
         if (err) *err = "edge not at its lookup slot";
         return false;
       }
     }
-    if ((meta & META_HAS_PLUS) && t.edges[base].wid != WID_PLUS) {
+    if ((meta & META_HAS_PLUS) && t.edges[base - t.slot_offset].wid != WID_PLUS) {
       if (err) *err = "missing '+' edge";
       return false;
     }
@@ -652,7 +686,7 @@ bool check_tables(const HostTables& t, std::string* err) {
     if (s.wid == WID_NONE || !(s.meta & META_HAS_EDGES)) continue;
     const uint32_t mask = (1u << (s.meta & META_CAPLOG2_MASK)) - 1u;
     for (uint32_t j = 0; j <= mask; ++j) {
-      const EdgeSlot& c = t.edges[s.child_base + j];
+      const EdgeSlot& c = t.edges[s.child_base - t.slot_offset + j];
       if (c.wid == WID_NONE || c.wid == WID_PLUS) continue;
       if (!litf_may_contain(s.meta, s.litf, c.wid)) {
         if (err) *err = "literal filter rejects a present word";

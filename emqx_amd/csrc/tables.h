@@ -63,6 +63,39 @@ struct FilterStore {
   uint32_t insert(const uint8_t* p, uint64_t n, bool* created);
 };
 
+// Word interner that outlives a build: incremental (delta) builds keep interning into it so
+// word ids stay those of the device vocab, and `table` is the host image of that vocab.
+struct VocabState {
+  std::vector<uint8_t> arena;
+  std::vector<uint32_t> off{0};
+  std::vector<uint32_t> h32;  // word_hash_bytes per word id
+  StrIdMap map;
+  std::vector<VocabSlot> table;
+  uint32_t mask = 0;
+
+  uint32_t intern(const uint8_t* p, uint64_t n);
+  uint64_t n_words() const { return h32.size(); }
+  // (Re)builds `table` for every word, at 2x load headroom.
+  void build_table();
+  // Inserts words [from, n_words()) into `table`; dirty slot indices appended.  False when
+  // the load would exceed 1/2 (the caller rebuilds everything).
+  bool insert_table(uint64_t from, std::vector<uint32_t>* dirty);
+};
+
+// Where a filter's id lives in a built trie: slot << 2 | kind (FIDLOC_HASH / FIDLOC_TERM:
+// the META_HAS_HASH / META_HAS_TERM flag of that slot), FIDLOC_ROOT_HASH (the root's '#'
+// filter, in the table view), or FIDLOC_NONE.
+constexpr uint64_t FIDLOC_HASH = 0, FIDLOC_TERM = 1;
+constexpr uint64_t FIDLOC_ROOT_HASH = ~0ull - 1, FIDLOC_NONE = ~0ull;
+
+struct BuildOpts {
+  const std::vector<uint32_t>* ids = nullptr;  // filters to include (null: every live filter)
+  uint64_t slot_offset = 0;                    // the trie's arrays start at this slot
+  VocabState* vocab = nullptr;                 // persistent interner (null: a private one)
+  bool vocab_table = true;                     // build the vocab table into HostTables
+  std::vector<uint64_t>* fid_loc = nullptr;    // out: per filter id (sized n_ids)
+};
+
 struct HostTables {
   std::vector<EdgeSlot> edges;
   std::vector<uint32_t> fids;  // 2 * edges.size() (see EdgeSlot)
@@ -76,10 +109,14 @@ struct HostTables {
   uint64_t n_words = 0;
   uint32_t max_depth = 0;
   uint64_t n_ph_nodes = 0;
+  uint64_t slot_offset = 0;  // edges[i] is slot slot_offset + i (child_base values are absolute)
 };
 
-// Builds the level trie of every live filter.  Returns false on size overflow.
-bool build_tables(const FilterStore& fs, HostTables& out, std::string* err);
+// Builds the level trie of the selected live filters.  Returns false on size overflow.
+bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out, std::string* err);
+inline bool build_tables(const FilterStore& fs, HostTables& out, std::string* err) {
+  return build_tables(fs, BuildOpts{}, out, err);
+}
 // Verifies the lookup invariants of a built table (host-side; used by tests).
 bool check_tables(const HostTables& t, std::string* err);
 

@@ -83,6 +83,8 @@ typedef struct emqx_stats {
   double last_build_ms;      /* host build time of the last commit                           */
   double last_match_ms;      /* device time of the last match call (hipEvent)                */
   double last_kernel_ms;     /* device time of its fused match kernel alone (hipEvent)       */
+  uint64_t delta_filters;    /* filters in the delta trie (created since the last full build)*/
+  uint64_t last_commit_kind; /* 0 = full rebuild, 1 = incremental (flag flips + delta trie)  */
 } emqx_stats;
 
 /* Lifecycle. */
@@ -103,7 +105,11 @@ int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n);
 int emqx_lookup_filter(emqx_engine* e, const uint8_t* bytes, uint64_t len, uint32_t* id_out);
 /* Copies the bytes of filter `id` into buf (cap bytes); *len_out = its length. */
 int emqx_filter_name(emqx_engine* e, uint32_t id, uint8_t* buf, uint64_t cap, uint64_t* len_out);
-/* Rebuilds the device tables from the live filter set and publishes them (epoch swap). */
+/* Publishes every insert/delete since the last commit (epoch swap; in-flight matches keep
+ * the snapshot they started with).  Incremental by default: a deleted / re-inserted filter
+ * of the last full build flips a meta flag of its slot in place, filters created since then
+ * live in a small delta trie rebuilt per commit; a full rebuild runs when the delta outgrows
+ * its headroom (emqx_set_tuning "delta_max", "incremental" = 0 forces full rebuilds). */
 int emqx_commit(emqx_engine* e);
 
 /* Batched match, host buffers.  out_offsets has n+1 entries.  On EMQX_EOVERFLOW nothing
