@@ -61,10 +61,14 @@ def main():
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
-    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E"],
+    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U"],
                     help="B = the headline (BASELINE configs[1]); A = configs[0]'s 100k-filter table, "
                          "D = the adversarial depth-16 table (configs[3], 100k-topic batches), "
-                         "E = publish fan-out (configs[4]): match + fan-out per step")
+                         "E = publish fan-out (configs[4]): match + fan-out per step, "
+                         "U = route updates (SURVEY §8 f2): subscribe/unsubscribe churn + incremental "
+                         "commits on config B's table")
+    ap.add_argument("--churn", type=int, default=10_000, help="--workload U: inserts and deletes per commit")
+    ap.add_argument("--rounds", type=int, default=10, help="--workload U: commits timed")
     ap.add_argument("--strategy", type=str, default="hash_clientid",
                     help="$share strategy for --workload E")
     ap.add_argument("--sharded", action="store_true",
@@ -95,6 +99,8 @@ def main():
         return sharded_bench(args, rank, world, dev)
     if args.workload == "E":
         return fanout_bench(args, rank, world, dev)
+    if args.workload == "U":
+        return update_bench(args, rank, world, dev)
     if args.workload == "A":
         wl = load_or_make(args, rank, lambda: W.config_a(n_topics=args.batch, seed=1 if rank == 0 else 1000 + rank))
     elif args.workload == "D":
@@ -437,6 +443,161 @@ def fanout_cpu_baseline(fw, args):
     return {"value": round(sample / dt, 1), "unit": "topics/s", "cores": 1, "kind": "port",
             "sample": f"first {sample} topics; C++ DFS match + Python dict fan-out, one thread",
             "deliveries_per_topic": round(nd / sample, 3)}
+
+
+def update_bench(args, rank, world, dev):
+    """Route updates (emqx_router:do_add_route/do_delete_route ->
+    emqx_trie:insert/delete in a mria transaction, emqx_router_utils.erl:33-70): on config B's
+    10M-filter table, each step unsubscribes `churn` random live filters, subscribes `churn`
+    new ones and commits (incremental: base-slot flag flips + a rebuilt delta trie).  value =
+    (inserts + deletes) / (time of the ops and their commits).  After the last commit the batch
+    is matched with the delta present and again after a full rebuild: the two CSRs must be
+    identical (ids sorted per topic), and both throughputs are reported."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    k, R = args.churn, args.rounds
+    t0 = time.time()
+    wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters + (R + 1) * k, n_topics=args.batch,
+                                                     seed=2, topic_seed=None if rank == 0 else 1000 + rank))
+    nb = wl.n_filters - (R + 1) * k
+    base = W.take(wl.filters, np.arange(nb))
+    log(f"[rank {rank}] workload: {nb} base filters + {(R + 1) * k} to subscribe ({time.time() - t0:.1f}s)")
+    eng = Engine(dev.index)
+    eng.insert_packed(*base)
+    eng.commit()
+    full_ms = eng.stats()["last_build_ms"]
+    rng = np.random.default_rng(7 + rank)
+    live = np.ones(nb, dtype=bool)
+    nxt = nb
+
+    def churn_once():
+        nonlocal nxt
+        dels = np.sort(rng.choice(np.nonzero(live)[0], k, replace=False)).astype(np.uint32)
+        adds = W.take(wl.filters, np.arange(nxt, nxt + k))
+        nxt += k
+        t = time.perf_counter()
+        eng.delete(dels)
+        ids = eng.insert_packed(*adds)
+        eng.commit()
+        dt = time.perf_counter() - t
+        live[dels[dels < nb]] = False
+        return dt, ids
+
+    churn_once()  # warm-up commit (first delta region)
+    if world > 1:
+        dist.barrier()
+    times, kinds, commit_ms = [], [], []
+    for _ in range(R):
+        dt, _ = churn_once()
+        st = eng.stats()
+        times.append(dt)
+        kinds.append(st["last_commit_kind"])
+        commit_ms.append(st["last_build_ms"])
+    elapsed = float(np.sum(times))
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if not all(x == 1 for x in kinds):
+        raise SystemExit(f"expected incremental commits, got kinds {kinds}")
+    delta_filters = eng.stats()["delta_filters"]
+
+    tb = torch.from_numpy(wl.topics[0]).to(dev)
+    to = torch.from_numpy(wl.topics[1].view(np.int64)).to(dev)
+    n = wl.n_topics
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def match_rate():
+        d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cap = max(64 * n, 1 << 20)
+        d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+        nout = eng.match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
+                                mode=0, stream=stream)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            eng.match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
+                             mode=0, stream=stream)
+        torch.cuda.synchronize()
+        rate = n * args.steps / (time.perf_counter() - t)
+        off = d_off.cpu().numpy()
+        ids = d_ids[:nout].cpu().numpy().view(np.uint32).astype(np.int64)
+        topic = np.repeat(np.arange(n, dtype=np.int64), np.diff(off))
+        key = np.sort(topic << 32 | ids)  # per-topic sorted id sets, as one array
+        return rate, eng.stats()["last_kernel_ms"], off, key
+
+    rate_delta, kms_delta, off_d, key_d = match_rate()
+    eng.set_tuning("incremental", 0)
+    eng.commit()
+    rebuild_ms = eng.stats()["last_build_ms"]
+    rate_full, kms_full, off_f, key_f = match_rate()
+    if not (np.array_equal(off_d, off_f) and np.array_equal(key_d, key_f)):
+        raise SystemExit("match CSR with the delta trie differs from the one after a full rebuild")
+
+    value = 2.0 * k * R * world / elapsed
+    result = {
+        "metric": "route updates committed/sec (subscribe + unsubscribe, incremental commit) at 10M subs",
+        "value": round(value, 1),
+        "unit": "updates/s",
+        "n_gpus": world,
+        "steps": R,
+        "warmup": 1,
+        "ms_per_step": round(1e3 * elapsed / R, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "U: config B table, churn of subscribe/unsubscribe batches with a commit each",
+                   "n_filters": nb, "churn_per_commit": k, "commits": R,
+                   "parallelism": f"replicated table x{world} (each rank commits its own copy)"},
+        "commit_ms_avg": round(float(np.mean(commit_ms)), 3),
+        "commit_ms_max": round(float(np.max(commit_ms)), 3),
+        "full_rebuild_ms": round(min(full_ms, rebuild_ms), 1),
+        "delta_filters_at_end": delta_filters,
+        "match_topics_per_s_with_delta": round(rate_delta, 1),
+        "match_topics_per_s_after_rebuild": round(rate_full, 1),
+        "kernel_ms_with_delta": round(kms_delta, 4),
+        "kernel_ms_after_rebuild": round(kms_full, 4),
+        "parity": "CSR with delta == CSR after full rebuild (per-topic sorted ids)",
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = update_cpu_baseline(wl, nb, k, args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def update_cpu_baseline(wl, nb, k, args):
+    """emqx_trie:insert/delete (refcounted TOPIC/PREFIX keys in one ordered key set,
+    oracle/trie_oracle.cpp) for the same churn, one thread: a bounded number of rounds on a
+    table of the first min(nb, 2M) base filters (the ordered-set cost grows with log N)."""
+    from emqx_amd import workloads as W
+    from oracle import cpp as C
+    nbase = min(nb, 2_000_000)
+    o = C.CppOracle(True)
+    o.add_packed(*W.take(wl.filters, np.arange(nbase)))
+    rng = np.random.default_rng(11)
+    pool = wl.n_filters - k
+    t_total, ops, r = 0.0, 0, 0
+    while t_total < 10.0 and r < 20:
+        dels = W.unpack(wl.filters, rng.choice(nbase, k, replace=False))
+        adds = W.take(wl.filters, np.arange(pool, pool + k))
+        t = time.perf_counter()
+        o.delete(dels)
+        o.add_packed(*adds)
+        t_total += time.perf_counter() - t
+        o.delete(W.unpack(adds))
+        o.add(dels)
+        ops += 2 * k
+        r += 1
+    return {"value": round(ops / t_total, 1), "unit": "updates/s", "cores": 1, "kind": "port",
+            "sample": f"{r} rounds of {k} deletes + {k} inserts on a {nbase}-filter table (C++ restatement "
+                      "of emqx_trie:insert/delete key maintenance, no mnesia transaction)"}
 
 
 def load_or_make(args, rank, make):
