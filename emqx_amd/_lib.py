@@ -37,6 +37,12 @@ EXPORTS = (
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
     "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_publish_batch",
 )
+# Every symbol include/emqx_retain.h declares (retained-message index).
+RETAIN_EXPORTS = (
+    "emqx_retain_create", "emqx_retain_destroy", "emqx_retain_store", "emqx_retain_delete",
+    "emqx_retain_lookup", "emqx_retain_topic", "emqx_retain_expired", "emqx_retain_commit",
+    "emqx_retain_match_batch", "emqx_retain_match_batch_device", "emqx_retain_stats_get",
+)
 
 NO_GROUP = 0xFFFFFFFF
 FANOUT_SHARED_BIT = 0x80000000
@@ -63,6 +69,18 @@ class Stats(ctypes.Structure):
         ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double),
         ("last_kernel_ms", ctypes.c_double),
         ("delta_filters", ctypes.c_uint64), ("last_commit_kind", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class RetainStats(ctypes.Structure):
+    _fields_ = [
+        ("n_ids", ctypes.c_uint64), ("n_live", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64),
+        ("n_words", ctypes.c_uint64), ("table_bytes", ctypes.c_uint64), ("epoch", ctypes.c_uint64),
+        ("last_ranges", ctypes.c_uint64), ("last_visits", ctypes.c_uint64), ("last_total", ctypes.c_uint64),
+        ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double), ("last_walk_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -115,6 +133,18 @@ def lib():
         "emqx_subtab_stats": (i32, [vp, vp]),
         "emqx_fanout_batch_device": (i32, [vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
         "emqx_publish_batch": (i32, [vp, vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_retain_create": (i32, [ctypes.c_int32, ctypes.POINTER(vp)]),
+        "emqx_retain_destroy": (i32, [vp]),
+        "emqx_retain_store": (i32, [vp, vp, vp, u64, vp, vp]),
+        "emqx_retain_delete": (i32, [vp, vp, u64]),
+        "emqx_retain_lookup": (i32, [vp, vp, u64, ctypes.POINTER(u32)]),
+        "emqx_retain_topic": (i32, [vp, u32, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_retain_expired": (i32, [vp, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_retain_commit": (i32, [vp]),
+        "emqx_retain_match_batch": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_retain_match_batch_device": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64,
+                                                 ctypes.POINTER(u64), vp]),
+        "emqx_retain_stats_get": (i32, [vp, ctypes.POINTER(RetainStats)]),
         "emqx_strerror": (ctypes.c_char_p, [i32]),
         "emqx_version": (ctypes.c_char_p, []),
     }

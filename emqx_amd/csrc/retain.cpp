@@ -1,0 +1,673 @@
+// C ABI of the retained-message index (include/emqx_retain.h): host topic store, trie build
+// with DFS-preorder ranks, snapshot upload/swap, and the match pipeline
+//   walk -> [D2H: ranges emitted] -> count -> scan -> [D2H: total] -> write.
+// Reference semantics: apps/emqx_retainer/src/emqx_retainer_mnesia.erl (see retain.h and
+// oracle/retain_ref.py).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/emqx_retain.h"
+#include "kernels.h"
+#include "retain.h"
+#include "tables.h"
+
+using namespace emqx;
+
+namespace {
+
+#define RT_TRY(expr)                             \
+  do {                                           \
+    hipError_t _e = (expr);                      \
+    if (_e != hipSuccess) return EMQX_EDEVICE;   \
+  } while (0)
+
+template <class T>
+void rfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+template <class T>
+hipError_t ralloc(T*& p, uint64_t count) {
+  rfree(p);
+  return hipMalloc(reinterpret_cast<void**>(&p), std::max<uint64_t>(count, 1) * sizeof(T));
+}
+
+// Device arrays of one committed snapshot (freed after draining the device).
+struct RSnapshot {
+  int device = 0;
+  RNode* nodes = nullptr;
+  REdge* edges = nullptr;
+  VocabSlot* vocab = nullptr;
+  uint8_t* arena = nullptr;
+  uint32_t* rank_id = nullptr;
+  int64_t* rank_exp = nullptr;
+  RetainView rv{};
+  uint64_t n_nodes = 0, n_words = 0, bytes = 0;
+  ~RSnapshot() {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
+    rfree(nodes);
+    rfree(edges);
+    rfree(vocab);
+    rfree(arena);
+    rfree(rank_id);
+    rfree(rank_exp);
+    (void)hipSetDevice(cur);
+  }
+};
+
+// Per-call scratch, grown on demand (one per concurrent caller).
+struct RWork {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evw = nullptr;
+  uint32_t* wids = nullptr;
+  uint64_t wids_cap = 0;
+  uint4* stack = nullptr;
+  uint64_t stack_items = 0;
+  uint32_t stack_cap = 4096;  // items per wave (grows on overflow)
+  RRange* ranges = nullptr;
+  uint32_t* rcount = nullptr;
+  uint32_t range_cap = 0;
+  uint32_t* ctrl = nullptr;
+  uint32_t* fcount = nullptr;
+  uint32_t* fcursor = nullptr;
+  uint64_t f_cap = 0;
+  uint64_t* partials = nullptr;
+  uint64_t partials_cap = 0;
+  uint64_t* h_pinned = nullptr;  // [8] readbacks
+  // host-API staging (device copies of the caller's buffers)
+  uint8_t* d_fb = nullptr;
+  uint64_t d_fb_cap = 0;
+  uint64_t* d_fo = nullptr;
+  uint64_t* d_oo = nullptr;
+  uint64_t d_n_cap = 0;
+  uint32_t* d_ids = nullptr;
+  uint64_t d_ids_cap = 0;
+  ~RWork() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    rfree(wids);
+    rfree(stack);
+    rfree(ranges);
+    rfree(rcount);
+    rfree(ctrl);
+    rfree(fcount);
+    rfree(fcursor);
+    rfree(partials);
+    rfree(d_fb);
+    rfree(d_fo);
+    rfree(d_oo);
+    rfree(d_ids);
+    if (h_pinned) (void)hipHostFree(h_pinned);
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (evw) (void)hipEventDestroy(evw);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+constexpr uint32_t MAX_WAVES = 2048;
+
+bool has_wild_level(const uint8_t* p, uint64_t n) {
+  uint64_t s = 0;
+  for (uint64_t i = 0; i <= n; ++i) {
+    if (i == n || p[i] == '/') {
+      if (i - s == 1 && (p[s] == '+' || p[s] == '#')) return true;
+      s = i + 1;
+    }
+  }
+  return false;
+}
+
+}  // namespace
+
+struct emqx_retain {
+  int device = 0;
+  std::mutex writer;
+  FilterStore store;           // topic bytes <-> id, liveness
+  std::vector<int64_t> expiry;  // per id
+  uint64_t epoch = 0;
+  double last_build_ms = 0;
+  std::mutex snap_mu;
+  std::shared_ptr<RSnapshot> snap;
+  std::mutex ws_mu;
+  std::vector<RWork*> free_ws;
+  std::vector<std::unique_ptr<RWork>> all_ws;
+  std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0};
+  std::atomic<double> last_match_ms{0}, last_walk_ms{0};
+};
+
+namespace {
+
+// Builds the trie of the live topics: BFS node ids (contiguous children), DFS preorder ranks.
+int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
+  const FilterStore& fs = r->store;
+  VocabState vs;
+  // pass 1: temporary trie, children as (parent, wid) -> node in a hash map
+  std::vector<uint32_t> first_child{WID_NONE}, next_sib{WID_NONE}, term{WID_NONE}, wid_of{WID_NONE};
+  std::vector<uint64_t> hkeys;
+  std::vector<uint32_t> hvals;
+  uint64_t hmask = 0, hsize = 0;
+  auto hrehash = [&](uint64_t cap) {
+    std::vector<uint64_t> ok;
+    std::vector<uint32_t> ov;
+    ok.swap(hkeys);
+    ov.swap(hvals);
+    hkeys.assign(cap, ~0ull);
+    hvals.assign(cap, 0);
+    hmask = cap - 1;
+    for (uint64_t i = 0; i < ok.size(); ++i) {
+      if (ok[i] == ~0ull) continue;
+      uint64_t j = (ok[i] * 0x9E3779B97F4A7C15ull >> 20) & hmask;
+      while (hkeys[j] != ~0ull) j = (j + 1) & hmask;
+      hkeys[j] = ok[i];
+      hvals[j] = ov[i];
+    }
+  };
+  hrehash(1024);
+  auto child_of = [&](uint32_t parent, uint32_t wid) -> uint32_t {
+    const uint64_t key = static_cast<uint64_t>(parent) << 32 | wid;
+    uint64_t j = (key * 0x9E3779B97F4A7C15ull >> 20) & hmask;
+    while (hkeys[j] != ~0ull) {
+      if (hkeys[j] == key) return hvals[j];
+      j = (j + 1) & hmask;
+    }
+    const uint32_t c = static_cast<uint32_t>(term.size());
+    first_child.push_back(WID_NONE);
+    term.push_back(WID_NONE);
+    wid_of.push_back(wid);
+    next_sib.push_back(first_child[parent]);
+    first_child[parent] = c;
+    hkeys[j] = key;
+    hvals[j] = c;
+    if (++hsize * 2 > hkeys.size()) hrehash(hkeys.size() * 2);
+    return c;
+  };
+  const uint64_t n_ids = fs.n_ids();
+  for (uint64_t id = 0; id < n_ids; ++id) {
+    if (!fs.live[id]) continue;
+    const uint8_t* p = fs.bytes.data() + fs.off[id];
+    const uint64_t n = fs.off[id + 1] - fs.off[id];
+    uint32_t node = 0;
+    uint64_t s = 0;
+    for (uint64_t i = 0; i <= n; ++i) {
+      if (i == n || p[i] == '/') {
+        node = child_of(node, vs.intern(p + s, i - s));
+        s = i + 1;
+      }
+    }
+    term[node] = static_cast<uint32_t>(id);
+  }
+  const uint64_t nn = term.size();
+  if (nn >= 0x7FFFFFFFull) return EMQX_ENOMEM;
+  // pass 2: BFS ids (children contiguous)
+  std::vector<uint32_t> order;  // bfs index -> temp node
+  order.reserve(nn);
+  std::vector<RNode> nodes(nn);
+  order.push_back(0);
+  for (uint64_t k = 0; k < order.size(); ++k) {
+    const uint32_t v = order[k];
+    const uint32_t cb = static_cast<uint32_t>(order.size());
+    uint32_t nc = 0;
+    for (uint32_t c = first_child[v]; c != WID_NONE; c = next_sib[c]) {
+      order.push_back(c);
+      ++nc;
+    }
+    nodes[k].cbeg = cb;
+    nodes[k].ncld = nc | (term[v] != WID_NONE ? RNODE_TERM : 0u);
+  }
+  // pass 3: DFS preorder ranks (a node's own topic, then its children's subtrees)
+  std::vector<uint32_t> rank_id;
+  rank_id.reserve(fs.n_live);
+  {
+    std::vector<std::pair<uint32_t, uint32_t>> st;  // (bfs node, next child index)
+    st.push_back({0, 0});
+    nodes[0].lo = 0;
+    while (!st.empty()) {
+      auto& [v, ci] = st.back();
+      RNode& rn = nodes[v];
+      const uint32_t nc = rn.ncld & ~RNODE_TERM;
+      if (ci < nc) {
+        const uint32_t c = rn.cbeg + ci;
+        ++ci;
+        RNode& cn = nodes[c];
+        cn.lo = static_cast<uint32_t>(rank_id.size());
+        if (cn.ncld & RNODE_TERM) rank_id.push_back(term[order[c]]);
+        st.push_back({c, 0});
+      } else {
+        rn.hi = static_cast<uint32_t>(rank_id.size());
+        st.pop_back();
+      }
+    }
+  }
+  std::vector<int64_t> rank_exp(rank_id.size());
+  uint32_t has_exp = 0;
+  for (uint64_t i = 0; i < rank_id.size(); ++i) {
+    rank_exp[i] = r->expiry[rank_id[i]];
+    has_exp |= rank_exp[i] != 0;
+  }
+  // literal lookup table (parent, wid) -> child
+  uint64_t ecap = 1024;
+  while (ecap < 2 * nn) ecap <<= 1;
+  std::vector<REdge> edges(ecap, REdge{WID_NONE, 0, 0, 0});
+  const uint32_t emask = static_cast<uint32_t>(ecap - 1);
+  for (uint64_t v = 0; v < nn; ++v) {
+    const uint32_t nc = nodes[v].ncld & ~RNODE_TERM;
+    for (uint32_t j = 0; j < nc; ++j) {
+      const uint32_t c = nodes[v].cbeg + j;
+      const uint32_t w = wid_of[order[c]];
+      uint32_t s = redge_slot0(static_cast<uint32_t>(v), w) & emask;
+      while (edges[s].parent != WID_NONE) s = (s + 1) & emask;
+      edges[s] = REdge{static_cast<uint32_t>(v), w, c, 0};
+    }
+  }
+  vs.build_table();
+
+  auto sn = std::make_shared<RSnapshot>();
+  sn->device = r->device;
+  const uint64_t nr = std::max<uint64_t>(rank_id.size(), 1);
+  RT_TRY(ralloc(sn->nodes, nn));
+  RT_TRY(ralloc(sn->edges, ecap));
+  RT_TRY(ralloc(sn->vocab, vs.table.size()));
+  RT_TRY(ralloc(sn->arena, vs.arena.size() + 16));
+  RT_TRY(ralloc(sn->rank_id, nr));
+  RT_TRY(ralloc(sn->rank_exp, nr));
+  RT_TRY(hipMemcpy(sn->nodes, nodes.data(), nn * sizeof(RNode), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->edges, edges.data(), ecap * sizeof(REdge), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->vocab, vs.table.data(), vs.table.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
+  if (!vs.arena.empty()) RT_TRY(hipMemcpy(sn->arena, vs.arena.data(), vs.arena.size(), hipMemcpyHostToDevice));
+  if (!rank_id.empty()) {
+    RT_TRY(hipMemcpy(sn->rank_id, rank_id.data(), rank_id.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    RT_TRY(hipMemcpy(sn->rank_exp, rank_exp.data(), rank_exp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  RetainView& rv = sn->rv;
+  rv.nodes = sn->nodes;
+  rv.edges = sn->edges;
+  rv.edge_mask = emask;
+  rv.vocab = sn->vocab;
+  rv.arena = sn->arena;
+  rv.vocab_mask = vs.mask;
+  rv.rank_id = sn->rank_id;
+  rv.rank_exp = sn->rank_exp;
+  rv.n_nodes = rank_id.empty() ? 0u : static_cast<uint32_t>(nn);
+  rv.has_expiring = has_exp;
+  sn->n_nodes = nn;
+  sn->n_words = vs.n_words();
+  sn->bytes = nn * sizeof(RNode) + ecap * sizeof(REdge) + vs.table.size() * sizeof(VocabSlot) + vs.arena.size() +
+              nr * (sizeof(uint32_t) + sizeof(int64_t));
+  *out = std::move(sn);
+  return EMQX_OK;
+}
+
+std::shared_ptr<RSnapshot> current(emqx_retain* r) {
+  std::lock_guard<std::mutex> g(r->snap_mu);
+  return r->snap;
+}
+
+int acquire(emqx_retain* r, RWork** out) {
+  {
+    std::lock_guard<std::mutex> g(r->ws_mu);
+    if (!r->free_ws.empty()) {
+      *out = r->free_ws.back();
+      r->free_ws.pop_back();
+      return EMQX_OK;
+    }
+  }
+  auto w = std::make_unique<RWork>();
+  w->device = r->device;
+  RT_TRY(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+  RT_TRY(hipEventCreate(&w->ev0));
+  RT_TRY(hipEventCreate(&w->ev1));
+  RT_TRY(hipEventCreate(&w->evw));
+  RT_TRY(ralloc(w->ctrl, RC_WORDS));
+  RT_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_pinned), 8 * sizeof(uint64_t), hipHostMallocDefault));
+  std::lock_guard<std::mutex> g(r->ws_mu);
+  *out = w.get();
+  r->all_ws.push_back(std::move(w));
+  return EMQX_OK;
+}
+
+void release(emqx_retain* r, RWork* w) {
+  std::lock_guard<std::mutex> g(r->ws_mu);
+  r->free_ws.push_back(w);
+}
+
+// The pipeline on device buffers.  *total = ids the batch needs; ids written iff it fits.
+int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb, const uint64_t* d_fo,
+              uint64_t n, uint64_t byte_span, int64_t now_ms, uint64_t* d_oo, uint32_t* d_ids, uint64_t cap,
+              hipStream_t s, uint64_t* total) {
+  RetainArgs a{};
+  a.rv = sn.rv;
+  a.fbytes = d_fb;
+  a.foffs = d_fo;
+  a.n = n;
+  a.now_ms = now_ms;
+  a.out_off = d_oo;
+  a.out_ids = d_ids;
+  a.out_cap = cap;
+  const uint64_t need_w = byte_span + n + 1;
+  if (need_w > w->wids_cap) {
+    RT_TRY(ralloc(w->wids, need_w + need_w / 4));
+    w->wids_cap = need_w + need_w / 4;
+  }
+  if (n > w->f_cap) {
+    RT_TRY(ralloc(w->fcount, n + n / 4));
+    RT_TRY(ralloc(w->fcursor, n + n / 4));
+    w->f_cap = n + n / 4;
+  }
+  const uint64_t np = scan_partials(n);
+  if (np > w->partials_cap) {
+    RT_TRY(ralloc(w->partials, np));
+    w->partials_cap = np;
+  }
+  if (w->range_cap == 0) {
+    const uint64_t rc = std::max<uint64_t>(4 * n, 1 << 16);
+    RT_TRY(ralloc(w->ranges, rc));
+    RT_TRY(ralloc(w->rcount, rc));
+    w->range_cap = static_cast<uint32_t>(rc);
+  }
+  const uint64_t ntiles = (n + 63) / 64;
+  a.waves = static_cast<uint32_t>(std::min<uint64_t>(ntiles, MAX_WAVES));
+  a.wids = w->wids;
+  a.ctrl = w->ctrl;
+  a.fcount = w->fcount;
+  a.fcursor = w->fcursor;
+  uint32_t nr = 0;
+  RT_TRY(hipEventRecord(w->ev0, s));
+  for (int attempt = 0;; ++attempt) {
+    if (static_cast<uint64_t>(a.waves) * w->stack_cap > w->stack_items) {
+      const uint64_t items = static_cast<uint64_t>(a.waves) * w->stack_cap;
+      RT_TRY(ralloc(w->stack, items));
+      w->stack_items = items;
+    }
+    a.stack = w->stack;
+    a.stack_cap = w->stack_cap;
+    a.ranges = w->ranges;
+    a.rcount = w->rcount;
+    a.range_cap = w->range_cap;
+    RT_TRY(hipMemsetAsync(w->ctrl, 0, RC_WORDS * sizeof(uint32_t), s));
+    RT_TRY(launch_retain_walk(a, s));
+    RT_TRY(hipEventRecord(w->evw, s));
+    RT_TRY(hipMemcpyAsync(w->h_pinned, w->ctrl, RC_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    RT_TRY(hipStreamSynchronize(s));
+    const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
+    const uint32_t ranges = c[RC_RANGES], visits = c[RC_VISITS], ovf = c[RC_STACK];
+    bool again = false;
+    if (ovf) {
+      if (w->stack_cap >= (1u << 24) || attempt > 8) return EMQX_ETOODEEP;
+      w->stack_cap *= 4;
+      again = true;
+    }
+    if (ranges > w->range_cap) {
+      const uint64_t rc = static_cast<uint64_t>(ranges) + ranges / 4 + 1024;
+      if (rc > 0xFFFFFFF0ull) return EMQX_ENOMEM;
+      RT_TRY(ralloc(w->ranges, rc));
+      RT_TRY(ralloc(w->rcount, rc));
+      w->range_cap = static_cast<uint32_t>(rc);
+      again = true;
+    }
+    if (!again) {
+      nr = ranges;
+      r->last_ranges.store(ranges);
+      r->last_visits.store(visits);
+      break;
+    }
+  }
+  a.ranges = w->ranges;
+  a.rcount = w->rcount;
+  a.range_cap = w->range_cap;
+  RT_TRY(hipMemsetAsync(w->fcount, 0, n * sizeof(uint32_t), s));
+  RT_TRY(hipMemsetAsync(w->fcursor, 0, n * sizeof(uint32_t), s));
+  RT_TRY(launch_retain_count(a, nr, s));
+  RT_TRY(launch_scan(w->fcount, n, d_oo, w->partials, s));
+  RT_TRY(hipMemcpyAsync(w->h_pinned, d_oo + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  RT_TRY(hipStreamSynchronize(s));
+  *total = w->h_pinned[0];
+  r->last_total.store(*total);
+  if (*total <= cap) RT_TRY(launch_retain_write(a, nr, s));
+  RT_TRY(hipEventRecord(w->ev1, s));
+  RT_TRY(hipStreamSynchronize(s));
+  float ms = 0, wms = 0;
+  if (hipEventElapsedTime(&ms, w->ev0, w->ev1) == hipSuccess) r->last_match_ms.store(ms);
+  if (hipEventElapsedTime(&wms, w->ev0, w->evw) == hipSuccess) r->last_walk_ms.store(wms);
+  return *total <= cap ? EMQX_OK : EMQX_EOVERFLOW;
+}
+
+}  // namespace
+
+extern "C" {
+
+int emqx_retain_create(int32_t device, emqx_retain** out) {
+  if (!out) return EMQX_EINVAL;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return EMQX_EDEVICE;
+  if (device < 0) RT_TRY(hipGetDevice(&device));
+  if (device >= nd) return EMQX_EINVAL;
+  emqx_retain* r = new (std::nothrow) emqx_retain();
+  if (!r) return EMQX_ENOMEM;
+  r->device = device;
+  *out = r;
+  return EMQX_OK;
+}
+
+int emqx_retain_destroy(emqx_retain* r) {
+  if (!r) return EMQX_EINVAL;
+  (void)hipSetDevice(r->device);
+  r->snap.reset();
+  r->all_ws.clear();
+  delete r;
+  return EMQX_OK;
+}
+
+int emqx_retain_store(emqx_retain* r, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                      const int64_t* expiry_ms, uint32_t* ids_out) {
+  if (!r || (n && (!bytes || !offsets))) return EMQX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 65535) return EMQX_EINVAL;
+    if (has_wild_level(bytes + offsets[i], offsets[i + 1] - offsets[i])) return EMQX_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(r->writer);
+  for (uint64_t i = 0; i < n; ++i) {
+    bool created = false;
+    const uint32_t id = r->store.insert(bytes + offsets[i], offsets[i + 1] - offsets[i], &created);
+    if (created) r->expiry.push_back(0);
+    r->expiry[id] = expiry_ms ? expiry_ms[i] : 0;
+    if (ids_out) ids_out[i] = id;
+  }
+  return EMQX_OK;
+}
+
+int emqx_retain_delete(emqx_retain* r, const uint32_t* ids, uint64_t n) {
+  if (!r || (n && !ids)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(r->writer);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (ids[i] < r->store.n_ids() && r->store.live[ids[i]]) {
+      r->store.live[ids[i]] = 0;
+      r->store.n_live -= 1;
+    }
+  }
+  return EMQX_OK;
+}
+
+int emqx_retain_lookup(emqx_retain* r, const uint8_t* bytes, uint64_t len, uint32_t* id_out) {
+  if (!r || (len && !bytes) || !id_out) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(r->writer);
+  const uint32_t id = r->store.find(bytes, len);
+  if (id == WID_NONE || !r->store.live[id]) return EMQX_ENOTFOUND;
+  *id_out = id;
+  return EMQX_OK;
+}
+
+int emqx_retain_topic(emqx_retain* r, uint32_t id, uint8_t* buf, uint64_t cap, uint64_t* len_out) {
+  if (!r || !len_out) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(r->writer);
+  if (id >= r->store.n_ids()) return EMQX_ENOTFOUND;
+  const uint64_t a = r->store.off[id], b = r->store.off[id + 1];
+  *len_out = b - a;
+  if (buf) std::memcpy(buf, r->store.bytes.data() + a, std::min(cap, b - a));
+  return EMQX_OK;
+}
+
+int emqx_retain_expired(emqx_retain* r, int64_t now_ms, uint32_t* ids_out, uint64_t cap, uint64_t* n_out) {
+  if (!r || !n_out) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(r->writer);
+  uint64_t k = 0;
+  for (uint64_t id = 0; id < r->store.n_ids(); ++id) {
+    if (!r->store.live[id] || r->expiry[id] == 0 || r->expiry[id] >= now_ms) continue;
+    if (ids_out && k < cap) ids_out[k] = static_cast<uint32_t>(id);
+    ++k;
+  }
+  *n_out = k;
+  return k <= cap ? EMQX_OK : EMQX_EOVERFLOW;
+}
+
+int emqx_retain_commit(emqx_retain* r) {
+  if (!r) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(r->writer);
+  RT_TRY(hipSetDevice(r->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  std::shared_ptr<RSnapshot> sn;
+  const int rc = build_and_upload(r, &sn);
+  if (rc != EMQX_OK) return rc;
+  {
+    std::lock_guard<std::mutex> gs(r->snap_mu);
+    r->snap = std::move(sn);
+  }
+  r->epoch += 1;
+  r->last_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return EMQX_OK;
+}
+
+int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_fb, const uint64_t* d_fo, uint64_t n,
+                                   int64_t now_ms, uint64_t* d_oo, uint32_t* d_ids, uint64_t out_cap,
+                                   uint64_t* n_out, void* stream) {
+  if (!r || !n_out || (n && (!d_fb || !d_fo)) || !d_oo) return EMQX_EINVAL;
+  RT_TRY(hipSetDevice(r->device));
+  auto sn = current(r);
+  if (!sn) {  // nothing committed yet: commit the (possibly empty) store
+    const int rc = emqx_retain_commit(r);
+    if (rc != EMQX_OK) return rc;
+    sn = current(r);
+  }
+  RWork* w = nullptr;
+  int rc = acquire(r, &w);
+  if (rc != EMQX_OK) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
+  uint64_t span = 0;
+  if (n) {
+    uint64_t ends[2];
+    rc = hipMemcpyAsync(&ends[0], d_fo, sizeof(uint64_t), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                 hipMemcpyAsync(&ends[1], d_fo + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                 hipStreamSynchronize(s) == hipSuccess
+             ? EMQX_OK
+             : EMQX_EDEVICE;
+    span = ends[1] - ends[0];
+  } else {
+    rc = hipMemsetAsync(d_oo, 0, sizeof(uint64_t), s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess
+             ? EMQX_OK
+             : EMQX_EDEVICE;
+    *n_out = 0;
+    release(r, w);
+    return rc;
+  }
+  uint64_t total = 0;
+  if (rc == EMQX_OK) rc = run_match(r, w, *sn, d_fb, d_fo, n, span, now_ms, d_oo, d_ids, out_cap, s, &total);
+  *n_out = total;
+  release(r, w);
+  return rc;
+}
+
+int emqx_retain_match_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* fo, uint64_t n, int64_t now_ms,
+                            uint64_t* out_offsets, uint32_t* out_ids, uint64_t out_cap, uint64_t* n_out) {
+  if (!r || !n_out || !out_offsets || (n && (!fb || !fo))) return EMQX_EINVAL;
+  if (n == 0) {
+    out_offsets[0] = 0;
+    *n_out = 0;
+    return EMQX_OK;
+  }
+  RT_TRY(hipSetDevice(r->device));
+  auto sn = current(r);
+  if (!sn) {
+    const int rc0 = emqx_retain_commit(r);
+    if (rc0 != EMQX_OK) return rc0;
+    sn = current(r);
+  }
+  RWork* w = nullptr;
+  int rc = acquire(r, &w);
+  if (rc != EMQX_OK) return rc;
+  const uint64_t span = fo[n] - fo[0];
+  auto stage = [&]() -> int {
+    if (span + 16 > w->d_fb_cap) {
+      RT_TRY(ralloc(w->d_fb, span + span / 4 + 16));
+      w->d_fb_cap = span + span / 4 + 16;
+    }
+    if (n + 1 > w->d_n_cap) {
+      RT_TRY(ralloc(w->d_fo, n + n / 4 + 1));
+      RT_TRY(ralloc(w->d_oo, n + n / 4 + 1));
+      w->d_n_cap = n + n / 4 + 1;
+    }
+    if (out_cap > w->d_ids_cap) {
+      RT_TRY(ralloc(w->d_ids, out_cap));
+      w->d_ids_cap = out_cap;
+    }
+    RT_TRY(hipMemcpyAsync(w->d_fb, fb + fo[0], span, hipMemcpyHostToDevice, w->stream));
+    // offsets rebased to the staged bytes
+    std::vector<uint64_t> ro(n + 1);
+    for (uint64_t i = 0; i <= n; ++i) ro[i] = fo[i] - fo[0];
+    RT_TRY(hipMemcpyAsync(w->d_fo, ro.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, w->stream));
+    RT_TRY(hipStreamSynchronize(w->stream));
+    return EMQX_OK;
+  };
+  rc = stage();
+  uint64_t total = 0;
+  if (rc == EMQX_OK)
+    rc = run_match(r, w, *sn, w->d_fb, w->d_fo, n, span, now_ms, w->d_oo, w->d_ids, out_cap, w->stream, &total);
+  if (rc == EMQX_OK || rc == EMQX_EOVERFLOW) {
+    if (hipMemcpy(out_offsets, w->d_oo, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = EMQX_EDEVICE;
+    else if (rc == EMQX_OK && total && out_ids &&
+             hipMemcpy(out_ids, w->d_ids, total * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = EMQX_EDEVICE;
+  }
+  *n_out = total;
+  release(r, w);
+  return rc;
+}
+
+int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out) {
+  if (!r || !out) return EMQX_EINVAL;
+  std::memset(out, 0, sizeof(*out));
+  {
+    std::lock_guard<std::mutex> g(r->writer);
+    out->n_ids = r->store.n_ids();
+    out->n_live = r->store.n_live;
+    out->epoch = r->epoch;
+    out->last_build_ms = r->last_build_ms;
+  }
+  auto sn = current(r);
+  if (sn) {
+    out->n_nodes = sn->n_nodes;
+    out->n_words = sn->n_words;
+    out->table_bytes = sn->bytes;
+  }
+  out->last_ranges = r->last_ranges.load();
+  out->last_visits = r->last_visits.load();
+  out->last_total = r->last_total.load();
+  out->last_match_ms = r->last_match_ms.load();
+  out->last_walk_ms = r->last_walk_ms.load();
+  return EMQX_OK;
+}
+
+}  // extern "C"

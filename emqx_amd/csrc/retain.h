@@ -1,0 +1,104 @@
+// Device layout and launch interface of the retained-message index (retain_kernels.hip,
+// retain.cpp).  See DESIGN.md §3.4.
+//
+// Reference: the mnesia retainer keeps one record per retained topic, keyed by its token list
+// (apps/emqx_retainer/src/emqx_retainer_mnesia.erl:74-98), and answers a wildcard
+// subscription with a full-table match-spec select (match_messages/1, :211-215, condition/1
+// :226-232).  Here the stored topics form a level trie over interned words (no wildcards in
+// it: they are published topics) and a FILTER walks it — the inverse of the route lookup:
+//   literal word -> one hashed child lookup;  '+' -> every child (one range item);
+//   final '#'    -> the node's whole subtree, which is ONE contiguous range of topic ranks,
+//                   because ranks are numbered in depth-first preorder.
+// So a walk emits rank ranges, and the output stage copies rank -> topic id for the live
+// (unexpired) ranks of each range: coalesced streaming reads, no per-topic pointer chasing.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "layout.h"
+
+namespace emqx {
+
+constexpr uint32_t RNODE_TERM = 0x80000000u;  // RNode.ncld: the node is a stored topic (rank lo)
+
+// One trie node (16 B).  Children are contiguous node ids [cbeg, cbeg + ncld) (BFS order);
+// the subtree's stored topics are ranks [lo, hi) (DFS preorder: the node's own topic first).
+struct alignas(16) RNode {
+  uint32_t cbeg;
+  uint32_t ncld;  // | RNODE_TERM
+  uint32_t lo;
+  uint32_t hi;
+};
+
+// Literal-edge lookup: open-addressed (parent, wid) -> child, 16 B per slot, load <= 1/2.
+struct alignas(16) REdge {
+  uint32_t parent;  // WID_NONE = empty slot
+  uint32_t wid;
+  uint32_t child;
+  uint32_t pad;
+};
+
+EMQX_HD uint32_t redge_slot0(uint32_t parent, uint32_t wid) {
+  return mix32(parent * 0x9E3779B1u ^ mix32(wid + 0x7F4A7C15u));
+}
+
+struct RetainView {
+  const RNode* nodes;
+  const REdge* edges;
+  uint32_t edge_mask;
+  const VocabSlot* vocab;
+  const uint8_t* arena;
+  uint32_t vocab_mask;
+  const uint32_t* rank_id;    // [n_ranks] topic id of each rank
+  const int64_t* rank_exp;    // [n_ranks] expiry (ms, 0 = never)
+  uint32_t n_nodes;           // 0: empty table
+  uint32_t has_expiring;      // some rank has a nonzero expiry
+};
+
+// Range emitted by the walk: filter f's matches include ranks [lo, hi).
+struct RRange {
+  uint32_t f;
+  uint32_t lo;
+  uint32_t hi;
+  uint32_t strict;  // expiry guard: 1 = expiry > now (match spec), 0 = expiry >= now (read)
+};
+
+// ctrl words of one call (zeroed per call)
+enum RCtrl : uint32_t {
+  RC_RANGES = 0,   // ranges emitted (may exceed range_cap: rerun)
+  RC_VISITS = 1,   // node visits
+  RC_STACK = 2,    // a wave's stack overflowed (rerun with a larger stack)
+  RC_WORDS = 4
+};
+
+struct RetainArgs {
+  RetainView rv;
+  const uint8_t* fbytes;   // filters, packed
+  const uint64_t* foffs;   // [n + 1]
+  uint64_t n;
+  int64_t now_ms;          // < 0: no expiry guard (match_delete_messages)
+  uint32_t* wids;          // [foffs[n] - foffs[0] + n] scratch: word ids, filter f at foffs[f] - foffs[0] + f
+  uint32_t* flev;          // [n] levels | 1 << 31 if the filter is a wildcard
+  uint4* stack;            // [waves * stack_cap] per-wave work stacks (range items)
+  uint32_t stack_cap;
+  uint32_t waves;
+  RRange* ranges;          // [range_cap]
+  uint32_t range_cap;
+  uint32_t* ctrl;          // [RC_WORDS]
+  uint32_t* rcount;        // [range_cap] live ranks per range
+  uint32_t* fcount;        // [n] live matches per filter
+  uint32_t* fcursor;       // [n] write cursor per filter
+  uint64_t* out_off;       // [n + 1]
+  uint32_t* out_ids;       // [out_cap]
+  uint64_t out_cap;
+};
+
+// tokenize + intern every filter, then walk the trie: ranges[], ctrl
+hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s);
+// live ranks per range -> rcount, fcount (nr = ranges emitted)
+hipError_t launch_retain_count(const RetainArgs& a, uint32_t nr, hipStream_t s);
+// ids of the live ranks -> out_ids at out_off[f] + cursor
+hipError_t launch_retain_write(const RetainArgs& a, uint32_t nr, hipStream_t s);
+
+}  // namespace emqx

@@ -1,0 +1,327 @@
+// Retained-message index kernels (retain.h): a batch of subscription filters against the
+// trie of stored retained topics (reference: the match-spec select of
+// apps/emqx_retainer/src/emqx_retainer_mnesia.erl:211-246 and read_messages/1 :198-208).
+//
+//   walk    one wavefront per tile of 64 filters (persistent waves).  Each lane tokenizes and
+//           interns its own filter (filters are short; subscription-path work), then the wave
+//           walks all 64 filters' frontiers from one shared work stack of RANGE items
+//           {first node, node count, level, filter}: a '+' level pushes its node's whole child
+//           range as one item, and every step hands the next 64 nodes of the stack's top items
+//           to the 64 lanes, so a wide '+' fan-out keeps every lane busy.  A final '#' emits the
+//           node's subtree as one rank range; a filter that ends on a stored topic emits its rank.
+//   count   live (unexpired) ranks per range; per-filter totals (one atomic per range)
+//   write   rank -> topic id for the live ranks of each range, at the filter's CSR offset plus
+//           a per-filter cursor: coalesced streaming reads of rank_id / rank_exp.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kernels.h"
+#include "retain.h"
+
+namespace emqx {
+
+namespace {
+
+__device__ __forceinline__ uint32_t rintern(const RetainView& rv, uint32_t h, uint32_t len, uint32_t w0, uint32_t w1,
+                                            uint32_t w2, uint32_t w3, const uint8_t* bytes, uint64_t ws) {
+  uint32_t i = vocab_slot0(h) & rv.vocab_mask;
+  for (uint32_t k = 0; k <= rv.vocab_mask; ++k) {
+    const uint4* vp = reinterpret_cast<const uint4*>(rv.vocab + i);
+    const uint4 hd = vp[0];  // hash, len, wid, off
+    if (hd.z == WID_NONE) return WID_NONE;
+    if (hd.x == h && hd.y == len) {
+      const uint4 in = vp[1];
+      bool eq = in.x == w0 && in.y == w1 && in.z == w2 && in.w == w3;
+      for (uint32_t b = 16; b < len && eq; ++b) eq = rv.arena[hd.w + b] == bytes[ws + b];
+      if (eq) return hd.z;
+    }
+    i = (i + 1) & rv.vocab_mask;
+  }
+  return WID_NONE;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// exclusive prefix of `v` over the wave; *tot = the wave's sum
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t* tot) {
+  uint32_t x = v;
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= static_cast<uint32_t>(d)) x += y;
+  }
+  *tot = __shfl(x, 63, 64);
+  return x - v;
+}
+
+__device__ __forceinline__ bool rank_live(const RetainView& rv, uint32_t i, int64_t now, uint32_t strict) {
+  const int64_t e = rv.rank_exp[i];
+  return e == 0 || (strict ? e > now : e >= now);
+}
+
+constexpr int RW_WAVES = 4;
+
+}  // namespace
+
+__global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a) {
+  const uint32_t lane = lane_id();
+  const uint32_t wib = threadIdx.x >> 6;
+  const uint32_t gw = blockIdx.x * RW_WAVES + wib;
+  __shared__ uint32_t s_pref[RW_WAVES][64];
+  __shared__ uint4 s_item[RW_WAVES][64];
+  __shared__ uint32_t s_nlev[RW_WAVES][64];
+  __shared__ uint64_t s_wb[RW_WAVES][64];
+  uint32_t* pref = s_pref[wib];
+  uint4* itm = s_item[wib];
+  uint32_t* nlevs = s_nlev[wib];
+  uint64_t* wbase = s_wb[wib];  // per filter of the tile: its first word id in a.wids
+  uint4* stk = a.stack + static_cast<uint64_t>(gw) * a.stack_cap;
+  const RetainView& rv = a.rv;
+  const uint64_t ntiles = (a.n + 63) / 64;
+  const uint64_t b0 = a.foffs[0];
+  uint32_t visits = 0;
+
+  for (uint64_t t = gw; t < ntiles; t += a.waves) {
+    const uint64_t f = t * 64 + lane;
+    const bool valid = f < a.n;
+    // ---- tokenize + intern (per lane) -------------------------------------------------
+    uint32_t nlev = 0, wild = 0;
+    if (valid) {
+      const uint64_t start = a.foffs[f], end = a.foffs[f + 1];
+      uint32_t* wout = a.wids + (start - b0) + f;
+      uint32_t len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+      uint64_t ws = start;
+      for (uint64_t i = start; i <= end; ++i) {
+        const uint32_t c = (i < end) ? a.fbytes[i] : static_cast<uint32_t>('/');
+        if (c != '/') {
+          if (len < 16) {
+            const uint32_t v = c << (8u * (len & 3u));
+            const uint32_t q = len >> 2;
+            w0 |= q == 0 ? v : 0u;
+            w1 |= q == 1 ? v : 0u;
+            w2 |= q == 2 ? v : 0u;
+            w3 |= q == 3 ? v : 0u;
+          }
+          ++len;
+        } else {
+          uint32_t wid;
+          if (len == 1 && w0 == '+') {
+            wid = WID_PLUS;
+            wild = 1;
+          } else if (len == 1 && w0 == '#') {
+            wid = i == end ? WID_HASH : WID_NONE;  // a non-final '#' is a token no topic has
+            wild = 1;
+          } else {
+            const uint32_t h = len <= 16 ? word_hash16(len, w0, w1, w2, w3) : word_hash_bytes(a.fbytes + ws, len);
+            wid = rv.n_nodes ? rintern(rv, h, len, w0, w1, w2, w3, a.fbytes, ws) : WID_NONE;
+          }
+          wout[nlev++] = wid;
+          len = 0;
+          w0 = w1 = w2 = w3 = 0;
+          ws = i + 1;
+        }
+      }
+    }
+    nlevs[lane] = nlev | (wild << 31);
+    wbase[lane] = valid ? (a.foffs[f] - b0) + f : 0;
+    // root items
+    const bool push0 = valid && rv.n_nodes != 0;
+    uint32_t ptot;
+    const uint32_t ppos = wave_excl(push0 ? 1u : 0u, &ptot);
+    if (push0) stk[ppos] = make_uint4(0u, 1u, 0u, lane);
+    uint32_t top = ptot;
+    bool overflow = false;
+    __threadfence_block();  // the stack lives in global memory: order this wave's stores and loads
+
+    while (top > 0) {
+      // ---- take the next (up to) 64 nodes from the top items ----------------------------
+      const uint32_t navail = top < 64 ? top : 64;
+      uint4 it = make_uint4(0, 0, 0, 0);
+      if (lane < navail) it = stk[top - 1 - lane];
+      uint32_t ctot;
+      const uint32_t cex = wave_excl(lane < navail ? it.y : 0u, &ctot);
+      pref[lane] = cex + (lane < navail ? it.y : 0u);  // inclusive
+      itm[lane] = it;
+      __builtin_amdgcn_wave_barrier();
+      // items fully consumed: inclusive prefix <= 64
+      const uint64_t full = __ballot(lane < navail && pref[lane] <= 64);
+      const uint32_t kfull = __popcll(full);  // a prefix of the lanes (counts >= 1)
+      const uint32_t taken = ctot < 64 ? ctot : 64;
+      if (kfull < navail && lane == 0) {  // the partially consumed item stays, shortened
+        const uint32_t used = 64 - (kfull ? pref[kfull - 1] : 0u);
+        uint4 p = itm[kfull];
+        p.x += used;
+        p.y -= used;
+        stk[top - 1 - kfull] = p;
+      }
+      top -= kfull;
+      // ---- this lane's node ---------------------------------------------------------------
+      bool act = lane < taken;
+      uint32_t v = 0, lev = 0, fl = 0;
+      if (act) {
+        uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pref[mid] > lane) hi = mid; else lo = mid + 1;
+        }
+        const uint32_t before = lo ? pref[lo - 1] : 0u;
+        const uint4 q = itm[lo];
+        v = q.x + (lane - before);
+        lev = q.z;
+        fl = q.w;
+      }
+      __builtin_amdgcn_wave_barrier();
+      bool emit = false, push = false;
+      RRange rg{0, 0, 0, 0};
+      uint4 np = make_uint4(0, 0, 0, 0);
+      if (act) {
+        ++visits;
+        const RNode rn = rv.nodes[v];
+        const uint32_t nl = nlevs[fl];
+        const uint32_t fn = nl & 0x7FFFFFFFu;
+        const uint64_t fg = t * 64 + fl;
+        rg.f = static_cast<uint32_t>(fg);
+        rg.strict = nl >> 31;
+        if (lev == fn) {
+          if (rn.ncld & RNODE_TERM) {
+            emit = true;
+            rg.lo = rn.lo;
+            rg.hi = rn.lo + 1;
+          }
+        } else {
+          const uint32_t w = a.wids[wbase[fl] + lev];
+          const uint32_t ncld = rn.ncld & ~RNODE_TERM;
+          if (w == WID_HASH) {
+            emit = rn.hi > rn.lo;
+            rg.lo = rn.lo;
+            rg.hi = rn.hi;
+          } else if (w == WID_PLUS) {
+            push = ncld != 0;
+            np = make_uint4(rn.cbeg, ncld, lev + 1, fl);
+          } else if (w != WID_NONE && ncld != 0) {
+            uint32_t s = redge_slot0(v, w) & rv.edge_mask;
+            for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
+              const REdge e = rv.edges[s];
+              if (e.parent == WID_NONE) break;
+              if (e.parent == v && e.wid == w) {
+                push = true;
+                np = make_uint4(e.child, 1u, lev + 1, fl);
+                break;
+              }
+              s = (s + 1) & rv.edge_mask;
+            }
+          }
+        }
+      }
+      // ---- emissions (one atomic per wave step) --------------------------------------------
+      uint32_t etot;
+      const uint32_t epos = wave_excl(emit ? 1u : 0u, &etot);
+      if (etot) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&a.ctrl[RC_RANGES], etot);
+        base = __shfl(base, 0, 64);
+        if (emit && base + epos < a.range_cap) a.ranges[base + epos] = rg;
+      }
+      // ---- pushes ---------------------------------------------------------------------------
+      uint32_t qtot;
+      const uint32_t qpos = wave_excl(push ? 1u : 0u, &qtot);
+      if (top + qtot > a.stack_cap) {
+        overflow = true;
+        break;
+      }
+      if (push) stk[top + qpos] = np;
+      top += qtot;
+      __threadfence_block();
+    }
+    if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
+  }
+  // visits: one atomic per wave
+  uint32_t vtot;
+  (void)wave_excl(visits, &vtot);
+  if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
+}
+
+// count (mode 0) / write (mode 1): one wave per 64 ranges (grid-stride).  Ranges of at most
+// one rank are handled lane-parallel; longer ones by the whole wave, 64 ranks at a time.
+template <int MODE>
+__global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t nr) {
+  const uint32_t lane = lane_id();
+  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+  const RetainView& rv = a.rv;
+  const bool guard = rv.has_expiring && a.now_ms >= 0;
+  for (uint64_t r0 = static_cast<uint64_t>(gw) * 64; r0 < nr; r0 += static_cast<uint64_t>(nw) * 64) {
+    const uint64_t r = r0 + lane;
+    const bool valid = r < nr;
+    RRange rg{0, 0, 0, 0};
+    if (valid) rg = a.ranges[r];
+    const uint32_t len = rg.hi - rg.lo;
+    uint32_t c = 0;
+    uint64_t pos = 0;
+    if (MODE == 0) {
+      if (valid && (!guard || len <= 1)) c = (!guard || (len == 1 && rank_live(rv, rg.lo, a.now_ms, rg.strict))) ? len : 0u;
+    } else if (valid) {
+      c = a.rcount[r];
+      if (c) pos = a.out_off[rg.f] + atomicAdd(&a.fcursor[rg.f], c);
+      if (c && len == 1 && pos < a.out_cap) a.out_ids[pos] = rv.rank_id[rg.lo];
+    }
+    // wave-cooperative ranges: longer than one rank (and, when counting, only under a guard)
+    uint64_t big = __ballot(valid && len > 1 && (MODE == 1 ? c != 0 : guard));
+    while (big) {
+      const uint32_t b = __ffsll(static_cast<unsigned long long>(big)) - 1;
+      big &= big - 1;
+      const uint32_t lo = __shfl(rg.lo, b, 64), hi = __shfl(rg.hi, b, 64), strict = __shfl(rg.strict, b, 64);
+      uint64_t p = __shfl(pos, b, 64);
+      uint32_t cnt = 0;
+      for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool live = i < hi && (!guard || rank_live(rv, i, a.now_ms, strict));
+        if (MODE == 0) {
+          cnt += live ? 1u : 0u;
+        } else {
+          const uint64_t m = __ballot(live);
+          const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+          if (live && p + rank < a.out_cap) a.out_ids[p + rank] = rv.rank_id[i];
+          p += __popcll(m);
+        }
+      }
+      if (MODE == 0) {
+        uint32_t tot;
+        (void)wave_excl(cnt, &tot);
+        if (lane == b) c = tot;
+      }
+    }
+    if (MODE == 0 && valid) {
+      a.rcount[r] = c;
+      if (c) atomicAdd(&a.fcount[rg.f], c);
+    }
+  }
+}
+
+hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  const uint32_t blocks = (a.waves + RW_WAVES - 1) / RW_WAVES;
+  hipLaunchKernelGGL(retain_walk_kernel, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
+  return hipGetLastError();
+}
+
+static uint32_t out_blocks(uint32_t nr) {
+  const uint64_t waves = (static_cast<uint64_t>(nr) + 63) / 64;
+  return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((waves + 3) / 4, 8192)));
+}
+
+hipError_t launch_retain_count(const RetainArgs& a, uint32_t nr, hipStream_t s) {
+  if (nr == 0) return hipSuccess;
+  hipLaunchKernelGGL(retain_out_kernel<0>, dim3(out_blocks(nr)), dim3(256), 0, s, a, nr);
+  return hipGetLastError();
+}
+
+hipError_t launch_retain_write(const RetainArgs& a, uint32_t nr, hipStream_t s) {
+  if (nr == 0) return hipSuccess;
+  hipLaunchKernelGGL(retain_out_kernel<1>, dim3(out_blocks(nr)), dim3(256), 0, s, a, nr);
+  return hipGetLastError();
+}
+
+}  // namespace emqx

@@ -1,0 +1,100 @@
+/*
+ * emqx_retain.h — C ABI of the retained-message index (libemqxmatch.so), SURVEY §8 f4.
+ *
+ * The "inverse" lookup of the mnesia retainer backend: a subscription filter -> the stored
+ * retained topics it matches.  Paths are relative to the reference checkout
+ * (xiongzhenhai-zh/emqx, EMQX 5.0.0-beta.3):
+ *
+ *   emqx_retainer_mnesia:store_retained/2     apps/emqx_retainer/src/emqx_retainer_mnesia.erl:74-98
+ *       -> emqx_retain_store (+ emqx_retain_commit: batched rebuild, snapshot swap)
+ *   emqx_retainer_mnesia:delete_message/2     emqx_retainer_mnesia.erl:112-122
+ *       -> emqx_retain_lookup + emqx_retain_delete (exact topic); a wildcard topic
+ *          (match_delete_messages/1, :217-223) -> emqx_retain_match_batch(now_ms = -1)
+ *          + emqx_retain_delete of the returned ids
+ *   emqx_retainer_mnesia:clear_expired/1      emqx_retainer_mnesia.erl:101-110
+ *       -> emqx_retain_expired + emqx_retain_delete
+ *   emqx_retainer:dispatch/4 -> read_message/2 (plain filter, :198-208) or match_messages/3
+ *       (wildcard filter, :211-215 + make_match_spec/1 :234-246)
+ *       -> emqx_retain_match_batch: one call for a batch of filters (a subscribe storm),
+ *          each filter answered as dispatch/4 would (plain: expiry == 0 || expiry >= now;
+ *          wildcard: expiry == 0 || expiry > now; no '$' rule — the match spec has none).
+ *   emqx_retainer_mnesia:size/1               emqx_retainer_mnesia.erl:174-176
+ *       -> emqx_retain_stats(...).n_live
+ *
+ * Ordering: the reference sorts a wildcard answer by message timestamp (sort_retained/1,
+ * qlc:sort in make_cursor/1); the index returns each filter's topic ids as a set (order
+ * unspecified) and the caller, who holds the messages, orders them.  Cursor batching
+ * (max_read_number) is likewise a caller-side slice of that list.
+ *
+ * Conventions as in emqx_match.h: int status, EMQX_* codes, packed byte buffers + uint64
+ * offsets[n+1], CSR results.  One writer (store/delete/commit) at a time; any number of
+ * concurrent emqx_retain_match_batch callers read an immutable snapshot.
+ */
+#ifndef EMQX_RETAIN_H
+#define EMQX_RETAIN_H
+
+#include <stdint.h>
+
+#include "emqx_match.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct emqx_retain emqx_retain;
+
+typedef struct emqx_retain_stats {
+  uint64_t n_ids;            /* topic ids ever assigned                                     */
+  uint64_t n_live;           /* retained topics stored (emqx_retainer_mnesia:size/1)        */
+  uint64_t n_nodes;          /* trie nodes of the committed snapshot                        */
+  uint64_t n_words;          /* interned words                                              */
+  uint64_t table_bytes;      /* device bytes of the committed snapshot                      */
+  uint64_t epoch;            /* commits so far                                              */
+  uint64_t last_ranges;      /* rank ranges the last match emitted                          */
+  uint64_t last_visits;      /* trie nodes the last match visited                           */
+  uint64_t last_total;       /* topic ids the last match returned                           */
+  double last_build_ms;      /* host build + upload time of the last commit                 */
+  double last_match_ms;      /* device time of the last match call (hipEvent)               */
+  double last_walk_ms;       /* ... of its walk kernel alone                                */
+} emqx_retain_stats;
+
+int emqx_retain_create(int32_t device, emqx_retain** out);
+int emqx_retain_destroy(emqx_retain* r);
+
+/* Stores n topics (no '+'/'#' level: EMQX_EINVAL, nothing stored).  expiry_ms[i] is the
+ * message's expiry time in ms (0 = never; emqx_retainer:get_expiry_time/1); NULL = all 0.
+ * Re-storing a topic keeps its id and replaces its expiry.  ids_out (may be NULL) gets ids. */
+int emqx_retain_store(emqx_retain* r, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                      const int64_t* expiry_ms, uint32_t* ids_out);
+/* Deletes topics by id (unknown / already deleted ids are ignored). */
+int emqx_retain_delete(emqx_retain* r, const uint32_t* ids, uint64_t n);
+/* Id of a stored (live) topic, EMQX_ENOTFOUND otherwise. */
+int emqx_retain_lookup(emqx_retain* r, const uint8_t* bytes, uint64_t len, uint32_t* id_out);
+/* Bytes of topic `id` (cap bytes copied); *len_out = its length. */
+int emqx_retain_topic(emqx_retain* r, uint32_t id, uint8_t* buf, uint64_t cap, uint64_t* len_out);
+/* Ids of live topics whose expiry is nonzero and < now_ms (clear_expired/1); *n_out = count,
+ * at most cap written (EMQX_EOVERFLOW if more: *n_out = the count needed). */
+int emqx_retain_expired(emqx_retain* r, int64_t now_ms, uint32_t* ids_out, uint64_t cap, uint64_t* n_out);
+/* Publishes every store/delete since the last commit (snapshot swap). */
+int emqx_retain_commit(emqx_retain* r);
+
+/* dispatch/4 for a batch of filters against the committed snapshot.  now_ms < 0: no expiry
+ * guard (match_delete_messages/1).  out_offsets[n+1], out_ids[out_offsets[n]] (topic ids);
+ * EMQX_EOVERFLOW when out_cap is too small (*n_out = the capacity needed, offsets valid). */
+int emqx_retain_match_batch(emqx_retain* r, const uint8_t* filter_bytes, const uint64_t* filter_offsets,
+                            uint64_t n, int64_t now_ms, uint64_t* out_offsets, uint32_t* out_ids,
+                            uint64_t out_cap, uint64_t* n_out);
+/* Same, with every buffer in device memory of the index's device, on `stream` (0 = the
+ * index's own).  Synchronizes the stream before returning. */
+int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes,
+                                   const uint64_t* d_filter_offsets, uint64_t n, int64_t now_ms,
+                                   uint64_t* d_out_offsets, uint32_t* d_out_ids, uint64_t out_cap,
+                                   uint64_t* n_out, void* stream);
+
+int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EMQX_RETAIN_H */

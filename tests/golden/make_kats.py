@@ -211,6 +211,50 @@ BENCH = {"src": "apps/emqx/src/emqx_broker_bench.erl:25-34,146-162",
          "expect_routes_per_topic": 1}
 
 
+# emqx_retainer_SUITE (mnesia backend): retained topics as stored, then the subscriptions a
+# client makes and the messages it receives.  ops: ["store", topic, expiry_ms] (0 = never,
+# emqx_retainer.erl:150-165 with msg_expiry_interval "0s"), ["publish_empty", topic] (a
+# retained empty payload deletes, emqx_retainer.erl:89-101), ["delete", topic]
+# (emqx_retainer:delete/1 -> delete_message/2, wildcard -> match_delete_messages/1).
+# queries: [now_ms, filter, expected sorted topics] — dispatch/4 picks read_message/2 for a
+# plain filter (expiry >= now) and match_messages/3 for a wildcard one (expiry > now).
+T0 = 1_000_000
+RETAIN_CASES = [
+    {"name": "t_wildcard_subscription", "src": "apps/emqx_retainer/test/emqx_retainer_SUITE.erl:154-177",
+     "ops": [["store", "retained/0", 0], ["store", "retained/1", 0], ["store", "retained/a/b/c", 0]],
+     "queries": [[T0, "retained/+", ["retained/0", "retained/1"]],
+                 [T0, "retained/+/b/#", ["retained/a/b/c"]]]},
+    {"name": "t_message_expiry", "src": "apps/emqx_retainer/test/emqx_retainer_SUITE.erl:179-221",
+     "ops": [["store", "retained/0", 0], ["store", "retained/1", T0 + 2000], ["store", "retained/2", T0 + 5000],
+             ["store", "retained/3", 0], ["store", "$SYS/retained/4", 0]],
+     "queries": [[T0, "retained/+", ["retained/0", "retained/1", "retained/2", "retained/3"]],
+                 [T0, "$SYS/retained/+", ["$SYS/retained/4"]],
+                 [T0 + 3000, "retained/+", ["retained/0", "retained/2", "retained/3"]],
+                 [T0 + 3000, "$SYS/retained/+", ["$SYS/retained/4"]]]},
+    {"name": "t_message_expiry_2", "src": "apps/emqx_retainer/test/emqx_retainer_SUITE.erl:223-238",
+     "ops": [["store", "retained", T0 + 2000]],
+     "queries": [[T0, "retained", ["retained"]], [T0 + 4000, "retained", []]]},
+    {"name": "t_clean", "src": "apps/emqx_retainer/test/emqx_retainer_SUITE.erl:240-263",
+     "ops": [["store", "retained/0", 0], ["store", "retained/1", 0], ["store", "retained/test/0", 0]],
+     "queries": [[T0, "retained/#", ["retained/0", "retained/1", "retained/test/0"]]],
+     "then": [["delete", "retained/test/0"], ["delete", "retained/+"]],
+     "after": [[T0, "retained/#", []]]},
+    {"name": "t_retain_handling", "src": "apps/emqx_retainer/test/emqx_retainer_SUITE.erl:110-152",
+     "ops": [],
+     "queries": [[T0, "retained", []], [T0, "retained/#", []]],
+     "then": [["store", "retained", 0]],
+     "after": [[T0, "retained", ["retained"]], [T0, "retained/#", ["retained"]]]},
+    {"name": "t_store_and_clean_empty_payload", "src": "apps/emqx_retainer/test/emqx_retainer_SUITE.erl:89-108",
+     "ops": [["store", "retained", 0]],
+     "queries": [[T0, "retained", ["retained"]]],
+     "then": [["publish_empty", "retained"]],
+     "after": [[T0, "retained", []]]},
+    {"name": "t_flow_control_set", "src": "apps/emqx_retainer/test/emqx_retainer_SUITE.erl:284-310",
+     "ops": [["store", "retained/0", 0], ["store", "retained/1", 0], ["store", "retained/3", 0]],
+     "queries": [[T0, "retained/#", ["retained/0", "retained/1", "retained/3"]]]},
+]
+
+
 def main():
     out = {
         "generated_by": "tests/golden/make_kats.py",
@@ -222,6 +266,7 @@ def main():
         "router_cases": ROUTER_CASES,
         "client": CLIENT,
         "bench": BENCH,
+        "retain_cases": RETAIN_CASES,
     }
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kats.json")
     with open(path, "w") as f:

@@ -21,8 +21,8 @@ def L():
     return _lib.lib()
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "emqx_match.h")).read()
+def header_functions(name="emqx_match.h"):
+    src = open(os.path.join(ROOT, "include", name)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(emqx_[a-z_]+)\s*\(", src)))
 
@@ -34,6 +34,15 @@ def test_exports_every_declared_symbol(L):
     assert sorted(_lib.EXPORTS) == declared
     for name in declared:
         assert hasattr(L, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared:
+        assert re.search(r"\bT %s\b" % name, nm), name
+
+
+def test_exports_every_retain_symbol(L):
+    from emqx_amd import _lib
+    declared = header_functions("emqx_retain.h")
+    assert sorted(_lib.RETAIN_EXPORTS) == declared
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     for name in declared:
         assert re.search(r"\bT %s\b" % name, nm), name

@@ -1,0 +1,182 @@
+"""Retained-message index on the GPU against the oracle of the reference's
+mnesia retainer (oracle/retain_ref.py): the emqx_retainer_SUITE KATs through the
+emqx_retainer_mnesia mirror, fuzzed tables/filters/expiry guards compared as sorted topic-id
+sets, deletes and recommits, wide '+' fan-outs, root '#', deep topics, and a config-B-scale
+table through the device entry point."""
+
+import random
+
+import numpy as np
+import pytest
+
+from oracle import retain_ref as RR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mod():
+    import torch  # noqa: F401
+    from emqx_amd import _lib, retainer
+    _lib.lib()
+    return retainer
+
+
+def test_retainer_suite_kats(mod, kats):
+    for case in kats["retain_cases"]:
+        st = mod.MnesiaRetainer()
+
+        def apply(op):
+            if op[0] == "store":
+                st.store_retained(mod.Message(op[1].encode(), b"payload", 0, op[2]))
+            elif op[0] == "publish_empty":
+                st.on_message_publish(mod.Message(op[1].encode(), b"", 0, 0))
+            else:
+                st.delete_message(op[1].encode())
+
+        def check(queries):
+            for now, filt, exp in queries:
+                got = sorted(m.topic.decode() for m in st.dispatch(filt.encode(), now))
+                assert got == sorted(exp), (case["name"], filt, now)
+
+        for op in case["ops"]:
+            apply(op)
+        check(case["queries"])
+        for op in case.get("then", []):
+            apply(op)
+        check(case.get("after", []))
+
+
+VOCAB = [b"a", b"b", b"c", b"", b"$SYS", b"dev", b"x$", b"long-word-over-sixteen-bytes"]
+
+
+def rand_topic(rng, maxd=6):
+    return b"/".join(rng.choice(VOCAB) for _ in range(rng.randint(1, maxd)))
+
+
+def rand_filter(rng, maxd=6):
+    lv = [rng.choice(VOCAB + [b"+", b"+", b"nope"]) for _ in range(rng.randint(1, maxd))]
+    r = rng.random()
+    if r < 0.35:
+        lv[-1] = b"#"
+    elif r < 0.38:
+        lv.insert(0, b"#")  # invalid: a non-final '#'
+    return b"/".join(lv)
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_fuzz_parity(mod, seed):
+    rng = random.Random(700 + seed)
+    idx = mod.RetainIndex()
+    names = sorted({rand_topic(rng) for _ in range(rng.randint(20, 400))})
+    expiry = [rng.choice([0, 0, 0, 90, 100, 110]) for _ in names]
+    ids = idx.store(names, expiry)
+    assert list(ids) == list(range(len(names)))
+    live = [True] * len(names)
+    idx.commit()
+    filters = [rand_filter(rng) for _ in range(700)] + [b"#", b"+", b"+/#", b"", b"/", b"$SYS/#"]
+    for step in range(3):
+        tt = RR.TokenTrie(names, expiry, live)
+        for now in (100, -1, 0):
+            got = idx.match(filters, now)
+            for f, g in zip(filters, got):
+                assert g == tt.dispatch(f, now), (step, f, now)
+        # deletes, re-stores with a new expiry, new topics
+        dead = rng.sample(range(len(names)), len(names) // 5)
+        idx.delete(dead)
+        for i in dead:
+            live[i] = False
+        back = rng.sample(dead, len(dead) // 2)
+        for i in back:
+            expiry[i] = rng.choice([0, 95, 105])
+        idx.store([names[i] for i in back], [expiry[i] for i in back])
+        for i in back:
+            live[i] = True
+        new = sorted({rand_topic(rng) for _ in range(40)} - set(names))
+        nid = idx.store(new, [0] * len(new))
+        assert list(nid) == list(range(len(names), len(names) + len(new)))
+        names += new
+        expiry += [0] * len(new)
+        live += [True] * len(new)
+        idx.commit()
+
+
+def test_wide_fanout_and_root_hash(mod):
+    idx = mod.RetainIndex()
+    names = [b"w/%d/x" % i for i in range(20000)] + [b"w/%d/y/z" % i for i in range(0, 20000, 7)] + [b"$SYS/s"]
+    idx.store(names)
+    idx.commit()
+    filters = [b"w/+/x", b"w/+/y/#", b"#", b"+/+/x", b"w/#", b"+/s", b"w/+/+/z", b"w/7/y/z"]
+    tt = RR.TokenTrie(names, [0] * len(names))
+    got = idx.match(filters, 1)
+    for f, g in zip(filters, got):
+        assert g == tt.dispatch(f, 1), f
+    assert len(got[2]) == len(names)  # '#' selects '$SYS/...' too: the match spec has no '$' rule
+
+
+def test_deep_topics(mod):
+    rng = random.Random(3)
+    idx = mod.RetainIndex()
+    names = [b"/".join(b"l%d" % (j % 3) for j in range(rng.randint(50, 120))) for _ in range(200)]
+    names = sorted(set(names))
+    idx.store(names)
+    idx.commit()
+    filters = [b"/".join([b"+"] * 60) + b"/#", b"/".join([b"+"] * 100), b"l0/#", b"/".join([b"l0", b"l1", b"l2"] * 20)]
+    filters += [b"/".join(rng.choice([b"l0", b"l1", b"l2", b"+"]) for _ in range(rng.randint(40, 130))) + b"/#"
+                for _ in range(100)]
+    tt = RR.TokenTrie(names, [0] * len(names))
+    for f, g in zip(filters, idx.match(filters, 1)):
+        assert g == tt.dispatch(f, 1)
+
+
+def test_empty_index_and_batches(mod):
+    idx = mod.RetainIndex()
+    assert idx.match([b"#", b"a"], 5) == [[], []]
+    idx.store([b"a"])
+    idx.commit()
+    assert idx.match([], 5) == []
+    with pytest.raises(Exception):
+        idx.store([b"a/+"])  # published topics carry no wildcard levels
+
+
+def test_large_table_device_api(mod):
+    """A config-B-scale store of retained topics (the topic generator of config B), 20k
+    subscription filters from its filter generator, through the device entry point."""
+    import torch
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import pack
+    wl = W.config_b(n_filters=20_000, n_topics=300_000, seed=31)
+    names = sorted(set(W.unpack(wl.topics)))
+    rng = np.random.default_rng(1)
+    expiry = np.where(rng.random(len(names)) < 0.1, 1000 + rng.integers(0, 200, len(names)), 0).astype(np.int64)
+    idx = mod.RetainIndex()
+    idx.store_packed(*pack(names), expiry)
+    idx.commit()
+    filters = W.unpack(wl.filters)
+    dev = torch.device("cuda:0")
+    fb, fo = pack(filters)
+    d_fb = torch.from_numpy(fb).to(dev)
+    d_fo = torch.from_numpy(fo.view(np.int64)).to(dev)
+    d_off = torch.empty(len(filters) + 1, dtype=torch.int64, device=dev)
+    cap = 4_000_000
+    d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    try:
+        n = idx.match_device(d_fb.data_ptr(), d_fo.data_ptr(), len(filters), 1100, d_off.data_ptr(),
+                             d_ids.data_ptr(), cap)
+    except mod.EngineError as err:
+        cap = err.needed
+        d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+        n = idx.match_device(d_fb.data_ptr(), d_fo.data_ptr(), len(filters), 1100, d_off.data_ptr(),
+                             d_ids.data_ptr(), cap)
+    off = d_off.cpu().numpy().view(np.uint64)
+    ids = d_ids[:n].cpu().numpy().view(np.uint32)
+    tt = RR.TokenTrie(names, expiry.tolist())
+    total = 0
+    for i in range(0, len(filters), 3):
+        g = sorted(ids[off[i]:off[i + 1]].tolist())
+        x = tt.dispatch(filters[i], 1100)
+        assert g == x, (i, filters[i])
+        total += len(x)
+    assert total > 0 and n == off[-1]
+    st = idx.stats()
+    assert st["n_live"] == len(names) and st["last_total"] == n
