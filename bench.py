@@ -61,12 +61,14 @@ def main():
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
-    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U"],
+    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R"],
                     help="B = the headline (BASELINE configs[1]); A = configs[0]'s 100k-filter table, "
                          "D = the adversarial depth-16 table (configs[3], 100k-topic batches), "
                          "E = publish fan-out (configs[4]): match + fan-out per step, "
                          "U = route updates (SURVEY §8 f2): subscribe/unsubscribe churn + incremental "
-                         "commits on config B's table")
+                         "commits on config B's table, R = retained-message lookup (SURVEY §8 f4): a batch "
+                         "of subscription filters against 1M stored retained topics")
+    ap.add_argument("--retained", type=int, default=1_000_000, help="--workload R: stored retained topics")
     ap.add_argument("--churn", type=int, default=10_000, help="--workload U: inserts and deletes per commit")
     ap.add_argument("--rounds", type=int, default=10, help="--workload U: commits timed")
     ap.add_argument("--strategy", type=str, default="hash_clientid",
@@ -101,6 +103,8 @@ def main():
         return fanout_bench(args, rank, world, dev)
     if args.workload == "U":
         return update_bench(args, rank, world, dev)
+    if args.workload == "R":
+        return retain_bench(args, rank, world, dev)
     if args.workload == "A":
         wl = load_or_make(args, rank, lambda: W.config_a(n_topics=args.batch, seed=1 if rank == 0 else 1000 + rank))
     elif args.workload == "D":
@@ -565,6 +569,130 @@ def update_bench(args, rank, world, dev):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = update_cpu_baseline(wl, nb, k, args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def retain_bench(args, rank, world, dev):
+    """Retained-message lookup (emqx_retainer:dispatch/4 ->
+    emqx_retainer_mnesia:match_messages/3 / read_message/2): a subscribe burst of
+    `--batch` (default 100k) config-B subscription filters (exact / '+' / '#' mix) against
+    `--retained` stored retained topics (config B's topic generator, 10% with an expiry).
+    A step = one emqx_retain_match_batch_device call on the resident batch -> CSR of topic
+    ids in HBM.  Replicated store: each rank answers its own filter batch (weak scaling)."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import pack
+    from emqx_amd.retainer import RetainIndex
+    from emqx_amd._lib import EngineError
+    nf = args.batch if args.batch != 1_000_000 else 100_000
+    t0 = time.time()
+    topics_wl = W.config_b(n_filters=max(args.retained // 10, 1000), n_topics=int(args.retained * 1.15), seed=41)
+    names = W.unpack(topics_wl.topics)
+    names = list(dict.fromkeys(names))[: args.retained]
+    filt_wl = W.config_b(n_filters=nf, n_topics=1000, seed=42 + rank)
+    rng = np.random.default_rng(5)
+    now = 1_000_000
+    expiry = np.where(rng.random(len(names)) < 0.1, now - 500 + rng.integers(0, 1000, len(names)), 0).astype(np.int64)
+    log(f"[rank {rank}] retained store: {len(names)} topics, {nf} filters ({time.time() - t0:.1f}s)")
+    idx = RetainIndex(dev.index)
+    tb, to = pack(names)
+    idx.store_packed(tb, to, expiry)
+    idx.commit()
+    st = idx.stats()
+    log(f"[rank {rank}] index: {st['n_nodes']} nodes, {st['n_words']} words, {st['table_bytes'] / 1e6:.1f} MB, "
+        f"build {st['last_build_ms']:.0f} ms")
+    fb, fo = filt_wl.filters
+    d_fb = torch.from_numpy(fb.copy()).to(dev)
+    d_fo = torch.from_numpy(fo.view(np.int64).copy()).to(dev)
+    d_off = torch.empty(nf + 1, dtype=torch.int64, device=dev)
+    cap = 1 << 24
+    d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        return idx.match_device(d_fb.data_ptr(), d_fo.data_ptr(), nf, now, d_off.data_ptr(), d_ids.data_ptr(), cap,
+                                stream=stream)
+
+    try:
+        nout = step()
+    except EngineError as err:
+        cap = int(err.needed * 1.25) + 1024
+        d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+        nout = step()
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    call_ms, walk_ms = [], []
+    for _ in range(args.steps):
+        step()
+        s2 = idx.stats()
+        call_ms.append(s2["last_match_ms"])
+        walk_ms.append(s2["last_walk_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = idx.stats()
+    visits, ranges = st["last_visits"], st["last_ranges"]
+    levels = int(np.count_nonzero(fb[: int(fo[-1])] == ord("/"))) + nf
+    # algorithmic bytes of one call: filter bytes, one 32-B vocab slot per level, per node visit
+    # its 16-B record and one 16-B edge probe, 16 B per range written + read twice, and per id
+    # out: rank_id read + id write (+ 8 B expiry read under the guard), offsets
+    alg = int(fo[-1]) + 32 * levels + 32 * visits + 48 * ranges + 16 * nout + 16 * nf
+    cms = float(np.median(call_ms))
+    achieved = alg / (cms * 1e-3) / 1e9
+    value = nf * args.steps * world / elapsed
+    result = {
+        "metric": "subscription filters resolved against the retained store /sec (retained lookup, 1M retained topics)",
+        "value": round(value, 1), "unit": "filters/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "R: retained lookup, config-B subscription filters vs config-B topics stored retained",
+                   "retained_topics": len(names), "filters_per_call": nf,
+                   "parallelism": f"replicated store x{world}"},
+        "ids_per_s": round(nout * args.steps * world / elapsed, 1),
+        "ids_per_filter": round(nout / nf, 3), "node_visits_per_filter": round(visits / nf, 3),
+        "ranges_per_filter": round(ranges / nf, 3), "call_ms_median": round(cms, 4),
+        "walk_ms_median": round(float(np.median(walk_ms)), 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "retain_walk_kernel + retain_out_kernel<0,1> (whole call, incl. 2 host syncs)",
+                     "alg_bytes_per_launch": alg,
+                     "alg_bytes_model": "len(F) + 32*L(F) + 32*visits + 48*ranges + 16*ids + 16 per filter"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpp as C
+        sc = C.RetainScan(tb, to, expiry)
+        sample = min(2000, nf)
+        sfb, sfo = W.take(filt_wl.filters, np.arange(sample))
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        t1 = time.perf_counter()
+        counts, sums = sc.select_packed(sfb, sfo, now, threads=threads)
+        dt = time.perf_counter() - t1
+        off = d_off[: sample + 1].cpu().numpy()
+        ids = d_ids[: int(off[-1])].cpu().numpy().view(np.uint32).astype(np.uint64)
+        cs = np.concatenate([np.zeros(1, np.uint64), np.cumsum(ids, dtype=np.uint64)])
+        gsum = cs[off[1:]] - cs[off[:-1]]
+        gcnt = np.diff(off)
+        if not (np.array_equal(gcnt, counts.astype(np.int64)) and np.array_equal(gsum, sums)):
+            raise SystemExit("retained lookup differs from the CPU port on the baseline sample")
+        result["cpu_baseline"] = {"value": round(sample / dt, 1), "unit": "filters/s", "cores": threads,
+                                  "kind": "port",
+                                  "sample": f"first {sample} filters; full-table match-spec scan per wildcard "
+                                            "filter, key read per plain one (mnesia set table), C++",
+                                  "parity": "per-filter count and id sum equal the GPU's"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

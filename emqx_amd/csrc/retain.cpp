@@ -50,6 +50,11 @@ struct RSnapshot {
   uint8_t* arena = nullptr;
   uint32_t* rank_id = nullptr;
   int64_t* rank_exp = nullptr;
+  RPostKey* pkeys = nullptr;
+  uint2* posts = nullptr;
+  uint32_t* dterm_off = nullptr;
+  uint32_t* dterm = nullptr;
+  uint16_t* rank_depth = nullptr;
   RetainView rv{};
   uint64_t n_nodes = 0, n_words = 0, bytes = 0;
   ~RSnapshot() {
@@ -63,6 +68,11 @@ struct RSnapshot {
     rfree(arena);
     rfree(rank_id);
     rfree(rank_exp);
+    rfree(pkeys);
+    rfree(posts);
+    rfree(dterm_off);
+    rfree(dterm);
+    rfree(rank_depth);
     (void)hipSetDevice(cur);
   }
 };
@@ -217,11 +227,13 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   order.reserve(nn);
   std::vector<RNode> nodes(nn);
   order.push_back(0);
+  std::vector<uint32_t> depth(nn, 0);
   for (uint64_t k = 0; k < order.size(); ++k) {
     const uint32_t v = order[k];
     const uint32_t cb = static_cast<uint32_t>(order.size());
     uint32_t nc = 0;
     for (uint32_t c = first_child[v]; c != WID_NONE; c = next_sib[c]) {
+      depth[order.size()] = depth[k] + 1;
       order.push_back(c);
       ++nc;
     }
@@ -252,6 +264,25 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
       }
     }
   }
+  // per-depth rank lists (ascending: ranks follow DFS preorder)
+  uint32_t max_depth = 0;
+  for (uint64_t k = 0; k < nn; ++k)
+    if (nodes[k].ncld & RNODE_TERM) max_depth = std::max(max_depth, depth[k]);
+  std::vector<uint32_t> dterm_off(max_depth + 2, 0), dterm(std::max<uint64_t>(rank_id.size(), 1));
+  std::vector<uint16_t> rank_depth;
+  for (uint64_t k = 0; k < nn; ++k)
+    if (nodes[k].ncld & RNODE_TERM) dterm_off[depth[k] + 1] += 1;
+  for (uint32_t d = 0; d <= max_depth; ++d) dterm_off[d + 1] += dterm_off[d];
+  {
+    std::vector<uint32_t> cur(dterm_off.begin(), dterm_off.end() - 1);
+    std::vector<uint32_t> depth_of_rank(rank_id.size());
+    for (uint64_t k = 0; k < nn; ++k)
+      if (nodes[k].ncld & RNODE_TERM) depth_of_rank[nodes[k].lo] = depth[k];
+    for (uint64_t rk = 0; rk < rank_id.size(); ++rk) dterm[cur[depth_of_rank[rk]]++] = static_cast<uint32_t>(rk);
+    rank_depth.resize(std::max<uint64_t>(rank_id.size(), 1), 0);
+    for (uint64_t rk = 0; rk < rank_id.size(); ++rk)
+      rank_depth[rk] = static_cast<uint16_t>(std::min<uint32_t>(depth_of_rank[rk], 65535));
+  }
   std::vector<int64_t> rank_exp(rank_id.size());
   uint32_t has_exp = 0;
   for (uint64_t i = 0; i < rank_id.size(); ++i) {
@@ -273,6 +304,34 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
       edges[s] = REdge{static_cast<uint32_t>(v), w, c, 0};
     }
   }
+  // level postings: nodes grouped by (depth, word), each group sorted by lo
+  std::vector<uint32_t> pid(nn > 0 ? nn - 1 : 0);
+  for (uint64_t k = 1; k < nn; ++k) pid[k - 1] = static_cast<uint32_t>(k);
+  std::sort(pid.begin(), pid.end(), [&](uint32_t x, uint32_t y) {
+    if (depth[x] != depth[y]) return depth[x] < depth[y];
+    const uint32_t wx = wid_of[order[x]], wy = wid_of[order[y]];
+    if (wx != wy) return wx < wy;
+    return nodes[x].lo < nodes[y].lo;
+  });
+  std::vector<uint2> posts(std::max<uint64_t>(pid.size(), 1));
+  std::vector<RPostKey> groups;
+  for (uint64_t i = 0; i < pid.size(); ++i) {
+    const uint32_t x = pid[i];
+    posts[i] = make_uint2(nodes[x].lo, x);
+    const uint32_t d = depth[x], w = wid_of[order[x]];
+    if (groups.empty() || groups.back().depth != d || groups.back().wid != w)
+      groups.push_back(RPostKey{d, w, static_cast<uint32_t>(i), 0});
+    groups.back().len += 1;
+  }
+  uint64_t pcap = 1024;
+  while (pcap < 2 * groups.size()) pcap <<= 1;
+  std::vector<RPostKey> pkeys(pcap, RPostKey{WID_NONE, 0, 0, 0});
+  const uint32_t pmask = static_cast<uint32_t>(pcap - 1);
+  for (const RPostKey& g : groups) {
+    uint32_t sl = rpost_slot0(g.depth, g.wid) & pmask;
+    while (pkeys[sl].depth != WID_NONE) sl = (sl + 1) & pmask;
+    pkeys[sl] = g;
+  }
   vs.build_table();
 
   auto sn = std::make_shared<RSnapshot>();
@@ -284,6 +343,16 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   RT_TRY(ralloc(sn->arena, vs.arena.size() + 16));
   RT_TRY(ralloc(sn->rank_id, nr));
   RT_TRY(ralloc(sn->rank_exp, nr));
+  RT_TRY(ralloc(sn->pkeys, pcap));
+  RT_TRY(ralloc(sn->posts, posts.size()));
+  RT_TRY(hipMemcpy(sn->pkeys, pkeys.data(), pcap * sizeof(RPostKey), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->posts, posts.data(), posts.size() * sizeof(uint2), hipMemcpyHostToDevice));
+  RT_TRY(ralloc(sn->dterm_off, dterm_off.size()));
+  RT_TRY(ralloc(sn->dterm, dterm.size()));
+  RT_TRY(hipMemcpy(sn->dterm_off, dterm_off.data(), dterm_off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->dterm, dterm.data(), dterm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  RT_TRY(ralloc(sn->rank_depth, rank_depth.size()));
+  RT_TRY(hipMemcpy(sn->rank_depth, rank_depth.data(), rank_depth.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   RT_TRY(hipMemcpy(sn->nodes, nodes.data(), nn * sizeof(RNode), hipMemcpyHostToDevice));
   RT_TRY(hipMemcpy(sn->edges, edges.data(), ecap * sizeof(REdge), hipMemcpyHostToDevice));
   RT_TRY(hipMemcpy(sn->vocab, vs.table.data(), vs.table.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
@@ -301,12 +370,20 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   rv.vocab_mask = vs.mask;
   rv.rank_id = sn->rank_id;
   rv.rank_exp = sn->rank_exp;
+  rv.pkeys = sn->pkeys;
+  rv.pkey_mask = pmask;
+  rv.posts = sn->posts;
+  rv.dterm_off = sn->dterm_off;
+  rv.dterm = sn->dterm;
+  rv.max_depth = max_depth;
+  rv.rank_depth = sn->rank_depth;
   rv.n_nodes = rank_id.empty() ? 0u : static_cast<uint32_t>(nn);
   rv.has_expiring = has_exp;
   sn->n_nodes = nn;
   sn->n_words = vs.n_words();
   sn->bytes = nn * sizeof(RNode) + ecap * sizeof(REdge) + vs.table.size() * sizeof(VocabSlot) + vs.arena.size() +
-              nr * (sizeof(uint32_t) + sizeof(int64_t));
+              nr * (sizeof(uint32_t) + sizeof(int64_t)) + pcap * sizeof(RPostKey) + posts.size() * sizeof(uint2) +
+              (dterm_off.size() + dterm.size()) * sizeof(uint32_t) + rank_depth.size() * sizeof(uint16_t);
   *out = std::move(sn);
   return EMQX_OK;
 }

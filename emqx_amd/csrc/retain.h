@@ -6,7 +6,8 @@
 // subscription with a full-table match-spec select (match_messages/1, :211-215, condition/1
 // :226-232).  Here the stored topics form a level trie over interned words (no wildcards in
 // it: they are published topics) and a FILTER walks it — the inverse of the route lookup:
-//   literal word -> one hashed child lookup;  '+' -> every child (one range item);
+//   literal word -> one hashed child lookup;  '+' -> every child (one range item), or, when
+//                   a literal follows the '+' run, one slice of that literal's level postings;
 //   final '#'    -> the node's whole subtree, which is ONE contiguous range of topic ranks,
 //                   because ranks are numbered in depth-first preorder.
 // So a walk emits rank ranges, and the output stage copies rank -> topic id for the live
@@ -43,6 +44,19 @@ EMQX_HD uint32_t redge_slot0(uint32_t parent, uint32_t wid) {
   return mix32(parent * 0x9E3779B1u ^ mix32(wid + 0x7F4A7C15u));
 }
 
+// Level postings: every node at depth d reached by word w, sorted by its first rank `lo`
+// (same-depth subtrees are disjoint, so `lo` orders them and a subtree of v is the slice with
+// lo in [v.lo, v.hi)).  A run of '+' levels followed by a literal w is answered from the
+// postings of (depth after the run, w) inside the current node's rank interval — a binary
+// search instead of visiting every child (and grandchild) the '+' run spans.
+struct alignas(16) RPostKey {
+  uint32_t depth;  // WID_NONE = empty slot
+  uint32_t wid;
+  uint32_t off;    // first entry in posts[]
+  uint32_t len;
+};
+EMQX_HD uint32_t rpost_slot0(uint32_t depth, uint32_t wid) { return mix32(wid * 0x9E3779B1u + depth * 0x85EBCA77u); }
+
 struct RetainView {
   const RNode* nodes;
   const REdge* edges;
@@ -52,16 +66,33 @@ struct RetainView {
   uint32_t vocab_mask;
   const uint32_t* rank_id;    // [n_ranks] topic id of each rank
   const int64_t* rank_exp;    // [n_ranks] expiry (ms, 0 = never)
+  const RPostKey* pkeys;      // (depth, wid) -> postings slice
+  uint32_t pkey_mask;
+  const uint2* posts;         // {lo, node} per node but the root, grouped by (depth, wid)
+  const uint32_t* dterm_off;  // [max_depth + 2] per depth: first entry in dterm
+  const uint32_t* dterm;      // ranks of the stored topics, grouped by depth (levels), ascending
+  const uint16_t* rank_depth; // [n_ranks] levels of each stored topic (capped at 65535)
+  uint32_t max_depth;
   uint32_t n_nodes;           // 0: empty table
   uint32_t has_expiring;      // some rank has a nonzero expiry
 };
 
-// Range emitted by the walk: filter f's matches include ranks [lo, hi).
+// Work item of the walk (uint4): x = first node (or first postings entry), y = count,
+// z = level, w = filter lane | RITEM_POST (the item is a postings slice)
+constexpr uint32_t RITEM_POST = 1u << 8;
+
+// Range emitted by the walk: filter f's matches include ranks [lo, hi), or, RRANGE_INDIRECT,
+// the ranks dterm[lo .. hi) (a filter ending in a '+' run: the stored topics of that many
+// levels inside a subtree, a contiguous slice of the per-depth rank list).
+constexpr uint32_t RRANGE_STRICT = 1;    // expiry guard expiry > now (match spec); else >= now (read)
+constexpr uint32_t RRANGE_INDIRECT = 2;
+constexpr uint32_t RRANGE_MIND_SHIFT = 8;  // flags >> 8: only ranks of at least this many levels
+                                           // (a '+' run then '#': the subtree minus shallow topics)
 struct RRange {
   uint32_t f;
   uint32_t lo;
   uint32_t hi;
-  uint32_t strict;  // expiry guard: 1 = expiry > now (match spec), 0 = expiry >= now (read)
+  uint32_t flags;  // RRANGE_*
 };
 
 // ctrl words of one call (zeroed per call)
@@ -79,7 +110,6 @@ struct RetainArgs {
   uint64_t n;
   int64_t now_ms;          // < 0: no expiry guard (match_delete_messages)
   uint32_t* wids;          // [foffs[n] - foffs[0] + n] scratch: word ids, filter f at foffs[f] - foffs[0] + f
-  uint32_t* flev;          // [n] levels | 1 << 31 if the filter is a wildcard
   uint4* stack;            // [waves * stack_cap] per-wave work stacks (range items)
   uint32_t stack_cap;
   uint32_t waves;

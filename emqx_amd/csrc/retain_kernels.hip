@@ -56,12 +56,32 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t* tot) {
   return x - v;
 }
 
-__device__ __forceinline__ bool rank_live(const RetainView& rv, uint32_t i, int64_t now, uint32_t strict) {
-  const int64_t e = rv.rank_exp[i];
-  return e == 0 || (strict ? e > now : e >= now);
+__device__ __forceinline__ bool rank_live(const RetainView& rv, uint32_t rank, int64_t now, uint32_t flags) {
+  const int64_t e = rv.rank_exp[rank];
+  return e == 0 || ((flags & RRANGE_STRICT) ? e > now : e >= now);
+}
+
+__device__ __forceinline__ bool rank_ok(const RetainView& rv, uint32_t rank, bool guard, int64_t now, uint32_t flags) {
+  const uint32_t mind = flags >> RRANGE_MIND_SHIFT;
+  return (!guard || rank_live(rv, rank, now, flags)) && (mind == 0 || rv.rank_depth[rank] >= mind);
+}
+
+__device__ __forceinline__ uint32_t rank_at(const RetainView& rv, uint32_t i, uint32_t flags) {
+  return (flags & RRANGE_INDIRECT) ? rv.dterm[i] : i;
+}
+
+// first index in [l, h) of the ascending u32 array a (stride in words) with a[i] >= x
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t stride, uint32_t l, uint32_t h,
+                                                    uint32_t x) {
+  while (l < h) {
+    const uint32_t m = (l + h) >> 1;
+    if (a[static_cast<uint64_t>(m) * stride] < x) l = m + 1; else h = m;
+  }
+  return l;
 }
 
 constexpr int RW_WAVES = 4;
+constexpr uint32_t RCHUNK = 2048;  // ranks per range record
 
 }  // namespace
 
@@ -169,8 +189,9 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
         const uint32_t before = lo ? pref[lo - 1] : 0u;
         const uint4 q = itm[lo];
         v = q.x + (lane - before);
+        if (q.w & RITEM_POST) v = rv.posts[v].y;  // a postings slice: entry -> node
         lev = q.z;
-        fl = q.w;
+        fl = q.w & 63u;
       }
       __builtin_amdgcn_wave_barrier();
       bool emit = false, push = false;
@@ -183,7 +204,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
         const uint32_t fn = nl & 0x7FFFFFFFu;
         const uint64_t fg = t * 64 + fl;
         rg.f = static_cast<uint32_t>(fg);
-        rg.strict = nl >> 31;
+        rg.flags = nl >> 31;  // wildcard filter: the match spec's strict guard
         if (lev == fn) {
           if (rn.ncld & RNODE_TERM) {
             emit = true;
@@ -198,8 +219,53 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
             rg.lo = rn.lo;
             rg.hi = rn.hi;
           } else if (w == WID_PLUS) {
-            push = ncld != 0;
-            np = make_uint4(rn.cbeg, ncld, lev + 1, fl);
+            // the '+' run from this level, then: a literal -> its postings at the depth after
+            // the run, inside this node's rank interval; else ('#', the filter's end) the
+            // children range
+            uint32_t j = lev + 1;
+            while (j < fn && a.wids[wbase[fl] + j] == WID_PLUS) ++j;
+            const uint32_t wl = j < fn ? a.wids[wbase[fl] + j] : WID_HASH;
+            if (ncld == 0 || wl == WID_NONE) {
+              push = false;
+            } else if (j == fn) {
+              // the filter ends with this '+' run: the stored topics of exactly fn levels in
+              // this subtree = one slice of the depth-fn rank list
+              if (fn <= rv.max_depth) {
+                const uint32_t d0 = rv.dterm_off[fn], d1 = rv.dterm_off[fn + 1];
+                const uint32_t b = v ? lower_bound_u32(rv.dterm, 1, d0, d1, rn.lo) : d0;
+                const uint32_t e = v ? lower_bound_u32(rv.dterm, 1, b, d1, rn.hi) : d1;
+                emit = e > b;
+                rg.lo = b;
+                rg.hi = e;
+                rg.flags |= RRANGE_INDIRECT;
+              }
+            } else if (wl == WID_HASH) {
+              // '+' run then the final '#': this subtree's topics of at least j levels — one
+              // rank range with a depth floor, filtered by the output kernels
+              emit = rn.hi > rn.lo;
+              rg.lo = rn.lo;
+              rg.hi = rn.hi;
+              rg.flags |= j << RRANGE_MIND_SHIFT;
+            } else {
+              uint32_t s = rpost_slot0(j + 1, wl) & rv.pkey_mask;
+              uint32_t off = 0, len = 0;
+              for (uint32_t k = 0; k <= rv.pkey_mask; ++k) {
+                const RPostKey pk = rv.pkeys[s];
+                if (pk.depth == WID_NONE) break;
+                if (pk.depth == j + 1 && pk.wid == wl) {
+                  off = pk.off;
+                  len = pk.len;
+                  break;
+                }
+                s = (s + 1) & rv.pkey_mask;
+              }
+              // slice of entries with lo in [rn.lo, rn.hi): two lower bounds
+              const uint32_t* px = reinterpret_cast<const uint32_t*>(rv.posts);
+              const uint32_t b = v ? lower_bound_u32(px + 2ull * off, 2, 0, len, rn.lo) : 0u;
+              const uint32_t e = v ? lower_bound_u32(px + 2ull * off, 2, b, len, rn.hi) : len;
+              push = e > b;
+              np = make_uint4(off + b, e - b, j + 1, fl | RITEM_POST);
+            }
           } else if (w != WID_NONE && ncld != 0) {
             uint32_t s = redge_slot0(v, w) & rv.edge_mask;
             for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
@@ -216,13 +282,22 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
         }
       }
       // ---- emissions (one atomic per wave step) --------------------------------------------
+      // a range longer than RCHUNK ranks goes out as several records, so the output kernels
+      // spread one '#' over the whole subtree across many waves
+      const uint32_t nrec = emit ? (rg.hi - rg.lo + RCHUNK - 1) / RCHUNK : 0u;
       uint32_t etot;
-      const uint32_t epos = wave_excl(emit ? 1u : 0u, &etot);
+      const uint32_t epos = wave_excl(nrec, &etot);
       if (etot) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(&a.ctrl[RC_RANGES], etot);
         base = __shfl(base, 0, 64);
-        if (emit && base + epos < a.range_cap) a.ranges[base + epos] = rg;
+        for (uint32_t k = 0; k < nrec; ++k) {
+          if (base + epos + k >= a.range_cap) break;
+          RRange part = rg;
+          part.lo = rg.lo + k * RCHUNK;
+          part.hi = min(rg.hi, part.lo + RCHUNK);
+          a.ranges[base + epos + k] = part;
+        }
       }
       // ---- pushes ---------------------------------------------------------------------------
       uint32_t qtot;
@@ -260,30 +335,33 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t 
     const uint32_t len = rg.hi - rg.lo;
     uint32_t c = 0;
     uint64_t pos = 0;
+    const bool check = guard || (rg.flags >> RRANGE_MIND_SHIFT) != 0;  // per-rank filtering needed
     if (MODE == 0) {
-      if (valid && (!guard || len <= 1)) c = (!guard || (len == 1 && rank_live(rv, rg.lo, a.now_ms, rg.strict))) ? len : 0u;
+      if (valid && (!check || len <= 1))
+        c = (!check || (len == 1 && rank_ok(rv, rank_at(rv, rg.lo, rg.flags), guard, a.now_ms, rg.flags))) ? len : 0u;
     } else if (valid) {
       c = a.rcount[r];
       if (c) pos = a.out_off[rg.f] + atomicAdd(&a.fcursor[rg.f], c);
-      if (c && len == 1 && pos < a.out_cap) a.out_ids[pos] = rv.rank_id[rg.lo];
+      if (c && len == 1 && pos < a.out_cap) a.out_ids[pos] = rv.rank_id[rank_at(rv, rg.lo, rg.flags)];
     }
     // wave-cooperative ranges: longer than one rank (and, when counting, only under a guard)
-    uint64_t big = __ballot(valid && len > 1 && (MODE == 1 ? c != 0 : guard));
+    uint64_t big = __ballot(valid && len > 1 && (MODE == 1 ? c != 0 : check));
     while (big) {
       const uint32_t b = __ffsll(static_cast<unsigned long long>(big)) - 1;
       big &= big - 1;
-      const uint32_t lo = __shfl(rg.lo, b, 64), hi = __shfl(rg.hi, b, 64), strict = __shfl(rg.strict, b, 64);
+      const uint32_t lo = __shfl(rg.lo, b, 64), hi = __shfl(rg.hi, b, 64), fg = __shfl(rg.flags, b, 64);
       uint64_t p = __shfl(pos, b, 64);
       uint32_t cnt = 0;
       for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
         const uint32_t i = i0 + lane;
-        const bool live = i < hi && (!guard || rank_live(rv, i, a.now_ms, strict));
+        const uint32_t rk = i < hi ? rank_at(rv, i, fg) : 0u;
+        const bool live = i < hi && rank_ok(rv, rk, guard, a.now_ms, fg);
         if (MODE == 0) {
           cnt += live ? 1u : 0u;
         } else {
           const uint64_t m = __ballot(live);
           const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-          if (live && p + rank < a.out_cap) a.out_ids[p + rank] = rv.rank_id[i];
+          if (live && p + rank < a.out_cap) a.out_ids[p + rank] = rv.rank_id[rk];
           p += __popcll(m);
         }
       }

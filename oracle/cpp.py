@@ -36,6 +36,10 @@ def lib():
         L.orc_match.argtypes = [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                 u32p, u32p, ctypes.c_uint32]
         L.orc_evals.argtypes = [vp, u8p, u64p, ctypes.c_uint64, u64p]
+        L.orr_create.restype = vp
+        L.orr_create.argtypes = [u8p, u64p, ctypes.c_uint64, vp]
+        L.orr_destroy.argtypes = [vp]
+        L.orr_select.argtypes = [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, u32p, u64p]
         L.orc_topic_match.restype = ctypes.c_int
         L.orc_topic_match.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64]
         _lib = L
@@ -118,3 +122,24 @@ def topic_match(name: bytes, filt: bytes) -> bool:
     nb = np.frombuffer(name or b"\0", np.uint8)
     fb = np.frombuffer(filt or b"\0", np.uint8)
     return bool(lib().orc_topic_match(_p(nb), len(name), _p(fb), len(filt)))
+
+
+class RetainScan:
+    """oracle/retain_oracle.cpp: the reference's retained lookup as it runs (full-table
+    match-spec select per wildcard filter, key read per plain one)."""
+
+    def __init__(self, buf, offs, expiry=None):
+        self._exp = None if expiry is None else np.ascontiguousarray(np.asarray(expiry, dtype=np.int64))
+        self.h = lib().orr_create(_p(buf), _p(offs), len(offs) - 1, _p(self._exp) if self._exp is not None else None)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orr_destroy(self.h)
+            self.h = None
+
+    def select_packed(self, buf, offs, now: int, threads: int = 1):
+        n = len(offs) - 1
+        counts = np.zeros(max(n, 1), dtype=np.uint32)
+        sums = np.zeros(max(n, 1), dtype=np.uint64)
+        lib().orr_select(self.h, _p(buf), _p(offs), n, now, threads, _p(counts), _p(sums))
+        return counts[:n], sums[:n]

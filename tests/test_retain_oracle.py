@@ -111,3 +111,28 @@ def test_token_trie_equals_brute_force():
                     exp = sorted(t.match_messages(f, None)) if R.wildcard(f) else sorted(
                         [t.ids[f]] if f in t.ids and t.live[t.ids[f]] else [])
                     assert got == exp, (f, "no guard")
+
+
+def test_cpp_scan_equals_python_oracle():
+    """oracle/retain_oracle.cpp (the bench's CPU baseline) == oracle/retain_ref.py."""
+    import numpy as np
+    from oracle import cpp as C
+    rng = random.Random(12)
+    vocab = [b"a", b"b", b"", b"$SYS", b"longer-than-sixteen-bytes"]
+    names = sorted({b"/".join(rng.choice(vocab) for _ in range(rng.randint(1, 5))) for _ in range(300)})
+    expiry = [rng.choice([0, 0, 50, 100, 150]) for _ in names]
+    filters = []
+    for _ in range(400):
+        lv = [rng.choice(vocab + [b"+", b"zz"]) for _ in range(rng.randint(1, 5))]
+        if rng.random() < 0.35:
+            lv[-1] = b"#"
+        filters.append(b"/".join(lv))
+    filters += [b"#", b"+", b"", b"#/#"]
+    sc = C.RetainScan(*C.pack(names), expiry)
+    tt = RR.TokenTrie(names, expiry)
+    for now in (100, -1):
+        counts, sums = sc.select_packed(*C.pack(filters), now, threads=3)
+        for k, f in enumerate(filters):
+            x = tt.dispatch(f, now)
+            assert int(counts[k]) == len(x) and int(sums[k]) == sum(x), (f, now)
+    assert np.all(counts >= 0)
