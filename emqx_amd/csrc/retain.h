@@ -3,8 +3,8 @@
 //
 // Reference: the mnesia retainer keeps one record per retained topic, keyed by its token list
 // (apps/emqx_retainer/src/emqx_retainer_mnesia.erl:74-98), and answers a wildcard
-// subscription with a full-table match-spec select (match_messages/1, :211-215, condition/1
-// :226-232).  Here the stored topics form a level trie over interned words (no wildcards in
+// subscription with a full-table match-spec select (match_messages/1, :212-215, condition/1
+// :225-231).  Here the stored topics form a level trie over interned words (no wildcards in
 // it: they are published topics) and a FILTER walks it — the inverse of the route lookup:
 //   literal word -> one hashed child lookup;  '+' -> every child (one range item), or, when
 //                   a literal follows the '+' run, one slice of that literal's level postings;

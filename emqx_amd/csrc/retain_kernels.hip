@@ -1,6 +1,6 @@
 // Retained-message index kernels (retain.h): a batch of subscription filters against the
 // trie of stored retained topics (reference: the match-spec select of
-// apps/emqx_retainer/src/emqx_retainer_mnesia.erl:211-246 and read_messages/1 :198-208).
+// apps/emqx_retainer/src/emqx_retainer_mnesia.erl:212-258 and read_messages/1 :199-208).
 //
 //   walk    one wavefront per tile of 64 filters (persistent waves).  Each lane tokenizes and
 //           interns its own filter (filters are short; subscription-path work), then the wave

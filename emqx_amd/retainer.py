@@ -8,12 +8,12 @@ messages on the host keyed by topic id, as the ``?TAB`` record keeps ``msg`` bes
 key, and asks the index which topics a subscription filter selects:
 
   store_retained/2   -> RetainIndex.store (table-full rule of :74-98)
-  read_message/2     -> exact id lookup, ``expiry == 0 or expiry >= now`` (:198-208)
+  read_message/2     -> exact id lookup, ``expiry == 0 or expiry >= now`` (:199-208)
   match_messages/3   -> RetainIndex.match, sorted by timestamp (sort_retained/1), cursor
-                        batches of max_read_number (:145-158, :181-196)
-  delete_message/2   -> exact delete, or match_delete_messages/1 for a wildcard (:112-122)
+                        batches of max_read_number (:146-158, :182-196)
+  delete_message/2   -> exact delete, or match_delete_messages/1 for a wildcard (:117-128)
   clear_expired/1, page_read/4, clean/1, size/1
-  dispatch/4         -> emqx_retainer.erl:122-131 (plain -> read, wildcard -> match)
+  dispatch/4         -> emqx_retainer.erl:119-131 (plain -> read, wildcard -> match)
 
 Mutations are published by one commit the next time a lookup needs them.
 """
@@ -175,7 +175,7 @@ class MnesiaRetainer:
     def size(self) -> int:
         return len(self._msgs)
 
-    # emqx_retainer_mnesia.erl:198-208
+    # emqx_retainer_mnesia.erl:199-208
     def read_message(self, topic: bytes, now: Optional[int] = None) -> List[Message]:
         now = now_ms() if now is None else now
         tid = self.index.lookup(topic)
@@ -189,7 +189,7 @@ class MnesiaRetainer:
         ms.sort(key=lambda m: m.timestamp)  # sort_retained/1: stable by timestamp
         return ms
 
-    # emqx_retainer_mnesia.erl:145-158 (+ start_batch_read/2, batch_read_messages/2)
+    # emqx_retainer_mnesia.erl:146-158 (+ start_batch_read/2, batch_read_messages/2)
     def match_messages(self, filt: bytes, cursor=None, now: Optional[int] = None):
         if cursor is None:
             self._sync()
@@ -206,7 +206,7 @@ class MnesiaRetainer:
         self._sync()
         return [self._sorted(ids) for ids in self.index.match(filters, now_ms() if now is None else now)]
 
-    # emqx_retainer_mnesia.erl:112-122, 217-223
+    # emqx_retainer_mnesia.erl:117-128, 217-223
     def delete_message(self, topic: bytes) -> None:
         from .topic import wildcard
         if wildcard(topic):
@@ -222,7 +222,7 @@ class MnesiaRetainer:
                     self._msgs.pop(int(i), None)
                 self._dirty = True
 
-    # emqx_retainer_mnesia.erl:101-110
+    # emqx_retainer_mnesia.erl:106-115
     def clear_expired(self, now: Optional[int] = None) -> None:
         with self._lock:
             ids = self.index.expired(now_ms() if now is None else now)
@@ -232,7 +232,7 @@ class MnesiaRetainer:
                     self._msgs.pop(int(i), None)
                 self._dirty = True
 
-    # emqx_retainer_mnesia.erl:133-143
+    # emqx_retainer_mnesia.erl:133-144
     def page_read(self, topic: Optional[bytes], page: int, limit: int, now: Optional[int] = None) -> List[Message]:
         self._sync()
         if topic is None:
@@ -252,7 +252,7 @@ class MnesiaRetainer:
             self._msgs.clear()
             self._dirty = True
 
-    # emqx_retainer.erl:89-106: retained publish stores, an empty retained payload deletes
+    # emqx_retainer.erl:90-107: retained publish stores, an empty retained payload deletes
     def on_message_publish(self, msg: Message, retain: bool = True) -> None:
         if not retain:
             return
@@ -261,7 +261,7 @@ class MnesiaRetainer:
         else:
             self.store_retained(msg)
 
-    # emqx_retainer.erl:122-131
+    # emqx_retainer.erl:119-131
     def dispatch(self, filt: bytes, now: Optional[int] = None) -> List[Message]:
         from .topic import wildcard
         if not wildcard(filt):

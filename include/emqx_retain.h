@@ -7,18 +7,18 @@
  *
  *   emqx_retainer_mnesia:store_retained/2     apps/emqx_retainer/src/emqx_retainer_mnesia.erl:74-98
  *       -> emqx_retain_store (+ emqx_retain_commit: batched rebuild, snapshot swap)
- *   emqx_retainer_mnesia:delete_message/2     emqx_retainer_mnesia.erl:112-122
+ *   emqx_retainer_mnesia:delete_message/2     emqx_retainer_mnesia.erl:117-128
  *       -> emqx_retain_lookup + emqx_retain_delete (exact topic); a wildcard topic
  *          (match_delete_messages/1, :217-223) -> emqx_retain_match_batch(now_ms = -1)
  *          + emqx_retain_delete of the returned ids
- *   emqx_retainer_mnesia:clear_expired/1      emqx_retainer_mnesia.erl:101-110
+ *   emqx_retainer_mnesia:clear_expired/1      emqx_retainer_mnesia.erl:106-115
  *       -> emqx_retain_expired + emqx_retain_delete
- *   emqx_retainer:dispatch/4 -> read_message/2 (plain filter, :198-208) or match_messages/3
- *       (wildcard filter, :211-215 + make_match_spec/1 :234-246)
+ *   emqx_retainer:dispatch/4 -> read_message/2 (plain filter, :199-208) or match_messages/3
+ *       (wildcard filter, :212-215 + make_match_spec/1 :233-245)
  *       -> emqx_retain_match_batch: one call for a batch of filters (a subscribe storm),
  *          each filter answered as dispatch/4 would (plain: expiry == 0 || expiry >= now;
  *          wildcard: expiry == 0 || expiry > now; no '$' rule — the match spec has none).
- *   emqx_retainer_mnesia:size/1               emqx_retainer_mnesia.erl:174-176
+ *   emqx_retainer_mnesia:size/1               emqx_retainer_mnesia.erl:164-165
  *       -> emqx_retain_stats(...).n_live
  *
  * Ordering: the reference sorts a wildcard answer by message timestamp (sort_retained/1,

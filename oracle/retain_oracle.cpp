@@ -3,9 +3,9 @@
 // C++ restatement of the reference's retained-message lookup, the way the reference runs it:
 //   * a wildcard filter is answered by mnesia:dirty_select(?TAB, MatchSpec) over a `set`
 //     table, i.e. a scan of EVERY record, testing condition/1's pattern against the record's
-//     token list and the expiry guard (apps/emqx_retainer/src/emqx_retainer_mnesia.erl:211-246)
+//     token list and the expiry guard (apps/emqx_retainer/src/emqx_retainer_mnesia.erl:212-258)
 //   * a plain filter is mnesia:dirty_read(?TAB, Tokens): one key lookup, then
-//     Et =:= 0 orelse Et >= NowMs (:198-208)
+//     Et =:= 0 orelse Et >= NowMs (:199-208)
 // Used as bench.py's cpu_baseline for --workload R (kind "port") and, on small tables, as
 // a second checker beside oracle/retain_ref.py.
 #include <stdint.h>

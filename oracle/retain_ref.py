@@ -6,18 +6,18 @@ matches).  Pure Python, for small tables:
 
   * topic2tokens/1            apps/emqx_retainer/src/emqx_retainer_mnesia.erl:178-179
                               (= emqx_topic:words/1, apps/emqx/src/emqx_topic.erl:153-164)
-  * condition/1               emqx_retainer_mnesia.erl:226-232: '+' -> '_' (any one token,
+  * condition/1               emqx_retainer_mnesia.erl:225-231: '+' -> '_' (any one token,
                               the empty level included); a final '#' is dropped (`Ws1 --
                               ['#']` removes the FIRST '#') and the list gets the improper
                               tail '_' (any tail, the empty one included).  Unlike routing
                               (emqx_topic:match/2) there is NO '$' rule: the match spec
                               never looks at the first level, so '#' and '+/...' match
                               '$SYS/...' topics too.
-  * make_match_spec/1         emqx_retainer_mnesia.erl:234-246: live iff expiry_time =:= 0
+  * make_match_spec/1         emqx_retainer_mnesia.erl:233-245: live iff expiry_time =:= 0
                               or expiry_time > NowMs
-  * read_messages/1           emqx_retainer_mnesia.erl:198-208: exact key, live iff
+  * read_messages/1           emqx_retainer_mnesia.erl:199-208: exact key, live iff
                               Et =:= 0 orelse Et >= NowMs   (note >= here, > above)
-  * dispatch/4                apps/emqx_retainer/src/emqx_retainer.erl:122-131: plain
+  * dispatch/4                apps/emqx_retainer/src/emqx_retainer.erl:119-131: plain
                               filter -> read_message/2, wildcard filter -> match_messages/3
   * match_delete_messages/1   emqx_retainer_mnesia.erl:217-223: condition/1 without the
                               expiry guard
@@ -37,7 +37,7 @@ def topic2tokens(topic: bytes) -> list:
 
 
 def condition(ws: list):
-    """emqx_retainer_mnesia.erl:226-232.  Returns (prefix, open_tail): the pattern matches a
+    """emqx_retainer_mnesia.erl:225-231.  Returns (prefix, open_tail): the pattern matches a
     token list L iff len(prefix) elements match pairwise (ANY matches anything) and either
     len(L) == len(prefix) or open_tail."""
     ws1 = [ANY if w == PLUS else w for w in ws]
@@ -100,13 +100,13 @@ class RetainTable:
         return [i] if (e == 0 or e >= now_ms) else []
 
     def dispatch(self, filt: bytes, now_ms: int) -> List[int]:
-        """emqx_retainer.erl:122-131 (the ids whose messages are delivered, unordered)."""
+        """emqx_retainer.erl:119-131 (the ids whose messages are delivered, unordered)."""
         if wildcard(filt):
             return self.match_messages(filt, now_ms)
         return self.read_messages(filt, now_ms)
 
     def delete_message(self, topic: bytes) -> None:
-        """emqx_retainer_mnesia.erl:112-122."""
+        """emqx_retainer_mnesia.erl:117-128."""
         if wildcard(topic):
             self.delete_ids(self.match_messages(topic, None))
         else:

@@ -213,8 +213,8 @@ BENCH = {"src": "apps/emqx/src/emqx_broker_bench.erl:25-34,146-162",
 
 # emqx_retainer_SUITE (mnesia backend): retained topics as stored, then the subscriptions a
 # client makes and the messages it receives.  ops: ["store", topic, expiry_ms] (0 = never,
-# emqx_retainer.erl:150-165 with msg_expiry_interval "0s"), ["publish_empty", topic] (a
-# retained empty payload deletes, emqx_retainer.erl:89-101), ["delete", topic]
+# emqx_retainer.erl:157-168 with msg_expiry_interval "0s"), ["publish_empty", topic] (a
+# retained empty payload deletes, emqx_retainer.erl:90-101), ["delete", topic]
 # (emqx_retainer:delete/1 -> delete_message/2, wildcard -> match_delete_messages/1).
 # queries: [now_ms, filter, expected sorted topics] — dispatch/4 picks read_message/2 for a
 # plain filter (expiry >= now) and match_messages/3 for a wildcard one (expiry > now).
