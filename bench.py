@@ -77,6 +77,12 @@ def main():
                     help="filter-sharded table (filter i on rank i mod N): rank 0's batch is broadcast over "
                          "RCCL, matched on every shard, gathered and concatenated on rank 0 (strong scaling)")
     ap.add_argument("--vocab-scale", type=int, default=1, help="4 = config C's vocabulary")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="HIP streams the timed batches alternate over (pipelined calls)")
+    ap.add_argument("--order", type=str, default="none", choices=["none", "sorted", "xcd"],
+                    help="experiment: host-side permutation of the topic batch (sorted = lexicographic; "
+                         "xcd = sorted, cut into 8 key-range segments, dealt 256 topics at a time so each "
+                         "XCD's blocks see one segment)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per kernel launch from PMC (rocprofv3 FETCH_SIZE/WRITE_SIZE)")
     args = ap.parse_args()
@@ -116,6 +122,8 @@ def main():
                                                          vocab_scale=args.vocab_scale,
                                                          topic_seed=None if rank == 0 else 1000 + rank))
     log(f"[rank {rank}] workload: {wl.n_filters} filters, {wl.n_topics} topics ({time.time() - t0:.1f}s)")
+    if args.order != "none":
+        wl = reorder_topics(wl, args.order)
 
     t0 = time.time()
     eng = Engine(local)
@@ -153,15 +161,23 @@ def main():
     # Timed steps are enqueued with emqx_match_batch_device_async, as a pipelined caller
     # would: every step runs the whole pipeline (fast + deep kernels, scan, scatter) and
     # writes its own summary; nothing is skipped, only the host no longer blocks per batch.
+    # Consecutive batches alternate over `--streams` HIP streams (own output buffers each), so
+    # one batch's output assembly overlaps the next batch's match kernel.
     summ = torch.zeros((max(args.steps, 1), eng.SUMMARY_WORDS), dtype=torch.int64, device=dev)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(args.streams - 1)]
+    outs = [(d_off, d_ids)] + [(torch.empty_like(d_off), torch.empty_like(d_ids)) for _ in range(args.streams - 1)]
+    for k in range(len(streams)):  # size each stream's workspace (a synchronous call learns its slab)
+        eng.match_device(tb.data_ptr(), to.data_ptr(), n, outs[k][0].data_ptr(), outs[k][1].data_ptr(), cap,
+                         mode=args.mode, stream=streams[k].cuda_stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        eng.match_device_async(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
-                               summ[k].data_ptr(), mode=args.mode, stream=stream)
+        j = k % len(streams)
+        eng.match_device_async(tb.data_ptr(), to.data_ptr(), n, outs[j][0].data_ptr(), outs[j][1].data_ptr(), cap,
+                               summ[k].data_ptr(), mode=args.mode, stream=streams[j].cuda_stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -726,6 +742,23 @@ def update_cpu_baseline(wl, nb, k, args):
     return {"value": round(ops / t_total, 1), "unit": "updates/s", "cores": 1, "kind": "port",
             "sample": f"{r} rounds of {k} deletes + {k} inserts on a {nbase}-filter table (C++ restatement "
                       "of emqx_trie:insert/delete key maintenance, no mnesia transaction)"}
+
+
+def reorder_topics(wl, order):
+    """A permutation of the same batch (the match sets per topic are unchanged)."""
+    from emqx_amd import workloads as W
+    names = W.unpack(wl.topics)
+    idx = sorted(range(len(names)), key=names.__getitem__)
+    if order == "xcd":
+        n = len(idx)
+        seg = [idx[k * n // 8:(k + 1) * n // 8] for k in range(8)]
+        out, pos = [], [0] * 8
+        while len(out) < n:
+            for k in range(8):
+                out.extend(seg[k][pos[k]:pos[k] + 256])
+                pos[k] += 256
+        idx = out
+    return W.Workload(wl.name, wl.filters, W.take(wl.topics, np.asarray(idx)))
 
 
 def load_or_make(args, rank, make):

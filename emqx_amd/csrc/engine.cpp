@@ -110,6 +110,7 @@ constexpr uint32_t DEEP_WAVES = 32;
 struct Workspace {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t last_stream = nullptr;  // stream of the last call enqueued with this workspace
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evk = nullptr;
   uint64_t cap_n = 0, cap_tiles = 0, cap_slab = 0;
   uint32_t slab_per_tile = 256;
@@ -186,6 +187,7 @@ struct emqx_engine {
   std::atomic<double> last_kernel_ms{0};
   std::atomic<int> forced_variant{-1};
   std::atomic<bool> diag_on{false};
+  std::atomic<uint32_t> slab_hint{256};  // largest slab per tile any workspace needed
   // incremental commits (under `writer`)
   DeltaState ds;
   std::vector<uint32_t> dirty;  // ids inserted / deleted since the last commit
@@ -406,15 +408,27 @@ int commit_locked(emqx_engine* e) {
   return EMQX_OK;
 }
 
-Workspace* acquire_ws(emqx_engine* e) {
+// A free workspace for a call on stream `want` (null: the workspace's own stream).  Prefers
+// one last used on that stream, then one whose last call has drained; otherwise a new one, so
+// calls pipelined on different streams never wait for each other's workspace.
+Workspace* acquire_ws(emqx_engine* e, hipStream_t want = nullptr) {
   std::lock_guard<std::mutex> g(e->ws_mu);
-  if (!e->free_ws.empty()) {
-    Workspace* w = e->free_ws.back();
-    e->free_ws.pop_back();
+  auto& f = e->free_ws;
+  auto take = [&](size_t i) {
+    Workspace* w = f[i];
+    f.erase(f.begin() + static_cast<std::ptrdiff_t>(i));
+    w->slab_per_tile = std::max(w->slab_per_tile, e->slab_hint.load());
     return w;
-  }
+  };
+  if (!f.empty() && !want) return take(f.size() - 1);
+  for (size_t i = f.size(); i-- > 0;)
+    if (f[i]->last_stream == want || !f[i]->last_stream) return take(i);
+  if (f.size() >= 8)  // many streams: reuse a drained workspace rather than grow the pool
+    for (size_t i = f.size(); i-- > 0;)
+      if (!f[i]->done || hipEventQuery(f[i]->done) == hipSuccess) return take(i);
   auto w = std::make_unique<Workspace>();
   w->device = e->device;
+  w->slab_per_tile = std::max(w->slab_per_tile, e->slab_hint.load());
   Workspace* p = w.get();
   e->all_ws.push_back(std::move(w));
   return p;
@@ -526,6 +540,7 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.summary = summary;
 
   HIP_TRY(hipStreamWaitEvent(s, w->done, 0));
+  w->last_stream = s;
   HIP_TRY(hipMemsetAsync(w->ctrl, 0, CTRL_WORDS * sizeof(uint32_t), s));
   HIP_TRY(hipEventRecord(w->ev0, s));
   HIP_TRY(launch_match_fast(a, pick_variant(e, snap), s));
@@ -556,7 +571,12 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
       return EMQX_EINVAL;
     }
     if (flags & SUM_F_RETRY) {
-      if (sm[SUM_NEED_SLAB] > w->slab_per_tile) w->slab_per_tile = static_cast<uint32_t>(round_pow2(sm[SUM_NEED_SLAB]));
+      if (sm[SUM_NEED_SLAB] > w->slab_per_tile) {
+        w->slab_per_tile = static_cast<uint32_t>(round_pow2(sm[SUM_NEED_SLAB]));
+        uint32_t h = e->slab_hint.load();  // later workspaces start at the learnt size
+        while (h < w->slab_per_tile && !e->slab_hint.compare_exchange_weak(h, w->slab_per_tile)) {
+        }
+      }
       if (err & CTRL_ERR_DEEP_SLAB) {
         w->deep_slab_cap = static_cast<uint32_t>(std::min<uint64_t>(round_pow2(sm[SUM_DEEP_FILL] + 1), 1u << 30));
         HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
@@ -711,7 +731,7 @@ int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topi
   if (!d_out_offsets) return EMQX_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   auto snap = current(e);
-  Workspace* w = acquire_ws(e);
+  Workspace* w = acquire_ws(e, static_cast<hipStream_t>(stream));
   int rc = ensure_ws(w, n);
   if (rc == EMQX_OK) {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
@@ -729,7 +749,7 @@ int emqx_match_batch_device_async(emqx_engine* e, uint32_t mode, const uint8_t* 
   if (!d_out_offsets) return EMQX_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   auto snap = current(e);
-  Workspace* w = acquire_ws(e);
+  Workspace* w = acquire_ws(e, static_cast<hipStream_t>(stream));
   int rc = ensure_ws(w, n);
   if (rc == EMQX_OK) {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
