@@ -29,6 +29,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+D_BATCH = 1_000_000  # config D: ~5000 node visits and ~1100 matches per topic
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -49,7 +50,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n-filters", type=int, default=10_000_000)
-    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="topics per batch (default 1M; --workload D: D_BATCH)")
     ap.add_argument("--mode", type=int, default=0, help="0 routes, 1 trie, 2 trie_wildcard")
     ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics in the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -86,6 +88,8 @@ def main():
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per kernel launch from PMC (rocprofv3 FETCH_SIZE/WRITE_SIZE)")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = D_BATCH if args.workload == "D" else 1_000_000
 
     import torch
     import torch.distributed as dist
@@ -114,8 +118,6 @@ def main():
     if args.workload == "A":
         wl = load_or_make(args, rank, lambda: W.config_a(n_topics=args.batch, seed=1 if rank == 0 else 1000 + rank))
     elif args.workload == "D":
-        if args.batch == 1_000_000:
-            args.batch = 100_000  # ~1000 node visits per topic: a 100k batch is ~0.1 G visits
         wl = load_or_make(args, rank, lambda: W.config_d(n_topics=args.batch, seed=4))
     else:
         wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
@@ -145,9 +147,6 @@ def main():
         return eng.match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
                                 mode=args.mode, stream=stream)
 
-    if args.ab:
-        return ab_variants(eng, step, args, wl)
-
     nout = 0
     for _ in range(max(args.warmup, 1)):  # synchronous calls: size the scratch areas once
         try:
@@ -158,6 +157,8 @@ def main():
             cap = int(err.needed * 1.25) + 1024
             d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
             nout = step()
+    if args.ab:
+        return ab_variants(eng, step, args, wl)
     # Timed steps are enqueued with emqx_match_batch_device_async, as a pipelined caller
     # would: every step runs the whole pipeline (fast + deep kernels, scan, scatter) and
     # writes its own summary; nothing is skipped, only the host no longer blocks per batch.

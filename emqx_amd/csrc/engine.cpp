@@ -105,8 +105,6 @@ struct DeltaState {
   uint64_t delta_filters = 0;
 };
 
-constexpr uint32_t DEEP_WAVES = 32;
-
 struct Workspace {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -132,7 +130,7 @@ struct Workspace {
   std::shared_ptr<Snapshot> inflight;  // table of the last async call (kept alive for it)
   uint32_t* deep_wids = nullptr;
   uint4* deep_stack = nullptr;
-  uint32_t deep_stack_cap = 1u << 16;
+  uint32_t deep_stack_cap = 1u << 14;
   uint64_t* deep_slab = nullptr;
   uint32_t deep_slab_cap = 1u << 20;
   // host-API staging
@@ -495,7 +493,7 @@ FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
   const int fv = e->forced_variant.load();
   const int forced = fv >= 0 ? fv : env_forced;
   if (forced >= 0 && forced < FAST_NVARIANTS) return static_cast<FastVariant>(forced);
-  return snap.max_depth > 12 ? FAST_K2_S2K : FAST_K1_S384;
+  return snap.max_depth > 12 ? FAST_K1_S512W : FAST_K1_S384;
 }
 
 // Enqueue one match call on stream s (no host synchronisation): memset of the control
@@ -578,7 +576,7 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
         }
       }
       if (err & CTRL_ERR_DEEP_SLAB) {
-        w->deep_slab_cap = static_cast<uint32_t>(std::min<uint64_t>(round_pow2(sm[SUM_DEEP_FILL] + 1), 1u << 30));
+        w->deep_slab_cap = static_cast<uint32_t>(std::min<uint64_t>(round_pow2(sm[SUM_DEEP_FILL] + uint64_t(DEEP_WAVES) * DEEP_CHUNK + 1), 1u << 30));
         HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
       }
       if (err & CTRL_ERR_TOO_DEEP) {

@@ -99,6 +99,12 @@ struct MatchArgs {
   uint64_t* summary;       // [SUM_WORDS] (device or host-pinned memory)
 };
 
+// Deep path: waves of match_deep_kernel, slab entries each wave reserves per atomic, and the
+// padding value of a reserved entry left unused.
+constexpr uint32_t DEEP_WAVES = 512;
+constexpr uint32_t DEEP_CHUNK = 256;
+constexpr uint64_t DEEP_PAD = ~0ull;
+
 // Fast-kernel variants: K items per lane per step, LDS stack / word-id capacity per wave.
 enum FastVariant {
   FAST_K1_S1K = 0,   // 4 waves/block, stack 1024, K=1
@@ -110,7 +116,9 @@ enum FastVariant {
   FAST_K2_S512 = 6,  // 4 waves/block, stack 512 (+HBM spill), 640 word ids
   FAST_K1_S384 = 7,  // 4 waves/block, stack 384 (+HBM spill), 640 word ids
   FAST_K2_S512W = 8, // 4 waves/block, stack 512 (+HBM spill), 512 word ids: 24 waves/CU
-  FAST_NVARIANTS = 9
+  FAST_K1_S768W = 9, // 4 waves/block, stack 768, 1024 word ids, K=1 (deep tables: 15 waves/CU)
+  FAST_K1_S512W = 10,// 4 waves/block, stack 512 (+HBM spill), 1024 word ids, K=1: 18 waves/CU
+  FAST_NVARIANTS = 11
 };
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);

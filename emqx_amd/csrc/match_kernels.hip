@@ -901,6 +901,14 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
   const uint32_t scap = a.deep_stack_cap;
   const uint32_t mode = a.mode;
 
+  // Slab entries are reserved in chunks of DEEP_CHUNK per wave (no same-address atomic per
+  // step); a chunk's unused tail is padded with DEEP_PAD, which the scatter skips.
+  uint32_t ccur = 0, cend = 0;  // wave-uniform
+  auto pad_chunk = [&]() {
+    for (uint32_t p = ccur + lane; p < cend; p += 64)
+      if (p < a.deep_slab_cap) a.deep_slab[p] = DEEP_PAD;
+    ccur = cend;
+  };
   for (uint32_t j = gw; j < ndef; j += a.deep_waves) {
     const uint32_t t = a.deferred[j];
     if (lane == 0) a.deep_rank[j] = 0;
@@ -958,10 +966,16 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       uint32_t tot;
       const uint32_t rel = wave_prefix<3>(c, lane, &tot);
       if (tot == 0) return;
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&a.ctrl[CTRL_DEEP_FILL], tot);
-      base = __shfl(base, 0, 64);
-      uint32_t pos = base + rel;
+      if (ccur + tot > cend) {  // reserve the next chunk (one atomic per DEEP_CHUNK entries)
+        pad_chunk();
+        const uint32_t want = max(tot, DEEP_CHUNK);
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&a.ctrl[CTRL_DEEP_FILL], want);
+        ccur = __shfl(base, 0, 64);
+        cend = ccur + want;
+      }
+      uint32_t pos = ccur + rel;
+      ccur += tot;
       const uint64_t tag = static_cast<uint64_t>(j) << 32;
       bool over = false;
       if (e0) { if (pos < a.deep_slab_cap) a.deep_slab[pos] = tag | g0; else over = true; ++pos; }
@@ -1047,6 +1061,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       atomicAdd(a.ctrl + CTRL_DEEP_EVALS, ev);
     }
   }
+  pad_chunk();
 }
 
 // ------------------------------------------------------------------------------------
@@ -1265,6 +1280,7 @@ __global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < fill;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint64_t e = a.deep_slab[i];
+    if (e == DEEP_PAD) continue;
     const uint32_t j = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
     const uint32_t t = a.deferred[j];
     const uint64_t p = a.out_off[t] + atomicAdd(&a.deep_rank[j], 1u);
@@ -1309,6 +1325,8 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K2_S512: launch_fast_t<4, 512, 640, 2>(a, ntiles, s); break;
     case FAST_K1_S384: launch_fast_t<4, 384, 640, 1>(a, ntiles, s); break;
     case FAST_K2_S512W: launch_fast_t<4, 512, 512, 2>(a, ntiles, s); break;
+    case FAST_K1_S768W: launch_fast_t<4, 768, 1024, 1>(a, ntiles, s); break;
+    case FAST_K1_S512W: launch_fast_t<4, 512, 1024, 1>(a, ntiles, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
