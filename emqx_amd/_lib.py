@@ -35,7 +35,7 @@ EXPORTS = (
     "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_batcher_create",
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
-    "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_publish_batch",
+    "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
 )
 # Every symbol include/emqx_retain.h declares (retained-message index).
 RETAIN_EXPORTS = (
@@ -132,6 +132,7 @@ def lib():
         "emqx_subtab_commit": (i32, [vp]),
         "emqx_subtab_stats": (i32, [vp, vp]),
         "emqx_fanout_batch_device": (i32, [vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
+        "emqx_fanout_batch_device_async": (i32, [vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, u64, vp, vp]),
         "emqx_publish_batch": (i32, [vp, vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]),
         "emqx_retain_create": (i32, [ctypes.c_int32, ctypes.POINTER(vp)]),
         "emqx_retain_destroy": (i32, [vp]),

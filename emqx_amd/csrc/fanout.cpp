@@ -192,6 +192,29 @@ struct DevTables {
 
 }  // namespace
 
+// Per-stream scratch of the fan-out pipeline: calls on one stream run in order on the device,
+// so they can share it; calls pipelined on different streams never do.
+struct FoScratch {
+  hipStream_t stream = nullptr;
+  uint32_t* entry_topic = nullptr;
+  uint64_t cap_entry_topic = 0;
+  uint32_t* ecount = nullptr;
+  uint64_t cap_ecount = 0;
+  uint64_t* eoff = nullptr;
+  uint64_t cap_eoff = 0;
+  uint64_t* partials = nullptr;
+  uint64_t cap_partials = 0;
+  uint64_t* h_sum = nullptr;  // host-mapped call summary (synchronous calls)
+  void release() {
+    fo_free(entry_topic);
+    fo_free(ecount);
+    fo_free(eoff);
+    fo_free(partials);
+    if (h_sum) (void)hipHostFree(h_sum);
+    h_sum = nullptr;
+  }
+};
+
 struct emqx_subtab {
   int device = 0;
   std::mutex mu;  // serialises mutations, commits and fan-out calls
@@ -210,14 +233,7 @@ struct emqx_subtab {
   uint64_t state_n = 0;                        // slots with device state
   uint64_t n_live_groups = 0;
   hipStream_t stream = nullptr;
-  uint32_t* entry_topic = nullptr;
-  uint64_t cap_entry_topic = 0;
-  uint32_t* ecount = nullptr;
-  uint64_t cap_ecount = 0;
-  uint64_t* eoff = nullptr;
-  uint64_t cap_eoff = 0;
-  uint64_t* partials = nullptr;
-  uint64_t cap_partials = 0;
+  std::vector<std::unique_ptr<FoScratch>> scratch;  // one per stream that called
   uint64_t* h_total = nullptr;
   uint32_t seed = 0x2545F491u;
   // emqx_publish_batch staging
@@ -242,10 +258,7 @@ struct emqx_subtab {
     (void)hipSetDevice(device);
     dev.release();
     fo_free(state);
-    fo_free(entry_topic);
-    fo_free(ecount);
-    fo_free(eoff);
-    fo_free(partials);
+    for (auto& c : scratch) c->release();
     fo_free(d_tbytes);
     fo_free(d_toffs);
     fo_free(d_moff);
@@ -347,13 +360,25 @@ int commit_locked(emqx_subtab* s) {
 }
 
 // The fan-out pipeline on device buffers (s->mu held).
-int run_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const uint32_t* d_mids, uint64_t n,
-               uint64_t m, const uint32_t* d_keys, uint64_t* d_out_off, uint32_t* d_out_subs, uint32_t* d_out_fil,
-               uint64_t cap, uint64_t* n_out, hipStream_t st) {
-  FO_TRY(fo_ensure(s->entry_topic, s->cap_entry_topic, m));
-  FO_TRY(fo_ensure(s->ecount, s->cap_ecount, m));
-  FO_TRY(fo_ensure(s->eoff, s->cap_eoff, m + 1));
-  FO_TRY(fo_ensure(s->partials, s->cap_partials, scan_partials(m)));
+FoScratch* scratch_for(emqx_subtab* s, hipStream_t st) {
+  for (auto& c : s->scratch)
+    if (c->stream == st) return c.get();
+  s->scratch.push_back(std::make_unique<FoScratch>());
+  s->scratch.back()->stream = st;
+  return s->scratch.back().get();
+}
+
+// Enqueue the fan-out of one match CSR on st, no host synchronisation; m_cap bounds the
+// match entries (sizes the scratch); the summary goes to `summary` (FO_SUM_WORDS u64).
+int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const uint32_t* d_mids, uint64_t n,
+                   uint64_t m_cap, const uint32_t* d_keys, uint64_t* d_out_off, uint32_t* d_out_subs,
+                   uint32_t* d_out_fil, uint64_t cap, uint64_t* summary, hipStream_t st) {
+  FoScratch* c = scratch_for(s, st);
+  const bool hash = strategy == EMQX_SHARE_HASH_CLIENTID || strategy == EMQX_SHARE_HASH_TOPIC;
+  if (hash) FO_TRY(fo_ensure(c->entry_topic, c->cap_entry_topic, m_cap));
+  FO_TRY(fo_ensure(c->ecount, c->cap_ecount, m_cap));
+  FO_TRY(fo_ensure(c->eoff, c->cap_eoff, m_cap + 1));
+  FO_TRY(fo_ensure(c->partials, c->cap_partials, 2 * FO_BLOCKS));
   FanoutArgs a{};
   a.recs = s->dev.recs;
   a.n_recs = s->dev.n_recs;
@@ -364,27 +389,38 @@ int run_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const 
   a.moff = d_moff;
   a.mids = d_mids;
   a.n = n;
-  a.m = m;
   a.keys = d_keys;
   a.strategy = strategy;
   s->seed = s->seed * 1664525u + 1013904223u;
   a.seed = s->seed;
-  a.entry_topic = s->entry_topic;
-  a.ecount = s->ecount;
-  a.eoff = s->eoff;
+  a.entry_topic = c->entry_topic;
+  a.ecount = c->ecount;
+  a.eoff = c->eoff;
+  a.partials = c->partials;
   a.out_off = d_out_off;
   a.out_subs = d_out_subs;
   a.out_filters = d_out_fil;
-  FO_TRY(launch_fanout_count(a, st));
-  FO_TRY(launch_scan(s->ecount, m, s->eoff, s->partials, st));
-  FO_TRY(launch_fanout_offsets(a, st));
-  FO_TRY(hipMemcpyAsync(s->h_total, s->eoff + m, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  a.cap = d_out_subs ? cap : 0;
+  a.summary = summary;
+  FO_TRY(launch_fanout(a, m_cap, st));
+  return EMQX_OK;
+}
+
+// Synchronous form: enqueue, drain, read the summary.  On overflow the write kernel wrote
+// nothing (and consumed no pick state); *n_out is the capacity required.
+int run_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const uint32_t* d_mids, uint64_t n,
+               uint64_t m, const uint32_t* d_keys, uint64_t* d_out_off, uint32_t* d_out_subs, uint32_t* d_out_fil,
+               uint64_t cap, uint64_t* n_out, hipStream_t st) {
+  FoScratch* c = scratch_for(s, st);
+  if (!c->h_sum)
+    FO_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_sum), FO_SUM_WORDS * sizeof(uint64_t), hipHostMallocDefault));
+  uint64_t* d_sum = nullptr;
+  FO_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_sum), c->h_sum, 0));
+  int rc = enqueue_fanout(s, strategy, d_moff, d_mids, n, m, d_keys, d_out_off, d_out_subs, d_out_fil, cap, d_sum, st);
+  if (rc != EMQX_OK) return rc;
   FO_TRY(hipStreamSynchronize(st));
-  *n_out = *s->h_total;
-  if (*n_out > cap) return EMQX_EOVERFLOW;
-  if (*n_out && !d_out_subs) return EMQX_EINVAL;
-  FO_TRY(launch_fanout_write(a, st));
-  FO_TRY(hipStreamSynchronize(st));
+  *n_out = c->h_sum[FO_SUM_TOTAL];
+  if (c->h_sum[FO_SUM_FLAGS] & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
   return EMQX_OK;
 }
 
@@ -529,8 +565,22 @@ int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* 
   bounds[1] = s->h_total[1];
   if (bounds[1] < bounds[0]) return EMQX_EINVAL;
   if (bounds[1] - bounds[0] && !d_match_ids) return EMQX_EINVAL;
-  return run_fanout(s, strategy, d_match_offsets, d_match_ids ? d_match_ids + bounds[0] : nullptr, n,
-                    bounds[1] - bounds[0], d_pick_keys, d_out_offsets, d_out_subs, d_out_filters, cap, n_out, st);
+  return run_fanout(s, strategy, d_match_offsets, d_match_ids, n, bounds[1] - bounds[0], d_pick_keys,
+                    d_out_offsets, d_out_subs, d_out_filters, cap, n_out, st);
+}
+
+int emqx_fanout_batch_device_async(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
+                                   const uint32_t* d_match_ids, uint64_t n, uint64_t match_cap,
+                                   const uint32_t* d_pick_keys, uint64_t* d_out_offsets, uint32_t* d_out_subs,
+                                   uint32_t* d_out_filters, uint64_t cap, uint64_t* summary, void* stream) {
+  if (!s || !summary || !d_match_offsets || !d_match_ids || !d_out_offsets || !d_out_subs ||
+      !strategy_ok(strategy, d_pick_keys != nullptr))
+    return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(s->mu);
+  FO_TRY(hipSetDevice(s->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
+  return enqueue_fanout(s, strategy, d_match_offsets, d_match_ids, n, match_cap, d_pick_keys, d_out_offsets,
+                        d_out_subs, d_out_filters, cap, summary, st);
 }
 
 int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const uint8_t* topic_bytes,

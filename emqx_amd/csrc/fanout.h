@@ -50,20 +50,27 @@ struct FanoutArgs {
   const uint64_t* moff;      // match CSR offsets [n+1]
   const uint32_t* mids;      // match CSR filter ids [moff[n]]
   uint64_t n;                // topics
-  uint64_t m;                // match entries (moff[n] - moff[0])
   const uint32_t* keys;      // per topic pick key (erlang:phash2 of ClientId / topic), or null
   uint32_t strategy;         // EMQX_SHARE_*
   uint32_t seed;             // per-call seed of the 'random' strategy
-  uint32_t* entry_topic;     // [m] scratch
+  uint32_t* entry_topic;     // [m] scratch (hash strategies)
   uint32_t* ecount;          // [m] scratch
   uint64_t* eoff;            // [m+1] scratch: per-entry output offsets
+  uint64_t* partials;        // [2 * FO_BLOCKS] scratch: chunk sums, chunk bases
   uint64_t* out_off;         // [n+1]
   uint32_t* out_subs;        // [cap]
   uint32_t* out_filters;     // [cap] or null
+  uint64_t cap;              // capacity of out_subs / out_filters
+  uint64_t* summary;         // [FO_SUM_WORDS] device or host-mapped
 };
 
-hipError_t launch_fanout_count(const FanoutArgs& a, hipStream_t s);
-hipError_t launch_fanout_offsets(const FanoutArgs& a, hipStream_t s);
-hipError_t launch_fanout_write(const FanoutArgs& a, hipStream_t s);
+// Chunks of the fixed-grid count/scan kernels (the entry count is only known on the device).
+constexpr uint32_t FO_BLOCKS = 1024;
+// Call summary words.
+constexpr uint32_t FO_SUM_FLAGS = 0, FO_SUM_TOTAL = 1, FO_SUM_ENTRIES = 2, FO_SUM_WORDS = 4;
+constexpr uint64_t FO_SUM_F_OVERFLOW = 1;
+
+// The whole fan-out of one batch, enqueued on s; m_cap bounds the match entries.
+hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s);
 
 }  // namespace emqx

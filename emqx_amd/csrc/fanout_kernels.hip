@@ -4,15 +4,21 @@
 // 500-524) and emqx_shared_sub:dispatch/3 -> pick/6 -> do_pick_subscriber/6
 // (apps/emqx/src/emqx_shared_sub.erl:113-126,251-288) for a whole batch of published topics.
 //
-// Pipeline, all on one stream, inputs = the match CSR left in HBM:
-//   entry_topic  one thread per topic: entry -> topic map (segmented fill)
-//   count        one thread per match entry: n_plain + n_groups of its filter
-//   scan         (match_kernels.hip) per-entry counts -> per-entry output offsets
+// Pipeline, all on one stream with no host synchronisation: the number of
+// match entries m = moff[n] - moff[0] is read on the device, so every kernel below runs a
+// fixed grid over a length it loads itself.
+//   entry_topic  one thread per topic: entry -> topic map (hash strategies only)
+//   count        FO_BLOCKS blocks, one contiguous chunk of entries each: per-entry count
+//                n_plain + n_groups of its filter, and the chunk's sum
+//   partials     one block: exclusive scan of the chunk sums, the total, the overflow flag
+//                and the call summary
+//   final        FO_BLOCKS blocks: per-entry output offsets (chunk scan + the chunk's base)
 //   offsets      per-topic output offsets = per-entry offsets at the match CSR boundaries
 //   write        one wavefront per 64 match entries: the wave walks its flattened outputs 64
 //                at a time (each lane finds its entry by a 6-step search over LDS prefix
 //                offsets), so plain-subscriber copies are coalesced reads and writes; each
-//                $share group contributes exactly one pick.
+//                $share group contributes exactly one pick.  Skipped entirely on overflow, so
+//                no pick state is consumed by a call that wrote nothing.
 // Bandwidth-bound streaming; no MFMA.
 #include <hip/hip_runtime.h>
 
@@ -39,16 +45,122 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_entry_topic_kernel(FanoutAr
   }
 }
 
+__device__ __forceinline__ uint64_t fo_entries(const FanoutArgs& a) { return a.moff[a.n] - a.moff[0]; }
+
+// Chunk [lo, hi) of block b out of FO_BLOCKS over m entries (multiples of 64).
+__device__ __forceinline__ void fo_chunk(uint64_t m, uint32_t b, uint64_t* lo, uint64_t* hi) {
+  const uint64_t per = ((m + FO_BLOCKS - 1) / FO_BLOCKS + 63) & ~63ull;
+  *lo = min<uint64_t>(m, per * b);
+  *hi = min<uint64_t>(m, per * (b + 1));
+}
+
+__device__ __forceinline__ uint64_t fo_wave_sum(uint64_t v) {
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Block-wide exclusive scan of one u64 per thread (FO_THREADS threads).
+__device__ __forceinline__ uint64_t fo_block_excl_scan(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t wsum[FO_THREADS / 64];
+  const uint32_t lane = fo_lane(), w = threadIdx.x >> 6;
+  uint64_t incl = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < FO_THREADS / 64; ++k) {
+    before += k < w ? wsum[k] : 0;
+    all += wsum[k];
+  }
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
+
 __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) {
-  for (uint64_t i = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; i < a.m;
-       i += uint64_t(gridDim.x) * FO_THREADS) {
-    const uint32_t f = a.mids[i];
+  __shared__ uint64_t bsum[FO_THREADS / 64];
+  const uint64_t base = a.moff[0];
+  uint64_t lo, hi;
+  fo_chunk(fo_entries(a), blockIdx.x, &lo, &hi);
+  uint64_t sum = 0;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += FO_THREADS) {
+    const uint32_t f = a.mids[base + i];
     uint32_t c = 0;
     if (f < a.n_recs) {
       const uint4 r = *reinterpret_cast<const uint4*>(a.recs + f);
       c = r.y + r.w;
     }
     a.ecount[i] = c;
+    sum += c;
+  }
+  sum = fo_wave_sum(sum);
+  if (fo_lane() == 0) bsum[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (uint32_t k = 0; k < FO_THREADS / 64; ++k) t += bsum[k];
+    a.partials[blockIdx.x] = t;
+  }
+}
+
+// One block of FO_BLOCKS threads: chunk bases, eoff[m] = total, the call summary.
+__global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a) {
+  __shared__ uint64_t wsum[FO_BLOCKS / 64];
+  const uint32_t lane = fo_lane(), w = threadIdx.x >> 6;
+  const uint64_t v = a.partials[threadIdx.x];
+  uint64_t incl = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  for (uint32_t k = 0; k < FO_BLOCKS / 64; ++k) {
+    before += k < w ? wsum[k] : 0;
+    all += wsum[k];
+  }
+  a.partials[FO_BLOCKS + threadIdx.x] = before + incl - v;
+  if (threadIdx.x == 0) {
+    const uint64_t m = fo_entries(a);
+    a.eoff[m] = all;
+    uint64_t* sm = a.summary;
+    sm[FO_SUM_FLAGS] = all > a.cap ? FO_SUM_F_OVERFLOW : 0u;
+    sm[FO_SUM_TOTAL] = all;
+    sm[FO_SUM_ENTRIES] = m;
+    __threadfence_system();
+  }
+}
+
+// Per-entry output offsets: each block rescans its chunk, FO_THREADS * 4 entries per round.
+__global__ __launch_bounds__(FO_THREADS) void fanout_final_kernel(FanoutArgs a) {
+  uint64_t lo, hi;
+  fo_chunk(fo_entries(a), blockIdx.x, &lo, &hi);
+  uint64_t carry = a.partials[FO_BLOCKS + blockIdx.x];
+  for (uint64_t r0 = lo; r0 < hi; r0 += FO_THREADS * 4) {
+    const uint64_t i0 = r0 + 4ull * threadIdx.x;
+    uint32_t c[4];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      c[k] = i0 + k < hi ? a.ecount[i0 + k] : 0u;
+      sum += c[k];
+    }
+    uint64_t tot;
+    uint64_t p = carry + fo_block_excl_scan(sum, &tot);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (i0 + k < hi) a.eoff[i0 + k] = p;
+      p += c[k];
+    }
+    carry += tot;
   }
 }
 
@@ -104,14 +216,18 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
   const uint32_t lane = fo_lane();
   const uint32_t wv = threadIdx.x >> 6;
   WaveLds& L = lds_all[wv];
+  const uint64_t base = a.moff[0];
+  const uint64_t m = fo_entries(a);
+  if (a.eoff[m] > a.cap) return;  // overflow: nothing is written, no pick state consumed
+  const bool need_topic = a.strategy == EMQX_SHARE_HASH_CLIENTID || a.strategy == EMQX_SHARE_HASH_TOPIC;
   const uint64_t nwaves = uint64_t(gridDim.x) * (FO_THREADS / 64);
-  for (uint64_t e0 = (uint64_t(blockIdx.x) * (FO_THREADS / 64) + wv) * 64; e0 < a.m; e0 += nwaves * 64) {
-    const uint64_t e1 = min<uint64_t>(e0 + 64, a.m);
+  for (uint64_t e0 = (uint64_t(blockIdx.x) * (FO_THREADS / 64) + wv) * 64; e0 < m; e0 += nwaves * 64) {
+    const uint64_t e1 = min<uint64_t>(e0 + 64, m);
     const uint64_t obase = a.eoff[e0];
     const uint32_t total = static_cast<uint32_t>(a.eoff[e1] - obase);
     const uint64_t i = e0 + lane;
     if (i < e1) {
-      const uint32_t f = a.mids[i];
+      const uint32_t f = a.mids[base + i];
       uint4 r = make_uint4(0, 0, 0, 0);
       if (f < a.n_recs) r = *reinterpret_cast<const uint4*>(a.recs + f);
       L.pre[lane] = static_cast<uint32_t>(a.eoff[i] - obase);
@@ -119,7 +235,7 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
       L.pb[lane] = r.x;
       L.np[lane] = r.y;
       L.gb[lane] = r.z;
-      L.top[lane] = a.entry_topic[i];
+      L.top[lane] = need_topic ? a.entry_topic[i] : 0u;
     } else {
       L.pre[lane] = total;  // never <= a valid output index
     }
@@ -163,19 +279,16 @@ uint32_t grid_for(uint64_t items, uint32_t per_block) {
 
 }  // namespace
 
-hipError_t launch_fanout_count(const FanoutArgs& a, hipStream_t s) {
-  if (a.n) hipLaunchKernelGGL(fanout_entry_topic_kernel, dim3(grid_for(a.n, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
-  if (a.m) hipLaunchKernelGGL(fanout_count_kernel, dim3(grid_for(a.m, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_fanout_offsets(const FanoutArgs& a, hipStream_t s) {
+hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s) {
+  const bool hash = a.strategy == EMQX_SHARE_HASH_CLIENTID || a.strategy == EMQX_SHARE_HASH_TOPIC;
+  if (a.n && hash)
+    hipLaunchKernelGGL(fanout_entry_topic_kernel, dim3(grid_for(a.n, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
+  hipLaunchKernelGGL(fanout_count_kernel, dim3(FO_BLOCKS), dim3(FO_THREADS), 0, s, a);
+  hipLaunchKernelGGL(fanout_partials_kernel, dim3(1), dim3(FO_BLOCKS), 0, s, a);
+  hipLaunchKernelGGL(fanout_final_kernel, dim3(FO_BLOCKS), dim3(FO_THREADS), 0, s, a);
   hipLaunchKernelGGL(fanout_offsets_kernel, dim3(grid_for(a.n + 1, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_fanout_write(const FanoutArgs& a, hipStream_t s) {
-  if (a.m) hipLaunchKernelGGL(fanout_write_kernel, dim3(grid_for(a.m, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
+  // one wave per 64 entries up to m_cap (waves past m exit at once)
+  hipLaunchKernelGGL(fanout_write_kernel, dim3(grid_for(m_cap, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
   return hipGetLastError();
 }
 

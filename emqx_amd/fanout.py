@@ -107,6 +107,19 @@ class SubTable:
         check(rc, "emqx_fanout_batch_device")
         return int(n_out.value)
 
+    SUMMARY_WORDS = 4  # {flags (bit 0: overflow), deliveries, match entries, 0}
+
+    def fanout_device_async(self, strategy, d_moff: int, d_mids: int, n: int, match_cap: int,
+                            d_keys: Optional[int], d_out_off: int, d_out_subs: int, d_out_filters: Optional[int],
+                            cap: int, d_summary: int, stream: Optional[int] = None) -> None:
+        """Enqueue the fan-out on ``stream`` without host synchronisation
+        (emqx_fanout_batch_device_async); the result counts land in ``d_summary``."""
+        check(_lib.lib().emqx_fanout_batch_device_async(
+            self._h, _strategy(strategy), ctypes.c_void_p(d_moff), ctypes.c_void_p(d_mids), n, match_cap,
+            ctypes.c_void_p(d_keys) if d_keys else None, ctypes.c_void_p(d_out_off), ctypes.c_void_p(d_out_subs),
+            ctypes.c_void_p(d_out_filters) if d_out_filters else None, cap, ctypes.c_void_p(d_summary),
+            ctypes.c_void_p(stream) if stream else None), "emqx_fanout_batch_device_async")
+
 
 def publish_packed(engine, subtab: SubTable, strategy, buf: np.ndarray, offs: np.ndarray,
                    keys: Optional[np.ndarray] = None, cap_hint: int = 1 << 16):

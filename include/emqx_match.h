@@ -205,6 +205,16 @@ int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* 
                              const uint32_t* d_match_ids, uint64_t n, const uint32_t* d_pick_keys,
                              uint64_t* d_out_offsets, uint32_t* d_out_subs, uint32_t* d_out_filters,
                              uint64_t cap, uint64_t* n_out, void* stream);
+/* Asynchronous form of emqx_fanout_batch_device for pipelined callers: the whole fan-out is
+ * enqueued on `stream` with no host synchronisation (the entry count is read on the device).
+ * match_cap bounds the match entries (the match call's id capacity; sizes the scratch).
+ * summary[4] (device or host-mapped memory) receives {flags (bit 0: overflow), deliveries,
+ * match entries, 0} when the call completes; on overflow nothing is written to the id arrays
+ * and no $share pick state is consumed. */
+int emqx_fanout_batch_device_async(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
+                                   const uint32_t* d_match_ids, uint64_t n, uint64_t match_cap,
+                                   const uint32_t* d_pick_keys, uint64_t* d_out_offsets, uint32_t* d_out_subs,
+                                   uint32_t* d_out_filters, uint64_t cap, uint64_t* summary, void* stream);
 /* emqx_broker:publish/1's lookup + fan-out for a batch of topics (host buffers): match
  * (mode EMQX_MODE_ROUTES) and fan-out run back to back on the device; the match CSR never
  * leaves HBM.  pick_keys[n] (host) as above. */

@@ -205,3 +205,75 @@ def test_empty_batches_and_tables(F):
     assert list(off) == [0, 0, 0]
     with pytest.raises(Exception):  # hash strategies need keys
         F.publish_packed(eng, st, "hash_topic", *pack([b"a/b"]))
+
+
+def test_async_fanout_pipelined_streams(F):
+    """emqx_fanout_batch_device_async: match + fan-out enqueued on three streams without host
+    synchronisation equals the synchronous call; an undersized output sets the overflow flag
+    and writes nothing; a CSR slice whose offsets do not start at 0 (moff[0] > 0) is read
+    from its own base."""
+    import torch
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    fw = W.config_e(n_filters=100_000, n_subscribers=50_000, n_topics=20_000, seed=6)
+    eng = Engine(0)
+    eng.insert_packed(*fw.wl.filters)
+    eng.commit()
+    st = F.SubTable(0)
+    st.add(fw.sub_filter, fw.sub_id, fw.sub_group)
+    st.commit()
+    dev = torch.device("cuda", 0)
+    tb = torch.from_numpy(fw.wl.topics[0]).to(dev)
+    to = torch.from_numpy(fw.wl.topics[1].view(np.int64)).to(dev)
+    keys = torch.from_numpy(fw.keys.view(np.int32)).to(dev)
+    n = fw.wl.n_topics
+    mcap = 64 * n
+    moff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    mids = torch.empty(mcap, dtype=torch.int32, device=dev)
+    nm = eng.match_device(tb.data_ptr(), to.data_ptr(), n, moff.data_ptr(), mids.data_ptr(), mcap)
+    ooff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    cap = 64 * n
+    osubs = torch.empty(cap, dtype=torch.int32, device=dev)
+    ofil = torch.empty(cap, dtype=torch.int32, device=dev)
+    tot = st.fanout_device("hash_clientid", moff.data_ptr(), mids.data_ptr(), n, keys.data_ptr(), ooff.data_ptr(),
+                           osubs.data_ptr(), ofil.data_ptr(), cap)
+    ref = (ooff.cpu().numpy(), osubs[:tot].cpu().numpy(), ofil[:tot].cpu().numpy())
+
+    streams = [torch.cuda.Stream(device=dev) for _ in range(3)]
+    outs = [[torch.empty_like(t) for t in (moff, mids, ooff, osubs, ofil)] for _ in streams]
+    summ = torch.zeros((6, st.SUMMARY_WORDS), dtype=torch.int64, device=dev)
+    msum = torch.zeros((6, eng.SUMMARY_WORDS), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    for k in range(6):
+        j = k % 3
+        mo, mi, oo, os_, of = outs[j]
+        s = streams[j].cuda_stream
+        eng.match_device_async(tb.data_ptr(), to.data_ptr(), n, mo.data_ptr(), mi.data_ptr(), mcap,
+                               msum[k].data_ptr(), stream=s)
+        st.fanout_device_async("hash_clientid", mo.data_ptr(), mi.data_ptr(), n, mcap, keys.data_ptr(),
+                               oo.data_ptr(), os_.data_ptr(), of.data_ptr(), cap, summ[k].data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    sm = summ.cpu().numpy()
+    assert (sm[:, 0] == 0).all() and (sm[:, 1] == tot).all() and (sm[:, 2] == nm).all()
+    for mo, mi, oo, os_, of in outs:
+        assert np.array_equal(oo.cpu().numpy(), ref[0])
+        assert np.array_equal(os_[:tot].cpu().numpy(), ref[1])
+        assert np.array_equal(of[:tot].cpu().numpy(), ref[2])
+
+    # overflow: flag set, output untouched
+    osubs.fill_(-7)
+    st.fanout_device_async("hash_clientid", moff.data_ptr(), mids.data_ptr(), n, mcap, keys.data_ptr(),
+                           ooff.data_ptr(), osubs.data_ptr(), ofil.data_ptr(), tot - 1, summ[0].data_ptr())
+    torch.cuda.synchronize()
+    s0 = summ[0].cpu().numpy()
+    assert s0[0] & 1 and s0[1] == tot
+    assert (osubs.cpu().numpy() == -7).all()
+
+    # a slice of the CSR (topics [h, n)): offsets start at moff[h] > 0
+    h = n // 2
+    oo_ref = ref[0]
+    sl = st.fanout_device("hash_clientid", moff[h:].data_ptr(), mids.data_ptr(), n - h, keys[h:].data_ptr(),
+                          ooff.data_ptr(), osubs.data_ptr(), ofil.data_ptr(), cap)
+    assert sl == int(oo_ref[n] - oo_ref[h])
+    assert np.array_equal(osubs[:sl].cpu().numpy(), ref[1][oo_ref[h]:])
+    assert np.array_equal(ooff[:n - h + 1].cpu().numpy(), oo_ref[h:] - oo_ref[h])
