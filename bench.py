@@ -37,10 +37,34 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class progress:
+    """Logs `label: N s` every `every` seconds while a long host phase runs (workload
+    generation, table build at 100M filters), so a live run is never silent for minutes."""
+
+    def __init__(self, label, every=30.0):
+        import threading
+        self.label, self.every, self.done = label, every, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.time()
+        while not self.done.wait(self.every):
+            log(f"{self.label}: {time.time() - t0:.0f} s")
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.done.set()
+        self.t.join()
+
+
 WORKLOAD_NAMES = {
     "A": "A: 100k filters site{i%1000}/+/dev{i/1000}/#, 1M-topic stream (configs[0] table on 1xMI355X)",
     "B": "B: 10M mixed exact/'+'/'#' subscriptions, 1xMI355X, batched topics of depth 4-8",
     "D": "D: adversarial '#'/'+'-rich table, 1M filters, depth-16 topics, 1xMI355X",
+    "C1": "C on one GPU: config-C table (B generator, vocab x4, seed 3) held whole on 1xMI355X, 1M-topic batches",
 }
 
 
@@ -120,17 +144,20 @@ def main():
     elif args.workload == "D":
         wl = load_or_make(args, rank, lambda: W.config_d(n_topics=args.batch, seed=4))
     else:
-        wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
-                                                         vocab_scale=args.vocab_scale,
-                                                         topic_seed=None if rank == 0 else 1000 + rank))
+        with progress(f"[rank {rank}] generating workload"):
+            wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch,
+                                                             seed=3 if args.vocab_scale > 1 else 2,
+                                                             vocab_scale=args.vocab_scale,
+                                                             topic_seed=None if rank == 0 else 1000 + rank))
     log(f"[rank {rank}] workload: {wl.n_filters} filters, {wl.n_topics} topics ({time.time() - t0:.1f}s)")
     if args.order != "none":
         wl = reorder_topics(wl, args.order)
 
     t0 = time.time()
     eng = Engine(local)
-    eng.insert_packed(*wl.filters)
-    eng.commit()
+    with progress(f"[rank {rank}] building table"):
+        eng.insert_packed(*wl.filters)
+        eng.commit()
     st = eng.stats()
     log(f"[rank {rank}] table: {st['n_nodes']} nodes, {st['n_slots']} slots, {st['n_words']} words, "
         f"{st['table_bytes'] / 1e9:.2f} GB, build {st['last_build_ms'] / 1e3:.1f}s ({time.time() - t0:.1f}s)")
@@ -239,7 +266,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": WORKLOAD_NAMES[args.workload],
+        "config": {"workload": WORKLOAD_NAMES["C1" if args.vocab_scale > 1 else args.workload],
                    "n_filters": wl.n_filters, "batch_topics_per_gpu": n, "mode": ["routes", "trie", "trie_wildcard"][args.mode],
                    "parallelism": f"replicated table, topic stream split x{world}"},
         "evals_per_s": round(evals_all * args.steps / elapsed, 1),
@@ -280,13 +307,15 @@ def sharded_bench(args, rank, world, dev):
     from emqx_amd.dist import ShardedMatcher
     seed = 3 if args.vocab_scale > 1 else 2
     t0 = time.time()
-    wl = W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=seed, vocab_scale=args.vocab_scale)
+    with progress(f"[rank {rank}] generating workload"):
+        wl = W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=seed, vocab_scale=args.vocab_scale)
     log(f"[rank {rank}] workload {wl.n_filters} filters ({time.time() - t0:.1f}s)")
     if world == 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    sm = ShardedMatcher(wl.filters, device=dev, mode=args.mode)
+    with progress(f"[rank {rank}] building shard"):
+        sm = ShardedMatcher(wl.filters, device=dev, mode=args.mode)
     st = sm.engine.stats()
     log(f"[rank {rank}] shard: {st['n_filters']} filters, {st['table_bytes'] / 1e9:.2f} GB")
     topics = None

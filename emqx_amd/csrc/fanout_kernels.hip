@@ -31,6 +31,7 @@ namespace emqx {
 namespace {
 
 constexpr int FO_THREADS = 256;
+constexpr uint32_t FO_UNROLL = 4;  // outputs per lane per round of the write kernel
 
 __device__ __forceinline__ uint32_t fo_lane() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -241,30 +242,43 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      if (j < total) {
+    // FO_UNROLL outputs per lane per round: all plain-subscriber loads of the round are in
+    // flight before the first store ($share picks, ~10 % of entries, resolve after them).
+    for (uint32_t j0 = 0; j0 < total; j0 += 64 * FO_UNROLL) {
+      uint32_t sub[FO_UNROLL], fl[FO_UNROLL], kk[FO_UNROLL], rr[FO_UNROLL];
+      bool act[FO_UNROLL], shr[FO_UNROLL];
+#pragma unroll
+      for (uint32_t u = 0; u < FO_UNROLL; ++u) {
+        const uint32_t j = j0 + lane + 64u * u;
+        act[u] = j < total;
         // largest k with pre[k] <= j (pre is non-decreasing, pre[0] = 0, unused lanes hold
         // `total`); k + step never exceeds 63
         uint32_t k = 0;
 #pragma unroll
         for (uint32_t step = 32; step >= 1; step >>= 1)
           if (L.pre[k + step] <= j) k += step;
-        const uint32_t r = j - L.pre[k];
-        const uint32_t f = L.fid[k];
-        uint32_t sub, fl;
-        if (r < L.np[k]) {
-          sub = a.plain[L.pb[k] + r];
-          fl = f;
-        } else {
-          const uint32_t gidx = L.gb[k] + (r - L.np[k]);
-          const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
-          const GroupRec g{gr.x, gr.y, gr.z, gr.w};
-          sub = pick_member(a, g, e0 + k, L.top[k], gidx);
-          fl = f | FANOUT_SHARED_BIT;
-        }
-        a.out_subs[obase + j] = sub;
-        if (a.out_filters) a.out_filters[obase + j] = fl;
+        kk[u] = k;
+        rr[u] = j - L.pre[k];
+        fl[u] = L.fid[k];
+        shr[u] = act[u] && rr[u] >= L.np[k];
+        sub[u] = (act[u] && !shr[u]) ? a.plain[L.pb[k] + rr[u]] : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < FO_UNROLL; ++u) {
+        if (!shr[u]) continue;
+        const uint32_t k = kk[u];
+        const uint32_t gidx = L.gb[k] + (rr[u] - L.np[k]);
+        const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
+        const GroupRec g{gr.x, gr.y, gr.z, gr.w};
+        sub[u] = pick_member(a, g, e0 + k, L.top[k], gidx);
+        fl[u] |= FANOUT_SHARED_BIT;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < FO_UNROLL; ++u) {
+        if (!act[u]) continue;
+        const uint32_t j = j0 + lane + 64u * u;
+        a.out_subs[obase + j] = sub[u];
+        if (a.out_filters) a.out_filters[obase + j] = fl[u];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
