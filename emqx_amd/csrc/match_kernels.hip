@@ -606,7 +606,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   // Each lane takes IW words per round: it loads their bytes (16-B windows, mostly L1/L2
   // hits after A1), hashes the head dwords (word_hash16) and loads their first vocab slot;
   // the exact byte check uses the same head dwords.
-  constexpr uint32_t IW = K > 2 ? 2 : K;
+  constexpr uint32_t IW = 2;  // words per lane per intern round (two vocab probes in flight)
   for (uint32_t j0 = 0; j0 < nwords; j0 += 64u * IW) {
     uint32_t jj[IW], ln[IW], sh[IW], hh[IW], w[IW][4];
     uint64_t wsa[IW];
