@@ -77,7 +77,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None,
                     help="topics per batch (default 1M; --workload D: D_BATCH)")
     ap.add_argument("--mode", type=int, default=0, help="0 routes, 1 trie, 2 trie_wildcard")
-    ap.add_argument("--cpu-sample", type=int, default=200_000, help="topics in the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="topics in the CPU baseline sample (default 200k; --workload D: 40k, ~15 s)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cache", type=str, default=None,
@@ -89,7 +90,7 @@ def main():
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
     ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R"],
                     help="B = the headline (BASELINE configs[1]); A = configs[0]'s 100k-filter table, "
-                         "D = the adversarial depth-16 table (configs[3], 100k-topic batches), "
+                         "D = the adversarial depth-16 table (configs[3], 1M-topic batches), "
                          "E = publish fan-out (configs[4]): match + fan-out per step, "
                          "U = route updates (SURVEY §8 f2): subscribe/unsubscribe churn + incremental "
                          "commits on config B's table, R = retained-message lookup (SURVEY §8 f4): a batch "
@@ -114,6 +115,8 @@ def main():
     args = ap.parse_args()
     if args.batch is None:
         args.batch = D_BATCH if args.workload == "D" else 1_000_000
+    if args.cpu_sample is None:
+        args.cpu_sample = 40_000 if args.workload == "D" else 200_000
 
     import torch
     import torch.distributed as dist
@@ -358,9 +361,11 @@ def measured_traffic(n, args):
     """HBM bytes per launch of the fused match kernel from the committed rocprofv3 PMC passes
     (profiles/pmc_match_fast.json, written from tools/gpu_round.sh's counter runs on the same
     workload), scaled to this batch.  None when the file is absent or the workload differs."""
-    path = os.path.join(ROOT, "profiles", "pmc_match_fast.json")
-    if (not os.path.exists(path) or args.workload != "B" or args.n_filters != 10_000_000 or args.mode != 0
-            or args.vocab_scale != 1):
+    fname = {"B": "pmc_match_fast.json", "D": "pmc_match_fast_D.json"}.get(args.workload)
+    if fname is None or args.mode != 0 or args.vocab_scale != 1 or (args.workload == "B" and args.n_filters != 10_000_000):
+        return None, None
+    path = os.path.join(ROOT, "profiles", fname)
+    if not os.path.exists(path):
         return None, None
     with open(path) as f:
         p = json.load(f)

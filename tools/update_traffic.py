@@ -8,7 +8,7 @@ once, and FETCH_SIZE / TCC_MISS comes out at 64 B — one 64-B request per miss,
 request shape (TCC_EA0_RDREQ ~= TCC_MISS, no 32-B requests) the match kernel shows.  So for
 this kernel HBM read bytes = FETCH_SIZE as reported (not x2, the streaming-read rule).
 
-    python tools/update_traffic.py gpurun_out/<tag>
+    python tools/update_traffic.py gpurun_out/<tag> [--workload D --cal-dir gpurun_out/<B tag>]
 """
 import csv
 import glob
@@ -33,16 +33,33 @@ def calibration(d):
             "pattern": "tools/gather_bench.hip indep_kernel: random 16-B reads of a 1 GiB table"}
 
 
+WORKLOADS = {
+    "B": ("B: 10M filters, 1M-topic batch (bench.py defaults)", "pmc_match_fast.json"),
+    "D": ("D: 1M adversarial filters, 1M-topic batch (bench.py --workload D)", "pmc_match_fast_D.json"),
+}
+
+
 def main():
-    d = sys.argv[1]
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir", help="gpurun_out/<tag> holding pmc_summary.json")
+    ap.add_argument("--workload", default="B", choices=sorted(WORKLOADS))
+    ap.add_argument("--cal-dir", default=None, help="directory holding the calibration run (default: dir)")
+    ap.add_argument("--copied-to", default=None, help="where pmc_summary.json is kept under profiles/")
+    args = ap.parse_args()
+    d = args.dir
     s = json.load(open(os.path.join(d, "pmc_summary.json")))
     c = s["counters_avg_per_dispatch"]
-    cal = calibration(d)
+    cal = calibration(args.cal_dir or d)
     per_miss = cal["fetch_bytes_per_l2_miss"] if cal else None
     fetch = s["fetch_bytes_raw"]
+    name, fname = WORKLOADS[args.workload]
+    src = os.path.relpath(os.path.join(d, "pmc_summary.json"), ROOT) + " (rocprofv3 --pmc passes)"
+    if args.copied_to:
+        src += "; copied to " + args.copied_to
     out = {
         "kernel": s["kernel"],
-        "workload": "B: 10M filters, 1M-topic batch (bench.py defaults)",
+        "workload": name,
         "batch_topics": 1000000,
         "fetch_bytes_raw_per_launch": fetch,
         "write_bytes_per_launch": s["write_bytes"],
@@ -54,9 +71,9 @@ def main():
         "l2_misses_per_launch": c["TCC_MISS_sum"],
         "l2_requests_per_launch": c["TCC_HIT_sum"] + c["TCC_MISS_sum"],
         "avg_kernel_ns": s.get("avg_ns"),
-        "source": os.path.relpath(os.path.join(d, "pmc_summary.json"), ROOT) + " (rocprofv3 --pmc passes, tools/gpu_round.sh; copied to profiles/r1_v3_pmc_summary.json)",
+        "source": src,
     }
-    with open(os.path.join(ROOT, "profiles", "pmc_match_fast.json"), "w") as f:
+    with open(os.path.join(ROOT, "profiles", fname), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
