@@ -104,8 +104,9 @@ def main():
                     help="filter-sharded table (filter i on rank i mod N): rank 0's batch is broadcast over "
                          "RCCL, matched on every shard, gathered and concatenated on rank 0 (strong scaling)")
     ap.add_argument("--vocab-scale", type=int, default=1, help="4 = config C's vocabulary")
-    ap.add_argument("--streams", type=int, default=3,
-                    help="HIP streams the timed batches alternate over (pipelined calls)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="HIP streams the timed batches alternate over (pipelined calls; default 3, "
+                         "--workload D: 1, see DESIGN.md §5)")
     ap.add_argument("--order", type=str, default="none", choices=["none", "sorted", "xcd"],
                     help="experiment: host-side permutation of the topic batch (sorted = lexicographic; "
                          "xcd = sorted, cut into 8 key-range segments, dealt 256 topics at a time so each "
@@ -115,6 +116,8 @@ def main():
     args = ap.parse_args()
     if args.batch is None:
         args.batch = D_BATCH if args.workload == "D" else 1_000_000
+    if args.streams is None:
+        args.streams = 1 if args.workload == "D" else 3
     if args.cpu_sample is None:
         args.cpu_sample = 40_000 if args.workload == "D" else 200_000
 
