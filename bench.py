@@ -78,7 +78,8 @@ def main():
                     help="topics per batch (default 1M; --workload D: D_BATCH)")
     ap.add_argument("--mode", type=int, default=0, help="0 routes, 1 trie, 2 trie_wildcard")
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="topics in the CPU baseline sample (default 200k; --workload D: 40k, ~15 s)")
+                    help="topics in the CPU baseline sample (default 200k; --workload D: 40k, ~15 s; A: the "
+                         "whole 1M batch)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cache", type=str, default=None,
@@ -119,7 +120,7 @@ def main():
     if args.streams is None:
         args.streams = 1 if args.workload in ("A", "D") else 3
     if args.cpu_sample is None:
-        args.cpu_sample = 40_000 if args.workload == "D" else 200_000
+        args.cpu_sample = {"D": 40_000, "A": 1_000_000}.get(args.workload, 200_000)
 
     import torch
     import torch.distributed as dist
