@@ -374,7 +374,7 @@ def measured_traffic(n, args):
     with open(path) as f:
         p = json.load(f)
     per_topic = p["traffic_bytes_per_launch"] / p["batch_topics"]
-    return round(per_topic * n), "profiles/pmc_match_fast.json (%s; %s)" % (p["traffic_rule"], p["source"])
+    return round(per_topic * n), "profiles/%s (%s; %s)" % (fname, p["traffic_rule"], p["source"])
 
 
 def fanout_bench(args, rank, world, dev):
