@@ -750,9 +750,12 @@ def retain_bench(args, rank, world, dev):
         "ids_per_filter": round(nout / nf, 3), "node_visits_per_filter": round(visits / nf, 3),
         "ranges_per_filter": round(ranges / nf, 3), "call_ms_median": round(cms, 4),
         "walk_ms_median": round(float(np.median(walk_ms)), 4),
+        "walk_spill_rounds": int(st["last_spill_rounds"]), "walk_spilled_items": int(st["last_spilled"]),
+        "walk_step_budget": os.environ.get("EMQX_RETAIN_STEP_BUDGET", "none (default)"),
+        "walk_tile_filters": int(os.environ.get("EMQX_RETAIN_TILE", "8")),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "retain_walk_kernel + retain_out_kernel<0,1> (whole call, incl. 2 host syncs)",
+                     "kernel": "retain_walk_kernel (+ spill rounds) + retain_out_kernel<0,1> (whole call, incl. host syncs)",
                      "alg_bytes_per_launch": alg,
                      "alg_bytes_model": "len(F) + 32*L(F) + 32*visits + 48*ranges + 16*ids + 16 per filter"},
     }

@@ -81,6 +81,7 @@ class RetainStats(ctypes.Structure):
         ("n_words", ctypes.c_uint64), ("table_bytes", ctypes.c_uint64), ("epoch", ctypes.c_uint64),
         ("last_ranges", ctypes.c_uint64), ("last_visits", ctypes.c_uint64), ("last_total", ctypes.c_uint64),
         ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double), ("last_walk_ms", ctypes.c_double),
+        ("last_spill_rounds", ctypes.c_uint64), ("last_spilled", ctypes.c_uint64),
     ]
 
     def as_dict(self):

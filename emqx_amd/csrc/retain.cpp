@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -93,7 +94,10 @@ struct RWork {
   uint32_t* ctrl = nullptr;
   uint32_t* fcount = nullptr;
   uint32_t* fcursor = nullptr;
+  uint32_t* fnlev = nullptr;
   uint64_t f_cap = 0;
+  uint4* spill[2] = {nullptr, nullptr};  // spill rounds: items in / items out, alternating
+  uint32_t spill_cap = 0;
   uint64_t* partials = nullptr;
   uint64_t partials_cap = 0;
   uint64_t* h_pinned = nullptr;  // [8] readbacks
@@ -115,6 +119,9 @@ struct RWork {
     rfree(ctrl);
     rfree(fcount);
     rfree(fcursor);
+    rfree(fnlev);
+    rfree(spill[0]);
+    rfree(spill[1]);
     rfree(partials);
     rfree(d_fb);
     rfree(d_fo);
@@ -128,7 +135,39 @@ struct RWork {
   }
 };
 
-constexpr uint32_t MAX_WAVES = 2048;
+constexpr uint32_t MAX_WAVES = 8192;
+// Load balance of the walk (opt-in, EMQX_RETAIN_STEP_BUDGET=N): a wave that has not emptied
+// its stack after N steps spills the rest, and the next round deals all spilled items evenly
+// over up to SPILL_WAVES waves.  Measured on config R it loses (each round costs a launch and a
+// host sync while the heavy filters' remaining work stays a dependent chain:
+// profiles/r1_v8_retain_sweep.txt), so the default is no budget.
+constexpr uint32_t STEP_BUDGET = ~0u;
+constexpr uint32_t SPILL_WAVES = 4096;
+constexpr uint32_t SPILL_CAP = 1u << 22;  // items per spill buffer (a full one: waves keep walking)
+constexpr int MAX_SPILL_ROUNDS = 64;      // then one round without a budget
+
+// Filters per wave tile.  The walk is latency-bound (a few dependent loads per step), so the
+// number of waves in flight, not lane fill, sets its rate: 64 filters per tile leaves ~6 waves
+// per CU for a 100K-filter batch; 8 runs the config-R walk in 10.8 ms against 18.1 ms
+// (profiles/r1_v8_retain_sweep.txt).
+constexpr uint32_t TILE_FILTERS = 8;
+
+uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* e = std::getenv(name);
+  if (!e || !*e) return dflt;
+  return static_cast<uint32_t>(std::min<unsigned long>(std::strtoul(e, nullptr, 10), 0xFFFFFFFFul));
+}
+
+uint32_t tile_filters() {  // per call (EMQX_RETAIN_TILE, experiments and tests)
+  return std::max<uint32_t>(1, std::min<uint32_t>(64, env_u32("EMQX_RETAIN_TILE", TILE_FILTERS)));
+}
+
+uint32_t step_budget() {  // per call, so tests can force many spill rounds
+  const char* e = std::getenv("EMQX_RETAIN_STEP_BUDGET");  // 0 = no budget
+  if (!e || !*e) return STEP_BUDGET;
+  const unsigned long v = std::strtoul(e, nullptr, 10);
+  return v == 0 ? ~0u : static_cast<uint32_t>(std::min<unsigned long>(v, 0xFFFFFFFEul));
+}
 
 bool has_wild_level(const uint8_t* p, uint64_t n) {
   uint64_t s = 0;
@@ -155,7 +194,7 @@ struct emqx_retain {
   std::mutex ws_mu;
   std::vector<RWork*> free_ws;
   std::vector<std::unique_ptr<RWork>> all_ws;
-  std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0};
+  std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0}, last_spill_rounds{0}, last_spilled{0};
   std::atomic<double> last_match_ms{0}, last_walk_ms{0};
 };
 
@@ -442,6 +481,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   if (n > w->f_cap) {
     RT_TRY(ralloc(w->fcount, n + n / 4));
     RT_TRY(ralloc(w->fcursor, n + n / 4));
+    RT_TRY(ralloc(w->fnlev, n + n / 4));
     w->f_cap = n + n / 4;
   }
   const uint64_t np = scan_partials(n);
@@ -455,7 +495,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     RT_TRY(ralloc(w->rcount, rc));
     w->range_cap = static_cast<uint32_t>(rc);
   }
-  const uint64_t ntiles = (n + 63) / 64;
+  a.tile_filters = tile_filters();
+  const uint64_t ntiles = (n + a.tile_filters - 1) / a.tile_filters;
   a.waves = static_cast<uint32_t>(std::min<uint64_t>(ntiles, MAX_WAVES));
   a.wids = w->wids;
   a.ctrl = w->ctrl;
@@ -463,9 +504,18 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   a.fcursor = w->fcursor;
   uint32_t nr = 0;
   RT_TRY(hipEventRecord(w->ev0, s));
+  if (w->spill_cap == 0) {
+    RT_TRY(ralloc(w->spill[0], SPILL_CAP));
+    RT_TRY(ralloc(w->spill[1], SPILL_CAP));
+    w->spill_cap = SPILL_CAP;
+  }
+  a.fnlev = w->fnlev;
+  a.spill_cap = w->spill_cap;
+  a.step_budget = step_budget();
   for (int attempt = 0;; ++attempt) {
-    if (static_cast<uint64_t>(a.waves) * w->stack_cap > w->stack_items) {
-      const uint64_t items = static_cast<uint64_t>(a.waves) * w->stack_cap;
+    const uint64_t stack_waves = static_cast<uint64_t>(w->stack_cap) <= (1u << 14) ? std::max(a.waves, SPILL_WAVES) : a.waves;
+    if (stack_waves * w->stack_cap > w->stack_items) {
+      const uint64_t items = stack_waves * w->stack_cap;
       RT_TRY(ralloc(w->stack, items));
       w->stack_items = items;
     }
@@ -474,11 +524,29 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     a.ranges = w->ranges;
     a.rcount = w->rcount;
     a.range_cap = w->range_cap;
+    a.spill_out = w->spill[0];
     RT_TRY(hipMemsetAsync(w->ctrl, 0, RC_WORDS * sizeof(uint32_t), s));
     RT_TRY(launch_retain_walk(a, s));
-    RT_TRY(hipEventRecord(w->evw, s));
-    RT_TRY(hipMemcpyAsync(w->h_pinned, w->ctrl, RC_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    RT_TRY(hipStreamSynchronize(s));
+    // spill rounds until no wave leaves work behind
+    uint64_t rounds = 0, spilled = 0;
+    for (int round = 0, cur = 0;; ++round) {
+      RT_TRY(hipEventRecord(w->evw, s));
+      RT_TRY(hipMemcpyAsync(w->h_pinned, w->ctrl, RC_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      RT_TRY(hipStreamSynchronize(s));
+      const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
+      const uint32_t n_sp = c[RC_SPILL];
+      if (n_sp == 0 || c[RC_STACK]) break;
+      ++rounds;
+      spilled += n_sp;
+      RetainArgs b = a;
+      const uint64_t fit = w->stack_items / w->stack_cap;
+      b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>({(n_sp + 3) / 4, SPILL_WAVES, fit})));
+      b.spill_out = w->spill[cur ^ 1];
+      if (round >= MAX_SPILL_ROUNDS) b.step_budget = ~0u;
+      RT_TRY(hipMemsetAsync(w->ctrl + RC_SPILL, 0, sizeof(uint32_t), s));
+      RT_TRY(launch_retain_walk_spill(b, w->spill[cur], n_sp, s));
+      cur ^= 1;
+    }
     const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
     const uint32_t ranges = c[RC_RANGES], visits = c[RC_VISITS], ovf = c[RC_STACK];
     bool again = false;
@@ -499,6 +567,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       nr = ranges;
       r->last_ranges.store(ranges);
       r->last_visits.store(visits);
+      r->last_spill_rounds.store(rounds);
+      r->last_spilled.store(spilled);
       break;
     }
   }
@@ -741,6 +811,8 @@ int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out) {
   }
   out->last_ranges = r->last_ranges.load();
   out->last_visits = r->last_visits.load();
+  out->last_spill_rounds = r->last_spill_rounds.load();
+  out->last_spilled = r->last_spilled.load();
   out->last_total = r->last_total.load();
   out->last_match_ms = r->last_match_ms.load();
   out->last_walk_ms = r->last_walk_ms.load();

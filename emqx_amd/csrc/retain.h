@@ -78,8 +78,9 @@ struct RetainView {
 };
 
 // Work item of the walk (uint4): x = first node (or first postings entry), y = count,
-// z = level, w = filter lane | RITEM_POST (the item is a postings slice)
-constexpr uint32_t RITEM_POST = 1u << 8;
+// z = level | RITEM_POST (the item is a postings slice), w = filter lane in the tile (first
+// round) or global filter id (spilled items)
+constexpr uint32_t RITEM_POST = 1u << 31;
 
 // Range emitted by the walk: filter f's matches include ranks [lo, hi), or, RRANGE_INDIRECT,
 // the ranks dterm[lo .. hi) (a filter ending in a '+' run: the stored topics of that many
@@ -100,6 +101,7 @@ enum RCtrl : uint32_t {
   RC_RANGES = 0,   // ranges emitted (may exceed range_cap: rerun)
   RC_VISITS = 1,   // node visits
   RC_STACK = 2,    // a wave's stack overflowed (rerun with a larger stack)
+  RC_SPILL = 3,    // items spilled by this round (walked by the next)
   RC_WORDS = 4
 };
 
@@ -113,6 +115,11 @@ struct RetainArgs {
   uint4* stack;            // [waves * stack_cap] per-wave work stacks (range items)
   uint32_t stack_cap;
   uint32_t waves;
+  uint32_t tile_filters;   // filters per wave tile of the first round (1..64)
+  uint32_t step_budget;    // wave steps before the rest of a stack spills (~0u: no budget)
+  uint4* spill_out;        // [spill_cap] items left when the budget ran out
+  uint32_t spill_cap;
+  uint32_t* fnlev;         // [n] levels | wildcard flag << 31 of each filter (spill rounds)
   RRange* ranges;          // [range_cap]
   uint32_t range_cap;
   uint32_t* ctrl;          // [RC_WORDS]
@@ -126,6 +133,8 @@ struct RetainArgs {
 
 // tokenize + intern every filter, then walk the trie: ranges[], ctrl
 hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s);
+// one rebalanced round over the n_in items a previous round spilled (a.waves waves)
+hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t n_in, hipStream_t s);
 // live ranks per range -> rcount, fcount (nr = ranges emitted)
 hipError_t launch_retain_count(const RetainArgs& a, uint32_t nr, hipStream_t s);
 // ids of the live ranks -> out_ids at out_off[f] + cursor

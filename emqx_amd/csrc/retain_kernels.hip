@@ -2,7 +2,7 @@
 // trie of stored retained topics (reference: the match-spec select of
 // apps/emqx_retainer/src/emqx_retainer_mnesia.erl:212-258 and read_messages/1 :199-208).
 //
-//   walk    one wavefront per tile of 64 filters (persistent waves).  Each lane tokenizes and
+//   walk    one wavefront per tile of up to 64 filters (persistent waves).  Each lane tokenizes and
 //           interns its own filter (filters are short; subscription-path work), then the wave
 //           walks all 64 filters' frontiers from one shared work stack of RANGE items
 //           {first node, node count, level, filter}: a '+' level pushes its node's whole child
@@ -83,6 +83,215 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t 
 constexpr int RW_WAVES = 4;
 constexpr uint32_t RCHUNK = 2048;  // ranks per range record
 
+// Reserve n slots of the spill buffer, all or nothing (a partial reservation would leave
+// unwritten items inside the counted prefix).  Called by one lane.
+__device__ __forceinline__ bool spill_reserve(uint32_t* ctr, uint32_t n, uint32_t cap, uint32_t* base) {
+  uint32_t old = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (old > cap || n > cap - old) return false;
+    const uint32_t prev = atomicCAS(ctr, old, old + n);
+    if (prev == old) {
+      *base = old;
+      return true;
+    }
+    old = prev;
+  }
+}
+
+// The walk of one wave's stack until it is empty or the step budget runs out; then the
+// remaining items go to a.spill_out (global filter ids) for the next, rebalanced round.
+// TILE: items name a filter lane of the tile whose first filter is `fbase` (its level count
+// and word base in LDS);
+// else items name a global filter id and the lane reads both from global memory.
+template <bool TILE>
+__device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint32_t top, uint64_t fbase,
+                                           const uint32_t* nlevs, const uint64_t* wbase, uint32_t* pref,
+                                           uint4* itm, uint32_t& visits, bool& overflow) {
+  const uint32_t lane = lane_id();
+  const RetainView& rv = a.rv;
+  const uint64_t b0 = a.foffs[0];
+  uint32_t steps = 0;
+  while (top > 0) {
+    if (steps++ == a.step_budget) {
+      uint32_t base = 0, ok = 0;
+      if (lane == 0) ok = spill_reserve(&a.ctrl[RC_SPILL], top, a.spill_cap, &base) ? 1u : 0u;
+      ok = __shfl(ok, 0, 64);
+      base = __shfl(base, 0, 64);
+      if (ok) {
+        for (uint32_t i = lane; i < top; i += 64) {
+          uint4 it = stk[i];
+          if (TILE) it.w += static_cast<uint32_t>(fbase);
+          a.spill_out[base + i] = it;
+        }
+        return;
+      }
+      // no room: this wave finishes its stack itself (the budget is checked once)
+    }
+    // ---- take the next (up to) 64 nodes from the top items ----------------------------
+    const uint32_t navail = top < 64 ? top : 64;
+    uint4 it = make_uint4(0, 0, 0, 0);
+    if (lane < navail) it = stk[top - 1 - lane];
+    uint32_t ctot;
+    const uint32_t cex = wave_excl(lane < navail ? it.y : 0u, &ctot);
+    pref[lane] = cex + (lane < navail ? it.y : 0u);  // inclusive
+    itm[lane] = it;
+    __builtin_amdgcn_wave_barrier();
+    // items fully consumed: inclusive prefix <= 64
+    const uint64_t full = __ballot(lane < navail && pref[lane] <= 64);
+    const uint32_t kfull = __popcll(full);  // a prefix of the lanes (counts >= 1)
+    const uint32_t taken = ctot < 64 ? ctot : 64;
+    if (kfull < navail && lane == 0) {  // the partially consumed item stays, shortened
+      const uint32_t used = 64 - (kfull ? pref[kfull - 1] : 0u);
+      uint4 p = itm[kfull];
+      p.x += used;
+      p.y -= used;
+      stk[top - 1 - kfull] = p;
+    }
+    top -= kfull;
+    // ---- this lane's node ---------------------------------------------------------------
+    bool act = lane < taken;
+    uint32_t v = 0, lev = 0, fl = 0;
+    if (act) {
+      uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pref[mid] > lane) hi = mid; else lo = mid + 1;
+      }
+      const uint32_t before = lo ? pref[lo - 1] : 0u;
+      const uint4 q = itm[lo];
+      v = q.x + (lane - before);
+      if (q.z & RITEM_POST) v = rv.posts[v].y;  // a postings slice: entry -> node
+      lev = q.z & ~RITEM_POST;
+      fl = q.w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    bool emit = false, push = false;
+    RRange rg{0, 0, 0, 0};
+    uint4 np = make_uint4(0, 0, 0, 0);
+    if (act) {
+      ++visits;
+      const RNode rn = rv.nodes[v];
+      uint32_t nl;
+      uint64_t wb, fg;
+      if (TILE) {
+        nl = nlevs[fl];
+        wb = wbase[fl];
+        fg = fbase + fl;
+      } else {
+        fg = fl;
+        nl = a.fnlev[fg];
+        wb = (a.foffs[fg] - b0) + fg;
+      }
+      const uint32_t fn = nl & 0x7FFFFFFFu;
+      rg.f = static_cast<uint32_t>(fg);
+      rg.flags = nl >> 31;  // wildcard filter: the match spec's strict guard
+      if (lev == fn) {
+        if (rn.ncld & RNODE_TERM) {
+          emit = true;
+          rg.lo = rn.lo;
+          rg.hi = rn.lo + 1;
+        }
+      } else {
+        const uint32_t w = a.wids[wb + lev];
+        const uint32_t ncld = rn.ncld & ~RNODE_TERM;
+        if (w == WID_HASH) {
+          emit = rn.hi > rn.lo;
+          rg.lo = rn.lo;
+          rg.hi = rn.hi;
+        } else if (w == WID_PLUS) {
+          // the '+' run from this level, then: a literal -> its postings at the depth after
+          // the run, inside this node's rank interval; else ('#', the filter's end) the
+          // children range
+          uint32_t j = lev + 1;
+          while (j < fn && a.wids[wb + j] == WID_PLUS) ++j;
+          const uint32_t wl = j < fn ? a.wids[wb + j] : WID_HASH;
+          if (ncld == 0 || wl == WID_NONE) {
+            push = false;
+          } else if (j == fn) {
+            // the filter ends with this '+' run: the stored topics of exactly fn levels in
+            // this subtree = one slice of the depth-fn rank list
+            if (fn <= rv.max_depth) {
+              const uint32_t d0 = rv.dterm_off[fn], d1 = rv.dterm_off[fn + 1];
+              const uint32_t b = v ? lower_bound_u32(rv.dterm, 1, d0, d1, rn.lo) : d0;
+              const uint32_t e = v ? lower_bound_u32(rv.dterm, 1, b, d1, rn.hi) : d1;
+              emit = e > b;
+              rg.lo = b;
+              rg.hi = e;
+              rg.flags |= RRANGE_INDIRECT;
+            }
+          } else if (wl == WID_HASH) {
+            // '+' run then the final '#': this subtree's topics of at least j levels — one
+            // rank range with a depth floor, filtered by the output kernels
+            emit = rn.hi > rn.lo;
+            rg.lo = rn.lo;
+            rg.hi = rn.hi;
+            rg.flags |= j << RRANGE_MIND_SHIFT;
+          } else {
+            uint32_t s = rpost_slot0(j + 1, wl) & rv.pkey_mask;
+            uint32_t off = 0, len = 0;
+            for (uint32_t k = 0; k <= rv.pkey_mask; ++k) {
+              const RPostKey pk = rv.pkeys[s];
+              if (pk.depth == WID_NONE) break;
+              if (pk.depth == j + 1 && pk.wid == wl) {
+                off = pk.off;
+                len = pk.len;
+                break;
+              }
+              s = (s + 1) & rv.pkey_mask;
+            }
+            // slice of entries with lo in [rn.lo, rn.hi): two lower bounds
+            const uint32_t* px = reinterpret_cast<const uint32_t*>(rv.posts);
+            const uint32_t b = v ? lower_bound_u32(px + 2ull * off, 2, 0, len, rn.lo) : 0u;
+            const uint32_t e = v ? lower_bound_u32(px + 2ull * off, 2, b, len, rn.hi) : len;
+            push = e > b;
+            np = make_uint4(off + b, e - b, (j + 1) | RITEM_POST, fl);
+          }
+        } else if (w != WID_NONE && ncld != 0) {
+          uint32_t s = redge_slot0(v, w) & rv.edge_mask;
+          for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
+            const REdge e = rv.edges[s];
+            if (e.parent == WID_NONE) break;
+            if (e.parent == v && e.wid == w) {
+              push = true;
+              np = make_uint4(e.child, 1u, lev + 1, fl);
+              break;
+            }
+            s = (s + 1) & rv.edge_mask;
+          }
+        }
+      }
+    }
+    // ---- emissions (one atomic per wave step) --------------------------------------------
+    // a range longer than RCHUNK ranks goes out as several records, so the output kernels
+    // spread one '#' over the whole subtree across many waves
+    const uint32_t nrec = emit ? (rg.hi - rg.lo + RCHUNK - 1) / RCHUNK : 0u;
+    uint32_t etot;
+    const uint32_t epos = wave_excl(nrec, &etot);
+    if (etot) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&a.ctrl[RC_RANGES], etot);
+      base = __shfl(base, 0, 64);
+      for (uint32_t k = 0; k < nrec; ++k) {
+        if (base + epos + k >= a.range_cap) break;
+        RRange part = rg;
+        part.lo = rg.lo + k * RCHUNK;
+        part.hi = min(rg.hi, part.lo + RCHUNK);
+        a.ranges[base + epos + k] = part;
+      }
+    }
+    // ---- pushes ---------------------------------------------------------------------------
+    uint32_t qtot;
+    const uint32_t qpos = wave_excl(push ? 1u : 0u, &qtot);
+    if (top + qtot > a.stack_cap) {
+      overflow = true;
+      return;
+    }
+    if (push) stk[top + qpos] = np;
+    top += qtot;
+    __threadfence_block();
+  }
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a) {
@@ -93,19 +302,19 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
   __shared__ uint4 s_item[RW_WAVES][64];
   __shared__ uint32_t s_nlev[RW_WAVES][64];
   __shared__ uint64_t s_wb[RW_WAVES][64];
-  uint32_t* pref = s_pref[wib];
-  uint4* itm = s_item[wib];
   uint32_t* nlevs = s_nlev[wib];
   uint64_t* wbase = s_wb[wib];  // per filter of the tile: its first word id in a.wids
   uint4* stk = a.stack + static_cast<uint64_t>(gw) * a.stack_cap;
   const RetainView& rv = a.rv;
-  const uint64_t ntiles = (a.n + 63) / 64;
+  const uint32_t tf = a.tile_filters;  // filters per wave tile (1..64): fewer = more waves in flight
+  const uint64_t ntiles = (a.n + tf - 1) / tf;
   const uint64_t b0 = a.foffs[0];
   uint32_t visits = 0;
+  bool overflow = false;
 
   for (uint64_t t = gw; t < ntiles; t += a.waves) {
-    const uint64_t f = t * 64 + lane;
-    const bool valid = f < a.n;
+    const uint64_t f = t * tf + lane;
+    const bool valid = lane < tf && f < a.n;
     // ---- tokenize + intern (per lane) -------------------------------------------------
     uint32_t nlev = 0, wild = 0;
     if (valid) {
@@ -143,6 +352,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
           ws = i + 1;
         }
       }
+      a.fnlev[f] = nlev | (wild << 31);  // for the spill rounds
     }
     nlevs[lane] = nlev | (wild << 31);
     wbase[lane] = valid ? (a.foffs[f] - b0) + f : 0;
@@ -151,172 +361,45 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
     uint32_t ptot;
     const uint32_t ppos = wave_excl(push0 ? 1u : 0u, &ptot);
     if (push0) stk[ppos] = make_uint4(0u, 1u, 0u, lane);
-    uint32_t top = ptot;
-    bool overflow = false;
     __threadfence_block();  // the stack lives in global memory: order this wave's stores and loads
-
-    while (top > 0) {
-      // ---- take the next (up to) 64 nodes from the top items ----------------------------
-      const uint32_t navail = top < 64 ? top : 64;
-      uint4 it = make_uint4(0, 0, 0, 0);
-      if (lane < navail) it = stk[top - 1 - lane];
-      uint32_t ctot;
-      const uint32_t cex = wave_excl(lane < navail ? it.y : 0u, &ctot);
-      pref[lane] = cex + (lane < navail ? it.y : 0u);  // inclusive
-      itm[lane] = it;
-      __builtin_amdgcn_wave_barrier();
-      // items fully consumed: inclusive prefix <= 64
-      const uint64_t full = __ballot(lane < navail && pref[lane] <= 64);
-      const uint32_t kfull = __popcll(full);  // a prefix of the lanes (counts >= 1)
-      const uint32_t taken = ctot < 64 ? ctot : 64;
-      if (kfull < navail && lane == 0) {  // the partially consumed item stays, shortened
-        const uint32_t used = 64 - (kfull ? pref[kfull - 1] : 0u);
-        uint4 p = itm[kfull];
-        p.x += used;
-        p.y -= used;
-        stk[top - 1 - kfull] = p;
-      }
-      top -= kfull;
-      // ---- this lane's node ---------------------------------------------------------------
-      bool act = lane < taken;
-      uint32_t v = 0, lev = 0, fl = 0;
-      if (act) {
-        uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (pref[mid] > lane) hi = mid; else lo = mid + 1;
-        }
-        const uint32_t before = lo ? pref[lo - 1] : 0u;
-        const uint4 q = itm[lo];
-        v = q.x + (lane - before);
-        if (q.w & RITEM_POST) v = rv.posts[v].y;  // a postings slice: entry -> node
-        lev = q.z;
-        fl = q.w & 63u;
-      }
-      __builtin_amdgcn_wave_barrier();
-      bool emit = false, push = false;
-      RRange rg{0, 0, 0, 0};
-      uint4 np = make_uint4(0, 0, 0, 0);
-      if (act) {
-        ++visits;
-        const RNode rn = rv.nodes[v];
-        const uint32_t nl = nlevs[fl];
-        const uint32_t fn = nl & 0x7FFFFFFFu;
-        const uint64_t fg = t * 64 + fl;
-        rg.f = static_cast<uint32_t>(fg);
-        rg.flags = nl >> 31;  // wildcard filter: the match spec's strict guard
-        if (lev == fn) {
-          if (rn.ncld & RNODE_TERM) {
-            emit = true;
-            rg.lo = rn.lo;
-            rg.hi = rn.lo + 1;
-          }
-        } else {
-          const uint32_t w = a.wids[wbase[fl] + lev];
-          const uint32_t ncld = rn.ncld & ~RNODE_TERM;
-          if (w == WID_HASH) {
-            emit = rn.hi > rn.lo;
-            rg.lo = rn.lo;
-            rg.hi = rn.hi;
-          } else if (w == WID_PLUS) {
-            // the '+' run from this level, then: a literal -> its postings at the depth after
-            // the run, inside this node's rank interval; else ('#', the filter's end) the
-            // children range
-            uint32_t j = lev + 1;
-            while (j < fn && a.wids[wbase[fl] + j] == WID_PLUS) ++j;
-            const uint32_t wl = j < fn ? a.wids[wbase[fl] + j] : WID_HASH;
-            if (ncld == 0 || wl == WID_NONE) {
-              push = false;
-            } else if (j == fn) {
-              // the filter ends with this '+' run: the stored topics of exactly fn levels in
-              // this subtree = one slice of the depth-fn rank list
-              if (fn <= rv.max_depth) {
-                const uint32_t d0 = rv.dterm_off[fn], d1 = rv.dterm_off[fn + 1];
-                const uint32_t b = v ? lower_bound_u32(rv.dterm, 1, d0, d1, rn.lo) : d0;
-                const uint32_t e = v ? lower_bound_u32(rv.dterm, 1, b, d1, rn.hi) : d1;
-                emit = e > b;
-                rg.lo = b;
-                rg.hi = e;
-                rg.flags |= RRANGE_INDIRECT;
-              }
-            } else if (wl == WID_HASH) {
-              // '+' run then the final '#': this subtree's topics of at least j levels — one
-              // rank range with a depth floor, filtered by the output kernels
-              emit = rn.hi > rn.lo;
-              rg.lo = rn.lo;
-              rg.hi = rn.hi;
-              rg.flags |= j << RRANGE_MIND_SHIFT;
-            } else {
-              uint32_t s = rpost_slot0(j + 1, wl) & rv.pkey_mask;
-              uint32_t off = 0, len = 0;
-              for (uint32_t k = 0; k <= rv.pkey_mask; ++k) {
-                const RPostKey pk = rv.pkeys[s];
-                if (pk.depth == WID_NONE) break;
-                if (pk.depth == j + 1 && pk.wid == wl) {
-                  off = pk.off;
-                  len = pk.len;
-                  break;
-                }
-                s = (s + 1) & rv.pkey_mask;
-              }
-              // slice of entries with lo in [rn.lo, rn.hi): two lower bounds
-              const uint32_t* px = reinterpret_cast<const uint32_t*>(rv.posts);
-              const uint32_t b = v ? lower_bound_u32(px + 2ull * off, 2, 0, len, rn.lo) : 0u;
-              const uint32_t e = v ? lower_bound_u32(px + 2ull * off, 2, b, len, rn.hi) : len;
-              push = e > b;
-              np = make_uint4(off + b, e - b, j + 1, fl | RITEM_POST);
-            }
-          } else if (w != WID_NONE && ncld != 0) {
-            uint32_t s = redge_slot0(v, w) & rv.edge_mask;
-            for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
-              const REdge e = rv.edges[s];
-              if (e.parent == WID_NONE) break;
-              if (e.parent == v && e.wid == w) {
-                push = true;
-                np = make_uint4(e.child, 1u, lev + 1, fl);
-                break;
-              }
-              s = (s + 1) & rv.edge_mask;
-            }
-          }
-        }
-      }
-      // ---- emissions (one atomic per wave step) --------------------------------------------
-      // a range longer than RCHUNK ranks goes out as several records, so the output kernels
-      // spread one '#' over the whole subtree across many waves
-      const uint32_t nrec = emit ? (rg.hi - rg.lo + RCHUNK - 1) / RCHUNK : 0u;
-      uint32_t etot;
-      const uint32_t epos = wave_excl(nrec, &etot);
-      if (etot) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&a.ctrl[RC_RANGES], etot);
-        base = __shfl(base, 0, 64);
-        for (uint32_t k = 0; k < nrec; ++k) {
-          if (base + epos + k >= a.range_cap) break;
-          RRange part = rg;
-          part.lo = rg.lo + k * RCHUNK;
-          part.hi = min(rg.hi, part.lo + RCHUNK);
-          a.ranges[base + epos + k] = part;
-        }
-      }
-      // ---- pushes ---------------------------------------------------------------------------
-      uint32_t qtot;
-      const uint32_t qpos = wave_excl(push ? 1u : 0u, &qtot);
-      if (top + qtot > a.stack_cap) {
-        overflow = true;
-        break;
-      }
-      if (push) stk[top + qpos] = np;
-      top += qtot;
-      __threadfence_block();
-    }
-    if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
+    walk_stack<true>(a, stk, ptot, t * tf, nlevs, wbase, s_pref[wib], s_item[wib], visits, overflow);
+    if (overflow) break;
   }
+  if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
   // visits: one atomic per wave
   uint32_t vtot;
   (void)wave_excl(visits, &vtot);
   if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
 }
+
+// A spill round: the items the previous round left (global filter ids) dealt evenly over
+// `a.waves` waves, each walking its share under the same step budget.
+__global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_spill_kernel(RetainArgs a, const uint4* in, uint32_t n_in) {
+  const uint32_t lane = lane_id();
+  const uint32_t wib = threadIdx.x >> 6;
+  const uint32_t gw = blockIdx.x * RW_WAVES + wib;
+  __shared__ uint32_t s_pref[RW_WAVES][64];
+  __shared__ uint4 s_item[RW_WAVES][64];
+  if (gw >= a.waves) return;
+  uint4* stk = a.stack + static_cast<uint64_t>(gw) * a.stack_cap;
+  const uint32_t per = (n_in + a.waves - 1) / a.waves;
+  const uint64_t lo = static_cast<uint64_t>(gw) * per;
+  const uint64_t hi = lo + per < n_in ? lo + per : static_cast<uint64_t>(n_in);
+  const uint32_t top = hi > lo ? static_cast<uint32_t>(hi - lo) : 0u;
+  uint32_t visits = 0;
+  bool overflow = top > a.stack_cap;
+  if (!overflow) {
+    for (uint32_t i = lane; i < top; i += 64) stk[i] = in[lo + i];
+    __threadfence_block();
+    walk_stack<false>(a, stk, top, 0, nullptr, nullptr, s_pref[wib], s_item[wib], visits, overflow);
+  }
+  if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
+  uint32_t vtot;
+  (void)wave_excl(visits, &vtot);
+  if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
+}
+
+namespace {
 
 // count (mode 0) / write (mode 1): one wave per 64 ranges (grid-stride).  Ranges of at most
 // one rank are handled lane-parallel; longer ones by the whole wave, 64 ranks at a time.
@@ -378,10 +461,19 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t 
   }
 }
 
+}  // namespace
+
 hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint32_t blocks = (a.waves + RW_WAVES - 1) / RW_WAVES;
   hipLaunchKernelGGL(retain_walk_kernel, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t n_in, hipStream_t s) {
+  if (n_in == 0 || a.waves == 0) return hipSuccess;
+  const uint32_t blocks = (a.waves + RW_WAVES - 1) / RW_WAVES;
+  hipLaunchKernelGGL(retain_walk_spill_kernel, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a, in, n_in);
   return hipGetLastError();
 }
 

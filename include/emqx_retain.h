@@ -55,7 +55,9 @@ typedef struct emqx_retain_stats {
   uint64_t last_total;       /* topic ids the last match returned                           */
   double last_build_ms;      /* host build + upload time of the last commit                 */
   double last_match_ms;      /* device time of the last match call (hipEvent)               */
-  double last_walk_ms;       /* ... of its walk kernel alone                                */
+  double last_walk_ms;       /* ... of its walk (first round and spill rounds)              */
+  uint64_t last_spill_rounds; /* walk rounds after the first (work left by waves over budget) */
+  uint64_t last_spilled;     /* work items handed to those rounds                           */
 } emqx_retain_stats;
 
 int emqx_retain_create(int32_t device, emqx_retain** out);
