@@ -751,7 +751,7 @@ def retain_bench(args, rank, world, dev):
         "ranges_per_filter": round(ranges / nf, 3), "call_ms_median": round(cms, 4),
         "walk_ms_median": round(float(np.median(walk_ms)), 4),
         "walk_spill_rounds": int(st["last_spill_rounds"]), "walk_spilled_items": int(st["last_spilled"]),
-        "walk_step_budget": os.environ.get("EMQX_RETAIN_STEP_BUDGET", "none (default)"),
+        "walk_step_budget": os.environ.get("EMQX_RETAIN_STEP_BUDGET", "128 (default)"),
         "walk_tile_filters": int(os.environ.get("EMQX_RETAIN_TILE", "8")),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,

@@ -136,12 +136,12 @@ struct RWork {
 };
 
 constexpr uint32_t MAX_WAVES = 8192;
-// Load balance of the walk (opt-in, EMQX_RETAIN_STEP_BUDGET=N): a wave that has not emptied
-// its stack after N steps spills the rest, and the next round deals all spilled items evenly
-// over up to SPILL_WAVES waves.  Measured on config R it loses (each round costs a launch and a
-// host sync while the heavy filters' remaining work stays a dependent chain:
-// profiles/r1_v8_retain_sweep.txt), so the default is no budget.
-constexpr uint32_t STEP_BUDGET = ~0u;
+// Load balance of the walk: a wave that has not emptied its stack after STEP_BUDGET steps
+// spills the rest as 64-node pieces, and the next round deals them evenly over up to
+// SPILL_WAVES waves.  The heavy filters' work is wide '+' slices (thousands of nodes per item):
+// config R's walk drops from 10.7 to 3.8 ms in 2 rounds (profiles/r1_v8_retain_sweep.txt).
+// EMQX_RETAIN_STEP_BUDGET overrides it (0 = no budget).
+constexpr uint32_t STEP_BUDGET = 128;
 constexpr uint32_t SPILL_WAVES = 4096;
 constexpr uint32_t SPILL_CAP = 1u << 22;  // items per spill buffer (a full one: waves keep walking)
 constexpr int MAX_SPILL_ROUNDS = 64;      // then one round without a budget

@@ -113,15 +113,32 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
   uint32_t steps = 0;
   while (top > 0) {
     if (steps++ == a.step_budget) {
+      // items wider than 64 nodes go out as 64-node pieces, so the next round can deal one
+      // wide '+' slice over many waves
+      uint32_t pieces = 0;
+      for (uint32_t i = lane; i < top; i += 64) pieces += (stk[i].y + 63) >> 6;
+      uint32_t ptot;
+      (void)wave_excl(pieces, &ptot);
       uint32_t base = 0, ok = 0;
-      if (lane == 0) ok = spill_reserve(&a.ctrl[RC_SPILL], top, a.spill_cap, &base) ? 1u : 0u;
+      if (lane == 0) ok = spill_reserve(&a.ctrl[RC_SPILL], ptot, a.spill_cap, &base) ? 1u : 0u;
       ok = __shfl(ok, 0, 64);
       base = __shfl(base, 0, 64);
       if (ok) {
-        for (uint32_t i = lane; i < top; i += 64) {
-          uint4 it = stk[i];
+        for (uint32_t i0 = 0; i0 < top; i0 += 64) {
+          const uint32_t i = i0 + lane;
+          uint4 it = make_uint4(0, 0, 0, 0);
+          if (i < top) it = stk[i];
+          const uint32_t np = i < top ? (it.y + 63) >> 6 : 0u;
+          uint32_t ctot;
+          const uint32_t off = wave_excl(np, &ctot);
           if (TILE) it.w += static_cast<uint32_t>(fbase);
-          a.spill_out[base + i] = it;
+          for (uint32_t k = 0; k < np; ++k) {
+            uint4 pc = it;
+            pc.x = it.x + 64 * k;
+            pc.y = min(64u, it.y - 64 * k);
+            a.spill_out[base + off + k] = pc;
+          }
+          base += ctot;
         }
         return;
       }
@@ -401,8 +418,9 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_spill_kernel(Retain
 
 namespace {
 
-// count (mode 0) / write (mode 1): one wave per 64 ranges (grid-stride).  Ranges of at most
-// one rank are handled lane-parallel; longer ones by the whole wave, 64 ranks at a time.
+// count (mode 0) / write (mode 1): one wave per 64 ranges (grid-stride, strided rows).  Ranges of at most
+// RSHORT ranks are handled lane-parallel; longer ones by the whole wave, 64 ranks at a time.
+constexpr uint32_t RSHORT = 32;
 template <int MODE>
 __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t nr) {
   const uint32_t lane = lane_id();
@@ -410,8 +428,11 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t 
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
   const RetainView& rv = a.rv;
   const bool guard = rv.has_expiring && a.now_ms >= 0;
-  for (uint64_t r0 = static_cast<uint64_t>(gw) * 64; r0 < nr; r0 += static_cast<uint64_t>(nw) * 64) {
-    const uint64_t r = r0 + lane;
+  // lane l of row j takes range l * nrows + j: one emission's consecutive records (a root '#'
+  // is hundreds of RCHUNK records) land in different waves instead of one wave's serial loop
+  const uint64_t nrows = (static_cast<uint64_t>(nr) + 63) / 64;
+  for (uint64_t row = gw; row < nrows; row += nw) {
+    const uint64_t r = static_cast<uint64_t>(lane) * nrows + row;
     const bool valid = r < nr;
     RRange rg{0, 0, 0, 0};
     if (valid) rg = a.ranges[r];
@@ -419,16 +440,30 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t 
     uint32_t c = 0;
     uint64_t pos = 0;
     const bool check = guard || (rg.flags >> RRANGE_MIND_SHIFT) != 0;  // per-rank filtering needed
+    // ranges of at most RSHORT ranks: this lane alone (independent loads, no wave-wide pass
+    // per range); longer ones: the whole wave
     if (MODE == 0) {
-      if (valid && (!check || len <= 1))
-        c = (!check || (len == 1 && rank_ok(rv, rank_at(rv, rg.lo, rg.flags), guard, a.now_ms, rg.flags))) ? len : 0u;
+      if (valid && !check) {
+        c = len;
+      } else if (valid && len <= RSHORT) {
+        for (uint32_t i = rg.lo; i < rg.hi; ++i) c += rank_ok(rv, rank_at(rv, i, rg.flags), guard, a.now_ms, rg.flags) ? 1u : 0u;
+      }
     } else if (valid) {
       c = a.rcount[r];
       if (c) pos = a.out_off[rg.f] + atomicAdd(&a.fcursor[rg.f], c);
-      if (c && len == 1 && pos < a.out_cap) a.out_ids[pos] = rv.rank_id[rank_at(rv, rg.lo, rg.flags)];
+      if (c && len <= RSHORT) {
+        uint64_t p = pos;
+        for (uint32_t i = rg.lo; i < rg.hi; ++i) {
+          const uint32_t rk = rank_at(rv, i, rg.flags);
+          if (len == 1 || rank_ok(rv, rk, guard, a.now_ms, rg.flags)) {
+            if (p < a.out_cap) a.out_ids[p] = rv.rank_id[rk];
+            ++p;
+          }
+        }
+      }
     }
-    // wave-cooperative ranges: longer than one rank (and, when counting, only under a guard)
-    uint64_t big = __ballot(valid && len > 1 && (MODE == 1 ? c != 0 : check));
+    // wave-cooperative ranges: longer than RSHORT ranks (and, when counting, only under a guard)
+    uint64_t big = __ballot(valid && len > RSHORT && (MODE == 1 ? c != 0 : check));
     while (big) {
       const uint32_t b = __ffsll(static_cast<unsigned long long>(big)) - 1;
       big &= big - 1;
