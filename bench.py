@@ -361,6 +361,19 @@ def sharded_bench(args, rank, world, dev):
     dist.destroy_process_group()
 
 
+def retain_traffic(nf, n_retained):
+    """HBM bytes of one config-R call from the committed PMC passes (profiles/pmc_retain.json,
+    tools/pmc_retain.py), when they were taken on this same workload; else (None, None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_retain.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        p = json.load(f)
+    if p.get("filters_per_call") != nf or p.get("retained_topics") != n_retained or p.get("traffic_bytes_per_call") is None:
+        return None, None
+    return round(p["traffic_bytes_per_call"]), "profiles/pmc_retain.json (%s; %s)" % (p["traffic_rule"], p["source"])
+
+
 def measured_traffic(n, args):
     """HBM bytes per launch of the fused match kernel from the committed rocprofv3 PMC passes
     (profiles/pmc_match_fast.json, written from tools/gpu_round.sh's counter runs on the same
@@ -754,7 +767,8 @@ def retain_bench(args, rank, world, dev):
         "walk_step_budget": os.environ.get("EMQX_RETAIN_STEP_BUDGET", "128 (default)"),
         "walk_tile_filters": int(os.environ.get("EMQX_RETAIN_TILE", "8")),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": retain_traffic(nf, len(names))[0],
+                     "traffic_source": retain_traffic(nf, len(names))[1],
                      "kernel": "retain_walk_kernel (+ spill rounds) + retain_out_kernel<0,1> (whole call, incl. host syncs)",
                      "alg_bytes_per_launch": alg,
                      "alg_bytes_model": "len(F) + 32*L(F) + 32*visits + 48*ranges + 16*ids + 16 per filter"},
