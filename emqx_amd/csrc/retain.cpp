@@ -143,6 +143,7 @@ constexpr uint32_t MAX_WAVES = 8192;
 // EMQX_RETAIN_STEP_BUDGET overrides it (0 = no budget).
 constexpr uint32_t STEP_BUDGET = 128;
 constexpr uint32_t SPILL_WAVES = 4096;
+constexpr uint32_t SPILL_PER_WAVE = 4;  // spilled pieces dealt to each wave of a spill round
 constexpr uint32_t SPILL_CAP = 1u << 22;  // items per spill buffer (a full one: waves keep walking)
 constexpr int MAX_SPILL_ROUNDS = 64;      // then one round without a budget
 
@@ -540,7 +541,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       spilled += n_sp;
       RetainArgs b = a;
       const uint64_t fit = w->stack_items / w->stack_cap;
-      b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>({(n_sp + 3) / 4, SPILL_WAVES, fit})));
+      const uint64_t per = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_SPILL_PER_WAVE", SPILL_PER_WAVE));
+      b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>({(n_sp + per - 1) / per, SPILL_WAVES, fit})));
       b.spill_out = w->spill[cur ^ 1];
       if (round >= MAX_SPILL_ROUNDS) b.step_budget = ~0u;
       RT_TRY(hipMemsetAsync(w->ctrl + RC_SPILL, 0, sizeof(uint32_t), s));
