@@ -70,14 +70,24 @@ __device__ __forceinline__ uint32_t rank_at(const RetainView& rv, uint32_t i, ui
   return (flags & RRANGE_INDIRECT) ? rv.dterm[i] : i;
 }
 
-// first index in [l, h) of the ascending u32 array a (stride in words) with a[i] >= x
-__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t stride, uint32_t l, uint32_t h,
-                                                    uint32_t x) {
-  while (l < h) {
-    const uint32_t m = (l + h) >> 1;
-    if (a[static_cast<uint64_t>(m) * stride] < x) l = m + 1; else h = m;
+// Both lower bounds of x1 <= x2 in [l, h) at once: two independent load chains in flight
+// instead of one after the other (the walk is latency-bound).  Same results as two calls.
+__device__ __forceinline__ void lower_bound2_u32(const uint32_t* a, uint32_t stride, uint32_t l, uint32_t h,
+                                                 uint32_t x1, uint32_t x2, uint32_t* r1, uint32_t* r2) {
+  uint32_t l1 = l, h1 = h, l2 = l, h2 = h;
+  while (l1 < h1 || l2 < h2) {
+    const uint32_t m1 = l1 < h1 ? (l1 + h1) >> 1 : l;  // in [l, h) either way
+    const uint32_t m2 = l2 < h2 ? (l2 + h2) >> 1 : l;
+    const uint32_t v1 = a[static_cast<uint64_t>(m1) * stride], v2 = a[static_cast<uint64_t>(m2) * stride];
+    if (l1 < h1) {
+      if (v1 < x1) l1 = m1 + 1; else h1 = m1;
+    }
+    if (l2 < h2) {
+      if (v2 < x2) l2 = m2 + 1; else h2 = m2;
+    }
   }
-  return l;
+  *r1 = l1;
+  *r2 = l2;
 }
 
 constexpr int RW_WAVES = 4;
@@ -229,8 +239,8 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
             // this subtree = one slice of the depth-fn rank list
             if (fn <= rv.max_depth) {
               const uint32_t d0 = rv.dterm_off[fn], d1 = rv.dterm_off[fn + 1];
-              const uint32_t b = v ? lower_bound_u32(rv.dterm, 1, d0, d1, rn.lo) : d0;
-              const uint32_t e = v ? lower_bound_u32(rv.dterm, 1, b, d1, rn.hi) : d1;
+              uint32_t b = d0, e = d1;
+              if (v) lower_bound2_u32(rv.dterm, 1, d0, d1, rn.lo, rn.hi, &b, &e);
               emit = e > b;
               rg.lo = b;
               rg.hi = e;
@@ -258,8 +268,8 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
             }
             // slice of entries with lo in [rn.lo, rn.hi): two lower bounds
             const uint32_t* px = reinterpret_cast<const uint32_t*>(rv.posts);
-            const uint32_t b = v ? lower_bound_u32(px + 2ull * off, 2, 0, len, rn.lo) : 0u;
-            const uint32_t e = v ? lower_bound_u32(px + 2ull * off, 2, b, len, rn.hi) : len;
+            uint32_t b = 0, e = len;
+            if (v) lower_bound2_u32(px + 2ull * off, 2, 0, len, rn.lo, rn.hi, &b, &e);
             push = e > b;
             np = make_uint4(off + b, e - b, (j + 1) | RITEM_POST, fl);
           }
