@@ -78,9 +78,10 @@ def main():
                     help="topics per batch (default 1M; --workload D: D_BATCH)")
     ap.add_argument("--mode", type=int, default=0, help="0 routes, 1 trie, 2 trie_wildcard")
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="topics in the CPU baseline sample (default 200k; --workload D: 40k, ~15 s; A: the "
-                         "whole 1M batch)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+                    help="topics in the CPU baseline sample, also the topics whose GPU match sets are compared "
+                         "ID-for-ID with the oracle (default: the whole 1M batch; --workload D: 40k, ~15 s)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (default 0: every host core this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cache", type=str, default=None,
                     help="npz path: reuse the generated workload across runs (profiling passes)")
@@ -120,7 +121,7 @@ def main():
     if args.streams is None:
         args.streams = 1 if args.workload in ("A", "D") else 3
     if args.cpu_sample is None:
-        args.cpu_sample = {"D": 40_000, "A": 1_000_000}.get(args.workload, 200_000)
+        args.cpu_sample = {"D": 40_000}.get(args.workload, 1_000_000)
 
     import torch
     import torch.distributed as dist
@@ -259,6 +260,9 @@ def main():
                 "traffic": traffic, "traffic_source": traffic_src, "kernel": "match_fast_kernel",
                 "kernel_ms_avg": round(kms, 4), "alg_bytes_per_launch": alg_bytes,
                 "alg_bytes_model": "len(T) + 64*L(T) + 64*evals(T) + 4*(|M(T)|+1) per topic (SURVEY §8 d)"}
+    rr = request_roofline(n, kms, args)
+    if rr is not None:
+        roofline["request_rate"] = rr
 
     result = {
         "metric": "published topics matched/sec (and match evals/sec) at 10M subs; % of HBM BW",
@@ -297,7 +301,12 @@ def main():
         result["diag_per_topic"]["kernel_ms_diag_call"] = round(eng.stats()["last_kernel_ms"], 4)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(wl, args)
+        # the GPU CSR of the last synchronous call (the whole batch), compared ID-for-ID
+        k = min(args.cpu_sample, n)
+        off_g = d_off[: k + 1].cpu().numpy()
+        ids_g = d_ids[: int(off_g[-1])].cpu().numpy().view(np.uint32)
+        result["cpu_baseline"] = cpu_baseline(wl, args, (off_g, ids_g))
+        result["parity"] = result["cpu_baseline"].pop("parity")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -388,6 +397,44 @@ def measured_traffic(n, args):
         p = json.load(f)
     per_topic = p["traffic_bytes_per_launch"] / p["batch_topics"]
     return round(per_topic * n), "profiles/%s (%s; %s)" % (fname, p["traffic_rule"], p["source"])
+
+
+def gather_ceiling():
+    """Random-access ceiling of the chip: the best rate of independent random 16-B reads from
+    a 1 GiB HBM-resident table (tools/gather_bench.hip, profiles/r1_gather16_ceiling.jsonl):
+    one L2 miss per read, so it is also the ceiling on L2 misses/s."""
+    path = os.path.join(ROOT, "profiles", "r1_gather16_ceiling.jsonl")
+    best = None
+    if os.path.exists(path):
+        with open(path) as f:
+            for line in f:
+                r = json.loads(line)
+                if r.get("shape") == "indep" and r.get("table_mb", 0) >= 1024:
+                    best = max(best or 0.0, float(r["records_per_s"]))
+    return best
+
+
+def request_roofline(n, kms, args):
+    """The request-rate roofline beside the byte one: the fused kernel's L2 misses per launch
+    (committed PMC passes, scaled to this batch) / its HIP-event time, against the measured
+    random-access ceiling.  The walk is a chain of dependent random 16-B probes, so this, not
+    the byte rate, is what bounds it."""
+    fname = {"B": "pmc_match_fast.json", "D": "pmc_match_fast_D.json"}.get(args.workload)
+    if fname is None or args.mode != 0 or args.vocab_scale != 1 or (args.workload == "B" and args.n_filters != 10_000_000):
+        return None
+    path = os.path.join(ROOT, "profiles", fname)
+    ceil = gather_ceiling()
+    if not os.path.exists(path) or not ceil:
+        return None
+    with open(path) as f:
+        p = json.load(f)
+    misses = p["l2_misses_per_launch"] / p["batch_topics"] * n
+    got = misses / (kms * 1e-3)
+    return {"bound": "random-access issue (L2 misses)", "l2_misses_per_launch": round(misses),
+            "l2_misses_per_topic": round(misses / n, 2), "l2_hit_rate": round(p["l2_hit_rate"], 4),
+            "achieved": round(got / 1e9, 2), "peak": round(ceil / 1e9, 2), "unit": "G misses/s",
+            "frac": round(got / ceil, 4),
+            "source": f"profiles/{fname} (TCC_MISS per launch); ceiling profiles/r1_gather16_ceiling.jsonl"}
 
 
 def fanout_bench(args, rank, world, dev):
@@ -778,7 +825,7 @@ def retain_bench(args, rank, world, dev):
         sc = C.RetainScan(tb, to, expiry)
         sample = min(2000, nf)
         sfb, sfo = W.take(filt_wl.filters, np.arange(sample))
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        threads = args.cpu_threads or host_threads()[0]
         t1 = time.perf_counter()
         counts, sums = sc.select_packed(sfb, sfo, now, threads=threads)
         dt = time.perf_counter() - t1
@@ -891,29 +938,70 @@ def ab_variants(eng, step, args, wl):
     print(json.dumps({"ab": out, "n_filters": wl.n_filters, "batch": wl.n_topics}), flush=True)
 
 
-def cpu_baseline(wl, args):
+def host_threads():
+    """Threads for the CPU baseline: the host cores this process may use (its affinity set,
+    capped by a cgroup CPU quota when one is set, as on the GPU box's per-GPU CPU share);
+    `nproc` (os.cpu_count()) is reported beside it."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    t = aff
+    for cap in (quota, share):
+        if cap:
+            t = min(t, cap)
+    return max(1, t), {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "omp_num_threads": share}
+
+
+def cpu_baseline(wl, args, gpu_csr=None):
     """emqx_trie compact-mode DFS (oracle/trie_oracle.cpp) + emqx_router exact union, timed on
-    a bounded sample of the same batch with one thread per core (kind "port": Erlang is absent
-    on the GPU box)."""
+    a bounded sample of the same batch with one thread per host core (kind "port": Erlang is
+    absent on the GPU box).  The oracle emits the full sorted id set of every sampled topic
+    (as match_routes/1 returns it); `gpu_csr` = (offsets, ids) of the GPU's call on the whole
+    batch is compared with it ID-for-ID and the bench fails on any mismatch."""
     from emqx_amd import workloads as W
     from oracle import cpp as C
     t0 = time.time()
-    o = C.CppOracle(True)
-    o.add_packed(*wl.filters)
-    o.freeze()
+    o = C.CppOracle(True, trie_all=(args.mode == C.MODE_TRIE))
+    with progress("cpu baseline: building the oracle table"):
+        o.add_packed(*wl.filters)
+        o.freeze()
     build_s = time.time() - t0
     sample = min(args.cpu_sample, wl.n_topics)
     s = W.take(wl.topics, np.arange(sample))
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads, host = host_threads()
+    if args.cpu_threads:
+        threads = args.cpu_threads
     t0 = time.perf_counter()
-    counts, _, lookups = o.match_packed(*s, mode=args.mode, threads=threads, want_ids=False)
+    off_o, ids_o, lookups = o.match_csr(*s, mode=args.mode, threads=threads)
     dt = time.perf_counter() - t0
     log(f"cpu baseline: {sample} topics in {dt:.2f}s on {threads} threads (table build {build_s:.1f}s)")
-    return {"value": round(sample / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
-            "sample": f"first {sample} topics of the batch vs the full {wl.n_filters}-filter table",
-            "ets_lookups_per_topic": round(lookups / sample, 2),
-            "matches_per_topic": round(float(np.mean(counts)), 3)}
-
+    res = {"value": round(sample / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
+           "sample": f"first {sample} topics of the batch vs the full {wl.n_filters}-filter table",
+           "host": host,
+           "ets_lookups_per_topic": round(lookups / sample, 2),
+           "matches_per_topic": round(float(off_o[-1]) / max(sample, 1), 3)}
+    if gpu_csr is not None:
+        off_g, ids_g = gpu_csr
+        off_g = off_g[: sample + 1]
+        bad = C.csr_mismatches(off_g, ids_g, off_o, ids_o)
+        res["parity"] = {"topics_checked": int(sample), "ids_checked": int(off_o[-1]),
+                         "mismatches": int(bad.size),
+                         "rule": "per-topic sorted filter-id sets, GPU CSR vs the oracle (SURVEY §8 S7)"}
+        if bad.size:
+            raise SystemExit(f"GPU match sets differ from the oracle on {bad.size} of {sample} topics, "
+                             f"first {bad[:10].tolist()}")
+    return res
 
 if __name__ == "__main__":
     main()

@@ -36,6 +36,10 @@ def lib():
         L.orc_match.argtypes = [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                 u32p, u32p, ctypes.c_uint32]
         L.orc_evals.argtypes = [vp, u8p, u64p, ctypes.c_uint64, u64p]
+        L.orc_match_csr.restype = vp
+        L.orc_match_csr.argtypes = [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, u64p, u64p]
+        L.orc_csr_copy.argtypes = [vp, u32p]
+        L.orc_csr_free.argtypes = [vp]
         L.orr_create.restype = vp
         L.orr_create.argtypes = [u8p, u64p, ctypes.c_uint64, vp]
         L.orr_destroy.argtypes = [vp]
@@ -104,6 +108,19 @@ class CppOracle:
                                   _p(ids) if want_ids else None, stride)
         return counts[:n], (ids[: n * stride].reshape(n, stride) if want_ids else None), int(lookups)
 
+    def match_csr(self, buf, offs, mode=MODE_ROUTES, threads=1):
+        """(offsets uint64 (n+1,), ids uint32 (offsets[n],) sorted per topic, total lookups)."""
+        n = len(offs) - 1
+        off = np.zeros(n + 1, dtype=np.uint64)
+        lk = np.zeros(1, dtype=np.uint64)
+        r = lib().orc_match_csr(self.h, _p(buf), _p(offs), n, mode, threads, _p(off), _p(lk))
+        try:
+            ids = np.zeros(max(int(off[-1]), 1), dtype=np.uint32)
+            lib().orc_csr_copy(r, _p(ids))
+        finally:
+            lib().orc_csr_free(r)
+        return off, ids[: int(off[-1])], int(lk[0])
+
     def match_lists(self, topics: Sequence[bytes], mode=MODE_ROUTES, threads=1, stride=256):
         buf, offs = pack(list(topics))
         counts, ids, _ = self.match_packed(buf, offs, mode, threads, stride)
@@ -143,3 +160,30 @@ class RetainScan:
         sums = np.zeros(max(n, 1), dtype=np.uint64)
         lib().orr_select(self.h, _p(buf), _p(offs), n, now, threads, _p(counts), _p(sums))
         return counts[:n], sums[:n]
+
+
+def csr_mismatches(off_g, ids_g, off_o, ids_o):
+    """Topics whose GPU match set differs from the oracle's (sorted filter-id
+    sets per topic).  off_*: (n+1,) offsets, ids_*: the CSR ids; the oracle's ids are sorted
+    per topic already, the GPU's are in any order.  Returns the sorted mismatching topic
+    indices (empty array = bit-exact)."""
+    off_g = np.asarray(off_g).astype(np.int64)
+    off_o = np.asarray(off_o).astype(np.int64)
+    n = len(off_o) - 1
+    cg, co = np.diff(off_g), np.diff(off_o)
+    bad = cg != co
+    same = ~bad
+    if int(off_g[-1] - off_g[0]) and same.any():
+        ids_g = np.asarray(ids_g)[off_g[0]:off_g[-1]].astype(np.uint32).astype(np.int64)
+        tg = np.repeat(np.arange(n, dtype=np.int64), cg)
+        kg = np.sort((tg << 32) | ids_g)
+        keep_g = same[kg >> 32]
+        ids_o = np.asarray(ids_o)[: off_o[-1]].astype(np.uint32).astype(np.int64)
+        to_ = np.repeat(np.arange(n, dtype=np.int64), co)
+        ko = (to_ << 32) | ids_o
+        ko = ko[same[to_]]
+        kg = kg[keep_g]
+        diff = kg != ko
+        if diff.any():
+            bad[np.unique(kg[diff] >> 32)] = True
+    return np.nonzero(bad)[0]

@@ -367,6 +367,72 @@ uint64_t orc_match(void* h, const uint8_t* bytes, const uint64_t* offs, uint64_t
   return total_lk.load();
 }
 
+// orc_match as a CSR (no per-topic stride): each thread matches a contiguous slice of the
+// topics into its own id list; out_off[n+1] receives the offsets; the concatenated sorted ids
+// stay in the returned result until orc_csr_copy / orc_csr_free.  *lookups = total lookups.
+struct CsrResult {
+  std::vector<std::vector<uint32_t>> parts;
+  uint64_t total = 0;
+};
+
+void* orc_match_csr(void* h, const uint8_t* bytes, const uint64_t* offs, uint64_t n, int mode, int nthreads,
+                    uint64_t* out_off, uint64_t* lookups) {
+  auto* o = static_cast<Oracle*>(h);
+  o->trie.freeze();
+  if (nthreads < 1) nthreads = 1;
+  auto* res = new CsrResult();
+  std::vector<uint32_t> counts(n ? n : 1);
+  const uint64_t chunk = (n + nthreads - 1) / std::max<uint64_t>(nthreads, 1);
+  const int parts = n ? static_cast<int>((n + chunk - 1) / chunk) : 0;
+  res->parts.resize(parts);
+  std::atomic<uint64_t> total_lk{0};
+  auto work = [&](int k) {
+    const uint64_t lo = k * chunk, hi = std::min<uint64_t>(n, lo + chunk);
+    std::vector<std::string> acc;
+    std::vector<uint32_t> out;
+    auto& dst = res->parts[k];
+    uint64_t lk = 0;
+    for (uint64_t t = lo; t < hi; ++t) {
+      const char* p = reinterpret_cast<const char*>(bytes + offs[t]);
+      size_t len = offs[t + 1] - offs[t];
+      acc.clear();
+      if (!(mode == 0 && o->trie.empty())) o->trie.match(p, len, acc, lk);
+      out.clear();
+      if (mode == 0) {
+        auto it = o->ids.find(std::string(p, len));
+        if (it != o->ids.end() && o->live[it->second]) out.push_back(it->second);
+      }
+      for (auto& f : acc) {
+        auto it = o->ids.find(f);
+        if (it != o->ids.end() && o->live[it->second]) out.push_back(it->second);
+      }
+      std::sort(out.begin(), out.end());
+      out.erase(std::unique(out.begin(), out.end()), out.end());
+      counts[t] = static_cast<uint32_t>(out.size());
+      dst.insert(dst.end(), out.begin(), out.end());
+    }
+    total_lk += lk;
+  };
+  std::vector<std::thread> th;
+  for (int k = 0; k < parts; ++k) th.emplace_back(work, k);
+  for (auto& x : th) x.join();
+  out_off[0] = 0;
+  for (uint64_t t = 0; t < n; ++t) out_off[t + 1] = out_off[t] + counts[t];
+  res->total = n ? out_off[n] : 0;
+  if (lookups) *lookups = total_lk.load();
+  return res;
+}
+
+void orc_csr_copy(void* r, uint32_t* dst) {
+  auto* res = static_cast<CsrResult*>(r);
+  for (auto& p : res->parts) {
+    if (!p.empty()) std::memcpy(dst, p.data(), p.size() * sizeof(uint32_t));
+    dst += p.size();
+  }
+}
+
+void orc_csr_free(void* r) { delete static_cast<CsrResult*>(r); }
+
 // evals(T) per SURVEY §8(d) over ALL live filters (exact and wildcard).
 void orc_evals(void* h, const uint8_t* bytes, const uint64_t* offs, uint64_t n, uint64_t* out) {
   auto* o = static_cast<Oracle*>(h);

@@ -189,6 +189,26 @@ def test_config_b_reduced(Engine):
     assert e.stats()["last_evals"] == int(o.evals_packed(*b.topics).sum())
 
 
+def test_config_b_full_table(Engine):
+    """The headline table itself (BASELINE configs[1]): all 10M config-B filters (seed 2, the
+    bench's table), 20K topics of config B's generator, every topic compared ID-for-ID with the oracle (routes mode and
+    the router's wildcard-only trie)."""
+    from emqx_amd import workloads as W
+    b = W.config_b(n_filters=10_000_000, n_topics=20_000)
+    e = Engine()
+    e.insert_packed(*b.filters)
+    e.commit()
+    o = C.CppOracle(True)  # the router's layout: wildcard filters in the trie
+    o.add_packed(*b.filters)
+    # routes (exact ∪ trie) and the router's wildcard-only trie (oracle mode 1 on that trie)
+    for mode, omode in ((0, C.MODE_ROUTES), (2, C.MODE_TRIE)):
+        off, ids = e.match_packed(*b.topics, mode=mode)
+        off_o, ids_o, _ = o.match_csr(*b.topics, mode=omode, threads=8)
+        bad = C.csr_mismatches(off, ids, off_o, ids_o)
+        assert bad.size == 0, (mode, bad[:10])
+        assert int(off_o[-1]) > 5 * len(off_o)
+
+
 def test_config_d_reduced(Engine):
     from emqx_amd import workloads as W
     d = W.config_d(n_filters=30_000, n_topics=3000)
