@@ -99,7 +99,9 @@ def main():
                          "of subscription filters against 1M stored retained topics")
     ap.add_argument("--retained", type=int, default=1_000_000, help="--workload R: stored retained topics")
     ap.add_argument("--churn", type=int, default=10_000, help="--workload U: inserts and deletes per commit")
-    ap.add_argument("--rounds", type=int, default=10, help="--workload U: commits timed")
+    ap.add_argument("--with-matches", action="store_true",
+                    help="--workload U: a 1M-topic match in flight on a second stream during every commit")
+    ap.add_argument("--rounds", type=int, default=50, help="--workload U: commits timed")
     ap.add_argument("--strategy", type=str, default="hash_clientid",
                     help="$share strategy for --workload E")
     ap.add_argument("--sharded", action="store_true",
@@ -597,10 +599,13 @@ def update_bench(args, rank, world, dev):
     """Route updates (emqx_router:do_add_route/do_delete_route ->
     emqx_trie:insert/delete in a mria transaction, emqx_router_utils.erl:33-70): on config B's
     10M-filter table, each step unsubscribes `churn` random live filters, subscribes `churn`
-    new ones and commits (incremental: base-slot flag flips + a rebuilt delta trie).  value =
+    new ones and commits (incremental: flag flips for the deletes, the new filters patched into
+    the committed table in place, emqx_amd/csrc/live_trie.cpp).  value =
     (inserts + deletes) / (time of the ops and their commits).  After the last commit the batch
-    is matched with the delta present and again after a full rebuild: the two CSRs must be
-    identical (ids sorted per topic), and both throughputs are reported."""
+    is matched on the patched table and again after a full rebuild: the two CSRs must be
+    identical (ids sorted per topic), and both throughputs are reported.  --with-matches keeps
+    a 1M-topic match call in flight on a second stream during every commit (commits no longer
+    drain the device)."""
     import torch
     import torch.distributed as dist
     from emqx_amd import workloads as W
@@ -620,11 +625,28 @@ def update_bench(args, rank, world, dev):
     live = np.ones(nb, dtype=bool)
     nxt = nb
 
+    side = None
+    if args.with_matches:  # a match call in flight on another stream during each commit
+        side_stream = torch.cuda.Stream(device=dev)
+        stb = torch.from_numpy(wl.topics[0]).to(dev)
+        sto = torch.from_numpy(wl.topics[1].view(np.int64)).to(dev)
+        sn = wl.n_topics
+        soff = torch.empty(sn + 1, dtype=torch.int64, device=dev)
+        scap = max(64 * sn, 1 << 20)
+        sids = torch.empty(scap, dtype=torch.int32, device=dev)
+        ssum = torch.zeros(eng.SUMMARY_WORDS, dtype=torch.int64, device=dev)
+        eng.match_device(stb.data_ptr(), sto.data_ptr(), sn, soff.data_ptr(), sids.data_ptr(), scap, mode=0,
+                         stream=side_stream.cuda_stream)
+        side = lambda: eng.match_device_async(stb.data_ptr(), sto.data_ptr(), sn, soff.data_ptr(), sids.data_ptr(),
+                                              scap, ssum.data_ptr(), mode=0, stream=side_stream.cuda_stream)
+
     def churn_once():
         nonlocal nxt
         dels = np.sort(rng.choice(np.nonzero(live)[0], k, replace=False)).astype(np.uint32)
         adds = W.take(wl.filters, np.arange(nxt, nxt + k))
         nxt += k
+        if side is not None:
+            side()
         t = time.perf_counter()
         eng.delete(dels)
         ids = eng.insert_packed(*adds)
@@ -633,16 +655,19 @@ def update_bench(args, rank, world, dev):
         live[dels[dels < nb]] = False
         return dt, ids
 
-    churn_once()  # warm-up commit (first delta region)
+    churn_once()  # warm-up commit
     if world > 1:
         dist.barrier()
-    times, kinds, commit_ms = [], [], []
-    for _ in range(R):
+    times, kinds, commit_ms, cst = [], [], [], []
+    for r in range(R):
         dt, _ = churn_once()
         st = eng.stats()
         times.append(dt)
         kinds.append(st["last_commit_kind"])
         commit_ms.append(st["last_build_ms"])
+        cst.append(eng.commit_stats())
+        if r % 10 == 9:
+            log(f"[rank {rank}] commit {r + 1}/{R}: {dt * 1e3:.1f} ms ({cst[-1]})")
     elapsed = float(np.sum(times))
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -676,13 +701,14 @@ def update_bench(args, rank, world, dev):
         key = np.sort(topic << 32 | ids)  # per-topic sorted id sets, as one array
         return rate, eng.stats()["last_kernel_ms"], off, key
 
+    torch.cuda.synchronize()
     rate_delta, kms_delta, off_d, key_d = match_rate()
     eng.set_tuning("incremental", 0)
     eng.commit()
     rebuild_ms = eng.stats()["last_build_ms"]
     rate_full, kms_full, off_f, key_f = match_rate()
     if not (np.array_equal(off_d, off_f) and np.array_equal(key_d, key_f)):
-        raise SystemExit("match CSR with the delta trie differs from the one after a full rebuild")
+        raise SystemExit("match CSR of the patched table differs from the one after a full rebuild")
 
     value = 2.0 * k * R * world / elapsed
     result = {
@@ -702,14 +728,23 @@ def update_bench(args, rank, world, dev):
                    "n_filters": nb, "churn_per_commit": k, "commits": R,
                    "parallelism": f"replicated table x{world} (each rank commits its own copy)"},
         "commit_ms_avg": round(float(np.mean(commit_ms)), 3),
+        "commit_ms_p50": round(float(np.median(commit_ms)), 3),
         "commit_ms_max": round(float(np.max(commit_ms)), 3),
+        "commit_ms_first5": round(float(np.mean(commit_ms[:5])), 3),
+        "commit_ms_last5": round(float(np.mean(commit_ms[-5:])), 3),
+        "step_ms_first5": round(1e3 * float(np.mean(times[:5])), 3),
+        "step_ms_last5": round(1e3 * float(np.mean(times[-5:])), 3),
+        "per_commit": {k: round(float(np.mean([c[k] for c in cst])), 1)
+                       for k in ("relocations", "in_place", "patches", "new_slots")},
+        "spare_used_at_end": cst[-1]["spare_used"], "spare_cap": cst[-1]["spare_cap"],
         "full_rebuild_ms": round(min(full_ms, rebuild_ms), 1),
-        "delta_filters_at_end": delta_filters,
-        "match_topics_per_s_with_delta": round(rate_delta, 1),
+        "filters_patched_in_since_build": delta_filters,
+        "match_topics_per_s_after_patches": round(rate_delta, 1),
         "match_topics_per_s_after_rebuild": round(rate_full, 1),
-        "kernel_ms_with_delta": round(kms_delta, 4),
+        "kernel_ms_after_patches": round(kms_delta, 4),
         "kernel_ms_after_rebuild": round(kms_full, 4),
-        "parity": "CSR with delta == CSR after full rebuild (per-topic sorted ids)",
+        "matches_in_flight_during_commits": bool(args.with_matches),
+        "parity": "CSR of the patched table == CSR after a full rebuild (per-topic sorted ids)",
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = update_cpu_baseline(wl, nb, k, args)
@@ -850,18 +885,19 @@ def retain_bench(args, rank, world, dev):
 
 def update_cpu_baseline(wl, nb, k, args):
     """emqx_trie:insert/delete (refcounted TOPIC/PREFIX keys in one ordered key set,
-    oracle/trie_oracle.cpp) for the same churn, one thread: a bounded number of rounds on a
-    table of the first min(nb, 2M) base filters (the ordered-set cost grows with log N)."""
+    oracle/trie_oracle.cpp) for the same churn on the same base table, one writer thread (the
+    reference serialises each route change in a mria transaction; one ordered set takes one
+    writer at a time): rounds of `k` deletes + `k` inserts for about 10 s."""
     from emqx_amd import workloads as W
     from oracle import cpp as C
-    nbase = min(nb, 2_000_000)
     o = C.CppOracle(True)
-    o.add_packed(*W.take(wl.filters, np.arange(nbase)))
+    with progress("update baseline: building the oracle table"):
+        o.add_packed(*W.take(wl.filters, np.arange(nb)))
     rng = np.random.default_rng(11)
     pool = wl.n_filters - k
     t_total, ops, r = 0.0, 0, 0
-    while t_total < 10.0 and r < 20:
-        dels = W.unpack(wl.filters, rng.choice(nbase, k, replace=False))
+    while t_total < 10.0 and r < 50:
+        dels = W.unpack(wl.filters, rng.choice(nb, k, replace=False))
         adds = W.take(wl.filters, np.arange(pool, pool + k))
         t = time.perf_counter()
         o.delete(dels)
@@ -872,8 +908,8 @@ def update_cpu_baseline(wl, nb, k, args):
         ops += 2 * k
         r += 1
     return {"value": round(ops / t_total, 1), "unit": "updates/s", "cores": 1, "kind": "port",
-            "sample": f"{r} rounds of {k} deletes + {k} inserts on a {nbase}-filter table (C++ restatement "
-                      "of emqx_trie:insert/delete key maintenance, no mnesia transaction)"}
+            "sample": f"{r} rounds of {k} deletes + {k} inserts on the same {nb}-filter table (C++ restatement "
+                      "of emqx_trie:insert/delete key maintenance, no mnesia transaction, one writer)"}
 
 
 def reorder_topics(wl, order):

@@ -36,6 +36,8 @@ EXPORTS = (
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
     "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
+    "emqx_commit_stats", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
+    "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check",
 )
 # Every symbol include/emqx_retain.h declares (retained-message index).
 RETAIN_EXPORTS = (
@@ -147,6 +149,14 @@ def lib():
         "emqx_retain_match_batch_device": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64,
                                                  ctypes.POINTER(u64), vp]),
         "emqx_retain_stats_get": (i32, [vp, ctypes.POINTER(RetainStats)]),
+        "emqx_commit_stats": (i32, [vp, vp, u32]),
+        "emqx_htrie_create": (i32, [u64, ctypes.POINTER(vp)]),
+        "emqx_htrie_destroy": (i32, [vp]),
+        "emqx_htrie_insert": (i32, [vp, vp, vp, u64, vp]),
+        "emqx_htrie_delete": (i32, [vp, vp, u64]),
+        "emqx_htrie_commit": (i32, [vp, i32, vp]),
+        "emqx_htrie_match": (i32, [vp, u32, vp, vp, u64, vp, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_htrie_check": (i32, [vp, ctypes.c_char_p, u64]),
         "emqx_strerror": (ctypes.c_char_p, [i32]),
         "emqx_version": (ctypes.c_char_p, []),
     }

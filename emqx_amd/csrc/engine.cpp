@@ -1,5 +1,6 @@
-// C ABI implementation (include/emqx_match.h): filter store, full and incremental commits
-// with an RCU-style snapshot swap, per-call workspaces, and the match pipeline
+// C ABI implementation (include/emqx_match.h): filter store, full commits with an RCU-style
+// snapshot swap, incremental commits patched into the committed table (live_trie.cpp),
+// per-call workspaces, and the match pipeline
 //   fast kernel -> deep kernel -> group reduce -> scatter -> summary (one sync per call).
 #include <hip/hip_runtime.h>
 
@@ -46,10 +47,10 @@ hipError_t dalloc(T*& p, uint64_t count) {
   return hipMalloc(reinterpret_cast<void**>(&p), std::max<uint64_t>(count, 1) * sizeof(T));
 }
 
-// Device buffers of one full build, with headroom for incremental commits: two delta-trie
-// regions behind the base slots (alternating per commit), vocab slots to fill, arena bytes to
-// append.  Shared by every snapshot published from that build; freed (after draining the
-// device: an async call may still read it) when the last one goes.
+// Device buffers of one full build, with headroom for incremental commits: a spare slot
+// region behind the built slots (new nodes and relocated arrays), vocab slots to fill, arena
+// bytes to append.  Shared by every snapshot published from that build; freed (after draining
+// the device: an async call may still read it) when the last one goes.
 struct DeviceTables {
   int device = 0;
   EdgeSlot* edges = nullptr;  // cap_slots
@@ -73,36 +74,32 @@ struct DeviceTables {
   }
 };
 
-// Lease on one delta region: a snapshot holds it while its walks may read the region; a
-// delta commit rewrites a region only when no snapshot but the writer's holds it.
-struct RegionLease {};
-
 struct Snapshot {
   std::shared_ptr<DeviceTables> dt;
-  std::shared_ptr<RegionLease> region;  // the delta region tv.delta_* points into (or null)
   TableView tv{};
   uint64_t n_nodes = 0, n_slots = 0, n_words = 0, bytes = 0;
   uint32_t max_depth = 0;
 };
 
-// Writer-side state of incremental commits (under emqx_engine::writer).  A filter is either
-// in the base trie (fixed at the last full build; deleting / re-inserting it flips its meta
-// flag in place) or in the delta trie (filters created after the build, rebuilt on every
-// commit into the delta region not in use).
-struct DeltaState {
+// Writer-side state of incremental commits (under emqx_engine::writer): the host image of
+// the committed table, patched per commit (tables.h LiveTrie), and the device buffers the
+// commit writes through.
+struct LiveState {
   bool valid = false;
   std::shared_ptr<DeviceTables> dt;
   std::unique_ptr<VocabState> vocab;
-  uint64_t base_slots = 0, region_slots = 0, base_n_ids = 0, base_nodes = 0, base_live = 0;
-  uint32_t base_depth = 0;
-  std::vector<uint64_t> loc;    // per id < base_n_ids: FIDLOC of its filter in the base
-  std::vector<uint8_t> on;      // ... whose flag is set on the device
-  std::vector<uint8_t> cand_flag;
-  std::vector<uint32_t> cand;   // ids that may live in the delta trie
-  std::shared_ptr<RegionLease> lease[2];
-  int next_region = 0;
-  uint32_t root_meta = 0;       // the base root's meta, '#' flag included
-  uint64_t delta_filters = 0;
+  std::unique_ptr<LiveTrie> lt;
+  uint64_t inserted = 0;        // filters placed by incremental commits since the full build
+  hipStream_t stream = nullptr; // commit stream (uploads + patch kernels; synchronised alone)
+  SlotPatch* d_patch = nullptr;
+  uint64_t cap_patch = 0;
+  std::vector<SlotPatch> patches;
+  int device = 0;
+  ~LiveState() {
+    (void)hipSetDevice(device);
+    if (d_patch) (void)hipFree(d_patch);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
 };
 
 struct Workspace {
@@ -187,12 +184,13 @@ struct emqx_engine {
   std::atomic<bool> diag_on{false};
   std::atomic<uint32_t> slab_hint{256};  // largest slab per tile any workspace needed
   // incremental commits (under `writer`)
-  DeltaState ds;
+  LiveState ls;
   std::vector<uint32_t> dirty;  // ids inserted / deleted since the last commit
   bool incremental = true;      // emqx_set_tuning("incremental", 0|1)
-  int64_t delta_max = -1;       // emqx_set_tuning("delta_max", n): delta filters before a full
-                                // rebuild (-1: max(min(65536, base / 4), base / 16))
+  int64_t delta_max = -1;       // emqx_set_tuning("delta_max", n): filters placed by incremental
+                                // commits before a full rebuild (-1: until the spare region is full)
   uint64_t last_commit_kind = 0;
+  uint64_t last_relocations = 0, last_in_place = 0, last_patches = 0, last_new_slots = 0;
 };
 
 namespace {
@@ -204,14 +202,17 @@ void publish(emqx_engine* e, std::shared_ptr<Snapshot> s) {
   e->snap = std::move(s);  // the old snapshot goes when its last reader returns
 }
 
-// Full rebuild: every live filter into a fresh base trie, uploaded into new device tables
-// with delta headroom; the old tables stay alive until their last reader returns.
+// Full rebuild: every live filter into a fresh trie, uploaded into new device tables with a
+// spare region for incremental commits; the old tables stay alive until their last reader
+// returns.  The host keeps the build's image for incremental commits (LiveTrie::adopt).
 int full_commit(emqx_engine* e) {
   auto vs = std::make_unique<VocabState>();
   std::vector<uint64_t> loc;
+  std::vector<uint32_t> slot_ids;
   BuildOpts o;
   o.vocab = vs.get();
   o.fid_loc = &loc;
+  o.slot_ids = &slot_ids;
   HostTables ht;
   std::string err;
   if (!build_tables(e->store, o, ht, &err)) {
@@ -219,10 +220,10 @@ int full_commit(emqx_engine* e) {
     return EMQX_ENOMEM;
   }
   const uint64_t n_slots = ht.edges.size();
-  const uint64_t region = std::max<uint64_t>(1u << 16, n_slots / 8);
+  const uint64_t spare = std::min<uint64_t>(std::max<uint64_t>(1u << 20, n_slots / 2), MAX_SLOTS - n_slots);
   auto dt = std::make_shared<DeviceTables>();
   dt->device = e->device;
-  dt->cap_slots = std::min<uint64_t>(n_slots + 2 * region, MAX_SLOTS);
+  dt->cap_slots = n_slots + spare;
   dt->n_vocab = ht.vocab.size();
   dt->cap_arena = ht.arena.size() + std::max<uint64_t>(1u << 20, ht.arena.size() / 4) + 16;
   HIP_TRY(dalloc(dt->edges, dt->cap_slots));
@@ -253,115 +254,72 @@ int full_commit(emqx_engine* e) {
   s->max_depth = ht.max_depth;
   s->bytes = dt->bytes();
 
-  DeltaState& d = e->ds;
-  d.valid = dt->cap_slots == n_slots + 2 * region;
+  LiveState& d = e->ls;
+  d.device = e->device;
   d.dt = dt;
   d.vocab = std::move(vs);
-  d.base_slots = n_slots;
-  d.region_slots = region;
-  d.base_n_ids = e->store.n_ids();
-  d.base_live = e->store.n_live;
-  d.base_nodes = ht.n_nodes;
-  d.base_depth = ht.max_depth;
-  d.loc = std::move(loc);
-  d.on.assign(d.base_n_ids, 0);
-  for (uint64_t id = 0; id < d.base_n_ids; ++id) d.on[id] = d.loc[id] != FIDLOC_NONE;
-  d.cand_flag.assign(d.base_n_ids, 0);
-  d.cand.clear();
-  d.lease[0] = std::make_shared<RegionLease>();
-  d.lease[1] = std::make_shared<RegionLease>();
-  d.next_region = 0;
-  d.root_meta = ht.root_meta;
-  d.delta_filters = 0;
+  if (!d.lt) d.lt = std::make_unique<LiveTrie>();
+  d.lt->adopt(ht, loc, slot_ids, spare, d.vocab.get());
+  d.valid = true;
+  d.inserted = 0;
   e->dirty.clear();
   publish(e, std::move(s));
   e->last_commit_kind = 0;
   return EMQX_OK;
 }
 
-// Incremental commit: flips the meta flags of base filters deleted / re-inserted since the
-// last commit and rebuilds the (small) delta trie of the filters created since the last full
-// build into the delta region no reader holds.  EMQX_NEED_FULL when the delta outgrows its
-// region, the vocab or the arena headroom, or e->delta_max.
-int delta_commit(emqx_engine* e) {
-  DeltaState& d = e->ds;
+// Incremental commit: the filters inserted / deleted since the last commit are patched into
+// the committed table (LiveTrie::apply), then the device gets the new spare-region slots and
+// the rewritten existing slots on the commit stream, which alone is synchronised.  A walk that
+// overlaps the commit sees each filter of it present or absent.  EMQX_NEED_FULL when the spare
+// region, the vocab or the arena headroom runs out, or e->delta_max is reached.
+int live_commit(emqx_engine* e) {
+  LiveState& d = e->ls;
+  LiveTrie& lt = *d.lt;
   const FilterStore& fs = e->store;
-  const uint64_t n_ids = fs.n_ids();
-  if (d.cand_flag.size() < n_ids) d.cand_flag.resize(n_ids, 0);
-  std::vector<uint2> patches;
-  uint32_t root_meta = d.root_meta;
-  std::vector<uint8_t> base_on = d.on;  // staged: committed only on success
-  for (uint32_t id : e->dirty) {
-    if (id < d.base_n_ids && d.loc[id] != FIDLOC_NONE) {
-      const uint8_t want = fs.live[id];
-      if (want == base_on[id]) continue;
-      base_on[id] = want;
-      const uint64_t l = d.loc[id];
-      if (l == FIDLOC_ROOT_HASH) {
-        root_meta = want ? (root_meta | META_HAS_HASH) : (root_meta & ~META_HAS_HASH);
-        continue;
-      }
-      const uint32_t bit = (l & 3) == FIDLOC_HASH ? META_HAS_HASH : META_HAS_TERM;
-      patches.push_back(make_uint2(static_cast<uint32_t>(l >> 2), bit | (want ? 0u : META_PATCH_CLEAR)));
-    } else if (!d.cand_flag[id]) {
-      d.cand_flag[id] = 1;
-      d.cand.push_back(id);
-    }
-  }
-  std::vector<uint32_t> ids;
-  for (uint32_t id : d.cand)
-    if (fs.live[id]) ids.push_back(id);
-  // default: a quarter of the base up to 64k filters, 1/16 of it beyond (an empty base always
-  // takes a full build: walks then start at one root)
-  const uint64_t cap = e->delta_max >= 0
-                           ? static_cast<uint64_t>(e->delta_max)
-                           : std::max<uint64_t>(std::min<uint64_t>(65536, d.base_live / 4), d.base_live / 16);
-  if (ids.size() > cap) return EMQX_NEED_FULL;
+  std::vector<uint32_t> ids(e->dirty);
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  uint64_t creates = 0;
+  for (uint32_t id : ids)
+    if (fs.live[id] && (id >= lt.loc.size() || lt.loc[id] == FIDLOC_NONE)) ++creates;
+  if (e->delta_max >= 0 && d.inserted + creates > static_cast<uint64_t>(e->delta_max)) return EMQX_NEED_FULL;
 
-  // the delta trie, into the region no published snapshot but the current one may hold
-  const int r = d.next_region;
+  lt.begin_commit();
   const uint64_t nw0 = d.vocab->n_words(), arena0 = d.vocab->arena.size();
-  HostTables dh;
-  if (!ids.empty()) {
-    BuildOpts o;
-    o.ids = &ids;
-    o.slot_offset = d.base_slots + r * d.region_slots;
-    o.vocab = d.vocab.get();
-    o.vocab_table = false;
-    std::string err;
-    if (!build_tables(fs, o, dh, &err) || dh.edges.size() > d.region_slots) return EMQX_NEED_FULL;
-  }
+  for (uint32_t id : ids)
+    if (!lt.apply(fs, id)) return EMQX_NEED_FULL;  // spare region exhausted: the host image is
+                                                   // rebuilt with the tables
   std::vector<uint32_t> vdirty;
   if (!d.vocab->insert_table(nw0, &vdirty) || d.vocab->arena.size() + 16 > d.dt->cap_arena) return EMQX_NEED_FULL;
+  lt.patches(d.patches);
 
-  // readers of region r (snapshots two commits old) must be gone, and their device work:
-  // drain the device, drop the async-call references idle workspaces keep, wait for the rest
-  HIP_TRY(hipDeviceSynchronize());
-  {
-    std::lock_guard<std::mutex> g(e->ws_mu);
-    for (Workspace* w : e->free_ws) w->inflight.reset();
-  }
-  while (d.lease[r].use_count() > 1) std::this_thread::yield();
-  HIP_TRY(hipDeviceSynchronize());
-  if (!ids.empty()) {
-    const uint64_t at = d.base_slots + r * d.region_slots;
-    HIP_TRY(hipMemcpy(d.dt->edges + at, dh.edges.data(), dh.edges.size() * sizeof(EdgeSlot), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d.dt->fids + 2 * at, dh.fids.data(), dh.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipSetDevice(e->device));
+  if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  hipStream_t st = d.stream;
+  const uint64_t a0 = lt.mark, a1 = lt.used;
+  if (a1 > a0) {
+    HIP_TRY(hipMemcpyAsync(d.dt->edges + a0, lt.edges.data() + a0, (a1 - a0) * sizeof(EdgeSlot),
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d.dt->fids + 2 * a0, lt.fids.data() + 2 * a0, 2 * (a1 - a0) * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, st));
   }
   if (d.vocab->arena.size() > arena0)
-    HIP_TRY(hipMemcpy(d.dt->arena + arena0, d.vocab->arena.data() + arena0, d.vocab->arena.size() - arena0,
-                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(d.dt->arena + arena0, d.vocab->arena.data() + arena0, d.vocab->arena.size() - arena0,
+                           hipMemcpyHostToDevice, st));
   for (uint32_t v : vdirty)
-    HIP_TRY(hipMemcpy(d.dt->vocab + v, &d.vocab->table[v], sizeof(VocabSlot), hipMemcpyHostToDevice));
-  if (!patches.empty()) {
-    uint2* dp = nullptr;
-    HIP_TRY(dalloc(dp, patches.size()));
-    HIP_TRY(hipMemcpy(dp, patches.data(), patches.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    HIP_TRY(launch_meta_patches(d.dt->edges, dp, static_cast<uint32_t>(patches.size()), nullptr));
-    HIP_TRY(hipDeviceSynchronize());
-    dfree(dp);
+    HIP_TRY(hipMemcpyAsync(d.dt->vocab + v, &d.vocab->table[v], sizeof(VocabSlot), hipMemcpyHostToDevice, st));
+  const uint64_t np = d.patches.size();
+  if (np) {
+    if (np > d.cap_patch) {
+      HIP_TRY(hipStreamSynchronize(st));
+      d.cap_patch = round_pow2(np);
+      HIP_TRY(dalloc(d.d_patch, d.cap_patch));
+    }
+    HIP_TRY(hipMemcpyAsync(d.d_patch, d.patches.data(), np * sizeof(SlotPatch), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_slot_patches(d.dt->edges, d.dt->fids, d.d_patch, static_cast<uint32_t>(np), st));
   }
-  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipStreamSynchronize(st));
 
   std::shared_ptr<Snapshot> cur;
   {
@@ -369,26 +327,18 @@ int delta_commit(emqx_engine* e) {
     cur = e->snap;
   }
   auto s = std::make_shared<Snapshot>(*cur);
-  s->tv.root_meta = root_meta;
-  if (ids.empty()) {
-    s->region = nullptr;
-    s->tv.delta_base = 0;
-    s->tv.delta_meta = 0;
-    s->tv.delta_hash_fid = FID_NONE;
-  } else {
-    s->region = d.lease[r];
-    s->tv.delta_base = dh.root_base;
-    s->tv.delta_meta = dh.root_meta;
-    s->tv.delta_hash_fid = dh.root_hash_fid;
-  }
-  s->n_nodes = d.base_nodes + (ids.empty() ? 0 : dh.n_nodes);
-  s->n_slots = d.base_slots + dh.edges.size();
+  s->tv.root_base = lt.root_base;
+  s->tv.root_meta = lt.root_meta;
+  s->tv.root_hash_fid = lt.root_hash_fid;
+  s->n_nodes = lt.n_nodes;
+  s->n_slots = lt.used;
   s->n_words = d.vocab->n_words();
-  s->max_depth = std::max(d.base_depth, dh.max_depth);
-  d.on.swap(base_on);
-  d.root_meta = root_meta;
-  d.delta_filters = ids.size();
-  d.next_region = 1 - r;
+  s->max_depth = lt.max_depth;
+  d.inserted += creates;
+  e->last_relocations = lt.relocations;
+  e->last_in_place = lt.in_place;
+  e->last_patches = np;
+  e->last_new_slots = a1 - a0;
   e->dirty.clear();
   publish(e, std::move(s));
   e->last_commit_kind = 1;
@@ -398,7 +348,7 @@ int delta_commit(emqx_engine* e) {
 int commit_locked(emqx_engine* e) {
   auto t0 = std::chrono::steady_clock::now();
   int rc = EMQX_NEED_FULL;
-  if (e->incremental && e->ds.valid && e->snap) rc = delta_commit(e);
+  if (e->incremental && e->ls.valid && e->snap) rc = live_commit(e);
   if (rc == EMQX_NEED_FULL) rc = full_commit(e);
   if (rc != EMQX_OK) return rc;
   e->epoch += 1;
@@ -673,7 +623,7 @@ int emqx_insert_filters_ext(emqx_engine* e, const uint8_t* bytes, const uint64_t
   for (uint64_t i = 0; i < n; ++i) {
     bool created = false;
     const uint32_t id = e->store.insert(bytes + offsets[i], offsets[i + 1] - offsets[i], &created);
-    if (e->store.ext[id] != ext_ids[i]) e->ds.valid = false;  // a changed report id: rebuild
+    if (e->store.ext[id] != ext_ids[i]) e->ls.valid = false;  // a changed report id: rebuild
     e->store.ext[id] = ext_ids[i];
     e->dirty.push_back(id);
     if (ids_out) ids_out[i] = id;
@@ -835,7 +785,7 @@ int emqx_stats_get(emqx_engine* e, emqx_stats* out) {
     out->n_ids = e->store.n_ids();
     out->epoch = e->epoch;
     out->last_build_ms = e->last_build_ms;
-    out->delta_filters = e->ds.delta_filters;
+    out->delta_filters = e->ls.inserted;
     out->last_commit_kind = e->last_commit_kind;
   }
   auto s = current(e);
@@ -888,6 +838,16 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
     return EMQX_OK;
   }
   return EMQX_ENOTFOUND;
+}
+
+int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n) {
+  if (!e || (n && !out)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(e->writer);
+  const LiveTrie* lt = e->ls.lt.get();
+  const uint64_t v[8] = {e->last_commit_kind, e->last_relocations, e->last_in_place, e->last_patches,
+                         e->last_new_slots, lt ? lt->used : 0, lt ? lt->cap : 0, lt ? lt->garbage : 0};
+  for (uint32_t i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  return EMQX_OK;
 }
 
 int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset) {

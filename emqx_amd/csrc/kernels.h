@@ -126,9 +126,9 @@ hipError_t launch_match_deep(const MatchArgs& a, hipStream_t s);
 // group sums -> per-tile offsets + ids (fast path), the deep path's ids, then out_off[n]
 // and the call summary
 hipError_t launch_assemble(const MatchArgs& a, hipStream_t s);
-// incremental commits: patches[i] = {slot, meta bits (| META_PATCH_CLEAR to clear them)}
-constexpr uint32_t META_PATCH_CLEAR = 1u << 31;
-hipError_t launch_meta_patches(EdgeSlot* edges, const uint2* patches, uint32_t n, hipStream_t s);
+// incremental commits (live_trie.cpp): whole-slot rewrites of the committed table, ids first
+hipError_t launch_slot_patches(EdgeSlot* edges, uint32_t* fids, const SlotPatch* patches, uint32_t n,
+                               hipStream_t s);
 // counts[n] -> offsets[n+1] (exclusive); partials: scratch of >= scan_partials(n) u64
 // (fan-out's entry scan).
 uint64_t scan_partials(uint64_t n);

@@ -76,6 +76,16 @@ struct alignas(16) EdgeSlot {
 static_assert(sizeof(EdgeSlot) == 16, "EdgeSlot must be 16 bytes");
 constexpr uint64_t MAX_SLOTS = (1ull << 31) - 1;  // references 2i + kind fit 32 bits
 
+// One in-place rewrite of an existing slot by an incremental commit (live_trie.cpp): the
+// slot's new content and its two filter ids.
+struct alignas(16) SlotPatch {
+  uint32_t slot;
+  uint32_t fid_h, fid_t;
+  uint32_t pad;
+  EdgeSlot s;
+};
+static_assert(sizeof(SlotPatch) == 32, "SlotPatch must be 32 bytes");
+
 // 32-byte vocab slot; words up to 16 bytes are verified from `inl` without a second load.
 struct alignas(16) VocabSlot {
   uint32_t hash;   // word_hash_bytes() of the word

@@ -1,0 +1,548 @@
+// Incremental commits: the committed level trie patched in place (tables.h, LiveTrie).
+//
+// Reference semantics (paths relative to /root/reference): emqx_trie:insert/1 and delete/1
+// add / remove one filter's keys (apps/emqx/src/emqx_trie.erl:115-137), called per route
+// change inside a mria transaction (apps/emqx/src/emqx_router_utils.erl:33-70); a filter is
+// visible to match/1 as soon as its transaction commits.  Here a commit publishes a batch of
+// such changes, and its cost is proportional to that batch:
+//
+//   * delete / re-insert of a filter already in the trie: flip its META_HAS_HASH / _TERM flag
+//     in the slot that describes its node (the filter ids stay, so a revival is a flip too);
+//   * insert of a new filter: walk the host image of the trie like the kernel does; at the
+//     first missing edge, the rest of the filter becomes a chain of one-edge nodes in the spare
+//     region, and the missing edge is placed into the existing node if that node's hashing has
+//     a free slot for it (perfect-hash slot, '+' slot 0, or a free slot of its primary /
+//     secondary 2-slot bucket), otherwise the node is relocated: rebuilt with one more entry,
+//     with slack, into the spare region.  Then the slot that describes the node (in its
+//     parent's array, or the table view for the root) is re-encoded: literal filter, XFID /
+//     inline filter ids, hashing parameters.
+//
+// Device writes per commit: the new spare-region slots [mark, used) in one copy, plus one
+// whole 16-B slot store per rewritten existing slot (filter ids first, slots second), so a
+// walk that overlaps a commit sees each slot old or new, and each new filter absent or present.
+#include <algorithm>
+#include <cstring>
+
+#include "tables.h"
+
+namespace emqx {
+
+namespace {
+
+constexpr uint32_t STRUCT_BITS =
+    META_CAPLOG2_MASK | META_HAS_PLUS | META_HAS_EDGES | META_PH | (0xFFu << META_SEED_SHIFT);
+constexpr uint32_t FILTER_BITS = META_HAS_HASH | META_HAS_TERM | META_TERM_WILD;
+constexpr EdgeSlot EMPTY_SLOT{WID_NONE, 0, 0, 0};
+constexpr uint32_t LINE = 8;  // slots per 128-B line
+constexpr uint32_t FULL_LINE = 0xFFu;
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+uint32_t log2u(uint64_t p) {
+  uint32_t l = 0;
+  while ((1ull << l) < p) ++l;
+  return l;
+}
+
+struct Entry {
+  uint32_t wid;
+  EdgeSlot s;  // slot content without the position's META_BUCKET_OVF bit
+  uint32_t fh, ft, ih, it;
+};
+
+}  // namespace
+
+void LiveTrie::adopt(HostTables& ht, std::vector<uint64_t>& fid_loc, std::vector<uint32_t>& slot_ids,
+                     uint64_t spare, VocabState* v) {
+  const uint64_t n = ht.edges.size();
+  edges.swap(ht.edges);
+  fids.swap(ht.fids);
+  sid.swap(slot_ids);
+  cap = std::min<uint64_t>(n + spare, MAX_SLOTS);
+  edges.resize(cap, EMPTY_SLOT);
+  fids.resize(2 * cap, FID_NONE);
+  sid.resize(2 * cap, WID_NONE);
+  used = n;
+  garbage = 0;
+  line_used = FULL_LINE;
+  root_base = ht.root_base;
+  root_meta = ht.root_meta;
+  root_hash_fid = ht.root_hash_fid;
+  root_hash_id = WID_NONE;
+  for (uint64_t id = 0; id < fid_loc.size(); ++id)
+    if (fid_loc[id] == FIDLOC_ROOT_HASH) root_hash_id = static_cast<uint32_t>(id);
+  n_nodes = ht.n_nodes;
+  max_depth = ht.max_depth;
+  loc.swap(fid_loc);
+  vocab = v;
+  mark = used;
+  dirty.clear();
+}
+
+void LiveTrie::begin_commit() {
+  mark = used;
+  line_used = FULL_LINE;  // never allocate into a line the device already holds
+  dirty.clear();
+  relocations = in_place = chains = flips = 0;
+}
+
+void LiveTrie::touch(uint64_t slot) {
+  if (slot < mark) dirty.push_back(static_cast<uint32_t>(slot));
+}
+
+bool LiveTrie::alloc(uint32_t caplog, uint64_t* at) {
+  const uint64_t c = 1ull << caplog;
+  if (c >= LINE) {
+    const uint64_t a = (used + LINE - 1) & ~uint64_t(LINE - 1);
+    if (a + c > cap) return false;
+    used = a + c;
+    line_used = FULL_LINE;
+    *at = a;
+    return true;
+  }
+  const uint32_t want = (1u << c) - 1u;
+  for (uint32_t o = 0; o < LINE; o += static_cast<uint32_t>(c))
+    if (!(line_used & (want << o))) {
+      line_used |= want << o;
+      *at = line + o;
+      return true;
+    }
+  const uint64_t l = (used + LINE - 1) & ~uint64_t(LINE - 1);
+  if (l + LINE > cap) return false;
+  line = l;
+  used = l + LINE;
+  line_used = want;
+  *at = l;
+  return true;
+}
+
+// The node's literal words, summarised as the builder does (tables.cpp pass 4).  Wide
+// (bucketed) nodes are summarised as "many" (an all-ones filter: no false negatives).
+void LiveTrie::lit_summary(uint32_t base, uint32_t meta, uint32_t* n_lit, uint32_t* only, uint32_t* bloom,
+                           uint32_t* bloom8) const {
+  *n_lit = 0;
+  *only = WID_NONE;
+  *bloom = 0;
+  *bloom8 = 0;
+  if (!(meta & META_HAS_EDGES)) return;
+  if (!(meta & META_PH)) {
+    *n_lit = LITF_BLOOM_MAX + 1;
+    return;
+  }
+  const uint32_t c = 1u << (meta & META_CAPLOG2_MASK);
+  for (uint32_t i = 0; i < c; ++i) {
+    const uint32_t w = edges[base + i].wid;
+    if (w == WID_NONE || w == WID_PLUS) continue;
+    *n_lit += 1;
+    *only = w;
+    const uint32_t h = litf_hash(w);
+    *bloom |= (1u << (h & 31u)) | (1u << ((h >> 5) & 31u));
+    *bloom8 |= 1u << (h & 7u);
+  }
+}
+
+// The slot that leads to a node: its structure (smeta & STRUCT_BITS), its filters (fmeta &
+// FILTER_BITS, fid_h / fid_t present or FID_NONE) and its literal filter — encoded exactly as
+// write_slot / meta_of in tables.cpp do.
+EdgeSlot LiveTrie::encode(uint32_t wid, bool has_edges, uint32_t base, uint32_t smeta, uint32_t fid_h,
+                          uint32_t fid_t, uint32_t fmeta) const {
+  EdgeSlot r{wid, 0, 0, 0};
+  if (!has_edges) {  // edgeless child: filter ids inline
+    r.meta = (fmeta & FILTER_BITS) | META_LITF_NONE;
+    r.child_base = fid_h;
+    r.litf = fid_t;
+    return r;
+  }
+  smeta = (smeta & STRUCT_BITS) | META_HAS_EDGES;
+  uint32_t n_lit, only, bloom, bloom8;
+  lit_summary(base, smeta, &n_lit, &only, &bloom, &bloom8);
+  uint32_t lf = 0, lflag = 0;
+  if (n_lit == 0) {
+    lflag = META_LITF_NONE;
+  } else if (n_lit == 1) {
+    lflag = META_LITF_EXACT;
+    lf = only;
+  } else {
+    lf = n_lit <= LITF_BLOOM_MAX ? bloom : ~0u;
+  }
+  const bool h = fid_h != FID_NONE, t = fid_t != FID_NONE;
+  if (h != t) {
+    uint32_t f8 = 0;
+    if (lflag & META_LITF_EXACT) f8 = litf_hash(only) >> 24;
+    else if (!(lflag & META_LITF_NONE)) f8 = n_lit > LITF_BLOOM_MAX ? 0xFFu : bloom8;
+    lflag |= META_XFID | (t ? META_XFID_TERM : 0u) | (f8 << META_F8_SHIFT);
+    lf = t ? fid_t : fid_h;
+  }
+  r.child_base = base;
+  r.meta = smeta | (fmeta & FILTER_BITS) | lflag;
+  r.litf = lf;
+  return r;
+}
+
+// Re-encodes slot `p` from its current node structure and filter ids.
+void LiveTrie::reencode(uint64_t p) {
+  const EdgeSlot s = edges[p];
+  const bool he = (s.meta & META_HAS_EDGES) != 0;
+  EdgeSlot r = encode(s.wid, he, he ? s.child_base : 0, s.meta, fids[2 * p], fids[2 * p + 1], s.meta);
+  r.meta |= s.meta & META_BUCKET_OVF;
+  edges[p] = r;
+  touch(p);
+}
+
+// Points the node reached through `pslot` (or the root) at a new edge array / structure.
+void LiveTrie::set_node(bool root, uint64_t pslot, uint32_t base, uint32_t smeta) {
+  if (root) {
+    uint32_t n_lit, only, bloom, bloom8;
+    const uint32_t sm = (smeta & STRUCT_BITS) | META_HAS_EDGES;
+    lit_summary(base, sm, &n_lit, &only, &bloom, &bloom8);
+    root_base = base;
+    root_meta = sm | (root_meta & META_HAS_HASH) | (n_lit == 0 ? META_LITF_NONE : n_lit == 1 ? META_LITF_EXACT : 0u);
+    return;
+  }
+  const EdgeSlot s = edges[pslot];
+  EdgeSlot r = encode(s.wid, true, base, smeta, fids[2 * pslot], fids[2 * pslot + 1], s.meta);
+  r.meta |= s.meta & META_BUCKET_OVF;
+  edges[pslot] = r;
+  touch(pslot);
+}
+
+bool LiveTrie::find_child(uint32_t base, uint32_t meta, uint32_t wid, uint32_t* slot) const {
+  if (!(meta & META_HAS_EDGES)) return false;
+  if (wid == WID_PLUS) {
+    *slot = base;
+    return edges[base].wid == WID_PLUS;
+  }
+  const uint32_t mask = (1u << (meta & META_CAPLOG2_MASK)) - 1u;
+  const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
+  if (meta & META_PH) {
+    *slot = base + lit_slot(wid, sd, mask);
+    return edges[*slot].wid == wid;
+  }
+  const uint32_t nbm = mask >> 1, b1 = bucket1(wid, sd, nbm);
+  for (uint32_t k = 0; k < 2; ++k)
+    if (edges[base + 2 * b1 + k].wid == wid) {
+      *slot = base + 2 * b1 + k;
+      return true;
+    }
+  if (!(edges[base + 2 * b1].meta & META_BUCKET_OVF)) return false;
+  const uint32_t b2 = bucket2(wid, sd, nbm);
+  for (uint32_t k = 0; k < 2; ++k)
+    if (edges[base + 2 * b2 + k].wid == wid) {
+      *slot = base + 2 * b2 + k;
+      return true;
+    }
+  return false;
+}
+
+// Adds edge `wid` -> `child` (slot content; filter ids fh/ft, engine ids ih/it) to the node
+// reached through `pslot` (or the root): in place when its hashing has room, else relocated.
+bool LiveTrie::place(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
+                     uint32_t ih, uint32_t it) {
+  const uint32_t base = root ? root_base : edges[pslot].child_base;
+  uint32_t smeta = (root ? root_meta : edges[pslot].meta) & STRUCT_BITS;
+  if (!(smeta & META_HAS_EDGES)) return relocate(root, pslot, wid, child, fh, ft, ih, it);
+  const uint32_t mask = (1u << (smeta & META_CAPLOG2_MASK)) - 1u;
+  const uint32_t sd = (smeta >> META_SEED_SHIFT) & 255u;
+  uint64_t target = ~0ull, ovf = ~0ull;
+  if (wid == WID_PLUS) {
+    if (edges[base].wid == WID_NONE) {
+      target = base;
+      smeta |= META_HAS_PLUS;
+    }
+  } else if (smeta & META_PH) {
+    const uint32_t j = lit_slot(wid, sd, mask);
+    if (edges[base + j].wid == WID_NONE) target = base + j;
+  } else {
+    const uint32_t nbm = mask >> 1, b1 = bucket1(wid, sd, nbm), b2 = bucket2(wid, sd, nbm);
+    for (uint32_t k = 0; k < 2 && target == ~0ull; ++k)
+      if (edges[base + 2 * b1 + k].wid == WID_NONE) target = base + 2 * b1 + k;
+    for (uint32_t k = 0; k < 2 && target == ~0ull; ++k)
+      if (edges[base + 2 * b2 + k].wid == WID_NONE) {
+        target = base + 2 * b2 + k;
+        ovf = base + 2 * b1;
+      }
+  }
+  if (target == ~0ull) return relocate(root, pslot, wid, child, fh, ft, ih, it);
+  const uint32_t keep = edges[target].meta & META_BUCKET_OVF;
+  edges[target] = child;
+  edges[target].meta = (child.meta & ~META_BUCKET_OVF) | keep;
+  fids[2 * target] = fh;
+  fids[2 * target + 1] = ft;
+  sid[2 * target] = ih;
+  sid[2 * target + 1] = it;
+  if (ih != WID_NONE) loc[ih] = target << 2 | FIDLOC_HASH;
+  if (it != WID_NONE) loc[it] = target << 2 | FIDLOC_TERM;
+  touch(target);
+  if (ovf != ~0ull && !(edges[ovf].meta & META_BUCKET_OVF)) {
+    edges[ovf].meta |= META_BUCKET_OVF;
+    touch(ovf);
+  }
+  set_node(root, pslot, base, smeta);
+  in_place += 1;
+  return true;
+}
+
+// Rebuilds the node's edge array with the new entry into the spare region (perfect hash for
+// up to 32 literals, with 1.5x slack so later inserts usually fit in place; 2-slot buckets at
+// load <= 1/8 beyond), then points the node's slot at it.
+bool LiveTrie::relocate(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh,
+                        uint32_t ft, uint32_t ih, uint32_t it) {
+  const uint32_t obase = root ? root_base : edges[pslot].child_base;
+  const uint32_t ometa = (root ? root_meta : edges[pslot].meta) & STRUCT_BITS;
+  std::vector<Entry> ent;
+  uint32_t ocap = 0;
+  if (ometa & META_HAS_EDGES) {
+    ocap = 1u << (ometa & META_CAPLOG2_MASK);
+    for (uint32_t i = 0; i < ocap; ++i) {
+      const uint64_t p = obase + i;
+      const EdgeSlot& s = edges[p];
+      if (s.wid == WID_NONE) continue;
+      EdgeSlot c = s;
+      c.meta &= ~META_BUCKET_OVF;
+      ent.push_back({s.wid, c, fids[2 * p], fids[2 * p + 1], sid[2 * p], sid[2 * p + 1]});
+    }
+  }
+  EdgeSlot c = child;
+  c.meta &= ~META_BUCKET_OVF;
+  ent.push_back({wid, c, fh, ft, ih, it});
+  const uint32_t e = static_cast<uint32_t>(ent.size());
+  bool has_plus = false;
+  for (auto& x : ent) has_plus |= x.wid == WID_PLUS;
+  const uint32_t n_lit = e - (has_plus ? 1u : 0u);
+
+  uint32_t caplog = 0, seed = 0;
+  bool ph = false;
+  std::vector<uint32_t> pos(e, 0);
+  std::vector<uint32_t> used_pos;
+  if (n_lit <= 32) {
+    const uint64_t cap0 = next_pow2(std::max<uint64_t>(2, e + e / 2));
+    const uint64_t cap_max = next_pow2(std::max<uint64_t>(16, 8ull * e));
+    for (uint64_t c2 = cap0; c2 <= cap_max && !ph && log2u(c2) <= PH_MAX_CAPLOG; c2 <<= 1) {
+      const uint32_t mask = static_cast<uint32_t>(c2 - 1);
+      for (uint32_t sd = 0; sd < 256 && !ph; ++sd) {
+        used_pos.clear();
+        bool ok = true;
+        for (uint32_t k = 0; k < e && ok; ++k) {
+          if (ent[k].wid == WID_PLUS) {
+            pos[k] = 0;
+            continue;
+          }
+          const uint32_t sl = lit_slot(ent[k].wid, sd, mask);
+          ok &= !(has_plus && sl == 0);
+          for (uint32_t x : used_pos) ok &= x != sl;
+          used_pos.push_back(sl);
+          pos[k] = sl;
+        }
+        if (ok) {
+          caplog = log2u(c2);
+          seed = sd;
+          ph = true;
+        }
+      }
+    }
+  }
+  std::vector<uint32_t> ovf_at;
+  if (!ph) {  // 2-slot buckets, two candidate buckets, random-walk eviction
+    caplog = log2u(next_pow2(8ull * e + 8));
+    bool ok = false;
+    std::vector<int32_t> owner;
+    for (uint32_t sd = 0; sd < CUCKOO_SEEDS && !ok; ++sd) {
+      const uint32_t cc = 1u << caplog, nbm = cc / 2 - 1;
+      owner.assign(cc, -1);
+      ok = true;
+      uint32_t rng = 0x9E3779B9u ^ (sd << 20) ^ e;
+      for (uint32_t k = 0; k < e; ++k)
+        if (ent[k].wid == WID_PLUS) owner[0] = static_cast<int32_t>(k);  // '+' pinned at slot 0
+      for (uint32_t k0 = 0; k0 < e && ok; ++k0) {
+        if (ent[k0].wid == WID_PLUS) continue;
+        int32_t k = static_cast<int32_t>(k0);
+        for (int kick = 0;; ++kick) {
+          const uint32_t w = ent[k].wid, b1 = bucket1(w, sd, nbm), b2 = bucket2(w, sd, nbm);
+          const uint32_t cand[4] = {2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1};
+          bool placed = false;
+          for (uint32_t q : cand)
+            if (owner[q] < 0) {
+              owner[q] = k;
+              placed = true;
+              break;
+            }
+          if (placed) break;
+          if (kick > 500) {
+            ok = false;
+            break;
+          }
+          rng = rng * 1664525u + 1013904223u;
+          const uint32_t victim = cand[(rng >> 16) & 3u];
+          if (ent[owner[victim]].wid == WID_PLUS) continue;
+          std::swap(k, owner[victim]);
+        }
+      }
+      if (ok) {
+        seed = sd;
+        for (uint32_t q = 0; q < cc; ++q)
+          if (owner[q] >= 0) pos[owner[q]] = q;
+        for (uint32_t k = 0; k < e; ++k) {
+          if (ent[k].wid == WID_PLUS) continue;
+          const uint32_t b1 = bucket1(ent[k].wid, sd, nbm);
+          if (pos[k] / 2 != b1) ovf_at.push_back(2 * b1);
+        }
+      }
+    }
+    if (!ok || caplog > 31) return false;
+  }
+  uint64_t nb = 0;
+  if (!alloc(caplog, &nb)) return false;
+  const uint32_t cc = 1u << caplog;
+  for (uint32_t i = 0; i < cc; ++i) {
+    edges[nb + i] = EMPTY_SLOT;
+    fids[2 * (nb + i)] = fids[2 * (nb + i) + 1] = FID_NONE;
+    sid[2 * (nb + i)] = sid[2 * (nb + i) + 1] = WID_NONE;
+  }
+  for (uint32_t k = 0; k < e; ++k) {
+    const uint64_t p = nb + pos[k];
+    edges[p] = ent[k].s;
+    fids[2 * p] = ent[k].fh;
+    fids[2 * p + 1] = ent[k].ft;
+    sid[2 * p] = ent[k].ih;
+    sid[2 * p + 1] = ent[k].it;
+    if (ent[k].ih != WID_NONE) loc[ent[k].ih] = p << 2 | FIDLOC_HASH;
+    if (ent[k].it != WID_NONE) loc[ent[k].it] = p << 2 | FIDLOC_TERM;
+  }
+  for (uint32_t q : ovf_at) edges[nb + q].meta |= META_BUCKET_OVF;
+  const uint32_t smeta = (caplog & META_CAPLOG2_MASK) | META_HAS_EDGES | (has_plus ? META_HAS_PLUS : 0u) |
+                         (ph ? META_PH : 0u) | (seed << META_SEED_SHIFT);
+  set_node(root, pslot, static_cast<uint32_t>(nb), smeta);
+  garbage += ocap;
+  relocations += 1;
+  return true;
+}
+
+bool LiveTrie::apply(const FilterStore& fs, uint32_t id) {
+  if (loc.size() < fs.n_ids()) loc.resize(fs.n_ids(), FIDLOC_NONE);
+  const bool want = fs.live[id] != 0;
+  const uint64_t l = loc[id];
+  if (l != FIDLOC_NONE) {  // in the trie: flag flip (delete / revival)
+    if (l == FIDLOC_ROOT_HASH) {
+      root_meta = want ? (root_meta | META_HAS_HASH) : (root_meta & ~META_HAS_HASH);
+    } else {
+      const uint64_t p = l >> 2;
+      const uint32_t bit = (l & 3) == FIDLOC_HASH ? META_HAS_HASH : META_HAS_TERM;
+      if (((edges[p].meta & bit) != 0) != want) {
+        edges[p].meta ^= bit;
+        touch(p);
+      }
+    }
+    flips += 1;
+    return true;
+  }
+  if (!want) return true;
+
+  // tokenize (emqx_topic:words/1); a final '#' is the parent level's hash filter
+  const uint8_t* p = fs.bytes.data() + fs.off[id];
+  const uint64_t n = fs.off[id + 1] - fs.off[id];
+  std::vector<uint32_t> w;
+  bool wild = false, final_hash = false;
+  uint64_t s = 0;
+  for (uint64_t i = 0; i <= n; ++i) {
+    if (i != n && p[i] != '/') continue;
+    const uint64_t len = i - s;
+    if (len == 1 && p[s] == '+') {
+      w.push_back(WID_PLUS);
+      wild = true;
+    } else if (len == 1 && p[s] == '#') {
+      wild = true;
+      if (i == n) final_hash = true;
+      else w.push_back(WID_HASH);
+    } else {
+      w.push_back(vocab->intern(p + s, len));
+    }
+    s = i + 1;
+  }
+  const uint32_t ext = fs.ext[id];
+  const uint32_t L = static_cast<uint32_t>(w.size());
+
+  bool root = true;
+  uint64_t pslot = 0;
+  uint32_t i = 0;
+  for (; i < L; ++i) {
+    const uint32_t base = root ? root_base : edges[pslot].child_base;
+    const uint32_t meta = root ? root_meta : edges[pslot].meta;
+    uint32_t c;
+    if (!find_child(base, meta, w[i], &c)) break;
+    root = false;
+    pslot = c;
+  }
+  if (i == L) {  // the filter's node exists: set its id and flag
+    if (final_hash && root) {
+      root_hash_fid = ext;
+      root_hash_id = id;
+      root_meta |= META_HAS_HASH;
+      loc[id] = FIDLOC_ROOT_HASH;
+      return true;
+    }
+    EdgeSlot& sl = edges[pslot];
+    if (final_hash) {
+      fids[2 * pslot] = ext;
+      sid[2 * pslot] = id;
+      sl.meta |= META_HAS_HASH;
+      loc[id] = pslot << 2 | FIDLOC_HASH;
+    } else {
+      fids[2 * pslot + 1] = ext;
+      sid[2 * pslot + 1] = id;
+      sl.meta |= META_HAS_TERM | (wild ? META_TERM_WILD : 0u);
+      loc[id] = pslot << 2 | FIDLOC_TERM;
+    }
+    reencode(pslot);
+    return true;
+  }
+
+  // new chain for levels i+1 .. L (bottom-up): the last node carries the filter
+  const uint32_t fmeta = final_hash ? META_HAS_HASH : (META_HAS_TERM | (wild ? META_TERM_WILD : 0u));
+  const uint32_t fh = final_hash ? ext : FID_NONE, ft = final_hash ? FID_NONE : ext;
+  const uint32_t ih = final_hash ? id : WID_NONE, it = final_hash ? WID_NONE : id;
+  EdgeSlot cur = encode(w[L - 1], false, 0, 0, fh, ft, fmeta);
+  uint32_t cfh = fh, cft = ft, cih = ih, cit = it;
+  for (uint32_t j = L - 1; j > i; --j) {  // node at depth j holds the edge w[j]
+    uint64_t nb = 0;
+    if (!alloc(1, &nb)) return false;
+    const bool plus = w[j] == WID_PLUS;
+    const uint32_t at = plus ? 0u : lit_slot(w[j], 0, 1);
+    edges[nb] = edges[nb + 1] = EMPTY_SLOT;
+    for (uint64_t q = 2 * nb; q < 2 * nb + 4; ++q) {
+      fids[q] = FID_NONE;
+      sid[q] = WID_NONE;
+    }
+    const uint64_t ps = nb + at;
+    edges[ps] = cur;
+    fids[2 * ps] = cfh;
+    fids[2 * ps + 1] = cft;
+    sid[2 * ps] = cih;
+    sid[2 * ps + 1] = cit;
+    if (cih != WID_NONE) loc[cih] = ps << 2 | FIDLOC_HASH;
+    if (cit != WID_NONE) loc[cit] = ps << 2 | FIDLOC_TERM;
+    const uint32_t sm = 1u | META_HAS_EDGES | META_PH | (plus ? META_HAS_PLUS : 0u);
+    cur = encode(w[j - 1], true, static_cast<uint32_t>(nb), sm, FID_NONE, FID_NONE, 0);
+    cfh = cft = FID_NONE;
+    cih = cit = WID_NONE;
+    n_nodes += 1;
+  }
+  n_nodes += 1;
+  max_depth = std::max(max_depth, L);
+  chains += 1;
+  return place(root, pslot, w[i], cur, cfh, cft, cih, cit);
+}
+
+void LiveTrie::patches(std::vector<SlotPatch>& out) const {
+  std::vector<uint32_t> d(dirty);
+  std::sort(d.begin(), d.end());
+  d.erase(std::unique(d.begin(), d.end()), d.end());
+  out.clear();
+  out.reserve(d.size());
+  for (uint32_t p : d) out.push_back(SlotPatch{p, fids[2 * uint64_t(p)], fids[2 * uint64_t(p) + 1], 0, edges[p]});
+}
+
+}  // namespace emqx

@@ -1288,15 +1288,19 @@ __global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a) {
   }
 }
 
-// Incremental commits: set (bit 31 clear) or clear (bit 31 set) meta flag bits of slots —
-// tombstones and revivals of filters in the base trie.  One 32-bit atomic per patch, so a
-// concurrent walk sees each filter present or absent, never a torn slot.
-__global__ void meta_patch_kernel(EdgeSlot* edges, const uint2* patches, uint32_t n) {
+// Incremental commits (live_trie.cpp): rewrites existing slots of the committed table in
+// place.  Phase 0 writes the slots' filter ids, phase 1 (a later launch) the slots, each with
+// one 16-B store, so a concurrent walk sees every slot either old or new, and never a slot
+// whose filter id is not yet readable.
+__global__ void slot_patch_kernel(EdgeSlot* edges, uint32_t* fids, const SlotPatch* patches, uint32_t n,
+                                  int phase) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint2 p = patches[i];
-    uint32_t* m = &edges[p.x].meta;
-    if (p.y & META_PATCH_CLEAR) atomicAnd(m, ~(p.y & ~META_PATCH_CLEAR));
-    else atomicOr(m, p.y);
+    const SlotPatch& p = patches[i];
+    if (phase == 0) {
+      *reinterpret_cast<uint2*>(fids + 2ull * p.slot) = make_uint2(p.fid_h, p.fid_t);
+    } else {
+      *reinterpret_cast<uint4*>(edges + p.slot) = make_uint4(p.s.wid, p.s.child_base, p.s.meta, p.s.litf);
+    }
   }
 }
 
@@ -1364,8 +1368,12 @@ hipError_t launch_assemble(const MatchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_meta_patches(EdgeSlot* edges, const uint2* patches, uint32_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(meta_patch_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 1024)), dim3(256), 0, s, edges, patches, n);
+hipError_t launch_slot_patches(EdgeSlot* edges, uint32_t* fids, const SlotPatch* patches, uint32_t n,
+                               hipStream_t s) {
+  if (!n) return hipSuccess;
+  const dim3 grid(std::min<uint32_t>((n + 255) / 256, 1024));
+  hipLaunchKernelGGL(slot_patch_kernel, grid, dim3(256), 0, s, edges, fids, patches, n, 0);
+  hipLaunchKernelGGL(slot_patch_kernel, grid, dim3(256), 0, s, edges, fids, patches, n, 1);
   return hipGetLastError();
 }
 

@@ -559,6 +559,7 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
   out.fids.assign(2 * n_slots, FID_NONE);
   const uint32_t off0 = static_cast<uint32_t>(opts.slot_offset);
   if (opts.fid_loc) opts.fid_loc->assign(n_ids, FIDLOC_NONE);
+  if (opts.slot_ids) opts.slot_ids->assign(2 * n_slots, WID_NONE);
   auto write_slot = [&](uint64_t at, uint32_t wid, uint32_t child) {
     EdgeSlot& r = out.edges[at];
     r.wid = wid;
@@ -573,6 +574,10 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
     r.litf = leaf ? term_fid[child] : lf[child];
     out.fids[2 * at] = hash_fid[child];
     out.fids[2 * at + 1] = term_fid[child];
+    if (opts.slot_ids) {
+      (*opts.slot_ids)[2 * at] = hash_id[child];
+      (*opts.slot_ids)[2 * at + 1] = term_id[child];
+    }
   };
   for (uint64_t v = 0; v < n_nodes; ++v) {
     if (!n_edges[v]) continue;

@@ -94,6 +94,7 @@ struct BuildOpts {
   VocabState* vocab = nullptr;                 // persistent interner (null: a private one)
   bool vocab_table = true;                     // build the vocab table into HostTables
   std::vector<uint64_t>* fid_loc = nullptr;    // out: per filter id (sized n_ids)
+  std::vector<uint32_t>* slot_ids = nullptr;   // out: per slot, the engine ids {hash, term} (2 per slot)
 };
 
 struct HostTables {
@@ -119,5 +120,60 @@ inline bool build_tables(const FilterStore& fs, HostTables& out, std::string* er
 }
 // Verifies the lookup invariants of a built table (host-side; used by tests).
 bool check_tables(const HostTables& t, std::string* err);
+
+// ---- incremental commits: the committed trie patched in place (live_trie.cpp) ---------
+//
+// The host keeps an image of the device slot array (edges + fids) with spare capacity behind
+// the built slots.  Publishing an insert walks the image like the kernel does; the filter's
+// missing tail becomes a chain of new one-edge nodes in the spare region, and its first edge is
+// placed into the existing node when that node's hashing has a free slot for it, else the node
+// is relocated (rebuilt one entry larger into the spare region).  Either way the device sees a
+// handful of new slots plus whole-slot (16-B) rewrites of existing ones — the edge's slot and
+// the parent slot that describes the node — so the cost of a commit is proportional to the
+// churn, not to the table or to earlier commits.  Deletes / revivals flip the filter's flag in
+// its slot.  A full rebuild (compaction) runs when the spare region is used up.
+struct LiveTrie {
+  std::vector<EdgeSlot> edges;  // host image of device slots [0, cap)
+  std::vector<uint32_t> fids;   // 2 per slot (reported ids)
+  std::vector<uint32_t> sid;    // 2 per slot (engine ids, for fid_loc upkeep)
+  uint64_t used = 0, cap = 0;   // append cursor / capacity in slots
+  uint64_t garbage = 0;         // slots of arrays superseded by relocations
+  uint64_t line = 0;            // open 128-B line of the small-array packer
+  uint32_t line_used = 0xFFu;
+  uint32_t root_base = 0, root_meta = 0, root_hash_fid = FID_NONE, root_hash_id = WID_NONE;
+  uint64_t n_nodes = 0;
+  uint32_t max_depth = 0;
+  std::vector<uint64_t> loc;    // per engine id: FIDLOC (tables.h)
+  VocabState* vocab = nullptr;
+  // per commit
+  uint64_t mark = 0;            // `used` when the commit began: [mark, used) is uploaded whole
+  std::vector<uint32_t> dirty;  // slots < mark rewritten in place (may repeat)
+  uint64_t relocations = 0, in_place = 0, chains = 0, flips = 0;
+
+  // Adopts a full build (moves its arrays) and reserves `spare` slots behind it.
+  void adopt(HostTables& ht, std::vector<uint64_t>& fid_loc, std::vector<uint32_t>& slot_ids, uint64_t spare,
+             VocabState* v);
+  void begin_commit();
+  // Brings filter `id` in line with fs.live[id]: flag flip, or insertion of a new filter.
+  // False when the spare region is exhausted (the caller then does a full rebuild).
+  bool apply(const FilterStore& fs, uint32_t id);
+  // The commit's device writes: slot patches (deduplicated) for slots < mark.
+  void patches(std::vector<SlotPatch>& out) const;
+
+ private:
+  bool find_child(uint32_t base, uint32_t meta, uint32_t wid, uint32_t* slot) const;
+  bool alloc(uint32_t caplog, uint64_t* at);
+  void touch(uint64_t slot);
+  void lit_summary(uint32_t base, uint32_t meta, uint32_t* n_lit, uint32_t* only, uint32_t* bloom,
+                   uint32_t* bloom8) const;
+  EdgeSlot encode(uint32_t wid, bool has_edges, uint32_t base, uint32_t nmeta, uint32_t fid_h, uint32_t fid_t,
+                  uint32_t flags) const;
+  void reencode(uint64_t pslot);
+  void set_node(bool root, uint64_t pslot, uint32_t base, uint32_t nmeta);
+  bool place(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
+             uint32_t ih, uint32_t it);
+  bool relocate(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
+                uint32_t ih, uint32_t it);
+};
 
 }  // namespace emqx

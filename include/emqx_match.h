@@ -28,10 +28,9 @@
  * offsets[i+1])).  Match results are CSR: out_offsets[n+1] and out_ids[out_offsets[n]].
  *
  * Threading: any number of threads may call emqx_match_batch* concurrently; each call
- * reads an immutable table snapshot.  Mutations (insert/delete/commit) must come from one
- * writer at a time (the reference serialises route mutations per topic through
- * router_pool, apps/emqx/src/emqx_router.erl:184-188); emqx_commit publishes a new
- * snapshot RCU-style — in-flight matches keep the old one until they return.
+ * reads the committed table.  Mutations (insert/delete/commit) must come from one writer at a
+ * time (the reference serialises route mutations per topic through router_pool,
+ * apps/emqx/src/emqx_router.erl:184-188); see emqx_commit for what a concurrent match sees.
  *
  * Ownership: the caller owns every buffer it passes for the duration of the call; the
  * engine owns device tables, staging and workspaces, all released by
@@ -83,8 +82,8 @@ typedef struct emqx_stats {
   double last_build_ms;      /* host build time of the last commit                           */
   double last_match_ms;      /* device time of the last match call (hipEvent)                */
   double last_kernel_ms;     /* device time of its fused match kernel alone (hipEvent)       */
-  uint64_t delta_filters;    /* filters in the delta trie (created since the last full build)*/
-  uint64_t last_commit_kind; /* 0 = full rebuild, 1 = incremental (flag flips + delta trie)  */
+  uint64_t delta_filters;    /* filters placed by incremental commits since the last full build */
+  uint64_t last_commit_kind; /* 0 = full rebuild, 1 = incremental (patched in place)          */
 } emqx_stats;
 
 /* Lifecycle. */
@@ -105,12 +104,19 @@ int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n);
 int emqx_lookup_filter(emqx_engine* e, const uint8_t* bytes, uint64_t len, uint32_t* id_out);
 /* Copies the bytes of filter `id` into buf (cap bytes); *len_out = its length. */
 int emqx_filter_name(emqx_engine* e, uint32_t id, uint8_t* buf, uint64_t cap, uint64_t* len_out);
-/* Publishes every insert/delete since the last commit (epoch swap; in-flight matches keep
- * the snapshot they started with).  Incremental by default: a deleted / re-inserted filter
- * of the last full build flips a meta flag of its slot in place, filters created since then
- * live in a small delta trie rebuilt per commit; a full rebuild runs when the delta outgrows
- * its headroom (emqx_set_tuning "delta_max", "incremental" = 0 forces full rebuilds). */
+/* Publishes every insert/delete since the last commit.  Incremental by default, at a cost
+ * proportional to the changes: a deleted / re-inserted filter flips a flag of its slot, a new
+ * filter's missing tail is added to the committed table in place (new nodes in a spare region,
+ * whole-slot rewrites of existing slots); a match call that overlaps the commit sees each
+ * changed filter present or absent, as concurrent ETS readers see a mria commit.  A full
+ * rebuild (fresh tables, epoch swap: in-flight matches keep the old tables) runs when the
+ * spare region is used up (emqx_set_tuning "delta_max": at most that many filters placed
+ * incrementally; "incremental" = 0 forces full rebuilds). */
 int emqx_commit(emqx_engine* e);
+/* Details of the last commit: out[0..7] = kind (0 full, 1 incremental), node relocations,
+ * edges placed in place, slots rewritten in place, new slots, spare-region cursor, spare-region
+ * capacity (slots), slots of superseded arrays. */
+int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n);
 
 /* Batched match, host buffers.  out_offsets has n+1 entries.  On EMQX_EOVERFLOW nothing
  * is written to out_ids and *n_out is the capacity required. */
@@ -241,6 +247,21 @@ int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset);
  * nodes, slots, interned words, perfect-hashed nodes.  err receives the failure reason. */
 int emqx_build_check(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* stats_out,
                      char* err, uint64_t err_cap);
+
+/* Host-only self-check of incremental commits (no device): a filter store + the table builder
+ * + the in-place patcher the engine uses, and a host walk of the patched table by the kernels'
+ * lookup and emission rules.  spare_slots: the spare region (0 = default); commit(full = 1)
+ * rebuilds; stats8 as emqx_commit_stats.  match supports EMQX_MODE_ROUTES / _TRIE_WILDCARD on
+ * non-wildcard topics.  check verifies the lookup invariants of every reachable node. */
+typedef struct emqx_htrie emqx_htrie;
+int emqx_htrie_create(uint64_t spare_slots, emqx_htrie** out);
+int emqx_htrie_destroy(emqx_htrie* h);
+int emqx_htrie_insert(emqx_htrie* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t* ids_out);
+int emqx_htrie_delete(emqx_htrie* h, const uint32_t* ids, uint64_t n);
+int emqx_htrie_commit(emqx_htrie* h, int full, uint64_t* stats8);
+int emqx_htrie_match(emqx_htrie* h, uint32_t mode, const uint8_t* topic_bytes, const uint64_t* topic_offsets,
+                     uint64_t n, uint64_t* out_offsets, uint32_t* out_ids, uint64_t cap, uint64_t* n_out);
+int emqx_htrie_check(emqx_htrie* h, char* err, uint64_t err_cap);
 
 const char* emqx_strerror(int code);
 /* Library version string. */
