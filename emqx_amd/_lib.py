@@ -150,7 +150,7 @@ def lib():
                                                  ctypes.POINTER(u64), vp]),
         "emqx_retain_stats_get": (i32, [vp, ctypes.POINTER(RetainStats)]),
         "emqx_commit_stats": (i32, [vp, vp, u32]),
-        "emqx_htrie_create": (i32, [u64, ctypes.POINTER(vp)]),
+        "emqx_htrie_create": (i32, [u64, i32, ctypes.POINTER(vp)]),
         "emqx_htrie_destroy": (i32, [vp]),
         "emqx_htrie_insert": (i32, [vp, vp, vp, u64, vp]),
         "emqx_htrie_delete": (i32, [vp, vp, u64]),

@@ -90,6 +90,7 @@ struct LiveState {
   std::unique_ptr<VocabState> vocab;
   std::unique_ptr<LiveTrie> lt;
   uint64_t inserted = 0;        // filters placed by incremental commits since the full build
+  uint64_t base_live = 0;       // live filters at the full build
   hipStream_t stream = nullptr; // commit stream (uploads + patch kernels; synchronised alone)
   SlotPatch* d_patch = nullptr;
   uint64_t cap_patch = 0;
@@ -191,6 +192,8 @@ struct emqx_engine {
                                 // commits before a full rebuild (-1: until the spare region is full)
   uint64_t last_commit_kind = 0;
   uint64_t last_relocations = 0, last_in_place = 0, last_patches = 0, last_new_slots = 0;
+  double last_host_ms = 0;      // host part (LiveTrie::commit) of the last incremental commit
+  int commit_threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
 };
 
 namespace {
@@ -262,6 +265,7 @@ int full_commit(emqx_engine* e) {
   d.lt->adopt(ht, loc, slot_ids, spare, d.vocab.get());
   d.valid = true;
   d.inserted = 0;
+  d.base_live = e->store.n_live;
   e->dirty.clear();
   publish(e, std::move(s));
   e->last_commit_kind = 0;
@@ -272,7 +276,8 @@ int full_commit(emqx_engine* e) {
 // the committed table (LiveTrie::apply), then the device gets the new spare-region slots and
 // the rewritten existing slots on the commit stream, which alone is synchronised.  A walk that
 // overlaps the commit sees each filter of it present or absent.  EMQX_NEED_FULL when the spare
-// region, the vocab or the arena headroom runs out, or e->delta_max is reached.
+// region, the vocab or the arena headroom runs out, e->delta_max is reached, or (delta_max
+// unset) the filters placed since the full build reach half of the filters it held.
 int live_commit(emqx_engine* e) {
   LiveState& d = e->ls;
   LiveTrie& lt = *d.lt;
@@ -283,13 +288,19 @@ int live_commit(emqx_engine* e) {
   uint64_t creates = 0;
   for (uint32_t id : ids)
     if (fs.live[id] && (id >= lt.loc.size() || lt.loc[id] == FIDLOC_NONE)) ++creates;
-  if (e->delta_max >= 0 && d.inserted + creates > static_cast<uint64_t>(e->delta_max)) return EMQX_NEED_FULL;
+  if (e->delta_max >= 0) {
+    if (d.inserted + creates > static_cast<uint64_t>(e->delta_max)) return EMQX_NEED_FULL;
+  } else if (creates && 2 * (d.inserted + creates) > d.base_live) {
+    // default policy: once the table has grown by half since its build (and at the first
+    // filters of an empty build), a fresh line-packed, perfect-hashed build serves it better
+    return EMQX_NEED_FULL;
+  }
 
-  lt.begin_commit();
   const uint64_t nw0 = d.vocab->n_words(), arena0 = d.vocab->arena.size();
-  for (uint32_t id : ids)
-    if (!lt.apply(fs, id)) return EMQX_NEED_FULL;  // spare region exhausted: the host image is
-                                                   // rebuilt with the tables
+  auto th0 = std::chrono::steady_clock::now();
+  if (!lt.commit(fs, ids, e->commit_threads)) return EMQX_NEED_FULL;  // spare region exhausted: the
+                                                                     // host image is rebuilt too
+  e->last_host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
   std::vector<uint32_t> vdirty;
   if (!d.vocab->insert_table(nw0, &vdirty) || d.vocab->arena.size() + 16 > d.dt->cap_arena) return EMQX_NEED_FULL;
   lt.patches(d.patches);
@@ -297,8 +308,8 @@ int live_commit(emqx_engine* e) {
   HIP_TRY(hipSetDevice(e->device));
   if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   hipStream_t st = d.stream;
-  const uint64_t a0 = lt.mark, a1 = lt.used;
-  if (a1 > a0) {
+  for (const auto& r : lt.ranges) {  // the commit's new slots, extent by extent
+    const uint64_t a0 = r.first, a1 = r.second;
     HIP_TRY(hipMemcpyAsync(d.dt->edges + a0, lt.edges.data() + a0, (a1 - a0) * sizeof(EdgeSlot),
                            hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(d.dt->fids + 2 * a0, lt.fids.data() + 2 * a0, 2 * (a1 - a0) * sizeof(uint32_t),
@@ -338,7 +349,7 @@ int live_commit(emqx_engine* e) {
   e->last_relocations = lt.relocations;
   e->last_in_place = lt.in_place;
   e->last_patches = np;
-  e->last_new_slots = a1 - a0;
+  e->last_new_slots = lt.new_slots();
   e->dirty.clear();
   publish(e, std::move(s));
   e->last_commit_kind = 1;
@@ -832,6 +843,12 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
     e->incremental = value != 0;
     return EMQX_OK;
   }
+  if (std::strcmp(key, "commit_threads") == 0) {
+    if (value < 1 || value > 256) return EMQX_EINVAL;
+    std::lock_guard<std::mutex> g(e->writer);
+    e->commit_threads = static_cast<int>(value);
+    return EMQX_OK;
+  }
   if (std::strcmp(key, "delta_max") == 0) {
     std::lock_guard<std::mutex> g(e->writer);
     e->delta_max = value;
@@ -844,9 +861,10 @@ int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n) {
   if (!e || (n && !out)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(e->writer);
   const LiveTrie* lt = e->ls.lt.get();
-  const uint64_t v[8] = {e->last_commit_kind, e->last_relocations, e->last_in_place, e->last_patches,
-                         e->last_new_slots, lt ? lt->used : 0, lt ? lt->cap : 0, lt ? lt->garbage : 0};
-  for (uint32_t i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  uint64_t host_us = static_cast<uint64_t>(e->last_host_ms * 1e3);
+  const uint64_t v[9] = {e->last_commit_kind, e->last_relocations, e->last_in_place, e->last_patches,
+                         e->last_new_slots, lt ? lt->used : 0, lt ? lt->cap : 0, lt ? lt->garbage : 0, host_us};
+  for (uint32_t i = 0; i < n && i < 9; ++i) out[i] = v[i];
   return EMQX_OK;
 }
 

@@ -26,6 +26,7 @@ struct emqx_htrie {
   bool built = false;
   uint64_t spare = 0;
   uint64_t kind = 0;
+  int threads = 1;
 };
 
 namespace {
@@ -199,11 +200,12 @@ bool check(const LiveTrie& t, std::string* err) {
 
 extern "C" {
 
-int emqx_htrie_create(uint64_t spare_slots, emqx_htrie** out) {
+int emqx_htrie_create(uint64_t spare_slots, int threads, emqx_htrie** out) {
   if (!out) return EMQX_EINVAL;
   auto* h = new (std::nothrow) emqx_htrie();
   if (!h) return EMQX_ENOMEM;
   h->spare = spare_slots;
+  h->threads = std::max(1, threads);
   *out = h;
   return EMQX_OK;
 }
@@ -245,9 +247,7 @@ int emqx_htrie_commit(emqx_htrie* h, int full, uint64_t* stats8) {
     std::vector<uint32_t> ids(h->dirty);
     std::sort(ids.begin(), ids.end());
     ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-    h->lt.begin_commit();
-    bool ok = true;
-    for (uint32_t id : ids) ok = ok && h->lt.apply(h->fs, id);
+    const bool ok = h->lt.commit(h->fs, ids, h->threads);
     h->kind = 1;
     if (!ok) full_build(h);  // spare region exhausted
     h->dirty.clear();
@@ -255,7 +255,7 @@ int emqx_htrie_commit(emqx_htrie* h, int full, uint64_t* stats8) {
   if (stats8) {
     std::vector<SlotPatch> p;
     h->lt.patches(p);
-    const uint64_t v[8] = {h->kind, h->lt.relocations, h->lt.in_place, p.size(), h->lt.used - h->lt.mark,
+    const uint64_t v[8] = {h->kind, h->lt.relocations, h->lt.in_place, p.size(), h->lt.new_slots(),
                            h->lt.used, h->lt.cap, h->lt.garbage};
     std::memcpy(stats8, v, sizeof(v));
   }

@@ -17,11 +17,18 @@
 //     parent's array, or the table view for the root) is re-encoded: literal filter, XFID /
 //     inline filter ids, hashing parameters.
 //
-// Device writes per commit: the new spare-region slots [mark, used) in one copy, plus one
-// whole 16-B slot store per rewritten existing slot (filter ids first, slots second), so a
-// walk that overlaps a commit sees each slot old or new, and each new filter absent or present.
+// Device writes per commit: the new spare-region extents (one copy each), plus one whole 16-B
+// slot store per rewritten existing slot (filter ids first, slots second), so a walk that
+// overlaps a commit sees each slot old or new, and each new filter absent or present.
+//
+// Threads: flips touch one slot each (atomic flag updates); inserts under different
+// first-level nodes touch disjoint parts of the table (the node, its descendants, their
+// slots, their filters' ids), so after the inserts that must change the root itself have run
+// serially, the rest run grouped by first-level node on up to `threads` threads, each
+// allocating from its own chunk of the spare region.
 #include <algorithm>
 #include <cstring>
+#include <thread>
 
 #include "tables.h"
 
@@ -48,12 +55,6 @@ uint32_t log2u(uint64_t p) {
   return l;
 }
 
-struct Entry {
-  uint32_t wid;
-  EdgeSlot s;  // slot content without the position's META_BUCKET_OVF bit
-  uint32_t fh, ft, ih, it;
-};
-
 }  // namespace
 
 void LiveTrie::adopt(HostTables& ht, std::vector<uint64_t>& fid_loc, std::vector<uint32_t>& slot_ids,
@@ -68,7 +69,6 @@ void LiveTrie::adopt(HostTables& ht, std::vector<uint64_t>& fid_loc, std::vector
   sid.resize(2 * cap, WID_NONE);
   used = n;
   garbage = 0;
-  line_used = FULL_LINE;
   root_base = ht.root_base;
   root_meta = ht.root_meta;
   root_hash_fid = ht.root_hash_fid;
@@ -81,43 +81,78 @@ void LiveTrie::adopt(HostTables& ht, std::vector<uint64_t>& fid_loc, std::vector
   vocab = v;
   mark = used;
   dirty.clear();
+  ranges.clear();
 }
 
-void LiveTrie::begin_commit() {
-  mark = used;
-  line_used = FULL_LINE;  // never allocate into a line the device already holds
-  dirty.clear();
-  relocations = in_place = chains = flips = 0;
-}
+namespace {
+constexpr uint64_t CHUNK = 8192;          // spare-region slots a thread takes at a time
+constexpr uint32_t WID_UNKNOWN = 0xFFFFFFFCu;  // tokenize(intern = false): a word not interned yet
+}  // namespace
 
-void LiveTrie::touch(uint64_t slot) {
-  if (slot < mark) dirty.push_back(static_cast<uint32_t>(slot));
-}
-
-bool LiveTrie::alloc(uint32_t caplog, uint64_t* at) {
-  const uint64_t c = 1ull << caplog;
-  if (c >= LINE) {
-    const uint64_t a = (used + LINE - 1) & ~uint64_t(LINE - 1);
-    if (a + c > cap) return false;
-    used = a + c;
-    line_used = FULL_LINE;
+// Spare-region allocation: arrays of >= 8 slots start on a 128-B line; smaller ones are packed
+// first-fit into the thread's open line (an array never straddles a line), as the builder's
+// line-packed layout does.  Large arrays come straight from the shared cursor.
+bool LiveTrie::alloc(Ctx& c, uint32_t caplog, uint64_t* at) {
+  const uint64_t n = 1ull << caplog;
+  auto grab = [&](uint64_t want, uint64_t* a) -> bool {
+    std::lock_guard<std::mutex> g(alloc_mu_);
+    const uint64_t b = (used + LINE - 1) & ~uint64_t(LINE - 1);
+    if (b + want > cap) return false;
+    used = b + want;
+    *a = b;
+    return true;
+  };
+  if (n >= CHUNK / 4) {
+    uint64_t a;
+    if (!grab(n, &a)) return false;
+    c.ranges.push_back({a, a + n});
     *at = a;
     return true;
   }
-  const uint32_t want = (1u << c) - 1u;
-  for (uint32_t o = 0; o < LINE; o += static_cast<uint32_t>(c))
-    if (!(line_used & (want << o))) {
-      line_used |= want << o;
-      *at = line + o;
-      return true;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (n >= LINE) {
+      const uint64_t a = (c.cur + LINE - 1) & ~uint64_t(LINE - 1);
+      if (a + n <= c.end) {
+        c.cur = a + n;
+        c.ranges.back().second = c.cur;
+        c.line_used = FULL_LINE;
+        *at = a;
+        return true;
+      }
+    } else {
+      const uint32_t want = (1u << n) - 1u;
+      for (uint32_t o = 0; o < LINE; o += static_cast<uint32_t>(n))
+        if (!(c.line_used & (want << o))) {
+          c.line_used |= want << o;
+          *at = c.line + o;
+          return true;
+        }
+      const uint64_t l = (c.cur + LINE - 1) & ~uint64_t(LINE - 1);
+      if (l + LINE <= c.end) {
+        c.line = l;
+        c.cur = l + LINE;
+        c.ranges.back().second = c.cur;
+        c.line_used = want;
+        *at = l;
+        return true;
+      }
     }
-  const uint64_t l = (used + LINE - 1) & ~uint64_t(LINE - 1);
-  if (l + LINE > cap) return false;
-  line = l;
-  used = l + LINE;
-  line_used = want;
-  *at = l;
-  return true;
+    uint64_t a, len = CHUNK;  // a new chunk (what is left, near the end of the region)
+    {
+      std::lock_guard<std::mutex> g(alloc_mu_);
+      const uint64_t b = (used + LINE - 1) & ~uint64_t(LINE - 1);
+      len = b < cap ? std::min<uint64_t>(CHUNK, cap - b) : 0;
+      if (len < std::max<uint64_t>(n, LINE)) return false;
+      used = b + len;
+      a = b;
+    }
+    c.garbage += c.end - c.cur;  // the old chunk's unused tail
+    c.cur = a;
+    c.end = a + len;
+    c.line_used = FULL_LINE;
+    c.ranges.push_back({a, a});
+  }
+  return false;
 }
 
 // The node's literal words, summarised as the builder does (tables.cpp pass 4).  Wide
@@ -184,17 +219,17 @@ EdgeSlot LiveTrie::encode(uint32_t wid, bool has_edges, uint32_t base, uint32_t 
 }
 
 // Re-encodes slot `p` from its current node structure and filter ids.
-void LiveTrie::reencode(uint64_t p) {
+void LiveTrie::reencode(Ctx& c, uint64_t p) {
   const EdgeSlot s = edges[p];
   const bool he = (s.meta & META_HAS_EDGES) != 0;
   EdgeSlot r = encode(s.wid, he, he ? s.child_base : 0, s.meta, fids[2 * p], fids[2 * p + 1], s.meta);
   r.meta |= s.meta & META_BUCKET_OVF;
   edges[p] = r;
-  touch(p);
+  touch(c, p);
 }
 
 // Points the node reached through `pslot` (or the root) at a new edge array / structure.
-void LiveTrie::set_node(bool root, uint64_t pslot, uint32_t base, uint32_t smeta) {
+void LiveTrie::set_node(Ctx& c, bool root, uint64_t pslot, uint32_t base, uint32_t smeta) {
   if (root) {
     uint32_t n_lit, only, bloom, bloom8;
     const uint32_t sm = (smeta & STRUCT_BITS) | META_HAS_EDGES;
@@ -207,7 +242,7 @@ void LiveTrie::set_node(bool root, uint64_t pslot, uint32_t base, uint32_t smeta
   EdgeSlot r = encode(s.wid, true, base, smeta, fids[2 * pslot], fids[2 * pslot + 1], s.meta);
   r.meta |= s.meta & META_BUCKET_OVF;
   edges[pslot] = r;
-  touch(pslot);
+  touch(c, pslot);
 }
 
 bool LiveTrie::find_child(uint32_t base, uint32_t meta, uint32_t wid, uint32_t* slot) const {
@@ -240,11 +275,11 @@ bool LiveTrie::find_child(uint32_t base, uint32_t meta, uint32_t wid, uint32_t* 
 
 // Adds edge `wid` -> `child` (slot content; filter ids fh/ft, engine ids ih/it) to the node
 // reached through `pslot` (or the root): in place when its hashing has room, else relocated.
-bool LiveTrie::place(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
-                     uint32_t ih, uint32_t it) {
+bool LiveTrie::place(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh,
+                     uint32_t ft, uint32_t ih, uint32_t it) {
   const uint32_t base = root ? root_base : edges[pslot].child_base;
   uint32_t smeta = (root ? root_meta : edges[pslot].meta) & STRUCT_BITS;
-  if (!(smeta & META_HAS_EDGES)) return relocate(root, pslot, wid, child, fh, ft, ih, it);
+  if (!(smeta & META_HAS_EDGES)) return relocate(cx, root, pslot, wid, child, fh, ft, ih, it);
   const uint32_t mask = (1u << (smeta & META_CAPLOG2_MASK)) - 1u;
   const uint32_t sd = (smeta >> META_SEED_SHIFT) & 255u;
   uint64_t target = ~0ull, ovf = ~0ull;
@@ -266,7 +301,7 @@ bool LiveTrie::place(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& ch
         ovf = base + 2 * b1;
       }
   }
-  if (target == ~0ull) return relocate(root, pslot, wid, child, fh, ft, ih, it);
+  if (target == ~0ull) return relocate(cx, root, pslot, wid, child, fh, ft, ih, it);
   const uint32_t keep = edges[target].meta & META_BUCKET_OVF;
   edges[target] = child;
   edges[target].meta = (child.meta & ~META_BUCKET_OVF) | keep;
@@ -276,24 +311,25 @@ bool LiveTrie::place(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& ch
   sid[2 * target + 1] = it;
   if (ih != WID_NONE) loc[ih] = target << 2 | FIDLOC_HASH;
   if (it != WID_NONE) loc[it] = target << 2 | FIDLOC_TERM;
-  touch(target);
+  touch(cx, target);
   if (ovf != ~0ull && !(edges[ovf].meta & META_BUCKET_OVF)) {
     edges[ovf].meta |= META_BUCKET_OVF;
-    touch(ovf);
+    touch(cx, ovf);
   }
-  set_node(root, pslot, base, smeta);
-  in_place += 1;
+  set_node(cx, root, pslot, base, smeta);
+  cx.in_place += 1;
   return true;
 }
 
 // Rebuilds the node's edge array with the new entry into the spare region (perfect hash for
 // up to 32 literals, with 1.5x slack so later inserts usually fit in place; 2-slot buckets at
 // load <= 1/8 beyond), then points the node's slot at it.
-bool LiveTrie::relocate(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh,
+bool LiveTrie::relocate(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh,
                         uint32_t ft, uint32_t ih, uint32_t it) {
   const uint32_t obase = root ? root_base : edges[pslot].child_base;
   const uint32_t ometa = (root ? root_meta : edges[pslot].meta) & STRUCT_BITS;
-  std::vector<Entry> ent;
+  std::vector<Entry>& ent = cx.ent;
+  ent.clear();
   uint32_t ocap = 0;
   if (ometa & META_HAS_EDGES) {
     ocap = 1u << (ometa & META_CAPLOG2_MASK);
@@ -316,25 +352,33 @@ bool LiveTrie::relocate(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot&
 
   uint32_t caplog = 0, seed = 0;
   bool ph = false;
-  std::vector<uint32_t> pos(e, 0);
-  std::vector<uint32_t> used_pos;
+  std::vector<uint32_t>& pos = cx.pos;
+  pos.assign(e, 0);
   if (n_lit <= 32) {
+    // perfect-hash seed search, one bitmap per trial (cap <= 512 here: 8 words); array sizes
+    // where 256 seeds would almost surely all fail (birthday bound) are skipped
     const uint64_t cap0 = next_pow2(std::max<uint64_t>(2, e + e / 2));
     const uint64_t cap_max = next_pow2(std::max<uint64_t>(16, 8ull * e));
-    for (uint64_t c2 = cap0; c2 <= cap_max && !ph && log2u(c2) <= PH_MAX_CAPLOG; c2 <<= 1) {
+    for (uint64_t c2 = cap0; c2 <= cap_max && !ph && log2u(c2) <= PH_MAX_CAPLOG && c2 <= 512; c2 <<= 1) {
+      double p_ok = 1.0;
+      const uint32_t avail = static_cast<uint32_t>(c2) - (has_plus ? 1u : 0u);
+      for (uint32_t k = 0; k < n_lit; ++k) p_ok *= k < avail ? double(avail - k) / double(c2) : 0.0;
+      if (p_ok * 256.0 < 0.02 && c2 < cap_max) continue;
       const uint32_t mask = static_cast<uint32_t>(c2 - 1);
       for (uint32_t sd = 0; sd < 256 && !ph; ++sd) {
-        used_pos.clear();
+        uint64_t bm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (has_plus) bm[0] = 1;
+        const uint32_t salt = sd * 0x9E3779B1u + 0x7F4A7C15u;
         bool ok = true;
         for (uint32_t k = 0; k < e && ok; ++k) {
           if (ent[k].wid == WID_PLUS) {
             pos[k] = 0;
             continue;
           }
-          const uint32_t sl = lit_slot(ent[k].wid, sd, mask);
-          ok &= !(has_plus && sl == 0);
-          for (uint32_t x : used_pos) ok &= x != sl;
-          used_pos.push_back(sl);
+          const uint32_t sl = mix32(ent[k].wid ^ salt) & mask;
+          const uint64_t bit = 1ull << (sl & 63u);
+          ok = !(bm[sl >> 6] & bit);
+          bm[sl >> 6] |= bit;
           pos[k] = sl;
         }
         if (ok) {
@@ -395,7 +439,7 @@ bool LiveTrie::relocate(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot&
     if (!ok || caplog > 31) return false;
   }
   uint64_t nb = 0;
-  if (!alloc(caplog, &nb)) return false;
+  if (!alloc(cx, caplog, &nb)) return false;
   const uint32_t cc = 1u << caplog;
   for (uint32_t i = 0; i < cc; ++i) {
     edges[nb + i] = EMPTY_SLOT;
@@ -415,66 +459,80 @@ bool LiveTrie::relocate(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot&
   for (uint32_t q : ovf_at) edges[nb + q].meta |= META_BUCKET_OVF;
   const uint32_t smeta = (caplog & META_CAPLOG2_MASK) | META_HAS_EDGES | (has_plus ? META_HAS_PLUS : 0u) |
                          (ph ? META_PH : 0u) | (seed << META_SEED_SHIFT);
-  set_node(root, pslot, static_cast<uint32_t>(nb), smeta);
-  garbage += ocap;
-  relocations += 1;
+  set_node(cx, root, pslot, static_cast<uint32_t>(nb), smeta);
+  cx.garbage += ocap;
+  cx.relocations += 1;
   return true;
 }
 
-bool LiveTrie::apply(const FilterStore& fs, uint32_t id) {
-  if (loc.size() < fs.n_ids()) loc.resize(fs.n_ids(), FIDLOC_NONE);
-  const bool want = fs.live[id] != 0;
+// Delete / revival of a filter already in the table: its flag in the slot of its node.
+void LiveTrie::flip(Ctx& c, uint32_t id, bool want, bool atomic) {
   const uint64_t l = loc[id];
-  if (l != FIDLOC_NONE) {  // in the trie: flag flip (delete / revival)
-    if (l == FIDLOC_ROOT_HASH) {
-      root_meta = want ? (root_meta | META_HAS_HASH) : (root_meta & ~META_HAS_HASH);
-    } else {
-      const uint64_t p = l >> 2;
-      const uint32_t bit = (l & 3) == FIDLOC_HASH ? META_HAS_HASH : META_HAS_TERM;
-      if (((edges[p].meta & bit) != 0) != want) {
-        edges[p].meta ^= bit;
-        touch(p);
-      }
-    }
-    flips += 1;
-    return true;
+  c.flips += 1;
+  if (l == FIDLOC_ROOT_HASH) {  // serial only
+    root_meta = want ? (root_meta | META_HAS_HASH) : (root_meta & ~META_HAS_HASH);
+    return;
   }
-  if (!want) return true;
+  const uint64_t p = l >> 2;
+  const uint32_t bit = (l & 3) == FIDLOC_HASH ? META_HAS_HASH : META_HAS_TERM;
+  if (((edges[p].meta & bit) != 0) == want) return;
+  if (atomic) {  // the hash and the term filter of one node may flip on two threads
+    if (want) __atomic_fetch_or(&edges[p].meta, bit, __ATOMIC_RELAXED);
+    else __atomic_fetch_and(&edges[p].meta, ~bit, __ATOMIC_RELAXED);
+  } else {
+    edges[p].meta ^= bit;
+  }
+  touch(c, p);
+}
 
-  // tokenize (emqx_topic:words/1); a final '#' is the parent level's hash filter
+// emqx_topic:words/1 (emqx_topic.erl:153-164) to word ids; a final '#' is the parent level's
+// hash filter.  intern = false: read-only lookups (thread-safe), unknown words -> WID_UNKNOWN.
+bool LiveTrie::tokenize(const FilterStore& fs, uint32_t id, std::vector<uint32_t>& w, bool* wild,
+                        bool* final_hash, bool intern) const {
   const uint8_t* p = fs.bytes.data() + fs.off[id];
   const uint64_t n = fs.off[id + 1] - fs.off[id];
-  std::vector<uint32_t> w;
-  bool wild = false, final_hash = false;
+  w.clear();
+  *wild = *final_hash = false;
+  bool unknown = false;
   uint64_t s = 0;
   for (uint64_t i = 0; i <= n; ++i) {
     if (i != n && p[i] != '/') continue;
     const uint64_t len = i - s;
     if (len == 1 && p[s] == '+') {
       w.push_back(WID_PLUS);
-      wild = true;
+      *wild = true;
     } else if (len == 1 && p[s] == '#') {
-      wild = true;
-      if (i == n) final_hash = true;
+      *wild = true;
+      if (i == n) *final_hash = true;
       else w.push_back(WID_HASH);
-    } else {
+    } else if (intern) {
       w.push_back(vocab->intern(p + s, len));
+    } else {
+      const VocabState& v = *vocab;
+      auto res = [&v](uint32_t k, const uint8_t*& q, uint64_t& m) {
+        q = v.arena.data() + v.off[k];
+        m = v.off[k + 1] - v.off[k];
+      };
+      const uint32_t k = v.map.find(p + s, len, hash64_bytes(p + s, len), res);
+      unknown |= k == WID_NONE;
+      w.push_back(k == WID_NONE ? WID_UNKNOWN : k);
     }
     s = i + 1;
   }
+  return !unknown;
+}
+
+bool LiveTrie::insert(Ctx& c, const FilterStore& fs, uint32_t id, const std::vector<uint32_t>& w, bool wild,
+                      bool final_hash, bool root, uint64_t pslot, uint32_t i) {
   const uint32_t ext = fs.ext[id];
   const uint32_t L = static_cast<uint32_t>(w.size());
-
-  bool root = true;
-  uint64_t pslot = 0;
-  uint32_t i = 0;
   for (; i < L; ++i) {
     const uint32_t base = root ? root_base : edges[pslot].child_base;
     const uint32_t meta = root ? root_meta : edges[pslot].meta;
-    uint32_t c;
-    if (!find_child(base, meta, w[i], &c)) break;
+    uint32_t ch;
+    if (!find_child(base, meta, w[i], &ch)) break;
     root = false;
-    pslot = c;
+    pslot = ch;
   }
   if (i == L) {  // the filter's node exists: set its id and flag
     if (final_hash && root) {
@@ -496,7 +554,7 @@ bool LiveTrie::apply(const FilterStore& fs, uint32_t id) {
       sl.meta |= META_HAS_TERM | (wild ? META_TERM_WILD : 0u);
       loc[id] = pslot << 2 | FIDLOC_TERM;
     }
-    reencode(pslot);
+    reencode(c, pslot);
     return true;
   }
 
@@ -508,7 +566,7 @@ bool LiveTrie::apply(const FilterStore& fs, uint32_t id) {
   uint32_t cfh = fh, cft = ft, cih = ih, cit = it;
   for (uint32_t j = L - 1; j > i; --j) {  // node at depth j holds the edge w[j]
     uint64_t nb = 0;
-    if (!alloc(1, &nb)) return false;
+    if (!alloc(c, 1, &nb)) return false;
     const bool plus = w[j] == WID_PLUS;
     const uint32_t at = plus ? 0u : lit_slot(w[j], 0, 1);
     edges[nb] = edges[nb + 1] = EMPTY_SLOT;
@@ -528,12 +586,153 @@ bool LiveTrie::apply(const FilterStore& fs, uint32_t id) {
     cur = encode(w[j - 1], true, static_cast<uint32_t>(nb), sm, FID_NONE, FID_NONE, 0);
     cfh = cft = FID_NONE;
     cih = cit = WID_NONE;
-    n_nodes += 1;
+    c.nodes += 1;
   }
-  n_nodes += 1;
-  max_depth = std::max(max_depth, L);
-  chains += 1;
-  return place(root, pslot, w[i], cur, cfh, cft, cih, cit);
+  c.nodes += 1;
+  c.max_depth = std::max(c.max_depth, L);
+  c.chains += 1;
+  return place(c, root, pslot, w[i], cur, cfh, cft, cih, cit);
+}
+
+bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, int threads) {
+  mark = used;
+  dirty.clear();
+  ranges.clear();
+  relocations = in_place = chains = flips = 0;
+  if (loc.size() < fs.n_ids()) loc.resize(fs.n_ids(), FIDLOC_NONE);
+  threads = std::max(1, threads);
+  std::vector<uint32_t> fl, ins;
+  for (uint32_t id : ids) {
+    if (loc[id] != FIDLOC_NONE) fl.push_back(id);
+    else if (fs.live[id]) ins.push_back(id);
+  }
+  std::vector<Ctx> cx(threads);
+  auto run = [&](uint64_t n, auto&& body) {  // body(ctx, i) over [0, n) on up to `threads` threads
+    const int t = static_cast<int>(std::min<uint64_t>(threads, (n + 255) / 256));
+    if (t <= 1) {
+      for (uint64_t i = 0; i < n; ++i) body(cx[0], i);
+      return;
+    }
+    std::vector<std::thread> th;
+    for (int k = 0; k < t; ++k)
+      th.emplace_back([&, k] {
+        for (uint64_t i = n * k / t; i < n * (k + 1) / t; ++i) body(cx[k], i);
+      });
+    for (auto& x : th) x.join();
+  };
+
+  // 1. flips (the root's '#' filter serially)
+  for (uint32_t id : fl)
+    if (loc[id] == FIDLOC_ROOT_HASH) flip(cx[0], id, fs.live[id] != 0, false);
+  run(fl.size(), [&](Ctx& c, uint64_t i) {
+    const uint32_t id = fl[i];
+    if (loc[id] != FIDLOC_ROOT_HASH) flip(c, id, fs.live[id] != 0, true);
+  });
+
+  // 2. tokenize (read-only vocab lookups in parallel; unknown words interned serially)
+  const uint64_t ni = ins.size();
+  std::vector<uint64_t> woff(ni + 1, 0);
+  std::vector<uint8_t> flags(ni, 0);  // bit 0 wild, bit 1 final '#', bit 2 unknown words
+  std::vector<std::vector<uint32_t>> wl(ni);
+  run(ni, [&](Ctx&, uint64_t k) {
+    bool wild, fh;
+    const bool known = tokenize(fs, ins[k], wl[k], &wild, &fh, false);
+    flags[k] = (wild ? 1 : 0) | (fh ? 2 : 0) | (known ? 0 : 4);
+  });
+  for (uint64_t k = 0; k < ni; ++k)
+    if (flags[k] & 4) {
+      bool wild, fh;
+      tokenize(fs, ins[k], wl[k], &wild, &fh, true);
+    }
+
+  // 3. inserts that change the root (a new first-level edge, or the filter '#'), serially
+  Ctx& c0 = cx[0];
+  if (c0.ranges.empty()) c0.cur = c0.end = 0;
+  std::vector<uint8_t> done(ni, 0);
+  for (uint64_t k = 0; k < ni; ++k) {
+    uint32_t ch;
+    if (wl[k].empty() || !find_child(root_base, root_meta, wl[k][0], &ch)) {
+      if (!insert(c0, fs, ins[k], wl[k], flags[k] & 1, flags[k] & 2, true, 0, 0)) return false;
+      done[k] = 1;
+    }
+  }
+  // 4. the rest grouped by first-level node, groups dealt to threads (largest first)
+  std::vector<std::pair<uint32_t, uint32_t>> key;  // (first-level slot, insert)
+  key.reserve(ni);
+  for (uint64_t k = 0; k < ni; ++k) {
+    if (done[k]) continue;
+    uint32_t ch = 0;
+    find_child(root_base, root_meta, wl[k][0], &ch);
+    key.push_back({ch, static_cast<uint32_t>(k)});
+  }
+  std::sort(key.begin(), key.end());
+  std::vector<std::pair<uint64_t, uint64_t>> groups;  // [begin, end) in key
+  for (uint64_t a = 0; a < key.size();) {
+    uint64_t b = a;
+    while (b < key.size() && key[b].first == key[a].first) ++b;
+    groups.push_back({a, b});
+    a = b;
+  }
+  const int t = static_cast<int>(std::min<uint64_t>(threads, std::max<uint64_t>(1, key.size() / 512)));
+  std::vector<std::vector<uint32_t>> mine(t);
+  {
+    std::vector<uint64_t> load(t, 0);
+    std::vector<uint32_t> order(groups.size());
+    for (uint32_t g = 0; g < groups.size(); ++g) order[g] = g;
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+      return groups[x].second - groups[x].first > groups[y].second - groups[y].first;
+    });
+    for (uint32_t g : order) {
+      const int k = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+      mine[k].push_back(g);
+      load[k] += groups[g].second - groups[g].first;
+    }
+  }
+  auto work = [&](int k) {
+    Ctx& c = cx[k];
+    for (uint32_t g : mine[k])
+      for (uint64_t j = groups[g].first; j < groups[g].second && !c.failed; ++j) {
+        const uint32_t q = key[j].second;
+        if (!insert(c, fs, ins[q], wl[q], flags[q] & 1, flags[q] & 2, false, key[j].first, 1)) c.failed = true;
+      }
+  };
+  if (t <= 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int k = 0; k < t; ++k) th.emplace_back(work, k);
+    for (auto& x : th) x.join();
+  }
+
+  // 5. merge
+  bool ok = true;
+  for (Ctx& c : cx) {
+    ok &= !c.failed;
+    dirty.insert(dirty.end(), c.dirty.begin(), c.dirty.end());
+    for (auto& r : c.ranges)
+      if (r.second > r.first) ranges.push_back(r);
+    garbage += c.garbage + (c.end - c.cur);
+    relocations += c.relocations;
+    in_place += c.in_place;
+    chains += c.chains;
+    flips += c.flips;
+    n_nodes += c.nodes;
+    max_depth = std::max(max_depth, c.max_depth);
+  }
+  std::sort(ranges.begin(), ranges.end());
+  std::vector<std::pair<uint64_t, uint64_t>> merged;
+  for (auto& r : ranges) {
+    if (!merged.empty() && merged.back().second == r.first) merged.back().second = r.second;
+    else merged.push_back(r);
+  }
+  ranges.swap(merged);
+  return ok;
+}
+
+uint64_t LiveTrie::new_slots() const {
+  uint64_t n = 0;
+  for (auto& r : ranges) n += r.second - r.first;
+  return n;
 }
 
 void LiveTrie::patches(std::vector<SlotPatch>& out) const {

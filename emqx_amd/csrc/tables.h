@@ -3,6 +3,7 @@
 
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -133,47 +134,78 @@ bool check_tables(const HostTables& t, std::string* err);
 // churn, not to the table or to earlier commits.  Deletes / revivals flip the filter's flag in
 // its slot.  A full rebuild (compaction) runs when the spare region is used up.
 struct LiveTrie {
+  struct Entry {
+    uint32_t wid;
+    EdgeSlot s;  // slot content without the position's META_BUCKET_OVF bit
+    uint32_t fh, ft, ih, it;
+  };
+  // Per-thread state of a commit: spare-region chunk, line packer, rewritten slots, counters,
+  // scratch.  Inserts under different first-level nodes touch disjoint parts of the table, so
+  // a commit runs them on several threads, one Ctx each.
+  struct Ctx {
+    uint64_t cur = 0, end = 0;          // current chunk of the spare region [cur, end)
+    uint64_t line = 0;
+    uint32_t line_used = 0xFFu;
+    std::vector<std::pair<uint64_t, uint64_t>> ranges;  // allocated extents (uploaded whole)
+    std::vector<uint32_t> dirty;        // slots < mark rewritten in place (may repeat)
+    uint64_t relocations = 0, in_place = 0, chains = 0, flips = 0, nodes = 0, garbage = 0;
+    uint32_t max_depth = 0;
+    bool failed = false;                // spare region exhausted
+    std::vector<Entry> ent;
+    std::vector<uint32_t> pos, w;
+  };
+
   std::vector<EdgeSlot> edges;  // host image of device slots [0, cap)
   std::vector<uint32_t> fids;   // 2 per slot (reported ids)
   std::vector<uint32_t> sid;    // 2 per slot (engine ids, for fid_loc upkeep)
-  uint64_t used = 0, cap = 0;   // append cursor / capacity in slots
+  uint64_t used = 0, cap = 0;   // spare-region cursor / capacity in slots
   uint64_t garbage = 0;         // slots of arrays superseded by relocations
-  uint64_t line = 0;            // open 128-B line of the small-array packer
-  uint32_t line_used = 0xFFu;
   uint32_t root_base = 0, root_meta = 0, root_hash_fid = FID_NONE, root_hash_id = WID_NONE;
   uint64_t n_nodes = 0;
   uint32_t max_depth = 0;
   std::vector<uint64_t> loc;    // per engine id: FIDLOC (tables.h)
   VocabState* vocab = nullptr;
   // per commit
-  uint64_t mark = 0;            // `used` when the commit began: [mark, used) is uploaded whole
+  uint64_t mark = 0;            // `used` when the commit began: slots >= mark are new
   std::vector<uint32_t> dirty;  // slots < mark rewritten in place (may repeat)
+  std::vector<std::pair<uint64_t, uint64_t>> ranges;  // new extents [begin, end) to upload
   uint64_t relocations = 0, in_place = 0, chains = 0, flips = 0;
 
   // Adopts a full build (moves its arrays) and reserves `spare` slots behind it.
   void adopt(HostTables& ht, std::vector<uint64_t>& fid_loc, std::vector<uint32_t>& slot_ids, uint64_t spare,
              VocabState* v);
-  void begin_commit();
-  // Brings filter `id` in line with fs.live[id]: flag flip, or insertion of a new filter.
-  // False when the spare region is exhausted (the caller then does a full rebuild).
-  bool apply(const FilterStore& fs, uint32_t id);
-  // The commit's device writes: slot patches (deduplicated) for slots < mark.
+  // Publishes the changes of `ids` (each brought in line with fs.live[id]: flag flip, or
+  // insertion of a new filter) on up to `threads` threads.  False when the spare region is
+  // exhausted (the caller then does a full rebuild).
+  bool commit(const FilterStore& fs, const std::vector<uint32_t>& ids, int threads);
+  // The commit's in-place rewrites (deduplicated slot patches for slots < mark).
   void patches(std::vector<SlotPatch>& out) const;
+  uint64_t new_slots() const;
 
  private:
   bool find_child(uint32_t base, uint32_t meta, uint32_t wid, uint32_t* slot) const;
-  bool alloc(uint32_t caplog, uint64_t* at);
-  void touch(uint64_t slot);
+  bool alloc(Ctx& c, uint32_t caplog, uint64_t* at);
+  void touch(Ctx& c, uint64_t slot) const {
+    if (slot < mark) c.dirty.push_back(static_cast<uint32_t>(slot));
+  }
   void lit_summary(uint32_t base, uint32_t meta, uint32_t* n_lit, uint32_t* only, uint32_t* bloom,
                    uint32_t* bloom8) const;
-  EdgeSlot encode(uint32_t wid, bool has_edges, uint32_t base, uint32_t nmeta, uint32_t fid_h, uint32_t fid_t,
-                  uint32_t flags) const;
-  void reencode(uint64_t pslot);
-  void set_node(bool root, uint64_t pslot, uint32_t base, uint32_t nmeta);
-  bool place(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
+  EdgeSlot encode(uint32_t wid, bool has_edges, uint32_t base, uint32_t smeta, uint32_t fid_h, uint32_t fid_t,
+                  uint32_t fmeta) const;
+  void reencode(Ctx& c, uint64_t pslot);
+  void set_node(Ctx& c, bool root, uint64_t pslot, uint32_t base, uint32_t smeta);
+  bool place(Ctx& c, bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
              uint32_t ih, uint32_t it);
-  bool relocate(bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
+  bool relocate(Ctx& c, bool root, uint64_t pslot, uint32_t wid, const EdgeSlot& child, uint32_t fh, uint32_t ft,
                 uint32_t ih, uint32_t it);
+  void flip(Ctx& c, uint32_t id, bool want, bool atomic);
+  // Inserts filter `id` (words w, final '#' flag) starting at the node reached through
+  // `pslot` (or the root) after `i` levels.
+  bool insert(Ctx& c, const FilterStore& fs, uint32_t id, const std::vector<uint32_t>& w, bool wild,
+              bool final_hash, bool root, uint64_t pslot, uint32_t i);
+  bool tokenize(const FilterStore& fs, uint32_t id, std::vector<uint32_t>& w, bool* wild, bool* final_hash,
+                bool intern) const;
+  std::mutex alloc_mu_;
 };
 
 }  // namespace emqx

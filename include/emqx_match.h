@@ -113,9 +113,10 @@ int emqx_filter_name(emqx_engine* e, uint32_t id, uint8_t* buf, uint64_t cap, ui
  * spare region is used up (emqx_set_tuning "delta_max": at most that many filters placed
  * incrementally; "incremental" = 0 forces full rebuilds). */
 int emqx_commit(emqx_engine* e);
-/* Details of the last commit: out[0..7] = kind (0 full, 1 incremental), node relocations,
+/* Details of the last commit: out[0..8] = kind (0 full, 1 incremental), node relocations,
  * edges placed in place, slots rewritten in place, new slots, spare-region cursor, spare-region
- * capacity (slots), slots of superseded arrays. */
+ * capacity (slots), slots of superseded arrays, host microseconds of the last incremental
+ * commit's table patching. */
 int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n);
 
 /* Batched match, host buffers.  out_offsets has n+1 entries.  On EMQX_EOVERFLOW nothing
@@ -237,7 +238,9 @@ int emqx_topic_wildcard(const uint8_t* topic, uint64_t len);
 
 /* Tuning hook (benchmarks / A-B runs).  Keys: "fast_variant" (-1 = automatic, otherwise a
  * fixed kernel variant, see emqx_amd/csrc/kernels.h), "diag" (1 = accumulate the kernel's
- * diagnostic counters).  EMQX_ENOTFOUND for unknown keys. */
+ * diagnostic counters), "incremental" (0 = every commit rebuilds), "delta_max" (filters placed
+ * incrementally before a rebuild, -1 = default policy), "commit_threads" (host threads of an
+ * incremental commit, default min(8, cores)).  EMQX_ENOTFOUND for unknown keys. */
 int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value);
 /* Reads (and optionally resets) the accumulated diagnostic counters (DIAG_* order). */
 int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset);
@@ -250,11 +253,12 @@ int emqx_build_check(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, 
 
 /* Host-only self-check of incremental commits (no device): a filter store + the table builder
  * + the in-place patcher the engine uses, and a host walk of the patched table by the kernels'
- * lookup and emission rules.  spare_slots: the spare region (0 = default); commit(full = 1)
+ * lookup and emission rules.  spare_slots: the spare region (0 = default); threads: commit
+ * threads (as the engine's "commit_threads" tuning key); commit(full = 1)
  * rebuilds; stats8 as emqx_commit_stats.  match supports EMQX_MODE_ROUTES / _TRIE_WILDCARD on
  * non-wildcard topics.  check verifies the lookup invariants of every reachable node. */
 typedef struct emqx_htrie emqx_htrie;
-int emqx_htrie_create(uint64_t spare_slots, emqx_htrie** out);
+int emqx_htrie_create(uint64_t spare_slots, int threads, emqx_htrie** out);
 int emqx_htrie_destroy(emqx_htrie* h);
 int emqx_htrie_insert(emqx_htrie* h, const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t* ids_out);
 int emqx_htrie_delete(emqx_htrie* h, const uint32_t* ids, uint64_t n);

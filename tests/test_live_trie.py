@@ -29,11 +29,11 @@ def pack(items):
 
 
 class HostTrie:
-    def __init__(self, spare=0):
+    def __init__(self, spare=0, threads=1):
         from emqx_amd import _lib
         self.L = _lib.lib()
         self.h = ctypes.c_void_p()
-        assert self.L.emqx_htrie_create(spare, ctypes.byref(self.h)) == 0
+        assert self.L.emqx_htrie_create(spare, threads, ctypes.byref(self.h)) == 0
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -222,4 +222,39 @@ def test_commit_work_is_proportional_to_churn():
     got = m.t.match(W.unpack(wl.topics))
     off_g = np.concatenate([[0], np.cumsum([len(g) for g in got])])
     ids_g = np.array([x for g in got for x in g], dtype=np.uint32)
+    assert C.csr_mismatches(off_g, ids_g, off_o, ids_o).size == 0
+
+
+def test_threaded_commits_equal_oracle():
+    """Commits large enough to run on several threads (flips in parallel, inserts grouped by
+    first-level node): every topic of a config-B batch equals the C++ oracle over the live set,
+    and the patched table equals the same churn applied on one thread."""
+    from emqx_amd import workloads as W
+    from oracle import cpp as C
+    wl = W.config_b(n_filters=40_000, n_topics=3000, seed=23)
+    names = W.unpack(wl.filters)
+    ms = [Model(HostTrie(spare=1 << 22, threads=t)) for t in (1, 6)]
+    for m in ms:
+        m.insert(names[:20_000])
+        m.t.commit()
+    rng = np.random.default_rng(9)
+    nxt = 20_000
+    for r in range(4):
+        live = [i for i, v in ms[0].live.items() if v]
+        dels = sorted(int(i) for i in rng.choice(live, 3000, replace=False))
+        for m in ms:
+            m.delete(dels)
+            m.insert(names[nxt:nxt + 5000] + [b"new%d/+/x" % (r * 10 + j) for j in range(5)])
+            assert m.t.commit()["kind"] == 1
+        nxt += 5000
+    topics = W.unpack(wl.topics)
+    outs = [m.t.match(topics) for m in ms]
+    assert outs[0] == outs[1]
+    m = ms[1]
+    m.t.check()
+    o = C.CppOracle(True)
+    o.add([f if m.live.get(i) else b"\x00dead/%d" % i for i, f in enumerate(m.names)])
+    off_o, ids_o, _ = o.match_csr(*wl.topics, mode=C.MODE_ROUTES, threads=4)
+    off_g = np.concatenate([[0], np.cumsum([len(g) for g in outs[1]])])
+    ids_g = np.array([x for g in outs[1] for x in g], dtype=np.uint32)
     assert C.csr_mismatches(off_g, ids_g, off_o, ids_o).size == 0
