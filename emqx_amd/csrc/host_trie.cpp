@@ -18,7 +18,18 @@
 
 using namespace emqx;
 
+// The table as the device holds it: written only the way the engine writes device memory
+// (the full build's slots; per incremental commit the new extents and the slot patches), so the
+// host walk below sees exactly what the kernels would.
+struct DevImage {
+  std::vector<EdgeSlot> edges;
+  std::vector<uint32_t> fids;
+  uint32_t root_base = 0, root_meta = 0, root_hash_fid = FID_NONE;
+  uint64_t used = 0;
+};
+
 struct emqx_htrie {
+  DevImage dev;
   FilterStore fs;
   std::unique_ptr<VocabState> vocab;
   LiveTrie lt;
@@ -43,20 +54,26 @@ void full_build(emqx_htrie* h) {
   std::string err;
   build_tables(h->fs, o, ht, &err);
   const uint64_t spare = h->spare ? h->spare : std::max<uint64_t>(1u << 16, ht.edges.size() / 2);
+  h->dev.edges.assign(ht.edges.size() + spare, EdgeSlot{WID_NONE, 0, 0, 0});
+  h->dev.fids.assign(2 * (ht.edges.size() + spare), FID_NONE);
+  std::copy(ht.edges.begin(), ht.edges.end(), h->dev.edges.begin());
+  std::copy(ht.fids.begin(), ht.fids.end(), h->dev.fids.begin());
   h->lt.adopt(ht, loc, sids, spare, h->vocab.get());
+  h->dev.edges.resize(h->lt.cap);
+  h->dev.fids.resize(2 * h->lt.cap);
   h->built = true;
   h->kind = 0;
   h->dirty.clear();
 }
 
-uint32_t hash_id_of(const LiveTrie& t, uint64_t c) {
+uint32_t hash_id_of(const DevImage& t, uint64_t c) {
   const EdgeSlot& s = t.edges[c];
   if (!(s.meta & META_HAS_EDGES)) return s.child_base;
   if ((s.meta & META_XFID) && !(s.meta & META_XFID_TERM)) return s.litf;
   return t.fids[2 * c];
 }
 
-uint32_t term_id_of(const LiveTrie& t, uint64_t c) {
+uint32_t term_id_of(const DevImage& t, uint64_t c) {
   const EdgeSlot& s = t.edges[c];
   if (!(s.meta & META_HAS_EDGES)) return s.litf;
   if ((s.meta & META_XFID) && (s.meta & META_XFID_TERM)) return s.litf;
@@ -64,7 +81,7 @@ uint32_t term_id_of(const LiveTrie& t, uint64_t c) {
 }
 
 // Lookup by the kernel's rule (match_kernels.hip probe_one).
-bool probe(const LiveTrie& t, uint32_t base, uint32_t meta, uint32_t wid, uint64_t* out) {
+bool probe(const DevImage& t, uint32_t base, uint32_t meta, uint32_t wid, uint64_t* out) {
   if (wid == WID_PLUS) {
     *out = base;
     return t.edges[base].wid == WID_PLUS;
@@ -99,7 +116,7 @@ struct Item {
 // Level-by-level frontier walk of one non-wildcard topic (emqx_trie.erl:272-334 semantics):
 // every reached node emits its '#' filter, the last level emits terminal filters (all of them
 // in ROUTES mode, wildcard ones in TRIE_WILDCARD mode); '$' topics skip the root's '+' and '#'.
-void walk(const LiveTrie& t, const VocabState& v, const uint8_t* p, uint64_t n, uint32_t mode,
+void walk(const DevImage& t, const VocabState& v, const uint8_t* p, uint64_t n, uint32_t mode,
           std::vector<uint32_t>& out) {
   std::vector<uint32_t> w;
   uint64_t s = 0;
@@ -145,7 +162,7 @@ void walk(const LiveTrie& t, const VocabState& v, const uint8_t* p, uint64_t n, 
 
 // Lookup invariants of every node reachable from the root (garbage arrays left behind by
 // relocations are not checked: nothing reaches them).
-bool check(const LiveTrie& t, std::string* err) {
+bool check(const DevImage& t, std::string* err) {
   std::vector<Item> st;
   if (t.root_meta & META_HAS_EDGES) st.push_back({t.root_base, t.root_meta, ~0u, true});
   while (!st.empty()) {
@@ -249,9 +266,28 @@ int emqx_htrie_commit(emqx_htrie* h, int full, uint64_t* stats8) {
     ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
     const bool ok = h->lt.commit(h->fs, ids, h->threads);
     h->kind = 1;
-    if (!ok) full_build(h);  // spare region exhausted
+    if (ok) {  // the engine's device writes: new extents, then filter ids, then slots
+      for (const auto& r : h->lt.ranges) {
+        std::copy(h->lt.edges.begin() + r.first, h->lt.edges.begin() + r.second, h->dev.edges.begin() + r.first);
+        std::copy(h->lt.fids.begin() + 2 * r.first, h->lt.fids.begin() + 2 * r.second,
+                  h->dev.fids.begin() + 2 * r.first);
+      }
+      std::vector<SlotPatch> p;
+      h->lt.patches(p);
+      for (const SlotPatch& q : p) {
+        h->dev.fids[2 * uint64_t(q.slot)] = q.fid_h;
+        h->dev.fids[2 * uint64_t(q.slot) + 1] = q.fid_t;
+      }
+      for (const SlotPatch& q : p) h->dev.edges[q.slot] = q.s;
+    } else {
+      full_build(h);  // spare region exhausted
+    }
     h->dirty.clear();
   }
+  h->dev.root_base = h->lt.root_base;  // the snapshot's table view
+  h->dev.root_meta = h->lt.root_meta;
+  h->dev.root_hash_fid = h->lt.root_hash_fid;
+  h->dev.used = h->lt.used;
   if (stats8) {
     std::vector<SlotPatch> p;
     h->lt.patches(p);
@@ -270,7 +306,7 @@ int emqx_htrie_match(emqx_htrie* h, uint32_t mode, const uint8_t* topic_bytes, c
   out_offsets[0] = 0;
   for (uint64_t i = 0; i < n; ++i) {
     one.clear();
-    walk(h->lt, *h->vocab, topic_bytes + topic_offsets[i], topic_offsets[i + 1] - topic_offsets[i], mode, one);
+    walk(h->dev, *h->vocab, topic_bytes + topic_offsets[i], topic_offsets[i + 1] - topic_offsets[i], mode, one);
     acc.insert(acc.end(), one.begin(), one.end());
     out_offsets[i + 1] = acc.size();
   }
@@ -283,7 +319,7 @@ int emqx_htrie_match(emqx_htrie* h, uint32_t mode, const uint8_t* topic_bytes, c
 int emqx_htrie_check(emqx_htrie* h, char* err, uint64_t err_cap) {
   if (!h || !h->built) return EMQX_EINVAL;
   std::string e;
-  const bool ok = check(h->lt, &e);
+  const bool ok = check(h->dev, &e);
   if (!ok && err && err_cap) {
     strncpy(err, e.c_str(), err_cap - 1);
     err[err_cap - 1] = 0;

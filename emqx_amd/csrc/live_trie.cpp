@@ -114,7 +114,7 @@ bool LiveTrie::alloc(Ctx& c, uint32_t caplog, uint64_t* at) {
       const uint64_t a = (c.cur + LINE - 1) & ~uint64_t(LINE - 1);
       if (a + n <= c.end) {
         c.cur = a + n;
-        c.ranges.back().second = c.cur;
+        c.ranges[c.chunk_range].second = c.cur;
         c.line_used = FULL_LINE;
         *at = a;
         return true;
@@ -131,7 +131,7 @@ bool LiveTrie::alloc(Ctx& c, uint32_t caplog, uint64_t* at) {
       if (l + LINE <= c.end) {
         c.line = l;
         c.cur = l + LINE;
-        c.ranges.back().second = c.cur;
+        c.ranges[c.chunk_range].second = c.cur;
         c.line_used = want;
         *at = l;
         return true;
@@ -150,6 +150,7 @@ bool LiveTrie::alloc(Ctx& c, uint32_t caplog, uint64_t* at) {
     c.cur = a;
     c.end = a + len;
     c.line_used = FULL_LINE;
+    c.chunk_range = c.ranges.size();
     c.ranges.push_back({a, a});
   }
   return false;

@@ -147,6 +147,7 @@ struct LiveTrie {
     uint64_t line = 0;
     uint32_t line_used = 0xFFu;
     std::vector<std::pair<uint64_t, uint64_t>> ranges;  // allocated extents (uploaded whole)
+    size_t chunk_range = 0;             // ranges[chunk_range] is the current chunk's extent
     std::vector<uint32_t> dirty;        // slots < mark rewritten in place (may repeat)
     uint64_t relocations = 0, in_place = 0, chains = 0, flips = 0, nodes = 0, garbage = 0;
     uint32_t max_depth = 0;
