@@ -83,6 +83,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (default 0: every host core this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-api", action="store_true", help="skip the host-buffer (PCIe-inclusive) rates")
     ap.add_argument("--cache", type=str, default=None,
                     help="npz path: reuse the generated workload across runs (profiling passes)")
     ap.add_argument("--ab", type=str, default=None,
@@ -90,13 +91,19 @@ def main():
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
-    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R"],
+    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R", "L"],
                     help="B = the headline (BASELINE configs[1]); A = configs[0]'s 100k-filter table, "
                          "D = the adversarial depth-16 table (configs[3], 1M-topic batches), "
                          "E = publish fan-out (configs[4]): match + fan-out per step, "
                          "U = route updates (SURVEY §8 f2): subscribe/unsubscribe churn + incremental "
                          "commits on config B's table, R = retained-message lookup (SURVEY §8 f4): a batch "
-                         "of subscription filters against 1M stored retained topics")
+                         "of subscription filters against 1M stored retained topics, L = the drop-in "
+                         "per-PUBLISH path: concurrent single-topic callers through the batcher on config "
+                         "B's table")
+    ap.add_argument("--callers", type=str, default="64,512,4096",
+                    help="--workload L: concurrent single-topic callers per run")
+    ap.add_argument("--max-batch", type=int, default=4096, help="--workload L: batcher max_batch")
+    ap.add_argument("--max-wait-us", type=int, default=200, help="--workload L: batcher max_wait_us")
     ap.add_argument("--retained", type=int, default=1_000_000, help="--workload R: stored retained topics")
     ap.add_argument("--churn", type=int, default=10_000, help="--workload U: inserts and deletes per commit")
     ap.add_argument("--with-matches", action="store_true",
@@ -149,6 +156,8 @@ def main():
         return update_bench(args, rank, world, dev)
     if args.workload == "R":
         return retain_bench(args, rank, world, dev)
+    if args.workload == "L":
+        return batcher_bench(args, rank, world, dev)
     if args.workload == "A":
         wl = load_or_make(args, rank, lambda: W.config_a(n_topics=args.batch, seed=1 if rank == 0 else 1000 + rank))
     elif args.workload == "D":
@@ -289,6 +298,9 @@ def main():
         "roofline": roofline,
     }
 
+    if world == 1 and not args.no_host_api:
+        result["host_api"] = host_api_rates(eng, wl, args, nout)
+
     if args.diag:
         eng.set_tuning("diag", 1)
         eng.diag(reset=True)
@@ -399,6 +411,107 @@ def measured_traffic(n, args):
         p = json.load(f)
     per_topic = p["traffic_bytes_per_launch"] / p["batch_topics"]
     return round(per_topic * n), "profiles/%s (%s; %s)" % (fname, p["traffic_rule"], p["source"])
+
+
+def host_api_rates(eng, wl, args, nout):
+    """The same batch through the host-memory entry points (PCIe included; never `value`):
+    emqx_match_batch from pageable numpy buffers (chunks staged through two pinned host
+    batches), and pinned host batches (emqx_host_batch_*, the NIF's buffers) with four
+    quarter-batches in flight."""
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import HostBatch
+    n = wl.n_topics
+    tb, to = wl.topics
+    out_off = np.zeros(n + 1, dtype=np.uint64)
+    reps = 5
+    off, ids = eng.match_packed(tb, to, mode=args.mode)  # sizes the pool's buffers
+    if int(off[-1]) != nout:
+        raise SystemExit(f"host API total {int(off[-1])} != device total {nout}")
+    t = time.perf_counter()
+    for _ in range(reps):
+        eng.match_packed(tb, to, mode=args.mode)
+    pageable = reps * n / (time.perf_counter() - t)
+    q = 4
+    parts = [W.take(wl.topics, np.arange(n * k // q, n * (k + 1) // q)) for k in range(q)]
+    hbs = []
+    for p_ in parts:
+        hb = HostBatch(eng, cap_topics=len(p_[1]), cap_bytes=int(p_[1][-1]) + 64, cap_ids=4 * nout // q + (1 << 20))
+        hb.pack(*p_)
+        hbs.append(hb)
+    tot = 0
+    for hb in hbs:
+        hb.submit(args.mode)
+    for hb in hbs:
+        tot += int(hb.wait(copy=False)[0][-1])
+    if tot != nout:
+        raise SystemExit(f"pinned host batches total {tot} != device total {nout}")
+    t = time.perf_counter()
+    for _ in range(reps):
+        for hb in hbs:
+            hb.submit(args.mode)
+        for hb in hbs:
+            hb.wait(copy=False)
+    pinned = reps * n / (time.perf_counter() - t)
+    for hb in hbs:
+        hb.close()
+    in_b = int(to[-1] - to[0]) + 8 * (n + 1)
+    out_b = 8 * (n + 1) + 4 * nout
+    return {"pageable_emqx_match_batch_topics_per_s": round(pageable, 1),
+            "pinned_host_batches_topics_per_s": round(pinned, 1),
+            "bytes_in_per_batch": in_b, "bytes_out_per_batch": out_b,
+            "pinned_pcie_gb_per_s": round((in_b + out_b) * pinned / n / 1e9, 2),
+            "note": "same 1M-topic batch from host memory: H2D + match + CSR back to host; pinned = 4 "
+                    "quarter-batches in flight (emqx_host_batch_*), pageable = emqx_match_batch on numpy "
+                    "arrays (2 pinned chunk buffers inside)"}
+
+
+def batcher_bench(args, rank, world, dev):
+    """The drop-in per-PUBLISH path (emqx_broker.erl:213 -> emqx_router:match_routes/1 per
+    message): C concurrent single-topic callers in a closed loop through the cross-caller
+    batcher (emqx_batcher_*, two pinned batches in flight) on config B's 10M-filter table.
+    tools/batch_load.cpp drives the callers natively; per C: topics/s and latency
+    percentiles (submit -> ids delivered to the caller's callback)."""
+    import ctypes
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    t0 = time.time()
+    with progress(f"[rank {rank}] generating workload"):
+        wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=2,
+                                                         topic_seed=None if rank == 0 else 1000 + rank))
+    eng = Engine(dev.index)
+    with progress(f"[rank {rank}] building table"):
+        eng.insert_packed(*wl.filters)
+        eng.commit()
+    log(f"[rank {rank}] table ready ({time.time() - t0:.1f}s)")
+    L = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libbatchload.so"))
+    L.batch_load.restype = ctypes.c_int
+    L.batch_load.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, ctypes.c_double,
+                             ctypes.c_void_p]
+    tb, to = wl.topics
+    to = np.ascontiguousarray(to.astype(np.uint64))
+    runs = []
+    for c in [int(x) for x in args.callers.split(",")]:
+        out = np.zeros(8, dtype=np.float64)
+        rc = L.batch_load(eng._h, args.mode, tb.ctypes.data, to.ctypes.data, wl.n_topics, c, args.max_batch,
+                          args.max_wait_us, 500.0, 3000.0, out.ctypes.data)
+        if rc != 0:
+            raise SystemExit(f"batch_load failed: {rc}")
+        runs.append({"callers": c, "topics_per_s": round(out[0] / out[1], 1), "p50_us": round(out[2], 1),
+                     "p90_us": round(out[3], 1), "p99_us": round(out[4], 1), "max_us": round(out[5], 1),
+                     "batches": int(out[6]), "topics_per_batch": round(out[7], 1)})
+        log(f"[rank {rank}] callers {c}: {runs[-1]}")
+    best = max(runs, key=lambda r: r["topics_per_s"])
+    res = {"metric": "per-PUBLISH match_routes/1 calls served/sec through the batcher (10M subs)",
+           "value": best["topics_per_s"], "unit": "topics/s", "n_gpus": world, "steps": len(runs),
+           "warmup": 1, "ms_per_step": 3000.0, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+           "config": {"workload": "L: concurrent single-topic callers -> emqx_batcher -> pinned host batches, "
+                                  "config B table", "n_filters": wl.n_filters, "max_batch": args.max_batch,
+                      "max_wait_us": args.max_wait_us, "parallelism": "replicated table"},
+           "runs": runs}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
 
 
 def gather_ceiling():

@@ -36,6 +36,8 @@ EXPORTS = (
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
     "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
+    "emqx_host_batch_create", "emqx_host_batch_destroy", "emqx_host_batch_reserve", "emqx_host_batch_submit",
+    "emqx_host_batch_wait", "emqx_host_batch_query",
     "emqx_commit_stats", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
     "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check",
 )
@@ -88,6 +90,16 @@ class RetainStats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class HostBatchStruct(ctypes.Structure):
+    """struct emqx_host_batch (include/emqx_match.h): pinned buffers of one host batch."""
+    _fields_ = [
+        ("topic_bytes", ctypes.POINTER(ctypes.c_uint8)), ("topic_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("cap_topics", ctypes.c_uint64), ("cap_bytes", ctypes.c_uint64), ("n", ctypes.c_uint64),
+        ("out_offsets", ctypes.POINTER(ctypes.c_uint64)), ("out_ids", ctypes.POINTER(ctypes.c_uint32)),
+        ("cap_ids", ctypes.c_uint64), ("n_out", ctypes.c_uint64), ("priv", ctypes.c_void_p),
+    ]
 
 
 BATCH_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64)
@@ -150,6 +162,12 @@ def lib():
                                                  ctypes.POINTER(u64), vp]),
         "emqx_retain_stats_get": (i32, [vp, ctypes.POINTER(RetainStats)]),
         "emqx_commit_stats": (i32, [vp, vp, u32]),
+        "emqx_host_batch_create": (i32, [vp, u64, u64, u64, ctypes.POINTER(ctypes.POINTER(HostBatchStruct))]),
+        "emqx_host_batch_destroy": (i32, [ctypes.POINTER(HostBatchStruct)]),
+        "emqx_host_batch_reserve": (i32, [ctypes.POINTER(HostBatchStruct), u64, u64, u64]),
+        "emqx_host_batch_submit": (i32, [ctypes.POINTER(HostBatchStruct), u32]),
+        "emqx_host_batch_wait": (i32, [ctypes.POINTER(HostBatchStruct)]),
+        "emqx_host_batch_query": (i32, [ctypes.POINTER(HostBatchStruct)]),
         "emqx_htrie_create": (i32, [u64, i32, ctypes.POINTER(vp)]),
         "emqx_htrie_destroy": (i32, [vp]),
         "emqx_htrie_insert": (i32, [vp, vp, vp, u64, vp]),

@@ -2,19 +2,27 @@
 //
 // emqx_router:match_routes/1 is called once per PUBLISH by each publisher's own process
 // (apps/emqx/src/emqx_broker.erl:213).  Many concurrent single-topic calls are coalesced here
-// into one device match: callers submit a topic and a context pointer and return at once; a
-// worker thread gathers submissions until `max_batch` topics are queued or `max_wait_us` has
-// passed since the oldest one, runs one emqx_match_batch over them and hands every caller its
-// filter ids through the callback.  The Erlang NIF uses the callback to enif_send the result to
-// the waiting process, so the Erlang call shape stays synchronous while the GPU sees batches.
+// into device batches: a caller's topic is copied straight into the pinned input buffer of the
+// batch being filled (emqx_host_batch, engine.cpp) and submit() returns at once.
+//
+// Two threads drive the batches, so that two are in flight while a third fills:
+//   * the dispatcher submits a batch when it holds `max_batch` topics, or `max_wait_us` after
+//     its first topic, as long as fewer than two batches are in flight — or at once when
+//     nothing is in flight (an idle device serves a lone PUBLISH without waiting);
+//   * the completer waits for the oldest batch in flight and calls cb(ctx, status, ids, n)
+//     for each of its topics (ids point into the batch's pinned output, valid during the
+//     call), then frees the buffer.
+// The Erlang NIF's callback enif_send()s the ids to the waiting process, so the Erlang call
+// shape stays synchronous while the GPU sees batches.  A full set of buffers blocks submit()
+// until one frees (backpressure instead of unbounded queues).
 #include <stdint.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
 #include <mutex>
-#include <string>
 #include <thread>
 #include <vector>
 
@@ -22,10 +30,15 @@
 
 namespace {
 
-struct Req {
-  std::string topic;
-  void* ctx;
-  std::chrono::steady_clock::time_point t;
+using Clock = std::chrono::steady_clock;
+constexpr int NBUF = 4;          // two in flight, one filling, one ready
+constexpr int MAX_INFLIGHT = 2;
+
+struct Buf {
+  emqx_host_batch* hb = nullptr;
+  std::vector<void*> ctx;
+  Clock::time_point t0;
+  uint64_t bytes = 0;
 };
 
 }  // namespace
@@ -37,61 +50,96 @@ struct emqx_batcher {
   uint32_t max_wait_us = 200;
   emqx_batch_cb cb = nullptr;
   std::mutex mu;
-  std::condition_variable cv;
-  std::deque<Req> q;
+  std::condition_variable cv;   // any state change
+  Buf buf[NBUF];
+  std::vector<int> free_;       // buffer indices
+  int filling = -1;
+  std::deque<int> ready, inflight;
   bool stop = false;
-  std::thread worker;
-  uint64_t n_batches = 0, n_topics = 0;
+  std::thread dispatcher, completer;
+  uint64_t n_batches = 0, n_topics = 0, max_inflight_seen = 0;
 
-  void run() {
-    std::vector<Req> batch;
-    std::vector<uint8_t> bytes;
-    std::vector<uint64_t> offs;
-    std::vector<uint64_t> out_off;
-    std::vector<uint32_t> out_ids(1 << 16);
+  // Takes the filling buffer out of the filling state (caller holds mu).
+  void seal() {
+    if (filling >= 0 && !buf[filling].ctx.empty()) ready.push_back(filling);
+    else if (filling >= 0) free_.push_back(filling);
+    filling = -1;
+  }
+
+  void dispatch_loop() {
+    std::unique_lock<std::mutex> lk(mu);
     while (true) {
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return stop || !q.empty(); });
-        if (q.empty() && stop) return;
-        // wait for a full batch or the oldest request's deadline
-        const auto deadline = q.front().t + std::chrono::microseconds(max_wait_us);
-        cv.wait_until(lk, deadline, [&] { return stop || q.size() >= max_batch; });
-        const size_t take = std::min<size_t>(q.size(), max_batch);
-        batch.clear();
-        for (size_t i = 0; i < take; ++i) {
-          batch.push_back(std::move(q.front()));
-          q.pop_front();
-        }
-      }
-      if (batch.empty()) continue;
-      bytes.clear();
-      offs.assign(1, 0);
-      for (auto& r : batch) {
-        bytes.insert(bytes.end(), r.topic.begin(), r.topic.end());
-        offs.push_back(bytes.size());
-      }
-      if (bytes.empty()) bytes.push_back(0);
-      out_off.assign(batch.size() + 1, 0);
-      uint64_t total = 0;
-      int rc = emqx_match_batch(e, mode, bytes.data(), offs.data(), batch.size(), out_off.data(), out_ids.data(),
-                                out_ids.size(), &total);
-      if (rc == EMQX_EOVERFLOW) {
-        out_ids.resize(total + 1024);
-        rc = emqx_match_batch(e, mode, bytes.data(), offs.data(), batch.size(), out_off.data(), out_ids.data(),
-                              out_ids.size(), &total);
-      }
-      for (size_t i = 0; i < batch.size(); ++i) {
-        if (rc == EMQX_OK)
-          cb(batch[i].ctx, rc, out_ids.data() + out_off[i], out_off[i + 1] - out_off[i]);
+      // a sealed batch, or the filling one once its deadline passed, and room in flight
+      while (true) {
+        // an idle device takes what is there at once (latency); a busy one lets the batch grow
+        // to max_batch or until max_wait_us after its first topic (throughput)
+        if (ready.empty() && filling >= 0 && !buf[filling].ctx.empty() &&
+            (stop || inflight.empty() || Clock::now() >= buf[filling].t0 + std::chrono::microseconds(max_wait_us)))
+          seal();
+        if (!ready.empty() && static_cast<int>(inflight.size()) < MAX_INFLIGHT) break;
+        if (stop && ready.empty() && (filling < 0 || buf[filling].ctx.empty())) return;
+        if (ready.empty() && filling >= 0 && !buf[filling].ctx.empty() &&
+            static_cast<int>(inflight.size()) < MAX_INFLIGHT)
+          cv.wait_until(lk, buf[filling].t0 + std::chrono::microseconds(max_wait_us));
         else
-          cb(batch[i].ctx, rc, nullptr, 0);
+          cv.wait(lk);
       }
-      std::lock_guard<std::mutex> g(mu);
-      n_batches += 1;
-      n_topics += batch.size();
+      const int k = ready.front();
+      ready.pop_front();
+      lk.unlock();
+      int rc = emqx_host_batch_submit(buf[k].hb, mode);
+      lk.lock();
+      if (rc != EMQX_OK) {  // report the failure to every caller of the batch
+        lk.unlock();
+        for (void* c : buf[k].ctx) cb(c, rc, nullptr, 0);
+        lk.lock();
+        recycle(k);
+        continue;
+      }
+      inflight.push_back(k);
+      max_inflight_seen = std::max<uint64_t>(max_inflight_seen, inflight.size());
+      cv.notify_all();
     }
   }
+
+  void complete_loop() {
+    std::unique_lock<std::mutex> lk(mu);
+    while (true) {
+      cv.wait(lk, [&] { return !inflight.empty() || (stop && ready.empty() && filling < 0 && dispatcher_done); });
+      if (inflight.empty()) return;
+      const int k = inflight.front();
+      lk.unlock();
+      emqx_host_batch* b = buf[k].hb;
+      int rc = emqx_host_batch_wait(b);
+      if (rc == EMQX_EOVERFLOW) {  // more ids than the buffer holds: grow it, rerun the batch
+        rc = emqx_host_batch_reserve(b, b->cap_topics, b->cap_bytes, b->n_out + (b->n_out >> 1) + 1024);
+        if (rc == EMQX_OK) rc = emqx_host_batch_submit(b, mode);
+        if (rc == EMQX_OK) rc = emqx_host_batch_wait(b);
+      }
+      const std::vector<void*>& ctx = buf[k].ctx;
+      for (size_t i = 0; i < ctx.size(); ++i) {
+        if (rc == EMQX_OK)
+          cb(ctx[i], rc, b->out_ids + b->out_offsets[i], b->out_offsets[i + 1] - b->out_offsets[i]);
+        else
+          cb(ctx[i], rc, nullptr, 0);
+      }
+      lk.lock();
+      inflight.pop_front();
+      n_batches += 1;
+      n_topics += ctx.size();
+      recycle(k);
+    }
+  }
+
+  void recycle(int k) {  // caller holds mu
+    buf[k].ctx.clear();
+    buf[k].bytes = 0;
+    buf[k].hb->n = 0;
+    free_.push_back(k);
+    cv.notify_all();
+  }
+
+  bool dispatcher_done = false;
 };
 
 extern "C" {
@@ -106,21 +154,70 @@ int emqx_batcher_create(emqx_engine* e, uint32_t mode, uint32_t max_batch, uint3
   b->max_batch = max_batch;
   b->max_wait_us = max_wait_us;
   b->cb = cb;
-  b->worker = std::thread([b] { b->run(); });
+  for (int k = 0; k < NBUF; ++k) {
+    // ~48 B per topic and 32 ids per topic to start with; both grow on demand
+    int rc = emqx_host_batch_create(e, max_batch, std::max<uint64_t>(48ull * max_batch, 1u << 16),
+                                    std::max<uint64_t>(32ull * max_batch, 1u << 16), &b->buf[k].hb);
+    if (rc != EMQX_OK) {
+      for (int j = 0; j < k; ++j) emqx_host_batch_destroy(b->buf[j].hb);
+      delete b;
+      return rc;
+    }
+    b->buf[k].hb->topic_offsets[0] = 0;
+    b->buf[k].hb->n = 0;
+    b->free_.push_back(k);
+  }
+  b->dispatcher = std::thread([b] {
+    b->dispatch_loop();
+    std::lock_guard<std::mutex> g(b->mu);
+    b->dispatcher_done = true;
+    b->cv.notify_all();
+  });
+  b->completer = std::thread([b] { b->complete_loop(); });
   *out = b;
   return EMQX_OK;
 }
 
 int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, void* ctx) {
   if (!b || (len && !topic)) return EMQX_EINVAL;
-  {
-    std::lock_guard<std::mutex> g(b->mu);
+  std::unique_lock<std::mutex> lk(b->mu);
+  while (true) {
     if (b->stop) return EMQX_EINVAL;
-    b->q.push_back(Req{std::string(reinterpret_cast<const char*>(topic), len), ctx,
-                       std::chrono::steady_clock::now()});
+    if (b->filling < 0) {
+      if (b->free_.empty()) {  // every buffer filling, sealed or in flight: wait for one
+        b->cv.wait(lk);
+        continue;
+      }
+      b->filling = b->free_.back();
+      b->free_.pop_back();
+      Buf& f = b->buf[b->filling];
+      f.ctx.clear();
+      f.bytes = 0;
+      f.hb->n = 0;
+      f.hb->topic_offsets[0] = 0;
+    }
+    Buf& f = b->buf[b->filling];
+    emqx_host_batch* hb = f.hb;
+    if (f.bytes + len > hb->cap_bytes) {
+      if (f.ctx.empty()) {  // a topic larger than the buffer: grow it
+        int rc = emqx_host_batch_reserve(hb, hb->cap_topics, len + (len >> 1) + 64, hb->cap_ids);
+        if (rc != EMQX_OK) return rc;
+      } else {
+        b->seal();
+        b->cv.notify_all();
+        continue;
+      }
+    }
+    if (len) std::memcpy(hb->topic_bytes + f.bytes, topic, len);
+    f.bytes += len;
+    hb->n += 1;
+    hb->topic_offsets[hb->n] = f.bytes;
+    f.ctx.push_back(ctx);
+    if (f.ctx.size() == 1) f.t0 = Clock::now();
+    if (f.ctx.size() >= b->max_batch) b->seal();
+    if (f.ctx.size() == 1 || b->filling < 0) b->cv.notify_all();
+    return EMQX_OK;
   }
-  b->cv.notify_one();
-  return EMQX_OK;
 }
 
 int emqx_batcher_destroy(emqx_batcher* b) {
@@ -130,7 +227,9 @@ int emqx_batcher_destroy(emqx_batcher* b) {
     b->stop = true;
   }
   b->cv.notify_all();
-  if (b->worker.joinable()) b->worker.join();  // drains pending submissions first
+  if (b->dispatcher.joinable()) b->dispatcher.join();  // pending submissions are dispatched
+  if (b->completer.joinable()) b->completer.join();    // and completed first
+  for (int k = 0; k < NBUF; ++k) emqx_host_batch_destroy(b->buf[k].hb);
   delete b;
   return EMQX_OK;
 }

@@ -131,15 +131,6 @@ struct Workspace {
   uint32_t deep_stack_cap = 1u << 14;
   uint64_t* deep_slab = nullptr;
   uint32_t deep_slab_cap = 1u << 20;
-  // host-API staging
-  uint8_t* d_tbytes = nullptr;
-  uint64_t cap_tbytes = 0;
-  uint64_t* d_toffs = nullptr;
-  uint64_t cap_toffs = 0;
-  uint64_t* d_out_off = nullptr;
-  uint64_t cap_out_off = 0;
-  uint32_t* d_out_ids = nullptr;
-  uint64_t cap_out_ids = 0;
   uint64_t* h_rb = nullptr;         // pinned call summary (SUM_WORDS), written by tile_scan_kernel
   bool deep_ready = false;
 
@@ -149,7 +140,6 @@ struct Workspace {
     dfree(tile_defer); dfree(spill); dfree(diag); dfree(ctrl); dfree(tile_sum); dfree(tile_stats);
     dfree(group_sum); dfree(group_stats);
     dfree(deep_wids); dfree(deep_stack); dfree(deep_slab);
-    dfree(d_tbytes); dfree(d_toffs); dfree(d_out_off); dfree(d_out_ids);
     if (h_rb) (void)hipHostFree(h_rb);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -193,6 +183,8 @@ struct emqx_engine {
   uint64_t last_commit_kind = 0;
   uint64_t last_relocations = 0, last_in_place = 0, last_patches = 0, last_new_slots = 0;
   double last_host_ms = 0;      // host part (LiveTrie::commit) of the last incremental commit
+  std::mutex hb_mu;             // pinned host batches of emqx_match_batch (pool)
+  std::vector<emqx_host_batch*> hb_free;
   int commit_threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
 };
 
@@ -568,6 +560,121 @@ std::shared_ptr<Snapshot> current(emqx_engine* e) {
   return e->snap;
 }
 
+// Device side of a pinned host batch (include/emqx_match.h, emqx_host_batch_*).
+struct HostBatchPriv {
+  emqx_engine* e = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* d_tbytes = nullptr;
+  uint64_t* d_toffs = nullptr;
+  uint64_t* d_out_off = nullptr;
+  uint32_t* d_out_ids = nullptr;
+  uint64_t* summary = nullptr;  // pinned, SUM_WORDS
+  std::shared_ptr<Snapshot> snap;
+  uint32_t mode = 0;
+  bool pending = false;
+};
+
+template <class T>
+hipError_t halloc(T*& p, uint64_t count) {
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  return hipHostMalloc(reinterpret_cast<void**>(&p), std::max<uint64_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+}
+
+int hb_alloc(emqx_host_batch* b, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_ids, bool keep_inputs) {
+  auto* p = static_cast<HostBatchPriv*>(b->priv);
+  HIP_TRY(hipSetDevice(p->e->device));
+  if (cap_topics > b->cap_topics) {
+    uint64_t* t = nullptr;
+    HIP_TRY(halloc(t, cap_topics + 1));
+    if (keep_inputs && b->topic_offsets) std::memcpy(t, b->topic_offsets, (b->cap_topics + 1) * sizeof(uint64_t));
+    if (b->topic_offsets) (void)hipHostFree(b->topic_offsets);
+    b->topic_offsets = t;
+    HIP_TRY(halloc(b->out_offsets, cap_topics + 1));
+    HIP_TRY(dalloc(p->d_toffs, cap_topics + 1));
+    HIP_TRY(dalloc(p->d_out_off, cap_topics + 1));
+    b->cap_topics = cap_topics;
+  }
+  if (cap_bytes > b->cap_bytes) {
+    uint8_t* t = nullptr;
+    HIP_TRY(halloc(t, cap_bytes + 16));
+    if (keep_inputs && b->topic_bytes) std::memcpy(t, b->topic_bytes, b->cap_bytes);
+    if (b->topic_bytes) (void)hipHostFree(b->topic_bytes);
+    b->topic_bytes = t;
+    HIP_TRY(dalloc(p->d_tbytes, cap_bytes + 16));
+    b->cap_bytes = cap_bytes;
+  }
+  if (cap_ids > b->cap_ids) {
+    HIP_TRY(halloc(b->out_ids, cap_ids));
+    HIP_TRY(dalloc(p->d_out_ids, cap_ids));
+    b->cap_ids = cap_ids;
+  }
+  return EMQX_OK;
+}
+
+// Enqueue: inputs to HBM (DMA from pinned memory), the match pipeline, the CSR back into the
+// pinned outputs; one event at the end.
+int hb_enqueue(emqx_host_batch* b) {
+  auto* p = static_cast<HostBatchPriv*>(b->priv);
+  emqx_engine* e = p->e;
+  const uint64_t n = b->n, nbytes = n ? b->topic_offsets[n] : 0;
+  hipStream_t s = p->stream;
+  if (nbytes) HIP_TRY(hipMemcpyAsync(p->d_tbytes, b->topic_bytes, nbytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(p->d_toffs, b->topic_offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  uint64_t* sum_dev = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&sum_dev), p->summary, 0));
+  p->snap = current(e);
+  Workspace* w = acquire_ws(e, s);
+  int rc = ensure_ws(w, n);
+  if (rc == EMQX_OK)
+    rc = enqueue_match(e, *p->snap, w, p->mode, p->d_tbytes, p->d_toffs, n, p->d_out_off, p->d_out_ids, b->cap_ids,
+                       sum_dev, s);
+  if (rc == EMQX_OK) w->inflight = p->snap;
+  release_ws(e, w);
+  if (rc != EMQX_OK) return rc;
+  uint64_t *h_off = nullptr;
+  uint32_t* h_ids = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_off), b->out_offsets, 0));
+  HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_ids), b->out_ids, 0));
+  HIP_TRY(launch_csr_to_host(p->d_out_off, n, p->d_out_ids, b->cap_ids, h_off, h_ids, s));
+  HIP_TRY(hipEventRecord(p->done, s));
+  p->pending = true;
+  return EMQX_OK;
+}
+
+int hb_wait(emqx_host_batch* b) {
+  auto* p = static_cast<HostBatchPriv*>(b->priv);
+  if (!p->pending) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(p->e->device));
+  p->pending = false;
+  HIP_TRY(hipEventSynchronize(p->done));
+  uint64_t flags = p->summary[SUM_FLAGS];
+  uint64_t total = p->summary[SUM_TOTAL];
+  if (flags & SUM_F_RETRY) {  // a scratch area overflowed: the synchronous path grows it and reruns
+    Workspace* w = acquire_ws(p->e, p->stream);
+    int rc = ensure_ws(w, b->n);
+    if (rc == EMQX_OK)
+      rc = run_match(p->e, *p->snap, w, p->mode, p->d_tbytes, p->d_toffs, b->n, p->d_out_off, p->d_out_ids,
+                     b->cap_ids, &total, p->stream);
+    release_ws(p->e, w);
+    if (rc != EMQX_OK && rc != EMQX_EOVERFLOW) return rc;
+    uint64_t *h_off = nullptr;
+    uint32_t* h_ids = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_off), b->out_offsets, 0));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_ids), b->out_ids, 0));
+    HIP_TRY(launch_csr_to_host(p->d_out_off, b->n, p->d_out_ids, b->cap_ids, h_off, h_ids, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    flags = total > b->cap_ids ? SUM_F_OVERFLOW : 0;
+  } else if (flags & SUM_F_ERROR) {
+    set_last_error("topic longer than 65535 bytes on the deep path");
+    return EMQX_EINVAL;
+  }
+  p->snap.reset();
+  b->n_out = total;
+  return (flags & SUM_F_OVERFLOW) ? EMQX_EOVERFLOW : EMQX_OK;
+}
+
 bool offsets_ok(const uint64_t* offs, uint64_t n) {
   if (!offs) return n == 0;
   for (uint64_t i = 0; i < n; ++i)
@@ -608,6 +715,8 @@ int emqx_engine_create(const emqx_engine_opts* opts, emqx_engine** out) {
 int emqx_engine_destroy(emqx_engine* e) {
   if (!e) return EMQX_EINVAL;
   (void)hipSetDevice(e->device);
+  for (emqx_host_batch* b : e->hb_free) emqx_host_batch_destroy(b);
+  e->hb_free.clear();
   delete e;
   return EMQX_OK;
 }
@@ -720,6 +829,86 @@ int emqx_match_batch_device_async(emqx_engine* e, uint32_t mode, const uint8_t* 
   return rc;
 }
 
+int emqx_host_batch_create(emqx_engine* e, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_ids,
+                           emqx_host_batch** out) {
+  if (!e || !out) return EMQX_EINVAL;
+  *out = nullptr;
+  auto* b = new (std::nothrow) emqx_host_batch();
+  auto* p = new (std::nothrow) HostBatchPriv();
+  if (!b || !p) {
+    delete b;
+    delete p;
+    return EMQX_ENOMEM;
+  }
+  std::memset(b, 0, sizeof(*b));
+  b->priv = p;
+  p->e = e;
+  int rc = EMQX_OK;
+  if (hipSetDevice(e->device) != hipSuccess || hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess || halloc(p->summary, SUM_WORDS) != hipSuccess)
+    rc = EMQX_EDEVICE;
+  if (rc == EMQX_OK)
+    rc = hb_alloc(b, std::max<uint64_t>(cap_topics, 1), std::max<uint64_t>(cap_bytes, 64), std::max<uint64_t>(cap_ids, 64),
+                  false);
+  if (rc != EMQX_OK) {
+    emqx_host_batch_destroy(b);
+    return rc;
+  }
+  *out = b;
+  return EMQX_OK;
+}
+
+int emqx_host_batch_destroy(emqx_host_batch* b) {
+  if (!b) return EMQX_EINVAL;
+  auto* p = static_cast<HostBatchPriv*>(b->priv);
+  (void)hipSetDevice(p->e->device);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  if (b->topic_bytes) (void)hipHostFree(b->topic_bytes);
+  if (b->topic_offsets) (void)hipHostFree(b->topic_offsets);
+  if (b->out_offsets) (void)hipHostFree(b->out_offsets);
+  if (b->out_ids) (void)hipHostFree(b->out_ids);
+  if (p->summary) (void)hipHostFree(p->summary);
+  dfree(p->d_tbytes);
+  dfree(p->d_toffs);
+  dfree(p->d_out_off);
+  dfree(p->d_out_ids);
+  if (p->done) (void)hipEventDestroy(p->done);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+  delete b;
+  return EMQX_OK;
+}
+
+int emqx_host_batch_reserve(emqx_host_batch* b, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_ids) {
+  if (!b || static_cast<HostBatchPriv*>(b->priv)->pending) return EMQX_EINVAL;
+  return hb_alloc(b, cap_topics, cap_bytes, cap_ids, true);
+}
+
+int emqx_host_batch_submit(emqx_host_batch* b, uint32_t mode) {
+  if (!b || mode > EMQX_MODE_TRIE_WILDCARD) return EMQX_EINVAL;
+  auto* p = static_cast<HostBatchPriv*>(b->priv);
+  if (p->pending || b->n > b->cap_topics) return EMQX_EINVAL;
+  const uint64_t* o = b->topic_offsets;
+  if (o[0] != 0 || o[b->n] > b->cap_bytes || !offsets_ok(o, b->n)) return EMQX_EINVAL;
+  HIP_TRY(hipSetDevice(p->e->device));
+  p->mode = mode;
+  return hb_enqueue(b);
+}
+
+int emqx_host_batch_wait(emqx_host_batch* b) {
+  if (!b) return EMQX_EINVAL;
+  return hb_wait(b);
+}
+
+int emqx_host_batch_query(emqx_host_batch* b) {
+  if (!b) return EMQX_EINVAL;
+  auto* p = static_cast<HostBatchPriv*>(b->priv);
+  return !p->pending || hipEventQuery(p->done) == hipSuccess ? 1 : 0;
+}
+
+// Host buffers of any kind: chunks of the batch flow through two pinned host batches of the
+// engine's pool — while one chunk is on the device, the previous chunk's results are copied
+// out and the next chunk is packed.
 int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, const uint64_t* topic_offsets,
                      uint64_t n, uint64_t* out_offsets, uint32_t* out_ids, uint64_t cap, uint64_t* n_out) {
   if (!e || !n_out || !out_offsets || mode > EMQX_MODE_TRIE_WILDCARD) return EMQX_EINVAL;
@@ -728,62 +917,86 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
   const uint64_t b0 = n ? topic_offsets[0] : 0, b1 = n ? topic_offsets[n] : 0;
   if (b1 > b0 && !topic_bytes) return EMQX_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
-  auto snap = current(e);
-  Workspace* w = acquire_ws(e);
-  int rc = ensure_ws(w, n);
-  if (rc != EMQX_OK) {
-    release_ws(e, w);
-    return rc;
+  constexpr uint64_t CH_TOPICS = 1u << 18, CH_BYTES = 16u << 20, CH_IDS = 8u << 20;
+  emqx_host_batch* hb[2] = {nullptr, nullptr};
+  {
+    std::lock_guard<std::mutex> g(e->hb_mu);
+    for (int k = 0; k < 2 && !e->hb_free.empty(); ++k) {
+      hb[k] = e->hb_free.back();
+      e->hb_free.pop_back();
+    }
   }
-  // stage inputs (bytes rebased to 0, padded)
-  const uint64_t nbytes = b1 - b0;
-  if (nbytes + 16 > w->cap_tbytes) {
-    w->cap_tbytes = round_pow2(nbytes + 16);
-    if (dalloc(w->d_tbytes, w->cap_tbytes) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
-  }
-  if (n + 1 > w->cap_toffs) {
-    w->cap_toffs = round_pow2(n + 1);
-    if (dalloc(w->d_toffs, w->cap_toffs) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
-  }
-  if (n + 1 > w->cap_out_off) {
-    w->cap_out_off = round_pow2(n + 1);
-    if (dalloc(w->d_out_off, w->cap_out_off) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
-  }
-  std::vector<uint64_t> rebased(n + 1);
-  for (uint64_t i = 0; i <= n; ++i) rebased[i] = n ? topic_offsets[i] - b0 : 0;
-  hipStream_t s = w->stream;
-  auto fail = [&](hipError_t err) {
-    set_last_error(hipGetErrorString(err));
-    release_ws(e, w);
-    return EMQX_EDEVICE;
+  int rc = EMQX_OK;
+  for (int k = 0; k < 2 && rc == EMQX_OK; ++k)
+    if (!hb[k]) rc = emqx_host_batch_create(e, CH_TOPICS, CH_BYTES, CH_IDS, &hb[k]);
+  uint64_t chunk_lo[2] = {0, 0}, total = 0, next = 0;
+  bool inflight[2] = {false, false}, overflow = false;
+  // pack topics [next, ...) into hb[k] (rebased offsets)
+  auto pack = [&](int k) -> int {
+    emqx_host_batch* b = hb[k];
+    const uint64_t lo = next;
+    uint64_t hi = lo;
+    const uint64_t base = topic_offsets[lo];
+    while (hi < n && hi - lo < b->cap_topics && topic_offsets[hi + 1] - base <= b->cap_bytes) ++hi;
+    if (hi == lo) {  // one topic larger than the chunk buffer
+      int r = emqx_host_batch_reserve(b, b->cap_topics, topic_offsets[lo + 1] - base + 16, b->cap_ids);
+      if (r != EMQX_OK) return r;
+      hi = lo + 1;
+    }
+    const uint64_t nb = topic_offsets[hi] - base;
+    if (nb) std::memcpy(b->topic_bytes, topic_bytes + base, nb);
+    for (uint64_t i = lo; i <= hi; ++i) b->topic_offsets[i - lo] = topic_offsets[i] - base;
+    b->n = hi - lo;
+    chunk_lo[k] = lo;
+    next = hi;
+    return emqx_host_batch_submit(b, mode);
   };
-  hipError_t he;
-  if (nbytes && (he = hipMemcpyAsync(w->d_tbytes, topic_bytes + b0, nbytes, hipMemcpyHostToDevice, s)) != hipSuccess)
-    return fail(he);
-  if ((he = hipMemcpyAsync(w->d_toffs, rebased.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s)) != hipSuccess)
-    return fail(he);
-  // results: size the id buffer lazily (first pass learns the total)
-  uint64_t total = 0;
-  uint32_t* d_ids = w->d_out_ids;
-  uint64_t dcap = w->cap_out_ids;
-  rc = run_match(e, *snap, w, mode, w->d_tbytes, w->d_toffs, n, w->d_out_off, d_ids, dcap, &total, s);
-  if (rc == EMQX_EOVERFLOW && total <= cap) {
-    w->cap_out_ids = round_pow2(total + 1);
-    if (dalloc(w->d_out_ids, w->cap_out_ids) != hipSuccess) { release_ws(e, w); return EMQX_ENOMEM; }
-    rc = run_match(e, *snap, w, mode, w->d_tbytes, w->d_toffs, n, w->d_out_off, w->d_out_ids, w->cap_out_ids,
-                   &total, s);
+  // results of hb[k] into the caller's arrays (offsets rebased to the running total)
+  auto drain = [&](int k) -> int {
+    emqx_host_batch* b = hb[k];
+    int r = emqx_host_batch_wait(b);
+    if (r == EMQX_EOVERFLOW) {  // more ids than the chunk's buffer: grow it and rerun the chunk
+      r = emqx_host_batch_reserve(b, b->cap_topics, b->cap_bytes, b->n_out + (b->n_out >> 2) + 1024);
+      if (r == EMQX_OK) r = emqx_host_batch_submit(b, mode);
+      if (r == EMQX_OK) r = emqx_host_batch_wait(b);
+    }
+    if (r != EMQX_OK) return r;
+    const uint64_t lo = chunk_lo[k], m = b->n_out;
+    for (uint64_t i = 0; i < b->n; ++i) out_offsets[lo + i] = total + b->out_offsets[i];
+    if (!overflow && out_ids && total + m <= cap) {
+      if (m) std::memcpy(out_ids + total, b->out_ids, m * sizeof(uint32_t));
+    } else if (m) {
+      overflow = true;
+    }
+    total += m;
+    return EMQX_OK;
+  };
+  int k = 0;
+  if (rc == EMQX_OK && n == 0) {
+    out_offsets[0] = 0;
+  } else {
+    while (rc == EMQX_OK && (next < n || inflight[0] || inflight[1])) {
+      if (inflight[k]) {
+        rc = drain(k);
+        inflight[k] = false;
+      }
+      if (rc == EMQX_OK && next < n) {
+        rc = pack(k);
+        inflight[k] = rc == EMQX_OK;
+      }
+      k ^= 1;
+    }
   }
+  for (int j = 0; j < 2; ++j)  // drain what an error left in flight before the batches go back
+    if (inflight[j]) (void)emqx_host_batch_wait(hb[j]);
+  out_offsets[n] = total;
   *n_out = total;
-  if (rc == EMQX_OK && total > cap) rc = EMQX_EOVERFLOW;
-  if (rc == EMQX_OK) {
-    if ((he = hipMemcpyAsync(out_offsets, w->d_out_off, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return fail(he);
-    if (total && out_ids &&
-        (he = hipMemcpyAsync(out_ids, w->d_out_ids, total * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
-      return fail(he);
-    if ((he = hipStreamSynchronize(s)) != hipSuccess) return fail(he);
+  {
+    std::lock_guard<std::mutex> g(e->hb_mu);
+    for (int j = 0; j < 2; ++j)
+      if (hb[j]) e->hb_free.push_back(hb[j]);
   }
-  release_ws(e, w);
+  if (rc == EMQX_OK && (overflow || total > cap)) rc = EMQX_EOVERFLOW;
   return rc;
 }
 

@@ -1288,6 +1288,26 @@ __global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a) {
   }
 }
 
+// Host batches (engine.cpp, emqx_host_batch_*): streams a finished CSR from HBM into the
+// batch's pinned host buffers — offsets [n+1] and min(total, cap) ids, total read on the
+// device — with 16-B stores, so the PCIe writes are full lines and the host needs no
+// size-dependent D2H copy.
+__global__ __launch_bounds__(256) void csr_to_host_kernel(const uint64_t* __restrict__ d_off, uint64_t n,
+                                                          const uint32_t* __restrict__ d_ids, uint64_t cap,
+                                                          uint64_t* h_off, uint32_t* h_ids) {
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nt = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t total = min(d_off[n], cap);
+  const uint64_t no2 = (n + 1) / 2;  // offsets, two per 16-B store
+  for (uint64_t i = tid; i < no2; i += nt)
+    reinterpret_cast<uint4*>(h_off)[i] = reinterpret_cast<const uint4*>(d_off)[i];
+  if (tid == 0 && ((n + 1) & 1)) h_off[n] = d_off[n];
+  const uint64_t nv = total / 4;     // ids, four per 16-B store
+  for (uint64_t i = tid; i < nv; i += nt)
+    reinterpret_cast<uint4*>(h_ids)[i] = reinterpret_cast<const uint4*>(d_ids)[i];
+  if (tid < total - 4 * nv) h_ids[4 * nv + tid] = d_ids[4 * nv + tid];
+}
+
 // Incremental commits (live_trie.cpp): rewrites existing slots of the committed table in
 // place.  Phase 0 writes the slots' filter ids, phase 1 (a later launch) the slots, each with
 // one 16-B store, so a concurrent walk sees every slot either old or new, and never a slot
@@ -1365,6 +1385,14 @@ hipError_t launch_assemble(const MatchArgs& a, hipStream_t s) {
   }
   hipLaunchKernelGGL(scatter_deep_kernel, dim3(64), dim3(256), 0, s, a);
   hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_csr_to_host(const uint64_t* d_off, uint64_t n, const uint32_t* d_ids, uint64_t cap,
+                               uint64_t* h_off, uint32_t* h_ids, hipStream_t s) {
+  const uint64_t work = std::max<uint64_t>((n + 1) / 2, cap / 4);
+  const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((work + 255) / 256 + 1, 2048));
+  hipLaunchKernelGGL(csr_to_host_kernel, dim3(blocks), dim3(256), 0, s, d_off, n, d_ids, cap, h_off, h_ids);
   return hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ import numpy as np
 from . import _lib
 from ._lib import MODE_ROUTES, MODE_TRIE, MODE_TRIE_WILDCARD, EngineError, check
 
-__all__ = ["Engine", "pack", "MODE_ROUTES", "MODE_TRIE", "MODE_TRIE_WILDCARD", "EngineError"]
+__all__ = ["Engine", "HostBatch", "pack", "MODE_ROUTES", "MODE_TRIE", "MODE_TRIE_WILDCARD", "EngineError"]
 
 
 def pack(items: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
@@ -176,3 +176,70 @@ class Engine:
             self._h, mode, ctypes.c_void_p(d_bytes_ptr), ctypes.c_void_p(d_offs_ptr), n,
             ctypes.c_void_p(d_out_off_ptr), ctypes.c_void_p(d_out_ids_ptr), cap, ctypes.c_void_p(d_summary_ptr),
             ctypes.c_void_p(stream) if stream else None), "emqx_match_batch_device_async")
+
+
+class HostBatch:
+    """A pinned host batch (emqx_host_batch_*): topics are packed straight into page-locked
+    buffers the engine owns, and results come back into page-locked buffers — the NIF's
+    "pinned batch buffers".  Several may be in flight at once: submit() returns at once,
+    wait() blocks for this batch only."""
+
+    def __init__(self, engine: "Engine", cap_topics: int = 1 << 16, cap_bytes: int = 4 << 20,
+                 cap_ids: int = 1 << 21):
+        self._engine = engine
+        p = ctypes.POINTER(_lib.HostBatchStruct)()
+        check(_lib.lib().emqx_host_batch_create(engine._h, cap_topics, cap_bytes, cap_ids, ctypes.byref(p)),
+              "emqx_host_batch_create")
+        self._p = p
+
+    @property
+    def s(self):
+        return self._p.contents
+
+    def close(self):
+        if getattr(self, "_p", None):
+            _lib.lib().emqx_host_batch_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def pack(self, buf: np.ndarray, offs: np.ndarray):
+        """Copies a packed batch (offsets rebased to 0) into the pinned inputs."""
+        n = len(offs) - 1
+        o = np.asarray(offs, dtype=np.uint64)
+        nb = int(o[-1] - o[0]) if n else 0
+        s = self.s
+        if n > s.cap_topics or nb > s.cap_bytes:
+            check(_lib.lib().emqx_host_batch_reserve(self._p, max(n, s.cap_topics), max(nb, s.cap_bytes), s.cap_ids),
+                  "emqx_host_batch_reserve")
+            s = self.s
+        if nb:
+            ctypes.memmove(s.topic_bytes, np.ascontiguousarray(buf[int(o[0]):int(o[-1])]).ctypes.data, nb)
+        dst = np.ctypeslib.as_array(s.topic_offsets, shape=(n + 1,))
+        dst[:] = o - o[0]
+        s.n = n
+
+    def submit(self, mode: int = MODE_ROUTES):
+        self._mode_last = mode
+        check(_lib.lib().emqx_host_batch_submit(self._p, mode), "emqx_host_batch_submit")
+
+    def wait(self, copy: bool = True):
+        """-> (offsets uint64 (n+1,), ids uint32): views of the pinned outputs (copy=False) or
+        copies.  Grows the id buffer and reruns once on EMQX_EOVERFLOW."""
+        rc = _lib.lib().emqx_host_batch_wait(self._p)
+        if rc == _lib.EMQX_EOVERFLOW:
+            s = self.s
+            check(_lib.lib().emqx_host_batch_reserve(self._p, s.cap_topics, s.cap_bytes, s.n_out + 1024),
+                  "emqx_host_batch_reserve")
+            rc = _lib.lib().emqx_host_batch_submit(self._p, self._mode_last)
+            if rc == 0:
+                rc = _lib.lib().emqx_host_batch_wait(self._p)
+        check(rc, "emqx_host_batch_wait")
+        s = self.s
+        off = np.ctypeslib.as_array(s.out_offsets, shape=(s.n + 1,))
+        ids = np.ctypeslib.as_array(s.out_ids, shape=(max(s.n_out, 1),))[: s.n_out]
+        return (off.copy(), ids.copy()) if copy else (off, ids)

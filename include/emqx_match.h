@@ -119,8 +119,10 @@ int emqx_commit(emqx_engine* e);
  * commit's table patching. */
 int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n);
 
-/* Batched match, host buffers.  out_offsets has n+1 entries.  On EMQX_EOVERFLOW nothing
- * is written to out_ids and *n_out is the capacity required. */
+/* Batched match, host buffers (any host memory).  out_offsets has n+1 entries.  On
+ * EMQX_EOVERFLOW *n_out is the capacity required and out_ids holds no complete result.
+ * Internally the batch is cut into chunks that flow through two pinned host batches, so the
+ * copies into and out of pinned memory overlap the device work of the other chunk. */
 int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes,
                      const uint64_t* topic_offsets, uint64_t n, uint64_t* out_offsets,
                      uint32_t* out_ids, uint64_t cap, uint64_t* n_out);
@@ -148,6 +150,35 @@ int emqx_match_batch_device_async(emqx_engine* e, uint32_t mode, const uint8_t* 
                                   uint64_t* summary, void* stream);
 
 int emqx_stats_get(emqx_engine* e, emqx_stats* out);
+
+/* ---- pinned host batches (the NIF's batch buffers) --------------------------------
+ * A host batch owns pinned (page-locked, device-mapped) input and output buffers and its own
+ * stream.  The caller packs topics straight into topic_bytes / topic_offsets (offsets[0] = 0,
+ * n topics), submits, and reads the CSR from out_offsets / out_ids after wait — no pageable
+ * copy anywhere: the inputs go to HBM by DMA, the match runs, and one kernel streams the
+ * finished CSR into the pinned outputs.  Several batches may be in flight at once (the
+ * batcher keeps two).  wait(): EMQX_OK, EMQX_EOVERFLOW (n_out = ids needed: reserve and
+ * submit again) or an error. */
+typedef struct emqx_host_batch {
+  uint8_t* topic_bytes;     /* pinned, cap_bytes                                             */
+  uint64_t* topic_offsets;  /* pinned, cap_topics + 1                                       */
+  uint64_t cap_topics, cap_bytes;
+  uint64_t n;               /* topics packed (set by the caller)                             */
+  uint64_t* out_offsets;    /* pinned, cap_topics + 1 (valid after wait)                     */
+  uint32_t* out_ids;        /* pinned, cap_ids                                               */
+  uint64_t cap_ids;
+  uint64_t n_out;           /* ids of the last call (after wait)                             */
+  void* priv;
+} emqx_host_batch;
+int emqx_host_batch_create(emqx_engine* e, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_ids,
+                           emqx_host_batch** out);
+int emqx_host_batch_destroy(emqx_host_batch* b);
+/* Grows the buffers (contents of the inputs kept); not while a call is in flight. */
+int emqx_host_batch_reserve(emqx_host_batch* b, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_ids);
+int emqx_host_batch_submit(emqx_host_batch* b, uint32_t mode);
+int emqx_host_batch_wait(emqx_host_batch* b);
+/* 1 when the batch's call has completed (wait will not block), 0 while in flight. */
+int emqx_host_batch_query(emqx_host_batch* b);
 
 /* Cross-caller batcher: coalesces concurrent single-topic matches (emqx_router:match_routes/1
  * is called once per PUBLISH from each publisher process, apps/emqx/src/emqx_broker.erl:213)

@@ -1,0 +1,142 @@
+"""The host-memory entry points (GPU): pinned host batches (emqx_host_batch_*, the NIF's batch
+buffers), emqx_match_batch on pageable buffers (chunked through two pinned batches), and the
+cross-caller batcher (two pinned batches in flight) under concurrent single-topic callers —
+each compared ID-for-ID with the oracle (emqx_router:match_routes/1 semantics,
+apps/emqx/src/emqx_router.erl:128-140)."""
+
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import cpp as C
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def table():
+    import torch  # noqa: F401
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    wl = W.config_b(n_filters=150_000, n_topics=30_000, seed=31)
+    e = Engine()
+    e.insert_packed(*wl.filters)
+    e.commit()
+    o = C.CppOracle(True)
+    o.add_packed(*wl.filters)
+    off_o, ids_o, _ = o.match_csr(*wl.topics, mode=C.MODE_ROUTES, threads=8)
+    return e, wl, off_o, ids_o
+
+
+def test_pinned_host_batches_in_flight(table):
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import HostBatch
+    e, wl, off_o, ids_o = table
+    n = wl.n_topics
+    cuts = [0, 7000, 7001, 19_000, n]  # ragged batches, one of a single topic
+    hbs = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        hb = HostBatch(e, cap_topics=8192, cap_bytes=1 << 20, cap_ids=1 << 18)
+        hb.pack(*W.take(wl.topics, np.arange(a, b)))  # grows past its capacity where needed
+        hbs.append(hb)
+    for hb in hbs:  # all four in flight at once
+        hb.submit(0)
+    offs, ids, base = [np.zeros(1, np.uint64)], [], 0
+    for hb in hbs:
+        o, i = hb.wait()
+        offs.append(o[1:] + base)
+        ids.append(i)
+        base += int(o[-1])
+    off_g, ids_g = np.concatenate(offs), np.concatenate(ids)
+    assert C.csr_mismatches(off_g, ids_g, off_o, ids_o).size == 0
+
+
+def test_host_batch_overflow_and_empty(table):
+    from emqx_amd import _lib
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import HostBatch
+    e, wl, off_o, ids_o = table
+    hb = HostBatch(e, cap_topics=4096, cap_bytes=1 << 18, cap_ids=64)
+    part = W.take(wl.topics, np.arange(0, 3000))
+    hb.pack(*part)
+    hb.submit(0)
+    assert _lib.lib().emqx_host_batch_wait(hb._p) == _lib.EMQX_EOVERFLOW
+    need = hb.s.n_out
+    assert need == int(off_o[3000])
+    hb.submit(0)
+    o, i = hb.wait()  # grows the id buffer and reruns
+    assert C.csr_mismatches(o, i, off_o[:3001], ids_o[: int(off_o[3000])]).size == 0
+    hb.pack(np.zeros(1, np.uint8), np.zeros(1, np.uint64))  # an empty batch
+    hb.submit(0)
+    o, i = hb.wait()
+    assert o.tolist() == [0] and i.size == 0
+
+
+def test_pageable_match_batch_chunks(table):
+    """emqx_match_batch from numpy (pageable) buffers, larger than one pinned chunk, with
+    offsets that do not start at 0, and the overflow contract (n_out = capacity needed)."""
+    from emqx_amd import _lib
+    e, wl, off_o, ids_o = table
+    tb, to = wl.topics
+    pad = 13  # shift the bytes: offsets start at 13
+    tb2 = np.concatenate([np.full(pad, ord("x"), np.uint8), tb])
+    to2 = to.astype(np.uint64) + pad
+    off, ids = e.match_packed(tb2, to2, mode=0)
+    assert C.csr_mismatches(off, ids, off_o, ids_o).size == 0
+    n = len(to) - 1
+    out_off = np.zeros(n + 1, np.uint64)
+    small = np.zeros(16, np.uint32)
+    tot = ctypes.c_uint64()
+    rc = _lib.lib().emqx_match_batch(e._h, 0, tb2.ctypes.data, to2.ctypes.data, n, out_off.ctypes.data,
+                                     small.ctypes.data, 16, ctypes.byref(tot))
+    assert rc == _lib.EMQX_EOVERFLOW and tot.value == int(off_o[-1])
+
+
+@pytest.mark.parametrize("callers", [1, 48])
+def test_batcher_many_callers(table, callers):
+    """Concurrent single-topic callers through the batcher: every caller gets exactly its own
+    topic's ids; with many callers the batches hold many topics."""
+    from emqx_amd import workloads as W
+    from emqx_amd.batcher import Batcher
+    e, wl, off_o, ids_o = table
+    topics = W.unpack(wl.topics)[:3000]
+    b = Batcher(e, mode=0, max_batch=1024, max_wait_us=500)
+    got = [None] * len(topics)
+
+    def worker(k):
+        for i in range(k, len(topics), callers):
+            got[i] = sorted(b.match(topics[i]))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(callers)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    st = b.stats()
+    b.close()
+    for i in range(len(topics)):
+        assert got[i] == ids_o[off_o[i]:off_o[i + 1]].tolist(), i
+    assert st["topics"] == len(topics)
+    if callers > 1:
+        assert st["batches"] < len(topics) // 3
+
+
+def test_batch_load_tool(table):
+    """tools/batch_load.cpp (the L bench's driver) runs closed-loop callers to completion."""
+    import os
+    e, wl, _, _ = table
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    L = ctypes.CDLL(os.path.join(root, "tools", "_build", "libbatchload.so"))
+    L.batch_load.restype = ctypes.c_int
+    L.batch_load.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, ctypes.c_double,
+                             ctypes.c_void_p]
+    tb, to = wl.topics
+    to = np.ascontiguousarray(to.astype(np.uint64))
+    out = np.zeros(8)
+    rc = L.batch_load(e._h, 0, tb.ctypes.data, to.ctypes.data, wl.n_topics, 256, 1024, 200, 100.0, 500.0,
+                      out.ctypes.data)
+    assert rc == 0
+    assert out[0] > 1000 and 0 < out[2] <= out[4] <= out[5]

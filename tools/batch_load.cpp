@@ -1,0 +1,145 @@
+// Load generator for the cross-caller batcher (bench.py --workload L): `callers` concurrent
+// single-topic callers in a closed loop — each submits one topic, waits for its ids, submits
+// the next — as EMQX publisher processes call emqx_router:match_routes/1 once per PUBLISH
+// (apps/emqx/src/emqx_broker.erl:213).  A few driver threads own the callers (caller c
+// belongs to driver c mod D); the batcher's completion callback hands a finished caller back
+// to its driver, which records the latency and resubmits.  Throughput and latency
+// percentiles over the measured window go to out[].
+//
+// Built by __graft_entry__.build() into tools/_build/libbatchload.so; the emqx_batcher_*
+// symbols resolve against libemqxmatch.so, which the caller has loaded (RTLD_GLOBAL).
+#include <stdint.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../include/emqx_match.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Driver {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<uint32_t> done;  // callers whose result arrived
+  bool waiting = false;
+};
+
+struct Load {
+  std::vector<Driver> drv;
+  std::vector<Clock::time_point> t_sub;  // per caller: submit time of its request in flight
+  std::vector<int> status;
+  uint32_t D = 1;
+};
+
+Load* g_load = nullptr;  // the run in progress (one at a time)
+
+// ctx = caller index + 1
+void on_result(void* ctx, int status, const uint32_t*, uint64_t) {
+  Load* L = g_load;
+  const uint32_t c = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ctx) - 1);
+  if (status != EMQX_OK) L->status[c] = status;
+  Driver& d = L->drv[c % L->D];
+  bool wake;
+  {
+    std::lock_guard<std::mutex> g(d.mu);
+    d.done.push_back(c);
+    wake = d.waiting;
+  }
+  if (wake) d.cv.notify_one();
+}
+
+}  // namespace
+
+extern "C" int batch_load(emqx_engine* e, uint32_t mode, const uint8_t* bytes, const uint64_t* offs, uint64_t n,
+                          uint32_t callers, uint32_t max_batch, uint32_t max_wait_us, double warmup_ms,
+                          double duration_ms, double* out) {
+  if (!e || !bytes || !offs || !n || !callers || !out) return EMQX_EINVAL;
+  Load L;
+  L.D = std::min<uint32_t>(callers, 8);
+  L.drv = std::vector<Driver>(L.D);
+  L.t_sub.resize(callers);
+  L.status.assign(callers, EMQX_OK);
+  g_load = &L;
+  emqx_batcher* b = nullptr;
+  int rc = emqx_batcher_create(e, mode, max_batch, max_wait_us, on_result, &b);
+  if (rc != EMQX_OK) return rc;
+  std::atomic<uint64_t> next{0};
+  const auto t_start = Clock::now();
+  const auto t_meas = t_start + std::chrono::microseconds(static_cast<int64_t>(warmup_ms * 1e3));
+  const auto t_end = t_meas + std::chrono::microseconds(static_cast<int64_t>(duration_ms * 1e3));
+  std::vector<std::vector<float>> lat(L.D);
+  std::vector<uint64_t> completed(L.D, 0);
+  std::atomic<int> err{EMQX_OK};
+  auto submit = [&](uint32_t c) {
+    const uint64_t i = next.fetch_add(1) % n;
+    L.t_sub[c] = Clock::now();
+    int r = emqx_batcher_submit(b, bytes + offs[i], offs[i + 1] - offs[i],
+                                reinterpret_cast<void*>(static_cast<uintptr_t>(c) + 1));
+    if (r != EMQX_OK) err = r;
+  };
+  std::vector<std::thread> th;
+  for (uint32_t d = 0; d < L.D; ++d)
+    th.emplace_back([&, d] {
+      Driver& me = L.drv[d];
+      uint64_t outstanding = 0;
+      for (uint32_t c = d; c < callers; c += L.D, ++outstanding) submit(c);
+      std::vector<uint32_t> got;
+      while (outstanding) {
+        {
+          std::unique_lock<std::mutex> lk(me.mu);
+          me.waiting = true;
+          me.cv.wait(lk, [&] { return !me.done.empty(); });
+          me.waiting = false;
+          got.swap(me.done);
+        }
+        const auto now = Clock::now();
+        for (uint32_t c : got) {
+          --outstanding;
+          if (now >= t_meas && L.t_sub[c] >= t_meas && now < t_end) {
+            lat[d].push_back(std::chrono::duration<float, std::micro>(now - L.t_sub[c]).count());
+            completed[d] += 1;
+          }
+          if (now < t_end && err.load() == EMQX_OK) {
+            submit(c);
+            ++outstanding;
+          }
+        }
+        got.clear();
+      }
+    });
+  for (auto& x : th) x.join();
+  const double secs = std::chrono::duration<double>(std::min(Clock::now(), t_end) - t_meas).count();
+  uint64_t nb = 0, nt = 0;
+  emqx_batcher_stats(b, &nb, &nt);
+  emqx_batcher_destroy(b);
+  g_load = nullptr;
+  std::vector<float> all;
+  uint64_t done = 0;
+  for (uint32_t d = 0; d < L.D; ++d) {
+    all.insert(all.end(), lat[d].begin(), lat[d].end());
+    done += completed[d];
+  }
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double q) -> double {
+    if (all.empty()) return 0;
+    return all[std::min<size_t>(all.size() - 1, static_cast<size_t>(q * all.size()))];
+  };
+  out[0] = static_cast<double>(done);
+  out[1] = secs;
+  out[2] = pct(0.50);
+  out[3] = pct(0.90);
+  out[4] = pct(0.99);
+  out[5] = all.empty() ? 0 : all.back();
+  out[6] = static_cast<double>(nb);
+  out[7] = nb ? static_cast<double>(nt) / nb : 0;
+  for (int s : L.status)
+    if (s != EMQX_OK) return s;
+  return err.load();
+}
