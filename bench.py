@@ -103,7 +103,7 @@ def main():
     ap.add_argument("--callers", type=str, default="64,512,4096",
                     help="--workload L: concurrent single-topic callers per run")
     ap.add_argument("--max-batch", type=int, default=4096, help="--workload L: batcher max_batch")
-    ap.add_argument("--max-wait-us", type=int, default=200, help="--workload L: batcher max_wait_us")
+    ap.add_argument("--max-wait-us", type=str, default="200", help="--workload L: batcher max_wait_us (comma list)")
     ap.add_argument("--retained", type=int, default=1_000_000, help="--workload R: stored retained topics")
     ap.add_argument("--churn", type=int, default=10_000, help="--workload U: inserts and deletes per commit")
     ap.add_argument("--with-matches", action="store_true",
@@ -491,15 +491,18 @@ def batcher_bench(args, rank, world, dev):
     tb, to = wl.topics
     to = np.ascontiguousarray(to.astype(np.uint64))
     runs = []
-    for c in [int(x) for x in args.callers.split(",")]:
-        out = np.zeros(8, dtype=np.float64)
+    waits = [int(x) for x in str(args.max_wait_us).split(",")]
+    for c, wus in [(int(x), w) for x in args.callers.split(",") for w in waits]:
+        out = np.zeros(12, dtype=np.float64)
         rc = L.batch_load(eng._h, args.mode, tb.ctypes.data, to.ctypes.data, wl.n_topics, c, args.max_batch,
-                          args.max_wait_us, 500.0, 3000.0, out.ctypes.data)
+                          wus, 500.0, 3000.0, out.ctypes.data)
         if rc != 0:
             raise SystemExit(f"batch_load failed: {rc}")
-        runs.append({"callers": c, "topics_per_s": round(out[0] / out[1], 1), "p50_us": round(out[2], 1),
+        runs.append({"callers": c, "max_wait_us": wus, "topics_per_s": round(out[0] / out[1], 1), "p50_us": round(out[2], 1),
                      "p90_us": round(out[3], 1), "p99_us": round(out[4], 1), "max_us": round(out[5], 1),
-                     "batches": int(out[6]), "topics_per_batch": round(out[7], 1)})
+                     "batches": int(out[6]), "topics_per_batch": round(out[7], 1),
+                     "max_in_flight": int(out[8]), "us_per_batch_device_wait": round(out[9], 1),
+                     "us_per_batch_callbacks": round(out[10], 1), "us_per_batch_submit": round(out[11], 1)})
         log(f"[rank {rank}] callers {c}: {runs[-1]}")
     best = max(runs, key=lambda r: r["topics_per_s"])
     res = {"metric": "per-PUBLISH match_routes/1 calls served/sec through the batcher (10M subs)",
@@ -508,7 +511,7 @@ def batcher_bench(args, rank, world, dev):
            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
            "config": {"workload": "L: concurrent single-topic callers -> emqx_batcher -> pinned host batches, "
                                   "config B table", "n_filters": wl.n_filters, "max_batch": args.max_batch,
-                      "max_wait_us": args.max_wait_us, "parallelism": "replicated table"},
+                      "parallelism": "replicated table"},
            "runs": runs}
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -33,7 +33,8 @@ EXPORTS = (
     "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
     "emqx_match_batch_device", "emqx_match_batch_device_async", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
     "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_batcher_create",
-    "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_strerror", "emqx_version",
+    "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_batcher_stats_ext",
+    "emqx_batcher_submit_many", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
     "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
     "emqx_host_batch_create", "emqx_host_batch_destroy", "emqx_host_batch_reserve", "emqx_host_batch_submit",
@@ -140,6 +141,8 @@ def lib():
         "emqx_batcher_submit": (i32, [vp, vp, u64, vp]),
         "emqx_batcher_destroy": (i32, [vp]),
         "emqx_batcher_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "emqx_batcher_stats_ext": (i32, [vp, vp, u32]),
+        "emqx_batcher_submit_many": (i32, [vp, vp, vp, u64, vp]),
         "emqx_subtab_create": (i32, [ctypes.c_int32, ctypes.POINTER(vp)]),
         "emqx_subtab_destroy": (i32, [vp]),
         "emqx_subtab_add": (i32, [vp, vp, vp, vp, u64]),

@@ -58,6 +58,7 @@ struct emqx_batcher {
   bool stop = false;
   std::thread dispatcher, completer;
   uint64_t n_batches = 0, n_topics = 0, max_inflight_seen = 0;
+  uint64_t ns_wait = 0, ns_callbacks = 0, ns_submit = 0;  // completer waiting / in callbacks; dispatcher submitting
 
   // Takes the filling buffer out of the filling state (caller holds mu).
   void seal() {
@@ -87,8 +88,11 @@ struct emqx_batcher {
       const int k = ready.front();
       ready.pop_front();
       lk.unlock();
+      const auto ts = Clock::now();
       int rc = emqx_host_batch_submit(buf[k].hb, mode);
+      const uint64_t dts = std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - ts).count();
       lk.lock();
+      ns_submit += dts;
       if (rc != EMQX_OK) {  // report the failure to every caller of the batch
         lk.unlock();
         for (void* c : buf[k].ctx) cb(c, rc, nullptr, 0);
@@ -110,12 +114,14 @@ struct emqx_batcher {
       const int k = inflight.front();
       lk.unlock();
       emqx_host_batch* b = buf[k].hb;
+      const auto tw = Clock::now();
       int rc = emqx_host_batch_wait(b);
       if (rc == EMQX_EOVERFLOW) {  // more ids than the buffer holds: grow it, rerun the batch
         rc = emqx_host_batch_reserve(b, b->cap_topics, b->cap_bytes, b->n_out + (b->n_out >> 1) + 1024);
         if (rc == EMQX_OK) rc = emqx_host_batch_submit(b, mode);
         if (rc == EMQX_OK) rc = emqx_host_batch_wait(b);
       }
+      const auto tc = Clock::now();
       const std::vector<void*>& ctx = buf[k].ctx;
       for (size_t i = 0; i < ctx.size(); ++i) {
         if (rc == EMQX_OK)
@@ -123,7 +129,10 @@ struct emqx_batcher {
         else
           cb(ctx[i], rc, nullptr, 0);
       }
+      const auto te = Clock::now();
       lk.lock();
+      ns_wait += std::chrono::duration_cast<std::chrono::nanoseconds>(tc - tw).count();
+      ns_callbacks += std::chrono::duration_cast<std::chrono::nanoseconds>(te - tc).count();
       inflight.pop_front();
       n_batches += 1;
       n_topics += ctx.size();
@@ -178,9 +187,12 @@ int emqx_batcher_create(emqx_engine* e, uint32_t mode, uint32_t max_batch, uint3
   return EMQX_OK;
 }
 
-int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, void* ctx) {
-  if (!b || (len && !topic)) return EMQX_EINVAL;
-  std::unique_lock<std::mutex> lk(b->mu);
+}  // extern "C"
+
+namespace {
+
+// One topic into the filling buffer (the caller holds b->mu through lk).
+int submit_locked(emqx_batcher* b, std::unique_lock<std::mutex>& lk, const uint8_t* topic, uint64_t len, void* ctx) {
   while (true) {
     if (b->stop) return EMQX_EINVAL;
     if (b->filling < 0) {
@@ -220,6 +232,29 @@ int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, voi
   }
 }
 
+}  // namespace
+
+extern "C" {
+
+int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, void* ctx) {
+  if (!b || (len && !topic)) return EMQX_EINVAL;
+  std::unique_lock<std::mutex> lk(b->mu);
+  return submit_locked(b, lk, topic, len, ctx);
+}
+
+int emqx_batcher_submit_many(emqx_batcher* b, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                             void* const* ctxs) {
+  if (!b || (n && (!offsets || !ctxs))) return EMQX_EINVAL;
+  std::unique_lock<std::mutex> lk(b->mu);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t len = offsets[i + 1] - offsets[i];
+    if (len && !bytes) return EMQX_EINVAL;
+    const int rc = submit_locked(b, lk, bytes + offsets[i], len, ctxs[i]);
+    if (rc != EMQX_OK) return rc;
+  }
+  return EMQX_OK;
+}
+
 int emqx_batcher_destroy(emqx_batcher* b) {
   if (!b) return EMQX_EINVAL;
   {
@@ -239,6 +274,14 @@ int emqx_batcher_stats(emqx_batcher* b, uint64_t* n_batches, uint64_t* n_topics)
   std::lock_guard<std::mutex> g(b->mu);
   if (n_batches) *n_batches = b->n_batches;
   if (n_topics) *n_topics = b->n_topics;
+  return EMQX_OK;
+}
+
+int emqx_batcher_stats_ext(emqx_batcher* b, uint64_t* out, uint32_t n) {
+  if (!b || (n && !out)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(b->mu);
+  const uint64_t v[6] = {b->n_batches, b->n_topics, b->max_inflight_seen, b->ns_wait, b->ns_callbacks, b->ns_submit};
+  for (uint32_t i = 0; i < n && i < 6; ++i) out[i] = v[i];
   return EMQX_OK;
 }
 

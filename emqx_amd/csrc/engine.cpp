@@ -573,6 +573,7 @@ struct HostBatchPriv {
   std::shared_ptr<Snapshot> snap;
   uint32_t mode = 0;
   bool pending = false;
+  uint64_t evals = 0, deferred = 0, max_stack = 0;  // of the last call
 };
 
 template <class T>
@@ -672,6 +673,18 @@ int hb_wait(emqx_host_batch* b) {
   }
   p->snap.reset();
   b->n_out = total;
+  if (!(flags & SUM_F_RETRY)) {  // (run_match already recorded a rerun's numbers)
+    p->evals = p->summary[SUM_EVALS];
+    p->deferred = p->summary[SUM_DEFERRED];
+    p->max_stack = p->summary[SUM_MAXSTACK];
+    p->e->last_evals.store(p->evals);
+    p->e->last_deferred.store(p->deferred);
+    p->e->last_max_stack.store(p->max_stack);
+  } else {
+    p->evals = p->e->last_evals.load();
+    p->deferred = p->e->last_deferred.load();
+    p->max_stack = p->e->last_max_stack.load();
+  }
   return (flags & SUM_F_OVERFLOW) ? EMQX_EOVERFLOW : EMQX_OK;
 }
 
@@ -929,7 +942,7 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
   int rc = EMQX_OK;
   for (int k = 0; k < 2 && rc == EMQX_OK; ++k)
     if (!hb[k]) rc = emqx_host_batch_create(e, CH_TOPICS, CH_BYTES, CH_IDS, &hb[k]);
-  uint64_t chunk_lo[2] = {0, 0}, total = 0, next = 0;
+  uint64_t chunk_lo[2] = {0, 0}, total = 0, next = 0, evals = 0, deferred = 0, max_stack = 0;
   bool inflight[2] = {false, false}, overflow = false;
   // pack topics [next, ...) into hb[k] (rebased offsets)
   auto pack = [&](int k) -> int {
@@ -961,6 +974,10 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
       if (r == EMQX_OK) r = emqx_host_batch_wait(b);
     }
     if (r != EMQX_OK) return r;
+    const auto* p = static_cast<const HostBatchPriv*>(b->priv);
+    evals += p->evals;
+    deferred += p->deferred;
+    max_stack = std::max(max_stack, p->max_stack);
     const uint64_t lo = chunk_lo[k], m = b->n_out;
     for (uint64_t i = 0; i < b->n; ++i) out_offsets[lo + i] = total + b->out_offsets[i];
     if (!overflow && out_ids && total + m <= cap) {
@@ -991,6 +1008,9 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
     if (inflight[j]) (void)emqx_host_batch_wait(hb[j]);
   out_offsets[n] = total;
   *n_out = total;
+  e->last_evals.store(evals);  // the whole call's numbers, over its chunks
+  e->last_deferred.store(deferred);
+  e->last_max_stack.store(max_stack);
   {
     std::lock_guard<std::mutex> g(e->hb_mu);
     for (int j = 0; j < 2; ++j)

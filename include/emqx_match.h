@@ -191,8 +191,15 @@ typedef void (*emqx_batch_cb)(void* ctx, int status, const uint32_t* ids, uint64
 int emqx_batcher_create(emqx_engine* e, uint32_t mode, uint32_t max_batch, uint32_t max_wait_us,
                         emqx_batch_cb cb, emqx_batcher** out);
 int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, void* ctx);
+/* n submissions at once (topic i = bytes[offsets[i] .. offsets[i+1]), context ctxs[i]): one
+ * lock for the lot, e.g. a NIF draining a scheduler's queue of match_routes/1 calls. */
+int emqx_batcher_submit_many(emqx_batcher* b, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                             void* const* ctxs);
 int emqx_batcher_destroy(emqx_batcher* b);
 int emqx_batcher_stats(emqx_batcher* b, uint64_t* n_batches, uint64_t* n_topics);
+/* out[0..5] = batches, topics, most batches in flight at once, ns the completer spent waiting
+ * for the device, ns it spent in callbacks, ns the dispatcher spent submitting. */
+int emqx_batcher_stats_ext(emqx_batcher* b, uint64_t* out, uint32_t n);
 
 /* ---- publish fan-out ------------------------------------------------------------
  * A subscription table maps the filter ids reported by a match (engine ids, or the ext ids of

@@ -135,7 +135,7 @@ def test_batch_load_tool(table):
                              ctypes.c_void_p]
     tb, to = wl.topics
     to = np.ascontiguousarray(to.astype(np.uint64))
-    out = np.zeros(8)
+    out = np.zeros(12)
     rc = L.batch_load(e._h, 0, tb.ctypes.data, to.ctypes.data, wl.n_topics, 256, 1024, 200, 100.0, 500.0,
                       out.ctypes.data)
     assert rc == 0

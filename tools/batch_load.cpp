@@ -3,8 +3,9 @@
 // the next — as EMQX publisher processes call emqx_router:match_routes/1 once per PUBLISH
 // (apps/emqx/src/emqx_broker.erl:213).  A few driver threads own the callers (caller c
 // belongs to driver c mod D); the batcher's completion callback hands a finished caller back
-// to its driver, which records the latency and resubmits.  Throughput and latency
-// percentiles over the measured window go to out[].
+// to its driver, which records the latency and resubmits its finished callers' next topics
+// with one emqx_batcher_submit_many (as a NIF draining a scheduler's queue would).  Throughput and latency
+// percentiles over the measured window go to out[] (12 entries).
 //
 // Built by __graft_entry__.build() into tools/_build/libbatchload.so; the emqx_batcher_*
 // symbols resolve against libemqxmatch.so, which the caller has loaded (RTLD_GLOBAL).
@@ -90,7 +91,10 @@ extern "C" int batch_load(emqx_engine* e, uint32_t mode, const uint8_t* bytes, c
       Driver& me = L.drv[d];
       uint64_t outstanding = 0;
       for (uint32_t c = d; c < callers; c += L.D, ++outstanding) submit(c);
-      std::vector<uint32_t> got;
+      std::vector<uint32_t> got, again;
+      std::vector<uint8_t> mb;
+      std::vector<uint64_t> mo;
+      std::vector<void*> mc;
       while (outstanding) {
         {
           std::unique_lock<std::mutex> lk(me.mu);
@@ -100,24 +104,39 @@ extern "C" int batch_load(emqx_engine* e, uint32_t mode, const uint8_t* bytes, c
           got.swap(me.done);
         }
         const auto now = Clock::now();
+        again.clear();
         for (uint32_t c : got) {
           --outstanding;
           if (now >= t_meas && L.t_sub[c] >= t_meas && now < t_end) {
             lat[d].push_back(std::chrono::duration<float, std::micro>(now - L.t_sub[c]).count());
             completed[d] += 1;
           }
-          if (now < t_end && err.load() == EMQX_OK) {
-            submit(c);
-            ++outstanding;
-          }
+          if (now < t_end && err.load() == EMQX_OK) again.push_back(c);
         }
         got.clear();
+        if (!again.empty()) {  // the finished callers' next topics, under one batcher lock
+          mb.clear();
+          mo.assign(1, 0);
+          mc.clear();
+          const auto ts = Clock::now();
+          for (uint32_t c : again) {
+            const uint64_t i = next.fetch_add(1) % n;
+            mb.insert(mb.end(), bytes + offs[i], bytes + offs[i + 1]);
+            mo.push_back(mb.size());
+            mc.push_back(reinterpret_cast<void*>(static_cast<uintptr_t>(c) + 1));
+            L.t_sub[c] = ts;
+          }
+          const int r = emqx_batcher_submit_many(b, mb.data(), mo.data(), again.size(), mc.data());
+          if (r != EMQX_OK) err = r;
+          outstanding += again.size();
+        }
       }
     });
   for (auto& x : th) x.join();
   const double secs = std::chrono::duration<double>(std::min(Clock::now(), t_end) - t_meas).count();
-  uint64_t nb = 0, nt = 0;
+  uint64_t nb = 0, nt = 0, ext[6] = {0, 0, 0, 0, 0, 0};
   emqx_batcher_stats(b, &nb, &nt);
+  emqx_batcher_stats_ext(b, ext, 6);
   emqx_batcher_destroy(b);
   g_load = nullptr;
   std::vector<float> all;
@@ -139,6 +158,10 @@ extern "C" int batch_load(emqx_engine* e, uint32_t mode, const uint8_t* bytes, c
   out[5] = all.empty() ? 0 : all.back();
   out[6] = static_cast<double>(nb);
   out[7] = nb ? static_cast<double>(nt) / nb : 0;
+  out[8] = static_cast<double>(ext[2]);          // most batches in flight
+  out[9] = nb ? ext[3] / 1e3 / nb : 0;           // us per batch: completer waiting for the device
+  out[10] = nb ? ext[4] / 1e3 / nb : 0;          // us per batch: callbacks
+  out[11] = nb ? ext[5] / 1e3 / nb : 0;          // us per batch: submit
   for (int s : L.status)
     if (s != EMQX_OK) return s;
   return err.load();
