@@ -5,6 +5,7 @@ then `python tools/host_trace.py --analyze <dir>` reports how much of the H2D co
 kernels and how much the batches overlap each other."""
 import argparse
 import glob
+import json
 import os
 import sys
 
@@ -43,48 +44,59 @@ def run(cache):
 
 
 def analyze(d):
+    """Steady state of the host-batch phase (from the 2nd csr_to_host_kernel on): how much of
+    the span has an H2D copy running, a kernel running, both at once, and two batches'
+    kernels at once."""
     import csv
+
     def load(pat):
         rows = []
         for f in glob.glob(os.path.join(d, "**", pat), recursive=True):
             with open(f) as fh:
                 rows += list(csv.DictReader(fh))
         return rows
-    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in load("*kernel_trace.csv")]
-    cs = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", "")) for r in load("*memory_copy_trace.csv")]
-    ks.sort()
-    cs.sort()
-    if not ks or not cs:
-        print({"kernels": len(ks), "copies": len(cs)})
+    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Stream_Id"])
+          for r in load("*kernel_trace.csv")]
+    cs = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Direction"]) for r in load("*memory_copy_trace.csv")]
+    c2h = sorted(a for a, _, n, _ in ks if "csr_to_host" in n)
+    if len(c2h) < 8:
+        print({"kernels": len(ks), "copies": len(cs), "note": "no host-batch phase found"})
         return
-
-    def union(iv):
-        out = []
-        for a, b in sorted(iv):
-            if out and a <= out[-1][1]:
-                out[-1][1] = max(out[-1][1], b)
-            else:
-                out.append([a, b])
-        return out
-
-    ku = union([(a, b) for a, b, _ in ks])
-    def overlap(a, b):
-        t = 0
-        for x, y in ku:
-            t += max(0, min(b, y) - max(a, x))
-        return t
-    h2d = [(a, b) for a, b, dr in cs if "HOST_TO_DEVICE" in dr.upper() or "H2D" in dr.upper()]
-    tot = sum(b - a for a, b in h2d)
-    ov = sum(overlap(a, b) for a, b in h2d)
-    span = max(b for _, b, _ in ks) - min(a for a, _, _ in ks)
-    kbusy = sum(b - a for a, b in ku)
+    w0, w1 = c2h[1], max(b for _, b, n, _ in ks if "csr_to_host" in n)
+    ks = [(max(a, w0), min(b, w1), n, s) for a, b, n, s in ks if b > w0 and a < w1]
+    cs = [(max(a, w0), min(b, w1), n) for a, b, n in cs if b > w0 and a < w1 and "HOST_TO_DEVICE" in n]
+    # sweep: count active kernels (per stream) and copies over time
+    ev = []
+    for a, b, _, st in ks:
+        ev += [(a, 0, 1, st), (b, 0, -1, st)]
+    for a, b, _ in cs:
+        ev += [(a, 1, 1, None), (b, 1, -1, None)]
+    ev.sort(key=lambda x: (x[0], -x[2]))
+    act = {}
+    ncopy = 0
+    t_prev = w0
+    tk = tc = tboth = tkk = 0
+    for t, kind, dlt, st in ev:
+        dt = t - t_prev
+        nk = sum(1 for v in act.values() if v > 0)
+        tk += dt if nk else 0
+        tc += dt if ncopy else 0
+        tboth += dt if (nk and ncopy) else 0
+        tkk += dt if nk >= 2 else 0
+        t_prev = t
+        if kind == 0:
+            act[st] = act.get(st, 0) + dlt
+        else:
+            ncopy += dlt
+    span = w1 - w0
     names = {}
-    for a, b, nme in ks:
-        k = nme.split("(")[0][:60]
+    for a, b, nme, _ in ks:
+        k = nme.split("(")[0].replace("void ", "")[:40]
         names[k] = names.get(k, 0) + (b - a)
-    print({"h2d_copies": len(h2d), "h2d_ns": tot, "h2d_ns_overlapping_kernels": ov,
-           "h2d_overlap_frac": round(ov / max(tot, 1), 3), "kernel_busy_frac_of_span": round(kbusy / max(span, 1), 3),
-           "kernel_ns_by_name": dict(sorted(names.items(), key=lambda x: -x[1])[:8])})
+    print(json.dumps({"window_us": round(span / 1e3, 1), "kernel_active_frac": round(tk / span, 3),
+                      "h2d_active_frac": round(tc / span, 3), "h2d_and_kernel_frac": round(tboth / span, 3),
+                      "two_batches_kernels_frac": round(tkk / span, 3),
+                      "kernel_us_by_name": {k: round(v / 1e3, 1) for k, v in sorted(names.items(), key=lambda x: -x[1])[:6]}}))
 
 
 if __name__ == "__main__":
