@@ -47,6 +47,7 @@ RETAIN_EXPORTS = (
     "emqx_retain_create", "emqx_retain_destroy", "emqx_retain_store", "emqx_retain_delete",
     "emqx_retain_lookup", "emqx_retain_topic", "emqx_retain_expired", "emqx_retain_commit",
     "emqx_retain_match_batch", "emqx_retain_match_batch_device", "emqx_retain_stats_get",
+    "emqx_retain_match_spec_batch",
 )
 
 NO_GROUP = 0xFFFFFFFF
@@ -67,6 +68,7 @@ class EngineOpts(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [
+        ("size", ctypes.c_uint64),
         ("n_filters", ctypes.c_uint64), ("n_ids", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64),
         ("n_slots", ctypes.c_uint64), ("n_words", ctypes.c_uint64), ("table_bytes", ctypes.c_uint64),
         ("epoch", ctypes.c_uint64), ("last_evals", ctypes.c_uint64), ("last_deferred", ctypes.c_uint64),
@@ -76,12 +78,17 @@ class Stats(ctypes.Structure):
         ("delta_filters", ctypes.c_uint64), ("last_commit_kind", ctypes.c_uint64),
     ]
 
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.size = ctypes.sizeof(self)
+
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "size"}
 
 
 class RetainStats(ctypes.Structure):
     _fields_ = [
+        ("size", ctypes.c_uint64),
         ("n_ids", ctypes.c_uint64), ("n_live", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64),
         ("n_words", ctypes.c_uint64), ("table_bytes", ctypes.c_uint64), ("epoch", ctypes.c_uint64),
         ("last_ranges", ctypes.c_uint64), ("last_visits", ctypes.c_uint64), ("last_total", ctypes.c_uint64),
@@ -89,8 +96,12 @@ class RetainStats(ctypes.Structure):
         ("last_spill_rounds", ctypes.c_uint64), ("last_spilled", ctypes.c_uint64),
     ]
 
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.size = ctypes.sizeof(self)
+
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "size"}
 
 
 class HostBatchStruct(ctypes.Structure):
@@ -161,6 +172,7 @@ def lib():
         "emqx_retain_expired": (i32, [vp, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]),
         "emqx_retain_commit": (i32, [vp]),
         "emqx_retain_match_batch": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_retain_match_spec_batch": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64, ctypes.POINTER(u64)]),
         "emqx_retain_match_batch_device": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64,
                                                  ctypes.POINTER(u64), vp]),
         "emqx_retain_stats_get": (i32, [vp, ctypes.POINTER(RetainStats)]),

@@ -1020,8 +1020,11 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
   return rc;
 }
 
-int emqx_stats_get(emqx_engine* e, emqx_stats* out) {
-  if (!e || !out) return EMQX_EINVAL;
+int emqx_stats_get(emqx_engine* e, emqx_stats* dst) {
+  if (!e || !dst || (dst->size && dst->size < sizeof(uint64_t))) return EMQX_EINVAL;
+  const uint64_t want = dst->size ? std::min<uint64_t>(dst->size, sizeof(emqx_stats)) : sizeof(emqx_stats);
+  emqx_stats full;
+  emqx_stats* out = &full;
   std::memset(out, 0, sizeof(*out));
   {
     std::lock_guard<std::mutex> g(e->writer);
@@ -1044,6 +1047,8 @@ int emqx_stats_get(emqx_engine* e, emqx_stats* out) {
   out->last_max_stack = e->last_max_stack.load();
   out->last_match_ms = e->last_match_ms.load();
   out->last_kernel_ms = e->last_kernel_ms.load();
+  out->size = want;
+  std::memcpy(dst, out, want);
   return EMQX_OK;
 }
 

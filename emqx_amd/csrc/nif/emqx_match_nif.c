@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include "../../../include/emqx_match.h"
+#include "grow_retry.h"
 
 static ErlNifResourceType* RES_ENGINE;
 static ErlNifResourceType* RES_SUBTAB;
@@ -174,9 +175,25 @@ static ERL_NIF_TERM nif_empty(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[
   engine_res* r;
   emqx_stats st;
   (void)argc;
+  st.size = sizeof(st);
   if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r)) return enif_make_badarg(env);
   if (emqx_stats_get(r->e, &st) != EMQX_OK) return enif_make_badarg(env);
   return st.n_filters == 0 ? ATOM_TRUE : ATOM_FALSE;
+}
+
+/* emqx_match_batch as an emqx_sized_call (grow_retry.h) */
+typedef struct {
+  emqx_engine* e;
+  unsigned mode;
+  const uint8_t* bytes;
+  const uint64_t* offs;
+  unsigned n;
+  uint64_t* out_off;
+} match_call;
+
+static int call_match(void* ctx, void* buf, uint64_t cap, uint64_t* need) {
+  match_call* c = (match_call*)ctx;
+  return emqx_match_batch(c->e, c->mode, c->bytes, c->offs, c->n, c->out_off, (uint32_t*)buf, cap, need);
 }
 
 /* match_batch(Eng, Mode, [Topic]) -> {ok, [[Id]]}  (batched emqx_trie:match/1 and
@@ -191,15 +208,11 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM
       !pack_binaries(env, argv[2], &bytes, &offs, &n))
     return enif_make_badarg(env);
   uint64_t* out_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
-  uint64_t cap = 16 * (uint64_t)n + 64, total = 0;
-  uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * cap);
-  int rc = emqx_match_batch(r->e, mode, bytes, offs, n, out_off, ids, cap, &total);
-  if (rc == EMQX_EOVERFLOW) {
-    free(ids);
-    cap = total;
-    ids = (uint32_t*)malloc(sizeof(uint32_t) * (cap ? cap : 1));
-    rc = emqx_match_batch(r->e, mode, bytes, offs, n, out_off, ids, cap, &total);
-  }
+  match_call mc = {r->e, mode, bytes, offs, n, out_off};
+  void* buf = NULL;
+  uint64_t cap = 0, total = 0;
+  int rc = emqx_call_growing(call_match, &mc, sizeof(uint32_t), 16 * (uint64_t)n + 64, &buf, &cap, &total);
+  const uint32_t* ids = (const uint32_t*)buf;
   ERL_NIF_TERM out;
   if (rc == EMQX_OK) {
     ERL_NIF_TERM l = enif_make_list(env, 0);
@@ -209,7 +222,7 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM
   } else {
     out = err_term(env, rc);
   }
-  free(ids);
+  free(buf);
   free(out_off);
   free(bytes);
   free(offs);
@@ -320,6 +333,26 @@ static ERL_NIF_TERM nif_subscribe(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
   return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
 }
 
+/* emqx_publish_batch as an emqx_sized_call: subscriber ids in buf[0, cap), filter ids in
+ * buf[cap, 2 cap) */
+typedef struct {
+  emqx_engine* e;
+  emqx_subtab* s;
+  unsigned strategy;
+  const uint8_t* bytes;
+  const uint64_t* offs;
+  unsigned n;
+  const uint32_t* keys;
+  uint64_t* out_off;
+} publish_call;
+
+static int call_publish(void* ctx, void* buf, uint64_t cap, uint64_t* need) {
+  publish_call* c = (publish_call*)ctx;
+  uint32_t* subs = (uint32_t*)buf;
+  return emqx_publish_batch(c->e, c->s, c->strategy, c->bytes, c->offs, c->n, c->keys, c->out_off, subs, subs + cap,
+                            cap, need);
+}
+
 /* publish_batch(Eng, Subtab, Strategy, [{Topic, Key}]) ->
  *   {ok, [[{SubId, FilterId, Shared :: boolean()}]]}
  * Key = erlang:phash2(ClientId) or erlang:phash2(Topic) computed by the caller (hash
@@ -353,10 +386,16 @@ static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TE
   uint8_t* bytes = (uint8_t*)malloc(offs[n] ? offs[n] : 1);
   for (unsigned i = 0; i < n; ++i) memcpy(bytes + offs[i], bins[i].data, bins[i].size);
   uint64_t* out_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
-  uint64_t cap = 64 * (uint64_t)n + 64, total = 0;
-  uint32_t* subs = (uint32_t*)malloc(sizeof(uint32_t) * cap * 2);
-  int rc = emqx_publish_batch(er->e, sr->s, strategy, bytes, offs, n, keys, out_off, subs, subs + cap, cap, &total);
+  /* deliveries: subscriber ids then filter ids, `cap` each (8 bytes per delivery); a topic
+   * with more subscribers than the first guess overflows and is retried at the size the
+   * engine reports (emqx_broker:publish/1 delivers to every subscriber, emqx_broker.erl:500-524) */
+  publish_call pc = {er->e, sr->s, strategy, bytes, offs, n, keys, out_off};
+  void* buf = NULL;
+  uint64_t cap = 0, total = 0;
+  int rc = emqx_call_growing(call_publish, &pc, 2 * sizeof(uint32_t), 64 * (uint64_t)n + 64, &buf, &cap, &total);
+  ERL_NIF_TERM out;
   if (rc == EMQX_OK) {
+    const uint32_t* subs = (const uint32_t*)buf;
     ERL_NIF_TERM rows = enif_make_list(env, 0);
     for (unsigned i = n; i > 0; --i) {
       ERL_NIF_TERM row = enif_make_list(env, 0);
@@ -369,21 +408,17 @@ static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TE
       }
       rows = enif_make_list_cell(env, row, rows);
     }
-    free(subs);
-    free(out_off);
-    free(bytes);
-    free(bins);
-    free(keys);
-    free(offs);
-    return enif_make_tuple2(env, ATOM_OK, rows);
+    out = enif_make_tuple2(env, ATOM_OK, rows);
+  } else {
+    out = err_term(env, rc);
   }
-  free(subs);
+  free(buf);
   free(out_off);
   free(bytes);
   free(bins);
   free(keys);
   free(offs);
-  return err_term(env, rc); /* overflow: the Erlang side splits the batch and retries */
+  return out;
 }
 
 /* topic_match(Name, Filter) -> boolean()  (emqx_topic:match/2 on binaries; normal scheduler) */

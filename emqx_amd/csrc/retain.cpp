@@ -464,9 +464,10 @@ void release(emqx_retain* r, RWork* w) {
 // The pipeline on device buffers.  *total = ids the batch needs; ids written iff it fits.
 int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb, const uint64_t* d_fo,
               uint64_t n, uint64_t byte_span, int64_t now_ms, uint64_t* d_oo, uint32_t* d_ids, uint64_t cap,
-              hipStream_t s, uint64_t* total) {
+              hipStream_t s, uint64_t* total, bool strict_all = false) {
   RetainArgs a{};
   a.rv = sn.rv;
+  a.strict_all = strict_all ? RRANGE_STRICT : 0u;
   a.fbytes = d_fb;
   a.foffs = d_fo;
   a.n = n;
@@ -738,8 +739,10 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_fb, const ui
   return rc;
 }
 
-int emqx_retain_match_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* fo, uint64_t n, int64_t now_ms,
-                            uint64_t* out_offsets, uint32_t* out_ids, uint64_t out_cap, uint64_t* n_out) {
+namespace {
+
+int match_host(emqx_retain* r, const uint8_t* fb, const uint64_t* fo, uint64_t n, int64_t now_ms,
+               uint64_t* out_offsets, uint32_t* out_ids, uint64_t out_cap, uint64_t* n_out, bool strict_all) {
   if (!r || !n_out || !out_offsets || (n && (!fb || !fo))) return EMQX_EINVAL;
   if (n == 0) {
     out_offsets[0] = 0;
@@ -782,7 +785,8 @@ int emqx_retain_match_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* f
   rc = stage();
   uint64_t total = 0;
   if (rc == EMQX_OK)
-    rc = run_match(r, w, *sn, w->d_fb, w->d_fo, n, span, now_ms, w->d_oo, w->d_ids, out_cap, w->stream, &total);
+    rc = run_match(r, w, *sn, w->d_fb, w->d_fo, n, span, now_ms, w->d_oo, w->d_ids, out_cap, w->stream, &total,
+                   strict_all);
   if (rc == EMQX_OK || rc == EMQX_EOVERFLOW) {
     if (hipMemcpy(out_offsets, w->d_oo, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
       rc = EMQX_EDEVICE;
@@ -795,8 +799,24 @@ int emqx_retain_match_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* f
   return rc;
 }
 
-int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out) {
-  if (!r || !out) return EMQX_EINVAL;
+}  // namespace
+
+int emqx_retain_match_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* fo, uint64_t n, int64_t now_ms,
+                            uint64_t* out_offsets, uint32_t* out_ids, uint64_t out_cap, uint64_t* n_out) {
+  return match_host(r, fb, fo, n, now_ms, out_offsets, out_ids, out_cap, n_out, false);
+}
+
+int emqx_retain_match_spec_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* fo, uint64_t n, int64_t now_ms,
+                                 uint64_t* out_offsets, uint32_t* out_ids, uint64_t out_cap, uint64_t* n_out) {
+  return match_host(r, fb, fo, n, now_ms, out_offsets, out_ids, out_cap, n_out, true);
+}
+
+int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* dst) {
+  if (!r || !dst || (dst->size && dst->size < sizeof(uint64_t))) return EMQX_EINVAL;
+  const uint64_t want =
+      dst->size ? std::min<uint64_t>(dst->size, sizeof(emqx_retain_stats)) : sizeof(emqx_retain_stats);
+  emqx_retain_stats full;
+  emqx_retain_stats* out = &full;
   std::memset(out, 0, sizeof(*out));
   {
     std::lock_guard<std::mutex> g(r->writer);
@@ -818,6 +838,8 @@ int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out) {
   out->last_total = r->last_total.load();
   out->last_match_ms = r->last_match_ms.load();
   out->last_walk_ms = r->last_walk_ms.load();
+  out->size = want;
+  std::memcpy(dst, out, want);
   return EMQX_OK;
 }
 

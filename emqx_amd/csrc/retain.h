@@ -111,6 +111,7 @@ struct RetainArgs {
   const uint64_t* foffs;   // [n + 1]
   uint64_t n;
   int64_t now_ms;          // < 0: no expiry guard (match_delete_messages)
+  uint32_t strict_all;     // RRANGE_STRICT for every filter (match spec calls), else wildcard ones only
   uint32_t* wids;          // [foffs[n] - foffs[0] + n] scratch: word ids, filter f at foffs[f] - foffs[0] + f
   uint4* stack;            // [waves * stack_cap] per-wave work stacks (range items)
   uint32_t stack_cap;

@@ -211,7 +211,9 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       }
       const uint32_t fn = nl & 0x7FFFFFFFu;
       rg.f = static_cast<uint32_t>(fg);
-      rg.flags = nl >> 31;  // wildcard filter: the match spec's strict guard
+      // the match spec's strict guard for wildcard filters, and for every filter of a match
+      // spec call (match_messages/3, page_read/4); read_message/2's `>=` otherwise
+      rg.flags = (nl >> 31) | a.strict_all;
       if (lev == fn) {
         if (rn.ncld & RNODE_TERM) {
           emit = true;

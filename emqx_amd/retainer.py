@@ -108,24 +108,27 @@ class RetainIndex:
         check(_lib.lib().emqx_retain_stats_get(self._h, ctypes.byref(st)), "emqx_retain_stats_get")
         return st.as_dict()
 
-    def match_packed(self, buf: np.ndarray, offs: np.ndarray, now: int) -> Tuple[np.ndarray, np.ndarray]:
-        """dispatch/4's topic ids for every filter: CSR (offsets[n+1] u64, ids u32)."""
+    def match_packed(self, buf: np.ndarray, offs: np.ndarray, now: int,
+                     match_spec: bool = False) -> Tuple[np.ndarray, np.ndarray]:
+        """dispatch/4's topic ids for every filter: CSR (offsets[n+1] u64, ids u32).  match_spec:
+        match_messages/3 / page_read/4 semantics instead (the strict expiry guard for every
+        filter, emqx_retain_match_spec_batch)."""
+        fn = _lib.lib().emqx_retain_match_spec_batch if match_spec else _lib.lib().emqx_retain_match_batch
         n = len(offs) - 1
         off = np.zeros(n + 1, dtype=np.uint64)
         cap = max(4 * n, 1024)
         while True:
             ids = np.zeros(cap, dtype=np.uint32)
             got = ctypes.c_uint64()
-            rc = _lib.lib().emqx_retain_match_batch(self._h, _ptr(buf), _ptr(offs), n, now, _ptr(off), _ptr(ids),
-                                                    cap, ctypes.byref(got))
+            rc = fn(self._h, _ptr(buf), _ptr(offs), n, now, _ptr(off), _ptr(ids), cap, ctypes.byref(got))
             if rc == EMQX_EOVERFLOW:
                 cap = int(got.value) + 16
                 continue
             check(rc, "emqx_retain_match_batch")
             return off, ids[: got.value]
 
-    def match(self, filters: Sequence[bytes], now: int) -> List[List[int]]:
-        off, ids = self.match_packed(*pack(list(filters)), now)
+    def match(self, filters: Sequence[bytes], now: int, match_spec: bool = False) -> List[List[int]]:
+        off, ids = self.match_packed(*pack(list(filters)), now, match_spec)
         return [sorted(int(x) for x in ids[off[i]:off[i + 1]]) for i in range(len(filters))]
 
     def match_device(self, d_bytes: int, d_offs: int, n: int, now: int, d_out_off: int, d_out_ids: int, cap: int,
@@ -193,7 +196,8 @@ class MnesiaRetainer:
     def match_messages(self, filt: bytes, cursor=None, now: Optional[int] = None):
         if cursor is None:
             self._sync()
-            ms = self._sorted(self.index.match([filt], now_ms() if now is None else now)[0])
+            # make_match_spec/1: the strict guard Et > Now, plain filters included
+            ms = self._sorted(self.index.match([filt], now_ms() if now is None else now, match_spec=True)[0])
             if self.max_read_number == 0:
                 return ms, None
             cursor = ms
@@ -204,7 +208,8 @@ class MnesiaRetainer:
     def match_messages_batch(self, filters: Sequence[bytes], now: Optional[int] = None) -> List[List[Message]]:
         """One device call for many subscriptions (a subscribe storm)."""
         self._sync()
-        return [self._sorted(ids) for ids in self.index.match(filters, now_ms() if now is None else now)]
+        return [self._sorted(ids) for ids in self.index.match(filters, now_ms() if now is None else now,
+                                                              match_spec=True)]
 
     # emqx_retainer_mnesia.erl:117-128, 217-223
     def delete_message(self, topic: bytes) -> None:
@@ -240,7 +245,7 @@ class MnesiaRetainer:
             t = now_ms() if now is None else now
             ms = [m for m in ms if m.expiry_time == 0 or m.expiry_time > t]
         else:
-            ms = self._sorted(self.index.match([topic], now_ms() if now is None else now)[0])
+            ms = self._sorted(self.index.match([topic], now_ms() if now is None else now, match_spec=True)[0])
         start = (page - 1) * limit if page > 1 else 0
         return ms[start:start + limit]
 

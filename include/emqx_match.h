@@ -68,7 +68,11 @@ typedef struct emqx_engine_opts {
   uint32_t flags;        /* reserved, must be 0                                             */
 } emqx_engine_opts;
 
+/* Versioned by size: the caller sets `size` to sizeof(emqx_stats) as it was compiled; the
+ * engine writes at most that many bytes (fields are only ever appended) and sets `size` to
+ * the bytes it wrote, so a caller built against an older, shorter struct stays safe. */
 typedef struct emqx_stats {
+  uint64_t size;             /* in: sizeof(emqx_stats) of the caller; out: bytes written      */
   uint64_t n_filters;        /* live filters                                                 */
   uint64_t n_ids;            /* ids ever assigned (ids are never reused)                    */
   uint64_t n_nodes;          /* level-trie nodes in the committed snapshot (root included)  */

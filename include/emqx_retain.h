@@ -43,7 +43,9 @@ extern "C" {
 
 typedef struct emqx_retain emqx_retain;
 
+/* Versioned by size, as emqx_stats: set `size` = sizeof(emqx_retain_stats) before the call. */
 typedef struct emqx_retain_stats {
+  uint64_t size;             /* in: sizeof(emqx_retain_stats) of the caller; out: bytes written */
   uint64_t n_ids;            /* topic ids ever assigned                                     */
   uint64_t n_live;           /* retained topics stored (emqx_retainer_mnesia:size/1)        */
   uint64_t n_nodes;          /* trie nodes of the committed snapshot                        */
@@ -86,6 +88,13 @@ int emqx_retain_commit(emqx_retain* r);
 int emqx_retain_match_batch(emqx_retain* r, const uint8_t* filter_bytes, const uint64_t* filter_offsets,
                             uint64_t n, int64_t now_ms, uint64_t* out_offsets, uint32_t* out_ids,
                             uint64_t out_cap, uint64_t* n_out);
+/* match_messages/3 and page_read/4 semantics (emqx_retainer_mnesia.erl:136-158,210-215,233-246):
+ * the match spec's strict guard (Et =:= 0 orelse Et > Now) for every filter, plain ones
+ * included — where emqx_retain_match_batch follows dispatch/4 (emqx_retainer.erl:119-131):
+ * read_message/2's Et >= Now for a plain filter, the match spec for a wildcard one. */
+int emqx_retain_match_spec_batch(emqx_retain* r, const uint8_t* filter_bytes, const uint64_t* filter_offsets,
+                                 uint64_t n, int64_t now_ms, uint64_t* out_offsets, uint32_t* out_ids,
+                                 uint64_t out_cap, uint64_t* n_out);
 /* Same, with every buffer in device memory of the index's device, on `stream` (0 = the
  * index's own).  Synchronizes the stream before returning. */
 int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes,

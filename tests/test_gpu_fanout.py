@@ -277,3 +277,47 @@ def test_async_fanout_pipelined_streams(F):
     assert sl == int(oo_ref[n] - oo_ref[h])
     assert np.array_equal(osubs[:sl].cpu().numpy(), ref[1][oo_ref[h]:])
     assert np.array_equal(ooff[:n - h + 1].cpu().numpy(), oo_ref[h:] - oo_ref[h])
+
+
+def test_publish_batch_overflow_retry_10k_subscribers():
+    """emqx_publish_batch on a topic with 10K subscribers (plus a $share group) through the
+    NIF's protocol (emqx_amd/csrc/nif/grow_retry.h): the 64-per-topic first guess overflows,
+    n_out reports the deliveries needed, the retry at that size returns every subscriber
+    (emqx_broker.erl:500-524) and one pick of the group (emqx_shared_sub.erl:251-288)."""
+    import ctypes
+    import torch  # noqa: F401
+    from emqx_amd import _lib
+    from emqx_amd.engine import Engine, pack
+    from emqx_amd.fanout import SubTable
+    e = Engine()
+    ids = e.insert([b"hot/topic", b"hot/+", b"other/x"])
+    e.commit()
+    st = SubTable()
+    subs = np.arange(10_000, dtype=np.uint32)
+    st.add(np.full(10_000, ids[0], np.uint32), subs)
+    st.add(np.full(5, ids[1], np.uint32), np.arange(20_000, 20_005, dtype=np.uint32), np.full(5, 3, np.uint32))
+    st.add(np.array([ids[2]], np.uint32), np.array([7], np.uint32))
+    st.commit()
+    buf, offs = pack([b"hot/topic", b"other/x"])
+    keys = np.array([11, 12], np.uint32)
+    L = _lib.lib()
+    out_off = np.zeros(3, np.uint64)
+    cap = 64 * 2 + 64
+    n_out = ctypes.c_uint64(0)
+    sb, fb = np.zeros(cap, np.uint32), np.zeros(cap, np.uint32)
+    rc = L.emqx_publish_batch(e._h, st.handle, _lib.SHARE_HASH_CLIENTID, buf.ctypes.data, offs.ctypes.data, 2,
+                              keys.ctypes.data, out_off.ctypes.data, sb.ctypes.data, fb.ctypes.data, cap,
+                              ctypes.byref(n_out))
+    assert rc == _lib.EMQX_EOVERFLOW and n_out.value == 10_000 + 1 + 1
+    cap = int(n_out.value)
+    sb, fb = np.zeros(cap, np.uint32), np.zeros(cap, np.uint32)
+    rc = L.emqx_publish_batch(e._h, st.handle, _lib.SHARE_HASH_CLIENTID, buf.ctypes.data, offs.ctypes.data, 2,
+                              keys.ctypes.data, out_off.ctypes.data, sb.ctypes.data, fb.ctypes.data, cap,
+                              ctypes.byref(n_out))
+    assert rc == 0 and out_off.tolist() == [0, 10_001, 10_002]
+    first = sb[:10_001]
+    plain = first[(fb[:10_001] & _lib.FANOUT_SHARED_BIT) == 0]
+    shared = first[(fb[:10_001] & _lib.FANOUT_SHARED_BIT) != 0]
+    assert sorted(plain.tolist()) == subs.tolist()
+    assert shared.tolist() == [20_000 + 11 % 5]   # hash_clientid: lists:nth(1 + Key rem N, Members)
+    assert sb[10_001] == 7

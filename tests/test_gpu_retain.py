@@ -230,3 +230,36 @@ def test_tile_sizes_parity(mod, monkeypatch, tile):
     assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
     for f, g, r in zip(filters, got, ref):
         assert g == r == tt.dispatch(f, 100), f
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_match_spec_strict_guard_for_plain_filters(mod, seed):
+    """match_messages/3 and page_read/4 run make_match_spec/1 for plain topics too, whose guard
+    is Et > Now (emqx_retainer_mnesia.erl:233-246); dispatch/4 reads a plain topic with
+    read_messages/1's Et >= Now (:197-208).  At expiry == now the two differ."""
+    rng = random.Random(900 + seed)
+    names = sorted({rand_topic(rng) for _ in range(300)})
+    expiry = [rng.choice([0, 99, 100, 101]) for _ in names]
+    idx = mod.RetainIndex()
+    idx.store(names, expiry)
+    idx.commit()
+    tab = RR.RetainTable()
+    for t, e in zip(names, expiry):
+        tab.store(t, e)
+    filters = names[::3] + [rand_filter(rng) for _ in range(200)]
+    now = 100
+    spec = idx.match(filters, now, match_spec=True)
+    disp = idx.match(filters, now)
+    for f, s_, d in zip(filters, spec, disp):
+        assert s_ == sorted(tab.match_messages(f, now)), f
+        assert d == sorted(tab.dispatch(f, now)), f
+    at_now = [t for t, e in zip(names, expiry) if e == now]
+    assert at_now
+    for t in at_now:  # the expiry == now topic: dispatched, not selected by the match spec
+        assert idx.match([t], now)[0] == [names.index(t)]
+        assert idx.match([t], now, match_spec=True)[0] == []
+    # and the mnesia mirror's page_read/4 on a plain topic follows the match spec
+    st = mod.MnesiaRetainer()
+    st.store_retained(mod.Message(b"p/q", b"x", 0, now))
+    assert st.page_read(b"p/q", 1, 10, now=now) == []
+    assert [m.topic for m in st.dispatch(b"p/q", now)] == [b"p/q"]
