@@ -112,8 +112,10 @@ def main():
     ap.add_argument("--strategy", type=str, default="hash_clientid",
                     help="$share strategy for --workload E")
     ap.add_argument("--sharded", action="store_true",
-                    help="filter-sharded table (filter i on rank i mod N): rank 0's batch is broadcast over "
-                         "RCCL, matched on every shard, gathered and concatenated on rank 0 (strong scaling)")
+                    help="filter-sharded table (filters by a hash of their first two levels, wildcard-keyed "
+                         "ones replicated): rank 0's batch is partitioned by owner rank, exchanged with one "
+                         "RCCL all-to-all, matched on one shard per topic, and the results return with a "
+                         "second all-to-all (strong scaling)")
     ap.add_argument("--vocab-scale", type=int, default=1, help="4 = config C's vocabulary")
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the timed batches alternate over (pipelined calls; default 3, "
@@ -220,11 +222,17 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t_start = time.perf_counter()
+    ev0.record(streams[0])
     for k in range(args.steps):
         j = k % len(streams)
+        if 0 < k < len(streams):  # the other streams start after the timed region began
+            streams[j].wait_event(ev0)
         eng.match_device_async(tb.data_ptr(), to.data_ptr(), n, outs[j][0].data_ptr(), outs[j][1].data_ptr(), cap,
                                summ[k].data_ptr(), mode=args.mode, stream=streams[j].cuda_stream)
+        evs[k].record(streams[j])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -255,6 +263,9 @@ def main():
     topics_total = float(n) * world * args.steps
     value = topics_total / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
+    # completion times of the steps (events on their streams), as intervals between completions
+    done = np.sort([ev0.elapsed_time(e) for e in evs]) if args.steps else np.zeros(0)
+    gaps = np.diff(np.concatenate([[0.0], done]))
 
     # roofline of the fused match kernel (rank 0's launch): algorithmic bytes / kernel time
     offs = wl.topics[1].astype(np.int64)
@@ -295,6 +306,8 @@ def main():
         "matches_per_topic": round(nout_all / (n * world), 3),
         "evals_per_topic": round(evals_all / (n * world), 3),
         "call_ms_avg": round(float(np.mean(call_ms)), 4),
+        "step_completion_gap_ms": {"p50": round(float(np.median(gaps)), 4) if gaps.size else None,
+                                   "max": round(float(np.max(gaps)), 4) if gaps.size else None},
         "roofline": roofline,
     }
 
@@ -329,8 +342,9 @@ def main():
 
 
 def sharded_bench(args, rank, world, dev):
-    """Config C style: the table is split over the ranks; every step broadcasts rank 0's batch,
-    matches it on every shard and gathers the merged CSR on rank 0."""
+    """Config C style: the table is split over the ranks (emqx_amd/dist.py); every step
+    partitions rank 0's batch by owner rank, exchanges the parts (all-to-all), matches each
+    topic on its one owner shard and returns the CSR to rank 0 in batch order."""
     import torch
     import torch.distributed as dist
     from emqx_amd import workloads as W
@@ -376,8 +390,8 @@ def sharded_bench(args, rank, world, dev):
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": f"{'C' if args.vocab_scale > 1 else 'B'}-generator table of {wl.n_filters} "
-                                   f"filters sharded x{world}, one {n}-topic batch broadcast per step",
-                       "parallelism": f"filter-sharded x{world}, RCCL broadcast + gather"},
+                                   f"filters sharded x{world}, one {n}-topic batch per step from rank 0",
+                       "parallelism": f"filter-sharded x{world} by the first two levels, RCCL all-to-all out and back"},
             "matches_per_topic": round(int(res[0][-1].item()) / n, 3),
         }), flush=True)
     dist.barrier()
@@ -651,6 +665,12 @@ def fanout_bench(args, rank, world, dev):
         elapsed = float(tt.item())
     fo = float(np.median(fo_ms))
     alg = 32 * nm + 12 * nd  # per match entry: id, filter record, offsets, topic; per delivery: read + 2 writes
+    froof = {"bound": "hbm", "achieved": round(alg / (fo * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(alg / (fo * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+             "traffic": None, "kernel": "fan-out call (count, scan, offsets, write kernels)",
+             "kernel_ms_avg": round(fo, 4), "alg_bytes_per_launch": alg,
+             "alg_bytes_model": "32 B per match entry + 12 B per delivery; time of the synchronous fan-out "
+                                "call (all its kernels)"}
     res = {
         "metric": "published topics matched and fanned out/sec (config E, 10M subscriptions)",
         "value": round(n * world * args.steps / elapsed, 1), "unit": "topics/s", "n_gpus": world,
@@ -662,15 +682,16 @@ def fanout_bench(args, rank, world, dev):
         "deliveries_per_s": round(nd * world * args.steps / elapsed, 1),
         "matches_per_topic": round(nm / n, 3), "deliveries_per_topic": round(nd / n, 3),
         "match_call_ms": round(float(np.median(kern)), 4), "fanout_call_ms": round(fo, 4),
-        "fanout_roofline": {"bound": "hbm", "achieved": round(alg / (fo * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": round(alg / (fo * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                            "alg_bytes_per_call": alg,
-                            "alg_bytes_model": "32 B per match entry + 12 B per delivery; call time incl. "
-                                               "count/scan/offsets, the write kernel and the synchronous "
-                                               "call's readbacks"},
+        "roofline": froof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = fanout_cpu_baseline(fw, args)
+        k = min(args.cpu_sample, n)
+        off_g = ooff[: k + 1].cpu().numpy().view(np.uint64)
+        tot_k = int(off_g[-1])
+        gpu = (off_g, osubs[:tot_k].cpu().numpy().view(np.uint32), ofil[:tot_k].cpu().numpy().view(np.uint32))
+        res["cpu_baseline"] = fanout_cpu_baseline(fw, args, gpu)
+        if "parity" in res["cpu_baseline"]:
+            res["parity"] = res["cpu_baseline"].pop("parity")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -678,37 +699,40 @@ def fanout_bench(args, rank, world, dev):
         dist.destroy_process_group()
 
 
-def fanout_cpu_baseline(fw, args):
-    """Host restatement of publish/1's lookup + dispatch on a bounded sample: the C++ port of
-    emqx_trie's DFS (oracle) for the match, then per matched filter a dictionary read of its
-    subscribers and one pick per $share group (like the ?SUBSCRIBER / shared-sub ETS reads)."""
+def fanout_cpu_baseline(fw, args, gpu=None):
+    """Host restatement of publish/1's lookup + dispatch on a bounded sample, one thread per
+    host core: the C++ port of emqx_trie's DFS + match_routes/1 (oracle/trie_oracle.cpp), then
+    route/aggre/do_dispatch and the hash $share pick per matched filter
+    (oracle/fanout_oracle.cpp).  `gpu` = (offsets, subs, filters) of the GPU's fan-out of the
+    same batch: per-topic delivery counts and multiset checksums must be equal (hash
+    strategies are deterministic given the caller's phash2 key)."""
     from emqx_amd import workloads as W
     from oracle import cpp as C
     o = C.CppOracle(True)
-    o.add_packed(*fw.wl.filters)
-    o.freeze()
-    plain, groups = {}, {}
-    for f, s_, g in zip(fw.sub_filter.tolist(), fw.sub_id.tolist(), fw.sub_group.tolist()):
-        if g == W.NO_GROUP:
-            plain.setdefault(f, []).append(s_)
-        else:
-            groups.setdefault(f, {}).setdefault(g, []).append(s_)
-    sample = min(20_000, fw.wl.n_topics)
+    with progress("E baseline: building the oracle table"):
+        o.add_packed(*fw.wl.filters)
+        o.freeze()
+    fo = C.FanoutOracle(fw.sub_filter, fw.sub_id, fw.sub_group)
+    sample = min(args.cpu_sample, fw.wl.n_topics)
     s = W.take(fw.wl.topics, np.arange(sample))
+    threads = args.cpu_threads or host_threads()[0]
     t0 = time.perf_counter()
-    counts, ids, _ = o.match_packed(*s, mode=0, threads=1, stride=256)
-    nd = 0
-    keys = fw.keys
-    for i in range(sample):
-        for f in ids[i, :counts[i]].tolist():
-            out = list(plain.get(f, ()))
-            for mem in groups.get(f, {}).values():
-                out.append(mem[keys[i] % len(mem)])
-            nd += len(out)
+    moff, mids, _ = o.match_csr(*s, mode=0, threads=threads)
+    counts, sums, total = fo.publish(moff, mids, fw.keys[:sample], threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": round(sample / dt, 1), "unit": "topics/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample} topics; C++ DFS match + Python dict fan-out, one thread",
-            "deliveries_per_topic": round(nd / sample, 3)}
+    res = {"value": round(sample / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
+           "sample": f"first {sample} topics; C++ DFS match + C++ route/dispatch with hash $share picks",
+           "deliveries_per_topic": round(total / max(sample, 1), 3)}
+    if gpu is not None and args.strategy in ("hash_clientid", "hash_topic", "hash"):
+        off_g, subs_g, fils_g = gpu
+        off_g = off_g[: sample + 1]
+        gsum = C.delivery_checksums(off_g, subs_g, fils_g)
+        bad = np.nonzero((np.diff(off_g.astype(np.int64)) != counts.astype(np.int64)) | (gsum != sums))[0]
+        res["parity"] = {"topics_checked": int(sample), "deliveries_checked": int(total), "mismatches": int(bad.size),
+                         "rule": "per-topic delivery count + order-free multiset checksum of (subscriber, filter)"}
+        if bad.size:
+            raise SystemExit(f"GPU fan-out differs from the oracle on {bad.size} topics, first {bad[:10].tolist()}")
+    return res
 
 
 def update_bench(args, rank, world, dev):

@@ -429,7 +429,7 @@ int ensure_ws(Workspace* w, uint64_t n) {
   }
   const uint64_t need_slab = std::max<uint64_t>(ntiles, 1) * w->slab_per_tile;
   if (need_slab > w->cap_slab) {
-    const uint64_t cap = round_pow2(need_slab);
+    const uint64_t cap = need_slab;
     HIP_TRY(dalloc(w->slab, cap));
     w->cap_slab = cap;
   }
@@ -523,7 +523,11 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
     }
     if (flags & SUM_F_RETRY) {
       if (sm[SUM_NEED_SLAB] > w->slab_per_tile) {
-        w->slab_per_tile = static_cast<uint32_t>(round_pow2(sm[SUM_NEED_SLAB]));
+        // the learnt need plus 1/8, in whole 512-entry (4 KiB) blocks: a power of two would
+        // nearly double the slab on a '#'-rich table (config D: 16 GB instead of ~9 GB per
+        // workspace), and every stream in flight holds its own
+        const uint64_t need = sm[SUM_NEED_SLAB];
+        w->slab_per_tile = static_cast<uint32_t>(((need + need / 8) + 511) / 512 * 512);
         uint32_t h = e->slab_hint.load();  // later workspaces start at the learnt size
         while (h < w->slab_per_tile && !e->slab_hint.compare_exchange_weak(h, w->slab_per_tile)) {
         }
@@ -1093,6 +1097,13 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
     return EMQX_OK;
   }
   return EMQX_ENOTFOUND;
+}
+
+int emqx_shard_owner_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t world,
+                            uint32_t levels, uint32_t* d_owner, void* stream) {
+  if ((n && (!d_bytes || !d_offsets || !d_owner)) || world == 0 || levels == 0) return EMQX_EINVAL;
+  HIP_TRY(launch_shard_owner(d_bytes, d_offsets, n, world, levels, d_owner, static_cast<hipStream_t>(stream)));
+  return EMQX_OK;
 }
 
 int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n) {

@@ -184,4 +184,29 @@ EMQX_HD bool litf_may_contain(uint32_t meta, uint32_t litf, uint32_t wid) {
 }
 constexpr uint32_t LITF_BLOOM_MAX = 16;  // wider children get an all-ones filter
 
+// Filter-sharded tables (emqx_amd/dist.py): the rank that owns a filter / topic is a hash of
+// its first `levels` levels (their bytes, separators included).  A filter with a '+' or '#'
+// among those levels, or with fewer levels, can match topics of more than one key, so it is
+// replicated on every rank (SHARD_ALL); every other filter lives with the topics of its key,
+// and each topic is matched on exactly one rank.  Topics: a key level that is '+' / '#' (a
+// wildcard "topic", matched byte for byte by match_routes/1 against replicated filters) sends
+// the topic to rank 0; a topic shorter than `levels` hashes the levels it has.
+constexpr uint32_t SHARD_ALL = 0xFFFFFFFFu;
+EMQX_HD uint32_t shard_owner(const uint8_t* p, uint64_t n, uint32_t world, uint32_t levels, bool topic) {
+  uint64_t s = 0, e = 0;
+  uint32_t k = 0;
+  while (k < levels) {
+    e = s;
+    while (e < n && p[e] != '/') ++e;
+    if (e - s == 1 && (p[s] == '+' || p[s] == '#')) return topic ? 0u : SHARD_ALL;
+    ++k;
+    if (e >= n) break;
+    s = e + 1;
+  }
+  if (k < levels && !topic) return SHARD_ALL;
+  uint32_t h = 0x811C9DC5u;  // FNV-1a over the key levels' bytes
+  for (uint64_t i = 0; i < e; ++i) h = (h ^ p[i]) * 0x01000193u;
+  return mix32(h ^ k) % world;
+}
+
 }  // namespace emqx

@@ -1308,6 +1308,18 @@ __global__ __launch_bounds__(256) void csr_to_host_kernel(const uint64_t* __rest
   if (tid < total - 4 * nv) h_ids[4 * nv + tid] = d_ids[4 * nv + tid];
 }
 
+// Filter-sharded tables: the owner rank of each topic of a batch (layout.h shard_owner).
+__global__ __launch_bounds__(256) void shard_owner_kernel(const uint8_t* __restrict__ tbytes,
+                                                          const uint64_t* __restrict__ toffs, uint64_t n,
+                                                          uint32_t world, uint32_t levels,
+                                                          uint32_t* __restrict__ owner) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t a = toffs[i], b = toffs[i + 1];
+    owner[i] = shard_owner(tbytes + a, b - a, world, levels, true);
+  }
+}
+
 // Incremental commits (live_trie.cpp): rewrites existing slots of the committed table in
 // place.  Phase 0 writes the slots' filter ids, phase 1 (a later launch) the slots, each with
 // one 16-B store, so a concurrent walk sees every slot either old or new, and never a slot
@@ -1393,6 +1405,14 @@ hipError_t launch_csr_to_host(const uint64_t* d_off, uint64_t n, const uint32_t*
   const uint64_t work = std::max<uint64_t>((n + 1) / 2, cap / 4);
   const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((work + 255) / 256 + 1, 2048));
   hipLaunchKernelGGL(csr_to_host_kernel, dim3(blocks), dim3(256), 0, s, d_off, n, d_ids, cap, h_off, h_ids);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_owner(const uint8_t* tbytes, const uint64_t* toffs, uint64_t n, uint32_t world,
+                              uint32_t levels, uint32_t* owner, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((n + 255) / 256, 4096));
+  hipLaunchKernelGGL(shard_owner_kernel, dim3(blocks), dim3(256), 0, s, tbytes, toffs, n, world, levels, owner);
   return hipGetLastError();
 }
 

@@ -74,6 +74,16 @@ extern "C" int emqx_topic_match(const uint8_t* name, uint64_t nlen, const uint8_
 // Host-only builder self-check (no device needed): builds the level trie of the given
 // filters and verifies its lookup invariants.  stats_out (optional, 4 entries): nodes,
 // slots, words, perfect-hashed nodes.
+extern "C" int emqx_shard_owner(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
+                                uint32_t levels, int topics, uint32_t* owner_out) {
+  if ((n && (!offsets || !owner_out)) || world == 0 || levels == 0) return EMQX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i]) return EMQX_EINVAL;
+    owner_out[i] = emqx::shard_owner(bytes + offsets[i], offsets[i + 1] - offsets[i], world, levels, topics != 0);
+  }
+  return EMQX_OK;
+}
+
 extern "C" int emqx_build_check(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* stats_out,
                                 char* err, uint64_t err_cap) {
   emqx::FilterStore fs;

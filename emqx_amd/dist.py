@@ -8,24 +8,30 @@ SURVEY §8(e).  Two layouts:
   across a cluster: every node holds a full mria copy of the route table
   (apps/emqx/src/emqx_router.erl:135, apps/emqx/src/emqx_trie.erl:72-77).
 
-* **Filter-sharded** (``ShardedMatcher``): filter ``i`` lives on rank ``i mod G``; each rank builds
-  the level trie of its shard with GLOBAL filter ids (``emqx_insert_filters_ext``).  A topic
-  batch is broadcast from its source rank, every rank matches it against its shard, and the
-  per-topic union — a concatenation, the shards being disjoint — is assembled on the
-  destination rank from an all-gather of per-topic counts and a gather of the id lists.
-
-Collective payloads per 1M-topic batch of config B: the batch (~44 MB) broadcast once, counts
-4 MB per rank, ids ~56 MB in total — large, few collectives, as ring collectives over the
-point-to-point xGMI links want.
+* **Filter-sharded** (``ShardedMatcher``): a filter lives on the rank its first SHARD_LEVELS
+  (2) levels hash to (``emqx_shard_owner``); a filter with ``+`` or ``#`` among those levels, or
+  with fewer levels, can match topics of several keys and is replicated on every rank (about a
+  tenth of config B's filters).  Two key levels instead of one keep a Zipf-hot first level
+  (a third of the topics on config C's generator) from landing on one rank.  So every filter that can match a topic
+  lives on the topic's owner rank, and each topic is matched on exactly one rank: a batch is
+  partitioned by owner on its source rank, the parts are exchanged with one all-to-all, every
+  rank matches only its part against its shard, and the per-topic results go back to the
+  destination with a second all-to-all, where they are put back in batch order.  Per-rank walk
+  work falls as 1/G; the collectives move each topic and each result once.
+  Each rank builds its shard's trie with GLOBAL filter ids (``emqx_insert_filters_ext``).
 """
 
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence, Tuple
+import ctypes
+from typing import Callable, List, Optional, Tuple
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+SHARD_ALL = 0xFFFFFFFF
+SHARD_LEVELS = 2
 
 
 def split_topics(packed: Tuple[np.ndarray, np.ndarray], rank: int, world: int):
@@ -36,44 +42,91 @@ def split_topics(packed: Tuple[np.ndarray, np.ndarray], rank: int, world: int):
     return take(packed, np.arange(lo, hi))
 
 
-def shard_of(ids: np.ndarray, world: int) -> np.ndarray:
-    """Filter-sharded mode: the rank that owns each global filter id."""
-    return (np.asarray(ids, dtype=np.int64) % world).astype(np.int64)
+def shard_owner(packed: Tuple[np.ndarray, np.ndarray], world: int, levels: int = SHARD_LEVELS,
+                topics: bool = False) -> np.ndarray:
+    """Owner rank of each filter (uint32; SHARD_ALL = replicated) or topic, emqx_shard_owner."""
+    from . import _lib
+    buf, offs = packed
+    offs = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
+    n = len(offs) - 1
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    b = np.ascontiguousarray(buf) if len(buf) else np.zeros(1, np.uint8)
+    _lib.check(_lib.lib().emqx_shard_owner(b.ctypes.data, offs.ctypes.data, n, world, levels, int(topics),
+                                           out.ctypes.data), "emqx_shard_owner")
+    return out[:n]
 
 
 def shard_filters(packed: Tuple[np.ndarray, np.ndarray], rank: int, world: int):
-    """(packed filters of this rank's shard, their global ids)."""
+    """(packed filters of this rank's shard, their global ids): the filters whose key levels
+    hash to `rank`, plus every replicated filter."""
     from .workloads import take
-    n = len(packed[1]) - 1
-    gids = np.nonzero(shard_of(np.arange(n), world) == rank)[0]
+    own = shard_owner(packed, world)
+    gids = np.nonzero((own == rank) | (own == SHARD_ALL))[0]
     return take(packed, gids), gids.astype(np.uint32)
 
 
-def concat_csr(counts: Sequence[torch.Tensor], ids: Sequence[torch.Tensor]):
-    """Per-topic concatenation of G CSR results of the same n topics (shard order).
+def topic_owner(tb: torch.Tensor, to: torch.Tensor, world: int, levels: int = SHARD_LEVELS) -> torch.Tensor:
+    """Owner rank of each topic of a batch (int64); on the batch's device (HIP kernel for a
+    GPU batch).  Wildcard key levels (wildcard "topics") go to rank 0."""
+    from . import _lib
+    n = to.numel() - 1
+    if tb.is_cuda:
+        own = torch.empty(max(n, 1), dtype=torch.int32, device=tb.device)
+        _lib.check(_lib.lib().emqx_shard_owner_device(
+            ctypes.c_void_p(tb.data_ptr()), ctypes.c_void_p(to.data_ptr()), n, world, levels,
+            ctypes.c_void_p(own.data_ptr()),
+            ctypes.c_void_p(torch.cuda.current_stream(tb.device).cuda_stream)), "emqx_shard_owner_device")
+        return own[:n].to(torch.int64)
+    return torch.from_numpy(shard_owner((tb.numpy(), to.numpy().view(np.uint64)), world, levels,
+                                        topics=True).astype(np.int64))
 
-    counts[r]: (n,) int64, ids[r]: (sum counts[r],) int32 laid out topic by topic.
-    Returns (offsets (n+1,) int64, ids (total,) int32) on the tensors' device."""
-    dev = counts[0].device
-    n = counts[0].numel()
-    C = torch.stack([c.to(torch.int64) for c in counts])          # (G, n)
-    total_per_topic = C.sum(0)
+
+def partition(tb: torch.Tensor, to: torch.Tensor, owner: torch.Tensor, world: int):
+    """Reorders a packed batch by owner rank (stable).  Returns (perm, lens in perm order,
+    bytes in perm order, topics per rank, bytes per rank): part r is perm[sum(n_to[:r]) :
+    sum(n_to[:r+1])].  Vectorized; no host round trip."""
+    dev = tb.device
+    n = owner.numel()
+    lens = (to[1:] - to[:-1]).to(torch.int64)
+    perm = torch.argsort(owner, stable=True)
+    n_to = torch.bincount(owner, minlength=world)
+    bytes_to = torch.zeros(world, dtype=torch.int64, device=dev).index_add_(0, owner, lens)
+    lens_p = lens[perm]
+    total = int(to[-1] - to[0]) if n else 0
+    if total:
+        starts_p = (to[:-1] - to[0])[perm]
+        new_off = torch.cumsum(lens_p, 0) - lens_p
+        seg = torch.repeat_interleave(torch.arange(n, device=dev), lens_p, output_size=total)
+        src = starts_p[seg] + (torch.arange(total, device=dev) - new_off[seg])
+        bytes_p = tb[int(to[0]):int(to[0]) + total][src]
+    else:
+        bytes_p = torch.zeros(0, dtype=torch.uint8, device=dev)
+    return perm, lens_p, bytes_p, n_to, bytes_to
+
+
+def merge_csr(recv_counts: torch.Tensor, recv_ids: torch.Tensor, perm: torch.Tensor):
+    """Puts per-topic results back in batch order.  recv_counts (n,) are the counts of the
+    topics in perm order (ranks' parts one after the other), recv_ids their ids laid out topic
+    by topic; perm[k] = the batch index of received topic k.  Returns (offsets (n+1,) int64,
+    ids int32) in batch order.  One host sync (the id total, for the allocation)."""
+    dev = recv_counts.device
+    n = perm.numel()
+    counts = torch.zeros(n, dtype=torch.int64, device=dev).scatter_(0, perm, recv_counts.to(torch.int64))
     offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    offsets[1:] = torch.cumsum(total_per_topic, 0)
-    before = torch.cumsum(C, 0) - C                                  # ids of earlier shards per topic
-    out = torch.empty(int(offsets[-1].item()), dtype=torch.int32, device=dev)
-    topic = torch.arange(n, device=dev)
-    for r in range(C.shape[0]):
-        c = C[r]
-        m = int(c.sum().item())
-        if m == 0:
-            continue
-        t_of = torch.repeat_interleave(topic, c)
-        local_off = torch.cumsum(c, 0) - c
-        j = torch.arange(m, device=dev) - local_off[t_of]
-        pos = offsets[t_of] + before[r][t_of] + j
-        out[pos] = ids[r][:m].to(torch.int32)
+    offsets[1:] = torch.cumsum(counts, 0)
+    total = int(recv_ids.numel())
+    out = torch.empty(total, dtype=torch.int32, device=dev)
+    if total:
+        rc = recv_counts.to(torch.int64)
+        recv_off = torch.cumsum(rc, 0) - rc
+        k = torch.repeat_interleave(torch.arange(n, device=dev), rc, output_size=total)
+        dest = offsets[perm[k]] + (torch.arange(total, device=dev) - recv_off[k])
+        out[dest] = recv_ids.to(torch.int32)
     return offsets, out
+
+
+def _a2a(out_t: torch.Tensor, in_t: torch.Tensor, out_splits: List[int], in_splits: List[int], group):
+    dist.all_to_all_single(out_t, in_t, out_splits, in_splits, group=group)
 
 
 class ShardedMatcher:
@@ -93,6 +146,7 @@ class ShardedMatcher:
         self.mode = mode
         self.local_filters, self.global_ids = shard_filters(filters, self.rank, self.world)
         self.engine = None
+        self.last_local_topics = 0
         if match_fn is None:
             from .engine import Engine
             self.engine = Engine(self.device.index if self.device.type == "cuda" else -1)
@@ -121,35 +175,70 @@ class ShardedMatcher:
         return d_off[1:] - d_off[:-1], d_ids[:m]
 
     def match(self, topics: Optional[Tuple[torch.Tensor, torch.Tensor]], src: int = 0, dst: int = 0):
-        """Match a batch held by rank ``src`` against every shard; rank ``dst`` gets the merged
-        CSR (offsets int64 (n+1,), ids int32), other ranks get None."""
-        dev = self.device
-        # 1. broadcast the batch: sizes, offsets, bytes
-        meta = torch.zeros(2, dtype=torch.int64, device=dev)
-        if self.rank == src:
+        """Match a batch held by rank ``src`` against the sharded table; rank ``dst`` gets the
+        CSR in batch order (offsets int64 (n+1,), ids int32), other ranks get None."""
+        dev, G, me, grp = self.device, self.world, self.rank, self.group
+        i64 = dict(dtype=torch.int64, device=dev)
+        # 1. the source partitions its batch by owner rank
+        if me == src:
             tb, to = topics
-            meta[0], meta[1] = to.numel() - 1, tb.numel()
-        dist.broadcast(meta, src, group=self.group)
-        n, nbytes = int(meta[0].item()), int(meta[1].item())
-        if self.rank != src:
-            to = torch.empty(n + 1, dtype=torch.int64, device=dev)
-            tb = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
-        dist.broadcast(to, src, group=self.group)
-        dist.broadcast(tb, src, group=self.group)
-        # 2. local match against this rank's shard (global filter ids)
-        counts, ids = self.match_fn(tb, to)
-        counts = counts.to(torch.int64)
-        # 3. all-gather per-topic counts, gather the id lists (padded to the largest shard)
-        all_counts = [torch.empty_like(counts) for _ in range(self.world)]
-        dist.all_gather(all_counts, counts, group=self.group)
-        sizes = [int(c.sum().item()) for c in all_counts]
-        pad = max(max(sizes), 1)
-        send = torch.zeros(pad, dtype=torch.int32, device=dev)
-        send[: ids.numel()] = ids.to(torch.int32)
-        gathered = [torch.empty(pad, dtype=torch.int32, device=dev) for _ in range(self.world)] \
-            if self.rank == dst else None
-        dist.gather(send, gathered, dst=dst, group=self.group)
-        if self.rank != dst:
+            tb, to = tb.to(dev), to.to(dev).to(torch.int64)
+            owner = topic_owner(tb, to, G)
+            perm, lens_p, bytes_p, n_to, bytes_to = partition(tb, to, owner, G)
+            send_meta = torch.stack([n_to, bytes_to], 1).reshape(-1)
+        else:
+            send_meta = torch.zeros(2 * G, **i64)
+        # 2. sizes: every rank learns what it receives from the source
+        recv_meta = torch.empty(2 * G, **i64)
+        _a2a(recv_meta, send_meta, [2] * G, [2] * G, grp)
+        rm = recv_meta.reshape(G, 2).cpu()
+        n_in, b_in = int(rm[src, 0]), int(rm[src, 1])
+        if me == src:
+            sm = send_meta.reshape(G, 2).cpu()
+            n_out_splits, b_out_splits = sm[:, 0].tolist(), sm[:, 1].tolist()
+        else:
+            lens_p = torch.zeros(0, **i64)
+            bytes_p = torch.zeros(0, dtype=torch.uint8, device=dev)
+            n_out_splits, b_out_splits = [0] * G, [0] * G
+        in_splits_n = [n_in if r == src else 0 for r in range(G)]
+        in_splits_b = [b_in if r == src else 0 for r in range(G)]
+        # 3. the parts: topic lengths and bytes (a rank's part may be empty)
+        my_lens = torch.empty(n_in, **i64)
+        _a2a(my_lens, lens_p, in_splits_n, n_out_splits, grp)
+        my_bytes = torch.empty(max(b_in, 1), dtype=torch.uint8, device=dev)
+        _a2a(my_bytes[:b_in], bytes_p, in_splits_b, b_out_splits, grp)
+        my_offs = torch.zeros(n_in + 1, **i64)
+        if n_in:
+            my_offs[1:] = torch.cumsum(my_lens, 0)
+        # 4. the local match, against this rank's shard only
+        counts, ids = self.match_fn(my_bytes, my_offs)
+        counts = counts.to(torch.int64).to(dev)
+        ids = ids.to(torch.int32).to(dev)
+        self.last_local_topics = n_in
+        # 5. results back to the destination: counts first (with the id totals), then ids
+        tot = torch.zeros(G, **i64)
+        tot[dst] = int(ids.numel())
+        tot_in = torch.empty(G, **i64)
+        _a2a(tot_in, tot, [1] * G, [1] * G, grp)
+        n_parts = [0] * G
+        if me == dst:
+            if me == src:
+                n_parts = n_out_splits
+            else:  # the destination learns the part sizes and the order from the source
+                np_t = torch.zeros(G, **i64)
+                dist.recv(np_t, src=src, group=grp)
+                n_parts = np_t.cpu().tolist()
+                perm = torch.empty(sum(n_parts), **i64)
+                dist.recv(perm, src=src, group=grp)
+        elif me == src:
+            dist.send(torch.tensor(n_out_splits, **i64), dst=dst, group=grp)
+            dist.send(perm.contiguous(), dst=dst, group=grp)
+        ids_in_splits = tot_in.cpu().tolist() if me == dst else [0] * G
+        cnt_in = torch.empty(sum(n_parts), **i64)
+        _a2a(cnt_in, counts, n_parts, [n_in if r == dst else 0 for r in range(G)], grp)
+        ids_in = torch.empty(sum(ids_in_splits), dtype=torch.int32, device=dev)
+        _a2a(ids_in, ids, ids_in_splits, [int(ids.numel()) if r == dst else 0 for r in range(G)], grp)
+        # 6. the destination puts the results back in batch order
+        if me != dst:
             return None
-        # 4. per-topic concatenation in shard order
-        return concat_csr(all_counts, [g[:s] for g, s in zip(gathered, sizes)])
+        return merge_csr(cnt_in, ids_in, perm)

@@ -272,6 +272,18 @@ int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const 
                        uint64_t* out_offsets, uint32_t* out_subs, uint32_t* out_filters, uint64_t cap,
                        uint64_t* n_out);
 
+/* Filter-sharded tables (emqx_amd/dist.py): owner_out[i] = the rank that holds filter / topic i
+ * in a world of `world` ranks — a hash of its first `levels` levels.  Filters (topics = 0): a
+ * '+' or '#' among those levels, or fewer levels, gives EMQX_SHARD_ALL (replicated on every
+ * rank).  Every filter that can match a topic lives on the topic's owner rank, so each topic is
+ * matched on one rank only.  Topics (topics = 1): a wildcard key level sends the topic to rank
+ * 0.  CPU form (any host memory) and device form (a topic batch in HBM, on `stream`). */
+#define EMQX_SHARD_ALL 0xFFFFFFFFu
+int emqx_shard_owner(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world, uint32_t levels,
+                     int topics, uint32_t* owner_out);
+int emqx_shard_owner_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t world,
+                            uint32_t levels, uint32_t* d_owner, void* stream);
+
 /* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */
 int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filter,
                      uint64_t filter_len);

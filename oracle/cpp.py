@@ -44,6 +44,12 @@ def lib():
         L.orr_create.argtypes = [u8p, u64p, ctypes.c_uint64, vp]
         L.orr_destroy.argtypes = [vp]
         L.orr_select.argtypes = [vp, u8p, u64p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, u32p, u64p]
+        L.orf_create.restype = vp
+        L.orf_create.argtypes = [u32p, u32p, u32p, ctypes.c_uint64]
+        L.orf_destroy.argtypes = [vp]
+        L.orf_publish.restype = ctypes.c_uint64
+        L.orf_publish.argtypes = [vp, u64p, u32p, ctypes.c_uint64, u32p, ctypes.c_int, u32p, u64p]
+        L.orf_checksum.argtypes = [u64p, u32p, u32p, ctypes.c_uint64, u64p]
         L.orc_topic_match.restype = ctypes.c_int
         L.orc_topic_match.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64]
         _lib = L
@@ -133,6 +139,42 @@ class CppOracle:
         out = np.zeros(max(n, 1), dtype=np.uint64)
         lib().orc_evals(self.h, _p(buf), _p(offs), n, _p(out))
         return out[:n]
+
+
+class FanoutOracle:
+    """oracle/fanout_oracle.cpp: route/aggre/do_dispatch + the hash $share picks, per topic a
+    delivery count and an order-free checksum of its deliveries."""
+
+    def __init__(self, sub_filter, sub_id, sub_group):
+        self._a = [np.ascontiguousarray(np.asarray(x, dtype=np.uint32)) for x in (sub_filter, sub_id, sub_group)]
+        self.h = lib().orf_create(_p(self._a[0]), _p(self._a[1]), _p(self._a[2]), len(self._a[0]))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orf_destroy(self.h)
+            self.h = None
+
+    def publish(self, moff, mids, keys, threads=1):
+        moff = np.ascontiguousarray(np.asarray(moff, dtype=np.uint64))
+        mids = np.ascontiguousarray(np.asarray(mids, dtype=np.uint32))
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.uint32))
+        n = len(moff) - 1
+        counts = np.zeros(max(n, 1), np.uint32)
+        sums = np.zeros(max(n, 1), np.uint64)
+        total = lib().orf_publish(self.h, _p(moff), _p(mids) if mids.size else None, n, _p(keys), threads,
+                                  _p(counts), _p(sums))
+        return counts[:n], sums[:n], int(total)
+
+
+def delivery_checksums(off, subs, fils):
+    """fanout_oracle.cpp's per-topic checksum of a delivery CSR (e.g. the GPU's)."""
+    off = np.ascontiguousarray(np.asarray(off, dtype=np.uint64))
+    subs = np.ascontiguousarray(np.asarray(subs, dtype=np.uint32))
+    fils = np.ascontiguousarray(np.asarray(fils, dtype=np.uint32))
+    n = len(off) - 1
+    sums = np.zeros(max(n, 1), np.uint64)
+    lib().orf_checksum(_p(off), _p(subs) if subs.size else None, _p(fils) if fils.size else None, n, _p(sums))
+    return sums[:n]
 
 
 def topic_match(name: bytes, filt: bytes) -> bool:

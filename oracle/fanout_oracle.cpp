@@ -1,0 +1,126 @@
+// CPU restatement of the publish fan-out — TEST INFRASTRUCTURE ONLY (the CPU baseline of
+// bench.py --workload E and a parity checker for its GPU fan-out).  Loaded through ctypes by
+// bench.py's cpu_baseline leg and tests/; never linked into the product library.
+//
+// Restates (paths relative to /root/reference), given the match_routes/1 ids of each topic:
+//   apps/emqx/src/emqx_broker.erl:244-272,500-524  route/aggre/do_dispatch: every plain
+//       subscriber of every matched filter gets one delivery ({shard, I} buckets are a storage
+//       split only, emqx_broker_helper.erl:81-86);
+//   apps/emqx/src/emqx_shared_sub.erl:113-126,251-288  dispatch/pick: one member per $share
+//       group of a matched filter; for hash_clientid / hash_topic the member is
+//       lists:nth(1 + Key rem N, Members), Members in subscription order (ETS bag order,
+//       :287-288), Key = the caller's erlang:phash2 value (not restated).
+// Per topic it reports the delivery count and an order-free checksum of its deliveries
+// (sum of mix(sub, filter | shared bit)), so a multiset comparison with the GPU's CSR needs no
+// sort.  Build: oracle/Makefile -> oracle/_build/liboracle.so.
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <thread>
+#include <vector>
+
+namespace {
+
+constexpr uint32_t NO_GROUP = 0xFFFFFFFFu;
+constexpr uint32_t SHARED_BIT = 0x80000000u;
+
+struct Group {
+  uint32_t id;
+  std::vector<uint32_t> members;  // subscription order
+};
+
+struct Fanout {
+  std::vector<std::vector<uint32_t>> plain;  // per filter id
+  std::vector<std::vector<Group>> groups;    // per filter id, groups in first-subscription order
+};
+
+inline uint64_t mix(uint32_t sub, uint32_t fil) {
+  uint64_t x = (uint64_t(sub) << 32) | fil;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* orf_create(const uint32_t* filt, const uint32_t* sub, const uint32_t* grp, uint64_t n) {
+  auto* f = new Fanout();
+  uint32_t nf = 0;
+  for (uint64_t i = 0; i < n; ++i) nf = std::max(nf, filt[i] + 1);
+  f->plain.resize(nf);
+  f->groups.resize(nf);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (grp[i] == NO_GROUP) {
+      f->plain[filt[i]].push_back(sub[i]);
+      continue;
+    }
+    auto& gs = f->groups[filt[i]];
+    auto it = std::find_if(gs.begin(), gs.end(), [&](const Group& g) { return g.id == grp[i]; });
+    if (it == gs.end()) {
+      gs.push_back(Group{grp[i], {}});
+      it = gs.end() - 1;
+    }
+    it->members.push_back(sub[i]);
+  }
+  return f;
+}
+
+void orf_destroy(void* h) { delete static_cast<Fanout*>(h); }
+
+// Hash strategies: deliveries of each topic of a match CSR (moff[n+1], mids).  counts[t],
+// sums[t] per topic; returns the total.
+uint64_t orf_publish(void* h, const uint64_t* moff, const uint32_t* mids, uint64_t n, const uint32_t* keys,
+                     int nthreads, uint32_t* counts, uint64_t* sums) {
+  const Fanout* f = static_cast<const Fanout*>(h);
+  if (nthreads < 1) nthreads = 1;
+  std::atomic<uint64_t> total{0};
+  auto work = [&](uint64_t lo, uint64_t hi) {
+    uint64_t tot = 0;
+    for (uint64_t t = lo; t < hi; ++t) {
+      uint32_t c = 0;
+      uint64_t s = 0;
+      for (uint64_t j = moff[t]; j < moff[t + 1]; ++j) {
+        const uint32_t fid = mids[j];
+        if (fid >= f->plain.size()) continue;
+        for (uint32_t sb : f->plain[fid]) {
+          ++c;
+          s += mix(sb, fid);
+        }
+        for (const Group& g : f->groups[fid]) {
+          if (g.members.empty()) continue;
+          ++c;
+          s += mix(g.members[keys[t] % g.members.size()], fid | SHARED_BIT);
+        }
+      }
+      counts[t] = c;
+      sums[t] = s;
+      tot += c;
+    }
+    total += tot;
+  };
+  std::vector<std::thread> th;
+  const uint64_t chunk = (n + nthreads - 1) / nthreads;
+  for (int k = 0; k < nthreads; ++k) {
+    const uint64_t lo = k * chunk, hi = std::min<uint64_t>(n, lo + chunk);
+    if (lo >= hi) break;
+    th.emplace_back(work, lo, hi);
+  }
+  for (auto& x : th) x.join();
+  return total.load();
+}
+
+// The same checksum of a GPU delivery CSR (off[n+1], subs, filters with the shared bit).
+void orf_checksum(const uint64_t* off, const uint32_t* subs, const uint32_t* fils, uint64_t n, uint64_t* sums) {
+  for (uint64_t t = 0; t < n; ++t) {
+    uint64_t s = 0;
+    for (uint64_t j = off[t]; j < off[t + 1]; ++j) s += mix(subs[j], fils[j]);
+    sums[t] = s;
+  }
+}
+
+}  // extern "C"

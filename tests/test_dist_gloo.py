@@ -1,9 +1,10 @@
-"""Multi-process (world_size 2, gloo, CPU) checks of the multi-GPU layouts in emqx_amd/dist.py.
+"""Multi-process (gloo, CPU, world sizes 2 and 4) checks of the multi-GPU layouts in
+emqx_amd/dist.py.
 
 The per-shard match is injected from the oracle (test infrastructure) so that the
-distribution logic — filter sharding, topic broadcast, count all-gather, id gather and the
-per-topic CSR concatenation — is checked against a single-table oracle run.  The HIP match
-itself is covered by the GPU tests."""
+distribution logic — first-level sharding with replicated root wildcards, the by-owner
+partition on the source rank, the two all-to-alls and the merge back into batch order — is
+checked against a single-table oracle run.  The HIP match itself is covered by the GPU tests."""
 
 import os
 import socket
@@ -25,92 +26,131 @@ def _free_port():
 
 def _oracle_match_fn(local_filters, global_ids):
     from oracle import cpp as C
+    o = C.CppOracle(True)
+    ids = o.add_packed(*local_filters)
+    l2g = np.zeros(max(len(ids), 1), dtype=np.uint32)
+    l2g[ids] = global_ids
 
     def fn(tb, to):
-        o = C.CppOracle(True)
-        ids = o.add_packed(*local_filters)
-        l2g = np.zeros(len(ids), dtype=np.uint32)
-        l2g[ids] = global_ids
         buf = tb.numpy().astype(np.uint8)
         offs = to.numpy().astype(np.uint64)
-        counts, oids, _ = o.match_packed(buf, offs, mode=0, threads=2, stride=512)
-        flat = np.concatenate([l2g[oids[i, :counts[i]]] for i in range(len(counts))]) if len(counts) else np.zeros(0)
-        return torch.from_numpy(counts.astype(np.int64)), torch.from_numpy(flat.astype(np.int32))
+        off, oids, _ = o.match_csr(buf, offs, mode=0, threads=2)
+        return (torch.from_numpy(np.diff(off.astype(np.int64))),
+                torch.from_numpy(l2g[oids].astype(np.int32) if oids.size else np.zeros(0, np.int32)))
     return fn
 
 
-def _worker(rank, world, port, q):
+def _batches():
+    from emqx_amd import workloads as W
+    wl = W.config_b(n_filters=60_000, n_topics=3000, seed=7)
+    extra = [b"", b"/", b"+", b"#", b"+/x", b"$SYS/a", b"a/+", b""]  # wildcard / empty / '$' topics
+    from emqx_amd.engine import pack
+    tb = np.concatenate([wl.topics[0][: int(wl.topics[1][-1])], pack(extra)[0][: sum(len(x) for x in extra)]])
+    to = np.concatenate([wl.topics[1].astype(np.uint64),
+                         wl.topics[1][-1] + np.cumsum([len(x) for x in extra]).astype(np.uint64)])
+    filters = (np.concatenate([wl.filters[0][: int(wl.filters[1][-1])], np.frombuffer(b"+/x#a/+", np.uint8)]),
+               np.concatenate([wl.filters[1].astype(np.uint64),
+                               wl.filters[1][-1] + np.array([3, 4, 7], np.uint64)]))
+    return filters, (tb, to)
+
+
+def _worker(rank, world, port, q, src, dst):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from emqx_amd import dist as D
-        from emqx_amd import workloads as W
-        wl = W.config_b(n_filters=60_000, n_topics=3000, seed=7)
-        local, gids = D.shard_filters(wl.filters, rank, world)
-        sm = D.ShardedMatcher.__new__(D.ShardedMatcher)
-        sm.group, sm.rank, sm.world, sm.device, sm.mode = None, rank, world, torch.device("cpu"), 0
-        sm.local_filters, sm.global_ids, sm.engine = local, gids, None
-        sm.match_fn = _oracle_match_fn(local, gids)
-        topics = (torch.from_numpy(wl.topics[0].copy()), torch.from_numpy(wl.topics[1].view(np.int64).copy())) \
-            if rank == 0 else None
-        res = sm.match(topics, src=0, dst=0)
-        # replicated mode: slices cover the batch exactly once
-        part = D.split_topics(wl.topics, rank, world)
-        if rank == 0:
-            off, ids = res
-            q.put(("sharded", off.numpy(), ids.numpy()))
+        filters, topics = _batches()
+        local, gids = D.shard_filters(filters, rank, world)
+        sm = D.ShardedMatcher(filters, device=torch.device("cpu"), match_fn=_oracle_match_fn(local, gids))
+        t = (torch.from_numpy(topics[0].copy()), torch.from_numpy(topics[1].astype(np.int64))) if rank == src else None
+        res = sm.match(t, src=src, dst=dst)
+        # an empty batch and a batch of empty topics go through the same collectives
+        empty = (torch.zeros(0, dtype=torch.uint8), torch.zeros(1, dtype=torch.int64)) if rank == src else None
+        r0 = sm.match(empty, src=src, dst=dst)
+        blanks = (torch.zeros(0, dtype=torch.uint8), torch.zeros(4, dtype=torch.int64)) if rank == src else None
+        r1 = sm.match(blanks, src=src, dst=dst)
+        if rank == dst:
+            q.put(("sharded", res[0].numpy(), res[1].numpy()))
+            q.put(("empty", r0[0].tolist(), r0[1].numel(), r1[0].numpy(), r1[1].numpy()))
+        else:
+            assert res is None and r0 is None and r1 is None
+        part = D.split_topics(topics, rank, world)
         q.put(("split", rank, len(part[1]) - 1))
     finally:
         dist.destroy_process_group()
 
 
+def _expected():
+    from oracle import cpp as C
+    filters, topics = _batches()
+    o = C.CppOracle(True)
+    o.add_packed(*filters)
+    return o.match_csr(*topics, mode=0, threads=4)
+
+
 @pytest.mark.timeout(300)
-def test_sharded_equals_single_table():
-    world = 2
+@pytest.mark.parametrize("world,src,dst", [(2, 0, 0), (4, 0, 0), (4, 2, 1)])
+def test_sharded_equals_single_table(world, src, dst):
+    from oracle import cpp as C
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, src, dst)) for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=240) for _ in range(world + 1)]
+    got = [q.get(timeout=240) for _ in range(world + 2)]
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    from emqx_amd import workloads as W
-    from oracle import cpp as C
-    wl = W.config_b(n_filters=60_000, n_topics=3000, seed=7)
-    o = C.CppOracle(True)
-    o.add_packed(*wl.filters)
-    counts, oids, _ = o.match_packed(*wl.topics, mode=0, threads=4, stride=512)
+    off_o, ids_o, _ = _expected()
     sharded = [g for g in got if g[0] == "sharded"][0]
-    off, ids = sharded[1], sharded[2]
-    assert np.array_equal(np.diff(off), counts.astype(np.int64))
-    for i in range(len(counts)):
-        assert np.array_equal(np.sort(ids[off[i]:off[i + 1]]), oids[i, :counts[i]])
+    assert C.csr_mismatches(sharded[1], sharded[2], off_o, ids_o).size == 0
+    empty = [g for g in got if g[0] == "empty"][0]
+    assert empty[1] == [0] and empty[2] == 0
+    o = C.CppOracle(True)
+    o.add_packed(*_batches()[0])
+    off3, ids3, _ = o.match_csr(np.zeros(1, np.uint8), np.zeros(4, np.uint64), mode=0)
+    assert C.csr_mismatches(empty[3], empty[4], off3, ids3).size == 0
     splits = sorted(g[2] for g in got if g[0] == "split")
-    assert sum(splits) == wl.n_topics
+    assert sum(splits) == len(_batches()[1][1]) - 1
 
 
-def test_concat_csr_layout():
-    from emqx_amd.dist import concat_csr
-    c0 = torch.tensor([1, 0, 2])
-    c1 = torch.tensor([0, 3, 1])
-    i0 = torch.tensor([10, 20, 21], dtype=torch.int32)
-    i1 = torch.tensor([5, 6, 7, 8], dtype=torch.int32)
-    off, ids = concat_csr([c0, c1], [i0, i1])
-    assert off.tolist() == [0, 1, 4, 7]
-    assert ids.tolist() == [10, 5, 6, 7, 20, 21, 8]
-
-
-def test_shard_partition_is_disjoint_and_complete():
+def test_shard_layout_covers_every_match():
+    """Every filter that matches a topic lives on the topic's owner rank (so one rank per
+    topic suffices), each non-root-wildcard filter on exactly one rank, root wildcards on all."""
     from emqx_amd import dist as D
-    from emqx_amd import workloads as W
-    wl = W.config_a(n_topics=10)
-    seen = []
-    for r in range(4):
-        _, g = D.shard_filters(wl.filters, r, 4)
-        seen.append(g)
-    allg = np.sort(np.concatenate(seen))
-    assert np.array_equal(allg, np.arange(wl.n_filters))
+    from oracle import cpp as C
+    filters, topics = _batches()
+    o = C.CppOracle(True)
+    o.add_packed(*filters)
+    off, ids, _ = o.match_csr(*topics, mode=0, threads=4)
+    for world in (2, 3, 8):
+        own_f = D.shard_owner(filters, world)
+        own_t = D.topic_owner(torch.from_numpy(topics[0]), torch.from_numpy(topics[1].astype(np.int64)), world).numpy()
+        tid = np.repeat(np.arange(len(own_t)), np.diff(off.astype(np.int64)))
+        fo = own_f[ids]
+        assert np.all((fo == D.SHARD_ALL) | (fo == own_t[tid]))
+        held = np.zeros(len(own_f), np.int64)
+        for r in range(world):
+            held[D.shard_filters(filters, r, world)[1]] += 1
+        assert np.all(held[own_f != D.SHARD_ALL] == 1) and np.all(held[own_f == D.SHARD_ALL] == world)
+
+
+def test_partition_and_merge_roundtrip():
+    from emqx_amd import dist as D
+    from emqx_amd.engine import pack
+    topics = [b"a/b", b"", b"x", b"a/c/d", b"q", b"+/z"]
+    buf, offs = pack(topics)
+    tb, to = torch.from_numpy(buf.copy()), torch.from_numpy(offs.astype(np.int64))
+    owner = torch.tensor([1, 0, 2, 1, 0, 0])
+    perm, lens_p, bytes_p, n_to, bytes_to = D.partition(tb, to, owner, 3)
+    assert perm.tolist() == [1, 4, 5, 0, 3, 2] and n_to.tolist() == [3, 2, 1]
+    parts = bytes(bytes_p.numpy()).decode()
+    assert parts == "q+/za/ba/c/dx" and bytes_to.tolist() == [4, 8, 1]
+    # results of the received topics (perm order), merged back into batch order
+    rc = torch.tensor([0, 2, 1, 1, 3, 0])
+    ri = torch.tensor([40, 41, 50, 0, 30, 31, 32], dtype=torch.int32)
+    off, ids = D.merge_csr(rc, ri, perm)
+    assert off.tolist() == [0, 1, 1, 1, 4, 6, 7]
+    assert ids.tolist() == [0, 30, 31, 32, 40, 41, 50]
