@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--max-batch", type=int, default=4096, help="--workload L: batcher max_batch")
     ap.add_argument("--max-wait-us", type=str, default="200", help="--workload L: batcher max_wait_us (comma list)")
     ap.add_argument("--retained", type=int, default=1_000_000, help="--workload R: stored retained topics")
+    ap.add_argument("--retain-tile", type=int, default=None, help="--workload R: filters per walk tile")
+    ap.add_argument("--retain-budget", type=int, default=None, help="--workload R: walk step budget (0 = none)")
     ap.add_argument("--churn", type=int, default=10_000, help="--workload U: inserts and deletes per commit")
     ap.add_argument("--with-matches", action="store_true",
                     help="--workload U: a 1M-topic match in flight on a second stream during every commit")
@@ -919,6 +921,9 @@ def retain_bench(args, rank, world, dev):
     expiry = np.where(rng.random(len(names)) < 0.1, now - 500 + rng.integers(0, 1000, len(names)), 0).astype(np.int64)
     log(f"[rank {rank}] retained store: {len(names)} topics, {nf} filters ({time.time() - t0:.1f}s)")
     idx = RetainIndex(dev.index)
+    for key, v in (("tile", args.retain_tile), ("step_budget", args.retain_budget)):
+        if v is not None:
+            idx.set_tuning(key, v)
     tb, to = pack(names)
     idx.store_packed(tb, to, expiry)
     idx.commit()
@@ -986,8 +991,8 @@ def retain_bench(args, rank, world, dev):
         "ranges_per_filter": round(ranges / nf, 3), "call_ms_median": round(cms, 4),
         "walk_ms_median": round(float(np.median(walk_ms)), 4),
         "walk_spill_rounds": int(st["last_spill_rounds"]), "walk_spilled_items": int(st["last_spilled"]),
-        "walk_step_budget": os.environ.get("EMQX_RETAIN_STEP_BUDGET", "128 (default)"),
-        "walk_tile_filters": int(os.environ.get("EMQX_RETAIN_TILE", "8")),
+        "walk_step_budget": args.retain_budget if args.retain_budget is not None else "128 (default)",
+        "walk_tile_filters": args.retain_tile if args.retain_tile is not None else 8,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": retain_traffic(nf, len(names))[0],
                      "traffic_source": retain_traffic(nf, len(names))[1],

@@ -12,7 +12,8 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libemqxmatch.so")
+# EMQX_LIB: an alternative build of the same library (experiments: `make retain-prof`)
+LIB_PATH = os.environ.get("EMQX_LIB") or os.path.join(HERE, "_build", "libemqxmatch.so")
 
 EMQX_OK = 0
 EMQX_EINVAL = -1
@@ -47,7 +48,7 @@ RETAIN_EXPORTS = (
     "emqx_retain_create", "emqx_retain_destroy", "emqx_retain_store", "emqx_retain_delete",
     "emqx_retain_lookup", "emqx_retain_topic", "emqx_retain_expired", "emqx_retain_commit",
     "emqx_retain_match_batch", "emqx_retain_match_batch_device", "emqx_retain_stats_get",
-    "emqx_retain_match_spec_batch",
+    "emqx_retain_match_spec_batch", "emqx_retain_set_tuning",
 )
 
 NO_GROUP = 0xFFFFFFFF
@@ -172,6 +173,7 @@ def lib():
         "emqx_retain_expired": (i32, [vp, ctypes.c_int64, vp, u64, ctypes.POINTER(u64)]),
         "emqx_retain_commit": (i32, [vp]),
         "emqx_retain_match_batch": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64, ctypes.POINTER(u64)]),
+        "emqx_retain_set_tuning": (i32, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "emqx_retain_match_spec_batch": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64, ctypes.POINTER(u64)]),
         "emqx_retain_match_batch_device": (i32, [vp, vp, vp, u64, ctypes.c_int64, vp, vp, u64,
                                                  ctypes.POINTER(u64), vp]),

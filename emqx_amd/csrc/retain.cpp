@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -52,7 +53,11 @@ struct RSnapshot {
   uint32_t* rank_id = nullptr;
   int64_t* rank_exp = nullptr;
   RPostKey* pkeys = nullptr;
-  uint2* posts = nullptr;
+  uint4* posts = nullptr;
+  uint32_t* pst = nullptr;  // RSTree levels
+  uint32_t* dst = nullptr;
+  uint32_t* pfence = nullptr;
+  uint32_t* dfence = nullptr;
   uint32_t* dterm_off = nullptr;
   uint32_t* dterm = nullptr;
   uint16_t* rank_depth = nullptr;
@@ -71,6 +76,10 @@ struct RSnapshot {
     rfree(rank_exp);
     rfree(pkeys);
     rfree(posts);
+    rfree(pst);
+    rfree(dst);
+    rfree(pfence);
+    rfree(dfence);
     rfree(dterm_off);
     rfree(dterm);
     rfree(rank_depth);
@@ -101,6 +110,7 @@ struct RWork {
   uint64_t* partials = nullptr;
   uint64_t partials_cap = 0;
   uint64_t* h_pinned = nullptr;  // [8] readbacks
+  uint64_t* prof = nullptr;      // [8] RETAIN_PROF builds with EMQX_RETAIN_PROF=1
   // host-API staging (device copies of the caller's buffers)
   uint8_t* d_fb = nullptr;
   uint64_t d_fb_cap = 0;
@@ -123,6 +133,7 @@ struct RWork {
     rfree(spill[0]);
     rfree(spill[1]);
     rfree(partials);
+    rfree(prof);
     rfree(d_fb);
     rfree(d_fo);
     rfree(d_oo);
@@ -145,7 +156,8 @@ constexpr uint32_t STEP_BUDGET = 128;
 constexpr uint32_t SPILL_WAVES = 4096;
 constexpr uint32_t SPILL_PER_WAVE = 4;  // spilled pieces dealt to each wave of a spill round
 constexpr uint32_t SPILL_CAP = 1u << 22;  // items per spill buffer (a full one: waves keep walking)
-constexpr int MAX_SPILL_ROUNDS = 64;      // then one round without a budget
+constexpr uint32_t SPILL_ROUNDS = 4;      // budgeted spill rounds per call, then one without a
+                                          // budget; all enqueued up front, empty ones exit at once
 
 // Filters per wave tile.  The walk is latency-bound (a few dependent loads per step), so the
 // number of waves in flight, not lane fill, sets its rate: 64 filters per tile leaves ~6 waves
@@ -157,17 +169,6 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* e = std::getenv(name);
   if (!e || !*e) return dflt;
   return static_cast<uint32_t>(std::min<unsigned long>(std::strtoul(e, nullptr, 10), 0xFFFFFFFFul));
-}
-
-uint32_t tile_filters() {  // per call (EMQX_RETAIN_TILE, experiments and tests)
-  return std::max<uint32_t>(1, std::min<uint32_t>(64, env_u32("EMQX_RETAIN_TILE", TILE_FILTERS)));
-}
-
-uint32_t step_budget() {  // per call, so tests can force many spill rounds
-  const char* e = std::getenv("EMQX_RETAIN_STEP_BUDGET");  // 0 = no budget
-  if (!e || !*e) return STEP_BUDGET;
-  const unsigned long v = std::strtoul(e, nullptr, 10);
-  return v == 0 ? ~0u : static_cast<uint32_t>(std::min<unsigned long>(v, 0xFFFFFFFEul));
 }
 
 bool has_wild_level(const uint8_t* p, uint64_t n) {
@@ -197,9 +198,31 @@ struct emqx_retain {
   std::vector<std::unique_ptr<RWork>> all_ws;
   std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0}, last_spill_rounds{0}, last_spilled{0};
   std::atomic<double> last_match_ms{0}, last_walk_ms{0};
+  // walk tuning (emqx_retain_set_tuning; the EMQX_RETAIN_* variables give the initial values)
+  bool prof_on = false;  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
+  std::atomic<uint32_t> tile{8}, step_budget{128}, spill_per_wave{4}, spill_rounds{4}, search{RSEARCH_FENCED};
 };
 
 namespace {
+
+// The levels of an RSTree over `k0` (level 0 = k0, level k = every 16^k-th key, until a level
+// has <= 16 entries), each rst_level_words long: 64-B aligned, with one spare block behind it
+// (a scan may read the block just past a level's end); t->n/levels set.
+std::vector<uint32_t> build_stree(const std::vector<uint32_t>& k0, RSTree* t) {
+  std::vector<uint32_t> buf;
+  uint64_t n = k0.size();
+  uint32_t k = 0;
+  for (;; ++k) {
+    const uint64_t base = buf.size(), step = 1ull << (RST_SH * k);
+    buf.resize(base + rst_level_words(static_cast<uint32_t>(n)), 0xFFFFFFFFu);
+    for (uint64_t i = 0; i < n; ++i) buf[base + i] = k0[i * step];
+    if (n <= RST_FAN || k + 1 == RST_MAX) break;
+    n = (n + RST_FAN - 1) / RST_FAN;
+  }
+  t->n = static_cast<uint32_t>(k0.size());
+  t->levels = k + 1;
+  return buf;
+}
 
 // Builds the trie of the live topics: BFS node ids (contiguous children), DFS preorder ranks.
 int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
@@ -332,7 +355,7 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   // literal lookup table (parent, wid) -> child
   uint64_t ecap = 1024;
   while (ecap < 2 * nn) ecap <<= 1;
-  std::vector<REdge> edges(ecap, REdge{WID_NONE, 0, 0, 0});
+  std::vector<REdge> edges(ecap, REdge{WID_NONE, 0, 0, 0, 0, 0, 0, 0});
   const uint32_t emask = static_cast<uint32_t>(ecap - 1);
   for (uint64_t v = 0; v < nn; ++v) {
     const uint32_t nc = nodes[v].ncld & ~RNODE_TERM;
@@ -341,7 +364,7 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
       const uint32_t w = wid_of[order[c]];
       uint32_t s = redge_slot0(static_cast<uint32_t>(v), w) & emask;
       while (edges[s].parent != WID_NONE) s = (s + 1) & emask;
-      edges[s] = REdge{static_cast<uint32_t>(v), w, c, 0};
+      edges[s] = REdge{static_cast<uint32_t>(v), w, c, nodes[c].ncld, nodes[c].lo, nodes[c].hi, 0, 0};
     }
   }
   // level postings: nodes grouped by (depth, word), each group sorted by lo
@@ -353,11 +376,11 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
     if (wx != wy) return wx < wy;
     return nodes[x].lo < nodes[y].lo;
   });
-  std::vector<uint2> posts(std::max<uint64_t>(pid.size(), 1));
+  std::vector<uint4> posts(std::max<uint64_t>(pid.size(), 1), make_uint4(0, 0, 0, 0));
   std::vector<RPostKey> groups;
   for (uint64_t i = 0; i < pid.size(); ++i) {
     const uint32_t x = pid[i];
-    posts[i] = make_uint2(nodes[x].lo, x);
+    posts[i] = make_uint4(nodes[x].lo, x, nodes[x].ncld, nodes[x].hi);
     const uint32_t d = depth[x], w = wid_of[order[x]];
     if (groups.empty() || groups.back().depth != d || groups.back().wid != w)
       groups.push_back(RPostKey{d, w, static_cast<uint32_t>(i), 0});
@@ -386,11 +409,29 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   RT_TRY(ralloc(sn->pkeys, pcap));
   RT_TRY(ralloc(sn->posts, posts.size()));
   RT_TRY(hipMemcpy(sn->pkeys, pkeys.data(), pcap * sizeof(RPostKey), hipMemcpyHostToDevice));
-  RT_TRY(hipMemcpy(sn->posts, posts.data(), posts.size() * sizeof(uint2), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->posts, posts.data(), posts.size() * sizeof(uint4), hipMemcpyHostToDevice));
   RT_TRY(ralloc(sn->dterm_off, dterm_off.size()));
   RT_TRY(ralloc(sn->dterm, dterm.size()));
   RT_TRY(hipMemcpy(sn->dterm_off, dterm_off.data(), dterm_off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   RT_TRY(hipMemcpy(sn->dterm, dterm.data(), dterm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  // search trees of the postings keys and the per-depth rank lists (RSTree)
+  std::vector<uint32_t> pkey(posts.size());
+  for (uint64_t i = 0; i < posts.size(); ++i) pkey[i] = posts[i].x;
+  RSTree pst{}, dst{};
+  const std::vector<uint32_t> pst_h = build_stree(pkey, &pst), dst_h = build_stree(dterm, &dst);
+  RT_TRY(ralloc(sn->pst, pst_h.size()));
+  RT_TRY(ralloc(sn->dst, dst_h.size()));
+  RT_TRY(hipMemcpy(sn->pst, pst_h.data(), pst_h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->dst, dst_h.data(), dst_h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  pst.keys = sn->pst;
+  dst.keys = sn->dst;
+  std::vector<uint32_t> pfence((posts.size() + RFENCE - 1) / RFENCE), dfence((dterm.size() + RFENCE - 1) / RFENCE);
+  for (uint64_t b = 0; b < pfence.size(); ++b) pfence[b] = posts[b * RFENCE].x;
+  for (uint64_t b = 0; b < dfence.size(); ++b) dfence[b] = dterm[b * RFENCE];
+  RT_TRY(ralloc(sn->pfence, pfence.size()));
+  RT_TRY(ralloc(sn->dfence, dfence.size()));
+  RT_TRY(hipMemcpy(sn->pfence, pfence.data(), pfence.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->dfence, dfence.data(), dfence.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   RT_TRY(ralloc(sn->rank_depth, rank_depth.size()));
   RT_TRY(hipMemcpy(sn->rank_depth, rank_depth.data(), rank_depth.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
   RT_TRY(hipMemcpy(sn->nodes, nodes.data(), nn * sizeof(RNode), hipMemcpyHostToDevice));
@@ -415,6 +456,10 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   rv.posts = sn->posts;
   rv.dterm_off = sn->dterm_off;
   rv.dterm = sn->dterm;
+  rv.pst = pst;
+  rv.dst = dst;
+  rv.pfence = sn->pfence;
+  rv.dfence = sn->dfence;
   rv.max_depth = max_depth;
   rv.rank_depth = sn->rank_depth;
   rv.n_nodes = rank_id.empty() ? 0u : static_cast<uint32_t>(nn);
@@ -422,8 +467,10 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   sn->n_nodes = nn;
   sn->n_words = vs.n_words();
   sn->bytes = nn * sizeof(RNode) + ecap * sizeof(REdge) + vs.table.size() * sizeof(VocabSlot) + vs.arena.size() +
-              nr * (sizeof(uint32_t) + sizeof(int64_t)) + pcap * sizeof(RPostKey) + posts.size() * sizeof(uint2) +
-              (dterm_off.size() + dterm.size()) * sizeof(uint32_t) + rank_depth.size() * sizeof(uint16_t);
+              nr * (sizeof(uint32_t) + sizeof(int64_t)) + pcap * sizeof(RPostKey) + posts.size() * sizeof(uint4) +
+              (dterm_off.size() + dterm.size() + pst_h.size() + dst_h.size() + pfence.size() + dfence.size()) *
+                  sizeof(uint32_t) +
+              rank_depth.size() * sizeof(uint16_t);
   *out = std::move(sn);
   return EMQX_OK;
 }
@@ -497,15 +544,14 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     RT_TRY(ralloc(w->rcount, rc));
     w->range_cap = static_cast<uint32_t>(rc);
   }
-  a.tile_filters = tile_filters();
+  a.tile_filters = std::max<uint32_t>(1, std::min<uint32_t>(64, r->tile.load()));
+  a.search = r->search.load();
   const uint64_t ntiles = (n + a.tile_filters - 1) / a.tile_filters;
   a.waves = static_cast<uint32_t>(std::min<uint64_t>(ntiles, MAX_WAVES));
   a.wids = w->wids;
   a.ctrl = w->ctrl;
   a.fcount = w->fcount;
   a.fcursor = w->fcursor;
-  uint32_t nr = 0;
-  RT_TRY(hipEventRecord(w->ev0, s));
   if (w->spill_cap == 0) {
     RT_TRY(ralloc(w->spill[0], SPILL_CAP));
     RT_TRY(ralloc(w->spill[1], SPILL_CAP));
@@ -513,7 +559,11 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   }
   a.fnlev = w->fnlev;
   a.spill_cap = w->spill_cap;
-  a.step_budget = step_budget();
+  const uint32_t budget = r->step_budget.load();
+  a.step_budget = budget == 0 ? ~0u : budget;
+  const uint32_t per_wave = std::max<uint32_t>(1, r->spill_per_wave.load());
+  const uint32_t rounds = a.step_budget == ~0u ? 0u : r->spill_rounds.load();
+  const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
   for (int attempt = 0;; ++attempt) {
     const uint64_t stack_waves = static_cast<uint64_t>(w->stack_cap) <= (1u << 14) ? std::max(a.waves, SPILL_WAVES) : a.waves;
     if (stack_waves * w->stack_cap > w->stack_items) {
@@ -527,30 +577,40 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     a.rcount = w->rcount;
     a.range_cap = w->range_cap;
     a.spill_out = w->spill[0];
+    a.spill_word = RC_SPILL;
+    // the whole call is enqueued at once: walk, `rounds` budgeted spill rounds and one without
+    // a budget (each reads its item count on the device; an empty round exits at once), the
+    // range count, the scan, the write (skipped on the device when the ids do not fit); then
+    // one readback of the control words and the total
+    RT_TRY(hipEventRecord(w->ev0, s));
     RT_TRY(hipMemsetAsync(w->ctrl, 0, RC_WORDS * sizeof(uint32_t), s));
-    RT_TRY(launch_retain_walk(a, s));
-    // spill rounds until no wave leaves work behind
-    uint64_t rounds = 0, spilled = 0;
-    for (int round = 0, cur = 0;; ++round) {
-      RT_TRY(hipEventRecord(w->evw, s));
-      RT_TRY(hipMemcpyAsync(w->h_pinned, w->ctrl, RC_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      RT_TRY(hipStreamSynchronize(s));
-      const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
-      const uint32_t n_sp = c[RC_SPILL];
-      if (n_sp == 0 || c[RC_STACK]) break;
-      ++rounds;
-      spilled += n_sp;
-      RetainArgs b = a;
-      const uint64_t fit = w->stack_items / w->stack_cap;
-      const uint64_t per = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_SPILL_PER_WAVE", SPILL_PER_WAVE));
-      b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>({(n_sp + per - 1) / per, SPILL_WAVES, fit})));
-      b.spill_out = w->spill[cur ^ 1];
-      if (round >= MAX_SPILL_ROUNDS) b.step_budget = ~0u;
-      RT_TRY(hipMemsetAsync(w->ctrl + RC_SPILL, 0, sizeof(uint32_t), s));
-      RT_TRY(launch_retain_walk_spill(b, w->spill[cur], n_sp, s));
-      cur ^= 1;
+    if (r->prof_on) {
+      if (!w->prof) RT_TRY(ralloc(w->prof, 8));
+      RT_TRY(hipMemsetAsync(w->prof, 0, 8 * sizeof(uint64_t), s));
+      a.prof = w->prof;
     }
-    const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
+    RT_TRY(launch_retain_walk(a, s));
+    const uint64_t fit = w->stack_items / w->stack_cap;
+    for (uint32_t k = 0; k <= rounds; ++k) {
+      RetainArgs b = a;
+      b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(SPILL_WAVES, fit)));
+      const uint32_t in_word = (k & 1) ? RC_SPILL2 : RC_SPILL, out_word = (k & 1) ? RC_SPILL : RC_SPILL2;
+      b.spill_word = out_word;
+      b.spill_out = w->spill[(k + 1) & 1];
+      if (k == rounds) b.step_budget = ~0u;  // the last round finishes every stack
+      RT_TRY(hipMemsetAsync(w->ctrl + out_word, 0, sizeof(uint32_t), s));
+      RT_TRY(launch_retain_walk_spill(b, w->spill[k & 1], in_word, per_wave, s));
+    }
+    RT_TRY(hipEventRecord(w->evw, s));
+    RT_TRY(hipMemsetAsync(w->fcount, 0, n * sizeof(uint32_t), s));
+    RT_TRY(hipMemsetAsync(w->fcursor, 0, n * sizeof(uint32_t), s));
+    RT_TRY(launch_retain_count(a, s));
+    RT_TRY(launch_scan(w->fcount, n, d_oo, w->partials, s));
+    RT_TRY(launch_retain_write(a, s));
+    RT_TRY(hipEventRecord(w->ev1, s));
+    RT_TRY(hipMemcpyAsync(w->h_pinned, w->ctrl, RC_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    RT_TRY(hipMemcpyAsync(w->h_pinned + RC_WORDS / 2, d_oo + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    RT_TRY(hipStreamSynchronize(s));
     const uint32_t ranges = c[RC_RANGES], visits = c[RC_VISITS], ovf = c[RC_STACK];
     bool again = false;
     if (ovf) {
@@ -566,29 +626,24 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       w->range_cap = static_cast<uint32_t>(rc);
       again = true;
     }
+    if (!again && r->prof_on) {
+      uint64_t pr[8];
+      if (hipMemcpy(pr, w->prof, sizeof(pr), hipMemcpyDeviceToHost) == hipSuccess)
+        std::fprintf(stderr, "RETAIN_PROF take %llu node %llu probe %llu search %llu emitpush %llu steps %llu active %llu searching %llu\n",
+                     (unsigned long long)pr[0], (unsigned long long)pr[1], (unsigned long long)pr[2],
+                     (unsigned long long)pr[3], (unsigned long long)pr[4], (unsigned long long)pr[5],
+                     (unsigned long long)pr[6], (unsigned long long)pr[7]);
+    }
     if (!again) {
-      nr = ranges;
       r->last_ranges.store(ranges);
       r->last_visits.store(visits);
-      r->last_spill_rounds.store(rounds);
-      r->last_spilled.store(spilled);
+      r->last_spill_rounds.store(c[RC_ROUNDS]);
+      r->last_spilled.store(c[RC_SPILLED]);
       break;
     }
   }
-  a.ranges = w->ranges;
-  a.rcount = w->rcount;
-  a.range_cap = w->range_cap;
-  RT_TRY(hipMemsetAsync(w->fcount, 0, n * sizeof(uint32_t), s));
-  RT_TRY(hipMemsetAsync(w->fcursor, 0, n * sizeof(uint32_t), s));
-  RT_TRY(launch_retain_count(a, nr, s));
-  RT_TRY(launch_scan(w->fcount, n, d_oo, w->partials, s));
-  RT_TRY(hipMemcpyAsync(w->h_pinned, d_oo + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  RT_TRY(hipStreamSynchronize(s));
-  *total = w->h_pinned[0];
+  *total = w->h_pinned[RC_WORDS / 2];
   r->last_total.store(*total);
-  if (*total <= cap) RT_TRY(launch_retain_write(a, nr, s));
-  RT_TRY(hipEventRecord(w->ev1, s));
-  RT_TRY(hipStreamSynchronize(s));
   float ms = 0, wms = 0;
   if (hipEventElapsedTime(&ms, w->ev0, w->ev1) == hipSuccess) r->last_match_ms.store(ms);
   if (hipEventElapsedTime(&wms, w->ev0, w->evw) == hipSuccess) r->last_walk_ms.store(wms);
@@ -608,6 +663,12 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   emqx_retain* r = new (std::nothrow) emqx_retain();
   if (!r) return EMQX_ENOMEM;
   r->device = device;
+  r->tile = std::max<uint32_t>(1, std::min<uint32_t>(64, env_u32("EMQX_RETAIN_TILE", TILE_FILTERS)));
+  r->step_budget = env_u32("EMQX_RETAIN_STEP_BUDGET", STEP_BUDGET);
+  r->spill_per_wave = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_SPILL_PER_WAVE", SPILL_PER_WAVE));
+  r->spill_rounds = env_u32("EMQX_RETAIN_SPILL_ROUNDS", SPILL_ROUNDS);
+  r->search = std::min<uint32_t>(env_u32("EMQX_RETAIN_SEARCH", RSEARCH_FENCED), RSEARCH_STREE);
+  r->prof_on = env_u32("EMQX_RETAIN_PROF", 0) != 0;
   *out = r;
   return EMQX_OK;
 }
@@ -809,6 +870,29 @@ int emqx_retain_match_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* f
 int emqx_retain_match_spec_batch(emqx_retain* r, const uint8_t* fb, const uint64_t* fo, uint64_t n, int64_t now_ms,
                                  uint64_t* out_offsets, uint32_t* out_ids, uint64_t out_cap, uint64_t* n_out) {
   return match_host(r, fb, fo, n, now_ms, out_offsets, out_ids, out_cap, n_out, true);
+}
+
+int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
+  if (!r || !key || value < 0 || value > 0xFFFFFFFFll) return EMQX_EINVAL;
+  const uint32_t v = static_cast<uint32_t>(value);
+  if (std::strcmp(key, "tile") == 0) {
+    if (v < 1 || v > 64) return EMQX_EINVAL;
+    r->tile = v;
+  } else if (std::strcmp(key, "step_budget") == 0) {
+    r->step_budget = v;  // 0 = no budget (no spill rounds)
+  } else if (std::strcmp(key, "spill_per_wave") == 0) {
+    if (v < 1) return EMQX_EINVAL;
+    r->spill_per_wave = v;
+  } else if (std::strcmp(key, "spill_rounds") == 0) {
+    if (v > 256) return EMQX_EINVAL;
+    r->spill_rounds = v;
+  } else if (std::strcmp(key, "search") == 0) {
+    if (v > RSEARCH_STREE) return EMQX_EINVAL;
+    r->search = v;
+  } else {
+    return EMQX_ENOTFOUND;
+  }
+  return EMQX_OK;
 }
 
 int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* dst) {

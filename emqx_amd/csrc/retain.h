@@ -32,12 +32,19 @@ struct alignas(16) RNode {
   uint32_t hi;
 };
 
-// Literal-edge lookup: open-addressed (parent, wid) -> child, 16 B per slot, load <= 1/2.
-struct alignas(16) REdge {
+// Literal-edge lookup: open-addressed (parent, wid) -> child, 32 B per slot, load <= 1/2.
+// The slot carries the child's node fields too, so a walk step that follows a literal edge
+// reads one slot (the probe's own line, usually still in L1/L2) instead of the probe plus a
+// random nodes[child] read: the walk's misses are its cost.  The probe reads the first half.
+struct alignas(32) REdge {
   uint32_t parent;  // WID_NONE = empty slot
   uint32_t wid;
   uint32_t child;
-  uint32_t pad;
+  uint32_t ncld;    // the child's RNode.ncld (| RNODE_TERM)
+  uint32_t lo;      // the child's rank interval
+  uint32_t hi;
+  uint32_t pad0;
+  uint32_t pad1;
 };
 
 EMQX_HD uint32_t redge_slot0(uint32_t parent, uint32_t wid) {
@@ -57,6 +64,28 @@ struct alignas(16) RPostKey {
 };
 EMQX_HD uint32_t rpost_slot0(uint32_t depth, uint32_t wid) { return mix32(wid * 0x9E3779B1u + depth * 0x85EBCA77u); }
 
+// Sorted-key search tree (S-tree) of one key array: level 0 = the keys, level k = every
+// 16^k-th key, each level 64-B aligned.  A lower bound inside a slice [L, H) of level 0 (keys
+// sorted within the slice) starts at the lowest level where the slice lies in one 16-key block
+// and goes down one level per step, each step one 64-B line read as four 16-B loads issued
+// together: ~6 round trips instead of the ~20 dependent loads of a binary search.
+constexpr uint32_t RST_MAX = 9;  // levels at most
+constexpr uint32_t RST_SH = 4;
+constexpr uint32_t RST_FAN = 1u << RST_SH;
+struct RSTree {
+  const uint32_t* keys;  // all levels; level k has n_k = ceil(n / 16^k) keys and takes
+                         // rst_level_words(n_k) words (its start is computed, not stored:
+                         // a dynamically indexed offset table costs the walk registers)
+  uint32_t n;            // level-0 keys
+  uint32_t levels;
+};
+EMQX_HD uint32_t rst_level_words(uint32_t nk) { return ((nk + RST_FAN - 1) & ~(RST_FAN - 1)) + RST_FAN; }
+
+// Two-level binary searches (RSEARCH_FENCED): every RFENCE-th key of posts[] / dterm[] in a
+// small fence array, searched first; the final search stays inside one block.
+constexpr uint32_t RFENCE = 32;
+enum RSearch : uint32_t { RSEARCH_FENCED = 0, RSEARCH_STREE = 1 };
+
 struct RetainView {
   const RNode* nodes;
   const REdge* edges;
@@ -68,19 +97,28 @@ struct RetainView {
   const int64_t* rank_exp;    // [n_ranks] expiry (ms, 0 = never)
   const RPostKey* pkeys;      // (depth, wid) -> postings slice
   uint32_t pkey_mask;
-  const uint2* posts;         // {lo, node} per node but the root, grouped by (depth, wid)
+  const uint4* posts;         // {lo, node, ncld, hi} per node but the root, grouped by (depth, wid):
+                              // a postings visit reads its node's fields from the (coalesced) slice
   const uint32_t* dterm_off;  // [max_depth + 2] per depth: first entry in dterm
   const uint32_t* dterm;      // ranks of the stored topics, grouped by depth (levels), ascending
   const uint16_t* rank_depth; // [n_ranks] levels of each stored topic (capped at 65535)
+  RSTree pst;                 // over posts[].x: the postings searches
+  RSTree dst;                 // over dterm[]: the per-depth rank-list searches
+  const uint32_t* pfence;     // posts[RFENCE * b].x: two-level binary searches (RSEARCH_FENCED)
+  const uint32_t* dfence;     // dterm[RFENCE * b]
   uint32_t max_depth;
   uint32_t n_nodes;           // 0: empty table
   uint32_t has_expiring;      // some rank has a nonzero expiry
 };
 
-// Work item of the walk (uint4): x = first node (or first postings entry), y = count,
-// z = level | RITEM_POST (the item is a postings slice), w = filter lane in the tile (first
-// round) or global filter id (spilled items)
+
+// Work item of the walk (uint4): x = first node (or first postings entry, or edge slot),
+// y = count, z = level | RITEM_POST (the item is a postings slice) | RITEM_EDGE (one node,
+// named by the edge slot that reached it), w = filter lane in the tile (first round) or
+// global filter id (spilled items)
 constexpr uint32_t RITEM_POST = 1u << 31;
+constexpr uint32_t RITEM_EDGE = 1u << 30;
+constexpr uint32_t RITEM_LEVEL = RITEM_EDGE - 1;
 
 // Range emitted by the walk: filter f's matches include ranks [lo, hi), or, RRANGE_INDIRECT,
 // the ranks dterm[lo .. hi) (a filter ending in a '+' run: the stored topics of that many
@@ -101,8 +139,11 @@ enum RCtrl : uint32_t {
   RC_RANGES = 0,   // ranges emitted (may exceed range_cap: rerun)
   RC_VISITS = 1,   // node visits
   RC_STACK = 2,    // a wave's stack overflowed (rerun with a larger stack)
-  RC_SPILL = 3,    // items spilled by this round (walked by the next)
-  RC_WORDS = 4
+  RC_SPILL = 3,    // items spilled by the walk / by even spill rounds (walked by the next round)
+  RC_SPILL2 = 4,   // ... by odd spill rounds
+  RC_ROUNDS = 5,   // spill rounds that had work
+  RC_SPILLED = 6,  // items those rounds took in
+  RC_WORDS = 8
 };
 
 struct RetainArgs {
@@ -117,9 +158,12 @@ struct RetainArgs {
   uint32_t stack_cap;
   uint32_t waves;
   uint32_t tile_filters;   // filters per wave tile of the first round (1..64)
+  uint32_t search;         // RSearch
+  uint64_t* prof;          // RETAIN_PROF builds: per-phase walk cycles (null otherwise)
   uint32_t step_budget;    // wave steps before the rest of a stack spills (~0u: no budget)
   uint4* spill_out;        // [spill_cap] items left when the budget ran out
   uint32_t spill_cap;
+  uint32_t spill_word;     // ctrl word counting the items this launch spills (RC_SPILL / RC_SPILL2)
   uint32_t* fnlev;         // [n] levels | wildcard flag << 31 of each filter (spill rounds)
   RRange* ranges;          // [range_cap]
   uint32_t range_cap;
@@ -134,11 +178,14 @@ struct RetainArgs {
 
 // tokenize + intern every filter, then walk the trie: ranges[], ctrl
 hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s);
-// one rebalanced round over the n_in items a previous round spilled (a.waves waves)
-hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t n_in, hipStream_t s);
-// live ranks per range -> rcount, fcount (nr = ranges emitted)
-hipError_t launch_retain_count(const RetainArgs& a, uint32_t nr, hipStream_t s);
-// ids of the live ranks -> out_ids at out_off[f] + cursor
-hipError_t launch_retain_write(const RetainArgs& a, uint32_t nr, hipStream_t s);
+// one rebalanced round over the items a previous round spilled: their count is read on the
+// device (ctrl[in_word]), dealt `per_wave` to a wave over at most a.waves waves; an empty
+// round exits at once, so a call enqueues its rounds without waiting for the host
+hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t in_word, uint32_t per_wave,
+                                    hipStream_t s);
+// live ranks per range -> rcount, fcount (the range count is read on the device)
+hipError_t launch_retain_count(const RetainArgs& a, hipStream_t s);
+// ids of the live ranks -> out_ids at out_off[f] + cursor; nothing when out_off[n] > out_cap
+hipError_t launch_retain_write(const RetainArgs& a, hipStream_t s);
 
 }  // namespace emqx

@@ -90,7 +90,111 @@ __device__ __forceinline__ void lower_bound2_u32(const uint32_t* a, uint32_t str
   *r2 = l2;
 }
 
+// Two-level form of lower_bound2_u32 over keys a[i * stride], i in [L, H) (global indices of
+// one sorted slice), with fence[b] = a[b * RFENCE * stride]: the fences whose block starts
+// inside the slice are searched first (a small, L2-resident array), then each bound is found
+// inside one block of RFENCE entries.  Same results as lower_bound2_u32(a, stride, L, H, ...).
+__device__ __forceinline__ void fenced_lower_bound2(const uint32_t* a, uint32_t stride, const uint32_t* fence,
+                                                    uint32_t L, uint32_t H, uint32_t x1, uint32_t x2, uint32_t* r1,
+                                                    uint32_t* r2) {
+  const uint32_t B0 = (L + RFENCE - 1) / RFENCE, B1 = (H + RFENCE - 1) / RFENCE;  // blocks starting in [L, H)
+  uint32_t f1 = B0, f2 = B0;
+  if (B1 > B0) lower_bound2_u32(fence, 1, B0, B1, x1, x2, &f1, &f2);
+  // the bound lies after block f-1's first key (< x) and at or before block f's first key
+  const uint32_t l1 = f1 > B0 ? (f1 - 1) * RFENCE + 1 : L, h1 = f1 < B1 ? f1 * RFENCE : H;
+  const uint32_t l2 = f2 > B0 ? (f2 - 1) * RFENCE + 1 : L, h2 = f2 < B1 ? f2 * RFENCE : H;
+  // interleaved final searches, each within one block
+  uint32_t a1 = l1, b1 = h1, a2 = l2, b2 = h2;
+  while (a1 < b1 || a2 < b2) {
+    const uint32_t m1 = a1 < b1 ? (a1 + b1) >> 1 : L;
+    const uint32_t m2 = a2 < b2 ? (a2 + b2) >> 1 : L;
+    const uint32_t v1 = a[static_cast<uint64_t>(m1) * stride], v2 = a[static_cast<uint64_t>(m2) * stride];
+    if (a1 < b1) {
+      if (v1 < x1) a1 = m1 + 1; else b1 = m1;
+    }
+    if (a2 < b2) {
+      if (v2 < x2) a2 = m2 + 1; else b2 = m2;
+    }
+  }
+  *r1 = a1;
+  *r2 = a2;
+}
+
+// ceil(x / 2^sh)
+__device__ __forceinline__ uint32_t ceil_shr(uint32_t x, uint32_t sh) {
+  return static_cast<uint32_t>((static_cast<uint64_t>(x) + (1ull << sh) - 1) >> sh);
+}
+
+// max(16 * blk, L) + #{j in block blk (16 keys, one 64-B line) and in [L, H) : a[j] < x}
+__device__ __forceinline__ uint32_t scan_block(const uint32_t* a, uint32_t blk, uint32_t L, uint32_t H, uint32_t x) {
+  const uint32_t b = blk * RST_FAN;
+  const uint4* p = reinterpret_cast<const uint4*>(a + b);
+  uint32_t lt = 0;  // bit i: key b + i < x
+#pragma unroll
+  for (uint32_t i = 0; i < RST_FAN / 4; ++i) {
+    const uint4 v = p[i];
+    lt |= ((v.x < x ? 1u : 0u) | (v.y < x ? 2u : 0u) | (v.z < x ? 4u : 0u) | (v.w < x ? 8u : 0u)) << (4 * i);
+  }
+  // keys of the block inside [L, H): one contiguous run of bits
+  const uint32_t lo = L > b ? L - b : 0u, hi = H > b ? min(H - b, RST_FAN) : 0u;
+  const uint32_t in = hi > lo ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+  const uint32_t c = __popc(lt & in);
+  return (b > L ? b : L) + c;
+}
+
+// Both lower bounds of x1 <= x2 in the slice [L, H) of t's level 0 (RSTree): from the lowest
+// level at which the slice lies in one 16-key block, one block scan per level.  The bound P at
+// level k+1 brackets level k's: key (P-1)*16 (if inside the slice) is < x, key P*16 (if inside)
+// >= x, so level k's bound lies in block P-1 (or, P at the slice's start, the slice's first).
+__device__ __forceinline__ void stree_lower_bound2(const RSTree& t, uint32_t L, uint32_t H, uint32_t x1, uint32_t x2,
+                                                   uint32_t* r1, uint32_t* r2) {
+  uint32_t k = 0, Lk = L, Hk = H, off = 0;  // off: level k's first word
+  while (k + 1 < t.levels && Hk > Lk && (Lk >> RST_SH) != ((Hk - 1) >> RST_SH)) {
+    off += rst_level_words(ceil_shr(t.n, RST_SH * k));
+    ++k;
+    Lk = ceil_shr(L, RST_SH * k);
+    Hk = ceil_shr(H, RST_SH * k);
+  }
+  uint32_t b1 = Lk >> RST_SH, b2 = b1;
+  for (;;) {
+    const uint32_t* a = t.keys + off;
+    const uint32_t p1 = scan_block(a, b1, Lk, Hk, x1), p2 = scan_block(a, b2, Lk, Hk, x2);
+    if (k == 0) {
+      *r1 = p1;
+      *r2 = p2;
+      return;
+    }
+    --k;
+    off -= rst_level_words(ceil_shr(t.n, RST_SH * k));
+    const uint32_t Ln = ceil_shr(L, RST_SH * k), Hn = ceil_shr(H, RST_SH * k);
+    b1 = p1 > Lk ? p1 - 1 : (Ln >> RST_SH);
+    b2 = p2 > Lk ? p2 - 1 : (Ln >> RST_SH);
+    Lk = Ln;
+    Hk = Hn;
+  }
+}
+
+// RETAIN_PROF builds (make retain-prof, experiments only): per-phase wave cycles of the
+// walk, summed into RetainArgs.prof[RPROF_SLOTS]: take (stack read + item split), node (its
+// fields + filter words), probe (edge / postings-key probes), search, emit+push; then steps,
+// active lanes, searching lanes.  Each mark waits for the wave's outstanding memory first.
+constexpr uint32_t RPROF_SLOTS = 8;
+#ifdef RETAIN_PROF
+#define RPROF_MARK(slot)                                   \
+  do {                                                     \
+    __builtin_amdgcn_s_waitcnt(0);                         \
+    const uint64_t _t = clock64();                         \
+    pacc[slot] += _t - tprev;                              \
+    tprev = _t;                                            \
+  } while (0)
+#define RPROF_ADD(slot, v) (pacc[slot] += (v))
+#else
+#define RPROF_MARK(slot) do {} while (0)
+#define RPROF_ADD(slot, v) do {} while (0)
+#endif
+
 constexpr int RW_WAVES = 4;
+enum : uint32_t { SK_NONE = 0, SK_DTERM = 1, SK_POSTS = 2 };
 constexpr uint32_t RCHUNK = 2048;  // ranks per range record
 
 // Reserve n slots of the spill buffer, all or nothing (a partial reservation would leave
@@ -113,15 +217,21 @@ __device__ __forceinline__ bool spill_reserve(uint32_t* ctr, uint32_t n, uint32_
 // TILE: items name a filter lane of the tile whose first filter is `fbase` (its level count
 // and word base in LDS);
 // else items name a global filter id and the lane reads both from global memory.
-template <bool TILE>
+// SEARCH: how the postings / rank-list slices are found (RetainArgs.search): RSEARCH_FENCED
+// two-level binary searches, RSEARCH_STREE the 16-ary search tree
+template <bool TILE, int SEARCH>
 __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint32_t top, uint64_t fbase,
                                            const uint32_t* nlevs, const uint64_t* wbase, uint32_t* pref,
-                                           uint4* itm, uint32_t& visits, bool& overflow) {
+                                           uint4* itm, uint32_t& visits, bool& overflow, uint64_t* pacc) {
   const uint32_t lane = lane_id();
   const RetainView& rv = a.rv;
   const uint64_t b0 = a.foffs[0];
   uint32_t steps = 0;
+#ifdef RETAIN_PROF
+  uint64_t tprev = clock64();
+#endif
   while (top > 0) {
+    RPROF_MARK(4);
     if (steps++ == a.step_budget) {
       // items wider than 64 nodes go out as 64-node pieces, so the next round can deal one
       // wide '+' slice over many waves
@@ -130,7 +240,7 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       uint32_t ptot;
       (void)wave_excl(pieces, &ptot);
       uint32_t base = 0, ok = 0;
-      if (lane == 0) ok = spill_reserve(&a.ctrl[RC_SPILL], ptot, a.spill_cap, &base) ? 1u : 0u;
+      if (lane == 0) ok = spill_reserve(&a.ctrl[a.spill_word], ptot, a.spill_cap, &base) ? 1u : 0u;
       ok = __shfl(ok, 0, 64);
       base = __shfl(base, 0, 64);
       if (ok) {
@@ -175,9 +285,11 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       stk[top - 1 - kfull] = p;
     }
     top -= kfull;
+    RPROF_MARK(0);
     // ---- this lane's node ---------------------------------------------------------------
     bool act = lane < taken;
     uint32_t v = 0, lev = 0, fl = 0;
+    RNode rn{0, 0, 0, 0};  // cbeg unused: the node's id instead
     if (act) {
       uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
       while (lo < hi) {
@@ -186,18 +298,37 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       }
       const uint32_t before = lo ? pref[lo - 1] : 0u;
       const uint4 q = itm[lo];
-      v = q.x + (lane - before);
-      if (q.z & RITEM_POST) v = rv.posts[v].y;  // a postings slice: entry -> node
-      lev = q.z & ~RITEM_POST;
+      const uint32_t x = q.x + (lane - before);
+      lev = q.z & RITEM_LEVEL;
       fl = q.w;
+      // the node's fields come with whatever reached it: a postings entry (coalesced over
+      // the slice), the edge slot the previous step probed, or (roots) the node array
+      if (q.z & RITEM_POST) {
+        const uint4 p = rv.posts[x];
+        v = p.y;
+        rn = RNode{0, p.z, p.x, p.w};
+      } else if (q.z & RITEM_EDGE) {
+        const uint4* ep = reinterpret_cast<const uint4*>(rv.edges + x);
+        const uint4 e0 = ep[0], e1 = ep[1];
+        v = e0.z;
+        rn = RNode{0, e0.w, e1.x, e1.y};
+      } else {
+        v = x;
+        rn = rv.nodes[v];
+      }
     }
     __builtin_amdgcn_wave_barrier();
+    RPROF_MARK(1);
+    RPROF_ADD(5, 1);
+    RPROF_ADD(6, __popcll(__ballot(act)));
     bool emit = false, push = false;
     RRange rg{0, 0, 0, 0};
     uint4 np = make_uint4(0, 0, 0, 0);
+    // a slice to cut to this node's rank interval: every lane that needs one searches at
+    // one call site below (SK_DTERM: the per-depth rank list, SK_POSTS: a postings group)
+    uint32_t skind = SK_NONE, sL = 0, sH = 0, plev = 0;
     if (act) {
       ++visits;
-      const RNode rn = rv.nodes[v];
       uint32_t nl;
       uint64_t wb, fg;
       if (TILE) {
@@ -238,15 +369,11 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
             push = false;
           } else if (j == fn) {
             // the filter ends with this '+' run: the stored topics of exactly fn levels in
-            // this subtree = one slice of the depth-fn rank list
+            // this subtree = one slice of the depth-fn rank list (searched below)
             if (fn <= rv.max_depth) {
-              const uint32_t d0 = rv.dterm_off[fn], d1 = rv.dterm_off[fn + 1];
-              uint32_t b = d0, e = d1;
-              if (v) lower_bound2_u32(rv.dterm, 1, d0, d1, rn.lo, rn.hi, &b, &e);
-              emit = e > b;
-              rg.lo = b;
-              rg.hi = e;
-              rg.flags |= RRANGE_INDIRECT;
+              skind = SK_DTERM;
+              sL = rv.dterm_off[fn];
+              sH = rv.dterm_off[fn + 1];
             }
           } else if (wl == WID_HASH) {
             // '+' run then the final '#': this subtree's topics of at least j levels — one
@@ -257,32 +384,27 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
             rg.flags |= j << RRANGE_MIND_SHIFT;
           } else {
             uint32_t s = rpost_slot0(j + 1, wl) & rv.pkey_mask;
-            uint32_t off = 0, len = 0;
             for (uint32_t k = 0; k <= rv.pkey_mask; ++k) {
               const RPostKey pk = rv.pkeys[s];
               if (pk.depth == WID_NONE) break;
               if (pk.depth == j + 1 && pk.wid == wl) {
-                off = pk.off;
-                len = pk.len;
+                skind = SK_POSTS;
+                sL = pk.off;
+                sH = pk.off + pk.len;
+                plev = j + 1;
                 break;
               }
               s = (s + 1) & rv.pkey_mask;
             }
-            // slice of entries with lo in [rn.lo, rn.hi): two lower bounds
-            const uint32_t* px = reinterpret_cast<const uint32_t*>(rv.posts);
-            uint32_t b = 0, e = len;
-            if (v) lower_bound2_u32(px + 2ull * off, 2, 0, len, rn.lo, rn.hi, &b, &e);
-            push = e > b;
-            np = make_uint4(off + b, e - b, (j + 1) | RITEM_POST, fl);
           }
         } else if (w != WID_NONE && ncld != 0) {
           uint32_t s = redge_slot0(v, w) & rv.edge_mask;
           for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
-            const REdge e = rv.edges[s];
-            if (e.parent == WID_NONE) break;
-            if (e.parent == v && e.wid == w) {
+            const uint4 e = *reinterpret_cast<const uint4*>(rv.edges + s);  // parent, wid, child, ncld
+            if (e.x == WID_NONE) break;
+            if (e.x == v && e.y == w) {
               push = true;
-              np = make_uint4(e.child, 1u, lev + 1, fl);
+              np = make_uint4(s, 1u, (lev + 1) | RITEM_EDGE, fl);
               break;
             }
             s = (s + 1) & rv.edge_mask;
@@ -290,6 +412,30 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
         }
       }
     }
+    RPROF_MARK(2);
+    RPROF_ADD(7, __popcll(__ballot(skind != SK_NONE)));
+    if (skind != SK_NONE) {
+      uint32_t b = sL, e = sH;
+      if (v) {  // the root's interval holds every rank: the whole slice
+        const bool dt = skind == SK_DTERM;
+        if (SEARCH == RSEARCH_STREE) {
+          stree_lower_bound2(dt ? rv.dst : rv.pst, sL, sH, rn.lo, rn.hi, &b, &e);
+        } else {
+          const uint32_t* keys = dt ? rv.dterm : reinterpret_cast<const uint32_t*>(rv.posts);
+          fenced_lower_bound2(keys, dt ? 1u : 4u, dt ? rv.dfence : rv.pfence, sL, sH, rn.lo, rn.hi, &b, &e);
+        }
+      }
+      if (skind == SK_DTERM) {
+        emit = e > b;
+        rg.lo = b;
+        rg.hi = e;
+        rg.flags |= RRANGE_INDIRECT;
+      } else {
+        push = e > b;
+        np = make_uint4(b, e - b, plev | RITEM_POST, fl);
+      }
+    }
+    RPROF_MARK(3);
     // ---- emissions (one atomic per wave step) --------------------------------------------
     // a range longer than RCHUNK ranks goes out as several records, so the output kernels
     // spread one '#' over the whole subtree across many waves
@@ -323,6 +469,7 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
 
 }  // namespace
 
+template <int SEARCH>
 __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
@@ -340,6 +487,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
   const uint64_t b0 = a.foffs[0];
   uint32_t visits = 0;
   bool overflow = false;
+  uint64_t pacc[RPROF_SLOTS] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   for (uint64_t t = gw; t < ntiles; t += a.waves) {
     const uint64_t f = t * tf + lane;
@@ -391,7 +539,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
     const uint32_t ppos = wave_excl(push0 ? 1u : 0u, &ptot);
     if (push0) stk[ppos] = make_uint4(0u, 1u, 0u, lane);
     __threadfence_block();  // the stack lives in global memory: order this wave's stores and loads
-    walk_stack<true>(a, stk, ptot, t * tf, nlevs, wbase, s_pref[wib], s_item[wib], visits, overflow);
+    walk_stack<true, SEARCH>(a, stk, ptot, t * tf, nlevs, wbase, s_pref[wib], s_item[wib], visits, overflow, pacc);
     if (overflow) break;
   }
   if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
@@ -399,33 +547,57 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
   uint32_t vtot;
   (void)wave_excl(visits, &vtot);
   if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
+#ifdef RETAIN_PROF
+  if (lane == 0 && a.prof)
+    for (uint32_t i = 0; i < RPROF_SLOTS; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(a.prof + i), pacc[i]);
+#else
+  (void)pacc;
+#endif
 }
 
-// A spill round: the items the previous round left (global filter ids) dealt evenly over
-// `a.waves` waves, each walking its share under the same step budget.
-__global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_spill_kernel(RetainArgs a, const uint4* in, uint32_t n_in) {
+// A spill round: the items the previous round left (global filter ids), their count read
+// from ctrl[in_word], dealt `per_wave` to a wave over at most gridDim waves, each walking its
+// share under the same step budget.  No items: every wave returns at once.
+template <int SEARCH>
+__global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_spill_kernel(RetainArgs a, const uint4* in,
+                                                                          uint32_t in_word, uint32_t per_wave) {
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * RW_WAVES + wib;
   __shared__ uint32_t s_pref[RW_WAVES][64];
   __shared__ uint4 s_item[RW_WAVES][64];
-  if (gw >= a.waves) return;
+  const uint32_t n_in = min(__hip_atomic_load(&a.ctrl[in_word], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                            a.spill_cap);
+  if (n_in == 0) return;
+  if (gw == 0 && lane == 0) {
+    atomicAdd(&a.ctrl[RC_ROUNDS], 1u);
+    atomicAdd(&a.ctrl[RC_SPILLED], n_in);
+  }
+  const uint32_t waves = max(1u, min(a.waves, (n_in + per_wave - 1) / per_wave));
+  if (gw >= waves) return;
   uint4* stk = a.stack + static_cast<uint64_t>(gw) * a.stack_cap;
-  const uint32_t per = (n_in + a.waves - 1) / a.waves;
+  const uint32_t per = (n_in + waves - 1) / waves;
   const uint64_t lo = static_cast<uint64_t>(gw) * per;
   const uint64_t hi = lo + per < n_in ? lo + per : static_cast<uint64_t>(n_in);
   const uint32_t top = hi > lo ? static_cast<uint32_t>(hi - lo) : 0u;
   uint32_t visits = 0;
   bool overflow = top > a.stack_cap;
+  uint64_t pacc[RPROF_SLOTS] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (!overflow) {
     for (uint32_t i = lane; i < top; i += 64) stk[i] = in[lo + i];
     __threadfence_block();
-    walk_stack<false>(a, stk, top, 0, nullptr, nullptr, s_pref[wib], s_item[wib], visits, overflow);
+    walk_stack<false, SEARCH>(a, stk, top, 0, nullptr, nullptr, s_pref[wib], s_item[wib], visits, overflow, pacc);
   }
   if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
   uint32_t vtot;
   (void)wave_excl(visits, &vtot);
   if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
+#ifdef RETAIN_PROF
+  if (lane == 0 && a.prof)
+    for (uint32_t i = 0; i < RPROF_SLOTS; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(a.prof + i), pacc[i]);
+#else
+  (void)pacc;
+#endif
 }
 
 namespace {
@@ -433,12 +605,16 @@ namespace {
 // count (mode 0) / write (mode 1): one wave per 64 ranges (grid-stride, strided rows).  Ranges of at most
 // RSHORT ranks are handled lane-parallel; longer ones by the whole wave, 64 ranks at a time.
 constexpr uint32_t RSHORT = 32;
+constexpr uint32_t RUNROLL = 4;
 template <int MODE>
-__global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t nr) {
+__global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
   const RetainView& rv = a.rv;
+  const uint32_t nr = min(a.ctrl[RC_RANGES], a.range_cap);  // ranges the walk emitted
+  if (MODE == 1 && a.out_off[a.n] > a.out_cap) return;      // too many ids: the caller grows
+                                                            // its buffer and asks again
   const bool guard = rv.has_expiring && a.now_ms >= 0;
   // lane l of row j takes range l * nrows + j: one emission's consecutive records (a root '#'
   // is hundreds of RCHUNK records) land in different waves instead of one wave's serial loop
@@ -482,17 +658,32 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t 
       const uint32_t lo = __shfl(rg.lo, b, 64), hi = __shfl(rg.hi, b, 64), fg = __shfl(rg.flags, b, 64);
       uint64_t p = __shfl(pos, b, 64);
       uint32_t cnt = 0;
-      for (uint32_t i0 = lo; i0 < hi; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint32_t rk = i < hi ? rank_at(rv, i, fg) : 0u;
-        const bool live = i < hi && rank_ok(rv, rk, guard, a.now_ms, fg);
+      // RUNROLL x 64 ranks per pass, every load of the pass issued before any is used (a
+      // long range is a latency chain otherwise: one round trip per 64 ranks)
+      for (uint32_t i0 = lo; i0 < hi; i0 += RUNROLL * 64) {
+        uint32_t rk[RUNROLL];
+        bool live[RUNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < RUNROLL; ++u) {
+          const uint32_t i = i0 + u * 64 + lane;
+          rk[u] = i < hi ? rank_at(rv, i, fg) : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < RUNROLL; ++u) live[u] = i0 + u * 64 + lane < hi && rank_ok(rv, rk[u], guard, a.now_ms, fg);
         if (MODE == 0) {
-          cnt += live ? 1u : 0u;
+#pragma unroll
+          for (uint32_t u = 0; u < RUNROLL; ++u) cnt += live[u] ? 1u : 0u;
         } else {
-          const uint64_t m = __ballot(live);
-          const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-          if (live && p + rank < a.out_cap) a.out_ids[p + rank] = rv.rank_id[rk];
-          p += __popcll(m);
+          uint32_t id[RUNROLL];
+#pragma unroll
+          for (uint32_t u = 0; u < RUNROLL; ++u) id[u] = live[u] ? rv.rank_id[rk[u]] : 0u;
+#pragma unroll
+          for (uint32_t u = 0; u < RUNROLL; ++u) {
+            const uint64_t m = __ballot(live[u]);
+            const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+            if (live[u] && p + rank < a.out_cap) a.out_ids[p + rank] = id[u];
+            p += __popcll(m);
+          }
         }
       }
       if (MODE == 0) {
@@ -513,31 +704,39 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a, uint32_t 
 hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint32_t blocks = (a.waves + RW_WAVES - 1) / RW_WAVES;
-  hipLaunchKernelGGL(retain_walk_kernel, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
+  if (a.search == RSEARCH_STREE)
+    hipLaunchKernelGGL(retain_walk_kernel<RSEARCH_STREE>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL(retain_walk_kernel<RSEARCH_FENCED>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t n_in, hipStream_t s) {
-  if (n_in == 0 || a.waves == 0) return hipSuccess;
+hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t in_word, uint32_t per_wave,
+                                    hipStream_t s) {
+  if (a.waves == 0) return hipSuccess;
   const uint32_t blocks = (a.waves + RW_WAVES - 1) / RW_WAVES;
-  hipLaunchKernelGGL(retain_walk_spill_kernel, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a, in, n_in);
+  if (a.search == RSEARCH_STREE)
+    hipLaunchKernelGGL(retain_walk_spill_kernel<RSEARCH_STREE>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a, in,
+                       in_word, std::max(1u, per_wave));
+  else
+    hipLaunchKernelGGL(retain_walk_spill_kernel<RSEARCH_FENCED>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a, in,
+                       in_word, std::max(1u, per_wave));
   return hipGetLastError();
 }
 
-static uint32_t out_blocks(uint32_t nr) {
-  const uint64_t waves = (static_cast<uint64_t>(nr) + 63) / 64;
+// grid of the output kernels: sized by the range capacity (the range count is on the device)
+static uint32_t out_blocks(uint32_t cap) {
+  const uint64_t waves = (static_cast<uint64_t>(cap) + 63) / 64;
   return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((waves + 3) / 4, 8192)));
 }
 
-hipError_t launch_retain_count(const RetainArgs& a, uint32_t nr, hipStream_t s) {
-  if (nr == 0) return hipSuccess;
-  hipLaunchKernelGGL(retain_out_kernel<0>, dim3(out_blocks(nr)), dim3(256), 0, s, a, nr);
+hipError_t launch_retain_count(const RetainArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(retain_out_kernel<0>, dim3(out_blocks(a.range_cap)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_retain_write(const RetainArgs& a, uint32_t nr, hipStream_t s) {
-  if (nr == 0) return hipSuccess;
-  hipLaunchKernelGGL(retain_out_kernel<1>, dim3(out_blocks(nr)), dim3(256), 0, s, a, nr);
+hipError_t launch_retain_write(const RetainArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(retain_out_kernel<1>, dim3(out_blocks(a.range_cap)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -103,6 +103,10 @@ class RetainIndex:
     def commit(self) -> None:
         check(_lib.lib().emqx_retain_commit(self._h), "emqx_retain_commit")
 
+    def set_tuning(self, key: str, value: int) -> None:
+        """emqx_retain_set_tuning: "tile", "step_budget", "spill_per_wave", "spill_rounds"."""
+        check(_lib.lib().emqx_retain_set_tuning(self._h, key.encode(), int(value)), "emqx_retain_set_tuning")
+
     def stats(self) -> dict:
         st = _lib.RetainStats()
         check(_lib.lib().emqx_retain_stats_get(self._h, ctypes.byref(st)), "emqx_retain_stats_get")

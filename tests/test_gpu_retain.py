@@ -183,10 +183,12 @@ def test_large_table_device_api(mod):
 
 
 @pytest.mark.parametrize("budget", [1, 2, 7])
-def test_spill_rounds_parity(mod, monkeypatch, budget):
+def test_spill_rounds_parity(mod, budget):
     """Load-balanced walk: with a tiny step budget every wave spills its stack and the items
-    are dealt over many waves for round after round (EMQX_RETAIN_STEP_BUDGET, read per call).
-    The result, the node-visit count and the range count must equal the unbudgeted walk's."""
+    are dealt over many waves for round after round (emqx_retain_set_tuning "step_budget",
+    "spill_rounds"; the rounds are enqueued without host round trips, the last one without a
+    budget).  The result, the node-visit count and the range count must equal the unbudgeted
+    walk's."""
     rng = random.Random(900 + budget)
     idx = mod.RetainIndex()
     names = sorted({rand_topic(rng) for _ in range(400)})
@@ -196,22 +198,24 @@ def test_spill_rounds_parity(mod, monkeypatch, budget):
     idx.commit()
     filters = [rand_filter(rng) for _ in range(500)] + [b"#", b"+", b"+/#", b"w/+/x", b"+/+/x", b"w/+/+/z"]
     tt = RR.TokenTrie(names, expiry)
-    monkeypatch.setenv("EMQX_RETAIN_STEP_BUDGET", "0")
+    idx.set_tuning("step_budget", 0)
     ref = idx.match(filters, 100)
     st0 = idx.stats()
     assert st0["last_spill_rounds"] == 0
-    monkeypatch.setenv("EMQX_RETAIN_STEP_BUDGET", str(budget))
-    got = idx.match(filters, 100)
-    st1 = idx.stats()
-    assert st1["last_spill_rounds"] > 0 and st1["last_spilled"] > 0
-    assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
-    for f, g, r in zip(filters, got, ref):
-        assert g == r == tt.dispatch(f, 100), f
+    idx.set_tuning("step_budget", budget)
+    for rounds in (0, 1, 6, 40):
+        idx.set_tuning("spill_rounds", rounds)
+        got = idx.match(filters, 100)
+        st1 = idx.stats()
+        assert 0 < st1["last_spill_rounds"] <= rounds + 1 and st1["last_spilled"] > 0
+        assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
+        for f, g, r in zip(filters, got, ref):
+            assert g == r == tt.dispatch(f, 100), f
 
 
 @pytest.mark.parametrize("tile", [1, 5, 64])
-def test_tile_sizes_parity(mod, monkeypatch, tile):
-    """Filters per wave tile of the first walk round (EMQX_RETAIN_TILE, read per call): any
+def test_tile_sizes_parity(mod, tile):
+    """Filters per wave tile of the first walk round (emqx_retain_set_tuning "tile"): any
     size from 1 to 64 gives the oracle's sets and the same visit and range counts."""
     rng = random.Random(950 + tile)
     idx = mod.RetainIndex()
@@ -221,10 +225,10 @@ def test_tile_sizes_parity(mod, monkeypatch, tile):
     idx.commit()
     filters = [rand_filter(rng) for _ in range(333)] + [b"#", b"+/#"]
     tt = RR.TokenTrie(names, expiry)
-    monkeypatch.setenv("EMQX_RETAIN_TILE", "64")
+    idx.set_tuning("tile", 64)
     ref = idx.match(filters, 100)
     st0 = idx.stats()
-    monkeypatch.setenv("EMQX_RETAIN_TILE", str(tile))
+    idx.set_tuning("tile", tile)
     got = idx.match(filters, 100)
     st1 = idx.stats()
     assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
