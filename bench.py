@@ -996,7 +996,7 @@ def retain_bench(args, rank, world, dev):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": retain_traffic(nf, len(names))[0],
                      "traffic_source": retain_traffic(nf, len(names))[1],
-                     "kernel": "retain_walk_kernel (+ spill rounds) + retain_out_kernel<0,1> (whole call, incl. host syncs)",
+                     "kernel": "retain_walk_kernel (+ spill rounds) + retain_out_kernel<0,1> (whole call, one host sync)",
                      "alg_bytes_per_launch": alg,
                      "alg_bytes_model": "len(F) + 32*L(F) + 32*visits + 48*ranges + 16*ids + 16 per filter"},
     }

@@ -46,8 +46,7 @@ hipError_t ralloc(T*& p, uint64_t count) {
 // Device arrays of one committed snapshot (freed after draining the device).
 struct RSnapshot {
   int device = 0;
-  RNode* nodes = nullptr;
-  REdge* edges = nullptr;
+  REdgeBucket* edges = nullptr;
   VocabSlot* vocab = nullptr;
   uint8_t* arena = nullptr;
   uint32_t* rank_id = nullptr;
@@ -68,7 +67,6 @@ struct RSnapshot {
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(device);
     (void)hipDeviceSynchronize();
-    rfree(nodes);
     rfree(edges);
     rfree(vocab);
     rfree(arena);
@@ -96,7 +94,7 @@ struct RWork {
   uint64_t wids_cap = 0;
   uint4* stack = nullptr;
   uint64_t stack_items = 0;
-  uint32_t stack_cap = 4096;  // items per wave (grows on overflow)
+  uint32_t stack_cap = 1024;  // items per wave beyond the LDS part (grows on overflow)
   RRange* ranges = nullptr;
   uint32_t* rcount = nullptr;
   uint32_t range_cap = 0;
@@ -109,7 +107,7 @@ struct RWork {
   uint32_t spill_cap = 0;
   uint64_t* partials = nullptr;
   uint64_t partials_cap = 0;
-  uint64_t* h_pinned = nullptr;  // [8] readbacks
+  uint64_t* h_pinned = nullptr;  // [16] readbacks: ctrl words, then the id total
   uint64_t* prof = nullptr;      // [8] RETAIN_PROF builds with EMQX_RETAIN_PROF=1
   // host-API staging (device copies of the caller's buffers)
   uint8_t* d_fb = nullptr;
@@ -199,8 +197,10 @@ struct emqx_retain {
   std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0}, last_spill_rounds{0}, last_spilled{0};
   std::atomic<double> last_match_ms{0}, last_walk_ms{0};
   // walk tuning (emqx_retain_set_tuning; the EMQX_RETAIN_* variables give the initial values)
-  bool prof_on = false;  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
-  std::atomic<uint32_t> tile{8}, step_budget{128}, spill_per_wave{4}, spill_rounds{4}, search{RSEARCH_FENCED};
+  bool prof_on = false;
+  uint32_t ablate = 0;  // EMQX_RETAIN_ABLATE (profiling builds only)  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
+  std::atomic<uint32_t> tile{8}, step_budget{128}, spill_per_wave{4}, spill_rounds{4}, search{RSEARCH_STREE},
+      walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES};
 };
 
 namespace {
@@ -352,21 +352,6 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
     rank_exp[i] = r->expiry[rank_id[i]];
     has_exp |= rank_exp[i] != 0;
   }
-  // literal lookup table (parent, wid) -> child
-  uint64_t ecap = 1024;
-  while (ecap < 2 * nn) ecap <<= 1;
-  std::vector<REdge> edges(ecap, REdge{WID_NONE, 0, 0, 0, 0, 0, 0, 0});
-  const uint32_t emask = static_cast<uint32_t>(ecap - 1);
-  for (uint64_t v = 0; v < nn; ++v) {
-    const uint32_t nc = nodes[v].ncld & ~RNODE_TERM;
-    for (uint32_t j = 0; j < nc; ++j) {
-      const uint32_t c = nodes[v].cbeg + j;
-      const uint32_t w = wid_of[order[c]];
-      uint32_t s = redge_slot0(static_cast<uint32_t>(v), w) & emask;
-      while (edges[s].parent != WID_NONE) s = (s + 1) & emask;
-      edges[s] = REdge{static_cast<uint32_t>(v), w, c, nodes[c].ncld, nodes[c].lo, nodes[c].hi, 0, 0};
-    }
-  }
   // level postings: nodes grouped by (depth, word), each group sorted by lo
   std::vector<uint32_t> pid(nn > 0 ? nn - 1 : 0);
   for (uint64_t k = 1; k < nn; ++k) pid[k - 1] = static_cast<uint32_t>(k);
@@ -395,13 +380,45 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
     while (pkeys[sl].depth != WID_NONE) sl = (sl + 1) & pmask;
     pkeys[sl] = g;
   }
+  // a node's name: its postings index (the root: RNAME_ROOT)
+  std::vector<uint32_t> name(nn, RNAME_ROOT);
+  for (uint64_t i = 0; i < pid.size(); ++i) name[pid[i]] = static_cast<uint32_t>(i);
+  // literal lookup table (parent name, wid) -> child name: buckets of REDGE_BUCKET edges at
+  // load <= 3/8; an edge goes to the first bucket from its hash with a free slot, flagging
+  // every full bucket it passes (REDGE_OVF)
+  uint64_t nbk = 256;
+  while (nbk * REDGE_BUCKET * 3 < 8 * nn) nbk <<= 1;
+  REdgeBucket empty{};
+  for (uint32_t i = 0; i < REDGE_BUCKET; ++i) {
+    empty.key[i] = make_uint2(WID_NONE, 0);
+    empty.child[i] = 0;
+  }
+  std::vector<REdgeBucket> edges(nbk, empty);
+  const uint32_t emask = static_cast<uint32_t>(nbk - 1);
+  for (uint64_t v = 0; v < nn; ++v) {
+    const uint32_t nc = nodes[v].ncld & ~RNODE_TERM;
+    for (uint32_t j = 0; j < nc; ++j) {
+      const uint32_t c = nodes[v].cbeg + j;
+      const uint32_t w = wid_of[order[c]];
+      uint32_t bk = redge_slot0(name[v], w) & emask;
+      uint32_t i = 0;
+      for (;;) {
+        i = 0;
+        while (i < REDGE_BUCKET && edges[bk].key[i].x != WID_NONE) ++i;
+        if (i < REDGE_BUCKET) break;
+        edges[bk].key[0].y |= REDGE_OVF;
+        bk = (bk + 1) & emask;
+      }
+      edges[bk].key[i] = make_uint2(name[v], w | (edges[bk].key[i].y & REDGE_OVF));
+      edges[bk].child[i] = name[c];
+    }
+  }
   vs.build_table();
 
   auto sn = std::make_shared<RSnapshot>();
   sn->device = r->device;
   const uint64_t nr = std::max<uint64_t>(rank_id.size(), 1);
-  RT_TRY(ralloc(sn->nodes, nn));
-  RT_TRY(ralloc(sn->edges, ecap));
+  RT_TRY(ralloc(sn->edges, nbk));
   RT_TRY(ralloc(sn->vocab, vs.table.size()));
   RT_TRY(ralloc(sn->arena, vs.arena.size() + 16));
   RT_TRY(ralloc(sn->rank_id, nr));
@@ -434,8 +451,7 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   RT_TRY(hipMemcpy(sn->dfence, dfence.data(), dfence.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   RT_TRY(ralloc(sn->rank_depth, rank_depth.size()));
   RT_TRY(hipMemcpy(sn->rank_depth, rank_depth.data(), rank_depth.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-  RT_TRY(hipMemcpy(sn->nodes, nodes.data(), nn * sizeof(RNode), hipMemcpyHostToDevice));
-  RT_TRY(hipMemcpy(sn->edges, edges.data(), ecap * sizeof(REdge), hipMemcpyHostToDevice));
+  RT_TRY(hipMemcpy(sn->edges, edges.data(), nbk * sizeof(REdgeBucket), hipMemcpyHostToDevice));
   RT_TRY(hipMemcpy(sn->vocab, vs.table.data(), vs.table.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
   if (!vs.arena.empty()) RT_TRY(hipMemcpy(sn->arena, vs.arena.data(), vs.arena.size(), hipMemcpyHostToDevice));
   if (!rank_id.empty()) {
@@ -443,7 +459,9 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
     RT_TRY(hipMemcpy(sn->rank_exp, rank_exp.data(), rank_exp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
   }
   RetainView& rv = sn->rv;
-  rv.nodes = sn->nodes;
+  rv.root_ncld = nn ? nodes[0].ncld : 0u;
+  rv.root_lo = nn ? nodes[0].lo : 0u;
+  rv.root_hi = nn ? nodes[0].hi : 0u;
   rv.edges = sn->edges;
   rv.edge_mask = emask;
   rv.vocab = sn->vocab;
@@ -466,7 +484,7 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
   rv.has_expiring = has_exp;
   sn->n_nodes = nn;
   sn->n_words = vs.n_words();
-  sn->bytes = nn * sizeof(RNode) + ecap * sizeof(REdge) + vs.table.size() * sizeof(VocabSlot) + vs.arena.size() +
+  sn->bytes = nbk * sizeof(REdgeBucket) + vs.table.size() * sizeof(VocabSlot) + vs.arena.size() +
               nr * (sizeof(uint32_t) + sizeof(int64_t)) + pcap * sizeof(RPostKey) + posts.size() * sizeof(uint4) +
               (dterm_off.size() + dterm.size() + pst_h.size() + dst_h.size() + pfence.size() + dfence.size()) *
                   sizeof(uint32_t) +
@@ -496,7 +514,7 @@ int acquire(emqx_retain* r, RWork** out) {
   RT_TRY(hipEventCreate(&w->ev1));
   RT_TRY(hipEventCreate(&w->evw));
   RT_TRY(ralloc(w->ctrl, RC_WORDS));
-  RT_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_pinned), 8 * sizeof(uint64_t), hipHostMallocDefault));
+  RT_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_pinned), 16 * sizeof(uint64_t), hipHostMallocDefault));
   std::lock_guard<std::mutex> g(r->ws_mu);
   *out = w.get();
   r->all_ws.push_back(std::move(w));
@@ -547,7 +565,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   a.tile_filters = std::max<uint32_t>(1, std::min<uint32_t>(64, r->tile.load()));
   a.search = r->search.load();
   const uint64_t ntiles = (n + a.tile_filters - 1) / a.tile_filters;
-  a.waves = static_cast<uint32_t>(std::min<uint64_t>(ntiles, MAX_WAVES));
+  const uint32_t spill_waves = std::max<uint32_t>(64, r->spill_waves.load());
+  a.waves = static_cast<uint32_t>(std::min<uint64_t>(ntiles, std::max<uint32_t>(64, r->walk_waves.load())));
   a.wids = w->wids;
   a.ctrl = w->ctrl;
   a.fcount = w->fcount;
@@ -565,7 +584,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   const uint32_t rounds = a.step_budget == ~0u ? 0u : r->spill_rounds.load();
   const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
   for (int attempt = 0;; ++attempt) {
-    const uint64_t stack_waves = static_cast<uint64_t>(w->stack_cap) <= (1u << 14) ? std::max(a.waves, SPILL_WAVES) : a.waves;
+    const uint64_t stack_waves = static_cast<uint64_t>(w->stack_cap) <= (1u << 14) ? std::max(a.waves, spill_waves) : a.waves;
     if (stack_waves * w->stack_cap > w->stack_items) {
       const uint64_t items = stack_waves * w->stack_cap;
       RT_TRY(ralloc(w->stack, items));
@@ -584,16 +603,19 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     // one readback of the control words and the total
     RT_TRY(hipEventRecord(w->ev0, s));
     RT_TRY(hipMemsetAsync(w->ctrl, 0, RC_WORDS * sizeof(uint32_t), s));
+    // reserved but unused record slots must read as empty ranges
+    RT_TRY(hipMemsetAsync(w->ranges, 0, static_cast<uint64_t>(w->range_cap) * sizeof(RRange), s));
     if (r->prof_on) {
       if (!w->prof) RT_TRY(ralloc(w->prof, 8));
       RT_TRY(hipMemsetAsync(w->prof, 0, 8 * sizeof(uint64_t), s));
       a.prof = w->prof;
+      a.ablate = r->ablate;
     }
     RT_TRY(launch_retain_walk(a, s));
     const uint64_t fit = w->stack_items / w->stack_cap;
     for (uint32_t k = 0; k <= rounds; ++k) {
       RetainArgs b = a;
-      b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(SPILL_WAVES, fit)));
+      b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(spill_waves, fit)));
       const uint32_t in_word = (k & 1) ? RC_SPILL2 : RC_SPILL, out_word = (k & 1) ? RC_SPILL : RC_SPILL2;
       b.spill_word = out_word;
       b.spill_out = w->spill[(k + 1) & 1];
@@ -611,7 +633,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     RT_TRY(hipMemcpyAsync(w->h_pinned, w->ctrl, RC_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     RT_TRY(hipMemcpyAsync(w->h_pinned + RC_WORDS / 2, d_oo + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RT_TRY(hipStreamSynchronize(s));
-    const uint32_t ranges = c[RC_RANGES], visits = c[RC_VISITS], ovf = c[RC_STACK];
+    const uint64_t ranges = static_cast<uint64_t>(c[RC_RANGES]) + c[RC_BIG];
+    const uint32_t visits = c[RC_VISITS], ovf = c[RC_STACK];
     bool again = false;
     if (ovf) {
       if (w->stack_cap >= (1u << 24) || attempt > 8) return EMQX_ETOODEEP;
@@ -619,7 +642,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       again = true;
     }
     if (ranges > w->range_cap) {
-      const uint64_t rc = static_cast<uint64_t>(ranges) + ranges / 4 + 1024;
+      const uint64_t rc = ranges + ranges / 4 + 1024;
       if (rc > 0xFFFFFFF0ull) return EMQX_ENOMEM;
       RT_TRY(ralloc(w->ranges, rc));
       RT_TRY(ralloc(w->rcount, rc));
@@ -628,14 +651,15 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     }
     if (!again && r->prof_on) {
       uint64_t pr[8];
-      if (hipMemcpy(pr, w->prof, sizeof(pr), hipMemcpyDeviceToHost) == hipSuccess)
+      if (hipMemcpy(pr, w->prof, sizeof(pr), hipMemcpyDeviceToHost) == hipSuccess) {
         std::fprintf(stderr, "RETAIN_PROF take %llu node %llu probe %llu search %llu emitpush %llu steps %llu active %llu searching %llu\n",
                      (unsigned long long)pr[0], (unsigned long long)pr[1], (unsigned long long)pr[2],
                      (unsigned long long)pr[3], (unsigned long long)pr[4], (unsigned long long)pr[5],
                      (unsigned long long)pr[6], (unsigned long long)pr[7]);
+      }
     }
     if (!again) {
-      r->last_ranges.store(ranges);
+      r->last_ranges.store(c[RC_EMITTED]);
       r->last_visits.store(visits);
       r->last_spill_rounds.store(c[RC_ROUNDS]);
       r->last_spilled.store(c[RC_SPILLED]);
@@ -667,8 +691,11 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   r->step_budget = env_u32("EMQX_RETAIN_STEP_BUDGET", STEP_BUDGET);
   r->spill_per_wave = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_SPILL_PER_WAVE", SPILL_PER_WAVE));
   r->spill_rounds = env_u32("EMQX_RETAIN_SPILL_ROUNDS", SPILL_ROUNDS);
-  r->search = std::min<uint32_t>(env_u32("EMQX_RETAIN_SEARCH", RSEARCH_FENCED), RSEARCH_STREE);
+  r->search = std::min<uint32_t>(env_u32("EMQX_RETAIN_SEARCH", RSEARCH_STREE), RSEARCH_STREE);
+  r->walk_waves = env_u32("EMQX_RETAIN_WALK_WAVES", MAX_WAVES);
+  r->spill_waves = env_u32("EMQX_RETAIN_SPILL_WAVES", SPILL_WAVES);
   r->prof_on = env_u32("EMQX_RETAIN_PROF", 0) != 0;
+  r->ablate = env_u32("EMQX_RETAIN_ABLATE", 0);
   *out = r;
   return EMQX_OK;
 }
@@ -886,6 +913,12 @@ int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
   } else if (std::strcmp(key, "spill_rounds") == 0) {
     if (v > 256) return EMQX_EINVAL;
     r->spill_rounds = v;
+  } else if (std::strcmp(key, "walk_waves") == 0) {
+    if (v < 64 || v > (1u << 20)) return EMQX_EINVAL;
+    r->walk_waves = v;
+  } else if (std::strcmp(key, "spill_waves") == 0) {
+    if (v < 64 || v > (1u << 20)) return EMQX_EINVAL;
+    r->spill_waves = v;
   } else if (std::strcmp(key, "search") == 0) {
     if (v > RSEARCH_STREE) return EMQX_EINVAL;
     r->search = v;

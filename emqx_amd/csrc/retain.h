@@ -32,21 +32,20 @@ struct alignas(16) RNode {
   uint32_t hi;
 };
 
-// Literal-edge lookup: open-addressed (parent, wid) -> child, 32 B per slot, load <= 1/2.
-// The slot carries the child's node fields too, so a walk step that follows a literal edge
-// reads one slot (the probe's own line, usually still in L1/L2) instead of the probe plus a
-// random nodes[child] read: the walk's misses are its cost.  The probe reads the first half.
-struct alignas(32) REdge {
-  uint32_t parent;  // WID_NONE = empty slot
-  uint32_t wid;
-  uint32_t child;
-  uint32_t ncld;    // the child's RNode.ncld (| RNODE_TERM)
-  uint32_t lo;      // the child's rank interval
-  uint32_t hi;
-  uint32_t pad0;
-  uint32_t pad1;
+// Literal-edge lookup: (parent name, wid) -> child name in 64-B buckets of REDGE_BUCKET
+// edges, bucket = hash & edge_mask, load <= 3/8 (a bucket overflows ~1 % of the time:
+// REDGE_OVF in its first key's word id sends the lookup on to the next bucket).  A node's
+// NAME is its postings index (RNAME_ROOT for the root), so a lookup needs no node load first,
+// and its hit is a postings index again: the child's fields are posts[child].  A lookup
+// reads the bucket's keys and child names (48 B) in one round trip, hit or miss.
+constexpr uint32_t REDGE_BUCKET = 4;
+constexpr uint32_t REDGE_OVF = 1u << 31;  // on key[0].wid (word ids < 2^31)
+constexpr uint32_t RNAME_ROOT = 0xFFFFFFF0u;
+struct alignas(64) REdgeBucket {
+  uint2 key[REDGE_BUCKET];      // {parent name, wid}; parent WID_NONE = empty
+  uint32_t child[REDGE_BUCKET]; // child names
+  uint32_t pad[4];
 };
-
 EMQX_HD uint32_t redge_slot0(uint32_t parent, uint32_t wid) {
   return mix32(parent * 0x9E3779B1u ^ mix32(wid + 0x7F4A7C15u));
 }
@@ -87,9 +86,9 @@ constexpr uint32_t RFENCE = 32;
 enum RSearch : uint32_t { RSEARCH_FENCED = 0, RSEARCH_STREE = 1 };
 
 struct RetainView {
-  const RNode* nodes;
-  const REdge* edges;
-  uint32_t edge_mask;
+  const REdgeBucket* edges;
+  uint32_t edge_mask;         // buckets - 1
+  uint32_t root_ncld, root_lo, root_hi;  // the root's RNode fields (the root has no postings entry)
   const VocabSlot* vocab;
   const uint8_t* arena;
   uint32_t vocab_mask;
@@ -98,6 +97,7 @@ struct RetainView {
   const RPostKey* pkeys;      // (depth, wid) -> postings slice
   uint32_t pkey_mask;
   const uint4* posts;         // {lo, node, ncld, hi} per node but the root, grouped by (depth, wid):
+                              // the index of a node's entry is its name (REdgeBucket);
                               // a postings visit reads its node's fields from the (coalesced) slice
   const uint32_t* dterm_off;  // [max_depth + 2] per depth: first entry in dterm
   const uint32_t* dterm;      // ranks of the stored topics, grouped by depth (levels), ascending
@@ -112,13 +112,11 @@ struct RetainView {
 };
 
 
-// Work item of the walk (uint4): x = first node (or first postings entry, or edge slot),
-// y = count, z = level | RITEM_POST (the item is a postings slice) | RITEM_EDGE (one node,
-// named by the edge slot that reached it), w = filter lane in the tile (first round) or
-// global filter id (spilled items)
+// Work item of the walk (uint4): x = first postings entry (node name), y = count, z = level |
+// RITEM_POST (else the item is the root), w = filter lane in the tile (first round) or global
+// filter id (spilled items)
 constexpr uint32_t RITEM_POST = 1u << 31;
-constexpr uint32_t RITEM_EDGE = 1u << 30;
-constexpr uint32_t RITEM_LEVEL = RITEM_EDGE - 1;
+constexpr uint32_t RITEM_LEVEL = RITEM_POST - 1;
 
 // Range emitted by the walk: filter f's matches include ranks [lo, hi), or, RRANGE_INDIRECT,
 // the ranks dterm[lo .. hi) (a filter ending in a '+' run: the stored topics of that many
@@ -136,14 +134,17 @@ struct RRange {
 
 // ctrl words of one call (zeroed per call)
 enum RCtrl : uint32_t {
-  RC_RANGES = 0,   // ranges emitted (may exceed range_cap: rerun)
+  RC_RANGES = 0,   // small range record slots reserved (with RC_BIG may exceed range_cap: rerun)
   RC_VISITS = 1,   // node visits
   RC_STACK = 2,    // a wave's stack overflowed (rerun with a larger stack)
   RC_SPILL = 3,    // items spilled by the walk / by even spill rounds (walked by the next round)
   RC_SPILL2 = 4,   // ... by odd spill rounds
   RC_ROUNDS = 5,   // spill rounds that had work
   RC_SPILLED = 6,  // items those rounds took in
-  RC_WORDS = 8
+  RC_EMITTED = 7,  // range records written (RC_RANGES counts reserved slots: waves reserve
+                   // RRES at a time, the unused ones stay zeroed = empty records)
+  RC_BIG = 8,      // big range records, stored from the top of ranges[] down
+  RC_WORDS = 16
 };
 
 struct RetainArgs {
@@ -160,6 +161,7 @@ struct RetainArgs {
   uint32_t tile_filters;   // filters per wave tile of the first round (1..64)
   uint32_t search;         // RSearch
   uint64_t* prof;          // RETAIN_PROF builds: per-phase walk cycles (null otherwise)
+  uint32_t ablate;         // RETAIN_PROF builds: output-stage ablation bits (EMQX_RETAIN_ABLATE)
   uint32_t step_budget;    // wave steps before the rest of a stack spills (~0u: no budget)
   uint4* spill_out;        // [spill_cap] items left when the budget ran out
   uint32_t spill_cap;

@@ -194,8 +194,23 @@ constexpr uint32_t RPROF_SLOTS = 8;
 #endif
 
 constexpr int RW_WAVES = 4;
+#ifndef RW_OCC
+#define RW_OCC 1  // waves per SIMD the walk kernels are compiled for (1: the compiler's choice)
+#endif
+// The walk's work stack: the top RSTK items of each wave in LDS (a step's reads and pushes stay
+// on chip); on overflow the bottom half moves to the wave's global area (a.stack) and comes
+// back when the LDS part runs empty.  192 items (3 KiB per wave) keeps 32 waves per CU.
+constexpr uint32_t RSTK = 192;
+constexpr uint32_t RSTK_HALF = 96;
+constexpr uint32_t RWORDS = 128;  // LDS word ids per wave tile (first round)
+// A wave's reservation of range records (emissions): [next, next + left) of a.ranges.
+constexpr uint32_t RRES = 32;
+struct RangeRes {
+  uint32_t next = 0, left = 0, emitted = 0;
+};
 enum : uint32_t { SK_NONE = 0, SK_DTERM = 1, SK_POSTS = 2 };
-constexpr uint32_t RCHUNK = 2048;  // ranks per range record
+constexpr uint32_t RBIG = 64;     // ranks of a small range record at most
+constexpr uint32_t RCHUNK = 256;  // ranks per big range record (one unrolled wave pass)
 
 // Reserve n slots of the spill buffer, all or nothing (a partial reservation would leave
 // unwritten items inside the counted prefix).  Called by one lane.
@@ -219,10 +234,18 @@ __device__ __forceinline__ bool spill_reserve(uint32_t* ctr, uint32_t n, uint32_
 // else items name a global filter id and the lane reads both from global memory.
 // SEARCH: how the postings / rank-list slices are found (RetainArgs.search): RSEARCH_FENCED
 // two-level binary searches, RSEARCH_STREE the 16-ary search tree
+// A filter word: from the tile's LDS copy (lwords, first round, when the tile's words fit) or
+// from the per-call word array in global memory.
+__device__ __forceinline__ uint32_t word_at(const RetainArgs& a, const uint32_t* lwords, uint64_t i) {
+  return lwords ? lwords[i] : a.wids[i];
+}
+
 template <bool TILE, int SEARCH>
-__device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint32_t top, uint64_t fbase,
-                                           const uint32_t* nlevs, const uint64_t* wbase, uint32_t* pref,
-                                           uint4* itm, uint32_t& visits, bool& overflow, uint64_t* pacc) {
+__device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint32_t top, uint4* stk, uint32_t gtop,
+                                           uint64_t fbase, const uint32_t* nlevs, const uint64_t* wbase,
+                                           const uint32_t* lwords,
+                                           uint32_t* pref, uint4* itm, uint32_t& visits, bool& overflow,
+                                           RangeRes& res, uint64_t* pacc) {
   const uint32_t lane = lane_id();
   const RetainView& rv = a.rv;
   const uint64_t b0 = a.foffs[0];
@@ -230,13 +253,14 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
 #ifdef RETAIN_PROF
   uint64_t tprev = clock64();
 #endif
-  while (top > 0) {
+  while (top + gtop > 0) {
     RPROF_MARK(4);
     if (steps++ == a.step_budget) {
-      // items wider than 64 nodes go out as 64-node pieces, so the next round can deal one
-      // wide '+' slice over many waves
+      // the rest goes out: items wider than 64 nodes as 64-node pieces, so the next round can
+      // deal one wide '+' slice over many waves (global part first, then the LDS part)
+      const uint32_t all = gtop + top;
       uint32_t pieces = 0;
-      for (uint32_t i = lane; i < top; i += 64) pieces += (stk[i].y + 63) >> 6;
+      for (uint32_t i = lane; i < all; i += 64) pieces += ((i < gtop ? stk[i].y : ls[i - gtop].y) + 63) >> 6;
       uint32_t ptot;
       (void)wave_excl(pieces, &ptot);
       uint32_t base = 0, ok = 0;
@@ -244,11 +268,11 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       ok = __shfl(ok, 0, 64);
       base = __shfl(base, 0, 64);
       if (ok) {
-        for (uint32_t i0 = 0; i0 < top; i0 += 64) {
+        for (uint32_t i0 = 0; i0 < all; i0 += 64) {
           const uint32_t i = i0 + lane;
           uint4 it = make_uint4(0, 0, 0, 0);
-          if (i < top) it = stk[i];
-          const uint32_t np = i < top ? (it.y + 63) >> 6 : 0u;
+          if (i < all) it = i < gtop ? stk[i] : ls[i - gtop];
+          const uint32_t np = i < all ? (it.y + 63) >> 6 : 0u;
           uint32_t ctot;
           const uint32_t off = wave_excl(np, &ctot);
           if (TILE) it.w += static_cast<uint32_t>(fbase);
@@ -264,10 +288,18 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       }
       // no room: this wave finishes its stack itself (the budget is checked once)
     }
+    if (top == 0) {
+      // refill the LDS stack from the global part's top
+      const uint32_t m = gtop < RSTK_HALF ? gtop : RSTK_HALF;
+      for (uint32_t i = lane; i < m; i += 64) ls[i] = stk[gtop - m + i];
+      gtop -= m;
+      top = m;
+      __builtin_amdgcn_wave_barrier();
+    }
     // ---- take the next (up to) 64 nodes from the top items ----------------------------
     const uint32_t navail = top < 64 ? top : 64;
     uint4 it = make_uint4(0, 0, 0, 0);
-    if (lane < navail) it = stk[top - 1 - lane];
+    if (lane < navail) it = ls[top - 1 - lane];
     uint32_t ctot;
     const uint32_t cex = wave_excl(lane < navail ? it.y : 0u, &ctot);
     pref[lane] = cex + (lane < navail ? it.y : 0u);  // inclusive
@@ -282,14 +314,21 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       uint4 p = itm[kfull];
       p.x += used;
       p.y -= used;
-      stk[top - 1 - kfull] = p;
+      ls[top - 1 - kfull] = p;
     }
     top -= kfull;
     RPROF_MARK(0);
     // ---- this lane's node ---------------------------------------------------------------
+    // A node is named by its postings index (RNAME_ROOT: the root), so its child lookup (the
+    // edge bucket), the postings key after a '+' run and its own fields (posts[name]) are
+    // all issued at once from the item and the filter's words: one round trip per step.
     bool act = lane < taken;
-    uint32_t v = 0, lev = 0, fl = 0;
-    RNode rn{0, 0, 0, 0};  // cbeg unused: the node's id instead
+    uint32_t name = RNAME_ROOT, lev = 0, fl = 0, nl = 0, fn = 0, w_cur = WID_NONE, j = 0, wl = WID_HASH;
+    uint64_t fg = 0;
+    RNode rn{0, 0, 0, 0};
+    uint4 ka = make_uint4(WID_NONE, 0, WID_NONE, 0), kb = ka, kc = make_uint4(0, 0, 0, 0);
+    RPostKey pk{WID_NONE, 0, 0, 0};
+    uint32_t bk = 0, ps = 0;
     if (act) {
       uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
       while (lo < hi) {
@@ -298,23 +337,41 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       }
       const uint32_t before = lo ? pref[lo - 1] : 0u;
       const uint4 q = itm[lo];
-      const uint32_t x = q.x + (lane - before);
       lev = q.z & RITEM_LEVEL;
       fl = q.w;
-      // the node's fields come with whatever reached it: a postings entry (coalesced over
-      // the slice), the edge slot the previous step probed, or (roots) the node array
-      if (q.z & RITEM_POST) {
-        const uint4 p = rv.posts[x];
-        v = p.y;
-        rn = RNode{0, p.z, p.x, p.w};
-      } else if (q.z & RITEM_EDGE) {
-        const uint4* ep = reinterpret_cast<const uint4*>(rv.edges + x);
-        const uint4 e0 = ep[0], e1 = ep[1];
-        v = e0.z;
-        rn = RNode{0, e0.w, e1.x, e1.y};
+      uint64_t wb;
+      if (TILE) {
+        nl = nlevs[fl];
+        wb = wbase[fl];
+        fg = fbase + fl;
       } else {
-        v = x;
-        rn = rv.nodes[v];
+        fg = fl;
+        nl = a.fnlev[fg];
+        wb = (a.foffs[fg] - b0) + fg;
+      }
+      fn = nl & 0x7FFFFFFFu;
+      w_cur = lev < fn ? word_at(a, lwords, wb + lev) : WID_NONE;
+      if (w_cur == WID_PLUS) {  // the '+' run and the word after it
+        j = lev + 1;
+        while (j < fn && word_at(a, lwords, wb + j) == WID_PLUS) ++j;
+        wl = j < fn ? word_at(a, lwords, wb + j) : WID_HASH;
+      }
+      if (q.z & RITEM_POST) {
+        name = q.x + (lane - before);
+        const uint4 p = rv.posts[name];
+        rn = RNode{0, p.z, p.x, p.w};
+      } else {
+        rn = RNode{0, rv.root_ncld, rv.root_lo, rv.root_hi};
+      }
+      if (w_cur < WID_HASH) {  // a literal: its bucket, whether or not the node has children
+        bk = redge_slot0(name, w_cur) & rv.edge_mask;
+        const uint4* kp = reinterpret_cast<const uint4*>(rv.edges + bk);
+        ka = kp[0];
+        kb = kp[1];
+        kc = kp[2];
+      } else if (w_cur == WID_PLUS && wl < WID_HASH && j < fn) {  // '+' run, then a literal
+        ps = rpost_slot0(j + 1, wl) & rv.pkey_mask;
+        pk = rv.pkeys[ps];
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -329,86 +386,72 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
     uint32_t skind = SK_NONE, sL = 0, sH = 0, plev = 0;
     if (act) {
       ++visits;
-      uint32_t nl;
-      uint64_t wb, fg;
-      if (TILE) {
-        nl = nlevs[fl];
-        wb = wbase[fl];
-        fg = fbase + fl;
-      } else {
-        fg = fl;
-        nl = a.fnlev[fg];
-        wb = (a.foffs[fg] - b0) + fg;
-      }
-      const uint32_t fn = nl & 0x7FFFFFFFu;
       rg.f = static_cast<uint32_t>(fg);
       // the match spec's strict guard for wildcard filters, and for every filter of a match
       // spec call (match_messages/3, page_read/4); read_message/2's `>=` otherwise
       rg.flags = (nl >> 31) | a.strict_all;
+      const uint32_t ncld = rn.ncld & ~RNODE_TERM;
       if (lev == fn) {
         if (rn.ncld & RNODE_TERM) {
           emit = true;
           rg.lo = rn.lo;
           rg.hi = rn.lo + 1;
         }
-      } else {
-        const uint32_t w = a.wids[wb + lev];
-        const uint32_t ncld = rn.ncld & ~RNODE_TERM;
-        if (w == WID_HASH) {
+      } else if (w_cur == WID_HASH) {
+        emit = rn.hi > rn.lo;
+        rg.lo = rn.lo;
+        rg.hi = rn.hi;
+      } else if (w_cur == WID_PLUS) {
+        // the '+' run from this level, then: a literal -> its postings at the depth after the
+        // run, inside this node's rank interval; the filter's end -> a slice of the per-depth
+        // rank list; the final '#' -> the subtree's ranks with a depth floor
+        if (ncld == 0 || wl == WID_NONE) {
+          push = false;
+        } else if (j == fn) {
+          if (fn <= rv.max_depth) {
+            skind = SK_DTERM;
+            sL = rv.dterm_off[fn];
+            sH = rv.dterm_off[fn + 1];
+          }
+        } else if (wl == WID_HASH) {
           emit = rn.hi > rn.lo;
           rg.lo = rn.lo;
           rg.hi = rn.hi;
-        } else if (w == WID_PLUS) {
-          // the '+' run from this level, then: a literal -> its postings at the depth after
-          // the run, inside this node's rank interval; else ('#', the filter's end) the
-          // children range
-          uint32_t j = lev + 1;
-          while (j < fn && a.wids[wb + j] == WID_PLUS) ++j;
-          const uint32_t wl = j < fn ? a.wids[wb + j] : WID_HASH;
-          if (ncld == 0 || wl == WID_NONE) {
-            push = false;
-          } else if (j == fn) {
-            // the filter ends with this '+' run: the stored topics of exactly fn levels in
-            // this subtree = one slice of the depth-fn rank list (searched below)
-            if (fn <= rv.max_depth) {
-              skind = SK_DTERM;
-              sL = rv.dterm_off[fn];
-              sH = rv.dterm_off[fn + 1];
-            }
-          } else if (wl == WID_HASH) {
-            // '+' run then the final '#': this subtree's topics of at least j levels — one
-            // rank range with a depth floor, filtered by the output kernels
-            emit = rn.hi > rn.lo;
-            rg.lo = rn.lo;
-            rg.hi = rn.hi;
-            rg.flags |= j << RRANGE_MIND_SHIFT;
-          } else {
-            uint32_t s = rpost_slot0(j + 1, wl) & rv.pkey_mask;
-            for (uint32_t k = 0; k <= rv.pkey_mask; ++k) {
-              const RPostKey pk = rv.pkeys[s];
-              if (pk.depth == WID_NONE) break;
-              if (pk.depth == j + 1 && pk.wid == wl) {
-                skind = SK_POSTS;
-                sL = pk.off;
-                sH = pk.off + pk.len;
-                plev = j + 1;
-                break;
-              }
-              s = (s + 1) & rv.pkey_mask;
-            }
-          }
-        } else if (w != WID_NONE && ncld != 0) {
-          uint32_t s = redge_slot0(v, w) & rv.edge_mask;
-          for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
-            const uint4 e = *reinterpret_cast<const uint4*>(rv.edges + s);  // parent, wid, child, ncld
-            if (e.x == WID_NONE) break;
-            if (e.x == v && e.y == w) {
-              push = true;
-              np = make_uint4(s, 1u, (lev + 1) | RITEM_EDGE, fl);
+          rg.flags |= j << RRANGE_MIND_SHIFT;
+        } else {
+          for (uint32_t k = 0; k <= rv.pkey_mask; ++k) {
+            if (pk.depth == WID_NONE) break;
+            if (pk.depth == j + 1 && pk.wid == wl) {
+              skind = SK_POSTS;
+              sL = pk.off;
+              sH = pk.off + pk.len;
+              plev = j + 1;
               break;
             }
-            s = (s + 1) & rv.edge_mask;
+            ps = (ps + 1) & rv.pkey_mask;
+            pk = rv.pkeys[ps];
           }
+        }
+      } else if (w_cur != WID_NONE && ncld != 0) {
+        // the bucket's four keys and child names came with the node; a bucket that overflowed
+        // (REDGE_OVF) continues in the next
+        for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
+          const uint32_t hit = (ka.x == name && (ka.y & ~REDGE_OVF) == w_cur) ? kc.x
+                               : (ka.z == name && ka.w == w_cur)             ? kc.y
+                               : (kb.x == name && kb.y == w_cur)             ? kc.z
+                               : (kb.z == name && kb.w == w_cur)             ? kc.w
+                                                                             : RNAME_ROOT;
+          if (hit != RNAME_ROOT) {
+            push = true;
+            np = make_uint4(hit, 1u, (lev + 1) | RITEM_POST, fl);
+            break;
+          }
+          if (!(ka.y & REDGE_OVF)) break;
+          bk = (bk + 1) & rv.edge_mask;
+          const uint4* kp = reinterpret_cast<const uint4*>(rv.edges + bk);
+          ka = kp[0];
+          kb = kp[1];
+          kc = kp[2];
         }
       }
     }
@@ -416,7 +459,7 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
     RPROF_ADD(7, __popcll(__ballot(skind != SK_NONE)));
     if (skind != SK_NONE) {
       uint32_t b = sL, e = sH;
-      if (v) {  // the root's interval holds every rank: the whole slice
+      if (name != RNAME_ROOT) {  // the root's interval holds every rank: the whole slice
         const bool dt = skind == SK_DTERM;
         if (SEARCH == RSEARCH_STREE) {
           stree_lower_bound2(dt ? rv.dst : rv.pst, sL, sH, rn.lo, rn.hi, &b, &e);
@@ -436,41 +479,75 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* stk, uint
       }
     }
     RPROF_MARK(3);
-    // ---- emissions (one atomic per wave step) --------------------------------------------
-    // a range longer than RCHUNK ranks goes out as several records, so the output kernels
-    // spread one '#' over the whole subtree across many waves
-    const uint32_t nrec = emit ? (rg.hi - rg.lo + RCHUNK - 1) / RCHUNK : 0u;
-    uint32_t etot;
-    const uint32_t epos = wave_excl(nrec, &etot);
+    // ---- emissions -----------------------------------------------------------------------
+    // a range of at most RBIG ranks is one small record (lane-parallel in the output
+    // kernels), from this wave's reservation, refilled RRES at a time (unused reserved slots
+    // stay zeroed: empty); a longer one goes out as RCHUNK-rank big records (one wave each
+    // in the output kernels), taken from the top of the buffer
+    const uint32_t len = emit ? rg.hi - rg.lo : 0u;
+    const uint32_t nsmall = emit && len <= RBIG ? 1u : 0u;
+    const uint32_t nbig = len > RBIG ? (len + RCHUNK - 1) / RCHUNK : 0u;
+    uint32_t etot, btot;
+    const uint32_t epos = wave_excl(nsmall, &etot);
+    const uint32_t bpos = wave_excl(nbig, &btot);
     if (etot) {
+      if (etot > res.left) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&a.ctrl[RC_RANGES], etot + RRES);
+        res.next = __shfl(base, 0, 64);
+        res.left = etot + RRES;
+      }
+      if (nsmall && res.next + epos < a.range_cap) a.ranges[res.next + epos] = rg;
+      res.next += etot;
+      res.left -= etot;
+      res.emitted += etot;
+    }
+    if (btot) {
       uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&a.ctrl[RC_RANGES], etot);
+      if (lane == 0) base = atomicAdd(&a.ctrl[RC_BIG], btot);
       base = __shfl(base, 0, 64);
-      for (uint32_t k = 0; k < nrec; ++k) {
-        if (base + epos + k >= a.range_cap) break;
+      for (uint32_t k = 0; k < nbig; ++k) {
+        const uint32_t at = base + bpos + k;  // from the top: ranges[range_cap - 1 - at]
+        if (at >= a.range_cap) break;
         RRange part = rg;
         part.lo = rg.lo + k * RCHUNK;
         part.hi = min(rg.hi, part.lo + RCHUNK);
-        a.ranges[base + epos + k] = part;
+        a.ranges[a.range_cap - 1 - at] = part;
       }
+      res.emitted += btot;
     }
     // ---- pushes ---------------------------------------------------------------------------
     uint32_t qtot;
     const uint32_t qpos = wave_excl(push ? 1u : 0u, &qtot);
-    if (top + qtot > a.stack_cap) {
-      overflow = true;
-      return;
+    if (top + qtot > RSTK) {
+      // the LDS stack's bottom half moves to the global part (top > RSTK - 64 >= RSTK_HALF)
+      if (gtop + RSTK_HALF > a.stack_cap) {
+        overflow = true;
+        return;
+      }
+      for (uint32_t i = lane; i < RSTK_HALF; i += 64) stk[gtop + i] = ls[i];
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i0 = 0; i0 < top - RSTK_HALF; i0 += 64) {  // shift down (reads stay ahead of writes)
+        const uint32_t i = i0 + lane;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (i < top - RSTK_HALF) x = ls[RSTK_HALF + i];
+        __builtin_amdgcn_wave_barrier();
+        if (i < top - RSTK_HALF) ls[i] = x;
+      }
+      gtop += RSTK_HALF;
+      top -= RSTK_HALF;
+      __threadfence_block();  // the global part is read back by other lanes
     }
-    if (push) stk[top + qpos] = np;
+    if (push) ls[top + qpos] = np;
     top += qtot;
-    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
 }  // namespace
 
 template <int SEARCH>
-__global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a) {
+__global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(RetainArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * RW_WAVES + wib;
@@ -478,6 +555,8 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
   __shared__ uint4 s_item[RW_WAVES][64];
   __shared__ uint32_t s_nlev[RW_WAVES][64];
   __shared__ uint64_t s_wb[RW_WAVES][64];
+  __shared__ uint4 s_stk[RW_WAVES][RSTK];
+  __shared__ uint32_t s_words[RW_WAVES][RWORDS];
   uint32_t* nlevs = s_nlev[wib];
   uint64_t* wbase = s_wb[wib];  // per filter of the tile: its first word id in a.wids
   uint4* stk = a.stack + static_cast<uint64_t>(gw) * a.stack_cap;
@@ -488,6 +567,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
   uint32_t visits = 0;
   bool overflow = false;
   uint64_t pacc[RPROF_SLOTS] = {0, 0, 0, 0, 0, 0, 0, 0};
+  RangeRes res;
 
   for (uint64_t t = gw; t < ntiles; t += a.waves) {
     const uint64_t f = t * tf + lane;
@@ -532,14 +612,24 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
       a.fnlev[f] = nlev | (wild << 31);  // for the spill rounds
     }
     nlevs[lane] = nlev | (wild << 31);
-    wbase[lane] = valid ? (a.foffs[f] - b0) + f : 0;
+    // the tile's words into LDS when they fit (the walk reads one or two per node visit)
+    uint32_t wtot;
+    const uint32_t wofs = wave_excl(valid ? nlev : 0u, &wtot);
+    const bool lds_words = wtot <= RWORDS;
+    if (lds_words && valid) {
+      const uint32_t* wsrc = a.wids + (a.foffs[f] - b0) + f;  // this lane's own stores above
+      for (uint32_t l = 0; l < nlev; ++l) s_words[wib][wofs + l] = wsrc[l];
+    }
+    wbase[lane] = !valid ? 0 : lds_words ? wofs : (a.foffs[f] - b0) + f;
     // root items
     const bool push0 = valid && rv.n_nodes != 0;
     uint32_t ptot;
     const uint32_t ppos = wave_excl(push0 ? 1u : 0u, &ptot);
-    if (push0) stk[ppos] = make_uint4(0u, 1u, 0u, lane);
-    __threadfence_block();  // the stack lives in global memory: order this wave's stores and loads
-    walk_stack<true, SEARCH>(a, stk, ptot, t * tf, nlevs, wbase, s_pref[wib], s_item[wib], visits, overflow, pacc);
+    if (push0) s_stk[wib][ppos] = make_uint4(0u, 1u, 0u, lane);
+    __builtin_amdgcn_wave_barrier();
+    walk_stack<true, SEARCH>(a, s_stk[wib], ptot, stk, 0, t * tf, nlevs, wbase,
+                             lds_words ? s_words[wib] : nullptr, s_pref[wib], s_item[wib], visits,
+                             overflow, res, pacc);
     if (overflow) break;
   }
   if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
@@ -547,6 +637,7 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
   uint32_t vtot;
   (void)wave_excl(visits, &vtot);
   if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
+  if (lane == 0 && res.emitted) atomicAdd(&a.ctrl[RC_EMITTED], res.emitted);
 #ifdef RETAIN_PROF
   if (lane == 0 && a.prof)
     for (uint32_t i = 0; i < RPROF_SLOTS; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(a.prof + i), pacc[i]);
@@ -559,13 +650,14 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_kernel(RetainArgs a
 // from ctrl[in_word], dealt `per_wave` to a wave over at most gridDim waves, each walking its
 // share under the same step budget.  No items: every wave returns at once.
 template <int SEARCH>
-__global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_spill_kernel(RetainArgs a, const uint4* in,
+__global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_spill_kernel(RetainArgs a, const uint4* in,
                                                                           uint32_t in_word, uint32_t per_wave) {
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * RW_WAVES + wib;
   __shared__ uint32_t s_pref[RW_WAVES][64];
   __shared__ uint4 s_item[RW_WAVES][64];
+  __shared__ uint4 s_stk[RW_WAVES][RSTK];
   const uint32_t n_in = min(__hip_atomic_load(&a.ctrl[in_word], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                             a.spill_cap);
   if (n_in == 0) return;
@@ -583,15 +675,19 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_spill_kernel(Retain
   uint32_t visits = 0;
   bool overflow = top > a.stack_cap;
   uint64_t pacc[RPROF_SLOTS] = {0, 0, 0, 0, 0, 0, 0, 0};
+  RangeRes res;
   if (!overflow) {
     for (uint32_t i = lane; i < top; i += 64) stk[i] = in[lo + i];
     __threadfence_block();
-    walk_stack<false, SEARCH>(a, stk, top, 0, nullptr, nullptr, s_pref[wib], s_item[wib], visits, overflow, pacc);
+    walk_stack<false, SEARCH>(a, s_stk[wib], 0, stk, top, 0, nullptr, nullptr, nullptr, s_pref[wib],
+                              s_item[wib], visits,
+                              overflow, res, pacc);
   }
   if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
   uint32_t vtot;
   (void)wave_excl(visits, &vtot);
   if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
+  if (lane == 0 && res.emitted) atomicAdd(&a.ctrl[RC_EMITTED], res.emitted);
 #ifdef RETAIN_PROF
   if (lane == 0 && a.prof)
     for (uint32_t i = 0; i < RPROF_SLOTS; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(a.prof + i), pacc[i]);
@@ -602,99 +698,147 @@ __global__ __launch_bounds__(RW_WAVES * 64) void retain_walk_spill_kernel(Retain
 
 namespace {
 
-// count (mode 0) / write (mode 1): one wave per 64 ranges (grid-stride, strided rows).  Ranges of at most
-// RSHORT ranks are handled lane-parallel; longer ones by the whole wave, 64 ranks at a time.
-constexpr uint32_t RSHORT = 32;
-constexpr uint32_t RUNROLL = 4;
+// count (mode 0) / write (mode 1), grid-stride over work units: a ROW of 8 consecutive small
+// records, one per 8-lane group, each lane of a group taking every 8th rank of the record
+// (at most RBIG / 8 = 8, all loads in flight at once); or one BIG record (its RCHUNK ranks, the
+// whole wave in one pass).  A record is one round trip (two when indirect), not one per rank.
+constexpr uint32_t RUNROLL = RCHUNK / 64;
+constexpr uint32_t RGROUP = 8;                // lanes per small record
+constexpr uint32_t RPER = RBIG / RGROUP;      // ranks per lane of a small record, at most
 template <int MODE>
 __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t grp = lane / RGROUP, sub = lane % RGROUP;
   const RetainView& rv = a.rv;
-  const uint32_t nr = min(a.ctrl[RC_RANGES], a.range_cap);  // ranges the walk emitted
+  const uint32_t ns = a.ctrl[RC_RANGES], nb = a.ctrl[RC_BIG];
+  if (static_cast<uint64_t>(ns) + nb > a.range_cap) return;  // the host reruns with more room
   if (MODE == 1 && a.out_off[a.n] > a.out_cap) return;      // too many ids: the caller grows
                                                             // its buffer and asks again
   const bool guard = rv.has_expiring && a.now_ms >= 0;
-  // lane l of row j takes range l * nrows + j: one emission's consecutive records (a root '#'
-  // is hundreds of RCHUNK records) land in different waves instead of one wave's serial loop
-  const uint64_t nrows = (static_cast<uint64_t>(nr) + 63) / 64;
-  for (uint64_t row = gw; row < nrows; row += nw) {
-    const uint64_t r = static_cast<uint64_t>(lane) * nrows + row;
-    const bool valid = r < nr;
-    RRange rg{0, 0, 0, 0};
-    if (valid) rg = a.ranges[r];
-    const uint32_t len = rg.hi - rg.lo;
-    uint32_t c = 0;
-    uint64_t pos = 0;
-    const bool check = guard || (rg.flags >> RRANGE_MIND_SHIFT) != 0;  // per-rank filtering needed
-    // ranges of at most RSHORT ranks: this lane alone (independent loads, no wave-wide pass
-    // per range); longer ones: the whole wave
-    if (MODE == 0) {
-      if (valid && !check) {
-        c = len;
-      } else if (valid && len <= RSHORT) {
-        for (uint32_t i = rg.lo; i < rg.hi; ++i) c += rank_ok(rv, rank_at(rv, i, rg.flags), guard, a.now_ms, rg.flags) ? 1u : 0u;
+  const uint64_t nrows = (static_cast<uint64_t>(ns) + 64 / RGROUP - 1) / (64 / RGROUP);
+#ifdef RETAIN_PROF
+  // ablations (timing experiments only): bit 0 no small rows, 1 no big records, 2 no atomics
+  const uint32_t abl = a.ablate;
+#else
+  const uint32_t abl = 0;
+#endif
+  for (uint64_t u = gw; u < nrows + nb; u += nw) {
+    if ((abl & 1) && u < nrows) continue;
+    if ((abl & 2) && u >= nrows) continue;
+    if (u < nrows) {
+      // ---- a row of 8 consecutive small records (at most RBIG ranks each), 8 lanes each ----
+      const uint64_t r = u * (64 / RGROUP) + grp;
+      RRange rg{0, 0, 0, 0};
+      if (r < ns) rg = a.ranges[r];  // an unused reserved slot reads as lo == hi
+      const bool check = guard || (rg.flags >> RRANGE_MIND_SHIFT) != 0;
+      uint32_t rk[RPER];
+      bool live[RPER];
+#pragma unroll
+      for (uint32_t k = 0; k < RPER; ++k) {
+        const uint32_t i = rg.lo + sub + RGROUP * k;
+        rk[k] = i < rg.hi ? rank_at(rv, i, rg.flags) : 0u;
       }
-    } else if (valid) {
-      c = a.rcount[r];
-      if (c) pos = a.out_off[rg.f] + atomicAdd(&a.fcursor[rg.f], c);
-      if (c && len <= RSHORT) {
-        uint64_t p = pos;
-        for (uint32_t i = rg.lo; i < rg.hi; ++i) {
-          const uint32_t rk = rank_at(rv, i, rg.flags);
-          if (len == 1 || rank_ok(rv, rk, guard, a.now_ms, rg.flags)) {
-            if (p < a.out_cap) a.out_ids[p] = rv.rank_id[rk];
-            ++p;
-          }
-        }
-      }
-    }
-    // wave-cooperative ranges: longer than RSHORT ranks (and, when counting, only under a guard)
-    uint64_t big = __ballot(valid && len > RSHORT && (MODE == 1 ? c != 0 : check));
-    while (big) {
-      const uint32_t b = __ffsll(static_cast<unsigned long long>(big)) - 1;
-      big &= big - 1;
-      const uint32_t lo = __shfl(rg.lo, b, 64), hi = __shfl(rg.hi, b, 64), fg = __shfl(rg.flags, b, 64);
-      uint64_t p = __shfl(pos, b, 64);
-      uint32_t cnt = 0;
-      // RUNROLL x 64 ranks per pass, every load of the pass issued before any is used (a
-      // long range is a latency chain otherwise: one round trip per 64 ranks)
-      for (uint32_t i0 = lo; i0 < hi; i0 += RUNROLL * 64) {
-        uint32_t rk[RUNROLL];
-        bool live[RUNROLL];
 #pragma unroll
-        for (uint32_t u = 0; u < RUNROLL; ++u) {
-          const uint32_t i = i0 + u * 64 + lane;
-          rk[u] = i < hi ? rank_at(rv, i, fg) : 0u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < RUNROLL; ++u) live[u] = i0 + u * 64 + lane < hi && rank_ok(rv, rk[u], guard, a.now_ms, fg);
-        if (MODE == 0) {
-#pragma unroll
-          for (uint32_t u = 0; u < RUNROLL; ++u) cnt += live[u] ? 1u : 0u;
-        } else {
-          uint32_t id[RUNROLL];
-#pragma unroll
-          for (uint32_t u = 0; u < RUNROLL; ++u) id[u] = live[u] ? rv.rank_id[rk[u]] : 0u;
-#pragma unroll
-          for (uint32_t u = 0; u < RUNROLL; ++u) {
-            const uint64_t m = __ballot(live[u]);
-            const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
-            if (live[u] && p + rank < a.out_cap) a.out_ids[p + rank] = id[u];
-            p += __popcll(m);
-          }
-        }
-      }
+      for (uint32_t k = 0; k < RPER; ++k)
+        live[k] = rg.lo + sub + RGROUP * k < rg.hi && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
+      uint32_t c = 0;
       if (MODE == 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < RPER; ++k) c += live[k] ? 1u : 0u;
+        c += __shfl_xor(c, 1, 64);
+        c += __shfl_xor(c, 2, 64);
+        c += __shfl_xor(c, 4, 64);
+        if (sub == 0 && r < ns && rg.hi > rg.lo) a.rcount[r] = c;
+      } else {
+        c = (r < ns && rg.hi > rg.lo) ? a.rcount[r] : 0u;
+      }
+      // Runs of consecutive records of one filter (a wave's step emits a filter's records
+      // side by side) take one per-filter atomic per run, from the run's last group: a broad
+      // filter's thousands of records would otherwise queue on one address.
+      const uint32_t f = (r < ns && rg.hi > rg.lo) ? rg.f : 0xFFFFFFFFu;
+      const uint32_t fprev = __shfl(f, (grp ? grp - 1 : 0) * RGROUP, 64);
+      const uint32_t fnext = __shfl(f, (grp + 1 < 64 / RGROUP ? grp + 1 : grp) * RGROUP, 64);
+      const bool head = grp == 0 || fprev != f, tail = grp + 1 == 64 / RGROUP || fnext != f;
+      const uint64_t hm = __ballot(head), tm = __ballot(tail);
+      uint32_t hb = 0, tb = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < 64 / RGROUP; ++g) {
+        hb |= static_cast<uint32_t>((hm >> (g * RGROUP)) & 1u) << g;
+        tb |= static_cast<uint32_t>((tm >> (g * RGROUP)) & 1u) << g;
+      }
+      uint32_t incl = c;  // inclusive prefix of the groups' counts
+#pragma unroll
+      for (uint32_t d = 1; d < 64 / RGROUP; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d * RGROUP, 64);
+        if (grp >= d) incl += y;
+      }
+      const uint32_t rstart = 31u - __clz(hb & ((2u << grp) - 1u));
+      const uint32_t rend = grp + __ffs(tb >> grp) - 1u;
+      const uint32_t prev_incl = __shfl(incl, (rstart ? rstart - 1 : 0) * RGROUP, 64);  // every lane takes part
+      const uint32_t before = rstart ? prev_incl : 0u;
+      const uint32_t rincl = incl - before;  // this run's count up to and including this group
+      if (MODE == 0) {
+        if (tail && sub == 0 && f != 0xFFFFFFFFu && rincl && !(abl & 4)) atomicAdd(&a.fcount[f], rincl);
+      } else {
+        uint64_t base = 0;
+        if (tail && sub == 0 && f != 0xFFFFFFFFu && rincl)
+          base = a.out_off[f] + ((abl & 4) ? 0u : atomicAdd(&a.fcursor[f], rincl));
+        base = __shfl(base, rend * RGROUP, 64);
+        uint64_t p = base + (rincl - c);  // this record's first position
+        uint32_t id[RPER];
+#pragma unroll
+        for (uint32_t k = 0; k < RPER; ++k) id[k] = live[k] ? rv.rank_id[rk[k]] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < RPER; ++k) {
+          const uint32_t bits = static_cast<uint32_t>(__ballot(live[k]) >> (grp * RGROUP)) & 0xFFu;
+          const uint32_t rank = __popc(bits & ((1u << sub) - 1u));
+          if (live[k] && p + rank < a.out_cap) a.out_ids[p + rank] = id[k];
+          p += __popc(bits);
+        }
+      }
+    } else {
+      // ---- one big record: RCHUNK ranks over the wave, every load of the pass in flight ----
+      const uint32_t br = a.range_cap - 1 - static_cast<uint32_t>(u - nrows);
+      const RRange rg = a.ranges[br];
+      const bool check = guard || (rg.flags >> RRANGE_MIND_SHIFT) != 0;
+      uint32_t rk[RUNROLL];
+      bool live[RUNROLL];
+#pragma unroll
+      for (uint32_t k = 0; k < RUNROLL; ++k) {
+        const uint32_t i = rg.lo + k * 64 + lane;
+        rk[k] = i < rg.hi ? rank_at(rv, i, rg.flags) : 0u;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < RUNROLL; ++k)
+        live[k] = rg.lo + k * 64 + lane < rg.hi && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
+      if (MODE == 0) {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < RUNROLL; ++k) cnt += live[k] ? 1u : 0u;
         uint32_t tot;
         (void)wave_excl(cnt, &tot);
-        if (lane == b) c = tot;
+        if (lane == 0) {
+          a.rcount[br] = tot;
+          if (tot && !(abl & 4)) atomicAdd(&a.fcount[rg.f], tot);
+        }
+      } else {
+        uint32_t id[RUNROLL];
+#pragma unroll
+        for (uint32_t k = 0; k < RUNROLL; ++k) id[k] = live[k] ? rv.rank_id[rk[k]] : 0u;
+        const uint32_t c = a.rcount[br];
+        uint64_t p = 0;
+        if (lane == 0 && c) p = a.out_off[rg.f] + ((abl & 4) ? 0u : atomicAdd(&a.fcursor[rg.f], c));
+        p = __shfl(p, 0, 64);
+#pragma unroll
+        for (uint32_t k = 0; k < RUNROLL; ++k) {
+          const uint64_t m = __ballot(live[k]);
+          const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+          if (live[k] && p + rank < a.out_cap) a.out_ids[p + rank] = id[k];
+          p += __popcll(m);
+        }
       }
-    }
-    if (MODE == 0 && valid) {
-      a.rcount[r] = c;
-      if (c) atomicAdd(&a.fcount[rg.f], c);
     }
   }
 }
@@ -726,7 +870,7 @@ hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32
 
 // grid of the output kernels: sized by the range capacity (the range count is on the device)
 static uint32_t out_blocks(uint32_t cap) {
-  const uint64_t waves = (static_cast<uint64_t>(cap) + 63) / 64;
+  const uint64_t waves = (static_cast<uint64_t>(cap) + 7) / 8;  // rows of 8 small records + big records
   return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((waves + 3) / 4, 8192)));
 }
 

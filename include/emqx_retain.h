@@ -107,8 +107,9 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes
  * stack spills to the next round, 0 = never, default 128), "spill_per_wave" (spilled pieces
  * per wave of a round, default 4), "spill_rounds" (budgeted rounds per call, then one without
  * a budget, default 4), "search" (0: two-level binary searches of the postings and rank lists,
- * 1: 16-ary search trees).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
- * _SEARCH give the initial values at create.  EMQX_ENOTFOUND for unknown keys. */
+ * 1: 16-ary search trees, default), "walk_waves" (persistent waves of the first round, default
+ * 8192), "spill_waves" (waves of a spill round at most, default 4096).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
+ * _SEARCH / _WALK_WAVES / _SPILL_WAVES give the initial values at create.  EMQX_ENOTFOUND for unknown keys. */
 int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value);
 int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out);
 

@@ -236,6 +236,36 @@ def test_tile_sizes_parity(mod, tile):
         assert g == r == tt.dispatch(f, 100), f
 
 
+@pytest.mark.parametrize("search", [0, 1])
+def test_search_variants_parity(mod, search):
+    """The postings / per-depth rank-list slices are cut by two-level binary searches
+    (search 0) or 16-ary search trees (search 1, several levels deep here: postings groups of
+    thousands of nodes).  Both give the oracle's sets and the same visit and range counts."""
+    rng = random.Random(1200 + search)
+    names = sorted({b"/".join([b"r%d" % rng.randrange(6), b"m%d" % rng.randrange(400),
+                               b"x%d" % rng.randrange(3), b"l%d" % rng.randrange(900)][: rng.randrange(2, 5)])
+                    for _ in range(20000)})
+    expiry = [rng.choice([0, 0, 0, 90, 110]) for _ in names]
+    idx = mod.RetainIndex()
+    idx.store(names, expiry)
+    idx.commit()
+    filters = [b"+/+/x1", b"+/+/x2/+", b"+/m7/+/#", b"r1/+/x0", b"+/+/+/l5", b"+/+/+", b"+/#", b"#", b"r2/+/+/+",
+               b"+/m3", b"r3/m9/+/l1", b"+/+/x0/l77", b"+/m400/#"]
+    filters += [b"/".join(rng.choice([b"+", b"r%d" % rng.randrange(6), b"m%d" % rng.randrange(400),
+                                      b"x%d" % rng.randrange(3), b"l%d" % rng.randrange(900)])
+                          for _ in range(rng.randrange(1, 5))) for _ in range(300)]
+    tt = RR.TokenTrie(names, expiry)
+    idx.set_tuning("search", 1 - search)
+    ref = idx.match(filters, 100)
+    st0 = idx.stats()
+    idx.set_tuning("search", search)
+    got = idx.match(filters, 100)
+    st1 = idx.stats()
+    assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
+    for f, g, r in zip(filters, got, ref):
+        assert g == r == tt.dispatch(f, 100), f
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_match_spec_strict_guard_for_plain_filters(mod, seed):
     """match_messages/3 and page_read/4 run make_match_spec/1 for plain topics too, whose guard
