@@ -240,9 +240,6 @@ int full_commit(emqx_engine* e) {
   s->tv.root_base = ht.root_base;
   s->tv.root_meta = ht.root_meta;
   s->tv.root_hash_fid = ht.root_hash_fid;
-  s->tv.delta_base = 0;
-  s->tv.delta_meta = 0;
-  s->tv.delta_hash_fid = FID_NONE;
   s->n_nodes = ht.n_nodes;
   s->n_slots = n_slots;
   s->n_words = ht.n_words;

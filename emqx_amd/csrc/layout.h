@@ -106,11 +106,6 @@ struct TableView {
   uint32_t root_base;      // root's edge array
   uint32_t root_meta;      // META_* of the root
   uint32_t root_hash_fid;  // filter '#' or FID_NONE
-  // delta trie (incremental commits): filters inserted since the last full build live in a
-  // second trie in the same slot space; walks start at both roots (delta_meta = 0: none)
-  uint32_t delta_base;
-  uint32_t delta_meta;
-  uint32_t delta_hash_fid;
 };
 
 // murmur3 fmix32: spreads word ids inside a node's edge array.

@@ -227,12 +227,9 @@ __device__ uint32_t exact_walk1(const TableView& tv, uint32_t root_base, uint32_
   return (meta & META_HAS_EDGES) ? tv.fids[2u * at + 1u] : term_inline;
 }
 
-// ... in the base trie, then in the delta trie (a live filter is in exactly one of them)
 template <class WidAt>
 __device__ uint32_t exact_walk(const TableView& tv, uint32_t nlev, WidAt wid_at) {
-  const uint32_t f = exact_walk1(tv, tv.root_base, tv.root_meta, tv.root_hash_fid, nlev, wid_at);
-  if (f != FID_NONE || !tv.delta_meta) return f;
-  return exact_walk1(tv, tv.delta_base, tv.delta_meta, tv.delta_hash_fid, nlev, wid_at);
+  return exact_walk1(tv, tv.root_base, tv.root_meta, tv.root_hash_fid, nlev, wid_at);
 }
 
 // Item (8 B):  x = edge-array base of the node
@@ -665,12 +662,11 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   uint32_t evals = 0;     // per lane
   uint32_t dg[DIAG_NCOUNT] = {};  // diagnostic counters (per lane)
 
-  // roots (the base trie's and, after incremental commits, the delta trie's): '#' emission,
-  // exact walk of wildcard topics, the root items
+  // the root: '#' emission, exact walk of wildcard topics, the root item
   {
-    bool e0 = false, e1 = false, e2 = false, push = false, push2 = false;
+    bool e0 = false, e1 = false, push = false;
     uint32_t g1 = 0;
-    uint2 it = make_uint2(0, 0), it2 = make_uint2(0, 0);
+    uint2 it = make_uint2(0, 0);
     if (valid && !defer) {
       if (wild) {
         if (mode == MODE_ROUTES) {
@@ -681,32 +677,24 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
         evals = 1;  // the root visit, F_0
         // filter '#'; '$' rule (emqx_trie.erl:272-279): no root-level '+' or '#' for '$' topics
         e0 = !dollar && (tv.root_meta & META_HAS_HASH);
-        e2 = !dollar && (tv.delta_meta & META_HAS_HASH);
         if (tv.root_meta & META_HAS_EDGES) {
           push = true;
           const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
           it = make_item(tv.root_base, rmeta, dollar, false, lane, wbase);
         }
-        if (tv.delta_meta & META_HAS_EDGES) {
-          push2 = true;
-          const uint32_t dmeta = dollar ? (tv.delta_meta & ~META_HAS_PLUS) : tv.delta_meta;
-          it2 = make_item(tv.delta_base, dmeta, dollar, false, lane, wbase);
-        }
       }
     }
-    const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u) + (e2 ? 1u : 0u);
+    const uint32_t c = (e0 ? 1u : 0u) + (e1 ? 1u : 0u);
     uint32_t tot;
     uint32_t pos = wave_prefix<2>(c, lane, &tot);
     const uint64_t tag = static_cast<uint64_t>(lane) << 32;
     if (e0) { if (pos < cap) slab[pos] = tag | tv.root_hash_fid; ++pos; }
     if (e1) { if (pos < cap) slab[pos] = tag | g1; ++pos; }
-    if (e2) { if (pos < cap) slab[pos] = tag | tv.delta_hash_fid; ++pos; }
     if (c) L.cnt[lane] = c;
     cursor = tot;
     uint32_t ptot;
-    uint32_t ppos = wave_prefix<2>((push ? 1u : 0u) + (push2 ? 1u : 0u), lane, &ptot);
-    if (push) L.stack[ppos++] = it;
-    if (push2) L.stack[ppos] = it2;
+    const uint32_t ppos = wave_prefix<2>(push ? 1u : 0u, lane, &ptot);
+    if (push) L.stack[ppos] = it;
     top = ptot;
     maxtop = top;
     wave_sync();
@@ -997,17 +985,11 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     } else {
       if (lane == 0) evals = 1;
       const bool eh = lane == 0 && !dollar && (tv.root_meta & META_HAS_HASH);
-      const bool dh = lane == 0 && !dollar && (tv.delta_meta & META_HAS_HASH);
-      emit(eh, tv.root_hash_fid, dh, tv.delta_hash_fid, false, 0, false, 0);
+      emit(eh, tv.root_hash_fid, false, 0, false, 0, false, 0);
       if (tv.root_meta & META_HAS_EDGES) {
         const uint32_t rmeta = dollar ? (tv.root_meta & ~META_HAS_PLUS) : tv.root_meta;
         if (lane == 0)
           stack[top] = make_uint4(tv.root_base, rmeta, 0u, dollar ? 1u : 0u);  // {base, meta, widx, droot}
-        top += 1;
-      }
-      if (tv.delta_meta & META_HAS_EDGES) {
-        const uint32_t dmeta = dollar ? (tv.delta_meta & ~META_HAS_PLUS) : tv.delta_meta;
-        if (lane == 0) stack[top] = make_uint4(tv.delta_base, dmeta, 0u, dollar ? 1u : 0u);
         top += 1;
       }
     }

@@ -18,7 +18,7 @@ timeout -k 10 600 python -u bench.py --cache /tmp/wlB > "$OUT/bench.json" 2> "$O
 cat "$OUT/bench.json"
 echo "== rocprofv3 kernel stats"; date
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o run -- python3 "$ROOT/bench.py" --cache /tmp/wlB --no-cpu-baseline --streams 1 > "$ROOT/$OUT/prof_bench.json" 2> "$ROOT/$OUT/prof_bench.err" || { echo rocprof failed; tail -20 "$ROOT/$OUT/prof_bench.err"; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o run -- python3 "$ROOT/bench.py" --cache /tmp/wlB --no-cpu-baseline --no-host-api --streams 1 > "$ROOT/$OUT/prof_bench.json" 2> "$ROOT/$OUT/prof_bench.err" || { echo rocprof failed; tail -20 "$ROOT/$OUT/prof_bench.err"; exit 1; }
 cd "$ROOT"
 find "$OUT/prof" -name "*kernel_stats.csv" -exec head -8 {} \;
 echo "== pmc passes"; date
@@ -26,7 +26,7 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   cd /tmp
-  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex match_fast_kernel --output-format csv -d "$ROOT/$OUT/pmc$i" -o pmc -- python3 "$ROOT/bench.py" --cache /tmp/wlB --no-cpu-baseline --streams 1 --steps 3 --warmup 1 > "$ROOT/$OUT/pmc$i.log" 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex match_fast_kernel --output-format csv -d "$ROOT/$OUT/pmc$i" -o pmc -- python3 "$ROOT/bench.py" --cache /tmp/wlB --no-cpu-baseline --no-host-api --streams 1 --steps 3 --warmup 1 > "$ROOT/$OUT/pmc$i.log" 2>&1
   rc=$?; cd "$ROOT"; echo "pmc pass $i ($grp) rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python tools/pmc_summary.py --dir "$OUT" --kernel match_fast_kernel | tee "$OUT/pmc_summary.json"
