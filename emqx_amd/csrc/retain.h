@@ -144,6 +144,7 @@ enum RCtrl : uint32_t {
   RC_EMITTED = 7,  // range records written (RC_RANGES counts reserved slots: waves reserve
                    // RRES at a time, the unused ones stay zeroed = empty records)
   RC_BIG = 8,      // big range records, stored from the top of ranges[] down
+  RC_TILE = 9,     // first-round tiles taken beyond the first a.waves
   RC_WORDS = 16
 };
 

@@ -569,7 +569,9 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
   uint64_t pacc[RPROF_SLOTS] = {0, 0, 0, 0, 0, 0, 0, 0};
   RangeRes res;
 
-  for (uint64_t t = gw; t < ntiles; t += a.waves) {
+  // tiles beyond the first wave-full are taken first come, first served (one atomic per
+  // tile): a wave whose tile was light takes the next one instead of a fixed stride's
+  for (uint64_t t = gw; t < ntiles;) {
     const uint64_t f = t * tf + lane;
     const bool valid = lane < tf && f < a.n;
     // ---- tokenize + intern (per lane) -------------------------------------------------
@@ -631,6 +633,9 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
                              lds_words ? s_words[wib] : nullptr, s_pref[wib], s_item[wib], visits,
                              overflow, res, pacc);
     if (overflow) break;
+    uint32_t nx = 0;
+    if (lane == 0) nx = atomicAdd(&a.ctrl[RC_TILE], 1u);
+    t = a.waves + static_cast<uint64_t>(__shfl(nx, 0, 64));
   }
   if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
   // visits: one atomic per wave
