@@ -413,12 +413,26 @@ def retain_traffic(nf, n_retained):
     return round(p["traffic_bytes_per_call"]), "profiles/pmc_retain.json (%s; %s)" % (p["traffic_rule"], p["source"])
 
 
+def pmc_file(args):
+    """The committed PMC summary of the fast kernel for this exact workload (B, D, or config C's
+    100M-filter table on one GPU), or None."""
+    if args.mode != 0:
+        return None
+    if args.workload == "D" and args.vocab_scale == 1:
+        return "pmc_match_fast_D.json"
+    if args.workload == "B" and args.vocab_scale == 1 and args.n_filters == 10_000_000:
+        return "pmc_match_fast.json"
+    if args.workload == "B" and args.vocab_scale == 4 and args.n_filters == 100_000_000:
+        return "pmc_match_fast_C1.json"
+    return None
+
+
 def measured_traffic(n, args):
     """HBM bytes per launch of the fused match kernel from the committed rocprofv3 PMC passes
     (profiles/pmc_match_fast.json, written from tools/gpu_round.sh's counter runs on the same
     workload), scaled to this batch.  None when the file is absent or the workload differs."""
-    fname = {"B": "pmc_match_fast.json", "D": "pmc_match_fast_D.json"}.get(args.workload)
-    if fname is None or args.mode != 0 or args.vocab_scale != 1 or (args.workload == "B" and args.n_filters != 10_000_000):
+    fname = pmc_file(args)
+    if fname is None:
         return None, None
     path = os.path.join(ROOT, "profiles", fname)
     if not os.path.exists(path):
@@ -553,8 +567,8 @@ def request_roofline(n, kms, args):
     (committed PMC passes, scaled to this batch) / its HIP-event time, against the measured
     random-access ceiling.  The walk is a chain of dependent random 16-B probes, so this, not
     the byte rate, is what bounds it."""
-    fname = {"B": "pmc_match_fast.json", "D": "pmc_match_fast_D.json"}.get(args.workload)
-    if fname is None or args.mode != 0 or args.vocab_scale != 1 or (args.workload == "B" and args.n_filters != 10_000_000):
+    fname = pmc_file(args)
+    if fname is None:
         return None
     path = os.path.join(ROOT, "profiles", fname)
     ceil = gather_ceiling()
@@ -992,7 +1006,7 @@ def retain_bench(args, rank, world, dev):
         "walk_ms_median": round(float(np.median(walk_ms)), 4),
         "walk_spill_rounds": int(st["last_spill_rounds"]), "walk_spilled_items": int(st["last_spilled"]),
         "walk_step_budget": args.retain_budget if args.retain_budget is not None else "128 (default)",
-        "walk_tile_filters": args.retain_tile if args.retain_tile is not None else 8,
+        "walk_tile_filters": args.retain_tile if args.retain_tile is not None else 10,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": retain_traffic(nf, len(names))[0],
                      "traffic_source": retain_traffic(nf, len(names))[1],

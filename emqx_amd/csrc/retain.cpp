@@ -1,6 +1,7 @@
 // C ABI of the retained-message index (include/emqx_retain.h): host topic store, trie build
 // with DFS-preorder ranks, snapshot upload/swap, and the match pipeline
-//   walk -> [D2H: ranges emitted] -> count -> scan -> [D2H: total] -> write.
+//   walk -> spill rounds -> count -> scan -> write -> [one D2H: control words + id total],
+// all enqueued at once (the device reads every count it needs).
 // Reference semantics: apps/emqx_retainer/src/emqx_retainer_mnesia.erl (see retain.h and
 // oracle/retain_ref.py).
 #include <hip/hip_runtime.h>
@@ -149,7 +150,7 @@ constexpr uint32_t MAX_WAVES = 8192;
 // spills the rest as 64-node pieces, and the next round deals them evenly over up to
 // SPILL_WAVES waves.  The heavy filters' work is wide '+' slices (thousands of nodes per item):
 // config R's walk drops from 10.7 to 3.8 ms in 2 rounds (profiles/r1_v8_retain_sweep.txt).
-// EMQX_RETAIN_STEP_BUDGET overrides it (0 = no budget).
+// emqx_retain_set_tuning "step_budget" overrides it (0 = no budget).
 constexpr uint32_t STEP_BUDGET = 128;
 constexpr uint32_t SPILL_WAVES = 4096;
 constexpr uint32_t SPILL_PER_WAVE = 4;  // spilled pieces dealt to each wave of a spill round
@@ -157,11 +158,12 @@ constexpr uint32_t SPILL_CAP = 1u << 22;  // items per spill buffer (a full one:
 constexpr uint32_t SPILL_ROUNDS = 4;      // budgeted spill rounds per call, then one without a
                                           // budget; all enqueued up front, empty ones exit at once
 
-// Filters per wave tile.  The walk is latency-bound (a few dependent loads per step), so the
+// Filters per wave tile.  The walk is latency-bound (one dependent round trip per step), so the
 // number of waves in flight, not lane fill, sets its rate: 64 filters per tile leaves ~6 waves
-// per CU for a 100K-filter batch; 8 runs the config-R walk in 10.8 ms against 18.1 ms
-// (profiles/r1_v8_retain_sweep.txt).
-constexpr uint32_t TILE_FILTERS = 8;
+// per CU for a 100K-filter batch.  With tiles taken first come first served, 10 (10K tiles over
+// 8192 waves) runs the config-R walk + spill in 1.96-1.99 ms against 2.23-2.25 ms for 8
+// (profiles/r2_retain_sweeps.txt).
+constexpr uint32_t TILE_FILTERS = 10;
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* e = std::getenv(name);
@@ -199,7 +201,7 @@ struct emqx_retain {
   // walk tuning (emqx_retain_set_tuning; the EMQX_RETAIN_* variables give the initial values)
   bool prof_on = false;
   uint32_t ablate = 0;  // EMQX_RETAIN_ABLATE (profiling builds only)  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
-  std::atomic<uint32_t> tile{8}, step_budget{128}, spill_per_wave{4}, spill_rounds{4}, search{RSEARCH_STREE},
+  std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{128}, spill_per_wave{4}, spill_rounds{4}, search{RSEARCH_STREE},
       walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES};
 };
 

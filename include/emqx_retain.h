@@ -103,7 +103,7 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes
                                    uint64_t* n_out, void* stream);
 
 /* Walk tuning (experiments and tests; results never depend on it).  Keys: "tile" (filters
- * per wave tile of the first round, 1..64, default 8), "step_budget" (wave steps before a
+ * per wave tile of the first round, 1..64, default 10), "step_budget" (wave steps before a
  * stack spills to the next round, 0 = never, default 128), "spill_per_wave" (spilled pieces
  * per wave of a round, default 4), "spill_rounds" (budgeted rounds per call, then one without
  * a budget, default 4), "search" (0: two-level binary searches of the postings and rank lists,

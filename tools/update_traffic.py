@@ -36,6 +36,8 @@ def calibration(d):
 WORKLOADS = {
     "B": ("B: 10M filters, 1M-topic batch (bench.py defaults)", "pmc_match_fast.json"),
     "D": ("D: 1M adversarial filters, 1M-topic batch (bench.py --workload D)", "pmc_match_fast_D.json"),
+    "C1": ("C1: config C's 100M-filter table on one GPU, 1M-topic batch (bench.py --n-filters 100000000 "
+           "--vocab-scale 4)", "pmc_match_fast_C1.json"),
 }
 
 
