@@ -126,6 +126,12 @@ def main():
                     help="experiment: host-side permutation of the topic batch (sorted = lexicographic; "
                          "xcd = sorted, cut into 8 key-range segments, dealt 256 topics at a time so each "
                          "XCD's blocks see one segment)")
+    ap.add_argument("--walk-order", type=str, default="auto", choices=["auto", "on", "off"],
+                    help="engine walk order (emqx_set_tuning 'order'): the batch is walked in prefix-key "
+                         "order with XCD-contiguous tile ranges, inside the call (auto: deep tables)")
+    ap.add_argument("--walk-level-bits", type=int, default=0, help="walk order: key bits per level (0 = auto)")
+    ap.add_argument("--walk-sort-bits", type=int, default=64, help="walk order: top key bits sorted on")
+    ap.add_argument("--walk-deal", type=int, default=1, help="walk order: deal tile ranges to XCDs (1) or not (0)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per kernel launch from PMC (rocprofv3 FETCH_SIZE/WRITE_SIZE)")
     args = ap.parse_args()
@@ -178,6 +184,7 @@ def main():
 
     t0 = time.time()
     eng = Engine(local)
+    set_walk_order(eng, args)
     with progress(f"[rank {rank}] building table"):
         eng.insert_packed(*wl.filters)
         eng.commit()
@@ -303,7 +310,8 @@ def main():
         "data": "synthetic",
         "config": {"workload": WORKLOAD_NAMES["C1" if args.vocab_scale > 1 else args.workload],
                    "n_filters": wl.n_filters, "batch_topics_per_gpu": n, "mode": ["routes", "trie", "trie_wildcard"][args.mode],
-                   "parallelism": f"replicated table, topic stream split x{world}"},
+                   "parallelism": f"replicated table, topic stream split x{world}",
+                   "walk_order": walk_order_desc(args, st)},
         "evals_per_s": round(evals_all * args.steps / elapsed, 1),
         "matches_per_topic": round(nout_all / (n * world), 3),
         "evals_per_topic": round(evals_all / (n * world), 3),
@@ -1069,6 +1077,24 @@ def update_cpu_baseline(wl, nb, k, args):
     return {"value": round(ops / t_total, 1), "unit": "updates/s", "cores": 1, "kind": "port",
             "sample": f"{r} rounds of {k} deletes + {k} inserts on the same {nb}-filter table (C++ restatement "
                       "of emqx_trie:insert/delete key maintenance, no mnesia transaction, one writer)"}
+
+
+def set_walk_order(eng, args):
+    eng.set_tuning("order", {"auto": -1, "on": 1, "off": 0}[args.walk_order])
+    eng.set_tuning("order_level_bits", args.walk_level_bits)
+    eng.set_tuning("order_sort_bits", args.walk_sort_bits)
+    eng.set_tuning("order_deal", args.walk_deal)
+
+
+def walk_order_desc(args, st):
+    """The engine's walk order for this table (engine.cpp use_order: auto = tables deeper than
+    12 levels, batches of >= 65536 topics)."""
+    on = args.walk_order == "on" or (args.walk_order == "auto" and st.get("max_depth", 0) > 12)
+    if not on:
+        return "batch order"
+    lb = args.walk_level_bits or (4 if st.get("max_depth", 0) > 12 else 8)
+    return (f"prefix-key order inside the call ({lb} bits per level, top {args.walk_sort_bits} bits sorted"
+            f"{', tile ranges dealt to XCDs' if args.walk_deal else ''})")
 
 
 def reorder_topics(wl, order):

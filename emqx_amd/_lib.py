@@ -77,6 +77,7 @@ class Stats(ctypes.Structure):
         ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double),
         ("last_kernel_ms", ctypes.c_double),
         ("delta_filters", ctypes.c_uint64), ("last_commit_kind", ctypes.c_uint64),
+        ("max_depth", ctypes.c_uint64), ("last_ordered", ctypes.c_uint64), ("last_order_ms", ctypes.c_double),
     ]
 
     def __init__(self, *a, **kw):

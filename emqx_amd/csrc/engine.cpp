@@ -133,6 +133,20 @@ struct Workspace {
   uint32_t deep_slab_cap = 1u << 20;
   uint64_t* h_rb = nullptr;         // pinned call summary (SUM_WORDS), written by tile_scan_kernel
   bool deep_ready = false;
+  // walk order (order_kernels.hip): prefix keys, sorted positions, the reordered batch
+  bool ordered = false;             // the last call enqueued walked in prefix-key order
+  hipEvent_t evo = nullptr;         // start of its reordering
+  uint64_t ord_cap_n = 0, ord_cap_bytes = 0, ord_temp_bytes = 0;
+  uint64_t* ord_keys = nullptr;
+  uint64_t* ord_keys_out = nullptr;
+  uint32_t* ord_idx = nullptr;
+  uint32_t* ord_perm = nullptr;
+  uint32_t* ord_lens = nullptr;
+  uint32_t* ord_corig = nullptr;
+  uint64_t* ord_noffs = nullptr;
+  uint64_t* ord_partials = nullptr;
+  uint8_t* ord_bytes = nullptr;
+  uint8_t* ord_temp = nullptr;
 
   ~Workspace() {
     (void)hipSetDevice(device);
@@ -140,10 +154,13 @@ struct Workspace {
     dfree(tile_defer); dfree(spill); dfree(diag); dfree(ctrl); dfree(tile_sum); dfree(tile_stats);
     dfree(group_sum); dfree(group_stats);
     dfree(deep_wids); dfree(deep_stack); dfree(deep_slab);
+    dfree(ord_keys); dfree(ord_keys_out); dfree(ord_idx); dfree(ord_perm); dfree(ord_lens); dfree(ord_corig);
+    dfree(ord_noffs); dfree(ord_partials); dfree(ord_bytes); dfree(ord_temp);
     if (h_rb) (void)hipHostFree(h_rb);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (evk) (void)hipEventDestroy(evk);
+    if (evo) (void)hipEventDestroy(evo);
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -186,6 +203,15 @@ struct emqx_engine {
   std::mutex hb_mu;             // pinned host batches of emqx_match_batch (pool)
   std::vector<emqx_host_batch*> hb_free;
   int commit_threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  // walk order (emqx_set_tuning): "order" -1 auto (deep tables, batches of >= ORDER_MIN_N
+  // topics) / 0 off / 1 on; "order_level_bits" key bits per level (0: 4 for deep tables, else
+  // 8); "order_sort_bits" top key bits sorted on; "order_deal" XCD-contiguous tile ranges
+  std::atomic<int> order{-1};
+  std::atomic<int> order_level_bits{0};
+  std::atomic<int> order_sort_bits{64};
+  std::atomic<int> order_deal{1};
+  std::atomic<uint64_t> last_ordered{0};
+  std::atomic<double> last_order_ms{0};
 };
 
 namespace {
@@ -393,6 +419,7 @@ int ensure_ws(Workspace* w, uint64_t n) {
     HIP_TRY(hipEventCreate(&w->ev0));
     HIP_TRY(hipEventCreate(&w->ev1));
     HIP_TRY(hipEventCreate(&w->evk));
+    HIP_TRY(hipEventCreate(&w->evo));
     HIP_TRY(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_rb), SUM_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     HIP_TRY(dalloc(w->ctrl, CTRL_WORDS));
@@ -429,6 +456,42 @@ int ensure_ws(Workspace* w, uint64_t n) {
     const uint64_t cap = need_slab;
     HIP_TRY(dalloc(w->slab, cap));
     w->cap_slab = cap;
+  }
+  return EMQX_OK;
+}
+
+constexpr uint64_t ORDER_MIN_N = 65536;
+
+bool use_order(const emqx_engine* e, const Snapshot& snap, uint64_t n) {
+  const int o = e->order.load();
+  if (o >= 0) return o > 0 && n > 0;
+  return snap.max_depth > 12 && n >= ORDER_MIN_N;
+}
+
+// Walk-order buffers for n topics; the reordered bytes buffer keeps `cap_bytes` (grown by
+// run_match when a call reports CTRL_ERR_ORDER_CAP).
+int ensure_order(Workspace* w, uint64_t n, uint32_t sort_bits) {
+  if (n > w->ord_cap_n) {
+    const uint64_t cap = round_pow2(std::max<uint64_t>(n, 1024));
+    HIP_TRY(dalloc(w->ord_keys, cap));
+    HIP_TRY(dalloc(w->ord_keys_out, cap));
+    HIP_TRY(dalloc(w->ord_idx, cap));
+    HIP_TRY(dalloc(w->ord_perm, cap));
+    HIP_TRY(dalloc(w->ord_lens, cap));
+    HIP_TRY(dalloc(w->ord_corig, cap));
+    HIP_TRY(dalloc(w->ord_noffs, cap + 1));
+    HIP_TRY(dalloc(w->ord_partials, scan_partials(cap)));
+    w->ord_cap_n = cap;
+  }
+  const uint64_t tb = order_sort_temp_bytes(n, sort_bits);
+  if (!w->ord_temp || tb > w->ord_temp_bytes) {
+    HIP_TRY(dalloc(w->ord_temp, tb));
+    w->ord_temp_bytes = tb;
+  }
+  if (!w->ord_bytes || w->ord_cap_bytes < 48 * n + 4096) {
+    const uint64_t cap = std::max<uint64_t>(w->ord_cap_bytes, 48 * n + 4096);
+    HIP_TRY(dalloc(w->ord_bytes, cap + 16));
+    w->ord_cap_bytes = cap;
   }
   return EMQX_OK;
 }
@@ -486,10 +549,46 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.out_ids = d_out_ids;
   a.out_cap = d_out_ids ? cap : 0;
   a.summary = summary;
+  const bool ordered = use_order(e, snap, n);
+  const uint32_t sort_bits = static_cast<uint32_t>(std::min(64, std::max(1, e->order_sort_bits.load())));
+  if (ordered) {
+    rc = ensure_order(w, n, sort_bits);
+    if (rc != EMQX_OK) return rc;
+  }
 
   HIP_TRY(hipStreamWaitEvent(s, w->done, 0));
   w->last_stream = s;
   HIP_TRY(hipMemsetAsync(w->ctrl, 0, CTRL_WORDS * sizeof(uint32_t), s));
+  w->ordered = ordered;
+  if (ordered) {
+    HIP_TRY(hipEventRecord(w->evo, s));
+    OrderArgs o{};
+    o.tbytes = d_tbytes;
+    o.toffs = d_toffs;
+    o.n = n;
+    const int lb = e->order_level_bits.load();
+    o.level_bits = static_cast<uint32_t>(lb > 0 ? std::min(lb, 32) : (snap.max_depth > 12 ? 4 : 8));
+    o.sort_bits = sort_bits;
+    o.keys = w->ord_keys;
+    o.keys_out = w->ord_keys_out;
+    o.idx = w->ord_idx;
+    o.perm = w->ord_perm;
+    o.lens = w->ord_lens;
+    o.noffs = w->ord_noffs;
+    o.partials = w->ord_partials;
+    o.obytes = w->ord_bytes;
+    o.cap_bytes = w->ord_cap_bytes;
+    o.temp = w->ord_temp;
+    o.temp_bytes = w->ord_temp_bytes;
+    o.ctrl = w->ctrl;
+    HIP_TRY(launch_order(o, s));
+    a.tbytes = w->ord_bytes;
+    a.toffs = w->ord_noffs;
+    a.perm = w->ord_perm;
+    a.deal = e->order_deal.load() ? 1u : 0u;
+    a.corig = w->ord_corig;
+    a.partials = w->ord_partials;
+  }
   HIP_TRY(hipEventRecord(w->ev0, s));
   HIP_TRY(launch_match_fast(a, pick_variant(e, snap), s));
   HIP_TRY(hipEventRecord(w->evk, s));
@@ -533,6 +632,15 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
         w->deep_slab_cap = static_cast<uint32_t>(std::min<uint64_t>(round_pow2(sm[SUM_DEEP_FILL] + uint64_t(DEEP_WAVES) * DEEP_CHUNK + 1), 1u << 30));
         HIP_TRY(dalloc(w->deep_slab, w->deep_slab_cap));
       }
+      if (err & CTRL_ERR_ORDER_CAP) {  // the batch's byte count, read once, sizes the reordered copy
+        uint64_t nb = 0;
+        HIP_TRY(hipMemcpy(&nb, d_toffs + n, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        uint64_t nb0 = 0;
+        HIP_TRY(hipMemcpy(&nb0, d_toffs, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        const uint64_t need = nb - nb0;
+        w->ord_cap_bytes = need + need / 8 + 4096;
+        HIP_TRY(dalloc(w->ord_bytes, w->ord_cap_bytes + 16));
+      }
       if (err & CTRL_ERR_TOO_DEEP) {
         if (w->deep_stack_cap >= (1u << 22)) {
           set_last_error("topic frontier exceeds the deep path's stack");
@@ -546,6 +654,11 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
     float kms = 0, ms = 0;
     if (hipEventElapsedTime(&kms, w->ev0, w->evk) == hipSuccess) e->last_kernel_ms.store(kms);
     if (hipEventElapsedTime(&ms, w->ev0, w->ev1) == hipSuccess) e->last_match_ms.store(ms);
+    float oms = 0;
+    if (w->ordered && hipEventElapsedTime(&oms, w->evo, w->ev0) == hipSuccess) ms += oms;
+    e->last_match_ms.store(ms);  // the call: reordering (if any) + match pipeline
+    e->last_order_ms.store(w->ordered ? oms : 0.0);
+    e->last_ordered.store(w->ordered ? 1 : 0);
     e->last_deferred.store(sm[SUM_DEFERRED]);
     e->last_evals.store(sm[SUM_EVALS]);
     e->last_max_stack.store(sm[SUM_MAXSTACK]);
@@ -1042,7 +1155,10 @@ int emqx_stats_get(emqx_engine* e, emqx_stats* dst) {
     out->n_slots = s->n_slots;
     out->n_words = s->n_words;
     out->table_bytes = s->bytes;
+    out->max_depth = s->max_depth;
   }
+  out->last_ordered = e->last_ordered.load();
+  out->last_order_ms = e->last_order_ms.load();
   out->last_evals = e->last_evals.load();
   out->last_deferred = e->last_deferred.load();
   out->last_max_stack = e->last_max_stack.load();
@@ -1086,6 +1202,25 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
     if (value < 1 || value > 256) return EMQX_EINVAL;
     std::lock_guard<std::mutex> g(e->writer);
     e->commit_threads = static_cast<int>(value);
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "order") == 0) {
+    if (value < -1 || value > 1) return EMQX_EINVAL;
+    e->order.store(static_cast<int>(value));
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "order_level_bits") == 0) {
+    if (value < 0 || value > 32) return EMQX_EINVAL;
+    e->order_level_bits.store(static_cast<int>(value));
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "order_sort_bits") == 0) {
+    if (value < 1 || value > 64) return EMQX_EINVAL;
+    e->order_sort_bits.store(static_cast<int>(value));
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "order_deal") == 0) {
+    e->order_deal.store(value != 0);
     return EMQX_OK;
   }
   if (std::strcmp(key, "delta_max") == 0) {

@@ -21,6 +21,7 @@ constexpr uint32_t GROUP_TILES = 256;  // tiles per group sum (two-level output 
 constexpr uint32_t CTRL_ERR_TOO_LONG = 1u;   // deferred topic longer than 65535 bytes
 constexpr uint32_t CTRL_ERR_TOO_DEEP = 2u;   // deep-path frontier exceeded its stack
 constexpr uint32_t CTRL_ERR_DEEP_SLAB = 4u;  // deep-path slab overflow
+constexpr uint32_t CTRL_ERR_ORDER_CAP = 8u;  // walk order: the reordered topic bytes exceed their buffer
 
 constexpr int TILE_TOPICS = 64;
 
@@ -97,6 +98,13 @@ struct MatchArgs {
   uint32_t* out_ids;       // [out_cap] CSR ids (caller's)
   uint64_t out_cap;
   uint64_t* summary;       // [SUM_WORDS] (device or host-pinned memory)
+  // walk order (order_kernels.hip): the batch is walked in prefix-key order
+  const uint32_t* perm;    // [n] batch position -> caller's topic index (nullptr: identity);
+                           // tbytes/toffs are then the reordered batch and out_off is in the
+                           // caller's order, filled by the scan of the counts put back
+  uint32_t deal;           // fast kernel: logical tiles dealt to XCDs in contiguous ranges
+  uint32_t* corig;         // [n] counts in the caller's order (perm set)
+  uint64_t* partials;      // [scan_partials(n)] scan scratch (perm set)
 };
 
 // Deep path: waves of match_deep_kernel, slab entries each wave reserves per atomic, and the
@@ -134,6 +142,31 @@ hipError_t launch_shard_owner(const uint8_t* tbytes, const uint64_t* toffs, uint
                               uint32_t levels, uint32_t* owner, hipStream_t s);
 // incremental commits (live_trie.cpp): whole-slot rewrites of the committed table, ids first
 hipError_t launch_slot_patches(EdgeSlot* edges, uint32_t* fids, const SlotPatch* patches, uint32_t n,
+                               hipStream_t s);
+// Walk order: prefix keys, radix sort, reordered topic bytes (order_kernels.hip).
+struct OrderArgs {
+  const uint8_t* tbytes;    // caller's batch
+  const uint64_t* toffs;
+  uint64_t n;
+  uint32_t level_bits;      // key bits per level (first level highest)
+  uint32_t sort_bits;       // top key bits the radix sort orders by (1..64)
+  uint64_t* keys;           // [n]
+  uint64_t* keys_out;       // [n]
+  uint32_t* idx;            // [n]
+  uint32_t* perm;           // [n] out: batch position -> caller's topic index
+  uint32_t* lens;           // [n]
+  uint64_t* noffs;          // [n + 1] out: offsets of the reordered batch
+  uint64_t* partials;       // [scan_partials(n)]
+  uint8_t* obytes;          // [cap_bytes] out: reordered topic bytes
+  uint64_t cap_bytes;
+  void* temp;               // radix sort scratch
+  uint64_t temp_bytes;
+  uint32_t* ctrl;           // CTRL_ERR_ORDER_CAP when the bytes exceed cap_bytes
+};
+uint64_t order_sort_temp_bytes(uint64_t n, uint32_t sort_bits);
+hipError_t launch_order(const OrderArgs& o, hipStream_t s);
+// after the walk: corig[perm[p]] = counts[p]
+hipError_t launch_order_counts(const uint32_t* counts, const uint32_t* perm, uint64_t n, uint32_t* corig,
                                hipStream_t s);
 // counts[n] -> offsets[n+1] (exclusive); partials: scratch of >= scan_partials(n) u64
 // (fan-out's entry scan).

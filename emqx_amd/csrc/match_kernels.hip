@@ -458,9 +458,17 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   const uint32_t lane = lane_id();
   const uint32_t wv = threadIdx.x >> 6;
   WaveLds& L = lds_all[wv];
-  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * WAVES + wv;
+  // With a reordered batch (a.deal), XCD x (blocks b = x mod 8, dispatched round robin)
+  // takes one contiguous range of logical blocks: neighbouring keys share its L2.
+  uint64_t blk = blockIdx.x;
+  if (a.deal) {
+    const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, j = blockIdx.x >> 3, q = nb >> 3, r = nb & 7u;
+    blk = static_cast<uint64_t>(x) * q + min(x, r) + j;
+  }
+  const uint64_t tile = blk * WAVES + wv;
   const uint64_t t0 = tile * TILE_TOPICS;
   if (t0 >= a.n) return;  // wave-uniform; the kernel uses no block-wide barrier
+  if (a.perm && (a.ctrl[CTRL_ERROR] & CTRL_ERR_ORDER_CAP)) return;  // no reordered batch: rerun
   const uint64_t clk0 = DIAG ? wall_clock64() : 0;
 
   const TableView& tv = a.tv;
@@ -1184,15 +1192,21 @@ __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
   const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4 + wv;
   const uint64_t t0 = tile * TILE_TOPICS;
   if (t0 >= a.n) return;
-  const uint64_t g = tile / GROUP_TILES, g0 = g * GROUP_TILES;
-  uint64_t before = 0;
-  for (uint64_t k = lane; k < g; k += 64) before += a.group_sum[k];
-  for (uint64_t j = g0 + lane; j < tile; j += 64) before += a.tile_sum[j];
-  before = wave_sum64(before);
   const uint64_t t = t0 + lane;
-  const uint64_t c = t < a.n ? a.counts[t] : 0;
-  const uint64_t off = before + wave_incl_scan64(c, lane) - c;
-  if (t < a.n) a.out_off[t] = off;
+  uint64_t off = 0;
+  if (a.perm) {  // reordered batch: out_off (the caller's order) is already scanned
+    if (a.ctrl[CTRL_ERROR] & CTRL_ERR_ORDER_CAP) return;
+    off = t < a.n ? a.out_off[a.perm[t]] : 0;
+  } else {
+    const uint64_t g = tile / GROUP_TILES, g0 = g * GROUP_TILES;
+    uint64_t before = 0;
+    for (uint64_t k = lane; k < g; k += 64) before += a.group_sum[k];
+    for (uint64_t j = g0 + lane; j < tile; j += 64) before += a.tile_sum[j];
+    before = wave_sum64(before);
+    const uint64_t c = t < a.n ? a.counts[t] : 0;
+    off = before + wave_incl_scan64(c, lane) - c;
+    if (t < a.n) a.out_off[t] = off;
+  }
   base[wv][lane] = off;
   run[wv][lane] = 0;
   wave_sync();
@@ -1240,7 +1254,7 @@ __global__ __launch_bounds__(64) void summary_kernel(MatchArgs a) {
     const uint32_t* c = a.ctrl;
     const uint32_t need = c[CTRL_NEED_SLAB], err = c[CTRL_ERROR];
     uint64_t flags = 0;
-    if (need > a.slab_cap || (err & (CTRL_ERR_DEEP_SLAB | CTRL_ERR_TOO_DEEP))) flags |= SUM_F_RETRY;
+    if (need > a.slab_cap || (err & (CTRL_ERR_DEEP_SLAB | CTRL_ERR_TOO_DEEP | CTRL_ERR_ORDER_CAP))) flags |= SUM_F_RETRY;
     if (tot > a.out_cap) flags |= SUM_F_OVERFLOW;
     if (err & CTRL_ERR_TOO_LONG) flags |= SUM_F_ERROR;
     a.out_off[a.n] = tot;
@@ -1265,7 +1279,7 @@ __global__ __launch_bounds__(256) void scatter_deep_kernel(MatchArgs a) {
     if (e == DEEP_PAD) continue;
     const uint32_t j = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
     const uint32_t t = a.deferred[j];
-    const uint64_t p = a.out_off[t] + atomicAdd(&a.deep_rank[j], 1u);
+    const uint64_t p = a.out_off[a.perm ? a.perm[t] : t] + atomicAdd(&a.deep_rank[j], 1u);
     if (p < a.out_cap) a.out_ids[p] = resolve_entry(a.tv, e);
   }
 }
@@ -1375,6 +1389,11 @@ hipError_t launch_assemble(const MatchArgs& a, hipStream_t s) {
   const uint64_t ntiles = (a.n + TILE_TOPICS - 1) / TILE_TOPICS;
   if (ntiles) {
     hipLaunchKernelGGL(group_reduce_kernel, dim3(a.ngroups), dim3(GROUP_TILES), 0, s, a, ntiles);
+    if (a.perm) {  // the counts back in the caller's order, scanned into out_off
+      hipError_t err = launch_order_counts(a.counts, a.perm, a.n, a.corig, s);
+      if (err == hipSuccess) err = launch_scan(a.corig, a.n, a.out_off, a.partials, s);
+      if (err != hipSuccess) return err;
+    }
     hipLaunchKernelGGL(scatter_fast_kernel, dim3(static_cast<uint32_t>((ntiles + 3) / 4)), dim3(256), 0, s, a);
   }
   hipLaunchKernelGGL(scatter_deep_kernel, dim3(64), dim3(256), 0, s, a);

@@ -1,0 +1,134 @@
+// Walk order (emqx_set_tuning "order"): a batch is matched in an order that groups topics by
+// prefix, so tiles that run together on one XCD walk the same subtrees and share its L2.
+//
+// The reference matches each published topic on its own (emqx_broker.erl:213 ->
+// emqx_router:match_routes/1, emqx_router.erl:128-133); the order in which a batch is walked
+// changes nothing in any topic's match set, and the CSR comes back in the caller's order.
+//
+//   order_key_kernel     per topic: a 64-bit prefix key (per level, the top `lbits` bits of a
+//                        hash of the word, first level in the highest bits) and its index
+//   radix sort           (rocprim) keys -> the topic indices in key order: perm[p] = topic
+//   order_len_kernel     lens[p] = length of topic perm[p]; a scan gives the new offsets
+//   order_gather_kernel  the topic bytes in the new order (one contiguous buffer again, as the
+//                        fast kernel's tokenizer wants)
+//   order_counts_kernel  after the walk: per-topic counts back to the caller's order, whose
+//                        scan is the output CSR's offsets (the scatter kernels write each
+//                        topic's ids at out_off[perm[p]])
+// The fast kernel also deals logical tiles to XCDs in contiguous ranges (MatchArgs::deal), so
+// each XCD walks one slice of the key space.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "kernels.h"
+
+namespace emqx {
+
+namespace {
+
+__global__ __launch_bounds__(256) void order_key_kernel(const uint8_t* __restrict__ tbytes,
+                                                        const uint64_t* __restrict__ toffs, uint64_t n,
+                                                        uint32_t lbits, uint32_t sort_bits, uint64_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ idx) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t s = toffs[i], e = toffs[i + 1];
+    uint64_t key = 0;
+    uint32_t room = 64, h = 0x811C9DC5u;
+    for (uint64_t p = s; p <= e && room; ++p) {
+      const uint32_t c = p < e ? tbytes[p] : static_cast<uint32_t>('/');
+      if (c == '/') {
+        const uint32_t take = min(lbits, room);
+        room -= take;
+        key |= static_cast<uint64_t>(mix32(h) >> (32u - take)) << room;
+        h = 0x811C9DC5u;
+      } else {
+        h = (h ^ c) * 0x01000193u;
+      }
+    }
+    keys[i] = key >> (64u - sort_bits);  // the sort orders bits [0, sort_bits)
+    idx[i] = static_cast<uint32_t>(i);
+  }
+}
+
+__global__ __launch_bounds__(256) void order_len_kernel(const uint64_t* __restrict__ toffs,
+                                                        const uint32_t* __restrict__ perm, uint64_t n,
+                                                        uint32_t* __restrict__ lens) {
+  for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < n;
+       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t t = perm[p];
+    lens[p] = static_cast<uint32_t>(toffs[t + 1] - toffs[t]);
+  }
+}
+
+// 16 lanes per topic, 16 topics per block; bytes beyond `cap` flag the call for a rerun with
+// a larger buffer (nothing is written then, and the match kernels skip the call).
+__global__ __launch_bounds__(256) void order_gather_kernel(const uint8_t* __restrict__ tbytes,
+                                                           const uint64_t* __restrict__ toffs,
+                                                           const uint32_t* __restrict__ perm, uint64_t n,
+                                                           const uint64_t* __restrict__ noffs,
+                                                           uint8_t* __restrict__ obytes, uint64_t cap,
+                                                           uint32_t* ctrl) {
+  if (noffs[n] > cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&ctrl[CTRL_ERROR], CTRL_ERR_ORDER_CAP);
+    return;
+  }
+  const uint32_t sub = threadIdx.x & 15u;
+  for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4; p < n;
+       p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 4) {
+    const uint32_t t = perm[p];
+    const uint64_t s = toffs[t], len = toffs[t + 1] - s, d = noffs[p];
+    for (uint64_t j = sub; j < len; j += 16) obytes[d + j] = tbytes[s + j];
+  }
+}
+
+__global__ __launch_bounds__(256) void order_counts_kernel(const uint32_t* __restrict__ counts,
+                                                           const uint32_t* __restrict__ perm, uint64_t n,
+                                                           uint32_t* __restrict__ corig) {
+  for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < n;
+       p += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    corig[perm[p]] = counts[p];
+}
+
+uint32_t grid_for(uint64_t n, uint32_t per_block) {
+  return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((n + per_block - 1) / per_block, 8192)));
+}
+
+}  // namespace
+
+// Scratch of the radix sort over n pairs on the top `sort_bits` key bits (the size depends on
+// the bit range, not only on n: fewer bits can take another algorithm).
+uint64_t order_sort_temp_bytes(uint64_t n, uint32_t sort_bits) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, static_cast<const uint64_t*>(nullptr),
+                                  static_cast<uint64_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
+                                  static_cast<uint32_t*>(nullptr), static_cast<size_t>(n), 0u, sort_bits);
+  return bytes;
+}
+
+hipError_t launch_order(const OrderArgs& o, hipStream_t s) {
+  if (o.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(order_key_kernel, dim3(grid_for(o.n, 256)), dim3(256), 0, s, o.tbytes, o.toffs, o.n, o.level_bits,
+                     o.sort_bits, o.keys, o.idx);
+  size_t tb = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, tb, o.keys, o.keys_out, o.idx, o.perm, static_cast<size_t>(o.n), 0u,
+                                  o.sort_bits, s);
+  if (tb > o.temp_bytes) return hipErrorInvalidValue;  // the caller sized the scratch for fewer bytes
+  hipError_t err = rocprim::radix_sort_pairs(o.temp, tb, o.keys, o.keys_out, o.idx, o.perm, static_cast<size_t>(o.n),
+                                             0u, o.sort_bits, s);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(order_len_kernel, dim3(grid_for(o.n, 256)), dim3(256), 0, s, o.toffs, o.perm, o.n, o.lens);
+  err = launch_scan(o.lens, o.n, o.noffs, o.partials, s);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(order_gather_kernel, dim3(grid_for(o.n, 16)), dim3(256), 0, s, o.tbytes, o.toffs, o.perm, o.n,
+                     o.noffs, o.obytes, o.cap_bytes, o.ctrl);
+  return hipGetLastError();
+}
+
+hipError_t launch_order_counts(const uint32_t* counts, const uint32_t* perm, uint64_t n, uint32_t* corig,
+                               hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(order_counts_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, counts, perm, n, corig);
+  return hipGetLastError();
+}
+
+}  // namespace emqx
