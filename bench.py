@@ -148,10 +148,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EMQX_BENCH_REHEARSE=1: rehearsal of the N-rank path on a box with fewer GPUs (ranks share
+    # devices round robin, gloo instead of RCCL); never used for a reported number
+    rehearse = os.environ.get("EMQX_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from emqx_amd import workloads as W
     from emqx_amd.engine import Engine, EngineError
@@ -222,7 +230,9 @@ def main():
     # Consecutive batches alternate over `--streams` HIP streams (own output buffers each), so
     # one batch's output assembly overlaps the next batch's match kernel.
     summ = torch.zeros((max(args.steps, 1), eng.SUMMARY_WORDS), dtype=torch.int64, device=dev)
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(args.streams - 1)]
+    # dedicated streams (not the null stream: the engine maps a null stream to its own one, so
+    # events recorded there would not follow the calls)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
     outs = [(d_off, d_ids)] + [(torch.empty_like(d_off), torch.empty_like(d_ids)) for _ in range(args.streams - 1)]
     for k in range(len(streams)):  # size each stream's workspace (a synchronous call learns its slab)
         eng.match_device(tb.data_ptr(), to.data_ptr(), n, outs[k][0].data_ptr(), outs[k][1].data_ptr(), cap,
@@ -242,6 +252,7 @@ def main():
         eng.match_device_async(tb.data_ptr(), to.data_ptr(), n, outs[j][0].data_ptr(), outs[j][1].data_ptr(), cap,
                                summ[k].data_ptr(), mode=args.mode, stream=streams[j].cuda_stream)
         evs[k].record(streams[j])
+    t_enq = time.perf_counter() - t_start  # host time to enqueue the steps (async calls)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -312,12 +323,15 @@ def main():
                    "n_filters": wl.n_filters, "batch_topics_per_gpu": n, "mode": ["routes", "trie", "trie_wildcard"][args.mode],
                    "parallelism": f"replicated table, topic stream split x{world}",
                    "walk_order": walk_order_desc(args, st)},
+        **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
+           if os.environ.get("EMQX_BENCH_REHEARSE") == "1" else {}),
         "evals_per_s": round(evals_all * args.steps / elapsed, 1),
         "matches_per_topic": round(nout_all / (n * world), 3),
         "evals_per_topic": round(evals_all / (n * world), 3),
         "call_ms_avg": round(float(np.mean(call_ms)), 4),
         "step_completion_gap_ms": {"p50": round(float(np.median(gaps)), 4) if gaps.size else None,
                                    "max": round(float(np.max(gaps)), 4) if gaps.size else None},
+        "host_enqueue_ms_per_step": round(1e3 * t_enq / max(args.steps, 1), 4),
         "roofline": roofline,
     }
 
@@ -644,7 +658,9 @@ def fanout_bench(args, rank, world, dev):
     # of one batch each, enqueued with no host synchronisation; consecutive batches alternate
     # over `--streams` HIP streams with their own buffers, so one batch's fan-out overlaps the
     # next batch's match kernel.  Every step writes both summaries; all must be complete.
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(args.streams - 1)]
+    # dedicated streams (not the null stream: the engine maps a null stream to its own one, so
+    # events recorded there would not follow the calls)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
     bufs = [(moff, mids, ooff, osubs, ofil)] + [tuple(torch.empty_like(t) for t in (moff, mids, ooff, osubs, ofil))
                                                 for _ in range(args.streams - 1)]
     msum = torch.zeros((max(args.steps, 1), eng.SUMMARY_WORDS), dtype=torch.int64, device=dev)

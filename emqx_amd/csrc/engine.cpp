@@ -211,6 +211,7 @@ struct emqx_engine {
   std::atomic<int> order_sort_bits{64};
   std::atomic<int> order_deal{1};
   std::atomic<uint64_t> last_ordered{0};
+  std::atomic<uint64_t> order_bpt{48};  // reordered-batch bytes per topic to provision (learnt)
   std::atomic<double> last_order_ms{0};
 };
 
@@ -470,7 +471,7 @@ bool use_order(const emqx_engine* e, const Snapshot& snap, uint64_t n) {
 
 // Walk-order buffers for n topics; the reordered bytes buffer keeps `cap_bytes` (grown by
 // run_match when a call reports CTRL_ERR_ORDER_CAP).
-int ensure_order(Workspace* w, uint64_t n, uint32_t sort_bits) {
+int ensure_order(emqx_engine* e, Workspace* w, uint64_t n, uint32_t sort_bits) {
   if (n > w->ord_cap_n) {
     const uint64_t cap = round_pow2(std::max<uint64_t>(n, 1024));
     HIP_TRY(dalloc(w->ord_keys, cap));
@@ -488,8 +489,9 @@ int ensure_order(Workspace* w, uint64_t n, uint32_t sort_bits) {
     HIP_TRY(dalloc(w->ord_temp, tb));
     w->ord_temp_bytes = tb;
   }
-  if (!w->ord_bytes || w->ord_cap_bytes < 48 * n + 4096) {
-    const uint64_t cap = std::max<uint64_t>(w->ord_cap_bytes, 48 * n + 4096);
+  const uint64_t want = e->order_bpt.load() * n + 4096;
+  if (!w->ord_bytes || w->ord_cap_bytes < want) {
+    const uint64_t cap = std::max<uint64_t>(w->ord_cap_bytes, want);
     HIP_TRY(dalloc(w->ord_bytes, cap + 16));
     w->ord_cap_bytes = cap;
   }
@@ -552,7 +554,7 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   const bool ordered = use_order(e, snap, n);
   const uint32_t sort_bits = static_cast<uint32_t>(std::min(64, std::max(1, e->order_sort_bits.load())));
   if (ordered) {
-    rc = ensure_order(w, n, sort_bits);
+    rc = ensure_order(e, w, n, sort_bits);
     if (rc != EMQX_OK) return rc;
   }
 
@@ -640,6 +642,10 @@ int run_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode,
         const uint64_t need = nb - nb0;
         w->ord_cap_bytes = need + need / 8 + 4096;
         HIP_TRY(dalloc(w->ord_bytes, w->ord_cap_bytes + 16));
+        const uint64_t bpt = (need + need / 8) / std::max<uint64_t>(n, 1) + 1;  // later workspaces start there
+        uint64_t h = e->order_bpt.load();
+        while (h < bpt && !e->order_bpt.compare_exchange_weak(h, bpt)) {
+        }
       }
       if (err & CTRL_ERR_TOO_DEEP) {
         if (w->deep_stack_cap >= (1u << 22)) {

@@ -1182,11 +1182,9 @@ __global__ __launch_bounds__(GROUP_TILES) void group_reduce_kernel(MatchArgs a, 
 // One wave per tile.  The tile's first output position is two short sums — the group sums
 // before its group and its group's tile sums before it — plus a wave scan of its 64 counts.
 // Then its slab entries, 64 at a time: lanes holding the same topic find each other with six
-// ballots (one per bit of the topic index), take ranks by popcount and the group's first
-// lane advances the topic's running count — no atomics.  Ids beyond out_cap are dropped.
+// ballots (one per bit of the topic index) and take ranks by popcount, and the same ballots
+// advance every topic's running position — no atomics.  Ids beyond out_cap are dropped.
 __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
-  __shared__ uint32_t run[4][64];
-  __shared__ uint64_t base[4][64];
   const uint32_t lane = lane_id();
   const uint32_t wv = threadIdx.x >> 6;
   const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4 + wv;
@@ -1207,32 +1205,47 @@ __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
     off = before + wave_incl_scan64(c, lane) - c;
     if (t < a.n) a.out_off[t] = off;
   }
-  base[wv][lane] = off;
-  run[wv][lane] = 0;
-  wave_sync();
+  // Lane L keeps topic L's next output position in a register.  Per round of 64 entries the
+  // six topic-bit ballots give each entry its rank among the round's entries of its topic and
+  // each lane its topic's count in the round; positions travel by cross-lane reads.  No LDS
+  // and no fence in the loop, so the id stores never hold the next round's loads back.
+  uint64_t next = off;
   const uint32_t fill = min(a.tile_fill[tile], a.slab_cap);
   const uint64_t dmask = a.tile_defer[tile];
   const uint64_t* slab = a.slab + tile * a.slab_cap;
   const uint64_t lt = lanemask_lt(lane);
-  for (uint32_t i0 = 0; i0 < fill; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    const uint64_t e = i < fill ? slab[i] : 0;
-    const uint32_t tl = static_cast<uint32_t>(e >> 32) & 63u;
-    const bool keep = i < fill && !((dmask >> tl) & 1ull);
-    uint64_t peers = __ballot(keep);
+  constexpr uint32_t U = 4;  // rounds whose slab loads and id lookups are in flight together
+  for (uint32_t i0 = 0; i0 < fill; i0 += 64 * U) {
+    uint64_t e[U];
+    uint32_t id[U];
 #pragma unroll
-    for (uint32_t bit = 0; bit < 6; ++bit) {
-      const uint64_t m = __ballot(keep && ((tl >> bit) & 1u));
-      peers &= ((tl >> bit) & 1u) ? m : ~m;
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + 64 * u + lane;
+      e[u] = i < fill ? slab[i] : ~0ull;
     }
-    const uint32_t rk = static_cast<uint32_t>(__popcll(peers & lt));
-    if (keep) {
-      const uint64_t p = base[wv][tl] + run[wv][tl] + rk;
-      if (p < a.out_cap) a.out_ids[p] = resolve_entry(a.tv, e);
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) id[u] = e[u] != ~0ull ? resolve_entry(a.tv, e[u]) : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t tl = static_cast<uint32_t>(e[u] >> 32) & 63u;
+      const bool keep = e[u] != ~0ull && !((dmask >> tl) & 1ull);
+      const uint64_t km = __ballot(keep);
+      uint64_t peers = km, mine = km;
+#pragma unroll
+      for (uint32_t bit = 0; bit < 6; ++bit) {
+        const uint64_t m = __ballot(keep && ((tl >> bit) & 1u));
+        peers &= ((tl >> bit) & 1u) ? m : ~m;
+        mine &= ((lane >> bit) & 1u) ? m : ~m;
+      }
+      const uint32_t rk = static_cast<uint32_t>(__popcll(peers & lt));
+      const uint32_t lo = __shfl(static_cast<uint32_t>(next), static_cast<int>(tl), 64);
+      const uint32_t hi = __shfl(static_cast<uint32_t>(next >> 32), static_cast<int>(tl), 64);
+      if (keep) {
+        const uint64_t p = ((static_cast<uint64_t>(hi) << 32) | lo) + rk;
+        if (p < a.out_cap) a.out_ids[p] = id[u];
+      }
+      next += static_cast<uint64_t>(__popcll(mine));
     }
-    wave_sync();
-    if (keep && rk == 0) run[wv][tl] += static_cast<uint32_t>(__popcll(peers));
-    wave_sync();
   }
 }
 

@@ -31,6 +31,17 @@ def main():
         if args.kernel in r["Name"]:
             out["avg_ns"] = float(r["AverageNs"])
             out["calls"] = int(r["Calls"])
+    # Launches that do no work (a call the engine reruns: e.g. the walk order's buffer-growth
+    # rerun, whose first fast kernel exits at once) would dilute the averages: per-launch
+    # numbers keep launches above 1 % of the median duration / counter total.
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            for r in rows(os.path.join(args.dir, "**", "*kernel_trace.csv")) if args.kernel in r["Kernel_Name"]]
+    if durs:
+        med = sorted(durs)[len(durs) // 2]
+        full = [d for d in durs if d >= 0.01 * med]
+        out["avg_ns"] = sum(full) / len(full)
+        out["calls"] = len(full)
+        out["calls_dropped_empty"] = len(durs) - len(full)
     per = defaultdict(lambda: defaultdict(float))  # (pass, dispatch) -> counter -> value
     for p in sorted(glob.glob(os.path.join(args.dir, "**", "*counter_collection.csv"), recursive=True)):
         with open(p, newline="") as f:
@@ -43,6 +54,9 @@ def main():
     for (p, d), cs in sorted(per.items()):
         by_pass[p].append(cs)
     for p, lst in by_pass.items():
+        tot = sorted(sum(cs.values()) for cs in lst)
+        med = tot[len(tot) // 2] if tot else 0
+        lst = [cs for cs in lst if sum(cs.values()) >= 0.01 * med]
         for cs in lst[args.skip:] or lst:
             for k, v in cs.items():
                 acc[k].append(v)
