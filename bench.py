@@ -263,12 +263,13 @@ def main():
         raise SystemExit(f"async steps incomplete or inconsistent: flags {set(sm[:, 0].tolist())}, "
                          f"totals {set(sm[:, 1].tolist())} vs {nout}")
     # kernel / call times from synchronous calls (HIP events on the engine's stream)
-    kern_ms, call_ms = [], []
+    kern_ms, call_ms, order_ms = [], [], []
     for _ in range(min(max(args.steps, 1), 10)):
         step()
         st = eng.stats()
         kern_ms.append(st["last_kernel_ms"])
         call_ms.append(st["last_match_ms"])
+        order_ms.append(st["last_order_ms"])
     evals = eng.stats()["last_evals"]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -329,6 +330,7 @@ def main():
         "matches_per_topic": round(nout_all / (n * world), 3),
         "evals_per_topic": round(evals_all / (n * world), 3),
         "call_ms_avg": round(float(np.mean(call_ms)), 4),
+        "order_ms_avg": round(float(np.mean(order_ms)), 4),
         "step_completion_gap_ms": {"p50": round(float(np.median(gaps)), 4) if gaps.size else None,
                                    "max": round(float(np.max(gaps)), 4) if gaps.size else None},
         "host_enqueue_ms_per_step": round(1e3 * t_enq / max(args.steps, 1), 4),

@@ -25,9 +25,10 @@ namespace emqx {
 
 namespace {
 
+template <class K>
 __global__ __launch_bounds__(256) void order_key_kernel(const uint8_t* __restrict__ tbytes,
                                                         const uint64_t* __restrict__ toffs, uint64_t n,
-                                                        uint32_t lbits, uint32_t sort_bits, uint64_t* __restrict__ keys,
+                                                        uint32_t lbits, uint32_t sort_bits, K* __restrict__ keys,
                                                         uint32_t* __restrict__ idx) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(256) void order_key_kernel(const uint8_t* __restric
         }
       }
     }
-    keys[i] = key >> (64u - sort_bits);  // the sort orders bits [0, sort_bits)
+    keys[i] = static_cast<K>(key >> (64u - sort_bits));  // the sort orders bits [0, sort_bits)
     idx[i] = static_cast<uint32_t>(i);
   }
 }
@@ -107,26 +108,35 @@ uint32_t grid_for(uint64_t n, uint32_t per_block) {
 
 }  // namespace
 
-// Scratch of the radix sort over n pairs on the top `sort_bits` key bits (the size depends on
-// the bit range, not only on n: fewer bits can take another algorithm).
+// Keys of at most 32 bits sort as u32 (rocprim's radix sort then runs its one-sweep passes
+// over half the bytes; 64-bit keys take its merge sort at these sizes).
+template <class K>
+hipError_t sort_pairs(void* temp, size_t& bytes, K* keys, K* keys_out, uint32_t* idx, uint32_t* perm, uint64_t n,
+                      uint32_t sort_bits, hipStream_t s) {
+  return rocprim::radix_sort_pairs(temp, bytes, keys, keys_out, idx, perm, static_cast<size_t>(n), 0u, sort_bits, s);
+}
+
+// Scratch of the radix sort over n pairs on `sort_bits` key bits (the size depends on the bit
+// range, not only on n: fewer bits can take another algorithm).
 uint64_t order_sort_temp_bytes(uint64_t n, uint32_t sort_bits) {
   size_t bytes = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, bytes, static_cast<const uint64_t*>(nullptr),
-                                  static_cast<uint64_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
-                                  static_cast<uint32_t*>(nullptr), static_cast<size_t>(n), 0u, sort_bits);
+  if (sort_bits <= 32)
+    (void)sort_pairs<uint32_t>(nullptr, bytes, nullptr, nullptr, nullptr, nullptr, n, sort_bits, nullptr);
+  else
+    (void)sort_pairs<uint64_t>(nullptr, bytes, nullptr, nullptr, nullptr, nullptr, n, sort_bits, nullptr);
   return bytes;
 }
 
-hipError_t launch_order(const OrderArgs& o, hipStream_t s) {
-  if (o.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(order_key_kernel, dim3(grid_for(o.n, 256)), dim3(256), 0, s, o.tbytes, o.toffs, o.n, o.level_bits,
-                     o.sort_bits, o.keys, o.idx);
+template <class K>
+hipError_t launch_order_t(const OrderArgs& o, hipStream_t s) {
+  K* keys = reinterpret_cast<K*>(o.keys);
+  K* keys_out = reinterpret_cast<K*>(o.keys_out);
+  hipLaunchKernelGGL(order_key_kernel<K>, dim3(grid_for(o.n, 256)), dim3(256), 0, s, o.tbytes, o.toffs, o.n,
+                     o.level_bits, o.sort_bits, keys, o.idx);
   size_t tb = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, tb, o.keys, o.keys_out, o.idx, o.perm, static_cast<size_t>(o.n), 0u,
-                                  o.sort_bits, s);
+  (void)sort_pairs<K>(nullptr, tb, keys, keys_out, o.idx, o.perm, o.n, o.sort_bits, s);
   if (tb > o.temp_bytes) return hipErrorInvalidValue;  // the caller sized the scratch for fewer bytes
-  hipError_t err = rocprim::radix_sort_pairs(o.temp, tb, o.keys, o.keys_out, o.idx, o.perm, static_cast<size_t>(o.n),
-                                             0u, o.sort_bits, s);
+  hipError_t err = sort_pairs<K>(o.temp, tb, keys, keys_out, o.idx, o.perm, o.n, o.sort_bits, s);
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(order_len_kernel, dim3(grid_for(o.n, 256)), dim3(256), 0, s, o.toffs, o.perm, o.n, o.lens);
   err = launch_scan(o.lens, o.n, o.noffs, o.partials, s);
@@ -134,6 +144,11 @@ hipError_t launch_order(const OrderArgs& o, hipStream_t s) {
   hipLaunchKernelGGL(order_gather_kernel, dim3(grid_for(o.n, 16)), dim3(256), 0, s, o.tbytes, o.toffs, o.perm, o.n,
                      o.noffs, o.obytes, o.cap_bytes, o.ctrl);
   return hipGetLastError();
+}
+
+hipError_t launch_order(const OrderArgs& o, hipStream_t s) {
+  if (o.n == 0) return hipSuccess;
+  return o.sort_bits <= 32 ? launch_order_t<uint32_t>(o, s) : launch_order_t<uint64_t>(o, s);
 }
 
 hipError_t launch_order_counts(const uint32_t* counts, const uint32_t* perm, uint64_t n, uint32_t* corig,
