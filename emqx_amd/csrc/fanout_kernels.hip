@@ -14,8 +14,8 @@
 //                and the call summary
 //   final        FO_BLOCKS blocks: per-entry output offsets (chunk scan + the chunk's base)
 //   offsets      per-topic output offsets = per-entry offsets at the match CSR boundaries
-//   write        one wavefront per 64 match entries: the wave walks its flattened outputs 64
-//                at a time (each lane finds its entry by a 6-step search over LDS prefix
+//   write        one wavefront per 256 match entries: the wave walks its flattened outputs 64
+//                at a time (each lane finds its entry by an 8-step search over LDS prefix
 //                offsets), so plain-subscriber copies are coalesced reads and writes; each
 //                $share group contributes exactly one pick.  Skipped entirely on overflow, so
 //                no pick state is consumed by a call that wrote nothing.
@@ -32,6 +32,7 @@ namespace {
 
 constexpr int FO_THREADS = 256;
 constexpr uint32_t FO_UNROLL = 4;  // outputs per lane per round of the write kernel
+constexpr uint32_t FO_WCHUNK = 256;  // match entries per wave chunk of the write kernel
 
 __device__ __forceinline__ uint32_t fo_lane() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -206,14 +207,15 @@ __device__ __forceinline__ uint32_t pick_member(const FanoutArgs& a, const Group
 
 __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) {
   struct WaveLds {
-    uint32_t pre[64];  // entry's first output, relative to the wave's first output
-    uint32_t fid[64];
-    uint32_t pb[64];
-    uint32_t np[64];
-    uint32_t gb[64];
-    uint32_t top[64];
+    uint32_t pre[FO_WCHUNK];  // entry's first output, relative to the chunk's first output
+    uint32_t fid[FO_WCHUNK];
+    uint32_t pb[FO_WCHUNK];
+    uint32_t np[FO_WCHUNK];
+    uint32_t gb[FO_WCHUNK];
+    uint32_t top[FO_WCHUNK];
   };
   __shared__ WaveLds lds_all[FO_THREADS / 64];
+  constexpr uint32_t EU = FO_WCHUNK / 64;  // entries per lane per chunk
   const uint32_t lane = fo_lane();
   const uint32_t wv = threadIdx.x >> 6;
   WaveLds& L = lds_all[wv];
@@ -222,23 +224,36 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
   if (a.eoff[m] > a.cap) return;  // overflow: nothing is written, no pick state consumed
   const bool need_topic = a.strategy == EMQX_SHARE_HASH_CLIENTID || a.strategy == EMQX_SHARE_HASH_TOPIC;
   const uint64_t nwaves = uint64_t(gridDim.x) * (FO_THREADS / 64);
-  for (uint64_t e0 = (uint64_t(blockIdx.x) * (FO_THREADS / 64) + wv) * 64; e0 < m; e0 += nwaves * 64) {
-    const uint64_t e1 = min<uint64_t>(e0 + 64, m);
+  for (uint64_t e0 = (uint64_t(blockIdx.x) * (FO_THREADS / 64) + wv) * FO_WCHUNK; e0 < m;
+       e0 += nwaves * FO_WCHUNK) {
+    const uint64_t e1 = min<uint64_t>(e0 + FO_WCHUNK, m);
     const uint64_t obase = a.eoff[e0];
     const uint32_t total = static_cast<uint32_t>(a.eoff[e1] - obase);
-    const uint64_t i = e0 + lane;
-    if (i < e1) {
-      const uint32_t f = a.mids[base + i];
-      uint4 r = make_uint4(0, 0, 0, 0);
-      if (f < a.n_recs) r = *reinterpret_cast<const uint4*>(a.recs + f);
-      L.pre[lane] = static_cast<uint32_t>(a.eoff[i] - obase);
-      L.fid[lane] = f;
-      L.pb[lane] = r.x;
-      L.np[lane] = r.y;
-      L.gb[lane] = r.z;
-      L.top[lane] = need_topic ? a.entry_topic[i] : 0u;
-    } else {
-      L.pre[lane] = total;  // never <= a valid output index
+    // the chunk's entries, EU per lane: every first-level load of the chunk is in flight
+    // before the filter records are fetched, and those before anything is stored to LDS
+    uint32_t f[EU], tp[EU];
+    uint64_t eo[EU];
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      const uint64_t i = e0 + lane + 64u * u;
+      const bool v = i < e1;
+      f[u] = v ? a.mids[base + i] : FID_NONE;
+      eo[u] = v ? a.eoff[i] : obase + total;
+      tp[u] = (v && need_topic) ? a.entry_topic[i] : 0u;
+    }
+    uint4 r[EU];
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u)
+      r[u] = f[u] < a.n_recs ? *reinterpret_cast<const uint4*>(a.recs + f[u]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      const uint32_t k = lane + 64u * u;
+      L.pre[k] = static_cast<uint32_t>(eo[u] - obase);  // past the chunk's end: `total`
+      L.fid[k] = f[u];
+      L.pb[k] = r[u].x;
+      L.np[k] = r[u].y;
+      L.gb[k] = r[u].z;
+      L.top[k] = tp[u];
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -251,11 +266,11 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
       for (uint32_t u = 0; u < FO_UNROLL; ++u) {
         const uint32_t j = j0 + lane + 64u * u;
         act[u] = j < total;
-        // largest k with pre[k] <= j (pre is non-decreasing, pre[0] = 0, unused lanes hold
-        // `total`); k + step never exceeds 63
+        // largest k with pre[k] <= j (pre is non-decreasing, pre[0] = 0, slots past the
+        // chunk's entries hold `total`); k + step never exceeds FO_WCHUNK - 1
         uint32_t k = 0;
 #pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1)
+        for (uint32_t step = FO_WCHUNK / 2; step >= 1; step >>= 1)
           if (L.pre[k + step] <= j) k += step;
         kk[u] = k;
         rr[u] = j - L.pre[k];
@@ -301,8 +316,9 @@ hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s) {
   hipLaunchKernelGGL(fanout_partials_kernel, dim3(1), dim3(FO_BLOCKS), 0, s, a);
   hipLaunchKernelGGL(fanout_final_kernel, dim3(FO_BLOCKS), dim3(FO_THREADS), 0, s, a);
   hipLaunchKernelGGL(fanout_offsets_kernel, dim3(grid_for(a.n + 1, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
-  // one wave per 64 entries up to m_cap (waves past m exit at once)
-  hipLaunchKernelGGL(fanout_write_kernel, dim3(grid_for(m_cap, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
+  // one wave per FO_WCHUNK entries up to m_cap (waves past m exit at once)
+  hipLaunchKernelGGL(fanout_write_kernel, dim3(grid_for(m_cap, FO_WCHUNK * (FO_THREADS / 64))), dim3(FO_THREADS), 0, s,
+                     a);
   return hipGetLastError();
 }
 
