@@ -356,14 +356,19 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
         while (j < fn && word_at(a, lwords, wb + j) == WID_PLUS) ++j;
         wl = j < fn ? word_at(a, lwords, wb + j) : WID_HASH;
       }
+      // A literal step needs only the edge bucket: a node without that child (a leaf
+      // included) has no key for it there, so its own fields are not loaded (one random line
+      // fewer per step of an exact filter).  Every other step reads them.
       if (q.z & RITEM_POST) {
         name = q.x + (lane - before);
-        const uint4 p = rv.posts[name];
-        rn = RNode{0, p.z, p.x, p.w};
+        if (w_cur >= WID_HASH) {
+          const uint4 p = rv.posts[name];
+          rn = RNode{0, p.z, p.x, p.w};
+        }
       } else {
         rn = RNode{0, rv.root_ncld, rv.root_lo, rv.root_hi};
       }
-      if (w_cur < WID_HASH) {  // a literal: its bucket, whether or not the node has children
+      if (w_cur < WID_HASH) {  // a literal: its bucket
         bk = redge_slot0(name, w_cur) & rv.edge_mask;
         const uint4* kp = reinterpret_cast<const uint4*>(rv.edges + bk);
         ka = kp[0];
@@ -432,9 +437,9 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
             pk = rv.pkeys[ps];
           }
         }
-      } else if (w_cur != WID_NONE && ncld != 0) {
-        // the bucket's four keys and child names came with the node; a bucket that overflowed
-        // (REDGE_OVF) continues in the next
+      } else if (w_cur < WID_HASH) {
+        // the bucket's four keys and child names; a bucket that overflowed (REDGE_OVF)
+        // continues in the next
         for (uint32_t k = 0; k <= rv.edge_mask; ++k) {
           const uint32_t hit = (ka.x == name && (ka.y & ~REDGE_OVF) == w_cur) ? kc.x
                                : (ka.z == name && ka.w == w_cur)             ? kc.y
