@@ -384,6 +384,38 @@ def test_sharded_matcher_world1_rccl(Engine):
     csr_equal(off.astype(np.uint64), ids, counts, oids)
 
 
+def test_sharded_matcher_config_c_generator(Engine):
+    """Config C's generator (BASELINE configs[2]: generator B, vocab x4, seed 3) through the
+    filter-sharded path on one GPU over RCCL, 1M filters and 20K topics, every topic compared
+    ID-for-ID with the oracle; the walk order forced on for the same batch gives the same CSR."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import workloads as W
+    from emqx_amd.dist import ShardedMatcher
+    wl = W.config_b(n_filters=1_000_000, n_topics=20_000, seed=3, vocab_scale=4)
+    dev = torch.device("cuda:0")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = "29543"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        sm = ShardedMatcher(wl.filters, device=dev)
+        topics = (torch.from_numpy(wl.topics[0]).to(dev), torch.from_numpy(wl.topics[1].view(np.int64)).to(dev))
+        off, ids = sm.match(topics)
+        off, ids = off.cpu().numpy(), ids.cpu().numpy().view(np.uint32)
+        sm.engine.set_tuning("order", 1)
+        off2, ids2 = sm.match(topics)
+        off2, ids2 = off2.cpu().numpy(), ids2.cpu().numpy().view(np.uint32)
+    finally:
+        dist.destroy_process_group()
+    o = C.CppOracle(True)
+    o.add_packed(*wl.filters)
+    off_o, ids_o, _ = o.match_csr(*wl.topics, mode=C.MODE_ROUTES, threads=8)
+    for a, b in ((off, ids), (off2, ids2)):
+        bad = C.csr_mismatches(a.astype(np.uint64), b, off_o, ids_o)
+        assert bad.size == 0, bad[:10]
+
+
 def test_batcher_coalesces_concurrent_callers(Engine):
     """Concurrent single-topic callers (one PUBLISH each, as emqx_broker:publish/1 calls
     match_routes/1) get exactly their own results, in batches larger than one."""
