@@ -334,6 +334,7 @@ def main():
         "step_completion_gap_ms": {"p50": round(float(np.median(gaps)), 4) if gaps.size else None,
                                    "max": round(float(np.max(gaps)), 4) if gaps.size else None},
         "host_enqueue_ms_per_step": round(1e3 * t_enq / max(args.steps, 1), 4),
+        "step_gaps_ms": [round(float(g), 3) for g in gaps] if args.steps <= 64 else None,
         "roofline": roofline,
     }
 
