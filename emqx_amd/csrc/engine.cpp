@@ -464,6 +464,7 @@ int ensure_ws(Workspace* w, uint64_t n) {
 constexpr uint64_t ORDER_MIN_N = 65536;
 
 bool use_order(const emqx_engine* e, const Snapshot& snap, uint64_t n) {
+  if (n > 0xFFFFFFFFull) return false;  // batch positions are 32-bit
   const int o = e->order.load();
   if (o >= 0) return o > 0 && n > 0;
   return snap.max_depth > 12 && n >= ORDER_MIN_N;

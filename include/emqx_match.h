@@ -89,8 +89,9 @@ typedef struct emqx_stats {
   uint64_t delta_filters;    /* filters placed by incremental commits since the last full build */
   uint64_t last_commit_kind; /* 0 = full rebuild, 1 = incremental (patched in place)          */
   uint64_t max_depth;        /* levels of the deepest filter in the committed snapshot       */
-  uint64_t last_ordered;     /* 1 if the last match call walked its batch in prefix-key order
-                              * (emqx_set_tuning "order"; the CSR is in the caller's order)  */
+  uint64_t last_ordered;     /* 1 if the last synchronous match call walked its batch in
+                              * prefix-key order (emqx_set_tuning "order"; the CSR is in the
+                              * caller's order either way)                                   */
   double last_order_ms;      /* device time of that call's reordering (keys, sort, gather)   */
 } emqx_stats;
 
