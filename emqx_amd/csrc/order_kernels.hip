@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void order_key_kernel(const uint8_t* __restric
                                                         uint32_t* __restrict__ idx) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint64_t s = toffs[i], e = toffs[i + 1];
+    const uint64_t s = toffs[i], e = toffs[i + 1], lim = toffs[n];
     uint64_t key = 0;
     uint32_t room = 64, h = 0x811C9DC5u;
     // the topic's bytes in 16-B aligned windows (a window holding a topic byte lies inside the
@@ -40,8 +40,17 @@ __global__ __launch_bounds__(256) void order_key_kernel(const uint8_t* __restric
     const uintptr_t a0 = reinterpret_cast<uintptr_t>(tbytes + s) & ~static_cast<uintptr_t>(15);
     const uintptr_t aend = reinterpret_cast<uintptr_t>(tbytes + e);
     const uintptr_t abeg = reinterpret_cast<uintptr_t>(tbytes + s);
+    const uintptr_t alim = reinterpret_cast<uintptr_t>(tbytes + lim);  // bytes below are readable
     for (uintptr_t c0 = a0; c0 <= aend && room; c0 += 16) {
-      const uint4 v = c0 < aend ? *reinterpret_cast<const uint4*>(c0) : make_uint4(0, 0, 0, 0);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (c0 + 16 <= alim) {
+        v = *reinterpret_cast<const uint4*>(c0);
+      } else if (c0 < aend) {  // the batch's last window: only its readable bytes
+        uint32_t t4[4] = {0, 0, 0, 0};
+        for (uint32_t b = 0; b < 16 && c0 + b < alim; ++b)
+          t4[b >> 2] |= static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(c0 + b)) << (8u * (b & 3u));
+        v = make_uint4(t4[0], t4[1], t4[2], t4[3]);
+      }
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (uint32_t b = 0; b < 16; ++b) {
