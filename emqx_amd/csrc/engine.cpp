@@ -235,6 +235,7 @@ int full_commit(emqx_engine* e) {
   o.vocab = vs.get();
   o.fid_loc = &loc;
   o.slot_ids = &slot_ids;
+  o.threads = e->commit_threads;
   HostTables ht;
   std::string err;
   if (!build_tables(e->store, o, ht, &err)) {

@@ -50,6 +50,7 @@ void full_build(emqx_htrie* h) {
   o.vocab = h->vocab.get();
   o.fid_loc = &loc;
   o.slot_ids = &sids;
+  o.threads = h->threads;
   HostTables ht;
   std::string err;
   build_tables(h->fs, o, ht, &err);

@@ -12,6 +12,9 @@
 #include "tables.h"
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -79,6 +82,11 @@ class EdgeMap {
       if (keys_[i] != EMPTY) f(keys_[i], vals_[i]);
   }
   uint64_t size() const { return size_; }
+  void swap_into(EdgeMap& o) {  // o takes this (empty) map's state: frees o's memory
+    keys_.swap(o.keys_);
+    vals_.swap(o.vals_);
+    std::swap(size_, o.size_);
+  }
 
  private:
   void rehash(uint64_t cap) {
@@ -101,6 +109,30 @@ class EdgeMap {
   std::vector<uint32_t> vals_;
   uint64_t size_ = 0;
 };
+
+// fn(begin, end, thread) over [0, n) in chunks taken first come, first served by `threads`
+// host threads (the calling thread is one of them).  The per-node passes of build_tables write
+// disjoint per-node state, so they need no other synchronisation.
+template <class F>
+void parallel_chunks(uint64_t n, int threads, uint64_t chunk, F&& fn) {
+  const int t = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(threads, (n + chunk - 1) / chunk)));
+  if (t <= 1) {
+    if (n) fn(0, n, 0);
+    return;
+  }
+  std::atomic<uint64_t> next{0};
+  auto run = [&](int k) {
+    for (;;) {
+      const uint64_t b = next.fetch_add(chunk);
+      if (b >= n) return;
+      fn(b, std::min(n, b + chunk), k);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < t; ++k) th.emplace_back(run, k);
+  run(0);
+  for (auto& x : th) x.join();
+}
 
 }  // namespace
 
@@ -233,102 +265,227 @@ uint32_t FilterStore::insert(const uint8_t* p, uint64_t n, bool* created) {
 
 bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out, std::string* err) {
   // ---- pass 1: intern words, build the level trie (old node ids) -----------------
+  // Filters are partitioned by their first level's bytes, so no two partitions create the
+  // same edge (the root's edges are split by word, everything below hangs off one of them).
+  // Each partition builds its own sub-trie with its own interner on its own thread; the
+  // merge renumbers nodes (root shared, then partition after partition) and maps each
+  // partition's words to the global interner in partition order.  One partition (few
+  // filters or one thread) interns into the global interner directly.
   VocabState own;
   VocabState& vb = opts.vocab ? *opts.vocab : own;
   vb.map.reserve(1024);
-  EdgeMap em;
   const uint64_t n_sel = opts.ids ? opts.ids->size() : fs.n_live;
-  em.reserve(n_sel * 2 + 16);
-  std::vector<uint32_t> depth{0}, n_edges{0};
-  std::vector<uint8_t> has_plus{0}, term_wild{0};
-  std::vector<uint32_t> hash_fid{FID_NONE}, term_fid{FID_NONE};
-  std::vector<uint32_t> hash_id{WID_NONE}, term_id{WID_NONE};  // engine ids (fid_loc)
-  uint32_t max_depth = 0;
-
+  const int nthreads = std::max(1, opts.threads);
   const uint64_t n_ids = fs.n_ids();
   const uint64_t n_iter = opts.ids ? opts.ids->size() : n_ids;
+  const uint32_t nparts = n_sel >= 200000 ? static_cast<uint32_t>(std::min(nthreads, 64)) : 1u;
+
+  struct Part {
+    VocabState lv;  // partition interner (nparts > 1)
+    EdgeMap em;
+    std::vector<uint32_t> ids;
+    std::vector<uint32_t> depth{0}, n_edges{0}, hash_fid{FID_NONE}, term_fid{FID_NONE};
+    std::vector<uint32_t> hash_id{WID_NONE}, term_id{WID_NONE}, parent_of{0}, wid_of{WID_NONE};
+    std::vector<uint8_t> has_plus{0}, term_wild{0};
+    uint32_t max_depth = 0;
+    bool too_many = false;
+  };
+  std::vector<Part> parts(nparts);
   for (uint64_t k = 0; k < n_iter; ++k) {
     const uint64_t id = opts.ids ? (*opts.ids)[k] : k;
     if (id >= n_ids || !fs.live[id]) continue;
-    const uint8_t* p = fs.bytes.data() + fs.off[id];
-    const uint64_t n = fs.off[id + 1] - fs.off[id];
-    // wildcard? (emqx_topic:wildcard/1)
-    bool wild = false;
-    {
+    uint32_t pt = 0;
+    if (nparts > 1) {
+      const uint8_t* p = fs.bytes.data() + fs.off[id];
+      const uint64_t n = fs.off[id + 1] - fs.off[id];
+      uint64_t e = 0;
+      while (e < n && p[e] != '/') ++e;
+      pt = static_cast<uint32_t>(hash64_bytes(p, e) % nparts);
+    }
+    parts[pt].ids.push_back(static_cast<uint32_t>(id));
+  }
+  auto insert_part = [&](Part& P, VocabState& iv) {
+    P.lv.map.reserve(1024);
+    P.em.reserve(P.ids.size() * 2 + 16);
+    for (uint32_t id : P.ids) {
+      const uint8_t* p = fs.bytes.data() + fs.off[id];
+      const uint64_t n = fs.off[id + 1] - fs.off[id];
+      // wildcard? (emqx_topic:wildcard/1)
+      bool wild = false;
+      {
+        uint64_t s = 0;
+        for (uint64_t i = 0; i <= n; ++i) {
+          if (i == n || p[i] == '/') {
+            if (i - s == 1 && (p[s] == '+' || p[s] == '#')) wild = true;
+            s = i + 1;
+          }
+        }
+      }
+      uint32_t node = 0;
+      bool ended_hash = false;
       uint64_t s = 0;
       for (uint64_t i = 0; i <= n; ++i) {
-        if (i == n || p[i] == '/') {
-          if (i - s == 1 && (p[s] == '+' || p[s] == '#')) wild = true;
-          s = i + 1;
+        if (i != n && p[i] != '/') continue;
+        const uint64_t len = i - s;
+        uint32_t wid;
+        if (len == 1 && p[s] == '+') {
+          wid = WID_PLUS;
+        } else if (len == 1 && p[s] == '#') {
+          if (i == n) {  // final '#': the parent level's hash filter
+            P.hash_fid[node] = fs.ext[id];
+            P.hash_id[node] = id;
+            ended_hash = true;
+            break;
+          }
+          wid = WID_HASH;
+        } else {
+          wid = iv.intern(p + s, len);
         }
+        const uint64_t key = (uint64_t(node) << 32) | wid;
+        bool inserted = false;
+        const uint32_t next_id = static_cast<uint32_t>(P.depth.size());
+        const uint32_t child = P.em.get_or_insert(key, next_id, &inserted);
+        if (inserted) {
+          if (P.depth.size() >= 0xFFFFFFF0u / nparts) {
+            P.too_many = true;
+            return;
+          }
+          P.depth.push_back(P.depth[node] + 1);
+          P.max_depth = std::max(P.max_depth, P.depth[node] + 1);
+          P.n_edges.push_back(0);
+          P.has_plus.push_back(0);
+          P.term_wild.push_back(0);
+          P.hash_fid.push_back(FID_NONE);
+          P.term_fid.push_back(FID_NONE);
+          P.hash_id.push_back(WID_NONE);
+          P.term_id.push_back(WID_NONE);
+          P.parent_of.push_back(node);
+          P.wid_of.push_back(wid);
+          P.n_edges[node] += 1;
+          if (wid == WID_PLUS) P.has_plus[node] = 1;
+        }
+        node = child;
+        s = i + 1;
+      }
+      if (!ended_hash) {
+        P.term_fid[node] = fs.ext[id];
+        P.term_id[node] = id;
+        P.term_wild[node] = wild ? 1 : 0;
       }
     }
-    uint32_t node = 0;
-    bool ended_hash = false;
-    uint64_t s = 0;
-    for (uint64_t i = 0; i <= n; ++i) {
-      if (i != n && p[i] != '/') continue;
-      const uint64_t len = i - s;
-      uint32_t wid;
-      if (len == 1 && p[s] == '+') {
-        wid = WID_PLUS;
-      } else if (len == 1 && p[s] == '#') {
-        if (i == n) {  // final '#': the parent level's hash filter
-          hash_fid[node] = fs.ext[id];
-          hash_id[node] = static_cast<uint32_t>(id);
-          ended_hash = true;
-          break;
-        }
-        wid = WID_HASH;
-      } else {
-        wid = vb.intern(p + s, len);
-      }
-      const uint64_t key = (uint64_t(node) << 32) | wid;
-      bool inserted = false;
-      const uint32_t next_id = static_cast<uint32_t>(depth.size());
-      const uint32_t child = em.get_or_insert(key, next_id, &inserted);
-      if (inserted) {
-        if (depth.size() >= 0xFFFFFFF0u) {
-          if (err) *err = "too many trie nodes";
-          return false;
-        }
-        depth.push_back(depth[node] + 1);
-        max_depth = std::max(max_depth, depth[node] + 1);
-        n_edges.push_back(0);
-        has_plus.push_back(0);
-        term_wild.push_back(0);
-        hash_fid.push_back(FID_NONE);
-        term_fid.push_back(FID_NONE);
-        hash_id.push_back(WID_NONE);
-        term_id.push_back(WID_NONE);
-        n_edges[node] += 1;
-        if (wid == WID_PLUS) has_plus[node] = 1;
-      }
-      node = child;
-      s = i + 1;
+    EdgeMap().swap_into(P.em);  // the edge map is not needed past pass 1
+  };
+  if (nparts == 1) {
+    insert_part(parts[0], vb);
+  } else {
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nparts; ++t) th.emplace_back([&, t] { insert_part(parts[t], parts[t].lv); });
+    insert_part(parts[0], parts[0].lv);
+    for (auto& x : th) x.join();
+  }
+  uint64_t total_nodes = 1;
+  for (const Part& P : parts) {
+    if (P.too_many) {
+      if (err) *err = "too many trie nodes";
+      return false;
     }
-    if (!ended_hash) {
-      term_fid[node] = fs.ext[id];
-      term_id[node] = static_cast<uint32_t>(id);
-      term_wild[node] = wild ? 1 : 0;
+    total_nodes += P.depth.size() - 1;
+  }
+  if (total_nodes >= 0xFFFFFFF0u) {
+    if (err) *err = "too many trie nodes";
+    return false;
+  }
+  std::vector<uint32_t> depth, n_edges, hash_fid, term_fid, hash_id, term_id, parent_of, wid_of;
+  std::vector<uint8_t> has_plus, term_wild;
+  uint32_t max_depth = 0;
+  if (nparts == 1) {
+    Part& P = parts[0];
+    depth.swap(P.depth);
+    n_edges.swap(P.n_edges);
+    hash_fid.swap(P.hash_fid);
+    term_fid.swap(P.term_fid);
+    hash_id.swap(P.hash_id);
+    term_id.swap(P.term_id);
+    parent_of.swap(P.parent_of);
+    wid_of.swap(P.wid_of);
+    has_plus.swap(P.has_plus);
+    term_wild.swap(P.term_wild);
+    max_depth = P.max_depth;
+  } else {
+    // global word ids of each partition's words, partition after partition
+    std::vector<std::vector<uint32_t>> gw(nparts);
+    for (uint32_t t = 0; t < nparts; ++t) {
+      const VocabState& lv = parts[t].lv;
+      gw[t].resize(lv.n_words());
+      for (uint64_t w = 0; w < lv.n_words(); ++w)
+        gw[t][w] = vb.intern(lv.arena.data() + lv.off[w], lv.off[w + 1] - lv.off[w]);
     }
+    std::vector<uint64_t> base(nparts + 1, 1);
+    for (uint32_t t = 0; t < nparts; ++t) base[t + 1] = base[t] + parts[t].depth.size() - 1;
+    depth.assign(total_nodes, 0);
+    n_edges.assign(total_nodes, 0);
+    hash_fid.assign(total_nodes, FID_NONE);
+    term_fid.assign(total_nodes, FID_NONE);
+    hash_id.assign(total_nodes, WID_NONE);
+    term_id.assign(total_nodes, WID_NONE);
+    parent_of.assign(total_nodes, 0);
+    wid_of.assign(total_nodes, WID_NONE);
+    has_plus.assign(total_nodes, 0);
+    term_wild.assign(total_nodes, 0);
+    // the root's fields, then every partition's nodes into its own range (in parallel)
+    for (const Part& P : parts) {
+      n_edges[0] += P.n_edges[0];
+      has_plus[0] |= P.has_plus[0];
+      if (P.hash_fid[0] != FID_NONE) {
+        hash_fid[0] = P.hash_fid[0];
+        hash_id[0] = P.hash_id[0];
+      }
+      max_depth = std::max(max_depth, P.max_depth);
+    }
+    std::vector<std::thread> th;
+    auto copy_part = [&](uint32_t t) {
+      Part& P = parts[t];
+      const uint64_t b = base[t];
+      for (uint64_t l = 1; l < P.depth.size(); ++l) {
+        const uint64_t g = b + l - 1;
+        depth[g] = P.depth[l];
+        n_edges[g] = P.n_edges[l];
+        hash_fid[g] = P.hash_fid[l];
+        term_fid[g] = P.term_fid[l];
+        hash_id[g] = P.hash_id[l];
+        term_id[g] = P.term_id[l];
+        has_plus[g] = P.has_plus[l];
+        term_wild[g] = P.term_wild[l];
+        const uint32_t pp = P.parent_of[l];
+        parent_of[g] = pp ? static_cast<uint32_t>(b + pp - 1) : 0u;
+        const uint32_t w = P.wid_of[l];
+        wid_of[g] = w < WID_HASH ? gw[t][w] : w;
+      }
+      P = Part();  // free the partition
+    };
+    for (uint32_t t = 1; t < nparts; ++t) th.emplace_back(copy_part, t);
+    copy_part(0);
+    for (auto& x : th) x.join();
   }
 
   // ---- pass 2: per-node child lists -----------------------------------------------
+  // (children in creation order: one linear pass over the nodes' in-edges, not two scans of
+  // the edge hash map)
   const uint64_t n_nodes = depth.size();
   std::vector<uint64_t> coff(n_nodes + 1, 0);
-  em.for_each([&](uint64_t key, uint32_t) { coff[(key >> 32) + 1] += 1; });
-  for (uint64_t v = 0; v < n_nodes; ++v) coff[v + 1] += coff[v];
+  for (uint64_t v = 0; v < n_nodes; ++v) coff[v + 1] = coff[v] + n_edges[v];
   std::vector<uint32_t> cwid(coff[n_nodes]), cid(coff[n_nodes]);
   {
     std::vector<uint64_t> fillp(coff.begin(), coff.end() - 1);
-    em.for_each([&](uint64_t key, uint32_t child) {
-      const uint64_t p = key >> 32;
-      cwid[fillp[p]] = static_cast<uint32_t>(key);
-      cid[fillp[p]] = child;
+    for (uint64_t c = 1; c < n_nodes; ++c) {
+      const uint32_t p = parent_of[c];
+      cwid[fillp[p]] = wid_of[c];
+      cid[fillp[p]] = static_cast<uint32_t>(c);
       fillp[p] += 1;
-    });
+    }
   }
+  std::vector<uint32_t>().swap(parent_of);
+  std::vector<uint32_t>().swap(wid_of);
 
   // A node with a '+' edge keeps it in slot 0.  (Replicating it at the head of every 128-B
   // line of a wide array, so that '+' and the literal probe share a line, cut L2 misses by
@@ -339,7 +496,6 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
   // Bucketed placement of node v's literal edges (2-slot buckets, two candidate buckets,
   // random-walk eviction) for one seed; false when some word cannot be placed.  The '+'
   // slots stay free.  Afterwards every word outside its primary bucket flags that bucket.
-  std::vector<uint32_t> ck_key, ck_child;
   auto bucket_place = [&](uint64_t v, uint32_t sd, uint32_t cap, std::vector<uint32_t>& key_out,
                           std::vector<uint32_t>& child_out) -> bool {
     const uint32_t nbm = cap / 2 - 1;
@@ -377,8 +533,12 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
   // ---- pass 3: hashing per node — perfect hash (seed search) or 2-slot buckets ---------
   std::vector<uint32_t> caplog(n_nodes, 0), seed(n_nodes, 0);
   std::vector<uint8_t> ph(n_nodes, 0);
-  std::vector<uint32_t> slots_tmp;
-  for (uint64_t v = 0; v < n_nodes; ++v) {
+  std::atomic<bool> failed{false};
+  std::string fail_msg;
+  std::mutex fail_mu;
+  parallel_chunks(n_nodes, nthreads, 1 << 14, [&](uint64_t v0, uint64_t v1, int) {
+  std::vector<uint32_t> slots_tmp, ck_key, ck_child;
+  for (uint64_t v = v0; v < v1; ++v) {
     const uint32_t e = n_edges[v];
     if (!e) continue;
     const uint32_t n_lit = e - (has_plus[v] ? 1u : 0u);
@@ -416,10 +576,17 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
         if (ok) seed[v] = sd;
       }
       if (!ok) {
-        if (err) *err = "bucket placement failed for a node with " + std::to_string(e) + " edges";
-        return false;
+        std::lock_guard<std::mutex> g(fail_mu);
+        fail_msg = "bucket placement failed for a node with " + std::to_string(e) + " edges";
+        failed = true;
+        return;
       }
     }
+  }
+  });
+  if (failed) {
+    if (err) *err = fail_msg;
+    return false;
   }
 
   // ---- pass 4: layout — line-packed preorder ----------------------------------------
@@ -493,7 +660,8 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
   }
   // literal-edge filter of each node (stored in the slot that leads to it)
   std::vector<uint32_t> lf(n_nodes, 0), lf_flag(n_nodes, 0);
-  for (uint64_t v = 0; v < n_nodes; ++v) {
+  parallel_chunks(n_nodes, nthreads, 1 << 16, [&](uint64_t v0, uint64_t v1, int) {
+  for (uint64_t v = v0; v < v1; ++v) {
     uint32_t n_lit = 0, only = WID_NONE, bloom = 0;
     for (uint64_t j = coff[v]; j < coff[v + 1]; ++j) {
       if (cwid[j] == WID_PLUS) continue;
@@ -511,6 +679,7 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       lf[v] = n_lit <= LITF_BLOOM_MAX ? bloom : ~0u;
     }
   }
+  });
   // A child with edges and exactly one filter id carries it in litf (META_XFID), so its
   // emission needs no fids[] reference; its literal filter moves to 8 bits of the meta: the
   // fingerprint of its only literal word, or an 8-bit Bloom mask.  (EMQX_XFID=0, A/B runs:
@@ -520,7 +689,8 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       const char* v = getenv("EMQX_XFID");
       return v && std::strcmp(v, "0") == 0;
     }();
-    for (uint64_t v = 1; v < n_nodes; ++v) {
+    parallel_chunks(n_nodes, nthreads, 1 << 16, [&](uint64_t v0, uint64_t v1, int) {
+    for (uint64_t v = std::max<uint64_t>(v0, 1); v < v1; ++v) {
       if (!n_edges[v]) continue;
       const bool h = hash_fid[v] != FID_NONE, t = term_fid[v] != FID_NONE;
       if (h == t) continue;
@@ -541,6 +711,7 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       lf_flag[v] |= META_XFID | (t ? META_XFID_TERM : 0u) | (f8 << META_F8_SHIFT);
       lf[v] = t ? term_fid[v] : hash_fid[v];
     }
+    });
   }
   auto meta_of = [&](uint32_t v) -> uint32_t {
     uint32_t m = caplog[v] & META_CAPLOG2_MASK;
@@ -579,7 +750,10 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       (*opts.slot_ids)[2 * at + 1] = term_id[child];
     }
   };
-  for (uint64_t v = 0; v < n_nodes; ++v) {
+  // every node writes only its own array's slots and its children's ids: nodes in parallel
+  parallel_chunks(n_nodes, nthreads, 1 << 14, [&](uint64_t v0, uint64_t v1, int) {
+  std::vector<uint32_t> ck_key, ck_child;
+  for (uint64_t v = v0; v < v1; ++v) {
     if (!n_edges[v]) continue;
     // '+' is pinned at slot 0
     for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
@@ -605,6 +779,7 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       if (i / 2 != b1) out.edges[base[v] + 2 * b1].meta |= META_BUCKET_OVF;
     }
   }
+  });
   out.root_hash_fid = hash_fid[0];
   if (opts.fid_loc && hash_id[0] != WID_NONE) (*opts.fid_loc)[hash_id[0]] = FIDLOC_ROOT_HASH;
   out.root_base = off0 + base[0];

@@ -96,6 +96,7 @@ struct BuildOpts {
   bool vocab_table = true;                     // build the vocab table into HostTables
   std::vector<uint64_t>* fid_loc = nullptr;    // out: per filter id (sized n_ids)
   std::vector<uint32_t>* slot_ids = nullptr;   // out: per slot, the engine ids {hash, term} (2 per slot)
+  int threads = 1;                             // host threads for the per-node passes
 };
 
 struct HostTables {

@@ -258,3 +258,40 @@ def test_threaded_commits_equal_oracle():
     off_g = np.concatenate([[0], np.cumsum([len(g) for g in outs[1]])])
     ids_g = np.array([x for g in outs[1] for x in g], dtype=np.uint32)
     assert C.csr_mismatches(off_g, ids_g, off_o, ids_o).size == 0
+
+
+def test_partitioned_build_equals_single_thread_build():
+    """A full build of >= 200K filters runs its trie pass in partitions by first level on
+    several threads (tables.cpp build_tables); its table must answer exactly like the
+    one-partition build, pass the lookup self-check, and survive incremental commits on top.
+    Checked against the C++ oracle on a config-B sample (emqx_trie.erl:315-334 semantics)."""
+    from emqx_amd import workloads as W
+    from oracle import cpp as C
+    b = W.config_b(n_filters=240_000, n_topics=3000, seed=21)
+    fl = W.unpack(b.filters)
+    topics = W.unpack(b.topics) + [b"", b"/", b"#", b"+/x"]
+    one, many = HostTrie(threads=1), HostTrie(threads=6)
+    for t in (one, many):
+        t.insert(fl)
+        t.commit(full=True)
+        t.check()
+    o = C.CppOracle(True)
+    o.add_packed(*b.filters)
+    tb, to = pack(topics)
+    off_o, ids_o, _ = o.match_csr(tb, to, mode=C.MODE_ROUTES, threads=4)
+    want = [sorted(ids_o[off_o[i]:off_o[i + 1]].tolist()) for i in range(len(topics))]
+    for mode in (0, 2):
+        a, m = one.match(topics, mode=mode), many.match(topics, mode=mode)
+        assert a == m, mode
+        if mode == 0:
+            assert a == want
+    # incremental commits patched into the partitioned build answer like a full rebuild
+    rng = random.Random(3)
+    extra = [b"zz%d/" % k + rand_filter(rng) for k in range(400)]
+    sample = [rand_topic(rng) for _ in range(200)] + [b"zz%d/a/b" % k for k in range(0, 400, 7)]
+    for t, full in ((many, False), (one, True)):
+        ids = t.insert(extra)
+        t.delete(ids[:50])
+        t.commit(full=full)
+        t.check()
+    assert many.match(sample, mode=0) == one.match(sample, mode=0)
