@@ -121,7 +121,7 @@ def main():
     ap.add_argument("--vocab-scale", type=int, default=1, help="4 = config C's vocabulary")
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the timed batches alternate over (pipelined calls; default 3, "
-                         "--workload A: 1, see DESIGN.md §5)")
+                         "see DESIGN.md §5)")
     ap.add_argument("--order", type=str, default="none", choices=["none", "sorted", "xcd"],
                     help="experiment: host-side permutation of the topic batch (sorted = lexicographic; "
                          "xcd = sorted, cut into 8 key-range segments, dealt 256 topics at a time so each "
@@ -138,7 +138,7 @@ def main():
     if args.batch is None:
         args.batch = D_BATCH if args.workload == "D" else 1_000_000
     if args.streams is None:
-        args.streams = 1 if args.workload == "A" else 3
+        args.streams = 3
     if args.cpu_sample is None:
         args.cpu_sample = {"D": 40_000}.get(args.workload, 1_000_000)
 
