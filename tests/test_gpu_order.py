@@ -139,3 +139,44 @@ def test_order_tuning_keys_validate(Engine):
     for key, bad in (("order", 2), ("order_level_bits", 33), ("order_sort_bits", 0)):
         with pytest.raises(EngineError):
             e.set_tuning(key, bad)
+
+
+def test_order_concurrent_callers(Engine):
+    """Several host threads matching through one engine with the walk order forced on: each
+    call reorders in its own workspace, and every caller gets the unordered walk's CSR."""
+    import threading
+    from emqx_amd import workloads as W
+    d = W.config_d(n_filters=20_000, n_topics=16_000, seed=8)
+    e = Engine()
+    e.insert_packed(*d.filters)
+    e.commit()
+    tb, to = d.topics
+    n = len(to) - 1
+    slices = [(k * n // 4, (k + 1) * n // 4) for k in range(4)]
+
+    def part(lo, hi):
+        o = (to[lo:hi + 1] - to[lo]).astype(np.uint64)
+        return tb[int(to[lo]):int(to[hi])].copy(), o
+
+    e.set_tuning("order", 0)
+    want = [e.match_packed(*part(lo, hi), mode=0) for lo, hi in slices]
+    e.set_tuning("order", 1)
+    got = [None] * 4
+    errs = []
+
+    def run(k):
+        try:
+            for _ in range(3):
+                got[k] = e.match_packed(*part(*slices[k]), mode=0)
+        except Exception as x:  # surfaced below
+            errs.append(x)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    e.set_tuning("order", -1)
+    assert not errs, errs
+    for w, g in zip(want, got):
+        same_csr(w, g)
