@@ -40,7 +40,9 @@ EXPORTS = (
     "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
     "emqx_host_batch_create", "emqx_host_batch_destroy", "emqx_host_batch_reserve", "emqx_host_batch_submit",
     "emqx_host_batch_wait", "emqx_host_batch_query",
-    "emqx_commit_stats", "emqx_shard_owner", "emqx_shard_owner_device", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
+    "emqx_commit_stats", "emqx_shard_owner", "emqx_shard_owner_device", "emqx_permute_scratch_bytes", "emqx_batch_permute_device", "emqx_owner_sort_scratch_bytes",
+    "emqx_owner_sort_device",
+    "emqx_csr_unpermute_device", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
     "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check",
 )
 # Every symbol include/emqx_retain.h declares (retained-message index).
@@ -182,6 +184,11 @@ def lib():
         "emqx_commit_stats": (i32, [vp, vp, u32]),
         "emqx_shard_owner": (i32, [vp, vp, u64, u32, u32, i32, vp]),
         "emqx_shard_owner_device": (i32, [vp, vp, u64, u32, u32, vp, vp]),
+        "emqx_permute_scratch_bytes": (u64, [u64]),
+        "emqx_owner_sort_scratch_bytes": (u64, [u64, u32]),
+        "emqx_owner_sort_device": (i32, [vp, u64, u32, vp, vp, vp]),
+        "emqx_batch_permute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),
+        "emqx_csr_unpermute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),
         "emqx_host_batch_create": (i32, [vp, u64, u64, u64, ctypes.POINTER(ctypes.POINTER(HostBatchStruct))]),
         "emqx_host_batch_destroy": (i32, [ctypes.POINTER(HostBatchStruct)]),
         "emqx_host_batch_reserve": (i32, [ctypes.POINTER(HostBatchStruct), u64, u64, u64]),

@@ -1239,6 +1239,33 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
   return EMQX_ENOTFOUND;
 }
 
+uint64_t emqx_permute_scratch_bytes(uint64_t n) { return permute_scratch_bytes(n); }
+
+uint64_t emqx_owner_sort_scratch_bytes(uint64_t n, uint32_t world) { return owner_sort_scratch_bytes(n, world); }
+
+int emqx_owner_sort_device(const uint32_t* d_owner, uint64_t n, uint32_t world, uint32_t* d_perm, void* d_scratch,
+                           void* stream) {
+  if (world == 0 || (n && (!d_owner || !d_perm || !d_scratch)) || n > 0xFFFFFFFFull) return EMQX_EINVAL;
+  HIP_TRY(launch_owner_sort(d_owner, n, world, d_perm, d_scratch, static_cast<hipStream_t>(stream)));
+  return EMQX_OK;
+}
+
+int emqx_batch_permute_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, const uint32_t* d_perm,
+                              uint8_t* d_out_bytes, uint64_t* d_out_offsets, void* d_scratch, void* stream) {
+  if (!d_out_offsets || !d_scratch || (n && (!d_bytes || !d_offsets || !d_perm || !d_out_bytes))) return EMQX_EINVAL;
+  HIP_TRY(launch_batch_permute(d_bytes, d_offsets, n, d_perm, d_out_bytes, d_out_offsets, d_scratch,
+                               static_cast<hipStream_t>(stream)));
+  return EMQX_OK;
+}
+
+int emqx_csr_unpermute_device(const uint32_t* d_counts, const uint32_t* d_ids, uint64_t n, const uint32_t* d_perm,
+                              uint64_t* d_out_offsets, uint32_t* d_out_ids, void* d_scratch, void* stream) {
+  if (!d_out_offsets || !d_scratch || (n && (!d_counts || !d_perm))) return EMQX_EINVAL;
+  HIP_TRY(launch_csr_unpermute(d_counts, d_ids, n, d_perm, d_out_offsets, d_out_ids, d_scratch,
+                               static_cast<hipStream_t>(stream)));
+  return EMQX_OK;
+}
+
 int emqx_shard_owner_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t world,
                             uint32_t levels, uint32_t* d_owner, void* stream) {
   if ((n && (!d_bytes || !d_offsets || !d_owner)) || world == 0 || levels == 0) return EMQX_EINVAL;

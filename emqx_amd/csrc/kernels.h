@@ -168,6 +168,16 @@ hipError_t launch_order(const OrderArgs& o, hipStream_t s);
 // after the walk: corig[perm[p]] = counts[p]
 hipError_t launch_order_counts(const uint32_t* counts, const uint32_t* perm, uint64_t n, uint32_t* corig,
                                hipStream_t s);
+// Batches regrouped by a permutation and their CSR put back (emqx_batch_permute_device,
+// emqx_csr_unpermute_device).
+uint64_t permute_scratch_bytes(uint64_t n);
+hipError_t launch_batch_permute(const uint8_t* tbytes, const uint64_t* toffs, uint64_t n, const uint32_t* perm,
+                                uint8_t* obytes, uint64_t* ooffs, void* scratch, hipStream_t s);
+hipError_t launch_csr_unpermute(const uint32_t* counts, const uint32_t* ids, uint64_t n, const uint32_t* perm,
+                                uint64_t* out_off, uint32_t* out_ids, void* scratch, hipStream_t s);
+uint64_t owner_sort_scratch_bytes(uint64_t n, uint32_t world);
+hipError_t launch_owner_sort(const uint32_t* owner, uint64_t n, uint32_t world, uint32_t* perm, void* scratch,
+                             hipStream_t s);
 // counts[n] -> offsets[n+1] (exclusive); partials: scratch of >= scan_partials(n) u64
 // (fan-out's entry scan).
 uint64_t scan_partials(uint64_t n);

@@ -111,6 +111,23 @@ __global__ __launch_bounds__(256) void order_counts_kernel(const uint32_t* __res
     corig[perm[p]] = counts[p];
 }
 
+// 16 lanes per topic: received topic k's ids (at recv_off[k]) to its batch position's slot
+// of the output CSR (out_off[perm[k]]).
+__global__ __launch_bounds__(256) void csr_unpermute_kernel(const uint32_t* __restrict__ counts,
+                                                            const uint64_t* __restrict__ recv_off,
+                                                            const uint32_t* __restrict__ ids,
+                                                            const uint32_t* __restrict__ perm, uint64_t n,
+                                                            const uint64_t* __restrict__ out_off,
+                                                            uint32_t* __restrict__ out_ids) {
+  const uint32_t sub = threadIdx.x & 15u;
+  for (uint64_t k = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4; k < n;
+       k += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 4) {
+    const uint32_t c = counts[k];
+    const uint64_t s = recv_off[k], d = out_off[perm[k]];
+    for (uint32_t j = sub; j < c; j += 16) out_ids[d + j] = ids[s + j];
+  }
+}
+
 uint32_t grid_for(uint64_t n, uint32_t per_block) {
   return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((n + per_block - 1) / per_block, 8192)));
 }
@@ -158,6 +175,90 @@ hipError_t launch_order_t(const OrderArgs& o, hipStream_t s) {
 hipError_t launch_order(const OrderArgs& o, hipStream_t s) {
   if (o.n == 0) return hipSuccess;
   return o.sort_bits <= 32 ? launch_order_t<uint32_t>(o, s) : launch_order_t<uint64_t>(o, s);
+}
+
+// Scratch of the batch (un)permute entry points: u32 [n] lengths / counts, u64 [n + 1]
+// offsets, the scan's partials, one control word block.
+namespace {
+uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+}  // namespace
+
+uint64_t permute_scratch_bytes(uint64_t n) {
+  return align16(4 * std::max<uint64_t>(n, 1)) + align16(8 * (n + 1)) + align16(8 * scan_partials(n)) +
+         align16(4 * CTRL_WORDS);
+}
+
+hipError_t launch_batch_permute(const uint8_t* tbytes, const uint64_t* toffs, uint64_t n, const uint32_t* perm,
+                                uint8_t* obytes, uint64_t* ooffs, void* scratch, hipStream_t s) {
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  uint32_t* lens = reinterpret_cast<uint32_t*>(p);
+  p += align16(4 * std::max<uint64_t>(n, 1)) + align16(8 * (n + 1));
+  uint64_t* partials = reinterpret_cast<uint64_t*>(p);
+  p += align16(8 * scan_partials(n));
+  uint32_t* ctrl = reinterpret_cast<uint32_t*>(p);
+  if (n) hipLaunchKernelGGL(order_len_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, toffs, perm, n, lens);
+  hipError_t err = launch_scan(lens, n, ooffs, partials, s);
+  if (err != hipSuccess || n == 0) return err;
+  hipLaunchKernelGGL(order_gather_kernel, dim3(grid_for(n, 16)), dim3(256), 0, s, tbytes, toffs, perm, n, ooffs,
+                     obytes, ~0ull, ctrl);
+  return hipGetLastError();
+}
+
+hipError_t launch_csr_unpermute(const uint32_t* counts, const uint32_t* ids, uint64_t n, const uint32_t* perm,
+                                uint64_t* out_off, uint32_t* out_ids, void* scratch, hipStream_t s) {
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  uint32_t* corig = reinterpret_cast<uint32_t*>(p);
+  p += align16(4 * std::max<uint64_t>(n, 1));
+  uint64_t* recv_off = reinterpret_cast<uint64_t*>(p);
+  p += align16(8 * (n + 1));
+  uint64_t* partials = reinterpret_cast<uint64_t*>(p);
+  if (n) hipLaunchKernelGGL(order_counts_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, counts, perm, n, corig);
+  hipError_t err = launch_scan(corig, n, out_off, partials, s);  // batch order
+  if (err == hipSuccess) err = launch_scan(counts, n, recv_off, partials, s);  // received order
+  if (err != hipSuccess || n == 0) return err;
+  hipLaunchKernelGGL(csr_unpermute_kernel, dim3(grid_for(n, 16)), dim3(256), 0, s, counts, recv_off, ids, perm, n,
+                     out_off, out_ids);
+  return hipGetLastError();
+}
+
+// Stable sort of a batch's topics by owner rank (the sharded layout's partition): a radix sort
+// of (owner, index) pairs over the owner's bits only — one pass for up to 256 ranks.
+namespace {
+__global__ __launch_bounds__(256) void iota_kernel(uint32_t* __restrict__ idx, uint64_t n) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    idx[i] = static_cast<uint32_t>(i);
+}
+uint32_t owner_bits(uint32_t world) {
+  uint32_t b = 1;
+  while (b < 32 && (1ull << b) < world) ++b;
+  return b;
+}
+}  // namespace
+
+uint64_t owner_sort_scratch_bytes(uint64_t n, uint32_t world) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
+                                  static_cast<uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
+                                  static_cast<uint32_t*>(nullptr), static_cast<size_t>(n), 0u, owner_bits(world));
+  return align16(bytes) + 2 * align16(4 * std::max<uint64_t>(n, 1));
+}
+
+hipError_t launch_owner_sort(const uint32_t* owner, uint64_t n, uint32_t world, uint32_t* perm, void* scratch,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  size_t tb = 0;
+  const uint32_t bits = owner_bits(world);
+  (void)rocprim::radix_sort_pairs(nullptr, tb, owner, static_cast<uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
+                                  perm, static_cast<size_t>(n), 0u, bits, s);
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  void* temp = p;
+  p += align16(tb);
+  uint32_t* keys_out = reinterpret_cast<uint32_t*>(p);
+  p += align16(4 * n);
+  uint32_t* idx = reinterpret_cast<uint32_t*>(p);
+  hipLaunchKernelGGL(iota_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, idx, n);
+  return rocprim::radix_sort_pairs(temp, tb, owner, keys_out, idx, perm, static_cast<size_t>(n), 0u, bits, s);
 }
 
 hipError_t launch_order_counts(const uint32_t* counts, const uint32_t* perm, uint64_t n, uint32_t* corig,

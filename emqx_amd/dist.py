@@ -84,12 +84,34 @@ def topic_owner(tb: torch.Tensor, to: torch.Tensor, world: int, levels: int = SH
 def partition(tb: torch.Tensor, to: torch.Tensor, owner: torch.Tensor, world: int):
     """Reorders a packed batch by owner rank (stable).  Returns (perm, lens in perm order,
     bytes in perm order, topics per rank, bytes per rank): part r is perm[sum(n_to[:r]) :
-    sum(n_to[:r+1])].  Vectorized; no host round trip."""
+    sum(n_to[:r+1])]; the permuted bytes are the first sum(bytes_to) of `bytes`.
+    Vectorized; no host round trip.  A device batch takes three HIP kernels
+    (owner sort, lengths + scan, byte gather: emqx_owner_sort_device, emqx_batch_permute_device)
+    and no atomics."""
     dev = tb.device
     n = owner.numel()
     lens = (to[1:] - to[:-1]).to(torch.int64)
-    perm = torch.argsort(owner, stable=True)
     n_to = torch.bincount(owner, minlength=world)
+    if tb.is_cuda and n:
+        from . import _lib
+        L = _lib.lib()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        perm32 = torch.empty(n, dtype=torch.int32, device=dev)
+        scratch = torch.empty(int(L.emqx_owner_sort_scratch_bytes(n, world)), dtype=torch.uint8, device=dev)
+        own32 = owner.to(torch.int32).contiguous()
+        _lib.check(L.emqx_owner_sort_device(ctypes.c_void_p(own32.data_ptr()), n, world,
+                                            ctypes.c_void_p(perm32.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                                            stream), "emqx_owner_sort_device")
+        perm = perm32.to(torch.int64)
+        lens_p = lens[perm]
+        # the permuted bytes (capacity: the whole buffer, so no host read of the byte total)
+        bytes_p = torch.empty(tb.numel() + 16, dtype=torch.uint8, device=dev)
+        ooffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        _device_call("emqx_batch_permute_device", tb, to, n, perm32, bytes_p, ooffs)
+        ends = torch.cumsum(n_to, 0)
+        bytes_to = ooffs[ends] - ooffs[ends - n_to]
+        return perm, lens_p, bytes_p, n_to, bytes_to
+    perm = torch.argsort(owner, stable=True)
     bytes_to = torch.zeros(world, dtype=torch.int64, device=dev).index_add_(0, owner, lens)
     lens_p = lens[perm]
     total = int(to[-1] - to[0]) if n else 0
@@ -111,6 +133,12 @@ def merge_csr(recv_counts: torch.Tensor, recv_ids: torch.Tensor, perm: torch.Ten
     ids int32) in batch order.  One host sync (the id total, for the allocation)."""
     dev = recv_counts.device
     n = perm.numel()
+    if recv_counts.is_cuda:  # one scatter kernel (emqx_csr_unpermute_device)
+        offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        out = torch.empty(max(int(recv_ids.numel()), 1), dtype=torch.int32, device=dev)
+        _device_call("emqx_csr_unpermute_device", recv_counts.to(torch.int32).contiguous(),
+                     recv_ids.to(torch.int32).contiguous(), n, perm.to(torch.int32), offsets, out)
+        return offsets, out[:int(recv_ids.numel())]
     counts = torch.zeros(n, dtype=torch.int64, device=dev).scatter_(0, perm, recv_counts.to(torch.int64))
     offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     offsets[1:] = torch.cumsum(counts, 0)
@@ -123,6 +151,18 @@ def merge_csr(recv_counts: torch.Tensor, recv_ids: torch.Tensor, perm: torch.Ten
         dest = offsets[perm[k]] + (torch.arange(total, device=dev) - recv_off[k])
         out[dest] = recv_ids.to(torch.int32)
     return offsets, out
+
+
+def _device_call(name: str, *args):
+    """A (un)permute entry point of the C ABI on the current stream, with its scratch."""
+    from . import _lib
+    L = _lib.lib()
+    n = next(a for a in args if isinstance(a, int))
+    dev = next(a for a in args if isinstance(a, torch.Tensor)).device
+    scratch = torch.empty(int(L.emqx_permute_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+    conv = [a if isinstance(a, int) else ctypes.c_void_p(a.data_ptr()) for a in args]
+    _lib.check(getattr(L, name)(*conv, ctypes.c_void_p(scratch.data_ptr()),
+                                ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), name)
 
 
 def _a2a(out_t: torch.Tensor, in_t: torch.Tensor, out_splits: List[int], in_splits: List[int], group):
@@ -206,7 +246,7 @@ class ShardedMatcher:
         my_lens = torch.empty(n_in, **i64)
         _a2a(my_lens, lens_p, in_splits_n, n_out_splits, grp)
         my_bytes = torch.empty(max(b_in, 1), dtype=torch.uint8, device=dev)
-        _a2a(my_bytes[:b_in], bytes_p, in_splits_b, b_out_splits, grp)
+        _a2a(my_bytes[:b_in], bytes_p[:sum(b_out_splits)], in_splits_b, b_out_splits, grp)
         my_offs = torch.zeros(n_in + 1, **i64)
         if n_in:
             my_offs[1:] = torch.cumsum(my_lens, 0)

@@ -288,6 +288,26 @@ int emqx_shard_owner(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, 
                      int topics, uint32_t* owner_out);
 int emqx_shard_owner_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t world,
                             uint32_t levels, uint32_t* d_owner, void* stream);
+/* Device batches regrouped for the filter-sharded layout (and their results put back), on
+ * `stream`, no host synchronisation.  d_perm[p] (< n, a permutation) names the batch topic at
+ * position p of the regrouped batch.
+ *   emqx_batch_permute_device: topic d_perm[p] of (d_bytes, d_offsets) -> topic p of
+ *     (d_out_bytes, d_out_offsets[n+1], starting at 0); d_out_bytes holds the batch's bytes.
+ *   emqx_csr_unpermute_device: per-topic results of the regrouped batch (d_counts[n] in
+ *     position order, d_ids topic after topic) -> the CSR in batch order (d_out_offsets[n+1],
+ *     d_out_ids).
+ * d_scratch: device memory of emqx_permute_scratch_bytes(n) bytes. */
+uint64_t emqx_permute_scratch_bytes(uint64_t n);
+/* d_perm = the batch's topics stably sorted by owner rank (d_owner[n] < world, from
+ * emqx_shard_owner_device): the regrouping emqx_batch_permute_device takes.  d_scratch:
+ * emqx_owner_sort_scratch_bytes(n, world) bytes. */
+uint64_t emqx_owner_sort_scratch_bytes(uint64_t n, uint32_t world);
+int emqx_owner_sort_device(const uint32_t* d_owner, uint64_t n, uint32_t world, uint32_t* d_perm, void* d_scratch,
+                           void* stream);
+int emqx_batch_permute_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, const uint32_t* d_perm,
+                              uint8_t* d_out_bytes, uint64_t* d_out_offsets, void* d_scratch, void* stream);
+int emqx_csr_unpermute_device(const uint32_t* d_counts, const uint32_t* d_ids, uint64_t n, const uint32_t* d_perm,
+                              uint64_t* d_out_offsets, uint32_t* d_out_ids, void* d_scratch, void* stream);
 
 /* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */
 int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filter,

@@ -445,3 +445,41 @@ def test_batcher_coalesces_concurrent_callers(Engine):
     assert got == expect
     assert st["topics"] == len(topics)
     assert st["batches"] < len(topics) // 4
+
+
+def test_batch_permute_and_csr_unpermute_device(Engine):
+    """emqx_batch_permute_device / emqx_csr_unpermute_device (the sharded layout's regrouping)
+    against their torch restatements, on a batch that does not start at byte 0, with empty
+    topics and topics without results."""
+    import torch
+    from emqx_amd import dist as D
+    rng = np.random.default_rng(5)
+    n = 5000
+    lens = rng.integers(0, 40, n)
+    lens[::97] = 0
+    pad = 7
+    tb_np = rng.integers(32, 127, pad + int(lens.sum()), dtype=np.uint8)
+    to_np = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64) + pad
+    dev = torch.device("cuda:0")
+    tb, to = torch.from_numpy(tb_np).to(dev), torch.from_numpy(to_np).to(dev)
+    owner = torch.from_numpy(rng.integers(0, 4, n)).to(dev)
+    perm, lens_p, bytes_p, n_to, bytes_to = D.partition(tb, to, owner, 4)
+    p = perm.cpu().numpy()
+    want = b"".join(bytes(tb_np[to_np[i]:to_np[i + 1]]) for i in p)
+    assert int(bytes_to.sum()) == len(want)
+    assert bytes(bytes_p[:len(want)].cpu().numpy()) == want
+    assert n_to.cpu().tolist() == np.bincount(owner.cpu().numpy(), minlength=4).tolist()
+    assert bytes_to.cpu().tolist() == [int(lens[owner.cpu().numpy() == r].sum()) for r in range(4)]
+    counts = torch.from_numpy(rng.integers(0, 6, n)).to(dev)
+    counts[::13] = 0
+    ids = torch.from_numpy(rng.integers(0, 1 << 30, int(counts.sum()))).to(torch.int32).to(dev)
+    off, out = D.merge_csr(counts, ids, perm)
+    c, i = counts.cpu().numpy(), ids.cpu().numpy()
+    roff = np.concatenate([[0], np.cumsum(c)])
+    per = [None] * n
+    for k in range(n):
+        per[p[k]] = i[roff[k]:roff[k + 1]]
+    o, u = off.cpu().numpy(), out.cpu().numpy()
+    assert o[-1] == len(i)
+    for t in range(n):
+        assert np.array_equal(u[o[t]:o[t + 1]], per[t]), t
