@@ -369,9 +369,11 @@ def main():
 
 
 def sharded_bench(args, rank, world, dev):
-    """Config C style: the table is split over the ranks (emqx_amd/dist.py); every step
-    partitions rank 0's batch by owner rank, exchanges the parts (all-to-all), matches each
-    topic on its one owner shard and returns the CSR to rank 0 in batch order."""
+    """Config C style: the table is split over the ranks (emqx_amd/dist.py); every rank
+    publishes its own batch each step (ShardedMatcher.match_all): it partitions the batch by
+    owner rank, one all-to-all sends every part to its owner, every rank matches what it
+    received against its shard, and the results come back to their source in batch order.
+    Weak scaling: per-rank batch fixed as the world grows."""
     import torch
     import torch.distributed as dist
     from emqx_amd import workloads as W
@@ -379,7 +381,8 @@ def sharded_bench(args, rank, world, dev):
     seed = 3 if args.vocab_scale > 1 else 2
     t0 = time.time()
     with progress(f"[rank {rank}] generating workload"):
-        wl = W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=seed, vocab_scale=args.vocab_scale)
+        wl = W.config_b(n_filters=args.n_filters, n_topics=args.batch, seed=seed, vocab_scale=args.vocab_scale,
+                        topic_seed=None if rank == 0 else 1000 + rank)
     log(f"[rank {rank}] workload {wl.n_filters} filters ({time.time() - t0:.1f}s)")
     if world == 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -389,18 +392,16 @@ def sharded_bench(args, rank, world, dev):
         sm = ShardedMatcher(wl.filters, device=dev, mode=args.mode)
     st = sm.engine.stats()
     log(f"[rank {rank}] shard: {st['n_filters']} filters, {st['table_bytes'] / 1e9:.2f} GB")
-    topics = None
-    if rank == 0:
-        topics = (torch.from_numpy(wl.topics[0]).to(dev), torch.from_numpy(wl.topics[1].view(np.int64)).to(dev))
+    topics = (torch.from_numpy(wl.topics[0]).to(dev), torch.from_numpy(wl.topics[1].view(np.int64)).to(dev))
     res = None
-    for _ in range(args.warmup):
-        res = sm.match(topics)
+    for _ in range(max(args.warmup, 1)):
+        res = sm.match_all(topics)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        res = sm.match(topics)
+        res = sm.match_all(topics)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -408,18 +409,21 @@ def sharded_bench(args, rank, world, dev):
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
+    n = wl.n_topics
+    mt = torch.tensor([float(res[0][-1].item()), float(sm.last_local_topics)], dtype=torch.float64, device=dev)
+    dist.all_reduce(mt, op=dist.ReduceOp.SUM)
     if rank == 0:
-        n = wl.n_topics
         print(json.dumps({
             "metric": "published topics matched/sec at a filter-sharded table (SURVEY §8 e)",
-            "value": round(n * args.steps / elapsed, 1), "unit": "topics/s", "n_gpus": world,
+            "value": round(n * world * args.steps / elapsed, 1), "unit": "topics/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": f"{'C' if args.vocab_scale > 1 else 'B'}-generator table of {wl.n_filters} "
-                                   f"filters sharded x{world}, one {n}-topic batch per step from rank 0",
+                                   f"filters sharded x{world}, every rank publishing its own {n}-topic batch per step",
                        "parallelism": f"filter-sharded x{world} by the first two levels, RCCL all-to-all out and back"},
-            "matches_per_topic": round(int(res[0][-1].item()) / n, 3),
+            "shard_filters_rank0": st["n_filters"],
+            "matches_per_topic": round(float(mt[0].item()) / (n * world), 3),
         }), flush=True)
     dist.barrier()
     dist.destroy_process_group()

@@ -282,3 +282,52 @@ class ShardedMatcher:
         if me != dst:
             return None
         return merge_csr(cnt_in, ids_in, perm)
+
+    def match_all(self, topics: Tuple[torch.Tensor, torch.Tensor]):
+        """Every rank matches its own batch against the sharded table and gets its own CSR
+        (offsets int64 (n+1,), ids int32) in batch order — the layout's weak-scaling use, one
+        publishing node per rank.  Each rank partitions its batch by owner; one all-to-all
+        sends every part to its owner, every rank matches all it received (from all sources)
+        in one engine call, and one all-to-all (counts, then ids) returns each source's
+        results, which it puts back in batch order.  The collectives move each topic and each
+        result once; the fixed cost per step does not grow with the number of sources."""
+        dev, G, grp = self.device, self.world, self.group
+        i64 = dict(dtype=torch.int64, device=dev)
+        tb, to = topics
+        tb, to = tb.to(dev), to.to(dev).to(torch.int64)
+        owner = topic_owner(tb, to, G)
+        perm, lens_p, bytes_p, n_to, bytes_to = partition(tb, to, owner, G)
+        # sizes: what every source sends to every owner
+        send_meta = torch.stack([n_to, bytes_to], 1).reshape(-1)
+        recv_meta = torch.empty(2 * G, **i64)
+        _a2a(recv_meta, send_meta, [2] * G, [2] * G, grp)
+        sm = send_meta.reshape(G, 2).cpu()
+        rm = recv_meta.reshape(G, 2).cpu()
+        n_out, b_out = sm[:, 0].tolist(), sm[:, 1].tolist()
+        n_in, b_in = rm[:, 0].tolist(), rm[:, 1].tolist()
+        # the parts, source after source
+        my_lens = torch.empty(sum(n_in), **i64)
+        _a2a(my_lens, lens_p, n_in, n_out, grp)
+        my_bytes = torch.empty(max(sum(b_in), 1), dtype=torch.uint8, device=dev)
+        _a2a(my_bytes[:sum(b_in)], bytes_p[:sum(b_out)], b_in, b_out, grp)
+        my_offs = torch.zeros(sum(n_in) + 1, **i64)
+        if sum(n_in):
+            my_offs[1:] = torch.cumsum(my_lens, 0)
+        counts, ids = self.match_fn(my_bytes, my_offs)
+        counts = counts.to(torch.int64).to(dev)
+        ids = ids.to(torch.int32).to(dev)
+        self.last_local_topics = sum(n_in)
+        # results back: counts per received part, and the id total of each part
+        bounds = torch.tensor([0] + list(np.cumsum(n_in)), **i64)
+        csum = torch.zeros(sum(n_in) + 1, **i64)
+        if sum(n_in):
+            csum[1:] = torch.cumsum(counts, 0)
+        ids_out = (csum[bounds[1:]] - csum[bounds[:-1]]).cpu().tolist()
+        ids_in_t = torch.empty(G, **i64)
+        _a2a(ids_in_t, torch.tensor(ids_out, **i64), [1] * G, [1] * G, grp)
+        ids_in = ids_in_t.cpu().tolist()
+        cnt_back = torch.empty(int(perm.numel()), **i64)
+        _a2a(cnt_back, counts, n_out, n_in, grp)
+        ids_back = torch.empty(sum(ids_in), dtype=torch.int32, device=dev)
+        _a2a(ids_back, ids, ids_in, ids_out, grp)
+        return merge_csr(cnt_back, ids_back, perm)

@@ -116,6 +116,49 @@ def test_sharded_equals_single_table(world, src, dst):
     assert sum(splits) == len(_batches()[1][1]) - 1
 
 
+def _worker_all(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from emqx_amd import dist as D
+        filters, topics = _batches()
+        local, gids = D.shard_filters(filters, rank, world)
+        sm = D.ShardedMatcher(filters, device=torch.device("cpu"), match_fn=_oracle_match_fn(local, gids))
+        # every rank publishes its own slice (rank 1 of 2+ an empty batch)
+        part = D.split_topics(topics, rank, world)
+        if rank == 1:
+            part = (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+        t = (torch.from_numpy(part[0].copy()), torch.from_numpy(part[1].astype(np.int64)))
+        off, ids = sm.match_all(t)
+        q.put((rank, part[0].copy(), part[1].copy(), off.numpy(), ids.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_match_all_sources(world):
+    """ShardedMatcher.match_all: every rank a source of its own batch, each gets its own CSR
+    equal to the single-table oracle's for that batch."""
+    from oracle import cpp as C
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_all, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    o = C.CppOracle(True)
+    o.add_packed(*_batches()[0])
+    for rank, tb, to, off, ids in got:
+        off_o, ids_o, _ = o.match_csr(tb if len(tb) else np.zeros(1, np.uint8), to, mode=0, threads=2)
+        assert C.csr_mismatches(off, ids, off_o, ids_o).size == 0, rank
+
+
 def test_shard_layout_covers_every_match():
     """Every filter that matches a topic lives on the topic's owner rank (so one rank per
     topic suffices), each non-root-wildcard filter on exactly one rank, root wildcards on all."""

@@ -406,12 +406,15 @@ def test_sharded_matcher_config_c_generator(Engine):
         sm.engine.set_tuning("order", 1)
         off2, ids2 = sm.match(topics)
         off2, ids2 = off2.cpu().numpy(), ids2.cpu().numpy().view(np.uint32)
+        sm.engine.set_tuning("order", -1)
+        off3, ids3 = sm.match_all(topics)  # every rank its own source (here the one rank)
+        off3, ids3 = off3.cpu().numpy(), ids3.cpu().numpy().view(np.uint32)
     finally:
         dist.destroy_process_group()
     o = C.CppOracle(True)
     o.add_packed(*wl.filters)
     off_o, ids_o, _ = o.match_csr(*wl.topics, mode=C.MODE_ROUTES, threads=8)
-    for a, b in ((off, ids), (off2, ids2)):
+    for a, b in ((off, ids), (off2, ids2), (off3, ids3)):
         bad = C.csr_mismatches(a.astype(np.uint64), b, off_o, ids_o)
         assert bad.size == 0, bad[:10]
 
