@@ -484,16 +484,38 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       fillp[p] += 1;
     }
   }
+  // EMQX_CHILD_ORDER=hash|size (A/B runs only): each node's children in the pseudo-random
+  // order of a hash of (node, word) — the order round 1's edge-map scan produced — or by
+  // subtree size, largest first, instead of creation order; the child order decides the
+  // line-packed layout below
+  static const int child_order = [] {
+    const char* v = getenv("EMQX_CHILD_ORDER");
+    return !v ? 0 : std::strcmp(v, "hash") == 0 ? 1 : std::strcmp(v, "size") == 0 ? 2 : 0;
+  }();
+  if (child_order == 2) {
+    std::vector<uint32_t> sub(n_nodes, 1);  // subtree node counts (a child's id exceeds its parent's)
+    for (uint64_t c = n_nodes; c-- > 1;) sub[parent_of[c]] += sub[c];
+    parallel_chunks(n_nodes, nthreads, 1 << 14, [&](uint64_t v0, uint64_t v1, int) {
+      std::vector<std::pair<uint64_t, uint32_t>> tmp;
+      for (uint64_t v = v0; v < v1; ++v) {
+        const uint64_t a = coff[v], b = coff[v + 1];
+        if (b - a < 2) continue;
+        tmp.clear();
+        for (uint64_t j = a; j < b; ++j) tmp.emplace_back(~uint64_t(sub[cid[j]]) << 32 | (j - a), static_cast<uint32_t>(j - a));
+        std::sort(tmp.begin(), tmp.end());
+        std::vector<uint32_t> w2(b - a), c2(b - a);
+        for (uint64_t k = 0; k < tmp.size(); ++k) {
+          w2[k] = cwid[a + tmp[k].second];
+          c2[k] = cid[a + tmp[k].second];
+        }
+        std::copy(w2.begin(), w2.end(), cwid.begin() + static_cast<std::ptrdiff_t>(a));
+        std::copy(c2.begin(), c2.end(), cid.begin() + static_cast<std::ptrdiff_t>(a));
+      }
+    });
+  }
   std::vector<uint32_t>().swap(parent_of);
   std::vector<uint32_t>().swap(wid_of);
-  // EMQX_CHILD_ORDER=hash (A/B runs only): each node's children in the pseudo-random order of
-  // a hash of (node, word) — the order round 1's edge-map scan produced — instead of creation
-  // order; the child order decides the line-packed layout below
-  static const bool hash_order = [] {
-    const char* v = getenv("EMQX_CHILD_ORDER");
-    return v && std::strcmp(v, "hash") == 0;
-  }();
-  if (hash_order) {
+  if (child_order == 1) {
     parallel_chunks(n_nodes, nthreads, 1 << 14, [&](uint64_t v0, uint64_t v1, int) {
       std::vector<std::pair<uint64_t, uint32_t>> tmp;
       for (uint64_t v = v0; v < v1; ++v) {
