@@ -617,7 +617,13 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       }
     }
     if (!done) {
-      caplog[v] = log2u(next_pow2(4ull * e + 4));  // 2-slot buckets at load <= 1/4
+      // 2-slot buckets at load <= 1/4 (EMQX_WIDE_SLACK=k, A/B runs only: load <= 1/k)
+      static const uint64_t slack = [] {
+        const char* x = getenv("EMQX_WIDE_SLACK");
+        const long k = x ? std::atol(x) : 0;
+        return static_cast<uint64_t>(k >= 2 && k <= 16 ? k : 4);
+      }();
+      caplog[v] = log2u(next_pow2(slack * e + slack));
       bool ok = false;
       for (uint32_t sd = 0; sd < CUCKOO_SEEDS && !ok; ++sd) {
         ok = bucket_place(v, sd, 1u << caplog[v], ck_key, ck_child);
