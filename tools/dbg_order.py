@@ -1,3 +1,6 @@
+"""Walk-order check on one GPU (diagnosis): per (level bits, sort bits, deal) setting, the
+ordered device call against the unordered one on a config-D sample — totals, per-topic
+count differences, deferred topics, max stack."""
 import sys, time, numpy as np
 sys.path.insert(0, '.')
 import torch
