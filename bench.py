@@ -126,6 +126,9 @@ def main():
                     help="experiment: host-side permutation of the topic batch (sorted = lexicographic; "
                          "xcd = sorted, cut into 8 key-range segments, dealt 256 topics at a time so each "
                          "XCD's blocks see one segment)")
+    ap.add_argument("--batches", type=int, default=4,
+                    help="distinct topic batches the timed steps rotate over (config B / C generator; "
+                         "4 x 44 MB of topic bytes, so steps do not replay one cache-resident batch)")
     ap.add_argument("--walk-order", type=str, default="auto", choices=["auto", "on", "off"],
                     help="engine walk order (emqx_set_tuning 'order'): the batch is walked in prefix-key "
                          "order with XCD-contiguous tile ranges, inside the call (auto: deep tables)")
@@ -182,10 +185,13 @@ def main():
         wl = load_or_make(args, rank, lambda: W.config_d(n_topics=args.batch, seed=4))
     else:
         with progress(f"[rank {rank}] generating workload"):
+            extra_seeds = tuple(5000 + 100 * rank + j for j in range(1, max(args.batches, 1)))
             wl = load_or_make(args, rank, lambda: W.config_b(n_filters=args.n_filters, n_topics=args.batch,
                                                              seed=3 if args.vocab_scale > 1 else 2,
                                                              vocab_scale=args.vocab_scale,
-                                                             topic_seed=None if rank == 0 else 1000 + rank))
+                                                             topic_seed=None if rank == 0 else 1000 + rank,
+                                                             extra_topic_seeds=extra_seeds),
+                              batches=max(args.batches, 1))
     log(f"[rank {rank}] workload: {wl.n_filters} filters, {wl.n_topics} topics ({time.time() - t0:.1f}s)")
     if args.order != "none":
         wl = reorder_topics(wl, args.order)
@@ -203,6 +209,11 @@ def main():
     tb = torch.from_numpy(wl.topics[0]).to(dev)
     to = torch.from_numpy(wl.topics[1].view(np.int64)).to(dev)
     n = wl.n_topics
+    # the timed steps rotate over distinct batches (batch 0 = the one the baselines and the
+    # parity check use); every batch has n topics
+    batches = [(tb, to)] + [(torch.from_numpy(b[0]).to(dev), torch.from_numpy(b[1].view(np.int64)).to(dev))
+                            for b in getattr(wl, "extra_topics", [])[: max(args.batches, 1) - 1]
+                            if len(b[1]) - 1 == n]
     d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
     cap = max(64 * n, 1 << 20)
     d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -234,9 +245,17 @@ def main():
     # events recorded there would not follow the calls)
     streams = [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
     outs = [(d_off, d_ids)] + [(torch.empty_like(d_off), torch.empty_like(d_ids)) for _ in range(args.streams - 1)]
-    for k in range(len(streams)):  # size each stream's workspace (a synchronous call learns its slab)
-        eng.match_device(tb.data_ptr(), to.data_ptr(), n, outs[k][0].data_ptr(), outs[k][1].data_ptr(), cap,
-                         mode=args.mode, stream=streams[k].cuda_stream)
+    nouts = []
+    for j, (btb, bto) in enumerate(batches):  # each batch's id total; size each stream's workspace
+        for k in range(len(streams)):           # (a synchronous call learns its slab)
+            try:
+                m = eng.match_device(btb.data_ptr(), bto.data_ptr(), n, outs[k][0].data_ptr(), outs[k][1].data_ptr(),
+                                     cap, mode=args.mode, stream=streams[k].cuda_stream)
+            except EngineError as err:
+                if getattr(err, "needed", None) is None:
+                    raise
+                raise SystemExit(f"batch {j} needs {err.needed} ids, over the {cap}-id buffers")
+        nouts.append(m)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -247,9 +266,10 @@ def main():
     ev0.record(streams[0])
     for k in range(args.steps):
         j = k % len(streams)
+        btb, bto = batches[k % len(batches)]
         if 0 < k < len(streams):  # the other streams start after the timed region began
             streams[j].wait_event(ev0)
-        eng.match_device_async(tb.data_ptr(), to.data_ptr(), n, outs[j][0].data_ptr(), outs[j][1].data_ptr(), cap,
+        eng.match_device_async(btb.data_ptr(), bto.data_ptr(), n, outs[j][0].data_ptr(), outs[j][1].data_ptr(), cap,
                                summ[k].data_ptr(), mode=args.mode, stream=streams[j].cuda_stream)
         evs[k].record(streams[j])
     t_enq = time.perf_counter() - t_start  # host time to enqueue the steps (async calls)
@@ -259,9 +279,12 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     sm = summ.cpu().numpy()
-    if args.steps and not ((sm[:, 0] == 0).all() and (sm[:, 1] == nout).all()):
+    want_tot = np.array([nouts[k % len(batches)] for k in range(args.steps)], dtype=np.int64)
+    if args.steps and not ((sm[:, 0] == 0).all() and (sm[:, 1] == want_tot).all()):
         raise SystemExit(f"async steps incomplete or inconsistent: flags {set(sm[:, 0].tolist())}, "
-                         f"totals {set(sm[:, 1].tolist())} vs {nout}")
+                         f"totals {set(sm[:, 1].tolist())} vs {set(want_tot.tolist())}")
+    if nouts[0] != nout:
+        raise SystemExit(f"batch 0 total {nouts[0]} != {nout}")
     # kernel / call times from synchronous calls (HIP events on the engine's stream)
     kern_ms, call_ms, order_ms = [], [], []
     for _ in range(min(max(args.steps, 1), 10)):
@@ -323,7 +346,8 @@ def main():
         "config": {"workload": WORKLOAD_NAMES["C1" if args.vocab_scale > 1 else args.workload],
                    "n_filters": wl.n_filters, "batch_topics_per_gpu": n, "mode": ["routes", "trie", "trie_wildcard"][args.mode],
                    "parallelism": f"replicated table, topic stream split x{world}",
-                   "walk_order": walk_order_desc(args, st)},
+                   "walk_order": walk_order_desc(args, st),
+                   "timed_batches": len(batches)},
         **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
            if os.environ.get("EMQX_BENCH_REHEARSE") == "1" else {}),
         "evals_per_s": round(evals_all * args.steps / elapsed, 1),
@@ -867,6 +891,11 @@ def update_bench(args, rank, world, dev):
     tb = torch.from_numpy(wl.topics[0]).to(dev)
     to = torch.from_numpy(wl.topics[1].view(np.int64)).to(dev)
     n = wl.n_topics
+    # the timed steps rotate over distinct batches (batch 0 = the one the baselines and the
+    # parity check use); every batch has n topics
+    batches = [(tb, to)] + [(torch.from_numpy(b[0]).to(dev), torch.from_numpy(b[1].view(np.int64)).to(dev))
+                            for b in getattr(wl, "extra_topics", [])[: max(args.batches, 1) - 1]
+                            if len(b[1]) - 1 == n]
     stream = torch.cuda.current_stream().cuda_stream
 
     def match_rate():
@@ -1137,15 +1166,21 @@ def reorder_topics(wl, order):
     return W.Workload(wl.name, wl.filters, W.take(wl.topics, np.asarray(idx)))
 
 
-def load_or_make(args, rank, make):
+def load_or_make(args, rank, make, batches=1):
     from emqx_amd.workloads import Workload
     path = f"{args.cache}.{rank}.npz" if args.cache else None
     if path and os.path.exists(path):
         z = np.load(path)
-        return Workload("B", (z["fb"], z["fo"]), (z["tb"], z["to"]))
+        wl = Workload("B", (z["fb"], z["fo"]), (z["tb"], z["to"]))
+        wl.extra_topics = [(z[f"tb{j}"], z[f"to{j}"]) for j in range(1, 64) if f"tb{j}" in z]
+        if len(wl.extra_topics) + 1 >= batches:
+            return wl
     wl = make()
     if path:
-        np.savez(path, fb=wl.filters[0], fo=wl.filters[1], tb=wl.topics[0], to=wl.topics[1])
+        extra = {}
+        for j, (tb, to) in enumerate(getattr(wl, "extra_topics", []), 1):
+            extra[f"tb{j}"], extra[f"to{j}"] = tb, to
+        np.savez(path, fb=wl.filters[0], fo=wl.filters[1], tb=wl.topics[0], to=wl.topics[1], **extra)
     return wl
 
 

@@ -226,11 +226,12 @@ def _b_filter_codes(rng, n, vocab_sizes, samplers):
 
 
 def config_b(n_filters: int = 10_000_000, n_topics: int = 1_000_000, seed: int = 2,
-             vocab_scale: int = 1, prefixes=B_PREFIX, topic_seed=None) -> Workload:
+             vocab_scale: int = 1, prefixes=B_PREFIX, topic_seed=None, extra_topic_seeds=()) -> Workload:
     """10M mixed exact/'+'/'#' filters, depth U{4..8}, Zipf(1.1) per-level vocab
     [64,1024,4096,65536,65536,1024,256,64]; 50% exact / 30% '+' / 20% '#'.  Topics depth
     U{4..8}: 50% instantiated from a random filter ('+' -> random word, '#' -> 0-3 words),
-    50% random (SURVEY §8 d)."""
+    50% random (SURVEY §8 d).  extra_topic_seeds: more independent topic batches over the same
+    table, as `.extra_topics` (the first batch is unchanged by them)."""
     rng = np.random.default_rng(seed)
     sizes = [v * vocab_scale for v in B_VOCAB]
     samplers = [zipf_sampler(rng, v) for v in sizes]
@@ -246,7 +247,18 @@ def config_b(n_filters: int = 10_000_000, n_topics: int = 1_000_000, seed: int =
     if topic_seed is not None:  # an independent topic stream over the same table
         rng = np.random.default_rng(topic_seed)
         samplers = [zipf_sampler(rng, v) for v in sizes]
+    topics = _b_topics(rng, samplers, fcodes, vs, n_filters, n_topics)
+    wl = Workload("B", filters, topics)
+    extra = []
+    for ts in extra_topic_seeds:
+        r2 = np.random.default_rng(ts)
+        extra.append(_b_topics(r2, [zipf_sampler(r2, v) for v in sizes], fcodes, vs, n_filters, n_topics))
+    wl.extra_topics = extra
+    return wl
 
+
+def _b_topics(rng, samplers, fcodes, vs, n_filters, n_topics):
+    """One topic batch of config B over the filter codes `fcodes` (see config_b)."""
     # topics (levels up to 8 + 3 for '#' expansion => pad to 11)
     TD = 11
     half = n_topics // 2
@@ -275,8 +287,7 @@ def config_b(n_filters: int = 10_000_000, n_topics: int = 1_000_000, seed: int =
     tcodes = tcodes[perm]
     # levels >= 8 use level-7 vocab words (instantiated '#' expansions)
     tv = vs[:8] + [vs[7]] * 3
-    topics = compose(tcodes, tv)
-    return Workload("B", filters, topics)
+    return compose(tcodes, tv)
 
 
 # ---------------------------------------------------------------------------------------
