@@ -98,6 +98,7 @@ struct RWork {
   uint32_t stack_cap = 1024;  // items per wave beyond the LDS part (grows on overflow)
   RRange* ranges = nullptr;
   uint32_t* rcount = nullptr;
+  uint64_t* rlive = nullptr;
   uint32_t range_cap = 0;
   uint32_t* ctrl = nullptr;
   uint32_t* fcount = nullptr;
@@ -125,6 +126,7 @@ struct RWork {
     rfree(stack);
     rfree(ranges);
     rfree(rcount);
+    rfree(rlive);
     rfree(ctrl);
     rfree(fcount);
     rfree(fcursor);
@@ -562,6 +564,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     const uint64_t rc = std::max<uint64_t>(4 * n, 1 << 16);
     RT_TRY(ralloc(w->ranges, rc));
     RT_TRY(ralloc(w->rcount, rc));
+    RT_TRY(ralloc(w->rlive, 5 * rc));
     w->range_cap = static_cast<uint32_t>(rc);
   }
   a.tile_filters = std::max<uint32_t>(1, std::min<uint32_t>(64, r->tile.load()));
@@ -596,6 +599,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     a.stack_cap = w->stack_cap;
     a.ranges = w->ranges;
     a.rcount = w->rcount;
+    a.rlive = w->rlive;
     a.range_cap = w->range_cap;
     a.spill_out = w->spill[0];
     a.spill_word = RC_SPILL;
@@ -648,6 +652,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       if (rc > 0xFFFFFFF0ull) return EMQX_ENOMEM;
       RT_TRY(ralloc(w->ranges, rc));
       RT_TRY(ralloc(w->rcount, rc));
+      RT_TRY(ralloc(w->rlive, 5 * rc));
       w->range_cap = static_cast<uint32_t>(rc);
       again = true;
     }

@@ -172,6 +172,9 @@ struct RetainArgs {
   uint32_t range_cap;
   uint32_t* ctrl;          // [RC_WORDS]
   uint32_t* rcount;        // [range_cap] live ranks per range
+  uint64_t* rlive;         // [5 * range_cap] live-rank masks of checked records (count pass -> write
+                           // pass): small record r at [r], big record j = range_cap-1-br at
+                           // [range_cap + 4j, +4)
   uint32_t* fcount;        // [n] live matches per filter
   uint32_t* fcursor;       // [n] write cursor per filter
   uint64_t* out_off;       // [n + 1]

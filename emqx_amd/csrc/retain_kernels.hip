@@ -750,17 +750,33 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a) {
         const uint32_t i = rg.lo + sub + RGROUP * k;
         rk[k] = i < rg.hi ? rank_at(rv, i, rg.flags) : 0u;
       }
+      // a checked record's live ranks: the count pass tests them (expiry, depth) and keeps the
+      // mask (bit sub + RGROUP * k), the write pass takes the mask instead of loading them again
+      uint64_t lm = 0;
+      if (MODE == 1 && check && r < ns && rg.hi > rg.lo) lm = a.rlive[r];
 #pragma unroll
-      for (uint32_t k = 0; k < RPER; ++k)
-        live[k] = rg.lo + sub + RGROUP * k < rg.hi && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
+      for (uint32_t k = 0; k < RPER; ++k) {
+        const bool in = rg.lo + sub + RGROUP * k < rg.hi;
+        if (MODE == 1 && check)
+          live[k] = (lm >> (sub + RGROUP * k)) & 1u;
+        else
+          live[k] = in && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
+      }
       uint32_t c = 0;
       if (MODE == 0) {
+        uint64_t m = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < RPER; ++k) c += live[k] ? 1u : 0u;
+        for (uint32_t k = 0; k < RPER; ++k) {
+          c += live[k] ? 1u : 0u;
+          m |= ((__ballot(live[k]) >> (grp * RGROUP)) & 0xFFull) << (RGROUP * k);
+        }
         c += __shfl_xor(c, 1, 64);
         c += __shfl_xor(c, 2, 64);
         c += __shfl_xor(c, 4, 64);
-        if (sub == 0 && r < ns && rg.hi > rg.lo) a.rcount[r] = c;
+        if (sub == 0 && r < ns && rg.hi > rg.lo) {
+          a.rcount[r] = c;
+          if (check) a.rlive[r] = m;
+        }
       } else {
         c = (r < ns && rg.hi > rg.lo) ? a.rcount[r] : 0u;
       }
@@ -820,13 +836,23 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a) {
         const uint32_t i = rg.lo + k * 64 + lane;
         rk[k] = i < rg.hi ? rank_at(rv, i, rg.flags) : 0u;
       }
+      uint64_t* const bm = a.rlive + a.range_cap + static_cast<uint64_t>(u - nrows) * RUNROLL;
+      if (MODE == 1 && check) {
 #pragma unroll
-      for (uint32_t k = 0; k < RUNROLL; ++k)
-        live[k] = rg.lo + k * 64 + lane < rg.hi && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
+        for (uint32_t k = 0; k < RUNROLL; ++k) live[k] = (bm[k] >> lane) & 1u;
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < RUNROLL; ++k)
+          live[k] = rg.lo + k * 64 + lane < rg.hi && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
+      }
       if (MODE == 0) {
         uint32_t cnt = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < RUNROLL; ++k) cnt += live[k] ? 1u : 0u;
+        for (uint32_t k = 0; k < RUNROLL; ++k) {
+          cnt += live[k] ? 1u : 0u;
+          const uint64_t m = __ballot(live[k]);
+          if (check && lane == k) bm[k] = m;
+        }
         uint32_t tot;
         (void)wave_excl(cnt, &tot);
         if (lane == 0) {
