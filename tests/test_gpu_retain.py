@@ -114,6 +114,24 @@ def test_wide_fanout_and_root_hash(mod):
     assert len(got[2]) == len(names)  # '#' selects '$SYS/...' too: the match spec has no '$' rule
 
 
+def test_wide_records_under_guard_and_depth_floor(mod):
+    """Checked records (expiry guard, '+'-then-'#' depth floor) of both sizes: the count pass
+    keeps each one's live-rank mask and the write pass emits from it (retain_out_kernel)."""
+    rng = random.Random(11)
+    idx = mod.RetainIndex()
+    names = [b"w/%d" % i for i in range(3000)] + [b"w/%d/x" % i for i in range(5000)]
+    names += [b"w/%d/x/%d" % (i, j) for i in range(0, 300, 3) for j in range(rng.randint(1, 90))]
+    names += [b"v/%d" % i for i in range(70)] + [b"v/%d/q" % i for i in range(40)]
+    expiry = [rng.choice([0, 0, 90, 100, 110]) for _ in names]
+    idx.store(names, expiry)
+    idx.commit()
+    filters = [b"#", b"w/#", b"w/+/#", b"+/+/#", b"w/+/x/#", b"v/+/#", b"v/#", b"w/+/x", b"+/+"]
+    tt = RR.TokenTrie(names, expiry)
+    for now in (100, -1, 95):
+        for f, g in zip(filters, idx.match(filters, now)):
+            assert g == tt.dispatch(f, now), (f, now)
+
+
 def test_deep_topics(mod):
     rng = random.Random(3)
     idx = mod.RetainIndex()
