@@ -17,6 +17,7 @@
 
 #include "../../include/emqx_match.h"
 #include "kernels.h"
+#include "streams.h"
 #include "tables.h"
 
 using namespace emqx;
@@ -938,7 +939,9 @@ int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topi
   int rc = ensure_ws(w, n);
   if (rc == EMQX_OK) {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
-    rc = run_match(e, *snap, w, mode, d_topic_bytes, d_topic_offsets, n, d_out_offsets, d_out_ids, cap, n_out, s);
+    if (!stream && after_null_stream(s) != hipSuccess) rc = EMQX_EDEVICE;
+    if (rc == EMQX_OK)
+      rc = run_match(e, *snap, w, mode, d_topic_bytes, d_topic_offsets, n, d_out_offsets, d_out_ids, cap, n_out, s);
   }
   release_ws(e, w);
   return rc;
@@ -956,7 +959,9 @@ int emqx_match_batch_device_async(emqx_engine* e, uint32_t mode, const uint8_t* 
   int rc = ensure_ws(w, n);
   if (rc == EMQX_OK) {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
-    rc = enqueue_match(e, *snap, w, mode, d_topic_bytes, d_topic_offsets, n, d_out_offsets, d_out_ids, cap,
+    if (!stream && after_null_stream(s) != hipSuccess) rc = EMQX_EDEVICE;
+    if (rc == EMQX_OK)
+      rc = enqueue_match(e, *snap, w, mode, d_topic_bytes, d_topic_offsets, n, d_out_offsets, d_out_ids, cap,
                        summary, s);
     w->inflight = snap;  // released when the workspace is next used (its stream has moved on)
   }

@@ -24,6 +24,7 @@
 #include "../../include/emqx_match.h"
 #include "fanout.h"
 #include "kernels.h"
+#include "streams.h"
 
 using namespace emqx;
 
@@ -556,6 +557,7 @@ int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* 
   std::lock_guard<std::mutex> g(s->mu);
   FO_TRY(hipSetDevice(s->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
+  if (!stream) FO_TRY(after_null_stream(st));
   // the number of match entries: one small readback of the CSR bounds
   uint64_t bounds[2] = {0, 0};
   FO_TRY(hipMemcpyAsync(s->h_total, d_match_offsets, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -579,6 +581,7 @@ int emqx_fanout_batch_device_async(emqx_subtab* s, uint32_t strategy, const uint
   std::lock_guard<std::mutex> g(s->mu);
   FO_TRY(hipSetDevice(s->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
+  if (!stream) FO_TRY(after_null_stream(st));
   return enqueue_fanout(s, strategy, d_match_offsets, d_match_ids, n, match_cap, d_pick_keys, d_out_offsets,
                         d_out_subs, d_out_filters, cap, summary, st);
 }

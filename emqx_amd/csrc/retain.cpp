@@ -20,6 +20,7 @@
 #include "../../include/emqx_retain.h"
 #include "kernels.h"
 #include "retain.h"
+#include "streams.h"
 #include "tables.h"
 
 using namespace emqx;
@@ -810,6 +811,10 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_fb, const ui
   int rc = acquire(r, &w);
   if (rc != EMQX_OK) return rc;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : w->stream;
+  if (!stream && after_null_stream(s) != hipSuccess) {
+    release(r, w);
+    return EMQX_EDEVICE;
+  }
   uint64_t span = 0;
   if (n) {
     uint64_t ends[2];

@@ -166,6 +166,13 @@ def _device_call(name: str, *args):
 
 
 def _a2a(out_t: torch.Tensor, in_t: torch.Tensor, out_splits: List[int], in_splits: List[int], group):
+    if out_t.is_cuda and dist.get_backend(group) == "gloo":
+        # device tensors over gloo (rehearsals of the N-rank path on a box with fewer GPUs):
+        # exchange host copies, ordered after the producing stream by the copy itself
+        host = torch.empty(out_t.shape, dtype=out_t.dtype)
+        dist.all_to_all_single(host, in_t.cpu(), out_splits, in_splits, group=group)
+        out_t.copy_(host)
+        return
     dist.all_to_all_single(out_t, in_t, out_splits, in_splits, group=group)
 
 

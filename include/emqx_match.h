@@ -137,7 +137,9 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes,
                      uint32_t* out_ids, uint64_t cap, uint64_t* n_out);
 
 /* Batched match, DEVICE buffers already resident in HBM (d_* pointers), ordered on the
- * given hipStream_t (NULL: the engine's own stream).  Same contract as above, except that on
+ * given hipStream_t (NULL: the engine's own stream, which first waits for the work already
+ * enqueued on the device's null stream, where such a caller produced its inputs; the same
+ * holds for every device entry point below that takes NULL).  Same contract as above, except that on
  * EMQX_EOVERFLOW d_out_offsets are complete and d_out_ids holds the first cap ids; *n_out is
  * a host pointer.  Returns after the results are complete on `stream`. */
 int emqx_match_batch_device(emqx_engine* e, uint32_t mode, const uint8_t* d_topic_bytes,

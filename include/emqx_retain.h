@@ -96,7 +96,8 @@ int emqx_retain_match_spec_batch(emqx_retain* r, const uint8_t* filter_bytes, co
                                  uint64_t n, int64_t now_ms, uint64_t* out_offsets, uint32_t* out_ids,
                                  uint64_t out_cap, uint64_t* n_out);
 /* Same, with every buffer in device memory of the index's device, on `stream` (0 = the
- * index's own).  Synchronizes the stream before returning. */
+ * index's own, ordered after the work already enqueued on the device's null stream).
+ * Synchronizes the stream before returning. */
 int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes,
                                    const uint64_t* d_filter_offsets, uint64_t n, int64_t now_ms,
                                    uint64_t* d_out_offsets, uint32_t* d_out_ids, uint64_t out_cap,
