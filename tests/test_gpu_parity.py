@@ -289,6 +289,37 @@ def test_device_api_matches_host_api(Engine):
         assert np.array_equal(np.sort(ids_d[off_d[i]:off_d[i + 1]]), np.sort(ids_h[off_h[i]:off_h[i + 1]]))
 
 
+def test_device_api_null_stream_waits_for_default_stream(Engine):
+    """A device call given no stream runs on the engine's own (non-blocking) stream after the
+    work already enqueued on the null stream (include/emqx_match.h): offsets written there
+    behind a long kernel must be the ones matched.  Unordered, the call would read the
+    all-zero offsets written first (every topic empty: no out-of-bounds reads) and return no ids."""
+    import torch
+    from emqx_amd import workloads as W
+    b = W.config_b(n_filters=50_000, n_topics=20_000)
+    e = Engine()
+    e.insert_packed(*b.filters)
+    e.commit()
+    off_h, ids_h = e.match_packed(*b.topics, mode=0)
+    assert ids_h.size > 0
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(b.topics[0]).to(dev)
+    to_real = torch.from_numpy(b.topics[1].view(np.int64)).to(dev)
+    to = torch.zeros_like(to_real)
+    d_off = torch.empty(len(b.topics[1]), dtype=torch.int64, device=dev)
+    d_ids = torch.empty(ids_h.size + 16, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        to.zero_()
+        torch.cuda.synchronize()
+        torch.cuda._sleep(100_000_000)  # tens of ms on the null stream
+        to.copy_(to_real)               # the real offsets, behind it
+        n = e.match_device(tb.data_ptr(), to.data_ptr(), len(b.topics[1]) - 1, d_off.data_ptr(),
+                           d_ids.data_ptr(), d_ids.numel(), mode=0, stream=0)
+        assert n == ids_h.size
+        assert np.array_equal(d_off.cpu().numpy().view(np.uint64), off_h)
+
+
 def test_async_device_api(Engine):
     """emqx_match_batch_device_async: pipelined calls on one stream give the synchronous
     call's CSR, each writes its summary, and the flags report a too-small id buffer and a
