@@ -448,6 +448,8 @@ def sharded_bench(args, rank, world, dev):
                        "parallelism": f"filter-sharded x{world} by the first two levels, RCCL all-to-all out and back"},
             "shard_filters_rank0": st["n_filters"],
             "matches_per_topic": round(float(mt[0].item()) / (n * world), 3),
+            **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
+               if os.environ.get("EMQX_BENCH_REHEARSE") == "1" else {}),
         }), flush=True)
     dist.barrier()
     dist.destroy_process_group()
