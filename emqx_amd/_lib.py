@@ -22,6 +22,7 @@ EMQX_EDEVICE = -3
 EMQX_EOVERFLOW = -4
 EMQX_ENOTFOUND = -5
 EMQX_ETOODEEP = -6
+EMQX_EBUSY = -7
 
 MODE_ROUTES = 0
 MODE_TRIE = 1
@@ -35,9 +36,14 @@ EXPORTS = (
     "emqx_match_batch_device", "emqx_match_batch_device_async", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
     "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_batcher_create",
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_batcher_stats_ext",
-    "emqx_batcher_submit_many", "emqx_strerror", "emqx_version",
+    "emqx_batcher_submit_many", "emqx_batcher_try_submit", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
-    "emqx_subtab_stats", "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
+    "emqx_subtab_stats", "emqx_subtab_commit_stats", "emqx_subtab_forget_publishers",
+    "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
+    "emqx_pub_batch_create", "emqx_pub_batch_destroy", "emqx_pub_batch_reserve", "emqx_pub_batch_submit",
+    "emqx_pub_batch_wait", "emqx_pub_batch_query",
+    "emqx_pub_batcher_create", "emqx_pub_batcher_submit", "emqx_pub_batcher_try_submit",
+    "emqx_pub_batcher_submit_many", "emqx_pub_batcher_destroy", "emqx_pub_batcher_stats_ext",
     "emqx_host_batch_create", "emqx_host_batch_destroy", "emqx_host_batch_reserve", "emqx_host_batch_submit",
     "emqx_host_batch_wait", "emqx_host_batch_query",
     "emqx_commit_stats", "emqx_shard_owner", "emqx_shard_owner_device", "emqx_permute_scratch_bytes", "emqx_batch_permute_device", "emqx_owner_sort_scratch_bytes",
@@ -118,7 +124,21 @@ class HostBatchStruct(ctypes.Structure):
     ]
 
 
+class PubBatchStruct(ctypes.Structure):
+    """struct emqx_pub_batch (include/emqx_match.h): pinned buffers of one publish batch."""
+    _fields_ = [
+        ("topic_bytes", ctypes.POINTER(ctypes.c_uint8)), ("topic_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("keys", ctypes.POINTER(ctypes.c_uint32)),
+        ("cap_topics", ctypes.c_uint64), ("cap_bytes", ctypes.c_uint64), ("n", ctypes.c_uint64),
+        ("out_offsets", ctypes.POINTER(ctypes.c_uint64)), ("out_subs", ctypes.POINTER(ctypes.c_uint32)),
+        ("out_filters", ctypes.POINTER(ctypes.c_uint32)),
+        ("cap_out", ctypes.c_uint64), ("n_out", ctypes.c_uint64), ("priv", ctypes.c_void_p),
+    ]
+
+
 BATCH_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64)
+PUB_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
+                          ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64)
 
 _lib = None
 
@@ -158,12 +178,27 @@ def lib():
         "emqx_batcher_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "emqx_batcher_stats_ext": (i32, [vp, vp, u32]),
         "emqx_batcher_submit_many": (i32, [vp, vp, vp, u64, vp]),
+        "emqx_batcher_try_submit": (i32, [vp, vp, u64, vp]),
         "emqx_subtab_create": (i32, [ctypes.c_int32, ctypes.POINTER(vp)]),
         "emqx_subtab_destroy": (i32, [vp]),
         "emqx_subtab_add": (i32, [vp, vp, vp, vp, u64]),
         "emqx_subtab_remove": (i32, [vp, vp, vp, vp, u64]),
         "emqx_subtab_commit": (i32, [vp]),
         "emqx_subtab_stats": (i32, [vp, vp]),
+        "emqx_subtab_commit_stats": (i32, [vp, vp, u32]),
+        "emqx_subtab_forget_publishers": (i32, [vp, vp, u64]),
+        "emqx_pub_batch_create": (i32, [vp, vp, u32, u64, u64, u64, ctypes.POINTER(ctypes.POINTER(PubBatchStruct))]),
+        "emqx_pub_batch_destroy": (i32, [ctypes.POINTER(PubBatchStruct)]),
+        "emqx_pub_batch_reserve": (i32, [ctypes.POINTER(PubBatchStruct), u64, u64, u64]),
+        "emqx_pub_batch_submit": (i32, [ctypes.POINTER(PubBatchStruct)]),
+        "emqx_pub_batch_wait": (i32, [ctypes.POINTER(PubBatchStruct)]),
+        "emqx_pub_batch_query": (i32, [ctypes.POINTER(PubBatchStruct)]),
+        "emqx_pub_batcher_create": (i32, [vp, vp, u32, u32, u32, PUB_CB, ctypes.POINTER(vp)]),
+        "emqx_pub_batcher_submit": (i32, [vp, vp, u64, u32, vp]),
+        "emqx_pub_batcher_try_submit": (i32, [vp, vp, u64, u32, vp]),
+        "emqx_pub_batcher_submit_many": (i32, [vp, vp, vp, vp, u64, vp]),
+        "emqx_pub_batcher_destroy": (i32, [vp]),
+        "emqx_pub_batcher_stats_ext": (i32, [vp, vp, u32]),
         "emqx_fanout_batch_device": (i32, [vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64), vp]),
         "emqx_fanout_batch_device_async": (i32, [vp, u32, vp, vp, u64, u64, vp, vp, vp, vp, u64, vp, vp]),
         "emqx_publish_batch": (i32, [vp, vp, u32, vp, vp, u64, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]),

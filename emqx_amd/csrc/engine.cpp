@@ -1191,6 +1191,7 @@ const char* emqx_strerror(int code) {
     case EMQX_EOVERFLOW: return "output capacity too small";
     case EMQX_ENOTFOUND: return "not found";
     case EMQX_ETOODEEP: return "topic frontier too deep";
+    case EMQX_EBUSY: return "busy: every batch buffer is in use";
     default: return "unknown error";
   }
 }

@@ -1,6 +1,7 @@
 // C ABI of the publish fan-out stage (include/emqx_match.h, emqx_subtab_* / emqx_fanout_* /
-// emqx_publish_batch): host subscription store, device snapshot build, and the fan-out
-// pipeline  entry_topic -> count -> scan -> offsets -> [one D2H of the total] -> write.
+// emqx_pub_batch_* / emqx_publish_batch): host subscription store, device tables patched in
+// place per commit, the per-publisher $share pick state, and the fan-out pipeline
+//   entry_topic -> count -> scan -> offsets -> write [-> resolve] -> finish   (one stream, no host sync)
 //
 // Store semantics follow the reference's ETS tables:
 //   plain subscriptions  ?SUBSCRIBER bag Topic -> SubPid (apps/emqx/src/emqx_broker.erl:146-158);
@@ -8,8 +9,16 @@
 //                        (emqx_broker_helper.erl:81-86) only split storage, so the device
 //                        array is the flattened union.
 //   $share memberships   emqx_shared_subscription bag keyed by Group, selected per
-//                        (Group, Topic) in insertion order (emqx_shared_sub.erl:288,300-314);
+//                        (Group, Topic) in insertion order (emqx_shared_sub.erl:287-288,308-322);
 //                        the member order is what lists:nth/2 indexes in pick_subscriber/6.
+//
+// Commits cost what changed: the host keeps an image of every device array;
+// a subscribe appends to its filter's plain list in place (or moves the list to the end of the
+// arena with twice the room), an unsubscribe moves the list's last entry into the hole; a
+// $share membership change rewrites that group's member list and its 16-B group record.  The
+// commit uploads the touched words and records only, ordered after the fan-outs in flight and
+// before the next ones by events (no fan-out reads a table while a commit writes it).  A full
+// rebuild (compaction) runs only when moved-away extents outweigh the live ones.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,19 +54,20 @@ inline uint64_t fo_mix64(uint64_t x) {
   return x;
 }
 
-// Open-addressed set of u64 keys with tombstones (keys never take the two reserved values:
+// Open-addressed map u64 -> u32 with tombstones (keys never take the two reserved values:
 // filter ids and slots are < 2^31).
-class U64Set {
+class U64Map {
  public:
-  bool contains(uint64_t k) const {
-    if (keys_.empty()) return false;
+  uint32_t find(uint64_t k) const {
+    if (keys_.empty()) return SUB_NONE;
     const uint64_t mask = keys_.size() - 1;
     for (uint64_t i = fo_mix64(k) & mask;; i = (i + 1) & mask) {
-      if (keys_[i] == EMPTY) return false;
-      if (keys_[i] == k) return true;
+      if (keys_[i] == EMPTY) return SUB_NONE;
+      if (keys_[i] == k) return vals_[i];
     }
   }
-  bool insert(uint64_t k) {  // true if newly inserted
+  // true if newly inserted (an existing key keeps its value)
+  bool insert(uint64_t k, uint32_t v) {
     if (keys_.empty()) rehash(1024);
     else if ((used_ + 1) * 4 >= keys_.size() * 3)  // double, or just drop tombstones
       rehash((size_ + 1) * 2 >= keys_.size() ? keys_.size() * 2 : keys_.size());
@@ -69,10 +79,19 @@ class U64Set {
       if (keys_[i] == EMPTY) {
         if (tomb != ~0ull) i = tomb; else ++used_;
         keys_[i] = k;
+        vals_[i] = v;
         ++size_;
         return true;
       }
     }
+  }
+  void assign(uint64_t k, uint32_t v) {  // k present
+    const uint64_t mask = keys_.size() - 1;
+    for (uint64_t i = fo_mix64(k) & mask;; i = (i + 1) & mask)
+      if (keys_[i] == k) {
+        vals_[i] = v;
+        return;
+      }
   }
   bool erase(uint64_t k) {
     if (keys_.empty()) return false;
@@ -86,66 +105,33 @@ class U64Set {
       }
     }
   }
+  bool contains(uint64_t k) const { return find(k) != SUB_NONE; }
   uint64_t size() const { return size_; }
 
  private:
   static constexpr uint64_t EMPTY = ~0ull, TOMB = ~0ull - 1;
   void rehash(uint64_t cap) {
-    std::vector<uint64_t> old;
-    old.swap(keys_);
+    std::vector<uint64_t> ok;
+    std::vector<uint32_t> ov;
+    ok.swap(keys_);
+    ov.swap(vals_);
     keys_.assign(cap, EMPTY);
+    vals_.assign(cap, 0);
     used_ = size_ = 0;
     const uint64_t mask = cap - 1;
-    for (uint64_t k : old) {
-      if (k == EMPTY || k == TOMB) continue;
-      uint64_t i = fo_mix64(k) & mask;
+    for (uint64_t j = 0; j < ok.size(); ++j) {
+      if (ok[j] == EMPTY || ok[j] == TOMB) continue;
+      uint64_t i = fo_mix64(ok[j]) & mask;
       while (keys_[i] != EMPTY) i = (i + 1) & mask;
-      keys_[i] = k;
+      keys_[i] = ok[j];
+      vals_[i] = ov[j];
       ++used_;
       ++size_;
     }
   }
   std::vector<uint64_t> keys_;
-  uint64_t used_ = 0, size_ = 0;  // used_ counts tombstones too
-};
-
-// u64 -> u32 map without deletion (group slots are persistent).
-class U64Map {
- public:
-  uint32_t find(uint64_t k) const {
-    if (keys_.empty()) return SUB_NONE;
-    const uint64_t mask = keys_.size() - 1;
-    for (uint64_t i = fo_mix64(k) & mask;; i = (i + 1) & mask) {
-      if (vals_[i] == SUB_NONE) return SUB_NONE;
-      if (keys_[i] == k) return vals_[i];
-    }
-  }
-  void insert_new(uint64_t k, uint32_t v) {
-    if ((size_ + 1) * 4 >= keys_.size() * 3) grow();
-    const uint64_t mask = keys_.size() - 1;
-    uint64_t i = fo_mix64(k) & mask;
-    while (vals_[i] != SUB_NONE) i = (i + 1) & mask;
-    keys_[i] = k;
-    vals_[i] = v;
-    ++size_;
-  }
-
- private:
-  void grow() {
-    const uint64_t cap = std::max<uint64_t>(1024, keys_.size() * 2);
-    std::vector<uint64_t> ok;
-    std::vector<uint32_t> ov;
-    ok.swap(keys_);
-    ov.swap(vals_);
-    keys_.assign(cap, 0);
-    vals_.assign(cap, SUB_NONE);
-    size_ = 0;
-    for (uint64_t i = 0; i < ok.size(); ++i)
-      if (ov[i] != SUB_NONE) insert_new(ok[i], ov[i]);
-  }
-  std::vector<uint64_t> keys_;
   std::vector<uint32_t> vals_;
-  uint64_t size_ = 0;
+  uint64_t used_ = 0, size_ = 0;  // used_ counts tombstones too
 };
 
 template <class T>
@@ -170,26 +156,41 @@ hipError_t fo_ensure(T*& p, uint64_t& cap, uint64_t need) {
   return e;
 }
 
+template <class T>
+void fo_hfree(T*& p) {
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+}
+
+template <class T>
+hipError_t fo_halloc(T*& p, uint64_t count) {
+  fo_hfree(p);
+  return hipHostMalloc(reinterpret_cast<void**>(&p), std::max<uint64_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+}
+
+template <class T>
+T* mapped(T* h) {
+  void* d = nullptr;
+  return hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? static_cast<T*>(d) : nullptr;
+}
+
 struct Slot {
   uint32_t filter, group;
   std::vector<uint32_t> members;  // subscription order
-  bool changed = false;
+  uint32_t mbegin = 0, mcap = 0;  // the member list's extent in the members arena
+  uint32_t live_idx = SUB_NONE;   // index in its filter's group list (SUB_NONE: no members)
+  bool dirty = false;
 };
 
-struct DevTables {
-  FilterRec* recs = nullptr;
-  uint32_t* plain = nullptr;
-  GroupRec* groups = nullptr;
-  uint32_t* members = nullptr;
-  uint32_t n_recs = 0;
-  uint64_t bytes = 0;
-  void release() {
-    fo_free(recs);
-    fo_free(plain);
-    fo_free(groups);
-    fo_free(members);
-  }
+// One device array with its capacity (elements).
+template <class T>
+struct DevArr {
+  T* p = nullptr;
+  uint64_t cap = 0;
 };
+
+constexpr uint64_t PS_INIT_CAP = 1ull << 20;
+constexpr uint64_t RANGE_COPY_MIN = 256;  // dirty ranges at least this long are copied, not patched
 
 }  // namespace
 
@@ -205,72 +206,85 @@ struct FoScratch {
   uint64_t cap_eoff = 0;
   uint64_t* partials = nullptr;
   uint64_t cap_partials = 0;
+  uint32_t* next = nullptr;  // pick chains (round_robin / sticky), by output position
+  uint64_t cap_next = 0;
+  unsigned long long* heads = nullptr;  // per pick-state entry (sized to the table)
+  uint32_t* touched = nullptr;
+  uint64_t cap_heads = 0;
+  unsigned long long* ctl = nullptr;
+  uint32_t stamp = 0;
   uint64_t* h_sum = nullptr;  // host-mapped call summary (synchronous calls)
+  hipEvent_t done = nullptr;  // end of the last fan-out enqueued on this stream
+  bool used = false;
   void release() {
     fo_free(entry_topic);
     fo_free(ecount);
     fo_free(eoff);
     fo_free(partials);
-    if (h_sum) (void)hipHostFree(h_sum);
-    h_sum = nullptr;
+    fo_free(next);
+    fo_free(heads);
+    fo_free(touched);
+    fo_free(ctl);
+    fo_hfree(h_sum);
+    if (done) (void)hipEventDestroy(done);
+    done = nullptr;
   }
 };
 
+struct PubBatchPriv;
+
 struct emqx_subtab {
   int device = 0;
-  std::mutex mu;  // serialises mutations, commits and fan-out calls
-  // host store
-  std::vector<std::vector<uint32_t>> plain;   // filter id -> plain subscribers
-  U64Set plain_set;                            // (filter << 32) | sub
-  U64Map slot_of;                              // (filter << 32) | group -> slot
+  std::mutex mu;  // serialises mutations, commits and fan-out enqueues
+  // ---- host store, and the image of every device array ----
+  std::vector<FilterRec> recs;                // per filter id
+  std::vector<uint32_t> pcap, gcap;           // capacities of the filter's plain / group extents
+  std::vector<uint32_t> plain;                // plain arena
+  std::vector<GroupRec> groups;               // group-record arena
+  std::vector<uint32_t> members;              // member arena
+  uint64_t garbage = 0;                       // words of extents moved away from
+  U64Map plain_pos;                           // (filter << 32 | sub) -> index in the plain list
+  U64Map slot_of;                             // (filter << 32 | group) -> slot
   std::vector<Slot> slots;
-  std::vector<std::vector<uint32_t>> fslots;   // filter id -> its slots (creation order)
-  U64Set member_set;                           // (slot << 32) | sub
-  uint64_t n_members = 0;
-  // device
-  DevTables dev;
-  GroupState* state = nullptr;
-  uint64_t state_cap = 0;
-  uint64_t state_n = 0;                        // slots with device state
-  uint64_t n_live_groups = 0;
-  hipStream_t stream = nullptr;
+  std::vector<std::vector<uint32_t>> fslots;  // filter id -> its slots (creation order)
+  U64Map member_set;                          // (slot << 32 | sub) -> 1
+  uint64_t n_members = 0, n_live_groups = 0;
+  // ---- changes since the last commit ----
+  std::vector<std::pair<uint64_t, uint64_t>> dirty_plain;  // (first word, words)
+  std::vector<uint32_t> dirty_recs, dirty_slots, dirty_glists;
+  std::vector<uint8_t> rec_flag, glist_flag;  // per filter: listed in dirty_recs / dirty_glists
+  bool need_full = true;
+  uint64_t ops_pending = 0;                   // mutations since the last commit
+  bool bulk = false;                          // so many that the next commit rebuilds: no dirt kept
+  // ---- device ----
+  DevArr<FilterRec> d_recs;
+  DevArr<uint32_t> d_plain, d_members;
+  DevArr<GroupRec> d_groups;
+  uint32_t dev_n_recs = 0;
+  hipStream_t stream = nullptr;       // commits and table maintenance
+  hipEvent_t commit_ev = nullptr;     // end of the last commit: later fan-outs wait for it
+  bool commit_pending = false;
+  std::vector<WordPatch> wpatch;
+  std::vector<RecPatch> rpatch;
+  DevArr<WordPatch> d_wpatch;
+  DevArr<RecPatch> d_rpatch;
+  // pick state per (group slot, publisher)
+  uint64_t* ps_keys = nullptr;
+  uint32_t* ps_vals = nullptr;
+  unsigned long long* ps_count = nullptr;
+  uint64_t ps_cap = 0;
+  unsigned long long* h_ps_seen = nullptr;  // host-mapped: occupancy after the last finished call
   std::vector<std::unique_ptr<FoScratch>> scratch;  // one per stream that called
   uint64_t* h_total = nullptr;
   uint32_t seed = 0x2545F491u;
-  // emqx_publish_batch staging
-  uint8_t* d_tbytes = nullptr;
-  uint64_t cap_tbytes = 0;
-  uint64_t* d_toffs = nullptr;
-  uint64_t cap_toffs = 0;
-  uint64_t* d_moff = nullptr;
-  uint64_t cap_moff = 0;
-  uint32_t* d_mids = nullptr;
-  uint64_t cap_mids = 0;
-  uint32_t* d_keys = nullptr;
-  uint64_t cap_keys = 0;
-  uint64_t* d_ooff = nullptr;
-  uint64_t cap_ooff = 0;
-  uint32_t* d_osubs = nullptr;
-  uint64_t cap_osubs = 0;
-  uint32_t* d_ofil = nullptr;
-  uint64_t cap_ofil = 0;
+  // commit statistics (emqx_subtab_commit_stats)
+  uint64_t st_commits = 0, st_full = 0, st_words = 0, st_records = 0, st_moves = 0, st_last_kind = 0;
+  double st_host_us = 0, st_total_us = 0;
+  // pinned publish batches of emqx_publish_batch (pool)
+  std::mutex pb_mu;
+  std::vector<emqx_pub_batch*> pb_free;
 
-  ~emqx_subtab() {
-    (void)hipSetDevice(device);
-    dev.release();
-    fo_free(state);
-    for (auto& c : scratch) c->release();
-    fo_free(d_tbytes);
-    fo_free(d_toffs);
-    fo_free(d_moff);
-    fo_free(d_mids);
-    fo_free(d_keys);
-    fo_free(d_ooff);
-    fo_free(d_osubs);
-    fo_free(d_ofil);
-    if (h_total) (void)hipHostFree(h_total);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
+  ~emqx_subtab();
 };
 
 namespace {
@@ -282,114 +296,501 @@ bool ids_ok(const uint32_t* f, const uint32_t* s, uint64_t n) {
   return true;
 }
 
-int commit_locked(emqx_subtab* s) {
-  FO_TRY(hipSetDevice(s->device));
-  // ---- host build -----------------------------------------------------------------
-  const uint64_t nf = std::max(s->plain.size(), s->fslots.size());
-  if (nf >= FANOUT_SHARED_BIT) return EMQX_EINVAL;
-  std::vector<FilterRec> recs(nf);
-  std::vector<uint32_t> plain, members;
-  std::vector<GroupRec> groups;
-  plain.reserve(s->plain_set.size());
-  members.reserve(s->n_members);
-  uint64_t live_groups = 0;
-  for (uint64_t f = 0; f < nf; ++f) {
-    FilterRec r{static_cast<uint32_t>(plain.size()), 0, static_cast<uint32_t>(groups.size()), 0};
-    if (f < s->plain.size()) {
-      const auto& v = s->plain[f];
-      plain.insert(plain.end(), v.begin(), v.end());
-      r.n_plain = static_cast<uint32_t>(v.size());
-    }
-    if (f < s->fslots.size()) {
-      for (uint32_t sl : s->fslots[f]) {
-        const Slot& slot = s->slots[sl];
-        if (slot.members.empty()) continue;  // no members -> no {Group, node()} route
-        groups.push_back(GroupRec{static_cast<uint32_t>(members.size()), static_cast<uint32_t>(slot.members.size()),
-                                  sl, slot.group});
-        members.insert(members.end(), slot.members.begin(), slot.members.end());
-        ++live_groups;
-      }
-      r.n_groups = static_cast<uint32_t>(groups.size()) - r.group_begin;
-    }
-    recs[f] = r;
-  }
-  if (plain.size() >= (1ull << 32) || members.size() >= (1ull << 32) || groups.size() >= (1ull << 32))
-    return EMQX_ENOMEM;
+void ensure_filter(emqx_subtab* s, uint32_t f) {
+  if (f < s->recs.size()) return;
+  const uint64_t n = uint64_t(f) + 1;
+  s->recs.resize(n, FilterRec{0, 0, 0, 0});
+  s->pcap.resize(n, 0);
+  s->gcap.resize(n, 0);
+  s->rec_flag.resize(n, 0);
+  s->glist_flag.resize(n, 0);
+  if (s->fslots.size() < n) s->fslots.resize(n);
+}
 
-  // ---- pick state: keep counters, drop sticky picks of members that left ------------
-  const uint64_t nslots = s->slots.size();
-  std::vector<GroupState> st(nslots, GroupState{0, SUB_NONE});
-  if (s->state_n) FO_TRY(hipMemcpy(st.data(), s->state, s->state_n * sizeof(GroupState), hipMemcpyDeviceToHost));
-  for (uint64_t i = 0; i < nslots; ++i) {
-    Slot& sl = s->slots[i];
-    if (sl.changed && st[i].sticky != SUB_NONE && !s->member_set.contains((i << 32) | st[i].sticky))
-      st[i].sticky = SUB_NONE;
-    sl.changed = false;
-  }
+// A bulk load (more mutations before a commit than a quarter of the table, at least 64K) is
+// cheaper as one full upload than as patches: past that point no dirt is recorded.
+void note_op(emqx_subtab* s) {
+  if (s->bulk || ++s->ops_pending <= std::max<uint64_t>(1u << 16, (s->plain_pos.size() + s->n_members) / 4)) return;
+  s->bulk = true;
+  std::vector<std::pair<uint64_t, uint64_t>>().swap(s->dirty_plain);
+  std::vector<uint32_t>().swap(s->dirty_recs);
+  std::vector<uint32_t>().swap(s->dirty_slots);
+  std::vector<uint32_t>().swap(s->dirty_glists);
+}
 
-  // ---- upload (the old tables are released after the new ones are in place) ---------
-  DevTables d;
-  auto up = [&](auto*& p, const auto& v) -> hipError_t {
-    hipError_t e = fo_alloc(p, v.size());
-    if (e == hipSuccess && !v.empty()) e = hipMemcpy(p, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice);
-    return e;
-  };
-  if (up(d.recs, recs) != hipSuccess || up(d.plain, plain) != hipSuccess || up(d.groups, groups) != hipSuccess ||
-      up(d.members, members) != hipSuccess) {
-    d.release();
-    return EMQX_ENOMEM;
+void mark_rec(emqx_subtab* s, uint32_t f) {
+  if (s->bulk) return;
+  if (!s->rec_flag[f]) {
+    s->rec_flag[f] = 1;
+    s->dirty_recs.push_back(f);
   }
-  d.n_recs = static_cast<uint32_t>(nf);
-  d.bytes = recs.size() * sizeof(FilterRec) + plain.size() * 4 + groups.size() * sizeof(GroupRec) + members.size() * 4;
-  if (nslots > s->state_cap) {
-    GroupState* ns = nullptr;
-    const uint64_t cap = std::max<uint64_t>(1024, nslots * 2);
-    if (fo_alloc(ns, cap) != hipSuccess) {
-      d.release();
-      return EMQX_ENOMEM;
-    }
-    fo_free(s->state);
-    s->state = ns;
-    s->state_cap = cap;
+}
+
+void mark_glist(emqx_subtab* s, uint32_t f) {
+  if (s->bulk) return;
+  if (!s->glist_flag[f]) {
+    s->glist_flag[f] = 1;
+    s->dirty_glists.push_back(f);
   }
-  if (nslots) FO_TRY(hipMemcpy(s->state, st.data(), nslots * sizeof(GroupState), hipMemcpyHostToDevice));
-  s->state_n = nslots;
-  s->dev.release();
-  s->dev = d;
-  s->n_live_groups = live_groups;
+}
+
+void mark_slot(emqx_subtab* s, uint32_t sl) {
+  if (s->bulk) return;
+  if (!s->slots[sl].dirty) {
+    s->slots[sl].dirty = true;
+    s->dirty_slots.push_back(sl);
+  }
+}
+
+uint32_t grow_cap(uint64_t n, uint32_t min_cap) {
+  return static_cast<uint32_t>(std::max<uint64_t>(min_cap, n + (n >> 1) + 1));
+}
+
+void plain_add(emqx_subtab* s, uint32_t f, uint32_t sub) {
+  const uint64_t key = (uint64_t(f) << 32) | sub;
+  ensure_filter(s, f);
+  FilterRec& r = s->recs[f];
+  if (!s->plain_pos.insert(key, r.n_plain)) return;  // ETS bag: a pair is stored once
+  if (r.n_plain == s->pcap[f]) {  // the extent is full: move the list to the arena's end
+    const uint64_t nb = s->plain.size();
+    const uint32_t cap = std::max<uint32_t>(4, 2 * r.n_plain);
+    s->plain.resize(nb + cap);
+    std::copy(s->plain.begin() + r.plain_begin, s->plain.begin() + r.plain_begin + r.n_plain, s->plain.begin() + nb);
+    if (r.n_plain && !s->bulk) s->dirty_plain.emplace_back(nb, r.n_plain);
+    s->garbage += s->pcap[f];
+    r.plain_begin = static_cast<uint32_t>(nb);
+    s->pcap[f] = cap;
+    ++s->st_moves;
+  }
+  const uint64_t w = uint64_t(r.plain_begin) + r.n_plain;
+  s->plain[w] = sub;
+  if (!s->bulk) s->dirty_plain.emplace_back(w, 1);
+  r.n_plain += 1;
+  mark_rec(s, f);
+  note_op(s);
+}
+
+void plain_remove(emqx_subtab* s, uint32_t f, uint32_t sub) {
+  const uint64_t key = (uint64_t(f) << 32) | sub;
+  const uint32_t pos = s->plain_pos.find(key);
+  if (pos == SUB_NONE) return;
+  s->plain_pos.erase(key);
+  FilterRec& r = s->recs[f];
+  const uint32_t last = r.n_plain - 1;
+  if (pos != last) {  // the last subscriber fills the hole (plain order carries no meaning)
+    const uint32_t moved = s->plain[uint64_t(r.plain_begin) + last];
+    s->plain[uint64_t(r.plain_begin) + pos] = moved;
+    s->plain_pos.assign((uint64_t(f) << 32) | moved, pos);
+    if (!s->bulk) s->dirty_plain.emplace_back(uint64_t(r.plain_begin) + pos, 1);
+  }
+  r.n_plain = last;
+  mark_rec(s, f);
+  note_op(s);
+}
+
+// ---- device side of a commit ----------------------------------------------------------------
+
+// Orders the commit stream after every fan-out in flight.
+int barrier_after_fanouts(emqx_subtab* s) {
+  for (auto& c : s->scratch)
+    if (c->used) FO_TRY(hipStreamWaitEvent(s->stream, c->done, 0));
   return EMQX_OK;
 }
 
-// The fan-out pipeline on device buffers (s->mu held).
+// Grows a device array to hold `need` elements, keeping its first `keep` elements.
+template <class T>
+int dev_reserve(emqx_subtab* s, DevArr<T>& a, uint64_t need, uint64_t keep, std::vector<T*>& retired) {
+  if (need <= a.cap && a.p) return EMQX_OK;
+  const uint64_t cap = std::max<uint64_t>(need + need / 2, 1u << 16);
+  T* p = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&p), cap * sizeof(T)) != hipSuccess) return EMQX_ENOMEM;
+  if (keep && a.p) FO_TRY(hipMemcpyAsync(p, a.p, keep * sizeof(T), hipMemcpyDeviceToDevice, s->stream));
+  if (cap > keep) FO_TRY(hipMemsetAsync(p + keep, 0, (cap - keep) * sizeof(T), s->stream));
+  if (a.p) retired.push_back(a.p);
+  a.p = p;
+  a.cap = cap;
+  return EMQX_OK;
+}
+
+// Rebuilds the image compactly (every extent with a quarter of slack) and marks it all dirty.
+void compact_image(emqx_subtab* s) {
+  const uint64_t nf = s->recs.size();
+  std::vector<uint32_t> plain;
+  std::vector<GroupRec> groups;
+  std::vector<uint32_t> members;
+  plain.reserve(s->plain_pos.size() + s->plain_pos.size() / 4 + 4 * nf);
+  members.reserve(s->n_members + s->n_members / 4);
+  s->n_live_groups = 0;
+  for (uint64_t f = 0; f < nf; ++f) {
+    FilterRec& r = s->recs[f];
+    const uint32_t pb = static_cast<uint32_t>(plain.size());
+    const uint32_t pc = r.n_plain ? r.n_plain + (r.n_plain >> 2) + 1 : 0;
+    plain.insert(plain.end(), s->plain.begin() + r.plain_begin, s->plain.begin() + r.plain_begin + r.n_plain);
+    plain.resize(uint64_t(pb) + pc, 0);
+    r.plain_begin = pb;
+    s->pcap[f] = pc;
+    const uint32_t gb = static_cast<uint32_t>(groups.size());
+    uint32_t ng = 0;
+    for (uint32_t sl : s->fslots[f]) {
+      Slot& S = s->slots[sl];
+      S.dirty = false;
+      S.live_idx = SUB_NONE;
+      const uint32_t nm = static_cast<uint32_t>(S.members.size());
+      S.mbegin = static_cast<uint32_t>(members.size());
+      S.mcap = nm ? nm + (nm >> 2) + 1 : 0;
+      members.insert(members.end(), S.members.begin(), S.members.end());
+      members.resize(uint64_t(S.mbegin) + S.mcap, 0);
+      if (!nm) continue;
+      S.live_idx = ng++;
+      groups.push_back(GroupRec{S.mbegin, nm, sl, S.group});
+    }
+    const uint32_t gc = ng ? ng + (ng >> 2) + 1 : 0;
+    groups.resize(uint64_t(gb) + gc, GroupRec{0, 0, 0, 0});
+    r.group_begin = gb;
+    r.n_groups = ng;
+    s->gcap[f] = gc;
+    s->n_live_groups += ng;
+  }
+  s->plain.swap(plain);
+  s->groups.swap(groups);
+  s->members.swap(members);
+  s->garbage = 0;
+  s->dirty_plain.clear();
+  s->dirty_recs.clear();
+  s->dirty_slots.clear();
+  s->dirty_glists.clear();
+  std::fill(s->rec_flag.begin(), s->rec_flag.end(), 0);
+  std::fill(s->glist_flag.begin(), s->glist_flag.end(), 0);
+}
+
+// Full commit: the compacted image uploaded into fresh device arrays.
+int full_commit(emqx_subtab* s) {
+  compact_image(s);
+  // the old plain positions are indices into the lists, which compaction keeps: nothing to redo
+  DevArr<FilterRec> recs;
+  DevArr<uint32_t> plain, members;
+  DevArr<GroupRec> groups;
+  auto up = [&](auto& d, const auto& v) -> int {
+    d.cap = std::max<uint64_t>(v.size() + v.size() / 2, 1u << 16);
+    if (hipMalloc(reinterpret_cast<void**>(&d.p), d.cap * sizeof(v[0])) != hipSuccess) return EMQX_ENOMEM;
+    FO_TRY(hipMemsetAsync(d.p, 0, d.cap * sizeof(v[0]), s->stream));
+    if (!v.empty()) FO_TRY(hipMemcpyAsync(d.p, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice, s->stream));
+    return EMQX_OK;
+  };
+  int rc = up(recs, s->recs);
+  if (rc == EMQX_OK) rc = up(plain, s->plain);
+  if (rc == EMQX_OK) rc = up(groups, s->groups);
+  if (rc == EMQX_OK) rc = up(members, s->members);
+  if (rc == EMQX_OK && hipStreamSynchronize(s->stream) != hipSuccess) rc = EMQX_EDEVICE;
+  if (rc != EMQX_OK) {
+    fo_free(recs.p);
+    fo_free(plain.p);
+    fo_free(groups.p);
+    fo_free(members.p);
+    return rc;
+  }
+  fo_free(s->d_recs.p);
+  fo_free(s->d_plain.p);
+  fo_free(s->d_groups.p);
+  fo_free(s->d_members.p);
+  s->d_recs = recs;
+  s->d_plain = plain;
+  s->d_groups = groups;
+  s->d_members = members;
+  s->dev_n_recs = static_cast<uint32_t>(s->recs.size());
+  s->st_words += s->plain.size() + s->members.size();
+  s->st_records += s->recs.size() + s->groups.size();
+  s->need_full = false;
+  ++s->st_full;
+  s->st_last_kind = 0;
+  return EMQX_OK;
+}
+
+// Incremental commit: member lists and group lists of the changed slots / filters are
+// rewritten in the image (moved to the arena's end when they outgrow their extent); then the
+// touched words and records go to the device.
+int live_commit(emqx_subtab* s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::pair<uint64_t, uint64_t>> member_ranges;
+  std::vector<uint64_t> group_idx;
+  for (uint32_t sl : s->dirty_slots) {
+    Slot& S = s->slots[sl];
+    S.dirty = false;
+    const uint32_t nm = static_cast<uint32_t>(S.members.size());
+    if (nm > S.mcap) {
+      s->garbage += S.mcap;
+      S.mbegin = static_cast<uint32_t>(s->members.size());
+      S.mcap = grow_cap(nm, 4);
+      s->members.resize(uint64_t(S.mbegin) + S.mcap, 0);
+      ++s->st_moves;
+    }
+    std::copy(S.members.begin(), S.members.end(), s->members.begin() + S.mbegin);
+    if (nm) member_ranges.emplace_back(S.mbegin, nm);
+    const bool was_live = S.live_idx != SUB_NONE;
+    if (was_live != (nm > 0)) {
+      mark_glist(s, S.filter);
+    } else if (nm) {
+      const uint64_t gi = uint64_t(s->recs[S.filter].group_begin) + S.live_idx;
+      s->groups[gi] = GroupRec{S.mbegin, nm, sl, S.group};
+      group_idx.push_back(gi);
+    }
+  }
+  for (uint32_t f : s->dirty_glists) {
+    s->glist_flag[f] = 0;
+    uint32_t ng = 0;
+    for (uint32_t sl : s->fslots[f]) ng += s->slots[sl].members.empty() ? 0u : 1u;
+    FilterRec& r = s->recs[f];
+    s->n_live_groups = s->n_live_groups - r.n_groups + ng;
+    if (ng > s->gcap[f]) {
+      s->garbage += s->gcap[f];
+      r.group_begin = static_cast<uint32_t>(s->groups.size());
+      s->gcap[f] = grow_cap(ng, 2);
+      s->groups.resize(uint64_t(r.group_begin) + s->gcap[f], GroupRec{0, 0, 0, 0});
+      ++s->st_moves;
+    }
+    uint32_t k = 0;
+    for (uint32_t sl : s->fslots[f]) {
+      Slot& S = s->slots[sl];
+      S.live_idx = SUB_NONE;
+      if (S.members.empty()) continue;
+      S.live_idx = k;
+      s->groups[uint64_t(r.group_begin) + k] = GroupRec{S.mbegin, static_cast<uint32_t>(S.members.size()), sl, S.group};
+      group_idx.push_back(uint64_t(r.group_begin) + k);
+      ++k;
+    }
+    r.n_groups = ng;
+    mark_rec(s, f);
+  }
+  if (s->plain.size() >= (1ull << 32) || s->members.size() >= (1ull << 32) || s->groups.size() >= (1ull << 32))
+    return EMQX_ENOMEM;
+
+  // ---- patches ----
+  s->wpatch.clear();
+  s->rpatch.clear();
+  std::vector<std::pair<uint64_t, uint64_t>> copies_plain, copies_members;
+  auto words = [&](const std::vector<std::pair<uint64_t, uint64_t>>& ranges, const std::vector<uint32_t>& img,
+                   std::vector<std::pair<uint64_t, uint64_t>>& copies) {
+    for (const auto& rg : ranges) {
+      if (rg.second >= RANGE_COPY_MIN) {
+        copies.push_back(rg);
+        continue;
+      }
+      for (uint64_t w = rg.first; w < rg.first + rg.second; ++w)
+        s->wpatch.push_back(WordPatch{static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32), img[w], 0});
+    }
+  };
+  words(s->dirty_plain, s->plain, copies_plain);
+  const uint64_t n_plain_w = s->wpatch.size();
+  words(member_ranges, s->members, copies_members);
+  const uint64_t n_member_w = s->wpatch.size() - n_plain_w;
+  std::sort(group_idx.begin(), group_idx.end());
+  group_idx.erase(std::unique(group_idx.begin(), group_idx.end()), group_idx.end());
+  for (uint64_t gi : group_idx) {
+    const GroupRec& g = s->groups[gi];
+    s->rpatch.push_back(RecPatch{static_cast<uint32_t>(gi), {0, 0, 0}, make_uint4(g.member_begin, g.n_members, g.slot, g.group_id)});
+  }
+  const uint64_t n_group_p = s->rpatch.size();
+  for (uint32_t f : s->dirty_recs) {
+    s->rec_flag[f] = 0;
+    const FilterRec& r = s->recs[f];
+    s->rpatch.push_back(RecPatch{f, {0, 0, 0}, make_uint4(r.plain_begin, r.n_plain, r.group_begin, r.n_groups)});
+  }
+  const uint64_t n_rec_p = s->rpatch.size() - n_group_p;
+  const auto t1 = std::chrono::steady_clock::now();
+
+  // ---- device: after the fan-outs in flight, before the next ones ----
+  int rc = barrier_after_fanouts(s);
+  std::vector<FilterRec*> rr;
+  std::vector<uint32_t*> ru;
+  std::vector<GroupRec*> rg;
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_recs, s->recs.size(), s->dev_n_recs, rr);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_plain, s->plain.size(), s->d_plain.cap, ru);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_members, s->members.size(), s->d_members.cap, ru);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_groups, s->groups.size(), s->d_groups.cap, rg);
+  if (rc == EMQX_OK) {
+    for (const auto& c : copies_plain)
+      if (hipMemcpyAsync(s->d_plain.p + c.first, s->plain.data() + c.first, c.second * 4, hipMemcpyHostToDevice,
+                         s->stream) != hipSuccess)
+        rc = EMQX_EDEVICE;
+    for (const auto& c : copies_members)
+      if (hipMemcpyAsync(s->d_members.p + c.first, s->members.data() + c.first, c.second * 4, hipMemcpyHostToDevice,
+                         s->stream) != hipSuccess)
+        rc = EMQX_EDEVICE;
+  }
+  if (rc == EMQX_OK && !s->wpatch.empty()) {
+    if (fo_ensure(s->d_wpatch.p, s->d_wpatch.cap, s->wpatch.size()) != hipSuccess ||
+        hipMemcpyAsync(s->d_wpatch.p, s->wpatch.data(), s->wpatch.size() * sizeof(WordPatch), hipMemcpyHostToDevice,
+                       s->stream) != hipSuccess)
+      rc = EMQX_EDEVICE;
+  }
+  if (rc == EMQX_OK && !s->rpatch.empty()) {
+    if (fo_ensure(s->d_rpatch.p, s->d_rpatch.cap, s->rpatch.size()) != hipSuccess ||
+        hipMemcpyAsync(s->d_rpatch.p, s->rpatch.data(), s->rpatch.size() * sizeof(RecPatch), hipMemcpyHostToDevice,
+                       s->stream) != hipSuccess)
+      rc = EMQX_EDEVICE;
+  }
+  if (rc == EMQX_OK &&
+      launch_subtab_patches(s->d_plain.p, s->d_members.p, s->d_wpatch.p, n_plain_w, n_member_w, s->d_groups.p,
+                            s->d_recs.p, s->d_rpatch.p, n_group_p, n_rec_p, s->stream) != hipSuccess)
+    rc = EMQX_EDEVICE;
+  if (hipStreamSynchronize(s->stream) != hipSuccess && rc == EMQX_OK) rc = EMQX_EDEVICE;
+  for (auto* p : rr) (void)hipFree(p);
+  for (auto* p : ru) (void)hipFree(p);
+  for (auto* p : rg) (void)hipFree(p);
+  if (rc != EMQX_OK) {
+    s->need_full = true;  // the device copy is in an unknown state: the next commit rebuilds it
+    return rc;
+  }
+  s->dev_n_recs = static_cast<uint32_t>(s->recs.size());
+  s->dirty_plain.clear();
+  s->dirty_recs.clear();
+  s->dirty_slots.clear();
+  s->dirty_glists.clear();
+  uint64_t cw = 0;
+  for (const auto& c : copies_plain) cw += c.second;
+  for (const auto& c : copies_members) cw += c.second;
+  s->st_words += n_plain_w + n_member_w + cw;
+  s->st_records += n_group_p + n_rec_p;
+  s->st_host_us = std::chrono::duration<double, std::micro>(t1 - t0).count();
+  s->st_last_kind = 1;
+  return EMQX_OK;
+}
+
+int commit_locked(emqx_subtab* s) {
+  FO_TRY(hipSetDevice(s->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  if (s->recs.size() >= FANOUT_SHARED_BIT) return EMQX_EINVAL;
+  const uint64_t live = s->plain_pos.size() + s->n_members + s->recs.size();
+  int rc;
+  if (s->need_full || s->bulk || s->garbage > std::max<uint64_t>(1u << 20, live)) {
+    int b = barrier_after_fanouts(s);
+    rc = b != EMQX_OK ? b : full_commit(s);
+  } else {
+    rc = live_commit(s);
+  }
+  if (rc != EMQX_OK) return rc;
+  s->ops_pending = 0;
+  s->bulk = false;
+  FO_TRY(hipEventRecord(s->commit_ev, s->stream));
+  s->commit_pending = true;
+  ++s->st_commits;
+  s->st_total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  return EMQX_OK;
+}
+
+// ---- pick state -----------------------------------------------------------------------------
+
+int ps_alloc(uint64_t cap, uint64_t*& keys, uint32_t*& vals, hipStream_t st) {
+  keys = nullptr;
+  vals = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&keys), cap * sizeof(uint64_t)) != hipSuccess) return EMQX_ENOMEM;
+  if (hipMalloc(reinterpret_cast<void**>(&vals), cap * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipFree(keys);
+    keys = nullptr;
+    return EMQX_ENOMEM;
+  }
+  FO_TRY(hipMemsetAsync(keys, 0xFF, cap * sizeof(uint64_t), st));  // PS_EMPTY
+  FO_TRY(hipMemsetAsync(vals, 0xFF, cap * sizeof(uint32_t), st));  // PS_NOVAL
+  return EMQX_OK;
+}
+
+// The table exists and is at most half full (as of the last finished call); growing it waits
+// for the fan-outs in flight.  Per-stream chain heads follow the table's size.
+int ps_ready(emqx_subtab* s) {
+  if (!s->ps_keys) {
+    if (!s->ps_count) FO_TRY(fo_alloc(s->ps_count, 1));
+    FO_TRY(hipMemsetAsync(s->ps_count, 0, sizeof(unsigned long long), s->stream));
+    int rc = ps_alloc(PS_INIT_CAP, s->ps_keys, s->ps_vals, s->stream);
+    if (rc != EMQX_OK) return rc;
+    FO_TRY(hipStreamSynchronize(s->stream));
+    s->ps_cap = PS_INIT_CAP;
+    return EMQX_OK;
+  }
+  if (*s->h_ps_seen * 2 <= s->ps_cap) return EMQX_OK;
+  int rc = barrier_after_fanouts(s);
+  if (rc != EMQX_OK) return rc;
+  const uint64_t cap = s->ps_cap * 4;
+  uint64_t* keys;
+  uint32_t* vals;
+  rc = ps_alloc(cap, keys, vals, s->stream);
+  if (rc != EMQX_OK) return rc;
+  FO_TRY(hipMemsetAsync(s->ps_count, 0, sizeof(unsigned long long), s->stream));
+  FO_TRY(launch_ps_rehash(s->ps_keys, s->ps_vals, s->ps_cap, keys, vals, cap - 1, s->ps_count, s->stream));
+  FO_TRY(hipStreamSynchronize(s->stream));
+  fo_free(s->ps_keys);
+  fo_free(s->ps_vals);
+  s->ps_keys = keys;
+  s->ps_vals = vals;
+  s->ps_cap = cap;
+  FO_TRY(hipMemcpy(s->h_ps_seen, s->ps_count, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return EMQX_OK;
+}
+
+// ---- the fan-out pipeline ---------------------------------------------------------------------
+
 FoScratch* scratch_for(emqx_subtab* s, hipStream_t st) {
   for (auto& c : s->scratch)
     if (c->stream == st) return c.get();
-  s->scratch.push_back(std::make_unique<FoScratch>());
-  s->scratch.back()->stream = st;
+  auto c = std::make_unique<FoScratch>();
+  c->stream = st;
+  if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) return nullptr;
+  s->scratch.push_back(std::move(c));
   return s->scratch.back().get();
 }
 
-// Enqueue the fan-out of one match CSR on st, no host synchronisation; m_cap bounds the
-// match entries (sizes the scratch); the summary goes to `summary` (FO_SUM_WORDS u64).
+// Enqueue the fan-out of one match CSR on st, no host synchronisation (s->mu held); m_cap
+// bounds the match entries (sizes the scratch; a longer CSR is refused on the device, as is
+// one whose match summary `msum` reports a problem); the summary goes to `summary`
+// (FO_SUM_WORDS u64).
 int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const uint32_t* d_mids, uint64_t n,
                    uint64_t m_cap, const uint32_t* d_keys, uint64_t* d_out_off, uint32_t* d_out_subs,
-                   uint32_t* d_out_fil, uint64_t cap, uint64_t* summary, hipStream_t st) {
+                   uint32_t* d_out_fil, uint64_t cap, uint64_t* summary, hipStream_t st, const uint64_t* msum) {
   FoScratch* c = scratch_for(s, st);
-  const bool hash = strategy == EMQX_SHARE_HASH_CLIENTID || strategy == EMQX_SHARE_HASH_TOPIC;
-  if (hash) FO_TRY(fo_ensure(c->entry_topic, c->cap_entry_topic, m_cap));
+  if (!c) return EMQX_EDEVICE;
+  const bool stateful = fo_stateful(strategy);
+  if (!d_out_subs) cap = 0;
+  if (stateful && cap >= (1ull << 32)) return EMQX_EINVAL;  // chain links are 32-bit positions
+  if (stateful) {
+    int rc = ps_ready(s);
+    if (rc != EMQX_OK) return rc;
+    if (c->cap_heads != s->ps_cap) {  // (a new table: the stream's earlier calls have drained)
+      FO_TRY(fo_alloc(c->heads, s->ps_cap));
+      FO_TRY(fo_alloc(c->touched, s->ps_cap));
+      FO_TRY(hipMemsetAsync(c->heads, 0, s->ps_cap * sizeof(unsigned long long), st));
+      c->cap_heads = s->ps_cap;
+    }
+    FO_TRY(fo_ensure(c->next, c->cap_next, cap));
+    if (++c->stamp == 0) c->stamp = 1;
+  }
+  if (d_keys && strategy != EMQX_SHARE_RANDOM) FO_TRY(fo_ensure(c->entry_topic, c->cap_entry_topic, m_cap));
   FO_TRY(fo_ensure(c->ecount, c->cap_ecount, m_cap));
   FO_TRY(fo_ensure(c->eoff, c->cap_eoff, m_cap + 1));
   FO_TRY(fo_ensure(c->partials, c->cap_partials, 2 * FO_BLOCKS));
+  if (!c->ctl) FO_TRY(fo_alloc(c->ctl, FO_CTL_WORDS));
+  if (!s->ps_count) FO_TRY(fo_alloc(s->ps_count, 1));
+  if (s->commit_pending) FO_TRY(hipStreamWaitEvent(st, s->commit_ev, 0));
+  FO_TRY(hipMemsetAsync(c->ctl, 0, FO_CTL_WORDS * sizeof(unsigned long long), st));
   FanoutArgs a{};
-  a.recs = s->dev.recs;
-  a.n_recs = s->dev.n_recs;
-  a.plain = s->dev.plain;
-  a.groups = s->dev.groups;
-  a.members = s->dev.members;
-  a.state = s->state;
+  a.recs = s->d_recs.p;
+  a.n_recs = s->dev_n_recs;
+  a.plain = s->d_plain.p;
+  a.groups = s->d_groups.p;
+  a.members = s->d_members.p;
+  a.ps_keys = s->ps_keys;
+  a.ps_vals = s->ps_vals;
+  a.ps_count = s->ps_count;
+  a.ps_mask = s->ps_cap ? s->ps_cap - 1 : 0;
+  a.heads = c->heads;
+  a.stamp = c->stamp;
+  a.next = c->next;
+  a.touched = c->touched;
+  a.ctl = c->ctl;
+  a.ps_seen = mapped(s->h_ps_seen);
   a.moff = d_moff;
   a.mids = d_mids;
   a.n = n;
+  a.m_cap = m_cap;
+  a.msum = msum;
   a.keys = d_keys;
   a.strategy = strategy;
   s->seed = s->seed * 1664525u + 1013904223u;
@@ -401,9 +802,11 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   a.out_off = d_out_off;
   a.out_subs = d_out_subs;
   a.out_filters = d_out_fil;
-  a.cap = d_out_subs ? cap : 0;
+  a.cap = cap;
   a.summary = summary;
   FO_TRY(launch_fanout(a, m_cap, st));
+  FO_TRY(hipEventRecord(c->done, st));
+  c->used = true;
   return EMQX_OK;
 }
 
@@ -413,14 +816,14 @@ int run_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const 
                uint64_t m, const uint32_t* d_keys, uint64_t* d_out_off, uint32_t* d_out_subs, uint32_t* d_out_fil,
                uint64_t cap, uint64_t* n_out, hipStream_t st) {
   FoScratch* c = scratch_for(s, st);
-  if (!c->h_sum)
-    FO_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_sum), FO_SUM_WORDS * sizeof(uint64_t), hipHostMallocDefault));
-  uint64_t* d_sum = nullptr;
-  FO_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_sum), c->h_sum, 0));
-  int rc = enqueue_fanout(s, strategy, d_moff, d_mids, n, m, d_keys, d_out_off, d_out_subs, d_out_fil, cap, d_sum, st);
+  if (!c) return EMQX_EDEVICE;
+  if (!c->h_sum) FO_TRY(fo_halloc(c->h_sum, FO_SUM_WORDS));
+  int rc = enqueue_fanout(s, strategy, d_moff, d_mids, n, m, d_keys, d_out_off, d_out_subs, d_out_fil, cap,
+                          mapped(c->h_sum), st, nullptr);
   if (rc != EMQX_OK) return rc;
   FO_TRY(hipStreamSynchronize(st));
   *n_out = c->h_sum[FO_SUM_TOTAL];
+  if (c->h_sum[FO_SUM_FLAGS] & FO_SUM_F_MATCH) return EMQX_EINVAL;
   if (c->h_sum[FO_SUM_FLAGS] & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
   return EMQX_OK;
 }
@@ -428,7 +831,12 @@ int run_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const 
 int ensure_stream(emqx_subtab* s) {
   if (!s->stream) {
     FO_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    FO_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->h_total), 2 * sizeof(uint64_t), hipHostMallocDefault));
+    FO_TRY(hipEventCreateWithFlags(&s->commit_ev, hipEventDisableTiming));
+    FO_TRY(fo_halloc(s->h_total, 2));
+    FO_TRY(fo_halloc(s->h_ps_seen, 1));
+    *s->h_ps_seen = 0;
+    FO_TRY(fo_alloc(s->ps_count, 1));  // (read by every call's finish kernel)
+    FO_TRY(hipMemset(s->ps_count, 0, sizeof(unsigned long long)));
   }
   return EMQX_OK;
 }
@@ -437,6 +845,183 @@ bool strategy_ok(uint32_t strategy, bool have_keys) {
   if (strategy > EMQX_SHARE_HASH_TOPIC) return false;
   if ((strategy == EMQX_SHARE_HASH_CLIENTID || strategy == EMQX_SHARE_HASH_TOPIC) && !have_keys) return false;
   return true;
+}
+
+}  // namespace
+
+// ---- pinned publish batches -------------------------------------------------------------------
+
+struct PubBatchPriv {
+  emqx_engine* e = nullptr;
+  emqx_subtab* s = nullptr;
+  uint32_t strategy = 0;
+  bool use_keys = true;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* d_tbytes = nullptr;
+  uint64_t* d_toffs = nullptr;
+  uint32_t* d_keys = nullptr;
+  uint64_t* d_moff = nullptr;
+  uint32_t* d_mids = nullptr;
+  uint64_t cap_mids = 0;
+  uint64_t* d_ooff = nullptr;
+  uint32_t* d_osubs = nullptr;
+  uint32_t* d_ofil = nullptr;
+  uint64_t* d_msum = nullptr;  // match summary (8 words) then fan-out summary (4 words)
+  uint64_t* h_sums = nullptr;  // pinned copy of both
+  uint64_t mids_per_topic = 16;  // learnt match ids per topic (sizes d_mids)
+  uint64_t limit = ~0ull;        // deliveries the submission may write (<= cap_out): a call that
+                                 // needs more writes nothing and consumes no pick state
+  bool pending = false;
+};
+
+emqx_subtab::~emqx_subtab() {
+  (void)hipSetDevice(device);
+  if (stream) (void)hipStreamSynchronize(stream);
+  for (auto& c : scratch)
+    if (c->used) (void)hipEventSynchronize(c->done);
+  for (emqx_pub_batch* b : pb_free) emqx_pub_batch_destroy(b);
+  fo_free(d_recs.p);
+  fo_free(d_plain.p);
+  fo_free(d_groups.p);
+  fo_free(d_members.p);
+  fo_free(d_wpatch.p);
+  fo_free(d_rpatch.p);
+  fo_free(ps_keys);
+  fo_free(ps_vals);
+  fo_free(ps_count);
+  for (auto& c : scratch) c->release();
+  fo_hfree(h_total);
+  fo_hfree(h_ps_seen);
+  if (commit_ev) (void)hipEventDestroy(commit_ev);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+namespace {
+
+constexpr uint64_t PB_MSUM_WORDS = 8;
+
+int pb_alloc(emqx_pub_batch* b, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_out, bool keep_inputs) {
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  FO_TRY(hipSetDevice(p->s->device));
+  if (cap_topics > b->cap_topics) {
+    uint64_t* t = nullptr;
+    uint32_t* k = nullptr;
+    FO_TRY(fo_halloc(t, cap_topics + 1));
+    FO_TRY(fo_halloc(k, cap_topics));
+    if (keep_inputs && b->topic_offsets) {
+      std::memcpy(t, b->topic_offsets, (b->cap_topics + 1) * sizeof(uint64_t));
+      std::memcpy(k, b->keys, b->cap_topics * sizeof(uint32_t));
+    }
+    fo_hfree(b->topic_offsets);
+    fo_hfree(b->keys);
+    b->topic_offsets = t;
+    b->keys = k;
+    FO_TRY(fo_halloc(b->out_offsets, cap_topics + 1));
+    FO_TRY(fo_alloc(p->d_toffs, cap_topics + 1));
+    FO_TRY(fo_alloc(p->d_keys, cap_topics));
+    FO_TRY(fo_alloc(p->d_moff, cap_topics + 1));
+    FO_TRY(fo_alloc(p->d_ooff, cap_topics + 1));
+    b->cap_topics = cap_topics;
+  }
+  if (cap_bytes > b->cap_bytes) {
+    uint8_t* t = nullptr;
+    FO_TRY(fo_halloc(t, cap_bytes + 16));
+    if (keep_inputs && b->topic_bytes) std::memcpy(t, b->topic_bytes, b->cap_bytes);
+    fo_hfree(b->topic_bytes);
+    b->topic_bytes = t;
+    FO_TRY(fo_alloc(p->d_tbytes, cap_bytes + 16));
+    b->cap_bytes = cap_bytes;
+  }
+  if (cap_out > b->cap_out) {
+    FO_TRY(fo_halloc(b->out_subs, cap_out));
+    FO_TRY(fo_halloc(b->out_filters, cap_out));
+    FO_TRY(fo_alloc(p->d_osubs, cap_out));
+    FO_TRY(fo_alloc(p->d_ofil, cap_out));
+    b->cap_out = cap_out;
+  }
+  return EMQX_OK;
+}
+
+// After the match ids of the batch are in HBM: fan-out, the delivery CSR into the pinned
+// outputs, both summaries into pinned memory (s->mu is taken here).
+int pb_enqueue_fanout(emqx_pub_batch* b, uint64_t m_cap, const uint64_t* msum) {
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  emqx_subtab* s = p->s;
+  uint64_t* fsum = p->d_msum + PB_MSUM_WORDS;
+  const uint64_t cap = std::min(b->cap_out, p->limit);
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    int rc = enqueue_fanout(s, p->strategy, p->d_moff, p->d_mids, b->n, m_cap, p->use_keys ? p->d_keys : nullptr,
+                            p->d_ooff, p->d_osubs, p->d_ofil, cap, fsum, p->stream, msum);
+    if (rc != EMQX_OK) return rc;
+  }
+  FO_TRY(launch_fanout_to_host(p->d_ooff, b->n, p->d_osubs, p->d_ofil, fsum, cap, mapped(b->out_offsets),
+                               mapped(b->out_subs), mapped(b->out_filters), p->stream));
+  FO_TRY(hipMemcpyAsync(p->h_sums, p->d_msum, (PB_MSUM_WORDS + FO_SUM_WORDS) * sizeof(uint64_t),
+                        hipMemcpyDeviceToHost, p->stream));
+  return EMQX_OK;
+}
+
+int pb_enqueue(emqx_pub_batch* b) {
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  const uint64_t n = b->n, nbytes = n ? b->topic_offsets[n] : 0;
+  hipStream_t st = p->stream;
+  if (nbytes) FO_TRY(hipMemcpyAsync(p->d_tbytes, b->topic_bytes, nbytes, hipMemcpyHostToDevice, st));
+  FO_TRY(hipMemcpyAsync(p->d_toffs, b->topic_offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  if (p->use_keys && n) FO_TRY(hipMemcpyAsync(p->d_keys, b->keys, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  const uint64_t want = p->mids_per_topic * n + 1024;
+  if (want > p->cap_mids) {
+    p->cap_mids = want + want / 4;
+    FO_TRY(fo_alloc(p->d_mids, p->cap_mids));
+  }
+  int rc = emqx_match_batch_device_async(p->e, EMQX_MODE_ROUTES, p->d_tbytes, p->d_toffs, n, p->d_moff, p->d_mids,
+                                         p->cap_mids, p->d_msum, st);
+  if (rc != EMQX_OK) return rc;
+  rc = pb_enqueue_fanout(b, p->cap_mids, p->d_msum);
+  if (rc != EMQX_OK) return rc;
+  FO_TRY(hipEventRecord(p->done, st));
+  p->pending = true;
+  return EMQX_OK;
+}
+
+int pb_wait(emqx_pub_batch* b) {
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  if (!p->pending) return EMQX_EINVAL;
+  FO_TRY(hipSetDevice(p->s->device));
+  p->pending = false;
+  FO_TRY(hipEventSynchronize(p->done));
+  const uint64_t* ms = p->h_sums;
+  const uint64_t* fs = p->h_sums + PB_MSUM_WORDS;
+  if (ms[0] != 0) {
+    // the match did not complete in the batch's buffers (its scratch learnt a larger size, or
+    // more ids than d_mids holds): rerun it synchronously, then the fan-out (which read nothing)
+    if (ms[0] & 4) return EMQX_EINVAL;  // a topic over 65535 bytes
+    uint64_t m = 0;
+    if (ms[1] + 1024 > p->cap_mids) {
+      p->cap_mids = ms[1] + ms[1] / 4 + 1024;
+      FO_TRY(fo_alloc(p->d_mids, p->cap_mids));
+    }
+    int rc = emqx_match_batch_device(p->e, EMQX_MODE_ROUTES, p->d_tbytes, p->d_toffs, b->n, p->d_moff, p->d_mids,
+                                     p->cap_mids, &m, p->stream);
+    if (rc == EMQX_EOVERFLOW) {
+      p->cap_mids = m + m / 4 + 1024;
+      FO_TRY(fo_alloc(p->d_mids, p->cap_mids));
+      rc = emqx_match_batch_device(p->e, EMQX_MODE_ROUTES, p->d_tbytes, p->d_toffs, b->n, p->d_moff, p->d_mids,
+                                   p->cap_mids, &m, p->stream);
+    }
+    if (rc != EMQX_OK) return rc;
+    rc = pb_enqueue_fanout(b, p->cap_mids, nullptr);
+    if (rc != EMQX_OK) return rc;
+    FO_TRY(hipStreamSynchronize(p->stream));
+    p->mids_per_topic = std::max<uint64_t>(p->mids_per_topic, m / std::max<uint64_t>(b->n, 1) + 1);
+  } else if (b->n) {
+    p->mids_per_topic = std::max<uint64_t>(4, (ms[1] + ms[1] / 4) / b->n + 1);
+  }
+  b->n_out = fs[FO_SUM_TOTAL];
+  if (fs[FO_SUM_FLAGS] & FO_SUM_F_MATCH) return EMQX_EDEVICE;
+  if (fs[FO_SUM_FLAGS] & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
+  return EMQX_OK;
 }
 
 }  // namespace
@@ -455,8 +1040,8 @@ int emqx_subtab_create(int32_t device, emqx_subtab** out) {
   auto* s = new (std::nothrow) emqx_subtab();
   if (!s) return EMQX_ENOMEM;
   s->device = dev;
-  int rc = commit_locked(s);
-  if (rc == EMQX_OK) rc = ensure_stream(s);
+  int rc = ensure_stream(s);
+  if (rc == EMQX_OK) rc = commit_locked(s);
   if (rc != EMQX_OK) {
     delete s;
     return rc;
@@ -479,26 +1064,24 @@ int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* 
     const uint32_t f = filter_ids[i], sub = sub_ids[i];
     const uint32_t grp = group_ids ? group_ids[i] : EMQX_NO_GROUP;
     if (grp == EMQX_NO_GROUP) {
-      if (s->plain_set.insert((uint64_t(f) << 32) | sub)) {
-        if (f >= s->plain.size()) s->plain.resize(uint64_t(f) + 1);
-        s->plain[f].push_back(sub);
-      }
+      plain_add(s, f, sub);
       continue;
     }
+    ensure_filter(s, f);
     const uint64_t key = (uint64_t(f) << 32) | grp;
     uint32_t sl = s->slot_of.find(key);
     if (sl == SUB_NONE) {
       if (s->slots.size() >= FANOUT_SHARED_BIT) return EMQX_ENOMEM;
       sl = static_cast<uint32_t>(s->slots.size());
-      s->slots.push_back(Slot{f, grp, {}, false});
-      s->slot_of.insert_new(key, sl);
-      if (f >= s->fslots.size()) s->fslots.resize(uint64_t(f) + 1);
+      s->slots.push_back(Slot{f, grp, {}, 0, 0, SUB_NONE, false});
+      s->slot_of.insert(key, sl);
       s->fslots[f].push_back(sl);
     }
-    if (s->member_set.insert((uint64_t(sl) << 32) | sub)) {
+    if (s->member_set.insert((uint64_t(sl) << 32) | sub, 1)) {
       s->slots[sl].members.push_back(sub);
-      s->slots[sl].changed = true;
       ++s->n_members;
+      mark_slot(s, sl);
+      note_op(s);
     }
   }
   return EMQX_OK;
@@ -511,13 +1094,9 @@ int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_
   for (uint64_t i = 0; i < n; ++i) {
     const uint32_t f = filter_ids[i], sub = sub_ids[i];
     const uint32_t grp = group_ids ? group_ids[i] : EMQX_NO_GROUP;
+    if (f >= s->recs.size()) continue;
     if (grp == EMQX_NO_GROUP) {
-      if (s->plain_set.erase((uint64_t(f) << 32) | sub)) {
-        auto& v = s->plain[f];
-        auto it = std::find(v.begin(), v.end(), sub);
-        *it = v.back();  // order of plain subscribers carries no meaning
-        v.pop_back();
-      }
+      plain_remove(s, f, sub);
       continue;
     }
     const uint32_t sl = s->slot_of.find((uint64_t(f) << 32) | grp);
@@ -525,8 +1104,9 @@ int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_
     if (s->member_set.erase((uint64_t(sl) << 32) | sub)) {
       auto& v = s->slots[sl].members;
       v.erase(std::find(v.begin(), v.end(), sub));  // keeps the others' order (ETS bag)
-      s->slots[sl].changed = true;
       --s->n_members;
+      mark_slot(s, sl);
+      note_op(s);
     }
   }
   return EMQX_OK;
@@ -541,11 +1121,43 @@ int emqx_subtab_commit(emqx_subtab* s) {
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4) {
   if (!s || !counts4) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
-  counts4[0] = s->plain_set.size();
+  counts4[0] = s->plain_pos.size();
   counts4[1] = s->n_members;
   counts4[2] = s->n_live_groups;
-  counts4[3] = s->dev.bytes;
+  counts4[3] = s->d_recs.cap * sizeof(FilterRec) + s->d_plain.cap * 4 + s->d_groups.cap * sizeof(GroupRec) +
+               s->d_members.cap * 4 + s->ps_cap * 12;
   return EMQX_OK;
+}
+
+int emqx_subtab_commit_stats(emqx_subtab* s, uint64_t* out, uint32_t n) {
+  if (!s || (n && !out)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(s->mu);
+  const uint64_t v[9] = {s->st_last_kind, s->st_commits, s->st_full, s->st_words, s->st_records, s->st_moves,
+                         s->garbage, static_cast<uint64_t>(s->st_host_us), static_cast<uint64_t>(s->st_total_us)};
+  for (uint32_t i = 0; i < n && i < 9; ++i) out[i] = v[i];
+  return EMQX_OK;
+}
+
+int emqx_subtab_forget_publishers(emqx_subtab* s, const uint32_t* publishers, uint64_t n) {
+  if (!s || (n && !publishers)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(s->mu);
+  if (!n || !s->ps_keys) return EMQX_OK;
+  FO_TRY(hipSetDevice(s->device));
+  std::vector<uint32_t> p(publishers, publishers + n);
+  std::sort(p.begin(), p.end());
+  p.erase(std::unique(p.begin(), p.end()), p.end());
+  int rc = barrier_after_fanouts(s);
+  if (rc != EMQX_OK) return rc;
+  uint32_t* d = nullptr;
+  FO_TRY(fo_alloc(d, p.size()));
+  rc = EMQX_OK;
+  if (hipMemcpyAsync(d, p.data(), p.size() * 4, hipMemcpyHostToDevice, s->stream) != hipSuccess ||
+      launch_ps_forget(s->ps_keys, s->ps_cap, d, p.size(), s->ps_count, s->stream) != hipSuccess ||
+      hipEventRecord(s->commit_ev, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess)
+    rc = EMQX_EDEVICE;
+  s->commit_pending = true;
+  fo_free(d);
+  return rc;
 }
 
 int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
@@ -559,16 +1171,14 @@ int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* 
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
   if (!stream) FO_TRY(after_null_stream(st));
   // the number of match entries: one small readback of the CSR bounds
-  uint64_t bounds[2] = {0, 0};
   FO_TRY(hipMemcpyAsync(s->h_total, d_match_offsets, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   FO_TRY(hipMemcpyAsync(s->h_total + 1, d_match_offsets + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   FO_TRY(hipStreamSynchronize(st));
-  bounds[0] = s->h_total[0];
-  bounds[1] = s->h_total[1];
-  if (bounds[1] < bounds[0]) return EMQX_EINVAL;
-  if (bounds[1] - bounds[0] && !d_match_ids) return EMQX_EINVAL;
-  return run_fanout(s, strategy, d_match_offsets, d_match_ids, n, bounds[1] - bounds[0], d_pick_keys,
-                    d_out_offsets, d_out_subs, d_out_filters, cap, n_out, st);
+  const uint64_t b0 = s->h_total[0], b1 = s->h_total[1];
+  if (b1 < b0) return EMQX_EINVAL;
+  if (b1 - b0 && !d_match_ids) return EMQX_EINVAL;
+  return run_fanout(s, strategy, d_match_offsets, d_match_ids, n, b1 - b0, d_pick_keys, d_out_offsets, d_out_subs,
+                    d_out_filters, cap, n_out, st);
 }
 
 int emqx_fanout_batch_device_async(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
@@ -583,9 +1193,112 @@ int emqx_fanout_batch_device_async(emqx_subtab* s, uint32_t strategy, const uint
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
   if (!stream) FO_TRY(after_null_stream(st));
   return enqueue_fanout(s, strategy, d_match_offsets, d_match_ids, n, match_cap, d_pick_keys, d_out_offsets,
-                        d_out_subs, d_out_filters, cap, summary, st);
+                        d_out_subs, d_out_filters, cap, summary, st, nullptr);
 }
 
+int emqx_pub_batch_create(emqx_engine* e, emqx_subtab* s, uint32_t strategy, uint64_t cap_topics, uint64_t cap_bytes,
+                          uint64_t cap_out, emqx_pub_batch** out) {
+  if (!e || !s || !out || strategy > EMQX_SHARE_HASH_TOPIC) return EMQX_EINVAL;
+  *out = nullptr;
+  auto* b = new (std::nothrow) emqx_pub_batch();
+  auto* p = new (std::nothrow) PubBatchPriv();
+  if (!b || !p) {
+    delete b;
+    delete p;
+    return EMQX_ENOMEM;
+  }
+  std::memset(b, 0, sizeof(*b));
+  b->priv = p;
+  p->e = e;
+  p->s = s;
+  p->strategy = strategy;
+  p->use_keys = strategy != EMQX_SHARE_RANDOM;
+  int rc = EMQX_OK;
+  if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess ||
+      fo_alloc(p->d_msum, PB_MSUM_WORDS + FO_SUM_WORDS) != hipSuccess ||
+      fo_halloc(p->h_sums, PB_MSUM_WORDS + FO_SUM_WORDS) != hipSuccess)
+    rc = EMQX_EDEVICE;
+  if (rc == EMQX_OK)
+    rc = pb_alloc(b, std::max<uint64_t>(cap_topics, 1), std::max<uint64_t>(cap_bytes, 64),
+                  std::max<uint64_t>(cap_out, 64), false);
+  if (rc != EMQX_OK) {
+    emqx_pub_batch_destroy(b);
+    return rc;
+  }
+  b->topic_offsets[0] = 0;
+  *out = b;
+  return EMQX_OK;
+}
+
+int emqx_pub_batch_destroy(emqx_pub_batch* b) {
+  if (!b) return EMQX_EINVAL;
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  (void)hipSetDevice(p->s->device);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  fo_hfree(b->topic_bytes);
+  fo_hfree(b->topic_offsets);
+  fo_hfree(b->keys);
+  fo_hfree(b->out_offsets);
+  fo_hfree(b->out_subs);
+  fo_hfree(b->out_filters);
+  fo_hfree(p->h_sums);
+  fo_free(p->d_tbytes);
+  fo_free(p->d_toffs);
+  fo_free(p->d_keys);
+  fo_free(p->d_moff);
+  fo_free(p->d_mids);
+  fo_free(p->d_ooff);
+  fo_free(p->d_osubs);
+  fo_free(p->d_ofil);
+  fo_free(p->d_msum);
+  {  // the subtab keeps a scratch per stream: it goes with the stream
+    std::lock_guard<std::mutex> g(p->s->mu);
+    auto& v = p->s->scratch;
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i]->stream == p->stream) {
+        v[i]->release();
+        v.erase(v.begin() + static_cast<std::ptrdiff_t>(i));
+        break;
+      }
+  }
+  if (p->done) (void)hipEventDestroy(p->done);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+  delete b;
+  return EMQX_OK;
+}
+
+int emqx_pub_batch_reserve(emqx_pub_batch* b, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_out) {
+  if (!b || static_cast<PubBatchPriv*>(b->priv)->pending) return EMQX_EINVAL;
+  return pb_alloc(b, cap_topics, cap_bytes, cap_out, true);
+}
+
+int emqx_pub_batch_submit(emqx_pub_batch* b) {
+  if (!b) return EMQX_EINVAL;
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  if (p->pending || b->n > b->cap_topics) return EMQX_EINVAL;
+  const uint64_t* o = b->topic_offsets;
+  if (o[0] != 0 || o[b->n] > b->cap_bytes) return EMQX_EINVAL;
+  for (uint64_t i = 0; i < b->n; ++i)
+    if (o[i + 1] < o[i]) return EMQX_EINVAL;
+  if (fo_stateful(p->strategy) && b->cap_out >= (1ull << 32)) return EMQX_EINVAL;
+  FO_TRY(hipSetDevice(p->s->device));
+  return pb_enqueue(b);
+}
+
+int emqx_pub_batch_wait(emqx_pub_batch* b) {
+  if (!b) return EMQX_EINVAL;
+  return pb_wait(b);
+}
+
+int emqx_pub_batch_query(emqx_pub_batch* b) {
+  if (!b) return EMQX_EINVAL;
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  return !p->pending || hipEventQuery(p->done) == hipSuccess ? 1 : 0;
+}
+
+// Host buffers of any kind: one pinned publish batch of the table's pool, grown to the call.
 int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const uint8_t* topic_bytes,
                        const uint64_t* topic_offsets, uint64_t n, const uint32_t* pick_keys, uint64_t* out_offsets,
                        uint32_t* out_subs, uint32_t* out_filters, uint64_t cap, uint64_t* n_out) {
@@ -595,58 +1308,56 @@ int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const 
     if (topic_offsets[i + 1] < topic_offsets[i]) return EMQX_EINVAL;
   const uint64_t b0 = n ? topic_offsets[0] : 0, b1 = n ? topic_offsets[n] : 0;
   if (b1 > b0 && !topic_bytes) return EMQX_EINVAL;
-  std::lock_guard<std::mutex> g(s->mu);
+  if (fo_stateful(strategy) && cap >= (1ull << 32)) cap = (1ull << 32) - 1;
   FO_TRY(hipSetDevice(s->device));
-  hipStream_t st = s->stream;
-  // stage topics (rebased, padded) and keys
-  FO_TRY(fo_ensure(s->d_tbytes, s->cap_tbytes, b1 - b0 + 16));
-  FO_TRY(fo_ensure(s->d_toffs, s->cap_toffs, n + 1));
-  FO_TRY(fo_ensure(s->d_moff, s->cap_moff, n + 1));
-  FO_TRY(fo_ensure(s->d_ooff, s->cap_ooff, n + 1));
-  std::vector<uint64_t> rebased(n + 1, 0);
-  for (uint64_t i = 0; i <= n && n; ++i) rebased[i] = topic_offsets[i] - b0;
-  if (b1 > b0) FO_TRY(hipMemcpyAsync(s->d_tbytes, topic_bytes + b0, b1 - b0, hipMemcpyHostToDevice, st));
-  FO_TRY(hipMemcpyAsync(s->d_toffs, rebased.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-  const uint32_t* d_keys = nullptr;
-  if (pick_keys && n) {
-    FO_TRY(fo_ensure(s->d_keys, s->cap_keys, n));
-    FO_TRY(hipMemcpyAsync(s->d_keys, pick_keys, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    d_keys = s->d_keys;
+  emqx_pub_batch* b = nullptr;
+  {
+    std::lock_guard<std::mutex> g(s->pb_mu);
+    for (size_t i = 0; i < s->pb_free.size(); ++i)
+      if (static_cast<PubBatchPriv*>(s->pb_free[i]->priv)->strategy == strategy &&
+          static_cast<PubBatchPriv*>(s->pb_free[i]->priv)->e == e) {
+        b = s->pb_free[i];
+        s->pb_free.erase(s->pb_free.begin() + static_cast<std::ptrdiff_t>(i));
+        break;
+      }
   }
-  FO_TRY(hipStreamSynchronize(st));
-  // match -> CSR in HBM (grow the id buffer once if needed)
-  uint64_t m = 0;
-  if (!s->d_mids) FO_TRY(fo_ensure(s->d_mids, s->cap_mids, 16 * n + 1024));
-  int rc = emqx_match_batch_device(e, EMQX_MODE_ROUTES, s->d_tbytes, s->d_toffs, n, s->d_moff, s->d_mids,
-                                   s->cap_mids, &m, st);
-  if (rc == EMQX_EOVERFLOW) {
-    FO_TRY(fo_ensure(s->d_mids, s->cap_mids, m));
-    rc = emqx_match_batch_device(e, EMQX_MODE_ROUTES, s->d_tbytes, s->d_toffs, n, s->d_moff, s->d_mids,
-                                 s->cap_mids, &m, st);
+  int rc = EMQX_OK;
+  if (!b) rc = emqx_pub_batch_create(e, s, strategy, n, b1 - b0, std::min<uint64_t>(cap, 64 * n + 64), &b);
+  if (rc == EMQX_OK) rc = emqx_pub_batch_reserve(b, n, b1 - b0, std::min<uint64_t>(cap, std::max<uint64_t>(b->cap_out, 64)));
+  if (rc == EMQX_OK) {
+    if (b1 > b0) std::memcpy(b->topic_bytes, topic_bytes + b0, b1 - b0);
+    for (uint64_t i = 0; i <= n; ++i) b->topic_offsets[i] = n ? topic_offsets[i] - b0 : 0;
+    if (pick_keys && n) std::memcpy(b->keys, pick_keys, n * sizeof(uint32_t));
+    else if (n) std::memset(b->keys, 0, n * sizeof(uint32_t));
+    b->n = n;
+    auto* p = static_cast<PubBatchPriv*>(b->priv);
+    p->limit = cap;  // a result the caller cannot take is not made (no pick state consumed)
+    rc = emqx_pub_batch_submit(b);
+    if (rc == EMQX_OK) rc = emqx_pub_batch_wait(b);
+    if (rc == EMQX_EOVERFLOW && b->n_out <= cap) {  // nothing was written and no pick state used
+      rc = emqx_pub_batch_reserve(b, n, b1 - b0, b->n_out);
+      if (rc == EMQX_OK) rc = emqx_pub_batch_submit(b);
+      if (rc == EMQX_OK) rc = emqx_pub_batch_wait(b);
+    }
+    p->limit = ~0ull;
+    *n_out = b->n_out;
+    if (rc == EMQX_OK) {
+      std::memcpy(out_offsets, b->out_offsets, (n + 1) * sizeof(uint64_t));
+      if (b->n_out > cap) {
+        rc = EMQX_EOVERFLOW;
+      } else {
+        if (out_subs && b->n_out) std::memcpy(out_subs, b->out_subs, b->n_out * sizeof(uint32_t));
+        if (out_filters && b->n_out) std::memcpy(out_filters, b->out_filters, b->n_out * sizeof(uint32_t));
+      }
+    } else if (rc == EMQX_EOVERFLOW) {
+      std::memcpy(out_offsets, b->out_offsets, (n + 1) * sizeof(uint64_t));
+    }
   }
-  if (rc != EMQX_OK) return rc;
-  // fan-out into the staging buffers; an overflow returns before the write kernel (no pick
-  // state consumed), so the buffers grow once and the call repeats
-  uint64_t total = 0;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    FO_TRY(fo_ensure(s->d_osubs, s->cap_osubs, 1));
-    FO_TRY(fo_ensure(s->d_ofil, s->cap_ofil, s->cap_osubs));
-    rc = run_fanout(s, strategy, s->d_moff, s->d_mids, n, m, d_keys, s->d_ooff, s->d_osubs, s->d_ofil,
-                    s->cap_osubs, &total, st);
-    if (rc != EMQX_EOVERFLOW) break;
-    *n_out = total;
-    if (total > cap) return EMQX_EOVERFLOW;
-    FO_TRY(fo_ensure(s->d_osubs, s->cap_osubs, total));
+  if (b) {
+    std::lock_guard<std::mutex> g(s->pb_mu);
+    s->pb_free.push_back(b);
   }
-  if (rc != EMQX_OK) return rc;
-  *n_out = total;
-  if (total > cap) return EMQX_EOVERFLOW;
-  FO_TRY(hipMemcpyAsync(out_offsets, s->d_ooff, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  if (total && out_subs) FO_TRY(hipMemcpyAsync(out_subs, s->d_osubs, total * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  if (total && out_filters)
-    FO_TRY(hipMemcpyAsync(out_filters, s->d_ofil, total * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  FO_TRY(hipStreamSynchronize(st));
-  return EMQX_OK;
+  return rc;
 }
 
 }  // extern "C"

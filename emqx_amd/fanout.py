@@ -10,10 +10,16 @@ apps/emqx/src/emqx_shared_sub.erl:98-126):
   (``emqx_publish_batch``); the result per topic is the list of deliveries
   ``(filter, subscriber, shared)`` that ``emqx_broker:route/2`` would dispatch.
 
+* ``PubBatcher`` — the cross-caller publish batcher (``emqx_pub_batcher_*``): single-message
+  submissions from many threads coalesced into pinned device batches, as the NIF's
+  ``publish_async/4`` does for many publisher processes.
+
 Subscriber and group handles are the caller's (any hashable); they are mapped to uint32 ids
-here, as the NIF maps pids and group names.  The hash strategies take per-message keys:
+here, as the NIF maps pids and group names.  Per-message keys: the hash strategies take
 ``erlang:phash2(ClientId)`` (``hash_clientid``) or ``erlang:phash2(Topic)`` (``hash_topic``),
-computed by the caller (the NIF does it in Erlang; phash2 is not restated here).
+computed by the caller (the NIF does it in Erlang; phash2 is not restated here);
+``round_robin`` and ``sticky`` take the *publisher* of the message, whose process dictionary
+holds that state in the reference (emqx_shared_sub.erl:234-247,279-285).
 """
 
 from __future__ import annotations
@@ -25,12 +31,12 @@ from typing import Dict, Hashable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from ._lib import (FANOUT_SHARED_BIT, NO_GROUP, SHARE_HASH_CLIENTID, SHARE_HASH_TOPIC, SHARE_RANDOM,
+from ._lib import (FANOUT_SHARED_BIT, NO_GROUP, PUB_CB, SHARE_HASH_CLIENTID, SHARE_HASH_TOPIC, SHARE_RANDOM,
                    SHARE_ROUND_ROBIN, SHARE_STICKY, EngineError, check)
 from .engine import pack
 from .router import Router
 
-__all__ = ["SubTable", "Broker", "STRATEGIES", "FANOUT_SHARED_BIT", "NO_GROUP"]
+__all__ = ["SubTable", "Broker", "PubBatcher", "STRATEGIES", "FANOUT_SHARED_BIT", "NO_GROUP"]
 
 # broker.shared_subscription_strategy values (emqx_shared_sub.erl:60-65); 'hash' = hash_clientid
 STRATEGIES = {"random": SHARE_RANDOM, "round_robin": SHARE_ROUND_ROBIN, "sticky": SHARE_STICKY,
@@ -89,6 +95,19 @@ class SubTable:
         c = np.zeros(4, dtype=np.uint64)
         check(_lib.lib().emqx_subtab_stats(self._h, _p(c)), "emqx_subtab_stats")
         return {"plain": int(c[0]), "shared_members": int(c[1]), "groups": int(c[2]), "device_bytes": int(c[3])}
+
+    COMMIT_STATS = ("kind", "commits", "full_commits", "words", "records", "moves", "garbage", "host_us", "total_us")
+
+    def commit_stats(self) -> dict:
+        """emqx_subtab_commit_stats: what the commits wrote (kind 0 = full, 1 = incremental)."""
+        c = np.zeros(len(self.COMMIT_STATS), dtype=np.uint64)
+        check(_lib.lib().emqx_subtab_commit_stats(self._h, _p(c), len(c)), "emqx_subtab_commit_stats")
+        return {k: int(v) for k, v in zip(self.COMMIT_STATS, c)}
+
+    def forget_publishers(self, publishers) -> None:
+        """Drops the round_robin / sticky state of these publishers (their processes ended)."""
+        p = _u32(publishers)
+        check(_lib.lib().emqx_subtab_forget_publishers(self._h, _p(p), len(p)), "emqx_subtab_forget_publishers")
 
     def fanout_device(self, strategy, d_moff: int, d_mids: int, n: int, d_keys: Optional[int], d_out_off: int,
                       d_out_subs: int, d_out_filters: Optional[int], cap: int, stream: Optional[int] = None) -> int:
@@ -238,3 +257,75 @@ class Broker:
 
     def publish(self, topic: bytes, key: int = 0):
         return self.publish_batch([topic], [key])[0]
+
+
+class PubBatcher:
+    """emqx_pub_batcher over an engine and a subscription table: ``submit`` one message (topic,
+    key) with a callback ``fn(status, subs, filters)`` (numpy copies), called from the batcher's
+    completion thread.  ``try_submit`` returns False instead of waiting when every pinned
+    buffer is busy (EMQX_EBUSY)."""
+
+    def __init__(self, engine, subtab: SubTable, strategy, max_batch: int = 4096, max_wait_us: int = 200):
+        self._fns: Dict[int, object] = {}
+        self._next = 1
+        self._mu = threading.Lock()
+
+        def on_done(ctx, status, subs, fils, n):
+            with self._mu:
+                fn = self._fns.pop(int(ctx or 0), None)
+            if fn is None:
+                return
+            if status == 0 and n:
+                s = np.ctypeslib.as_array(subs, shape=(n,)).copy()
+                f = np.ctypeslib.as_array(fils, shape=(n,)).copy()
+            else:
+                s = f = np.zeros(0, np.uint32)
+            fn(status, s, f)
+
+        self._cb = PUB_CB(on_done)  # kept alive with the batcher
+        h = ctypes.c_void_p()
+        check(_lib.lib().emqx_pub_batcher_create(engine._h, subtab.handle, _strategy(strategy), max_batch, max_wait_us,
+                                                 self._cb, ctypes.byref(h)), "emqx_pub_batcher_create")
+        self._h = h
+
+    def _register(self, fn) -> int:
+        with self._mu:
+            k = self._next
+            self._next += 1
+            self._fns[k] = fn
+        return k
+
+    def submit(self, topic: bytes, key: int, fn) -> None:
+        k = self._register(fn)
+        rc = _lib.lib().emqx_pub_batcher_submit(self._h, topic, len(topic), key & 0xFFFFFFFF, ctypes.c_void_p(k))
+        if rc != 0:
+            with self._mu:
+                self._fns.pop(k, None)
+        check(rc, "emqx_pub_batcher_submit")
+
+    def try_submit(self, topic: bytes, key: int, fn) -> bool:
+        k = self._register(fn)
+        rc = _lib.lib().emqx_pub_batcher_try_submit(self._h, topic, len(topic), key & 0xFFFFFFFF, ctypes.c_void_p(k))
+        if rc != 0:
+            with self._mu:
+                self._fns.pop(k, None)
+        if rc == _lib.EMQX_EBUSY:
+            return False
+        check(rc, "emqx_pub_batcher_try_submit")
+        return True
+
+    def stats(self) -> dict:
+        c = np.zeros(6, dtype=np.uint64)
+        check(_lib.lib().emqx_pub_batcher_stats_ext(self._h, _p(c), 6), "emqx_pub_batcher_stats_ext")
+        return {"batches": int(c[0]), "messages": int(c[1]), "max_inflight": int(c[2])}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().emqx_pub_batcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -54,6 +54,7 @@ extern "C" {
 #define EMQX_EOVERFLOW -4     /* out_ids too small: *n_out holds the required capacity       */
 #define EMQX_ENOTFOUND -5     /* unknown filter id / name                                     */
 #define EMQX_ETOODEEP -6      /* a topic exceeded the engine's frontier capacity             */
+#define EMQX_EBUSY -7         /* *_try_submit: every batch buffer is busy; nothing was queued */
 
 /* ---- match modes --------------------------------------------------------------- */
 #define EMQX_MODE_ROUTES 0          /* emqx_router:match_routes/1 — exact ∪ wildcard    */
@@ -196,12 +197,17 @@ int emqx_host_batch_query(emqx_host_batch* b);
  * into one device batch.  submit() returns at once; a worker thread runs a batch when
  * max_batch topics are queued or max_wait_us after the oldest submission, then calls
  * cb(ctx, status, ids, n) once per submission from that thread (ids valid during the call).
- * destroy() drains pending submissions.  The NIF's cb enif_send()s the ids to the caller. */
+ * destroy() drains pending submissions.  The NIF's cb enif_send()s the ids to the caller.
+ * submit() blocks while every pinned buffer is filling, sealed or in flight (backpressure);
+ * try_submit() never waits: it returns EMQX_EBUSY instead (nothing queued, cb not called), and
+ * likewise when the topic would need a larger pinned buffer.  A NIF on a normal scheduler uses
+ * try_submit and moves to a dirty scheduler only on EMQX_EBUSY. */
 typedef struct emqx_batcher emqx_batcher;
 typedef void (*emqx_batch_cb)(void* ctx, int status, const uint32_t* ids, uint64_t n);
 int emqx_batcher_create(emqx_engine* e, uint32_t mode, uint32_t max_batch, uint32_t max_wait_us,
                         emqx_batch_cb cb, emqx_batcher** out);
 int emqx_batcher_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, void* ctx);
+int emqx_batcher_try_submit(emqx_batcher* b, const uint8_t* topic, uint64_t len, void* ctx);
 /* n submissions at once (topic i = bytes[offsets[i] .. offsets[i+1]), context ctxs[i]): one
  * lock for the lot, e.g. a NIF draining a scheduler's queue of match_routes/1 calls. */
 int emqx_batcher_submit_many(emqx_batcher* b, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
@@ -223,21 +229,30 @@ int emqx_batcher_stats_ext(emqx_batcher* b, uint64_t* out, uint32_t n);
  * Subscriber ids and group ids are the caller's uint32 handles (the NIF maps pids and group
  * names to them).  Filter ids must be < 2^31.  A delivery is (subscriber id, filter id); the
  * filter id has EMQX_FANOUT_SHARED_BIT set when the delivery is a $share pick ({share, To, ...}
- * in publish_result(), emqx_types.erl:201-206).  Fan-out calls on one table are serialised
- * (the round_robin and sticky strategies update per-group state). */
+ * in publish_result(), emqx_types.erl:201-206).
+ *
+ * Per-message keys (pick_keys / d_pick_keys / emqx_pub_batch.keys), by strategy:
+ *   hash_clientid / hash_topic: the caller's erlang:phash2(ClientId) / phash2(Topic) (required);
+ *   round_robin / sticky: the PUBLISHER of the message (a uint32 handle of the dispatching
+ *     process): the reference keeps this state in the publishing process's dictionary under
+ *     {shared_sub_round_robin | shared_sub_sticky, Group, Topic} (emqx_shared_sub.erl:234-247,
+ *     279-285), so the device keeps it per (group slot, publisher).  NULL = one publisher.
+ *     Picks of one publisher in one call are made in message order;
+ *   random: ignored. */
 #define EMQX_NO_GROUP 0xFFFFFFFFu
 #define EMQX_FANOUT_SHARED_BIT 0x80000000u
 
 /* broker.shared_subscription_strategy (emqx_shared_sub.erl:60-65) */
-#define EMQX_SHARE_RANDOM 0          /* rand:uniform(N)                               */
-#define EMQX_SHARE_ROUND_ROBIN 1     /* per-group counter                              */
-#define EMQX_SHARE_STICKY 2          /* first pick random, then kept while subscribed  */
-#define EMQX_SHARE_HASH_CLIENTID 3   /* 1 + Key rem N, Key = erlang:phash2(ClientId)   */
-#define EMQX_SHARE_HASH_TOPIC 4      /* 1 + Key rem N, Key = erlang:phash2(Topic)      */
+#define EMQX_SHARE_RANDOM 0          /* rand:uniform(N)                                         */
+#define EMQX_SHARE_ROUND_ROBIN 1     /* per publisher: rand:uniform(N) - 1 first, then +1 rem N  */
+#define EMQX_SHARE_STICKY 2          /* per publisher: first pick random, kept while subscribed  */
+#define EMQX_SHARE_HASH_CLIENTID 3   /* 1 + Key rem N, Key = erlang:phash2(ClientId)             */
+#define EMQX_SHARE_HASH_TOPIC 4      /* 1 + Key rem N, Key = erlang:phash2(Topic)                */
 
 typedef struct emqx_subtab emqx_subtab; /* opaque */
 
 int emqx_subtab_create(int32_t device, emqx_subtab** out);
+/* Destroy the table's emqx_pub_batch / emqx_pub_batcher objects first. */
 int emqx_subtab_destroy(emqx_subtab* s);
 /* emqx_broker:subscribe/3 (emqx_broker.erl:124-163): subscriber sub_ids[i] subscribes to
  * filter_ids[i], plainly (group_ids NULL or EMQX_NO_GROUP) or in $share group group_ids[i].
@@ -247,37 +262,100 @@ int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* 
 /* emqx_broker:unsubscribe/1 (emqx_broker.erl:169-195); absent pairs are ignored. */
 int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids,
                        const uint32_t* group_ids, uint64_t n);
-/* Publishes the mutations to the device (sticky picks of members that left are dropped). */
+/* Publishes the mutations to the device at a cost proportional to them: the touched list
+ * words and 16-B records are patched in place (a list that outgrows its extent moves to the
+ * arena's end with room to grow); a full rebuild compacts the arenas only when moved-away
+ * extents outweigh the live ones.  Ordered after the fan-outs in flight and before later
+ * ones (device events); a sticky member that left its group is replaced at its next pick. */
 int emqx_subtab_commit(emqx_subtab* s);
 /* counts[0..3] = live plain subscriptions, live shared memberships, groups with members,
  * device bytes */
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4);
+/* out[0..8] = last commit kind (0 full, 1 incremental), commits, full commits, words written,
+ * 16-B records written, extents moved, garbage words, host us of the last incremental commit's
+ * image update, us of the last commit in total. */
+int emqx_subtab_commit_stats(emqx_subtab* s, uint64_t* out, uint32_t n);
+/* Drops the round_robin / sticky state of the given publishers (their processes ended: the
+ * reference's state dies with the process dictionary). */
+int emqx_subtab_forget_publishers(emqx_subtab* s, const uint32_t* publishers, uint64_t n);
 
 /* Fan-out of a match CSR already in HBM (d_match_offsets[n+1], d_match_ids): per-topic CSR of
  * deliveries d_out_offsets[n+1], d_out_subs[], d_out_filters[] (optional, may be NULL).
- * d_pick_keys[n] (device) is required for the hash strategies.  On EMQX_EOVERFLOW nothing is
- * written to the id arrays and *n_out is the capacity required. */
+ * d_pick_keys[n] (device): per-message keys as above.  On EMQX_EOVERFLOW nothing is written to
+ * the id arrays, no pick state is consumed, and *n_out is the capacity required. */
 int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
                              const uint32_t* d_match_ids, uint64_t n, const uint32_t* d_pick_keys,
                              uint64_t* d_out_offsets, uint32_t* d_out_subs, uint32_t* d_out_filters,
                              uint64_t cap, uint64_t* n_out, void* stream);
 /* Asynchronous form of emqx_fanout_batch_device for pipelined callers: the whole fan-out is
  * enqueued on `stream` with no host synchronisation (the entry count is read on the device).
- * match_cap bounds the match entries (the match call's id capacity; sizes the scratch).
- * summary[4] (device or host-mapped memory) receives {flags (bit 0: overflow), deliveries,
- * match entries, 0} when the call completes; on overflow nothing is written to the id arrays
- * and no $share pick state is consumed. */
+ * match_cap bounds the match entries (the match call's id capacity; sizes the scratch): a CSR
+ * with more entries (a match call that overflowed its ids) is not read.  summary[4] (device or
+ * host-mapped memory) receives {flags, deliveries, match entries, live pick-state keys} when the
+ * call completes; flags bit 0: more deliveries than cap (nothing written to the id arrays, no
+ * $share pick state consumed); bit 1: the CSR was refused (nothing read); bit 2: a
+ * round_robin / sticky pick found no room for its state (it was picked at random; the table
+ * grows before the next call). */
 int emqx_fanout_batch_device_async(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
                                    const uint32_t* d_match_ids, uint64_t n, uint64_t match_cap,
                                    const uint32_t* d_pick_keys, uint64_t* d_out_offsets, uint32_t* d_out_subs,
                                    uint32_t* d_out_filters, uint64_t cap, uint64_t* summary, void* stream);
 /* emqx_broker:publish/1's lookup + fan-out for a batch of topics (host buffers): match
  * (mode EMQX_MODE_ROUTES) and fan-out run back to back on the device; the match CSR never
- * leaves HBM.  pick_keys[n] (host) as above. */
+ * leaves HBM.  pick_keys[n] (host) as above.  Runs through a pinned publish batch of the
+ * table's pool (no pageable staging, one host synchronisation).  On EMQX_EOVERFLOW out_offsets
+ * are complete, *n_out is the capacity required and no pick state was consumed. */
 int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const uint8_t* topic_bytes,
                        const uint64_t* topic_offsets, uint64_t n, const uint32_t* pick_keys,
                        uint64_t* out_offsets, uint32_t* out_subs, uint32_t* out_filters, uint64_t cap,
                        uint64_t* n_out);
+
+/* ---- pinned publish batches (the NIF's publish buffers) ---------------------------
+ * The publish counterpart of emqx_host_batch: pinned inputs (topics, per-message keys) and
+ * pinned outputs (the delivery CSR).  submit() enqueues, on the batch's own stream with no host
+ * synchronisation: inputs to HBM, the match (EMQX_MODE_ROUTES), the fan-out of its CSR in HBM,
+ * and the delivery CSR streamed into the pinned outputs.  wait(): EMQX_OK, EMQX_EOVERFLOW
+ * (n_out = deliveries needed: reserve and submit again; nothing was delivered and no pick state
+ * consumed) or an error. */
+typedef struct emqx_pub_batch {
+  uint8_t* topic_bytes;     /* pinned, cap_bytes                                             */
+  uint64_t* topic_offsets;  /* pinned, cap_topics + 1 (offsets[0] = 0)                      */
+  uint32_t* keys;           /* pinned, cap_topics: per-message keys (see above)             */
+  uint64_t cap_topics, cap_bytes;
+  uint64_t n;               /* messages packed (set by the caller)                          */
+  uint64_t* out_offsets;    /* pinned, cap_topics + 1 (valid after wait)                    */
+  uint32_t* out_subs;       /* pinned, cap_out: subscriber ids                              */
+  uint32_t* out_filters;    /* pinned, cap_out: filter ids | EMQX_FANOUT_SHARED_BIT         */
+  uint64_t cap_out;
+  uint64_t n_out;           /* deliveries of the last call (after wait)                     */
+  void* priv;
+} emqx_pub_batch;
+int emqx_pub_batch_create(emqx_engine* e, emqx_subtab* s, uint32_t strategy, uint64_t cap_topics,
+                          uint64_t cap_bytes, uint64_t cap_out, emqx_pub_batch** out);
+int emqx_pub_batch_destroy(emqx_pub_batch* b);
+int emqx_pub_batch_reserve(emqx_pub_batch* b, uint64_t cap_topics, uint64_t cap_bytes, uint64_t cap_out);
+int emqx_pub_batch_submit(emqx_pub_batch* b);
+int emqx_pub_batch_wait(emqx_pub_batch* b);
+int emqx_pub_batch_query(emqx_pub_batch* b);
+
+/* Cross-caller publish batcher: the emqx_batcher counterpart for emqx_broker:publish/1, which
+ * each publisher process calls once per PUBLISH (emqx_channel.erl:608-617 -> emqx_broker.erl:
+ * 203-214).  Concurrent single-message submissions are packed into the pinned publish batch
+ * being filled; batches run match + fan-out with two in flight; a completion thread calls
+ * cb(ctx, status, subs, filters, n) per message (arrays valid during the call).  Same
+ * submit / try_submit contract as emqx_batcher. */
+typedef struct emqx_pub_batcher emqx_pub_batcher;
+typedef void (*emqx_pub_cb)(void* ctx, int status, const uint32_t* subs, const uint32_t* filters, uint64_t n);
+int emqx_pub_batcher_create(emqx_engine* e, emqx_subtab* s, uint32_t strategy, uint32_t max_batch,
+                            uint32_t max_wait_us, emqx_pub_cb cb, emqx_pub_batcher** out);
+int emqx_pub_batcher_submit(emqx_pub_batcher* b, const uint8_t* topic, uint64_t len, uint32_t key, void* ctx);
+int emqx_pub_batcher_try_submit(emqx_pub_batcher* b, const uint8_t* topic, uint64_t len, uint32_t key,
+                                void* ctx);
+int emqx_pub_batcher_submit_many(emqx_pub_batcher* b, const uint8_t* bytes, const uint64_t* offsets,
+                                 const uint32_t* keys, uint64_t n, void* const* ctxs);
+int emqx_pub_batcher_destroy(emqx_pub_batcher* b);
+/* out[0..5] as emqx_batcher_stats_ext. */
+int emqx_pub_batcher_stats_ext(emqx_pub_batcher* b, uint64_t* out, uint32_t n);
 
 /* Filter-sharded tables (emqx_amd/dist.py): owner_out[i] = the rank that holds filter / topic i
  * in a world of `world` ranks — a hash of its first `levels` levels.  Filters (topics = 0): a

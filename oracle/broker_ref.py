@@ -24,8 +24,14 @@ Restates (EMQX 5.0.0-beta.3, paths relative to ``/root/reference``):
 ``erlang:phash2`` (ERTS C, OTP 24.1.5) is NOT restated: the hash strategies take the
 caller's phash2 value as ``key`` (the NIF computes ``erlang:phash2(ClientId)`` /
 ``erlang:phash2(Topic)`` in Erlang), so the pick ``lists:nth(1 + Key rem N, Subs)`` is exact.
-``random`` and ``round_robin`` (first value ``rand:uniform(N) - 1``, per publisher process) and
-``sticky`` are non-deterministic in the reference; tests check their invariants only.
+
+``round_robin`` and ``sticky`` keep their state in the *publishing process's* dictionary under
+``{shared_sub_round_robin | shared_sub_sticky, Group, Topic}`` (emqx_shared_sub.erl:234-247,
+279-285): here a dict keyed ``(publisher, group, topic)``, where the publisher is the message's
+``key`` (the engine's C ABI takes the publisher handle in the same per-message key slot for
+these two strategies).  Their first pick is ``rand:uniform(N) - 1`` / a random member: the
+oracle takes it from ``first(n)`` (default 0), so a test can seed it with the pick the device
+made and check every later pick exactly.  ``random`` is checked by its distribution only.
 """
 
 from __future__ import annotations
@@ -45,7 +51,8 @@ class SharedSub:
 
     def __init__(self):
         self.tab: List[Tuple[object, bytes, object]] = []
-        self.rr: Dict[Tuple[object, bytes], int] = {}
+        self.rr: Dict[Tuple[object, object, bytes], int] = {}      # (publisher, group, topic) -> Rem
+        self.sticky: Dict[Tuple[object, object, bytes], object] = {}  # (publisher, group, topic) -> Sub
 
     def subscribe(self, group, topic: bytes, sub) -> bool:
         """Returns True when this is the group's first member on `topic` (route to add)."""
@@ -65,25 +72,35 @@ class SharedSub:
     def subscribers(self, group, topic: bytes) -> list:
         return [s for g, t, s in self.tab if g == group and t == topic]
 
-    def pick(self, strategy: int, key: int, group, topic: bytes):
-        """do_pick/6 with FailedSubs = [] (dispatch never fails here): ``False`` when the group
-        has no member, else the picked member."""
+    def pick(self, strategy: int, key: int, group, topic: bytes, first=None):
+        """pick/6 -> do_pick/6 with FailedSubs = [] (dispatch never fails here): ``False`` when
+        the group has no member, else the picked member.  ``key``: phash2 value (hash
+        strategies) or the publisher (round_robin, sticky).  ``first(n)``: the 0-based index the
+        reference draws with rand:uniform(N) (default 0)."""
         subs = self.subscribers(group, topic)
         if not subs:
             return False
-        if len(subs) == 1:  # pick_subscriber/6, first clause
-            return subs[0]
         n = len(subs)
+        draw = (lambda k: 0) if first is None else first
+        if strategy == STICKY:  # pick/6 :234-247; "active" = still subscribed to the group here
+            sk = (key, group, topic)
+            cur = self.sticky.get(sk)
+            if cur is not None and cur in subs:
+                return cur
+            sub = subs[draw(n) % n] if n > 1 else subs[0]
+            self.sticky[sk] = sub
+            return sub
+        if n == 1:  # pick_subscriber/6, first clause: the strategy is not consulted
+            return subs[0]
         if strategy in (HASH_CLIENTID, HASH_TOPIC):
             nth = 1 + key % n
-        elif strategy == ROUND_ROBIN:
-            # the reference seeds the per-process counter with rand:uniform(N) - 1; the
-            # engine's counter starts at 0 (SURVEY §8 d config E)
-            rem = (self.rr[(group, topic)] + 1) % n if (group, topic) in self.rr else 0
-            self.rr[(group, topic)] = rem
+        elif strategy == ROUND_ROBIN:  # do_pick_subscriber/6 :279-285
+            rk = (key, group, topic)
+            rem = (self.rr[rk] + 1) % n if rk in self.rr else draw(n) % n
+            self.rr[rk] = rem
             nth = rem + 1
         else:
-            raise ValueError("random/sticky picks are not deterministic; test invariants")
+            raise ValueError("random picks are not deterministic; test their distribution")
         return subs[nth - 1]
 
 
@@ -133,15 +150,16 @@ class Broker:
                 acc = sorted(set([(to, dest[0])] + acc), key=repr)
         return acc
 
-    def publish(self, topic: bytes, key: int = 0, strategy: int = HASH_CLIENTID):
-        """Deliveries of one PUBLISH: list of (filter, subscriber, shared)."""
+    def publish(self, topic: bytes, key: int = 0, strategy: int = HASH_CLIENTID, first=None):
+        """Deliveries of one PUBLISH: list of (filter, subscriber, shared).  ``key`` as in
+        SharedSub.pick; ``first(n)`` seeds a publisher's first round_robin / sticky pick."""
         out = []
         for to, dest in self.aggre(self.router.match_routes(topic)):
             if dest == NODE:
                 for sub in self.subscriber.get(to, []):  # do_dispatch/2 (shards flattened)
                     out.append((to, sub, False))
             else:
-                sub = self.shared.pick(strategy, key, dest, to)
+                sub = self.shared.pick(strategy, key, dest, to, first)
                 if sub is not False:
                     out.append((to, sub, True))
         return out

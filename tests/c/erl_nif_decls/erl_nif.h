@@ -7,6 +7,8 @@
 #include <stddef.h>
 
 typedef unsigned long ERL_NIF_TERM;
+typedef long ErlNifSInt64;
+typedef unsigned long ErlNifUInt64;
 typedef struct enif_environment_t ErlNifEnv;
 typedef struct enif_resource_type_t ErlNifResourceType;
 typedef struct { ERL_NIF_TERM pid; } ErlNifPid;
@@ -29,6 +31,7 @@ typedef struct {
 int enif_get_resource(ErlNifEnv*, ERL_NIF_TERM, ErlNifResourceType*, void**);
 int enif_get_int(ErlNifEnv*, ERL_NIF_TERM, int*);
 int enif_get_uint(ErlNifEnv*, ERL_NIF_TERM, unsigned*);
+int enif_get_int64(ErlNifEnv*, ERL_NIF_TERM, ErlNifSInt64*);
 int enif_get_list_length(ErlNifEnv*, ERL_NIF_TERM, unsigned*);
 int enif_get_list_cell(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM*, ERL_NIF_TERM*);
 int enif_get_tuple(ErlNifEnv*, ERL_NIF_TERM, int*, const ERL_NIF_TERM**);
@@ -39,6 +42,9 @@ ERL_NIF_TERM enif_make_list_cell(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_tuple2(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_tuple3(ErlNifEnv*, ERL_NIF_TERM, ERL_NIF_TERM, ERL_NIF_TERM);
 ERL_NIF_TERM enif_make_uint(ErlNifEnv*, unsigned);
+ERL_NIF_TERM enif_make_uint64(ErlNifEnv*, ErlNifUInt64);
+ERL_NIF_TERM enif_schedule_nif(ErlNifEnv*, const char*, int,
+                               ERL_NIF_TERM (*)(ErlNifEnv*, int, const ERL_NIF_TERM[]), int, const ERL_NIF_TERM[]);
 ERL_NIF_TERM enif_make_atom(ErlNifEnv*, const char*);
 ERL_NIF_TERM enif_make_badarg(ErlNifEnv*);
 ERL_NIF_TERM enif_make_resource(ErlNifEnv*, void*);
