@@ -91,7 +91,7 @@ def main():
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
-    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R", "L"],
+    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R", "L", "P", "S"],
                     help="B = the headline (BASELINE configs[1]); A = configs[0]'s 100k-filter table, "
                          "D = the adversarial depth-16 table (configs[3], 1M-topic batches), "
                          "E = publish fan-out (configs[4]): match + fan-out per step, "
@@ -99,7 +99,10 @@ def main():
                          "commits on config B's table, R = retained-message lookup (SURVEY §8 f4): a batch "
                          "of subscription filters against 1M stored retained topics, L = the drop-in "
                          "per-PUBLISH path: concurrent single-topic callers through the batcher on config "
-                         "B's table")
+                         "B's table, P = the drop-in emqx_broker:publish/1 path: concurrent single-message "
+                         "callers through the publish batcher (match + fan-out) on config E's 10M "
+                         "subscriptions, S = subscription churn: subscribe/unsubscribe ops committed to "
+                         "config E's 10M-subscription table")
     ap.add_argument("--callers", type=str, default="64,512,4096",
                     help="--workload L: concurrent single-topic callers per run")
     ap.add_argument("--max-batch", type=int, default=4096, help="--workload L: batcher max_batch")
@@ -179,6 +182,10 @@ def main():
         return retain_bench(args, rank, world, dev)
     if args.workload == "L":
         return batcher_bench(args, rank, world, dev)
+    if args.workload == "P":
+        return pub_batcher_bench(args, rank, world, dev)
+    if args.workload == "S":
+        return subscribe_bench(args, rank, world, dev)
     if args.workload == "A":
         wl = load_or_make(args, rank, lambda: W.config_a(n_topics=args.batch, seed=1 if rank == 0 else 1000 + rank))
     elif args.workload == "D":
@@ -598,6 +605,188 @@ def batcher_bench(args, rank, world, dev):
                                   "config B table", "n_filters": wl.n_filters, "max_batch": args.max_batch,
                       "parallelism": "replicated table"},
            "runs": runs}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def config_e_tables(args, rank, dev):
+    """Config E's tables on this rank's device: the 2M-filter route table and the 10M-subscription
+    table (one full commit)."""
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    from emqx_amd.fanout import SubTable
+    t0 = time.time()
+    with progress(f"[rank {rank}] generating config E"):
+        fw = W.config_e(n_topics=args.batch)
+    eng = Engine(dev.index)
+    with progress(f"[rank {rank}] building tables"):
+        eng.insert_packed(*fw.wl.filters)
+        eng.commit()
+        st = SubTable(dev.index)
+        st.add(fw.sub_filter, fw.sub_id, fw.sub_group)
+        t1 = time.perf_counter()
+        st.commit()
+        full_ms = 1e3 * (time.perf_counter() - t1)
+    log(f"[rank {rank}] config E: {fw.wl.n_filters} filters, {fw.n_subscriptions} subscriptions, "
+        f"subtab {st.stats()} ({time.time() - t0:.1f}s)")
+    return fw, eng, st, full_ms
+
+
+def pub_batcher_bench(args, rank, world, dev):
+    """The drop-in per-PUBLISH fan-out (emqx_channel -> emqx_broker:publish/1, emqx_broker.erl:
+    203-214, once per message from each publisher process): C concurrent single-message callers
+    in a closed loop through the publish batcher (emqx_pub_batcher_*: pinned batches, match +
+    fan-out on the device with no host sync in between, two batches in flight) on config E's
+    10M subscriptions.  Per C: messages/s and latency percentiles (submit -> deliveries in the
+    caller's callback)."""
+    import ctypes
+    from emqx_amd import _lib
+    fw, eng, st, _ = config_e_tables(args, rank, dev)
+    L = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libbatchload.so"))
+    L.pub_load.restype = ctypes.c_int
+    L.pub_load.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                           ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+    from emqx_amd.fanout import STRATEGIES
+    strat = STRATEGIES[args.strategy]
+    tb, to = fw.wl.topics
+    to = np.ascontiguousarray(to.astype(np.uint64))
+    keys = np.ascontiguousarray(fw.keys.astype(np.uint32))
+    runs = []
+    waits = [int(x) for x in str(args.max_wait_us).split(",")]
+    for c, wus in [(int(x), w) for x in args.callers.split(",") for w in waits]:
+        out = np.zeros(13, dtype=np.float64)
+        rc = L.pub_load(eng._h, st.handle, strat, tb.ctypes.data, to.ctypes.data, keys.ctypes.data, fw.wl.n_topics, c,
+                        args.max_batch, wus, 500.0, 3000.0, out.ctypes.data)
+        if rc != 0:
+            raise SystemExit(f"pub_load failed: {rc} ({_lib.lib().emqx_strerror(rc).decode()})")
+        runs.append({"callers": c, "max_wait_us": wus, "messages_per_s": round(out[0] / out[1], 1),
+                     "p50_us": round(out[2], 1), "p90_us": round(out[3], 1), "p99_us": round(out[4], 1),
+                     "max_us": round(out[5], 1), "batches": int(out[6]), "messages_per_batch": round(out[7], 1),
+                     "deliveries_per_message": round(out[12], 3), "max_in_flight": int(out[8]),
+                     "us_per_batch_device_wait": round(out[9], 1), "us_per_batch_callbacks": round(out[10], 1),
+                     "us_per_batch_submit": round(out[11], 1)})
+        log(f"[rank {rank}] callers {c}: {runs[-1]}")
+    best = max(runs, key=lambda r: r["messages_per_s"])
+    res = {"metric": "per-PUBLISH emqx_broker:publish/1 fan-outs served/sec through the publish batcher "
+                     "(config E, 10M subscriptions)",
+           "value": best["messages_per_s"], "unit": "messages/s", "n_gpus": world, "steps": len(runs),
+           "warmup": 1, "ms_per_step": 3000.0, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+           "config": {"workload": "P: concurrent single-message publishers -> emqx_pub_batcher -> pinned publish "
+                                  "batches (match + fan-out) on config E's tables",
+                      "n_filters": fw.wl.n_filters, "subscriptions": fw.n_subscriptions,
+                      "strategy": args.strategy, "max_batch": args.max_batch, "parallelism": "replicated tables"},
+           "runs": runs}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        args.cpu_sample = min(args.cpu_sample, 200_000)
+        res["cpu_baseline"] = fanout_cpu_baseline(fw, args)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def subscribe_bench(args, rank, world, dev):
+    """Subscription churn on config E's 10M-subscription table (emqx_broker:subscribe/3 and
+    unsubscribe/1, emqx_broker.erl:124-195; emqx_shared_sub's subscribe/unsubscribe,
+    emqx_shared_sub.erl:308-322): `--rounds` commits of `--churn` unsubscribes of live
+    subscriptions plus `--churn` new subscriptions (10% into existing $share groups), each round
+    = emqx_subtab_remove + emqx_subtab_add + emqx_subtab_commit (patched in place on the device).
+    After the rounds the device fan-out of a topic sample is compared with the oracle's after
+    the same ops (count + order-free checksum per topic, hash_clientid picks); the CPU baseline
+    is the oracle applying the same ops to its ETS-bag restatement on the host cores."""
+    import torch
+    from emqx_amd import workloads as W
+    from oracle import cpp as C
+    fw, eng, st, full_ms = config_e_tables(args, rank, dev)
+    rng = np.random.default_rng(21)
+    k = args.churn
+    n_sub = len(fw.sub_id)
+    present = np.ones(n_sub, bool)
+    shared_idx = np.flatnonzero(fw.sub_group != W.NO_GROUP)
+    next_sub = int(fw.sub_id.max()) + 1
+    nf = int(fw.wl.n_filters)
+    ops_f, ops_s, ops_g, ops_a = [], [], [], []
+    times, commit_ms = [], []
+    c0 = st.commit_stats()
+    for r in range(args.rounds):
+        idx = rng.choice(n_sub, k + k // 4, replace=False)
+        rem = idx[present[idx]][:k]
+        present[rem] = False
+        # new subscriptions: 90% plain to random filters, 10% new members of existing groups
+        n_sh = k // 10
+        gi = rng.choice(shared_idx, n_sh)
+        af = np.concatenate([rng.integers(0, nf, k - n_sh).astype(np.uint32), fw.sub_filter[gi]])
+        asub = np.arange(next_sub, next_sub + k, dtype=np.uint32)
+        next_sub += k
+        ag = np.concatenate([np.full(k - n_sh, W.NO_GROUP, np.uint32), fw.sub_group[gi]])
+        rf, rs, rg = fw.sub_filter[rem], fw.sub_id[rem], fw.sub_group[rem]
+        t = time.perf_counter()
+        st.remove(rf, rs, rg)
+        st.add(af, asub, ag)
+        tc = time.perf_counter()
+        st.commit()
+        t_end = time.perf_counter()
+        times.append(t_end - t)
+        commit_ms.append(1e3 * (t_end - tc))
+        ops_f += [rf, af]
+        ops_s += [rs, asub]
+        ops_g += [rg, ag]
+        ops_a += [np.zeros(len(rf), np.uint8), np.ones(len(af), np.uint8)]
+    c1 = st.commit_stats()
+    n_ops = int(sum(len(a) for a in ops_a))
+    value = n_ops / sum(times)
+    # parity after the churn: device fan-out of a topic sample vs the oracle with the same ops
+    n = fw.wl.n_topics
+    sample = min(args.cpu_sample, n, 200_000)
+    tb = torch.from_numpy(fw.wl.topics[0]).to(dev)
+    to = torch.from_numpy(fw.wl.topics[1].view(np.int64)).to(dev)
+    moff = torch.empty(sample + 1, dtype=torch.int64, device=dev)
+    mcap = 64 * sample
+    mids = torch.empty(mcap, dtype=torch.int32, device=dev)
+    nm = eng.match_device(tb.data_ptr(), to.data_ptr(), sample, moff.data_ptr(), mids.data_ptr(), mcap)
+    keys = torch.from_numpy(fw.keys[:sample].view(np.int32)).to(dev)
+    ooff = torch.empty(sample + 1, dtype=torch.int64, device=dev)
+    ocap = 256 * sample
+    osubs = torch.empty(ocap, dtype=torch.int32, device=dev)
+    ofil = torch.empty(ocap, dtype=torch.int32, device=dev)
+    tot = st.fanout_device("hash_clientid", moff.data_ptr(), mids.data_ptr(), sample, keys.data_ptr(), ooff.data_ptr(),
+                           osubs.data_ptr(), ofil.data_ptr(), ocap)
+    off_g = ooff.cpu().numpy().view(np.uint64)
+    gsum = C.delivery_checksums(off_g, osubs[:tot].cpu().numpy().view(np.uint32), ofil[:tot].cpu().numpy().view(np.uint32))
+    fo = C.FanoutOracle(fw.sub_filter, fw.sub_id, fw.sub_group)
+    threads = args.cpu_threads or host_threads()[0]
+    of, os_, og, oa = (np.concatenate(x) for x in (ops_f, ops_s, ops_g, ops_a))
+    t = time.perf_counter()
+    changed = fo.churn(of, os_, og, oa, threads=threads)
+    cpu_s = time.perf_counter() - t
+    mo, mi = moff.cpu().numpy().view(np.uint64), mids[:nm].cpu().numpy().view(np.uint32)
+    counts, sums, total = fo.publish(mo, mi, fw.keys[:sample], threads=threads)
+    bad = np.nonzero((np.diff(off_g.astype(np.int64)) != counts.astype(np.int64)) | (gsum != sums))[0]
+    if bad.size:
+        raise SystemExit(f"fan-out after churn differs from the oracle on {bad.size} topics, first {bad[:10].tolist()}")
+    res = {"metric": "subscription ops/s (subscribe + unsubscribe, committed to the device) at 10M subscriptions",
+           "value": round(value, 1), "unit": "ops/s", "n_gpus": world, "steps": args.rounds, "warmup": 0,
+           "ms_per_step": round(1e3 * float(np.mean(times)), 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+           "config": {"workload": "S: subscription churn on config E's 10M-subscription table",
+                      "subscriptions": fw.n_subscriptions, "ops_per_commit": n_ops // args.rounds,
+                      "shared_fraction_of_new": 0.1, "parallelism": "replicated tables"},
+           "commit_ms": {"p50": round(float(np.median(commit_ms)), 3), "p99": round(float(np.percentile(commit_ms, 99)), 3),
+                         "first": round(commit_ms[0], 3), "last": round(commit_ms[-1], 3)},
+           "full_build_commit_ms": round(full_ms, 1),
+           "commit_stats": {"incremental_commits": int(c1["commits"] - c0["commits"] - (c1["full_commits"] - c0["full_commits"])),
+                            "full_commits": int(c1["full_commits"] - c0["full_commits"]),
+                            "words_per_commit": round((c1["words"] - c0["words"]) / args.rounds, 1),
+                            "records_per_commit": round((c1["records"] - c0["records"]) / args.rounds, 1),
+                            "extents_moved_per_commit": round((c1["moves"] - c0["moves"]) / args.rounds, 1),
+                            "host_us_last_commit": c1["host_us"]},
+           "cpu_baseline": {"value": round(n_ops / cpu_s, 1), "unit": "ops/s", "cores": threads, "kind": "port",
+                            "sample": f"the same {n_ops} ops (oracle/fanout_oracle.cpp orf_churn: ETS-bag insert / "
+                                      "delete_object restatement, ops split by filter over the threads, no mria)",
+                            "changed": changed},
+           "parity": {"topics_checked": int(sample), "deliveries_checked": int(total), "mismatches": 0,
+                      "rule": "after all rounds: per-topic delivery count + order-free multiset checksum of "
+                              "(subscriber, filter), device fan-out vs the oracle with the same ops"}}
     if rank == 0:
         print(json.dumps(res), flush=True)
 

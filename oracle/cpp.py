@@ -50,6 +50,8 @@ def lib():
         L.orf_publish.restype = ctypes.c_uint64
         L.orf_publish.argtypes = [vp, u64p, u32p, ctypes.c_uint64, u32p, ctypes.c_int, u32p, u64p]
         L.orf_checksum.argtypes = [u64p, u32p, u32p, ctypes.c_uint64, u64p]
+        L.orf_churn.restype = ctypes.c_uint64
+        L.orf_churn.argtypes = [vp, u32p, u32p, u32p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
         L.orc_topic_match.restype = ctypes.c_int
         L.orc_topic_match.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint64]
         _lib = L
@@ -164,6 +166,14 @@ class FanoutOracle:
         total = lib().orf_publish(self.h, _p(moff), _p(mids) if mids.size else None, n, _p(keys), threads,
                                   _p(counts), _p(sums))
         return counts[:n], sums[:n], int(total)
+
+    def churn(self, sub_filter, sub_id, sub_group, add, threads=1) -> int:
+        """Subscribe (add) / unsubscribe operations as the reference's ETS bags take them
+        (oracle/fanout_oracle.cpp orf_churn); returns the ops that changed the table."""
+        a = [np.ascontiguousarray(np.asarray(x, dtype=np.uint32)) for x in (sub_filter, sub_id, sub_group)]
+        ad = np.ascontiguousarray(np.asarray(add, dtype=np.uint8))
+        return int(lib().orf_churn(self.h, _p(a[0]), _p(a[1]), _p(a[2]), ad.ctypes.data_as(ctypes.c_void_p), len(ad),
+                                   threads))
 
 
 def delivery_checksums(off, subs, fils):

@@ -12,7 +12,16 @@
 //       :287-288), Key = the caller's erlang:phash2 value (not restated).
 // Per topic it reports the delivery count and an order-free checksum of its deliveries
 // (sum of mix(sub, filter | shared bit)), so a multiset comparison with the GPU's CSR needs no
-// sort.  Build: oracle/Makefile -> oracle/_build/liboracle.so.
+// sort.  orf_churn applies subscribe / unsubscribe operations as the reference's tables take
+// them (the CPU baseline of bench.py --workload S):
+//   emqx_broker:do_subscribe/3 ets:insert(?SUBSCRIBER, {Topic, SubPid}) on a bag
+//       (apps/emqx/src/emqx_broker.erl:146-164; an identical object is stored once);
+//   emqx_broker:do_unsubscribe ets:delete_object(?SUBSCRIBER, {Topic, SubPid}) (:183-195);
+//   emqx_shared_sub subscribe/unsubscribe: the {Group, Topic, SubPid} bag write / delete_object
+//       (emqx_shared_sub.erl:308-322), members kept in insertion order.
+// ETS takes writes to different keys concurrently (write_concurrency), so the ops are split by
+// filter over the threads, each thread applying its filters' ops in order.
+// Build: oracle/Makefile -> oracle/_build/liboracle.so.
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -112,6 +121,52 @@ uint64_t orf_publish(void* h, const uint64_t* moff, const uint32_t* mids, uint64
   }
   for (auto& x : th) x.join();
   return total.load();
+}
+
+// Subscribe (add = 1) / unsubscribe (add = 0) operations, in order per filter.  Returns the
+// operations that changed the table.
+uint64_t orf_churn(void* h, const uint32_t* filt, const uint32_t* sub, const uint32_t* grp, const uint8_t* add,
+                   uint64_t n, int nthreads) {
+  Fanout* f = static_cast<Fanout*>(h);
+  uint32_t nf = static_cast<uint32_t>(f->plain.size());
+  for (uint64_t i = 0; i < n; ++i) nf = std::max(nf, filt[i] + 1);
+  f->plain.resize(nf);
+  f->groups.resize(nf);
+  if (nthreads < 1) nthreads = 1;
+  std::atomic<uint64_t> changed{0};
+  auto work = [&](int k) {
+    uint64_t ch = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint32_t fid = filt[i];
+      if (static_cast<int>(fid % static_cast<uint32_t>(nthreads)) != k) continue;
+      std::vector<uint32_t>* v;
+      if (grp[i] == NO_GROUP) {
+        v = &f->plain[fid];
+      } else {
+        auto& gs = f->groups[fid];
+        auto it = std::find_if(gs.begin(), gs.end(), [&](const Group& g) { return g.id == grp[i]; });
+        if (it == gs.end()) {
+          if (!add[i]) continue;
+          gs.push_back(Group{grp[i], {}});
+          it = gs.end() - 1;
+        }
+        v = &it->members;
+      }
+      auto pos = std::find(v->begin(), v->end(), sub[i]);
+      if (add[i] && pos == v->end()) {
+        v->push_back(sub[i]);
+        ++ch;
+      } else if (!add[i] && pos != v->end()) {
+        v->erase(pos);  // keeps the others' order
+        ++ch;
+      }
+    }
+    changed += ch;
+  };
+  std::vector<std::thread> th;
+  for (int k = 0; k < nthreads; ++k) th.emplace_back(work, k);
+  for (auto& x : th) x.join();
+  return changed.load();
 }
 
 // The same checksum of a GPU delivery CSR (off[n+1], subs, filters with the shared bit).

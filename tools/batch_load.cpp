@@ -7,6 +7,11 @@
 // with one emqx_batcher_submit_many (as a NIF draining a scheduler's queue would).  Throughput and latency
 // percentiles over the measured window go to out[] (12 entries).
 //
+// pub_load does the same through the publish batcher (emqx_pub_batcher_*: match + fan-out per
+// message, as emqx_broker:publish/1 is called once per PUBLISH, emqx_broker.erl:203-214), with
+// each caller's message key (the phash2 key of the hash strategies, or the caller's own
+// publisher handle for round_robin / sticky).
+//
 // Built by __graft_entry__.build() into tools/_build/libbatchload.so; the emqx_batcher_*
 // symbols resolve against libemqxmatch.so, which the caller has loaded (RTLD_GLOBAL).
 #include <stdint.h>
@@ -41,6 +46,8 @@ struct Load {
 
 Load* g_load = nullptr;  // the run in progress (one at a time)
 
+std::atomic<uint64_t> g_deliveries{0};
+
 // ctx = caller index + 1
 void on_result(void* ctx, int status, const uint32_t*, uint64_t) {
   Load* L = g_load;
@@ -56,7 +63,156 @@ void on_result(void* ctx, int status, const uint32_t*, uint64_t) {
   if (wake) d.cv.notify_one();
 }
 
+void on_publish(void* ctx, int status, const uint32_t*, const uint32_t*, uint64_t n) {
+  g_deliveries.fetch_add(n, std::memory_order_relaxed);
+  on_result(ctx, status, nullptr, n);
+}
+
+// The closed loop shared by both batchers: `submit_one(c, i)` / `submit_batch(cs, is)` hand the
+// batcher caller c's next message i.
+template <class One, class Many>
+int run_load(uint64_t n, uint32_t callers, double warmup_ms, double duration_ms, Load& L, One submit_one,
+             Many submit_many, std::vector<std::vector<float>>& lat, std::vector<uint64_t>& completed, double* secs) {
+  std::atomic<uint64_t> next{0};
+  const auto t_start = Clock::now();
+  const auto t_meas = t_start + std::chrono::microseconds(static_cast<int64_t>(warmup_ms * 1e3));
+  const auto t_end = t_meas + std::chrono::microseconds(static_cast<int64_t>(duration_ms * 1e3));
+  std::atomic<int> err{EMQX_OK};
+  std::vector<std::thread> th;
+  for (uint32_t d = 0; d < L.D; ++d)
+    th.emplace_back([&, d] {
+      Driver& me = L.drv[d];
+      uint64_t outstanding = 0;
+      for (uint32_t c = d; c < callers; c += L.D, ++outstanding) {
+        L.t_sub[c] = Clock::now();
+        const int r = submit_one(c, next.fetch_add(1) % n);
+        if (r != EMQX_OK) err = r;
+      }
+      std::vector<uint32_t> got, again;
+      std::vector<uint64_t> idx;
+      while (outstanding) {
+        {
+          std::unique_lock<std::mutex> lk(me.mu);
+          me.waiting = true;
+          me.cv.wait(lk, [&] { return !me.done.empty(); });
+          me.waiting = false;
+          got.swap(me.done);
+        }
+        const auto now = Clock::now();
+        again.clear();
+        for (uint32_t c : got) {
+          --outstanding;
+          if (now >= t_meas && L.t_sub[c] >= t_meas && now < t_end) {
+            lat[d].push_back(std::chrono::duration<float, std::micro>(now - L.t_sub[c]).count());
+            completed[d] += 1;
+          }
+          if (now < t_end && err.load() == EMQX_OK) again.push_back(c);
+        }
+        got.clear();
+        if (!again.empty()) {  // the finished callers' next messages, under one batcher lock
+          idx.clear();
+          const auto ts = Clock::now();
+          for (uint32_t c : again) {
+            idx.push_back(next.fetch_add(1) % n);
+            L.t_sub[c] = ts;
+          }
+          const int r = submit_many(again, idx);
+          if (r != EMQX_OK) err = r;
+          outstanding += again.size();
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  *secs = std::chrono::duration<double>(std::min(Clock::now(), t_end) - t_meas).count();
+  return err.load();
+}
+
+void summarize(Load& L, std::vector<std::vector<float>>& lat, std::vector<uint64_t>& completed, double secs,
+               const uint64_t* ext, double* out) {
+  std::vector<float> all;
+  uint64_t done = 0;
+  for (uint32_t d = 0; d < L.D; ++d) {
+    all.insert(all.end(), lat[d].begin(), lat[d].end());
+    done += completed[d];
+  }
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double q) -> double {
+    if (all.empty()) return 0;
+    return all[std::min<size_t>(all.size() - 1, static_cast<size_t>(q * all.size()))];
+  };
+  const uint64_t nb = ext[0], nt = ext[1];
+  out[0] = static_cast<double>(done);
+  out[1] = secs;
+  out[2] = pct(0.50);
+  out[3] = pct(0.90);
+  out[4] = pct(0.99);
+  out[5] = all.empty() ? 0 : all.back();
+  out[6] = static_cast<double>(nb);
+  out[7] = nb ? static_cast<double>(nt) / nb : 0;
+  out[8] = static_cast<double>(ext[2]);          // most batches in flight
+  out[9] = nb ? ext[3] / 1e3 / nb : 0;           // us per batch: completer waiting for the device
+  out[10] = nb ? ext[4] / 1e3 / nb : 0;          // us per batch: callbacks
+  out[11] = nb ? ext[5] / 1e3 / nb : 0;          // us per batch: submit
+}
+
 }  // namespace
+
+// Publish batcher: out[0..11] as batch_load, out[12] = deliveries per message.
+extern "C" int pub_load(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const uint8_t* bytes, const uint64_t* offs,
+                        const uint32_t* keys, uint64_t n, uint32_t callers, uint32_t max_batch, uint32_t max_wait_us,
+                        double warmup_ms, double duration_ms, double* out) {
+  if (!e || !s || !bytes || !offs || !n || !callers || !out) return EMQX_EINVAL;
+  Load L;
+  L.D = std::min<uint32_t>(callers, 8);
+  L.drv = std::vector<Driver>(L.D);
+  L.t_sub.resize(callers);
+  L.status.assign(callers, EMQX_OK);
+  g_load = &L;
+  g_deliveries = 0;
+  emqx_pub_batcher* b = nullptr;
+  int rc = emqx_pub_batcher_create(e, s, strategy, max_batch, max_wait_us, on_publish, &b);
+  if (rc != EMQX_OK) return rc;
+  // round_robin / sticky: the key is the publisher, i.e. the caller; hash strategies: the
+  // message's own phash2 key
+  const bool per_caller = strategy == EMQX_SHARE_ROUND_ROBIN || strategy == EMQX_SHARE_STICKY;
+  auto key_of = [&](uint32_t c, uint64_t i) -> uint32_t { return per_caller ? c : (keys ? keys[i] : 0u); };
+  std::vector<std::vector<float>> lat(L.D);
+  std::vector<uint64_t> completed(L.D, 0);
+  double secs = 0;
+  auto one = [&](uint32_t c, uint64_t i) {
+    return emqx_pub_batcher_submit(b, bytes + offs[i], offs[i + 1] - offs[i], key_of(c, i),
+                                   reinterpret_cast<void*>(static_cast<uintptr_t>(c) + 1));
+  };
+  thread_local std::vector<uint8_t> mb;
+  thread_local std::vector<uint64_t> mo;
+  thread_local std::vector<uint32_t> mk;
+  thread_local std::vector<void*> mc;
+  auto many = [&](const std::vector<uint32_t>& cs, const std::vector<uint64_t>& is) {
+    mb.clear();
+    mo.assign(1, 0);
+    mk.clear();
+    mc.clear();
+    for (size_t j = 0; j < cs.size(); ++j) {
+      const uint64_t i = is[j];
+      mb.insert(mb.end(), bytes + offs[i], bytes + offs[i + 1]);
+      mo.push_back(mb.size());
+      mk.push_back(key_of(cs[j], i));
+      mc.push_back(reinterpret_cast<void*>(static_cast<uintptr_t>(cs[j]) + 1));
+    }
+    return emqx_pub_batcher_submit_many(b, mb.data(), mo.data(), mk.data(), cs.size(), mc.data());
+  };
+  const uint64_t before = 0;
+  int err = run_load(n, callers, warmup_ms, duration_ms, L, one, many, lat, completed, &secs);
+  uint64_t ext[6] = {0, 0, 0, 0, 0, 0};
+  emqx_pub_batcher_stats_ext(b, ext, 6);
+  emqx_pub_batcher_destroy(b);
+  g_load = nullptr;
+  summarize(L, lat, completed, secs, ext, out);
+  out[12] = ext[1] ? static_cast<double>(g_deliveries.load() - before) / ext[1] : 0;
+  for (int st : L.status)
+    if (st != EMQX_OK) return st;
+  return err;
+}
 
 extern "C" int batch_load(emqx_engine* e, uint32_t mode, const uint8_t* bytes, const uint64_t* offs, uint64_t n,
                           uint32_t callers, uint32_t max_batch, uint32_t max_wait_us, double warmup_ms,
