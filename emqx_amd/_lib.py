@@ -46,7 +46,8 @@ EXPORTS = (
     "emqx_pub_batcher_submit_many", "emqx_pub_batcher_destroy", "emqx_pub_batcher_stats_ext",
     "emqx_host_batch_create", "emqx_host_batch_destroy", "emqx_host_batch_reserve", "emqx_host_batch_submit",
     "emqx_host_batch_wait", "emqx_host_batch_query",
-    "emqx_commit_stats", "emqx_shard_owner", "emqx_shard_owner_device", "emqx_permute_scratch_bytes", "emqx_batch_permute_device", "emqx_owner_sort_scratch_bytes",
+    "emqx_commit_stats", "emqx_shard_owner", "emqx_shard_owner_device",
+    "emqx_shard_plan", "emqx_shard_place", "emqx_shard_route", "emqx_shard_route_device", "emqx_permute_scratch_bytes", "emqx_batch_permute_device", "emqx_owner_sort_scratch_bytes",
     "emqx_owner_sort_device",
     "emqx_csr_unpermute_device", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
     "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check",
@@ -60,6 +61,7 @@ RETAIN_EXPORTS = (
 )
 
 NO_GROUP = 0xFFFFFFFF
+SHARD_NONE = 0xFFFFFFFF
 FANOUT_SHARED_BIT = 0x80000000
 SHARE_RANDOM, SHARE_ROUND_ROBIN, SHARE_STICKY, SHARE_HASH_CLIENTID, SHARE_HASH_TOPIC = 0, 1, 2, 3, 4
 
@@ -219,6 +221,10 @@ def lib():
         "emqx_commit_stats": (i32, [vp, vp, u32]),
         "emqx_shard_owner": (i32, [vp, vp, u64, u32, u32, i32, vp]),
         "emqx_shard_owner_device": (i32, [vp, vp, u64, u32, u32, vp, vp]),
+        "emqx_shard_plan": (i32, [vp, vp, u64, u32, u32, vp, u32, ctypes.POINTER(u32)]),
+        "emqx_shard_place": (i32, [vp, vp, u64, u32, vp, u32, vp, vp, vp]),
+        "emqx_shard_route": (i32, [vp, vp, u64, u32, vp, u32, vp]),
+        "emqx_shard_route_device": (i32, [vp, vp, u64, u32, vp, u32, vp, vp]),
         "emqx_permute_scratch_bytes": (u64, [u64]),
         "emqx_owner_sort_scratch_bytes": (u64, [u64, u32]),
         "emqx_owner_sort_device": (i32, [vp, u64, u32, vp, vp, vp]),

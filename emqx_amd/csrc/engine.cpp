@@ -1279,6 +1279,14 @@ int emqx_shard_owner_device(const uint8_t* d_bytes, const uint64_t* d_offsets, u
   return EMQX_OK;
 }
 
+int emqx_shard_route_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t world,
+                            const emqx_shard_split* d_splits, uint32_t n_splits, uint32_t* d_req2, void* stream) {
+  if ((n && (!d_bytes || !d_offsets || !d_req2)) || world == 0 || (n_splits && !d_splits)) return EMQX_EINVAL;
+  HIP_TRY(launch_shard_route(d_bytes, d_offsets, n, world, reinterpret_cast<const ShardSplitE*>(d_splits), n_splits,
+                             d_req2, static_cast<hipStream_t>(stream)));
+  return EMQX_OK;
+}
+
 int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n) {
   if (!e || (n && !out)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(e->writer);

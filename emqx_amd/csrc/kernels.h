@@ -140,6 +140,8 @@ hipError_t launch_csr_to_host(const uint64_t* d_off, uint64_t n, const uint32_t*
 // filter-sharded tables: owner rank of every topic of a device batch
 hipError_t launch_shard_owner(const uint8_t* tbytes, const uint64_t* toffs, uint64_t n, uint32_t world,
                               uint32_t levels, uint32_t* owner, hipStream_t s);
+hipError_t launch_shard_route(const uint8_t* tbytes, const uint64_t* toffs, uint64_t n, uint32_t world,
+                              const ShardSplitE* splits, uint32_t n_splits, uint32_t* req2, hipStream_t s);
 // incremental commits (live_trie.cpp): whole-slot rewrites of the committed table, ids first
 hipError_t launch_slot_patches(EdgeSlot* edges, uint32_t* fids, const SlotPatch* patches, uint32_t n,
                                hipStream_t s);

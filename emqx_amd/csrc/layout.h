@@ -204,4 +204,142 @@ EMQX_HD uint32_t shard_owner(const uint8_t* p, uint64_t n, uint32_t world, uint3
   return mix32(h ^ k) % world;
 }
 
+// ---- filter-sharded layout with two key spaces (emqx_amd/dist.py) ----------
+// A topic t = l1/l2/l3/... can be matched by three kinds of filter:
+//   root-wildcard  '#', '+', '+/#', '+/+/...'      -> every rank (replicated)
+//   space L        a literal first level l1         -> placed by (l1, l2)
+//   space P        '+' then a literal second level  -> placed by (l2, l3)
+// A space's key is its first level (l1, or l2 for space P); a key with few filters lives on one
+// rank (a hash of it), a hot key (the plan, emqx_shard_plan) is split over `span` consecutive
+// ranks by the next level, filters whose next level is a wildcard (or who end at the key...
+// see shard_place_key) going to all `span` ranks of the key.  A topic is sent to its L-space
+// rank (engine "A": space L + root-wildcard filters) and, when it has two levels and does not
+// start with '$', to its P-space rank (engine "B": space P filters): every filter that can match
+// it lives on one of the two, exactly once, so the two answers concatenate into the match set.
+constexpr uint32_t SHARD_NONE = 0xFFFFFFFFu;
+constexpr uint32_t SHARD_SPACE_P = 0x80000000u;  // key bit of space P keys
+constexpr uint32_t SHARD_PAIR = 0x40000000u;     // key bit of (split key, next level) entries
+constexpr uint32_t SHARD_HASH_MASK = 0x3FFFFFFFu;
+constexpr uint32_t SHARD_ABSENT = 0x9E3779B9u;   // the hash of "no next level"
+
+// One plan entry: a key (space bit | 30-bit level hash; info = first rank | span << 16), or a
+// next level of a split key (SHARD_PAIR | space bit | 30-bit pair hash; info = its rank).
+struct ShardSplitE {
+  uint32_t key, info;
+};
+
+EMQX_HD uint32_t shard_level_hash(const uint8_t* p, uint64_t s, uint64_t e) {
+  uint32_t h = 0x811C9DC5u;  // FNV-1a over the level's bytes
+  for (uint64_t i = s; i < e; ++i) h = (h ^ p[i]) * 0x01000193u;
+  return mix32(h ^ static_cast<uint32_t>(e - s));
+}
+
+EMQX_HD uint32_t shard_split_find(const ShardSplitE* sp, uint32_t n, uint32_t key) {
+  uint32_t lo = 0, hi = n;  // sorted by key
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sp[mid].key < key) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && sp[lo].key == key ? sp[lo].info : SHARD_NONE;
+}
+
+// Level k of p[0, n): bounds [*s, *e); false if the name has fewer levels.
+EMQX_HD bool shard_level(const uint8_t* p, uint64_t n, uint32_t k, uint64_t* s, uint64_t* e) {
+  uint64_t a = 0;
+  for (uint32_t j = 0; j < k; ++j) {
+    while (a < n && p[a] != '/') ++a;
+    if (a >= n) return false;
+    ++a;
+  }
+  uint64_t b = a;
+  while (b < n && p[b] != '/') ++b;
+  *s = a;
+  *e = b;
+  return true;
+}
+
+EMQX_HD bool shard_is_wild(const uint8_t* p, uint64_t s, uint64_t e) {
+  return e - s == 1 && (p[s] == '+' || p[s] == '#');
+}
+
+// Rank range [*first, *first + *span) (mod world) of key hash `hk` in `space` given its next
+// level: `next` = its hash, or SHARD_ABSENT (no next level), or SHARD_NONE (a wildcard: every
+// rank of the key).
+EMQX_HD void shard_place_key(uint32_t space, uint32_t hk, uint32_t next, uint32_t world, const ShardSplitE* sp,
+                             uint32_t nsp, uint32_t* first, uint32_t* span) {
+  const uint32_t info = shard_split_find(sp, nsp, space | (hk & SHARD_HASH_MASK));
+  if (info == SHARD_NONE) {
+    *first = mix32(hk ^ (space ? 0x5BD1E995u : 0x27D4EB2Fu)) % world;
+    *span = 1;
+    return;
+  }
+  const uint32_t base = info & 0xFFFFu, s = info >> 16;
+  if (next == SHARD_NONE) {
+    *first = base;
+    *span = s;
+    return;
+  }
+  const uint32_t pair = mix32(next ^ hk);
+  const uint32_t pinfo = s > 1 && next != SHARD_ABSENT
+                             ? shard_split_find(sp, nsp, SHARD_PAIR | space | (pair & SHARD_HASH_MASK))
+                             : SHARD_NONE;
+  *first = pinfo != SHARD_NONE ? (pinfo & 0xFFFFu) : (base + pair % s) % world;
+  *span = 1;
+}
+
+// Placement of filter p[0, n): *engine 0 (A: space L, root-wildcard) or 1 (B: space P).
+EMQX_HD void shard_place_filter(const uint8_t* p, uint64_t n, uint32_t world, const ShardSplitE* sp, uint32_t nsp,
+                                uint32_t* first, uint32_t* span, uint32_t* engine) {
+  uint64_t s1, e1, s2, e2, s3, e3;
+  shard_level(p, n, 0, &s1, &e1);
+  const bool has2 = shard_level(p, n, 1, &s2, &e2);
+  *engine = 0;
+  if (shard_is_wild(p, s1, e1)) {
+    if (p[s1] == '#' || !has2 || shard_is_wild(p, s2, e2)) {  // '#', '+', '+/#', '+/+/...'
+      *first = 0;
+      *span = world;
+      return;
+    }
+    *engine = 1;  // '+/x/...': space P, keyed by x, split by the third level
+    const bool has3 = shard_level(p, n, 2, &s3, &e3);
+    const uint32_t next = !has3 ? SHARD_ABSENT : shard_is_wild(p, s3, e3) ? SHARD_NONE : shard_level_hash(p, s3, e3);
+    shard_place_key(SHARD_SPACE_P, shard_level_hash(p, s2, e2), next, world, sp, nsp, first, span);
+    return;
+  }
+  const uint32_t next = !has2 ? SHARD_ABSENT : shard_is_wild(p, s2, e2) ? SHARD_NONE : shard_level_hash(p, s2, e2);
+  shard_place_key(0, shard_level_hash(p, s1, e1), next, world, sp, nsp, first, span);
+}
+
+// The requests of topic p[0, n): req[0] to engine A, req[1] to engine B, each rank * 2 + engine
+// or SHARD_NONE.  A wildcard topic (match_routes/1 returns only its byte-identical filter, S3)
+// makes one request, to the first rank of that filter.
+EMQX_HD void shard_route_topic(const uint8_t* p, uint64_t n, uint32_t world, const ShardSplitE* sp, uint32_t nsp,
+                               uint32_t* req) {
+  req[0] = req[1] = SHARD_NONE;
+  bool wild = false;
+  for (uint64_t a = 0; a < n && !wild;) {
+    uint64_t b = a;
+    while (b < n && p[b] != '/') ++b;
+    wild = shard_is_wild(p, a, b);
+    a = b + 1;
+  }
+  uint32_t first, span, engine;
+  if (wild) {
+    shard_place_filter(p, n, world, sp, nsp, &first, &span, &engine);
+    req[engine] = 2 * first + engine;
+    return;
+  }
+  uint64_t s1, e1, s2, e2, s3, e3;
+  shard_level(p, n, 0, &s1, &e1);
+  const bool has2 = shard_level(p, n, 1, &s2, &e2);
+  shard_place_key(0, shard_level_hash(p, s1, e1), has2 ? shard_level_hash(p, s2, e2) : SHARD_ABSENT, world, sp, nsp,
+                  &first, &span);
+  req[0] = 2 * first;
+  if (!has2 || (n > 0 && p[0] == '$')) return;  // '+/x/...' never matches a '$' topic (S5)
+  const bool has3 = shard_level(p, n, 2, &s3, &e3);
+  shard_place_key(SHARD_SPACE_P, shard_level_hash(p, s2, e2), has3 ? shard_level_hash(p, s3, e3) : SHARD_ABSENT,
+                  world, sp, nsp, &first, &span);
+  req[1] = 2 * first + 1;
+}
+
 }  // namespace emqx

@@ -7,7 +7,10 @@
 
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "../../include/emqx_match.h"
 #include "tables.h"
@@ -80,6 +83,160 @@ extern "C" int emqx_shard_owner(const uint8_t* bytes, const uint64_t* offsets, u
   for (uint64_t i = 0; i < n; ++i) {
     if (offsets[i + 1] < offsets[i]) return EMQX_EINVAL;
     owner_out[i] = emqx::shard_owner(bytes + offsets[i], offsets[i + 1] - offsets[i], world, levels, topics != 0);
+  }
+  return EMQX_OK;
+}
+
+// Filter-sharded layout with two key spaces (layout.h shard_place_filter / shard_route_topic).
+namespace {
+
+// The level hashes a filter contributes to the plan: its key (space bit | 30-bit hash) and its
+// next level (hash, SHARD_ABSENT, or SHARD_NONE for a wildcard).  false for root wildcards.
+bool plan_key(const uint8_t* p, uint64_t len, uint32_t* key, uint32_t* hk, uint32_t* next) {
+  uint64_t s1, e1, s2, e2, s3, e3;
+  emqx::shard_level(p, len, 0, &s1, &e1);
+  const bool has2 = emqx::shard_level(p, len, 1, &s2, &e2);
+  if (!emqx::shard_is_wild(p, s1, e1)) {
+    *hk = emqx::shard_level_hash(p, s1, e1);
+    *key = *hk & emqx::SHARD_HASH_MASK;
+    *next = !has2 ? emqx::SHARD_ABSENT : emqx::shard_is_wild(p, s2, e2) ? emqx::SHARD_NONE
+                                                                        : emqx::shard_level_hash(p, s2, e2);
+    return true;
+  }
+  if (p[s1] != '+' || !has2 || emqx::shard_is_wild(p, s2, e2)) return false;
+  *hk = emqx::shard_level_hash(p, s2, e2);
+  *key = emqx::SHARD_SPACE_P | (*hk & emqx::SHARD_HASH_MASK);
+  const bool has3 = emqx::shard_level(p, len, 2, &s3, &e3);
+  *next = !has3 ? emqx::SHARD_ABSENT : emqx::shard_is_wild(p, s3, e3) ? emqx::SHARD_NONE
+                                                                      : emqx::shard_level_hash(p, s3, e3);
+  return true;
+}
+
+}  // namespace
+
+extern "C" int emqx_shard_plan(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
+                               uint32_t max_piece_pm, emqx_shard_split* out, uint32_t cap, uint32_t* n_out) {
+  if ((n && !offsets) || !n_out || world == 0 || world > 65535 || max_piece_pm == 0 || (cap && !out))
+    return EMQX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return EMQX_EINVAL;
+  // per key of each space: its filters, and those whose next level is a wildcard (they go to
+  // every rank of a split key); root-wildcard filters are everywhere and count for no key
+  struct KeyLoad {
+    uint64_t all = 0, wild_next = 0;
+  };
+  std::unordered_map<uint32_t, KeyLoad> per_key;
+  uint32_t key, hk, next;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!plan_key(bytes + offsets[i], offsets[i + 1] - offsets[i], &key, &hk, &next)) continue;
+    KeyLoad& k = per_key[key];
+    ++k.all;
+    k.wild_next += next == emqx::SHARD_NONE ? 1u : 0u;
+  }
+  // Largest keys first onto the least-loaded ranks (LPT).  A key over max_piece_pm / 1000 of a
+  // rank's share is split over the fewest consecutive ranks that bring each piece under it: its
+  // wildcard-next filters go to all of them, its next-level words are placed one by one (the
+  // largest first) on the least-loaded rank of that window.  Every key or next word down to
+  // 1/4096 of a share is placed this way; the many smaller ones are left to the hash.
+  const double share = static_cast<double>(n) / world;
+  const double piece = share * max_piece_pm / 1000.0;
+  const double small = std::max(2.0, share / 4096.0);
+  std::vector<std::pair<uint32_t, KeyLoad>> keys;
+  for (const auto& kv : per_key)
+    if (static_cast<double>(kv.second.all) >= small) keys.push_back(kv);
+  auto by_size = [](const std::pair<uint32_t, KeyLoad>& a, const std::pair<uint32_t, KeyLoad>& b) {
+    return a.second.all != b.second.all ? a.second.all > b.second.all : a.first < b.first;
+  };
+  std::sort(keys.begin(), keys.end(), by_size);
+  std::unordered_map<uint32_t, std::pair<uint32_t, uint32_t>> split;  // key -> (first rank, span)
+  std::vector<uint32_t> span_of(keys.size(), 1);
+  for (size_t q = 0; q < keys.size(); ++q) {
+    uint32_t span = 1;
+    while (span < world && static_cast<double>(keys[q].second.all) / span > piece) span *= 2;
+    span_of[q] = std::min(span, world);
+    if (span_of[q] > 1) split[keys[q].first] = {0, span_of[q]};
+  }
+  // next-level words of the split keys
+  std::unordered_map<uint64_t, uint64_t> per_pair;  // key << 32 | pair hash -> filters
+  if (!split.empty()) {
+    for (uint64_t i = 0; i < n; ++i) {
+      if (!plan_key(bytes + offsets[i], offsets[i + 1] - offsets[i], &key, &hk, &next)) continue;
+      if (next == emqx::SHARD_NONE || next == emqx::SHARD_ABSENT || !split.count(key)) continue;
+      ++per_pair[(uint64_t(key) << 32) | (emqx::mix32(next ^ hk) & emqx::SHARD_HASH_MASK)];
+    }
+  }
+  std::unordered_map<uint32_t, std::vector<std::pair<uint32_t, uint64_t>>> pairs_of;
+  for (const auto& kv : per_pair)
+    if (static_cast<double>(kv.second) >= small)
+      pairs_of[static_cast<uint32_t>(kv.first >> 32)].push_back({static_cast<uint32_t>(kv.first), kv.second});
+  std::vector<double> load(world, 0.0);
+  std::vector<emqx_shard_split> sp;
+  for (size_t q = 0; q < keys.size(); ++q) {
+    const uint32_t span = span_of[q];
+    const double c = static_cast<double>(keys[q].second.all), g = static_cast<double>(keys[q].second.wild_next);
+    uint32_t best = 0;
+    double best_m = 0;
+    for (uint32_t b = 0; b < world; ++b) {  // the window of `span` ranks whose busiest is least busy
+      double m = 0;
+      for (uint32_t k = 0; k < span; ++k) m = std::max(m, load[(b + k) % world]);
+      if (b == 0 || m < best_m) {
+        best = b;
+        best_m = m;
+      }
+    }
+    sp.push_back(emqx_shard_split{keys[q].first, best | (span << 16)});
+    if (span == 1) {
+      load[best] += c;
+      continue;
+    }
+    for (uint32_t k = 0; k < span; ++k) load[(best + k) % world] += g;
+    auto& pv = pairs_of[keys[q].first];
+    std::sort(pv.begin(), pv.end(), [](const std::pair<uint32_t, uint64_t>& a, const std::pair<uint32_t, uint64_t>& b) {
+      return a.second != b.second ? a.second > b.second : a.first < b.first;
+    });
+    double placed = g;
+    for (const auto& pr : pv) {
+      uint32_t r = best;
+      for (uint32_t k = 1; k < span; ++k)
+        if (load[(best + k) % world] < load[r]) r = (best + k) % world;
+      load[r] += static_cast<double>(pr.second);
+      placed += static_cast<double>(pr.second);
+      sp.push_back(emqx_shard_split{emqx::SHARD_PAIR | (keys[q].first & emqx::SHARD_SPACE_P) | pr.first, r});
+    }
+    for (uint32_t k = 0; k < span; ++k) load[(best + k) % world] += (c - placed) / span;  // hashed rest
+  }
+  std::sort(sp.begin(), sp.end(), [](const emqx_shard_split& a, const emqx_shard_split& b) { return a.key < b.key; });
+  sp.erase(std::unique(sp.begin(), sp.end(),
+                       [](const emqx_shard_split& a, const emqx_shard_split& b) { return a.key == b.key; }),
+           sp.end());  // (a 30-bit collision: either entry gives a consistent placement)
+  *n_out = static_cast<uint32_t>(sp.size());
+  if (sp.size() > cap) return EMQX_EOVERFLOW;
+  std::copy(sp.begin(), sp.end(), out);
+  return EMQX_OK;
+}
+
+static_assert(sizeof(emqx_shard_split) == sizeof(emqx::ShardSplitE), "split layout");
+
+extern "C" int emqx_shard_place(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
+                                const emqx_shard_split* splits, uint32_t n_splits, uint32_t* first, uint32_t* span,
+                                uint32_t* engine) {
+  if ((n && (!offsets || !first || !span || !engine)) || world == 0 || (n_splits && !splits)) return EMQX_EINVAL;
+  const auto* sp = reinterpret_cast<const emqx::ShardSplitE*>(splits);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i]) return EMQX_EINVAL;
+    emqx::shard_place_filter(bytes + offsets[i], offsets[i + 1] - offsets[i], world, sp, n_splits, &first[i], &span[i],
+                             &engine[i]);
+  }
+  return EMQX_OK;
+}
+
+extern "C" int emqx_shard_route(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
+                                const emqx_shard_split* splits, uint32_t n_splits, uint32_t* req2) {
+  if ((n && (!offsets || !req2)) || world == 0 || (n_splits && !splits)) return EMQX_EINVAL;
+  const auto* sp = reinterpret_cast<const emqx::ShardSplitE*>(splits);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i]) return EMQX_EINVAL;
+    emqx::shard_route_topic(bytes + offsets[i], offsets[i + 1] - offsets[i], world, sp, n_splits, req2 + 2 * i);
   }
   return EMQX_OK;
 }

@@ -8,17 +8,23 @@ SURVEY §8(e).  Two layouts:
   across a cluster: every node holds a full mria copy of the route table
   (apps/emqx/src/emqx_router.erl:135, apps/emqx/src/emqx_trie.erl:72-77).
 
-* **Filter-sharded** (``ShardedMatcher``): a filter lives on the rank its first SHARD_LEVELS
-  (2) levels hash to (``emqx_shard_owner``); a filter with ``+`` or ``#`` among those levels, or
-  with fewer levels, can match topics of several keys and is replicated on every rank (about a
-  tenth of config B's filters).  Two key levels instead of one keep a Zipf-hot first level
-  (a third of the topics on config C's generator) from landing on one rank.  So every filter that can match a topic
-  lives on the topic's owner rank, and each topic is matched on exactly one rank: a batch is
-  partitioned by owner on its source rank, the parts are exchanged with one all-to-all, every
-  rank matches only its part against its shard, and the per-topic results go back to the
-  destination with a second all-to-all, where they are put back in batch order.  Per-rank walk
-  work falls as 1/G; the collectives move each topic and each result once.
-  Each rank builds its shard's trie with GLOBAL filter ids (``emqx_insert_filters_ext``).
+* **Filter-sharded** (``ShardedMatcher``, tables past one GPU): the filters are divided over
+  the ranks by two key spaces (include/emqx_match.h emqx_shard_*, layout.h):
+    - root-wildcard filters ('#', '+', '+/#', '+/+/...') live on every rank (engine A);
+    - space L: a filter with a literal first level l1 lives on the rank of l1 (engine A);
+    - space P: a filter '+/x/...' lives on the rank of x (engine B);
+    - a key with many filters (the plan, ``shard_plan``: Zipf-hot first words) is split over
+      consecutive ranks by the next level, its filters whose next level is a wildcard on all
+      of them.
+  A topic l1/l2/... makes one request to its L-space rank's engine A and, if it has a second
+  level and is not a '$' topic, one to its P-space rank's engine B; every filter that can match
+  it lives, once, on one of the two, so the answers concatenate (``shard_route``).  Each rank
+  partitions its batch's requests by (rank, engine), one all-to-all carries them to their
+  owners, each rank matches what it received on its two engines, and one all-to-all brings the
+  results back, where they are merged per topic in batch order.  The busiest rank holds
+  18 % of config C's filters at G = 8 (the replicated share was 29 % with the
+  round-2 layout), and each rank walks ~1/G of the topics' node visits.
+  Each engine is built with GLOBAL filter ids (``emqx_insert_filters_ext``).
 """
 
 from __future__ import annotations
@@ -176,143 +182,216 @@ def _a2a(out_t: torch.Tensor, in_t: torch.Tensor, out_splits: List[int], in_spli
     dist.all_to_all_single(out_t, in_t, out_splits, in_splits, group=group)
 
 
-class ShardedMatcher:
-    """A filter-sharded table over the ranks of a process group.
+SHARD_NONE = 0xFFFFFFFF
+MAX_PIECE_PM = 250  # a key is split when its filters exceed a quarter of a rank's share
 
-    ``match_fn(local_topics_bytes, local_topic_offsets) -> (counts int64 (n,), ids int32)`` does
-    the per-shard match; the default is this rank's HIP engine (device tensors).  Tests inject
-    the oracle to check the distribution logic over gloo on CPU."""
+
+def shard_plan(filters: Tuple[np.ndarray, np.ndarray], world: int, max_piece_pm: int = MAX_PIECE_PM) -> np.ndarray:
+    """The hot keys of a filter set (emqx_shard_plan): (k, 2) uint32 rows (key, first rank | span
+    << 16), sorted by key.  Every rank computes the same plan from the same filters."""
+    from . import _lib
+    buf, offs = filters
+    offs = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
+    n = len(offs) - 1
+    b = np.ascontiguousarray(buf) if len(buf) else np.zeros(1, np.uint8)
+    cap = 1024
+    while True:
+        out = np.zeros((cap, 2), dtype=np.uint32)
+        got = ctypes.c_uint32(0)
+        rc = _lib.lib().emqx_shard_plan(b.ctypes.data, offs.ctypes.data, n, world, max_piece_pm, out.ctypes.data,
+                                        cap, ctypes.byref(got))
+        if rc == _lib.EMQX_EOVERFLOW:
+            cap = int(got.value)
+            continue
+        _lib.check(rc, "emqx_shard_plan")
+        return out[: got.value].copy()
+
+
+def shard_place(filters: Tuple[np.ndarray, np.ndarray], world: int, plan: np.ndarray):
+    """(first rank, span, engine) per filter (emqx_shard_place): filter i lives on ranks
+    first[i] .. first[i] + span[i] - 1 (mod world), in engine A (0) or B (1)."""
+    from . import _lib
+    buf, offs = filters
+    offs = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
+    n = len(offs) - 1
+    first, span, eng = (np.zeros(max(n, 1), np.uint32) for _ in range(3))
+    b = np.ascontiguousarray(buf) if len(buf) else np.zeros(1, np.uint8)
+    pl = np.ascontiguousarray(plan, dtype=np.uint32) if len(plan) else np.zeros((1, 2), np.uint32)
+    _lib.check(_lib.lib().emqx_shard_place(b.ctypes.data, offs.ctypes.data, n, world, pl.ctypes.data, len(plan),
+                                           first.ctypes.data, span.ctypes.data, eng.ctypes.data), "emqx_shard_place")
+    return first[:n], span[:n], eng[:n]
+
+
+def shard_engines(filters: Tuple[np.ndarray, np.ndarray], rank: int, world: int, plan: np.ndarray):
+    """[(packed filters, global ids) of engine A, ... of engine B] for this rank."""
+    from .workloads import take
+    first, span, eng = shard_place(filters, world, plan)
+    held = ((rank - first.astype(np.int64)) % world) < span
+    out = []
+    for e in (0, 1):
+        gids = np.nonzero(held & (eng == e))[0]
+        out.append((take(filters, gids), gids.astype(np.uint32)))
+    return out
+
+
+def topic_requests(tb: torch.Tensor, to: torch.Tensor, world: int, plan: np.ndarray,
+                   plan_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(n, 2) int64 requests of each topic (emqx_shard_route): column 0 = rank * 2 of its engine-A
+    request, column 1 = rank * 2 + 1 of its engine-B request; -1 = none.  On the batch's
+    device (a HIP kernel for a GPU batch)."""
+    from . import _lib
+    n = to.numel() - 1
+    if tb.is_cuda:
+        req = torch.empty(max(2 * n, 2), dtype=torch.int32, device=tb.device)
+        if plan_dev is None:
+            plan_dev = torch.from_numpy(np.ascontiguousarray(plan, dtype=np.uint32).view(np.int32)).to(tb.device)
+        _lib.check(_lib.lib().emqx_shard_route_device(
+            ctypes.c_void_p(tb.data_ptr()), ctypes.c_void_p(to.data_ptr()), n, world,
+            ctypes.c_void_p(plan_dev.data_ptr()) if len(plan) else None, len(plan), ctypes.c_void_p(req.data_ptr()),
+            ctypes.c_void_p(torch.cuda.current_stream(tb.device).cuda_stream)), "emqx_shard_route_device")
+        return req[: 2 * n].to(torch.int64).reshape(n, 2)
+    buf = tb.numpy() if tb.numel() else np.zeros(1, np.uint8)
+    offs = np.ascontiguousarray(to.numpy().astype(np.uint64))
+    req = np.zeros(max(2 * n, 2), dtype=np.uint32)
+    pl = np.ascontiguousarray(plan, dtype=np.uint32) if len(plan) else np.zeros((1, 2), np.uint32)
+    _lib.check(_lib.lib().emqx_shard_route(np.ascontiguousarray(buf).ctypes.data, offs.ctypes.data, n, world,
+                                           pl.ctypes.data, len(plan), req.ctypes.data), "emqx_shard_route")
+    return torch.from_numpy(req[: 2 * n].view(np.int32).astype(np.int64)).reshape(n, 2)
+
+
+def _gather_topics(tb: torch.Tensor, to: torch.Tensor, idx: torch.Tensor):
+    """Topics idx[0], idx[1], ... of a packed batch as a new packed batch (bytes, offsets int64),
+    with a HIP gather for a device batch.  idx may repeat topics."""
+    dev = tb.device
+    k = idx.numel()
+    lens = (to[1:] - to[:-1]).to(torch.int64)[idx] if k else torch.zeros(0, dtype=torch.int64, device=dev)
+    offs = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+    if k:
+        offs[1:] = torch.cumsum(lens, 0)
+    if tb.is_cuda and k:
+        out = torch.empty(tb.numel() * 2 + 16, dtype=torch.uint8, device=dev)  # a topic appears at most twice
+        ooffs = torch.empty(k + 1, dtype=torch.int64, device=dev)
+        _device_call("emqx_batch_permute_device", tb, to, k, idx.to(torch.int32).contiguous(), out, ooffs)
+        return out, offs
+    total = int(offs[-1]) if k else 0
+    if not total:
+        return torch.zeros(0, dtype=torch.uint8, device=dev), offs
+    starts = (to[:-1] - to[0])[idx]
+    seg = torch.repeat_interleave(torch.arange(k, device=dev), lens, output_size=total)
+    src = starts[seg] + (torch.arange(total, device=dev) - (offs[:-1])[seg])
+    return tb[int(to[0]):][src], offs
+
+
+def _p2p(t: Optional[torch.Tensor], peer: int, send: bool, group, like: Optional[torch.Tensor] = None):
+    """Point-to-point copy of a tensor (host copies when a device tensor goes over gloo)."""
+    gloo = dist.get_backend(group) == "gloo"
+    if send:
+        dist.send(t.cpu() if (gloo and t.is_cuda) else t, dst=peer, group=group)
+        return None
+    host = gloo and like.is_cuda
+    buf = torch.empty(like.shape, dtype=like.dtype) if host else like
+    dist.recv(buf, src=peer, group=group)
+    if host:
+        like.copy_(buf)
+    return like
+
+
+class ShardedMatcher:
+    """A filter-sharded table over the ranks of a process group (two engines per rank).
+
+    ``match_fn(engine, local_topics_bytes, local_topic_offsets) -> (counts int64 (n,), ids int32)``
+    does the per-shard match on engine 0 (A) or 1 (B); the default is this rank's two HIP
+    engines (device tensors).  Tests inject the oracle to check the distribution logic over gloo
+    on CPU."""
 
     def __init__(self, filters: Tuple[np.ndarray, np.ndarray], group=None, device: Optional[torch.device] = None,
-                 mode: int = 0, match_fn: Optional[Callable] = None):
+                 mode: int = 0, match_fn: Optional[Callable] = None, max_piece_pm: int = MAX_PIECE_PM):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
                                  else torch.device("cpu"))
         self.mode = mode
-        self.local_filters, self.global_ids = shard_filters(filters, self.rank, self.world)
-        self.engine = None
+        self.plan = shard_plan(filters, self.world, max_piece_pm)
+        self.plan_dev = (torch.from_numpy(self.plan.view(np.int32).copy()).to(self.device)
+                         if self.device.type == "cuda" and len(self.plan) else None)
+        self.local = shard_engines(filters, self.rank, self.world, self.plan)
+        self.engines = []
         self.last_local_topics = 0
         if match_fn is None:
             from .engine import Engine
-            self.engine = Engine(self.device.index if self.device.type == "cuda" else -1)
-            self.engine.insert_packed_ext(*self.local_filters, self.global_ids)
-            self.engine.commit()
+            for packed, gids in self.local:
+                e = Engine(self.device.index if self.device.type == "cuda" else -1)
+                if len(gids):
+                    e.insert_packed_ext(*packed, gids)
+                e.commit()
+                self.engines.append(e)
             match_fn = self._engine_match
         self.match_fn = match_fn
 
-    def _engine_match(self, tb: torch.Tensor, to: torch.Tensor):
+    @property
+    def n_local_filters(self) -> int:
+        return int(sum(len(g) for _, g in self.local))
+
+    def _engine_match(self, which: int, tb: torch.Tensor, to: torch.Tensor):
         n = to.numel() - 1
         d_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
-        cap = max(1 << 16, getattr(self, "_cap", 1 << 20))
+        caps = getattr(self, "_caps", [1 << 20, 1 << 20])
+        cap = max(1 << 16, caps[which])
+        stream = torch.cuda.current_stream(self.device).cuda_stream
         while True:
             d_ids = torch.empty(cap, dtype=torch.int32, device=self.device)
             try:
-                m = self.engine.match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(),
-                                             cap, mode=self.mode,
-                                             stream=torch.cuda.current_stream(self.device).cuda_stream)
+                m = self.engines[which].match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(),
+                                                     d_ids.data_ptr(), cap, mode=self.mode, stream=stream)
                 break
             except Exception as e:  # EMQX_EOVERFLOW: retry with the exact capacity
                 need = getattr(e, "needed", None)
                 if need is None:
                     raise
                 cap = need + 1
-        self._cap = max(cap, getattr(self, "_cap", 0))
+        caps[which] = max(cap, caps[which])
+        self._caps = caps
         return d_off[1:] - d_off[:-1], d_ids[:m]
-
-    def match(self, topics: Optional[Tuple[torch.Tensor, torch.Tensor]], src: int = 0, dst: int = 0):
-        """Match a batch held by rank ``src`` against the sharded table; rank ``dst`` gets the
-        CSR in batch order (offsets int64 (n+1,), ids int32), other ranks get None."""
-        dev, G, me, grp = self.device, self.world, self.rank, self.group
-        i64 = dict(dtype=torch.int64, device=dev)
-        # 1. the source partitions its batch by owner rank
-        if me == src:
-            tb, to = topics
-            tb, to = tb.to(dev), to.to(dev).to(torch.int64)
-            owner = topic_owner(tb, to, G)
-            perm, lens_p, bytes_p, n_to, bytes_to = partition(tb, to, owner, G)
-            send_meta = torch.stack([n_to, bytes_to], 1).reshape(-1)
-        else:
-            send_meta = torch.zeros(2 * G, **i64)
-        # 2. sizes: every rank learns what it receives from the source
-        recv_meta = torch.empty(2 * G, **i64)
-        _a2a(recv_meta, send_meta, [2] * G, [2] * G, grp)
-        rm = recv_meta.reshape(G, 2).cpu()
-        n_in, b_in = int(rm[src, 0]), int(rm[src, 1])
-        if me == src:
-            sm = send_meta.reshape(G, 2).cpu()
-            n_out_splits, b_out_splits = sm[:, 0].tolist(), sm[:, 1].tolist()
-        else:
-            lens_p = torch.zeros(0, **i64)
-            bytes_p = torch.zeros(0, dtype=torch.uint8, device=dev)
-            n_out_splits, b_out_splits = [0] * G, [0] * G
-        in_splits_n = [n_in if r == src else 0 for r in range(G)]
-        in_splits_b = [b_in if r == src else 0 for r in range(G)]
-        # 3. the parts: topic lengths and bytes (a rank's part may be empty)
-        my_lens = torch.empty(n_in, **i64)
-        _a2a(my_lens, lens_p, in_splits_n, n_out_splits, grp)
-        my_bytes = torch.empty(max(b_in, 1), dtype=torch.uint8, device=dev)
-        _a2a(my_bytes[:b_in], bytes_p[:sum(b_out_splits)], in_splits_b, b_out_splits, grp)
-        my_offs = torch.zeros(n_in + 1, **i64)
-        if n_in:
-            my_offs[1:] = torch.cumsum(my_lens, 0)
-        # 4. the local match, against this rank's shard only
-        counts, ids = self.match_fn(my_bytes, my_offs)
-        counts = counts.to(torch.int64).to(dev)
-        ids = ids.to(torch.int32).to(dev)
-        self.last_local_topics = n_in
-        # 5. results back to the destination: counts first (with the id totals), then ids
-        tot = torch.zeros(G, **i64)
-        tot[dst] = int(ids.numel())
-        tot_in = torch.empty(G, **i64)
-        _a2a(tot_in, tot, [1] * G, [1] * G, grp)
-        n_parts = [0] * G
-        if me == dst:
-            if me == src:
-                n_parts = n_out_splits
-            else:  # the destination learns the part sizes and the order from the source
-                np_t = torch.zeros(G, **i64)
-                dist.recv(np_t, src=src, group=grp)
-                n_parts = np_t.cpu().tolist()
-                perm = torch.empty(sum(n_parts), **i64)
-                dist.recv(perm, src=src, group=grp)
-        elif me == src:
-            dist.send(torch.tensor(n_out_splits, **i64), dst=dst, group=grp)
-            dist.send(perm.contiguous(), dst=dst, group=grp)
-        ids_in_splits = tot_in.cpu().tolist() if me == dst else [0] * G
-        cnt_in = torch.empty(sum(n_parts), **i64)
-        _a2a(cnt_in, counts, n_parts, [n_in if r == dst else 0 for r in range(G)], grp)
-        ids_in = torch.empty(sum(ids_in_splits), dtype=torch.int32, device=dev)
-        _a2a(ids_in, ids, ids_in_splits, [int(ids.numel()) if r == dst else 0 for r in range(G)], grp)
-        # 6. the destination puts the results back in batch order
-        if me != dst:
-            return None
-        return merge_csr(cnt_in, ids_in, perm)
 
     def match_all(self, topics: Tuple[torch.Tensor, torch.Tensor]):
         """Every rank matches its own batch against the sharded table and gets its own CSR
         (offsets int64 (n+1,), ids int32) in batch order — the layout's weak-scaling use, one
-        publishing node per rank.  Each rank partitions its batch by owner; one all-to-all
-        sends every part to its owner, every rank matches all it received (from all sources)
-        in one engine call, and one all-to-all (counts, then ids) returns each source's
-        results, which it puts back in batch order.  The collectives move each topic and each
-        result once; the fixed cost per step does not grow with the number of sources."""
+        publishing node per rank.  Two host synchronisations per call: the size matrix of the
+        requests and the id totals of the answers (the all-to-all split lists)."""
         dev, G, grp = self.device, self.world, self.group
         i64 = dict(dtype=torch.int64, device=dev)
         tb, to = topics
         tb, to = tb.to(dev), to.to(dev).to(torch.int64)
-        owner = topic_owner(tb, to, G)
-        perm, lens_p, bytes_p, n_to, bytes_to = partition(tb, to, owner, G)
-        # sizes: what every source sends to every owner
-        send_meta = torch.stack([n_to, bytes_to], 1).reshape(-1)
-        recv_meta = torch.empty(2 * G, **i64)
-        _a2a(recv_meta, send_meta, [2] * G, [2] * G, grp)
-        sm = send_meta.reshape(G, 2).cpu()
-        rm = recv_meta.reshape(G, 2).cpu()
-        n_out, b_out = sm[:, 0].tolist(), sm[:, 1].tolist()
-        n_in, b_in = rm[:, 0].tolist(), rm[:, 1].tolist()
-        # the parts, source after source
+        n = to.numel() - 1
+        # 1. requests: (topic, rank * 2 + engine), sorted by destination bucket (stable)
+        req = topic_requests(tb, to, G, self.plan, self.plan_dev).reshape(-1)
+        bucket = torch.where(req < 0, torch.full_like(req, 2 * G), req)
+        order = torch.sort(bucket, stable=True)[1]
+        counts = torch.bincount(bucket, minlength=2 * G + 1)[: 2 * G]  # per (rank, engine)
+        req_topic = torch.div(order, 2, rounding_mode="floor")
+        lens = (to[1:] - to[:-1]).to(torch.int64)
+        rank_of = torch.arange(2 * G, device=dev) // 2
+        valid_lens = lens[req_topic] * (bucket[order] < 2 * G).to(torch.int64)
+        bytes_per_bucket = torch.zeros(2 * G + 1, **i64).index_add_(0, bucket[order], valid_lens)[: 2 * G]
+        bytes_to = torch.zeros(G, **i64).index_add_(0, rank_of, bytes_per_bucket)
+        # 2. sizes: one all-to-all of (A requests, B requests, bytes) per destination
+        send_meta = torch.stack([counts[0::2], counts[1::2], bytes_to], 1).reshape(-1)
+        recv_meta = torch.empty(3 * G, **i64)
+        _a2a(recv_meta, send_meta, [3] * G, [3] * G, grp)
+        meta = torch.stack([send_meta, recv_meta]).cpu()  # host sync 1
+        sm, rm = meta[0].reshape(G, 3), meta[1].reshape(G, 3)
+        n_out = (sm[:, 0] + sm[:, 1]).tolist()
+        b_out = sm[:, 2].tolist()
+        nA_in, nB_in = rm[:, 0].tolist(), rm[:, 1].tolist()
+        n_in = [a + b for a, b in zip(nA_in, nB_in)]
+        b_in = rm[:, 2].tolist()
+        n_req = sum(n_out)
+        req_topic = req_topic[:n_req]
+        req_engine = (bucket[order][:n_req] % 2)
+        # 3. the requests' topics, grouped by destination, to their owners
+        bytes_p, offs_p = _gather_topics(tb, to, req_topic)
+        lens_p = offs_p[1:] - offs_p[:-1]
         my_lens = torch.empty(sum(n_in), **i64)
         _a2a(my_lens, lens_p, n_in, n_out, grp)
         my_bytes = torch.empty(max(sum(b_in), 1), dtype=torch.uint8, device=dev)
@@ -320,21 +399,77 @@ class ShardedMatcher:
         my_offs = torch.zeros(sum(n_in) + 1, **i64)
         if sum(n_in):
             my_offs[1:] = torch.cumsum(my_lens, 0)
-        counts, ids = self.match_fn(my_bytes, my_offs)
-        counts = counts.to(torch.int64).to(dev)
-        ids = ids.to(torch.int32).to(dev)
+        # 4. received: [src 0: A..., B...][src 1: A..., B...]...; match the A part and the B part
+        starts = np.concatenate([[0], np.cumsum(n_in)[:-1]]).astype(np.int64)
+        idx = [torch.cat([torch.arange(int(starts[s] + (nA_in[s] if e else 0)),
+                                       int(starts[s] + nA_in[s] + (nB_in[s] if e else 0)), **i64)
+                          for s in range(G)]) for e in (0, 1)]
+        cnts, idss = [], []
+        for e in (0, 1):
+            if idx[e].numel():
+                eb, eo = _gather_topics(my_bytes, my_offs, idx[e])
+                c, i_ = self.match_fn(e, eb, eo)
+            else:
+                c, i_ = torch.zeros(0, **i64), torch.zeros(0, dtype=torch.int32, device=dev)
+            cnts.append(c.to(torch.int64).to(dev))
+            idss.append(i_.to(torch.int32).to(dev))
         self.last_local_topics = sum(n_in)
-        # results back: counts per received part, and the id total of each part
-        bounds = torch.tensor([0] + list(np.cumsum(n_in)), **i64)
-        csum = torch.zeros(sum(n_in) + 1, **i64)
-        if sum(n_in):
-            csum[1:] = torch.cumsum(counts, 0)
-        ids_out = (csum[bounds[1:]] - csum[bounds[:-1]]).cpu().tolist()
+        # back in received order (a permutation of the received positions)
+        r_off, r_ids = merge_csr(torch.cat(cnts), torch.cat(idss), torch.cat(idx))
+        r_cnt = r_off[1:] - r_off[:-1]
+        # 5. answers back to each source: counts per request, then ids (totals first)
+        bounds = torch.tensor(np.concatenate([[0], np.cumsum(n_in)]).astype(np.int64), **i64)
+        ids_out_t = r_off[bounds[1:]] - r_off[bounds[:-1]]
         ids_in_t = torch.empty(G, **i64)
-        _a2a(ids_in_t, torch.tensor(ids_out, **i64), [1] * G, [1] * G, grp)
-        ids_in = ids_in_t.cpu().tolist()
-        cnt_back = torch.empty(int(perm.numel()), **i64)
-        _a2a(cnt_back, counts, n_out, n_in, grp)
+        _a2a(ids_in_t, ids_out_t, [1] * G, [1] * G, grp)
+        tot = torch.stack([ids_out_t, ids_in_t]).cpu()  # host sync 2
+        ids_out, ids_in = tot[0].tolist(), tot[1].tolist()
+        cnt_back = torch.empty(n_req, **i64)
+        _a2a(cnt_back, r_cnt, n_out, n_in, grp)
         ids_back = torch.empty(sum(ids_in), dtype=torch.int32, device=dev)
-        _a2a(ids_back, ids, ids_in, ids_out, grp)
-        return merge_csr(cnt_back, ids_back, perm)
+        _a2a(ids_back, r_ids, ids_in, ids_out, grp)
+        # 6. merge per topic in batch order: a topic's engine-A answer, then its engine-B answer
+        return merge_requests(cnt_back, ids_back, req_topic, req_engine, n, sum(ids_in))
+
+    def match(self, topics: Optional[Tuple[torch.Tensor, torch.Tensor]], src: int = 0, dst: int = 0):
+        """Match a batch held by rank ``src``; rank ``dst`` gets the CSR in batch order
+        (offsets int64 (n+1,), ids int32), the other ranks None.  Every rank takes part (the
+        others with empty batches)."""
+        dev = self.device
+        empty = (torch.zeros(0, dtype=torch.uint8, device=dev), torch.zeros(1, dtype=torch.int64, device=dev))
+        res = self.match_all(topics if self.rank == src else empty)
+        if src == dst:
+            return res if self.rank == dst else None
+        if self.rank == src:
+            off, ids = res
+            _p2p(torch.tensor([off.numel(), ids.numel()], dtype=torch.int64), dst, True, self.group)
+            _p2p(off, dst, True, self.group)
+            _p2p(ids, dst, True, self.group)
+            return None
+        if self.rank == dst:
+            sz = _p2p(None, src, False, self.group, like=torch.zeros(2, dtype=torch.int64))
+            off = _p2p(None, src, False, self.group, like=torch.empty(int(sz[0]), dtype=torch.int64, device=dev))
+            ids = _p2p(None, src, False, self.group, like=torch.empty(int(sz[1]), dtype=torch.int32, device=dev))
+            return off, ids
+        return None
+
+
+def merge_requests(cnt: torch.Tensor, ids: torch.Tensor, req_topic: torch.Tensor, req_engine: torch.Tensor, n: int,
+                   total: int):
+    """Per-request answers (counts in request order, ids request after request) -> the CSR of
+    n topics in batch order, each topic's engine-A ids before its engine-B ids.  `total` = the
+    id count (known on the host from the exchange), so no further synchronisation."""
+    dev = cnt.device
+    cnt = cnt.to(torch.int64)
+    per_topic = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, req_topic, cnt)
+    a_part = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, req_topic, cnt * (req_engine == 0))
+    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    if n:
+        offsets[1:] = torch.cumsum(per_topic, 0)
+    out = torch.empty(total, dtype=torch.int32, device=dev)
+    if total:
+        base = offsets[req_topic] + a_part[req_topic] * (req_engine == 1)
+        roff = torch.cumsum(cnt, 0) - cnt
+        k = torch.repeat_interleave(torch.arange(cnt.numel(), device=dev), cnt, output_size=total)
+        out[base[k] + (torch.arange(total, device=dev) - roff[k])] = ids.to(torch.int32)
+    return offsets, out

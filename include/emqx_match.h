@@ -368,6 +368,35 @@ int emqx_shard_owner(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, 
                      int topics, uint32_t* owner_out);
 int emqx_shard_owner_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t world,
                             uint32_t levels, uint32_t* d_owner, void* stream);
+/* Filter-sharded layout with two key spaces (emqx_amd/dist.py): the tables past
+ * one GPU.  A topic l1/l2/l3/... is matched by root-wildcard filters ('#', '+', '+/#',
+ * '+/+/...', replicated on every rank), by filters with a literal first level (space L, placed by
+ * l1) and by filters '+/x/...' (space P, placed by x = the second level).  A key with many filters
+ * (emqx_shard_plan: more than max_piece_pm / 1000 of a rank's share) is split over `span`
+ * consecutive ranks by the next level; its filters whose next level is '+' / '#' live on all of
+ * them.  Each rank holds two engines: "A" (space L + root-wildcard) and "B" (space P).
+ *   emqx_shard_plan   the hot keys of a filter set (sorted; EMQX_EOVERFLOW: *n_out = needed)
+ *   emqx_shard_place  filters: ranks [first, first + span) (mod world) of engine A (0) or B (1)
+ *   emqx_shard_route  topics: req2[2i] = rank * 2 of its engine-A request, req2[2i + 1] = rank * 2
+ *                     + 1 of its engine-B request or EMQX_SHARD_NONE ('$' topics and one-level
+ *                     topics make no B request; a wildcard topic makes one request, to the first
+ *                     rank of its byte-identical filter).  Every filter that can match the topic
+ *                     lives, once, on one of the two: the two answers concatenate.
+ *   emqx_shard_route_device  the same for a topic batch in HBM, on `stream`. */
+#define EMQX_SHARD_NONE 0xFFFFFFFFu
+typedef struct emqx_shard_split {
+  uint32_t key;   /* space bit (0x80000000 = space P) | 31-bit level hash                       */
+  uint32_t info;  /* first rank | span << 16                                                    */
+} emqx_shard_split;
+int emqx_shard_plan(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world, uint32_t max_piece_pm,
+                    emqx_shard_split* out, uint32_t cap, uint32_t* n_out);
+int emqx_shard_place(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
+                     const emqx_shard_split* splits, uint32_t n_splits, uint32_t* first, uint32_t* span,
+                     uint32_t* engine);
+int emqx_shard_route(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
+                     const emqx_shard_split* splits, uint32_t n_splits, uint32_t* req2);
+int emqx_shard_route_device(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint32_t world,
+                            const emqx_shard_split* d_splits, uint32_t n_splits, uint32_t* d_req2, void* stream);
 /* Device batches regrouped for the filter-sharded layout (and their results put back), on
  * `stream`, no host synchronisation.  d_perm[p] (< n, a permutation) names the batch topic at
  * position p of the regrouped batch.

@@ -392,8 +392,9 @@ def test_async_device_api(Engine):
 
 
 def test_sharded_matcher_world1_rccl(Engine):
-    """The filter-sharded path end to end on one GPU over RCCL (world size 1): broadcast,
-    global-id shard table, gather and concatenation give the single-engine result."""
+    """The filter-sharded path end to end on one GPU over RCCL (world size 1): requests to the
+    two engines (space L + root wildcards, space P), global-id shard tables, the exchange and
+    the per-topic merge give the single-engine result."""
     import os
     import torch
     import torch.distributed as dist
@@ -434,10 +435,12 @@ def test_sharded_matcher_config_c_generator(Engine):
         topics = (torch.from_numpy(wl.topics[0]).to(dev), torch.from_numpy(wl.topics[1].view(np.int64)).to(dev))
         off, ids = sm.match(topics)
         off, ids = off.cpu().numpy(), ids.cpu().numpy().view(np.uint32)
-        sm.engine.set_tuning("order", 1)
+        for e in sm.engines:
+            e.set_tuning("order", 1)
         off2, ids2 = sm.match(topics)
         off2, ids2 = off2.cpu().numpy(), ids2.cpu().numpy().view(np.uint32)
-        sm.engine.set_tuning("order", -1)
+        for e in sm.engines:
+            e.set_tuning("order", -1)
         off3, ids3 = sm.match_all(topics)  # every rank its own source (here the one rank)
         off3, ids3 = off3.cpu().numpy(), ids3.cpu().numpy().view(np.uint32)
     finally:

@@ -5,6 +5,9 @@
 //   chase  every lane follows its own chain of R dependent loads (latency x concurrency)
 // Prints one JSON line per (shape, table size, waves per CU).  Used to price the roofline of
 // match_fast_kernel against random-access HBM rather than the streaming 8 TB/s figure.
+// `gather_bench cal`: FETCH_SIZE / WRITE_SIZE calibration kernels instead — a 1 GiB buffer read
+// once with 4-B lanes (stream_dword_kernel), once with 16-B lanes (stream_x4_kernel) and written
+// once with 4-B lanes (write_dword_kernel): known byte counts for the fan-out's access widths.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/_build/gather_bench tools/gather_bench.hip
 #include <hip/hip_runtime.h>
@@ -70,7 +73,49 @@ __global__ void chase_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t ite
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+__global__ void stream_dword_kernel(const uint32_t* __restrict__ a, uint64_t n, uint32_t* out) {
+  uint32_t acc = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    acc += a[i];
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+__global__ void stream_x4_kernel(const uint4* __restrict__ a, uint64_t n, uint32_t* out) {
+  uint32_t acc = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 x = a[i];
+    acc += x.x ^ x.y ^ x.z ^ x.w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+__global__ void write_dword_kernel(uint32_t* __restrict__ a, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    a[i] = (uint32_t)i;
+}
+
+static int calibrate() {
+  const uint64_t bytes = 1ull << 30;
+  uint32_t* buf;
+  uint32_t* out;
+  CK(hipMalloc(&buf, bytes));
+  CK(hipMalloc(&out, 64));
+  for (int rep = 0; rep < 3; ++rep) {
+    hipLaunchKernelGGL(write_dword_kernel, dim3(8192), dim3(256), 0, 0, buf, bytes / 4);
+    hipLaunchKernelGGL(stream_dword_kernel, dim3(8192), dim3(256), 0, 0, buf, bytes / 4, out);
+    hipLaunchKernelGGL(stream_x4_kernel, dim3(8192), dim3(256), 0, 0, reinterpret_cast<const uint4*>(buf), bytes / 16,
+                       out);
+  }
+  CK(hipDeviceSynchronize());
+  printf("{\"calibration\": \"1 GiB per kernel: write_dword_kernel writes it, stream_dword_kernel and "
+         "stream_x4_kernel read it\", \"bytes_per_dispatch\": %llu}\n", (unsigned long long)bytes);
+  CK(hipFree(buf));
+  CK(hipFree(out));
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'c') return calibrate();
   const uint64_t sizes_mb[] = {2, 64, 1024};
   const int wpc[] = {8, 16, 24, 32};
   uint32_t* out;

@@ -1,14 +1,15 @@
-"""Per-rank walk work of the filter-sharded layouts, computed by the oracle's
-evals (SURVEY §8 d: node visits of the canonical level trie, the quantity the engine's walk
-count equals) on config C's generator (config B's, vocab x4, seed 3) at a reduced filter
-count, for G = 1, 2, 4, 8:
+"""Per-rank capacity and walk work of the filter-sharded layout (emqx_amd/dist.py),
+computed with the oracle's evals (SURVEY §8 d: node visits of the canonical level trie, the
+quantity the engine's walk count equals) on config C's generator (config B's, vocab x4,
+seed 3) at a reduced filter count, for G = 1, 2, 4, 8:
 
-* first-level sharding (emqx_amd/dist.py): rank r holds the filters whose first level hashes
-  to r plus every root-wildcard filter, and matches only the topics it owns;
-* round-1's layout (filter i on rank i mod G): every rank walks every topic.
+* two key spaces (round 3): engine A of rank r holds the root-wildcard filters and the space-L
+  filters placed on r, engine B the space-P filters placed on r; a topic walks engine A of its
+  L rank and engine B of its P rank (shard_plan / shard_place / topic_requests);
+* the round-2 layout (first two levels hashed, wildcard-keyed filters replicated), for
+  comparison: filters on the busiest rank.
 
-Prints one JSON line per G: evals per batch topic on the busiest rank, the mean rank, and
-topics per rank.  Usage: python tools/shard_evals.py [--filters 2000000] [--topics 100000]"""
+Prints one JSON line per G.  Usage: python tools/shard_evals.py [--filters 2000000] [--topics 100000]"""
 import argparse
 import json
 import os
@@ -34,32 +35,39 @@ def main():
     o.add_packed(*wl.filters)
     base = o.evals_packed(*wl.topics).astype(np.float64)
     del o
+    tt = (torch.from_numpy(wl.topics[0]), torch.from_numpy(wl.topics[1].astype(np.int64)))
     for G in (1, 2, 4, 8):
-        own_f = D.shard_owner(wl.filters, G)
-        own_t = D.topic_owner(torch.from_numpy(wl.topics[0]), torch.from_numpy(wl.topics[1].astype(np.int64)),
-                              G).numpy()
-        new_ev, new_n, rr_ev = [], [], []
+        plan = D.shard_plan(wl.filters, G)
+        first, span, eng = D.shard_place(wl.filters, G, plan)
+        req = D.topic_requests(*tt, G, plan).numpy()
+        held, ev, visits = [], [], []
         for r in range(G):
-            shard = W.take(wl.filters, np.nonzero((own_f == r) | (own_f == D.SHARD_ALL))[0])
-            o = C.CppOracle(True)
-            o.add_packed(*shard)
-            mine = np.nonzero(own_t == r)[0]
-            new_ev.append(float(o.evals_packed(*W.take(wl.topics, mine)).sum()) if mine.size else 0.0)
-            new_n.append(int(mine.size))
-            del o
-            o = C.CppOracle(True)
-            o.add_packed(*W.take(wl.filters, np.arange(r, wl.n_filters, G)))
-            rr_ev.append(float(o.evals_packed(*wl.topics).sum()))
-            del o
+            engines = D.shard_engines(wl.filters, r, G, plan)
+            held.append(sum(len(g) for _, g in engines))
+            e_r, v_r = 0.0, 0
+            for e, (packed, gids) in enumerate(engines):
+                mine = np.nonzero(req[:, e] == 2 * r + e)[0]
+                v_r += int(mine.size)
+                if mine.size and len(gids):
+                    o = C.CppOracle(True)
+                    o.add_packed(*packed)
+                    e_r += float(o.evals_packed(*W.take(wl.topics, mine)).sum())
+                    del o
+            ev.append(e_r)
+            visits.append(v_r)
+        own2 = D.shard_owner(wl.filters, G)
+        r2 = max(np.count_nonzero((own2 == r) | (own2 == D.SHARD_ALL)) for r in range(G))
         print(json.dumps({
             "G": G, "filters": wl.n_filters, "topics": n, "evals_per_topic_single_table": round(base.mean(), 2),
-            "first_level_sharding": {"max_rank_evals_per_batch_topic": round(max(new_ev) / n, 3),
-                                     "mean_rank_evals_per_batch_topic": round(float(np.mean(new_ev)) / n, 3),
-                                     "topics_per_rank_max_frac": round(max(new_n) / n, 4),
-                                     "filters_on_busiest_rank_frac": round(float(max(
-                                         np.count_nonzero((own_f == r) | (own_f == D.SHARD_ALL)) for r in range(G))
-                                         / wl.n_filters), 4)},
-            "round1_mod_G": {"max_rank_evals_per_batch_topic": round(max(rr_ev) / n, 3)}}), flush=True)
+            "two_key_spaces": {"filters_on_busiest_rank_frac": round(max(held) / wl.n_filters, 4),
+                               "target_1_5_over_G": round(1.5 / G, 4),
+                               "filters_stored_total_x": round(sum(held) / wl.n_filters, 3),
+                               "plan_keys": int(len(plan)),
+                               "max_rank_evals_per_batch_topic": round(max(ev) / n, 3),
+                               "mean_rank_evals_per_batch_topic": round(float(np.mean(ev)) / n, 3),
+                               "requests_per_topic": round(float(np.count_nonzero(req >= 0)) / n, 3),
+                               "max_rank_requests_frac": round(max(visits) / n, 4)},
+            "round2_two_level_hash": {"filters_on_busiest_rank_frac": round(r2 / wl.n_filters, 4)}}), flush=True)
 
 
 if __name__ == "__main__":
