@@ -34,7 +34,7 @@ EXPORTS = (
     "emqx_delete_filters",
     "emqx_lookup_filter", "emqx_filter_name", "emqx_commit", "emqx_match_batch",
     "emqx_match_batch_device", "emqx_match_batch_device_async", "emqx_stats_get", "emqx_topic_match", "emqx_topic_wildcard",
-    "emqx_set_tuning", "emqx_diag_read", "emqx_build_check", "emqx_batcher_create",
+    "emqx_set_tuning", "emqx_diag_read", "emqx_diag_timeline", "emqx_build_check", "emqx_batcher_create",
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_batcher_stats_ext",
     "emqx_batcher_submit_many", "emqx_batcher_try_submit", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
@@ -173,6 +173,7 @@ def lib():
         "emqx_topic_wildcard": (i32, [vp, u64]),
         "emqx_set_tuning": (i32, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "emqx_diag_read": (i32, [vp, vp, u32, i32]),
+        "emqx_diag_timeline": (i32, [vp, vp, u64, ctypes.POINTER(u64)]),
         "emqx_build_check": (i32, [vp, vp, u64, vp, ctypes.c_char_p, u64]),
         "emqx_batcher_create": (i32, [vp, u32, u32, u32, BATCH_CB, ctypes.POINTER(vp)]),
         "emqx_batcher_submit": (i32, [vp, vp, u64, vp]),

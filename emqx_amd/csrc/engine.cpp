@@ -191,6 +191,8 @@ struct emqx_engine {
   std::atomic<double> last_kernel_ms{0};
   std::atomic<int> forced_variant{-1};
   std::atomic<bool> diag_on{false};
+  uint4* timeline = nullptr;          // emqx_set_tuning("timeline", tiles): per-tile wall clocks of
+  uint64_t timeline_cap = 0;          // the fast kernel (diag calls), read by emqx_diag_timeline
   std::atomic<uint32_t> slab_hint{256};  // largest slab per tile any workspace needed
   // incremental commits (under `writer`)
   LiveState ls;
@@ -535,6 +537,7 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.tile_defer = w->tile_defer;
   a.spill = w->spill;
   a.diag = e->diag_on.load() ? w->diag : nullptr;
+  a.timeline = a.diag && e->timeline && (n + TILE_TOPICS - 1) / TILE_TOPICS <= e->timeline_cap ? e->timeline : nullptr;
   a.spill_cap = w->spill_cap;
   a.ctrl = w->ctrl;
   a.deferred = w->deferred;
@@ -853,6 +856,7 @@ int emqx_engine_destroy(emqx_engine* e) {
   (void)hipSetDevice(e->device);
   for (emqx_host_batch* b : e->hb_free) emqx_host_batch_destroy(b);
   e->hb_free.clear();
+  dfree(e->timeline);
   delete e;
   return EMQX_OK;
 }
@@ -1207,6 +1211,19 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
     e->diag_on.store(value != 0);
     return EMQX_OK;
   }
+  if (std::strcmp(key, "timeline") == 0) {  // tiles to record (0: off); diag calls only
+    if (value < 0) return EMQX_EINVAL;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipDeviceSynchronize());
+    dfree(e->timeline);
+    e->timeline_cap = 0;
+    if (value) {
+      HIP_TRY(dalloc(e->timeline, static_cast<uint64_t>(value)));
+      HIP_TRY(hipMemset(e->timeline, 0, static_cast<uint64_t>(value) * sizeof(uint4)));
+      e->timeline_cap = static_cast<uint64_t>(value);
+    }
+    return EMQX_OK;
+  }
   if (std::strcmp(key, "incremental") == 0) {
     std::lock_guard<std::mutex> g(e->writer);
     e->incremental = value != 0;
@@ -1310,6 +1327,16 @@ int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset) {
     if (reset) HIP_TRY(hipMemset(w->diag, 0, DIAG_WORDS * sizeof(uint64_t)));
   }
   for (uint32_t i = 0; i < n && i < DIAG_WORDS; ++i) out[i] = acc[i];
+  return EMQX_OK;
+}
+
+int emqx_diag_timeline(emqx_engine* e, uint32_t* out, uint64_t cap_tiles, uint64_t* n_tiles) {
+  if (!e || !n_tiles || (cap_tiles && !out)) return EMQX_EINVAL;
+  *n_tiles = e->timeline_cap;
+  if (!e->timeline || !cap_tiles) return EMQX_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, e->timeline, std::min(cap_tiles, e->timeline_cap) * sizeof(uint4), hipMemcpyDeviceToHost));
   return EMQX_OK;
 }
 

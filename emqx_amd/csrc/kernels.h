@@ -78,6 +78,8 @@ struct MatchArgs {
   uint32_t* ctrl;          // [CTRL_WORDS]
   uint32_t* deferred;      // [n]
   uint64_t* diag;          // optional [DIAG_WORDS] counters (nullptr = off)
+  uint4* timeline;         // optional (diag on): per tile {start lo, start hi, phase-A end, end}
+                           // in 100 MHz wall-clock ticks (end / A-end relative to start), CU id
   uint2* spill;            // [ntiles * spill_cap] HBM overflow of the per-wave LDS stack
   uint32_t spill_cap;
   // deep path

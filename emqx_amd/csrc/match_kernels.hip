@@ -857,6 +857,10 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     dg[9] = lane == 0 ? static_cast<uint32_t>(clk1 - clk0) : 0u;
     dg[10] = lane == 0 ? static_cast<uint32_t>(clk2 - clk1) : 0u;
     dg[11] = lane == 0 ? 1u : 0u;
+    if (a.timeline && lane == 0)
+      a.timeline[tile] = make_uint4(static_cast<uint32_t>(clk0), static_cast<uint32_t>(clk0 >> 32),
+                                    static_cast<uint32_t>(clk1 - clk0) | (static_cast<uint32_t>(__smid()) << 20),
+                                    static_cast<uint32_t>(clk2 - clk0));
 #pragma unroll
     for (int i = 0; i < DIAG_NCOUNT; ++i) {
       const uint32_t v = wave_sum(dg[i]);

@@ -428,10 +428,15 @@ int emqx_topic_wildcard(const uint8_t* topic, uint64_t len);
  * fixed kernel variant, see emqx_amd/csrc/kernels.h), "diag" (1 = accumulate the kernel's
  * diagnostic counters), "incremental" (0 = every commit rebuilds), "delta_max" (filters placed
  * incrementally before a rebuild, -1 = default policy), "commit_threads" (host threads of an
- * incremental commit, default min(8, cores)).  EMQX_ENOTFOUND for unknown keys. */
+ * incremental commit, default min(8, cores)), "timeline" (tiles of emqx_diag_timeline to record,
+ * 0 = off).  EMQX_ENOTFOUND for unknown keys. */
 int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value);
 /* Reads (and optionally resets) the accumulated diagnostic counters (DIAG_* order). */
 int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset);
+/* Per-tile timeline of the fast kernel's last "diag" call (emqx_set_tuning "timeline" = tiles to
+ * record): 4 uint32 per tile {start (100 MHz ticks, low), start high, phase-A ticks | CU id << 20,
+ * end - start ticks}; *n_tiles = the recorded capacity. */
+int emqx_diag_timeline(emqx_engine* e, uint32_t* out, uint64_t cap_tiles, uint64_t* n_tiles);
 
 /* Host-only self-check of the table builder (no device needed): builds the level trie of
  * the given filters and verifies its lookup invariants.  stats_out (4 entries, optional):
