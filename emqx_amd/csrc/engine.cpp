@@ -697,6 +697,7 @@ struct HostBatchPriv {
   uint32_t* d_out_ids = nullptr;
   uint64_t* summary = nullptr;  // pinned, SUM_WORDS
   std::shared_ptr<Snapshot> snap;
+  std::shared_ptr<Snapshot> pin;  // set by emqx_match_batch: every chunk of one call reads one table version
   uint32_t mode = 0;
   bool pending = false;
   uint64_t evals = 0, deferred = 0, max_stack = 0;  // of the last call
@@ -751,7 +752,7 @@ int hb_enqueue(emqx_host_batch* b) {
   HIP_TRY(hipMemcpyAsync(p->d_toffs, b->topic_offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   uint64_t* sum_dev = nullptr;
   HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&sum_dev), p->summary, 0));
-  p->snap = current(e);
+  p->snap = p->pin ? p->pin : current(e);
   Workspace* w = acquire_ws(e, s);
   int rc = ensure_ws(w, n);
   if (rc == EMQX_OK)
@@ -1073,6 +1074,11 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
   int rc = EMQX_OK;
   for (int k = 0; k < 2 && rc == EMQX_OK; ++k)
     if (!hb[k]) rc = emqx_host_batch_create(e, CH_TOPICS, CH_BYTES, CH_IDS, &hb[k]);
+  // one table version for the whole call: a commit landing between two chunks (or before a
+  // chunk's rerun) must not mix versions within one result
+  const std::shared_ptr<Snapshot> pin = current(e);
+  for (int k = 0; k < 2; ++k)
+    if (hb[k]) static_cast<HostBatchPriv*>(hb[k]->priv)->pin = pin;
   uint64_t chunk_lo[2] = {0, 0}, total = 0, next = 0, evals = 0, deferred = 0, max_stack = 0;
   bool inflight[2] = {false, false}, overflow = false;
   // pack topics [next, ...) into hb[k] (rebased offsets)
@@ -1099,7 +1105,9 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
   auto drain = [&](int k) -> int {
     emqx_host_batch* b = hb[k];
     int r = emqx_host_batch_wait(b);
-    if (r == EMQX_EOVERFLOW) {  // more ids than the chunk's buffer: grow it and rerun the chunk
+    // more ids than the chunk's buffer: grow it to the reported need and rerun the chunk (same
+    // pinned snapshot, so the need cannot move; the loop only guards against that anyway)
+    for (int tries = 0; r == EMQX_EOVERFLOW && tries < 4; ++tries) {
       r = emqx_host_batch_reserve(b, b->cap_topics, b->cap_bytes, b->n_out + (b->n_out >> 2) + 1024);
       if (r == EMQX_OK) r = emqx_host_batch_submit(b, mode);
       if (r == EMQX_OK) r = emqx_host_batch_wait(b);
@@ -1142,6 +1150,8 @@ int emqx_match_batch(emqx_engine* e, uint32_t mode, const uint8_t* topic_bytes, 
   e->last_evals.store(evals);  // the whole call's numbers, over its chunks
   e->last_deferred.store(deferred);
   e->last_max_stack.store(max_stack);
+  for (int j = 0; j < 2; ++j)
+    if (hb[j]) static_cast<HostBatchPriv*>(hb[j]->priv)->pin.reset();
   {
     std::lock_guard<std::mutex> g(e->hb_mu);
     for (int j = 0; j < 2; ++j)
