@@ -50,7 +50,7 @@ EXPORTS = (
     "emqx_shard_plan", "emqx_shard_place", "emqx_shard_route", "emqx_shard_route_device", "emqx_permute_scratch_bytes", "emqx_batch_permute_device", "emqx_owner_sort_scratch_bytes",
     "emqx_owner_sort_device",
     "emqx_csr_unpermute_device", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
-    "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check",
+    "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check", "emqx_htrie_walk_sim",
 )
 # Every symbol include/emqx_retain.h declares (retained-message index).
 RETAIN_EXPORTS = (
@@ -244,6 +244,7 @@ def lib():
         "emqx_htrie_commit": (i32, [vp, i32, vp]),
         "emqx_htrie_match": (i32, [vp, u32, vp, vp, u64, vp, vp, u64, ctypes.POINTER(u64)]),
         "emqx_htrie_check": (i32, [vp, ctypes.c_char_p, u64]),
+        "emqx_htrie_walk_sim": (i32, [vp, vp, vp, u64, vp, vp, u32]),
         "emqx_strerror": (ctypes.c_char_p, [i32]),
         "emqx_version": (ctypes.c_char_p, []),
     }

@@ -191,6 +191,7 @@ struct emqx_engine {
   std::atomic<double> last_kernel_ms{0};
   std::atomic<int> forced_variant{-1};
   std::atomic<bool> diag_on{false};
+  std::atomic<uint32_t> diag_stop{0};  // emqx_set_tuning("diag_stop", 1): diag calls skip the walk
   uint4* timeline = nullptr;          // emqx_set_tuning("timeline", tiles): per-tile wall clocks of
   uint64_t timeline_cap = 0;          // the fast kernel (diag calls), read by emqx_diag_timeline
   std::atomic<uint32_t> slab_hint{256};  // largest slab per tile any workspace needed
@@ -271,6 +272,7 @@ int full_commit(emqx_engine* e) {
   s->tv.root_base = ht.root_base;
   s->tv.root_meta = ht.root_meta;
   s->tv.root_hash_fid = ht.root_hash_fid;
+  s->tv.plus_mask = ht.plus_mask;
   s->n_nodes = ht.n_nodes;
   s->n_slots = n_slots;
   s->n_words = ht.n_words;
@@ -537,6 +539,7 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.tile_defer = w->tile_defer;
   a.spill = w->spill;
   a.diag = e->diag_on.load() ? w->diag : nullptr;
+  a.diag_stop = a.diag ? e->diag_stop.load() : 0u;
   a.timeline = a.diag && e->timeline && (n + TILE_TOPICS - 1) / TILE_TOPICS <= e->timeline_cap ? e->timeline : nullptr;
   a.spill_cap = w->spill_cap;
   a.ctrl = w->ctrl;
@@ -1219,6 +1222,10 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
   }
   if (std::strcmp(key, "diag") == 0) {
     e->diag_on.store(value != 0);
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "diag_stop") == 0) {
+    e->diag_stop.store(static_cast<uint32_t>(value));
     return EMQX_OK;
   }
   if (std::strcmp(key, "timeline") == 0) {  // tiles to record (0: off); diag calls only

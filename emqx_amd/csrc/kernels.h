@@ -80,6 +80,8 @@ struct MatchArgs {
   uint64_t* diag;          // optional [DIAG_WORDS] counters (nullptr = off)
   uint4* timeline;         // optional (diag on): per tile {start lo, start hi, phase-A end, end}
                            // in 100 MHz wall-clock ticks (end / A-end relative to start), CU id
+  uint32_t diag_stop;      // diag kernels only: 1 = skip the walk after phase A (counter passes
+                           // that split the kernel's misses by phase; the output is then wrong)
   uint2* spill;            // [ntiles * spill_cap] HBM overflow of the per-wave LDS stack
   uint32_t spill_cap;
   // deep path

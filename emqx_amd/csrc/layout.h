@@ -106,7 +106,28 @@ struct TableView {
   uint32_t root_base;      // root's edge array
   uint32_t root_meta;      // META_* of the root
   uint32_t root_hash_fid;  // filter '#' or FID_NONE
+  uint32_t plus_mask;      // ~(PLUS_LINE - 1) when the table holds '+' copies (plus_copies), else 0
 };
+
+// '+' copies: in a table built with them, a node with a '+' edge and an array of 8 to
+// 2^PLUS_COPY_MAX_CAPLOG slots keeps a copy of that edge in slot 0 of every 64-B line
+// (PLUS_LINE slots) of its array, and no literal edge sits there.  A step that probes both the
+// '+' edge and a literal then reads the copy in the literal's line: two loads of one line cost
+// one L2 request (tools/gather_bench pair), where slot 0 is usually another line.  Arrays of
+// PLUS_LINE slots or more start on a line boundary (layout pass).  Larger arrays keep '+' in
+// slot 0 alone: an incremental commit rewrites every copy when the '+' edge's record changes,
+// and in the wide upper nodes that is thousands of slot patches per change (measured: commits
+// 40x slower with copies in every array), while those nodes' lines are L2-resident anyway.
+constexpr uint32_t PLUS_LINE = 4;
+constexpr uint32_t PLUS_COPY_MAX_CAPLOG = 10;
+// Does the array of a node (its meta's caplog, whether it has a '+' edge) hold '+' copies?
+EMQX_HD bool plus_copies(uint32_t plus_mask, bool has_plus, uint32_t caplog) {
+  return plus_mask != 0 && has_plus && caplog > 2 && caplog <= PLUS_COPY_MAX_CAPLOG;
+}
+// Is slot i of such an array a '+' position (slot 0, or a line head when it holds copies)?
+EMQX_HD bool plus_position(uint32_t i, bool copies) { return copies ? (i & (PLUS_LINE - 1u)) == 0 : i == 0; }
+// The '+' slot a step reads beside literal slot i1: the copy in i1's line, or slot 0.
+EMQX_HD uint32_t plus_copy(uint32_t i1, bool copies) { return copies ? (i1 & ~(PLUS_LINE - 1u)) : 0u; }
 
 // murmur3 fmix32: spreads word ids inside a node's edge array.
 EMQX_HD uint32_t mix32(uint32_t x) {
@@ -145,10 +166,18 @@ EMQX_HD uint32_t word_hash_bytes(const uint8_t* p, uint32_t n) {
 
 EMQX_HD uint32_t vocab_slot0(uint32_t hash) { return hash; }
 
-// Slot of literal word `wid` in a perfect-hashed node's array (mask = cap - 1).
-EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask) {
-  return mix32(wid ^ (seed * 0x9E3779B1u + 0x7F4A7C15u)) & mask;
+// Slot of literal word `wid` in a perfect-hashed node's array (mask = cap - 1).  In an array
+// that holds '+' copies (copies = plus_copies(...)) the literal slots are the 3/4 of the array
+// that are not line heads: the hash picks one of them directly (multiply-high over their
+// count), so the copies cost the perfect hash no seeds and no larger arrays.
+EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask, bool copies) {
+  const uint32_t h = mix32(wid ^ (seed * 0x9E3779B1u + 0x7F4A7C15u));
+  if (!copies) return h & mask;
+  const uint32_t n3 = ((mask + 1u) / PLUS_LINE) * (PLUS_LINE - 1u);
+  const uint32_t k = static_cast<uint32_t>((static_cast<uint64_t>(h) * n3) >> 32);
+  return (k / (PLUS_LINE - 1u)) * PLUS_LINE + 1u + k % (PLUS_LINE - 1u);
 }
+
 
 // Wide (non-perfect-hashed) nodes use 2-slot buckets: a word lives in its primary bucket,
 // or — rarely, flagged by META_BUCKET_OVF on the primary bucket's first slot —
@@ -160,6 +189,21 @@ EMQX_HD uint32_t bucket1(uint32_t wid, uint32_t seed, uint32_t nbmask) {
 EMQX_HD uint32_t bucket2(uint32_t wid, uint32_t seed, uint32_t nbmask) {
   const uint32_t a = bucket1(wid, seed, nbmask), b = mix32(wid ^ (0xDAA66D2Bu + seed * 0x7F4A7C15u)) & nbmask;
   return b != a ? b : ((a + 1) & nbmask);
+}
+// First slot of word `wid`'s primary (second = false) or secondary 2-slot bucket in a wide
+// array (mask = cap - 1).  In an array holding '+' copies, a bucket is a window of two of the
+// three literal slots of a 64-B line — slots {1, 2} or {2, 3} after the line's '+' copy — so
+// both candidate slots and the copy share a line, and adding '+' later finds every line head
+// free.  (The windows of a line overlap; each has its own first slot for META_BUCKET_OVF.)
+EMQX_HD uint32_t wide_slot(uint32_t wid, uint32_t seed, uint32_t mask, bool copies, bool second) {
+  if (!copies) return 2u * (second ? bucket2(wid, seed, mask >> 1) : bucket1(wid, seed, mask >> 1));
+  const uint32_t lm = (mask + 1u) / PLUS_LINE - 1u;  // line mask
+  const uint32_t h1 = mix32(wid ^ (0x3C6EF372u + seed * 0x9E3779B9u));
+  const uint32_t w1 = (((h1 >> 1) & lm) * PLUS_LINE) + 1u + (h1 & 1u);
+  if (!second) return w1;
+  const uint32_t h2 = mix32(wid ^ (0xDAA66D2Bu + seed * 0x7F4A7C15u));
+  const uint32_t w2 = (((h2 >> 1) & lm) * PLUS_LINE) + 1u + (h2 & 1u);
+  return w2 != w1 ? w2 : (w1 ^ 3u);  // the same window: the line's other one ({1,2} <-> {2,3})
 }
 constexpr uint32_t CUCKOO_SEEDS = 128;
 

@@ -79,9 +79,41 @@ void LiveTrie::adopt(HostTables& ht, std::vector<uint64_t>& fid_loc, std::vector
   max_depth = ht.max_depth;
   loc.swap(fid_loc);
   vocab = v;
+  plus_mask = ht.plus_mask;
+  pcap.assign(plus_mask ? cap : 0, 0);
+  if (plus_mask) {  // arrays whose '+' edge has copies: the root's and every slot's child array
+    auto note = [&](uint32_t base, uint32_t meta) {
+      const uint32_t cl = meta & META_CAPLOG2_MASK;
+      if ((meta & META_HAS_EDGES) && plus_copies(plus_mask, meta & META_HAS_PLUS, cl)) pcap[base] = static_cast<uint8_t>(cl);
+    };
+    note(root_base, root_meta);
+    for (uint64_t i = 0; i < n; ++i)
+      if (edges[i].wid != WID_NONE) note(edges[i].child_base, edges[i].meta);
+  }
   mark = used;
   dirty.clear();
   ranges.clear();
+}
+
+void LiveTrie::sync_plus(Ctx& c, uint64_t p) {
+  if (!has_copies(p)) return;
+  const uint64_t end = p + (1ull << pcap[p]);
+  const EdgeSlot& h = edges[p];
+  const EdgeSlot& c1 = edges[p + PLUS_LINE];
+  if (c1.wid == h.wid && c1.child_base == h.child_base && c1.litf == h.litf &&
+      ((c1.meta ^ h.meta) & ~META_BUCKET_OVF) == 0 && fids[2 * (p + PLUS_LINE)] == fids[2 * p] &&
+      fids[2 * (p + PLUS_LINE) + 1] == fids[2 * p + 1])
+    return;  // the copies hold this record already (every copy is written together)
+  for (uint64_t q = p + PLUS_LINE; q < end; q += PLUS_LINE) {
+    const uint32_t keep = edges[q].meta & META_BUCKET_OVF;
+    edges[q] = edges[p];
+    edges[q].meta = (edges[p].meta & ~META_BUCKET_OVF) | keep;
+    fids[2 * q] = fids[2 * p];
+    fids[2 * q + 1] = fids[2 * p + 1];
+    sid[2 * q] = sid[2 * p];
+    sid[2 * q + 1] = sid[2 * p + 1];
+    touch(c, q);
+  }
 }
 
 namespace {
@@ -227,6 +259,7 @@ void LiveTrie::reencode(Ctx& c, uint64_t p) {
   r.meta |= s.meta & META_BUCKET_OVF;
   edges[p] = r;
   touch(c, p);
+  sync_plus(c, p);
 }
 
 // Points the node reached through `pslot` (or the root) at a new edge array / structure.
@@ -244,6 +277,7 @@ void LiveTrie::set_node(Ctx& c, bool root, uint64_t pslot, uint32_t base, uint32
   r.meta |= s.meta & META_BUCKET_OVF;
   edges[pslot] = r;
   touch(c, pslot);
+  sync_plus(c, pslot);
 }
 
 bool LiveTrie::find_child(uint32_t base, uint32_t meta, uint32_t wid, uint32_t* slot) const {
@@ -255,20 +289,21 @@ bool LiveTrie::find_child(uint32_t base, uint32_t meta, uint32_t wid, uint32_t* 
   const uint32_t mask = (1u << (meta & META_CAPLOG2_MASK)) - 1u;
   const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
   if (meta & META_PH) {
-    *slot = base + lit_slot(wid, sd, mask);
+    *slot = base + lit_slot(wid, sd, mask, plus_copies(plus_mask, meta & META_HAS_PLUS, meta & META_CAPLOG2_MASK));
     return edges[*slot].wid == wid;
   }
-  const uint32_t nbm = mask >> 1, b1 = bucket1(wid, sd, nbm);
+  const bool cp = plus_copies(plus_mask, meta & META_HAS_PLUS, meta & META_CAPLOG2_MASK);
+  const uint32_t b1 = wide_slot(wid, sd, mask, cp, false);
   for (uint32_t k = 0; k < 2; ++k)
-    if (edges[base + 2 * b1 + k].wid == wid) {
-      *slot = base + 2 * b1 + k;
+    if (edges[base + b1 + k].wid == wid) {
+      *slot = base + b1 + k;
       return true;
     }
-  if (!(edges[base + 2 * b1].meta & META_BUCKET_OVF)) return false;
-  const uint32_t b2 = bucket2(wid, sd, nbm);
+  if (!(edges[base + b1].meta & META_BUCKET_OVF)) return false;
+  const uint32_t b2 = wide_slot(wid, sd, mask, cp, true);
   for (uint32_t k = 0; k < 2; ++k)
-    if (edges[base + 2 * b2 + k].wid == wid) {
-      *slot = base + 2 * b2 + k;
+    if (edges[base + b2 + k].wid == wid) {
+      *slot = base + b2 + k;
       return true;
     }
   return false;
@@ -285,21 +320,29 @@ bool LiveTrie::place(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const Edg
   const uint32_t sd = (smeta >> META_SEED_SHIFT) & 255u;
   uint64_t target = ~0ull, ovf = ~0ull;
   if (wid == WID_PLUS) {
-    if (edges[base].wid == WID_NONE) {
+    bool free = edges[base].wid == WID_NONE;
+    // with copies, the literals of a perfect-hashed array are hashed over the non-head slots:
+    // a '+' joining one of more than PLUS_LINE slots rehashes it (relocation)
+    // an array that would hold copies hashes its literals over the non-head slots once it has
+    // '+' (lit_slot, wide_slot): a '+' joining one is placed by relocation, which rehashes
+    if (plus_copies(plus_mask, true, smeta & META_CAPLOG2_MASK)) free = false;
+    if (free) {
       target = base;
       smeta |= META_HAS_PLUS;
     }
   } else if (smeta & META_PH) {
-    const uint32_t j = lit_slot(wid, sd, mask);
+    const uint32_t j =
+        lit_slot(wid, sd, mask, plus_copies(plus_mask, smeta & META_HAS_PLUS, smeta & META_CAPLOG2_MASK));
     if (edges[base + j].wid == WID_NONE) target = base + j;
   } else {
-    const uint32_t nbm = mask >> 1, b1 = bucket1(wid, sd, nbm), b2 = bucket2(wid, sd, nbm);
+    const bool cp = plus_copies(plus_mask, smeta & META_HAS_PLUS, smeta & META_CAPLOG2_MASK);
+    const uint32_t b1 = wide_slot(wid, sd, mask, cp, false), b2 = wide_slot(wid, sd, mask, cp, true);
     for (uint32_t k = 0; k < 2 && target == ~0ull; ++k)
-      if (edges[base + 2 * b1 + k].wid == WID_NONE) target = base + 2 * b1 + k;
+      if (edges[base + b1 + k].wid == WID_NONE) target = base + b1 + k;
     for (uint32_t k = 0; k < 2 && target == ~0ull; ++k)
-      if (edges[base + 2 * b2 + k].wid == WID_NONE) {
-        target = base + 2 * b2 + k;
-        ovf = base + 2 * b1;
+      if (edges[base + b2 + k].wid == WID_NONE) {
+        target = base + b2 + k;
+        ovf = base + b1;
       }
   }
   if (target == ~0ull) return relocate(cx, root, pslot, wid, child, fh, ft, ih, it);
@@ -313,6 +356,10 @@ bool LiveTrie::place(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const Edg
   if (ih != WID_NONE) loc[ih] = target << 2 | FIDLOC_HASH;
   if (it != WID_NONE) loc[it] = target << 2 | FIDLOC_TERM;
   touch(cx, target);
+  if (wid == WID_PLUS && plus_copies(plus_mask, true, smeta & META_CAPLOG2_MASK)) {
+    pcap[base] = static_cast<uint8_t>(smeta & META_CAPLOG2_MASK);
+    sync_plus(cx, base);
+  }
   if (ovf != ~0ull && !(edges[ovf].meta & META_BUCKET_OVF)) {
     edges[ovf].meta |= META_BUCKET_OVF;
     touch(cx, ovf);
@@ -362,21 +409,22 @@ bool LiveTrie::relocate(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const 
     const uint64_t cap_max = next_pow2(std::max<uint64_t>(16, 8ull * e));
     for (uint64_t c2 = cap0; c2 <= cap_max && !ph && log2u(c2) <= PH_MAX_CAPLOG && c2 <= 512; c2 <<= 1) {
       double p_ok = 1.0;
-      const uint32_t avail = static_cast<uint32_t>(c2) - (has_plus ? 1u : 0u);
-      for (uint32_t k = 0; k < n_lit; ++k) p_ok *= k < avail ? double(avail - k) / double(c2) : 0.0;
+      const bool cp = plus_copies(plus_mask, has_plus, log2u(c2));
+      const uint32_t room = cp ? static_cast<uint32_t>(c2 / PLUS_LINE * (PLUS_LINE - 1)) : static_cast<uint32_t>(c2);
+      const uint32_t avail = room - (has_plus && !cp ? 1u : 0u);
+      for (uint32_t k = 0; k < n_lit; ++k) p_ok *= k < avail ? double(avail - k) / double(room) : 0.0;
       if (p_ok * 256.0 < 0.02 && c2 < cap_max) continue;
       const uint32_t mask = static_cast<uint32_t>(c2 - 1);
       for (uint32_t sd = 0; sd < 256 && !ph; ++sd) {
         uint64_t bm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (has_plus) bm[0] = 1;
-        const uint32_t salt = sd * 0x9E3779B1u + 0x7F4A7C15u;
+        if (has_plus) bm[0] = 1;  // slot 0 (a copy array's literals never hash to a line head)
         bool ok = true;
         for (uint32_t k = 0; k < e && ok; ++k) {
           if (ent[k].wid == WID_PLUS) {
             pos[k] = 0;
             continue;
           }
-          const uint32_t sl = mix32(ent[k].wid ^ salt) & mask;
+          const uint32_t sl = lit_slot(ent[k].wid, sd, mask, cp);
           const uint64_t bit = 1ull << (sl & 63u);
           ok = !(bm[sl >> 6] & bit);
           bm[sl >> 6] |= bit;
@@ -395,19 +443,21 @@ bool LiveTrie::relocate(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const 
     caplog = log2u(next_pow2(8ull * e + 8));
     bool ok = false;
     std::vector<int32_t> owner;
+    const bool cp = plus_copies(plus_mask, has_plus, caplog);
     for (uint32_t sd = 0; sd < CUCKOO_SEEDS && !ok; ++sd) {
-      const uint32_t cc = 1u << caplog, nbm = cc / 2 - 1;
+      const uint32_t cc = 1u << caplog, mk = cc - 1;
       owner.assign(cc, -1);
       ok = true;
       uint32_t rng = 0x9E3779B9u ^ (sd << 20) ^ e;
-      for (uint32_t k = 0; k < e; ++k)
-        if (ent[k].wid == WID_PLUS) owner[0] = static_cast<int32_t>(k);  // '+' pinned at slot 0
+      for (uint32_t k = 0; k < e; ++k)  // '+' pinned at slot 0 (and its copies at every line head)
+        if (ent[k].wid == WID_PLUS)
+          for (uint32_t q = 0; q < cc; q += cp ? PLUS_LINE : cc) owner[q] = static_cast<int32_t>(k);
       for (uint32_t k0 = 0; k0 < e && ok; ++k0) {
         if (ent[k0].wid == WID_PLUS) continue;
         int32_t k = static_cast<int32_t>(k0);
         for (int kick = 0;; ++kick) {
-          const uint32_t w = ent[k].wid, b1 = bucket1(w, sd, nbm), b2 = bucket2(w, sd, nbm);
-          const uint32_t cand[4] = {2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1};
+          const uint32_t w = ent[k].wid, b1 = wide_slot(w, sd, mk, cp, false), b2 = wide_slot(w, sd, mk, cp, true);
+          const uint32_t cand[4] = {b1, b1 + 1, b2, b2 + 1};
           bool placed = false;
           for (uint32_t q : cand)
             if (owner[q] < 0) {
@@ -428,12 +478,12 @@ bool LiveTrie::relocate(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const 
       }
       if (ok) {
         seed = sd;
-        for (uint32_t q = 0; q < cc; ++q)
+        for (uint32_t q = cc; q-- > 0;)  // (the '+' entry ends at slot 0)
           if (owner[q] >= 0) pos[owner[q]] = q;
         for (uint32_t k = 0; k < e; ++k) {
           if (ent[k].wid == WID_PLUS) continue;
-          const uint32_t b1 = bucket1(ent[k].wid, sd, nbm);
-          if (pos[k] / 2 != b1) ovf_at.push_back(2 * b1);
+          const uint32_t b1 = wide_slot(ent[k].wid, sd, mk, cp, false);
+          if (pos[k] != b1 && pos[k] != b1 + 1) ovf_at.push_back(b1);
         }
       }
     }
@@ -456,6 +506,10 @@ bool LiveTrie::relocate(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const 
     sid[2 * p + 1] = ent[k].it;
     if (ent[k].ih != WID_NONE) loc[ent[k].ih] = p << 2 | FIDLOC_HASH;
     if (ent[k].it != WID_NONE) loc[ent[k].it] = p << 2 | FIDLOC_TERM;
+  }
+  if (plus_mask) {
+    pcap[nb] = plus_copies(plus_mask, has_plus, caplog) ? static_cast<uint8_t>(caplog) : 0u;
+    sync_plus(cx, nb);  // (new slots: nothing to touch)
   }
   for (uint32_t q : ovf_at) edges[nb + q].meta |= META_BUCKET_OVF;
   const uint32_t smeta = (caplog & META_CAPLOG2_MASK) | META_HAS_EDGES | (has_plus ? META_HAS_PLUS : 0u) |
@@ -484,6 +538,7 @@ void LiveTrie::flip(Ctx& c, uint32_t id, bool want, bool atomic) {
     edges[p].meta ^= bit;
   }
   touch(c, p);
+  if (has_copies(p)) c.plus_heads.push_back(static_cast<uint32_t>(p));  // copies: after the flips
 }
 
 // emqx_topic:words/1 (emqx_topic.erl:153-164) to word ids; a final '#' is the parent level's
@@ -569,7 +624,7 @@ bool LiveTrie::insert(Ctx& c, const FilterStore& fs, uint32_t id, const std::vec
     uint64_t nb = 0;
     if (!alloc(c, 1, &nb)) return false;
     const bool plus = w[j] == WID_PLUS;
-    const uint32_t at = plus ? 0u : lit_slot(w[j], 0, 1);
+    const uint32_t at = plus ? 0u : lit_slot(w[j], 0, 1, false);
     edges[nb] = edges[nb + 1] = EMPTY_SLOT;
     for (uint64_t q = 2 * nb; q < 2 * nb + 4; ++q) {
       fids[q] = FID_NONE;
@@ -629,6 +684,10 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
     const uint32_t id = fl[i];
     if (loc[id] != FIDLOC_ROOT_HASH) flip(c, id, fs.live[id] != 0, true);
   });
+  for (Ctx& c : cx) {  // '+' edges flipped in place: their copies, serially (two flips may share one)
+    for (uint32_t p : c.plus_heads) sync_plus(cx[0], p);
+    c.plus_heads.clear();
+  }
 
   // 2. tokenize (read-only vocab lookups in parallel; unknown words interned serially)
   const uint64_t ni = ins.size();

@@ -174,8 +174,8 @@ __device__ __forceinline__ uint32_t intern_word(const TableView& tv, uint32_t h,
 
 // Probe one node's edge array (slots [base, base + cap)) for `wid` ('+' sits in slot 0;
 // literals perfect-hashed, or in 2-slot buckets, according to the node's meta).
-__device__ __forceinline__ bool probe_one(const EdgeSlot* edges, uint32_t base, uint32_t meta, uint32_t wid,
-                                          Slot* out) {
+__device__ __forceinline__ bool probe_one(const EdgeSlot* edges, uint32_t plus_mask, uint32_t base,
+                                          uint32_t meta, uint32_t wid, Slot* out) {
   if (wid == WID_PLUS) {
     *out = load_slot(edges, base);
     return out->a.x == WID_PLUS;
@@ -183,17 +183,18 @@ __device__ __forceinline__ bool probe_one(const EdgeSlot* edges, uint32_t base, 
   const uint32_t mask = (1u << (meta & META_CAPLOG2_MASK)) - 1u;
   const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
   if (meta & META_PH) {
-    *out = load_slot(edges, base + lit_slot(wid, sd, mask));
+    const bool cp = plus_copies(plus_mask, (meta & META_HAS_PLUS) != 0, meta & META_CAPLOG2_MASK);
+    *out = load_slot(edges, base + lit_slot(wid, sd, mask, cp));
     return out->a.x == wid;
   }
-  const uint32_t nbm = mask >> 1;
-  const uint32_t b1 = bucket1(wid, sd, nbm);
-  const Slot x = load_slot(edges, base + 2 * b1), y = load_slot(edges, base + 2 * b1 + 1);
+  const bool cp = plus_copies(plus_mask, (meta & META_HAS_PLUS) != 0, meta & META_CAPLOG2_MASK);
+  const uint32_t b1 = wide_slot(wid, sd, mask, cp, false);
+  const Slot x = load_slot(edges, base + b1), y = load_slot(edges, base + b1 + 1);
   if (x.a.x == wid) { *out = x; return true; }
   if (y.a.x == wid) { *out = y; return true; }
   if (!(x.a.z & META_BUCKET_OVF)) return false;
-  const uint32_t b2 = bucket2(wid, sd, nbm);
-  const Slot u = load_slot(edges, base + 2 * b2), v = load_slot(edges, base + 2 * b2 + 1);
+  const uint32_t b2 = wide_slot(wid, sd, mask, cp, true);
+  const Slot u = load_slot(edges, base + b2), v = load_slot(edges, base + b2 + 1);
   if (u.a.x == wid) { *out = u; return true; }
   if (v.a.x == wid) { *out = v; return true; }
   return false;
@@ -216,7 +217,7 @@ __device__ uint32_t exact_walk1(const TableView& tv, uint32_t root_base, uint32_
     }
     if (w == WID_NONE || !(meta & META_HAS_EDGES)) return FID_NONE;
     Slot s;
-    if (!probe_one(tv.edges, base, meta, w, &s)) return FID_NONE;
+    if (!probe_one(tv.edges, tv.plus_mask, base, meta, w, &s)) return FID_NONE;
     base = s.a.y;
     meta = s.a.z;
     term_inline = s.a.w;
@@ -255,33 +256,78 @@ __device__ __forceinline__ uint2 make_item(uint32_t base, uint32_t meta, bool dr
 
 __device__ __forceinline__ uint32_t item_topic(uint2 it) { return (it.y >> IT_TOPIC_SHIFT) & 63u; }
 
+// The three probe loads of one item — '+' slot, literal slot, the bucket's second slot — each
+// on the lanes that need it, issued back to back under one wait.  Written as one asm block
+// because the compiler, given `if (need) x = load(...)`, tests the '+' slot inside its own
+// branch (a wait there: two dependent round trips per step, measured), and narrows the
+// literal loads to their key dwords, fetching the chosen slot's other 12 bytes after the
+// compare (a third).  Masked-off lanes keep the empty slot.  Vector loads and exec writes
+// only.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load3_masked(const EdgeSlot* edges, uint32_t ip, uint32_t il, uint32_t ia, bool np,
+                                             bool nl, bool na, Slot& p, Slot& l, Slot& a) {
+  const uint64_t mp = __ballot(np), ml = __ballot(nl), ma = __ballot(na);
+  const EdgeSlot* pp = edges + ip;
+  const EdgeSlot* pl = edges + il;
+  const EdgeSlot* pa = edges + ia;
+  u32x4 vp = {WID_NONE, 0u, 0u, 0u}, vl = vp, va = vp;
+  uint64_t save;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_and_b64 exec, %[sv], %[mp]\n\t"
+      "global_load_dwordx4 %[p], %[ap], off\n\t"
+      "s_and_b64 exec, %[sv], %[ml]\n\t"
+      "global_load_dwordx4 %[l], %[al], off\n\t"
+      "s_and_b64 exec, %[sv], %[ma]\n\t"
+      "global_load_dwordx4 %[a], %[aa], off\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+      "s_waitcnt vmcnt(0)"
+      : [p] "+v"(vp), [l] "+v"(vl), [a] "+v"(va), [sv] "=&s"(save)
+      : [ap] "v"(pp), [al] "v"(pl), [aa] "v"(pa), [mp] "s"(mp), [ml] "s"(ml), [ma] "s"(ma)
+      : "memory");
+  p.a = make_uint4(vp.x, vp.y, vp.z, vp.w);
+  p.idx = ip;
+  l.a = make_uint4(vl.x, vl.y, vl.z, vl.w);
+  l.idx = il;
+  a.a = make_uint4(va.x, va.y, va.z, va.w);
+  a.idx = ia;
+}
+
 // Probe the '+' edge and the literal edge of K nodes at once: every load is issued
 // before any result is consumed, so a step costs one dependent round trip (plus one more for
 // the ~1% of wide-node words displaced to their secondary bucket).  Perfect-hashed nodes
 // answer in one slot load; wide nodes load their word's 2-slot bucket (one 32-B pair).
 template <int K>
-__device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, const uint32_t (&base)[K],
+__device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, uint32_t plus_mask,
+                                            const uint32_t (&base)[K],
                                             const uint32_t (&hparams)[K], const bool (&isph)[K],
-                                            const bool (&needL)[K], const uint32_t (&wid)[K],
+                                            const bool (&cpy)[K], const bool (&needL)[K], const uint32_t (&wid)[K],
                                             const bool (&needP)[K], Slot (&lit)[K], bool (&fL)[K],
                                             Slot (&pls)[K], bool (&fP)[K], uint32_t& extra) {
   Slot alt[K];
   bool wide[K], again[K];
-  uint32_t sdk[K], nbm[K];
+  uint32_t sdk[K], msk[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t caplog = isph[k] ? (hparams[k] & 15u) : (hparams[k] & 31u);
     sdk[k] = isph[k] ? (hparams[k] >> 4) : (hparams[k] >> 5);
     const uint32_t mask = (1u << caplog) - 1u;
-    nbm[k] = mask >> 1;
+    msk[k] = mask;
     wide[k] = needL[k] && !isph[k];
-    const uint32_t i1 = isph[k] ? lit_slot(wid[k], sdk[k], mask) : 2u * bucket1(wid[k], sdk[k], nbm[k]);
-    pls[k] = empty_slot();
-    lit[k] = pls[k];
-    alt[k] = pls[k];
-    if (needP[k]) pls[k] = load_slot(edges, base[k]);
-    if (needL[k]) lit[k] = load_slot(edges, base[k] + i1);
-    if (wide[k]) alt[k] = load_slot(edges, base[k] + i1 + 1);  // same 32-B bucket
+    const uint32_t i1 = isph[k] ? lit_slot(wid[k], sdk[k], mask, cpy[k]) : wide_slot(wid[k], sdk[k], mask, cpy[k], false);
+    // the '+' edge: its copy in the literal probe's line when the table has copies (one L2
+    // request for both loads), else slot 0
+    const uint32_t at_p = base[k] + (needL[k] ? plus_copy(i1, cpy[k]) : 0u), at_l = base[k] + i1;
+    if constexpr (K == 1) {
+      load3_masked(edges, at_p, at_l, at_l + 1, needP[k], needL[k], wide[k], pls[k], lit[k], alt[k]);
+    } else {
+      pls[k] = empty_slot();
+      lit[k] = pls[k];
+      alt[k] = pls[k];
+      if (needP[k]) pls[k] = load_slot(edges, at_p);
+      if (needL[k]) lit[k] = load_slot(edges, at_l);
+      if (wide[k]) alt[k] = load_slot(edges, at_l + 1);  // same 32-B bucket
+    }
   }
   bool any_again = false;
 #pragma unroll
@@ -299,7 +345,7 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (!again[k]) continue;
-      const uint32_t i2 = 2u * bucket2(wid[k], sdk[k], nbm[k]);
+      const uint32_t i2 = wide_slot(wid[k], sdk[k], msk[k], cpy[k], true);
       const Slot u = load_slot(edges, base[k] + i2), v = load_slot(edges, base[k] + i2 + 1);
       ++extra;
       if (u.a.x == wid[k]) { lit[k] = u; fL[k] = true; }
@@ -708,6 +754,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     wave_sync();
   }
 
+  if (DIAG && a.diag_stop) top = 0;  // phase A alone (diagnostic counter passes)
   constexpr uint32_t POP = 64u * K;
   constexpr uint32_t HALF = STACK_CAP / 2;
   while (true) {
@@ -775,7 +822,12 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     wave_sync();
     Slot lit[K], pls[K];
     bool fL[K], fP[K];
-    probe_items<K>(tv.edges, ibase, hpar, isph, needL, wid, needP, lit, fL, pls, fP, dg[4]);
+    bool cpy[K];  // the node's array holds '+' copies (a '$' topic's root item keeps them too)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      cpy[k] = plus_copies(tv.plus_mask, (it[k].y & IT_PLUS) || (droot[k] && (tv.root_meta & META_HAS_PLUS)),
+                           isph[k] ? (hpar[k] & 15u) : (hpar[k] & 31u));
+    probe_items<K>(tv.edges, tv.plus_mask, ibase, hpar, isph, cpy, needL, wid, needP, lit, fL, pls, fP, dg[4]);
     if (DIAG) {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -1031,7 +1083,9 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       Slot lit[1], pls[1];
       bool fL[1], fP[1];
       uint32_t extra = 0;
-      probe_items<1>(tv.edges, qbase, qhp, qph, nL, w, nP, lit, fL, pls, fP, extra);
+      const bool qcp[1] = {plus_copies(tv.plus_mask, (q.y & META_HAS_PLUS) || (droot && (tv.root_meta & META_HAS_PLUS)),
+                                       q.y & META_CAPLOG2_MASK)};
+      probe_items<1>(tv.edges, tv.plus_mask, qbase, qhp, qph, qcp, nL, w, nP, lit, fL, pls, fP, extra);
       evals += (fL[0] ? 1u : 0u) + (fP[0] ? 1u : 0u);
       const uint32_t m0 = lit[0].a.z, m1 = pls[0].a.z;
       const bool e0 = fL[0] && (m0 & META_HAS_HASH), e1 = fL[0] && leaf && term_ok(m0, mode, droot);

@@ -535,18 +535,29 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
     });
   }
 
-  // A node with a '+' edge keeps it in slot 0.  (Replicating it at the head of every 128-B
-  // line of a wide array, so that '+' and the literal probe share a line, cut L2 misses by
-  // 12% but made the kernel 6% slower: the walk is bound by per-lane access issue, not by
-  // line fetches — DESIGN.md §4.)
-  auto plus_slot = [&](uint64_t v, uint64_t /*cap*/, uint32_t i) -> bool { return has_plus[v] && i == 0; };
+  // A node with a '+' edge keeps it in slot 0, and a copy at the head of every other 64-B line
+  // of its array, so that the '+' probe and the literal probe of a step read one line (one L2
+  // request: tools/gather_bench pair).  (Round 1 measured copies per 128-B line
+  // as 6% slower: then the kernel waited for the '+' load before issuing the literal one.)
+  // A copy of the '+' edge at the head of every 64-B line of the array (layout.h plus_copy);
+  // EMQX_PLUS_LINES=0 (A/B runs only): slot 0 alone
+  static const bool plus_lines = [] {
+    const char* x = getenv("EMQX_PLUS_LINES");
+    return !(x && std::strcmp(x, "0") == 0);
+  }();
+  const uint32_t plus_mask = plus_lines ? ~(PLUS_LINE - 1u) : 0u;
+  out.plus_mask = plus_mask;
+  auto plus_slot = [&](uint64_t v, uint64_t cap, uint32_t i) -> bool {
+    return has_plus[v] && plus_position(i, plus_copies(plus_mask, true, log2u(cap)));
+  };
 
   // Bucketed placement of node v's literal edges (2-slot buckets, two candidate buckets,
   // random-walk eviction) for one seed; false when some word cannot be placed.  The '+'
   // slots stay free.  Afterwards every word outside its primary bucket flags that bucket.
   auto bucket_place = [&](uint64_t v, uint32_t sd, uint32_t cap, std::vector<uint32_t>& key_out,
                           std::vector<uint32_t>& child_out) -> bool {
-    const uint32_t nbm = cap / 2 - 1;
+    const uint32_t mk = cap - 1;
+    const bool cp = plus_copies(plus_mask, has_plus[v], log2u(cap));
     key_out.assign(cap, WID_NONE);
     child_out.assign(cap, 0);
     for (uint32_t i = 0; i < cap; ++i)
@@ -556,8 +567,8 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       if (cwid[j] == WID_PLUS) continue;
       uint32_t key = cwid[j], ch = cid[j];
       for (int kick = 0;; ++kick) {
-        const uint32_t b1 = bucket1(key, sd, nbm), b2 = bucket2(key, sd, nbm);
-        const uint32_t cand[4] = {2 * b1, 2 * b1 + 1, 2 * b2, 2 * b2 + 1};
+        const uint32_t b1 = wide_slot(key, sd, mk, cp, false), b2 = wide_slot(key, sd, mk, cp, true);
+        const uint32_t cand[4] = {b1, b1 + 1, b2, b2 + 1};
         bool placed = false;
         for (uint32_t c : cand)
           if (key_out[c] == WID_NONE) {
@@ -602,7 +613,7 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
           bool ok = true;
           for (uint64_t j = coff[v]; j < coff[v + 1] && ok; ++j) {
             if (cwid[j] == WID_PLUS) continue;
-            const uint32_t sl = lit_slot(cwid[j], sd, mask);
+            const uint32_t sl = lit_slot(cwid[j], sd, mask, plus_copies(plus_mask, has_plus[v], log2u(cap)));
             ok &= !plus_slot(v, cap, sl);
             for (uint32_t x : slots_tmp) ok &= (x != sl);
             slots_tmp.push_back(sl);
@@ -623,7 +634,10 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
         const long k = x ? std::atol(x) : 0;
         return static_cast<uint64_t>(k >= 2 && k <= 16 ? k : 4);
       }();
-      caplog[v] = log2u(next_pow2(slack * e + slack));
+      // (an array holding '+' copies loses a quarter of its slots to them, and one candidate
+      // slot of every other bucket: twice the room keeps later inserts in place)
+      const uint64_t sl = slack;
+      caplog[v] = log2u(next_pow2(sl * e + sl));
       bool ok = false;
       for (uint32_t sd = 0; sd < CUCKOO_SEEDS && !ok; ++sd) {
         ok = bucket_place(v, sd, 1u << caplog[v], ck_key, ck_child);
@@ -809,28 +823,32 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
   std::vector<uint32_t> ck_key, ck_child;
   for (uint64_t v = v0; v < v1; ++v) {
     if (!n_edges[v]) continue;
-    // '+' is pinned at slot 0
+    // '+' is pinned at slot 0, its copies at the other line heads (slot 0 written last: the
+    // filter-id locations, fid_loc, name slot 0)
     for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
       if (cwid[j] == WID_PLUS)
-        for (uint32_t i = 0; i < (1u << caplog[v]); ++i)
+        for (uint32_t i = (1u << caplog[v]); i-- > 0;)
           if (plus_slot(v, 1ull << caplog[v], i)) write_slot(base[v] + i, WID_PLUS, cid[j]);
     if (ph[v]) {
       const uint32_t mask = (1u << caplog[v]) - 1;
       for (uint64_t j = coff[v]; j < coff[v + 1]; ++j)
-        if (cwid[j] != WID_PLUS) write_slot(base[v] + lit_slot(cwid[j], seed[v], mask), cwid[j], cid[j]);
+        if (cwid[j] != WID_PLUS)
+          write_slot(base[v] + lit_slot(cwid[j], seed[v], mask, plus_copies(plus_mask, has_plus[v], caplog[v])), cwid[j],
+                     cid[j]);
       continue;
     }
     // wide node: re-run the placement found in pass 3 (deterministic for its seed), then
     // flag every primary bucket that overflowed
-    const uint32_t cap = 1u << caplog[v], nbm = cap / 2 - 1;
+    const uint32_t cap = 1u << caplog[v];
+    const bool cp = plus_copies(plus_mask, has_plus[v], caplog[v]);
     bucket_place(v, seed[v], cap, ck_key, ck_child);
     for (uint32_t i = 0; i < cap; ++i)
       if (ck_key[i] != WID_NONE && ck_key[i] != WID_PLUS) write_slot(base[v] + i, ck_key[i], ck_child[i]);
     for (uint32_t i = 0; i < cap; ++i) {
       const uint32_t key = ck_key[i];
       if (key == WID_NONE || key == WID_PLUS) continue;
-      const uint32_t b1 = bucket1(key, seed[v], nbm);
-      if (i / 2 != b1) out.edges[base[v] + 2 * b1].meta |= META_BUCKET_OVF;
+      const uint32_t b1 = wide_slot(key, seed[v], cap - 1, cp, false);
+      if (i != b1 && i != b1 + 1) out.edges[base[v] + b1].meta |= META_BUCKET_OVF;
     }
   }
   });
@@ -876,7 +894,7 @@ bool check_tables(const HostTables& t, std::string* err) {
       const EdgeSlot& s = t.edges[base - t.slot_offset + i];
       if (s.wid == WID_NONE) continue;
       if (s.wid == WID_PLUS) {
-        if (i != 0 || !(meta & META_HAS_PLUS)) {
+        if (!plus_position(i, plus_copies(t.plus_mask, true, caplog)) || !(meta & META_HAS_PLUS)) {
           if (err) *err = "'+' edge outside its slots";
           return false;
         }
@@ -884,11 +902,15 @@ bool check_tables(const HostTables& t, std::string* err) {
       }
       ++n_lit;
       bool found;
-      if (ph) found = lit_slot(s.wid, (meta >> META_SEED_SHIFT) & 255u, mask) == i;
+      if (ph)
+        found = lit_slot(s.wid, (meta >> META_SEED_SHIFT) & 255u, mask,
+                         plus_copies(t.plus_mask, meta & META_HAS_PLUS, caplog)) == i;
       else {
-        const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u, nbm = mask / 2;
-        const uint32_t b1 = bucket1(s.wid, sd, nbm), b2 = bucket2(s.wid, sd, nbm);
-        found = i / 2 == b1 || (i / 2 == b2 && (t.edges[base - t.slot_offset + 2 * b1].meta & META_BUCKET_OVF));
+        const uint32_t sd = (meta >> META_SEED_SHIFT) & 255u;
+        const bool cp = plus_copies(t.plus_mask, meta & META_HAS_PLUS, caplog);
+        const uint32_t b1 = wide_slot(s.wid, sd, mask, cp, false), b2 = wide_slot(s.wid, sd, mask, cp, true);
+        found = i == b1 || i == b1 + 1 ||
+                ((i == b2 || i == b2 + 1) && (t.edges[base - t.slot_offset + b1].meta & META_BUCKET_OVF));
       }
       if (!found) {
         if (err) *err = "edge not at its lookup slot";

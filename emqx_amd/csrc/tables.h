@@ -108,6 +108,7 @@ struct HostTables {
   uint32_t root_base = 0;
   uint32_t root_meta = 0;
   uint32_t root_hash_fid = FID_NONE;
+  uint32_t plus_mask = 0;    // TableView::plus_mask of the build
   uint64_t n_nodes = 0;
   uint64_t n_words = 0;
   uint32_t max_depth = 0;
@@ -155,6 +156,7 @@ struct LiveTrie {
     bool failed = false;                // spare region exhausted
     std::vector<Entry> ent;
     std::vector<uint32_t> pos, w;
+    std::vector<uint32_t> plus_heads;   // '+' slots flipped in place: copies synced after the flips
   };
 
   std::vector<EdgeSlot> edges;  // host image of device slots [0, cap)
@@ -167,6 +169,10 @@ struct LiveTrie {
   uint32_t max_depth = 0;
   std::vector<uint64_t> loc;    // per engine id: FIDLOC (tables.h)
   VocabState* vocab = nullptr;
+  // '+' copies (layout.h plus_copy): plus_mask of the build, and per array base slot the caplog
+  // of an array whose '+' edge has copies (cap > PLUS_LINE), else 0
+  uint32_t plus_mask = 0;
+  std::vector<uint8_t> pcap;
   // per commit
   uint64_t mark = 0;            // `used` when the commit began: slots >= mark are new
   std::vector<uint32_t> dirty;  // slots < mark rewritten in place (may repeat)
@@ -190,6 +196,10 @@ struct LiveTrie {
   void touch(Ctx& c, uint64_t slot) const {
     if (slot < mark) c.dirty.push_back(static_cast<uint32_t>(slot));
   }
+  bool has_copies(uint64_t slot) const { return plus_mask && pcap[slot] && edges[slot].wid == WID_PLUS; }
+  // Writes the '+' edge at array base `slot` into its copies (each keeps its own
+  // META_BUCKET_OVF position bit) and touches them.
+  void sync_plus(Ctx& c, uint64_t slot);
   void lit_summary(uint32_t base, uint32_t meta, uint32_t* n_lit, uint32_t* only, uint32_t* bloom,
                    uint32_t* bloom8) const;
   EdgeSlot encode(uint32_t wid, bool has_edges, uint32_t base, uint32_t smeta, uint32_t fid_h, uint32_t fid_t,

@@ -459,6 +459,16 @@ int emqx_htrie_commit(emqx_htrie* h, int full, uint64_t* stats8);
 int emqx_htrie_match(emqx_htrie* h, uint32_t mode, const uint8_t* topic_bytes, const uint64_t* topic_offsets,
                      uint64_t n, uint64_t* out_offsets, uint32_t* out_ids, uint64_t cap, uint64_t* n_out);
 int emqx_htrie_check(emqx_htrie* h, char* err, uint64_t err_cap);
+/* Diagnostic (tools/walk_sim.py): an L2 model of the fast kernel's walk over this image.
+ * params[8]: XCDs, L2 bytes per XCD, line bytes, ways, resident tiles per XCD, phase-A ticks,
+ * slab writes (1: allocate in L2, 0: streamed past it), what-if layout flags.
+ * out[n_out]: topics, tiles, items, 16-B loads, L2 accesses, misses, vocab loads, vocab
+ * misses, items with both probes, ... of them in different lines, chain items, their misses,
+ * misses by item level 0..7+, items by level 0..7+, wide items, their misses, steps, '+' probe
+ * misses, literal probe misses, emissions, '+' loads, perfect-hash loads, wide-bucket loads,
+ * hits by item level 0..7+. */
+int emqx_htrie_walk_sim(emqx_htrie* h, const uint8_t* topic_bytes, const uint64_t* topic_offsets, uint64_t n,
+                        const uint64_t* params, uint64_t* out, uint32_t n_out);
 
 const char* emqx_strerror(int code);
 /* Library version string. */

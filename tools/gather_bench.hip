@@ -60,6 +60,25 @@ __global__ void indep_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t ite
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Two 16-B loads per lane per iteration (`gather_bench pair`): in one 64-B line (SAME = 1) or in
+// two random lines (SAME = 0).  Prices the '+' probe sharing the literal probe's line: does the
+// second load of a line cost an L2 request and a miss of its own?
+template <int SAME>
+__global__ void pair_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t iters, uint32_t* out) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t acc = 0;
+  uint32_t h = mix(gid * 0x9e3779b9u + 4321u);
+  for (uint32_t k = 0; k < iters; ++k) {
+    h = mix(h + k);
+    const uint32_t i = (h % n) & ~3u;
+    const uint32_t j = SAME ? (i | (1u + (h >> 30))) : (mix(h ^ 0x5bd1e995u) % n);
+    const uint4 x = *reinterpret_cast<const uint4*>(t + i);
+    const uint4 y = *reinterpret_cast<const uint4*>(t + j);
+    acc ^= x.x + x.y + y.z + y.w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 __global__ void chase_kernel(const Rec* __restrict__ t, uint32_t n, uint32_t iters, uint32_t* out) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t i = mix(gid * 0x9e3779b9u + 777u) % n;
@@ -114,8 +133,41 @@ static int calibrate() {
   return 0;
 }
 
+static int pairs() {
+  const uint64_t bytes = 1ull << 30;
+  const uint32_t n = (uint32_t)(bytes / sizeof(Rec));
+  Rec* t;
+  uint32_t* out;
+  CK(hipMalloc(&t, bytes));
+  CK(hipMalloc(&out, 64));
+  hipLaunchKernelGGL(init_kernel, dim3(4096), dim3(256), 0, 0, t, n, 2654435761u % n | 1u);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const uint32_t blocks = 256u * 24 / 4u, iters = 256;
+  for (int rep = 0; rep < 3; ++rep) {
+    for (int v = 0; v < 3; ++v) {
+      CK(hipEventRecord(e0));
+      if (v == 0) hipLaunchKernelGGL(indep_kernel, dim3(blocks), dim3(256), 0, 0, t, n, iters, out);
+      if (v == 1) hipLaunchKernelGGL(pair_kernel<1>, dim3(blocks), dim3(256), 0, 0, t, n, iters, out);
+      if (v == 2) hipLaunchKernelGGL(pair_kernel<0>, dim3(blocks), dim3(256), 0, 0, t, n, iters, out);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (rep == 2)
+        printf("{\"pair\": \"%s\", \"ms\": %.4f, \"iters_per_s\": %.4g}\n",
+               v == 0 ? "one load" : v == 1 ? "two loads, one 64-B line" : "two loads, two lines", ms,
+               (double)blocks * 256 * iters / (ms * 1e-3));
+    }
+  }
+  CK(hipFree(t));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && argv[1][0] == 'c') return calibrate();
+  if (argc > 1 && argv[1][0] == 'p') return pairs();
   const uint64_t sizes_mb[] = {2, 64, 1024};
   const int wpc[] = {8, 16, 24, 32};
   uint32_t* out;
