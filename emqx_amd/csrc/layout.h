@@ -166,16 +166,21 @@ EMQX_HD uint32_t word_hash_bytes(const uint8_t* p, uint32_t n) {
 
 EMQX_HD uint32_t vocab_slot0(uint32_t hash) { return hash; }
 
-// Slot of literal word `wid` in a perfect-hashed node's array (mask = cap - 1).  In an array
-// that holds '+' copies (copies = plus_copies(...)) the literal slots are the 3/4 of the array
-// that are not line heads: the hash picks one of them directly (multiply-high over their
-// count), so the copies cost the perfect hash no seeds and no larger arrays.
+// The per-node hash of a literal word (seed = the node's hashing seed): one fmix32 serves the
+// perfect-hash slot and the primary bucket alike, so a walk step computes it once whatever the
+// node's hashing (the kernels are bound by their per-step instruction count).
+EMQX_HD uint32_t node_hash(uint32_t wid, uint32_t seed) { return mix32(wid ^ (seed * 0x9E3779B1u + 0x7F4A7C15u)); }
+
+// Slot of a literal word with node hash h in a perfect-hashed node's array (mask = cap - 1).
+// In an array that holds '+' copies (copies = plus_copies(...)) the literal slots are the 3/4
+// of the array that are not line heads: a hash landing on a head moves to slot 1 or 2 of its
+// line (by its top bit), so the copies cost the perfect hash no larger arrays.
+EMQX_HD uint32_t ph_slot(uint32_t h, uint32_t mask, bool copies) {
+  const uint32_t s = h & mask;
+  return (!copies || (s & (PLUS_LINE - 1u))) ? s : s + 1u + (h >> 31);
+}
 EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask, bool copies) {
-  const uint32_t h = mix32(wid ^ (seed * 0x9E3779B1u + 0x7F4A7C15u));
-  if (!copies) return h & mask;
-  const uint32_t n3 = ((mask + 1u) / PLUS_LINE) * (PLUS_LINE - 1u);
-  const uint32_t k = static_cast<uint32_t>((static_cast<uint64_t>(h) * n3) >> 32);
-  return (k / (PLUS_LINE - 1u)) * PLUS_LINE + 1u + k % (PLUS_LINE - 1u);
+  return ph_slot(node_hash(wid, seed), mask, copies);
 }
 
 
@@ -183,9 +188,7 @@ EMQX_HD uint32_t lit_slot(uint32_t wid, uint32_t seed, uint32_t mask, bool copie
 // or — rarely, flagged by META_BUCKET_OVF on the primary bucket's first slot —
 // in its secondary bucket.  Bucket 0's slot 0 is '+'.  `seed` (7 bits) is re-drawn by the
 // builder until every word fits.
-EMQX_HD uint32_t bucket1(uint32_t wid, uint32_t seed, uint32_t nbmask) {
-  return mix32(wid ^ (0x3C6EF372u + seed * 0x9E3779B9u)) & nbmask;
-}
+EMQX_HD uint32_t bucket1(uint32_t wid, uint32_t seed, uint32_t nbmask) { return node_hash(wid, seed) & nbmask; }
 EMQX_HD uint32_t bucket2(uint32_t wid, uint32_t seed, uint32_t nbmask) {
   const uint32_t a = bucket1(wid, seed, nbmask), b = mix32(wid ^ (0xDAA66D2Bu + seed * 0x7F4A7C15u)) & nbmask;
   return b != a ? b : ((a + 1) & nbmask);
@@ -195,11 +198,15 @@ EMQX_HD uint32_t bucket2(uint32_t wid, uint32_t seed, uint32_t nbmask) {
 // three literal slots of a 64-B line — slots {1, 2} or {2, 3} after the line's '+' copy — so
 // both candidate slots and the copy share a line, and adding '+' later finds every line head
 // free.  (The windows of a line overlap; each has its own first slot for META_BUCKET_OVF.)
+// Primary window / bucket from the node hash h (wide_slot(.., false) = wide_slot1(node_hash)).
+EMQX_HD uint32_t wide_slot1(uint32_t h, uint32_t mask, bool copies) {
+  if (!copies) return 2u * (h & (mask >> 1));
+  return (((h >> 1) & ((mask + 1u) / PLUS_LINE - 1u)) * PLUS_LINE) + 1u + (h & 1u);
+}
 EMQX_HD uint32_t wide_slot(uint32_t wid, uint32_t seed, uint32_t mask, bool copies, bool second) {
   if (!copies) return 2u * (second ? bucket2(wid, seed, mask >> 1) : bucket1(wid, seed, mask >> 1));
   const uint32_t lm = (mask + 1u) / PLUS_LINE - 1u;  // line mask
-  const uint32_t h1 = mix32(wid ^ (0x3C6EF372u + seed * 0x9E3779B9u));
-  const uint32_t w1 = (((h1 >> 1) & lm) * PLUS_LINE) + 1u + (h1 & 1u);
+  const uint32_t w1 = wide_slot1(node_hash(wid, seed), mask, true);
   if (!second) return w1;
   const uint32_t h2 = mix32(wid ^ (0xDAA66D2Bu + seed * 0x7F4A7C15u));
   const uint32_t w2 = (((h2 >> 1) & lm) * PLUS_LINE) + 1u + (h2 & 1u);
@@ -207,7 +214,12 @@ EMQX_HD uint32_t wide_slot(uint32_t wid, uint32_t seed, uint32_t mask, bool copi
 }
 constexpr uint32_t CUCKOO_SEEDS = 128;
 
-EMQX_HD uint32_t litf_hash(uint32_t wid) { return mix32(wid ^ 0xA5A5A5A5u); }
+// Hash of a word for the literal filters (Bloom bits, fingerprints): one multiply and a fold,
+// computed per walk step for the topic's next word.
+EMQX_HD uint32_t litf_hash(uint32_t wid) {
+  const uint32_t m = (wid ^ 0xA5A5A5A5u) * 0x9E3779B1u;
+  return m ^ (m >> 15);
+}
 
 // May the child (meta, litf) have a literal edge for `wid`?  No false negatives.
 EMQX_HD bool litf_may_contain(uint32_t meta, uint32_t litf, uint32_t wid) {

@@ -49,14 +49,16 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
 // Exclusive prefix of a small per-lane value (< 2^BITS) across the wave; *total = wave sum.
+// (per bit: one ballot, v_mbcnt_lo/hi for the lanes below, a scalar popcount for the total)
 template <int BITS>
 __device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t lane, uint32_t* total) {
-  const uint64_t lt = lanemask_lt(lane);
+  (void)lane;
   uint32_t pre = 0, tot = 0;
 #pragma unroll
   for (int b = 0; b < BITS; ++b) {
     const uint64_t m = __ballot((v >> b) & 1u);
-    pre += static_cast<uint32_t>(__popcll(m & lt)) << b;
+    pre += __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u))
+           << b;
     tot += static_cast<uint32_t>(__popcll(m)) << b;
   }
   *total = tot;
@@ -293,6 +295,51 @@ __device__ __forceinline__ void load3_masked(const EdgeSlot* edges, uint32_t ip,
   a.idx = ia;
 }
 
+// K = 2: the six loads of two items per lane, one asm group under one wait (as load3_masked).
+__device__ __forceinline__ void load6_masked(const EdgeSlot* edges, const uint32_t (&ip)[2], const uint32_t (&il)[2],
+                                             const bool (&np)[2], const bool (&nl)[2], const bool (&na)[2],
+                                             Slot (&p)[2], Slot (&l)[2], Slot (&a)[2]) {
+  const uint64_t mp0 = __ballot(np[0]), ml0 = __ballot(nl[0]), ma0 = __ballot(na[0]);
+  const uint64_t mp1 = __ballot(np[1]), ml1 = __ballot(nl[1]), ma1 = __ballot(na[1]);
+  const EdgeSlot *pp0 = edges + ip[0], *pl0 = edges + il[0], *pa0 = edges + il[0] + 1;
+  const EdgeSlot *pp1 = edges + ip[1], *pl1 = edges + il[1], *pa1 = edges + il[1] + 1;
+  u32x4 vp0 = {WID_NONE, 0u, 0u, 0u}, vl0 = vp0, va0 = vp0, vp1 = vp0, vl1 = vp0, va1 = vp0;
+  uint64_t save;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_and_b64 exec, %[sv], %[mp0]\n\t"
+      "global_load_dwordx4 %[p0], %[ap0], off\n\t"
+      "s_and_b64 exec, %[sv], %[ml0]\n\t"
+      "global_load_dwordx4 %[l0], %[al0], off\n\t"
+      "s_and_b64 exec, %[sv], %[ma0]\n\t"
+      "global_load_dwordx4 %[a0], %[aa0], off\n\t"
+      "s_and_b64 exec, %[sv], %[mp1]\n\t"
+      "global_load_dwordx4 %[p1], %[ap1], off\n\t"
+      "s_and_b64 exec, %[sv], %[ml1]\n\t"
+      "global_load_dwordx4 %[l1], %[al1], off\n\t"
+      "s_and_b64 exec, %[sv], %[ma1]\n\t"
+      "global_load_dwordx4 %[a1], %[aa1], off\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+      "s_waitcnt vmcnt(0)"
+      : [p0] "+v"(vp0), [l0] "+v"(vl0), [a0] "+v"(va0), [p1] "+v"(vp1), [l1] "+v"(vl1), [a1] "+v"(va1),
+        [sv] "=&s"(save)
+      : [ap0] "v"(pp0), [al0] "v"(pl0), [aa0] "v"(pa0), [ap1] "v"(pp1), [al1] "v"(pl1), [aa1] "v"(pa1),
+        [mp0] "s"(mp0), [ml0] "s"(ml0), [ma0] "s"(ma0), [mp1] "s"(mp1), [ml1] "s"(ml1), [ma1] "s"(ma1)
+      : "memory");
+  p[0].a = make_uint4(vp0.x, vp0.y, vp0.z, vp0.w);
+  p[0].idx = ip[0];
+  l[0].a = make_uint4(vl0.x, vl0.y, vl0.z, vl0.w);
+  l[0].idx = il[0];
+  a[0].a = make_uint4(va0.x, va0.y, va0.z, va0.w);
+  a[0].idx = il[0] + 1;
+  p[1].a = make_uint4(vp1.x, vp1.y, vp1.z, vp1.w);
+  p[1].idx = ip[1];
+  l[1].a = make_uint4(vl1.x, vl1.y, vl1.z, vl1.w);
+  l[1].idx = il[1];
+  a[1].a = make_uint4(va1.x, va1.y, va1.z, va1.w);
+  a[1].idx = il[1] + 1;
+}
+
 // Probe the '+' edge and the literal edge of K nodes at once: every load is issued
 // before any result is consumed, so a step costs one dependent round trip (plus one more for
 // the ~1% of wide-node words displaced to their secondary bucket).  Perfect-hashed nodes
@@ -306,7 +353,7 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
                                             Slot (&pls)[K], bool (&fP)[K], uint32_t& extra) {
   Slot alt[K];
   bool wide[K], again[K];
-  uint32_t sdk[K], msk[K];
+  uint32_t sdk[K], msk[K], atp[K], atl[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t caplog = isph[k] ? (hparams[k] & 15u) : (hparams[k] & 31u);
@@ -314,19 +361,26 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
     const uint32_t mask = (1u << caplog) - 1u;
     msk[k] = mask;
     wide[k] = needL[k] && !isph[k];
-    const uint32_t i1 = isph[k] ? lit_slot(wid[k], sdk[k], mask, cpy[k]) : wide_slot(wid[k], sdk[k], mask, cpy[k], false);
+    const uint32_t h = node_hash(wid[k], sdk[k]);
+    const uint32_t i1 = isph[k] ? ph_slot(h, mask, cpy[k]) : wide_slot1(h, mask, cpy[k]);
     // the '+' edge: its copy in the literal probe's line when the table has copies (one L2
     // request for both loads), else slot 0
-    const uint32_t at_p = base[k] + (needL[k] ? plus_copy(i1, cpy[k]) : 0u), at_l = base[k] + i1;
-    if constexpr (K == 1) {
-      load3_masked(edges, at_p, at_l, at_l + 1, needP[k], needL[k], wide[k], pls[k], lit[k], alt[k]);
-    } else {
+    atp[k] = base[k] + (needL[k] ? plus_copy(i1, cpy[k]) : 0u);
+    atl[k] = base[k] + i1;
+  }
+  if constexpr (K == 1) {
+    load3_masked(edges, atp[0], atl[0], atl[0] + 1, needP[0], needL[0], wide[0], pls[0], lit[0], alt[0]);
+  } else if constexpr (K == 2) {
+    load6_masked(edges, atp, atl, needP, needL, wide, pls, lit, alt);
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
       pls[k] = empty_slot();
       lit[k] = pls[k];
       alt[k] = pls[k];
-      if (needP[k]) pls[k] = load_slot(edges, at_p);
-      if (needL[k]) lit[k] = load_slot(edges, at_l);
-      if (wide[k]) alt[k] = load_slot(edges, at_l + 1);  // same 32-B bucket
+      if (needP[k]) pls[k] = load_slot(edges, atp[k]);
+      if (needL[k]) lit[k] = load_slot(edges, atl[k]);
+      if (wide[k]) alt[k] = load_slot(edges, atl[k] + 1);  // same 32-B bucket
     }
   }
   bool any_again = false;

@@ -240,6 +240,40 @@ __device__ __forceinline__ uint32_t word_at(const RetainArgs& a, const uint32_t*
   return lwords ? lwords[i] : a.wids[i];
 }
 
+// The loads of one walk step — the node's fields (posts[name]), its edge bucket (three 16-B
+// parts), the postings key after a '+' run — each on the lanes that need it, issued back to
+// back under one wait, as one asm block: left to the compiler, a lane's node-field load sat in
+// its own branch with its own wait before the others were issued (two dependent round trips
+// per '+' step).  Masked-off lanes keep the defaults.  Vector loads and exec writes only.
+typedef uint32_t ru32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void step_loads(const uint4* pa, const uint4* pb, const RPostKey* pc, bool na, bool nb,
+                                           bool nc, uint4& a, uint4& b0, uint4& b1, uint4& b2, RPostKey& c) {
+  const uint64_t ma = __ballot(na), mb = __ballot(nb), mc = __ballot(nc);
+  ru32x4 va = {0u, 0u, 0u, 0u}, vb0 = {b0.x, b0.y, b0.z, b0.w}, vb1 = {b1.x, b1.y, b1.z, b1.w},
+         vb2 = {b2.x, b2.y, b2.z, b2.w}, vc = {c.depth, c.wid, c.off, c.len};
+  uint64_t save;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_and_b64 exec, %[sv], %[ma]\n\t"
+      "global_load_dwordx4 %[a], %[pa], off\n\t"
+      "s_and_b64 exec, %[sv], %[mb]\n\t"
+      "global_load_dwordx4 %[b0], %[pb], off\n\t"
+      "global_load_dwordx4 %[b1], %[pb], off offset:16\n\t"
+      "global_load_dwordx4 %[b2], %[pb], off offset:32\n\t"
+      "s_and_b64 exec, %[sv], %[mc]\n\t"
+      "global_load_dwordx4 %[c], %[pc], off\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+      "s_waitcnt vmcnt(0)"
+      : [a] "+v"(va), [b0] "+v"(vb0), [b1] "+v"(vb1), [b2] "+v"(vb2), [c] "+v"(vc), [sv] "=&s"(save)
+      : [pa] "v"(pa), [pb] "v"(pb), [pc] "v"(pc), [ma] "s"(ma), [mb] "s"(mb), [mc] "s"(mc)
+      : "memory");
+  a = make_uint4(va.x, va.y, va.z, va.w);
+  b0 = make_uint4(vb0.x, vb0.y, vb0.z, vb0.w);
+  b1 = make_uint4(vb1.x, vb1.y, vb1.z, vb1.w);
+  b2 = make_uint4(vb2.x, vb2.y, vb2.z, vb2.w);
+  c = RPostKey{vc.x, vc.y, vc.z, vc.w};
+}
+
 template <bool TILE, int SEARCH>
 __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint32_t top, uint4* stk, uint32_t gtop,
                                            uint64_t fbase, const uint32_t* nlevs, const uint64_t* wbase,
@@ -329,6 +363,7 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
     uint4 ka = make_uint4(WID_NONE, 0, WID_NONE, 0), kb = ka, kc = make_uint4(0, 0, 0, 0);
     RPostKey pk{WID_NONE, 0, 0, 0};
     uint32_t bk = 0, ps = 0;
+    bool nA = false, nB = false, nC = false;  // loads: node fields, edge bucket, postings key
     if (act) {
       uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
       while (lo < hi) {
@@ -361,23 +396,23 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
       // fewer per step of an exact filter).  Every other step reads them.
       if (q.z & RITEM_POST) {
         name = q.x + (lane - before);
-        if (w_cur >= WID_HASH) {
-          const uint4 p = rv.posts[name];
-          rn = RNode{0, p.z, p.x, p.w};
-        }
+        nA = w_cur >= WID_HASH;
       } else {
         rn = RNode{0, rv.root_ncld, rv.root_lo, rv.root_hi};
       }
       if (w_cur < WID_HASH) {  // a literal: its bucket
         bk = redge_slot0(name, w_cur) & rv.edge_mask;
-        const uint4* kp = reinterpret_cast<const uint4*>(rv.edges + bk);
-        ka = kp[0];
-        kb = kp[1];
-        kc = kp[2];
+        nB = true;
       } else if (w_cur == WID_PLUS && wl < WID_HASH && j < fn) {  // '+' run, then a literal
         ps = rpost_slot0(j + 1, wl) & rv.pkey_mask;
-        pk = rv.pkeys[ps];
+        nC = true;
       }
+    }
+    {  // the step's loads, one group under one wait (step_loads)
+      uint4 pa;
+      step_loads(rv.posts + name, reinterpret_cast<const uint4*>(rv.edges + bk), rv.pkeys + ps, nA, nB, nC, pa, ka, kb,
+                 kc, pk);
+      if (nA) rn = RNode{0, pa.z, pa.x, pa.w};
     }
     __builtin_amdgcn_wave_barrier();
     RPROF_MARK(1);

@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 ROOT=$(pwd)
 [ -s "$OUT/counters.txt" ] || timeout -s KILL 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --cache /tmp/wlB"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-host-api --streams 1 --cache /tmp/wlB"
 timeout -k 10 300 python -u bench.py $ARGS > "$OUT/prime.json" 2> "$OUT/prime.err" || { echo prime failed; exit 1; }
 for v in "$@"; do
   i=0
