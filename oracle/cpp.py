@@ -50,6 +50,7 @@ def lib():
         L.orf_publish.restype = ctypes.c_uint64
         L.orf_publish.argtypes = [vp, u64p, u32p, ctypes.c_uint64, u32p, ctypes.c_int, u32p, u64p]
         L.orf_checksum.argtypes = [u64p, u32p, u32p, ctypes.c_uint64, u64p]
+        L.orf_publish_list.argtypes = [vp, u64p, u32p, ctypes.c_uint64, u32p, ctypes.c_int, u64p, u32p, u32p]
         L.orf_churn.restype = ctypes.c_uint64
         L.orf_churn.argtypes = [vp, u32p, u32p, u32p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
         L.orc_topic_match.restype = ctypes.c_int
@@ -167,6 +168,22 @@ class FanoutOracle:
                                   _p(counts), _p(sums))
         return counts[:n], sums[:n], int(total)
 
+    def publish_list(self, moff, mids, keys, threads=1):
+        """Deliveries listed: (offsets[n+1], subscribers, filters | SHARED_BIT), route order per
+        topic (oracle/fanout_oracle.cpp orf_publish_list)."""
+        counts, _, total = self.publish(moff, mids, keys, threads)
+        moff = np.ascontiguousarray(np.asarray(moff, dtype=np.uint64))
+        mids = np.ascontiguousarray(np.asarray(mids, dtype=np.uint32))
+        keys = np.ascontiguousarray(np.asarray(keys, dtype=np.uint32))
+        n = len(moff) - 1
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum(counts, dtype=np.uint64)
+        subs = np.zeros(max(total, 1), np.uint32)
+        fils = np.zeros(max(total, 1), np.uint32)
+        lib().orf_publish_list(self.h, _p(moff), _p(mids) if mids.size else None, n, _p(keys), threads, _p(off),
+                               _p(subs), _p(fils))
+        return off, subs[:total], fils[:total]
+
     def churn(self, sub_filter, sub_id, sub_group, add, threads=1) -> int:
         """Subscribe (add) / unsubscribe operations as the reference's ETS bags take them
         (oracle/fanout_oracle.cpp orf_churn); returns the ops that changed the table."""
@@ -212,6 +229,28 @@ class RetainScan:
         sums = np.zeros(max(n, 1), dtype=np.uint64)
         lib().orr_select(self.h, _p(buf), _p(offs), n, now, threads, _p(counts), _p(sums))
         return counts[:n], sums[:n]
+
+
+def pair_csr_mismatches(off_g, a_g, b_g, off_o, a_o, b_o):
+    """Topics whose (a, b) pair multisets differ between two CSRs (vectorised: pairs sorted
+    within each topic, then compared element-wise)."""
+    off_g = np.asarray(off_g, dtype=np.int64)
+    off_o = np.asarray(off_o, dtype=np.int64)
+    n = len(off_g) - 1
+    cnt_g, cnt_o = np.diff(off_g), np.diff(off_o)
+    bad = np.nonzero(cnt_g != cnt_o)[0]
+    if bad.size or not n:
+        return bad
+
+    def canon(off, a, b):
+        t = np.repeat(np.arange(n, dtype=np.int64), np.diff(off))
+        key = (np.asarray(a, dtype=np.uint64) << np.uint64(32)) | np.asarray(b, dtype=np.uint64)
+        o = np.lexsort((key, t))
+        return key[o], t[o]
+
+    kg, tg = canon(off_g, a_g, b_g)
+    ko, _ = canon(off_o, a_o, b_o)
+    return np.unique(tg[kg != ko])
 
 
 def csr_mismatches(off_g, ids_g, off_o, ids_o):

@@ -123,6 +123,41 @@ uint64_t orf_publish(void* h, const uint64_t* moff, const uint32_t* mids, uint64
   return total.load();
 }
 
+// Hash strategies, deliveries listed: per topic of a match CSR its (subscriber, filter) pairs
+// (filter | SHARED_BIT for a $share pick) at out_off[t] (exclusive prefix of the counts, which
+// the caller sizes with orf_publish).  The per-topic order is route order, not sorted.
+void orf_publish_list(void* h, const uint64_t* moff, const uint32_t* mids, uint64_t n, const uint32_t* keys,
+                      int nthreads, const uint64_t* out_off, uint32_t* out_subs, uint32_t* out_fils) {
+  const Fanout* f = static_cast<const Fanout*>(h);
+  if (nthreads < 1) nthreads = 1;
+  auto work = [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t t = lo; t < hi; ++t) {
+      uint64_t at = out_off[t];
+      for (uint64_t j = moff[t]; j < moff[t + 1]; ++j) {
+        const uint32_t fid = mids[j];
+        if (fid >= f->plain.size()) continue;
+        for (uint32_t sb : f->plain[fid]) {
+          out_subs[at] = sb;
+          out_fils[at++] = fid;
+        }
+        for (const Group& g : f->groups[fid]) {
+          if (g.members.empty()) continue;
+          out_subs[at] = g.members[keys[t] % g.members.size()];
+          out_fils[at++] = fid | SHARED_BIT;
+        }
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  const uint64_t chunk = (n + nthreads - 1) / nthreads;
+  for (int k = 0; k < nthreads; ++k) {
+    const uint64_t lo = k * chunk, hi = std::min<uint64_t>(n, lo + chunk);
+    if (lo >= hi) break;
+    th.emplace_back(work, lo, hi);
+  }
+  for (auto& x : th) x.join();
+}
+
 // Subscribe (add = 1) / unsubscribe (add = 0) operations, in order per filter.  Returns the
 // operations that changed the table.
 uint64_t orf_churn(void* h, const uint32_t* filt, const uint32_t* sub, const uint32_t* grp, const uint8_t* add,

@@ -99,3 +99,33 @@ def test_dollar_and_wildcard_topics_follow_match_routes():
     b.subscribe(b"a/+", "exact-wild")  # a wildcard *topic* publish hits only the identical filter
     assert b.publish(b"$SYS/x", 0) == [(b"$SYS/#", "sys", False)]
     assert sorted(b.publish(b"a/+", 0), key=repr) == [(b"a/+", "exact-wild", False)]
+
+
+def test_cpp_fanout_lists_agree_with_counts_and_checksums():
+    """oracle/fanout_oracle.cpp: the listed deliveries (orf_publish_list, used for ID-for-ID
+    checks at config E's full size) give the same per-topic counts and order-free checksums as
+    orf_publish, and pair_csr_mismatches finds a swapped pair but not a reordering."""
+    import numpy as np
+    from oracle import cpp as C
+    from emqx_amd import workloads as W
+    fw = W.config_e(n_filters=20_000, n_subscribers=5_000, n_topics=2_000, seed=9)
+    o = C.CppOracle(True)
+    o.add_packed(*fw.wl.filters)
+    moff, mids, _ = o.match_csr(*fw.wl.topics, mode=C.MODE_ROUTES, threads=4)
+    fo = C.FanoutOracle(fw.sub_filter, fw.sub_id, fw.sub_group)
+    counts, sums, total = fo.publish(moff, mids, fw.keys, threads=4)
+    off, subs, fils = fo.publish_list(moff, mids, fw.keys, threads=4)
+    assert int(off[-1]) == total > 1000
+    assert np.array_equal(np.diff(off.astype(np.int64)), counts.astype(np.int64))
+    assert np.array_equal(C.delivery_checksums(off, subs, fils), sums)
+    assert C.pair_csr_mismatches(off, subs, fils, off, subs, fils).size == 0
+    t = int(np.argmax(np.diff(off.astype(np.int64)) > 2))
+    a, b = int(off[t]), int(off[t + 1])
+    rev = subs.copy()
+    rev[a:b] = rev[a:b][::-1]
+    fr = fils.copy()
+    fr[a:b] = fr[a:b][::-1]
+    assert C.pair_csr_mismatches(off, rev, fr, off, subs, fils).size == 0  # order within a topic is free
+    bad = subs.copy()
+    bad[a] ^= 1
+    assert C.pair_csr_mismatches(off, bad, fils, off, subs, fils).tolist() == [t]

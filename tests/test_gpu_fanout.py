@@ -321,3 +321,57 @@ def test_publish_batch_overflow_retry_10k_subscribers():
     assert sorted(plain.tolist()) == subs.tolist()
     assert shared.tolist() == [20_000 + 11 % 5]   # hash_clientid: lists:nth(1 + Key rem N, Members)
     assert sb[10_001] == 7
+
+
+def test_config_e_full_size_id_for_id(F):
+    """Config E at its full size (SURVEY §8 d: 2M filters, 1M subscribers x 10 = 10M
+    subscriptions, 10% in $share groups): a 100K-topic batch matched and fanned out on the
+    device (hash_clientid), every topic's (subscriber, filter) multiset compared ID-for-ID with
+    the C++ restatement of route/aggre/do_dispatch (oracle/fanout_oracle.cpp) over the C++ DFS's
+    match CSR — and that match CSR with the device's."""
+    import os
+    import torch
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import Engine
+    from oracle import cpp as C
+    threads = min(16, os.cpu_count() or 4)
+    fw = W.config_e(n_topics=100_000)
+    assert fw.n_subscriptions > 9_900_000 and fw.wl.n_filters == 2_000_000
+    eng = Engine(0)
+    eng.insert_packed(*fw.wl.filters)
+    eng.commit()
+    st = F.SubTable(0)
+    st.add(fw.sub_filter, fw.sub_id, fw.sub_group)
+    st.commit()
+    dev = torch.device("cuda", 0)
+    n = fw.wl.n_topics
+    tb = torch.from_numpy(fw.wl.topics[0]).to(dev)
+    to = torch.from_numpy(fw.wl.topics[1].view(np.int64)).to(dev)
+    moff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    mids = torch.empty(64 * n, dtype=torch.int32, device=dev)
+    nm = eng.match_device(tb.data_ptr(), to.data_ptr(), n, moff.data_ptr(), mids.data_ptr(), 64 * n)
+    keys = torch.from_numpy(fw.keys.view(np.int32)).to(dev)
+    ooff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    with pytest.raises(Exception) as ei:
+        st.fanout_device("hash_clientid", moff.data_ptr(), mids.data_ptr(), n, keys.data_ptr(), ooff.data_ptr(),
+                         0, 0, 0)
+    need = ei.value.needed
+    osubs = torch.empty(need, dtype=torch.int32, device=dev)
+    ofil = torch.empty(need, dtype=torch.int32, device=dev)
+    tot = st.fanout_device("hash_clientid", moff.data_ptr(), mids.data_ptr(), n, keys.data_ptr(), ooff.data_ptr(),
+                           osubs.data_ptr(), ofil.data_ptr(), need)
+    torch.cuda.synchronize()
+    assert tot == need > 30 * n
+    # the match CSR against the C++ DFS
+    o = C.CppOracle(True)
+    o.add_packed(*fw.wl.filters)
+    off_o, ids_o, _ = o.match_csr(*fw.wl.topics, mode=C.MODE_ROUTES, threads=threads)
+    mo = moff.cpu().numpy().view(np.uint64)
+    assert C.csr_mismatches(mo, mids[:nm].cpu().numpy().view(np.uint32), off_o, ids_o).size == 0
+    # deliveries, ID-for-ID per topic
+    fo = C.FanoutOracle(fw.sub_filter, fw.sub_id, fw.sub_group)
+    off_d, subs_d, fils_d = fo.publish_list(off_o, ids_o, fw.keys, threads=threads)
+    oo = ooff.cpu().numpy().view(np.uint64)
+    bad = C.pair_csr_mismatches(oo, osubs.cpu().numpy().view(np.uint32), ofil.cpu().numpy().view(np.uint32),
+                                off_d, subs_d, fils_d)
+    assert bad.size == 0, bad[:10]

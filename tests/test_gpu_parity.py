@@ -221,6 +221,28 @@ def test_config_d_reduced(Engine):
     assert counts.mean() > 3
 
 
+def test_config_d_full_table(Engine):
+    """Config D at its full size (1M adversarial filters, depth-16 topics): 16K topics
+    compared ID-for-ID with the C++ DFS, in batch order and with the walk order forced on (the
+    prefix-key sort and XCD dealing the engine turns on for D's 1M-topic batches)."""
+    import os
+    from emqx_amd import workloads as W
+    d = W.config_d(n_filters=1_000_000, n_topics=16_384)
+    e = Engine()
+    e.insert_packed(*d.filters)
+    e.commit()
+    o = C.CppOracle(True)
+    o.add_packed(*d.filters)
+    off_o, ids_o, _ = o.match_csr(*d.topics, mode=C.MODE_ROUTES, threads=min(16, os.cpu_count() or 4))
+    assert int(off_o[-1]) > 3 * (len(off_o) - 1)
+    for order in (0, 1):
+        e.set_tuning("order", order)
+        off, ids = e.match_packed(*d.topics, mode=0)
+        bad = C.csr_mismatches(off, ids, off_o, ids_o)
+        assert bad.size == 0, (order, bad[:10])
+    e.set_tuning("order", -1)
+
+
 def test_deep_topics_take_deep_path(Engine):
     """Topics beyond the fast path's LDS budget (WID_CAP/8 levels) run on the deep path."""
     rng = random.Random(5)
