@@ -119,7 +119,7 @@ struct TableView {
 // and in the wide upper nodes that is thousands of slot patches per change (measured: commits
 // 40x slower with copies in every array), while those nodes' lines are L2-resident anyway.
 constexpr uint32_t PLUS_LINE = 4;
-constexpr uint32_t PLUS_COPY_MAX_CAPLOG = 10;
+constexpr uint32_t PLUS_COPY_MAX_CAPLOG = 14;
 // Does the array of a node (its meta's caplog, whether it has a '+' edge) hold '+' copies?
 EMQX_HD bool plus_copies(uint32_t plus_mask, bool has_plus, uint32_t caplog) {
   return plus_mask != 0 && has_plus && caplog > 2 && caplog <= PLUS_COPY_MAX_CAPLOG;

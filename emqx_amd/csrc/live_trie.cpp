@@ -384,7 +384,7 @@ bool LiveTrie::relocate(Ctx& cx, bool root, uint64_t pslot, uint32_t wid, const 
     for (uint32_t i = 0; i < ocap; ++i) {
       const uint64_t p = obase + i;
       const EdgeSlot& s = edges[p];
-      if (s.wid == WID_NONE) continue;
+      if (s.wid == WID_NONE || (s.wid == WID_PLUS && i != 0)) continue;  // (a '+' copy: slot 0's edge)
       EdgeSlot c = s;
       c.meta &= ~META_BUCKET_OVF;
       ent.push_back({s.wid, c, fids[2 * p], fids[2 * p + 1], sid[2 * p], sid[2 * p + 1]});

@@ -636,8 +636,7 @@ bool build_tables(const FilterStore& fs, const BuildOpts& opts, HostTables& out,
       }();
       // (an array holding '+' copies loses a quarter of its slots to them, and one candidate
       // slot of every other bucket: twice the room keeps later inserts in place)
-      const uint64_t sl = slack;
-      caplog[v] = log2u(next_pow2(sl * e + sl));
+      caplog[v] = log2u(next_pow2(slack * e + slack));
       bool ok = false;
       for (uint32_t sd = 0; sd < CUCKOO_SEEDS && !ok; ++sd) {
         ok = bucket_place(v, sd, 1u << caplog[v], ck_key, ck_child);
