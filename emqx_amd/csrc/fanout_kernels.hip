@@ -278,20 +278,38 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
     const uint32_t total = static_cast<uint32_t>(a.eoff[e1] - obase);
     // the chunk's entries, EU per lane: every first-level load of the chunk is in flight
     // before the filter records are fetched, and those before anything is stored to LDS
+    // (loads are unconditional, from a clamped index, and masked after: under a per-lane
+    // `if` the compiler waited for each entry's loads before issuing the next entry's)
     uint32_t f[EU], tp[EU];
     uint64_t eo[EU];
+    bool v[EU];
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
       const uint64_t i = e0 + lane + 64u * u;
-      const bool v = i < e1;
-      f[u] = v ? a.mids[base + i] : FID_NONE;
-      eo[u] = v ? a.eoff[i] : obase + total;
-      tp[u] = (v && need_topic) ? a.entry_topic[i] : 0u;
+      v[u] = i < e1;
+      const uint64_t ic = v[u] ? i : e0;
+      f[u] = a.mids[base + ic];
+      eo[u] = a.eoff[ic];
+      tp[u] = need_topic ? a.entry_topic[ic] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      f[u] = v[u] ? f[u] : FID_NONE;
+      eo[u] = v[u] ? eo[u] : obase + total;
+      tp[u] = v[u] ? tp[u] : 0u;
     }
     uint4 r[EU];
+    if (a.n_recs) {
 #pragma unroll
-    for (uint32_t u = 0; u < EU; ++u)
-      r[u] = f[u] < a.n_recs ? *reinterpret_cast<const uint4*>(a.recs + f[u]) : make_uint4(0, 0, 0, 0);
+      for (uint32_t u = 0; u < EU; ++u) {
+        const bool in = f[u] < a.n_recs;
+        const uint4 x = *reinterpret_cast<const uint4*>(a.recs + (in ? f[u] : 0u));
+        r[u] = in ? x : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t u = 0; u < EU; ++u) r[u] = make_uint4(0, 0, 0, 0);
+    }
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
       const uint32_t k = lane + 64u * u;
