@@ -106,6 +106,7 @@ class RetainStats(ctypes.Structure):
         ("last_ranges", ctypes.c_uint64), ("last_visits", ctypes.c_uint64), ("last_total", ctypes.c_uint64),
         ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double), ("last_walk_ms", ctypes.c_double),
         ("last_spill_rounds", ctypes.c_uint64), ("last_spilled", ctypes.c_uint64),
+        ("last_spill_full", ctypes.c_uint64),
     ]
 
     def __init__(self, *a, **kw):

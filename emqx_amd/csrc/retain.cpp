@@ -110,7 +110,7 @@ struct RWork {
   uint32_t spill_cap = 0;
   uint64_t* partials = nullptr;
   uint64_t partials_cap = 0;
-  uint64_t* h_pinned = nullptr;  // [16] readbacks: ctrl words, then the id total
+  uint64_t* h_pinned = nullptr;  // [RC_WORDS / 2 + 1] readbacks: ctrl words, then the id total
   uint64_t* prof = nullptr;      // [8] RETAIN_PROF builds with EMQX_RETAIN_PROF=1
   // host-API staging (device copies of the caller's buffers)
   uint8_t* d_fb = nullptr;
@@ -153,8 +153,13 @@ constexpr uint32_t MAX_WAVES = 8192;
 // spills the rest as 64-node pieces, and the next round deals them evenly over up to
 // SPILL_WAVES waves.  The heavy filters' work is wide '+' slices (thousands of nodes per item):
 // config R's walk drops from 10.7 to 3.8 ms in 2 rounds (profiles/r1_v8_retain_sweep.txt).
-// emqx_retain_set_tuning "step_budget" overrides it (0 = no budget).
-constexpr uint32_t STEP_BUDGET = 128;
+// A round lasts as long as its busiest wave, so short budgets rebalance sooner: 32 steps for
+// the first round and 64 for the spill rounds run the config-R walk in 1.41-1.43 ms against
+// 1.95-1.96 ms for 128/128 (profiles/r3_retain_budget_sweep/; small budgets only paid once the
+// spill reservation stopped being a compare-and-swap loop, see spill_reserve).
+// emqx_retain_set_tuning "step_budget" / "spill_budget" override them (0 = no budget / the same).
+constexpr uint32_t STEP_BUDGET = 32;
+constexpr uint32_t SPILL_BUDGET = 64;
 constexpr uint32_t SPILL_WAVES = 4096;
 constexpr uint32_t SPILL_PER_WAVE = 4;  // spilled pieces dealt to each wave of a spill round
 constexpr uint32_t SPILL_CAP = 1u << 22;  // items per spill buffer (a full one: waves keep walking)
@@ -199,13 +204,13 @@ struct emqx_retain {
   std::mutex ws_mu;
   std::vector<RWork*> free_ws;
   std::vector<std::unique_ptr<RWork>> all_ws;
-  std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0}, last_spill_rounds{0}, last_spilled{0};
+  std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0}, last_spill_rounds{0}, last_spilled{0}, last_spill_full{0};
   std::atomic<double> last_match_ms{0}, last_walk_ms{0};
   // walk tuning (emqx_retain_set_tuning; the EMQX_RETAIN_* variables give the initial values)
   bool prof_on = false;
   uint32_t ablate = 0;  // EMQX_RETAIN_ABLATE (profiling builds only)  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
-  std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{128}, spill_per_wave{4}, spill_rounds{4}, search{RSEARCH_STREE},
-      walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES};
+  std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
+      walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP};
 };
 
 namespace {
@@ -519,7 +524,7 @@ int acquire(emqx_retain* r, RWork** out) {
   RT_TRY(hipEventCreate(&w->ev1));
   RT_TRY(hipEventCreate(&w->evw));
   RT_TRY(ralloc(w->ctrl, RC_WORDS));
-  RT_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_pinned), 16 * sizeof(uint64_t), hipHostMallocDefault));
+  RT_TRY(hipHostMalloc(reinterpret_cast<void**>(&w->h_pinned), (RC_WORDS / 2 + 1) * sizeof(uint64_t), hipHostMallocDefault));
   std::lock_guard<std::mutex> g(r->ws_mu);
   *out = w.get();
   r->all_ws.push_back(std::move(w));
@@ -583,11 +588,12 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     w->spill_cap = SPILL_CAP;
   }
   a.fnlev = w->fnlev;
-  a.spill_cap = w->spill_cap;
+  a.spill_cap = std::min<uint32_t>(w->spill_cap, r->spill_cap.load());
   const uint32_t budget = r->step_budget.load();
   a.step_budget = budget == 0 ? ~0u : budget;
   const uint32_t per_wave = std::max<uint32_t>(1, r->spill_per_wave.load());
   const uint32_t rounds = a.step_budget == ~0u ? 0u : r->spill_rounds.load();
+  const uint32_t spill_budget = r->spill_budget.load();
   const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
   for (int attempt = 0;; ++attempt) {
     const uint64_t stack_waves = static_cast<uint64_t>(w->stack_cap) <= (1u << 14) ? std::max(a.waves, spill_waves) : a.waves;
@@ -623,11 +629,11 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     for (uint32_t k = 0; k <= rounds; ++k) {
       RetainArgs b = a;
       b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(spill_waves, fit)));
-      const uint32_t in_word = (k & 1) ? RC_SPILL2 : RC_SPILL, out_word = (k & 1) ? RC_SPILL : RC_SPILL2;
-      b.spill_word = out_word;
+      const uint32_t in_word = RC_SPILL + k;
+      b.spill_word = in_word + 1;
       b.spill_out = w->spill[(k + 1) & 1];
       if (k == rounds) b.step_budget = ~0u;  // the last round finishes every stack
-      RT_TRY(hipMemsetAsync(w->ctrl + out_word, 0, sizeof(uint32_t), s));
+      else if (spill_budget) b.step_budget = spill_budget;
       RT_TRY(launch_retain_walk_spill(b, w->spill[k & 1], in_word, per_wave, s));
     }
     RT_TRY(hipEventRecord(w->evw, s));
@@ -657,6 +663,9 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       w->range_cap = static_cast<uint32_t>(rc);
       again = true;
     }
+    if (!again && r->prof_on)
+      std::fprintf(stderr, "RETAIN_CTRL spilled %u rounds %u spill_fail %u spill_max %u visits %u\n", c[RC_SPILLED],
+                   c[RC_ROUNDS], c[RC_SPILLFAIL], c[RC_SPILLMAX], c[RC_VISITS]);
     if (!again && r->prof_on) {
       uint64_t pr[8];
       if (hipMemcpy(pr, w->prof, sizeof(pr), hipMemcpyDeviceToHost) == hipSuccess) {
@@ -671,6 +680,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       r->last_visits.store(visits);
       r->last_spill_rounds.store(c[RC_ROUNDS]);
       r->last_spilled.store(c[RC_SPILLED]);
+      r->last_spill_full.store(c[RC_SPILLFAIL]);
       break;
     }
   }
@@ -697,8 +707,9 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   r->device = device;
   r->tile = std::max<uint32_t>(1, std::min<uint32_t>(64, env_u32("EMQX_RETAIN_TILE", TILE_FILTERS)));
   r->step_budget = env_u32("EMQX_RETAIN_STEP_BUDGET", STEP_BUDGET);
+  r->spill_budget = env_u32("EMQX_RETAIN_SPILL_BUDGET", SPILL_BUDGET);
   r->spill_per_wave = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_SPILL_PER_WAVE", SPILL_PER_WAVE));
-  r->spill_rounds = env_u32("EMQX_RETAIN_SPILL_ROUNDS", SPILL_ROUNDS);
+  r->spill_rounds = std::min<uint32_t>(RC_MAX_ROUNDS, env_u32("EMQX_RETAIN_SPILL_ROUNDS", SPILL_ROUNDS));
   r->search = std::min<uint32_t>(env_u32("EMQX_RETAIN_SEARCH", RSEARCH_STREE), RSEARCH_STREE);
   r->walk_waves = env_u32("EMQX_RETAIN_WALK_WAVES", MAX_WAVES);
   r->spill_waves = env_u32("EMQX_RETAIN_SPILL_WAVES", SPILL_WAVES);
@@ -919,11 +930,13 @@ int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
     r->tile = v;
   } else if (std::strcmp(key, "step_budget") == 0) {
     r->step_budget = v;  // 0 = no budget (no spill rounds)
+  } else if (std::strcmp(key, "spill_budget") == 0) {
+    r->spill_budget = v;  // 0 = the walk's step budget
   } else if (std::strcmp(key, "spill_per_wave") == 0) {
     if (v < 1) return EMQX_EINVAL;
     r->spill_per_wave = v;
   } else if (std::strcmp(key, "spill_rounds") == 0) {
-    if (v > 256) return EMQX_EINVAL;
+    if (v > RC_MAX_ROUNDS) return EMQX_EINVAL;
     r->spill_rounds = v;
   } else if (std::strcmp(key, "walk_waves") == 0) {
     if (v < 64 || v > (1u << 20)) return EMQX_EINVAL;
@@ -931,6 +944,9 @@ int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
   } else if (std::strcmp(key, "spill_waves") == 0) {
     if (v < 64 || v > (1u << 20)) return EMQX_EINVAL;
     r->spill_waves = v;
+  } else if (std::strcmp(key, "spill_cap") == 0) {
+    if (v < 64 || v > SPILL_CAP) return EMQX_EINVAL;
+    r->spill_cap = v;
   } else if (std::strcmp(key, "search") == 0) {
     if (v > RSEARCH_STREE) return EMQX_EINVAL;
     r->search = v;
@@ -964,6 +980,7 @@ int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* dst) {
   out->last_visits = r->last_visits.load();
   out->last_spill_rounds = r->last_spill_rounds.load();
   out->last_spilled = r->last_spilled.load();
+  out->last_spill_full = r->last_spill_full.load();
   out->last_total = r->last_total.load();
   out->last_match_ms = r->last_match_ms.load();
   out->last_walk_ms = r->last_walk_ms.load();

@@ -137,16 +137,19 @@ enum RCtrl : uint32_t {
   RC_RANGES = 0,   // small range record slots reserved (with RC_BIG may exceed range_cap: rerun)
   RC_VISITS = 1,   // node visits
   RC_STACK = 2,    // a wave's stack overflowed (rerun with a larger stack)
-  RC_SPILL = 3,    // items spilled by the walk / by even spill rounds (walked by the next round)
-  RC_SPILL2 = 4,   // ... by odd spill rounds
   RC_ROUNDS = 5,   // spill rounds that had work
   RC_SPILLED = 6,  // items those rounds took in
   RC_EMITTED = 7,  // range records written (RC_RANGES counts reserved slots: waves reserve
                    // RRES at a time, the unused ones stay zeroed = empty records)
   RC_BIG = 8,      // big range records, stored from the top of ranges[] down
   RC_TILE = 9,     // first-round tiles taken beyond the first a.waves
-  RC_WORDS = 16
+  RC_SPILLFAIL = 10,  // waves whose spill found no room (they finish their stacks themselves)
+  RC_SPILLMAX = 11,   // the most pieces one wave's spill asked for
+  RC_SPILL = 16,   // items spilled by the walk; RC_SPILL + 1 + k: by spill round k (each
+                   // round its own word, all zeroed with the rest at the call's start)
+  RC_WORDS = 64
 };
+constexpr uint32_t RC_MAX_ROUNDS = RC_WORDS - RC_SPILL - 2;  // budgeted spill rounds per call at most
 
 struct RetainArgs {
   RetainView rv;
@@ -166,7 +169,7 @@ struct RetainArgs {
   uint32_t step_budget;    // wave steps before the rest of a stack spills (~0u: no budget)
   uint4* spill_out;        // [spill_cap] items left when the budget ran out
   uint32_t spill_cap;
-  uint32_t spill_word;     // ctrl word counting the items this launch spills (RC_SPILL / RC_SPILL2)
+  uint32_t spill_word;     // ctrl word counting the items this launch spills (RC_SPILL + round)
   uint32_t* fnlev;         // [n] levels | wildcard flag << 31 of each filter (spill rounds)
   RRange* ranges;          // [range_cap]
   uint32_t range_cap;

@@ -215,16 +215,12 @@ constexpr uint32_t RCHUNK = 256;  // ranks per big range record (one unrolled wa
 // Reserve n slots of the spill buffer, all or nothing (a partial reservation would leave
 // unwritten items inside the counted prefix).  Called by one lane.
 __device__ __forceinline__ bool spill_reserve(uint32_t* ctr, uint32_t n, uint32_t cap, uint32_t* base) {
-  uint32_t old = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (;;) {
-    if (old > cap || n > cap - old) return false;
-    const uint32_t prev = atomicCAS(ctr, old, old + n);
-    if (prev == old) {
-      *base = old;
-      return true;
-    }
-    old = prev;
-  }
+  // one fetch-add, not a compare-and-swap loop: waves of a round reach their budget together,
+  // and 4096 of them retrying one CAS serialised a round for ~20 ms (budget 32).  A reservation
+  // past `cap` fails; its part below `cap` is padded with empty items by the caller
+  const uint32_t old = atomicAdd(ctr, n);
+  *base = old;
+  return old <= cap && n <= cap - old;
 }
 
 // The walk of one wave's stack until it is empty or the step budget runs out; then the
@@ -298,9 +294,15 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
       uint32_t ptot;
       (void)wave_excl(pieces, &ptot);
       uint32_t base = 0, ok = 0;
-      if (lane == 0) ok = spill_reserve(&a.ctrl[a.spill_word], ptot, a.spill_cap, &base) ? 1u : 0u;
+      if (lane == 0) {
+        ok = spill_reserve(&a.ctrl[a.spill_word], ptot, a.spill_cap, &base) ? 1u : 0u;
+        atomicMax(&a.ctrl[RC_SPILLMAX], ptot);
+        if (!ok) atomicAdd(&a.ctrl[RC_SPILLFAIL], 1u);
+      }
       ok = __shfl(ok, 0, 64);
       base = __shfl(base, 0, 64);
+      if (!ok)  // the reserved slots below the cap: empty items (no nodes), which the next round skips
+        for (uint32_t i = base + lane; i < a.spill_cap && i - base < ptot; i += 64) a.spill_out[i] = make_uint4(0, 0, 0, 0);
       if (ok) {
         for (uint32_t i0 = 0; i0 < all; i0 += 64) {
           const uint32_t i = i0 + lane;

@@ -104,7 +104,7 @@ class RetainIndex:
         check(_lib.lib().emqx_retain_commit(self._h), "emqx_retain_commit")
 
     def set_tuning(self, key: str, value: int) -> None:
-        """emqx_retain_set_tuning: "tile", "step_budget", "spill_per_wave", "spill_rounds"."""
+        """emqx_retain_set_tuning: "tile", "step_budget", "spill_budget", "spill_per_wave", "spill_rounds"."""
         check(_lib.lib().emqx_retain_set_tuning(self._h, key.encode(), int(value)), "emqx_retain_set_tuning")
 
     def stats(self) -> dict:

@@ -60,6 +60,7 @@ typedef struct emqx_retain_stats {
   double last_walk_ms;       /* ... of its walk (first round and spill rounds)              */
   uint64_t last_spill_rounds; /* walk rounds after the first (work left by waves over budget) */
   uint64_t last_spilled;     /* work items handed to those rounds                           */
+  uint64_t last_spill_full;  /* waves whose spill found the buffer full (walked on themselves)  */
 } emqx_retain_stats;
 
 int emqx_retain_create(int32_t device, emqx_retain** out);
@@ -105,11 +106,13 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes
 
 /* Walk tuning (experiments and tests; results never depend on it).  Keys: "tile" (filters
  * per wave tile of the first round, 1..64, default 10), "step_budget" (wave steps before a
- * stack spills to the next round, 0 = never, default 128), "spill_per_wave" (spilled pieces
+ * stack spills to the next round, 0 = never, default 32), "spill_budget" (the same for the
+ * budgeted spill rounds, 0 = step_budget, default 64), "spill_per_wave" (spilled pieces
  * per wave of a round, default 4), "spill_rounds" (budgeted rounds per call, then one without
- * a budget, default 4), "search" (0: two-level binary searches of the postings and rank lists,
+ * a budget, default 4, at most 46), "spill_cap" (spill-buffer items a round may use, 64..4M,
+ * default 4M; tests), "search" (0: two-level binary searches of the postings and rank lists,
  * 1: 16-ary search trees, default), "walk_waves" (persistent waves of the first round, default
- * 8192), "spill_waves" (waves of a spill round at most, default 4096).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
+ * 8192), "spill_waves" (waves of a spill round at most, default 4096).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
  * _SEARCH / _WALK_WAVES / _SPILL_WAVES give the initial values at create.  EMQX_ENOTFOUND for unknown keys. */
 int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value);
 int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out);

@@ -221,14 +221,46 @@ def test_spill_rounds_parity(mod, budget):
     st0 = idx.stats()
     assert st0["last_spill_rounds"] == 0
     idx.set_tuning("step_budget", budget)
-    for rounds in (0, 1, 6, 40):
+    for rounds, spill_budget in ((0, 0), (1, 0), (6, 3), (40, 1), (46, 0)):
         idx.set_tuning("spill_rounds", rounds)
+        idx.set_tuning("spill_budget", spill_budget)
         got = idx.match(filters, 100)
         st1 = idx.stats()
         assert 0 < st1["last_spill_rounds"] <= rounds + 1 and st1["last_spilled"] > 0
+        assert st1["last_spill_full"] == 0
         assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
         for f, g, r in zip(filters, got, ref):
             assert g == r == tt.dispatch(f, 100), f
+    with pytest.raises(Exception):
+        idx.set_tuning("spill_rounds", 47)
+
+
+def test_spill_buffer_full_parity(mod):
+    """A spill buffer too small for what the waves spill (emqx_retain_set_tuning "spill_cap"):
+    a wave whose reservation does not fit walks its stack on itself, and the part of its
+    reservation below the cap is padded with empty items the next round skips.  The result and
+    the visit and range counts stay the unbudgeted walk's."""
+    rng = random.Random(977)
+    idx = mod.RetainIndex()
+    names = sorted({rand_topic(rng) for _ in range(300)})
+    names += [b"v/%d/x" % i for i in range(4000)] + [b"v/%d/y/%d" % (i, i % 5) for i in range(0, 4000, 3)]
+    idx.store(names, [0] * len(names))
+    idx.commit()
+    filters = [rand_filter(rng) for _ in range(300)] + [b"#", b"+/+", b"v/+/x", b"+/+/y/+", b"v/#"] * 8
+    tt = RR.TokenTrie(names, [0] * len(names))
+    idx.set_tuning("step_budget", 0)
+    ref = idx.match(filters, 100)
+    st0 = idx.stats()
+    idx.set_tuning("step_budget", 1)
+    idx.set_tuning("spill_budget", 1)
+    idx.set_tuning("spill_rounds", 3)
+    idx.set_tuning("spill_cap", 64)
+    got = idx.match(filters, 100)
+    st1 = idx.stats()
+    assert st1["last_spill_full"] > 0 and st1["last_spill_rounds"] > 0
+    assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
+    for f, g, r in zip(filters, got, ref):
+        assert g == r == tt.dispatch(f, 100), f
 
 
 @pytest.mark.parametrize("tile", [1, 5, 64])
