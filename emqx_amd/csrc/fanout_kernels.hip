@@ -34,8 +34,14 @@ namespace emqx {
 namespace {
 
 constexpr int FO_THREADS = 256;
-constexpr uint32_t FO_UNROLL = 4;  // outputs per lane per round of the write kernel
-constexpr uint32_t FO_WCHUNK = 256;  // match entries per wave chunk of the write kernel
+#ifndef FO_UNROLL_V
+#define FO_UNROLL_V 4
+#endif
+#ifndef FO_WCHUNK_V
+#define FO_WCHUNK_V 256
+#endif
+constexpr uint32_t FO_UNROLL = FO_UNROLL_V;  // outputs per lane per round of the write kernel
+constexpr uint32_t FO_WCHUNK = FO_WCHUNK_V;  // match entries per wave chunk of the write kernel
 
 __device__ __forceinline__ uint32_t fo_lane() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -371,19 +377,12 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
           if (g.n_members > 1) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(FO_SUM_F_STATE_FULL));
         } else if (shr[u]) {
           sub[u] = gidx;
+          // a push onto the entry's chain: one exchange, no retry loop (many lanes of a hot
+          // group push at once); the chain is read only by the resolve kernel, a later launch
           const unsigned long long mine = (static_cast<unsigned long long>(a.stamp) << 32) | static_cast<uint32_t>(pos);
-          unsigned long long old = __hip_atomic_load(a.heads + ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          while (true) {
-            const bool fresh = static_cast<uint32_t>(old >> 32) != a.stamp;
-            a.next[pos] = fresh ? SUB_NONE : static_cast<uint32_t>(old);
-            __threadfence();
-            const unsigned long long seen = atomicCAS(a.heads + ent, old, mine);
-            if (seen == old) {
-              first = fresh;
-              break;
-            }
-            old = seen;
-          }
+          const unsigned long long old = atomicExch(a.heads + ent, mine);
+          first = static_cast<uint32_t>(old >> 32) != a.stamp;
+          a.next[pos] = first ? SUB_NONE : static_cast<uint32_t>(old);
         }
         wave_append(a.ctl + FO_CTL_TOUCHED, a.touched, first, static_cast<uint32_t>(ent));
       }
