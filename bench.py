@@ -1238,7 +1238,8 @@ def update_bench(args, rank, world, dev):
         "step_ms_first5": round(1e3 * float(np.mean(times[:5])), 3),
         "step_ms_last5": round(1e3 * float(np.mean(times[-5:])), 3),
         "per_commit": {k: round(float(np.mean([c[k] for c in cst])), 1)
-                       for k in ("relocations", "in_place", "patches", "new_slots", "host_us")},
+                       for k in ("relocations", "in_place", "patches", "new_slots", "host_us", "extents",
+                                 "vocab_slots", "upload_us")},
         "spare_used_at_end": cst[-1]["spare_used"], "spare_cap": cst[-1]["spare_cap"],
         "full_rebuild_ms": round(min(full_ms, rebuild_ms), 1),
         "filters_patched_in_since_build": delta_filters,

@@ -204,6 +204,8 @@ struct emqx_engine {
   uint64_t last_commit_kind = 0;
   uint64_t last_relocations = 0, last_in_place = 0, last_patches = 0, last_new_slots = 0;
   double last_host_ms = 0;      // host part (LiveTrie::commit) of the last incremental commit
+  uint64_t last_extents = 0, last_vocab_slots = 0;  // its new-slot extents and new vocab slots
+  double last_upload_ms = 0;    // from the end of the host part to the end of the uploads + patches
   std::mutex hb_mu;             // pinned host batches of emqx_match_batch (pool)
   std::vector<emqx_host_batch*> hb_free;
   int commit_threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
@@ -305,8 +307,7 @@ int live_commit(emqx_engine* e) {
   LiveTrie& lt = *d.lt;
   const FilterStore& fs = e->store;
   std::vector<uint32_t> ids(e->dirty);
-  std::sort(ids.begin(), ids.end());
-  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  sort_unique_u32(ids);
   uint64_t creates = 0;
   for (uint32_t id : ids)
     if (fs.live[id] && (id >= lt.loc.size() || lt.loc[id] == FIDLOC_NONE)) ++creates;
@@ -326,6 +327,9 @@ int live_commit(emqx_engine* e) {
   std::vector<uint32_t> vdirty;
   if (!d.vocab->insert_table(nw0, &vdirty) || d.vocab->arena.size() + 16 > d.dt->cap_arena) return EMQX_NEED_FULL;
   lt.patches(d.patches);
+  e->last_extents = lt.ranges.size();
+  e->last_vocab_slots = vdirty.size();
+  const auto tu0 = std::chrono::steady_clock::now();
 
   HIP_TRY(hipSetDevice(e->device));
   if (!d.stream) HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
@@ -353,6 +357,7 @@ int live_commit(emqx_engine* e) {
     HIP_TRY(launch_slot_patches(d.dt->edges, d.dt->fids, d.d_patch, static_cast<uint32_t>(np), st));
   }
   HIP_TRY(hipStreamSynchronize(st));
+  e->last_upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tu0).count();
 
   std::shared_ptr<Snapshot> cur;
   {
@@ -1326,9 +1331,10 @@ int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n) {
   std::lock_guard<std::mutex> g(e->writer);
   const LiveTrie* lt = e->ls.lt.get();
   uint64_t host_us = static_cast<uint64_t>(e->last_host_ms * 1e3);
-  const uint64_t v[9] = {e->last_commit_kind, e->last_relocations, e->last_in_place, e->last_patches,
-                         e->last_new_slots, lt ? lt->used : 0, lt ? lt->cap : 0, lt ? lt->garbage : 0, host_us};
-  for (uint32_t i = 0; i < n && i < 9; ++i) out[i] = v[i];
+  const uint64_t v[12] = {e->last_commit_kind, e->last_relocations, e->last_in_place, e->last_patches,
+                          e->last_new_slots, lt ? lt->used : 0, lt ? lt->cap : 0, lt ? lt->garbage : 0, host_us,
+                          e->last_extents, e->last_vocab_slots, static_cast<uint64_t>(e->last_upload_ms * 1e3)};
+  for (uint32_t i = 0; i < n && i < 12; ++i) out[i] = v[i];
   return EMQX_OK;
 }
 

@@ -795,10 +795,34 @@ uint64_t LiveTrie::new_slots() const {
   return n;
 }
 
+void sort_unique_u32(std::vector<uint32_t>& v) {
+  if (v.size() < 64) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    return;
+  }
+  uint32_t mx = 0;
+  for (uint32_t x : v) mx = std::max(mx, x);
+  std::vector<uint32_t> tmp(v.size());
+  std::vector<uint32_t> cnt(1u << 11);
+  for (uint32_t sh = 0; sh < 32 && (sh == 0 || (mx >> sh) != 0); sh += 11) {
+    std::fill(cnt.begin(), cnt.end(), 0u);
+    for (uint32_t x : v) ++cnt[(x >> sh) & 2047u];
+    uint32_t sum = 0;
+    for (uint32_t& c : cnt) {
+      const uint32_t t = c;
+      c = sum;
+      sum += t;
+    }
+    for (uint32_t x : v) tmp[cnt[(x >> sh) & 2047u]++] = x;
+    v.swap(tmp);
+  }
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+
 void LiveTrie::patches(std::vector<SlotPatch>& out) const {
   std::vector<uint32_t> d(dirty);
-  std::sort(d.begin(), d.end());
-  d.erase(std::unique(d.begin(), d.end()), d.end());
+  sort_unique_u32(d);
   out.clear();
   out.reserve(d.size());
   for (uint32_t p : d) out.push_back(SlotPatch{p, fids[2 * uint64_t(p)], fids[2 * uint64_t(p) + 1], 0, edges[p]});

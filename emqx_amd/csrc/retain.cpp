@@ -104,8 +104,9 @@ struct RWork {
   uint32_t* ctrl = nullptr;
   uint32_t* fcount = nullptr;
   uint32_t* fcursor = nullptr;
-  uint32_t* fnlev = nullptr;
   uint64_t f_cap = 0;
+  uint4* wdesc = nullptr;  // per-level step descriptors for the spill rounds
+  uint64_t wdesc_cap = 0;
   uint4* spill[2] = {nullptr, nullptr};  // spill rounds: items in / items out, alternating
   uint32_t spill_cap = 0;
   uint64_t* partials = nullptr;
@@ -131,7 +132,7 @@ struct RWork {
     rfree(ctrl);
     rfree(fcount);
     rfree(fcursor);
-    rfree(fnlev);
+    rfree(wdesc);
     rfree(spill[0]);
     rfree(spill[1]);
     rfree(partials);
@@ -555,10 +556,14 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     RT_TRY(ralloc(w->wids, need_w + need_w / 4));
     w->wids_cap = need_w + need_w / 4;
   }
+  const uint64_t need_d = byte_span + 2 * n + 1;
+  if (need_d > w->wdesc_cap) {
+    RT_TRY(ralloc(w->wdesc, need_d + need_d / 4));
+    w->wdesc_cap = need_d + need_d / 4;
+  }
   if (n > w->f_cap) {
     RT_TRY(ralloc(w->fcount, n + n / 4));
     RT_TRY(ralloc(w->fcursor, n + n / 4));
-    RT_TRY(ralloc(w->fnlev, n + n / 4));
     w->f_cap = n + n / 4;
   }
   const uint64_t np = scan_partials(n);
@@ -587,7 +592,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     RT_TRY(ralloc(w->spill[1], SPILL_CAP));
     w->spill_cap = SPILL_CAP;
   }
-  a.fnlev = w->fnlev;
+  a.wdesc = w->wdesc;
   a.spill_cap = std::min<uint32_t>(w->spill_cap, r->spill_cap.load());
   const uint32_t budget = r->step_budget.load();
   a.step_budget = budget == 0 ? ~0u : budget;

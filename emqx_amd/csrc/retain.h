@@ -170,7 +170,10 @@ struct RetainArgs {
   uint4* spill_out;        // [spill_cap] items left when the budget ran out
   uint32_t spill_cap;
   uint32_t spill_word;     // ctrl word counting the items this launch spills (RC_SPILL + round)
-  uint32_t* fnlev;         // [n] levels | wildcard flag << 31 of each filter (spill rounds)
+  uint4* wdesc;            // [foffs[n] - foffs[0] + 2n] per-level step descriptors of the spill
+                           // rounds, filter f's level l at foffs[f] - foffs[0] + 2f + l, levels
+                           // 0..nlev: {word, end of the '+' run from l, the word after it
+                           // (WID_HASH: none), nlev | wildcard flag << 31}
   RRange* ranges;          // [range_cap]
   uint32_t range_cap;
   uint32_t* ctrl;          // [RC_WORDS]

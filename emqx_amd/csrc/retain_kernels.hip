@@ -381,17 +381,25 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
         nl = nlevs[fl];
         wb = wbase[fl];
         fg = fbase + fl;
+        fn = nl & 0x7FFFFFFFu;
+        w_cur = lev < fn ? word_at(a, lwords, wb + lev) : WID_NONE;
+        if (w_cur == WID_PLUS) {  // the '+' run and the word after it
+          j = lev + 1;
+          while (j < fn && word_at(a, lwords, wb + j) == WID_PLUS) ++j;
+          wl = j < fn ? word_at(a, lwords, wb + j) : WID_HASH;
+        }
       } else {
+        // a spill round: the level's descriptor, written by the first round, holds the word,
+        // the '+' run's end and the word after it (one load, not a chain of word loads)
         fg = fl;
-        nl = a.fnlev[fg];
-        wb = (a.foffs[fg] - b0) + fg;
-      }
-      fn = nl & 0x7FFFFFFFu;
-      w_cur = lev < fn ? word_at(a, lwords, wb + lev) : WID_NONE;
-      if (w_cur == WID_PLUS) {  // the '+' run and the word after it
-        j = lev + 1;
-        while (j < fn && word_at(a, lwords, wb + j) == WID_PLUS) ++j;
-        wl = j < fn ? word_at(a, lwords, wb + j) : WID_HASH;
+        const uint4 d = a.wdesc[(a.foffs[fg] - b0) + 2 * fg + lev];
+        nl = d.w;
+        fn = nl & 0x7FFFFFFFu;
+        w_cur = d.x;
+        if (w_cur == WID_PLUS) {
+          j = d.y;
+          wl = d.z;
+        }
       }
       // A literal step needs only the edge bucket: a node without that child (a leaf
       // included) has no key for it there, so its own fields are not loaded (one random line
@@ -653,7 +661,21 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
           ws = i + 1;
         }
       }
-      a.fnlev[f] = nlev | (wild << 31);  // for the spill rounds
+      // the step descriptors of the spill rounds (RetainArgs.wdesc), last level first
+      {
+        uint4* dout = a.wdesc + (start - b0) + 2 * f;
+        const uint32_t nw = nlev | (wild << 31);
+        dout[nlev] = make_uint4(WID_NONE, 0u, WID_HASH, nw);
+        uint32_t jn = nlev, wn = WID_HASH;  // the first non-'+' level above l, its word
+        for (uint32_t l = nlev; l-- > 0;) {
+          const uint32_t wl = wout[l];
+          dout[l] = make_uint4(wl, jn, wn, nw);
+          if (wl != WID_PLUS) {
+            jn = l;
+            wn = wl;
+          }
+        }
+      }
     }
     nlevs[lane] = nlev | (wild << 31);
     // the tile's words into LDS when they fit (the walk reads one or two per node visit)

@@ -11,6 +11,10 @@
 
 namespace emqx {
 
+// Sorts v ascending and drops repeats: LSD radix passes of 11 bits over the bits the largest
+// value uses (commit paths: 20K filter ids, 10^5 dirty slots; std::sort took milliseconds).
+void sort_unique_u32(std::vector<uint32_t>& v);
+
 uint64_t hash64_bytes(const uint8_t* p, uint64_t n);
 
 // Open-addressed map from byte strings (kept in an external arena) to uint32 ids.

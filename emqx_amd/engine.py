@@ -111,12 +111,12 @@ class Engine:
         check(_lib.lib().emqx_commit(self._h), "emqx_commit")
 
     COMMIT_STATS = ("kind", "relocations", "in_place", "patches", "new_slots", "spare_used", "spare_cap",
-                    "garbage", "host_us")
+                    "garbage", "host_us", "extents", "vocab_slots", "upload_us")
 
     def commit_stats(self) -> dict:
         """Details of the last commit (emqx_commit_stats)."""
-        out = np.zeros(9, dtype=np.uint64)
-        check(_lib.lib().emqx_commit_stats(self._h, _ptr(out), 9), "emqx_commit_stats")
+        out = np.zeros(len(self.COMMIT_STATS), dtype=np.uint64)
+        check(_lib.lib().emqx_commit_stats(self._h, _ptr(out), len(out)), "emqx_commit_stats")
         return {k: int(out[i]) for i, k in enumerate(self.COMMIT_STATS)}
 
     def stats(self) -> dict:

@@ -123,10 +123,11 @@ int emqx_filter_name(emqx_engine* e, uint32_t id, uint8_t* buf, uint64_t cap, ui
  * spare region is used up (emqx_set_tuning "delta_max": at most that many filters placed
  * incrementally; "incremental" = 0 forces full rebuilds). */
 int emqx_commit(emqx_engine* e);
-/* Details of the last commit: out[0..8] = kind (0 full, 1 incremental), node relocations,
+/* Details of the last commit: out[0..11] = kind (0 full, 1 incremental), node relocations,
  * edges placed in place, slots rewritten in place, new slots, spare-region cursor, spare-region
  * capacity (slots), slots of superseded arrays, host microseconds of the last incremental
- * commit's table patching. */
+ * commit's table patching, its new-slot extents, its new vocab slots, microseconds of its
+ * uploads and device patches.  n < 12 returns the first n. */
 int emqx_commit_stats(emqx_engine* e, uint64_t* out, uint32_t n);
 
 /* Batched match, host buffers (any host memory).  out_offsets has n+1 entries.  On
