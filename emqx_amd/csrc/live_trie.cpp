@@ -27,6 +27,9 @@
 // serially, the rest run grouped by first-level node on up to `threads` threads, each
 // allocating from its own chunk of the spare region.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -651,6 +654,10 @@ bool LiveTrie::insert(Ctx& c, const FilterStore& fs, uint32_t id, const std::vec
 }
 
 bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, int threads) {
+  static const bool prof_phases = [] {
+    const char* e = std::getenv("EMQX_COMMIT_PROF");
+    return e && *e && *e != '0';
+  }();
   mark = used;
   dirty.clear();
   ranges.clear();
@@ -677,6 +684,7 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
     for (auto& x : th) x.join();
   };
 
+  const auto t0 = std::chrono::steady_clock::now();
   // 1. flips (the root's '#' filter serially)
   for (uint32_t id : fl)
     if (loc[id] == FIDLOC_ROOT_HASH) flip(cx[0], id, fs.live[id] != 0, false);
@@ -689,6 +697,7 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
     c.plus_heads.clear();
   }
 
+  const auto t1 = std::chrono::steady_clock::now();
   // 2. tokenize (read-only vocab lookups in parallel; unknown words interned serially)
   const uint64_t ni = ins.size();
   std::vector<uint64_t> woff(ni + 1, 0);
@@ -705,6 +714,7 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
       tokenize(fs, ins[k], wl[k], &wild, &fh, true);
     }
 
+  const auto t2 = std::chrono::steady_clock::now();
   // 3. inserts that change the root (a new first-level edge, or the filter '#'), serially
   Ctx& c0 = cx[0];
   if (c0.ranges.empty()) c0.cur = c0.end = 0;
@@ -716,6 +726,7 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
       done[k] = 1;
     }
   }
+  const auto t3 = std::chrono::steady_clock::now();
   // 4. the rest grouped by first-level node, groups dealt to threads (largest first)
   std::vector<std::pair<uint32_t, uint32_t>> key;  // (first-level slot, insert)
   key.reserve(ni);
@@ -748,6 +759,7 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
       load[k] += groups[g].second - groups[g].first;
     }
   }
+  const auto t4 = std::chrono::steady_clock::now();
   auto work = [&](int k) {
     Ctx& c = cx[k];
     for (uint32_t g : mine[k])
@@ -764,6 +776,7 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
     for (auto& x : th) x.join();
   }
 
+  const auto t5 = std::chrono::steady_clock::now();
   // 5. merge
   bool ok = true;
   for (Ctx& c : cx) {
@@ -786,6 +799,13 @@ bool LiveTrie::commit(const FilterStore& fs, const std::vector<uint32_t>& ids, i
     else merged.push_back(r);
   }
   ranges.swap(merged);
+  if (prof_phases) {
+    const auto t6 = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr, "COMMIT_PROF flips %.3f tokenize %.3f root %.3f group %.3f insert %.3f merge %.3f (fl %zu ins %llu)\n",
+                 ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5), ms(t5, t6), fl.size(),
+                 static_cast<unsigned long long>(ni));
+  }
   return ok;
 }
 
