@@ -156,6 +156,7 @@ struct LiveTrie {
     size_t chunk_range = 0;             // ranges[chunk_range] is the current chunk's extent
     std::vector<uint32_t> dirty;        // slots < mark rewritten in place (may repeat)
     uint64_t relocations = 0, in_place = 0, chains = 0, flips = 0, nodes = 0, garbage = 0;
+    uint64_t reloc_ns = 0, ph_ns = 0;   // EMQX_COMMIT_PROF: time in relocate / its seed search
     uint32_t max_depth = 0;
     bool failed = false;                // spare region exhausted
     std::vector<Entry> ent;
