@@ -71,7 +71,9 @@ WORKLOAD_NAMES = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 1000 for the batch-match workloads A / B / C1, so the timed "
+                         "region lasts ~0.1-1 s rather than ~10 ms; 20 for the others)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n-filters", type=int, default=10_000_000)
     ap.add_argument("--batch", type=int, default=None,
@@ -147,6 +149,8 @@ def main():
         args.streams = 3
     if args.cpu_sample is None:
         args.cpu_sample = {"D": 40_000}.get(args.workload, 1_000_000)
+    if args.steps is None:
+        args.steps = 1000 if args.workload in ("A", "B") and not args.sharded and not args.ab else 20
 
     import torch
     import torch.distributed as dist
