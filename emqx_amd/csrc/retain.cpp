@@ -210,7 +210,7 @@ struct emqx_retain {
   // walk tuning (emqx_retain_set_tuning; the EMQX_RETAIN_* variables give the initial values)
   bool prof_on = false;
   uint32_t ablate = 0;  // EMQX_RETAIN_ABLATE (profiling builds only)  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
-  std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
+  std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_decay{0}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
       walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP};
 };
 
@@ -599,6 +599,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   const uint32_t per_wave = std::max<uint32_t>(1, r->spill_per_wave.load());
   const uint32_t rounds = a.step_budget == ~0u ? 0u : r->spill_rounds.load();
   const uint32_t spill_budget = r->spill_budget.load();
+  const uint32_t spill_decay = r->spill_decay.load();  // round k's budget: spill_budget >> (k * decay), >= 8
   const uint32_t* c = reinterpret_cast<const uint32_t*>(w->h_pinned);
   for (int attempt = 0;; ++attempt) {
     const uint64_t stack_waves = static_cast<uint64_t>(w->stack_cap) <= (1u << 14) ? std::max(a.waves, spill_waves) : a.waves;
@@ -638,7 +639,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       b.spill_word = in_word + 1;
       b.spill_out = w->spill[(k + 1) & 1];
       if (k == rounds) b.step_budget = ~0u;  // the last round finishes every stack
-      else if (spill_budget) b.step_budget = spill_budget;
+      else if (spill_budget) b.step_budget = std::max<uint32_t>(8u, spill_budget >> std::min<uint32_t>(k * spill_decay, 31u));
       RT_TRY(launch_retain_walk_spill(b, w->spill[k & 1], in_word, per_wave, s));
     }
     RT_TRY(hipEventRecord(w->evw, s));
@@ -713,6 +714,7 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   r->tile = std::max<uint32_t>(1, std::min<uint32_t>(64, env_u32("EMQX_RETAIN_TILE", TILE_FILTERS)));
   r->step_budget = env_u32("EMQX_RETAIN_STEP_BUDGET", STEP_BUDGET);
   r->spill_budget = env_u32("EMQX_RETAIN_SPILL_BUDGET", SPILL_BUDGET);
+  r->spill_decay = std::min<uint32_t>(4, env_u32("EMQX_RETAIN_SPILL_DECAY", 0));
   r->spill_per_wave = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_SPILL_PER_WAVE", SPILL_PER_WAVE));
   r->spill_rounds = std::min<uint32_t>(RC_MAX_ROUNDS, env_u32("EMQX_RETAIN_SPILL_ROUNDS", SPILL_ROUNDS));
   r->search = std::min<uint32_t>(env_u32("EMQX_RETAIN_SEARCH", RSEARCH_STREE), RSEARCH_STREE);
