@@ -1357,7 +1357,7 @@ def retain_bench(args, rank, world, dev):
         "ranges_per_filter": round(ranges / nf, 3), "call_ms_median": round(cms, 4),
         "walk_ms_median": round(float(np.median(walk_ms)), 4),
         "walk_spill_rounds": int(st["last_spill_rounds"]), "walk_spilled_items": int(st["last_spilled"]),
-        "walk_step_budget": args.retain_budget if args.retain_budget is not None else "32, spill rounds 64 (default)",
+        "walk_step_budget": args.retain_budget if args.retain_budget is not None else "24, spill rounds 64 (default)",
         "walk_spill_full": int(st.get("last_spill_full", 0)),
         "walk_tile_filters": args.retain_tile if args.retain_tile is not None else 10,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

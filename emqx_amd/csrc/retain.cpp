@@ -154,12 +154,12 @@ constexpr uint32_t MAX_WAVES = 8192;
 // spills the rest as 64-node pieces, and the next round deals them evenly over up to
 // SPILL_WAVES waves.  The heavy filters' work is wide '+' slices (thousands of nodes per item):
 // config R's walk drops from 10.7 to 3.8 ms in 2 rounds (profiles/r1_v8_retain_sweep.txt).
-// A round lasts as long as its busiest wave, so short budgets rebalance sooner: 32 steps for
-// the first round and 64 for the spill rounds run the config-R walk in 1.41-1.43 ms against
-// 1.95-1.96 ms for 128/128 (profiles/r3_retain_budget_sweep/; small budgets only paid once the
+// A round lasts as long as its busiest wave, so short budgets rebalance sooner: 24 steps for
+// the first round and 64 for the spill rounds run the config-R walk in 1.38-1.41 ms against
+// 1.95-1.96 ms for 128/128 (32: 1.40-1.43 ms; profiles/r3_retain_budget_sweep/; small budgets only paid once the
 // spill reservation stopped being a compare-and-swap loop, see spill_reserve).
 // emqx_retain_set_tuning "step_budget" / "spill_budget" override them (0 = no budget / the same).
-constexpr uint32_t STEP_BUDGET = 32;
+constexpr uint32_t STEP_BUDGET = 24;
 constexpr uint32_t SPILL_BUDGET = 64;
 constexpr uint32_t SPILL_WAVES = 4096;
 constexpr uint32_t SPILL_PER_WAVE = 4;  // spilled pieces dealt to each wave of a spill round

@@ -106,7 +106,7 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes
 
 /* Walk tuning (experiments and tests; results never depend on it).  Keys: "tile" (filters
  * per wave tile of the first round, 1..64, default 10), "step_budget" (wave steps before a
- * stack spills to the next round, 0 = never, default 32), "spill_budget" (the same for the
+ * stack spills to the next round, 0 = never, default 24), "spill_budget" (the same for the
  * budgeted spill rounds, 0 = step_budget, default 64), "spill_per_wave" (spilled pieces
  * per wave of a round, default 4), "spill_rounds" (budgeted rounds per call, then one without
  * a budget, default 4, at most 46), "spill_cap" (spill-buffer items a round may use, 64..4M,
