@@ -117,7 +117,10 @@ def main():
                     help="--workload U: a 1M-topic match in flight on a second stream during every commit")
     ap.add_argument("--rounds", type=int, default=50, help="--workload U: commits timed")
     ap.add_argument("--strategy", type=str, default="hash_clientid",
-                    help="$share strategy for --workload E")
+                    help="$share strategy for --workload E / P")
+    ap.add_argument("--publishers", type=int, default=0,
+                    help="--workload E / P with round_robin / sticky: publishers the messages come from "
+                         "(message key = generated key mod N; 0: the generated keys, ~1M distinct)")
     ap.add_argument("--sharded", action="store_true",
                     help="filter-sharded table (filters by a hash of their first two levels, wildcard-keyed "
                          "ones replicated): rank 0's batch is partitioned by owner rank, exchanged with one "
@@ -648,6 +651,7 @@ def config_e_tables(args, rank, dev):
     t0 = time.time()
     with progress(f"[rank {rank}] generating config E"):
         fw = W.config_e(n_topics=args.batch)
+        publisher_keys(fw, args)
     eng = Engine(dev.index)
     with progress(f"[rank {rank}] building tables"):
         eng.insert_packed(*fw.wl.filters)
@@ -901,6 +905,13 @@ def match_roofline(n, kms, args, tbytes, levels, evals, nout, traffic, traffic_s
     return out
 
 
+def publisher_keys(fw, args):
+    """round_robin / sticky take the publisher as the message key: `--publishers N` folds the
+    generated keys onto N publishers (N = 1: one publisher sends the whole batch, a bridge)."""
+    if args.publishers and args.strategy in ("round_robin", "sticky"):
+        fw.keys = (fw.keys % np.uint32(args.publishers)).astype(np.uint32)
+
+
 def fanout_bench(args, rank, world, dev):
     """Config E: 10M subscriptions (1M subscribers x 10 filters over a 2M-filter config-B table,
     10% in $share groups of 2-16 members).  A step = match (emqx_match_batch_device) + fan-out
@@ -913,6 +924,7 @@ def fanout_bench(args, rank, world, dev):
     from emqx_amd.fanout import SubTable
     t0 = time.time()
     fw = W.config_e(n_topics=args.batch)
+    publisher_keys(fw, args)
     log(f"[rank {rank}] config E: {fw.wl.n_filters} filters, {fw.n_subscriptions} subscriptions ({time.time() - t0:.1f}s)")
     eng = Engine(dev.index)
     eng.insert_packed(*fw.wl.filters)
@@ -1006,7 +1018,8 @@ def fanout_bench(args, rank, world, dev):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": "E: end-to-end publish fan-out, match -> subscriber ids incl. $share, 10M subs",
                    "n_filters": fw.wl.n_filters, "subscriptions": fw.n_subscriptions, "batch_topics_per_gpu": n,
-                   "strategy": args.strategy, "parallelism": f"replicated tables, topic stream split x{world}"},
+                   "strategy": args.strategy, "publishers": args.publishers or "generated keys (~1M)",
+                   "parallelism": f"replicated tables, topic stream split x{world}"},
         "deliveries_per_s": round(nd * world * args.steps / elapsed, 1),
         "matches_per_topic": round(nm / n, 3), "deliveries_per_topic": round(nd / n, 3),
         "match_call_ms": round(float(np.median(kern)), 4), "fanout_call_ms": round(fo, 4),
@@ -1085,13 +1098,20 @@ def fanout_cpu_baseline(fw, args, gpu=None):
     res = {"value": round(sample / dt, 1), "unit": "topics/s", "cores": threads, "kind": "port",
            "sample": f"first {sample} topics; C++ DFS match + C++ route/dispatch with hash $share picks",
            "deliveries_per_topic": round(total / max(sample, 1), 3)}
-    if gpu is not None and args.strategy in ("hash_clientid", "hash_topic", "hash"):
+    if gpu is not None:
         off_g, subs_g, fils_g = gpu
         off_g = off_g[: sample + 1]
-        gsum = C.delivery_checksums(off_g, subs_g, fils_g)
-        bad = np.nonzero((np.diff(off_g.astype(np.int64)) != counts.astype(np.int64)) | (gsum != sums))[0]
+        cnt_bad = np.diff(off_g.astype(np.int64)) != counts.astype(np.int64)
+        if args.strategy in ("hash_clientid", "hash_topic", "hash"):
+            gsum = C.delivery_checksums(off_g, subs_g, fils_g)
+            bad = np.nonzero(cnt_bad | (gsum != sums))[0]
+            rule = "per-topic delivery count + order-free multiset checksum of (subscriber, filter)"
+        else:  # round_robin / sticky / random picks: exact parity is the GPU tests' (replayed draws)
+            bad = np.nonzero(cnt_bad)[0]
+            rule = ("per-topic delivery count (the picks of stateful / random strategies are checked pick by "
+                    "pick in tests/test_gpu_share_parity.py)")
         res["parity"] = {"topics_checked": int(sample), "deliveries_checked": int(total), "mismatches": int(bad.size),
-                         "rule": "per-topic delivery count + order-free multiset checksum of (subscriber, filter)"}
+                         "rule": rule}
         if bad.size:
             raise SystemExit(f"GPU fan-out differs from the oracle on {bad.size} topics, first {bad[:10].tolist()}")
     return res

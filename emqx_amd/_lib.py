@@ -38,7 +38,8 @@ EXPORTS = (
     "emqx_batcher_submit", "emqx_batcher_destroy", "emqx_batcher_stats", "emqx_batcher_stats_ext",
     "emqx_batcher_submit_many", "emqx_batcher_try_submit", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
-    "emqx_subtab_stats", "emqx_subtab_commit_stats", "emqx_subtab_forget_publishers",
+    "emqx_subtab_stats", "emqx_subtab_commit_stats", "emqx_subtab_forget_publishers", "emqx_subtab_set_alive",
+    "emqx_share_repick",
     "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
     "emqx_pub_batch_create", "emqx_pub_batch_destroy", "emqx_pub_batch_reserve", "emqx_pub_batch_submit",
     "emqx_pub_batch_wait", "emqx_pub_batch_query",
@@ -63,6 +64,8 @@ RETAIN_EXPORTS = (
 NO_GROUP = 0xFFFFFFFF
 SHARD_NONE = 0xFFFFFFFF
 FANOUT_SHARED_BIT = 0x80000000
+FANOUT_RETRY_BIT = 0x40000000
+PICK_NONE, PICK_FRESH, PICK_RETRY = 0, 1, 2
 SHARE_RANDOM, SHARE_ROUND_ROBIN, SHARE_STICKY, SHARE_HASH_CLIENTID, SHARE_HASH_TOPIC = 0, 1, 2, 3, 4
 
 
@@ -191,6 +194,8 @@ def lib():
         "emqx_subtab_stats": (i32, [vp, vp]),
         "emqx_subtab_commit_stats": (i32, [vp, vp, u32]),
         "emqx_subtab_forget_publishers": (i32, [vp, vp, u64]),
+        "emqx_subtab_set_alive": (i32, [vp, vp, u64, i32]),
+        "emqx_share_repick": (i32, [vp, u32, u64, vp, vp, vp, vp, vp, vp, vp]),
         "emqx_pub_batch_create": (i32, [vp, vp, u32, u64, u64, u64, ctypes.POINTER(ctypes.POINTER(PubBatchStruct))]),
         "emqx_pub_batch_destroy": (i32, [ctypes.POINTER(PubBatchStruct)]),
         "emqx_pub_batch_reserve": (i32, [ctypes.POINTER(PubBatchStruct), u64, u64, u64]),

@@ -206,13 +206,19 @@ struct FoScratch {
   uint64_t cap_eoff = 0;
   uint64_t* partials = nullptr;
   uint64_t cap_partials = 0;
-  uint32_t* next = nullptr;  // pick chains (round_robin / sticky), by output position
-  uint64_t cap_next = 0;
-  unsigned long long* heads = nullptr;  // per pick-state entry (sized to the table)
-  uint32_t* touched = nullptr;
-  uint64_t cap_heads = 0;
+  // round_robin / sticky: $share groups per chunk of entries, the pick list, its sorted copy and
+  // the sort's scratch, per state entry the run info of the resolve
+  uint32_t* gchunk = nullptr;
+  uint64_t cap_gchunk = 0;
+  uint32_t* pk = nullptr;       // 4 arrays of pk_cap: keys, vals, sorted keys, sorted vals
+  uint64_t pk_cap = 0;
+  uint8_t* sort_temp = nullptr;
+  uint64_t sort_temp_bytes = 0;
+  uint32_t sort_bits = 0;       // entry bits the sort scratch was sized for
+  unsigned long long* seg = nullptr;
+  uint32_t* seg_from = nullptr;
+  uint64_t cap_seg = 0;
   unsigned long long* ctl = nullptr;
-  uint32_t stamp = 0;
   uint64_t* h_sum = nullptr;  // host-mapped call summary (synchronous calls)
   hipEvent_t done = nullptr;  // end of the last fan-out enqueued on this stream
   bool used = false;
@@ -221,9 +227,11 @@ struct FoScratch {
     fo_free(ecount);
     fo_free(eoff);
     fo_free(partials);
-    fo_free(next);
-    fo_free(heads);
-    fo_free(touched);
+    fo_free(gchunk);
+    fo_free(pk);
+    fo_free(sort_temp);
+    fo_free(seg);
+    fo_free(seg_from);
     fo_free(ctl);
     fo_hfree(h_sum);
     if (done) (void)hipEventDestroy(done);
@@ -253,6 +261,8 @@ struct emqx_subtab {
   std::vector<std::pair<uint64_t, uint64_t>> dirty_plain;  // (first word, words)
   std::vector<uint32_t> dirty_recs, dirty_slots, dirty_glists;
   std::vector<uint8_t> rec_flag, glist_flag;  // per filter: listed in dirty_recs / dirty_glists
+  std::vector<uint32_t> alive;                // liveness bitmap image (bit per subscriber id)
+  std::vector<uint32_t> dirty_alive;          // words of it changed since the last commit
   bool need_full = true;
   uint64_t ops_pending = 0;                   // mutations since the last commit
   bool bulk = false;                          // so many that the next commit rebuilds: no dirt kept
@@ -260,10 +270,13 @@ struct emqx_subtab {
   DevArr<FilterRec> d_recs;
   DevArr<uint32_t> d_plain, d_members;
   DevArr<GroupRec> d_groups;
-  uint32_t dev_n_recs = 0;
+  DevArr<uint32_t> d_alive;
+  uint32_t dev_n_recs = 0, dev_n_alive = 0;
   hipStream_t stream = nullptr;       // commits and table maintenance
   hipEvent_t commit_ev = nullptr;     // end of the last commit: later fan-outs wait for it
   bool commit_pending = false;
+  hipEvent_t state_ev = nullptr;      // end of the last round_robin / sticky resolve (or re-pick):
+  bool state_pending = false;         // the next one waits for it, so state updates follow call order
   std::vector<WordPatch> wpatch;
   std::vector<RecPatch> rpatch;
   DevArr<WordPatch> d_wpatch;
@@ -272,8 +285,16 @@ struct emqx_subtab {
   uint64_t* ps_keys = nullptr;
   uint32_t* ps_vals = nullptr;
   unsigned long long* ps_count = nullptr;
+  unsigned long long* ps_tombs = nullptr;
   uint64_t ps_cap = 0;
-  unsigned long long* h_ps_seen = nullptr;  // host-mapped: occupancy after the last finished call
+  bool ps_force_grow = false;               // a call found no room for a key: grow before the next
+  unsigned long long* h_ps_seen = nullptr;  // host-mapped [3]: live keys, tombstones, picks of the
+                                            // last finished call
+  std::vector<uint32_t> pending_forget;     // publishers to drop (emqx_subtab_forget_publishers)
+  DevArr<uint32_t> d_forget;                // the last flushed list, from pinned staging h_forget
+  uint32_t* h_forget = nullptr;
+  hipEvent_t forget_ev = nullptr;           // end of the last flush's pass
+  bool forget_pending = false;
   std::vector<std::unique_ptr<FoScratch>> scratch;  // one per stream that called
   uint64_t* h_total = nullptr;
   uint32_t seed = 0x2545F491u;
@@ -292,8 +313,22 @@ namespace {
 bool ids_ok(const uint32_t* f, const uint32_t* s, uint64_t n) {
   if (n && (!f || !s)) return false;
   for (uint64_t i = 0; i < n; ++i)
-    if (f[i] & FANOUT_SHARED_BIT || s[i] == SUB_NONE) return false;
+    if (f[i] >= FANOUT_ID_LIMIT || s[i] == SUB_NONE) return false;
   return true;
+}
+
+// Sets subscriber `sub`'s liveness bit in the image (dirty words go out with the next commit).
+void set_alive_bit(emqx_subtab* s, uint32_t sub, bool on) {
+  const uint64_t w = sub >> 5;
+  if (w >= s->alive.size()) {
+    if (!on) return;
+    s->alive.resize(std::max<uint64_t>(w + 1, s->alive.size() + s->alive.size() / 2), 0u);
+  }
+  const uint32_t bit = 1u << (sub & 31u), old = s->alive[w];
+  const uint32_t nv = on ? old | bit : old & ~bit;
+  if (nv == old) return;
+  s->alive[w] = nv;
+  s->dirty_alive.push_back(static_cast<uint32_t>(w));
 }
 
 void ensure_filter(emqx_subtab* s, uint32_t f) {
@@ -477,27 +512,34 @@ int full_commit(emqx_subtab* s) {
     if (!v.empty()) FO_TRY(hipMemcpyAsync(d.p, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice, s->stream));
     return EMQX_OK;
   };
+  DevArr<uint32_t> alive;
   int rc = up(recs, s->recs);
   if (rc == EMQX_OK) rc = up(plain, s->plain);
   if (rc == EMQX_OK) rc = up(groups, s->groups);
   if (rc == EMQX_OK) rc = up(members, s->members);
+  if (rc == EMQX_OK) rc = up(alive, s->alive);
   if (rc == EMQX_OK && hipStreamSynchronize(s->stream) != hipSuccess) rc = EMQX_EDEVICE;
   if (rc != EMQX_OK) {
     fo_free(recs.p);
     fo_free(plain.p);
     fo_free(groups.p);
     fo_free(members.p);
+    fo_free(alive.p);
     return rc;
   }
   fo_free(s->d_recs.p);
   fo_free(s->d_plain.p);
   fo_free(s->d_groups.p);
   fo_free(s->d_members.p);
+  fo_free(s->d_alive.p);
   s->d_recs = recs;
   s->d_plain = plain;
   s->d_groups = groups;
   s->d_members = members;
+  s->d_alive = alive;
   s->dev_n_recs = static_cast<uint32_t>(s->recs.size());
+  s->dev_n_alive = static_cast<uint32_t>(s->alive.size());
+  s->dirty_alive.clear();
   s->st_words += s->plain.size() + s->members.size();
   s->st_records += s->recs.size() + s->groups.size();
   s->need_full = false;
@@ -583,6 +625,10 @@ int live_commit(emqx_subtab* s) {
   const uint64_t n_plain_w = s->wpatch.size();
   words(member_ranges, s->members, copies_members);
   const uint64_t n_member_w = s->wpatch.size() - n_plain_w;
+  std::sort(s->dirty_alive.begin(), s->dirty_alive.end());
+  s->dirty_alive.erase(std::unique(s->dirty_alive.begin(), s->dirty_alive.end()), s->dirty_alive.end());
+  for (uint32_t w : s->dirty_alive) s->wpatch.push_back(WordPatch{w, 0u, s->alive[w], 0});
+  const uint64_t n_alive_w = s->dirty_alive.size();
   std::sort(group_idx.begin(), group_idx.end());
   group_idx.erase(std::unique(group_idx.begin(), group_idx.end()), group_idx.end());
   for (uint64_t gi : group_idx) {
@@ -607,6 +653,7 @@ int live_commit(emqx_subtab* s) {
   if (rc == EMQX_OK) rc = dev_reserve(s, s->d_plain, s->plain.size(), s->d_plain.cap, ru);
   if (rc == EMQX_OK) rc = dev_reserve(s, s->d_members, s->members.size(), s->d_members.cap, ru);
   if (rc == EMQX_OK) rc = dev_reserve(s, s->d_groups, s->groups.size(), s->d_groups.cap, rg);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_alive, s->alive.size(), s->dev_n_alive, ru);
   if (rc == EMQX_OK) {
     for (const auto& c : copies_plain)
       if (hipMemcpyAsync(s->d_plain.p + c.first, s->plain.data() + c.first, c.second * 4, hipMemcpyHostToDevice,
@@ -630,8 +677,9 @@ int live_commit(emqx_subtab* s) {
       rc = EMQX_EDEVICE;
   }
   if (rc == EMQX_OK &&
-      launch_subtab_patches(s->d_plain.p, s->d_members.p, s->d_wpatch.p, n_plain_w, n_member_w, s->d_groups.p,
-                            s->d_recs.p, s->d_rpatch.p, n_group_p, n_rec_p, s->stream) != hipSuccess)
+      launch_subtab_patches(s->d_plain.p, s->d_members.p, s->d_alive.p, s->d_wpatch.p, n_plain_w, n_member_w,
+                            n_alive_w, s->d_groups.p, s->d_recs.p, s->d_rpatch.p, n_group_p, n_rec_p,
+                            s->stream) != hipSuccess)
     rc = EMQX_EDEVICE;
   if (hipStreamSynchronize(s->stream) != hipSuccess && rc == EMQX_OK) rc = EMQX_EDEVICE;
   for (auto* p : rr) (void)hipFree(p);
@@ -642,6 +690,8 @@ int live_commit(emqx_subtab* s) {
     return rc;
   }
   s->dev_n_recs = static_cast<uint32_t>(s->recs.size());
+  s->dev_n_alive = static_cast<uint32_t>(s->alive.size());
+  s->dirty_alive.clear();
   s->dirty_plain.clear();
   s->dirty_recs.clear();
   s->dirty_slots.clear();
@@ -649,7 +699,7 @@ int live_commit(emqx_subtab* s) {
   uint64_t cw = 0;
   for (const auto& c : copies_plain) cw += c.second;
   for (const auto& c : copies_members) cw += c.second;
-  s->st_words += n_plain_w + n_member_w + cw;
+  s->st_words += n_plain_w + n_member_w + n_alive_w + cw;
   s->st_records += n_group_p + n_rec_p;
   s->st_host_us = std::chrono::duration<double, std::micro>(t1 - t0).count();
   s->st_last_kind = 1;
@@ -694,27 +744,35 @@ int ps_alloc(uint64_t cap, uint64_t*& keys, uint32_t*& vals, hipStream_t st) {
   return EMQX_OK;
 }
 
-// The table exists and is at most half full (as of the last finished call); growing it waits
-// for the fan-outs in flight.  Per-stream chain heads follow the table's size.
-int ps_ready(emqx_subtab* s) {
+// The table exists and will stay at most half full (live keys and tombstones as of the last
+// finished call, plus `incoming` new keys) — otherwise it is rehashed, dropping the tombstones,
+// into a table of at least four times the live keys; that waits for the fan-outs in flight.
+int ps_ready(emqx_subtab* s, uint64_t incoming) {
   if (!s->ps_keys) {
-    if (!s->ps_count) FO_TRY(fo_alloc(s->ps_count, 1));
+    uint64_t cap = PS_INIT_CAP;
+    while (cap < 4 * incoming) cap <<= 1;
     FO_TRY(hipMemsetAsync(s->ps_count, 0, sizeof(unsigned long long), s->stream));
-    int rc = ps_alloc(PS_INIT_CAP, s->ps_keys, s->ps_vals, s->stream);
+    FO_TRY(hipMemsetAsync(s->ps_tombs, 0, sizeof(unsigned long long), s->stream));
+    int rc = ps_alloc(cap, s->ps_keys, s->ps_vals, s->stream);
     if (rc != EMQX_OK) return rc;
     FO_TRY(hipStreamSynchronize(s->stream));
-    s->ps_cap = PS_INIT_CAP;
+    s->ps_cap = cap;
     return EMQX_OK;
   }
-  if (*s->h_ps_seen * 2 <= s->ps_cap) return EMQX_OK;
+  const uint64_t live = s->h_ps_seen[0], tombs = s->h_ps_seen[1];
+  if (!s->ps_force_grow && (live + tombs + incoming) * 2 <= s->ps_cap) return EMQX_OK;
   int rc = barrier_after_fanouts(s);
   if (rc != EMQX_OK) return rc;
-  const uint64_t cap = s->ps_cap * 4;
+  if (s->state_pending) FO_TRY(hipStreamWaitEvent(s->stream, s->state_ev, 0));
+  uint64_t cap = PS_INIT_CAP;
+  while (cap < 4 * (live + incoming)) cap <<= 1;
+  if (s->ps_force_grow) cap = std::max(cap, 2 * s->ps_cap);
   uint64_t* keys;
   uint32_t* vals;
   rc = ps_alloc(cap, keys, vals, s->stream);
   if (rc != EMQX_OK) return rc;
   FO_TRY(hipMemsetAsync(s->ps_count, 0, sizeof(unsigned long long), s->stream));
+  FO_TRY(hipMemsetAsync(s->ps_tombs, 0, sizeof(unsigned long long), s->stream));
   FO_TRY(launch_ps_rehash(s->ps_keys, s->ps_vals, s->ps_cap, keys, vals, cap - 1, s->ps_count, s->stream));
   FO_TRY(hipStreamSynchronize(s->stream));
   fo_free(s->ps_keys);
@@ -722,7 +780,34 @@ int ps_ready(emqx_subtab* s) {
   s->ps_keys = keys;
   s->ps_vals = vals;
   s->ps_cap = cap;
+  s->ps_force_grow = false;
   FO_TRY(hipMemcpy(s->h_ps_seen, s->ps_count, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  s->h_ps_seen[1] = 0;
+  return EMQX_OK;
+}
+
+// Applies the queued forget_publishers calls on stream st (before a stateful call's write
+// kernel inserts keys of those publishers' possible successors): one pass over the table.
+int flush_forgets(emqx_subtab* s, hipStream_t st) {
+  if (s->pending_forget.empty() || !s->ps_keys) {
+    s->pending_forget.clear();
+    return EMQX_OK;
+  }
+  std::vector<uint32_t>& p = s->pending_forget;
+  std::sort(p.begin(), p.end());
+  p.erase(std::unique(p.begin(), p.end()), p.end());
+  // the previous pass has read its list (pinned staging and device copy) before they are reused
+  if (s->forget_pending) FO_TRY(hipEventSynchronize(s->forget_ev));
+  if (s->d_forget.cap < p.size()) {
+    FO_TRY(fo_ensure(s->d_forget.p, s->d_forget.cap, p.size()));
+    FO_TRY(fo_halloc(s->h_forget, s->d_forget.cap));
+  }
+  std::memcpy(s->h_forget, p.data(), p.size() * 4);
+  FO_TRY(hipMemcpyAsync(s->d_forget.p, s->h_forget, p.size() * 4, hipMemcpyHostToDevice, st));
+  FO_TRY(launch_ps_forget(s->ps_keys, s->ps_cap, s->d_forget.p, p.size(), s->ps_count, s->ps_tombs, st));
+  FO_TRY(hipEventRecord(s->forget_ev, st));
+  s->forget_pending = true;
+  p.clear();
   return EMQX_OK;
 }
 
@@ -738,10 +823,48 @@ FoScratch* scratch_for(emqx_subtab* s, hipStream_t st) {
   return s->scratch.back().get();
 }
 
+// Bits of a state-entry index (the pick list's sort key).
+uint32_t ent_bits(uint64_t ps_cap) {
+  uint32_t b = 1;
+  while ((1ull << b) < ps_cap) ++b;
+  return b;
+}
+
+// Sizes the stateful scratch of c for m_cap entries and the learnt number of picks.
+int stateful_scratch(emqx_subtab* s, FoScratch* c, uint64_t m_cap, uint64_t cap) {
+  FO_TRY(fo_ensure(c->gchunk, c->cap_gchunk, m_cap / FO_WCHUNK + 2));
+  // the pick list: the last finished call's picks with a margin (a call with more is flagged,
+  // writes nothing and is rerun after this grows); never more than the delivery capacity
+  const uint64_t seen = s->h_ps_seen[2];
+  uint64_t want = std::max<uint64_t>(c->pk_cap, std::max<uint64_t>(1u << 16, seen + seen / 2 + 4096));
+  want = std::min<uint64_t>(want, std::max<uint64_t>(cap, 1u << 16));
+  const uint32_t bits = ent_bits(s->ps_cap);
+  if (want > c->pk_cap || !c->pk) {
+    FO_TRY(fo_alloc(c->pk, 4 * want));
+    c->pk_cap = want;
+    c->sort_bits = 0;
+  }
+  if (c->sort_bits != bits) {
+    const uint64_t tb = fanout_sort_temp_bytes(c->pk_cap, bits);
+    if (tb > c->sort_temp_bytes || !c->sort_temp) {
+      FO_TRY(fo_alloc(c->sort_temp, tb));
+      c->sort_temp_bytes = tb;
+    }
+    c->sort_bits = bits;
+  }
+  if (c->cap_seg != s->ps_cap) {  // (a new table: the stream's earlier calls have drained)
+    FO_TRY(fo_alloc(c->seg, s->ps_cap));
+    FO_TRY(fo_alloc(c->seg_from, s->ps_cap));
+    c->cap_seg = s->ps_cap;
+  }
+  return EMQX_OK;
+}
+
 // Enqueue the fan-out of one match CSR on st, no host synchronisation (s->mu held); m_cap
 // bounds the match entries (sizes the scratch; a longer CSR is refused on the device, as is
 // one whose match summary `msum` reports a problem); the summary goes to `summary`
-// (FO_SUM_WORDS u64).
+// (FO_SUM_WORDS u64).  round_robin / sticky: the resolve waits for the table's previous one, so
+// the per-publisher state advances call after call in the order the calls were enqueued.
 int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const uint32_t* d_mids, uint64_t n,
                    uint64_t m_cap, const uint32_t* d_keys, uint64_t* d_out_off, uint32_t* d_out_subs,
                    uint32_t* d_out_fil, uint64_t cap, uint64_t* summary, hipStream_t st, const uint64_t* msum) {
@@ -749,25 +872,19 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   if (!c) return EMQX_EDEVICE;
   const bool stateful = fo_stateful(strategy);
   if (!d_out_subs) cap = 0;
-  if (stateful && cap >= (1ull << 32)) return EMQX_EINVAL;  // chain links are 32-bit positions
+  if (stateful && cap >= (1ull << 32)) return EMQX_EINVAL;  // pick positions are 32-bit
   if (stateful) {
-    int rc = ps_ready(s);
+    const uint64_t pk_guess = std::max<uint64_t>(c->pk_cap, std::max<uint64_t>(1u << 16, s->h_ps_seen[2] * 2));
+    int rc = ps_ready(s, std::min<uint64_t>(pk_guess, std::max<uint64_t>(cap, 1u << 16)));
+    if (rc == EMQX_OK) rc = stateful_scratch(s, c, m_cap, cap);
+    if (rc == EMQX_OK) rc = flush_forgets(s, st);
     if (rc != EMQX_OK) return rc;
-    if (c->cap_heads != s->ps_cap) {  // (a new table: the stream's earlier calls have drained)
-      FO_TRY(fo_alloc(c->heads, s->ps_cap));
-      FO_TRY(fo_alloc(c->touched, s->ps_cap));
-      FO_TRY(hipMemsetAsync(c->heads, 0, s->ps_cap * sizeof(unsigned long long), st));
-      c->cap_heads = s->ps_cap;
-    }
-    FO_TRY(fo_ensure(c->next, c->cap_next, cap));
-    if (++c->stamp == 0) c->stamp = 1;
   }
   if (d_keys && strategy != EMQX_SHARE_RANDOM) FO_TRY(fo_ensure(c->entry_topic, c->cap_entry_topic, m_cap));
   FO_TRY(fo_ensure(c->ecount, c->cap_ecount, m_cap));
   FO_TRY(fo_ensure(c->eoff, c->cap_eoff, m_cap + 1));
-  FO_TRY(fo_ensure(c->partials, c->cap_partials, 2 * FO_BLOCKS));
+  FO_TRY(fo_ensure(c->partials, c->cap_partials, 4 * FO_BLOCKS));
   if (!c->ctl) FO_TRY(fo_alloc(c->ctl, FO_CTL_WORDS));
-  if (!s->ps_count) FO_TRY(fo_alloc(s->ps_count, 1));
   if (s->commit_pending) FO_TRY(hipStreamWaitEvent(st, s->commit_ev, 0));
   FO_TRY(hipMemsetAsync(c->ctl, 0, FO_CTL_WORDS * sizeof(unsigned long long), st));
   FanoutArgs a{};
@@ -776,14 +893,23 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   a.plain = s->d_plain.p;
   a.groups = s->d_groups.p;
   a.members = s->d_members.p;
+  a.alive = s->d_alive.p;
+  a.n_alive_words = s->dev_n_alive;
   a.ps_keys = s->ps_keys;
   a.ps_vals = s->ps_vals;
   a.ps_count = s->ps_count;
+  a.ps_tombs = s->ps_tombs;
   a.ps_mask = s->ps_cap ? s->ps_cap - 1 : 0;
-  a.heads = c->heads;
-  a.stamp = c->stamp;
-  a.next = c->next;
-  a.touched = c->touched;
+  if (stateful) {
+    a.gchunk = c->gchunk;
+    a.pk_keys = c->pk;
+    a.pk_vals = c->pk + c->pk_cap;
+    a.pk_skeys = c->pk + 2 * c->pk_cap;
+    a.pk_svals = c->pk + 3 * c->pk_cap;
+    a.pk_cap = c->pk_cap;
+    a.seg = c->seg;
+    a.seg_from = c->seg_from;
+  }
   a.ctl = c->ctl;
   a.ps_seen = mapped(s->h_ps_seen);
   a.moff = d_moff;
@@ -805,38 +931,60 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   a.cap = cap;
   a.summary = summary;
   FO_TRY(launch_fanout(a, m_cap, st));
+  if (stateful) {
+    if (s->state_pending) FO_TRY(hipStreamWaitEvent(st, s->state_ev, 0));
+    FO_TRY(launch_fanout_resolve(a, c->sort_temp, c->sort_temp_bytes, c->sort_bits, st));
+    FO_TRY(hipEventRecord(s->state_ev, st));
+    s->state_pending = true;
+  }
   FO_TRY(hipEventRecord(c->done, st));
   c->used = true;
   return EMQX_OK;
 }
 
+// After a call flagged FO_SUM_F_RERUN: what to grow before it runs again.
+void note_rerun(emqx_subtab* s, uint64_t flags) {
+  if (flags & FO_SUM_F_STATE_FULL) s->ps_force_grow = true;
+  // FO_SUM_F_PICKS: the finish kernel reported the call's picks in h_ps_seen[2]
+}
+
 // Synchronous form: enqueue, drain, read the summary.  On overflow the write kernel wrote
-// nothing (and consumed no pick state); *n_out is the capacity required.
+// nothing (and consumed no pick state); *n_out is the capacity required.  A call flagged for a
+// rerun (state table or pick scratch too small: nothing consumed) grows them and runs again.
 int run_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const uint32_t* d_mids, uint64_t n,
                uint64_t m, const uint32_t* d_keys, uint64_t* d_out_off, uint32_t* d_out_subs, uint32_t* d_out_fil,
                uint64_t cap, uint64_t* n_out, hipStream_t st) {
   FoScratch* c = scratch_for(s, st);
   if (!c) return EMQX_EDEVICE;
   if (!c->h_sum) FO_TRY(fo_halloc(c->h_sum, FO_SUM_WORDS));
-  int rc = enqueue_fanout(s, strategy, d_moff, d_mids, n, m, d_keys, d_out_off, d_out_subs, d_out_fil, cap,
-                          mapped(c->h_sum), st, nullptr);
-  if (rc != EMQX_OK) return rc;
-  FO_TRY(hipStreamSynchronize(st));
-  *n_out = c->h_sum[FO_SUM_TOTAL];
-  if (c->h_sum[FO_SUM_FLAGS] & FO_SUM_F_MATCH) return EMQX_EINVAL;
-  if (c->h_sum[FO_SUM_FLAGS] & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
-  return EMQX_OK;
+  for (int attempt = 0;; ++attempt) {
+    int rc = enqueue_fanout(s, strategy, d_moff, d_mids, n, m, d_keys, d_out_off, d_out_subs, d_out_fil, cap,
+                            mapped(c->h_sum), st, nullptr);
+    if (rc != EMQX_OK) return rc;
+    FO_TRY(hipStreamSynchronize(st));
+    *n_out = c->h_sum[FO_SUM_TOTAL];
+    const uint64_t fl = c->h_sum[FO_SUM_FLAGS];
+    if (fl & FO_SUM_F_MATCH) return EMQX_EINVAL;
+    if (fl & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
+    if (!(fl & FO_SUM_F_RERUN)) return EMQX_OK;
+    if (attempt >= 3) return EMQX_ENOMEM;
+    note_rerun(s, fl);
+  }
 }
 
 int ensure_stream(emqx_subtab* s) {
   if (!s->stream) {
     FO_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     FO_TRY(hipEventCreateWithFlags(&s->commit_ev, hipEventDisableTiming));
+    FO_TRY(hipEventCreateWithFlags(&s->state_ev, hipEventDisableTiming));
+    FO_TRY(hipEventCreateWithFlags(&s->forget_ev, hipEventDisableTiming));
     FO_TRY(fo_halloc(s->h_total, 2));
-    FO_TRY(fo_halloc(s->h_ps_seen, 1));
-    *s->h_ps_seen = 0;
+    FO_TRY(fo_halloc(s->h_ps_seen, 3));
+    s->h_ps_seen[0] = s->h_ps_seen[1] = s->h_ps_seen[2] = 0;
     FO_TRY(fo_alloc(s->ps_count, 1));  // (read by every call's finish kernel)
+    FO_TRY(fo_alloc(s->ps_tombs, 1));
     FO_TRY(hipMemset(s->ps_count, 0, sizeof(unsigned long long)));
+    FO_TRY(hipMemset(s->ps_tombs, 0, sizeof(unsigned long long)));
   }
   return EMQX_OK;
 }
@@ -887,13 +1035,19 @@ emqx_subtab::~emqx_subtab() {
   fo_free(d_members.p);
   fo_free(d_wpatch.p);
   fo_free(d_rpatch.p);
+  fo_free(d_alive.p);
+  fo_free(d_forget.p);
   fo_free(ps_keys);
   fo_free(ps_vals);
   fo_free(ps_count);
+  fo_free(ps_tombs);
   for (auto& c : scratch) c->release();
   fo_hfree(h_total);
   fo_hfree(h_ps_seen);
   if (commit_ev) (void)hipEventDestroy(commit_ev);
+  if (state_ev) (void)hipEventDestroy(state_ev);
+  if (forget_ev) (void)hipEventDestroy(forget_ev);
+  fo_hfree(h_forget);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -1018,6 +1172,17 @@ int pb_wait(emqx_pub_batch* b) {
   } else if (b->n) {
     p->mids_per_topic = std::max<uint64_t>(4, (ms[1] + ms[1] / 4) / b->n + 1);
   }
+  // round_robin / sticky state table or pick scratch too small: nothing was consumed; grow, rerun
+  for (int attempt = 0; (fs[FO_SUM_FLAGS] & FO_SUM_F_RERUN) && !(fs[FO_SUM_FLAGS] & ~FO_SUM_F_RERUN); ++attempt) {
+    if (attempt >= 3) return EMQX_ENOMEM;
+    {
+      std::lock_guard<std::mutex> g(p->s->mu);
+      note_rerun(p->s, fs[FO_SUM_FLAGS]);
+    }
+    int rc = pb_enqueue_fanout(b, p->cap_mids, nullptr);
+    if (rc != EMQX_OK) return rc;
+    FO_TRY(hipStreamSynchronize(p->stream));
+  }
   b->n_out = fs[FO_SUM_TOTAL];
   if (fs[FO_SUM_FLAGS] & FO_SUM_F_MATCH) return EMQX_EDEVICE;
   if (fs[FO_SUM_FLAGS] & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
@@ -1063,6 +1228,7 @@ int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* 
   for (uint64_t i = 0; i < n; ++i) {
     const uint32_t f = filter_ids[i], sub = sub_ids[i];
     const uint32_t grp = group_ids ? group_ids[i] : EMQX_NO_GROUP;
+    set_alive_bit(s, sub, true);  // a subscribing process is alive
     if (grp == EMQX_NO_GROUP) {
       plain_add(s, f, sub);
       continue;
@@ -1141,22 +1307,105 @@ int emqx_subtab_commit_stats(emqx_subtab* s, uint64_t* out, uint32_t n) {
 int emqx_subtab_forget_publishers(emqx_subtab* s, const uint32_t* publishers, uint64_t n) {
   if (!s || (n && !publishers)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
-  if (!n || !s->ps_keys) return EMQX_OK;
+  if (!s->ps_keys) return EMQX_OK;  // no state kept yet
+  // queued: the next stateful fan-out or re-pick applies every queued publisher in one pass
+  s->pending_forget.insert(s->pending_forget.end(), publishers, publishers + n);
+  return EMQX_OK;
+}
+
+int emqx_subtab_set_alive(emqx_subtab* s, const uint32_t* sub_ids, uint64_t n, int alive) {
+  if (!s || (n && !sub_ids)) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(s->mu);
+  for (uint64_t i = 0; i < n; ++i)
+    if (sub_ids[i] != SUB_NONE) set_alive_bit(s, sub_ids[i], alive != 0);
+  return EMQX_OK;
+}
+
+int emqx_share_repick(emqx_subtab* s, uint32_t strategy, uint64_t n, const uint32_t* filter_ids,
+                      const uint32_t* group_ids, const uint32_t* keys, const uint64_t* failed_offsets,
+                      const uint32_t* failed_subs, uint32_t* out_subs, uint32_t* out_kind) {
+  if (!s || strategy > EMQX_SHARE_HASH_TOPIC || (n && (!filter_ids || !group_ids || !failed_offsets || !out_subs ||
+                                                       !out_kind)))
+    return EMQX_EINVAL;
+  if ((strategy == EMQX_SHARE_HASH_CLIENTID || strategy == EMQX_SHARE_HASH_TOPIC) && n && !keys) return EMQX_EINVAL;
+  if (n == 0) return EMQX_OK;
+  if (failed_offsets[0] != 0) return EMQX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (failed_offsets[i + 1] < failed_offsets[i]) return EMQX_EINVAL;
+  const uint64_t nf = failed_offsets[n];
+  if (nf && !failed_subs) return EMQX_EINVAL;
+  std::lock_guard<std::mutex> g(s->mu);
   FO_TRY(hipSetDevice(s->device));
-  std::vector<uint32_t> p(publishers, publishers + n);
-  std::sort(p.begin(), p.end());
-  p.erase(std::unique(p.begin(), p.end()), p.end());
-  int rc = barrier_after_fanouts(s);
+  hipStream_t st = s->stream;
+  int rc = ps_ready(s, n);
+  if (rc == EMQX_OK) rc = flush_forgets(s, st);
   if (rc != EMQX_OK) return rc;
-  uint32_t* d = nullptr;
-  FO_TRY(fo_alloc(d, p.size()));
+  // one device block: the requests, the failed lists, the outputs, a flag word
+  const uint64_t bytes = 12 * n + 8 * (n + 1) + 4 * nf + 8 * n + 64;
+  uint8_t* h = nullptr;
+  uint8_t* d = nullptr;
+  if (fo_halloc(h, bytes) != hipSuccess) return EMQX_ENOMEM;
+  if (fo_alloc(d, bytes) != hipSuccess) {
+    fo_hfree(h);
+    return EMQX_ENOMEM;
+  }
+  auto place = [&](uint64_t& off, uint64_t sz) {
+    const uint64_t o = off;
+    off = (off + sz + 7) & ~7ull;
+    return o;
+  };
+  uint64_t off = 0;
+  const uint64_t o_f = place(off, 4 * n), o_g = place(off, 4 * n), o_k = place(off, 4 * n);
+  const uint64_t o_fo = place(off, 8 * (n + 1)), o_fs = place(off, 4 * nf), o_os = place(off, 4 * n);
+  const uint64_t o_ok = place(off, 4 * n), o_ctl = place(off, 8);
+  std::memcpy(h + o_f, filter_ids, 4 * n);
+  std::memcpy(h + o_g, group_ids, 4 * n);
+  if (keys) std::memcpy(h + o_k, keys, 4 * n);
+  else std::memset(h + o_k, 0, 4 * n);
+  std::memcpy(h + o_fo, failed_offsets, 8 * (n + 1));
+  if (nf) std::memcpy(h + o_fs, failed_subs, 4 * nf);
+  std::memset(h + o_ctl, 0, 8);
+  RepickArgs a{};
+  a.recs = s->d_recs.p;
+  a.n_recs = s->dev_n_recs;
+  a.groups = s->d_groups.p;
+  a.members = s->d_members.p;
+  a.alive = s->d_alive.p;
+  a.n_alive_words = s->dev_n_alive;
+  a.ps_keys = s->ps_keys;
+  a.ps_vals = s->ps_vals;
+  a.ps_count = s->ps_count;
+  a.ps_mask = s->ps_cap - 1;
+  a.strategy = strategy;
+  s->seed = s->seed * 1664525u + 1013904223u;
+  a.seed = s->seed;
+  a.n = n;
+  a.filter_ids = reinterpret_cast<const uint32_t*>(d + o_f);
+  a.group_ids = reinterpret_cast<const uint32_t*>(d + o_g);
+  a.keys = reinterpret_cast<const uint32_t*>(d + o_k);
+  a.failed_off = reinterpret_cast<const uint64_t*>(d + o_fo);
+  a.failed = reinterpret_cast<const uint32_t*>(d + o_fs);
+  a.out_subs = reinterpret_cast<uint32_t*>(d + o_os);
+  a.out_kind = reinterpret_cast<uint32_t*>(d + o_ok);
+  a.ctl = reinterpret_cast<unsigned long long*>(d + o_ctl);
+  // after the last commit and the last stateful resolve; the next stateful call waits for this
   rc = EMQX_OK;
-  if (hipMemcpyAsync(d, p.data(), p.size() * 4, hipMemcpyHostToDevice, s->stream) != hipSuccess ||
-      launch_ps_forget(s->ps_keys, s->ps_cap, d, p.size(), s->ps_count, s->stream) != hipSuccess ||
-      hipEventRecord(s->commit_ev, s->stream) != hipSuccess || hipStreamSynchronize(s->stream) != hipSuccess)
+  if ((s->commit_pending && hipStreamWaitEvent(st, s->commit_ev, 0) != hipSuccess) ||
+      (s->state_pending && hipStreamWaitEvent(st, s->state_ev, 0) != hipSuccess) ||
+      hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, st) != hipSuccess || launch_share_repick(a, st) != hipSuccess ||
+      hipMemcpyAsync(h + o_os, d + o_os, off - o_os, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipEventRecord(s->state_ev, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
     rc = EMQX_EDEVICE;
-  s->commit_pending = true;
+  s->state_pending = true;
+  if (rc == EMQX_OK) {
+    std::memcpy(out_subs, h + o_os, 4 * n);
+    std::memcpy(out_kind, h + o_ok, 4 * n);
+    uint64_t fl;
+    std::memcpy(&fl, h + o_ctl, 8);
+    if (fl & FO_SUM_F_STATE_FULL) s->ps_force_grow = true;  // (those picks were made without state)
+  }
   fo_free(d);
+  fo_hfree(h);
   return rc;
 }
 

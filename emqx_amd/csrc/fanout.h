@@ -17,6 +17,8 @@ namespace emqx {
 
 constexpr uint32_t SUB_NONE = 0xFFFFFFFFu;
 constexpr uint32_t FANOUT_SHARED_BIT = 0x80000000u;  // set in out_filters[] for $share picks
+constexpr uint32_t FANOUT_RETRY_BIT = 0x40000000u;   // ... of type retry (do_pick/6's {retry, Sub})
+constexpr uint32_t FANOUT_ID_LIMIT = 0x40000000u;    // filter ids stay below the flag bits
 
 // Per filter id (16 B, one load per matched filter).  The plain list and the group list are
 // extents of their arenas with room to grow in place (incremental commits, fanout.cpp).
@@ -43,11 +45,19 @@ constexpr uint64_t PS_EMPTY = ~0ull;
 constexpr uint64_t PS_TOMB = ~0ull - 1;
 constexpr uint32_t PS_NOVAL = 0xFFFFFFFFu;
 constexpr uint32_t PS_MAX_PROBES = 64;
+// Pick-list key of an element without a state entry (sorts after every entry index).
+constexpr uint32_t PK_PAD = 0xFFFFFFFFu;
 
 // Per-call control words of one scratch (memset per call).
-constexpr uint32_t FO_CTL_TOUCHED = 0;  // state-table entries this call deferred picks to
-constexpr uint32_t FO_CTL_FLAGS = 1;    // FO_SUM_F_* bits raised by the write kernel
+constexpr uint32_t FO_CTL_PICKS = 0;  // round_robin / sticky picks of the call (the pick list's length)
+constexpr uint32_t FO_CTL_FLAGS = 1;  // FO_SUM_F_* bits raised by the kernels
 constexpr uint32_t FO_CTL_WORDS = 2;
+
+// Liveness of subscribers: erlang:is_process_alive/1 (emqx_shared_sub.erl:386-393), one bit per
+// subscriber id; a sticky pick stays while its subscriber is alive, member or not.
+__host__ __device__ inline bool fo_alive(const uint32_t* alive, uint32_t n_words, uint32_t sub) {
+  return sub != SUB_NONE && (sub >> 5) < n_words && ((alive[sub >> 5] >> (sub & 31u)) & 1u);
+}
 
 struct FanoutArgs {
   const FilterRec* recs;
@@ -55,17 +65,26 @@ struct FanoutArgs {
   const uint32_t* plain;
   const GroupRec* groups;
   const uint32_t* members;
+  const uint32_t* alive;     // [n_alive_words] liveness bitmap
+  uint32_t n_alive_words;
   // pick state (round_robin / sticky)
   uint64_t* ps_keys;         // [ps_mask + 1]
   uint32_t* ps_vals;         // [ps_mask + 1]
   unsigned long long* ps_count;  // live keys (device)
+  unsigned long long* ps_tombs;  // tombstones (device)
   uint64_t ps_mask;
-  unsigned long long* heads; // [ps_mask + 1] per-call chains: stamp << 32 | first output position
-  uint32_t stamp;            // this call's stamp (never 0)
-  uint32_t* next;            // [cap] chain links, by output position
-  uint32_t* touched;         // [ps_mask + 1] state entries with a chain in this call
+  // the call's pick list (round_robin / sticky): one (state entry, output position) pair per
+  // $share pick, written in output order, then stably sorted by entry
+  uint32_t* gchunk;          // [ceil(m_cap / FO_WCHUNK)] $share groups per chunk of FO_WCHUNK entries
+  uint32_t* pk_keys;         // [pk_cap] state entry (PK_PAD past the call's picks)
+  uint32_t* pk_vals;         // [pk_cap] output position
+  uint32_t* pk_skeys;        // [pk_cap] sorted keys (resolve); before the sort: the pick's group record
+  uint32_t* pk_svals;        // [pk_cap] their positions; before the sort: the pick's publisher
+  uint64_t pk_cap;
+  unsigned long long* seg;   // [ps_mask + 1] per entry with picks: first list index | first pick << 32
+  uint32_t* seg_from;        // [ps_mask + 1] sticky: list index from which the pick is constant
   unsigned long long* ctl;   // [FO_CTL_WORDS]
-  unsigned long long* ps_seen;  // host-mapped: ps_count as of the last finished call (growth check)
+  unsigned long long* ps_seen;  // host-mapped [3]: live keys, tombstones, picks of the last finished call
   // the match CSR
   const uint64_t* moff;      // match CSR offsets [n+1]
   const uint32_t* mids;      // match CSR filter ids [moff[n] - moff[0]]
@@ -78,7 +97,7 @@ struct FanoutArgs {
   uint32_t* entry_topic;     // [m] scratch (strategies that read per-topic keys)
   uint32_t* ecount;          // [m] scratch
   uint64_t* eoff;            // [m+1] scratch: per-entry output offsets
-  uint64_t* partials;        // [2 * FO_BLOCKS] scratch: chunk sums, chunk bases
+  uint64_t* partials;        // [4 * FO_BLOCKS] scratch: chunk sums, chunk bases (deliveries, then picks)
   uint64_t* out_off;         // [n+1]
   uint32_t* out_subs;        // [cap]
   uint32_t* out_filters;     // [cap] or null
@@ -86,21 +105,61 @@ struct FanoutArgs {
   uint64_t* summary;         // [FO_SUM_WORDS] device or host-mapped
 };
 
-// Chunks of the fixed-grid count/scan kernels (the entry count is only known on the device).
+// Chunks of the fixed-grid count/scan kernels (the entry count is only known on the device):
+// FO_BLOCKS blocks, each a whole number of FO_WCHUNK-entry chunks (the write kernel's unit).
 constexpr uint32_t FO_BLOCKS = 1024;
+constexpr uint32_t FO_WCHUNK = 256;
 // Call summary words: flags, deliveries, match entries, live pick-state keys.
 constexpr uint32_t FO_SUM_FLAGS = 0, FO_SUM_TOTAL = 1, FO_SUM_ENTRIES = 2, FO_SUM_STATE = 3, FO_SUM_WORDS = 4;
 constexpr uint64_t FO_SUM_F_OVERFLOW = 1;    // more deliveries than cap: nothing written
 constexpr uint64_t FO_SUM_F_MATCH = 2;       // the match call flagged an error/overflow: nothing read
-constexpr uint64_t FO_SUM_F_STATE_FULL = 4;  // a pick found no room in the pick-state table
+constexpr uint64_t FO_SUM_F_STATE_FULL = 4;  // a pick found no room in the pick-state table: no pick
+                                             // state consumed, $share outputs not final (rerun)
+constexpr uint64_t FO_SUM_F_PICKS = 8;       // more round_robin / sticky picks than the pick list
+                                             // holds: nothing written (rerun; the list grows)
+constexpr uint64_t FO_SUM_F_RERUN = FO_SUM_F_STATE_FULL | FO_SUM_F_PICKS;
 
 // True for the strategies whose picks depend on state kept per publisher.
 __host__ __device__ inline bool fo_stateful(uint32_t strategy) { return strategy == 1u || strategy == 2u; }
 // True for the strategies that read the per-topic key.
 __host__ __device__ inline bool fo_needs_topic(uint32_t strategy) { return strategy != 0u; }
 
-// The whole fan-out of one batch, enqueued on s; m_cap bounds the match entries.
+// The whole fan-out of one batch, enqueued on s; m_cap bounds the match entries.  Stateful
+// strategies: launch_fanout enqueues the count / scan / write kernels, the caller orders the
+// stream after the subtable's last resolve, then launch_fanout_resolve sorts the pick list and
+// makes the picks (sort_temp: fanout_sort_temp_bytes(pk_cap) bytes; ent_bits: log2 of the state
+// table's size).
 hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s);
+uint64_t fanout_sort_temp_bytes(uint64_t pk_cap, uint32_t ent_bits);
+hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t sort_temp_bytes, uint32_t ent_bits,
+                                 hipStream_t s);
+
+// emqx_shared_sub:dispatch/4's retry after a failed delivery (emqx_shared_sub.erl:118-130):
+// pick/6 -> do_pick/6 with FailedSubs, in request order, one wave.
+struct RepickArgs {
+  const FilterRec* recs;
+  uint32_t n_recs;
+  const GroupRec* groups;
+  const uint32_t* members;
+  const uint32_t* alive;
+  uint32_t n_alive_words;
+  uint64_t* ps_keys;
+  uint32_t* ps_vals;
+  unsigned long long* ps_count;
+  uint64_t ps_mask;
+  uint32_t strategy;
+  uint32_t seed;
+  uint64_t n;
+  const uint32_t* filter_ids;   // [n]
+  const uint32_t* group_ids;    // [n]
+  const uint32_t* keys;         // [n]
+  const uint64_t* failed_off;   // [n + 1]
+  const uint32_t* failed;       // [failed_off[n]]
+  uint32_t* out_subs;           // [n]
+  uint32_t* out_kind;           // [n] EMQX_PICK_*
+  unsigned long long* ctl;      // [1]: FO_SUM_F_STATE_FULL when a state entry found no room
+};
+hipError_t launch_share_repick(const RepickArgs& a, hipStream_t s);
 
 // One 16-B record / one u32 word written into a device table by an incremental commit.
 struct RecPatch {
@@ -113,16 +172,19 @@ struct WordPatch {
   uint32_t value;
   uint32_t pad;
 };
-hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, const WordPatch* wp, uint64_t n_plain_w,
-                                 uint64_t n_member_w, GroupRec* groups, FilterRec* recs, const RecPatch* rp,
-                                 uint64_t n_group_p, uint64_t n_rec_p, hipStream_t s);
+// Word patches go to plain[] (the first n_plain_w), members[] (the next n_member_w), then the
+// liveness bitmap alive[] (n_alive_w).
+hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, uint32_t* alive, const WordPatch* wp,
+                                 uint64_t n_plain_w, uint64_t n_member_w, uint64_t n_alive_w, GroupRec* groups,
+                                 FilterRec* recs, const RecPatch* rp, uint64_t n_group_p, uint64_t n_rec_p,
+                                 hipStream_t s);
 
 // Pick-state table maintenance: rehash into a larger table; drop the keys of the given
 // publishers (sorted, unique).
 hipError_t launch_ps_rehash(const uint64_t* old_keys, const uint32_t* old_vals, uint64_t old_cap, uint64_t* keys,
                             uint32_t* vals, uint64_t mask, unsigned long long* count, hipStream_t s);
 hipError_t launch_ps_forget(uint64_t* keys, uint64_t cap, const uint32_t* pubs, uint64_t n_pubs,
-                            unsigned long long* count, hipStream_t s);
+                            unsigned long long* count, unsigned long long* tombs, hipStream_t s);
 
 // Copies a delivery CSR into host-mapped pinned memory (the pinned publish batches): offsets
 // always, ids when the call's total (summary) fits cap.

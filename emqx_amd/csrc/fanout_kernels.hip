@@ -19,11 +19,17 @@
 //                offsets), so plain-subscriber copies are coalesced reads and writes; each
 //                $share group contributes exactly one pick.  Skipped entirely on overflow, so
 //                no pick state is consumed by a call that wrote nothing.
-//   resolve      round_robin / sticky only: the picks of one (group slot, publisher) are made
-//                in message order from that publisher's state, one thread per such pair
+//   pad, sort,   round_robin / sticky only: the write kernel puts one (state entry, output
+//   resolve      position) pair per $share pick into a list in output order; a stable radix sort
+//                by entry makes each (group slot, publisher) entry's picks one run in message
+//                order; a head thread per run takes the stored state (round_robin: the run's
+//                first index; sticky: the stored subscriber, re-picked while it is not alive),
+//                then every pick is made from its rank in the run in parallel (O(k) per run,
+//                no chains, no same-address atomics)
 //   finish       one thread: pick-state occupancy into the summary
 // Bandwidth-bound streaming; no MFMA.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "../../include/emqx_match.h"
 #include "fanout.h"
@@ -37,11 +43,7 @@ constexpr int FO_THREADS = 256;
 #ifndef FO_UNROLL_V
 #define FO_UNROLL_V 4
 #endif
-#ifndef FO_WCHUNK_V
-#define FO_WCHUNK_V 256
-#endif
 constexpr uint32_t FO_UNROLL = FO_UNROLL_V;  // outputs per lane per round of the write kernel
-constexpr uint32_t FO_WCHUNK = FO_WCHUNK_V;  // match entries per wave chunk of the write kernel
 
 __device__ __forceinline__ uint32_t fo_lane() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -65,9 +67,12 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_entry_topic_kernel(FanoutAr
   }
 }
 
-// Chunk [lo, hi) of block b out of FO_BLOCKS over m entries (multiples of 64).
+// Chunk [lo, hi) of block b out of FO_BLOCKS over m entries (whole FO_WCHUNK-entry chunks).
+__device__ __forceinline__ uint64_t fo_per_block(uint64_t m) {
+  return ((m + FO_BLOCKS - 1) / FO_BLOCKS + FO_WCHUNK - 1) & ~static_cast<uint64_t>(FO_WCHUNK - 1);
+}
 __device__ __forceinline__ void fo_chunk(uint64_t m, uint32_t b, uint64_t* lo, uint64_t* hi) {
-  const uint64_t per = ((m + FO_BLOCKS - 1) / FO_BLOCKS + 63) & ~63ull;
+  const uint64_t per = fo_per_block(m);
   *lo = min<uint64_t>(m, per * b);
   *hi = min<uint64_t>(m, per * (b + 1));
 }
@@ -101,37 +106,69 @@ __device__ __forceinline__ uint64_t fo_block_excl_scan(uint64_t v, uint64_t* tot
   return before + incl - v;
 }
 
+// Per-entry delivery counts (n_plain + n_groups of the entry's filter) and per-block sums; for
+// round_robin / sticky also the $share groups per FO_WCHUNK-entry chunk (gchunk) and per block.
+// Each wave takes whole chunks (4 entries per lane, all loads of a chunk in flight together).
 __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) {
-  __shared__ uint64_t bsum[FO_THREADS / 64];
+  __shared__ uint64_t bsum[2][FO_THREADS / 64];
   const uint64_t base = a.moff[0];
+  const bool stateful = fo_stateful(a.strategy);
+  const uint32_t lane = fo_lane(), wv = threadIdx.x >> 6;
+  constexpr uint32_t EU = FO_WCHUNK / 64;
   uint64_t lo, hi;
   fo_chunk(fo_entries(a), blockIdx.x, &lo, &hi);
-  uint64_t sum = 0;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += FO_THREADS) {
-    const uint32_t f = a.mids[base + i];
-    uint32_t c = 0;
-    if (f < a.n_recs) {
-      const uint4 r = *reinterpret_cast<const uint4*>(a.recs + f);
-      c = r.y + r.w;
+  uint64_t sum = 0, gsum = 0;
+  for (uint64_t c0 = lo + uint64_t(wv) * FO_WCHUNK; c0 < hi; c0 += uint64_t(FO_THREADS / 64) * FO_WCHUNK) {
+    uint32_t f[EU];
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      const uint64_t i = c0 + lane + 64u * u;
+      f[u] = i < hi ? a.mids[base + i] : FID_NONE;
     }
-    a.ecount[i] = c;
-    sum += c;
+    uint32_t c[EU], g[EU];
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      const bool in = f[u] < a.n_recs;
+      const uint4 r = *reinterpret_cast<const uint4*>(a.recs + (in ? f[u] : 0u));
+      c[u] = in ? r.y + r.w : 0u;
+      g[u] = in ? r.w : 0u;
+    }
+    uint32_t gl = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      const uint64_t i = c0 + lane + 64u * u;
+      if (i < hi) a.ecount[i] = c[u];
+      sum += c[u];
+      gl += g[u];
+    }
+    if (stateful) {
+      const uint64_t gc = fo_wave_sum(gl);
+      if (lane == 0) a.gchunk[c0 / FO_WCHUNK] = static_cast<uint32_t>(gc);
+      gsum += gl;
+    }
   }
   sum = fo_wave_sum(sum);
-  if (fo_lane() == 0) bsum[threadIdx.x >> 6] = sum;
+  gsum = fo_wave_sum(gsum);
+  if (lane == 0) {
+    bsum[0][wv] = sum;
+    bsum[1][wv] = gsum;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (uint32_t k = 0; k < FO_THREADS / 64; ++k) t += bsum[k];
+    uint64_t t = 0, tg = 0;
+    for (uint32_t k = 0; k < FO_THREADS / 64; ++k) {
+      t += bsum[0][k];
+      tg += bsum[1][k];
+    }
     a.partials[blockIdx.x] = t;
+    a.partials[2 * FO_BLOCKS + blockIdx.x] = tg;
   }
 }
 
-// One block of FO_BLOCKS threads: chunk bases, eoff[m] = total, the call summary.
-__global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a) {
+// Exclusive scan of one u64 per thread across the FO_BLOCKS threads of a block.
+__device__ __forceinline__ uint64_t fo_blocks_excl_scan(uint64_t v, uint64_t* total) {
   __shared__ uint64_t wsum[FO_BLOCKS / 64];
   const uint32_t lane = fo_lane(), w = threadIdx.x >> 6;
-  const uint64_t v = a.partials[threadIdx.x];
   uint64_t incl = v;
 #pragma unroll
   for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -145,15 +182,33 @@ __global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a
     before += k < w ? wsum[k] : 0;
     all += wsum[k];
   }
-  a.partials[FO_BLOCKS + threadIdx.x] = before + incl - v;
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
+
+// One block of FO_BLOCKS threads: chunk bases (deliveries; $share picks of the stateful
+// strategies), eoff[m] = total, the call summary.  A call whose deliveries exceed cap, or whose
+// picks exceed the pick list, is flagged here and writes nothing.
+__global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a) {
+  uint64_t all = 0, picks = 0;
+  a.partials[FO_BLOCKS + threadIdx.x] = fo_blocks_excl_scan(a.partials[threadIdx.x], &all);
+  const bool stateful = fo_stateful(a.strategy);
+  if (stateful) a.partials[3 * FO_BLOCKS + threadIdx.x] = fo_blocks_excl_scan(a.partials[2 * FO_BLOCKS + threadIdx.x], &picks);
   if (threadIdx.x == 0) {
     const bool refused = fo_refused(a);
     const uint64_t m = fo_entries(a);
     a.eoff[m] = all;
     uint64_t* sm = a.summary;
-    sm[FO_SUM_FLAGS] = refused ? FO_SUM_F_MATCH : (all > a.cap ? FO_SUM_F_OVERFLOW : 0u);
+    uint64_t fl = 0;
+    if (refused) fl = FO_SUM_F_MATCH;
+    else if (all > a.cap) fl = FO_SUM_F_OVERFLOW;
+    else if (stateful && picks > a.pk_cap) fl = FO_SUM_F_PICKS;
+    sm[FO_SUM_FLAGS] = fl;
     sm[FO_SUM_TOTAL] = all;
     sm[FO_SUM_ENTRIES] = refused ? fo_entries_raw(a) : m;
+    a.ctl[FO_CTL_PICKS] = refused ? 0 : picks;
+    if (fl) a.ctl[FO_CTL_FLAGS] |= fl;
     __threadfence_system();
   }
 }
@@ -204,15 +259,15 @@ __device__ __forceinline__ uint64_t ps_hash(uint64_t k) {
 
 // The state-table entry of `key`, inserting it when absent; PS_EMPTY when the table has no room
 // within PS_MAX_PROBES.  *created: this lane inserted it.
-__device__ __forceinline__ uint64_t ps_find_or_insert(const FanoutArgs& a, uint64_t key, bool* created) {
+__device__ __forceinline__ uint64_t ps_probe_insert(uint64_t* keys, uint64_t mask, uint64_t key, bool* created) {
   *created = false;
-  uint64_t i = ps_hash(key) & a.ps_mask;
-  for (uint32_t p = 0; p < PS_MAX_PROBES; ++p, i = (i + 1) & a.ps_mask) {
-    uint64_t cur = __hip_atomic_load(a.ps_keys + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t i = ps_hash(key) & mask;
+  for (uint32_t p = 0; p < PS_MAX_PROBES; ++p, i = (i + 1) & mask) {
+    uint64_t cur = __hip_atomic_load(keys + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == key) return i;
     if (cur == PS_EMPTY) {
       const unsigned long long old =
-          atomicCAS(reinterpret_cast<unsigned long long*>(a.ps_keys + i), static_cast<unsigned long long>(PS_EMPTY),
+          atomicCAS(reinterpret_cast<unsigned long long*>(keys + i), static_cast<unsigned long long>(PS_EMPTY),
                     static_cast<unsigned long long>(key));
       if (old == PS_EMPTY) {
         *created = true;
@@ -224,16 +279,8 @@ __device__ __forceinline__ uint64_t ps_find_or_insert(const FanoutArgs& a, uint6
   return PS_EMPTY;
 }
 
-// Appends one u32 per predicated lane to list[*counter ...] with one atomic per wave (every
-// active lane must call it).
-__device__ __forceinline__ void wave_append(unsigned long long* counter, uint32_t* list, bool pred, uint32_t v) {
-  const uint64_t m = __ballot(pred);
-  if (!m) return;
-  const uint32_t leader = __ffsll(static_cast<long long>(m)) - 1;
-  unsigned long long base = 0;
-  if (fo_lane() == leader) base = atomicAdd(counter, static_cast<unsigned long long>(__popcll(m)));
-  base = __shfl(base, leader, 64);
-  if (pred) list[base + __popcll(m & ((1ull << fo_lane()) - 1))] = v;
+__device__ __forceinline__ uint64_t ps_find_or_insert(const FanoutArgs& a, uint64_t key, bool* created) {
+  return ps_probe_insert(a.ps_keys, a.ps_mask, key, created);
 }
 
 __device__ __forceinline__ void wave_count(unsigned long long* counter, bool pred) {
@@ -265,6 +312,7 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
     uint32_t np[FO_WCHUNK];
     uint32_t gb[FO_WCHUNK];
     uint32_t top[FO_WCHUNK];
+    uint32_t go[FO_WCHUNK];   // stateful strategies: the entry's first pick-list index
   };
   __shared__ WaveLds lds_all[FO_THREADS / 64];
   constexpr uint32_t EU = FO_WCHUNK / 64;  // entries per lane per chunk
@@ -273,7 +321,8 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
   WaveLds& L = lds_all[wv];
   const uint64_t base = a.moff[0];
   const uint64_t m = fo_entries(a);
-  if (a.eoff[m] > a.cap) return;  // overflow: nothing is written, no pick state consumed
+  // overflow (deliveries or picks): nothing is written, no pick state consumed
+  if (a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS)) return;
   const bool need_topic = a.keys && a.strategy != EMQX_SHARE_RANDOM;
   const bool stateful = fo_stateful(a.strategy);
   const uint64_t nwaves = uint64_t(gridDim.x) * (FO_THREADS / 64);
@@ -297,6 +346,16 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
       f[u] = a.mids[base + ic];
       eo[u] = a.eoff[ic];
       tp[u] = need_topic ? a.entry_topic[ic] : 0u;
+    }
+    // round_robin / sticky: the chunk's first pick-list index = its block's base + the chunks of
+    // the block before it (the list is in output order, one pick per $share group of an entry)
+    uint64_t gbase = 0;
+    if (stateful) {
+      const uint64_t per = fo_per_block(m);
+      const uint64_t blk = e0 / per;
+      uint64_t gl = 0;
+      for (uint64_t q = blk * per / FO_WCHUNK + lane; q < e0 / FO_WCHUNK; q += 64) gl += a.gchunk[q];
+      gbase = a.partials[3 * FO_BLOCKS + blk] + fo_wave_sum(gl);
     }
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
@@ -326,6 +385,20 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
       L.gb[k] = r[u].z;
       L.top[k] = tp[u];
     }
+    if (stateful) {  // entry k's first pick-list index: exclusive scan of n_groups in entry order
+#pragma unroll
+      for (uint32_t u = 0; u < EU; ++u) {
+        const uint32_t g = r[u].w;
+        uint32_t incl = g;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += y;
+        }
+        L.go[lane + 64u * u] = static_cast<uint32_t>(gbase) + incl - g;
+        gbase += __shfl(incl, 63, 64);
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // FO_UNROLL outputs per lane per round: all plain-subscriber loads of the round are in
@@ -351,40 +424,25 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
       }
 #pragma unroll
       for (uint32_t u = 0; u < FO_UNROLL; ++u) {
+        if (!shr[u]) continue;
         const uint32_t k = kk[u];
-        const uint32_t gidx = shr[u] ? L.gb[k] + (rr[u] - L.np[k]) : 0u;
-        GroupRec g{0, 0, 0, 0};
-        if (shr[u]) {
-          const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
-          g = GroupRec{gr.x, gr.y, gr.z, gr.w};
-          fl[u] |= FANOUT_SHARED_BIT;
-        }
+        const uint32_t gidx = L.gb[k] + (rr[u] - L.np[k]);
+        fl[u] |= FANOUT_SHARED_BIT;
         if (!stateful) {
-          if (shr[u]) sub[u] = pick_stateless(a, g, e0 + k, L.top[k], gidx);
+          const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
+          sub[u] = pick_stateless(a, GroupRec{gr.x, gr.y, gr.z, gr.w}, e0 + k, L.top[k], gidx);
           continue;
         }
-        // round_robin / sticky: the pick is deferred to the resolve kernel, which takes this
-        // publisher's picks of the slot in message order.  The output holds the group record
-        // until then, and the output position joins the (slot, publisher) entry's chain.
-        const uint64_t pos = obase + j0 + lane + 64u * u;
-        const uint32_t pub = a.keys ? a.keys[L.top[k]] : 0u;
-        bool created = false;
-        const uint64_t ent = shr[u] ? ps_find_or_insert(a, (uint64_t(g.slot) << 32) | pub, &created) : PS_EMPTY;
-        wave_count(a.ps_count, created);
-        bool first = false;
-        if (shr[u] && ent == PS_EMPTY) {  // no room: a stateless random pick, flagged
-          sub[u] = pick_stateless(a, g, e0 + k, 0u, gidx);
-          if (g.n_members > 1) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(FO_SUM_F_STATE_FULL));
-        } else if (shr[u]) {
-          sub[u] = gidx;
-          // a push onto the entry's chain: one exchange, no retry loop (many lanes of a hot
-          // group push at once); the chain is read only by the resolve kernel, a later launch
-          const unsigned long long mine = (static_cast<unsigned long long>(a.stamp) << 32) | static_cast<uint32_t>(pos);
-          const unsigned long long old = atomicExch(a.heads + ent, mine);
-          first = static_cast<uint32_t>(old >> 32) != a.stamp;
-          a.next[pos] = first ? SUB_NONE : static_cast<uint32_t>(old);
-        }
-        wave_append(a.ctl + FO_CTL_TOUCHED, a.touched, first, static_cast<uint32_t>(ent));
+        // round_robin / sticky: the pick is made after the write by the probe / sort / resolve
+        // kernels, which take each (slot, publisher) entry's picks in message order.  The output
+        // holds the group record until then; the pick goes to the list at its place in output
+        // order (the entry's first pick-list index + its group's rank in the entry) as
+        // {position, group record, publisher}.
+        const uint32_t li = L.go[k] + (rr[u] - L.np[k]);
+        a.pk_vals[li] = static_cast<uint32_t>(obase + j0 + lane + 64u * u);
+        a.pk_skeys[li] = gidx;
+        a.pk_svals[li] = a.keys ? a.keys[L.top[k]] : 0u;
+        sub[u] = gidx;
       }
 #pragma unroll
       for (uint32_t u = 0; u < FO_UNROLL; ++u) {
@@ -399,53 +457,120 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
   }
 }
 
-__device__ __forceinline__ bool is_member(const FanoutArgs& a, const GroupRec& g, uint32_t sub) {
-  for (uint32_t i = 0; i < g.n_members; ++i)
-    if (a.members[g.member_begin + i] == sub) return true;
-  return false;
+// The pick list's state entries: per pick, the (group slot, publisher) entry of the state table,
+// inserted when absent (in parallel over the list, off the write kernel's critical path); past
+// the call's picks, PK_PAD keys, which sort last.
+__global__ __launch_bounds__(FO_THREADS) void fanout_pick_probe_kernel(FanoutArgs a) {
+  if (a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS | FO_SUM_F_MATCH)) return;
+  const uint64_t S = a.ctl[FO_CTL_PICKS];
+  const uint64_t stride = uint64_t(gridDim.x) * FO_THREADS;
+  for (uint64_t i0 = blockIdx.x * uint64_t(FO_THREADS); i0 < a.pk_cap; i0 += stride) {
+    const uint64_t i = i0 + threadIdx.x;
+    const bool pick = i < S;
+    bool created = false;
+    uint64_t ent = PS_EMPTY;
+    if (pick) {
+      const uint32_t slot = a.groups[a.pk_skeys[i]].slot;
+      ent = ps_find_or_insert(a, (uint64_t(slot) << 32) | a.pk_svals[i], &created);
+      if (ent == PS_EMPTY) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(FO_SUM_F_STATE_FULL));
+    }
+    wave_count(a.ps_count, created);
+    if (i < a.pk_cap) a.pk_keys[i] = ent == PS_EMPTY ? PK_PAD : static_cast<uint32_t>(ent);
+  }
 }
 
-// round_robin / sticky: one thread per (slot, publisher) entry touched by this call.  Its
-// chain holds the output positions of its picks (any order); they are taken in increasing
-// position — message order — as the publisher's process would make them one PUBLISH at a time.
-//   round_robin (do_pick_subscriber/6, :279-285): Rem = rand:uniform(N) - 1 the first time,
-//     else (Last + 1) rem N; one member: that member, the state untouched (:265)
-//   sticky (pick/6, :234-247): the stored member while it is still subscribed to the group,
-//     else a random member, which becomes the stored one
-__global__ __launch_bounds__(FO_THREADS) void fanout_resolve_kernel(FanoutArgs a) {
-  const uint64_t nt = a.ctl[FO_CTL_TOUCHED];
-  for (uint64_t t = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; t < nt; t += uint64_t(gridDim.x) * FO_THREADS) {
-    const uint32_t ent = a.touched[t];
-    const uint32_t head = static_cast<uint32_t>(a.heads[ent]);
-    const uint32_t gidx = a.out_subs[head];
+// The idx-th member of g that is not `excl` (count = members - [excl] > idx); member order.
+__device__ __forceinline__ uint32_t nth_member_except(const FanoutArgs& a, const GroupRec& g, uint32_t excl,
+                                                      uint32_t idx) {
+  for (uint32_t i = 0; i < g.n_members; ++i) {
+    const uint32_t s = a.members[g.member_begin + i];
+    if (s == excl) continue;
+    if (idx == 0) return s;
+    --idx;
+  }
+  return SUB_NONE;
+}
+
+__device__ __forceinline__ bool fo_busy_flags(const FanoutArgs& a) { return a.ctl[FO_CTL_FLAGS] != 0; }
+
+// Resolve, part 1: one thread per (slot, publisher) entry with picks in this call (the first
+// element of its run in the sorted list).  The run's positions are in message order.
+//   round_robin (do_pick_subscriber/6, :279-285): the run's first index, Rem = rand:uniform(N) - 1
+//     without state, else (Last + 1) rem N; with one member the state is not consulted (:265)
+//   sticky (pick/6, :234-240): the stored subscriber while its process is alive (is_active_sub/2
+//     with no failed subscribers, :386-393; membership is not checked), else do_pick(random, ...,
+//     [Sub0]) (:243): a random member other than Sub0, or {retry, any member} when Sub0 is the
+//     only one (:251-263); the new pick is stored (:245).  Made message by message until the
+//     stored subscriber is alive, from where on the run is constant.
+__global__ __launch_bounds__(FO_THREADS) void fanout_resolve_heads_kernel(FanoutArgs a) {
+  if (fo_busy_flags(a)) return;  // nothing resolved: the call is rerun
+  const uint64_t S = a.ctl[FO_CTL_PICKS];
+  const bool sticky = a.strategy == EMQX_SHARE_STICKY;
+  for (uint64_t i = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; i < S; i += uint64_t(gridDim.x) * FO_THREADS) {
+    const uint32_t k = a.pk_skeys[i];
+    if (k == PK_PAD || (i > 0 && a.pk_skeys[i - 1] == k)) continue;
+    const uint32_t pos = a.pk_svals[i];
+    const uint32_t gidx = a.out_subs[pos];
     const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
     const GroupRec g{gr.x, gr.y, gr.z, gr.w};
     const uint32_t n = g.n_members;
-    uint32_t val = a.ps_vals[ent];
-    // positions in increasing order: the smallest one above the last taken, per step
-    int64_t last = -1;
-    while (true) {
-      uint32_t best = SUB_NONE;
-      for (uint32_t p = head; p != SUB_NONE; p = a.next[p])
-        if (static_cast<int64_t>(p) > last && (best == SUB_NONE || p < best)) best = p;
-      if (best == SUB_NONE) break;
-      last = best;
-      uint32_t pick;
-      if (a.strategy == EMQX_SHARE_ROUND_ROBIN) {
-        if (n == 1) {
-          pick = a.members[g.member_begin];
-        } else {
-          val = val == PS_NOVAL ? fo_rand(a.seed, best, ent) % n : (val + 1) % n;
-          pick = a.members[g.member_begin + val];
-        }
-      } else {  // EMQX_SHARE_STICKY
-        if (val == PS_NOVAL || !is_member(a, g, val))
-          val = a.members[g.member_begin + (n > 1 ? fo_rand(a.seed, best, ent) % n : 0u)];
-        pick = val;
-      }
-      a.out_subs[best] = pick;
+    uint32_t val = a.ps_vals[k];
+    if (!sticky) {
+      const uint32_t first = n <= 1 ? 0u : (val == PS_NOVAL ? fo_rand(a.seed, pos, k) % n : (val + 1) % n);
+      a.seg[k] = static_cast<unsigned long long>(i) | (static_cast<unsigned long long>(first) << 32);
+      continue;
     }
-    a.ps_vals[ent] = val;
+    uint64_t j = i;
+    for (; j < S && a.pk_skeys[j] == k; ++j) {
+      if (fo_alive(a.alive, a.n_alive_words, val)) break;  // constant from here on
+      const uint32_t p = a.pk_svals[j];
+      bool in = false;  // Sub0 among the members?
+      for (uint32_t q = 0; q < n && !in; ++q) in = a.members[g.member_begin + q] == val;
+      const uint32_t cnt = in ? n - 1 : n;
+      uint32_t pick;
+      bool retry = false;
+      if (cnt == 0) {  // All -- [Sub0] = []: {retry, the only member}
+        pick = a.members[g.member_begin];
+        retry = true;
+      } else {
+        pick = nth_member_except(a, g, val, cnt > 1 ? fo_rand(a.seed, p, k) % cnt : 0u);
+      }
+      a.out_subs[p] = pick;
+      if (retry && a.out_filters) a.out_filters[p] |= FANOUT_RETRY_BIT;
+      val = pick;
+    }
+    a.seg[k] = static_cast<unsigned long long>(i) | (static_cast<unsigned long long>(val) << 32);
+    a.seg_from[k] = static_cast<uint32_t>(j);
+    a.ps_vals[k] = val;
+  }
+}
+
+// Resolve, part 2: every pick of the list from its run's first pick and its rank in the run;
+// the last pick of a round_robin run stores the state.
+__global__ __launch_bounds__(FO_THREADS) void fanout_resolve_apply_kernel(FanoutArgs a) {
+  if (fo_busy_flags(a)) return;
+  const uint64_t S = a.ctl[FO_CTL_PICKS];
+  const bool sticky = a.strategy == EMQX_SHARE_STICKY;
+  for (uint64_t i = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; i < S; i += uint64_t(gridDim.x) * FO_THREADS) {
+    const uint32_t k = a.pk_skeys[i];
+    if (k == PK_PAD) continue;
+    const uint32_t pos = a.pk_svals[i];
+    const unsigned long long sg = a.seg[k];
+    const uint32_t start = static_cast<uint32_t>(sg), first = static_cast<uint32_t>(sg >> 32);
+    if (sticky) {
+      if (i >= a.seg_from[k]) a.out_subs[pos] = first;  // (earlier ones: written by the head)
+      continue;
+    }
+    const uint32_t gidx = a.out_subs[pos];
+    const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
+    const uint32_t n = gr.y;
+    if (n <= 1) {
+      a.out_subs[pos] = a.members[gr.x];
+      continue;
+    }
+    const uint32_t idx = static_cast<uint32_t>((first + (i - start)) % n);
+    a.out_subs[pos] = a.members[gr.x + idx];
+    if (i + 1 == S || a.pk_skeys[i + 1] != k) a.ps_vals[k] = idx;
   }
 }
 
@@ -453,8 +578,136 @@ __global__ void fanout_finish_kernel(FanoutArgs a) {
   const unsigned long long c = *a.ps_count;
   a.summary[FO_SUM_STATE] = c;
   a.summary[FO_SUM_FLAGS] |= a.ctl[FO_CTL_FLAGS];
-  if (a.ps_seen) *a.ps_seen = c;
+  if (a.ps_seen) {
+    a.ps_seen[0] = c;
+    a.ps_seen[1] = *a.ps_tombs;
+    a.ps_seen[2] = a.ctl[FO_CTL_PICKS];
+  }
   __threadfence_system();
+}
+
+// ---- emqx_shared_sub:dispatch/4 retries (emqx_shared_sub.erl:118-130,234-288) ----------------
+// One wave, requests in order (each sees the state the previous ones left).  Lanes share the
+// member scans: a member is "failed" when it is in the request's FailedSubs (or is the excluded
+// sticky subscriber).
+__device__ __forceinline__ bool rp_excluded(const RepickArgs& a, uint64_t f0, uint64_t f1, uint32_t extra,
+                                            uint32_t s) {
+  if (s == extra) return true;
+  for (uint64_t q = f0; q < f1; ++q)
+    if (a.failed[q] == s) return true;
+  return false;
+}
+
+// Lane 0 only: the request's state entry (inserted when absent) and its value.
+__device__ __forceinline__ uint64_t rp_entry(const RepickArgs& a, uint64_t key, uint32_t* val) {
+  bool created = false;
+  const uint64_t ent = ps_probe_insert(a.ps_keys, a.ps_mask, key, &created);
+  if (created) atomicAdd(a.ps_count, 1ull);
+  if (ent == PS_EMPTY) atomicOr(a.ctl, static_cast<unsigned long long>(FO_SUM_F_STATE_FULL));
+  *val = ent == PS_EMPTY ? PS_NOVAL : __hip_atomic_load(a.ps_vals + ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ent;
+}
+
+__device__ __forceinline__ void rp_store(const RepickArgs& a, uint64_t ent, uint32_t v) {
+  __hip_atomic_store(a.ps_vals + ent, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) void share_repick_kernel(RepickArgs a) {
+  const uint32_t lane = fo_lane();
+  for (uint64_t r = 0; r < a.n; ++r) {
+    const uint32_t f = a.filter_ids[r], grp = a.group_ids[r], key = a.keys ? a.keys[r] : 0u;
+    const uint64_t f0 = a.failed_off[r], f1 = a.failed_off[r + 1];
+    // the group's record: the filter's live groups, searched by the lanes
+    GroupRec g{0, 0, 0, 0};
+    bool found = false;
+    if (f < a.n_recs) {
+      const FilterRec fr = a.recs[f];
+      for (uint32_t q0 = 0; q0 < fr.n_groups && !found; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool hit = q < fr.n_groups && a.groups[fr.group_begin + q].group_id == grp;
+        const uint64_t m = __ballot(hit);
+        if (m) {
+          g = a.groups[fr.group_begin + q0 + __ffsll(static_cast<long long>(m)) - 1];
+          found = true;
+        }
+      }
+    }
+    uint32_t pick = SUB_NONE, kind = EMQX_PICK_NONE;
+    if (found && g.n_members) {
+      const uint64_t skey = (uint64_t(g.slot) << 32) | key;
+      uint32_t extra = SUB_NONE;  // sticky: Sub0 joins the excluded list
+      uint32_t strategy = a.strategy;
+      uint64_t sent = PS_EMPTY;
+      bool done = false;
+      if (strategy == EMQX_SHARE_STICKY) {
+        uint32_t v = PS_NOVAL;
+        if (lane == 0) sent = rp_entry(a, skey, &v);
+        sent = __shfl(sent, 0, 64);
+        v = __shfl(v, 0, 64);
+        if (fo_alive(a.alive, a.n_alive_words, v) && !rp_excluded(a, f0, f1, SUB_NONE, v)) {
+          pick = v;  // is_active_sub(Sub0, FailedSubs): {fresh, Sub0}
+          kind = EMQX_PICK_FRESH;
+          done = true;
+        } else {
+          extra = v;
+          strategy = EMQX_SHARE_RANDOM;  // do_pick(random, ..., [Sub0 | FailedSubs])
+        }
+      }
+      if (!done) {
+        // Subs = All -- Excluded (member order); [] -> {retry, pick over All}
+        uint32_t cnt = 0;
+        for (uint32_t q0 = 0; q0 < g.n_members; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          const bool keep = q < g.n_members && !rp_excluded(a, f0, f1, extra, a.members[g.member_begin + q]);
+          cnt += __popcll(__ballot(keep));
+        }
+        const bool retry = cnt == 0;
+        const uint32_t count = retry ? g.n_members : cnt;
+        uint32_t idx = 0;
+        if (count > 1) {  // pick_subscriber/6 with one candidate: it, no strategy (:265)
+          if (strategy == EMQX_SHARE_HASH_CLIENTID || strategy == EMQX_SHARE_HASH_TOPIC) {
+            idx = key % count;
+          } else if (strategy == EMQX_SHARE_ROUND_ROBIN) {
+            if (lane == 0) {
+              uint32_t last = PS_NOVAL;
+              const uint64_t ent = rp_entry(a, skey, &last);
+              idx = last == PS_NOVAL ? fo_rand(a.seed, r, g.slot) % count : (last + 1) % count;
+              if (ent != PS_EMPTY) rp_store(a, ent, idx);
+            }
+            idx = __shfl(idx, 0, 64);
+          } else {
+            idx = fo_rand(a.seed, r, g.slot + 0x632BE5ABu) % count;
+          }
+        }
+        // the idx-th kept member
+        uint32_t seen = 0;
+        for (uint32_t q0 = 0; q0 < g.n_members && pick == SUB_NONE; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          const uint32_t s = q < g.n_members ? a.members[g.member_begin + q] : SUB_NONE;
+          const bool keep = q < g.n_members && (retry || !rp_excluded(a, f0, f1, extra, s));
+          const uint64_t m = __ballot(keep);
+          const uint32_t c = __popcll(m);
+          if (idx < seen + c) {
+            // the (idx - seen)-th set bit of m
+            uint64_t mm = m;
+            for (uint32_t t = idx - seen; t; --t) mm &= mm - 1;
+            const uint32_t src = __ffsll(static_cast<long long>(mm)) - 1;
+            pick = __shfl(s, src, 64);
+          }
+          seen += c;
+        }
+        kind = retry ? EMQX_PICK_RETRY : EMQX_PICK_FRESH;
+        if (a.strategy == EMQX_SHARE_STICKY && sent != PS_EMPTY && lane == 0)
+          rp_store(a, sent, pick);  // stick to whatever was picked (:245)
+      }
+    }
+    if (lane == 0) {
+      a.out_subs[r] = pick;
+      a.out_kind[r] = kind;
+    }
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 uint32_t grid_for(uint64_t items, uint32_t per_block) {
@@ -463,13 +716,13 @@ uint32_t grid_for(uint64_t items, uint32_t per_block) {
 }
 
 // ---- incremental commits of the subscription table ----------------------------------------
-__global__ __launch_bounds__(256) void subtab_word_patch_kernel(uint32_t* plain, uint32_t* members,
+__global__ __launch_bounds__(256) void subtab_word_patch_kernel(uint32_t* plain, uint32_t* members, uint32_t* alive,
                                                                 const WordPatch* wp, uint64_t n_plain,
-                                                                uint64_t n_total) {
+                                                                uint64_t n_plain_members, uint64_t n_total) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n_total; i += uint64_t(gridDim.x) * 256) {
     const WordPatch p = wp[i];
     const uint64_t idx = (uint64_t(p.index_hi) << 32) | p.index_lo;
-    (i < n_plain ? plain : members)[idx] = p.value;
+    (i < n_plain ? plain : (i < n_plain_members ? members : alive))[idx] = p.value;
   }
 }
 
@@ -502,7 +755,8 @@ __global__ __launch_bounds__(256) void ps_rehash_kernel(const uint64_t* old_keys
 }
 
 __global__ __launch_bounds__(256) void ps_forget_kernel(uint64_t* keys, uint64_t cap, const uint32_t* pubs,
-                                                        uint64_t n_pubs, unsigned long long* count) {
+                                                        uint64_t n_pubs, unsigned long long* count,
+                                                        unsigned long long* tombs) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < cap; i += uint64_t(gridDim.x) * 256) {
     const uint64_t k = keys[i];
     if (k == PS_EMPTY || k == PS_TOMB) continue;
@@ -515,6 +769,7 @@ __global__ __launch_bounds__(256) void ps_forget_kernel(uint64_t* keys, uint64_t
     if (lo < n_pubs && pubs[lo] == p) {
       keys[i] = PS_TOMB;  // probes continue past it; a rehash drops it
       atomicAdd(count, ~0ull);
+      atomicAdd(tombs, 1ull);
     }
   }
 }
@@ -526,7 +781,8 @@ __global__ __launch_bounds__(256) void fanout_to_host_kernel(const uint64_t* d_o
   const uint64_t stride = uint64_t(gridDim.x) * 256;
   const uint64_t t0 = blockIdx.x * 256ull + threadIdx.x;
   for (uint64_t t = t0; t <= n; t += stride) h_off[t] = d_off[t];
-  const uint64_t total = (d_summary[FO_SUM_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_MATCH)) ? 0 : d_summary[FO_SUM_TOTAL];
+  const uint64_t total =
+      (d_summary[FO_SUM_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_MATCH | FO_SUM_F_PICKS)) ? 0 : d_summary[FO_SUM_TOTAL];
   if (total > cap) return;
   for (uint64_t i = t0; i < total; i += stride) {
     h_subs[i] = d_subs[i];
@@ -547,21 +803,56 @@ hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s) {
   // one wave per FO_WCHUNK entries up to m_cap (waves past m exit at once)
   hipLaunchKernelGGL(fanout_write_kernel, dim3(grid_for(m_cap, FO_WCHUNK * (FO_THREADS / 64))), dim3(FO_THREADS), 0, s,
                      a);
-  if (fo_stateful(a.strategy)) {
-    const uint64_t most = a.ps_mask + 1 < a.cap ? a.ps_mask + 1 : a.cap;  // entries touched at most
-    hipLaunchKernelGGL(fanout_resolve_kernel, dim3(grid_for(most, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
-  }
+  if (fo_stateful(a.strategy))
+    hipLaunchKernelGGL(fanout_pick_probe_kernel, dim3(grid_for(a.pk_cap, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(1), 0, s, a);
+  return hipGetLastError();
+}
+
+// Onesweep at every size (rocprim's default takes its merge sort below 1M items: three times
+// slower on these 21-24-bit keys).
+using PickSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                  rocprim::default_config, 0>;
+
+uint64_t fanout_sort_temp_bytes(uint64_t pk_cap, uint32_t ent_bits) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs<PickSortConfig>(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
+                                                  static_cast<uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
+                                                  static_cast<uint32_t*>(nullptr), static_cast<size_t>(pk_cap), 0u,
+                                                  ent_bits + 1);
+  return bytes;
+}
+
+hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t sort_temp_bytes, uint32_t ent_bits,
+                                 hipStream_t s) {
+  // stable by entry: each entry's run keeps output (message) order; PK_PAD sorts last
+  size_t tb = sort_temp_bytes;
+  hipError_t e = rocprim::radix_sort_pairs<PickSortConfig>(sort_temp, tb, a.pk_keys, a.pk_skeys, a.pk_vals,
+                                                           a.pk_svals, static_cast<size_t>(a.pk_cap), 0u,
+                                                           ent_bits + 1, s);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = grid_for(a.pk_cap, FO_THREADS * 4);
+  hipLaunchKernelGGL(fanout_resolve_heads_kernel, dim3(grid), dim3(FO_THREADS), 0, s, a);
+  hipLaunchKernelGGL(fanout_resolve_apply_kernel, dim3(grid), dim3(FO_THREADS), 0, s, a);
   hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(1), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, const WordPatch* wp, uint64_t n_plain_w,
-                                 uint64_t n_member_w, GroupRec* groups, FilterRec* recs, const RecPatch* rp,
-                                 uint64_t n_group_p, uint64_t n_rec_p, hipStream_t s) {
+hipError_t launch_share_repick(const RepickArgs& a, hipStream_t s) {
+  if (a.n) hipLaunchKernelGGL(share_repick_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, uint32_t* alive, const WordPatch* wp,
+                                 uint64_t n_plain_w, uint64_t n_member_w, uint64_t n_alive_w, GroupRec* groups,
+                                 FilterRec* recs, const RecPatch* rp, uint64_t n_group_p, uint64_t n_rec_p,
+                                 hipStream_t s) {
   // words first (the lists), then the records that point at them
-  if (n_plain_w + n_member_w)
-    hipLaunchKernelGGL(subtab_word_patch_kernel, dim3(grid_for(n_plain_w + n_member_w, 256)), dim3(256), 0, s, plain,
-                       members, wp, n_plain_w, n_plain_w + n_member_w);
+  const uint64_t nw = n_plain_w + n_member_w + n_alive_w;
+  if (nw)
+    hipLaunchKernelGGL(subtab_word_patch_kernel, dim3(grid_for(nw, 256)), dim3(256), 0, s, plain, members, alive, wp,
+                       n_plain_w, n_plain_w + n_member_w, nw);
   if (n_group_p)
     hipLaunchKernelGGL(subtab_rec_patch_kernel, dim3(grid_for(n_group_p, 256)), dim3(256), 0, s, groups, recs, rp,
                        n_group_p, n_group_p);
@@ -580,9 +871,10 @@ hipError_t launch_ps_rehash(const uint64_t* old_keys, const uint32_t* old_vals, 
 }
 
 hipError_t launch_ps_forget(uint64_t* keys, uint64_t cap, const uint32_t* pubs, uint64_t n_pubs,
-                            unsigned long long* count, hipStream_t s) {
+                            unsigned long long* count, unsigned long long* tombs, hipStream_t s) {
   if (cap && n_pubs)
-    hipLaunchKernelGGL(ps_forget_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, s, keys, cap, pubs, n_pubs, count);
+    hipLaunchKernelGGL(ps_forget_kernel, dim3(grid_for(cap, 256)), dim3(256), 0, s, keys, cap, pubs, n_pubs, count,
+                       tombs);
   return hipGetLastError();
 }
 

@@ -42,7 +42,7 @@ typedef struct { emqx_pub_batcher* b; engine_res* eng; subtab_res* tab; } pub_ba
 typedef struct { emqx_retain* r; } retain_res;
 
 static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_EINVAL, ATOM_ENOMEM, ATOM_DEVICE,
-    ATOM_OVERFLOW, ATOM_NOTFOUND, ATOM_TOODEEP, ATOM_BUSY, ATOM_UNKNOWN;
+    ATOM_OVERFLOW, ATOM_NOTFOUND, ATOM_TOODEEP, ATOM_BUSY, ATOM_UNKNOWN, ATOM_FRESH, ATOM_RETRY;
 
 static ERL_NIF_TERM err_term(ErlNifEnv* env, int rc) {
   ERL_NIF_TERM a;
@@ -126,6 +126,14 @@ static int pack_binaries(ErlNifEnv* env, ERL_NIF_TERM list, uint8_t** bytes, uin
   }
   *n_out = n;
   return 1;
+}
+
+/* A delivery's filter id and its kind: false (plain), true ($share pick) or retry (a $share
+ * pick made as do_pick/6's {retry, Sub}: sent without an ack request). */
+static uint32_t filter_of(uint32_t fl) { return fl & ~(EMQX_FANOUT_SHARED_BIT | EMQX_FANOUT_RETRY_BIT); }
+static ERL_NIF_TERM shared_term(uint32_t fl) {
+  if (!(fl & EMQX_FANOUT_SHARED_BIT)) return ATOM_FALSE;
+  return (fl & EMQX_FANOUT_RETRY_BIT) ? ATOM_RETRY : ATOM_TRUE;
 }
 
 static ERL_NIF_TERM u32_list(ErlNifEnv* env, const uint32_t* v, uint64_t n) {
@@ -403,7 +411,7 @@ static int call_publish(void* ctx, void* buf, uint64_t cap, uint64_t* need) {
 }
 
 /* publish_batch(Eng, Subtab, Strategy, [{Topic, Key}]) ->
- *   {ok, [[{SubId, FilterId, Shared :: boolean()}]]}
+ *   {ok, [[{SubId, FilterId, Shared :: boolean() | retry}]]}
  * Key = erlang:phash2(ClientId) or erlang:phash2(Topic) computed by the caller (hash
  * strategies); the publisher's handle, erlang:phash2(self()), for round_robin / sticky, whose
  * state the reference keeps in the publishing process's dictionary
@@ -452,9 +460,8 @@ static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TE
       ERL_NIF_TERM row = enif_make_list(env, 0);
       for (uint64_t j = out_off[i]; j > out_off[i - 1]; --j) {
         const uint32_t fl = subs[cap + j - 1];
-        ERL_NIF_TERM d = enif_make_tuple3(env, enif_make_uint(env, subs[j - 1]),
-                                          enif_make_uint(env, fl & ~EMQX_FANOUT_SHARED_BIT),
-                                          (fl & EMQX_FANOUT_SHARED_BIT) ? ATOM_TRUE : ATOM_FALSE);
+        ERL_NIF_TERM d = enif_make_tuple3(env, enif_make_uint(env, subs[j - 1]), enif_make_uint(env, filter_of(fl)),
+                                          shared_term(fl));
         row = enif_make_list_cell(env, d, row);
       }
       rows = enif_make_list_cell(env, row, rows);
@@ -477,11 +484,9 @@ static ERL_NIF_TERM deliveries(ErlNifEnv* env, const uint32_t* subs, const uint3
   ERL_NIF_TERM row = enif_make_list(env, 0);
   for (uint64_t j = n; j > 0; --j) {
     const uint32_t fl = fils[j - 1];
-    row = enif_make_list_cell(env,
-                              enif_make_tuple3(env, enif_make_uint(env, subs[j - 1]),
-                                               enif_make_uint(env, fl & ~EMQX_FANOUT_SHARED_BIT),
-                                               (fl & EMQX_FANOUT_SHARED_BIT) ? ATOM_TRUE : ATOM_FALSE),
-                              row);
+    row = enif_make_list_cell(
+        env, enif_make_tuple3(env, enif_make_uint(env, subs[j - 1]), enif_make_uint(env, filter_of(fl)), shared_term(fl)),
+        row);
   }
   return row;
 }
@@ -582,6 +587,63 @@ static ERL_NIF_TERM nif_forget_publishers(ErlNifEnv* env, int argc, const ERL_NI
   int rc = emqx_subtab_forget_publishers(r->s, keys, n);
   free(keys);
   return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
+}
+
+/* subscriber_down(Subtab, [SubId]) -> ok: the subscribers' processes ended (the 'DOWN' that
+ * emqx_shared_sub monitors, emqx_shared_sub.erl:347-350): a sticky pick leaves them at once;
+ * their subscriptions are removed by the caller's cleanup as cleanup_down/1 does (:369-376). */
+static ERL_NIF_TERM nif_subscriber_down(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  subtab_res* r;
+  unsigned n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_SUBTAB, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
+    return enif_make_badarg(env);
+  uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!ids) return err_term(env, EMQX_ENOMEM);
+  ERL_NIF_TERM head, tail = argv[1];
+  for (unsigned i = 0; i < n; ++i) {
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_uint(env, head, &ids[i])) {
+      free(ids);
+      return enif_make_badarg(env);
+    }
+  }
+  int rc = emqx_subtab_set_alive(r->s, ids, n, 0);
+  if (rc == EMQX_OK) rc = emqx_subtab_commit(r->s);
+  free(ids);
+  return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
+}
+
+/* share_repick(Subtab, Strategy, FilterId, GroupId, Key, [FailedSubId]) ->
+ *   {fresh, SubId} | {retry, SubId} | false
+ * emqx_shared_sub:dispatch/4's next pick after a nack / timeout / 'DOWN' of the delivery to
+ * SubId (shared_dispatch_ack_enabled, emqx_shared_sub.erl:118-130,165-189): do_pick/6 over
+ * All -- FailedSubs with the publisher's round_robin / sticky state (Key as in
+ * publish_batch/4).  Dirty CPU: it waits for the device. */
+static ERL_NIF_TERM nif_share_repick(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  subtab_res* r;
+  unsigned strategy, fid, gid, key, n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_SUBTAB, (void**)&r) || !enif_get_uint(env, argv[1], &strategy) ||
+      !enif_get_uint(env, argv[2], &fid) || !enif_get_uint(env, argv[3], &gid) || !enif_get_uint(env, argv[4], &key) ||
+      !enif_get_list_length(env, argv[5], &n))
+    return enif_make_badarg(env);
+  uint32_t* failed = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!failed) return err_term(env, EMQX_ENOMEM);
+  ERL_NIF_TERM head, tail = argv[5];
+  for (unsigned i = 0; i < n; ++i) {
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_uint(env, head, &failed[i])) {
+      free(failed);
+      return enif_make_badarg(env);
+    }
+  }
+  const uint32_t f = fid, g = gid, k = key;
+  const uint64_t off[2] = {0, n};
+  uint32_t sub = 0, kind = EMQX_PICK_NONE;
+  int rc = emqx_share_repick(r->s, strategy, 1, &f, &g, &k, off, failed, &sub, &kind);
+  free(failed);
+  if (rc != EMQX_OK) return err_term(env, rc);
+  if (kind == EMQX_PICK_NONE) return ATOM_FALSE;
+  return enif_make_tuple2(env, kind == EMQX_PICK_RETRY ? ATOM_RETRY : ATOM_FRESH, enif_make_uint(env, sub));
 }
 
 /* ---- retained-message index (include/emqx_retain.h) ------------------------------------
@@ -803,6 +865,8 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   ATOM_TOODEEP = enif_make_atom(env, "too_deep");
   ATOM_BUSY = enif_make_atom(env, "busy");
   ATOM_UNKNOWN = enif_make_atom(env, "unknown");
+  ATOM_FRESH = enif_make_atom(env, "fresh");
+  ATOM_RETRY = enif_make_atom(env, "retry");
   return RES_ENGINE && RES_SUBTAB && RES_BATCHER && RES_PUB_BATCHER && RES_RETAIN ? 0 : 1;
 }
 
@@ -825,6 +889,8 @@ static ErlNifFunc nif_funcs[] = {
     {"new_pub_batcher", 5, nif_new_pub_batcher, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"publish_async", 4, nif_publish_async, 0},
     {"forget_publishers", 2, nif_forget_publishers, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"subscriber_down", 2, nif_subscriber_down, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"share_repick", 6, nif_share_repick, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"topic_match", 2, nif_topic_match, 0},
     {"new_retain", 1, nif_new_retain, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"retain_store", 3, nif_retain_store, ERL_NIF_DIRTY_JOB_CPU_BOUND},

@@ -31,12 +31,17 @@ from typing import Dict, Hashable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from ._lib import (FANOUT_SHARED_BIT, NO_GROUP, PUB_CB, SHARE_HASH_CLIENTID, SHARE_HASH_TOPIC, SHARE_RANDOM,
-                   SHARE_ROUND_ROBIN, SHARE_STICKY, EngineError, check)
+from ._lib import (FANOUT_RETRY_BIT, FANOUT_SHARED_BIT, NO_GROUP, PICK_FRESH, PICK_NONE, PICK_RETRY, PUB_CB,
+                   SHARE_HASH_CLIENTID, SHARE_HASH_TOPIC, SHARE_RANDOM, SHARE_ROUND_ROBIN, SHARE_STICKY, EngineError,
+                   check)
 from .engine import pack
 from .router import Router
 
-__all__ = ["SubTable", "Broker", "PubBatcher", "STRATEGIES", "FANOUT_SHARED_BIT", "NO_GROUP"]
+__all__ = ["SubTable", "Broker", "PubBatcher", "STRATEGIES", "FANOUT_SHARED_BIT", "FANOUT_RETRY_BIT", "NO_GROUP",
+           "PICK_KINDS"]
+
+# emqx_shared_sub:do_pick/6 result types (EMQX_PICK_*): false, {fresh, Sub}, {retry, Sub}
+PICK_KINDS = {PICK_NONE: None, PICK_FRESH: "fresh", PICK_RETRY: "retry"}
 
 # broker.shared_subscription_strategy values (emqx_shared_sub.erl:60-65); 'hash' = hash_clientid
 STRATEGIES = {"random": SHARE_RANDOM, "round_robin": SHARE_ROUND_ROBIN, "sticky": SHARE_STICKY,
@@ -108,6 +113,26 @@ class SubTable:
         """Drops the round_robin / sticky state of these publishers (their processes ended)."""
         p = _u32(publishers)
         check(_lib.lib().emqx_subtab_forget_publishers(self._h, _p(p), len(p)), "emqx_subtab_forget_publishers")
+
+    def set_alive(self, sub_ids, alive: bool) -> None:
+        """emqx_subtab_set_alive: subscriber processes up / down (published by the next commit)."""
+        s = _u32(sub_ids)
+        check(_lib.lib().emqx_subtab_set_alive(self._h, _p(s), len(s), 1 if alive else 0), "emqx_subtab_set_alive")
+
+    def repick(self, strategy, filter_ids, group_ids, keys, failed_lists) -> Tuple[np.ndarray, np.ndarray]:
+        """emqx_share_repick: dispatch/4's retries, request i with FailedSubs = failed_lists[i];
+        returns (subs, kinds) with kinds EMQX_PICK_NONE / _FRESH / _RETRY."""
+        f, g = _u32(filter_ids), _u32(group_ids)
+        n = len(f)
+        k = None if keys is None else _u32(keys)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(x) for x in failed_lists]) if n else []
+        flat = _u32([x for lst in failed_lists for x in lst]) if n and off[-1] else np.zeros(1, np.uint32)
+        subs = np.zeros(max(n, 1), dtype=np.uint32)
+        kinds = np.zeros(max(n, 1), dtype=np.uint32)
+        check(_lib.lib().emqx_share_repick(self._h, _strategy(strategy), n, _p(f), _p(g), _p(k), _p(off), _p(flat),
+                                           _p(subs), _p(kinds)), "emqx_share_repick")
+        return subs[:n], kinds[:n]
 
     def fanout_device(self, strategy, d_moff: int, d_mids: int, n: int, d_keys: Optional[int], d_out_off: int,
                       d_out_subs: int, d_out_filters: Optional[int], cap: int, stream: Optional[int] = None) -> int:
@@ -237,9 +262,11 @@ class Broker:
             self.subs.commit()
             self._dirty = False
 
-    def publish_batch(self, topics: Sequence[bytes], keys: Optional[Sequence[int]] = None, strategy=None):
+    def publish_batch(self, topics: Sequence[bytes], keys: Optional[Sequence[int]] = None, strategy=None,
+                      with_retry: bool = False):
         """Deliveries per topic: [(filter, subscriber, shared)] as emqx_broker:publish/1 routes them
-        on this node."""
+        on this node (``with_retry``: (filter, subscriber, shared, retry), retry = a do_pick/6
+        {retry, Sub} pick, sent without an ack request)."""
         self._sync()
         st = self.strategy if strategy is None else _strategy(strategy)
         buf, offs = pack(list(topics))
@@ -251,12 +278,34 @@ class Broker:
             row = []
             for s, f in zip(subs[out_off[i]:out_off[i + 1]], fils[out_off[i]:out_off[i + 1]]):
                 shared = bool(int(f) & FANOUT_SHARED_BIT)
-                row.append((names[int(f) & ~FANOUT_SHARED_BIT], self._subs_by_id[int(s)], shared))
+                fid = int(f) & ~(FANOUT_SHARED_BIT | FANOUT_RETRY_BIT)
+                d = (names[fid], self._subs_by_id[int(s)], shared)
+                row.append(d + (bool(int(f) & FANOUT_RETRY_BIT),) if with_retry else d)
             res.append(row)
         return res
 
     def publish(self, topic: bytes, key: int = 0):
         return self.publish_batch([topic], [key])[0]
+
+    def down(self, sub) -> None:
+        """The subscriber's process went down (is_alive_sub/1 false); its subscriptions stay
+        until cleaned up, as between the 'DOWN' and cleanup_down/1 in the reference."""
+        with self._lock:
+            self.subs.set_alive([self._sid(sub)], False)
+            self._dirty = True
+
+    def repick(self, topic: bytes, share, key: int, failed, strategy=None):
+        """emqx_shared_sub:dispatch/4's next pick after deliveries to ``failed`` failed:
+        (type, sub) with type "fresh" / "retry", or False when the group has no member."""
+        self._sync()
+        st = self.strategy if strategy is None else _strategy(strategy)
+        fid = self.router.engine.lookup(topic)
+        gid = self._group_ids.get(share)
+        if fid is None or gid is None:
+            return False
+        subs, kinds = self.subs.repick(st, [fid], [gid], [key], [[self._sid(x) for x in failed]])
+        kind = PICK_KINDS[int(kinds[0])]
+        return False if kind is None else (kind, self._subs_by_id[int(subs[0])])
 
 
 class PubBatcher:

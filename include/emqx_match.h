@@ -228,25 +228,32 @@ int emqx_batcher_stats_ext(emqx_batcher* b, uint64_t* out, uint32_t n);
  *   route/2 + aggre/1 + do_dispatch/2,3            apps/emqx/src/emqx_broker.erl:244-272,500-524
  *   emqx_shared_sub:dispatch/3, pick/6, do_pick/6  apps/emqx/src/emqx_shared_sub.erl:113-126,251-288
  * Subscriber ids and group ids are the caller's uint32 handles (the NIF maps pids and group
- * names to them).  Filter ids must be < 2^31.  A delivery is (subscriber id, filter id); the
+ * names to them).  Filter ids must be < 2^30.  A delivery is (subscriber id, filter id); the
  * filter id has EMQX_FANOUT_SHARED_BIT set when the delivery is a $share pick ({share, To, ...}
- * in publish_result(), emqx_types.erl:201-206).
+ * in publish_result(), emqx_types.erl:201-206), and also EMQX_FANOUT_RETRY_BIT when do_pick/6
+ * made it as {retry, Sub} (the message then goes out without an ack request,
+ * emqx_shared_sub.erl:152-155,251-263; only a sticky re-pick whose dead subscriber is the
+ * group's only member does this in a fan-out).
  *
  * Per-message keys (pick_keys / d_pick_keys / emqx_pub_batch.keys), by strategy:
  *   hash_clientid / hash_topic: the caller's erlang:phash2(ClientId) / phash2(Topic) (required);
- *   round_robin / sticky: the PUBLISHER of the message (a uint32 handle of the dispatching
- *     process): the reference keeps this state in the publishing process's dictionary under
- *     {shared_sub_round_robin | shared_sub_sticky, Group, Topic} (emqx_shared_sub.erl:234-247,
- *     279-285), so the device keeps it per (group slot, publisher).  NULL = one publisher.
- *     Picks of one publisher in one call are made in message order;
+ *   round_robin / sticky: the PUBLISHER of the message (a collision-free uint32 handle of the
+ *     dispatching process): the reference keeps this state in the publishing
+ *     process's dictionary under {shared_sub_round_robin | shared_sub_sticky, Group, Topic}
+ *     (emqx_shared_sub.erl:234-247,279-285), so the device keeps it per (group slot, publisher).
+ *     NULL = one publisher.  Picks of one publisher in one call are made in message order, and
+ *     the state updates of concurrent calls are made one call after the other, in the order
+ *     the calls were made (a publisher that waits for each publish, as emqx_broker:publish/1
+ *     does, sees its messages picked in order);
  *   random: ignored. */
 #define EMQX_NO_GROUP 0xFFFFFFFFu
 #define EMQX_FANOUT_SHARED_BIT 0x80000000u
+#define EMQX_FANOUT_RETRY_BIT 0x40000000u
 
 /* broker.shared_subscription_strategy (emqx_shared_sub.erl:60-65) */
 #define EMQX_SHARE_RANDOM 0          /* rand:uniform(N)                                         */
 #define EMQX_SHARE_ROUND_ROBIN 1     /* per publisher: rand:uniform(N) - 1 first, then +1 rem N  */
-#define EMQX_SHARE_STICKY 2          /* per publisher: first pick random, kept while subscribed  */
+#define EMQX_SHARE_STICKY 2          /* per publisher: first pick random, kept while alive       */
 #define EMQX_SHARE_HASH_CLIENTID 3   /* 1 + Key rem N, Key = erlang:phash2(ClientId)             */
 #define EMQX_SHARE_HASH_TOPIC 4      /* 1 + Key rem N, Key = erlang:phash2(Topic)                */
 
@@ -263,11 +270,18 @@ int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* 
 /* emqx_broker:unsubscribe/1 (emqx_broker.erl:169-195); absent pairs are ignored. */
 int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids,
                        const uint32_t* group_ids, uint64_t n);
+/* Liveness of subscriber processes (erlang:is_process_alive/1 and the ?ALIVE_SUBS table of
+ * remote pids, emqx_shared_sub.erl:365-393): alive = 0 when a subscriber's process went down
+ * (the channel-down hook, before its subscriptions are cleaned up, as cleanup_down/1 does);
+ * emqx_subtab_add marks its subscribers alive.  sticky keeps its stored subscriber while it is
+ * alive, whether or not it is still a member (pick/6, :234-240), and re-picks among the other
+ * members once it is not.  Published by the next commit. */
+int emqx_subtab_set_alive(emqx_subtab* s, const uint32_t* sub_ids, uint64_t n, int alive);
 /* Publishes the mutations to the device at a cost proportional to them: the touched list
  * words and 16-B records are patched in place (a list that outgrows its extent moves to the
  * arena's end with room to grow); a full rebuild compacts the arenas only when moved-away
  * extents outweigh the live ones.  Ordered after the fan-outs in flight and before later
- * ones (device events); a sticky member that left its group is replaced at its next pick. */
+ * ones (device events). */
 int emqx_subtab_commit(emqx_subtab* s);
 /* counts[0..3] = live plain subscriptions, live shared memberships, groups with members,
  * device bytes */
@@ -277,8 +291,29 @@ int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4);
  * image update, us of the last commit in total. */
 int emqx_subtab_commit_stats(emqx_subtab* s, uint64_t* out, uint32_t n);
 /* Drops the round_robin / sticky state of the given publishers (their processes ended: the
- * reference's state dies with the process dictionary). */
+ * reference's state dies with the process dictionary).  Queued on the host and applied on the
+ * device before the table's next stateful fan-out or re-pick (one pass for many publishers). */
 int emqx_subtab_forget_publishers(emqx_subtab* s, const uint32_t* publishers, uint64_t n);
+
+/* emqx_shared_sub:dispatch/4's retry after a failed delivery (shared_dispatch_ack_enabled:
+ * a nack, a timeout or the subscriber going down, emqx_shared_sub.erl:118-130,165-189): request i
+ * picks again for (filter_ids[i], group_ids[i]) with FailedSubs = failed_subs[failed_offsets[i]
+ * .. failed_offsets[i+1]) (host buffers), as pick/6 -> do_pick/6 do (:234-263): Subs = All --
+ * FailedSubs in member order; none left -> {retry, pick over All}; one -> it (the strategy is
+ * not consulted); else the strategy over Subs (round_robin: (Last + 1) rem length(Subs), the
+ * publisher's state advanced again; hash: 1 + Key rem length(Subs); random).  sticky keeps
+ * its stored subscriber while it is alive and not failed, else re-picks at random among All
+ * -- [Sub0 | FailedSubs] and stores the pick.  keys[i]: as the fan-out's per-message key (the
+ * publisher for round_robin / sticky, phash2 for the hash strategies).  out_subs[i] = the pick,
+ * out_kind[i] = EMQX_PICK_FRESH / EMQX_PICK_RETRY, or EMQX_PICK_NONE when the group has no
+ * member ({error, no_subscribers}).  Requests are made in order, after the fan-outs already
+ * enqueued on the table; the call returns when they are done. */
+#define EMQX_PICK_NONE 0
+#define EMQX_PICK_FRESH 1
+#define EMQX_PICK_RETRY 2
+int emqx_share_repick(emqx_subtab* s, uint32_t strategy, uint64_t n, const uint32_t* filter_ids,
+                      const uint32_t* group_ids, const uint32_t* keys, const uint64_t* failed_offsets,
+                      const uint32_t* failed_subs, uint32_t* out_subs, uint32_t* out_kind);
 
 /* Fan-out of a match CSR already in HBM (d_match_offsets[n+1], d_match_ids): per-topic CSR of
  * deliveries d_out_offsets[n+1], d_out_subs[], d_out_filters[] (optional, may be NULL).
@@ -295,8 +330,10 @@ int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* 
  * host-mapped memory) receives {flags, deliveries, match entries, live pick-state keys} when the
  * call completes; flags bit 0: more deliveries than cap (nothing written to the id arrays, no
  * $share pick state consumed); bit 1: the CSR was refused (nothing read); bit 2: a
- * round_robin / sticky pick found no room for its state (it was picked at random; the table
- * grows before the next call). */
+ * round_robin / sticky pick found no room for its state, bit 3: more round_robin / sticky picks
+ * than the table's pick scratch holds: in both cases no pick state was consumed and the $share
+ * deliveries are not final: redo the batch with emqx_fanout_batch_device, which grows the
+ * state table / the scratch (once) and reruns. */
 int emqx_fanout_batch_device_async(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
                                    const uint32_t* d_match_ids, uint64_t n, uint64_t match_cap,
                                    const uint32_t* d_pick_keys, uint64_t* d_out_offsets, uint32_t* d_out_subs,

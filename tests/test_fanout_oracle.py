@@ -129,3 +129,80 @@ def test_cpp_fanout_lists_agree_with_counts_and_checksums():
     bad = subs.copy()
     bad[a] ^= 1
     assert C.pair_csr_mismatches(off, bad, fils, off, subs, fils).tolist() == [t]
+
+
+# ---- round 4: sticky liveness and dispatch/4's retries (emqx_shared_sub.erl:113-130,234-263,
+# 385-393), restated by SharedSub.pick_typed / dispatch -------------------------------------------
+
+def three_member(strategy_members=("A", "B", "C")):
+    b = B.Broker()
+    for m in strategy_members:
+        b.subscribe(b"t/+", m, group=b"g")
+    return b
+
+
+def test_sticky_keeps_an_alive_member_that_unsubscribed():
+    """pick(sticky) checks is_active_sub(Sub0, []), i.e. is_process_alive, not membership."""
+    b = three_member()
+    first = picked(b.publish(b"t/1", 9, B.STICKY, draw=lambda c: c.index("B")))
+    assert first == "B"
+    b.unsubscribe(b"t/+", "B", group=b"g")
+    assert picked(b.publish(b"t/1", 9, B.STICKY)) == "B"      # still alive: still sticky
+    b.down("B")
+    # dead: do_pick(random, ..., [Sub0]) over All -- [B] = [A, C]
+    seen = []
+    got = picked(b.publish(b"t/1", 9, B.STICKY, draw=lambda c: (seen.append(list(c)), 1)[1]))
+    assert seen == [["A", "C"]] and got == "C"
+    assert picked(b.publish(b"t/1", 9, B.STICKY)) == "C"
+
+
+def test_sticky_dead_member_still_listed_is_excluded_then_retry_when_alone():
+    b = three_member(("A",))
+    assert picked(b.publish(b"t/1", 1, B.STICKY)) == "A"
+    b.down("A")  # not yet cleaned up: still the only member
+    assert b.shared.pick_typed(B.STICKY, 1, b"g", b"t/+") == ("retry", "A")
+    b.subscribe(b"t/+", "A", group=b"g")  # a live process with that handle again
+    assert b.shared.pick_typed(B.STICKY, 1, b"g", b"t/+") == ("fresh", "A")
+
+
+def test_repick_excludes_failed_then_retries_over_all():
+    """dispatch/4: [SubPid | FailedSubs]; do_pick: All -- FailedSubs, [] -> {retry, ...}."""
+    b = three_member()
+    sh = b.shared
+    # hash: 1 + Key rem length(Subs) over the shrinking candidate list
+    assert sh.pick_typed(B.HASH_CLIENTID, 4, b"g", b"t/+") == ("fresh", "B")          # 1 + 4 rem 3
+    assert sh.pick_typed(B.HASH_CLIENTID, 4, b"g", b"t/+", ["B"]) == ("fresh", "A")   # [A, C]: 1 + 4 rem 2
+    assert sh.pick_typed(B.HASH_CLIENTID, 4, b"g", b"t/+", ["A", "B"]) == ("fresh", "C")
+    assert sh.pick_typed(B.HASH_CLIENTID, 4, b"g", b"t/+", ["C", "A", "B"]) == ("retry", "B")
+    # round_robin: the publisher's Rem advances on every pick, modulo the candidate count
+    assert sh.pick_typed(B.ROUND_ROBIN, 7, b"g", b"t/+") == ("fresh", "A")            # first draw: 0
+    assert sh.pick_typed(B.ROUND_ROBIN, 7, b"g", b"t/+", ["A"]) == ("fresh", "C")     # (0+1) rem 2 over [B, C]
+    assert sh.rr[(7, b"g", b"t/+")] == 1
+    assert sh.pick_typed(B.ROUND_ROBIN, 7, b"g", b"t/+", ["B", "C"]) == ("fresh", "A")  # one left: no state
+    assert sh.rr[(7, b"g", b"t/+")] == 1
+    # sticky: a failed Sub0 is replaced and the replacement sticks
+    assert sh.pick_typed(B.STICKY, 3, b"g", b"t/+", draw=lambda c: 2) == ("fresh", "C")
+    assert sh.pick_typed(B.STICKY, 3, b"g", b"t/+", ["C"], draw=lambda c: c.index("A")) == ("fresh", "A")
+    assert sh.sticky[(3, b"g", b"t/+")] == "A"
+
+
+def test_dispatch_loop_until_ack_or_retry():
+    b = three_member()
+    attempts, res = b.shared.dispatch(B.HASH_CLIENTID, 4, b"g", b"t/+", deliver=lambda s: s == "C")
+    assert attempts == [("fresh", "B"), ("fresh", "A"), ("fresh", "C")] and res == ("ok", 1)
+    attempts, res = b.shared.dispatch(B.HASH_CLIENTID, 4, b"g", b"t/+", deliver=lambda s: False)
+    assert attempts[-1] == ("retry", "B") and len(attempts) == 4 and res == ("ok", 1)
+    attempts, res = b.shared.dispatch(B.HASH_CLIENTID, 4, b"nogroup", b"t/+", deliver=lambda s: True)
+    assert attempts == [] and res == ("error", "no_subscribers")
+
+
+def test_cleanup_down_removes_memberships_and_empty_group_routes():
+    b = B.Broker()
+    b.subscribe(b"t/+", "A", group=b"g")
+    b.subscribe(b"u/#", "A", group=b"h")
+    b.subscribe(b"u/#", "B", group=b"h")
+    b.down("A")
+    b.cleanup_down("A")
+    assert b.shared.subscribers(b"g", b"t/+") == [] and b.shared.subscribers(b"h", b"u/#") == ["B"]
+    assert b.publish(b"t/1", 0, B.HASH_CLIENTID) == []
+    assert b.publish(b"u/1", 0, B.HASH_CLIENTID) == [(b"u/#", "B", True)]

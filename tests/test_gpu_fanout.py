@@ -91,11 +91,15 @@ def test_not_so_sticky_and_dispatch(F):
     b.unsubscribe(b"foo/bar", "C1", share=b"group1")
     b.subscribe(b"foo/#", "C1", share=b"group1")
     assert b.publish(b"foo/bar") == [(b"foo/#", "C1", True)]
-    # a sticky member that leaves is replaced by one still subscribed
+    # a sticky member that leaves but stays alive keeps the publisher's messages
+    # (is_active_sub/2 is process liveness, emqx_shared_sub.erl:234-240,385-393); once its
+    # process is down it is replaced by another member
     b.subscribe(b"foo/#", "C2", share=b"group1")
     first = b.publish(b"foo/bar")[0][1]
     b.unsubscribe(b"foo/#", first, share=b"group1")
     other = "C2" if first == "C1" else "C1"
+    assert [b.publish(b"foo/bar")[0][1] for _ in range(3)] == [first] * 3
+    b.down(first)
     assert [b.publish(b"foo/bar")[0][1] for _ in range(3)] == [other] * 3
 
 
