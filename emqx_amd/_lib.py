@@ -39,7 +39,9 @@ EXPORTS = (
     "emqx_batcher_submit_many", "emqx_batcher_try_submit", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
     "emqx_subtab_stats", "emqx_subtab_commit_stats", "emqx_subtab_forget_publishers", "emqx_subtab_set_alive",
-    "emqx_share_repick",
+    "emqx_share_repick", "emqx_coalescer_create", "emqx_coalescer_insert_filters", "emqx_coalescer_delete_filters",
+    "emqx_coalescer_subscribe", "emqx_coalescer_set_alive", "emqx_coalescer_flush", "emqx_coalescer_destroy",
+    "emqx_coalescer_stats",
     "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
     "emqx_pub_batch_create", "emqx_pub_batch_destroy", "emqx_pub_batch_reserve", "emqx_pub_batch_submit",
     "emqx_pub_batch_wait", "emqx_pub_batch_query",
@@ -143,6 +145,7 @@ class PubBatchStruct(ctypes.Structure):
 
 
 BATCH_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64)
+DONE_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int)
 PUB_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
                           ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64)
 
@@ -196,6 +199,14 @@ def lib():
         "emqx_subtab_forget_publishers": (i32, [vp, vp, u64]),
         "emqx_subtab_set_alive": (i32, [vp, vp, u64, i32]),
         "emqx_share_repick": (i32, [vp, u32, u64, vp, vp, vp, vp, vp, vp, vp]),
+        "emqx_coalescer_create": (i32, [vp, vp, u32, DONE_CB, ctypes.POINTER(vp)]),
+        "emqx_coalescer_insert_filters": (i32, [vp, vp, vp, u64, vp, vp]),
+        "emqx_coalescer_delete_filters": (i32, [vp, vp, u64, vp]),
+        "emqx_coalescer_subscribe": (i32, [vp, vp, vp, vp, u64, i32, vp]),
+        "emqx_coalescer_set_alive": (i32, [vp, vp, u64, i32, vp]),
+        "emqx_coalescer_flush": (i32, [vp]),
+        "emqx_coalescer_destroy": (i32, [vp]),
+        "emqx_coalescer_stats": (i32, [vp, vp, u32]),
         "emqx_pub_batch_create": (i32, [vp, vp, u32, u64, u64, u64, ctypes.POINTER(ctypes.POINTER(PubBatchStruct))]),
         "emqx_pub_batch_destroy": (i32, [ctypes.POINTER(PubBatchStruct)]),
         "emqx_pub_batch_reserve": (i32, [ctypes.POINTER(PubBatchStruct), u64, u64, u64]),

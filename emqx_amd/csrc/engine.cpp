@@ -903,8 +903,9 @@ int emqx_insert_filters_ext(emqx_engine* e, const uint8_t* bytes, const uint64_t
 int emqx_delete_filters(emqx_engine* e, const uint32_t* ids, uint64_t n) {
   if (!e || (n && !ids)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(e->writer);
-  for (uint64_t i = 0; i < n; ++i) {
+  for (uint64_t i = 0; i < n; ++i)  // all or nothing: an unknown id leaves the store unchanged
     if (ids[i] >= e->store.n_ids()) return EMQX_ENOTFOUND;
+  for (uint64_t i = 0; i < n; ++i) {
     if (e->store.live[ids[i]]) {
       e->store.live[ids[i]] = 0;
       e->store.n_live -= 1;

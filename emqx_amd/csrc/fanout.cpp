@@ -214,10 +214,14 @@ struct FoScratch {
   uint64_t pk_cap = 0;
   uint8_t* sort_temp = nullptr;
   uint64_t sort_temp_bytes = 0;
-  uint32_t sort_bits = 0;       // entry bits the sort scratch was sized for
+  uint32_t* run_ent = nullptr;  // per run id (pk_cap)
+  uint32_t* run_cnt = nullptr;  // per run id (pk_cap): picks per run (small path)
+  unsigned long long* multi = nullptr;  // [FO_MULTI_CAP] (small path)
   unsigned long long* seg = nullptr;
   uint32_t* seg_from = nullptr;
-  uint64_t cap_seg = 0;
+  unsigned long long* tag = nullptr;  // per state entry (ps_cap): stamp << 32 | run id
+  uint64_t cap_tag = 0;
+  uint32_t stamp = 0;
   unsigned long long* ctl = nullptr;
   uint64_t* h_sum = nullptr;  // host-mapped call summary (synchronous calls)
   hipEvent_t done = nullptr;  // end of the last fan-out enqueued on this stream
@@ -230,8 +234,12 @@ struct FoScratch {
     fo_free(gchunk);
     fo_free(pk);
     fo_free(sort_temp);
+    fo_free(run_ent);
+    fo_free(run_cnt);
+    fo_free(multi);
     fo_free(seg);
     fo_free(seg_from);
+    fo_free(tag);
     fo_free(ctl);
     fo_hfree(h_sum);
     if (done) (void)hipEventDestroy(done);
@@ -243,7 +251,10 @@ struct PubBatchPriv;
 
 struct emqx_subtab {
   int device = 0;
-  std::mutex mu;  // serialises mutations, commits and fan-out enqueues
+  std::mutex mu;   // serialises mutations, the host half of commits, and fan-out enqueues
+  std::mutex cmu;  // one commit at a time (held across its device half, which s->mu is not)
+  uint8_t* h_stage = nullptr;  // pinned staging of a commit's uploads (one commit at a time)
+  uint64_t stage_cap = 0;
   // ---- host store, and the image of every device array ----
   std::vector<FilterRec> recs;                // per filter id
   std::vector<uint32_t> pcap, gcap;           // capacities of the filter's plain / group extents
@@ -288,8 +299,8 @@ struct emqx_subtab {
   unsigned long long* ps_tombs = nullptr;
   uint64_t ps_cap = 0;
   bool ps_force_grow = false;               // a call found no room for a key: grow before the next
-  unsigned long long* h_ps_seen = nullptr;  // host-mapped [3]: live keys, tombstones, picks of the
-                                            // last finished call
+  unsigned long long* h_ps_seen = nullptr;  // host-mapped [4]: live keys, tombstones, picks and run
+                                            // ids of the last finished call
   std::vector<uint32_t> pending_forget;     // publishers to drop (emqx_subtab_forget_publishers)
   DevArr<uint32_t> d_forget;                // the last flushed list, from pinned staging h_forget
   uint32_t* h_forget = nullptr;
@@ -434,7 +445,7 @@ int barrier_after_fanouts(emqx_subtab* s) {
 
 // Grows a device array to hold `need` elements, keeping its first `keep` elements.
 template <class T>
-int dev_reserve(emqx_subtab* s, DevArr<T>& a, uint64_t need, uint64_t keep, std::vector<T*>& retired) {
+int dev_reserve(emqx_subtab* s, DevArr<T>& a, uint64_t need, uint64_t keep, std::vector<void*>& retired) {
   if (need <= a.cap && a.p) return EMQX_OK;
   const uint64_t cap = std::max<uint64_t>(need + need / 2, 1u << 16);
   T* p = nullptr;
@@ -551,7 +562,7 @@ int full_commit(emqx_subtab* s) {
 // Incremental commit: member lists and group lists of the changed slots / filters are
 // rewritten in the image (moved to the arena's end when they outgrow their extent); then the
 // touched words and records go to the device.
-int live_commit(emqx_subtab* s) {
+int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<std::pair<uint64_t, uint64_t>> member_ranges;
   std::vector<uint64_t> group_idx;
@@ -645,46 +656,46 @@ int live_commit(emqx_subtab* s) {
   const auto t1 = std::chrono::steady_clock::now();
 
   // ---- device: after the fan-outs in flight, before the next ones ----
+  // Everything the device reads comes from pinned staging (a snapshot of the image taken here),
+  // so the commit's copies and patch kernels run after s->mu is released; later fan-outs wait for
+  // commit_ev; arrays a growth replaced are freed once it has passed (commit_finish).
+  uint64_t cw = 0;
+  for (const auto& c : copies_plain) cw += c.second;
+  for (const auto& c : copies_members) cw += c.second;
+  const uint64_t wp_bytes = s->wpatch.size() * sizeof(WordPatch), rp_bytes = s->rpatch.size() * sizeof(RecPatch);
+  const uint64_t stage = cw * 4 + wp_bytes + rp_bytes;
   int rc = barrier_after_fanouts(s);
-  std::vector<FilterRec*> rr;
-  std::vector<uint32_t*> ru;
-  std::vector<GroupRec*> rg;
-  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_recs, s->recs.size(), s->dev_n_recs, rr);
-  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_plain, s->plain.size(), s->d_plain.cap, ru);
-  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_members, s->members.size(), s->d_members.cap, ru);
-  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_groups, s->groups.size(), s->d_groups.cap, rg);
-  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_alive, s->alive.size(), s->dev_n_alive, ru);
-  if (rc == EMQX_OK) {
-    for (const auto& c : copies_plain)
-      if (hipMemcpyAsync(s->d_plain.p + c.first, s->plain.data() + c.first, c.second * 4, hipMemcpyHostToDevice,
-                         s->stream) != hipSuccess)
-        rc = EMQX_EDEVICE;
-    for (const auto& c : copies_members)
-      if (hipMemcpyAsync(s->d_members.p + c.first, s->members.data() + c.first, c.second * 4, hipMemcpyHostToDevice,
-                         s->stream) != hipSuccess)
-        rc = EMQX_EDEVICE;
+  if (rc == EMQX_OK && stage > s->stage_cap) {
+    fo_hfree(s->h_stage);
+    const uint64_t cap = std::max<uint64_t>(stage + stage / 2, 1u << 20);
+    if (fo_halloc(s->h_stage, cap) != hipSuccess) rc = EMQX_ENOMEM;
+    s->stage_cap = rc == EMQX_OK ? cap : 0;
   }
-  if (rc == EMQX_OK && !s->wpatch.empty()) {
-    if (fo_ensure(s->d_wpatch.p, s->d_wpatch.cap, s->wpatch.size()) != hipSuccess ||
-        hipMemcpyAsync(s->d_wpatch.p, s->wpatch.data(), s->wpatch.size() * sizeof(WordPatch), hipMemcpyHostToDevice,
-                       s->stream) != hipSuccess)
-      rc = EMQX_EDEVICE;
-  }
-  if (rc == EMQX_OK && !s->rpatch.empty()) {
-    if (fo_ensure(s->d_rpatch.p, s->d_rpatch.cap, s->rpatch.size()) != hipSuccess ||
-        hipMemcpyAsync(s->d_rpatch.p, s->rpatch.data(), s->rpatch.size() * sizeof(RecPatch), hipMemcpyHostToDevice,
-                       s->stream) != hipSuccess)
-      rc = EMQX_EDEVICE;
-  }
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_recs, s->recs.size(), s->dev_n_recs, retired);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_plain, s->plain.size(), s->d_plain.cap, retired);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_members, s->members.size(), s->d_members.cap, retired);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_groups, s->groups.size(), s->d_groups.cap, retired);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_alive, s->alive.size(), s->dev_n_alive, retired);
+  uint8_t* h = s->h_stage;
+  auto up = [&](void* dst, const void* src, uint64_t bytes) {
+    if (rc != EMQX_OK || !bytes) return;
+    std::memcpy(h, src, bytes);
+    if (hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, s->stream) != hipSuccess) rc = EMQX_EDEVICE;
+    h += bytes;
+  };
+  for (const auto& c : copies_plain) up(s->d_plain.p + c.first, s->plain.data() + c.first, c.second * 4);
+  for (const auto& c : copies_members) up(s->d_members.p + c.first, s->members.data() + c.first, c.second * 4);
+  if (rc == EMQX_OK && !s->wpatch.empty() && fo_ensure(s->d_wpatch.p, s->d_wpatch.cap, s->wpatch.size()) != hipSuccess)
+    rc = EMQX_ENOMEM;
+  up(s->d_wpatch.p, s->wpatch.data(), wp_bytes);
+  if (rc == EMQX_OK && !s->rpatch.empty() && fo_ensure(s->d_rpatch.p, s->d_rpatch.cap, s->rpatch.size()) != hipSuccess)
+    rc = EMQX_ENOMEM;
+  up(s->d_rpatch.p, s->rpatch.data(), rp_bytes);
   if (rc == EMQX_OK &&
       launch_subtab_patches(s->d_plain.p, s->d_members.p, s->d_alive.p, s->d_wpatch.p, n_plain_w, n_member_w,
                             n_alive_w, s->d_groups.p, s->d_recs.p, s->d_rpatch.p, n_group_p, n_rec_p,
                             s->stream) != hipSuccess)
     rc = EMQX_EDEVICE;
-  if (hipStreamSynchronize(s->stream) != hipSuccess && rc == EMQX_OK) rc = EMQX_EDEVICE;
-  for (auto* p : rr) (void)hipFree(p);
-  for (auto* p : ru) (void)hipFree(p);
-  for (auto* p : rg) (void)hipFree(p);
   if (rc != EMQX_OK) {
     s->need_full = true;  // the device copy is in an unknown state: the next commit rebuilds it
     return rc;
@@ -696,9 +707,6 @@ int live_commit(emqx_subtab* s) {
   s->dirty_recs.clear();
   s->dirty_slots.clear();
   s->dirty_glists.clear();
-  uint64_t cw = 0;
-  for (const auto& c : copies_plain) cw += c.second;
-  for (const auto& c : copies_members) cw += c.second;
   s->st_words += n_plain_w + n_member_w + n_alive_w + cw;
   s->st_records += n_group_p + n_rec_p;
   s->st_host_us = std::chrono::duration<double, std::micro>(t1 - t0).count();
@@ -706,17 +714,18 @@ int live_commit(emqx_subtab* s) {
   return EMQX_OK;
 }
 
-int commit_locked(emqx_subtab* s) {
+// The host half of a commit (s->mu held): the image's changes into device operations enqueued
+// on s->stream, ending with commit_ev.  `retired`: device arrays to free after commit_ev.
+int commit_enqueue(emqx_subtab* s, std::vector<void*>& retired) {
   FO_TRY(hipSetDevice(s->device));
-  const auto t0 = std::chrono::steady_clock::now();
-  if (s->recs.size() >= FANOUT_SHARED_BIT) return EMQX_EINVAL;
+  if (s->recs.size() >= FANOUT_ID_LIMIT) return EMQX_EINVAL;
   const uint64_t live = s->plain_pos.size() + s->n_members + s->recs.size();
   int rc;
   if (s->need_full || s->bulk || s->garbage > std::max<uint64_t>(1u << 20, live)) {
     int b = barrier_after_fanouts(s);
-    rc = b != EMQX_OK ? b : full_commit(s);
+    rc = b != EMQX_OK ? b : full_commit(s);  // (synchronous: bulk loads and compactions)
   } else {
-    rc = live_commit(s);
+    rc = live_commit(s, retired);
   }
   if (rc != EMQX_OK) return rc;
   s->ops_pending = 0;
@@ -724,8 +733,26 @@ int commit_locked(emqx_subtab* s) {
   FO_TRY(hipEventRecord(s->commit_ev, s->stream));
   s->commit_pending = true;
   ++s->st_commits;
-  s->st_total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   return EMQX_OK;
+}
+
+// A whole commit (s->cmu held, s->mu not): the host half under s->mu, then the wait for the
+// device half without it, so fan-outs are enqueued meanwhile (they wait for commit_ev on the
+// device, not on the host).
+int commit_now(emqx_subtab* s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<void*> retired;
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(s->mu);
+    rc = commit_enqueue(s, retired);
+  }
+  if (rc == EMQX_OK && hipEventSynchronize(s->commit_ev) != hipSuccess) rc = EMQX_EDEVICE;
+  for (void* p : retired) (void)hipFree(p);
+  std::lock_guard<std::mutex> g(s->mu);
+  if (rc != EMQX_OK) s->need_full = true;
+  s->st_total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
 }
 
 // ---- pick state -----------------------------------------------------------------------------
@@ -823,13 +850,6 @@ FoScratch* scratch_for(emqx_subtab* s, hipStream_t st) {
   return s->scratch.back().get();
 }
 
-// Bits of a state-entry index (the pick list's sort key).
-uint32_t ent_bits(uint64_t ps_cap) {
-  uint32_t b = 1;
-  while ((1ull << b) < ps_cap) ++b;
-  return b;
-}
-
 // Sizes the stateful scratch of c for m_cap entries and the learnt number of picks.
 int stateful_scratch(emqx_subtab* s, FoScratch* c, uint64_t m_cap, uint64_t cap) {
   FO_TRY(fo_ensure(c->gchunk, c->cap_gchunk, m_cap / FO_WCHUNK + 2));
@@ -837,25 +857,30 @@ int stateful_scratch(emqx_subtab* s, FoScratch* c, uint64_t m_cap, uint64_t cap)
   // writes nothing and is rerun after this grows); never more than the delivery capacity
   const uint64_t seen = s->h_ps_seen[2];
   uint64_t want = std::max<uint64_t>(c->pk_cap, std::max<uint64_t>(1u << 16, seen + seen / 2 + 4096));
-  want = std::min<uint64_t>(want, std::max<uint64_t>(cap, 1u << 16));
-  const uint32_t bits = ent_bits(s->ps_cap);
+  want = std::min<uint64_t>(want, std::max<uint64_t>(cap + 1, 1u << 16));
   if (want > c->pk_cap || !c->pk) {
     FO_TRY(fo_alloc(c->pk, 4 * want));
+    FO_TRY(fo_alloc(c->run_ent, want));
+    FO_TRY(fo_alloc(c->run_cnt, want));
+    FO_TRY(fo_alloc(c->seg, want));
+    FO_TRY(fo_alloc(c->seg_from, want));
     c->pk_cap = want;
-    c->sort_bits = 0;
-  }
-  if (c->sort_bits != bits) {
-    const uint64_t tb = fanout_sort_temp_bytes(c->pk_cap, bits);
+    const uint64_t tb = fanout_sort_temp_bytes(want);
     if (tb > c->sort_temp_bytes || !c->sort_temp) {
       FO_TRY(fo_alloc(c->sort_temp, tb));
       c->sort_temp_bytes = tb;
     }
-    c->sort_bits = bits;
   }
-  if (c->cap_seg != s->ps_cap) {  // (a new table: the stream's earlier calls have drained)
-    FO_TRY(fo_alloc(c->seg, s->ps_cap));
-    FO_TRY(fo_alloc(c->seg_from, s->ps_cap));
-    c->cap_seg = s->ps_cap;
+  if (c->cap_tag != s->ps_cap) {  // (a new table: the stream's earlier calls have drained)
+    FO_TRY(fo_alloc(c->tag, s->ps_cap));
+    FO_TRY(hipMemsetAsync(c->tag, 0, s->ps_cap * sizeof(unsigned long long), c->stream));
+    c->cap_tag = s->ps_cap;
+    c->stamp = 0;
+  }
+  if (!c->multi) FO_TRY(fo_alloc(c->multi, FO_MULTI_CAP));
+  if (++c->stamp == 0) {  // stamps wrapped: no tag may look current
+    FO_TRY(hipMemsetAsync(c->tag, 0, s->ps_cap * sizeof(unsigned long long), c->stream));
+    c->stamp = 1;
   }
   return EMQX_OK;
 }
@@ -907,8 +932,19 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
     a.pk_skeys = c->pk + 2 * c->pk_cap;
     a.pk_svals = c->pk + 3 * c->pk_cap;
     a.pk_cap = c->pk_cap;
+    a.tag = c->tag;
+    a.stamp = c->stamp;
+    a.run_ent = c->run_ent;
     a.seg = c->seg;
     a.seg_from = c->seg_from;
+    // the small resolve path (no sort) unless the last finished call had many picks per run:
+    // picks - runs bounds the picks of multi-pick runs by half
+    const uint64_t S_last = s->h_ps_seen[2], R_last = s->h_ps_seen[3];
+    if (S_last < R_last + FO_MULTI_CAP / 2) {
+      a.run_cnt = c->run_cnt;
+      a.multi = c->multi;
+      FO_TRY(hipMemsetAsync(c->run_cnt, 0, c->pk_cap * sizeof(uint32_t), st));
+    }
   }
   a.ctl = c->ctl;
   a.ps_seen = mapped(s->h_ps_seen);
@@ -933,7 +969,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   FO_TRY(launch_fanout(a, m_cap, st));
   if (stateful) {
     if (s->state_pending) FO_TRY(hipStreamWaitEvent(st, s->state_ev, 0));
-    FO_TRY(launch_fanout_resolve(a, c->sort_temp, c->sort_temp_bytes, c->sort_bits, st));
+    FO_TRY(launch_fanout_resolve(a, c->sort_temp, c->sort_temp_bytes, st));
     FO_TRY(hipEventRecord(s->state_ev, st));
     s->state_pending = true;
   }
@@ -979,8 +1015,8 @@ int ensure_stream(emqx_subtab* s) {
     FO_TRY(hipEventCreateWithFlags(&s->state_ev, hipEventDisableTiming));
     FO_TRY(hipEventCreateWithFlags(&s->forget_ev, hipEventDisableTiming));
     FO_TRY(fo_halloc(s->h_total, 2));
-    FO_TRY(fo_halloc(s->h_ps_seen, 3));
-    s->h_ps_seen[0] = s->h_ps_seen[1] = s->h_ps_seen[2] = 0;
+    FO_TRY(fo_halloc(s->h_ps_seen, 4));
+    s->h_ps_seen[0] = s->h_ps_seen[1] = s->h_ps_seen[2] = s->h_ps_seen[3] = 0;
     FO_TRY(fo_alloc(s->ps_count, 1));  // (read by every call's finish kernel)
     FO_TRY(fo_alloc(s->ps_tombs, 1));
     FO_TRY(hipMemset(s->ps_count, 0, sizeof(unsigned long long)));
@@ -1044,6 +1080,7 @@ emqx_subtab::~emqx_subtab() {
   for (auto& c : scratch) c->release();
   fo_hfree(h_total);
   fo_hfree(h_ps_seen);
+  fo_hfree(h_stage);
   if (commit_ev) (void)hipEventDestroy(commit_ev);
   if (state_ev) (void)hipEventDestroy(state_ev);
   if (forget_ev) (void)hipEventDestroy(forget_ev);
@@ -1206,7 +1243,10 @@ int emqx_subtab_create(int32_t device, emqx_subtab** out) {
   if (!s) return EMQX_ENOMEM;
   s->device = dev;
   int rc = ensure_stream(s);
-  if (rc == EMQX_OK) rc = commit_locked(s);
+  if (rc == EMQX_OK) {
+    std::lock_guard<std::mutex> g(s->cmu);
+    rc = commit_now(s);
+  }
   if (rc != EMQX_OK) {
     delete s;
     return rc;
@@ -1280,8 +1320,8 @@ int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_
 
 int emqx_subtab_commit(emqx_subtab* s) {
   if (!s) return EMQX_EINVAL;
-  std::lock_guard<std::mutex> g(s->mu);
-  return commit_locked(s);
+  std::lock_guard<std::mutex> g(s->cmu);
+  return commit_now(s);
 }
 
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4) {

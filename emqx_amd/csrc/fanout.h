@@ -45,13 +45,15 @@ constexpr uint64_t PS_EMPTY = ~0ull;
 constexpr uint64_t PS_TOMB = ~0ull - 1;
 constexpr uint32_t PS_NOVAL = 0xFFFFFFFFu;
 constexpr uint32_t PS_MAX_PROBES = 64;
-// Pick-list key of an element without a state entry (sorts after every entry index).
-constexpr uint32_t PK_PAD = 0xFFFFFFFFu;
-
 // Per-call control words of one scratch (memset per call).
 constexpr uint32_t FO_CTL_PICKS = 0;  // round_robin / sticky picks of the call (the pick list's length)
 constexpr uint32_t FO_CTL_FLAGS = 1;  // FO_SUM_F_* bits raised by the kernels
-constexpr uint32_t FO_CTL_WORDS = 2;
+constexpr uint32_t FO_CTL_RUNS = 2;   // run ids handed out (one per state entry the call touches)
+constexpr uint32_t FO_CTL_MULTI = 3;  // small path: picks of runs with more than one pick
+constexpr uint32_t FO_CTL_NAMED = 4;  // runs of the call (state entries it touches)
+constexpr uint32_t FO_CTL_WORDS = 5;
+// Small resolve path: at most this many picks in runs of more than one pick (sorted in LDS).
+constexpr uint32_t FO_MULTI_CAP = 4096;
 
 // Liveness of subscribers: erlang:is_process_alive/1 (emqx_shared_sub.erl:386-393), one bit per
 // subscriber id; a sticky pick stays while its subscriber is alive, member or not.
@@ -73,18 +75,25 @@ struct FanoutArgs {
   unsigned long long* ps_count;  // live keys (device)
   unsigned long long* ps_tombs;  // tombstones (device)
   uint64_t ps_mask;
-  // the call's pick list (round_robin / sticky): one (state entry, output position) pair per
-  // $share pick, written in output order, then stably sorted by entry
+  // the call's pick list (round_robin / sticky): one (run, output position) pair per $share pick,
+  // written in output order, then stably sorted by run.  A run is the call's picks of one
+  // (group slot, publisher) state entry, named by a small per-call id (so the sort reads few
+  // key bits); run ids are < pk_cap - 1, and pk_cap - 1 pads the list past the call's picks.
   uint32_t* gchunk;          // [ceil(m_cap / FO_WCHUNK)] $share groups per chunk of FO_WCHUNK entries
-  uint32_t* pk_keys;         // [pk_cap] state entry (PK_PAD past the call's picks)
+  uint32_t* pk_keys;         // [pk_cap] run id
   uint32_t* pk_vals;         // [pk_cap] output position
   uint32_t* pk_skeys;        // [pk_cap] sorted keys (resolve); before the sort: the pick's group record
   uint32_t* pk_svals;        // [pk_cap] their positions; before the sort: the pick's publisher
   uint64_t pk_cap;
-  unsigned long long* seg;   // [ps_mask + 1] per entry with picks: first list index | first pick << 32
-  uint32_t* seg_from;        // [ps_mask + 1] sticky: list index from which the pick is constant
+  unsigned long long* tag;   // [ps_mask + 1] per state entry: call stamp << 32 | its run id in that call
+  uint32_t stamp;            // this call's stamp (never 0)
+  uint32_t* run_ent;         // [pk_cap] run id -> state entry
+  unsigned long long* seg;   // [pk_cap] per run: first list index | first pick << 32
+  uint32_t* seg_from;        // [pk_cap] sticky: list index from which the run's pick is constant
+  uint32_t* run_cnt;         // small path ([pk_cap], zeroed per call): picks per run; null: large path
+  unsigned long long* multi; // small path [FO_MULTI_CAP]: run << 32 | list index of multi-pick runs' picks
   unsigned long long* ctl;   // [FO_CTL_WORDS]
-  unsigned long long* ps_seen;  // host-mapped [3]: live keys, tombstones, picks of the last finished call
+  unsigned long long* ps_seen;  // host-mapped [4]: live keys, tombstones, picks, runs of the last finished call
   // the match CSR
   const uint64_t* moff;      // match CSR offsets [n+1]
   const uint32_t* mids;      // match CSR filter ids [moff[n] - moff[0]]
@@ -127,12 +136,10 @@ __host__ __device__ inline bool fo_needs_topic(uint32_t strategy) { return strat
 // The whole fan-out of one batch, enqueued on s; m_cap bounds the match entries.  Stateful
 // strategies: launch_fanout enqueues the count / scan / write kernels, the caller orders the
 // stream after the subtable's last resolve, then launch_fanout_resolve sorts the pick list and
-// makes the picks (sort_temp: fanout_sort_temp_bytes(pk_cap) bytes; ent_bits: log2 of the state
-// table's size).
+// makes the picks (sort_temp: fanout_sort_temp_bytes(pk_cap) bytes).
 hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s);
-uint64_t fanout_sort_temp_bytes(uint64_t pk_cap, uint32_t ent_bits);
-hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t sort_temp_bytes, uint32_t ent_bits,
-                                 hipStream_t s);
+uint64_t fanout_sort_temp_bytes(uint64_t pk_cap);
+hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t sort_temp_bytes, hipStream_t s);
 
 // emqx_shared_sub:dispatch/4's retry after a failed delivery (emqx_shared_sub.erl:118-130):
 // pick/6 -> do_pick/6 with FailedSubs, in request order, one wave.

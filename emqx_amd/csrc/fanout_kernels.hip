@@ -19,13 +19,14 @@
 //                offsets), so plain-subscriber copies are coalesced reads and writes; each
 //                $share group contributes exactly one pick.  Skipped entirely on overflow, so
 //                no pick state is consumed by a call that wrote nothing.
-//   pad, sort,   round_robin / sticky only: the write kernel puts one (state entry, output
-//   resolve      position) pair per $share pick into a list in output order; a stable radix sort
-//                by entry makes each (group slot, publisher) entry's picks one run in message
-//                order; a head thread per run takes the stored state (round_robin: the run's
-//                first index; sticky: the stored subscriber, re-picked while it is not alive),
-//                then every pick is made from its rank in the run in parallel (O(k) per run,
-//                no chains, no same-address atomics)
+//   probe, sort, round_robin / sticky only: the write kernel puts one {position, group record,
+//   resolve      publisher} record per $share pick into a list in output order; the probe kernel
+//                finds each pick's (group slot, publisher) state entry and names the call's run of
+//                that entry with a small id; a stable radix sort by run id makes each run one
+//                segment in message order; a head thread per run takes the stored state
+//                (round_robin: the run's first index; sticky: the stored subscriber, re-picked
+//                while it is not alive), then every pick is made from its rank in the run in
+//                parallel (O(k) per run, no chains, no same-address atomics)
 //   finish       one thread: pick-state occupancy into the summary
 // Bandwidth-bound streaming; no MFMA.
 #include <hip/hip_runtime.h>
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a
     uint64_t fl = 0;
     if (refused) fl = FO_SUM_F_MATCH;
     else if (all > a.cap) fl = FO_SUM_F_OVERFLOW;
-    else if (stateful && picks > a.pk_cap) fl = FO_SUM_F_PICKS;
+    else if (stateful && picks + 1 > a.pk_cap) fl = FO_SUM_F_PICKS;
     sm[FO_SUM_FLAGS] = fl;
     sm[FO_SUM_TOTAL] = all;
     sm[FO_SUM_ENTRIES] = refused ? fo_entries_raw(a) : m;
@@ -457,12 +458,16 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
   }
 }
 
-// The pick list's state entries: per pick, the (group slot, publisher) entry of the state table,
-// inserted when absent (in parallel over the list, off the write kernel's critical path); past
-// the call's picks, PK_PAD keys, which sort last.
+// The pick list's runs: per pick, the (group slot, publisher) entry of the state table (inserted
+// when absent; in parallel over the list, off the write kernel's critical path) and the call's
+// run id of that entry (the first pick to see the entry in this call names the run; ids are
+// handed out one atomic per wave); past the call's picks the pad key pk_cap - 1, which sorts
+// last.  run_cnt (small path): picks per run.
 __global__ __launch_bounds__(FO_THREADS) void fanout_pick_probe_kernel(FanoutArgs a) {
   if (a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS | FO_SUM_F_MATCH)) return;
   const uint64_t S = a.ctl[FO_CTL_PICKS];
+  const uint32_t pad = static_cast<uint32_t>(a.pk_cap - 1);
+  const uint32_t lane = fo_lane();
   const uint64_t stride = uint64_t(gridDim.x) * FO_THREADS;
   for (uint64_t i0 = blockIdx.x * uint64_t(FO_THREADS); i0 < a.pk_cap; i0 += stride) {
     const uint64_t i = i0 + threadIdx.x;
@@ -475,7 +480,38 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_pick_probe_kernel(FanoutArg
       if (ent == PS_EMPTY) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(FO_SUM_F_STATE_FULL));
     }
     wave_count(a.ps_count, created);
-    if (i < a.pk_cap) a.pk_keys[i] = ent == PS_EMPTY ? PK_PAD : static_cast<uint32_t>(ent);
+    unsigned long long cur = 0;
+    if (ent != PS_EMPTY) cur = __hip_atomic_load(a.tag + ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool fresh = ent != PS_EMPTY && static_cast<uint32_t>(cur >> 32) != a.stamp;
+    // new run ids for the wave's lanes that saw no run yet: one atomic per wave
+    const uint64_t m = __ballot(fresh);
+    uint32_t id = 0;
+    if (m) {
+      const uint32_t leader = __ffsll(static_cast<long long>(m)) - 1;
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(a.ctl + FO_CTL_RUNS, static_cast<unsigned long long>(__popcll(m)));
+      base = __shfl(base, leader, 64);
+      id = static_cast<uint32_t>(base) + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1)));
+    }
+    uint32_t key = pad;
+    if (ent != PS_EMPTY) {
+      if (!fresh) {
+        key = static_cast<uint32_t>(cur);
+      } else {
+        const unsigned long long mine = (static_cast<unsigned long long>(a.stamp) << 32) | id;
+        const unsigned long long prev = atomicCAS(a.tag + ent, cur, mine);
+        if (prev == cur) {
+          key = id;
+          a.run_ent[id] = static_cast<uint32_t>(ent);
+        } else {
+          key = static_cast<uint32_t>(prev);  // another pick of this call named the run first
+        }
+      }
+      if (a.run_cnt) atomicAdd(a.run_cnt + key, 1u);
+    }
+    // runs named (ids handed out to lanes that lost the naming race are not runs)
+    wave_count(a.ctl + FO_CTL_NAMED, ent != PS_EMPTY && fresh && key == id);
+    if (i < a.pk_cap) a.pk_keys[i] = key;
   }
 }
 
@@ -493,30 +529,67 @@ __device__ __forceinline__ uint32_t nth_member_except(const FanoutArgs& a, const
 
 __device__ __forceinline__ bool fo_busy_flags(const FanoutArgs& a) { return a.ctl[FO_CTL_FLAGS] != 0; }
 
-// Resolve, part 1: one thread per (slot, publisher) entry with picks in this call (the first
-// element of its run in the sorted list).  The run's positions are in message order.
-//   round_robin (do_pick_subscriber/6, :279-285): the run's first index, Rem = rand:uniform(N) - 1
-//     without state, else (Last + 1) rem N; with one member the state is not consulted (:265)
-//   sticky (pick/6, :234-240): the stored subscriber while its process is alive (is_active_sub/2
-//     with no failed subscribers, :386-393; membership is not checked), else do_pick(random, ...,
-//     [Sub0]) (:243): a random member other than Sub0, or {retry, any member} when Sub0 is the
-//     only one (:251-263); the new pick is stored (:245).  Made message by message until the
-//     stored subscriber is alive, from where on the run is constant.
+__device__ __forceinline__ GroupRec fo_group(const FanoutArgs& a, uint32_t gidx) {
+  const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
+  return GroupRec{gr.x, gr.y, gr.z, gr.w};
+}
+
+// round_robin, one message (do_pick_subscriber/6, :279-285): Rem = rand:uniform(N) - 1 without
+// state, else (Last + 1) rem N; with one member the state is neither consulted nor changed (:265).
+__device__ __forceinline__ uint32_t rr_step(const FanoutArgs& a, const GroupRec& g, uint32_t* val, uint32_t pos,
+                                            uint32_t ent) {
+  const uint32_t n = g.n_members;
+  if (n <= 1) return a.members[g.member_begin];
+  *val = *val == PS_NOVAL ? fo_rand(a.seed, pos, ent) % n : (*val + 1) % n;
+  return a.members[g.member_begin + *val];
+}
+
+// sticky, one message (pick/6, :234-247): the stored subscriber while its process is alive
+// (is_active_sub/2 with no failed subscribers, :386-393; membership is not checked), else
+// do_pick(random, ..., [Sub0]) (:243): a random member other than Sub0, or {retry, any member}
+// when Sub0 is the only one (:251-263); the pick is stored (:245).
+__device__ __forceinline__ uint32_t sticky_step(const FanoutArgs& a, const GroupRec& g, uint32_t* val, uint32_t pos,
+                                                uint32_t ent, bool* retry) {
+  *retry = false;
+  if (fo_alive(a.alive, a.n_alive_words, *val)) return *val;
+  const uint32_t n = g.n_members;
+  bool in = false;  // Sub0 among the members?
+  for (uint32_t q = 0; q < n && !in; ++q) in = a.members[g.member_begin + q] == *val;
+  const uint32_t cnt = in ? n - 1 : n;
+  uint32_t pick;
+  if (cnt == 0) {  // All -- [Sub0] = []: {retry, the only member}
+    pick = a.members[g.member_begin];
+    *retry = true;
+  } else {
+    pick = nth_member_except(a, g, *val, cnt > 1 ? fo_rand(a.seed, pos, ent) % cnt : 0u);
+  }
+  *val = pick;
+  return pick;
+}
+
+__device__ __forceinline__ void fo_put_pick(const FanoutArgs& a, uint32_t pos, uint32_t sub, bool retry) {
+  a.out_subs[pos] = sub;
+  if (retry && a.out_filters) a.out_filters[pos] |= FANOUT_RETRY_BIT;
+}
+
+// ---- large path (many picks per run: few publishers) ---------------------------------------
+// Resolve, part 1: one thread per run (its first element in the sorted list; the run's positions
+// are in message order): round_robin's first index of the run; sticky's picks made message by
+// message until the stored subscriber is alive, from where on the run is constant.
 __global__ __launch_bounds__(FO_THREADS) void fanout_resolve_heads_kernel(FanoutArgs a) {
   if (fo_busy_flags(a)) return;  // nothing resolved: the call is rerun
   const uint64_t S = a.ctl[FO_CTL_PICKS];
   const bool sticky = a.strategy == EMQX_SHARE_STICKY;
   for (uint64_t i = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; i < S; i += uint64_t(gridDim.x) * FO_THREADS) {
     const uint32_t k = a.pk_skeys[i];
-    if (k == PK_PAD || (i > 0 && a.pk_skeys[i - 1] == k)) continue;
+    if (k + 1 >= a.pk_cap || (i > 0 && a.pk_skeys[i - 1] == k)) continue;
+    const uint32_t ent = a.run_ent[k];
     const uint32_t pos = a.pk_svals[i];
-    const uint32_t gidx = a.out_subs[pos];
-    const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
-    const GroupRec g{gr.x, gr.y, gr.z, gr.w};
-    const uint32_t n = g.n_members;
-    uint32_t val = a.ps_vals[k];
+    const GroupRec g = fo_group(a, a.out_subs[pos]);
+    uint32_t val = a.ps_vals[ent];
     if (!sticky) {
-      const uint32_t first = n <= 1 ? 0u : (val == PS_NOVAL ? fo_rand(a.seed, pos, k) % n : (val + 1) % n);
+      const uint32_t n = g.n_members;
+      const uint32_t first = n <= 1 ? 0u : (val == PS_NOVAL ? fo_rand(a.seed, pos, ent) % n : (val + 1) % n);
       a.seg[k] = static_cast<unsigned long long>(i) | (static_cast<unsigned long long>(first) << 32);
       continue;
     }
@@ -524,24 +597,12 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_resolve_heads_kernel(Fanout
     for (; j < S && a.pk_skeys[j] == k; ++j) {
       if (fo_alive(a.alive, a.n_alive_words, val)) break;  // constant from here on
       const uint32_t p = a.pk_svals[j];
-      bool in = false;  // Sub0 among the members?
-      for (uint32_t q = 0; q < n && !in; ++q) in = a.members[g.member_begin + q] == val;
-      const uint32_t cnt = in ? n - 1 : n;
-      uint32_t pick;
-      bool retry = false;
-      if (cnt == 0) {  // All -- [Sub0] = []: {retry, the only member}
-        pick = a.members[g.member_begin];
-        retry = true;
-      } else {
-        pick = nth_member_except(a, g, val, cnt > 1 ? fo_rand(a.seed, p, k) % cnt : 0u);
-      }
-      a.out_subs[p] = pick;
-      if (retry && a.out_filters) a.out_filters[p] |= FANOUT_RETRY_BIT;
-      val = pick;
+      bool retry;
+      fo_put_pick(a, p, sticky_step(a, g, &val, p, ent, &retry), retry);
     }
     a.seg[k] = static_cast<unsigned long long>(i) | (static_cast<unsigned long long>(val) << 32);
     a.seg_from[k] = static_cast<uint32_t>(j);
-    a.ps_vals[k] = val;
+    a.ps_vals[ent] = val;
   }
 }
 
@@ -553,7 +614,7 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_resolve_apply_kernel(Fanout
   const bool sticky = a.strategy == EMQX_SHARE_STICKY;
   for (uint64_t i = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; i < S; i += uint64_t(gridDim.x) * FO_THREADS) {
     const uint32_t k = a.pk_skeys[i];
-    if (k == PK_PAD) continue;
+    if (k + 1 >= a.pk_cap) continue;
     const uint32_t pos = a.pk_svals[i];
     const unsigned long long sg = a.seg[k];
     const uint32_t start = static_cast<uint32_t>(sg), first = static_cast<uint32_t>(sg >> 32);
@@ -570,7 +631,93 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_resolve_apply_kernel(Fanout
     }
     const uint32_t idx = static_cast<uint32_t>((first + (i - start)) % n);
     a.out_subs[pos] = a.members[gr.x + idx];
-    if (i + 1 == S || a.pk_skeys[i + 1] != k) a.ps_vals[k] = idx;
+    if (i + 1 == S || a.pk_skeys[i + 1] != k) a.ps_vals[a.run_ent[k]] = idx;
+  }
+}
+
+// ---- small path (few picks per run: many publishers) -----------------------------------------
+// No sort: a run of one pick (the common case) is resolved where it lies; the picks of runs with
+// more than one are gathered (at most FO_MULTI_CAP of them), sorted by (run, list index) in LDS
+// by one block and resolved run by run.  A call with more multi-pick picks is flagged before any
+// state is consumed and rerun on the large path.
+__global__ __launch_bounds__(FO_THREADS) void fanout_pick_classify_kernel(FanoutArgs a) {
+  if (fo_busy_flags(a)) return;
+  const uint64_t S = a.ctl[FO_CTL_PICKS];
+  const uint32_t lane = fo_lane();
+  const uint64_t stride = uint64_t(gridDim.x) * FO_THREADS;
+  for (uint64_t i0 = blockIdx.x * uint64_t(FO_THREADS); i0 < S; i0 += stride) {
+    const uint64_t i = i0 + threadIdx.x;
+    const uint32_t k = i < S ? a.pk_keys[i] : a.pk_cap - 1;
+    const bool multi = k + 1 < a.pk_cap && a.run_cnt[k] > 1;
+    const uint64_t m = __ballot(multi);
+    if (!m) continue;
+    const uint32_t leader = __ffsll(static_cast<long long>(m)) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(a.ctl + FO_CTL_MULTI, static_cast<unsigned long long>(__popcll(m)));
+    base = __shfl(base, leader, 64);
+    const uint64_t slot = base + __popcll(m & ((1ull << lane) - 1));
+    if (multi && slot < FO_MULTI_CAP) a.multi[slot] = (static_cast<unsigned long long>(k) << 32) | static_cast<uint32_t>(i);
+  }
+}
+
+__global__ __launch_bounds__(1024) void fanout_resolve_small_kernel(FanoutArgs a) {
+  __shared__ unsigned long long srt[FO_MULTI_CAP];
+  if (fo_busy_flags(a)) return;
+  const uint64_t M = a.ctl[FO_CTL_MULTI];
+  if (M > FO_MULTI_CAP) {  // too many: nothing consumed, the host reruns on the large path
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(FO_SUM_F_PICKS));
+    return;
+  }
+  const uint64_t S = a.ctl[FO_CTL_PICKS];
+  const bool sticky = a.strategy == EMQX_SHARE_STICKY;
+  if (blockIdx.x == 0) {
+    if (M == 0) return;
+    uint32_t P = 1;
+    while (P < M) P <<= 1;
+    for (uint32_t t = threadIdx.x; t < P; t += 1024) srt[t] = t < M ? a.multi[t] : ~0ull;
+    __syncthreads();
+    for (uint32_t k2 = 2; k2 <= P; k2 <<= 1)  // bitonic sort by (run, list index)
+      for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+        for (uint32_t t = threadIdx.x; t < P; t += 1024) {
+          const uint32_t o = t ^ j;
+          if (o > t) {
+            const unsigned long long x = srt[t], y = srt[o];
+            if (((t & k2) == 0) == (x > y)) {
+              srt[t] = y;
+              srt[o] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (uint32_t t = threadIdx.x; t < M; t += 1024) {  // a thread per run, in message order
+      const uint32_t k = static_cast<uint32_t>(srt[t] >> 32);
+      if (t > 0 && static_cast<uint32_t>(srt[t - 1] >> 32) == k) continue;
+      const uint32_t ent = a.run_ent[k];
+      uint32_t val = a.ps_vals[ent];
+      for (uint32_t u = t; u < M && static_cast<uint32_t>(srt[u] >> 32) == k; ++u) {
+        const uint32_t pos = a.pk_vals[static_cast<uint32_t>(srt[u])];
+        const GroupRec g = fo_group(a, a.out_subs[pos]);
+        bool retry = false;
+        const uint32_t sub = sticky ? sticky_step(a, g, &val, pos, ent, &retry) : rr_step(a, g, &val, pos, ent);
+        fo_put_pick(a, pos, sub, retry);
+      }
+      a.ps_vals[ent] = val;
+    }
+    return;
+  }
+  // the other blocks: runs of one pick
+  for (uint64_t i = (blockIdx.x - 1) * 1024ull + threadIdx.x; i < S; i += uint64_t(gridDim.x - 1) * 1024) {
+    const uint32_t k = a.pk_keys[i];
+    if (k + 1 >= a.pk_cap || a.run_cnt[k] != 1) continue;
+    const uint32_t ent = a.run_ent[k];
+    const uint32_t pos = a.pk_vals[i];
+    const GroupRec g = fo_group(a, a.out_subs[pos]);
+    uint32_t val = a.ps_vals[ent];
+    bool retry = false;
+    const uint32_t sub = sticky ? sticky_step(a, g, &val, pos, ent, &retry) : rr_step(a, g, &val, pos, ent);
+    fo_put_pick(a, pos, sub, retry);
+    a.ps_vals[ent] = val;
   }
 }
 
@@ -582,6 +729,7 @@ __global__ void fanout_finish_kernel(FanoutArgs a) {
     a.ps_seen[0] = c;
     a.ps_seen[1] = *a.ps_tombs;
     a.ps_seen[2] = a.ctl[FO_CTL_PICKS];
+    a.ps_seen[3] = a.ctl[FO_CTL_NAMED];
   }
   __threadfence_system();
 }
@@ -811,26 +959,37 @@ hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s) {
 }
 
 // Onesweep at every size (rocprim's default takes its merge sort below 1M items: three times
-// slower on these 21-24-bit keys).
+// slower on these keys).
 using PickSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                   rocprim::default_config, 0>;
 
-uint64_t fanout_sort_temp_bytes(uint64_t pk_cap, uint32_t ent_bits) {
+uint32_t pick_key_bits(uint64_t pk_cap) {  // run ids and the pad key are < pk_cap
+  uint32_t b = 1;
+  while (b < 32 && (1ull << b) < pk_cap) ++b;
+  return b;
+}
+
+uint64_t fanout_sort_temp_bytes(uint64_t pk_cap) {
   size_t bytes = 0;
   (void)rocprim::radix_sort_pairs<PickSortConfig>(nullptr, bytes, static_cast<const uint32_t*>(nullptr),
                                                   static_cast<uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
                                                   static_cast<uint32_t*>(nullptr), static_cast<size_t>(pk_cap), 0u,
-                                                  ent_bits + 1);
+                                                  pick_key_bits(pk_cap));
   return bytes;
 }
 
-hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t sort_temp_bytes, uint32_t ent_bits,
-                                 hipStream_t s) {
-  // stable by entry: each entry's run keeps output (message) order; PK_PAD sorts last
+hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t sort_temp_bytes, hipStream_t s) {
+  if (a.run_cnt) {  // small path
+    hipLaunchKernelGGL(fanout_pick_classify_kernel, dim3(grid_for(a.pk_cap, FO_THREADS * 4)), dim3(FO_THREADS), 0, s, a);
+    hipLaunchKernelGGL(fanout_resolve_small_kernel, dim3(1 + grid_for(a.pk_cap, 1024 * 4)), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(1), 0, s, a);
+    return hipGetLastError();
+  }
+  // large path: stable by run: each run keeps output (message) order; the pad sorts last
   size_t tb = sort_temp_bytes;
   hipError_t e = rocprim::radix_sort_pairs<PickSortConfig>(sort_temp, tb, a.pk_keys, a.pk_skeys, a.pk_vals,
                                                            a.pk_svals, static_cast<size_t>(a.pk_cap), 0u,
-                                                           ent_bits + 1, s);
+                                                           pick_key_bits(a.pk_cap), s);
   if (e != hipSuccess) return e;
   const uint32_t grid = grid_for(a.pk_cap, FO_THREADS * 4);
   hipLaunchKernelGGL(fanout_resolve_heads_kernel, dim3(grid), dim3(FO_THREADS), 0, s, a);

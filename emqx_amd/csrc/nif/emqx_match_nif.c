@@ -34,12 +34,14 @@ static ErlNifResourceType* RES_SUBTAB;
 static ErlNifResourceType* RES_BATCHER;
 static ErlNifResourceType* RES_PUB_BATCHER;
 static ErlNifResourceType* RES_RETAIN;
+static ErlNifResourceType* RES_COALESCER;
 
 typedef struct { emqx_engine* e; } engine_res;
 typedef struct { emqx_subtab* s; } subtab_res;
 typedef struct { emqx_batcher* b; engine_res* owner; } batcher_res;
 typedef struct { emqx_pub_batcher* b; engine_res* eng; subtab_res* tab; } pub_batcher_res;
 typedef struct { emqx_retain* r; } retain_res;
+typedef struct { emqx_coalescer* c; engine_res* eng; subtab_res* tab; } coalescer_res;
 
 static ERL_NIF_TERM ATOM_OK, ATOM_ERROR, ATOM_TRUE, ATOM_FALSE, ATOM_EINVAL, ATOM_ENOMEM, ATOM_DEVICE,
     ATOM_OVERFLOW, ATOM_NOTFOUND, ATOM_TOODEEP, ATOM_BUSY, ATOM_UNKNOWN, ATOM_FRESH, ATOM_RETRY;
@@ -93,6 +95,17 @@ static void pub_batcher_dtor(ErlNifEnv* env, void* obj) {
   r->eng = NULL;
 }
 
+static void coalescer_dtor(ErlNifEnv* env, void* obj) {
+  (void)env;
+  coalescer_res* r = (coalescer_res*)obj;
+  if (r->c) emqx_coalescer_destroy(r->c); /* commits and notifies what is pending */
+  r->c = NULL;
+  if (r->tab) enif_release_resource(r->tab);
+  if (r->eng) enif_release_resource(r->eng);
+  r->tab = NULL;
+  r->eng = NULL;
+}
+
 static void retain_dtor(ErlNifEnv* env, void* obj) {
   (void)env;
   retain_res* r = (retain_res*)obj;
@@ -100,11 +113,13 @@ static void retain_dtor(ErlNifEnv* env, void* obj) {
   r->r = NULL;
 }
 
-/* Packs a list of binaries into one buffer + offsets (malloc'd; caller frees). */
+/* Packs a list of binaries into one buffer + offsets (malloc'd; caller frees).  Returns 1, 0
+ * for a bad argument, -1 when out of memory (nothing to free in either failure). */
 static int pack_binaries(ErlNifEnv* env, ERL_NIF_TERM list, uint8_t** bytes, uint64_t** offs, unsigned* n_out) {
   unsigned n;
   if (!enif_get_list_length(env, list, &n)) return 0;
   *offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  if (!*offs) return -1;
   size_t total = 0;
   ERL_NIF_TERM head, tail = list;
   ErlNifBinary bin;
@@ -116,6 +131,10 @@ static int pack_binaries(ErlNifEnv* env, ERL_NIF_TERM list, uint8_t** bytes, uin
     total += bin.size;
   }
   *bytes = (uint8_t*)malloc(total ? total : 1);
+  if (!*bytes) {
+    free(*offs);
+    return -1;
+  }
   (*offs)[0] = 0;
   tail = list;
   for (unsigned i = 0; i < n; ++i) {
@@ -166,10 +185,16 @@ static ERL_NIF_TERM nif_insert(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   uint8_t* bytes;
   uint64_t* offs;
   unsigned n;
+  int pk = 0;
   (void)argc;
-  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !pack_binaries(env, argv[1], &bytes, &offs, &n))
-    return enif_make_badarg(env);
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || (pk = pack_binaries(env, argv[1], &bytes, &offs, &n)) != 1)
+    return pk < 0 ? err_term(env, EMQX_ENOMEM) : enif_make_badarg(env);
   uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!ids) {
+    free(bytes);
+    free(offs);
+    return err_term(env, EMQX_ENOMEM);
+  }
   int rc = emqx_insert_filters(r->e, bytes, offs, n, ids);
   ERL_NIF_TERM out = rc == EMQX_OK ? enif_make_tuple2(env, ATOM_OK, u32_list(env, ids, n)) : err_term(env, rc);
   free(ids);
@@ -186,6 +211,7 @@ static ERL_NIF_TERM nif_delete(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv
   if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
     return enif_make_badarg(env);
   uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!ids) return err_term(env, EMQX_ENOMEM);
   ERL_NIF_TERM head, tail = argv[1];
   for (unsigned i = 0; i < n; ++i) {
     if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_uint(env, head, &ids[i])) {
@@ -240,11 +266,16 @@ static ERL_NIF_TERM nif_match_batch(ErlNifEnv* env, int argc, const ERL_NIF_TERM
   unsigned mode, n;
   uint8_t* bytes;
   uint64_t* offs;
+  int pk = 0;
   (void)argc;
-  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !enif_get_uint(env, argv[1], &mode) ||
-      !pack_binaries(env, argv[2], &bytes, &offs, &n))
-    return enif_make_badarg(env);
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&r) || !enif_get_uint(env, argv[1], &mode) || (pk = pack_binaries(env, argv[2], &bytes, &offs, &n)) != 1)
+    return pk < 0 ? err_term(env, EMQX_ENOMEM) : enif_make_badarg(env);
   uint64_t* out_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  if (!out_off) {
+    free(bytes);
+    free(offs);
+    return err_term(env, EMQX_ENOMEM);
+  }
   match_call mc = {r->e, mode, bytes, offs, n, out_off};
   void* buf = NULL;
   uint64_t cap = 0, total = 0;
@@ -361,16 +392,70 @@ static ERL_NIF_TERM nif_new_subtab(ErlNifEnv* env, int argc, const ERL_NIF_TERM 
   return enif_make_tuple2(env, ATOM_OK, t);
 }
 
-/* subscribe(Subtab, [{FilterId, SubId, GroupId | none}], Add :: boolean()) -> ok
- * (emqx_broker:subscribe/3 and emqx_shared_sub's subscribe: one ETS / mria write each; the
- * commit patches only what these calls changed) */
-static ERL_NIF_TERM nif_subscribe(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  subtab_res* r;
+/* ---- route and subscription changes through the commit coalescer -------------------------
+ * One SUBSCRIBE is one ETS write in the reference (emqx_broker.erl:146-164), a new topic's route
+ * one mria transaction (emqx_router.erl:111-124); here every change of every caller is applied at
+ * once and committed with the others that arrive meanwhile (emqx_coalescer, group commit), and
+ * the caller gets {Ref, ok | {error, Reason}} when the commit carrying it has reached the device. */
+static void change_done(void* ctx, int status) {
+  waiter* w = (waiter*)ctx;
+  enif_send(NULL, &w->pid, w->env, enif_make_tuple2(w->env, w->ref, status == EMQX_OK ? ATOM_OK : err_term(w->env, status)));
+  enif_free_env(w->env);
+  enif_free(w);
+}
+
+static waiter* new_waiter(ErlNifEnv* env, ERL_NIF_TERM ref) {
+  waiter* w = (waiter*)enif_alloc(sizeof(waiter));
+  if (!w) return NULL;
+  enif_self(env, &w->pid);
+  w->env = enif_alloc_env();
+  w->ref = enif_make_copy(w->env, ref);
+  return w;
+}
+
+static void drop_waiter(waiter* w) {
+  enif_free_env(w->env);
+  enif_free(w);
+}
+
+/* new_coalescer(Eng, Subtab, MaxWaitUs) -> {ok, Ref} */
+static ERL_NIF_TERM nif_new_coalescer(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  engine_res* er;
+  subtab_res* sr;
+  unsigned max_wait;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_ENGINE, (void**)&er) ||
+      !enif_get_resource(env, argv[1], RES_SUBTAB, (void**)&sr) || !enif_get_uint(env, argv[2], &max_wait))
+    return enif_make_badarg(env);
+  coalescer_res* c = (coalescer_res*)enif_alloc_resource(RES_COALESCER, sizeof(coalescer_res));
+  c->eng = NULL;
+  c->tab = NULL;
+  int rc = emqx_coalescer_create(er->e, sr->s, max_wait, change_done, &c->c);
+  if (rc != EMQX_OK) {
+    c->c = NULL;
+    enif_release_resource(c);
+    return err_term(env, rc);
+  }
+  enif_keep_resource(er); /* the engine and the table outlive their coalescer */
+  enif_keep_resource(sr);
+  c->eng = er;
+  c->tab = sr;
+  ERL_NIF_TERM t = enif_make_resource(env, c);
+  enif_release_resource(c);
+  return enif_make_tuple2(env, ATOM_OK, t);
+}
+
+/* subscribe_async(Coal, [{FilterId, SubId, GroupId | none}], Add :: boolean(), Ref) -> ok; then
+ * {Ref, ok | {error, Reason}} once committed (emqx_broker:subscribe/3 and unsubscribe/1,
+ * emqx_broker.erl:124-195; emqx_shared_sub's subscribe / unsubscribe, emqx_shared_sub.erl:308-322) */
+static ERL_NIF_TERM nif_subscribe_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  coalescer_res* r;
   unsigned n;
   (void)argc;
-  if (!enif_get_resource(env, argv[0], RES_SUBTAB, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
+  if (!enif_get_resource(env, argv[0], RES_COALESCER, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
     return enif_make_badarg(env);
   uint32_t* f = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1) * 3);
+  if (!f) return err_term(env, EMQX_ENOMEM);
   uint32_t *s = f + n, *g = f + 2 * n;
   ERL_NIF_TERM head, tail = argv[1];
   for (unsigned i = 0; i < n; ++i) {
@@ -383,10 +468,62 @@ static ERL_NIF_TERM nif_subscribe(ErlNifEnv* env, int argc, const ERL_NIF_TERM a
     }
     if (!enif_get_uint(env, tup[2], &g[i])) g[i] = EMQX_NO_GROUP; /* 'none' */
   }
-  int rc = enif_is_identical(argv[2], ATOM_TRUE) ? emqx_subtab_add(r->s, f, s, g, n)
-                                                 : emqx_subtab_remove(r->s, f, s, g, n);
-  if (rc == EMQX_OK) rc = emqx_subtab_commit(r->s);
+  waiter* w = new_waiter(env, argv[3]);
+  if (!w) {
+    free(f);
+    return err_term(env, EMQX_ENOMEM);
+  }
+  int rc = emqx_coalescer_subscribe(r->c, f, s, g, n, enif_is_identical(argv[2], ATOM_TRUE), w);
   free(f);
+  if (rc != EMQX_OK) drop_waiter(w);
+  return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
+}
+
+/* route_add_async(Coal, [Filter], Ref) -> {ok, [Id]}; then {Ref, ok | {error, Reason}} once the
+ * filters are in the committed trie (emqx_trie:insert/1 via emqx_router_utils:insert_trie_route/2,
+ * emqx_router_utils.erl:33-50,97-125) */
+static ERL_NIF_TERM nif_route_add_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  coalescer_res* r;
+  uint8_t* bytes;
+  uint64_t* offs;
+  unsigned n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_COALESCER, (void**)&r)) return enif_make_badarg(env);
+  int pk = pack_binaries(env, argv[1], &bytes, &offs, &n);
+  if (pk < 0) return err_term(env, EMQX_ENOMEM);
+  if (!pk) return enif_make_badarg(env);
+  uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  waiter* w = ids ? new_waiter(env, argv[2]) : NULL;
+  int rc = w ? emqx_coalescer_insert_filters(r->c, bytes, offs, n, ids, w) : EMQX_ENOMEM;
+  if (rc != EMQX_OK && w) drop_waiter(w);
+  ERL_NIF_TERM out = rc == EMQX_OK ? enif_make_tuple2(env, ATOM_OK, u32_list(env, ids, n)) : err_term(env, rc);
+  free(ids);
+  free(bytes);
+  free(offs);
+  return out;
+}
+
+/* route_delete_async(Coal, [Id], Ref) -> ok; then {Ref, ok | {error, Reason}} (emqx_trie:delete/1
+ * via delete_trie_route/2, emqx_router_utils.erl:52-70) */
+static ERL_NIF_TERM nif_route_delete_async(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
+  coalescer_res* r;
+  unsigned n;
+  (void)argc;
+  if (!enif_get_resource(env, argv[0], RES_COALESCER, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
+    return enif_make_badarg(env);
+  uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!ids) return err_term(env, EMQX_ENOMEM);
+  ERL_NIF_TERM head, tail = argv[1];
+  for (unsigned i = 0; i < n; ++i) {
+    if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_uint(env, head, &ids[i])) {
+      free(ids);
+      return enif_make_badarg(env);
+    }
+  }
+  waiter* w = new_waiter(env, argv[2]);
+  int rc = w ? emqx_coalescer_delete_filters(r->c, ids, n, w) : EMQX_ENOMEM;
+  if (rc != EMQX_OK && w) drop_waiter(w);
+  free(ids);
   return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
 }
 
@@ -428,6 +565,12 @@ static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TE
   uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
   uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
   ErlNifBinary* bins = (ErlNifBinary*)malloc(sizeof(ErlNifBinary) * (n ? n : 1));
+  if (!offs || !keys || !bins) {
+    free(offs);
+    free(keys);
+    free(bins);
+    return err_term(env, EMQX_ENOMEM);
+  }
   ERL_NIF_TERM head, tail = argv[3];
   offs[0] = 0;
   for (unsigned i = 0; i < n; ++i) {
@@ -443,8 +586,16 @@ static ERL_NIF_TERM nif_publish_batch(ErlNifEnv* env, int argc, const ERL_NIF_TE
     offs[i + 1] = offs[i] + bins[i].size;
   }
   uint8_t* bytes = (uint8_t*)malloc(offs[n] ? offs[n] : 1);
-  for (unsigned i = 0; i < n; ++i) memcpy(bytes + offs[i], bins[i].data, bins[i].size);
   uint64_t* out_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  if (!bytes || !out_off) {
+    free(bytes);
+    free(out_off);
+    free(offs);
+    free(keys);
+    free(bins);
+    return err_term(env, EMQX_ENOMEM);
+  }
+  for (unsigned i = 0; i < n; ++i) memcpy(bytes + offs[i], bins[i].data, bins[i].size);
   /* deliveries: subscriber ids then filter ids, `cap` each (8 bytes per delivery); a topic
    * with more subscribers than the first guess overflows and is retried at the size the
    * engine reports (emqx_broker:publish/1 delivers to every subscriber, emqx_broker.erl:500-524) */
@@ -577,6 +728,7 @@ static ERL_NIF_TERM nif_forget_publishers(ErlNifEnv* env, int argc, const ERL_NI
   if (!enif_get_resource(env, argv[0], RES_SUBTAB, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
     return enif_make_badarg(env);
   uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!keys) return err_term(env, EMQX_ENOMEM);
   ERL_NIF_TERM head, tail = argv[1];
   for (unsigned i = 0; i < n; ++i) {
     if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_uint(env, head, &keys[i])) {
@@ -589,14 +741,15 @@ static ERL_NIF_TERM nif_forget_publishers(ErlNifEnv* env, int argc, const ERL_NI
   return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
 }
 
-/* subscriber_down(Subtab, [SubId]) -> ok: the subscribers' processes ended (the 'DOWN' that
- * emqx_shared_sub monitors, emqx_shared_sub.erl:347-350): a sticky pick leaves them at once;
- * their subscriptions are removed by the caller's cleanup as cleanup_down/1 does (:369-376). */
+/* subscriber_down(Coal, [SubId]) -> ok: the subscribers' processes ended (the 'DOWN' that
+ * emqx_shared_sub monitors, emqx_shared_sub.erl:347-350): a sticky pick leaves them from the next
+ * commit on, which the coalescer runs at once when idle; their subscriptions are removed by the
+ * caller's cleanup as cleanup_down/1 does (:369-376).  Does not wait for the commit. */
 static ERL_NIF_TERM nif_subscriber_down(ErlNifEnv* env, int argc, const ERL_NIF_TERM argv[]) {
-  subtab_res* r;
+  coalescer_res* r;
   unsigned n;
   (void)argc;
-  if (!enif_get_resource(env, argv[0], RES_SUBTAB, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
+  if (!enif_get_resource(env, argv[0], RES_COALESCER, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
     return enif_make_badarg(env);
   uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
   if (!ids) return err_term(env, EMQX_ENOMEM);
@@ -607,8 +760,7 @@ static ERL_NIF_TERM nif_subscriber_down(ErlNifEnv* env, int argc, const ERL_NIF_
       return enif_make_badarg(env);
     }
   }
-  int rc = emqx_subtab_set_alive(r->s, ids, n, 0);
-  if (rc == EMQX_OK) rc = emqx_subtab_commit(r->s);
+  int rc = emqx_coalescer_set_alive(r->c, ids, n, 0, NULL);
   free(ids);
   return rc == EMQX_OK ? ATOM_OK : err_term(env, rc);
 }
@@ -674,10 +826,10 @@ static ERL_NIF_TERM nif_retain_store(ErlNifEnv* env, int argc, const ERL_NIF_TER
   uint8_t* bytes;
   uint64_t* offs;
   unsigned n, ne;
+  int pk = 0;
   (void)argc;
-  if (!enif_get_resource(env, argv[0], RES_RETAIN, (void**)&r) || !enif_get_list_length(env, argv[2], &ne) ||
-      !pack_binaries(env, argv[1], &bytes, &offs, &n))
-    return enif_make_badarg(env);
+  if (!enif_get_resource(env, argv[0], RES_RETAIN, (void**)&r) || !enif_get_list_length(env, argv[2], &ne) || (pk = pack_binaries(env, argv[1], &bytes, &offs, &n)) != 1)
+    return pk < 0 ? err_term(env, EMQX_ENOMEM) : enif_make_badarg(env);
   if (ne != n) {
     free(bytes);
     free(offs);
@@ -685,6 +837,13 @@ static ERL_NIF_TERM nif_retain_store(ErlNifEnv* env, int argc, const ERL_NIF_TER
   }
   int64_t* exp = (int64_t*)malloc(sizeof(int64_t) * (n ? n : 1));
   uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!exp || !ids) {
+    free(exp);
+    free(ids);
+    free(bytes);
+    free(offs);
+    return err_term(env, EMQX_ENOMEM);
+  }
   ERL_NIF_TERM head, tail = argv[2];
   int ok = 1;
   for (unsigned i = 0; i < n && ok; ++i) {
@@ -714,6 +873,7 @@ static ERL_NIF_TERM nif_retain_delete(ErlNifEnv* env, int argc, const ERL_NIF_TE
   if (!enif_get_resource(env, argv[0], RES_RETAIN, (void**)&r) || !enif_get_list_length(env, argv[1], &n))
     return enif_make_badarg(env);
   uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  if (!ids) return err_term(env, EMQX_ENOMEM);
   ERL_NIF_TERM head, tail = argv[1];
   for (unsigned i = 0; i < n; ++i) {
     if (!enif_get_list_cell(env, tail, &head, &tail) || !enif_get_uint(env, head, &ids[i])) {
@@ -759,11 +919,16 @@ static ERL_NIF_TERM nif_retain_match(ErlNifEnv* env, int argc, const ERL_NIF_TER
   uint64_t* offs;
   unsigned n;
   ErlNifSInt64 now;
+  int pk = 0;
   (void)argc;
-  if (!enif_get_resource(env, argv[0], RES_RETAIN, (void**)&r) || !enif_get_int64(env, argv[2], &now) ||
-      !pack_binaries(env, argv[1], &bytes, &offs, &n))
-    return enif_make_badarg(env);
+  if (!enif_get_resource(env, argv[0], RES_RETAIN, (void**)&r) || !enif_get_int64(env, argv[2], &now) || (pk = pack_binaries(env, argv[1], &bytes, &offs, &n)) != 1)
+    return pk < 0 ? err_term(env, EMQX_ENOMEM) : enif_make_badarg(env);
   uint64_t* out_off = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+  if (!out_off) {
+    free(bytes);
+    free(offs);
+    return err_term(env, EMQX_ENOMEM);
+  }
   retain_call rc_ = {r->r, bytes, offs, n, (int64_t)now, out_off};
   void* buf = NULL;
   uint64_t cap = 0, total = 0;
@@ -853,6 +1018,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   RES_BATCHER = enif_open_resource_type(env, NULL, "emqx_match_batcher", batcher_dtor, fl, NULL);
   RES_PUB_BATCHER = enif_open_resource_type(env, NULL, "emqx_match_pub_batcher", pub_batcher_dtor, fl, NULL);
   RES_RETAIN = enif_open_resource_type(env, NULL, "emqx_match_retain", retain_dtor, fl, NULL);
+  RES_COALESCER = enif_open_resource_type(env, NULL, "emqx_match_coalescer", coalescer_dtor, fl, NULL);
   ATOM_OK = enif_make_atom(env, "ok");
   ATOM_ERROR = enif_make_atom(env, "error");
   ATOM_TRUE = enif_make_atom(env, "true");
@@ -867,7 +1033,7 @@ static int load(ErlNifEnv* env, void** priv, ERL_NIF_TERM info) {
   ATOM_UNKNOWN = enif_make_atom(env, "unknown");
   ATOM_FRESH = enif_make_atom(env, "fresh");
   ATOM_RETRY = enif_make_atom(env, "retry");
-  return RES_ENGINE && RES_SUBTAB && RES_BATCHER && RES_PUB_BATCHER && RES_RETAIN ? 0 : 1;
+  return RES_ENGINE && RES_SUBTAB && RES_BATCHER && RES_PUB_BATCHER && RES_RETAIN && RES_COALESCER ? 0 : 1;
 }
 
 /* Flags: DIRTY for every call that can wait on the device or on a lock held across device
@@ -884,7 +1050,10 @@ static ErlNifFunc nif_funcs[] = {
     {"new_batcher", 4, nif_new_batcher, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"match_async", 3, nif_match_async, 0},
     {"new_subtab", 1, nif_new_subtab, ERL_NIF_DIRTY_JOB_CPU_BOUND},
-    {"subscribe", 3, nif_subscribe, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"new_coalescer", 3, nif_new_coalescer, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"subscribe_async", 4, nif_subscribe_async, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_add_async", 3, nif_route_add_async, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"route_delete_async", 3, nif_route_delete_async, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"publish_batch", 4, nif_publish_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"new_pub_batcher", 5, nif_new_pub_batcher, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"publish_async", 4, nif_publish_async, 0},

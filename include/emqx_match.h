@@ -348,6 +348,35 @@ int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const 
                        uint64_t* out_offsets, uint32_t* out_subs, uint32_t* out_filters, uint64_t cap,
                        uint64_t* n_out);
 
+/* ---- commit coalescer -------------------------------------------------------------
+ * The per-call boundary for route and subscription changes.  The reference applies each one on
+ * its own: emqx_broker:subscribe/3 / unsubscribe/1 write ?SUBSCRIBER per call
+ * (emqx_broker.erl:124-195), emqx_shared_sub's handlers per call (emqx_shared_sub.erl:308-322),
+ * a topic's first / last subscriber adds / deletes its route in one mria transaction
+ * (emqx_router.erl:111-124 -> emqx_router_utils.erl:97-125).  Through a coalescer, a change is
+ * applied to the host store when the call returns (insert_filters writes ids_out), and
+ * cb(ctx, status) runs from the coalescer's thread once the commit that carries it has reached
+ * the device (ctx NULL: no callback).  The thread commits whenever changes are pending and it is
+ * idle — the changes that arrive during one commit make the next one — waiting max_wait_us
+ * after the first pending change when max_wait_us > 0.  Route changes commit before
+ * subscription changes in each round.  flush() returns when everything submitted before it is
+ * committed (the last commit's status); destroy() commits and notifies what is pending.
+ * stats out[0..5]: commits, changes, most changes in one commit, us spent committing, engine
+ * commits, subscription-table commits.  e or s may be NULL (then its calls return EINVAL). */
+typedef struct emqx_coalescer emqx_coalescer;
+typedef void (*emqx_done_cb)(void* ctx, int status);
+int emqx_coalescer_create(emqx_engine* e, emqx_subtab* s, uint32_t max_wait_us, emqx_done_cb cb,
+                          emqx_coalescer** out);
+int emqx_coalescer_insert_filters(emqx_coalescer* c, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                                  uint32_t* ids_out, void* ctx);
+int emqx_coalescer_delete_filters(emqx_coalescer* c, const uint32_t* ids, uint64_t n, void* ctx);
+int emqx_coalescer_subscribe(emqx_coalescer* c, const uint32_t* filter_ids, const uint32_t* sub_ids,
+                             const uint32_t* group_ids, uint64_t n, int add, void* ctx);
+int emqx_coalescer_set_alive(emqx_coalescer* c, const uint32_t* sub_ids, uint64_t n, int alive, void* ctx);
+int emqx_coalescer_flush(emqx_coalescer* c);
+int emqx_coalescer_destroy(emqx_coalescer* c);
+int emqx_coalescer_stats(emqx_coalescer* c, uint64_t* out, uint32_t n);
+
 /* ---- pinned publish batches (the NIF's publish buffers) ---------------------------
  * The publish counterpart of emqx_host_batch: pinned inputs (topics, per-message keys) and
  * pinned outputs (the delivery CSR).  submit() enqueues, on the batch's own stream with no host

@@ -90,7 +90,8 @@ def test_integration_exports_are_bound():
     text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     m = re.search(r"-export\(\[(.*?)\]\)\.", text, re.S)
     exports = {(n, int(a)) for n, a in re.findall(r"(\w+)/(\d+)", m.group(1))}
-    wrappers = {("match", 2), ("publish", 3)}  # Erlang wrappers over the async NIFs
+    # Erlang wrappers over the async NIFs
+    wrappers = {("match", 2), ("publish", 3), ("subscribe", 3), ("route_add", 2), ("route_delete", 2)}
     funcs = set(nif_funcs())
     missing = sorted(exports - wrappers - funcs)
     assert not missing, missing
@@ -107,6 +108,21 @@ def test_batcher_never_waits_when_busy(tmp_path):
                     "-I", os.path.join(ROOT, "include"), "-o", str(exe),
                     os.path.join(ROOT, "tests/c/test_batcher_busy.cpp"),
                     os.path.join(ROOT, "emqx_amd/csrc/batcher.cpp")], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "ok"
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_commit_coalescer_group_commits(tmp_path):
+    """emqx_amd/csrc/coalescer.cpp against a fake engine / subscription table: callbacks only after
+    the commit that carries the change, group commit, routes before subscriptions, failures
+    reported, destroy drains (tests/c/test_coalescer.cpp)."""
+    exe = tmp_path / "test_coalescer"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-pthread",
+                    "-I", os.path.join(ROOT, "include"), "-o", str(exe),
+                    os.path.join(ROOT, "tests/c/test_coalescer.cpp"),
+                    os.path.join(ROOT, "emqx_amd/csrc/coalescer.cpp")], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip() == "ok"
