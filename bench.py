@@ -93,7 +93,7 @@ def main():
                          "prints per-variant kernel/call times instead of the bench line")
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", action="store_true", help="one extra call with kernel counters, added as 'diag'")
-    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R", "L", "P", "S"],
+    ap.add_argument("--workload", type=str, default="B", choices=["A", "B", "D", "E", "U", "R", "L", "P", "S", "T"],
                     help="B = the headline (BASELINE configs[1]); A = configs[0]'s 100k-filter table, "
                          "D = the adversarial depth-16 table (configs[3], 1M-topic batches), "
                          "E = publish fan-out (configs[4]): match + fan-out per step, "
@@ -104,7 +104,9 @@ def main():
                          "B's table, P = the drop-in emqx_broker:publish/1 path: concurrent single-message "
                          "callers through the publish batcher (match + fan-out) on config E's 10M "
                          "subscriptions, S = subscription churn: subscribe/unsubscribe ops committed to "
-                         "config E's 10M-subscription table")
+                         "config E's 10M-subscription table, T = the per-call subscribe / route boundary: "
+                         "closed-loop callers through the commit coalescer on config E's tables, single-op "
+                         "latency, throughput at --callers, and P's throughput during a subscribe storm")
     ap.add_argument("--callers", type=str, default="64,512,4096",
                     help="--workload L: concurrent single-topic callers per run")
     ap.add_argument("--max-batch", type=int, default=4096, help="--workload L: batcher max_batch")
@@ -193,6 +195,8 @@ def main():
         return pub_batcher_bench(args, rank, world, dev)
     if args.workload == "S":
         return subscribe_bench(args, rank, world, dev)
+    if args.workload == "T":
+        return storm_bench(args, rank, world, dev)
     if args.workload == "A":
         wl = load_or_make(args, rank, lambda: W.config_a(n_topics=args.batch, seed=1 if rank == 0 else 1000 + rank))
     elif args.workload == "D":
@@ -715,6 +719,88 @@ def pub_batcher_bench(args, rank, world, dev):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         args.cpu_sample = min(args.cpu_sample, 200_000)
         res["cpu_baseline"] = fanout_cpu_baseline(fw, args)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def storm_bench(args, rank, world, dev):
+    """The per-call boundary for subscription and route changes: EMQX applies each
+    SUBSCRIBE as its own ETS write (emqx_broker.erl:124-164) and each new topic's route as its own
+    mria transaction (emqx_router.erl:111-124, emqx_router_utils.erl:97-125).  Here closed-loop
+    callers (tools/batch_load.cpp sub_load) subscribe / unsubscribe one (filter, subscriber) pair
+    per call, or add / delete one route per call, through the commit coalescer
+    (emqx_coalescer_*: group commit; a call returns when the commit carrying it has reached the
+    device) on config E's tables (2M filters, 10M subscriptions).  Reports single-op latency
+    (1 caller), ops/s and latency at --callers, and the publish batcher's throughput (P, 512
+    callers, round_robin) alone and while 512 callers subscribe and unsubscribe."""
+    import ctypes
+    import threading
+    from emqx_amd import _lib
+    from emqx_amd.fanout import STRATEGIES
+    fw, eng, st, _ = config_e_tables(args, rank, dev)
+    L = ctypes.CDLL(os.path.join(ROOT, "tools", "_build", "libbatchload.so"))
+    L.sub_load.restype = ctypes.c_int
+    L.sub_load.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                           ctypes.c_int, ctypes.c_uint32, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+    L.pub_load.restype = ctypes.c_int
+    L.pub_load.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                           ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+    nf = int(fw.wl.n_filters)
+    first_sub = int(fw.sub_id.max()) + 1
+
+    def sub_run(callers, route=0, dur_ms=2000.0, base=first_sub):
+        out = np.zeros(13, dtype=np.float64)
+        rc = L.sub_load(eng._h, st.handle, callers, nf, base, route, 0, 300.0, dur_ms, out.ctypes.data)
+        if rc != 0:
+            raise SystemExit(f"sub_load failed: {rc} ({_lib.lib().emqx_strerror(rc).decode()})")
+        r = {"callers": callers, "op": "route add/delete" if route else "subscribe/unsubscribe",
+             "ops_per_s": round(out[0] / out[1], 1), "p50_us": round(out[2], 1), "p90_us": round(out[3], 1),
+             "p99_us": round(out[4], 1), "max_us": round(out[5], 1), "commits": int(out[6]),
+             "ops_per_commit": round(out[7], 1), "us_per_commit": round(out[12], 1)}
+        log(f"[rank {rank}] {r}")
+        return r
+
+    tb, to = fw.wl.topics
+    to = np.ascontiguousarray(to.astype(np.uint64))
+    keys = np.ascontiguousarray(fw.keys.astype(np.uint32))
+    strat = STRATEGIES["round_robin"]
+
+    def pub_run(callers, dur_ms=2000.0):
+        out = np.zeros(13, dtype=np.float64)
+        rc = L.pub_load(eng._h, st.handle, strat, tb.ctypes.data, to.ctypes.data, keys.ctypes.data, fw.wl.n_topics,
+                        callers, args.max_batch, 200, 500.0, dur_ms, out.ctypes.data)
+        if rc != 0:
+            raise SystemExit(f"pub_load failed: {rc} ({_lib.lib().emqx_strerror(rc).decode()})")
+        return {"callers": callers, "messages_per_s": round(out[0] / out[1], 1), "p50_us": round(out[2], 1),
+                "p99_us": round(out[4], 1)}
+
+    single_sub = sub_run(1)
+    single_route = sub_run(1, route=1)
+    storms = [sub_run(int(c)) for c in args.callers.split(",")]
+    p_alone = pub_run(512)
+    storm_box = {}
+
+    def storm():
+        storm_box["r"] = sub_run(512, dur_ms=3500.0, base=first_sub + 100_000)
+
+    th = threading.Thread(target=storm)
+    th.start()
+    time.sleep(0.5)
+    p_storm = pub_run(512)
+    th.join()
+    p_storm["storm"] = storm_box.get("r")
+    best = storms[-1]
+    res = {"metric": "per-call subscribe/unsubscribe operations committed/sec through the commit coalescer "
+                     "(config E, 10M subscriptions)",
+           "value": best["ops_per_s"], "unit": "ops/s", "n_gpus": world, "steps": len(storms) + 4, "warmup": 1,
+           "ms_per_step": 2000.0, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+           "data": "synthetic",
+           "config": {"workload": "T: closed-loop per-call subscribe / route changes -> emqx_coalescer (group "
+                                  "commit) on config E's tables; P beside it", "n_filters": nf,
+                      "subscriptions": fw.n_subscriptions, "callers": args.callers, "parallelism": "replicated tables"},
+           "single_op": {"subscribe": single_sub, "route_add_delete": single_route},
+           "storm": storms, "publish_alone": p_alone, "publish_during_storm": p_storm}
     if rank == 0:
         print(json.dumps(res), flush=True)
 

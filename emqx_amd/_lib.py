@@ -40,7 +40,7 @@ EXPORTS = (
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
     "emqx_subtab_stats", "emqx_subtab_commit_stats", "emqx_subtab_forget_publishers", "emqx_subtab_set_alive",
     "emqx_share_repick", "emqx_coalescer_create", "emqx_coalescer_insert_filters", "emqx_coalescer_delete_filters",
-    "emqx_coalescer_subscribe", "emqx_coalescer_set_alive", "emqx_coalescer_flush", "emqx_coalescer_destroy",
+    "emqx_coalescer_subscribe", "emqx_coalescer_subscribe_many", "emqx_coalescer_set_alive", "emqx_coalescer_flush", "emqx_coalescer_destroy",
     "emqx_coalescer_stats",
     "emqx_fanout_batch_device", "emqx_fanout_batch_device_async", "emqx_publish_batch",
     "emqx_pub_batch_create", "emqx_pub_batch_destroy", "emqx_pub_batch_reserve", "emqx_pub_batch_submit",
@@ -203,6 +203,7 @@ def lib():
         "emqx_coalescer_insert_filters": (i32, [vp, vp, vp, u64, vp, vp]),
         "emqx_coalescer_delete_filters": (i32, [vp, vp, u64, vp]),
         "emqx_coalescer_subscribe": (i32, [vp, vp, vp, vp, u64, i32, vp]),
+        "emqx_coalescer_subscribe_many": (i32, [vp, vp, vp, vp, vp, u64, vp]),
         "emqx_coalescer_set_alive": (i32, [vp, vp, u64, i32, vp]),
         "emqx_coalescer_flush": (i32, [vp]),
         "emqx_coalescer_destroy": (i32, [vp]),

@@ -140,6 +140,36 @@ int emqx_coalescer_subscribe(emqx_coalescer* c, const uint32_t* filter_ids, cons
   });
 }
 
+int emqx_coalescer_subscribe_many(emqx_coalescer* c, const uint32_t* filter_ids, const uint32_t* sub_ids,
+                                  const uint32_t* group_ids, const uint8_t* adds, uint64_t n, void* const* ctxs) {
+  if (!c || !c->s || (n && (!filter_ids || !sub_ids || !adds))) return EMQX_EINVAL;
+  if (n == 0) return EMQX_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->stop) return EMQX_EINVAL;
+  // runs of the same kind, one table call each; all or nothing is not promised across runs, so
+  // the contexts of the runs applied are queued before an error returns
+  uint64_t i = 0;
+  int rc = EMQX_OK;
+  while (i < n && rc == EMQX_OK) {
+    uint64_t j = i + 1;
+    while (j < n && (adds[j] != 0) == (adds[i] != 0)) ++j;
+    const uint32_t* gr = group_ids ? group_ids + i : nullptr;
+    rc = adds[i] ? emqx_subtab_add(c->s, filter_ids + i, sub_ids + i, gr, j - i)
+                 : emqx_subtab_remove(c->s, filter_ids + i, sub_ids + i, gr, j - i);
+    if (rc != EMQX_OK) break;
+    if (c->seq_submitted == c->seq_done) c->first_at = Clock::now();
+    if (ctxs)
+      for (uint64_t k = i; k < j; ++k)
+        if (ctxs[k]) c->pending.push_back(ctxs[k]);
+    c->pending_ops += j - i;
+    c->sub_dirty = true;
+    ++c->seq_submitted;
+    i = j;
+  }
+  c->cv.notify_one();
+  return rc;
+}
+
 int emqx_coalescer_set_alive(emqx_coalescer* c, const uint32_t* sub_ids, uint64_t n, int alive, void* ctx) {
   if (!c || !c->s) return EMQX_EINVAL;
   return submit(c, n, false, ctx, [&] { return emqx_subtab_set_alive(c->s, sub_ids, n, alive); });

@@ -216,6 +216,7 @@ struct FoScratch {
   uint64_t sort_temp_bytes = 0;
   uint32_t* run_ent = nullptr;  // per run id (pk_cap)
   uint32_t* run_cnt = nullptr;  // per run id (pk_cap): picks per run (small path)
+  uint32_t* run_named = nullptr;  // [FO_BLOCKS] per probe block: runs named
   unsigned long long* multi = nullptr;  // [FO_MULTI_CAP] (small path)
   unsigned long long* seg = nullptr;
   uint32_t* seg_from = nullptr;
@@ -236,6 +237,7 @@ struct FoScratch {
     fo_free(sort_temp);
     fo_free(run_ent);
     fo_free(run_cnt);
+    fo_free(run_named);
     fo_free(multi);
     fo_free(seg);
     fo_free(seg_from);
@@ -878,6 +880,7 @@ int stateful_scratch(emqx_subtab* s, FoScratch* c, uint64_t m_cap, uint64_t cap)
     c->stamp = 0;
   }
   if (!c->multi) FO_TRY(fo_alloc(c->multi, FO_MULTI_CAP));
+  if (!c->run_named) FO_TRY(fo_alloc(c->run_named, FO_BLOCKS));
   if (++c->stamp == 0) {  // stamps wrapped: no tag may look current
     FO_TRY(hipMemsetAsync(c->tag, 0, s->ps_cap * sizeof(unsigned long long), c->stream));
     c->stamp = 1;
@@ -935,6 +938,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
     a.tag = c->tag;
     a.stamp = c->stamp;
     a.run_ent = c->run_ent;
+    a.run_named = c->run_named;
     a.seg = c->seg;
     a.seg_from = c->seg_from;
     // the small resolve path (no sort) unless the last finished call had many picks per run:

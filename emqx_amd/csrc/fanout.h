@@ -48,10 +48,9 @@ constexpr uint32_t PS_MAX_PROBES = 64;
 // Per-call control words of one scratch (memset per call).
 constexpr uint32_t FO_CTL_PICKS = 0;  // round_robin / sticky picks of the call (the pick list's length)
 constexpr uint32_t FO_CTL_FLAGS = 1;  // FO_SUM_F_* bits raised by the kernels
-constexpr uint32_t FO_CTL_RUNS = 2;   // run ids handed out (one per state entry the call touches)
+constexpr uint32_t FO_CTL_SPARE = 2;
 constexpr uint32_t FO_CTL_MULTI = 3;  // small path: picks of runs with more than one pick
-constexpr uint32_t FO_CTL_NAMED = 4;  // runs of the call (state entries it touches)
-constexpr uint32_t FO_CTL_WORDS = 5;
+constexpr uint32_t FO_CTL_WORDS = 4;
 // Small resolve path: at most this many picks in runs of more than one pick (sorted in LDS).
 constexpr uint32_t FO_MULTI_CAP = 4096;
 
@@ -77,13 +76,15 @@ struct FanoutArgs {
   uint64_t ps_mask;
   // the call's pick list (round_robin / sticky): one (run, output position) pair per $share pick,
   // written in output order, then stably sorted by run.  A run is the call's picks of one
-  // (group slot, publisher) state entry, named by a small per-call id (so the sort reads few
-  // key bits); run ids are < pk_cap - 1, and pk_cap - 1 pads the list past the call's picks.
+  // (group slot, publisher) state entry, named by the list index of its first pick to be probed
+  // (so ids are < picks <= pk_cap - 1, few key bits), and pk_cap - 1 pads the list past the
+  // call's picks.
   uint32_t* gchunk;          // [ceil(m_cap / FO_WCHUNK)] $share groups per chunk of FO_WCHUNK entries
-  uint32_t* pk_keys;         // [pk_cap] run id
+  uint32_t* pk_keys;         // [pk_cap] run id (written by the probe)
   uint32_t* pk_vals;         // [pk_cap] output position
-  uint32_t* pk_skeys;        // [pk_cap] sorted keys (resolve); before the sort: the pick's group record
-  uint32_t* pk_svals;        // [pk_cap] their positions; before the sort: the pick's publisher
+  uint32_t* pk_skeys;        // [pk_cap] sorted keys (large path); before: the pick's group record
+  uint32_t* pk_svals;        // [pk_cap] their positions (large path); before: the pick's publisher,
+                             // then (probe) its state entry
   uint64_t pk_cap;
   unsigned long long* tag;   // [ps_mask + 1] per state entry: call stamp << 32 | its run id in that call
   uint32_t stamp;            // this call's stamp (never 0)
@@ -91,6 +92,7 @@ struct FanoutArgs {
   unsigned long long* seg;   // [pk_cap] per run: first list index | first pick << 32
   uint32_t* seg_from;        // [pk_cap] sticky: list index from which the run's pick is constant
   uint32_t* run_cnt;         // small path ([pk_cap], zeroed per call): picks per run; null: large path
+  uint32_t* run_named;       // [FO_BLOCKS] runs named per block of the probe kernel
   unsigned long long* multi; // small path [FO_MULTI_CAP]: run << 32 | list index of multi-pick runs' picks
   unsigned long long* ctl;   // [FO_CTL_WORDS]
   unsigned long long* ps_seen;  // host-mapped [4]: live keys, tombstones, picks, runs of the last finished call

@@ -434,11 +434,12 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
           sub[u] = pick_stateless(a, GroupRec{gr.x, gr.y, gr.z, gr.w}, e0 + k, L.top[k], gidx);
           continue;
         }
-        // round_robin / sticky: the pick is made after the write by the probe / sort / resolve
-        // kernels, which take each (slot, publisher) entry's picks in message order.  The output
-        // holds the group record until then; the pick goes to the list at its place in output
-        // order (the entry's first pick-list index + its group's rank in the entry) as
-        // {position, group record, publisher}.
+        // round_robin / sticky: the pick is made after the write by the probe / resolve kernels,
+        // which take each (slot, publisher) entry's picks in message order.  The output holds the
+        // group record until then; the pick goes to the list at its place in output order (the
+        // entry's first pick-list index + its group's rank in the entry) as {position, group
+        // record, publisher} (the group's record is not loaded here: the probe kernel reads its
+        // slot off this kernel's critical path).
         const uint32_t li = L.go[k] + (rr[u] - L.np[k]);
         a.pk_vals[li] = static_cast<uint32_t>(obase + j0 + lane + 64u * u);
         a.pk_skeys[li] = gidx;
@@ -460,15 +461,20 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
 
 // The pick list's runs: per pick, the (group slot, publisher) entry of the state table (inserted
 // when absent; in parallel over the list, off the write kernel's critical path) and the call's
-// run id of that entry (the first pick to see the entry in this call names the run; ids are
-// handed out one atomic per wave); past the call's picks the pad key pk_cap - 1, which sorts
-// last.  run_cnt (small path): picks per run.
+// run id of that entry: the list index of the first pick that names it (no counter, no atomics
+// on a shared word); past the call's picks the pad key pk_cap - 1, which sorts last.  run_cnt
+// (small path): picks per run.  Runs named, per block, to run_named[block] (the finish kernel
+// adds them up).  A fixed grid of at most FO_BLOCKS blocks strides over the list.
 __global__ __launch_bounds__(FO_THREADS) void fanout_pick_probe_kernel(FanoutArgs a) {
-  if (a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS | FO_SUM_F_MATCH)) return;
+  __shared__ uint32_t s_named[FO_THREADS / 64];
+  if (a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS | FO_SUM_F_MATCH)) {
+    if (threadIdx.x == 0) a.run_named[blockIdx.x] = 0;
+    return;
+  }
   const uint64_t S = a.ctl[FO_CTL_PICKS];
   const uint32_t pad = static_cast<uint32_t>(a.pk_cap - 1);
-  const uint32_t lane = fo_lane();
   const uint64_t stride = uint64_t(gridDim.x) * FO_THREADS;
+  uint32_t named = 0;
   for (uint64_t i0 = blockIdx.x * uint64_t(FO_THREADS); i0 < a.pk_cap; i0 += stride) {
     const uint64_t i = i0 + threadIdx.x;
     const bool pick = i < S;
@@ -478,40 +484,37 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_pick_probe_kernel(FanoutArg
       const uint32_t slot = a.groups[a.pk_skeys[i]].slot;
       ent = ps_find_or_insert(a, (uint64_t(slot) << 32) | a.pk_svals[i], &created);
       if (ent == PS_EMPTY) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(FO_SUM_F_STATE_FULL));
+      a.pk_svals[i] = static_cast<uint32_t>(ent);  // (the small path reads a pick's entry here)
     }
     wave_count(a.ps_count, created);
-    unsigned long long cur = 0;
-    if (ent != PS_EMPTY) cur = __hip_atomic_load(a.tag + ent, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool fresh = ent != PS_EMPTY && static_cast<uint32_t>(cur >> 32) != a.stamp;
-    // new run ids for the wave's lanes that saw no run yet: one atomic per wave
-    const uint64_t m = __ballot(fresh);
-    uint32_t id = 0;
-    if (m) {
-      const uint32_t leader = __ffsll(static_cast<long long>(m)) - 1;
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(a.ctl + FO_CTL_RUNS, static_cast<unsigned long long>(__popcll(m)));
-      base = __shfl(base, leader, 64);
-      id = static_cast<uint32_t>(base) + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1)));
-    }
     uint32_t key = pad;
     if (ent != PS_EMPTY) {
-      if (!fresh) {
+      unsigned long long* t = a.tag + ent;
+      const unsigned long long cur = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (static_cast<uint32_t>(cur >> 32) == a.stamp) {
         key = static_cast<uint32_t>(cur);
       } else {
-        const unsigned long long mine = (static_cast<unsigned long long>(a.stamp) << 32) | id;
-        const unsigned long long prev = atomicCAS(a.tag + ent, cur, mine);
+        const unsigned long long mine = (static_cast<unsigned long long>(a.stamp) << 32) | static_cast<uint32_t>(i);
+        const unsigned long long prev = atomicCAS(t, cur, mine);
         if (prev == cur) {
-          key = id;
-          a.run_ent[id] = static_cast<uint32_t>(ent);
+          key = static_cast<uint32_t>(i);
+          a.run_ent[i] = static_cast<uint32_t>(ent);
+          ++named;
         } else {
           key = static_cast<uint32_t>(prev);  // another pick of this call named the run first
         }
       }
       if (a.run_cnt) atomicAdd(a.run_cnt + key, 1u);
     }
-    // runs named (ids handed out to lanes that lost the naming race are not runs)
-    wave_count(a.ctl + FO_CTL_NAMED, ent != PS_EMPTY && fresh && key == id);
     if (i < a.pk_cap) a.pk_keys[i] = key;
+  }
+  const uint32_t wn = static_cast<uint32_t>(fo_wave_sum(named));
+  if (fo_lane() == 0) s_named[threadIdx.x >> 6] = wn;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < FO_THREADS / 64; ++k) t += s_named[k];
+    a.run_named[blockIdx.x] = t;
   }
 }
 
@@ -706,13 +709,13 @@ __global__ __launch_bounds__(1024) void fanout_resolve_small_kernel(FanoutArgs a
     }
     return;
   }
-  // the other blocks: runs of one pick
+  // the other blocks: runs of one pick (the pick's entry, group record and position were left
+  // in the list by the write and probe kernels: no chain through out_subs / run_ent)
   for (uint64_t i = (blockIdx.x - 1) * 1024ull + threadIdx.x; i < S; i += uint64_t(gridDim.x - 1) * 1024) {
     const uint32_t k = a.pk_keys[i];
+    const uint32_t ent = a.pk_svals[i], gidx = a.pk_skeys[i], pos = a.pk_vals[i];
     if (k + 1 >= a.pk_cap || a.run_cnt[k] != 1) continue;
-    const uint32_t ent = a.run_ent[k];
-    const uint32_t pos = a.pk_vals[i];
-    const GroupRec g = fo_group(a, a.out_subs[pos]);
+    const GroupRec g = fo_group(a, gidx);
     uint32_t val = a.ps_vals[ent];
     bool retry = false;
     const uint32_t sub = sticky ? sticky_step(a, g, &val, pos, ent, &retry) : rr_step(a, g, &val, pos, ent);
@@ -721,7 +724,19 @@ __global__ __launch_bounds__(1024) void fanout_resolve_small_kernel(FanoutArgs a
   }
 }
 
-__global__ void fanout_finish_kernel(FanoutArgs a) {
+// One block of FO_THREADS: the call summary's state words; stateful calls add up the probe
+// kernel's per-block run counts.
+__global__ __launch_bounds__(FO_THREADS) void fanout_finish_kernel(FanoutArgs a, uint32_t probe_blocks) {
+  uint64_t named = 0;
+  if (a.run_named)
+    for (uint32_t b = threadIdx.x; b < probe_blocks; b += FO_THREADS) named += a.run_named[b];
+  named = fo_wave_sum(named);
+  __shared__ uint64_t s_n[FO_THREADS / 64];
+  if (fo_lane() == 0) s_n[threadIdx.x >> 6] = named;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  named = 0;
+  for (uint32_t k = 0; k < FO_THREADS / 64; ++k) named += s_n[k];
   const unsigned long long c = *a.ps_count;
   a.summary[FO_SUM_STATE] = c;
   a.summary[FO_SUM_FLAGS] |= a.ctl[FO_CTL_FLAGS];
@@ -729,7 +744,7 @@ __global__ void fanout_finish_kernel(FanoutArgs a) {
     a.ps_seen[0] = c;
     a.ps_seen[1] = *a.ps_tombs;
     a.ps_seen[2] = a.ctl[FO_CTL_PICKS];
-    a.ps_seen[3] = a.ctl[FO_CTL_NAMED];
+    a.ps_seen[3] = named;
   }
   __threadfence_system();
 }
@@ -863,6 +878,11 @@ uint32_t grid_for(uint64_t items, uint32_t per_block) {
   return static_cast<uint32_t>(g < 1 ? 1 : (g > 65536 ? 65536 : g));
 }
 
+uint32_t probe_blocks(uint64_t pk_cap) {
+  const uint32_t g = grid_for(pk_cap, FO_THREADS);
+  return g < FO_BLOCKS ? g : FO_BLOCKS;
+}
+
 // ---- incremental commits of the subscription table ----------------------------------------
 __global__ __launch_bounds__(256) void subtab_word_patch_kernel(uint32_t* plain, uint32_t* members, uint32_t* alive,
                                                                 const WordPatch* wp, uint64_t n_plain,
@@ -952,9 +972,9 @@ hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s) {
   hipLaunchKernelGGL(fanout_write_kernel, dim3(grid_for(m_cap, FO_WCHUNK * (FO_THREADS / 64))), dim3(FO_THREADS), 0, s,
                      a);
   if (fo_stateful(a.strategy))
-    hipLaunchKernelGGL(fanout_pick_probe_kernel, dim3(grid_for(a.pk_cap, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
+    hipLaunchKernelGGL(fanout_pick_probe_kernel, dim3(probe_blocks(a.pk_cap)), dim3(FO_THREADS), 0, s, a);
   else
-    hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(1), 0, s, a);
+    hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(FO_THREADS), 0, s, a, 0u);
   return hipGetLastError();
 }
 
@@ -981,8 +1001,8 @@ uint64_t fanout_sort_temp_bytes(uint64_t pk_cap) {
 hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t sort_temp_bytes, hipStream_t s) {
   if (a.run_cnt) {  // small path
     hipLaunchKernelGGL(fanout_pick_classify_kernel, dim3(grid_for(a.pk_cap, FO_THREADS * 4)), dim3(FO_THREADS), 0, s, a);
-    hipLaunchKernelGGL(fanout_resolve_small_kernel, dim3(1 + grid_for(a.pk_cap, 1024 * 4)), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(1), 0, s, a);
+    hipLaunchKernelGGL(fanout_resolve_small_kernel, dim3(1 + grid_for(a.pk_cap, 1024)), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(FO_THREADS), 0, s, a, probe_blocks(a.pk_cap));
     return hipGetLastError();
   }
   // large path: stable by run: each run keeps output (message) order; the pad sorts last
@@ -994,7 +1014,7 @@ hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t 
   const uint32_t grid = grid_for(a.pk_cap, FO_THREADS * 4);
   hipLaunchKernelGGL(fanout_resolve_heads_kernel, dim3(grid), dim3(FO_THREADS), 0, s, a);
   hipLaunchKernelGGL(fanout_resolve_apply_kernel, dim3(grid), dim3(FO_THREADS), 0, s, a);
-  hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(1), 0, s, a);
+  hipLaunchKernelGGL(fanout_finish_kernel, dim3(1), dim3(FO_THREADS), 0, s, a, probe_blocks(a.pk_cap));
   return hipGetLastError();
 }
 

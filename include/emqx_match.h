@@ -372,6 +372,10 @@ int emqx_coalescer_insert_filters(emqx_coalescer* c, const uint8_t* bytes, const
 int emqx_coalescer_delete_filters(emqx_coalescer* c, const uint32_t* ids, uint64_t n, void* ctx);
 int emqx_coalescer_subscribe(emqx_coalescer* c, const uint32_t* filter_ids, const uint32_t* sub_ids,
                              const uint32_t* group_ids, uint64_t n, int add, void* ctx);
+/* n changes of n callers under one lock (a NIF draining a scheduler's queue of SUBSCRIBEs):
+ * change i subscribes (adds[i] != 0) or unsubscribes, and ctxs[i] (or NULL) is called back. */
+int emqx_coalescer_subscribe_many(emqx_coalescer* c, const uint32_t* filter_ids, const uint32_t* sub_ids,
+                                  const uint32_t* group_ids, const uint8_t* adds, uint64_t n, void* const* ctxs);
 int emqx_coalescer_set_alive(emqx_coalescer* c, const uint32_t* sub_ids, uint64_t n, int alive, void* ctx);
 int emqx_coalescer_flush(emqx_coalescer* c);
 int emqx_coalescer_destroy(emqx_coalescer* c);

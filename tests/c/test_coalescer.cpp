@@ -177,6 +177,32 @@ int main() {
     CHECK(g_log[log_before] == "S1" && g_log[log_before + 1] == "S200");
   }
 
+  // 2b. many callers' changes under one call: runs of adds and removes, every context called back
+  //     after the one commit that carries them all
+  {
+    gate_set(false);
+    Done hold;
+    CHECK(emqx_coalescer_subscribe(c, &f, &sub, nullptr, 1, 1, &hold) == EMQX_OK);
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    std::vector<Done> ds(7);
+    const uint32_t fs[7] = {1, 2, 3, 4, 5, 6, 7}, ss[7] = {1, 2, 3, 4, 5, 6, 7};
+    const uint8_t adds[7] = {1, 1, 0, 0, 1, 0, 1};
+    void* ctxs[7];
+    for (int i = 0; i < 7; ++i) ctxs[i] = &ds[i];
+    ctxs[3] = nullptr;  // a change nobody waits for
+    CHECK(emqx_coalescer_subscribe_many(c, fs, ss, nullptr, adds, 7, ctxs) == EMQX_OK);
+    size_t log_before;
+    {
+      std::lock_guard<std::mutex> g(g_mu);
+      log_before = g_log.size();
+    }
+    gate_set(true);
+    CHECK(emqx_coalescer_flush(c) == EMQX_OK);
+    for (int i = 0; i < 7; ++i) CHECK(ds[i].calls == (i == 3 ? 0 : 1));
+    std::lock_guard<std::mutex> g(g_mu);
+    CHECK(g_log.size() == log_before + 2 && g_log[log_before + 1] == "S7");
+  }
+
   // 3. a round with both kinds: engine first
   Done a, b;
   CHECK(emqx_coalescer_subscribe(c, &f, &sub, nullptr, 1, 1, &a) == EMQX_OK);

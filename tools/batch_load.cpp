@@ -12,9 +12,17 @@
 // each caller's message key (the phash2 key of the hash strategies, or the caller's own
 // publisher handle for round_robin / sticky).
 //
+// sub_load drives the commit coalescer (emqx_coalescer_*) the same way: each caller in a closed
+// loop subscribes to a filter, waits until the commit carrying it has reached the device,
+// unsubscribes, waits, ... (emqx_broker:subscribe/3 / unsubscribe/1 per call from each channel,
+// emqx_broker.erl:124-195), or, with route_ops, adds a new topic's route and deletes it
+// (emqx_router.erl:111-124 -> the trie).  It has its own globals, so a pub_load may run beside it
+// (publishes during a subscribe storm).
+//
 // Built by __graft_entry__.build() into tools/_build/libbatchload.so; the emqx_batcher_*
 // symbols resolve against libemqxmatch.so, which the caller has loaded (RTLD_GLOBAL).
 #include <stdint.h>
+#include <stdio.h>
 
 #include <algorithm>
 #include <atomic>
@@ -44,13 +52,29 @@ struct Load {
   uint32_t D = 1;
 };
 
-Load* g_load = nullptr;  // the run in progress (one at a time)
+Load* g_load = nullptr;   // the batcher run in progress (one at a time)
+Load* g_sload = nullptr;  // the coalescer run in progress (one at a time, beside a batcher run)
 
 std::atomic<uint64_t> g_deliveries{0};
 
 // ctx = caller index + 1
 void on_result(void* ctx, int status, const uint32_t*, uint64_t) {
   Load* L = g_load;
+  const uint32_t c = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ctx) - 1);
+  if (status != EMQX_OK) L->status[c] = status;
+  Driver& d = L->drv[c % L->D];
+  bool wake;
+  {
+    std::lock_guard<std::mutex> g(d.mu);
+    d.done.push_back(c);
+    wake = d.waiting;
+  }
+  if (wake) d.cv.notify_one();
+}
+
+// coalescer callbacks: the same hand-back as on_result, to g_sload's drivers
+void on_change(void* ctx, int status) {
+  Load* L = g_sload;
   const uint32_t c = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ctx) - 1);
   if (status != EMQX_OK) L->status[c] = status;
   Driver& d = L->drv[c % L->D];
@@ -321,4 +345,97 @@ extern "C" int batch_load(emqx_engine* e, uint32_t mode, const uint8_t* bytes, c
   for (int s : L.status)
     if (s != EMQX_OK) return s;
   return err.load();
+}
+
+// Commit coalescer: `callers` closed-loop callers; caller c's ops alternate subscribe / unsubscribe
+// of subscriber first_sub + c to a pseudo-random filter id < n_filters (route_ops = 0), or add /
+// delete the route of a new filter "storm/<c>/<k>" (route_ops = 1).  out[0..11] as batch_load
+// (batches = commits, messages per batch = changes per commit), out[12] = the coalescer's us per
+// commit.
+extern "C" int sub_load(emqx_engine* e, emqx_subtab* s, uint32_t callers, uint32_t n_filters, uint32_t first_sub,
+                        int route_ops, uint32_t max_wait_us, double warmup_ms, double duration_ms, double* out) {
+  if (!e || !s || !callers || (!route_ops && !n_filters) || !out) return EMQX_EINVAL;
+  Load L;
+  L.D = std::min<uint32_t>(callers, 8);
+  L.drv = std::vector<Driver>(L.D);
+  L.t_sub.resize(callers);
+  L.status.assign(callers, EMQX_OK);
+  g_sload = &L;
+  emqx_coalescer* co = nullptr;
+  int rc = emqx_coalescer_create(e, s, max_wait_us, on_change, &co);
+  if (rc != EMQX_OK) return rc;
+  std::vector<uint64_t> step(callers, 0);   // caller's op count
+  std::vector<uint32_t> held(callers, 0);   // filter (or route id) of its live subscription
+  auto one = [&](uint32_t c, uint64_t) -> int {
+    void* ctx = reinterpret_cast<void*>(static_cast<uintptr_t>(c) + 1);
+    const uint64_t k = step[c]++;
+    const bool add = (k & 1) == 0;
+    if (!route_ops) {
+      if (add) {
+        uint64_t x = (uint64_t(c) << 32) ^ (k * 0x9E3779B97F4A7C15ull);
+        x ^= x >> 31;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 29;
+        held[c] = static_cast<uint32_t>(x % n_filters);
+      }
+      const uint32_t sub = first_sub + c, f = held[c];
+      return emqx_coalescer_subscribe(co, &f, &sub, nullptr, 1, add ? 1 : 0, ctx);
+    }
+    if (add) {
+      char name[64];
+      const int len = snprintf(name, sizeof(name), "storm/%u/%llu", c, static_cast<unsigned long long>(k));
+      const uint64_t offs[2] = {0, static_cast<uint64_t>(len)};
+      return emqx_coalescer_insert_filters(co, reinterpret_cast<const uint8_t*>(name), offs, 1, &held[c], ctx);
+    }
+    return emqx_coalescer_delete_filters(co, &held[c], 1, ctx);
+  };
+  // a driver's finished callers resubmit under one coalescer lock (subscription ops), as a NIF
+  // draining a scheduler's queue would; route ops go one by one
+  thread_local std::vector<uint32_t> mf, ms;
+  thread_local std::vector<uint8_t> ma;
+  thread_local std::vector<void*> mc;
+  auto many = [&](const std::vector<uint32_t>& cs, const std::vector<uint64_t>& is) -> int {
+    if (route_ops) {
+      for (size_t j = 0; j < cs.size(); ++j) {
+        const int r = one(cs[j], is[j]);
+        if (r != EMQX_OK) return r;
+      }
+      return EMQX_OK;
+    }
+    mf.clear();
+    ms.clear();
+    ma.clear();
+    mc.clear();
+    for (uint32_t c : cs) {
+      const uint64_t k = step[c]++;
+      const bool add = (k & 1) == 0;
+      if (add) {
+        uint64_t x = (uint64_t(c) << 32) ^ (k * 0x9E3779B97F4A7C15ull);
+        x ^= x >> 31;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 29;
+        held[c] = static_cast<uint32_t>(x % n_filters);
+      }
+      mf.push_back(held[c]);
+      ms.push_back(first_sub + c);
+      ma.push_back(add ? 1 : 0);
+      mc.push_back(reinterpret_cast<void*>(static_cast<uintptr_t>(c) + 1));
+    }
+    return emqx_coalescer_subscribe_many(co, mf.data(), ms.data(), nullptr, ma.data(), cs.size(), mc.data());
+  };
+  std::vector<std::vector<float>> lat(L.D);
+  std::vector<uint64_t> completed(L.D, 0);
+  double secs = 0;
+  int err = run_load(1, callers, warmup_ms, duration_ms, L, one, many, lat, completed, &secs);
+  emqx_coalescer_flush(co);
+  uint64_t cs[6] = {0, 0, 0, 0, 0, 0};
+  emqx_coalescer_stats(co, cs, 6);
+  emqx_coalescer_destroy(co);
+  g_sload = nullptr;
+  const uint64_t ext[6] = {cs[0], cs[1], 0, 0, 0, 0};
+  summarize(L, lat, completed, secs, ext, out);
+  out[12] = cs[0] ? static_cast<double>(cs[3]) / cs[0] : 0;
+  for (int st : L.status)
+    if (st != EMQX_OK) return st;
+  return err;
 }
