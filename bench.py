@@ -123,6 +123,8 @@ def main():
     ap.add_argument("--publishers", type=int, default=0,
                     help="--workload E / P with round_robin / sticky: publishers the messages come from "
                          "(message key = generated key mod N; 0: the generated keys, ~1M distinct)")
+    ap.add_argument("--parity-sample", type=int, default=10000,
+                    help="--sharded past 10M filters: topics of rank 0's batch checked against the oracle")
     ap.add_argument("--sharded", action="store_true",
                     help="filter-sharded table (filters by a hash of their first two levels, wildcard-keyed "
                          "ones replicated): rank 0's batch is partitioned by owner rank, exchanged with one "
@@ -444,9 +446,13 @@ def sharded_bench(args, rank, world, dev):
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed = float(tt.item())
     n = wl.n_topics
-    # parity at every rank: its match_all CSR against a replicated table of the whole
-    # filter set on the same GPU, ID-for-ID per topic (sorted (topic, id) keys)
-    mism = 0
+    # parity, per rank, ID-for-ID per topic (oracle/cpp.py csr_mismatches): up to 10M filters
+    # every rank's whole batch against a replicated table of the whole filter set on its GPU;
+    # past that (config C's 100M) rank 0's first --parity-sample topics against the oracle
+    # (oracle/trie_oracle.cpp) restated on the filters that can match them (oracle/pruned.py)
+    from oracle import cpp as C
+    bad_rank = torch.zeros(world, dtype=torch.float64, device=dev)
+    checked = torch.zeros(world, dtype=torch.float64, device=dev)
     if args.n_filters <= 10_000_000:
         from emqx_amd.engine import Engine
         full = Engine(dev.index)
@@ -457,16 +463,34 @@ def sharded_bench(args, rank, world, dev):
         d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
         m = full.match_device(topics[0].data_ptr(), topics[1].data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
                               mode=args.mode, stream=torch.cuda.current_stream(dev).cuda_stream)
-
-        def keys(off, ids):
-            cnt = off[1:] - off[:-1]
-            t = torch.repeat_interleave(torch.arange(n, device=dev), cnt)
-            return torch.sort((t << 32) | ids.to(torch.int64).bitwise_and(0xFFFFFFFF))[0]
-
-        a, b = keys(d_off, d_ids[:m]), keys(res[0], res[1])
-        mism = 1 if a.numel() != b.numel() else int(bool((a != b).any().item()))
+        off_r, ids_r = d_off.cpu().numpy(), d_ids[:m].cpu().numpy().view(np.uint32)
+        # the replicated CSR sorted per topic (the oracle-side argument of csr_mismatches)
+        tt = np.repeat(np.arange(n, dtype=np.int64), np.diff(off_r.astype(np.int64)))
+        ids_r = (np.sort((tt << 32) | ids_r.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)
+        bad = C.csr_mismatches(res[0].cpu().numpy().astype(np.uint64), res[1].cpu().numpy().view(np.uint32),
+                               off_r.astype(np.uint64), ids_r)
+        bad_rank[rank] = float(bad.size)
+        checked[rank] = float(n)
+        parity_rule = "every rank's whole batch vs a replicated table of all filters on its GPU, ID-for-ID per topic"
         del full
-    mt = torch.tensor([float(res[0][-1].item()), float(sm.last_local_topics), float(mism), float(sm.n_local_filters)],
+    else:
+        k = min(args.parity_sample, n)
+        if rank == 0:
+            from oracle import pruned
+            with progress(f"[rank 0] parity: oracle over the filters that can match {k} topics"):
+                off_o, ids_o, cand = pruned.slice_csr(wl.filters, wl.fcodes, W.take(wl.topics, np.arange(k)),
+                                                      wl.tcodes[:k], mode=args.mode, threads=host_threads()[0])
+            off_g = res[0][: k + 1].cpu().numpy().astype(np.uint64)
+            ids_g = res[1][: int(off_g[-1])].cpu().numpy().view(np.uint32)
+            bad_rank[0] = float(C.csr_mismatches(off_g, ids_g, off_o, ids_o).size)
+            checked[0] = float(k)
+            log(f"[rank 0] parity: {k} topics, {int(off_o[-1])} ids, oracle table {len(cand)} of {wl.n_filters} filters")
+        parity_rule = (f"rank 0's first {k} topics vs the oracle (emqx_trie DFS + match_routes/1 union, "
+                       f"oracle/trie_oracle.cpp) over the filters that can match them (oracle/pruned.py), ID-for-ID")
+    dist.all_reduce(bad_rank, op=dist.ReduceOp.SUM)
+    dist.all_reduce(checked, op=dist.ReduceOp.SUM)
+    mism = int(bad_rank[rank].item())
+    mt = torch.tensor([float(res[0][-1].item()), float(sm.last_local_topics), 0.0, float(sm.n_local_filters)],
                       dtype=torch.float64, device=dev)
     most = mt[3:4].clone()
     dist.all_reduce(mt, op=dist.ReduceOp.SUM)
@@ -487,16 +511,18 @@ def sharded_bench(args, rank, world, dev):
             "shard_filters_max_rank": int(most.item()), "shard_filters_max_frac": round(float(most.item()) / wl.n_filters, 4),
             "shard_plan_keys": len(sm.plan),
             "matches_per_topic": round(float(mt[0].item()) / (n * world), 3),
-            "parity": ({"ranks_checked": world, "rule": "every rank's CSR vs a replicated table on its GPU, "
-                        "ID-for-ID per topic", "ranks_mismatching": int(mt[2].item())}
-                       if args.n_filters <= 10_000_000 else None),
+            "parity": {"rule": parity_rule,
+                       "topics_checked_per_rank": [int(x) for x in checked.cpu().tolist()],
+                       "mismatching_topics_per_rank": [int(x) for x in bad_rank.cpu().tolist()]},
+            "step": "device kernels (emqx_shard_step_*: route + sort + pack, unpack, answer, merge), "
+                    "engines async with learnt capacities, two host syncs (split sizes)",
             **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
                if rehearse else {}),
         }), flush=True)
     dist.barrier()
     dist.destroy_process_group()
     if mism:
-        raise SystemExit(f"rank {rank}: sharded CSR differs from the replicated table")
+        raise SystemExit(f"rank {rank}: sharded CSR differs on {mism} topics")
 
 
 def retain_traffic(nf, n_retained):

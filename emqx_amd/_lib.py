@@ -51,7 +51,8 @@ EXPORTS = (
     "emqx_host_batch_wait", "emqx_host_batch_query",
     "emqx_commit_stats", "emqx_shard_owner", "emqx_shard_owner_device",
     "emqx_shard_plan", "emqx_shard_place", "emqx_shard_route", "emqx_shard_route_device", "emqx_permute_scratch_bytes", "emqx_batch_permute_device", "emqx_owner_sort_scratch_bytes",
-    "emqx_owner_sort_device",
+    "emqx_owner_sort_device", "emqx_shard_step_create", "emqx_shard_step_destroy", "emqx_shard_send_cap",
+    "emqx_shard_step_send", "emqx_shard_step_recv", "emqx_shard_step_answer", "emqx_shard_step_merge",
     "emqx_csr_unpermute_device", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
     "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check", "emqx_htrie_walk_sim",
 )
@@ -247,6 +248,13 @@ def lib():
         "emqx_permute_scratch_bytes": (u64, [u64]),
         "emqx_owner_sort_scratch_bytes": (u64, [u64, u32]),
         "emqx_owner_sort_device": (i32, [vp, u64, u32, vp, vp, vp]),
+        "emqx_shard_step_create": (i32, [i32, u32, vp, u32, ctypes.POINTER(vp)]),
+        "emqx_shard_step_destroy": (i32, [vp]),
+        "emqx_shard_send_cap": (u64, [u64, u64, u32]),
+        "emqx_shard_step_send": (i32, [vp, vp, vp, u64, vp, u64, vp, vp]),
+        "emqx_shard_step_recv": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "emqx_shard_step_answer": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "emqx_shard_step_merge": (i32, [vp, vp, vp, vp, vp, vp]),
         "emqx_batch_permute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),
         "emqx_csr_unpermute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),
         "emqx_host_batch_create": (i32, [vp, u64, u64, u64, ctypes.POINTER(ctypes.POINTER(HostBatchStruct))]),

@@ -1,7 +1,7 @@
 // C ABI of the publish fan-out stage (include/emqx_match.h, emqx_subtab_* / emqx_fanout_* /
 // emqx_pub_batch_* / emqx_publish_batch): host subscription store, device tables patched in
 // place per commit, the per-publisher $share pick state, and the fan-out pipeline
-//   entry_topic -> count -> scan -> offsets -> write [-> resolve] -> finish   (one stream, no host sync)
+//   entry_topic -> count -> scan -> write (+ offsets) [-> resolve] -> finish   (one stream, no host sync)
 //
 // Store semantics follow the reference's ETS tables:
 //   plain subscriptions  ?SUBSCRIBER bag Topic -> SubPid (apps/emqx/src/emqx_broker.erl:146-158);
@@ -21,13 +21,18 @@
 // rebuild (compaction) runs only when moved-away extents outweigh the live ones.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/emqx_match.h"
@@ -55,84 +60,92 @@ inline uint64_t fo_mix64(uint64_t x) {
 }
 
 // Open-addressed map u64 -> u32 with tombstones (keys never take the two reserved values:
-// filter ids and slots are < 2^31).
+// filter ids and slots are < 2^31).  Key and value share one 16-B entry, so a probe that misses
+// the caches costs one line, and prefetch() lets a batch start the next ops' lines early.
 class U64Map {
  public:
   uint32_t find(uint64_t k) const {
-    if (keys_.empty()) return SUB_NONE;
-    const uint64_t mask = keys_.size() - 1;
+    if (e_.empty()) return SUB_NONE;
+    const uint64_t mask = e_.size() - 1;
     for (uint64_t i = fo_mix64(k) & mask;; i = (i + 1) & mask) {
-      if (keys_[i] == EMPTY) return SUB_NONE;
-      if (keys_[i] == k) return vals_[i];
+      if (e_[i].k == EMPTY) return SUB_NONE;
+      if (e_[i].k == k) return e_[i].v;
     }
   }
   // true if newly inserted (an existing key keeps its value)
   bool insert(uint64_t k, uint32_t v) {
-    if (keys_.empty()) rehash(1024);
-    else if ((used_ + 1) * 4 >= keys_.size() * 3)  // double, or just drop tombstones
-      rehash((size_ + 1) * 2 >= keys_.size() ? keys_.size() * 2 : keys_.size());
-    const uint64_t mask = keys_.size() - 1;
+    if (e_.empty()) rehash(1024);
+    else if ((used_ + 1) * 4 >= e_.size() * 3)  // double, or just drop tombstones
+      rehash((size_ + 1) * 2 >= e_.size() ? e_.size() * 2 : e_.size());
+    const uint64_t mask = e_.size() - 1;
     uint64_t tomb = ~0ull;
     for (uint64_t i = fo_mix64(k) & mask;; i = (i + 1) & mask) {
-      if (keys_[i] == k) return false;
-      if (keys_[i] == TOMB && tomb == ~0ull) tomb = i;
-      if (keys_[i] == EMPTY) {
+      if (e_[i].k == k) return false;
+      if (e_[i].k == TOMB && tomb == ~0ull) tomb = i;
+      if (e_[i].k == EMPTY) {
         if (tomb != ~0ull) i = tomb; else ++used_;
-        keys_[i] = k;
-        vals_[i] = v;
+        e_[i].k = k;
+        e_[i].v = v;
         ++size_;
         return true;
       }
     }
   }
   void assign(uint64_t k, uint32_t v) {  // k present
-    const uint64_t mask = keys_.size() - 1;
+    const uint64_t mask = e_.size() - 1;
     for (uint64_t i = fo_mix64(k) & mask;; i = (i + 1) & mask)
-      if (keys_[i] == k) {
-        vals_[i] = v;
+      if (e_[i].k == k) {
+        e_[i].v = v;
         return;
       }
   }
   bool erase(uint64_t k) {
-    if (keys_.empty()) return false;
-    const uint64_t mask = keys_.size() - 1;
+    if (e_.empty()) return false;
+    const uint64_t mask = e_.size() - 1;
     for (uint64_t i = fo_mix64(k) & mask;; i = (i + 1) & mask) {
-      if (keys_[i] == EMPTY) return false;
-      if (keys_[i] == k) {
-        keys_[i] = TOMB;
+      if (e_[i].k == EMPTY) return false;
+      if (e_[i].k == k) {
+        e_[i].k = TOMB;
         --size_;
         return true;
       }
     }
+  }
+  void prefetch(uint64_t k) const {
+    if (!e_.empty()) __builtin_prefetch(&e_[fo_mix64(k) & (e_.size() - 1)], 1);
   }
   bool contains(uint64_t k) const { return find(k) != SUB_NONE; }
   uint64_t size() const { return size_; }
 
  private:
   static constexpr uint64_t EMPTY = ~0ull, TOMB = ~0ull - 1;
+  struct Ent {
+    uint64_t k;
+    uint32_t v, pad;
+  };
   void rehash(uint64_t cap) {
-    std::vector<uint64_t> ok;
-    std::vector<uint32_t> ov;
-    ok.swap(keys_);
-    ov.swap(vals_);
-    keys_.assign(cap, EMPTY);
-    vals_.assign(cap, 0);
+    std::vector<Ent> old;
+    old.swap(e_);
+    e_.assign(cap, Ent{EMPTY, 0, 0});
     used_ = size_ = 0;
     const uint64_t mask = cap - 1;
-    for (uint64_t j = 0; j < ok.size(); ++j) {
-      if (ok[j] == EMPTY || ok[j] == TOMB) continue;
-      uint64_t i = fo_mix64(ok[j]) & mask;
-      while (keys_[i] != EMPTY) i = (i + 1) & mask;
-      keys_[i] = ok[j];
-      vals_[i] = ov[j];
+    for (const Ent& x : old) {
+      if (x.k == EMPTY || x.k == TOMB) continue;
+      uint64_t i = fo_mix64(x.k) & mask;
+      while (e_[i].k != EMPTY) i = (i + 1) & mask;
+      e_[i] = Ent{x.k, x.v, 0};
       ++used_;
       ++size_;
     }
   }
-  std::vector<uint64_t> keys_;
-  std::vector<uint32_t> vals_;
+  std::vector<Ent> e_;
   uint64_t used_ = 0, size_ = 0;  // used_ counts tombstones too
 };
+
+// The plain positions, sharded by filter: a batch's plain ops run on one thread per shard
+// (their filters' lists and map entries are the shard's alone).
+constexpr uint32_t PP_SHARDS = 16;
+inline uint32_t pp_shard(uint32_t f) { return (f * 0x9E3779B1u) >> 28; }
 
 template <class T>
 void fo_free(T*& p) {
@@ -200,10 +213,8 @@ struct FoScratch {
   hipStream_t stream = nullptr;
   uint32_t* entry_topic = nullptr;
   uint64_t cap_entry_topic = 0;
-  uint32_t* ecount = nullptr;
-  uint64_t cap_ecount = 0;
-  uint64_t* eoff = nullptr;
-  uint64_t cap_eoff = 0;
+  uint64_t* csum = nullptr;
+  uint64_t cap_csum = 0;
   uint64_t* partials = nullptr;
   uint64_t cap_partials = 0;
   // round_robin / sticky: $share groups per chunk of entries, the pick list, its sorted copy and
@@ -229,8 +240,7 @@ struct FoScratch {
   bool used = false;
   void release() {
     fo_free(entry_topic);
-    fo_free(ecount);
-    fo_free(eoff);
+    fo_free(csum);
     fo_free(partials);
     fo_free(gchunk);
     fo_free(pk);
@@ -264,7 +274,9 @@ struct emqx_subtab {
   std::vector<GroupRec> groups;               // group-record arena
   std::vector<uint32_t> members;              // member arena
   uint64_t garbage = 0;                       // words of extents moved away from
-  U64Map plain_pos;                           // (filter << 32 | sub) -> index in the plain list
+  U64Map plain_pos[PP_SHARDS];                // (filter << 32 | sub) -> index in the plain list,
+                                              // by pp_shard(filter)
+  std::vector<uint8_t> plocal;                // batch ops: the filter's list is in its thread's arena
   U64Map slot_of;                             // (filter << 32 | group) -> slot
   std::vector<Slot> slots;
   std::vector<std::vector<uint32_t>> fslots;  // filter id -> its slots (creation order)
@@ -274,6 +286,11 @@ struct emqx_subtab {
   std::vector<std::pair<uint64_t, uint64_t>> dirty_plain;  // (first word, words)
   std::vector<uint32_t> dirty_recs, dirty_slots, dirty_glists;
   std::vector<uint8_t> rec_flag, glist_flag;  // per filter: listed in dirty_recs / dirty_glists
+  uint64_t plain_count() const {
+    uint64_t n = 0;
+    for (const U64Map& m : plain_pos) n += m.size();
+    return n;
+  }
   std::vector<uint32_t> alive;                // liveness bitmap image (bit per subscriber id)
   std::vector<uint32_t> dirty_alive;          // words of it changed since the last commit
   bool need_full = true;
@@ -352,18 +369,27 @@ void ensure_filter(emqx_subtab* s, uint32_t f) {
   s->gcap.resize(n, 0);
   s->rec_flag.resize(n, 0);
   s->glist_flag.resize(n, 0);
+  s->plocal.resize(n, 0);
   if (s->fslots.size() < n) s->fslots.resize(n);
 }
 
 // A bulk load (more mutations before a commit than a quarter of the table, at least 64K) is
 // cheaper as one full upload than as patches: past that point no dirt is recorded.
-void note_op(emqx_subtab* s) {
-  if (s->bulk || ++s->ops_pending <= std::max<uint64_t>(1u << 16, (s->plain_pos.size() + s->n_members) / 4)) return;
+uint64_t bulk_threshold(const emqx_subtab* s) {
+  return std::max<uint64_t>(1u << 16, (s->plain_count() + s->n_members) / 4);
+}
+
+void go_bulk(emqx_subtab* s) {
   s->bulk = true;
   std::vector<std::pair<uint64_t, uint64_t>>().swap(s->dirty_plain);
   std::vector<uint32_t>().swap(s->dirty_recs);
   std::vector<uint32_t>().swap(s->dirty_slots);
   std::vector<uint32_t>().swap(s->dirty_glists);
+}
+
+void note_op(emqx_subtab* s) {
+  if (s->bulk || ++s->ops_pending <= bulk_threshold(s)) return;
+  go_bulk(s);
 }
 
 void mark_rec(emqx_subtab* s, uint32_t f) {
@@ -398,7 +424,7 @@ void plain_add(emqx_subtab* s, uint32_t f, uint32_t sub) {
   const uint64_t key = (uint64_t(f) << 32) | sub;
   ensure_filter(s, f);
   FilterRec& r = s->recs[f];
-  if (!s->plain_pos.insert(key, r.n_plain)) return;  // ETS bag: a pair is stored once
+  if (!s->plain_pos[pp_shard(f)].insert(key, r.n_plain)) return;  // ETS bag: a pair is stored once
   if (r.n_plain == s->pcap[f]) {  // the extent is full: move the list to the arena's end
     const uint64_t nb = s->plain.size();
     const uint32_t cap = std::max<uint32_t>(4, 2 * r.n_plain);
@@ -420,20 +446,169 @@ void plain_add(emqx_subtab* s, uint32_t f, uint32_t sub) {
 
 void plain_remove(emqx_subtab* s, uint32_t f, uint32_t sub) {
   const uint64_t key = (uint64_t(f) << 32) | sub;
-  const uint32_t pos = s->plain_pos.find(key);
+  U64Map& pp = s->plain_pos[pp_shard(f)];
+  const uint32_t pos = pp.find(key);
   if (pos == SUB_NONE) return;
-  s->plain_pos.erase(key);
+  pp.erase(key);
   FilterRec& r = s->recs[f];
   const uint32_t last = r.n_plain - 1;
   if (pos != last) {  // the last subscriber fills the hole (plain order carries no meaning)
     const uint32_t moved = s->plain[uint64_t(r.plain_begin) + last];
     s->plain[uint64_t(r.plain_begin) + pos] = moved;
-    s->plain_pos.assign((uint64_t(f) << 32) | moved, pos);
+    pp.assign((uint64_t(f) << 32) | moved, pos);
     if (!s->bulk) s->dirty_plain.emplace_back(uint64_t(r.plain_begin) + pos, 1);
   }
   r.n_plain = last;
   mark_rec(s, f);
   note_op(s);
+}
+
+// ---- batched plain ops on several threads --------------------------------------------------
+// A batch of plain subscribes or unsubscribes runs one thread per filter shard (pp_shard): a
+// shard's filters, their records, extents and map entries belong to its thread alone, and a
+// list that outgrows its extent moves into the thread's own arena, appended to the shared one
+// after the batch (its filters' extents rebased then).  Ops on one filter keep their order, so
+// the result equals the serial loop's.  The random lines of the next ops are prefetched.
+constexpr uint64_t PAR_MIN = 4096;  // smaller batches stay on the caller's thread
+
+unsigned par_threads() {
+  static const unsigned t = [] {
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = static_cast<unsigned>(CPU_COUNT(&cs));
+    if (const char* e = std::getenv("EMQX_SUBTAB_THREADS")) n = static_cast<unsigned>(std::max(1, std::atoi(e)));
+    return std::max(1u, std::min(n, PP_SHARDS));
+  }();
+  return t;
+}
+
+struct PlainLocal {
+  std::vector<uint32_t> arena;                        // lists moved in this batch
+  std::vector<std::pair<uint64_t, uint64_t>> dirty;  // touched words of the shared arena
+  std::vector<uint32_t> recs;                         // records newly dirty
+  std::vector<uint32_t> moved;                        // filters whose list is in `arena`
+  uint64_t garbage = 0, moves = 0, ops = 0;
+};
+
+void plain_batch_shard(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, const uint32_t* idx, uint64_t cnt,
+                       bool add, PlainLocal& L) {
+  const bool bulk = s->bulk;
+  uint32_t* const shared = s->plain.data();
+  const uint64_t nrec = s->recs.size();
+  constexpr uint64_t AHEAD = 8;
+  for (uint64_t j = 0; j < cnt; ++j) {
+    if (j + AHEAD < cnt) {
+      const uint64_t q2 = idx[j + AHEAD];
+      const uint32_t f2 = fs[q2];
+      if (f2 < nrec) {
+        s->plain_pos[pp_shard(f2)].prefetch((uint64_t(f2) << 32) | subs[q2]);
+        __builtin_prefetch(&s->recs[f2], 1);
+      }
+    }
+    const uint64_t q = idx[j];
+    const uint32_t f = fs[q], sub = subs[q];
+    if (f >= nrec) continue;  // an unsubscribe from a filter never seen
+    U64Map& pp = s->plain_pos[pp_shard(f)];
+    FilterRec& r = s->recs[f];
+    const uint64_t key = (uint64_t(f) << 32) | sub;
+    if (add) {
+      if (!pp.insert(key, r.n_plain)) continue;  // ETS bag: a pair is stored once
+      if (r.n_plain == s->pcap[f]) {             // full: into this thread's arena, twice the room
+        const uint32_t cap = std::max<uint32_t>(4, 2 * r.n_plain);
+        const uint64_t nb = L.arena.size();
+        L.arena.resize(nb + cap);
+        const uint32_t* from = (s->plocal[f] ? L.arena.data() : shared) + r.plain_begin;
+        std::copy(from, from + r.n_plain, L.arena.data() + nb);
+        L.garbage += s->pcap[f];
+        if (!s->plocal[f]) {
+          s->plocal[f] = 1;
+          L.moved.push_back(f);
+        }
+        r.plain_begin = static_cast<uint32_t>(nb);
+        s->pcap[f] = cap;
+        ++L.moves;
+      }
+      (s->plocal[f] ? L.arena.data() : shared)[uint64_t(r.plain_begin) + r.n_plain] = sub;
+      if (!bulk && !s->plocal[f]) L.dirty.emplace_back(uint64_t(r.plain_begin) + r.n_plain, 1);
+      r.n_plain += 1;
+    } else {
+      const uint32_t pos = pp.find(key);
+      if (pos == SUB_NONE) continue;
+      pp.erase(key);
+      const uint32_t last = r.n_plain - 1;
+      if (pos != last) {  // the last subscriber fills the hole
+        uint32_t* l = (s->plocal[f] ? L.arena.data() : shared) + r.plain_begin;
+        const uint32_t moved = l[last];
+        l[pos] = moved;
+        pp.assign((uint64_t(f) << 32) | moved, pos);
+        if (!bulk && !s->plocal[f]) L.dirty.emplace_back(uint64_t(r.plain_begin) + pos, 1);
+      }
+      r.n_plain = last;
+    }
+    ++L.ops;
+    if (!bulk && !s->rec_flag[f]) {
+      s->rec_flag[f] = 1;
+      L.recs.push_back(f);
+    }
+  }
+}
+
+// n plain subscribes (add) or unsubscribes, s->mu held.
+void plain_batch(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, uint64_t n, bool add) {
+  if (add) {
+    uint32_t fmax = 0;
+    for (uint64_t i = 0; i < n; ++i) fmax = std::max(fmax, fs[i]);
+    ensure_filter(s, fmax);
+    for (uint64_t i = 0; i < n; ++i) set_alive_bit(s, subs[i], true);  // a subscribing process is alive
+  }
+  if (!s->bulk && s->ops_pending + n > bulk_threshold(s)) go_bulk(s);
+  // the ops by shard, in order within each
+  uint64_t start[PP_SHARDS + 1] = {};
+  for (uint64_t i = 0; i < n; ++i) ++start[pp_shard(fs[i]) + 1];
+  for (uint32_t k = 0; k < PP_SHARDS; ++k) start[k + 1] += start[k];
+  std::vector<uint32_t> idx(n);
+  {
+    uint64_t pos[PP_SHARDS];
+    std::copy(start, start + PP_SHARDS, pos);
+    for (uint64_t i = 0; i < n; ++i) idx[pos[pp_shard(fs[i])]++] = static_cast<uint32_t>(i);
+  }
+  std::vector<PlainLocal> loc(PP_SHARDS);
+  std::atomic<uint32_t> next{0};
+  auto work = [&] {
+    for (uint32_t k; (k = next.fetch_add(1)) < PP_SHARDS;)
+      plain_batch_shard(s, fs, subs, idx.data() + start[k], start[k + 1] - start[k], add, loc[k]);
+  };
+  const unsigned T = std::min<unsigned>(par_threads(), static_cast<unsigned>((n + PAR_MIN / 4 - 1) / (PAR_MIN / 4)));
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < T; ++t) {
+    try {
+      th.emplace_back(work);
+    } catch (...) {
+      break;  // fewer threads: the others take more shards
+    }
+  }
+  work();
+  for (auto& t : th) t.join();
+  // merge, shard by shard: moved lists appended to the shared arena
+  for (PlainLocal& L : loc) {
+    if (!L.arena.empty()) {
+      const uint64_t base = s->plain.size();
+      s->plain.insert(s->plain.end(), L.arena.begin(), L.arena.end());
+      for (uint32_t f : L.moved) {
+        FilterRec& r = s->recs[f];
+        r.plain_begin = static_cast<uint32_t>(r.plain_begin + base);
+        s->plocal[f] = 0;
+        if (!s->bulk && r.n_plain) s->dirty_plain.emplace_back(r.plain_begin, r.n_plain);
+      }
+    }
+    if (!s->bulk) {
+      s->dirty_plain.insert(s->dirty_plain.end(), L.dirty.begin(), L.dirty.end());
+      s->dirty_recs.insert(s->dirty_recs.end(), L.recs.begin(), L.recs.end());
+    }
+    s->garbage += L.garbage;
+    s->st_moves += L.moves;
+    s->ops_pending += L.ops;
+  }
 }
 
 // ---- device side of a commit ----------------------------------------------------------------
@@ -466,7 +641,7 @@ void compact_image(emqx_subtab* s) {
   std::vector<uint32_t> plain;
   std::vector<GroupRec> groups;
   std::vector<uint32_t> members;
-  plain.reserve(s->plain_pos.size() + s->plain_pos.size() / 4 + 4 * nf);
+  plain.reserve(s->plain_count() + s->plain_count() / 4 + 4 * nf);
   members.reserve(s->n_members + s->n_members / 4);
   s->n_live_groups = 0;
   for (uint64_t f = 0; f < nf; ++f) {
@@ -721,7 +896,7 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
 int commit_enqueue(emqx_subtab* s, std::vector<void*>& retired) {
   FO_TRY(hipSetDevice(s->device));
   if (s->recs.size() >= FANOUT_ID_LIMIT) return EMQX_EINVAL;
-  const uint64_t live = s->plain_pos.size() + s->n_members + s->recs.size();
+  const uint64_t live = s->plain_count() + s->n_members + s->recs.size();
   int rc;
   if (s->need_full || s->bulk || s->garbage > std::max<uint64_t>(1u << 20, live)) {
     int b = barrier_after_fanouts(s);
@@ -908,9 +1083,8 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
     if (rc == EMQX_OK) rc = flush_forgets(s, st);
     if (rc != EMQX_OK) return rc;
   }
-  if (d_keys && strategy != EMQX_SHARE_RANDOM) FO_TRY(fo_ensure(c->entry_topic, c->cap_entry_topic, m_cap));
-  FO_TRY(fo_ensure(c->ecount, c->cap_ecount, m_cap));
-  FO_TRY(fo_ensure(c->eoff, c->cap_eoff, m_cap + 1));
+  FO_TRY(fo_ensure(c->entry_topic, c->cap_entry_topic, std::max<uint64_t>(m_cap, 1)));
+  FO_TRY(fo_ensure(c->csum, c->cap_csum, m_cap / FO_WCHUNK + 2));
   FO_TRY(fo_ensure(c->partials, c->cap_partials, 4 * FO_BLOCKS));
   if (!c->ctl) FO_TRY(fo_alloc(c->ctl, FO_CTL_WORDS));
   if (s->commit_pending) FO_TRY(hipStreamWaitEvent(st, s->commit_ev, 0));
@@ -962,8 +1136,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   s->seed = s->seed * 1664525u + 1013904223u;
   a.seed = s->seed;
   a.entry_topic = c->entry_topic;
-  a.ecount = c->ecount;
-  a.eoff = c->eoff;
+  a.csum = c->csum;
   a.partials = c->partials;
   a.out_off = d_out_off;
   a.out_subs = d_out_subs;
@@ -1265,11 +1438,41 @@ int emqx_subtab_destroy(emqx_subtab* s) {
   return EMQX_OK;
 }
 
+// A long batch: its plain ops go through plain_batch (threads), and *rest_out = the indices of
+// its $share ops, which the caller applies serially after them (plain lists and group
+// memberships are separate structures, so the split changes no result).  False: a short batch.
+bool plain_parallel(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, const uint32_t* group_ids,
+                    uint64_t n, bool add, std::vector<uint32_t>* rest_out) {
+  if (n < PAR_MIN || par_threads() < 2) return false;
+  rest_out->clear();
+  if (!group_ids) {
+    plain_batch(s, fs, subs, n, add);
+    return true;
+  }
+  std::vector<uint32_t> pf, ps;
+  pf.reserve(n);
+  ps.reserve(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (group_ids[i] == EMQX_NO_GROUP) {
+      pf.push_back(fs[i]);
+      ps.push_back(subs[i]);
+    } else {
+      rest_out->push_back(static_cast<uint32_t>(i));
+    }
+  }
+  if (!pf.empty()) plain_batch(s, pf.data(), ps.data(), pf.size(), add);
+  return true;
+}
+
 int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids, const uint32_t* group_ids,
                     uint64_t n) {
   if (!s || !ids_ok(filter_ids, sub_ids, n)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
-  for (uint64_t i = 0; i < n; ++i) {
+  std::vector<uint32_t> rest;
+  const bool split = plain_parallel(s, filter_ids, sub_ids, group_ids, n, true, &rest);
+  const uint64_t nl = split ? rest.size() : n;
+  for (uint64_t j = 0; j < nl; ++j) {
+    const uint64_t i = split ? rest[j] : j;
     const uint32_t f = filter_ids[i], sub = sub_ids[i];
     const uint32_t grp = group_ids ? group_ids[i] : EMQX_NO_GROUP;
     set_alive_bit(s, sub, true);  // a subscribing process is alive
@@ -1301,7 +1504,11 @@ int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_
                        uint64_t n) {
   if (!s || !ids_ok(filter_ids, sub_ids, n)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
-  for (uint64_t i = 0; i < n; ++i) {
+  std::vector<uint32_t> rest;
+  const bool split = plain_parallel(s, filter_ids, sub_ids, group_ids, n, false, &rest);
+  const uint64_t nl = split ? rest.size() : n;
+  for (uint64_t j = 0; j < nl; ++j) {
+    const uint64_t i = split ? rest[j] : j;
     const uint32_t f = filter_ids[i], sub = sub_ids[i];
     const uint32_t grp = group_ids ? group_ids[i] : EMQX_NO_GROUP;
     if (f >= s->recs.size()) continue;
@@ -1331,7 +1538,7 @@ int emqx_subtab_commit(emqx_subtab* s) {
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4) {
   if (!s || !counts4) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
-  counts4[0] = s->plain_pos.size();
+  counts4[0] = s->plain_count();
   counts4[1] = s->n_members;
   counts4[2] = s->n_live_groups;
   counts4[3] = s->d_recs.cap * sizeof(FilterRec) + s->d_plain.cap * 4 + s->d_groups.cap * sizeof(GroupRec) +

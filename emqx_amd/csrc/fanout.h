@@ -105,9 +105,8 @@ struct FanoutArgs {
   const uint32_t* keys;      // per topic: phash2 key (hash strategies) / publisher (rr, sticky), or null
   uint32_t strategy;         // EMQX_SHARE_*
   uint32_t seed;             // per-call seed of random picks
-  uint32_t* entry_topic;     // [m] scratch (strategies that read per-topic keys)
-  uint32_t* ecount;          // [m] scratch
-  uint64_t* eoff;            // [m+1] scratch: per-entry output offsets
+  uint32_t* entry_topic;     // [m] scratch: entry -> topic
+  uint64_t* csum;            // [ceil(m / FO_WCHUNK)] scratch: deliveries per chunk of FO_WCHUNK entries
   uint64_t* partials;        // [4 * FO_BLOCKS] scratch: chunk sums, chunk bases (deliveries, then picks)
   uint64_t* out_off;         // [n+1]
   uint32_t* out_subs;        // [cap]

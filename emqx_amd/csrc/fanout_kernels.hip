@@ -7,18 +7,21 @@
 // Pipeline, all on one stream with no host synchronisation: the number of
 // match entries m = moff[n] - moff[0] is read on the device, so every kernel below runs a
 // fixed grid over a length it loads itself.
-//   entry_topic  one thread per topic: entry -> topic map (strategies that read per-topic keys)
-//   count        FO_BLOCKS blocks, one contiguous chunk of entries each: per-entry count
-//                n_plain + n_groups of its filter, and the chunk's sum
-//   partials     one block: exclusive scan of the chunk sums, the total, the overflow flag
+//   entry_topic  one thread per topic: entry -> topic map (a refused or empty CSR: zero
+//                offsets, as nothing else runs)
+//   count        FO_BLOCKS blocks, one contiguous range of entries each: per FO_WCHUNK-entry
+//                chunk the deliveries (n_plain + n_groups of each entry's filter), per block
+//                their sum
+//   partials     one block: exclusive scan of the block sums, the total, the overflow flag
 //                and the call summary
-//   final        FO_BLOCKS blocks: per-entry output offsets (chunk scan + the chunk's base)
-//   offsets      per-topic output offsets = per-entry offsets at the match CSR boundaries
-//   write        one wavefront per 256 match entries: the wave walks its flattened outputs 64
-//                at a time (each lane finds its entry by an 8-step search over LDS prefix
-//                offsets), so plain-subscriber copies are coalesced reads and writes; each
-//                $share group contributes exactly one pick.  Skipped entirely on overflow, so
-//                no pick state is consumed by a call that wrote nothing.
+//   write        one wavefront per 256 match entries: the chunk's base (its block's base + the
+//                block's earlier chunks), its entries' offsets by a wave scan of the counts of
+//                the records it loads anyway, the per-topic output offsets of the topics that
+//                start in the chunk; then the wave walks its flattened outputs 64 at a time
+//                (each lane finds its entry by an 8-step search over LDS prefix offsets), so
+//                plain-subscriber copies are coalesced reads and writes; each $share group
+//                contributes exactly one pick.  On overflow only the offsets are written, so
+//                no pick state is consumed by a call that wrote no deliveries.
 //   probe, sort, round_robin / sticky only: the write kernel puts one {position, group record,
 //   resolve      publisher} record per $share pick into a list in output order; the probe kernel
 //                finds each pick's (group slot, publisher) state entry and names the call's run of
@@ -59,7 +62,11 @@ __device__ __forceinline__ bool fo_refused(const FanoutArgs& a) {
 __device__ __forceinline__ uint64_t fo_entries(const FanoutArgs& a) { return fo_refused(a) ? 0 : fo_entries_raw(a); }
 
 __global__ __launch_bounds__(FO_THREADS) void fanout_entry_topic_kernel(FanoutArgs a) {
-  if (fo_refused(a)) return;
+  if (fo_entries(a) == 0) {  // refused or no entries: every topic's deliveries start at 0
+    for (uint64_t t = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; t <= a.n; t += uint64_t(gridDim.x) * FO_THREADS)
+      a.out_off[t] = 0;
+    return;
+  }
   const uint64_t base = a.moff[0];
   for (uint64_t t = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; t < a.n;
        t += uint64_t(gridDim.x) * FO_THREADS) {
@@ -84,31 +91,8 @@ __device__ __forceinline__ uint64_t fo_wave_sum(uint64_t v) {
   return v;
 }
 
-// Block-wide exclusive scan of one u64 per thread (FO_THREADS threads).
-__device__ __forceinline__ uint64_t fo_block_excl_scan(uint64_t v, uint64_t* total) {
-  __shared__ uint64_t wsum[FO_THREADS / 64];
-  const uint32_t lane = fo_lane(), w = threadIdx.x >> 6;
-  uint64_t incl = v;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  uint64_t before = 0, all = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < FO_THREADS / 64; ++k) {
-    before += k < w ? wsum[k] : 0;
-    all += wsum[k];
-  }
-  __syncthreads();
-  *total = all;
-  return before + incl - v;
-}
-
-// Per-entry delivery counts (n_plain + n_groups of the entry's filter) and per-block sums; for
-// round_robin / sticky also the $share groups per FO_WCHUNK-entry chunk (gchunk) and per block.
+// Deliveries per FO_WCHUNK-entry chunk (n_plain + n_groups of each entry's filter, csum) and per
+// block; for round_robin / sticky also the $share groups per chunk (gchunk) and per block.
 // Each wave takes whole chunks (4 entries per lane, all loads of a chunk in flight together).
 __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) {
   __shared__ uint64_t bsum[2][FO_THREADS / 64];
@@ -135,20 +119,21 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) 
       g[u] = in ? r.w : 0u;
     }
     uint32_t gl = 0;
+    uint64_t cs = 0;
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
-      const uint64_t i = c0 + lane + 64u * u;
-      if (i < hi) a.ecount[i] = c[u];
-      sum += c[u];
+      cs += c[u];
       gl += g[u];
     }
+    cs = fo_wave_sum(cs);
+    if (lane == 0) a.csum[c0 / FO_WCHUNK] = cs;
+    sum += cs;
     if (stateful) {
       const uint64_t gc = fo_wave_sum(gl);
       if (lane == 0) a.gchunk[c0 / FO_WCHUNK] = static_cast<uint32_t>(gc);
       gsum += gl;
     }
   }
-  sum = fo_wave_sum(sum);
   gsum = fo_wave_sum(gsum);
   if (lane == 0) {
     bsum[0][wv] = sum;
@@ -189,7 +174,7 @@ __device__ __forceinline__ uint64_t fo_blocks_excl_scan(uint64_t v, uint64_t* to
 }
 
 // One block of FO_BLOCKS threads: chunk bases (deliveries; $share picks of the stateful
-// strategies), eoff[m] = total, the call summary.  A call whose deliveries exceed cap, or whose
+// strategies), the total, the call summary.  A call whose deliveries exceed cap, or whose
 // picks exceed the pick list, is flagged here and writes nothing.
 __global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a) {
   uint64_t all = 0, picks = 0;
@@ -199,7 +184,6 @@ __global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a
   if (threadIdx.x == 0) {
     const bool refused = fo_refused(a);
     const uint64_t m = fo_entries(a);
-    a.eoff[m] = all;
     uint64_t* sm = a.summary;
     uint64_t fl = 0;
     if (refused) fl = FO_SUM_F_MATCH;
@@ -212,39 +196,6 @@ __global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a
     if (fl) a.ctl[FO_CTL_FLAGS] |= fl;
     __threadfence_system();
   }
-}
-
-// Per-entry output offsets: each block rescans its chunk, FO_THREADS * 4 entries per round.
-__global__ __launch_bounds__(FO_THREADS) void fanout_final_kernel(FanoutArgs a) {
-  uint64_t lo, hi;
-  fo_chunk(fo_entries(a), blockIdx.x, &lo, &hi);
-  uint64_t carry = a.partials[FO_BLOCKS + blockIdx.x];
-  for (uint64_t r0 = lo; r0 < hi; r0 += FO_THREADS * 4) {
-    const uint64_t i0 = r0 + 4ull * threadIdx.x;
-    uint32_t c[4];
-    uint64_t sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      c[k] = i0 + k < hi ? a.ecount[i0 + k] : 0u;
-      sum += c[k];
-    }
-    uint64_t tot;
-    uint64_t p = carry + fo_block_excl_scan(sum, &tot);
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      if (i0 + k < hi) a.eoff[i0 + k] = p;
-      p += c[k];
-    }
-    carry += tot;
-  }
-}
-
-__global__ __launch_bounds__(FO_THREADS) void fanout_offsets_kernel(FanoutArgs a) {
-  const uint64_t base = a.moff[0];
-  const bool refused = fo_refused(a);
-  for (uint64_t t = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; t <= a.n;
-       t += uint64_t(gridDim.x) * FO_THREADS)
-    a.out_off[t] = refused ? 0 : a.eoff[a.moff[t] - base];
 }
 
 __device__ __forceinline__ uint32_t fo_rand(uint32_t seed, uint64_t i, uint32_t salt) {
@@ -322,22 +273,20 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
   WaveLds& L = lds_all[wv];
   const uint64_t base = a.moff[0];
   const uint64_t m = fo_entries(a);
-  // overflow (deliveries or picks): nothing is written, no pick state consumed
-  if (a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS)) return;
-  const bool need_topic = a.keys && a.strategy != EMQX_SHARE_RANDOM;
+  // overflow (deliveries or picks): offsets only, no deliveries, no pick state consumed
+  const bool ids = !(a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS));
   const bool stateful = fo_stateful(a.strategy);
   const uint64_t nwaves = uint64_t(gridDim.x) * (FO_THREADS / 64);
+  const uint64_t per = fo_per_block(m);
   for (uint64_t e0 = (uint64_t(blockIdx.x) * (FO_THREADS / 64) + wv) * FO_WCHUNK; e0 < m;
        e0 += nwaves * FO_WCHUNK) {
     const uint64_t e1 = min<uint64_t>(e0 + FO_WCHUNK, m);
-    const uint64_t obase = a.eoff[e0];
-    const uint32_t total = static_cast<uint32_t>(a.eoff[e1] - obase);
+    const uint64_t blk = e0 / per;
     // the chunk's entries, EU per lane: every first-level load of the chunk is in flight
     // before the filter records are fetched, and those before anything is stored to LDS
     // (loads are unconditional, from a clamped index, and masked after: under a per-lane
     // `if` the compiler waited for each entry's loads before issuing the next entry's)
     uint32_t f[EU], tp[EU];
-    uint64_t eo[EU];
     bool v[EU];
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
@@ -345,25 +294,21 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
       v[u] = i < e1;
       const uint64_t ic = v[u] ? i : e0;
       f[u] = a.mids[base + ic];
-      eo[u] = a.eoff[ic];
-      tp[u] = need_topic ? a.entry_topic[ic] : 0u;
+      tp[u] = a.entry_topic[ic];
     }
-    // round_robin / sticky: the chunk's first pick-list index = its block's base + the chunks of
-    // the block before it (the list is in output order, one pick per $share group of an entry)
-    uint64_t gbase = 0;
-    if (stateful) {
-      const uint64_t per = fo_per_block(m);
-      const uint64_t blk = e0 / per;
-      uint64_t gl = 0;
-      for (uint64_t q = blk * per / FO_WCHUNK + lane; q < e0 / FO_WCHUNK; q += 64) gl += a.gchunk[q];
-      gbase = a.partials[3 * FO_BLOCKS + blk] + fo_wave_sum(gl);
+    const uint32_t prev_topic = e0 ? a.entry_topic[e0 - 1] : FID_NONE;
+    // the chunk's first output: its block's base + the block's chunks before it; round_robin /
+    // sticky also the chunk's first pick-list index the same way (the list is in output order,
+    // one pick per $share group of an entry)
+    uint64_t cl = 0, gl = 0;
+    for (uint64_t q = blk * per / FO_WCHUNK + lane; q < e0 / FO_WCHUNK; q += 64) {
+      cl += a.csum[q];
+      if (stateful) gl += a.gchunk[q];
     }
+    const uint64_t obase = a.partials[FO_BLOCKS + blk] + fo_wave_sum(cl);
+    uint64_t gbase = stateful ? a.partials[3 * FO_BLOCKS + blk] + fo_wave_sum(gl) : 0;
 #pragma unroll
-    for (uint32_t u = 0; u < EU; ++u) {
-      f[u] = v[u] ? f[u] : FID_NONE;
-      eo[u] = v[u] ? eo[u] : obase + total;
-      tp[u] = v[u] ? tp[u] : 0u;
-    }
+    for (uint32_t u = 0; u < EU; ++u) f[u] = v[u] ? f[u] : FID_NONE;
     uint4 r[EU];
     if (a.n_recs) {
 #pragma unroll
@@ -376,15 +321,44 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
 #pragma unroll
       for (uint32_t u = 0; u < EU; ++u) r[u] = make_uint4(0, 0, 0, 0);
     }
+    // entry offsets: exclusive scan of the entries' counts in entry order (k = lane + 64 u);
+    // entries past the chunk count 0, so their offset is the chunk's total
+    uint32_t total = 0;
+    uint32_t pre[EU];
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      const uint32_t c = r[u].y + r[u].w;
+      uint32_t incl = c;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      pre[u] = total + incl - c;
+      total += __shfl(incl, 63, 64);
+    }
+    // per-topic offsets: the first entry of a topic writes its offset for it and for the
+    // entry-less topics just before it; the chunk holding the last entry, for those after it
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) {
+      const uint32_t up = __shfl_up(tp[u], 1, 64);
+      const uint32_t last_prev = u ? __shfl(tp[u ? u - 1 : 0], 63, 64) : prev_topic;
+      const uint32_t pt = lane ? up : last_prev;
+      if (v[u] && tp[u] != pt)
+        for (uint64_t t = pt == FID_NONE ? 0 : uint64_t(pt) + 1; t <= tp[u]; ++t) a.out_off[t] = obase + pre[u];
+    }
+    if (e1 == m && lane == 0)
+      for (uint64_t t = uint64_t(a.entry_topic[m - 1]) + 1; t <= a.n; ++t) a.out_off[t] = obase + total;
+    if (!ids) continue;
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
       const uint32_t k = lane + 64u * u;
-      L.pre[k] = static_cast<uint32_t>(eo[u] - obase);  // past the chunk's end: `total`
+      L.pre[k] = pre[u];  // past the chunk's end: `total`
       L.fid[k] = f[u];
       L.pb[k] = r[u].x;
       L.np[k] = r[u].y;
       L.gb[k] = r[u].z;
-      L.top[k] = tp[u];
+      L.top[k] = v[u] ? tp[u] : 0u;
     }
     if (stateful) {  // entry k's first pick-list index: exclusive scan of n_groups in entry order
 #pragma unroll
@@ -961,13 +935,9 @@ __global__ __launch_bounds__(256) void fanout_to_host_kernel(const uint64_t* d_o
 }  // namespace
 
 hipError_t launch_fanout(const FanoutArgs& a, uint64_t m_cap, hipStream_t s) {
-  const bool need_topic = a.keys && a.strategy != EMQX_SHARE_RANDOM;
-  if (a.n && need_topic)
-    hipLaunchKernelGGL(fanout_entry_topic_kernel, dim3(grid_for(a.n, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
+  hipLaunchKernelGGL(fanout_entry_topic_kernel, dim3(grid_for(a.n + 1, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
   hipLaunchKernelGGL(fanout_count_kernel, dim3(FO_BLOCKS), dim3(FO_THREADS), 0, s, a);
   hipLaunchKernelGGL(fanout_partials_kernel, dim3(1), dim3(FO_BLOCKS), 0, s, a);
-  hipLaunchKernelGGL(fanout_final_kernel, dim3(FO_BLOCKS), dim3(FO_THREADS), 0, s, a);
-  hipLaunchKernelGGL(fanout_offsets_kernel, dim3(grid_for(a.n + 1, FO_THREADS)), dim3(FO_THREADS), 0, s, a);
   // one wave per FO_WCHUNK entries up to m_cap (waves past m exit at once)
   hipLaunchKernelGGL(fanout_write_kernel, dim3(grid_for(m_cap, FO_WCHUNK * (FO_THREADS / 64))), dim3(FO_THREADS), 0, s,
                      a);

@@ -296,6 +296,31 @@ def _p2p(t: Optional[torch.Tensor], peer: int, send: bool, group, like: Optional
     return like
 
 
+class _DeviceStep:
+    """An emqx_shard_step (shard_step.hip) on this rank's device, for the rank's plan."""
+
+    def __init__(self, device: torch.device, world: int, plan: np.ndarray):
+        from . import _lib
+        self._lib = _lib
+        pl = np.ascontiguousarray(plan, dtype=np.uint32) if len(plan) else np.zeros((1, 2), np.uint32)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().emqx_shard_step_create(device.index if device.index is not None else 0, world,
+                                                     pl.ctypes.data, len(plan), ctypes.byref(h)),
+                   "emqx_shard_step_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self._lib.lib().emqx_shard_step_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ShardedMatcher:
     """A filter-sharded table over the ranks of a process group (two engines per rank).
 
@@ -328,12 +353,24 @@ class ShardedMatcher:
                 self.engines.append(e)
             match_fn = self._engine_match
         self.match_fn = match_fn
+        # the device step (emqx_shard_step_*) when this rank's own HIP engines do the matching;
+        # an injected match_fn (tests on CPU over gloo) takes the tensor path below
+        self._step = _DeviceStep(self.device, self.world, self.plan) if (
+            self.device.type == "cuda" and self.match_fn == self._engine_match) else None
+        self._caps = [1 << 20, 1 << 20]
+        self._bufs = {}
+        self._stream = None
 
     @property
     def n_local_filters(self) -> int:
         return int(sum(len(g) for _, g in self.local))
 
     def _engine_match(self, which: int, tb: torch.Tensor, to: torch.Tensor):
+        d_off, d_ids = self._engine_csr(which, tb, to)
+        return d_off[1:] - d_off[:-1], d_ids
+
+    def _engine_csr(self, which: int, tb: torch.Tensor, to: torch.Tensor):
+        """Synchronous match on engine `which`, growing the id buffer to the exact need."""
         n = to.numel() - 1
         d_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         caps = getattr(self, "_caps", [1 << 20, 1 << 20])
@@ -352,13 +389,132 @@ class ShardedMatcher:
                 cap = need + 1
         caps[which] = max(cap, caps[which])
         self._caps = caps
-        return d_off[1:] - d_off[:-1], d_ids[:m]
+        return d_off, d_ids[:m]
 
     def match_all(self, topics: Tuple[torch.Tensor, torch.Tensor]):
         """Every rank matches its own batch against the sharded table and gets its own CSR
         (offsets int64 (n+1,), ids int32) in batch order — the layout's weak-scaling use, one
-        publishing node per rank.  Two host synchronisations per call: the size matrix of the
-        requests and the id totals of the answers (the all-to-all split lists)."""
+        publishing node per rank.  Two host synchronisations per call: the split sizes of the
+        requests and of the answers (the all-to-all split lists)."""
+        if self._step is not None:
+            # on a stream of its own: the engines take a null stream handle for "their own
+            # stream", so the step's kernels and the engine calls must share a real one
+            caller = torch.cuda.current_stream(self.device)
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(device=self.device)
+            self._stream.wait_stream(caller)
+            with torch.cuda.stream(self._stream):
+                res = self._match_all_device(topics)
+            caller.wait_stream(self._stream)
+            for t in res:
+                t.record_stream(caller)
+            return res
+        return self._match_all_tensors(topics)
+
+    def _buf(self, name: str, n: int, dtype) -> torch.Tensor:
+        """A reused device buffer of at least n elements (every use is ordered on one stream)."""
+        b = self._bufs.get(name)
+        if b is None or b.numel() < n:
+            b = torch.empty(max(int(n * 1.25), 64), dtype=dtype, device=self.device)
+            self._bufs[name] = b
+        return b
+
+    def _match_all_device(self, topics: Tuple[torch.Tensor, torch.Tensor]):
+        """match_all on device kernels (emqx_shard_step_*, shard_step.hip): route + stable sort
+        + pack the requests, one all-to-all of sizes and one of chunks, unpack into the two
+        engines' batches, both engines matched asynchronously into learnt capacities, the
+        answers packed per source, one all-to-all of sizes and one of answers, merged back in
+        batch order.  The host only reads the split sizes (two syncs)."""
+        from . import _lib
+        L = _lib.lib()
+        dev, G, grp = self.device, self.world, self.group
+        st = self._step.h
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        S = ctypes.c_void_p(stream)
+        tb, to = topics
+        tb = tb.to(dev)
+        to = to.to(dev).to(torch.int64)
+        if tb.numel() == 0:
+            tb = torch.zeros(16, dtype=torch.uint8, device=dev)
+        n = to.numel() - 1
+        # 1. requests -> one chunk per destination
+        cap = int(L.emqx_shard_send_cap(n, tb.numel(), G))
+        send = self._buf("send", cap, torch.uint8)
+        meta = torch.empty(5 * G, dtype=torch.int64, device=dev)
+        _lib.check(L.emqx_shard_step_send(st, P(tb), P(to), n, P(send), send.numel(), P(meta), S),
+                   "emqx_shard_step_send")
+        meta_in = torch.empty_like(meta)
+        _a2a(meta_in, meta, [5] * G, [5] * G, grp)
+        mh = torch.stack([meta, meta_in]).cpu().numpy()  # host sync 1
+        mo, mi = mh[0].reshape(G, 5), np.ascontiguousarray(mh[1].reshape(G, 5))
+        if (mo[:, 0] < 0).any() or (mi[:, 0] < 0).any():
+            raise RuntimeError("emqx_shard_step_send: chunks over the send buffer")
+        out_b, in_b = mo[:, 0].tolist(), mi[:, 0].tolist()
+        recv = self._buf("recv", sum(in_b) + 16, torch.uint8)
+        _a2a(recv[: sum(in_b)], send[: sum(out_b)], in_b, out_b, grp)
+        NA, NB = int(mi[:, 1].sum()), int(mi[:, 2].sum())
+        a_bytes = self._buf("a_bytes", int(mi[:, 3].sum()) + 16, torch.uint8)
+        b_bytes = self._buf("b_bytes", int(mi[:, 4].sum()) + 16, torch.uint8)
+        a_off = self._buf("a_off", NA + 1, torch.int64)
+        b_off = self._buf("b_off", NB + 1, torch.int64)
+        _lib.check(L.emqx_shard_step_recv(st, P(recv), mi.ctypes.data, P(a_bytes), P(a_off), P(b_bytes), P(b_off), S),
+                   "emqx_shard_step_recv")
+        self.last_local_topics = NA + NB
+        # 2. the two engines, asynchronously, into learnt capacities
+        batches = [(a_bytes, a_off, NA), (b_bytes, b_off, NB)]
+        outs = []
+        summ = self._buf("summary", 16, torch.int64)
+        summ[:16].zero_()
+        for e, (eb, eo, ne) in enumerate(batches):
+            cap_e = max(self._caps[e], 1 << 16)
+            ro = self._buf(f"off{e}", ne + 1, torch.int64)
+            ri = self._buf(f"ids{e}", cap_e, torch.int32)
+            if ne:
+                self.engines[e].match_device_async(eb.data_ptr(), eo.data_ptr(), ne, ro.data_ptr(), ri.data_ptr(),
+                                                   ri.numel(), summ[8 * e:].data_ptr(), mode=self.mode, stream=stream)
+            else:
+                ro[:1].zero_()
+            outs.append([ro, ri])
+        # 3. answers, one chunk per source; a call that did not complete is redone before the
+        # exchange (every rank learns every rank's flag from the size exchange)
+        redo = False
+        while True:
+            ans = self._buf("answer", 4 * G + NA + NB + outs[0][1].numel() + outs[1][1].numel(), torch.int32)
+            ans_meta = torch.empty(2 * G, dtype=torch.int64, device=dev)
+            sp = [None if redo else P(summ[8 * e:]) for e in (0, 1)]
+            _lib.check(L.emqx_shard_step_answer(st, P(outs[0][0]), P(outs[0][1]), sp[0], P(outs[1][0]),
+                                                P(outs[1][1]), sp[1], P(ans), P(ans_meta), S), "emqx_shard_step_answer")
+            ans_in = torch.empty_like(ans_meta)
+            _a2a(ans_in, ans_meta, [2] * G, [2] * G, grp)
+            h = torch.cat([ans_meta, ans_in, summ[:16]]).cpu().numpy()  # host sync 2
+            am, ai, sm = h[: 2 * G].reshape(G, 2), np.ascontiguousarray(h[2 * G: 4 * G]), h[4 * G:].reshape(2, 8)
+            if not redo:
+                for e in (0, 1):  # learn the id capacities from this call's totals
+                    if sm[e, 0] == 0:
+                        self._caps[e] = max(self._caps[e], int(sm[e, 1] * 1.25) + 4096)
+            if not ai.reshape(G, 2)[:, 1].any():
+                break
+            if am[0, 1]:  # this rank's call did not complete: redo it synchronously, exact size
+                for e, (eb, eo, ne) in enumerate(batches):
+                    if ne and sm[e, 0]:
+                        outs[e] = list(self._engine_csr(e, eb, eo[: ne + 1]))
+                        self._caps[e] = max(self._caps[e], int(outs[e][1].numel() * 1.25) + 4096)
+            redo = True
+        # 4. answers back to their sources, merged per topic in batch order
+        out_w, in_w = am[:, 0].tolist(), ai.reshape(G, 2)[:, 0].tolist()
+        back = self._buf("back", sum(in_w) + 16, torch.int32)
+        _a2a(back[: sum(in_w)], ans[: sum(out_w)], in_w, out_w, grp)
+        total = int(sum(in_w) - 4 * G - mo[:, 1].sum() - mo[:, 2].sum())
+        out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        out_ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        _lib.check(L.emqx_shard_step_merge(st, P(back), ai.ctypes.data, P(out_off), P(out_ids), S),
+                   "emqx_shard_step_merge")
+        return out_off, out_ids[:total]
+
+    def _match_all_tensors(self, topics: Tuple[torch.Tensor, torch.Tensor]):
+        """match_all with torch tensor ops (an injected match_fn: the distribution logic on CPU
+        over gloo in the tests)."""
         dev, G, grp = self.device, self.world, self.group
         i64 = dict(dtype=torch.int64, device=dev)
         tb, to = topics

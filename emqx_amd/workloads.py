@@ -11,6 +11,7 @@ HASH_CODE = '#', ABSENT = level not present.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Sequence, Tuple
 
@@ -58,8 +59,10 @@ def _padded(vb: np.ndarray, vo: np.ndarray) -> np.ndarray:
     lens = np.diff(vo)
     V, W = len(lens), int(lens.max(initial=0))
     t = np.full((V, max(W, 1)), PAD, dtype=np.uint8)
-    for k in range(V):
-        t[k, : lens[k]] = vb[vo[k]:vo[k + 1]]
+    if V and W:
+        col = np.arange(W)[None, :]
+        inside = col < lens[:, None]
+        t[inside] = vb[(vo[:-1, None] + col)[inside]]
     return t
 
 
@@ -80,10 +83,8 @@ def compose(codes: np.ndarray, level_vocabs: List[Tuple[np.ndarray, np.ndarray]]
         extra[0, 0] = ord("+")
         extra[1, 0] = ord("#")
         tables.append(np.concatenate([t, extra]))
-    out_bufs, out_lens = [], []
-    for c0 in range(0, N, chunk):
+    def one(c0):
         c = codes[c0:c0 + chunk]
-        n = c.shape[0]
         cols = []
         for l in range(D):
             tb = tables[l]
@@ -96,8 +97,12 @@ def compose(codes: np.ndarray, level_vocabs: List[Tuple[np.ndarray, np.ndarray]]
             cols.append(tb[idx])
         mat = np.concatenate(cols, axis=1)
         keep = mat != PAD
-        out_lens.append(keep.sum(1))
-        out_bufs.append(mat[keep])
+        return keep.sum(1), mat[keep]
+
+    # chunks are independent (numpy releases the GIL in these kernels): a thread pool, same bytes
+    parts = _pmap(one, range(0, N, chunk))
+    out_lens = [p[0] for p in parts]
+    out_bufs = [p[1] for p in parts]
     lens = np.concatenate(out_lens) if out_lens else np.zeros(0, np.int64)
     offs = np.zeros(N + 1, dtype=np.uint64)
     offs[1:] = np.cumsum(lens)
@@ -143,11 +148,37 @@ def dedupe_rows(codes: np.ndarray) -> np.ndarray:
     return codes[np.sort(first)]
 
 
+def _threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def _pmap(fn, items):
+    """[fn(x) for x in items] on a thread pool (the generators' numpy kernels release the GIL;
+    results in order, so the output is the same as the serial loop's)."""
+    items = list(items)
+    if len(items) <= 1 or _threads() == 1:
+        return [fn(x) for x in items]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(_threads()) as ex:
+        return list(ex.map(fn, items))
+
+
 def zipf_sampler(rng: np.random.Generator, vsize: int, s: float = 1.1):
     p = 1.0 / np.arange(1, vsize + 1, dtype=np.float64) ** s
     cdf = np.cumsum(p)
     cdf /= cdf[-1]
-    return lambda n: np.minimum(np.searchsorted(cdf, rng.random(n)), vsize - 1).astype(np.int32)
+
+    def draw(n):
+        u = rng.random(n)  # one draw from the generator's stream, as before
+        step = 1 << 21
+        parts = _pmap(lambda a: np.searchsorted(cdf, u[a:a + step]), range(0, n, step))
+        idx = np.concatenate(parts) if parts else np.zeros(0, np.int64)
+        return np.minimum(idx, vsize - 1).astype(np.int32)
+    return draw
 
 
 def level_vocabs(prefixes: Sequence[bytes], sizes: Sequence[int]):
@@ -247,8 +278,9 @@ def config_b(n_filters: int = 10_000_000, n_topics: int = 1_000_000, seed: int =
     if topic_seed is not None:  # an independent topic stream over the same table
         rng = np.random.default_rng(topic_seed)
         samplers = [zipf_sampler(rng, v) for v in sizes]
-    topics = _b_topics(rng, samplers, fcodes, vs, n_filters, n_topics)
+    topics, tcodes = _b_topics(rng, samplers, fcodes, vs, n_filters, n_topics, codes=True)
     wl = Workload("B", filters, topics)
+    wl.fcodes, wl.tcodes = fcodes, tcodes  # level codes (oracle/pruned.py narrows the oracle's table)
     extra = []
     for ts in extra_topic_seeds:
         r2 = np.random.default_rng(ts)
@@ -257,7 +289,7 @@ def config_b(n_filters: int = 10_000_000, n_topics: int = 1_000_000, seed: int =
     return wl
 
 
-def _b_topics(rng, samplers, fcodes, vs, n_filters, n_topics):
+def _b_topics(rng, samplers, fcodes, vs, n_filters, n_topics, codes=False):
     """One topic batch of config B over the filter codes `fcodes` (see config_b)."""
     # topics (levels up to 8 + 3 for '#' expansion => pad to 11)
     TD = 11
@@ -287,7 +319,8 @@ def _b_topics(rng, samplers, fcodes, vs, n_filters, n_topics):
     tcodes = tcodes[perm]
     # levels >= 8 use level-7 vocab words (instantiated '#' expansions)
     tv = vs[:8] + [vs[7]] * 3
-    return compose(tcodes, tv)
+    packed = compose(tcodes, tv)
+    return (packed, tcodes) if codes else packed
 
 
 # ---------------------------------------------------------------------------------------

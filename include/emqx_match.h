@@ -489,6 +489,48 @@ int emqx_batch_permute_device(const uint8_t* d_bytes, const uint64_t* d_offsets,
 int emqx_csr_unpermute_device(const uint32_t* d_counts, const uint32_t* d_ids, uint64_t n, const uint32_t* d_perm,
                               uint64_t* d_out_offsets, uint32_t* d_out_ids, void* d_scratch, void* stream);
 
+/* One rank's filter-sharded match step on the device (emqx_amd/dist.py ShardedMatcher.match_all;
+ * DESIGN.md §6), split at the exchanges the caller makes with its collectives (all_to_all over
+ * RCCL): each call enqueues on `stream` and returns, nothing waits for the device, and the
+ * step's scratch (learnt, grown with the batch) stays on the step.  One step at a time per
+ * object; world <= EMQX_SHARD_MAX_WORLD; a batch holds fewer than 2^31 topics.
+ *   send    routes each topic (emqx_shard_route rules), sorts its requests by destination
+ *           (stable) and packs one chunk per destination rank into d_send (send_cap >=
+ *           emqx_shard_send_cap(n, batch bytes, world) bytes), chunk r first at the sum of the
+ *           sizes before it:
+ *             [u32 nA, nB, bytesA, bytesB][u32 offsets of the nA A-requests, + 1][B, + 1] pad 16
+ *             [A topic bytes][B topic bytes] pad 16
+ *           d_meta[5 * world] (i64, device): per destination the chunk bytes (-1: over send_cap),
+ *           nA, nB, bytesA, bytesB — what the destination passes to recv.
+ *   recv    meta_in[5 * world] (host) = the meta the sources sent this rank, d_recv their
+ *           chunks in source order -> the engine-A batch (every source's A requests in source
+ *           order: sum nA topics, sum bytesA bytes, offsets from 0) and the engine-B batch.
+ *   answer  the two engines' CSRs over those batches (and their emqx_match_batch_device_async
+ *           summaries, or NULL) -> one answer chunk per source in d_answer (u32 words, chunk s
+ *           first at the sum of the sizes before it; room for 4 * world + NA + NB + ids):
+ *             [nA, nB, idsA, idsB][counts of the A requests][counts of B][A ids][B ids]
+ *           d_ans_meta[2 * world] (i64, device): per source the chunk's words and a flag, 1 when
+ *           an engine call did not complete (its summary flags): then no ids were copied and the
+ *           caller redoes that match and the answer before the exchange.
+ *   merge   ans_meta_in[2 * world] (host) = what the destinations sent, d_back their chunks ->
+ *           the CSR of the batch given to send, in batch order (d_out_offsets[n + 1], d_out_ids:
+ *           each topic's engine-A ids, then its engine-B ids). */
+#define EMQX_SHARD_MAX_WORLD 64
+typedef struct emqx_shard_step emqx_shard_step;
+int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* splits, uint32_t n_splits,
+                           emqx_shard_step** out);
+int emqx_shard_step_destroy(emqx_shard_step* st);
+uint64_t emqx_shard_send_cap(uint64_t n, uint64_t batch_bytes, uint32_t world);
+int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                         uint8_t* d_send, uint64_t send_cap, int64_t* d_meta, void* stream);
+int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* d_recv, const int64_t* meta_in, uint8_t* d_a_bytes,
+                         uint64_t* d_a_offsets, uint8_t* d_b_bytes, uint64_t* d_b_offsets, void* stream);
+int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* d_a_offsets, const uint32_t* d_a_ids,
+                           const uint64_t* d_a_summary, const uint64_t* d_b_offsets, const uint32_t* d_b_ids,
+                           const uint64_t* d_b_summary, uint32_t* d_answer, int64_t* d_ans_meta, void* stream);
+int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* d_back, const int64_t* ans_meta_in,
+                          uint64_t* d_out_offsets, uint32_t* d_out_ids, void* stream);
+
 /* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */
 int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filter,
                      uint64_t filter_len);

@@ -1,0 +1,163 @@
+"""The filter-sharded step on device kernels (emqx_amd/csrc/shard_step.hip, emqx_shard_step_*,
+driven by emqx_amd/dist.py ShardedMatcher.match_all), ID-for-ID against the oracle
+(oracle/trie_oracle.cpp: emqx_trie DFS + match_routes/1, apps/emqx/src/emqx_router.erl:128-133):
+
+* edge batches at world 1 over RCCL: an empty batch, one-level topics (no engine-B request),
+  '$' topics (no '+/x' match, emqx_topic.erl:71-74), wildcard topic names (one request, to
+  their byte-identical filter), topics whose only matches are root wildcards;
+* the redo path: id capacities far too small, so both engine calls overflow and are redone
+  before the answer exchange;
+* two ranks sharing the one GPU over gloo (a rehearsal of the N-rank exchange on real device
+  kernels), each rank's own batch checked ID-for-ID.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cpp as C
+
+pytestmark = pytest.mark.gpu
+
+FILTERS = [b"#", b"+", b"+/#", b"+/+", b"+/+/#", b"a", b"a/b", b"a/+", b"a/#", b"+/b", b"+/b/c", b"+/b/#",
+           b"$SYS/#", b"$SYS/x", b"$SYS/+/y", b"a/b/c/d/e", b"q/+/+/+/#", b"x/y", b"+/y/z", b"m/#",
+           b"s/+", b"s/t/#", b"a/+/c", b"+/+/c"]
+TOPICS = [b"a", b"a/b", b"a/b/c", b"$SYS/x", b"$SYS/x/y", b"$SYS", b"x/y", b"x/y/z", b"q/1/2/3",
+          b"q/1/2/3/4/5", b"m", b"zz", b"s/t", b"s/t/u", b"a/+", b"+/b", b"#", b"a/#", b"+/y/z",
+          b"a/b/c/d/e", b"/", b"a//", b"//b", b"c", b"a/q/c"]
+
+
+def _init(port):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+
+
+def _dev_topics(packed):
+    import torch
+    buf, offs = packed
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(np.array(buf, dtype=np.uint8)).to(dev) if len(buf) else torch.zeros(0, dtype=torch.uint8, device=dev)
+    return tb, torch.from_numpy(np.asarray(offs).astype(np.int64)).to(dev)
+
+
+def _oracle(filters, topics):
+    o = C.CppOracle(True)
+    o.add_packed(*filters)
+    o.freeze()
+    off, ids, _ = o.match_csr(*topics, mode=C.MODE_ROUTES, threads=4)
+    return off, ids
+
+
+def _check(res, filters, topics):
+    off, ids = res[0].cpu().numpy(), res[1].cpu().numpy().view(np.uint32)
+    off_o, ids_o = _oracle(filters, topics)
+    assert len(off) == len(off_o)
+    bad = C.csr_mismatches(off.astype(np.uint64), ids, off_o, ids_o)
+    assert bad.size == 0, bad[:10]
+    return int(off_o[-1])
+
+
+def test_shard_step_edge_batches_world1():
+    import torch
+    import torch.distributed as dist
+    from emqx_amd.dist import ShardedMatcher
+    from emqx_amd.engine import pack
+    filters = pack(FILTERS)
+    _init(29561)
+    try:
+        sm = ShardedMatcher(filters, device=torch.device("cuda:0"))
+        assert sm._step is not None  # the device step, not the tensor path
+        topics = pack(TOPICS)
+        got = sm.match_all(_dev_topics(topics))
+        assert _check(got, filters, topics) > 0
+        # the same batch through the tensor path (engines as match_fn): the same CSR, in order
+        off_t, ids_t = sm._match_all_tensors(_dev_topics(topics))
+        assert torch.equal(off_t.cpu(), got[0].cpu()) and torch.equal(ids_t.cpu(), got[1].cpu())
+        # an empty batch, a one-topic batch, and a batch of topics no filter besides roots matches
+        empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+        off, ids = sm.match_all(_dev_topics(empty))
+        assert off.cpu().tolist() == [0] and ids.numel() == 0
+        for batch in ([b"a/b"], [b"zz/yy/xx"] * 7, [b"$SYS"] * 3):
+            t = pack(batch)
+            _check(sm.match_all(_dev_topics(t)), filters, t)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_step_redo_on_small_capacities():
+    """Both engine calls overflow their (forced) tiny id buffers: the answer kernel flags them,
+    every rank learns it from the size exchange, the calls are redone, and the CSR is exact."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import workloads as W
+    from emqx_amd.dist import ShardedMatcher
+    wl = W.config_b(n_filters=300_000, n_topics=30_000, seed=3, vocab_scale=4)
+    _init(29563)
+    try:
+        sm = ShardedMatcher(wl.filters, device=torch.device("cuda:0"))
+        sm._caps = [1, 1]  # the floor of 64K ids is below this batch's ids on both engines
+        got = sm.match_all(_dev_topics(wl.topics))
+        total = _check(got, wl.filters, wl.topics)
+        assert total > 2 * 65536
+        assert max(sm._caps) > 65536  # learnt from the redo
+        again = sm.match_all(_dev_topics(wl.topics))  # learnt capacities: no redo
+        assert torch.equal(again[0].cpu(), got[0].cpu()) and torch.equal(again[1].cpu(), got[1].cpu())
+    finally:
+        dist.destroy_process_group()
+
+
+def _rank_main(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import workloads as W
+    from emqx_amd.dist import ShardedMatcher
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        wl = W.config_b(n_filters=200_000, n_topics=8000, seed=3, vocab_scale=4,
+                        topic_seed=None if rank == 0 else 1000 + rank)
+        sm = ShardedMatcher(wl.filters, device=torch.device("cuda:0"))
+        assert sm._step is not None
+        # two steps: the second reuses the learnt buffers; a third with an empty batch on rank 1
+        sm.match_all(_dev_topics(wl.topics))
+        got = sm.match_all(_dev_topics(wl.topics))
+        empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+        third = sm.match_all(_dev_topics(empty if rank == 1 else wl.topics))
+        off, ids = got[0].cpu().numpy(), got[1].cpu().numpy().view(np.uint32)
+        off_o, ids_o = _oracle(wl.filters, wl.topics)
+        bad = C.csr_mismatches(off.astype(np.uint64), ids, off_o, ids_o)
+        if rank == 1:
+            third_ok = third[0].numel() == 1 and third[1].numel() == 0
+        else:  # the same topics on a smaller exchange: the same sets (in-topic order may differ)
+            third_ok = C.csr_mismatches(third[0].cpu().numpy().astype(np.uint64),
+                                        third[1].cpu().numpy().view(np.uint32), off_o, ids_o).size == 0
+        q.put((rank, int(bad.size), int(off_o[-1]), sm.last_local_topics, bool(third_ok), sm.n_local_filters))
+    except Exception as e:  # reported to the parent
+        q.put((rank, -1, repr(e), 0, False, 0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_step_two_ranks_share_one_gpu():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, 29565
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=110) for _ in range(world)]
+    for p in ps:
+        p.join(30)
+    res.sort()
+    for rank, bad, ids, local, third_ok, nf in res:
+        assert bad == 0, (rank, ids)
+        assert ids > 0 and local > 0 and third_ok
+    # every rank holds part of the table (two key spaces), not all of it
+    assert all(r[5] < 200_000 for r in res)
