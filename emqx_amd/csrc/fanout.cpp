@@ -26,8 +26,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -264,7 +266,7 @@ struct PubBatchPriv;
 struct emqx_subtab {
   int device = 0;
   std::mutex mu;   // serialises mutations, the host half of commits, and fan-out enqueues
-  std::mutex cmu;  // one commit at a time (held across its device half, which s->mu is not)
+  std::mutex cmu;  // one commit at a time (held while it drains the previous device half, which s->mu is not)
   uint8_t* h_stage = nullptr;  // pinned staging of a commit's uploads (one commit at a time)
   uint64_t stage_cap = 0;
   // ---- host store, and the image of every device array ----
@@ -305,6 +307,8 @@ struct emqx_subtab {
   hipStream_t stream = nullptr;       // commits and table maintenance
   hipEvent_t commit_ev = nullptr;     // end of the last commit: later fan-outs wait for it
   bool commit_pending = false;
+  bool commit_inflight = false;       // (s->cmu) the last commit's device half not yet waited for
+  std::vector<void*> retired_prev;    // (s->cmu) device arrays it replaced: freed once it is done
   hipEvent_t state_ev = nullptr;      // end of the last round_robin / sticky resolve (or re-pick):
   bool state_pending = false;         // the next one waits for it, so state updates follow call order
   std::vector<WordPatch> wpatch;
@@ -463,6 +467,17 @@ void plain_remove(emqx_subtab* s, uint32_t f, uint32_t sub) {
   note_op(s);
 }
 
+// The device form of filter f's record (fanout.h FO_INLINE): a short plain list and no
+// groups inline, otherwise the image's record.
+uint4 dev_rec(const emqx_subtab* s, uint32_t f) {
+  const FilterRec& r = s->recs[f];
+  if (r.n_groups == 0 && r.n_plain >= 1 && r.n_plain <= FO_INLINE) {
+    const uint32_t* p = s->plain.data() + r.plain_begin;
+    return make_uint4(p[0], r.n_plain | FO_INLINE_BIT, r.n_plain > 1 ? p[1] : 0u, r.n_plain > 2 ? p[2] : 0u);
+  }
+  return make_uint4(r.plain_begin, r.n_plain, r.group_begin, r.n_groups);
+}
+
 // ---- batched plain ops on several threads --------------------------------------------------
 // A batch of plain subscribes or unsubscribes runs one thread per filter shard (pp_shard): a
 // shard's filters, their records, extents and map entries belong to its thread alone, and a
@@ -481,6 +496,65 @@ unsigned par_threads() {
   }();
   return t;
 }
+
+// A small pool of worker threads, kept for the process (spawning 16 threads per batch cost more
+// than the batch's work): run(fn, t) runs fn on the caller and t - 1 workers and returns when
+// all are done.  One run at a time (callers hold s->mu; several tables share the pool through
+// its own lock).
+class WorkPool {
+ public:
+  static WorkPool& get() {
+    static WorkPool* p = new WorkPool();  // never destroyed: workers may outlive static teardown
+    return *p;
+  }
+  void run(const std::function<void()>& fn, unsigned t) {
+    std::lock_guard<std::mutex> one(run_mu_);
+    t = std::max(1u, t);
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      while (workers_.size() < t - 1) {
+        try {
+          workers_.emplace_back([this, id = workers_.size()] { loop(id); });
+        } catch (...) {
+          break;
+        }
+      }
+      job_ = &fn;
+      want_ = std::min<size_t>(t - 1, workers_.size());
+      left_ = want_;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(size_t id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void()>* job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= want_) continue;
+        job = job_;
+      }
+      (*job)();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> workers_;
+  const std::function<void()>* job_ = nullptr;
+  size_t want_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+};
 
 struct PlainLocal {
   std::vector<uint32_t> arena;                        // lists moved in this batch
@@ -574,21 +648,11 @@ void plain_batch(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, uint6
   }
   std::vector<PlainLocal> loc(PP_SHARDS);
   std::atomic<uint32_t> next{0};
-  auto work = [&] {
+  const std::function<void()> work = [&] {
     for (uint32_t k; (k = next.fetch_add(1)) < PP_SHARDS;)
       plain_batch_shard(s, fs, subs, idx.data() + start[k], start[k + 1] - start[k], add, loc[k]);
   };
-  const unsigned T = std::min<unsigned>(par_threads(), static_cast<unsigned>((n + PAR_MIN / 4 - 1) / (PAR_MIN / 4)));
-  std::vector<std::thread> th;
-  for (unsigned t = 1; t < T; ++t) {
-    try {
-      th.emplace_back(work);
-    } catch (...) {
-      break;  // fewer threads: the others take more shards
-    }
-  }
-  work();
-  for (auto& t : th) t.join();
+  WorkPool::get().run(work, std::min<unsigned>(par_threads(), static_cast<unsigned>((n + PAR_MIN / 4 - 1) / (PAR_MIN / 4))));
   // merge, shard by shard: moved lists appended to the shared arena
   for (PlainLocal& L : loc) {
     if (!L.arena.empty()) {
@@ -701,7 +765,12 @@ int full_commit(emqx_subtab* s) {
     return EMQX_OK;
   };
   DevArr<uint32_t> alive;
-  int rc = up(recs, s->recs);
+  std::vector<FilterRec> drecs(s->recs.size());  // the device form (inline short lists)
+  for (uint64_t f = 0; f < drecs.size(); ++f) {
+    const uint4 v = dev_rec(s, static_cast<uint32_t>(f));
+    drecs[f] = FilterRec{v.x, v.y, v.z, v.w};
+  }
+  int rc = up(recs, drecs);
   if (rc == EMQX_OK) rc = up(plain, s->plain);
   if (rc == EMQX_OK) rc = up(groups, s->groups);
   if (rc == EMQX_OK) rc = up(members, s->members);
@@ -800,7 +869,9 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   std::vector<std::pair<uint64_t, uint64_t>> copies_plain, copies_members;
   auto words = [&](const std::vector<std::pair<uint64_t, uint64_t>>& ranges, const std::vector<uint32_t>& img,
                    std::vector<std::pair<uint64_t, uint64_t>>& copies) {
-    for (const auto& rg : ranges) {
+    for (size_t i = 0; i < ranges.size(); ++i) {
+      if (i + 16 < ranges.size()) __builtin_prefetch(img.data() + ranges[i + 16].first);  // random words
+      const auto& rg = ranges[i];
       if (rg.second >= RANGE_COPY_MIN) {
         copies.push_back(rg);
         continue;
@@ -824,10 +895,18 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
     s->rpatch.push_back(RecPatch{static_cast<uint32_t>(gi), {0, 0, 0}, make_uint4(g.member_begin, g.n_members, g.slot, g.group_id)});
   }
   const uint64_t n_group_p = s->rpatch.size();
-  for (uint32_t f : s->dirty_recs) {
-    s->rec_flag[f] = 0;
-    const FilterRec& r = s->recs[f];
-    s->rpatch.push_back(RecPatch{f, {0, 0, 0}, make_uint4(r.plain_begin, r.n_plain, r.group_begin, r.n_groups)});
+  {  // two-stage prefetch: the record 16 ahead, its plain list (inline candidates) 8 ahead
+    const std::vector<uint32_t>& dr = s->dirty_recs;
+    for (size_t i = 0; i < dr.size(); ++i) {
+      if (i + 16 < dr.size()) __builtin_prefetch(&s->recs[dr[i + 16]]);
+      if (i + 8 < dr.size()) {
+        const FilterRec& r8 = s->recs[dr[i + 8]];
+        if (r8.n_plain && r8.n_plain <= FO_INLINE) __builtin_prefetch(s->plain.data() + r8.plain_begin);
+      }
+      const uint32_t f = dr[i];
+      s->rec_flag[f] = 0;
+      s->rpatch.push_back(RecPatch{f, {0, 0, 0}, dev_rec(s, f)});
+    }
   }
   const uint64_t n_rec_p = s->rpatch.size() - n_group_p;
   const auto t1 = std::chrono::steady_clock::now();
@@ -913,22 +992,35 @@ int commit_enqueue(emqx_subtab* s, std::vector<void*>& retired) {
   return EMQX_OK;
 }
 
-// A whole commit (s->cmu held, s->mu not): the host half under s->mu, then the wait for the
-// device half without it, so fan-outs are enqueued meanwhile (they wait for commit_ev on the
-// device, not on the host).
+// The previous commit's device half (s->cmu held): waited for, and the arrays it replaced
+// freed.  Its staging is then free for the next host half.
+int commit_drain(emqx_subtab* s) {
+  int rc = EMQX_OK;
+  if (s->commit_inflight && hipEventSynchronize(s->commit_ev) != hipSuccess) rc = EMQX_EDEVICE;
+  s->commit_inflight = false;
+  for (void* p : s->retired_prev) (void)hipFree(p);
+  s->retired_prev.clear();
+  return rc;
+}
+
+// A whole commit (s->cmu held, s->mu not): the previous commit's device half is drained first
+// (outside s->mu), then the host half runs under s->mu and the call returns without waiting for
+// its own device half: every fan-out enqueued after the return waits for commit_ev on the
+// device, so the changes are visible to it all the same, and the caller's next changes (the next
+// subscribe round, the coalescer's next batch) are prepared while the device applies these.  A
+// device error of a commit is reported by the next one (which then rebuilds the tables).
 int commit_now(emqx_subtab* s) {
   const auto t0 = std::chrono::steady_clock::now();
+  int rc = commit_drain(s);
   std::vector<void*> retired;
-  int rc;
   {
     std::lock_guard<std::mutex> g(s->mu);
-    rc = commit_enqueue(s, retired);
+    if (rc == EMQX_OK) rc = commit_enqueue(s, retired);
+    if (rc != EMQX_OK) s->need_full = true;
+    s->st_total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   }
-  if (rc == EMQX_OK && hipEventSynchronize(s->commit_ev) != hipSuccess) rc = EMQX_EDEVICE;
-  for (void* p : retired) (void)hipFree(p);
-  std::lock_guard<std::mutex> g(s->mu);
-  if (rc != EMQX_OK) s->need_full = true;
-  s->st_total_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  s->retired_prev = std::move(retired);
+  s->commit_inflight = rc == EMQX_OK;
   return rc;
 }
 
@@ -1239,6 +1331,7 @@ struct PubBatchPriv {
 emqx_subtab::~emqx_subtab() {
   (void)hipSetDevice(device);
   if (stream) (void)hipStreamSynchronize(stream);
+  for (void* p : retired_prev) (void)hipFree(p);
   for (auto& c : scratch)
     if (c->used) (void)hipEventSynchronize(c->done);
   for (emqx_pub_batch* b : pb_free) emqx_pub_batch_destroy(b);

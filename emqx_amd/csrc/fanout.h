@@ -28,6 +28,13 @@ struct FilterRec {
   uint32_t group_begin;  // first entry in groups[]
   uint32_t n_groups;     // $share groups with >= 1 member
 };
+// The device copy of a record whose filter has 1..FO_INLINE plain subscribers and no $share
+// group holds them inline: {s0, n_plain | FO_INLINE_BIT, s1, s2}, so its deliveries cost no
+// second random line (the host image keeps the arena form; fanout.cpp dev_rec).
+constexpr uint32_t FO_INLINE = 3;
+constexpr uint32_t FO_INLINE_BIT = 0x80000000u;
+__host__ __device__ inline uint32_t fo_rec_plain(uint4 r) { return r.y & ~FO_INLINE_BIT; }
+__host__ __device__ inline uint32_t fo_rec_groups(uint4 r) { return (r.y & FO_INLINE_BIT) ? 0u : r.w; }
 
 // Per ($share group, filter) with members (16 B).
 struct GroupRec {

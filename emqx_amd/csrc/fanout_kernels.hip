@@ -115,8 +115,8 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) 
     for (uint32_t u = 0; u < EU; ++u) {
       const bool in = f[u] < a.n_recs;
       const uint4 r = *reinterpret_cast<const uint4*>(a.recs + (in ? f[u] : 0u));
-      c[u] = in ? r.y + r.w : 0u;
-      g[u] = in ? r.w : 0u;
+      c[u] = in ? fo_rec_plain(r) + fo_rec_groups(r) : 0u;
+      g[u] = in ? fo_rec_groups(r) : 0u;
     }
     uint32_t gl = 0;
     uint64_t cs = 0;
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
     uint32_t pre[EU];
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
-      const uint32_t c = r[u].y + r[u].w;
+      const uint32_t c = fo_rec_plain(r[u]) + fo_rec_groups(r[u]);
       uint32_t incl = c;
 #pragma unroll
       for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -355,22 +355,23 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
       const uint32_t k = lane + 64u * u;
       L.pre[k] = pre[u];  // past the chunk's end: `total`
       L.fid[k] = f[u];
-      L.pb[k] = r[u].x;
-      L.np[k] = r[u].y;
-      L.gb[k] = r[u].z;
+      L.pb[k] = r[u].x;   // inline record: its first subscriber
+      L.np[k] = r[u].y;   // with FO_INLINE_BIT
+      L.gb[k] = r[u].z;   // inline: the second
+      L.go[k] = r[u].w;   // inline: the third (stateful: replaced below for records with groups)
       L.top[k] = v[u] ? tp[u] : 0u;
     }
     if (stateful) {  // entry k's first pick-list index: exclusive scan of n_groups in entry order
 #pragma unroll
       for (uint32_t u = 0; u < EU; ++u) {
-        const uint32_t g = r[u].w;
+        const uint32_t g = fo_rec_groups(r[u]);
         uint32_t incl = g;
 #pragma unroll
         for (uint32_t d = 1; d < 64; d <<= 1) {
           const uint32_t y = __shfl_up(incl, d, 64);
           if (lane >= d) incl += y;
         }
-        L.go[lane + 64u * u] = static_cast<uint32_t>(gbase) + incl - g;
+        if (g) L.go[lane + 64u * u] = static_cast<uint32_t>(gbase) + incl - g;
         gbase += __shfl(incl, 63, 64);
       }
     }
@@ -394,14 +395,21 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
         kk[u] = k;
         rr[u] = j - L.pre[k];
         fl[u] = L.fid[k];
-        shr[u] = act[u] && rr[u] >= L.np[k];
-        sub[u] = (act[u] && !shr[u]) ? a.plain[L.pb[k] + rr[u]] : 0u;
+        const uint32_t npr = L.np[k], np = npr & ~FO_INLINE_BIT;
+        const bool inl = (npr & FO_INLINE_BIT) != 0;
+        shr[u] = act[u] && rr[u] >= np;
+        // the load stays unconditional (all of a round's in flight together): an inline or
+        // inactive output reads plain[0] and discards it
+        const bool arena = act[u] && !shr[u] && !inl;
+        const uint32_t x = a.plain[arena ? L.pb[k] + rr[u] : 0u];
+        const uint32_t iv = rr[u] == 0 ? L.pb[k] : (rr[u] == 1 ? L.gb[k] : L.go[k]);
+        sub[u] = (act[u] && !shr[u]) ? (inl ? iv : x) : 0u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < FO_UNROLL; ++u) {
         if (!shr[u]) continue;
         const uint32_t k = kk[u];
-        const uint32_t gidx = L.gb[k] + (rr[u] - L.np[k]);
+        const uint32_t gidx = L.gb[k] + (rr[u] - L.np[k]);  // (a record with groups is never inline)
         fl[u] |= FANOUT_SHARED_BIT;
         if (!stateful) {
           const uint4 gr = *reinterpret_cast<const uint4*>(a.groups + gidx);
@@ -759,9 +767,10 @@ __global__ __launch_bounds__(64) void share_repick_kernel(RepickArgs a) {
     bool found = false;
     if (f < a.n_recs) {
       const FilterRec fr = a.recs[f];
-      for (uint32_t q0 = 0; q0 < fr.n_groups && !found; q0 += 64) {
+      const uint32_t ngr = fo_rec_groups(make_uint4(fr.plain_begin, fr.n_plain, fr.group_begin, fr.n_groups));
+      for (uint32_t q0 = 0; q0 < ngr && !found; q0 += 64) {
         const uint32_t q = q0 + lane;
-        const bool hit = q < fr.n_groups && a.groups[fr.group_begin + q].group_id == grp;
+        const bool hit = q < ngr && a.groups[fr.group_begin + q].group_id == grp;
         const uint64_t m = __ballot(hit);
         if (m) {
           g = a.groups[fr.group_begin + q0 + __ffsll(static_cast<long long>(m)) - 1];

@@ -360,6 +360,7 @@ class ShardedMatcher:
         self._caps = [1 << 20, 1 << 20]
         self._bufs = {}
         self._stream = None
+        self._stream_b = None
 
     @property
     def n_local_filters(self) -> int:
@@ -461,21 +462,30 @@ class ShardedMatcher:
         _lib.check(L.emqx_shard_step_recv(st, P(recv), mi.ctypes.data, P(a_bytes), P(a_off), P(b_bytes), P(b_off), S),
                    "emqx_shard_step_recv")
         self.last_local_topics = NA + NB
-        # 2. the two engines, asynchronously, into learnt capacities
+        # 2. the two engines, asynchronously, into learnt capacities; engine B on a second
+        # stream, so the two walks overlap
         batches = [(a_bytes, a_off, NA), (b_bytes, b_off, NB)]
         outs = []
         summ = self._buf("summary", 16, torch.int64)
         summ[:16].zero_()
+        cur = torch.cuda.current_stream(dev)
+        if self._stream_b is None:
+            self._stream_b = torch.cuda.Stream(device=dev)
+        self._stream_b.wait_stream(cur)
         for e, (eb, eo, ne) in enumerate(batches):
             cap_e = max(self._caps[e], 1 << 16)
             ro = self._buf(f"off{e}", ne + 1, torch.int64)
             ri = self._buf(f"ids{e}", cap_e, torch.int32)
+            es = cur if e == 0 else self._stream_b
             if ne:
                 self.engines[e].match_device_async(eb.data_ptr(), eo.data_ptr(), ne, ro.data_ptr(), ri.data_ptr(),
-                                                   ri.numel(), summ[8 * e:].data_ptr(), mode=self.mode, stream=stream)
+                                                   ri.numel(), summ[8 * e:].data_ptr(), mode=self.mode,
+                                                   stream=es.cuda_stream)
             else:
-                ro[:1].zero_()
+                with torch.cuda.stream(es):
+                    ro[:1].zero_()
             outs.append([ro, ri])
+        cur.wait_stream(self._stream_b)
         # 3. answers, one chunk per source; a call that did not complete is redone before the
         # exchange (every rank learns every rank's flag from the size exchange)
         redo = False

@@ -281,7 +281,9 @@ int emqx_subtab_set_alive(emqx_subtab* s, const uint32_t* sub_ids, uint64_t n, i
  * words and 16-B records are patched in place (a list that outgrows its extent moves to the
  * arena's end with room to grow); a full rebuild compacts the arenas only when moved-away
  * extents outweigh the live ones.  Ordered after the fan-outs in flight and before later
- * ones (device events). */
+ * ones (device events): the call returns once the changes are enqueued (the previous commit's
+ * device half is waited for first), and every fan-out / publish / re-pick called after it sees
+ * them.  A device error of a commit's device half is returned by the next commit. */
 int emqx_subtab_commit(emqx_subtab* s);
 /* counts[0..3] = live plain subscriptions, live shared memberships, groups with members,
  * device bytes */
