@@ -215,14 +215,12 @@ struct FoScratch {
   hipStream_t stream = nullptr;
   uint32_t* entry_topic = nullptr;
   uint64_t cap_entry_topic = 0;
-  uint64_t* csum = nullptr;
-  uint64_t cap_csum = 0;
+  uint64_t* csum = nullptr;      // chunk offsets: per-chunk deliveries and picks, block sums
+  uint64_t* gchunk = nullptr;
+  uint64_t cap_chunks = 0;
   uint64_t* partials = nullptr;
-  uint64_t cap_partials = 0;
-  // round_robin / sticky: $share groups per chunk of entries, the pick list, its sorted copy and
-  // the sort's scratch, per state entry the run info of the resolve
-  uint32_t* gchunk = nullptr;
-  uint64_t cap_gchunk = 0;
+  // round_robin / sticky: the pick list, its sorted copy and the sort's scratch, per state entry
+  // the run info of the resolve
   uint32_t* pk = nullptr;       // 4 arrays of pk_cap: keys, vals, sorted keys, sorted vals
   uint64_t pk_cap = 0;
   uint8_t* sort_temp = nullptr;
@@ -243,8 +241,8 @@ struct FoScratch {
   void release() {
     fo_free(entry_topic);
     fo_free(csum);
-    fo_free(partials);
     fo_free(gchunk);
+    fo_free(partials);
     fo_free(pk);
     fo_free(sort_temp);
     fo_free(run_ent);
@@ -880,7 +878,53 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
         s->wpatch.push_back(WordPatch{static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32), img[w], 0});
     }
   };
-  words(s->dirty_plain, s->plain, copies_plain);
+  if (s->dirty_plain.size() >= PAR_MIN && par_threads() > 1) {
+    // many touched plain words: the patches are built on the pool, a slice of ranges per
+    // thread (counted, then written at their place)
+    const auto& R = s->dirty_plain;
+    const unsigned T = par_threads();
+    std::vector<uint64_t> cnt(T + 1, 0);
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> cp(T);
+    auto slice = [&](unsigned t, size_t* b, size_t* e) {
+      *b = R.size() * t / T;
+      *e = R.size() * (t + 1) / T;
+    };
+    std::atomic<unsigned> next{0};
+    const std::function<void()> count = [&] {
+      for (unsigned t; (t = next.fetch_add(1)) < T;) {
+        size_t b, e;
+        slice(t, &b, &e);
+        uint64_t c = 0;
+        for (size_t i = b; i < e; ++i)
+          if (R[i].second < RANGE_COPY_MIN) c += R[i].second;
+          else cp[t].push_back(R[i]);
+        cnt[t + 1] = c;
+      }
+    };
+    WorkPool::get().run(count, T);
+    for (unsigned t = 0; t < T; ++t) cnt[t + 1] += cnt[t];
+    s->wpatch.resize(cnt[T]);
+    next = 0;
+    const uint32_t* img = s->plain.data();
+    WordPatch* out = s->wpatch.data();
+    const std::function<void()> fill = [&] {
+      for (unsigned t; (t = next.fetch_add(1)) < T;) {
+        size_t b, e;
+        slice(t, &b, &e);
+        uint64_t o = cnt[t];
+        for (size_t i = b; i < e; ++i) {
+          if (i + 16 < e) __builtin_prefetch(img + R[i + 16].first);
+          if (R[i].second >= RANGE_COPY_MIN) continue;
+          for (uint64_t w = R[i].first; w < R[i].first + R[i].second; ++w)
+            out[o++] = WordPatch{static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32), img[w], 0};
+        }
+      }
+    };
+    WorkPool::get().run(fill, T);
+    for (auto& c : cp) copies_plain.insert(copies_plain.end(), c.begin(), c.end());
+  } else {
+    words(s->dirty_plain, s->plain, copies_plain);
+  }
   const uint64_t n_plain_w = s->wpatch.size();
   words(member_ranges, s->members, copies_members);
   const uint64_t n_member_w = s->wpatch.size() - n_plain_w;
@@ -895,17 +939,33 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
     s->rpatch.push_back(RecPatch{static_cast<uint32_t>(gi), {0, 0, 0}, make_uint4(g.member_begin, g.n_members, g.slot, g.group_id)});
   }
   const uint64_t n_group_p = s->rpatch.size();
-  {  // two-stage prefetch: the record 16 ahead, its plain list (inline candidates) 8 ahead
+  {  // two-stage prefetch: the record 16 ahead, its plain list (inline candidates) 8 ahead;
+     // a long list on the pool, a slice per thread
     const std::vector<uint32_t>& dr = s->dirty_recs;
-    for (size_t i = 0; i < dr.size(); ++i) {
-      if (i + 16 < dr.size()) __builtin_prefetch(&s->recs[dr[i + 16]]);
-      if (i + 8 < dr.size()) {
-        const FilterRec& r8 = s->recs[dr[i + 8]];
-        if (r8.n_plain && r8.n_plain <= FO_INLINE) __builtin_prefetch(s->plain.data() + r8.plain_begin);
+    const uint64_t r0 = s->rpatch.size();
+    s->rpatch.resize(r0 + dr.size());
+    RecPatch* out = s->rpatch.data() + r0;
+    auto part = [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; ++i) {
+        if (i + 16 < e) __builtin_prefetch(&s->recs[dr[i + 16]]);
+        if (i + 8 < e) {
+          const FilterRec& r8 = s->recs[dr[i + 8]];
+          if (r8.n_plain && r8.n_plain <= FO_INLINE) __builtin_prefetch(s->plain.data() + r8.plain_begin);
+        }
+        const uint32_t f = dr[i];
+        s->rec_flag[f] = 0;
+        out[i] = RecPatch{f, {0, 0, 0}, dev_rec(s, f)};
       }
-      const uint32_t f = dr[i];
-      s->rec_flag[f] = 0;
-      s->rpatch.push_back(RecPatch{f, {0, 0, 0}, dev_rec(s, f)});
+    };
+    const unsigned T = dr.size() >= PAR_MIN ? par_threads() : 1u;
+    if (T > 1) {
+      std::atomic<unsigned> next{0};
+      const std::function<void()> run = [&] {
+        for (unsigned t; (t = next.fetch_add(1)) < T;) part(dr.size() * t / T, dr.size() * (t + 1) / T);
+      };
+      WorkPool::get().run(run, T);
+    } else {
+      part(0, dr.size());
     }
   }
   const uint64_t n_rec_p = s->rpatch.size() - n_group_p;
@@ -1121,9 +1181,8 @@ FoScratch* scratch_for(emqx_subtab* s, hipStream_t st) {
 
 // Sizes the stateful scratch of c for m_cap entries and the learnt number of picks.
 int stateful_scratch(emqx_subtab* s, FoScratch* c, uint64_t m_cap, uint64_t cap) {
-  FO_TRY(fo_ensure(c->gchunk, c->cap_gchunk, m_cap / FO_WCHUNK + 2));
   // the pick list: the last finished call's picks with a margin (a call with more is flagged,
-  // writes nothing and is rerun after this grows); never more than the delivery capacity
+  // writes no ids and is rerun after this grows); never more than the delivery capacity
   const uint64_t seen = s->h_ps_seen[2];
   uint64_t want = std::max<uint64_t>(c->pk_cap, std::max<uint64_t>(1u << 16, seen + seen / 2 + 4096));
   want = std::min<uint64_t>(want, std::max<uint64_t>(cap + 1, 1u << 16));
@@ -1176,8 +1235,15 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
     if (rc != EMQX_OK) return rc;
   }
   FO_TRY(fo_ensure(c->entry_topic, c->cap_entry_topic, std::max<uint64_t>(m_cap, 1)));
-  FO_TRY(fo_ensure(c->csum, c->cap_csum, m_cap / FO_WCHUNK + 2));
-  FO_TRY(fo_ensure(c->partials, c->cap_partials, 4 * FO_BLOCKS));
+  {
+    const uint64_t chunks = m_cap / FO_WCHUNK + 2;
+    if (chunks > c->cap_chunks || !c->csum) {
+      FO_TRY(fo_alloc(c->csum, chunks));
+      FO_TRY(fo_alloc(c->gchunk, chunks));
+      c->cap_chunks = chunks;
+    }
+    if (!c->partials) FO_TRY(fo_alloc(c->partials, 4 * FO_BLOCKS));
+  }
   if (!c->ctl) FO_TRY(fo_alloc(c->ctl, FO_CTL_WORDS));
   if (s->commit_pending) FO_TRY(hipStreamWaitEvent(st, s->commit_ev, 0));
   FO_TRY(hipMemsetAsync(c->ctl, 0, FO_CTL_WORDS * sizeof(unsigned long long), st));
@@ -1195,7 +1261,6 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   a.ps_tombs = s->ps_tombs;
   a.ps_mask = s->ps_cap ? s->ps_cap - 1 : 0;
   if (stateful) {
-    a.gchunk = c->gchunk;
     a.pk_keys = c->pk;
     a.pk_vals = c->pk + c->pk_cap;
     a.pk_skeys = c->pk + 2 * c->pk_cap;
@@ -1229,6 +1294,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   a.seed = s->seed;
   a.entry_topic = c->entry_topic;
   a.csum = c->csum;
+  a.gchunk = c->gchunk;
   a.partials = c->partials;
   a.out_off = d_out_off;
   a.out_subs = d_out_subs;
@@ -1324,7 +1390,7 @@ struct PubBatchPriv {
   uint64_t* h_sums = nullptr;  // pinned copy of both
   uint64_t mids_per_topic = 16;  // learnt match ids per topic (sizes d_mids)
   uint64_t limit = ~0ull;        // deliveries the submission may write (<= cap_out): a call that
-                                 // needs more writes nothing and consumes no pick state
+                                 // needs more writes no ids and consumes no pick state
   bool pending = false;
 };
 

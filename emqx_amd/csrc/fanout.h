@@ -86,7 +86,6 @@ struct FanoutArgs {
   // (group slot, publisher) state entry, named by the list index of its first pick to be probed
   // (so ids are < picks <= pk_cap - 1, few key bits), and pk_cap - 1 pads the list past the
   // call's picks.
-  uint32_t* gchunk;          // [ceil(m_cap / FO_WCHUNK)] $share groups per chunk of FO_WCHUNK entries
   uint32_t* pk_keys;         // [pk_cap] run id (written by the probe)
   uint32_t* pk_vals;         // [pk_cap] output position
   uint32_t* pk_skeys;        // [pk_cap] sorted keys (large path); before: the pick's group record
@@ -113,8 +112,9 @@ struct FanoutArgs {
   uint32_t strategy;         // EMQX_SHARE_*
   uint32_t seed;             // per-call seed of random picks
   uint32_t* entry_topic;     // [m] scratch: entry -> topic
-  uint64_t* csum;            // [ceil(m / FO_WCHUNK)] scratch: deliveries per chunk of FO_WCHUNK entries
-  uint64_t* partials;        // [4 * FO_BLOCKS] scratch: chunk sums, chunk bases (deliveries, then picks)
+  uint64_t* csum;            // [m_cap / FO_WCHUNK + 2] deliveries per chunk of FO_WCHUNK entries
+  uint64_t* gchunk;          // [m_cap / FO_WCHUNK + 2] $share picks per chunk (round_robin / sticky)
+  uint64_t* partials;        // [4 * FO_BLOCKS] block sums and bases (deliveries, then picks)
   uint64_t* out_off;         // [n+1]
   uint32_t* out_subs;        // [cap]
   uint32_t* out_filters;     // [cap] or null
@@ -128,12 +128,12 @@ constexpr uint32_t FO_BLOCKS = 1024;
 constexpr uint32_t FO_WCHUNK = 256;
 // Call summary words: flags, deliveries, match entries, live pick-state keys.
 constexpr uint32_t FO_SUM_FLAGS = 0, FO_SUM_TOTAL = 1, FO_SUM_ENTRIES = 2, FO_SUM_STATE = 3, FO_SUM_WORDS = 4;
-constexpr uint64_t FO_SUM_F_OVERFLOW = 1;    // more deliveries than cap: nothing written
+constexpr uint64_t FO_SUM_F_OVERFLOW = 1;    // more deliveries than cap: offsets only, no ids written
 constexpr uint64_t FO_SUM_F_MATCH = 2;       // the match call flagged an error/overflow: nothing read
 constexpr uint64_t FO_SUM_F_STATE_FULL = 4;  // a pick found no room in the pick-state table: no pick
                                              // state consumed, $share outputs not final (rerun)
 constexpr uint64_t FO_SUM_F_PICKS = 8;       // more round_robin / sticky picks than the pick list
-                                             // holds: nothing written (rerun; the list grows)
+                                             // holds: no ids written (rerun; the list grows)
 constexpr uint64_t FO_SUM_F_RERUN = FO_SUM_F_STATE_FULL | FO_SUM_F_PICKS;
 
 // True for the strategies whose picks depend on state kept per publisher.

@@ -10,10 +10,10 @@
 //   entry_topic  one thread per topic: entry -> topic map (a refused or empty CSR: zero
 //                offsets, as nothing else runs)
 //   count        FO_BLOCKS blocks, one contiguous range of entries each: per FO_WCHUNK-entry
-//                chunk the deliveries (n_plain + n_groups of each entry's filter), per block
-//                their sum
-//   partials     one block: exclusive scan of the block sums, the total, the overflow flag
-//                and the call summary
+//                chunk the deliveries (n_plain + n_groups of each entry's filter) and picks,
+//                per block their sums
+//   partials     one block: exclusive scan of the block sums, the totals, the flags and the
+//                call summary
 //   write        one wavefront per 256 match entries: the chunk's base (its block's base + the
 //                block's earlier chunks), its entries' offsets by a wave scan of the counts of
 //                the records it loads anyway, the per-topic output offsets of the topics that
@@ -62,27 +62,46 @@ __device__ __forceinline__ bool fo_refused(const FanoutArgs& a) {
 __device__ __forceinline__ uint64_t fo_entries(const FanoutArgs& a) { return fo_refused(a) ? 0 : fo_entries_raw(a); }
 
 __global__ __launch_bounds__(FO_THREADS) void fanout_entry_topic_kernel(FanoutArgs a) {
-  if (fo_entries(a) == 0) {  // refused or no entries: every topic's deliveries start at 0
+  if (fo_entries(a) == 0) {  // refused or no entries: every topic's deliveries start at 0, and
+                             // no chunk runs, so the summary is written here
     for (uint64_t t = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; t <= a.n; t += uint64_t(gridDim.x) * FO_THREADS)
       a.out_off[t] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      const bool refused = fo_refused(a);
+      const uint64_t fl = refused ? FO_SUM_F_MATCH : 0;
+      a.summary[FO_SUM_FLAGS] = fl;
+      a.summary[FO_SUM_TOTAL] = 0;
+      a.summary[FO_SUM_ENTRIES] = refused ? fo_entries_raw(a) : 0;
+      a.ctl[FO_CTL_PICKS] = 0;
+      if (fl) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(fl));
+      __threadfence_system();
+    }
     return;
   }
+  // a wave per 64 topics: their 65 offsets, then the entries they span written lane by lane
+  // (coalesced), each lane finding its entry's topic by a 6-step search over the offsets
+  __shared__ uint64_t s_off[FO_THREADS / 64][65];
+  const uint32_t lane = fo_lane(), wv = threadIdx.x >> 6;
+  uint64_t* so = s_off[wv];
   const uint64_t base = a.moff[0];
-  for (uint64_t t = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; t < a.n;
-       t += uint64_t(gridDim.x) * FO_THREADS) {
-    const uint64_t b = a.moff[t] - base, e = a.moff[t + 1] - base;
-    for (uint64_t i = b; i < e; ++i) a.entry_topic[i] = static_cast<uint32_t>(t);
+  const uint64_t nwaves = uint64_t(gridDim.x) * (FO_THREADS / 64);
+  for (uint64_t t0 = (uint64_t(blockIdx.x) * (FO_THREADS / 64) + wv) * 64; t0 < a.n; t0 += nwaves * 64) {
+    const uint64_t nt = min<uint64_t>(64, a.n - t0);
+    so[lane] = a.moff[t0 + min<uint64_t>(lane, nt)] - base;
+    if (lane == 0) so[64] = a.moff[t0 + nt] - base;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t b = so[0], e = so[nt];
+    for (uint64_t i = b + lane; i < e; i += 64) {
+      uint32_t k = 0;  // largest k < nt with so[k] <= i
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1)
+        if (k + step < nt && so[k + step] <= i) k += step;
+      a.entry_topic[i] = static_cast<uint32_t>(t0 + k);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
-}
-
-// Chunk [lo, hi) of block b out of FO_BLOCKS over m entries (whole FO_WCHUNK-entry chunks).
-__device__ __forceinline__ uint64_t fo_per_block(uint64_t m) {
-  return ((m + FO_BLOCKS - 1) / FO_BLOCKS + FO_WCHUNK - 1) & ~static_cast<uint64_t>(FO_WCHUNK - 1);
-}
-__device__ __forceinline__ void fo_chunk(uint64_t m, uint32_t b, uint64_t* lo, uint64_t* hi) {
-  const uint64_t per = fo_per_block(m);
-  *lo = min<uint64_t>(m, per * b);
-  *hi = min<uint64_t>(m, per * (b + 1));
 }
 
 __device__ __forceinline__ uint64_t fo_wave_sum(uint64_t v) {
@@ -91,17 +110,24 @@ __device__ __forceinline__ uint64_t fo_wave_sum(uint64_t v) {
   return v;
 }
 
-// Deliveries per FO_WCHUNK-entry chunk (n_plain + n_groups of each entry's filter, csum) and per
-// block; for round_robin / sticky also the $share groups per chunk (gchunk) and per block.
-// Each wave takes whole chunks (4 entries per lane, all loads of a chunk in flight together).
+// Chunk offsets in two passes: count: per FO_WCHUNK-entry chunk the deliveries (csum) and $share
+// picks (gchunk), per block their sums; partials: one block scans the block sums and writes the
+// call's totals, flags and summary; the write kernel then adds the block's earlier chunks to
+// its block's base.  (A one-pass decoupled look-back in the write kernel measured slower: its
+// chains of unpublished predecessors at the kernel's start, and the registers it held, cost
+// more than the count kernel, profiles/r4_v16_fanout_onepass_ab.txt.)
+__device__ __forceinline__ uint64_t fo_per_block(uint64_t m) {
+  return ((m + FO_BLOCKS - 1) / FO_BLOCKS + FO_WCHUNK - 1) & ~static_cast<uint64_t>(FO_WCHUNK - 1);
+}
+
 __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) {
   __shared__ uint64_t bsum[2][FO_THREADS / 64];
   const uint64_t base = a.moff[0];
   const bool stateful = fo_stateful(a.strategy);
   const uint32_t lane = fo_lane(), wv = threadIdx.x >> 6;
   constexpr uint32_t EU = FO_WCHUNK / 64;
-  uint64_t lo, hi;
-  fo_chunk(fo_entries(a), blockIdx.x, &lo, &hi);
+  const uint64_t m = fo_entries(a), per = fo_per_block(m);
+  const uint64_t lo = min<uint64_t>(m, per * blockIdx.x), hi = min<uint64_t>(m, per * (blockIdx.x + 1));
   uint64_t sum = 0, gsum = 0;
   for (uint64_t c0 = lo + uint64_t(wv) * FO_WCHUNK; c0 < hi; c0 += uint64_t(FO_THREADS / 64) * FO_WCHUNK) {
     uint32_t f[EU];
@@ -110,31 +136,23 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) 
       const uint64_t i = c0 + lane + 64u * u;
       f[u] = i < hi ? a.mids[base + i] : FID_NONE;
     }
-    uint32_t c[EU], g[EU];
+    uint64_t cs = 0, gl = 0;
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
       const bool in = f[u] < a.n_recs;
       const uint4 r = *reinterpret_cast<const uint4*>(a.recs + (in ? f[u] : 0u));
-      c[u] = in ? fo_rec_plain(r) + fo_rec_groups(r) : 0u;
-      g[u] = in ? fo_rec_groups(r) : 0u;
-    }
-    uint32_t gl = 0;
-    uint64_t cs = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < EU; ++u) {
-      cs += c[u];
-      gl += g[u];
+      cs += in ? fo_rec_plain(r) + fo_rec_groups(r) : 0u;
+      gl += in ? fo_rec_groups(r) : 0u;
     }
     cs = fo_wave_sum(cs);
-    if (lane == 0) a.csum[c0 / FO_WCHUNK] = cs;
-    sum += cs;
-    if (stateful) {
-      const uint64_t gc = fo_wave_sum(gl);
-      if (lane == 0) a.gchunk[c0 / FO_WCHUNK] = static_cast<uint32_t>(gc);
-      gsum += gl;
+    gl = fo_wave_sum(gl);
+    if (lane == 0) {
+      a.csum[c0 / FO_WCHUNK] = cs;
+      if (stateful) a.gchunk[c0 / FO_WCHUNK] = gl;
     }
+    sum += cs;
+    gsum += gl;
   }
-  gsum = fo_wave_sum(gsum);
   if (lane == 0) {
     bsum[0][wv] = sum;
     bsum[1][wv] = gsum;
@@ -151,7 +169,6 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) 
   }
 }
 
-// Exclusive scan of one u64 per thread across the FO_BLOCKS threads of a block.
 __device__ __forceinline__ uint64_t fo_blocks_excl_scan(uint64_t v, uint64_t* total) {
   __shared__ uint64_t wsum[FO_BLOCKS / 64];
   const uint32_t lane = fo_lane(), w = threadIdx.x >> 6;
@@ -173,27 +190,21 @@ __device__ __forceinline__ uint64_t fo_blocks_excl_scan(uint64_t v, uint64_t* to
   return before + incl - v;
 }
 
-// One block of FO_BLOCKS threads: chunk bases (deliveries; $share picks of the stateful
-// strategies), the total, the call summary.  A call whose deliveries exceed cap, or whose
-// picks exceed the pick list, is flagged here and writes nothing.
 __global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a) {
   uint64_t all = 0, picks = 0;
   a.partials[FO_BLOCKS + threadIdx.x] = fo_blocks_excl_scan(a.partials[threadIdx.x], &all);
   const bool stateful = fo_stateful(a.strategy);
   if (stateful) a.partials[3 * FO_BLOCKS + threadIdx.x] = fo_blocks_excl_scan(a.partials[2 * FO_BLOCKS + threadIdx.x], &picks);
-  if (threadIdx.x == 0) {
-    const bool refused = fo_refused(a);
-    const uint64_t m = fo_entries(a);
-    uint64_t* sm = a.summary;
+  if (threadIdx.x == 0 && fo_entries(a)) {  // (no entries: the entry-topic kernel wrote it)
     uint64_t fl = 0;
-    if (refused) fl = FO_SUM_F_MATCH;
-    else if (all > a.cap) fl = FO_SUM_F_OVERFLOW;
+    if (all > a.cap) fl = FO_SUM_F_OVERFLOW;
     else if (stateful && picks + 1 > a.pk_cap) fl = FO_SUM_F_PICKS;
+    uint64_t* sm = a.summary;
     sm[FO_SUM_FLAGS] = fl;
     sm[FO_SUM_TOTAL] = all;
-    sm[FO_SUM_ENTRIES] = refused ? fo_entries_raw(a) : m;
-    a.ctl[FO_CTL_PICKS] = refused ? 0 : picks;
-    if (fl) a.ctl[FO_CTL_FLAGS] |= fl;
+    sm[FO_SUM_ENTRIES] = fo_entries(a);
+    a.ctl[FO_CTL_PICKS] = stateful ? picks : 0;
+    if (fl) atomicOr(a.ctl + FO_CTL_FLAGS, static_cast<unsigned long long>(fl));
     __threadfence_system();
   }
 }
@@ -273,11 +284,11 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) 
   WaveLds& L = lds_all[wv];
   const uint64_t base = a.moff[0];
   const uint64_t m = fo_entries(a);
-  // overflow (deliveries or picks): offsets only, no deliveries, no pick state consumed
-  const bool ids = !(a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS));
   const bool stateful = fo_stateful(a.strategy);
-  const uint64_t nwaves = uint64_t(gridDim.x) * (FO_THREADS / 64);
+  // over cap (deliveries or picks): offsets only, no ids, no pick state consumed
+  const bool ids = !(a.ctl[FO_CTL_FLAGS] & (FO_SUM_F_OVERFLOW | FO_SUM_F_PICKS));
   const uint64_t per = fo_per_block(m);
+  const uint64_t nwaves = uint64_t(gridDim.x) * (FO_THREADS / 64);
   for (uint64_t e0 = (uint64_t(blockIdx.x) * (FO_THREADS / 64) + wv) * FO_WCHUNK; e0 < m;
        e0 += nwaves * FO_WCHUNK) {
     const uint64_t e1 = min<uint64_t>(e0 + FO_WCHUNK, m);

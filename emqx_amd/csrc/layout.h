@@ -366,36 +366,61 @@ EMQX_HD void shard_place_filter(const uint8_t* p, uint64_t n, uint32_t world, co
   shard_place_key(0, shard_level_hash(p, s1, e1), next, world, sp, nsp, first, span);
 }
 
-// The requests of topic p[0, n): req[0] to engine A, req[1] to engine B, each rank * 2 + engine
-// or SHARD_NONE.  A wildcard topic (match_routes/1 returns only its byte-identical filter, S3)
-// makes one request, to the first rank of that filter.
-EMQX_HD void shard_route_topic(const uint8_t* p, uint64_t n, uint32_t world, const ShardSplitE* sp, uint32_t nsp,
-                               uint32_t* req) {
-  req[0] = req[1] = SHARD_NONE;
-  bool wild = false;
-  for (uint64_t a = 0; a < n && !wild;) {
-    uint64_t b = a;
-    while (b < n && p[b] != '/') ++b;
-    wild = shard_is_wild(p, a, b);
-    a = b + 1;
+// What routing reads of a topic name: its level count (levels 0..2 hashed), whether some level
+// is a wildcard, its first byte.  One pass (shard_topic_levels here; the device's shard step
+// fills it from 16-B windows, shard_step.hip).
+struct ShardTopicLevels {
+  uint32_t n_levels;  // '/' count + 1
+  uint32_t h[3];      // shard_level_hash of levels 0..2 (those present)
+  bool wild;          // some level is exactly '+' or '#'
+};
+
+EMQX_HD void shard_topic_levels(const uint8_t* p, uint64_t n, ShardTopicLevels* L) {
+  L->n_levels = 0;
+  L->wild = false;
+  uint32_t h = 0x811C9DC5u, len = 0;
+  uint8_t c0 = 0;
+  for (uint64_t i = 0; i <= n; ++i) {
+    const uint8_t c = i < n ? p[i] : static_cast<uint8_t>('/');
+    if (c == '/') {
+      if (L->n_levels < 3) L->h[L->n_levels] = mix32(h ^ len);
+      if (len == 1 && (c0 == '+' || c0 == '#')) L->wild = true;
+      ++L->n_levels;
+      h = 0x811C9DC5u;
+      len = 0;
+    } else {
+      if (len == 0) c0 = c;
+      h = (h ^ c) * 0x01000193u;
+      ++len;
+    }
   }
+}
+
+// The requests of topic p[0, n) from its level summary: req[0] to engine A, req[1] to engine B,
+// each rank * 2 + engine or SHARD_NONE.  A wildcard topic (match_routes/1 returns only its
+// byte-identical filter, S3) makes one request, to the first rank of that filter.
+EMQX_HD void shard_route_levels(const uint8_t* p, uint64_t n, const ShardTopicLevels& L, uint32_t world,
+                                const ShardSplitE* sp, uint32_t nsp, uint32_t* req) {
+  req[0] = req[1] = SHARD_NONE;
   uint32_t first, span, engine;
-  if (wild) {
+  if (L.wild) {
     shard_place_filter(p, n, world, sp, nsp, &first, &span, &engine);
     req[engine] = 2 * first + engine;
     return;
   }
-  uint64_t s1, e1, s2, e2, s3, e3;
-  shard_level(p, n, 0, &s1, &e1);
-  const bool has2 = shard_level(p, n, 1, &s2, &e2);
-  shard_place_key(0, shard_level_hash(p, s1, e1), has2 ? shard_level_hash(p, s2, e2) : SHARD_ABSENT, world, sp, nsp,
-                  &first, &span);
+  const bool has2 = L.n_levels >= 2, has3 = L.n_levels >= 3;
+  shard_place_key(0, L.h[0], has2 ? L.h[1] : SHARD_ABSENT, world, sp, nsp, &first, &span);
   req[0] = 2 * first;
   if (!has2 || (n > 0 && p[0] == '$')) return;  // '+/x/...' never matches a '$' topic (S5)
-  const bool has3 = shard_level(p, n, 2, &s3, &e3);
-  shard_place_key(SHARD_SPACE_P, shard_level_hash(p, s2, e2), has3 ? shard_level_hash(p, s3, e3) : SHARD_ABSENT,
-                  world, sp, nsp, &first, &span);
+  shard_place_key(SHARD_SPACE_P, L.h[1], has3 ? L.h[2] : SHARD_ABSENT, world, sp, nsp, &first, &span);
   req[1] = 2 * first + 1;
+}
+
+EMQX_HD void shard_route_topic(const uint8_t* p, uint64_t n, uint32_t world, const ShardSplitE* sp, uint32_t nsp,
+                               uint32_t* req) {
+  ShardTopicLevels L;
+  shard_topic_levels(p, n, &L);
+  shard_route_levels(p, n, L, world, sp, nsp, req);
 }
 
 }  // namespace emqx

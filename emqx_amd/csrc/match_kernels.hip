@@ -1441,21 +1441,6 @@ __global__ __launch_bounds__(256) void shard_owner_kernel(const uint8_t* __restr
   }
 }
 
-// Two-key-space sharded layout: the (up to) two requests of each topic (layout.h shard_route_topic).
-__global__ __launch_bounds__(256) void shard_route_kernel(const uint8_t* __restrict__ tbytes,
-                                                          const uint64_t* __restrict__ toffs, uint64_t n, uint32_t world,
-                                                          const ShardSplitE* __restrict__ splits, uint32_t n_splits,
-                                                          uint32_t* __restrict__ req2) {
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint64_t a = toffs[i], b = toffs[i + 1];
-    uint32_t r[2];
-    shard_route_topic(tbytes + a, b - a, world, splits, n_splits, r);
-    req2[2 * i] = r[0];
-    req2[2 * i + 1] = r[1];
-  }
-}
-
 // Incremental commits (live_trie.cpp): rewrites existing slots of the committed table in
 // place.  Phase 0 writes the slots' filter ids, phase 1 (a later launch) the slots, each with
 // one 16-B store, so a concurrent walk sees every slot either old or new, and never a slot
@@ -1554,15 +1539,6 @@ hipError_t launch_shard_owner(const uint8_t* tbytes, const uint64_t* toffs, uint
   if (!n) return hipSuccess;
   const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((n + 255) / 256, 4096));
   hipLaunchKernelGGL(shard_owner_kernel, dim3(blocks), dim3(256), 0, s, tbytes, toffs, n, world, levels, owner);
-  return hipGetLastError();
-}
-
-hipError_t launch_shard_route(const uint8_t* tbytes, const uint64_t* toffs, uint64_t n, uint32_t world,
-                              const ShardSplitE* splits, uint32_t n_splits, uint32_t* req2, hipStream_t s) {
-  if (!n) return hipSuccess;
-  const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((n + 255) / 256, 4096));
-  hipLaunchKernelGGL(shard_route_kernel, dim3(blocks), dim3(256), 0, s, tbytes, toffs, n, world, splits, n_splits,
-                     req2);
   return hipGetLastError();
 }
 

@@ -48,6 +48,18 @@ struct ShardTab {
 
 __host__ __device__ inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 
+// A topic's bytes from src to dst (any alignment: gfx950 global loads and stores take
+// unaligned addresses), `lanes` lanes of one request together (sub = this lane's index among
+// them): 16-B moves, then the tail byte by byte.
+typedef uint4 __attribute__((aligned(1))) u4u;
+__device__ __forceinline__ void copy_bytes(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t len,
+                                           uint32_t sub, uint32_t lanes) {
+  const uint64_t full = len & ~15ull;
+  for (uint64_t j = 16ull * sub; j < full; j += 16ull * lanes)
+    *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
+  for (uint64_t j = full + sub; j < len; j += lanes) dst[j] = src[j];
+}
+
 uint32_t grid_of(uint64_t items, uint32_t per_block, uint32_t cap = 8192) {
   return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((items + per_block - 1) / per_block, cap)));
 }
@@ -60,15 +72,60 @@ uint32_t bucket_bits(uint32_t world) {  // keys 0 .. 2 * world (2 * world = no r
 
 // ---- send -------------------------------------------------------------------------------
 
+// shard_topic_levels (layout.h) over the topic's bytes read as 16-B aligned windows (a window
+// holding a topic byte lies inside the batch's allocation; the batch's last window only up to
+// its end): the same summary, one load per 16 bytes instead of one per byte.
+__device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb, uint64_t s, uint64_t e,
+                                                 uint64_t lim, ShardTopicLevels* L) {
+  L->n_levels = 0;
+  L->wild = false;
+  L->h[0] = L->h[1] = L->h[2] = 0;
+  uint32_t h = 0x811C9DC5u, len = 0, c0 = 0;
+  const uintptr_t abeg = reinterpret_cast<uintptr_t>(tb + s), aend = reinterpret_cast<uintptr_t>(tb + e);
+  const uintptr_t alim = reinterpret_cast<uintptr_t>(tb + lim);
+  for (uintptr_t w0 = abeg & ~static_cast<uintptr_t>(15); w0 <= aend; w0 += 16) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (w0 + 16 <= alim) {
+      v = *reinterpret_cast<const uint4*>(w0);
+    } else if (w0 < aend) {
+      uint32_t t4[4] = {0, 0, 0, 0};
+      for (uint32_t b = 0; b < 16 && w0 + b < alim; ++b)
+        t4[b >> 2] |= static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(w0 + b)) << (8u * (b & 3u));
+      v = make_uint4(t4[0], t4[1], t4[2], t4[3]);
+    }
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t b = 0; b < 16; ++b) {
+      const uintptr_t q = w0 + b;
+      if (q < abeg || q > aend) continue;
+      const uint32_t c = q < aend ? (wd[b >> 2] >> (8u * (b & 3u))) & 0xFFu : static_cast<uint32_t>('/');
+      if (c == '/') {
+        if (L->n_levels < 3) L->h[L->n_levels] = mix32(h ^ len);
+        if (len == 1 && (c0 == '+' || c0 == '#')) L->wild = true;
+        ++L->n_levels;
+        h = 0x811C9DC5u;
+        len = 0;
+      } else {
+        if (len == 0) c0 = c;
+        h = (h ^ c) * 0x01000193u;
+        ++len;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restrict__ tb,
                                                         const uint64_t* __restrict__ to, uint64_t n, uint32_t world,
                                                         const ShardSplitE* __restrict__ sp, uint32_t nsp,
                                                         uint32_t* __restrict__ key, uint32_t* __restrict__ idx) {
+  const uint64_t lim = n ? to[n] : 0;
   for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
        t += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint64_t a = to[t], b = to[t + 1];
+    ShardTopicLevels L;
+    topic_levels_dev(tb, a, b, lim, &L);
     uint32_t r[2];
-    shard_route_topic(tb + a, b - a, world, sp, nsp, r);
+    shard_route_levels(tb + a, b - a, L, world, sp, nsp, r);
     *reinterpret_cast<uint2*>(key + 2 * t) =
         make_uint2(r[0] == kNone ? 2 * world : r[0], r[1] == kNone ? 2 * world : r[1]);
     *reinterpret_cast<uint2*>(idx + 2 * t) = make_uint2(static_cast<uint32_t>(2 * t), static_cast<uint32_t>(2 * t + 1));
@@ -145,7 +202,8 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
   h[4 + nA + 1 + nB] = static_cast<uint32_t>(bB);  // B offsets[nB]
 }
 
-// 16 lanes per request: its offset entry and its topic's bytes into the destination's chunk.
+// 4 lanes per request (16 requests a wave, their loads in flight together): its offset entry
+// and its topic's bytes (16-B moves) into the destination's chunk.
 __global__ __launch_bounds__(256) void shard_pack_kernel(const uint8_t* __restrict__ tb,
                                                          const uint64_t* __restrict__ to,
                                                          const uint32_t* __restrict__ key_s,
@@ -156,9 +214,9 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const uint8_t* __restri
                                                          const uint32_t* __restrict__ err, uint8_t* __restrict__ send) {
   if (err[0]) return;
   const uint32_t nreq = start[2 * world];
-  const uint32_t sub = threadIdx.x & 15u;
-  for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4; p < nreq;
-       p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 4) {
+  const uint32_t sub = threadIdx.x & 3u;
+  for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; p < nreq;
+       p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
     const uint32_t b = key_s[p], r = b >> 1, e = b & 1u;
     const uint32_t s0 = start[2 * r], s1 = start[2 * r + 1], s2 = start[2 * r + 2];
     const uint32_t nA = s1 - s0, nB = s2 - s1;
@@ -169,32 +227,43 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const uint8_t* __restri
     const uint64_t data = 16 + al16(4ull * (nA + nB + 2)) + (e ? sc[s1] - sc[s0] : 0) + rel;
     const uint32_t t = perm[p] >> 1;
     const uint64_t a = to[t], len = to[t + 1] - a;
-    for (uint64_t j = sub; j < len; j += 16) c[data + j] = tb[a + j];
+    copy_bytes(tb + a, c + data, len, sub, 4);
+  }
+}
+
+// emqx_shard_route_device: the raw requests (req2[2t], req2[2t + 1]) with the same scanner.
+__global__ __launch_bounds__(256) void shard_route_kernel(const uint8_t* __restrict__ tb,
+                                                          const uint64_t* __restrict__ to, uint64_t n, uint32_t world,
+                                                          const ShardSplitE* __restrict__ sp, uint32_t nsp,
+                                                          uint32_t* __restrict__ req2) {
+  const uint64_t lim = n ? to[n] : 0;
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
+       t += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t a = to[t], b = to[t + 1];
+    ShardTopicLevels L;
+    topic_levels_dev(tb, a, b, lim, &L);
+    uint32_t r[2];
+    shard_route_levels(tb + a, b - a, L, world, sp, nsp, r);
+    req2[2 * t] = r[0];
+    req2[2 * t + 1] = r[1];
   }
 }
 
 // ---- recv -------------------------------------------------------------------------------
 
-// grid (x, source, engine): the source's offsets rebased into the batch, then its bytes.
+// grid (x, source, engine): the source's offsets rebased into the batch (its bytes are one
+// contiguous region each, moved by the copy engine: emqx_shard_step_recv).
 __global__ __launch_bounds__(256) void shard_unpack_kernel(const uint8_t* __restrict__ recv, ShardTab tab,
-                                                           uint8_t* __restrict__ a_bytes, uint64_t* __restrict__ a_off,
-                                                           uint8_t* __restrict__ b_bytes,
-                                                           uint64_t* __restrict__ b_off) {
+                                                           uint64_t* __restrict__ a_off, uint64_t* __restrict__ b_off) {
   const uint32_t s = blockIdx.y, e = blockIdx.z;
   const uint32_t nA = tab.a0[s + 1] - tab.a0[s], nB = tab.b0[s + 1] - tab.b0[s];
-  const uint64_t bA = tab.ab0[s + 1] - tab.ab0[s], bB = tab.bb0[s + 1] - tab.bb0[s];
-  const uint8_t* c = recv + tab.base[s];
-  const uint32_t* offs = reinterpret_cast<const uint32_t*>(c) + 4 + (e ? nA + 1 : 0);
+  const uint32_t* offs = reinterpret_cast<const uint32_t*>(recv + tab.base[s]) + 4 + (e ? nA + 1 : 0);
   const uint32_t n = e ? nB : nA;
   const uint64_t dbase = e ? tab.bb0[s] : tab.ab0[s];
   uint64_t* doff = (e ? b_off : a_off) + (e ? tab.b0[s] : tab.a0[s]);
-  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t k = tid; k <= n; k += stride) doff[k] = dbase + offs[k];
-  const uint8_t* src = c + 16 + al16(4ull * (nA + nB + 2)) + (e ? bA : 0);
-  uint8_t* dst = (e ? b_bytes : a_bytes) + dbase;
-  const uint64_t nb = e ? bB : bA;
-  for (uint64_t j = tid; j < nb; j += stride) dst[j] = src[j];
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k <= n; k += stride)
+    doff[k] = dbase + offs[k];
 }
 
 // ---- answer -----------------------------------------------------------------------------
@@ -270,35 +339,49 @@ __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t*
   }
 }
 
-// 16 lanes per topic: its engine-A answer, then its engine-B answer, to out_off[t].
+// 4 lanes per request, in request (send) order: its answer's ids, read from the answer chunk
+// where they lie in that same order (coalesced), to its topic's place in the output: the
+// topic's offset, after the topic's engine-A ids for an engine-B request.
 __global__ __launch_bounds__(256) void shard_merge_kernel(const uint32_t* __restrict__ back, ShardTab tab,
                                                           const uint32_t* __restrict__ key_s,
+                                                          const uint32_t* __restrict__ perm,
                                                           const uint32_t* __restrict__ start,
                                                           const uint32_t* __restrict__ cnt,
                                                           const uint64_t* __restrict__ csc,
-                                                          const uint32_t* __restrict__ pos, uint64_t n,
+                                                          const uint32_t* __restrict__ pos, uint32_t world,
                                                           const uint64_t* __restrict__ out_off,
                                                           uint32_t* __restrict__ out_ids) {
-  const uint32_t sub = threadIdx.x & 15u;
-  for (uint64_t t = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 4; t < n;
-       t += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 4) {
-    uint64_t d = out_off[t];
-    for (uint32_t e = 0; e < 2; ++e) {
-      const uint32_t p = pos[2 * t + e];
-      if (p == kNone) continue;
-      const uint32_t b = key_s[p], r = b >> 1;
-      const uint32_t* ch = back + tab.base[r];
-      const uint64_t src = 4ull + ch[0] + ch[1] + ((b & 1u) ? ch[2] : 0u) + (csc[p] - csc[start[b]]);
-      const uint32_t c = cnt[p];
-      for (uint32_t j = sub; j < c; j += 16) out_ids[d + j] = ch[src + j];
-      d += c;
+  const uint32_t nreq = start[2 * world];
+  const uint32_t sub = threadIdx.x & 3u;
+  for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; p < nreq;
+       p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
+    const uint32_t c = cnt[p];
+    if (c == 0) continue;
+    const uint32_t q = perm[p], t = q >> 1, e = q & 1u;
+    const uint32_t b = key_s[p], r = b >> 1;
+    const uint32_t* ch = back + tab.base[r];
+    const uint64_t src = 4ull + ch[0] + ch[1] + (e ? ch[2] : 0u) + (csc[p] - csc[start[b]]);
+    uint64_t dst = out_off[t];
+    if (e) {
+      const uint32_t pa = pos[2 * t];
+      if (pa != kNone) dst += cnt[pa];
     }
+    for (uint32_t j = sub; j < c; j += 4) out_ids[dst + j] = ch[src + j];
   }
 }
 
 using SortCfg = rocprim::default_config;
 
 }  // namespace
+
+hipError_t launch_shard_route(const uint8_t* tbytes, const uint64_t* toffs, uint64_t n, uint32_t world,
+                              const ShardSplitE* splits, uint32_t n_splits, uint32_t* req2, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(shard_route_kernel, dim3(grid_of(n, 256, 4096)), dim3(256), 0, s, tbytes, toffs, n, world, splits,
+                     n_splits, req2);
+  return hipGetLastError();
+}
+
 }  // namespace emqx
 
 using namespace emqx;
@@ -455,7 +538,7 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
   hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->sc, G, d_send, send_cap, d_meta,
                      st->cbase, st->err);
   if (m)
-    hipLaunchKernelGGL(shard_pack_kernel, dim3(grid_of(m, 16)), dim3(256), 0, s, d_bytes, d_offsets, st->key_s,
+    hipLaunchKernelGGL(shard_pack_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, d_bytes, d_offsets, st->key_s,
                        st->perm, st->start, st->sc, st->cbase, G, st->err, d_send);
   SS_TRY(hipGetLastError());
   st->n = n;
@@ -486,11 +569,17 @@ int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* d_recv, const int64
   if ((t.base[G] && !d_recv) || (t.ab0[G] && !d_a_bytes) || (t.bb0[G] && !d_b_bytes)) return EMQX_EINVAL;
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
-  const uint64_t per = (t.a0[G] + t.b0[G] + (t.ab0[G] + t.bb0[G]) / 4) / (2 * G) + 1;  // items per (source, engine)
+  const uint64_t per = (t.a0[G] + t.b0[G]) / (2 * G) + 1;  // offsets per (source, engine)
   const uint32_t x = grid_of(per, 256, std::max<uint32_t>(1, 1024 / G));
-  hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, 2), dim3(256), 0, s, d_recv, t, d_a_bytes, d_a_offsets, d_b_bytes,
-                     d_b_offsets);
+  hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, 2), dim3(256), 0, s, d_recv, t, d_a_offsets, d_b_offsets);
   SS_TRY(hipGetLastError());
+  for (uint32_t r = 0; r < G; ++r) {  // each source's A bytes, then its B bytes: contiguous both sides
+    const uint64_t nA = t.a0[r + 1] - t.a0[r], nB = t.b0[r + 1] - t.b0[r];
+    const uint64_t bA = t.ab0[r + 1] - t.ab0[r], bB = t.bb0[r + 1] - t.bb0[r];
+    const uint8_t* data = d_recv + t.base[r] + 16 + al16(4ull * (nA + nB + 2));
+    if (bA) SS_TRY(hipMemcpyAsync(d_a_bytes + t.ab0[r], data, bA, hipMemcpyDeviceToDevice, s));
+    if (bB) SS_TRY(hipMemcpyAsync(d_b_bytes + t.bb0[r], data + bA, bB, hipMemcpyDeviceToDevice, s));
+  }
   st->have_recv = true;
   return EMQX_OK;
 }
@@ -533,8 +622,8 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* d_back, const int
   SS_TRY(launch_scan(st->tcnt, n, d_out_offsets, st->partials, s));
   if (n) {
     if (!d_out_ids) return EMQX_EINVAL;
-    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(n, 16)), dim3(256), 0, s, d_back, t, st->key_s, st->start,
-                       st->len, st->sc, st->pos, n, d_out_offsets, d_out_ids);
+    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, d_back, t, st->key_s, st->perm,
+                       st->start, st->len, st->sc, st->pos, G, d_out_offsets, d_out_ids);
   }
   SS_TRY(hipGetLastError());
   return EMQX_OK;

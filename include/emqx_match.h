@@ -319,8 +319,9 @@ int emqx_share_repick(emqx_subtab* s, uint32_t strategy, uint64_t n, const uint3
 
 /* Fan-out of a match CSR already in HBM (d_match_offsets[n+1], d_match_ids): per-topic CSR of
  * deliveries d_out_offsets[n+1], d_out_subs[], d_out_filters[] (optional, may be NULL).
- * d_pick_keys[n] (device): per-message keys as above.  On EMQX_EOVERFLOW nothing is written to
- * the id arrays, no pick state is consumed, and *n_out is the capacity required. */
+ * d_pick_keys[n] (device): per-message keys as above.  On EMQX_EOVERFLOW d_out_offsets are
+ * complete, nothing is written to the id arrays, no pick state is consumed, and *n_out is the
+ * capacity required. */
 int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* d_match_offsets,
                              const uint32_t* d_match_ids, uint64_t n, const uint32_t* d_pick_keys,
                              uint64_t* d_out_offsets, uint32_t* d_out_subs, uint32_t* d_out_filters,
@@ -330,8 +331,8 @@ int emqx_fanout_batch_device(emqx_subtab* s, uint32_t strategy, const uint64_t* 
  * match_cap bounds the match entries (the match call's id capacity; sizes the scratch): a CSR
  * with more entries (a match call that overflowed its ids) is not read.  summary[4] (device or
  * host-mapped memory) receives {flags, deliveries, match entries, live pick-state keys} when the
- * call completes; flags bit 0: more deliveries than cap (nothing written to the id arrays, no
- * $share pick state consumed); bit 1: the CSR was refused (nothing read); bit 2: a
+ * call completes; flags bit 0: more deliveries than cap (offsets complete, nothing written to
+ * the id arrays, no $share pick state consumed); bit 1: the CSR was refused (nothing read); bit 2: a
  * round_robin / sticky pick found no room for its state, bit 3: more round_robin / sticky picks
  * than the table's pick scratch holds: in both cases no pick state was consumed and the $share
  * deliveries are not final: redo the batch with emqx_fanout_batch_device, which grows the

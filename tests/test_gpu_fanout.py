@@ -264,14 +264,16 @@ def test_async_fanout_pipelined_streams(F):
         assert np.array_equal(os_[:tot].cpu().numpy(), ref[1])
         assert np.array_equal(of[:tot].cpu().numpy(), ref[2])
 
-    # overflow: flag set, output untouched
+    # overflow: flag set, the total reported, the offsets complete, the id arrays untouched
     osubs.fill_(-7)
+    ooff.fill_(-7)
     st.fanout_device_async("hash_clientid", moff.data_ptr(), mids.data_ptr(), n, mcap, keys.data_ptr(),
                            ooff.data_ptr(), osubs.data_ptr(), ofil.data_ptr(), tot - 1, summ[0].data_ptr())
     torch.cuda.synchronize()
     s0 = summ[0].cpu().numpy()
     assert s0[0] & 1 and s0[1] == tot
     assert (osubs.cpu().numpy() == -7).all()
+    assert np.array_equal(ooff.cpu().numpy(), ref[0])
 
     # a slice of the CSR (topics [h, n)): offsets start at moff[h] > 0
     h = n // 2

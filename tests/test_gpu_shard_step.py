@@ -161,3 +161,26 @@ def test_shard_step_two_ranks_share_one_gpu():
         assert ids > 0 and local > 0 and third_ok
     # every rank holds part of the table (two key spaces), not all of it
     assert all(r[5] < 200_000 for r in res)
+
+
+def test_device_routing_equals_host_routing():
+    """The device scanner (16-B windows, shard_step.hip topic_levels_dev) routes every topic as
+    the host's shard_route_topic does: config C topics and edge names (wildcards, '$', one level,
+    empty levels, long names, the batch's last bytes), at world 1, 2 and 8 with a split plan."""
+    import torch
+    from emqx_amd import dist as D
+    from emqx_amd import workloads as W
+    from emqx_amd.engine import pack
+    wl = W.config_b(n_filters=200_000, n_topics=20_000, seed=3, vocab_scale=4)
+    extra = TOPICS + [b"", b"/", b"//", b"$", b"+", b"#", b"a/+/b", b"x" * 100 + b"/" + b"y" * 37,
+                      b"/".join([b"l%d" % i for i in range(40)]), b"$share/g/a", b"a/b/c/"]
+    eb, eo = pack(extra)
+    buf = np.concatenate([wl.topics[0][: int(wl.topics[1][-1])], eb])
+    offs = np.concatenate([wl.topics[1].astype(np.uint64), eo[1:].astype(np.uint64) + np.uint64(wl.topics[1][-1])])
+    for world in (1, 2, 8):
+        plan = D.shard_plan(wl.filters, world)
+        tb_c = torch.from_numpy(buf.copy())
+        to_c = torch.from_numpy(offs.astype(np.int64))
+        host = D.topic_requests(tb_c, to_c, world, plan)
+        dev = D.topic_requests(tb_c.cuda(), to_c.cuda(), world, plan).cpu()
+        assert torch.equal(host, dev), world
