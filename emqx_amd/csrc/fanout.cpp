@@ -1246,7 +1246,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   }
   if (!c->ctl) FO_TRY(fo_alloc(c->ctl, FO_CTL_WORDS));
   if (s->commit_pending) FO_TRY(hipStreamWaitEvent(st, s->commit_ev, 0));
-  FO_TRY(hipMemsetAsync(c->ctl, 0, FO_CTL_WORDS * sizeof(unsigned long long), st));
+  // (c->ctl is zeroed by the call's first kernel, fanout_entry_topic)
   FanoutArgs a{};
   a.recs = s->d_recs.p;
   a.n_recs = s->dev_n_recs;

@@ -62,6 +62,11 @@ __device__ __forceinline__ bool fo_refused(const FanoutArgs& a) {
 __device__ __forceinline__ uint64_t fo_entries(const FanoutArgs& a) { return fo_refused(a) ? 0 : fo_entries_raw(a); }
 
 __global__ __launch_bounds__(FO_THREADS) void fanout_entry_topic_kernel(FanoutArgs a) {
+  // the call's control words start at zero (the first kernel of the call: no memset launch)
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < FO_CTL_WORDS) a.ctl[threadIdx.x] = 0;
+    __syncthreads();
+  }
   if (fo_entries(a) == 0) {  // refused or no entries: every topic's deliveries start at 0, and
                              // no chunk runs, so the summary is written here
     for (uint64_t t = blockIdx.x * uint64_t(FO_THREADS) + threadIdx.x; t <= a.n; t += uint64_t(gridDim.x) * FO_THREADS)

@@ -1242,6 +1242,30 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_final_kernel(const uint32_t
   }
 }
 
+// A scan of at most SCAN_TILE counts in one launch (small batches: the host batcher's calls,
+// where each launch of the three-kernel scan costs more than the scan).
+__global__ __launch_bounds__(SCAN_THREADS) void scan_single_kernel(const uint32_t* counts, uint64_t n,
+                                                                   uint64_t* offsets) {
+  const uint64_t base = static_cast<uint64_t>(threadIdx.x) * SCAN_ITEMS;
+  uint32_t v[SCAN_ITEMS];
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    v[k] = i < n ? counts[i] : 0u;
+    s += v[k];
+  }
+  uint64_t tot;
+  uint64_t run = block_excl_scan(s, &tot);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    const uint64_t i = base + k;
+    if (i < n) offsets[i] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 0) offsets[n] = tot;
+}
+
 // ------------------------------------------------------------------------------------
 // Output assembly: tile scan -> per-tile offsets; scatter: slab entries -> CSR out_ids
 // ------------------------------------------------------------------------------------
@@ -1500,8 +1524,8 @@ uint64_t scan_partials(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1;
 hipError_t launch_scan(const uint32_t* counts, uint64_t n, uint64_t* offsets, uint64_t* partials,
                        hipStream_t s) {
   const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
-  if (nb == 0) {
-    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, partials, 0, offsets, n);
+  if (nb <= 1) {  // one tile (or none): one launch
+    hipLaunchKernelGGL(scan_single_kernel, dim3(1), dim3(SCAN_THREADS), 0, s, counts, n, offsets);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(scan_reduce_kernel, dim3(static_cast<uint32_t>(nb)), dim3(SCAN_THREADS), 0, s, counts, n, partials);
