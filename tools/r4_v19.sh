@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4_v19}
 mkdir -p $OUT
 timeout -k 10 500 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_fanout.py \
-  tests/test_gpu_fanout_state.py tests/test_gpu_share_parity.py tests/test_gpu_host.py > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+  tests/test_gpu_fanout_state.py tests/test_gpu_share_parity.py tests/test_gpu_host.py tests/test_gpu_retain.py > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log
 timeout -k 10 400 python -u bench.py --workload P > $OUT/bench_P.json 2> $OUT/bench_P.err || { tail -20 $OUT/bench_P.err; exit 1; }
 python3 -c "
@@ -15,3 +15,5 @@ timeout -k 10 400 python -u bench.py --workload L > $OUT/bench_L.json 2> $OUT/be
 python3 -c "
 import json;d=json.load(open('$OUT/bench_L.json'))
 print('L', d['value']); [print({k:r.get(k) for k in ('callers','topics_per_s','p50_us','p99_us','us_per_batch_device_wait','topics_per_batch')}) for r in d.get('runs',[])]"
+timeout -k 10 400 python -u bench.py --workload R > $OUT/bench_R.json 2> $OUT/bench_R.err || { tail -20 $OUT/bench_R.err; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/bench_R.json'));print('R', d['value'], d['ms_per_step'], d.get('parity'))"
