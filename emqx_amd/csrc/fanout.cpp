@@ -1597,6 +1597,32 @@ int emqx_subtab_destroy(emqx_subtab* s) {
   return EMQX_OK;
 }
 
+// The serial ops: a plain op's map entry and record, a $share op's (filter, group) slot 16 ops
+// ahead and its membership line 8 ops ahead are prefetched (the maps are too large for the
+// caches; each op was one or two dependent misses).
+void prefetch_op(const emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, const uint32_t* gs,
+                 const uint32_t* idx, uint64_t j, uint64_t nl) {
+  if (j + 16 < nl) {
+    const uint64_t i = idx ? idx[j + 16] : j + 16;
+    if (gs && gs[i] != EMQX_NO_GROUP) {
+      s->slot_of.prefetch((uint64_t(fs[i]) << 32) | gs[i]);
+    } else if (fs[i] < s->recs.size()) {  // a plain op: its map entry and record
+      s->plain_pos[pp_shard(fs[i])].prefetch((uint64_t(fs[i]) << 32) | subs[i]);
+      __builtin_prefetch(&s->recs[fs[i]]);
+    }
+  }
+  if (j + 8 < nl) {
+    const uint64_t i = idx ? idx[j + 8] : j + 8;
+    if (gs && gs[i] != EMQX_NO_GROUP) {
+      const uint32_t sl = s->slot_of.find((uint64_t(fs[i]) << 32) | gs[i]);
+      if (sl != SUB_NONE) {
+        s->member_set.prefetch((uint64_t(sl) << 32) | subs[i]);
+        __builtin_prefetch(&s->slots[sl]);
+      }
+    }
+  }
+}
+
 // A long batch: its plain ops go through plain_batch (threads), and *rest_out = the indices of
 // its $share ops, which the caller applies serially after them (plain lists and group
 // memberships are separate structures, so the split changes no result).  False: a short batch.
@@ -1631,6 +1657,7 @@ int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* 
   const bool split = plain_parallel(s, filter_ids, sub_ids, group_ids, n, true, &rest);
   const uint64_t nl = split ? rest.size() : n;
   for (uint64_t j = 0; j < nl; ++j) {
+    prefetch_op(s, filter_ids, sub_ids, group_ids, split ? rest.data() : nullptr, j, nl);
     const uint64_t i = split ? rest[j] : j;
     const uint32_t f = filter_ids[i], sub = sub_ids[i];
     const uint32_t grp = group_ids ? group_ids[i] : EMQX_NO_GROUP;
@@ -1667,6 +1694,7 @@ int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_
   const bool split = plain_parallel(s, filter_ids, sub_ids, group_ids, n, false, &rest);
   const uint64_t nl = split ? rest.size() : n;
   for (uint64_t j = 0; j < nl; ++j) {
+    prefetch_op(s, filter_ids, sub_ids, group_ids, split ? rest.data() : nullptr, j, nl);
     const uint64_t i = split ? rest[j] : j;
     const uint32_t f = filter_ids[i], sub = sub_ids[i];
     const uint32_t grp = group_ids ? group_ids[i] : EMQX_NO_GROUP;
