@@ -1495,7 +1495,9 @@ def retain_bench(args, rank, world, dev):
         "ids_per_filter": round(nout / nf, 3), "node_visits_per_filter": round(visits / nf, 3),
         "ranges_per_filter": round(ranges / nf, 3), "call_ms_median": round(cms, 4),
         "walk_ms_median": round(float(np.median(walk_ms)), 4),
+        "walk_balance": "spill rounds" if os.environ.get("EMQX_RETAIN_BALANCE") == "0" else "work-sharing queue",
         "walk_spill_rounds": int(st["last_spill_rounds"]), "walk_spilled_items": int(st["last_spilled"]),
+        "walk_shares": int(st.get("last_shares", 0)), "walk_queue_aborts": int(st.get("queue_aborts", 0)),
         "walk_step_budget": args.retain_budget if args.retain_budget is not None else "24, spill rounds 64 (default)",
         "walk_spill_full": int(st.get("last_spill_full", 0)),
         "walk_tile_filters": args.retain_tile if args.retain_tile is not None else 10,

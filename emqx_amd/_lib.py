@@ -113,6 +113,8 @@ class RetainStats(ctypes.Structure):
         ("last_build_ms", ctypes.c_double), ("last_match_ms", ctypes.c_double), ("last_walk_ms", ctypes.c_double),
         ("last_spill_rounds", ctypes.c_uint64), ("last_spilled", ctypes.c_uint64),
         ("last_spill_full", ctypes.c_uint64),
+        ("last_shares", ctypes.c_uint64),
+        ("queue_aborts", ctypes.c_uint64),
     ]
 
     def __init__(self, *a, **kw):

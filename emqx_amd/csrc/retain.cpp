@@ -109,10 +109,13 @@ struct RWork {
   uint64_t wdesc_cap = 0;
   uint4* spill[2] = {nullptr, nullptr};  // spill rounds: items in / items out, alternating
   uint32_t spill_cap = 0;
+  uint4* queue = nullptr;  // queue mode's shared pieces (all zero when a call starts)
+  uint32_t queue_cap = 0;
+  uint32_t* qctl = nullptr;  // queue mode's per-shard control words (likewise)
   uint64_t* partials = nullptr;
   uint64_t partials_cap = 0;
   uint64_t* h_pinned = nullptr;  // [RC_WORDS / 2 + 1] readbacks: ctrl words, then the id total
-  uint64_t* prof = nullptr;      // [8] RETAIN_PROF builds with EMQX_RETAIN_PROF=1
+  uint64_t* prof = nullptr;      // [16] RETAIN_PROF builds with EMQX_RETAIN_PROF=1
   // host-API staging (device copies of the caller's buffers)
   uint8_t* d_fb = nullptr;
   uint64_t d_fb_cap = 0;
@@ -135,6 +138,8 @@ struct RWork {
     rfree(wdesc);
     rfree(spill[0]);
     rfree(spill[1]);
+    rfree(queue);
+    rfree(qctl);
     rfree(partials);
     rfree(prof);
     rfree(d_fb);
@@ -166,6 +171,17 @@ constexpr uint32_t SPILL_PER_WAVE = 4;  // spilled pieces dealt to each wave of 
 constexpr uint32_t SPILL_CAP = 1u << 22;  // items per spill buffer (a full one: waves keep walking)
 constexpr uint32_t SPILL_ROUNDS = 4;      // budgeted spill rounds per call, then one without a
                                           // budget; all enqueued up front, empty ones exit at once
+// Queue mode (balance 1, the default): no rounds; a wave that runs out of tiles waits on a ticket
+// of the shared-work queue, and busy waves share the bottom of their stacks while waves wait
+// (retain_walk_queue_kernel).  A round lasts as long as its busiest wave; the queue has no rounds.
+enum : uint32_t { BALANCE_SPILL = 0, BALANCE_QUEUE = 1 };
+constexpr uint32_t QUEUE_CAP = 1u << 22;   // shared pieces per call at most (a full queue: waves keep walking)
+constexpr uint32_t QUEUE_PIECE = 256;      // nodes per shared piece (4 wave steps)
+constexpr uint32_t QUEUE_CHECK = 8;        // steps between a busy wave's looks at the waiting count
+constexpr uint32_t QUEUE_POLL_LIMIT = 1u << 20;  // ~1 s of polls: then RC_QABORT, rerun in spill mode
+constexpr uint32_t QUEUE_MAX_WAIT = 2048;        // waves waiting on tickets at most
+constexpr uint32_t QUEUE_SLEEP = 1;              // s_sleep(16) per poll
+constexpr uint32_t QUEUE_SHARDS = 64;            // queue shards (waves w % 64 share with each other)
 
 // Filters per wave tile.  The walk is latency-bound (one dependent round trip per step), so the
 // number of waves in flight, not lane fill, sets its rate: 64 filters per tile leaves ~6 waves
@@ -205,13 +221,16 @@ struct emqx_retain {
   std::mutex ws_mu;
   std::vector<RWork*> free_ws;
   std::vector<std::unique_ptr<RWork>> all_ws;
-  std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0}, last_spill_rounds{0}, last_spilled{0}, last_spill_full{0};
+  std::atomic<uint64_t> last_ranges{0}, last_visits{0}, last_total{0}, last_spill_rounds{0}, last_spilled{0}, last_spill_full{0},
+      last_shares{0}, queue_aborts{0};
   std::atomic<double> last_match_ms{0}, last_walk_ms{0};
   // walk tuning (emqx_retain_set_tuning; the EMQX_RETAIN_* variables give the initial values)
   bool prof_on = false;
   uint32_t ablate = 0;  // EMQX_RETAIN_ABLATE (profiling builds only)  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
   std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_decay{0}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
-      walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP};
+      walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP}, balance{BALANCE_QUEUE},
+      queue_piece{QUEUE_PIECE}, queue_check{QUEUE_CHECK}, queue_cap{QUEUE_CAP}, queue_wait{QUEUE_MAX_WAIT},
+      queue_sleep{QUEUE_SLEEP}, queue_shards{QUEUE_SHARDS};
 };
 
 namespace {
@@ -594,6 +613,24 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   }
   a.wdesc = w->wdesc;
   a.spill_cap = std::min<uint32_t>(w->spill_cap, r->spill_cap.load());
+  bool queue = r->balance.load() == BALANCE_QUEUE;
+  if (queue && w->queue_cap == 0) {
+    RT_TRY(ralloc(w->queue, QUEUE_CAP));
+    RT_TRY(hipMemsetAsync(w->queue, 0, static_cast<uint64_t>(QUEUE_CAP) * sizeof(uint4), s));
+    RT_TRY(ralloc(w->qctl, static_cast<uint64_t>(QS_MAX_SHARDS) * QS_STRIDE));
+    RT_TRY(hipMemsetAsync(w->qctl, 0, static_cast<uint64_t>(QS_MAX_SHARDS) * QS_STRIDE * sizeof(uint32_t), s));
+    w->queue_cap = QUEUE_CAP;
+  }
+  a.qctl = w->qctl;
+  a.qshards = r->queue_shards.load();
+  a.queue = w->queue;
+  a.queue_cap = std::min<uint32_t>(w->queue_cap, r->queue_cap.load());
+  a.qpiece = std::max<uint32_t>(64, r->queue_piece.load());
+  a.qcheck = r->queue_check.load();
+  a.qpoll_limit = QUEUE_POLL_LIMIT;
+  a.qmaxwait = r->queue_wait.load();
+  a.qsleep = r->queue_sleep.load();
+  a.ntiles = static_cast<uint32_t>(ntiles);
   const uint32_t budget = r->step_budget.load();
   a.step_budget = budget == 0 ? ~0u : budget;
   const uint32_t per_wave = std::max<uint32_t>(1, r->spill_per_wave.load());
@@ -625,14 +662,18 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     // reserved but unused record slots must read as empty ranges
     RT_TRY(hipMemsetAsync(w->ranges, 0, static_cast<uint64_t>(w->range_cap) * sizeof(RRange), s));
     if (r->prof_on) {
-      if (!w->prof) RT_TRY(ralloc(w->prof, 8));
-      RT_TRY(hipMemsetAsync(w->prof, 0, 8 * sizeof(uint64_t), s));
+      if (!w->prof) RT_TRY(ralloc(w->prof, 16));
+      RT_TRY(hipMemsetAsync(w->prof, 0, 16 * sizeof(uint64_t), s));
       a.prof = w->prof;
       a.ablate = r->ablate;
     }
-    RT_TRY(launch_retain_walk(a, s));
     const uint64_t fit = w->stack_items / w->stack_cap;
-    for (uint32_t k = 0; k <= rounds; ++k) {
+    if (queue) {
+      RT_TRY(launch_retain_walk_queue(a, s));  // its last kernel zeroes the queue again
+    } else {
+      RT_TRY(launch_retain_walk(a, s));
+    }
+    for (uint32_t k = 0; !queue && k <= rounds; ++k) {
       RetainArgs b = a;
       b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(spill_waves, fit)));
       const uint32_t in_word = RC_SPILL + k;
@@ -653,8 +694,22 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     RT_TRY(hipMemcpyAsync(w->h_pinned + RC_WORDS / 2, d_oo + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     RT_TRY(hipStreamSynchronize(s));
     const uint64_t ranges = static_cast<uint64_t>(c[RC_RANGES]) + c[RC_BIG];
-    const uint32_t visits = c[RC_VISITS], ovf = c[RC_STACK];
+    uint32_t visits = 0, emitted = 0, qpieces = 0, qshares = 0;
+    for (uint32_t l = 0; l < RC_STAT_LINES; ++l) {
+      visits += c[RC_STAT + 16 * l];
+      emitted += c[RC_STAT + 16 * l + 1];
+      qpieces += c[RC_STAT + 16 * l + 2];
+      qshares += c[RC_STAT + 16 * l + 3];
+    }
+    const uint32_t ovf = c[RC_STACK];
     bool again = false;
+    if (queue && c[RC_QABORT]) {
+      // a waiting wave gave up (never expected: the safety valve of the queue's termination):
+      // rerun in spill mode
+      r->queue_aborts.fetch_add(1);
+      queue = false;
+      again = true;
+    }
     if (ovf) {
       if (w->stack_cap >= (1u << 24) || attempt > 8) return EMQX_ETOODEEP;
       w->stack_cap *= 4;
@@ -670,23 +725,28 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       again = true;
     }
     if (!again && r->prof_on)
-      std::fprintf(stderr, "RETAIN_CTRL spilled %u rounds %u spill_fail %u spill_max %u visits %u\n", c[RC_SPILLED],
-                   c[RC_ROUNDS], c[RC_SPILLFAIL], c[RC_SPILLMAX], c[RC_VISITS]);
+      std::fprintf(stderr, "RETAIN_CTRL spilled %u rounds %u spill_fail %u spill_max %u visits %u small %u big %u emitted %u\n",
+                   c[RC_SPILLED], c[RC_ROUNDS], c[RC_SPILLFAIL], c[RC_SPILLMAX], visits, c[RC_RANGES], c[RC_BIG], emitted);
     if (!again && r->prof_on) {
-      uint64_t pr[8];
+      uint64_t pr[16];
       if (hipMemcpy(pr, w->prof, sizeof(pr), hipMemcpyDeviceToHost) == hipSuccess) {
         std::fprintf(stderr, "RETAIN_PROF take %llu node %llu probe %llu search %llu emitpush %llu steps %llu active %llu searching %llu\n",
                      (unsigned long long)pr[0], (unsigned long long)pr[1], (unsigned long long)pr[2],
                      (unsigned long long)pr[3], (unsigned long long)pr[4], (unsigned long long)pr[5],
                      (unsigned long long)pr[6], (unsigned long long)pr[7]);
+        std::fprintf(stderr, "RETAIN_QPROF wait %llu ticket %llu retire %llu share %llu pieces %llu tilewalk %llu piecewalk %llu capped %llu\n",
+                     (unsigned long long)pr[8], (unsigned long long)pr[9], (unsigned long long)pr[10],
+                     (unsigned long long)pr[11], (unsigned long long)pr[12], (unsigned long long)pr[13],
+                     (unsigned long long)pr[14], (unsigned long long)pr[15]);
       }
     }
     if (!again) {
-      r->last_ranges.store(c[RC_EMITTED]);
+      r->last_ranges.store(emitted);
       r->last_visits.store(visits);
-      r->last_spill_rounds.store(c[RC_ROUNDS]);
-      r->last_spilled.store(c[RC_SPILLED]);
-      r->last_spill_full.store(c[RC_SPILLFAIL]);
+      r->last_spill_rounds.store(queue ? 0u : c[RC_ROUNDS]);
+      r->last_spilled.store(queue ? qpieces : c[RC_SPILLED]);
+      r->last_spill_full.store(queue ? 0u : c[RC_SPILLFAIL]);
+      r->last_shares.store(queue ? qshares : 0u);
       break;
     }
   }
@@ -720,6 +780,15 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   r->search = std::min<uint32_t>(env_u32("EMQX_RETAIN_SEARCH", RSEARCH_STREE), RSEARCH_STREE);
   r->walk_waves = env_u32("EMQX_RETAIN_WALK_WAVES", MAX_WAVES);
   r->spill_waves = env_u32("EMQX_RETAIN_SPILL_WAVES", SPILL_WAVES);
+  r->balance = std::min<uint32_t>(env_u32("EMQX_RETAIN_BALANCE", BALANCE_QUEUE), BALANCE_QUEUE);
+  {
+    const uint32_t qc = env_u32("EMQX_RETAIN_QUEUE_CHECK", QUEUE_CHECK);
+    r->queue_check = qc >= 1 && qc <= 1024 && (qc & (qc - 1)) == 0 ? qc : QUEUE_CHECK;
+  }
+  r->queue_piece = std::max<uint32_t>(64, env_u32("EMQX_RETAIN_QUEUE_PIECE", QUEUE_PIECE));
+  r->queue_wait = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_QUEUE_WAIT", QUEUE_MAX_WAIT));
+  r->queue_sleep = std::min<uint32_t>(64, env_u32("EMQX_RETAIN_QUEUE_SLEEP", QUEUE_SLEEP));
+  r->queue_shards = std::max<uint32_t>(1, std::min<uint32_t>(QS_MAX_SHARDS, env_u32("EMQX_RETAIN_QUEUE_SHARDS", QUEUE_SHARDS)));
   r->prof_on = env_u32("EMQX_RETAIN_PROF", 0) != 0;
   r->ablate = env_u32("EMQX_RETAIN_ABLATE", 0);
   *out = r;
@@ -957,6 +1026,27 @@ int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
   } else if (std::strcmp(key, "search") == 0) {
     if (v > RSEARCH_STREE) return EMQX_EINVAL;
     r->search = v;
+  } else if (std::strcmp(key, "balance") == 0) {
+    if (v > BALANCE_QUEUE) return EMQX_EINVAL;
+    r->balance = v;
+  } else if (std::strcmp(key, "queue_piece") == 0) {
+    if (v < 64 || v > (1u << 20)) return EMQX_EINVAL;
+    r->queue_piece = v;
+  } else if (std::strcmp(key, "queue_check") == 0) {
+    if (v < 1 || v > 1024 || (v & (v - 1)) != 0) return EMQX_EINVAL;
+    r->queue_check = v;
+  } else if (std::strcmp(key, "queue_wait") == 0) {
+    if (v < 1 || v > (1u << 20)) return EMQX_EINVAL;
+    r->queue_wait = v;
+  } else if (std::strcmp(key, "queue_sleep") == 0) {
+    if (v > 64) return EMQX_EINVAL;
+    r->queue_sleep = v;
+  } else if (std::strcmp(key, "queue_shards") == 0) {
+    if (v < 1 || v > QS_MAX_SHARDS) return EMQX_EINVAL;
+    r->queue_shards = v;
+  } else if (std::strcmp(key, "queue_cap") == 0) {
+    if (v < 64 || v > QUEUE_CAP) return EMQX_EINVAL;
+    r->queue_cap = v;
   } else {
     return EMQX_ENOTFOUND;
   }
@@ -988,6 +1078,8 @@ int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* dst) {
   out->last_spill_rounds = r->last_spill_rounds.load();
   out->last_spilled = r->last_spilled.load();
   out->last_spill_full = r->last_spill_full.load();
+  out->last_shares = r->last_shares.load();
+  out->queue_aborts = r->queue_aborts.load();
   out->last_total = r->last_total.load();
   out->last_match_ms = r->last_match_ms.load();
   out->last_walk_ms = r->last_walk_ms.load();

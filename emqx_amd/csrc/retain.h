@@ -132,24 +132,43 @@ struct RRange {
   uint32_t flags;  // RRANGE_*
 };
 
-// ctrl words of one call (zeroed per call)
+// ctrl words of one call (zeroed per call).  Words that many waves update or poll sit on 64-B
+// lines of their own: same-address (and same-line) traffic from thousands of waves is served
+// one request at a time at one memory channel (~25 ns each), so it is spread or kept rare.
 enum RCtrl : uint32_t {
-  RC_RANGES = 0,   // small range record slots reserved (with RC_BIG may exceed range_cap: rerun)
-  RC_VISITS = 1,   // node visits
-  RC_STACK = 2,    // a wave's stack overflowed (rerun with a larger stack)
-  RC_ROUNDS = 5,   // spill rounds that had work
-  RC_SPILLED = 6,  // items those rounds took in
-  RC_EMITTED = 7,  // range records written (RC_RANGES counts reserved slots: waves reserve
-                   // RRES at a time, the unused ones stay zeroed = empty records)
-  RC_BIG = 8,      // big range records, stored from the top of ranges[] down
-  RC_TILE = 9,     // first-round tiles taken beyond the first a.waves
-  RC_SPILLFAIL = 10,  // waves whose spill found no room (they finish their stacks themselves)
-  RC_SPILLMAX = 11,   // the most pieces one wave's spill asked for
-  RC_SPILL = 16,   // items spilled by the walk; RC_SPILL + 1 + k: by spill round k (each
-                   // round its own word, all zeroed with the rest at the call's start)
-  RC_WORDS = 64
+  RC_RANGES = 0,    // small range record slots reserved (with RC_BIG may exceed range_cap: rerun)
+  RC_BIG = 16,      // big range records, stored from the top of ranges[] down
+  RC_TILE = 32,     // first-round tiles taken beyond the first a.waves (queue mode: all tiles)
+  RC_STACK = 48,    // a wave's stack overflowed (rerun with a larger stack)
+  RC_ROUNDS = 49,   // spill rounds that had work
+  RC_SPILLED = 50,  // items those rounds took in
+  RC_SPILLFAIL = 51,  // waves whose spill found no room (they finish their stacks themselves)
+  RC_SPILLMAX = 52,   // the most pieces one wave's spill asked for
+  // per-wave totals, added when a wave ends on line (wave % RC_STAT_LINES) of 16 words:
+  // [RC_STAT + 16 l + 0] node visits, [.. + 1] range records written (RC_RANGES counts reserved
+  // slots: waves reserve RRES at a time, the unused ones stay zeroed = empty records),
+  // [.. + 2] pieces shared, [.. + 3] sharing events (queue mode)
+  RC_STAT = 64,
+  RC_STAT_LINES = 16,
+  RC_QABORT = 320,  // queue mode: a waiting wave gave up (poll limit); the host reruns in spill mode
+  RC_SPILL = 384,   // items spilled by the walk; RC_SPILL + 1 + k: by spill round k (each
+                    // round its own word, all zeroed with the rest at the call's start)
+  RC_WORDS = 432
 };
 constexpr uint32_t RC_MAX_ROUNDS = RC_WORDS - RC_SPILL - 2;  // budgeted spill rounds per call at most
+
+// Queue mode: the control words of one shard (RetainArgs.qctl + shard * QS_STRIDE; all zero when
+// a call starts, zeroed again by the call's last kernel)
+enum QCtrl : uint32_t {
+  QS_HEAD = 0,   // tickets taken by waves waiting for shared work (slot = ticket)
+  QS_TAIL = 1,   // slots reserved by waves sharing work (read with QS_HEAD as one u64)
+  QS_PEND = 2,   // units held (a tile being walked, or about to be taken) + pieces not yet walked
+  QS_TILES = 3,  // tile tickets taken (tile s + shards * ticket)
+  QS_DONE = 4,   // the shard's walk is over (set by the wave whose retire ended it)
+  QS_FAIL = 5,   // ~(first slot of a reservation past the shard's end), atomicMax; 0: none
+};
+constexpr uint32_t QS_STRIDE = 1088;  // words between shards' control lines (4352 B)
+constexpr uint32_t QS_MAX_SHARDS = 256;
 
 struct RetainArgs {
   RetainView rv;
@@ -170,6 +189,17 @@ struct RetainArgs {
   uint4* spill_out;        // [spill_cap] items left when the budget ran out
   uint32_t spill_cap;
   uint32_t spill_word;     // ctrl word counting the items this launch spills (RC_SPILL + round)
+  uint4* queue;            // [queue_cap] shared work (queue mode), all zero when a call starts;
+                           // shard s has slots [s * cap/S, (s + 1) * cap/S)
+  uint32_t queue_cap;
+  uint32_t* qctl;          // [qshards * QS_STRIDE] the shards' control words
+  uint32_t qshards;
+  uint32_t qpiece;         // nodes per shared piece (queue mode)
+  uint32_t qcheck;         // steps between a busy wave's looks at the waiting count (power of 2)
+  uint32_t qpoll_limit;    // polls before a waiting wave gives up (RC_QABORT; a safety valve)
+  uint32_t qmaxwait;       // waves waiting on tickets of one shard at most (more return)
+  uint32_t qsleep;         // s_sleep(16) (1024 clocks) per poll of a waiting wave
+  uint32_t ntiles;         // tiles of the call (queue mode's termination count)
   uint4* wdesc;            // [foffs[n] - foffs[0] + 2n] per-level step descriptors of the spill
                            // rounds, filter f's level l at foffs[f] - foffs[0] + 2f + l, levels
                            // 0..nlev: {word, end of the '+' run from l, the word after it
@@ -195,6 +225,10 @@ hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s);
 // round exits at once, so a call enqueues its rounds without waiting for the host
 hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t in_word, uint32_t per_wave,
                                     hipStream_t s);
+// the walk with work sharing instead of spill rounds: waves take tiles, then shared pieces from
+// a ticket queue; a busy wave that sees waiting waves shares the bottom half of its stack
+// (as qpiece-node pieces); every wave exits when no work is held or queued (ctrl[RC_QPEND])
+hipError_t launch_retain_walk_queue(const RetainArgs& a, hipStream_t s);
 // live ranks per range -> rcount, fcount (the range count is read on the device)
 hipError_t launch_retain_count(const RetainArgs& a, hipStream_t s);
 // ids of the live ranks -> out_ids at out_off[f] + cursor; nothing when out_off[n] > out_cap

@@ -178,7 +178,7 @@ __device__ __forceinline__ void stree_lower_bound2(const RSTree& t, uint32_t L, 
 // walk, summed into RetainArgs.prof[RPROF_SLOTS]: take (stack read + item split), node (its
 // fields + filter words), probe (edge / postings-key probes), search, emit+push; then steps,
 // active lanes, searching lanes.  Each mark waits for the wave's outstanding memory first.
-constexpr uint32_t RPROF_SLOTS = 8;
+constexpr uint32_t RPROF_SLOTS = 16;  // 8..15: queue mode (retain_walk_queue_kernel)
 #ifdef RETAIN_PROF
 #define RPROF_MARK(slot)                                   \
   do {                                                     \
@@ -188,9 +188,11 @@ constexpr uint32_t RPROF_SLOTS = 8;
     tprev = _t;                                            \
   } while (0)
 #define RPROF_ADD(slot, v) (pacc[slot] += (v))
+#define RPROF_NOW() clock64()
 #else
 #define RPROF_MARK(slot) do {} while (0)
 #define RPROF_ADD(slot, v) do {} while (0)
+#define RPROF_NOW() 0ull
 #endif
 
 constexpr int RW_WAVES = 4;
@@ -273,12 +275,204 @@ __device__ __forceinline__ void step_loads(const uint4* pa, const uint4* pb, con
   c = RPostKey{vc.x, vc.y, vc.z, vc.w};
 }
 
-template <bool TILE, int SEARCH>
+// Tokenize filter f and intern its words (one lane): word ids to a.wids (at foffs[f] - foffs[0]
+// + f) and the step descriptors of the untiled walks to a.wdesc; returns nlev | wildcard << 31.
+__device__ __forceinline__ uint32_t tokenize_filter(const RetainArgs& a, uint64_t f) {
+  const RetainView& rv = a.rv;
+  const uint64_t b0 = a.foffs[0];
+  uint32_t nlev = 0, wild = 0;
+  const uint64_t start = a.foffs[f], end = a.foffs[f + 1];
+  uint32_t* wout = a.wids + (start - b0) + f;
+  uint32_t len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  uint64_t ws = start;
+  for (uint64_t i = start; i <= end; ++i) {
+    const uint32_t c = (i < end) ? a.fbytes[i] : static_cast<uint32_t>('/');
+    if (c != '/') {
+      if (len < 16) {
+        const uint32_t v = c << (8u * (len & 3u));
+        const uint32_t q = len >> 2;
+        w0 |= q == 0 ? v : 0u;
+        w1 |= q == 1 ? v : 0u;
+        w2 |= q == 2 ? v : 0u;
+        w3 |= q == 3 ? v : 0u;
+      }
+      ++len;
+    } else {
+      uint32_t wid;
+      if (len == 1 && w0 == '+') {
+        wid = WID_PLUS;
+        wild = 1;
+      } else if (len == 1 && w0 == '#') {
+        wid = i == end ? WID_HASH : WID_NONE;  // a non-final '#' is a token no topic has
+        wild = 1;
+      } else {
+        const uint32_t h = len <= 16 ? word_hash16(len, w0, w1, w2, w3) : word_hash_bytes(a.fbytes + ws, len);
+        wid = rv.n_nodes ? rintern(rv, h, len, w0, w1, w2, w3, a.fbytes, ws) : WID_NONE;
+      }
+      wout[nlev++] = wid;
+      len = 0;
+      w0 = w1 = w2 = w3 = 0;
+      ws = i + 1;
+    }
+  }
+  // the step descriptors of the untiled walks (RetainArgs.wdesc), last level first
+  uint4* dout = a.wdesc + (start - b0) + 2 * f;
+  const uint32_t nw = nlev | (wild << 31);
+  dout[nlev] = make_uint4(WID_NONE, 0u, WID_HASH, nw);
+  uint32_t jn = nlev, wn = WID_HASH;  // the first non-'+' level above l, its word
+  for (uint32_t l = nlev; l-- > 0;) {
+    const uint32_t wl = wout[l];
+    dout[l] = make_uint4(wl, jn, wn, nw);
+    if (wl != WID_PLUS) {
+      jn = l;
+      wn = wl;
+    }
+  }
+  return nw;
+}
+
+// ---- work sharing (queue mode) --------------------------------------------------------------
+// A shared piece is one queue slot, written as two 8-B stores at agent scope in either order:
+// {x, y} with y = node count >= 1 and {z | QREADY, w} with w = global filter id.  A waiting
+// wave takes the slot of its ticket once both halves read as written.  The queue is all zero
+// when a call starts (the host clears the slots below the previous call's ticket count).
+constexpr uint32_t QREADY = 1u << 30;  // in z, above any level
+constexpr uint32_t QEND = 0xFFFFFFFFu;  // y of the end marker: the walk is over
+
+// The queue is sharded: wave w works in shard w % qshards, with its own tiles (t = s + S*j), its
+// own slots and its own control words (QS_*) on a line of their own, QS_STRIDE words from the
+// next shard's (distinct memory channels): every ticket, reservation and retire is an atomic on
+// one address, and one address serves ~40 M of them per second, so a single queue's counters
+// became the walk's bottleneck (and slowed every load that shared their channel).
+struct QShard {
+  uint32_t* c;       // control words
+  uint4* q;          // slots
+  uint32_t cap;      // slots
+  uint32_t ntiles;   // tiles of this shard
+  uint32_t s;
+};
+__device__ __forceinline__ QShard qshard(const RetainArgs& a, uint32_t gw) {
+  const uint32_t S = a.qshards, s = gw % S, cap = a.queue_cap / S;
+  return QShard{a.qctl + static_cast<uint64_t>(s) * QS_STRIDE, a.queue + static_cast<uint64_t>(s) * cap, cap,
+                a.ntiles > s ? (a.ntiles - s + S - 1) / S : 0u, s};
+}
+
+__device__ __forceinline__ void queue_put(uint4* q, uint4 it) {
+  uint64_t* p = reinterpret_cast<uint64_t*>(q);
+  __hip_atomic_store(p + 1, static_cast<uint64_t>(it.z | QREADY) | (static_cast<uint64_t>(it.w) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p, static_cast<uint64_t>(it.x) | (static_cast<uint64_t>(it.y) << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// slot q if both halves are written (*it = the piece), else false; the second half is read only
+// once the first is (one load per poll)
+__device__ __forceinline__ bool queue_get(uint4* q, uint4* it) {
+  uint64_t* p = reinterpret_cast<uint64_t*>(q);
+  const uint64_t a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((a >> 32) == 0) return false;
+  const uint64_t b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!(static_cast<uint32_t>(b) & QREADY)) return false;
+  *it = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b) & ~QREADY,
+                   static_cast<uint32_t>(b >> 32));
+  return true;
+}
+
+// Share the bottom of this wave's stack with the waiting waves: the whole global part if there is
+// one, else the bottom half of the LDS part, else (one item) all but its first qpiece nodes; as
+// pieces of at most qpiece nodes.  The pending count is raised (and the raise performed) before
+// any piece can be seen, so the walk cannot look finished while a piece is queued.  A full queue:
+// nothing is shared (the wave keeps walking its stack).
+template <bool TILE>
+__device__ __forceinline__ void share_work(const RetainArgs& a, const QShard& qs, uint4* ls, uint32_t& top, uint4* stk,
+                                           uint32_t& gtop, uint64_t fbase, uint32_t& npieces) {
+  const uint32_t lane = lane_id();
+  const uint32_t QP = a.qpiece;
+  uint32_t kind, nd;  // 0: stk[0, nd)  1: ls[0, nd)  2: ls[0] beyond its first QP nodes
+  if (gtop > 0) {
+    kind = 0;
+    nd = gtop;
+  } else if (top >= 2) {
+    kind = 1;
+    nd = top / 2;
+  } else if (top == 1 && ls[0].y > 2 * QP) {
+    kind = 2;
+    nd = 1;
+  } else {
+    return;
+  }
+  auto item = [&](uint32_t i) -> uint4 {
+    if (kind == 0) return stk[i];
+    uint4 it = ls[i];
+    if (kind == 2) {
+      it.x += QP;
+      it.y -= QP;
+    }
+    return it;
+  };
+  uint32_t ptot = 0;
+  for (uint32_t i0 = 0; i0 < nd; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint32_t np = i < nd ? (item(i).y + QP - 1) / QP : 0u;
+    uint32_t t;
+    (void)wave_excl(np, &t);
+    ptot += t;
+  }
+  uint32_t base = 0, ok = 0;
+  if (lane == 0) {
+    base = atomicAdd(&qs.c[QS_TAIL], ptot);
+    ok = base <= qs.cap && ptot <= qs.cap - base ? 1u : 0u;
+    if (!ok) atomicMax(&qs.c[QS_FAIL], ~base);  // slots from `base` on are never written
+    if (ok) {
+      atomicAdd(&qs.c[QS_PEND], ptot);
+      __builtin_amdgcn_s_waitcnt(0);  // the raise is performed before a piece is written
+    }
+  }
+  ok = __shfl(ok, 0, 64);
+  base = __shfl(base, 0, 64);
+  if (!ok) return;
+  npieces += ptot;
+  for (uint32_t i0 = 0; i0 < nd; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    uint4 it = make_uint4(0, 0, 0, 0);
+    if (i < nd) it = item(i);
+    const uint32_t np = i < nd ? (it.y + QP - 1) / QP : 0u;
+    uint32_t ctot;
+    const uint32_t off = wave_excl(np, &ctot);
+    if (TILE) it.w += static_cast<uint32_t>(fbase);
+    for (uint32_t k = 0; k < np; ++k) {
+      uint4 pc = it;
+      pc.x = it.x + QP * k;
+      pc.y = min(QP, it.y - QP * k);
+      queue_put(qs.q + base + off + k, pc);
+    }
+    base += ctot;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (kind == 0) {
+    gtop = 0;
+  } else if (kind == 1) {
+    for (uint32_t i0 = 0; i0 < top - nd; i0 += 64) {  // shift down (reads stay ahead of writes)
+      const uint32_t i = i0 + lane;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (i < top - nd) x = ls[nd + i];
+      __builtin_amdgcn_wave_barrier();
+      if (i < top - nd) ls[i] = x;
+    }
+    top -= nd;
+  } else if (lane == 0) {
+    ls[0].y = QP;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <bool TILE, int SEARCH, bool QUEUE>
 __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint32_t top, uint4* stk, uint32_t gtop,
                                            uint64_t fbase, const uint32_t* nlevs, const uint64_t* wbase,
                                            const uint32_t* lwords,
                                            uint32_t* pref, uint4* itm, uint32_t& visits, bool& overflow,
-                                           RangeRes& res, uint64_t* pacc) {
+                                           RangeRes& res, uint64_t* pacc, const QShard* qs = nullptr,
+                                           uint32_t* qstat = nullptr) {
   const uint32_t lane = lane_id();
   const RetainView& rv = a.rv;
   const uint64_t b0 = a.foffs[0];
@@ -288,7 +482,14 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
 #endif
   while (top + gtop > 0) {
     RPROF_MARK(4);
-    if (steps++ == a.step_budget) {
+    // queue mode: every qcheck steps lane 0 reads the waiting count (tickets - reserved slots);
+    // the load overlaps the step, its answer is used after the pushes
+    uint64_t ht = 0;
+    const bool look = QUEUE && (++steps & (a.qcheck - 1)) == 0;
+    if (look && lane == 0)
+      ht = __hip_atomic_load(reinterpret_cast<const uint64_t*>(qs->c + QS_HEAD), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    if (!QUEUE && steps++ == a.step_budget) {
       // the rest goes out: items wider than 64 nodes as 64-node pieces, so the next round can
       // deal one wide '+' slice over many waves (global part first, then the LDS part)
       const uint32_t all = gtop + top;
@@ -594,6 +795,16 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
     if (push) ls[top + qpos] = np;
     top += qtot;
     __builtin_amdgcn_wave_barrier();
+    if (QUEUE && look) {  // the waiting count, loaded at the step's start
+      const uint32_t hungry =
+          static_cast<int32_t>(static_cast<uint32_t>(ht) - static_cast<uint32_t>(ht >> 32)) > 0 ? 1u : 0u;
+      if (__shfl(hungry, 0, 64)) {
+        const uint64_t ts = RPROF_NOW();
+        share_work<TILE>(a, *qs, ls, top, stk, gtop, fbase, qstat[0]);
+        ++qstat[1];
+        RPROF_ADD(11, RPROF_NOW() - ts);
+      }
+    }
   }
 }
 
@@ -619,7 +830,7 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
   const uint64_t b0 = a.foffs[0];
   uint32_t visits = 0;
   bool overflow = false;
-  uint64_t pacc[RPROF_SLOTS] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t pacc[RPROF_SLOTS] = {};
   RangeRes res;
 
   // tiles beyond the first wave-full are taken first come, first served (one atomic per
@@ -628,59 +839,9 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
     const uint64_t f = t * tf + lane;
     const bool valid = lane < tf && f < a.n;
     // ---- tokenize + intern (per lane) -------------------------------------------------
-    uint32_t nlev = 0, wild = 0;
-    if (valid) {
-      const uint64_t start = a.foffs[f], end = a.foffs[f + 1];
-      uint32_t* wout = a.wids + (start - b0) + f;
-      uint32_t len = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-      uint64_t ws = start;
-      for (uint64_t i = start; i <= end; ++i) {
-        const uint32_t c = (i < end) ? a.fbytes[i] : static_cast<uint32_t>('/');
-        if (c != '/') {
-          if (len < 16) {
-            const uint32_t v = c << (8u * (len & 3u));
-            const uint32_t q = len >> 2;
-            w0 |= q == 0 ? v : 0u;
-            w1 |= q == 1 ? v : 0u;
-            w2 |= q == 2 ? v : 0u;
-            w3 |= q == 3 ? v : 0u;
-          }
-          ++len;
-        } else {
-          uint32_t wid;
-          if (len == 1 && w0 == '+') {
-            wid = WID_PLUS;
-            wild = 1;
-          } else if (len == 1 && w0 == '#') {
-            wid = i == end ? WID_HASH : WID_NONE;  // a non-final '#' is a token no topic has
-            wild = 1;
-          } else {
-            const uint32_t h = len <= 16 ? word_hash16(len, w0, w1, w2, w3) : word_hash_bytes(a.fbytes + ws, len);
-            wid = rv.n_nodes ? rintern(rv, h, len, w0, w1, w2, w3, a.fbytes, ws) : WID_NONE;
-          }
-          wout[nlev++] = wid;
-          len = 0;
-          w0 = w1 = w2 = w3 = 0;
-          ws = i + 1;
-        }
-      }
-      // the step descriptors of the spill rounds (RetainArgs.wdesc), last level first
-      {
-        uint4* dout = a.wdesc + (start - b0) + 2 * f;
-        const uint32_t nw = nlev | (wild << 31);
-        dout[nlev] = make_uint4(WID_NONE, 0u, WID_HASH, nw);
-        uint32_t jn = nlev, wn = WID_HASH;  // the first non-'+' level above l, its word
-        for (uint32_t l = nlev; l-- > 0;) {
-          const uint32_t wl = wout[l];
-          dout[l] = make_uint4(wl, jn, wn, nw);
-          if (wl != WID_PLUS) {
-            jn = l;
-            wn = wl;
-          }
-        }
-      }
-    }
-    nlevs[lane] = nlev | (wild << 31);
+    const uint32_t nw = valid ? tokenize_filter(a, f) : 0u;
+    const uint32_t nlev = nw & 0x7FFFFFFFu;
+    nlevs[lane] = nw;
     // the tile's words into LDS when they fit (the walk reads one or two per node visit)
     uint32_t wtot;
     const uint32_t wofs = wave_excl(valid ? nlev : 0u, &wtot);
@@ -696,7 +857,7 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
     const uint32_t ppos = wave_excl(push0 ? 1u : 0u, &ptot);
     if (push0) s_stk[wib][ppos] = make_uint4(0u, 1u, 0u, lane);
     __builtin_amdgcn_wave_barrier();
-    walk_stack<true, SEARCH>(a, s_stk[wib], ptot, stk, 0, t * tf, nlevs, wbase,
+    walk_stack<true, SEARCH, false>(a, s_stk[wib], ptot, stk, 0, t * tf, nlevs, wbase,
                              lds_words ? s_words[wib] : nullptr, s_pref[wib], s_item[wib], visits,
                              overflow, res, pacc);
     if (overflow) break;
@@ -708,8 +869,8 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
   // visits: one atomic per wave
   uint32_t vtot;
   (void)wave_excl(visits, &vtot);
-  if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
-  if (lane == 0 && res.emitted) atomicAdd(&a.ctrl[RC_EMITTED], res.emitted);
+  if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_STAT + 16 * (gw % RC_STAT_LINES)], vtot);
+  if (lane == 0 && res.emitted) atomicAdd(&a.ctrl[RC_STAT + 16 * (gw % RC_STAT_LINES) + 1], res.emitted);
 #ifdef RETAIN_PROF
   if (lane == 0 && a.prof)
     for (uint32_t i = 0; i < RPROF_SLOTS; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(a.prof + i), pacc[i]);
@@ -746,26 +907,228 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_spill_kerne
   const uint32_t top = hi > lo ? static_cast<uint32_t>(hi - lo) : 0u;
   uint32_t visits = 0;
   bool overflow = top > a.stack_cap;
-  uint64_t pacc[RPROF_SLOTS] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t pacc[RPROF_SLOTS] = {};
   RangeRes res;
   if (!overflow) {
     for (uint32_t i = lane; i < top; i += 64) stk[i] = in[lo + i];
     __threadfence_block();
-    walk_stack<false, SEARCH>(a, s_stk[wib], 0, stk, top, 0, nullptr, nullptr, nullptr, s_pref[wib],
+    walk_stack<false, SEARCH, false>(a, s_stk[wib], 0, stk, top, 0, nullptr, nullptr, nullptr, s_pref[wib],
                               s_item[wib], visits,
                               overflow, res, pacc);
   }
   if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
   uint32_t vtot;
   (void)wave_excl(visits, &vtot);
-  if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_VISITS], vtot);
-  if (lane == 0 && res.emitted) atomicAdd(&a.ctrl[RC_EMITTED], res.emitted);
+  if (lane == 0 && vtot) atomicAdd(&a.ctrl[RC_STAT + 16 * (gw % RC_STAT_LINES)], vtot);
+  if (lane == 0 && res.emitted) atomicAdd(&a.ctrl[RC_STAT + 16 * (gw % RC_STAT_LINES) + 1], res.emitted);
 #ifdef RETAIN_PROF
   if (lane == 0 && a.prof)
     for (uint32_t i = 0; i < RPROF_SLOTS; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(a.prof + i), pacc[i]);
 #else
   (void)pacc;
 #endif
+}
+
+// Retire one unit of the shard (a tile or a piece walked to its end, or a tile ticket that found
+// none).  A retire that leaves nothing held or queued once the shard's tiles are all taken ends
+// the shard's walk: the wave sets QS_DONE, then writes the end marker into every slot a waiting
+// wave can hold: tickets below the head it reads after setting QS_DONE, from the reserved count
+// (or the first never-written slot) on.  A wave whose ticket comes later reads QS_DONE after
+// taking it; one past the shard's slots polls QS_DONE.  (Two waves may both end it: the markers
+// are the same.)
+__device__ __forceinline__ void retire_unit(const QShard& qs) {
+  const uint32_t lane = lane_id();
+  uint32_t lo = 0, hi = 0;
+  if (lane == 0) {
+    const uint32_t old = atomicAdd(&qs.c[QS_PEND], 0xFFFFFFFFu);
+    if (old == 1u &&
+        __hip_atomic_load(&qs.c[QS_TILES], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= qs.ntiles) {
+      __hip_atomic_store(&qs.c[QS_DONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);  // done is set before the head is read
+      const uint64_t ht = __hip_atomic_load(reinterpret_cast<const uint64_t*>(qs.c + QS_HEAD), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t fail = ~__hip_atomic_load(&qs.c[QS_FAIL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      lo = min(static_cast<uint32_t>(ht >> 32), fail);
+      hi = min(static_cast<uint32_t>(ht), qs.cap);
+    }
+  }
+  lo = __shfl(lo, 0, 64);
+  hi = __shfl(hi, 0, 64);
+  for (uint32_t k = lo + lane; k < hi; k += 64) queue_put(qs.q + k, make_uint4(0u, QEND, 0u, 0u));
+}
+
+// Queue mode, first kernel: every filter tokenized and interned (one lane each), so the walk's
+// waves can take any filter's pieces: the word ids and step descriptors are written by a launch
+// that has finished, not by another wave of the same one.
+__global__ __launch_bounds__(256) void retain_tokenize_kernel(RetainArgs a) {
+  const uint64_t f = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (f < a.n) (void)tokenize_filter(a, f);
+}
+
+// Queue mode, the walk.  Wave w works in shard s = w % qshards: it takes the shard's tiles by
+// ticket (QS_TILES), then its shared pieces by ticket (QS_HEAD; a ticket names a slot).  Busy
+// waves share when waves of their shard wait (share_work).  QS_PEND counts the units held or
+// queued, and only a wave holding one (or announcing a tile ticket, raised before the ticket is
+// taken) raises it, so once it is 0 with the tiles all taken nothing is held or queued and no
+// piece can come: the wave whose retire saw that wakes the waiting ones (retire_unit).  A wave
+// holds work only after it started, so waves not yet resident hold nothing and the grid drains;
+// a waiting wave also gives up after qpoll_limit polls (RC_QABORT; the host reruns the call in
+// spill mode), a safety valve that a correct walk never reaches.
+template <int SEARCH>
+__global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_queue_kernel(RetainArgs a) {
+  const uint32_t lane = lane_id();
+  const uint32_t wib = threadIdx.x >> 6;
+  const uint32_t gw = blockIdx.x * RW_WAVES + wib;
+  __shared__ uint32_t s_pref[RW_WAVES][64];
+  __shared__ uint4 s_item[RW_WAVES][64];
+  __shared__ uint32_t s_nlev[RW_WAVES][64];
+  __shared__ uint64_t s_wb[RW_WAVES][64];
+  __shared__ uint4 s_stk[RW_WAVES][RSTK];
+  __shared__ uint32_t s_words[RW_WAVES][RWORDS];
+  uint32_t* nlevs = s_nlev[wib];
+  uint64_t* wbase = s_wb[wib];
+  uint4* stk = a.stack + static_cast<uint64_t>(gw) * a.stack_cap;
+  const RetainView& rv = a.rv;
+  const uint32_t tf = a.tile_filters;
+  const uint64_t b0 = a.foffs[0];
+  const QShard qs = qshard(a, gw);
+  const uint32_t maxwait = max(2u, a.qmaxwait / a.qshards);
+  uint32_t visits = 0, qstat[2] = {0, 0};
+  bool overflow = false;
+  uint64_t pacc[RPROF_SLOTS] = {};
+  RangeRes res;
+  // ---- the shard's tiles ----------------------------------------------------------------------
+  for (;;) {
+    uint32_t t = 0;
+    uint64_t tq = RPROF_NOW();
+    if (lane == 0) {
+      atomicAdd(&qs.c[QS_PEND], 1u);  // announced before the ticket: see retire_unit
+      __builtin_amdgcn_s_waitcnt(0);
+      t = qs.s + a.qshards * atomicAdd(&qs.c[QS_TILES], 1u);
+    }
+    t = __shfl(t, 0, 64);
+    RPROF_ADD(9, RPROF_NOW() - tq);
+    if (t >= a.ntiles) {
+      retire_unit(qs);  // no tile: the announcement is withdrawn
+      break;
+    }
+    const uint64_t f = static_cast<uint64_t>(t) * tf + lane;
+    const bool valid = lane < tf && f < a.n;
+    uint32_t nw = 0;
+    uint64_t wsrc = 0;
+    if (valid) {
+      wsrc = (a.foffs[f] - b0) + f;
+      nw = a.wdesc[wsrc + f].w;  // level 0's descriptor (foffs[f] - b0 + 2f)
+    }
+    const uint32_t nlev = nw & 0x7FFFFFFFu;
+    nlevs[lane] = nw;
+    uint32_t wtot;
+    const uint32_t wofs = wave_excl(valid ? nlev : 0u, &wtot);
+    const bool lds_words = wtot <= RWORDS;
+    if (lds_words && valid)
+      for (uint32_t l = 0; l < nlev; ++l) s_words[wib][wofs + l] = a.wids[wsrc + l];
+    wbase[lane] = !valid ? 0 : lds_words ? wofs : wsrc;
+    const bool push0 = valid && rv.n_nodes != 0;
+    uint32_t ptot;
+    const uint32_t ppos = wave_excl(push0 ? 1u : 0u, &ptot);
+    if (push0) s_stk[wib][ppos] = make_uint4(0u, 1u, 0u, lane);
+    __builtin_amdgcn_wave_barrier();
+    uint64_t t0 = RPROF_NOW();
+    walk_stack<true, SEARCH, true>(a, s_stk[wib], ptot, stk, 0, static_cast<uint64_t>(t) * tf, nlevs, wbase,
+                                   lds_words ? s_words[wib] : nullptr, s_pref[wib], s_item[wib], visits, overflow,
+                                   res, pacc, &qs, qstat);
+    uint64_t t1 = RPROF_NOW();
+    RPROF_ADD(13, t1 - t0);
+    retire_unit(qs);  // this tile is walked (or abandoned)
+    RPROF_ADD(10, RPROF_NOW() - t1);
+    if (overflow) break;
+  }
+  // ---- the shard's shared pieces --------------------------------------------------------------
+  // At most `maxwait` waves of a shard wait at once: a wave that finds that many tickets beyond
+  // the reserved slots returns instead of taking one.  Safe: a shared piece's slot is below the
+  // reserved count, so either its ticket is taken already or fewer than maxwait wait and the next
+  // wave to come (at the latest the one that shared it, once its own stack is empty) takes one.
+  uint32_t polls = 0;
+  while (!overflow) {
+    uint32_t k = 0, state = 0;  // 1: a piece, 2: the walk is over (or enough waves wait)
+    uint64_t tq = RPROF_NOW();
+    if (lane == 0) {
+      const uint64_t ht = __hip_atomic_load(reinterpret_cast<const uint64_t*>(qs.c + QS_HEAD), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      if (static_cast<int32_t>(static_cast<uint32_t>(ht) - static_cast<uint32_t>(ht >> 32)) >=
+          static_cast<int32_t>(maxwait))
+        state = 2;
+      else
+        k = atomicAdd(&qs.c[QS_HEAD], 1u);
+    }
+    state = __shfl(state, 0, 64);
+    if (state == 2) {
+      RPROF_ADD(15, 1);
+      break;
+    }
+    k = __shfl(k, 0, 64);
+    uint4 it = make_uint4(0, 0, 0, 0);
+    if (lane == 0 && __hip_atomic_load(&qs.c[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) state = 2;
+    state = __shfl(state, 0, 64);
+    const uint64_t tw = RPROF_NOW();
+    RPROF_ADD(9, tw - tq);
+    for (;;) {
+      if (lane == 0 && state == 0) {
+        if (k < qs.cap) {
+          if (queue_get(qs.q + k, &it)) state = it.y == QEND ? 2u : 1u;
+        } else if (__hip_atomic_load(&qs.c[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          state = 2;
+        }
+        if (state == 0 && ++polls > a.qpoll_limit) {
+          atomicOr(&a.ctrl[RC_QABORT], 1u);
+          state = 2;
+        }
+      }
+      state = __shfl(state, 0, 64);
+      if (state) break;
+      for (uint32_t z = 0; z < a.qsleep; ++z) __builtin_amdgcn_s_sleep(16);
+    }
+    const uint64_t tp = RPROF_NOW();
+    RPROF_ADD(8, tp - tw);
+    if (state == 2) break;
+    RPROF_ADD(12, 1);
+    if (lane == 0) s_stk[wib][0] = it;
+    __builtin_amdgcn_wave_barrier();
+    walk_stack<false, SEARCH, true>(a, s_stk[wib], 1, stk, 0, 0, nullptr, nullptr, nullptr, s_pref[wib],
+                                    s_item[wib], visits, overflow, res, pacc, &qs, qstat);
+    const uint64_t te = RPROF_NOW();
+    RPROF_ADD(14, te - tp);
+    retire_unit(qs);
+    RPROF_ADD(10, RPROF_NOW() - te);
+  }
+  if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
+  uint32_t vtot;
+  (void)wave_excl(visits, &vtot);
+  uint32_t* st = a.ctrl + RC_STAT + 16 * (gw % RC_STAT_LINES);
+  if (lane == 0 && vtot) atomicAdd(&st[0], vtot);
+  if (lane == 0 && res.emitted) atomicAdd(&st[1], res.emitted);
+  if (lane == 0 && qstat[0]) atomicAdd(&st[2], qstat[0]);
+  if (lane == 0 && qstat[1]) atomicAdd(&st[3], qstat[1]);
+#ifdef RETAIN_PROF
+  if (lane == 0 && a.prof)
+    for (uint32_t i = 0; i < RPROF_SLOTS; ++i) atomicAdd(reinterpret_cast<unsigned long long*>(a.prof + i), pacc[i]);
+#else
+  (void)pacc;
+#endif
+}
+
+// Queue mode, the call's last walk step: every shard's written slots (below its ticket and
+// reserved counts) and its control words back to zero for the next call.
+__global__ __launch_bounds__(256) void retain_queue_clear_kernel(RetainArgs a) {
+  __shared__ uint32_t s_n;
+  uint32_t* c = a.qctl + static_cast<uint64_t>(blockIdx.x) * QS_STRIDE;
+  const uint32_t cap = a.queue_cap / a.qshards;
+  if (threadIdx.x == 0) s_n = min(max(c[QS_HEAD], c[QS_TAIL]), cap);
+  __syncthreads();
+  uint4* q = a.queue + static_cast<uint64_t>(blockIdx.x) * cap;
+  for (uint32_t k = threadIdx.x; k < s_n; k += blockDim.x) q[k] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  if (threadIdx.x < 16) c[threadIdx.x] = 0;
 }
 
 namespace {
@@ -789,7 +1152,8 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a) {
   if (MODE == 1 && a.out_off[a.n] > a.out_cap) return;      // too many ids: the caller grows
                                                             // its buffer and asks again
   const bool guard = rv.has_expiring && a.now_ms >= 0;
-  const uint64_t nrows = (static_cast<uint64_t>(ns) + 64 / RGROUP - 1) / (64 / RGROUP);
+  // units: SUPER-ROWS of 64 consecutive small records (8 rows of 8), then the big records
+  const uint64_t nrows = (static_cast<uint64_t>(ns) + 63) / 64;
 #ifdef RETAIN_PROF
   // ablations (timing experiments only): bit 0 no small rows, 1 no big records, 2 no atomics
   const uint32_t abl = a.ablate;
@@ -800,91 +1164,105 @@ __global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a) {
     if ((abl & 1) && u < nrows) continue;
     if ((abl & 2) && u >= nrows) continue;
     if (u < nrows) {
-      // ---- a row of 8 consecutive small records (at most RBIG ranks each), 8 lanes each ----
-      const uint64_t r = u * (64 / RGROUP) + grp;
-      RRange rg{0, 0, 0, 0};
-      if (r < ns) rg = a.ranges[r];  // an unused reserved slot reads as lo == hi
-      const bool check = guard || (rg.flags >> RRANGE_MIND_SHIFT) != 0;
-      uint32_t rk[RPER];
-      bool live[RPER];
-#pragma unroll
-      for (uint32_t k = 0; k < RPER; ++k) {
-        const uint32_t i = rg.lo + sub + RGROUP * k;
-        rk[k] = i < rg.hi ? rank_at(rv, i, rg.flags) : 0u;
-      }
-      // a checked record's live ranks: the count pass tests them (expiry, depth) and keeps the
-      // mask (bit sub + RGROUP * k), the write pass takes the mask instead of loading them again
-      uint64_t lm = 0;
-      if (MODE == 1 && check && r < ns && rg.hi > rg.lo) lm = a.rlive[r];
-#pragma unroll
-      for (uint32_t k = 0; k < RPER; ++k) {
-        const bool in = rg.lo + sub + RGROUP * k < rg.hi;
-        if (MODE == 1 && check)
-          live[k] = (lm >> (sub + RGROUP * k)) & 1u;
-        else
-          live[k] = in && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
-      }
-      uint32_t c = 0;
-      if (MODE == 0) {
-        uint64_t m = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < RPER; ++k) {
-          c += live[k] ? 1u : 0u;
-          m |= ((__ballot(live[k]) >> (grp * RGROUP)) & 0xFFull) << (RGROUP * k);
-        }
-        c += __shfl_xor(c, 1, 64);
-        c += __shfl_xor(c, 2, 64);
-        c += __shfl_xor(c, 4, 64);
-        if (sub == 0 && r < ns && rg.hi > rg.lo) {
-          a.rcount[r] = c;
-          if (check) a.rlive[r] = m;
-        }
-      } else {
-        c = (r < ns && rg.hi > rg.lo) ? a.rcount[r] : 0u;
-      }
-      // Runs of consecutive records of one filter (a wave's step emits a filter's records
-      // side by side) take one per-filter atomic per run, from the run's last group: a broad
-      // filter's thousands of records would otherwise queue on one address.
-      const uint32_t f = (r < ns && rg.hi > rg.lo) ? rg.f : 0xFFFFFFFFu;
-      const uint32_t fprev = __shfl(f, (grp ? grp - 1 : 0) * RGROUP, 64);
-      const uint32_t fnext = __shfl(f, (grp + 1 < 64 / RGROUP ? grp + 1 : grp) * RGROUP, 64);
-      const bool head = grp == 0 || fprev != f, tail = grp + 1 == 64 / RGROUP || fnext != f;
-      const uint64_t hm = __ballot(head), tm = __ballot(tail);
-      uint32_t hb = 0, tb = 0;
-#pragma unroll
-      for (uint32_t g = 0; g < 64 / RGROUP; ++g) {
-        hb |= static_cast<uint32_t>((hm >> (g * RGROUP)) & 1u) << g;
-        tb |= static_cast<uint32_t>((tm >> (g * RGROUP)) & 1u) << g;
-      }
-      uint32_t incl = c;  // inclusive prefix of the groups' counts
-#pragma unroll
-      for (uint32_t d = 1; d < 64 / RGROUP; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d * RGROUP, 64);
-        if (grp >= d) incl += y;
-      }
-      const uint32_t rstart = 31u - __clz(hb & ((2u << grp) - 1u));
-      const uint32_t rend = grp + __ffs(tb >> grp) - 1u;
-      const uint32_t prev_incl = __shfl(incl, (rstart ? rstart - 1 : 0) * RGROUP, 64);  // every lane takes part
-      const uint32_t before = rstart ? prev_incl : 0u;
-      const uint32_t rincl = incl - before;  // this run's count up to and including this group
-      if (MODE == 0) {
-        if (tail && sub == 0 && f != 0xFFFFFFFFu && rincl && !(abl & 4)) atomicAdd(&a.fcount[f], rincl);
-      } else {
+      // ---- a super-row: lane i holds record u*64 + i for the per-filter totals; each of its 8
+      // rows gives every record 8 lanes (every 8th rank, all loads of the record in flight) ----
+      const uint64_t rme = u * 64 + lane;
+      RRange mine{0, 0, 0, 0};
+      if (rme < ns) mine = a.ranges[rme];  // an unused reserved slot reads as lo == hi
+      // Per-filter totals: a filter's records sit side by side (a wave's step emits them
+      // together), so runs of equal filters over the 64 records take one atomic per run, from
+      // the run's last lane (a broad filter's thousands of records would otherwise queue on one
+      // address).  Empty records end runs.
+      const uint32_t fme = mine.hi > mine.lo ? mine.f : 0xFFFFFFFFu;
+      const uint32_t fprev = __shfl_up(fme, 1, 64), fnext = __shfl_down(fme, 1, 64);
+      const uint64_t hm = __ballot(lane == 0 || fprev != fme), tm = __ballot(lane == 63 || fnext != fme);
+      const uint32_t rstart = 63u - __clzll(hm & (~0ull >> (63 - lane)));  // this run's first lane
+      const uint32_t rend = lane + __ffsll(static_cast<long long>(tm >> lane)) - 1u;  // its last
+      const bool tail = (tm >> lane) & 1u;
+      uint32_t cme = 0;  // this lane's record's live ranks
+      uint64_t pos = 0;  // write pass: its first output position
+      if (MODE == 1) {
+        cme = fme != 0xFFFFFFFFu ? a.rcount[rme] : 0u;
+        uint32_t tot;
+        const uint32_t incl = wave_excl(cme, &tot) + cme;
+        const uint32_t prev = __shfl(incl, rstart ? rstart - 1 : 0, 64);  // every lane takes part
+        const uint32_t before = rstart ? prev : 0u;
+        const uint32_t rincl = incl - before;
         uint64_t base = 0;
-        if (tail && sub == 0 && f != 0xFFFFFFFFu && rincl)
-          base = a.out_off[f] + ((abl & 4) ? 0u : atomicAdd(&a.fcursor[f], rincl));
-        base = __shfl(base, rend * RGROUP, 64);
-        uint64_t p = base + (rincl - c);  // this record's first position
-        uint32_t id[RPER];
-#pragma unroll
-        for (uint32_t k = 0; k < RPER; ++k) id[k] = live[k] ? rv.rank_id[rk[k]] : 0u;
+        if (tail && fme != 0xFFFFFFFFu && rincl)
+          base = a.out_off[fme] + ((abl & 4) ? 0u : atomicAdd(&a.fcursor[fme], rincl));
+        const uint32_t blo = __shfl(static_cast<uint32_t>(base), rend, 64);
+        const uint32_t bhi = __shfl(static_cast<uint32_t>(base >> 32), rend, 64);
+        pos = ((static_cast<uint64_t>(bhi) << 32) | blo) + (rincl - cme);
+      }
+#pragma unroll 1
+      for (uint32_t row = 0; row < 8; ++row) {
+        const uint32_t src = row * 8 + grp;  // the lane holding this group's record
+        const uint64_t r = u * 64 + src;
+        RRange rg;
+        rg.f = __shfl(mine.f, src, 64);
+        rg.lo = __shfl(mine.lo, src, 64);
+        rg.hi = __shfl(mine.hi, src, 64);
+        rg.flags = __shfl(mine.flags, src, 64);
+        const bool check = guard || (rg.flags >> RRANGE_MIND_SHIFT) != 0;
+        uint32_t rk[RPER];
+        bool live[RPER];
 #pragma unroll
         for (uint32_t k = 0; k < RPER; ++k) {
-          const uint32_t bits = static_cast<uint32_t>(__ballot(live[k]) >> (grp * RGROUP)) & 0xFFu;
-          const uint32_t rank = __popc(bits & ((1u << sub) - 1u));
-          if (live[k] && p + rank < a.out_cap) a.out_ids[p + rank] = id[k];
-          p += __popc(bits);
+          const uint32_t i = rg.lo + sub + RGROUP * k;
+          rk[k] = i < rg.hi ? rank_at(rv, i, rg.flags) : 0u;
         }
+        // a checked record's live ranks: the count pass tests them (expiry, depth) and keeps the
+        // mask (bit sub + RGROUP * k), the write pass takes the mask instead of loading them again
+        uint64_t lm = 0;
+        if (MODE == 1 && check && rg.hi > rg.lo) lm = a.rlive[r];
+#pragma unroll
+        for (uint32_t k = 0; k < RPER; ++k) {
+          const bool in = rg.lo + sub + RGROUP * k < rg.hi;
+          if (MODE == 1 && check)
+            live[k] = (lm >> (sub + RGROUP * k)) & 1u;
+          else
+            live[k] = in && (!check || rank_ok(rv, rk[k], guard, a.now_ms, rg.flags));
+        }
+        if (MODE == 0) {
+          uint32_t c = 0;
+          uint64_t m = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < RPER; ++k) {
+            c += live[k] ? 1u : 0u;
+            m |= ((__ballot(live[k]) >> (grp * RGROUP)) & 0xFFull) << (RGROUP * k);
+          }
+          c += __shfl_xor(c, 1, 64);
+          c += __shfl_xor(c, 2, 64);
+          c += __shfl_xor(c, 4, 64);
+          if (sub == 0 && rg.hi > rg.lo) {
+            a.rcount[r] = c;
+            if (check) a.rlive[r] = m;
+          }
+          const uint32_t cr = __shfl(c, (lane & 7) * 8, 64);  // row `row`'s group (lane & 7)
+          if ((lane >> 3) == row) cme = cr;
+        } else {
+          uint64_t p = (static_cast<uint64_t>(__shfl(static_cast<uint32_t>(pos >> 32), src, 64)) << 32) |
+                       __shfl(static_cast<uint32_t>(pos), src, 64);
+          uint32_t id[RPER];
+#pragma unroll
+          for (uint32_t k = 0; k < RPER; ++k) id[k] = live[k] ? rv.rank_id[rk[k]] : 0u;
+#pragma unroll
+          for (uint32_t k = 0; k < RPER; ++k) {
+            const uint32_t bits = static_cast<uint32_t>(__ballot(live[k]) >> (grp * RGROUP)) & 0xFFu;
+            const uint32_t rank = __popc(bits & ((1u << sub) - 1u));
+            if (live[k] && p + rank < a.out_cap) a.out_ids[p + rank] = id[k];
+            p += __popc(bits);
+          }
+        }
+      }
+      if (MODE == 0) {
+        uint32_t tot;
+        const uint32_t incl = wave_excl(cme, &tot) + cme;
+        const uint32_t prev = __shfl(incl, rstart ? rstart - 1 : 0, 64);  // every lane takes part
+        const uint32_t before = rstart ? prev : 0u;
+        const uint32_t rincl = incl - before;
+        if (tail && fme != 0xFFFFFFFFu && rincl && !(abl & 4)) atomicAdd(&a.fcount[fme], rincl);
       }
     } else {
       // ---- one big record: RCHUNK ranks over the wave, every load of the pass in flight ----
@@ -953,6 +1331,18 @@ hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_retain_walk_queue(const RetainArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(retain_tokenize_kernel, dim3(static_cast<uint32_t>((a.n + 255) / 256)), dim3(256), 0, s, a);
+  const uint32_t blocks = (a.waves + RW_WAVES - 1) / RW_WAVES;
+  if (a.search == RSEARCH_STREE)
+    hipLaunchKernelGGL(retain_walk_queue_kernel<RSEARCH_STREE>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL(retain_walk_queue_kernel<RSEARCH_FENCED>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
+  hipLaunchKernelGGL(retain_queue_clear_kernel, dim3(a.qshards), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32_t in_word, uint32_t per_wave,
                                     hipStream_t s) {
   if (a.waves == 0) return hipSuccess;
@@ -968,7 +1358,7 @@ hipError_t launch_retain_walk_spill(const RetainArgs& a, const uint4* in, uint32
 
 // grid of the output kernels: sized by the range capacity (the range count is on the device)
 static uint32_t out_blocks(uint32_t cap) {
-  const uint64_t waves = (static_cast<uint64_t>(cap) + 7) / 8;  // rows of 8 small records + big records
+  const uint64_t waves = (static_cast<uint64_t>(cap) + 7) / 8;  // one per 8 slots (super-rows of 64 + big records)
   return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((waves + 3) / 4, 8192)));
 }
 

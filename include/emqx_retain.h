@@ -61,6 +61,8 @@ typedef struct emqx_retain_stats {
   uint64_t last_spill_rounds; /* walk rounds after the first (work left by waves over budget) */
   uint64_t last_spilled;     /* work items handed to those rounds                           */
   uint64_t last_spill_full;  /* waves whose spill found the buffer full (walked on themselves)  */
+  uint64_t last_shares;      /* queue mode: times a busy wave shared work (last_spilled: pieces) */
+  uint64_t queue_aborts;     /* queue-mode calls rerun in spill mode (a waiting wave gave up; 0) */
 } emqx_retain_stats;
 
 int emqx_retain_create(int32_t device, emqx_retain** out);
@@ -112,8 +114,13 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes
  * a budget, default 4, at most 46), "spill_cap" (spill-buffer items a round may use, 64..4M,
  * default 4M; tests), "search" (0: two-level binary searches of the postings and rank lists,
  * 1: 16-ary search trees, default), "walk_waves" (persistent waves of the first round, default
- * 8192), "spill_waves" (waves of a spill round at most, default 4096).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
- * _SEARCH / _WALK_WAVES / _SPILL_WAVES give the initial values at create.  EMQX_ENOTFOUND for unknown keys. */
+ * 8192), "spill_waves" (waves of a spill round at most, default 4096), "balance" (1: the
+ * work-sharing walk, default: waves out of tiles wait on tickets of a queue of shared pieces and
+ * busy waves share the bottom of their stacks, no rounds; 0: the spill rounds above),
+ * "queue_piece" (nodes per shared piece, 64..1M, default 256), "queue_check" (steps between a
+ * busy wave's looks at the waiting count, a power of 2 up to 1024, default 8), "queue_cap"
+ * (queue slots a call may use, 64..4M, default 4M; tests).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
+ * _SEARCH / _WALK_WAVES / _SPILL_WAVES / _BALANCE / _QUEUE_PIECE / _QUEUE_CHECK give the initial values at create.  EMQX_ENOTFOUND for unknown keys. */
 int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value);
 int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out);
 

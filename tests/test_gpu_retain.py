@@ -216,6 +216,7 @@ def test_spill_rounds_parity(mod, budget):
     idx.commit()
     filters = [rand_filter(rng) for _ in range(500)] + [b"#", b"+", b"+/#", b"w/+/x", b"+/+/x", b"w/+/+/z"]
     tt = RR.TokenTrie(names, expiry)
+    idx.set_tuning("balance", 0)  # the spill rounds (the default is the work-sharing walk)
     idx.set_tuning("step_budget", 0)
     ref = idx.match(filters, 100)
     st0 = idx.stats()
@@ -248,6 +249,7 @@ def test_spill_buffer_full_parity(mod):
     idx.commit()
     filters = [rand_filter(rng) for _ in range(300)] + [b"#", b"+/+", b"v/+/x", b"+/+/y/+", b"v/#"] * 8
     tt = RR.TokenTrie(names, [0] * len(names))
+    idx.set_tuning("balance", 0)
     idx.set_tuning("step_budget", 0)
     ref = idx.match(filters, 100)
     st0 = idx.stats()
@@ -261,6 +263,84 @@ def test_spill_buffer_full_parity(mod):
     assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
     for f, g, r in zip(filters, got, ref):
         assert g == r == tt.dispatch(f, 100), f
+
+
+def _sharing_case(seed):
+    rng = random.Random(seed)
+    names = sorted({rand_topic(rng) for _ in range(400)})
+    names += [b"w/%d/x" % i for i in range(6000)] + [b"w/%d/y/z" % i for i in range(0, 6000, 7)]
+    names += [b"q/%d/%d/e" % (i % 50, i) for i in range(4000)]
+    expiry = [rng.choice([0, 0, 0, 90, 100, 110]) for _ in names]
+    filters = [rand_filter(rng) for _ in range(500)]
+    filters += [b"#", b"+", b"+/#", b"w/+/x", b"+/+/x", b"w/+/+/z", b"q/+/+/e", b"+/+/+/e", b"q/+/#"] * 3
+    return names, expiry, filters
+
+
+@pytest.mark.parametrize("piece,check,shards", [(64, 1, 1), (64, 2, 4), (256, 8, 64), (1024, 64, 16)])
+def test_queue_sharing_parity(mod, piece, check, shards):
+    """The work-sharing walk (balance 1, the default): waves out of tiles wait on tickets of
+    their shard's queue of shared pieces, busy waves share the bottom of their stacks every
+    `check` steps while waves of their shard wait, in pieces of `piece` nodes.  Results, visit
+    and range counts equal the one-wave-per-tile walk with no budget (balance 0, step_budget 0);
+    the safety valve never fires."""
+    names, expiry, filters = _sharing_case(1300 + piece + check)
+    idx = mod.RetainIndex()
+    idx.store(names, expiry)
+    idx.commit()
+    tt = RR.TokenTrie(names, expiry)
+    idx.set_tuning("balance", 0)
+    idx.set_tuning("step_budget", 0)
+    ref = idx.match(filters, 100)
+    st0 = idx.stats()
+    idx.set_tuning("balance", 1)
+    idx.set_tuning("queue_piece", piece)
+    idx.set_tuning("queue_check", check)
+    idx.set_tuning("queue_shards", shards)
+    shared = 0
+    for tile in (10, 1, 64):
+        idx.set_tuning("tile", tile)
+        for _ in range(2):  # the queue is left all zero for the next call
+            got = idx.match(filters, 100)
+            st1 = idx.stats()
+            assert st1["queue_aborts"] == 0 and st1["last_spill_rounds"] == 0
+            assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
+            for f, g, r in zip(filters, got, ref):
+                assert g == r == tt.dispatch(f, 100), (f, tile)
+            shared += st1["last_shares"]
+    if check <= 2:
+        assert shared > 0
+    for key, bad in (("queue_check", 3), ("queue_piece", 63), ("balance", 2), ("queue_shards", 0)):
+        with pytest.raises(Exception):
+            idx.set_tuning(key, bad)
+
+
+def test_queue_full_parity(mod):
+    """A queue too small for what the waves share (emqx_retain_set_tuning "queue_cap"): a share
+    whose reservation does not fit is not made (the wave walks on), the tickets past the cap wait
+    for the walk's end.  Same results and counts; then a full-size queue again."""
+    names, expiry, filters = _sharing_case(1399)
+    idx = mod.RetainIndex()
+    idx.store(names, expiry)
+    idx.commit()
+    tt = RR.TokenTrie(names, expiry)
+    idx.set_tuning("balance", 0)
+    idx.set_tuning("step_budget", 0)
+    ref = idx.match(filters, 100)
+    st0 = idx.stats()
+    idx.set_tuning("balance", 1)
+    idx.set_tuning("queue_piece", 64)
+    idx.set_tuning("queue_check", 1)
+    idx.set_tuning("queue_shards", 4)
+    for cap in (64, 4 << 20):
+        idx.set_tuning("queue_cap", cap)
+        got = idx.match(filters, 100)
+        st1 = idx.stats()
+        assert st1["queue_aborts"] == 0
+        assert st1["last_visits"] == st0["last_visits"] and st1["last_ranges"] == st0["last_ranges"]
+        if cap == 64:
+            assert st1["last_spilled"] <= 64
+        for f, g, r in zip(filters, got, ref):
+            assert g == r == tt.dispatch(f, 100), (f, cap)
 
 
 @pytest.mark.parametrize("tile", [1, 5, 64])
