@@ -1498,13 +1498,16 @@ def retain_bench(args, rank, world, dev):
         "walk_balance": "spill rounds" if os.environ.get("EMQX_RETAIN_BALANCE") == "0" else "work-sharing queue",
         "walk_spill_rounds": int(st["last_spill_rounds"]), "walk_spilled_items": int(st["last_spilled"]),
         "walk_shares": int(st.get("last_shares", 0)), "walk_queue_aborts": int(st.get("queue_aborts", 0)),
-        "walk_step_budget": args.retain_budget if args.retain_budget is not None else "24, spill rounds 64 (default)",
+        "walk_step_budget": (args.retain_budget if args.retain_budget is not None else "24, spill rounds 64 (default)")
+        if os.environ.get("EMQX_RETAIN_BALANCE") == "0" else None,
         "walk_spill_full": int(st.get("last_spill_full", 0)),
         "walk_tile_filters": args.retain_tile if args.retain_tile is not None else 10,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": retain_traffic(nf, len(names))[0],
                      "traffic_source": retain_traffic(nf, len(names))[1],
-                     "kernel": "retain_walk_kernel (+ spill rounds) + retain_out_kernel<0,1> (whole call, one host sync)",
+                     "kernel": ("retain_walk_kernel (+ spill rounds)" if os.environ.get("EMQX_RETAIN_BALANCE") == "0"
+                                else "retain_walk_queue_kernel (work-sharing walk) + retain_queue_clear_kernel")
+                     + " + retain_out_kernel<0,1> (whole call, one host sync)",
                      "alg_bytes_per_launch": alg,
                      "alg_bytes_model": "len(F) + 32*L(F) + 32*visits + 48*ranges + 16*ids + 16 per filter"},
     }

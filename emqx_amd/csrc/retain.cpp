@@ -176,12 +176,13 @@ constexpr uint32_t SPILL_ROUNDS = 4;      // budgeted spill rounds per call, the
 // (retain_walk_queue_kernel).  A round lasts as long as its busiest wave; the queue has no rounds.
 enum : uint32_t { BALANCE_SPILL = 0, BALANCE_QUEUE = 1 };
 constexpr uint32_t QUEUE_CAP = 1u << 22;   // shared pieces per call at most (a full queue: waves keep walking)
-constexpr uint32_t QUEUE_PIECE = 256;      // nodes per shared piece (4 wave steps)
-constexpr uint32_t QUEUE_CHECK = 8;        // steps between a busy wave's looks at the waiting count
+constexpr uint32_t QUEUE_PIECE = 512;      // nodes per shared piece (8 wave steps)
+constexpr uint32_t QUEUE_CHECK = 4;        // steps between a busy wave's looks at the waiting count
 constexpr uint32_t QUEUE_POLL_LIMIT = 1u << 20;  // ~1 s of polls: then RC_QABORT, rerun in spill mode
-constexpr uint32_t QUEUE_MAX_WAIT = 2048;        // waves waiting on tickets at most
+constexpr uint32_t QUEUE_MAX_WAIT = 1u << 16;   // waves waiting on tickets at most (no cap: r4_q7)
 constexpr uint32_t QUEUE_SLEEP = 1;              // s_sleep(16) per poll
-constexpr uint32_t QUEUE_SHARDS = 64;            // queue shards (waves w % 64 share with each other)
+constexpr uint32_t QUEUE_SHARDS = 512;           // queue shards (waves w % 512 share with each other)
+constexpr uint32_t QUEUE_ROAM = 4;               // other shards a wave helps once its own is done
 
 // Filters per wave tile.  The walk is latency-bound (one dependent round trip per step), so the
 // number of waves in flight, not lane fill, sets its rate: 64 filters per tile leaves ~6 waves
@@ -230,7 +231,7 @@ struct emqx_retain {
   std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_decay{0}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
       walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP}, balance{BALANCE_QUEUE},
       queue_piece{QUEUE_PIECE}, queue_check{QUEUE_CHECK}, queue_cap{QUEUE_CAP}, queue_wait{QUEUE_MAX_WAIT},
-      queue_sleep{QUEUE_SLEEP}, queue_shards{QUEUE_SHARDS};
+      queue_sleep{QUEUE_SLEEP}, queue_shards{QUEUE_SHARDS}, queue_roam{QUEUE_ROAM};
 };
 
 namespace {
@@ -612,6 +613,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     w->spill_cap = SPILL_CAP;
   }
   a.wdesc = w->wdesc;
+  a.wdesc_n = need_d;
   a.spill_cap = std::min<uint32_t>(w->spill_cap, r->spill_cap.load());
   bool queue = r->balance.load() == BALANCE_QUEUE;
   if (queue && w->queue_cap == 0) {
@@ -630,6 +632,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   a.qpoll_limit = QUEUE_POLL_LIMIT;
   a.qmaxwait = r->queue_wait.load();
   a.qsleep = r->queue_sleep.load();
+  a.qroam = std::min<uint32_t>(r->queue_roam.load(), a.qshards - 1);
   a.ntiles = static_cast<uint32_t>(ntiles);
   const uint32_t budget = r->step_budget.load();
   a.step_budget = budget == 0 ? ~0u : budget;
@@ -789,6 +792,7 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   r->queue_wait = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_QUEUE_WAIT", QUEUE_MAX_WAIT));
   r->queue_sleep = std::min<uint32_t>(64, env_u32("EMQX_RETAIN_QUEUE_SLEEP", QUEUE_SLEEP));
   r->queue_shards = std::max<uint32_t>(1, std::min<uint32_t>(QS_MAX_SHARDS, env_u32("EMQX_RETAIN_QUEUE_SHARDS", QUEUE_SHARDS)));
+  r->queue_roam = std::min<uint32_t>(QS_MAX_SHARDS, env_u32("EMQX_RETAIN_QUEUE_ROAM", QUEUE_ROAM));
   r->prof_on = env_u32("EMQX_RETAIN_PROF", 0) != 0;
   r->ablate = env_u32("EMQX_RETAIN_ABLATE", 0);
   *out = r;
@@ -1044,6 +1048,9 @@ int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
   } else if (std::strcmp(key, "queue_shards") == 0) {
     if (v < 1 || v > QS_MAX_SHARDS) return EMQX_EINVAL;
     r->queue_shards = v;
+  } else if (std::strcmp(key, "queue_roam") == 0) {
+    if (v > QS_MAX_SHARDS) return EMQX_EINVAL;
+    r->queue_roam = v;
   } else if (std::strcmp(key, "queue_cap") == 0) {
     if (v < 64 || v > QUEUE_CAP) return EMQX_EINVAL;
     r->queue_cap = v;

@@ -162,13 +162,14 @@ constexpr uint32_t RC_MAX_ROUNDS = RC_WORDS - RC_SPILL - 2;  // budgeted spill r
 enum QCtrl : uint32_t {
   QS_HEAD = 0,   // tickets taken by waves waiting for shared work (slot = ticket)
   QS_TAIL = 1,   // slots reserved by waves sharing work (read with QS_HEAD as one u64)
-  QS_PEND = 2,   // units held (a tile being walked, or about to be taken) + pieces not yet walked
-  QS_TILES = 3,  // tile tickets taken (tile s + shards * ticket)
-  QS_DONE = 4,   // the shard's walk is over (set by the wave whose retire ended it)
+  QS_TILES = 2,  // tile tickets taken (tile s + shards * ticket)
+  QS_DONE = 3,   // the shard's walk is over (set by the wave whose retire ended it; read with
+                 // QS_TILES as one u64)
+  QS_PEND = 4,   // units held (a tile being walked, or about to be taken) + pieces not yet walked
   QS_FAIL = 5,   // ~(first slot of a reservation past the shard's end), atomicMax; 0: none
 };
 constexpr uint32_t QS_STRIDE = 1088;  // words between shards' control lines (4352 B)
-constexpr uint32_t QS_MAX_SHARDS = 256;
+constexpr uint32_t QS_MAX_SHARDS = 1024;
 
 struct RetainArgs {
   RetainView rv;
@@ -199,7 +200,9 @@ struct RetainArgs {
   uint32_t qpoll_limit;    // polls before a waiting wave gives up (RC_QABORT; a safety valve)
   uint32_t qmaxwait;       // waves waiting on tickets of one shard at most (more return)
   uint32_t qsleep;         // s_sleep(16) (1024 clocks) per poll of a waiting wave
+  uint32_t qroam;          // other shards a wave visits once its own shard's walk is over
   uint32_t ntiles;         // tiles of the call (queue mode's termination count)
+  uint64_t wdesc_n;        // entries of wdesc (foffs[n] - foffs[0] + 2n + 1)
   uint4* wdesc;            // [foffs[n] - foffs[0] + 2n] per-level step descriptors of the spill
                            // rounds, filter f's level l at foffs[f] - foffs[0] + 2f + l, levels
                            // 0..nlev: {word, end of the '+' run from l, the word after it

@@ -275,8 +275,28 @@ __device__ __forceinline__ void step_loads(const uint4* pa, const uint4* pb, con
   c = RPostKey{vc.x, vc.y, vc.z, vc.w};
 }
 
+// A step descriptor stored / loaded at agent scope (two 8-B halves): queue mode's tiles write
+// them and other waves of the same launch, on any XCD, read them.
+__device__ __forceinline__ void desc_store_sc(uint4* p, uint4 d) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+  __hip_atomic_store(q, static_cast<uint64_t>(d.x) | (static_cast<uint64_t>(d.y) << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, static_cast<uint64_t>(d.z) | (static_cast<uint64_t>(d.w) << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint4 desc_load_sc(const uint4* p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+  const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
+                    static_cast<uint32_t>(b >> 32));
+}
+
 // Tokenize filter f and intern its words (one lane): word ids to a.wids (at foffs[f] - foffs[0]
 // + f) and the step descriptors of the untiled walks to a.wdesc; returns nlev | wildcard << 31.
+// DESC: the step descriptors are stored (the spill rounds read them) or not (queue mode
+// publishes a filter's descriptors when it first shares one of its pieces: publish_desc).
+template <bool DESC>
 __device__ __forceinline__ uint32_t tokenize_filter(const RetainArgs& a, uint64_t f) {
   const RetainView& rv = a.rv;
   const uint64_t b0 = a.foffs[0];
@@ -315,20 +335,40 @@ __device__ __forceinline__ uint32_t tokenize_filter(const RetainArgs& a, uint64_
       ws = i + 1;
     }
   }
-  // the step descriptors of the untiled walks (RetainArgs.wdesc), last level first
-  uint4* dout = a.wdesc + (start - b0) + 2 * f;
   const uint32_t nw = nlev | (wild << 31);
-  dout[nlev] = make_uint4(WID_NONE, 0u, WID_HASH, nw);
-  uint32_t jn = nlev, wn = WID_HASH;  // the first non-'+' level above l, its word
+  if (DESC) {  // the step descriptors of the untiled walks (RetainArgs.wdesc), last level first
+    uint4* dout = a.wdesc + (start - b0) + 2 * f;
+    dout[nlev] = make_uint4(WID_NONE, 0u, WID_HASH, nw);
+    uint32_t jn = nlev, wn = WID_HASH;  // the first non-'+' level above l, its word
+    for (uint32_t l = nlev; l-- > 0;) {
+      const uint32_t wl = wout[l];
+      dout[l] = make_uint4(wl, jn, wn, nw);
+      if (wl != WID_PLUS) {
+        jn = l;
+        wn = wl;
+      }
+    }
+  }
+  return nw;
+}
+
+// Queue mode: filter f's step descriptors (as tokenize_filter's), stored at agent scope from its
+// word ids (written by this wave): other waves of the launch, on any XCD, read them.
+__device__ __forceinline__ void publish_desc(const RetainArgs& a, uint64_t f, uint32_t nw) {
+  const uint64_t b0 = a.foffs[0], start = a.foffs[f];
+  const uint32_t nlev = nw & 0x7FFFFFFFu;
+  const uint32_t* wids = a.wids + (start - b0) + f;
+  uint4* dout = a.wdesc + (start - b0) + 2 * f;
+  desc_store_sc(dout + nlev, make_uint4(WID_NONE, 0u, WID_HASH, nw));
+  uint32_t jn = nlev, wn = WID_HASH;
   for (uint32_t l = nlev; l-- > 0;) {
-    const uint32_t wl = wout[l];
-    dout[l] = make_uint4(wl, jn, wn, nw);
+    const uint32_t wl = wids[l];
+    desc_store_sc(dout + l, make_uint4(wl, jn, wn, nw));
     if (wl != WID_PLUS) {
       jn = l;
       wn = wl;
     }
   }
-  return nw;
 }
 
 // ---- work sharing (queue mode) --------------------------------------------------------------
@@ -338,6 +378,8 @@ __device__ __forceinline__ uint32_t tokenize_filter(const RetainArgs& a, uint64_
 // when a call starts (the host clears the slots below the previous call's ticket count).
 constexpr uint32_t QREADY = 1u << 30;  // in z, above any level
 constexpr uint32_t QEND = 0xFFFFFFFFu;  // y of the end marker: the walk is over
+constexpr uint32_t QNLEV_SHIFT = 16;  // a queued piece's z: level | nlev << 16 | QREADY | RITEM_POST
+constexpr uint32_t QDESC = 12;  // step descriptors of a piece's filter kept in LDS (levels 0..11; 7 blocks per CU)
 
 // The queue is sharded: wave w works in shard w % qshards, with its own tiles (t = s + S*j), its
 // own slots and its own control words (QS_*) on a line of their own, QS_STRIDE words from the
@@ -351,11 +393,12 @@ struct QShard {
   uint32_t ntiles;   // tiles of this shard
   uint32_t s;
 };
-__device__ __forceinline__ QShard qshard(const RetainArgs& a, uint32_t gw) {
-  const uint32_t S = a.qshards, s = gw % S, cap = a.queue_cap / S;
+__device__ __forceinline__ QShard qshard_at(const RetainArgs& a, uint32_t s) {
+  const uint32_t S = a.qshards, cap = a.queue_cap / S;
   return QShard{a.qctl + static_cast<uint64_t>(s) * QS_STRIDE, a.queue + static_cast<uint64_t>(s) * cap, cap,
                 a.ntiles > s ? (a.ntiles - s + S - 1) / S : 0u, s};
 }
+__device__ __forceinline__ QShard qshard(const RetainArgs& a, uint32_t gw) { return qshard_at(a, gw % a.qshards); }
 
 __device__ __forceinline__ void queue_put(uint4* q, uint4 it) {
   uint64_t* p = reinterpret_cast<uint64_t*>(q);
@@ -383,9 +426,13 @@ __device__ __forceinline__ bool queue_get(uint4* q, uint4* it) {
 // pieces of at most qpiece nodes.  The pending count is raised (and the raise performed) before
 // any piece can be seen, so the walk cannot look finished while a piece is queued.  A full queue:
 // nothing is shared (the wave keeps walking its stack).
+// TILE: items name lanes of the tile at fbase; a filter's descriptors are published with its first
+// shared piece (pub: the tile's lanes already published).  Else the wave walks one piece's filter,
+// of `pnw` (nlev | wildcard flag), whose descriptors are out already.
 template <bool TILE>
 __device__ __forceinline__ void share_work(const RetainArgs& a, const QShard& qs, uint4* ls, uint32_t& top, uint4* stk,
-                                           uint32_t& gtop, uint64_t fbase, uint32_t& npieces) {
+                                           uint32_t& gtop, uint64_t fbase, uint32_t& npieces, const uint32_t* nlevs,
+                                           uint64_t* pub, uint32_t pnw) {
   const uint32_t lane = lane_id();
   const uint32_t QP = a.qpiece;
   uint32_t kind, nd;  // 0: stk[0, nd)  1: ls[0, nd)  2: ls[0] beyond its first QP nodes
@@ -418,6 +465,12 @@ __device__ __forceinline__ void share_work(const RetainArgs& a, const QShard& qs
     (void)wave_excl(np, &t);
     ptot += t;
   }
+  if (TILE && !*pub) {
+    // the tile's first share publishes every filter's descriptors, a lane each (before the
+    // pieces: the waitcnt below covers these stores too)
+    if (nlevs[lane] != 0xFFFFFFFFu) publish_desc(a, fbase + lane, nlevs[lane]);
+    *pub = 1;
+  }
   uint32_t base = 0, ok = 0;
   if (lane == 0) {
     base = atomicAdd(&qs.c[QS_TAIL], ptot);
@@ -439,7 +492,9 @@ __device__ __forceinline__ void share_work(const RetainArgs& a, const QShard& qs
     const uint32_t np = i < nd ? (it.y + QP - 1) / QP : 0u;
     uint32_t ctot;
     const uint32_t off = wave_excl(np, &ctot);
+    const uint32_t nlev = (TILE ? nlevs[it.w & 63] : pnw) & 0x7FFFFFFFu;
     if (TILE) it.w += static_cast<uint32_t>(fbase);
+    it.z |= min(nlev, (QREADY >> QNLEV_SHIFT) - 1u) << QNLEV_SHIFT;
     for (uint32_t k = 0; k < np; ++k) {
       uint4 pc = it;
       pc.x = it.x + QP * k;
@@ -472,7 +527,8 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
                                            const uint32_t* lwords,
                                            uint32_t* pref, uint4* itm, uint32_t& visits, bool& overflow,
                                            RangeRes& res, uint64_t* pacc, const QShard* qs = nullptr,
-                                           uint32_t* qstat = nullptr) {
+                                           uint32_t* qstat = nullptr, const uint4* ldesc = nullptr,
+                                           uint32_t ldn = 0, uint64_t* pub = nullptr, uint32_t pnw = 0) {
   const uint32_t lane = lane_id();
   const RetainView& rv = a.rv;
   const uint64_t b0 = a.foffs[0];
@@ -595,8 +651,12 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
       } else {
         // a spill round: the level's descriptor, written by the first round, holds the word,
         // the '+' run's end and the word after it (one load, not a chain of word loads)
+        // (queue mode: a piece's walk is one filter's, its first levels' descriptors in LDS,
+        // deeper ones read at agent scope: its tile's wave wrote them in this launch)
         fg = fl;
-        const uint4 d = a.wdesc[(a.foffs[fg] - b0) + 2 * fg + lev];
+        const uint4 d = !QUEUE         ? a.wdesc[(a.foffs[fg] - b0) + 2 * fg + lev]
+                        : lev < ldn    ? ldesc[lev]
+                                       : desc_load_sc(a.wdesc + (a.foffs[fg] - b0) + 2 * fg + lev);
         nl = d.w;
         fn = nl & 0x7FFFFFFFu;
         w_cur = d.x;
@@ -800,7 +860,7 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
           static_cast<int32_t>(static_cast<uint32_t>(ht) - static_cast<uint32_t>(ht >> 32)) > 0 ? 1u : 0u;
       if (__shfl(hungry, 0, 64)) {
         const uint64_t ts = RPROF_NOW();
-        share_work<TILE>(a, *qs, ls, top, stk, gtop, fbase, qstat[0]);
+        share_work<TILE>(a, *qs, ls, top, stk, gtop, fbase, qstat[0], nlevs, pub, pnw);
         ++qstat[1];
         RPROF_ADD(11, RPROF_NOW() - ts);
       }
@@ -839,7 +899,7 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
     const uint64_t f = t * tf + lane;
     const bool valid = lane < tf && f < a.n;
     // ---- tokenize + intern (per lane) -------------------------------------------------
-    const uint32_t nw = valid ? tokenize_filter(a, f) : 0u;
+    const uint32_t nw = valid ? tokenize_filter<true>(a, f) : 0u;
     const uint32_t nlev = nw & 0x7FFFFFFFu;
     nlevs[lane] = nw;
     // the tile's words into LDS when they fit (the walk reads one or two per node visit)
@@ -957,14 +1017,6 @@ __device__ __forceinline__ void retire_unit(const QShard& qs) {
   for (uint32_t k = lo + lane; k < hi; k += 64) queue_put(qs.q + k, make_uint4(0u, QEND, 0u, 0u));
 }
 
-// Queue mode, first kernel: every filter tokenized and interned (one lane each), so the walk's
-// waves can take any filter's pieces: the word ids and step descriptors are written by a launch
-// that has finished, not by another wave of the same one.
-__global__ __launch_bounds__(256) void retain_tokenize_kernel(RetainArgs a) {
-  const uint64_t f = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (f < a.n) (void)tokenize_filter(a, f);
-}
-
 // Queue mode, the walk.  Wave w works in shard s = w % qshards: it takes the shard's tiles by
 // ticket (QS_TILES), then its shared pieces by ticket (QS_HEAD; a ticket names a slot).  Busy
 // waves share when waves of their shard wait (share_work).  QS_PEND counts the units held or
@@ -974,8 +1026,12 @@ __global__ __launch_bounds__(256) void retain_tokenize_kernel(RetainArgs a) {
 // holds work only after it started, so waves not yet resident hold nothing and the grid drains;
 // a waiting wave also gives up after qpoll_limit polls (RC_QABORT; the host reruns the call in
 // spill mode), a safety valve that a correct walk never reaches.
+// compiled for 4 waves per SIMD (<= 128 VGPRs): 16 resident waves per CU instead of 12
+#ifndef QW_OCC
+#define QW_OCC 4
+#endif
 template <int SEARCH>
-__global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_queue_kernel(RetainArgs a) {
+__global__ __launch_bounds__(RW_WAVES * 64, QW_OCC) void retain_walk_queue_kernel(RetainArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * RW_WAVES + wib;
@@ -985,6 +1041,7 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_queue_kerne
   __shared__ uint64_t s_wb[RW_WAVES][64];
   __shared__ uint4 s_stk[RW_WAVES][RSTK];
   __shared__ uint32_t s_words[RW_WAVES][RWORDS];
+  __shared__ uint4 s_desc[RW_WAVES][QDESC];
   uint32_t* nlevs = s_nlev[wib];
   uint64_t* wbase = s_wb[wib];
   uint4* stk = a.stack + static_cast<uint64_t>(gw) * a.stack_cap;
@@ -1017,11 +1074,11 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_queue_kerne
     uint32_t nw = 0;
     uint64_t wsrc = 0;
     if (valid) {
+      nw = tokenize_filter<false>(a, f);  // descriptors: published with the filter's first piece
       wsrc = (a.foffs[f] - b0) + f;
-      nw = a.wdesc[wsrc + f].w;  // level 0's descriptor (foffs[f] - b0 + 2f)
     }
     const uint32_t nlev = nw & 0x7FFFFFFFu;
-    nlevs[lane] = nw;
+    nlevs[lane] = valid ? nw : 0xFFFFFFFFu;  // (no filter: share_work publishes nothing for it)
     uint32_t wtot;
     const uint32_t wofs = wave_excl(valid ? nlev : 0u, &wtot);
     const bool lds_words = wtot <= RWORDS;
@@ -1034,54 +1091,68 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_queue_kerne
     if (push0) s_stk[wib][ppos] = make_uint4(0u, 1u, 0u, lane);
     __builtin_amdgcn_wave_barrier();
     uint64_t t0 = RPROF_NOW();
+    uint64_t pub = 0;  // tile lanes whose step descriptors are published (share_work)
     walk_stack<true, SEARCH, true>(a, s_stk[wib], ptot, stk, 0, static_cast<uint64_t>(t) * tf, nlevs, wbase,
                                    lds_words ? s_words[wib] : nullptr, s_pref[wib], s_item[wib], visits, overflow,
-                                   res, pacc, &qs, qstat);
+                                   res, pacc, &qs, qstat, nullptr, 0, &pub);
     uint64_t t1 = RPROF_NOW();
     RPROF_ADD(13, t1 - t0);
     retire_unit(qs);  // this tile is walked (or abandoned)
     RPROF_ADD(10, RPROF_NOW() - t1);
     if (overflow) break;
   }
-  // ---- the shard's shared pieces --------------------------------------------------------------
+  // ---- shared pieces: the home shard's, then (roaming) other shards' ------------------------
   // At most `maxwait` waves of a shard wait at once: a wave that finds that many tickets beyond
-  // the reserved slots returns instead of taking one.  Safe: a shared piece's slot is below the
+  // the reserved slots moves on instead of taking one.  Safe: a shared piece's slot is below the
   // reserved count, so either its ticket is taken already or fewer than maxwait wait and the next
   // wave to come (at the latest the one that shared it, once its own stack is empty) takes one.
-  uint32_t polls = 0;
+  // A wave whose shard's walk is over visits up to qroam other shards (an odd stride over the
+  // ring, so each visit is a new one) and helps the ones still walking: the shards' work is
+  // uneven (a few broad filters), and the launch lasts as long as its slowest shard.
+  uint32_t polls = 0, hops = 0;
+  const uint32_t stride = 2u * ((gw / a.qshards) % max(1u, a.qshards / 2)) + 1u;
+  QShard cur = qs;
   while (!overflow) {
-    uint32_t k = 0, state = 0;  // 1: a piece, 2: the walk is over (or enough waves wait)
+    uint32_t k = 0, state = 0;  // 1: a piece, 2: this shard's walk is over (or enough waves wait)
     uint64_t tq = RPROF_NOW();
     if (lane == 0) {
-      const uint64_t ht = __hip_atomic_load(reinterpret_cast<const uint64_t*>(qs.c + QS_HEAD), __ATOMIC_RELAXED,
+      // a shard is worth waiting in if its walk is not over and one of its own waves has
+      // started: that wave takes all its tiles in turn, so the shard ends.  (A shard none of
+      // whose waves is resident yet must not collect waiting visitors: they would hold the slots
+      // its waves need.)
+      const uint64_t td = __hip_atomic_load(reinterpret_cast<const uint64_t*>(cur.c + QS_TILES), __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
-      if (static_cast<int32_t>(static_cast<uint32_t>(ht) - static_cast<uint32_t>(ht >> 32)) >=
-          static_cast<int32_t>(maxwait))
+      if ((td >> 32) != 0 || static_cast<uint32_t>(td) == 0) {
         state = 2;
-      else
-        k = atomicAdd(&qs.c[QS_HEAD], 1u);
+      } else {
+        const uint64_t ht = __hip_atomic_load(reinterpret_cast<const uint64_t*>(cur.c + QS_HEAD), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        if (static_cast<int32_t>(static_cast<uint32_t>(ht) - static_cast<uint32_t>(ht >> 32)) >=
+            static_cast<int32_t>(maxwait))
+          state = 2;
+        else
+          k = atomicAdd(&cur.c[QS_HEAD], 1u);
+      }
     }
     state = __shfl(state, 0, 64);
-    if (state == 2) {
-      RPROF_ADD(15, 1);
-      break;
-    }
     k = __shfl(k, 0, 64);
     uint4 it = make_uint4(0, 0, 0, 0);
-    if (lane == 0 && __hip_atomic_load(&qs.c[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) state = 2;
-    state = __shfl(state, 0, 64);
+    if (state == 0) {
+      if (lane == 0 && __hip_atomic_load(&cur.c[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) state = 2;
+      state = __shfl(state, 0, 64);
+    }
     const uint64_t tw = RPROF_NOW();
     RPROF_ADD(9, tw - tq);
-    for (;;) {
-      if (lane == 0 && state == 0) {
-        if (k < qs.cap) {
-          if (queue_get(qs.q + k, &it)) state = it.y == QEND ? 2u : 1u;
-        } else if (__hip_atomic_load(&qs.c[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    while (state == 0) {
+      if (lane == 0) {
+        if (k < cur.cap) {
+          if (queue_get(cur.q + k, &it)) state = it.y == QEND ? 2u : 1u;
+        } else if (__hip_atomic_load(&cur.c[QS_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           state = 2;
         }
         if (state == 0 && ++polls > a.qpoll_limit) {
           atomicOr(&a.ctrl[RC_QABORT], 1u);
-          state = 2;
+          state = 3;  // give up entirely
         }
       }
       state = __shfl(state, 0, 64);
@@ -1090,15 +1161,32 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_queue_kerne
     }
     const uint64_t tp = RPROF_NOW();
     RPROF_ADD(8, tp - tw);
-    if (state == 2) break;
+    if (state == 3) break;
+    if (state == 2) {
+      if (hops++ >= a.qroam) {
+        RPROF_ADD(15, 1);
+        break;
+      }
+      cur = qshard_at(a, (cur.s + stride) % a.qshards);
+      continue;
+    }
     RPROF_ADD(12, 1);
-    if (lane == 0) s_stk[wib][0] = it;
+    // the piece: its level, its filter's level count (carried in z), and the filter's step
+    // descriptors from the piece's level down (one round trip; the walk only goes deeper and
+    // stays inside this filter) into LDS
+    const uint32_t pz = __shfl(it.z, 0, 64), pw = __shfl(it.w, 0, 64);
+    const uint32_t lev0 = pz & ((1u << QNLEV_SHIFT) - 1u), pnlev = (pz & ~RITEM_POST) >> QNLEV_SHIFT;
+    if (lane == 0) s_stk[wib][0] = make_uint4(it.x, it.y, lev0 | (pz & RITEM_POST), pw);
+    const uint64_t dbase = (a.foffs[pw] - b0) + 2ull * pw;
+    const uint32_t ldn = min(QDESC, pnlev + 1u);
+    if (lane >= lev0 && lane < ldn) s_desc[wib][lane] = desc_load_sc(a.wdesc + dbase + lane);
     __builtin_amdgcn_wave_barrier();
     walk_stack<false, SEARCH, true>(a, s_stk[wib], 1, stk, 0, 0, nullptr, nullptr, nullptr, s_pref[wib],
-                                    s_item[wib], visits, overflow, res, pacc, &qs, qstat);
+                                    s_item[wib], visits, overflow, res, pacc, &cur, qstat, s_desc[wib], ldn, nullptr,
+                                    pnlev);
     const uint64_t te = RPROF_NOW();
     RPROF_ADD(14, te - tp);
-    retire_unit(qs);
+    retire_unit(cur);
     RPROF_ADD(10, RPROF_NOW() - te);
   }
   if (overflow && lane == 0) atomicOr(&a.ctrl[RC_STACK], 1u);
@@ -1333,7 +1421,6 @@ hipError_t launch_retain_walk(const RetainArgs& a, hipStream_t s) {
 
 hipError_t launch_retain_walk_queue(const RetainArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(retain_tokenize_kernel, dim3(static_cast<uint32_t>((a.n + 255) / 256)), dim3(256), 0, s, a);
   const uint32_t blocks = (a.waves + RW_WAVES - 1) / RW_WAVES;
   if (a.search == RSEARCH_STREE)
     hipLaunchKernelGGL(retain_walk_queue_kernel<RSEARCH_STREE>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);

@@ -276,13 +276,14 @@ def _sharing_case(seed):
     return names, expiry, filters
 
 
-@pytest.mark.parametrize("piece,check,shards", [(64, 1, 1), (64, 2, 4), (256, 8, 64), (1024, 64, 16)])
-def test_queue_sharing_parity(mod, piece, check, shards):
+@pytest.mark.parametrize("piece,check,shards,roam", [(64, 1, 1, 0), (64, 2, 4, 3), (256, 8, 64, 8), (1024, 64, 16, 15),
+                                                     (512, 4, 64, 0)])
+def test_queue_sharing_parity(mod, piece, check, shards, roam):
     """The work-sharing walk (balance 1, the default): waves out of tiles wait on tickets of
     their shard's queue of shared pieces, busy waves share the bottom of their stacks every
     `check` steps while waves of their shard wait, in pieces of `piece` nodes.  Results, visit
     and range counts equal the one-wave-per-tile walk with no budget (balance 0, step_budget 0);
-    the safety valve never fires."""
+    the safety valve never fires.  Waves whose shard is done help `roam` other shards."""
     names, expiry, filters = _sharing_case(1300 + piece + check)
     idx = mod.RetainIndex()
     idx.store(names, expiry)
@@ -296,6 +297,7 @@ def test_queue_sharing_parity(mod, piece, check, shards):
     idx.set_tuning("queue_piece", piece)
     idx.set_tuning("queue_check", check)
     idx.set_tuning("queue_shards", shards)
+    idx.set_tuning("queue_roam", roam)
     shared = 0
     for tile in (10, 1, 64):
         idx.set_tuning("tile", tile)

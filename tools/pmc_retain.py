@@ -32,7 +32,7 @@ def main():
                     v = float(r["Counter_Value"]) * 1024  # KiB
                     tot += v
                     per_kernel[name.split("(")[0]] += v
-                    if "retain_walk_kernel" in name:
+                    if "retain_walk_kernel" in name or "retain_walk_queue_kernel" in name:
                         walks.add((p, r["Dispatch_Id"]))
         if walks:
             res[counter] = {"bytes_per_call": tot / len(walks), "calls": len(walks),

@@ -4,9 +4,9 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4_q7}
 mkdir -p $OUT
-B="balance=1,queue_check=8,queue_wait=65536,queue_piece=256,queue_sleep=1,queue_shards=64"
-timeout -k 10 400 python -u tools/retain_sweep.py 'balance=0' "$B" "${B/piece=256/piece=512}" "${B/piece=256/piece=1024}" "${B/piece=256/piece=512},queue_sleep=4" \
-  "${B/piece=256/piece=512},queue_check=4" 'balance=0' "$B" "${B/piece=256/piece=512}" > $OUT/sweep.jsonl 2> $OUT/sweep.err || { tail -20 $OUT/sweep.err; exit 1; }
+B="balance=1,queue_check=4,queue_wait=65536,queue_piece=512,queue_sleep=1,queue_shards=64,queue_roam=8"
+timeout -k 10 400 python -u tools/retain_sweep.py 'balance=0' "$B" "${B/roam=8/roam=0}" "${B/roam=8/roam=2}" "${B/roam=8/roam=24}" "${B/roam=8/roam=63}" \
+  "${B/shards=64/shards=128}" "${B/shards=64/shards=32}" "${B/piece=512/piece=256}" 'balance=0' "$B" > $OUT/sweep.jsonl 2> $OUT/sweep.err || { tail -20 $OUT/sweep.err; exit 1; }
 cat $OUT/sweep.jsonl
 ROOT=$(pwd)
 cd /tmp
@@ -17,6 +17,6 @@ python3 - "$f" <<'PY'
 import csv,sys
 for r in csv.DictReader(open(sys.argv[1])):
     n=r['Name']
-    if 'retain' not in n and 'scan' not in n: continue
+    if 'retain' not in n and 'scan' not in n and 'fill' not in n: continue
     print("%-60s %5s %10.1f us avg %10.1f min %10.1f max" % (n[:60], r['Calls'], float(r['AverageNs'])/1e3, float(r['MinNs'])/1e3, float(r['MaxNs'])/1e3))
 PY
