@@ -1501,7 +1501,8 @@ def retain_bench(args, rank, world, dev):
         "walk_step_budget": (args.retain_budget if args.retain_budget is not None else "24, spill rounds 64 (default)")
         if os.environ.get("EMQX_RETAIN_BALANCE") == "0" else None,
         "walk_spill_full": int(st.get("last_spill_full", 0)),
-        "walk_tile_filters": args.retain_tile if args.retain_tile is not None else 10,
+        "walk_tile_filters": args.retain_tile if args.retain_tile is not None
+        else (10 if os.environ.get("EMQX_RETAIN_BALANCE") == "0" else 16),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": retain_traffic(nf, len(names))[0],
                      "traffic_source": retain_traffic(nf, len(names))[1],

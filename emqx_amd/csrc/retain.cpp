@@ -188,8 +188,10 @@ constexpr uint32_t QUEUE_ROAM = 4;               // other shards a wave helps on
 // number of waves in flight, not lane fill, sets its rate: 64 filters per tile leaves ~6 waves
 // per CU for a 100K-filter batch.  With tiles taken first come first served, 10 (10K tiles over
 // 8192 waves) runs the config-R walk + spill in 1.96-1.99 ms against 2.23-2.25 ms for 8
-// (profiles/r2_retain_sweeps.txt).
+// (profiles/r2_retain_sweeps.txt).  The work-sharing walk: 16 (1.055 ms per call against 1.16
+// for 10, 1.10 for 14, 1.19 for 20; profiles/r4_retain_queue_sweep.txt, r4_q24/q25).
 constexpr uint32_t TILE_FILTERS = 10;
+constexpr uint32_t QUEUE_TILE_FILTERS = 16;
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* e = std::getenv(name);
@@ -228,7 +230,8 @@ struct emqx_retain {
   // walk tuning (emqx_retain_set_tuning; the EMQX_RETAIN_* variables give the initial values)
   bool prof_on = false;
   uint32_t ablate = 0;  // EMQX_RETAIN_ABLATE (profiling builds only)  // EMQX_RETAIN_PROF=1 (a RETAIN_PROF build fills the phase counters)
-  std::atomic<uint32_t> tile{TILE_FILTERS}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_decay{0}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
+  // tile 0: the balance mode's default
+  std::atomic<uint32_t> tile{0}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_decay{0}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
       walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP}, balance{BALANCE_QUEUE},
       queue_piece{QUEUE_PIECE}, queue_check{QUEUE_CHECK}, queue_cap{QUEUE_CAP}, queue_wait{QUEUE_MAX_WAIT},
       queue_sleep{QUEUE_SLEEP}, queue_shards{QUEUE_SHARDS}, queue_roam{QUEUE_ROAM};
@@ -598,7 +601,9 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     RT_TRY(ralloc(w->rlive, 5 * rc));
     w->range_cap = static_cast<uint32_t>(rc);
   }
-  a.tile_filters = std::max<uint32_t>(1, std::min<uint32_t>(64, r->tile.load()));
+  bool queue = r->balance.load() == BALANCE_QUEUE;
+  const uint32_t tile = r->tile.load();
+  a.tile_filters = tile ? std::min<uint32_t>(64, tile) : queue ? QUEUE_TILE_FILTERS : TILE_FILTERS;
   a.search = r->search.load();
   const uint64_t ntiles = (n + a.tile_filters - 1) / a.tile_filters;
   const uint32_t spill_waves = std::max<uint32_t>(64, r->spill_waves.load());
@@ -615,7 +620,6 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   a.wdesc = w->wdesc;
   a.wdesc_n = need_d;
   a.spill_cap = std::min<uint32_t>(w->spill_cap, r->spill_cap.load());
-  bool queue = r->balance.load() == BALANCE_QUEUE;
   if (queue && w->queue_cap == 0) {
     RT_TRY(ralloc(w->queue, QUEUE_CAP));
     RT_TRY(hipMemsetAsync(w->queue, 0, static_cast<uint64_t>(QUEUE_CAP) * sizeof(uint4), s));
@@ -774,7 +778,7 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   emqx_retain* r = new (std::nothrow) emqx_retain();
   if (!r) return EMQX_ENOMEM;
   r->device = device;
-  r->tile = std::max<uint32_t>(1, std::min<uint32_t>(64, env_u32("EMQX_RETAIN_TILE", TILE_FILTERS)));
+  r->tile = std::min<uint32_t>(64, env_u32("EMQX_RETAIN_TILE", 0));  // 0: the mode's default
   r->step_budget = env_u32("EMQX_RETAIN_STEP_BUDGET", STEP_BUDGET);
   r->spill_budget = env_u32("EMQX_RETAIN_SPILL_BUDGET", SPILL_BUDGET);
   r->spill_decay = std::min<uint32_t>(4, env_u32("EMQX_RETAIN_SPILL_DECAY", 0));

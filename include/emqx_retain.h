@@ -107,7 +107,8 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes
                                    uint64_t* n_out, void* stream);
 
 /* Walk tuning (experiments and tests; results never depend on it).  Keys: "tile" (filters
- * per wave tile of the first round, 1..64, default 10), "step_budget" (wave steps before a
+ * per wave tile of the first round, 1..64, default 16 with the work-sharing walk, 10 with the
+ * spill rounds), "step_budget" (wave steps before a
  * stack spills to the next round, 0 = never, default 24), "spill_budget" (the same for the
  * budgeted spill rounds, 0 = step_budget, default 64), "spill_per_wave" (spilled pieces
  * per wave of a round, default 4), "spill_rounds" (budgeted rounds per call, then one without
