@@ -567,7 +567,10 @@ void plain_batch_shard(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs,
   const bool bulk = s->bulk;
   uint32_t* const shared = s->plain.data();
   const uint64_t nrec = s->recs.size();
-  constexpr uint64_t AHEAD = 8;
+  // two-stage prefetch: 16 ops ahead the op's map entry, record and per-filter flags (each its
+  // own random line); 4 ahead, from the record fetched by then, the list word it will write
+  // (add) or move (remove)
+  constexpr uint64_t AHEAD = 16, AHEAD2 = 4;
   for (uint64_t j = 0; j < cnt; ++j) {
     if (j + AHEAD < cnt) {
       const uint64_t q2 = idx[j + AHEAD];
@@ -575,6 +578,17 @@ void plain_batch_shard(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs,
       if (f2 < nrec) {
         s->plain_pos[pp_shard(f2)].prefetch((uint64_t(f2) << 32) | subs[q2]);
         __builtin_prefetch(&s->recs[f2], 1);
+        __builtin_prefetch(&s->pcap[f2], 1);
+        __builtin_prefetch(&s->plocal[f2], 1);
+        __builtin_prefetch(&s->rec_flag[f2], 1);
+      }
+    }
+    if (j + AHEAD2 < cnt) {
+      const uint32_t f3 = fs[idx[j + AHEAD2]];
+      if (f3 < nrec && !s->plocal[f3]) {
+        const FilterRec& r3 = s->recs[f3];
+        const uint64_t w3 = uint64_t(r3.plain_begin) + r3.n_plain - (add || r3.n_plain == 0 ? 0u : 1u);
+        if (w3 < s->plain.size()) __builtin_prefetch(shared + w3, 1);
       }
     }
     const uint64_t q = idx[j];
@@ -650,7 +664,8 @@ void plain_batch(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, uint6
     for (uint32_t k; (k = next.fetch_add(1)) < PP_SHARDS;)
       plain_batch_shard(s, fs, subs, idx.data() + start[k], start[k + 1] - start[k], add, loc[k]);
   };
-  WorkPool::get().run(work, std::min<unsigned>(par_threads(), static_cast<unsigned>((n + PAR_MIN / 4 - 1) / (PAR_MIN / 4))));
+  // every thread (the ops are cache misses, not compute: more threads, more misses in flight)
+  WorkPool::get().run(work, par_threads());
   // merge, shard by shard: moved lists appended to the shared arena
   for (PlainLocal& L : loc) {
     if (!L.arena.empty()) {
@@ -806,8 +821,27 @@ int full_commit(emqx_subtab* s) {
 // Incremental commit: member lists and group lists of the changed slots / filters are
 // rewritten in the image (moved to the arena's end when they outgrow their extent); then the
 // touched words and records go to the device.
+// EMQX_SUBTAB_PROF=1: per add/remove call and per commit, where the host time goes, on stderr
+// (experiments)
+static bool subtab_prof() {
+  static const bool on = [] {
+    const char* e = std::getenv("EMQX_SUBTAB_PROF");
+    return e && *e == '1';
+  }();
+  return on;
+}
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   const auto t0 = std::chrono::steady_clock::now();
+  double pt[8] = {};
+  int np = 0;
+  auto mark = [&] {
+    if (subtab_prof() && np < 8) pt[np++] = now_us();
+  };
+  mark();
   std::vector<std::pair<uint64_t, uint64_t>> member_ranges;
   std::vector<uint64_t> group_idx;
   for (uint32_t sl : s->dirty_slots) {
@@ -860,6 +894,7 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   }
   if (s->plain.size() >= (1ull << 32) || s->members.size() >= (1ull << 32) || s->groups.size() >= (1ull << 32))
     return EMQX_ENOMEM;
+  mark();  // 1: slots and group lists
 
   // ---- patches ----
   s->wpatch.clear();
@@ -926,12 +961,14 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
     words(s->dirty_plain, s->plain, copies_plain);
   }
   const uint64_t n_plain_w = s->wpatch.size();
+  mark();  // 2: plain words
   words(member_ranges, s->members, copies_members);
   const uint64_t n_member_w = s->wpatch.size() - n_plain_w;
   std::sort(s->dirty_alive.begin(), s->dirty_alive.end());
   s->dirty_alive.erase(std::unique(s->dirty_alive.begin(), s->dirty_alive.end()), s->dirty_alive.end());
   for (uint32_t w : s->dirty_alive) s->wpatch.push_back(WordPatch{w, 0u, s->alive[w], 0});
   const uint64_t n_alive_w = s->dirty_alive.size();
+  mark();  // 3: member and alive words
   std::sort(group_idx.begin(), group_idx.end());
   group_idx.erase(std::unique(group_idx.begin(), group_idx.end()), group_idx.end());
   for (uint64_t gi : group_idx) {
@@ -939,6 +976,7 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
     s->rpatch.push_back(RecPatch{static_cast<uint32_t>(gi), {0, 0, 0}, make_uint4(g.member_begin, g.n_members, g.slot, g.group_id)});
   }
   const uint64_t n_group_p = s->rpatch.size();
+  mark();  // 4: group records
   {  // two-stage prefetch: the record 16 ahead, its plain list (inline candidates) 8 ahead;
      // a long list on the pool, a slice per thread
     const std::vector<uint32_t>& dr = s->dirty_recs;
@@ -970,6 +1008,7 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   }
   const uint64_t n_rec_p = s->rpatch.size() - n_group_p;
   const auto t1 = std::chrono::steady_clock::now();
+  mark();  // 5: filter records
 
   // ---- device: after the fan-outs in flight, before the next ones ----
   // Everything the device reads comes from pinned staging (a snapshot of the image taken here),
@@ -1027,6 +1066,13 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   s->st_records += n_group_p + n_rec_p;
   s->st_host_us = std::chrono::duration<double, std::micro>(t1 - t0).count();
   s->st_last_kind = 1;
+  mark();  // 6: staging and uploads
+  if (subtab_prof() && np == 7)
+    std::fprintf(stderr,
+                 "SUBTAB_PROF commit slots_us %.1f plain_us %.1f members_alive_us %.1f groups_us %.1f recs_us %.1f "
+                 "upload_us %.1f alive %llu slots_recs %llu\n",
+                 pt[1] - pt[0], pt[2] - pt[1], pt[3] - pt[2], pt[4] - pt[3], pt[5] - pt[4], pt[6] - pt[5],
+                 (unsigned long long)n_alive_w, (unsigned long long)n_rec_p);
   return EMQX_OK;
 }
 
@@ -1654,8 +1700,20 @@ int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* 
   if (!s || !ids_ok(filter_ids, sub_ids, n)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
   std::vector<uint32_t> rest;
+  const double t0 = subtab_prof() ? now_us() : 0;
   const bool split = plain_parallel(s, filter_ids, sub_ids, group_ids, n, true, &rest);
+  const double t1 = subtab_prof() ? now_us() : 0;
   const uint64_t nl = split ? rest.size() : n;
+  struct Report {
+    double t0, t1;
+    uint64_t n, nl;
+    const char* what;
+    ~Report() {
+      if (subtab_prof())
+        std::fprintf(stderr, "SUBTAB_PROF %s n %llu plain_us %.1f serial %llu serial_us %.1f\n", what,
+                     (unsigned long long)n, t1 - t0, (unsigned long long)nl, now_us() - t1);
+    }
+  } report{t0, t1, n, nl, "add"};
   for (uint64_t j = 0; j < nl; ++j) {
     prefetch_op(s, filter_ids, sub_ids, group_ids, split ? rest.data() : nullptr, j, nl);
     const uint64_t i = split ? rest[j] : j;
@@ -1691,8 +1749,20 @@ int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_
   if (!s || !ids_ok(filter_ids, sub_ids, n)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
   std::vector<uint32_t> rest;
+  const double t0 = subtab_prof() ? now_us() : 0;
   const bool split = plain_parallel(s, filter_ids, sub_ids, group_ids, n, false, &rest);
+  const double t1 = subtab_prof() ? now_us() : 0;
   const uint64_t nl = split ? rest.size() : n;
+  struct Report {
+    double t0, t1;
+    uint64_t n, nl;
+    const char* what;
+    ~Report() {
+      if (subtab_prof())
+        std::fprintf(stderr, "SUBTAB_PROF %s n %llu plain_us %.1f serial %llu serial_us %.1f\n", what,
+                     (unsigned long long)n, t1 - t0, (unsigned long long)nl, now_us() - t1);
+    }
+  } report{t0, t1, n, nl, "remove"};
   for (uint64_t j = 0; j < nl; ++j) {
     prefetch_op(s, filter_ids, sub_ids, group_ids, split ? rest.data() : nullptr, j, nl);
     const uint64_t i = split ? rest[j] : j;
