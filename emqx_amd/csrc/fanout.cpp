@@ -844,7 +844,17 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   mark();
   std::vector<std::pair<uint64_t, uint64_t>> member_ranges;
   std::vector<uint64_t> group_idx;
-  for (uint32_t sl : s->dirty_slots) {
+  const std::vector<uint32_t>& ds = s->dirty_slots;
+  for (size_t di = 0; di < ds.size(); ++di) {
+    // the slot 8 ahead, its member list, image extent and filter record 4 ahead (random lines)
+    if (di + 8 < ds.size()) __builtin_prefetch(&s->slots[ds[di + 8]], 1);
+    if (di + 4 < ds.size()) {
+      const Slot& S4 = s->slots[ds[di + 4]];
+      __builtin_prefetch(S4.members.data());
+      if (uint64_t(S4.mbegin) < s->members.size()) __builtin_prefetch(s->members.data() + S4.mbegin, 1);
+      __builtin_prefetch(&s->recs[S4.filter]);
+    }
+    const uint32_t sl = ds[di];
     Slot& S = s->slots[sl];
     S.dirty = false;
     const uint32_t nm = static_cast<uint32_t>(S.members.size());
@@ -971,7 +981,9 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   mark();  // 3: member and alive words
   std::sort(group_idx.begin(), group_idx.end());
   group_idx.erase(std::unique(group_idx.begin(), group_idx.end()), group_idx.end());
-  for (uint64_t gi : group_idx) {
+  for (size_t k = 0; k < group_idx.size(); ++k) {
+    if (k + 8 < group_idx.size()) __builtin_prefetch(&s->groups[group_idx[k + 8]]);
+    const uint64_t gi = group_idx[k];
     const GroupRec& g = s->groups[gi];
     s->rpatch.push_back(RecPatch{static_cast<uint32_t>(gi), {0, 0, 0}, make_uint4(g.member_begin, g.n_members, g.slot, g.group_id)});
   }
