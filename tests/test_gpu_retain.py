@@ -429,3 +429,53 @@ def test_match_spec_strict_guard_for_plain_filters(mod, seed):
     st.store_retained(mod.Message(b"p/q", b"x", 0, now))
     assert st.page_read(b"p/q", 1, 10, now=now) == []
     assert [m.topic for m in st.dispatch(b"p/q", now)] == [b"p/q"]
+
+
+def test_concurrent_callers_parity(mod):
+    """Calls from several host threads at once, each on its own stream and buffers (the R line
+    runs two such callers): each call takes its own work area (its own queue shards), the
+    work-sharing walks of concurrent calls share the GPU, and every result equals the oracle's."""
+    import threading
+
+    import torch
+    from emqx_amd.engine import pack
+    names, expiry, filters = _sharing_case(1444)
+    idx = mod.RetainIndex()
+    idx.store(names, expiry)
+    idx.commit()
+    tt = RR.TokenTrie(names, expiry)
+    want = [tt.dispatch(f, 100) for f in filters]
+    dev = torch.device("cuda:0")
+    fb, fo = pack(filters)
+    d_fb = torch.from_numpy(fb.copy()).to(dev)
+    d_fo = torch.from_numpy(fo.view(np.int64).copy()).to(dev)
+    n, cap, T, rounds = len(filters), 1 << 20, 3, 6
+    streams = [torch.cuda.Stream(device=dev) for _ in range(T)]
+    outs = [(torch.empty(n + 1, dtype=torch.int64, device=dev), torch.empty(cap, dtype=torch.int32, device=dev))
+            for _ in range(T)]
+    errs, bad = [], []
+
+    def worker(t):
+        try:
+            off_d, ids_d = outs[t]
+            for _ in range(rounds):
+                tot = idx.match_device(d_fb.data_ptr(), d_fo.data_ptr(), n, 100, off_d.data_ptr(), ids_d.data_ptr(), cap,
+                                       stream=streams[t].cuda_stream)
+                off = off_d.cpu().numpy().view(np.uint64)
+                ids = ids_d[:tot].cpu().numpy().view(np.uint32)
+                for i in range(n):
+                    if sorted(ids[off[i]:off[i + 1]].tolist()) != want[i]:
+                        bad.append((t, i))
+                        return
+        except Exception as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    if errs:
+        raise errs[0]
+    assert not bad, bad[:5]
+    assert idx.stats()["queue_aborts"] == 0
