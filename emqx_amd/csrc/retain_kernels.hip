@@ -9,7 +9,12 @@
 //           range as one item, and every step hands the next 64 nodes of the stack's top items
 //           to the 64 lanes, so a wide '+' fan-out keeps every lane busy.  A final '#' emits the
 //           node's subtree as one rank range; a filter that ends on a stored topic emits its rank.
-//   count   live (unexpired) ranks per range; per-filter totals (one atomic per range)
+//           Load balance (retain.cpp "balance"): the work-sharing walk (retain_walk_queue_kernel,
+//           the default) shares the bottom of busy waves' stacks as pieces through sharded ticket
+//           queues while waves wait; the spill rounds (retain_walk_kernel + _spill_kernel) move
+//           whatever is left after a step budget into rebalanced rounds.
+//   count   live (unexpired) ranks per range; per-filter totals (one atomic per run of a
+//           filter's records in a 64-record super-row)
 //   write   rank -> topic id for the live ranks of each range, at the filter's CSR offset plus
 //           a per-filter cursor: coalesced streaming reads of rank_id / rank_exp.
 #include <hip/hip_runtime.h>
