@@ -476,6 +476,19 @@ uint4 dev_rec(const emqx_subtab* s, uint32_t f) {
   return make_uint4(r.plain_begin, r.n_plain, r.group_begin, r.n_groups);
 }
 
+// EMQX_SUBTAB_PROF=1: per add/remove call and per commit, where the host time goes, on stderr
+// (experiments)
+static bool subtab_prof() {
+  static const bool on = [] {
+    const char* e = std::getenv("EMQX_SUBTAB_PROF");
+    return e && *e == '1';
+  }();
+  return on;
+}
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // ---- batched plain ops on several threads --------------------------------------------------
 // A batch of plain subscribes or unsubscribes runs one thread per filter shard (pp_shard): a
 // shard's filters, their records, extents and map entries belong to its thread alone, and a
@@ -641,6 +654,7 @@ void plain_batch_shard(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs,
 
 // n plain subscribes (add) or unsubscribes, s->mu held.
 void plain_batch(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, uint64_t n, bool add) {
+  const double p0 = subtab_prof() ? now_us() : 0;
   if (add) {
     uint32_t fmax = 0;
     for (uint64_t i = 0; i < n; ++i) fmax = std::max(fmax, fs[i]);
@@ -665,7 +679,9 @@ void plain_batch(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, uint6
       plain_batch_shard(s, fs, subs, idx.data() + start[k], start[k + 1] - start[k], add, loc[k]);
   };
   // every thread (the ops are cache misses, not compute: more threads, more misses in flight)
+  const double p1 = subtab_prof() ? now_us() : 0;
   WorkPool::get().run(work, par_threads());
+  const double p2 = subtab_prof() ? now_us() : 0;
   // merge, shard by shard: moved lists appended to the shared arena
   for (PlainLocal& L : loc) {
     if (!L.arena.empty()) {
@@ -686,6 +702,9 @@ void plain_batch(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, uint6
     s->st_moves += L.moves;
     s->ops_pending += L.ops;
   }
+  if (subtab_prof())
+    std::fprintf(stderr, "SUBTAB_PROF plain_batch %s prep_us %.1f run_us %.1f merge_us %.1f\n", add ? "add" : "remove",
+                 p1 - p0, p2 - p1, now_us() - p2);
 }
 
 // ---- device side of a commit ----------------------------------------------------------------
@@ -821,19 +840,6 @@ int full_commit(emqx_subtab* s) {
 // Incremental commit: member lists and group lists of the changed slots / filters are
 // rewritten in the image (moved to the arena's end when they outgrow their extent); then the
 // touched words and records go to the device.
-// EMQX_SUBTAB_PROF=1: per add/remove call and per commit, where the host time goes, on stderr
-// (experiments)
-static bool subtab_prof() {
-  static const bool on = [] {
-    const char* e = std::getenv("EMQX_SUBTAB_PROF");
-    return e && *e == '1';
-  }();
-  return on;
-}
-static double now_us() {
-  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   const auto t0 = std::chrono::steady_clock::now();
   double pt[8] = {};
