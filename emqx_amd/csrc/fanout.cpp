@@ -41,6 +41,7 @@
 #include "fanout.h"
 #include "kernels.h"
 #include "streams.h"
+#include "workpool.h"
 
 using namespace emqx;
 
@@ -508,64 +509,7 @@ unsigned par_threads() {
   return t;
 }
 
-// A small pool of worker threads, kept for the process (spawning 16 threads per batch cost more
-// than the batch's work): run(fn, t) runs fn on the caller and t - 1 workers and returns when
-// all are done.  One run at a time (callers hold s->mu; several tables share the pool through
-// its own lock).
-class WorkPool {
- public:
-  static WorkPool& get() {
-    static WorkPool* p = new WorkPool();  // never destroyed: workers may outlive static teardown
-    return *p;
-  }
-  void run(const std::function<void()>& fn, unsigned t) {
-    std::lock_guard<std::mutex> one(run_mu_);
-    t = std::max(1u, t);
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      while (workers_.size() < t - 1) {
-        try {
-          workers_.emplace_back([this, id = workers_.size()] { loop(id); });
-        } catch (...) {
-          break;
-        }
-      }
-      job_ = &fn;
-      want_ = std::min<size_t>(t - 1, workers_.size());
-      left_ = want_;
-      ++gen_;
-    }
-    cv_.notify_all();
-    fn();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return left_ == 0; });
-    job_ = nullptr;
-  }
-
- private:
-  void loop(size_t id) {
-    uint64_t seen = 0;
-    for (;;) {
-      const std::function<void()>* job;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (id >= want_) continue;
-        job = job_;
-      }
-      (*job)();
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--left_ == 0) done_.notify_one();
-    }
-  }
-  std::mutex run_mu_, mu_;
-  std::condition_variable cv_, done_;
-  std::vector<std::thread> workers_;
-  const std::function<void()>* job_ = nullptr;
-  size_t want_ = 0, left_ = 0;
-  uint64_t gen_ = 0;
-};
+// (WorkPool: workpool.h; spawning 16 threads per batch cost more than the batch's work)
 
 struct PlainLocal {
   std::vector<uint32_t> arena;                        // lists moved in this batch
