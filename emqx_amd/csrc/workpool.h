@@ -6,7 +6,8 @@
 // so waking sleeping workers through a condition variable cost a noticeable share of each run.
 // Workers now spin on the run generation for a while after each run (and the caller on the
 // completion count) before they block: a run that follows within the spin window starts without
-// a wake-up.  Everything the spin reads is an atomic; the blocking path keeps the usual
+// a wake-up (EMQX_POOL_SPIN_US sets the window, 200 by default; 0 never spins).  Everything
+// the spin reads is an atomic; the blocking path keeps the usual
 // lock-then-notify order, so no wake-up is lost.
 #pragma once
 
@@ -15,6 +16,7 @@
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -25,7 +27,11 @@ namespace emqx {
 class WorkPool {
  public:
   static WorkPool& get() {
-    static WorkPool* p = new WorkPool();  // never destroyed: workers may outlive static teardown
+    static WorkPool* p = [] {
+      auto* w = new WorkPool();  // never destroyed: workers may outlive static teardown
+      if (const char* e = std::getenv("EMQX_POOL_SPIN_US")) w->set_spin_us(static_cast<uint32_t>(std::atoi(e)));
+      return w;
+    }();
     return *p;
   }
   // spin budget of a waiting thread before it blocks (tests set it to 0 or large)
