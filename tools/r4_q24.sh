@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4_q24}
 mkdir -p $OUT
 S=""
-for rep in 1 2; do S="$S tile=16 tile=12 tile=14 tile=20 tile=24 tile=16,walk_waves=16384 tile=16,queue_piece=768 tile=16,queue_piece=384"; done
+for rep in 1 2; do S="$S balance=1 queue_check=8 queue_check=2,queue_check=4 queue_roam=8 queue_roam=2,queue_roam=4 queue_shards=1024 queue_shards=256,queue_shards=512 queue_piece=256 queue_piece=1024,queue_piece=512 tile=18 tile=15,tile=16"; done
 timeout -k 10 400 python -u tools/retain_sweep.py --calls=20 $S > $OUT/sweep.jsonl 2> $OUT/sweep.err || { tail -20 $OUT/sweep.err; exit 1; }
 python3 - $OUT/sweep.jsonl <<'PY'
 import json,sys,collections
