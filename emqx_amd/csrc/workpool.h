@@ -2,13 +2,14 @@
 // (fanout.cpp: threaded plain ops, commit patch lists): run(fn, t) runs fn on the caller and on
 // t - 1 workers and returns when all are done.  One run at a time (a lock of its own).
 //
-// A run is short (a few hundred µs) and runs come in bursts (remove, add, the commit's passes),
-// so waking sleeping workers through a condition variable cost a noticeable share of each run.
-// Workers now spin on the run generation for a while after each run (and the caller on the
-// completion count) before they block: a run that follows within the spin window starts without
-// a wake-up (EMQX_POOL_SPIN_US sets the window, 200 by default; 0 never spins).  Everything
-// the spin reads is an atomic; the blocking path keeps the usual
-// lock-then-notify order, so no wake-up is lost.
+// Runs come in bursts (remove, add, the commit's passes).  Workers can spin on the run
+// generation for a while after each run (and the caller on the completion count) before they
+// block, so that a run following within the window starts without a wake-up
+// (EMQX_POOL_SPIN_US; default 0, never spin: measured, the S churn line did not gain — a run's
+// time is its ops' cache misses — and the T storm at 4096 callers lost half its rate to the
+// spinning workers, 12.7 -> 6.7 M ops/s, profiles/r4_q39_bench_T.json).  Everything the spin
+// reads is an atomic; the blocking path keeps the usual lock-then-notify order, so no wake-up
+// is lost.
 #pragma once
 
 #include <atomic>
@@ -109,7 +110,7 @@ class WorkPool {
   size_t want_ = 0;
   std::atomic<int> left_{0};
   std::atomic<uint64_t> gen_{0};
-  std::atomic<uint32_t> spin_us_{200};
+  std::atomic<uint32_t> spin_us_{0};
 };
 
 }  // namespace emqx
