@@ -982,52 +982,41 @@ def request_roofline(n, kms, args):
         p = json.load(f)
     misses = p["l2_misses_per_launch"] / p["batch_topics"] * n
     got = misses / (kms * 1e-3)
-    return {"bound": "random-access issue (L2 misses)", "l2_misses_per_launch": round(misses),
+    return {"bound": "random-gather ceiling", "l2_misses_per_launch": round(misses),
             "l2_misses_per_topic": round(misses / n, 2), "l2_hit_rate": round(p["l2_hit_rate"], 4),
             "achieved": round(got / 1e9, 2), "peak": round(ceil / 1e9, 2), "unit": "G misses/s",
             "frac": round(got / ceil, 4),
             "source": f"profiles/{fname} (TCC_MISS per launch); ceiling profiles/r1_gather16_ceiling.jsonl"}
 
 
-RANDOM_LINE_BYTES = 64  # one L2 miss = one 64-B HBM request (FETCH_SIZE calibration)
-
-
 def match_roofline(n, kms, args, tbytes, levels, evals, nout, traffic, traffic_src):
-    """The match kernel's roofline.  The walk is a chain of dependent random 16-B probes: what
-    bounds it is the rate of random line requests the chip can serve, measured at 55.8 G
-    independent random 16-B reads/s of a 1 GiB table (one L2 miss = one 64-B HBM request each,
-    tools/gather_bench.hip).  So `achieved` = the kernel's L2 misses per launch (committed PMC
-    passes on this workload, scaled to the batch) x 64 B over its live HIP-event time, `peak` =
-    that ceiling x 64 B; frac cannot exceed 1 by more than the ceiling's own measurement error.
-    `traffic` = FETCH_SIZE + WRITE_SIZE per launch (PMC), and `hbm_stream` sets it against the
-    8 TB/s streaming peak.  The 64-B-per-node-visit model of SURVEY §8(d) is kept as
-    `model_bytes` (it charges L2 hits as HBM bytes, so its frac can pass 1: config D, round 2).
-    Without committed PMC passes for the workload the model is all there is, and says so."""
+    """The match kernel's roofline on SURVEY §8(d)'s basis: `achieved` = the ALGORITHMIC bytes
+    of one launch (per topic len(T) + 64*L(T) + 64*evals(T) + 4*(|M(T)|+1): the topic bytes, one
+    64-B intern probe per level, one 64-B transaction per trie-node visit, the CSR ids and offset)
+    over the kernel's live HIP-event time, against the 8 TB/s HBM peak; `traffic` = the HBM bytes
+    the counters saw per launch (FETCH_SIZE + WRITE_SIZE, committed PMC passes, scaled to the
+    batch).  The model charges L2 hits as HBM bytes, so counted traffic can sit below it (config
+    B: 46 % of the probes hit in L2).
+
+    What actually bounds the walk is the rate of random line requests the chip serves (a chain of
+    dependent random 16-B probes): `request_rate` sets the kernel's L2 misses per launch against
+    the measured random-gather ceiling (55.8 G independent random 16-B reads/s of a 1 GiB table,
+    tools/gather_bench.hip, one L2 miss each), labelled "random-gather ceiling"."""
     alg_bytes = tbytes + 64 * levels + 64 * evals + 4 * (nout + n)
-    model_gbs = alg_bytes / (kms * 1e-3) / 1e9
-    model = {"achieved": round(model_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": round(model_gbs / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg_bytes,
-             "rule": "len(T) + 64*L(T) + 64*evals(T) + 4*(|M(T)|+1) per topic (SURVEY §8 d); L2 hits "
-                     "counted as HBM bytes"}
-    rr = request_roofline(n, kms, args)
-    if rr is None:
-        return {"bound": "hbm", "achieved": model["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": model["frac"], "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "match_fast_kernel", "kernel_ms_avg": round(kms, 4),
-                "basis": "64-B-per-visit model bytes (no committed PMC passes for this workload)",
-                "model_bytes": model}
-    line_gbs = rr["achieved"] * RANDOM_LINE_BYTES
-    peak_gbs = rr["peak"] * RANDOM_LINE_BYTES
-    out = {"bound": "hbm", "achieved": round(line_gbs, 1), "peak": round(peak_gbs, 1), "unit": "GB/s",
-           "frac": rr["frac"], "traffic": traffic, "traffic_source": traffic_src,
-           "kernel": "match_fast_kernel", "kernel_ms_avg": round(kms, 4),
-           "basis": "random 64-B line requests: L2 misses per launch (PMC) x 64 B / kernel time, against the "
-                    "measured random-gather ceiling x 64 B (= request_rate.frac)",
-           "request_rate": rr, "model_bytes": model}
+    gbs = alg_bytes / (kms * 1e-3) / 1e9
+    out = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+           "kernel": "match_fast_kernel", "kernel_ms_avg": round(kms, 4), "alg_bytes_per_launch": alg_bytes,
+           "basis": "algorithmic bytes per launch (SURVEY §8 d: len(T) + 64*L(T) + 64*evals(T) + 4*(|M(T)|+1) "
+                    "per topic) / live kernel time (HIP events on the engine's stream), against 8 TB/s"}
     if traffic:
         tgbs = traffic / (kms * 1e-3) / 1e9
-        out["hbm_stream"] = {"achieved": round(tgbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(tgbs / HBM_PEAK_GBS, 4), "rule": "counted FETCH_SIZE + WRITE_SIZE per launch"}
+        out["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
+        out["traffic_vs_alg"] = round(traffic / alg_bytes, 4)
+    rr = request_roofline(n, kms, args)
+    if rr is not None:
+        rr["bound"] = "random-gather ceiling"
+        out["request_rate"] = rr
     return out
 
 

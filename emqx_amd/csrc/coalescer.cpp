@@ -62,7 +62,10 @@ void run(emqx_coalescer* c) {
     const auto t0 = Clock::now();
     int rc = EMQX_OK;
     if (ed) rc = emqx_commit(c->e);
+    // the callbacks say "committed": the subtable commit's device half (which emqx_subtab_commit
+    // leaves in flight) is waited for first, so a device error reaches this batch's callers
     if (rc == EMQX_OK && sd) rc = emqx_subtab_commit(c->s);
+    if (rc == EMQX_OK && sd) rc = emqx_subtab_commit_wait(c->s);
     const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
     for (void* ctx : batch) c->cb(ctx, rc);
     batch.clear();

@@ -237,6 +237,9 @@ struct FoScratch {
   uint32_t stamp = 0;
   unsigned long long* ctl = nullptr;
   uint64_t* h_sum = nullptr;  // host-mapped call summary (synchronous calls)
+  unsigned long long* h_seen = nullptr;  // host-mapped [2]: picks and runs of this stream's last call
+  uint64_t rerun_picks = 0;   // a rerun after FO_SUM_F_PICKS: the flagged call's own picks ...
+  bool rerun_large = false;   // ... and the large resolve path for it
   hipEvent_t done = nullptr;  // end of the last fan-out enqueued on this stream
   bool used = false;
   void release() {
@@ -255,6 +258,7 @@ struct FoScratch {
     fo_free(tag);
     fo_free(ctl);
     fo_hfree(h_sum);
+    fo_hfree(h_seen);
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
   }
@@ -1168,6 +1172,8 @@ int flush_forgets(emqx_subtab* s, hipStream_t st) {
   }
   std::memcpy(s->h_forget, p.data(), p.size() * 4);
   FO_TRY(hipMemcpyAsync(s->d_forget.p, s->h_forget, p.size() * 4, hipMemcpyHostToDevice, st));
+  // resolves in flight on other streams write ps_vals of entries this pass may tombstone: after them
+  if (s->state_pending) FO_TRY(hipStreamWaitEvent(st, s->state_ev, 0));
   FO_TRY(launch_ps_forget(s->ps_keys, s->ps_cap, s->d_forget.p, p.size(), s->ps_count, s->ps_tombs, st));
   FO_TRY(hipEventRecord(s->forget_ev, st));
   s->forget_pending = true;
@@ -1191,7 +1197,7 @@ FoScratch* scratch_for(emqx_subtab* s, hipStream_t st) {
 int stateful_scratch(emqx_subtab* s, FoScratch* c, uint64_t m_cap, uint64_t cap) {
   // the pick list: the last finished call's picks with a margin (a call with more is flagged,
   // writes no ids and is rerun after this grows); never more than the delivery capacity
-  const uint64_t seen = s->h_ps_seen[2];
+  const uint64_t seen = std::max<uint64_t>(s->h_ps_seen[2], c->rerun_picks);
   uint64_t want = std::max<uint64_t>(c->pk_cap, std::max<uint64_t>(1u << 16, seen + seen / 2 + 4096));
   want = std::min<uint64_t>(want, std::max<uint64_t>(cap + 1, 1u << 16));
   if (want > c->pk_cap || !c->pk) {
@@ -1253,6 +1259,10 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
     if (!c->partials) FO_TRY(fo_alloc(c->partials, 4 * FO_BLOCKS));
   }
   if (!c->ctl) FO_TRY(fo_alloc(c->ctl, FO_CTL_WORDS));
+  if (!c->h_seen) {
+    FO_TRY(fo_halloc(c->h_seen, 2));
+    c->h_seen[0] = c->h_seen[1] = 0;
+  }
   if (s->commit_pending) FO_TRY(hipStreamWaitEvent(st, s->commit_ev, 0));
   // (c->ctl is zeroed by the call's first kernel, fanout_entry_topic)
   FanoutArgs a{};
@@ -1283,7 +1293,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
     // the small resolve path (no sort) unless the last finished call had many picks per run:
     // picks - runs bounds the picks of multi-pick runs by half
     const uint64_t S_last = s->h_ps_seen[2], R_last = s->h_ps_seen[3];
-    if (S_last < R_last + FO_MULTI_CAP / 2) {
+    if (!c->rerun_large && S_last < R_last + FO_MULTI_CAP / 2) {
       a.run_cnt = c->run_cnt;
       a.multi = c->multi;
       FO_TRY(hipMemsetAsync(c->run_cnt, 0, c->pk_cap * sizeof(uint32_t), st));
@@ -1291,6 +1301,9 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   }
   a.ctl = c->ctl;
   a.ps_seen = mapped(s->h_ps_seen);
+  a.call_seen = mapped(c->h_seen);
+  c->rerun_picks = 0;  // (consumed by this call's sizing)
+  c->rerun_large = false;
   a.moff = d_moff;
   a.mids = d_mids;
   a.n = n;
@@ -1321,10 +1334,20 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   return EMQX_OK;
 }
 
-// After a call flagged FO_SUM_F_RERUN: what to grow before it runs again.
-void note_rerun(emqx_subtab* s, uint64_t flags) {
+// After a call on stream st flagged FO_SUM_F_RERUN: what to grow before it runs again.  The
+// sizes come from the flagged call's own counts (its scratch's h_seen, written by its finish
+// kernel), not from the shared h_ps_seen, which a smaller call on another stream may have
+// overwritten since: the rerun sizes its pick list from them and takes the large resolve path
+// (FO_SUM_F_PICKS is raised for a list too short and for too many multi-pick picks alike).
+void note_rerun(emqx_subtab* s, hipStream_t st, uint64_t flags) {
   if (flags & FO_SUM_F_STATE_FULL) s->ps_force_grow = true;
-  // FO_SUM_F_PICKS: the finish kernel reported the call's picks in h_ps_seen[2]
+  if (flags & FO_SUM_F_PICKS) {
+    FoScratch* c = scratch_for(s, st);
+    if (c && c->h_seen) {
+      c->rerun_picks = c->h_seen[0];
+      c->rerun_large = true;
+    }
+  }
 }
 
 // Synchronous form: enqueue, drain, read the summary.  On overflow the write kernel wrote
@@ -1347,7 +1370,7 @@ int run_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, const 
     if (fl & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
     if (!(fl & FO_SUM_F_RERUN)) return EMQX_OK;
     if (attempt >= 3) return EMQX_ENOMEM;
-    note_rerun(s, fl);
+    note_rerun(s, st, fl);
   }
 }
 
@@ -1558,7 +1581,7 @@ int pb_wait(emqx_pub_batch* b) {
     if (attempt >= 3) return EMQX_ENOMEM;
     {
       std::lock_guard<std::mutex> g(p->s->mu);
-      note_rerun(p->s, fs[FO_SUM_FLAGS]);
+      note_rerun(p->s, p->stream, fs[FO_SUM_FLAGS]);
     }
     int rc = pb_enqueue_fanout(b, p->cap_mids, nullptr);
     if (rc != EMQX_OK) return rc;
@@ -1568,6 +1591,31 @@ int pb_wait(emqx_pub_batch* b) {
   if (fs[FO_SUM_FLAGS] & FO_SUM_F_MATCH) return EMQX_EDEVICE;
   if (fs[FO_SUM_FLAGS] & FO_SUM_F_OVERFLOW) return EMQX_EOVERFLOW;
   return EMQX_OK;
+}
+
+}  // namespace
+
+namespace {
+
+// Entry points that grow host tables: an allocation failure (here or on a pool worker) becomes
+// EMQX_ENOMEM instead of an exception through the C ABI (which would end the hosting VM); the
+// image may hold part of the call's ops, so the next commit rebuilds the device tables.
+template <class F>
+int subtab_guarded(emqx_subtab* s, F f) {
+  int rc;
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    rc = EMQX_ENOMEM;
+  } catch (...) {
+    rc = EMQX_EDEVICE;
+  }
+  try {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->need_full = true;
+  } catch (...) {
+  }
+  return rc;
 }
 
 }  // namespace
@@ -1657,7 +1705,7 @@ bool plain_parallel(emqx_subtab* s, const uint32_t* fs, const uint32_t* subs, co
   return true;
 }
 
-int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids, const uint32_t* group_ids,
+static int subtab_add_impl(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids, const uint32_t* group_ids,
                     uint64_t n) {
   if (!s || !ids_ok(filter_ids, sub_ids, n)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
@@ -1706,7 +1754,7 @@ int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* 
   return EMQX_OK;
 }
 
-int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids, const uint32_t* group_ids,
+static int subtab_remove_impl(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids, const uint32_t* group_ids,
                        uint64_t n) {
   if (!s || !ids_ok(filter_ids, sub_ids, n)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
@@ -1750,8 +1798,26 @@ int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_
 
 int emqx_subtab_commit(emqx_subtab* s) {
   if (!s) return EMQX_EINVAL;
+  return subtab_guarded(s, [&] {
+    std::lock_guard<std::mutex> g(s->cmu);
+    return commit_now(s);
+  });
+}
+
+int emqx_subtab_commit_wait(emqx_subtab* s) {
+  if (!s) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->cmu);
-  return commit_now(s);
+  if (hipSetDevice(s->device) != hipSuccess) return EMQX_EDEVICE;
+  int rc = commit_drain(s);
+  if (rc == EMQX_OK) return EMQX_OK;
+  // the device half failed: its tables are in an unknown state, so they are rebuilt from the
+  // host image now (a full commit), and the error goes to the callers of the failed commit
+  {
+    std::lock_guard<std::mutex> m(s->mu);
+    s->need_full = true;
+  }
+  if (commit_now(s) == EMQX_OK) (void)commit_drain(s);
+  return rc;
 }
 
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4) {
@@ -1774,7 +1840,7 @@ int emqx_subtab_commit_stats(emqx_subtab* s, uint64_t* out, uint32_t n) {
   return EMQX_OK;
 }
 
-int emqx_subtab_forget_publishers(emqx_subtab* s, const uint32_t* publishers, uint64_t n) {
+static int subtab_forget_publishers_impl(emqx_subtab* s, const uint32_t* publishers, uint64_t n) {
   if (!s || (n && !publishers)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
   if (!s->ps_keys) return EMQX_OK;  // no state kept yet
@@ -1783,7 +1849,7 @@ int emqx_subtab_forget_publishers(emqx_subtab* s, const uint32_t* publishers, ui
   return EMQX_OK;
 }
 
-int emqx_subtab_set_alive(emqx_subtab* s, const uint32_t* sub_ids, uint64_t n, int alive) {
+static int subtab_set_alive_impl(emqx_subtab* s, const uint32_t* sub_ids, uint64_t n, int alive) {
   if (!s || (n && !sub_ids)) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->mu);
   for (uint64_t i = 0; i < n; ++i)
@@ -2077,6 +2143,28 @@ int emqx_publish_batch(emqx_engine* e, emqx_subtab* s, uint32_t strategy, const 
     s->pb_free.push_back(b);
   }
   return rc;
+}
+
+int emqx_subtab_add(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids, const uint32_t* group_ids,
+                    uint64_t n) {
+  if (!s) return EMQX_EINVAL;
+  return subtab_guarded(s, [&] { return subtab_add_impl(s, filter_ids, sub_ids, group_ids, n); });
+}
+
+int emqx_subtab_remove(emqx_subtab* s, const uint32_t* filter_ids, const uint32_t* sub_ids, const uint32_t* group_ids,
+                       uint64_t n) {
+  if (!s) return EMQX_EINVAL;
+  return subtab_guarded(s, [&] { return subtab_remove_impl(s, filter_ids, sub_ids, group_ids, n); });
+}
+
+int emqx_subtab_set_alive(emqx_subtab* s, const uint32_t* sub_ids, uint64_t n, int alive) {
+  if (!s) return EMQX_EINVAL;
+  return subtab_guarded(s, [&] { return subtab_set_alive_impl(s, sub_ids, n, alive); });
+}
+
+int emqx_subtab_forget_publishers(emqx_subtab* s, const uint32_t* publishers, uint64_t n) {
+  if (!s) return EMQX_EINVAL;
+  return subtab_guarded(s, [&] { return subtab_forget_publishers_impl(s, publishers, n); });
 }
 
 }  // extern "C"

@@ -102,6 +102,8 @@ struct FanoutArgs {
   unsigned long long* multi; // small path [FO_MULTI_CAP]: run << 32 | list index of multi-pick runs' picks
   unsigned long long* ctl;   // [FO_CTL_WORDS]
   unsigned long long* ps_seen;  // host-mapped [4]: live keys, tombstones, picks, runs of the last finished call
+  unsigned long long* call_seen;  // host-mapped [2] of the calling stream's scratch: this call's picks, runs
+                                  // (the shared ps_seen holds whichever call finished last)
   // the match CSR
   const uint64_t* moff;      // match CSR offsets [n+1]
   const uint32_t* mids;      // match CSR filter ids [moff[n] - moff[0]]

@@ -744,6 +744,10 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_finish_kernel(FanoutArgs a,
     a.ps_seen[2] = a.ctl[FO_CTL_PICKS];
     a.ps_seen[3] = named;
   }
+  if (a.call_seen) {
+    a.call_seen[0] = a.ctl[FO_CTL_PICKS];
+    a.call_seen[1] = named;
+  }
   __threadfence_system();
 }
 

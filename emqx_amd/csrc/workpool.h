@@ -18,6 +18,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -56,11 +57,24 @@ class WorkPool {
       gen_.fetch_add(1, std::memory_order_release);  // publishes job_ / want_ to spinning workers
     }
     cv_.notify_all();
-    fn();
+    std::exception_ptr mine;
+    try {
+      fn();
+    } catch (...) {
+      mine = std::current_exception();
+    }
     if (!spin_until([&] { return left_.load(std::memory_order_acquire) == 0; })) {
       std::unique_lock<std::mutex> lk(mu_);
       done_.wait(lk, [&] { return left_.load(std::memory_order_acquire) == 0; });
     }
+    std::exception_ptr theirs;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      theirs = err_;
+      err_ = nullptr;
+    }
+    if (mine) std::rethrow_exception(mine);
+    if (theirs) std::rethrow_exception(theirs);
   }
 
  private:
@@ -95,7 +109,12 @@ class WorkPool {
         want = want_;
       }
       if (id >= want) continue;
-      (*job)();
+      try {
+        (*job)();
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!err_) err_ = std::current_exception();
+      }
       if (left_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
         std::lock_guard<std::mutex> lk(mu_);  // the caller may be about to block on done_
         done_.notify_one();
@@ -107,6 +126,7 @@ class WorkPool {
   std::condition_variable cv_, done_;
   std::vector<std::thread> workers_;
   const std::function<void()>* job_ = nullptr;
+  std::exception_ptr err_;  // first exception of a worker's job in the current run (under mu_)
   size_t want_ = 0;
   std::atomic<int> left_{0};
   std::atomic<uint64_t> gen_{0};

@@ -283,8 +283,14 @@ int emqx_subtab_set_alive(emqx_subtab* s, const uint32_t* sub_ids, uint64_t n, i
  * extents outweigh the live ones.  Ordered after the fan-outs in flight and before later
  * ones (device events): the call returns once the changes are enqueued (the previous commit's
  * device half is waited for first), and every fan-out / publish / re-pick called after it sees
- * them.  A device error of a commit's device half is returned by the next commit. */
+ * them.  A device error of a commit's device half is returned by the next commit, or by
+ * emqx_subtab_commit_wait. */
 int emqx_subtab_commit(emqx_subtab* s);
+/* Waits for the last commit's device half and returns its status.  On a device error the
+ * tables are rebuilt from the host image at once (a full commit) and the error is returned, so
+ * it reaches the callers of the failed commit (the commit coalescer calls this before it runs a
+ * batch's callbacks). */
+int emqx_subtab_commit_wait(emqx_subtab* s);
 /* counts[0..3] = live plain subscriptions, live shared memberships, groups with members,
  * device bytes */
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4);

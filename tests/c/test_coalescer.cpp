@@ -7,7 +7,9 @@
 //   2. group commit: changes submitted while a commit runs all go into the next one;
 //   3. route (engine) changes commit before subscription changes in a round;
 //   4. flush waits for everything submitted before it; destroy commits and notifies the rest;
-//   5. a failing commit reports its status to every change it carried.
+//   5. a failing commit reports its status to every change it carried, including a failure of
+//      the subtable commit's device half (emqx_subtab_commit_wait), which the batch's callbacks
+//      wait for.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -38,6 +40,8 @@ bool g_open = true;
 std::vector<std::string> g_log;  // "E<ops>" engine commit, "S<ops>" subtab commit, in order
 uint64_t g_eng_applied = 0, g_sub_applied = 0, g_eng_seen = 0, g_sub_seen = 0;
 int g_fail = EMQX_OK;
+int g_wait_fail = EMQX_OK;      // status of the subtable commit's device half
+uint64_t g_waits = 0;           // emqx_subtab_commit_wait calls
 uint32_t g_next_id = 100;
 
 void gate_wait() {
@@ -124,6 +128,11 @@ int emqx_subtab_commit(emqx_subtab*) {
   g_log.push_back("S" + std::to_string(upto - g_sub_seen));
   g_sub_seen = upto;
   return g_fail;
+}
+int emqx_subtab_commit_wait(emqx_subtab*) {
+  std::lock_guard<std::mutex> g(g_mu);
+  ++g_waits;
+  return g_wait_fail;
 }
 
 }  // extern "C"
@@ -224,6 +233,25 @@ int main() {
   CHECK(emqx_coalescer_flush(c) == EMQX_EDEVICE);
   CHECK(failed.calls == 1 && failed.status == EMQX_EDEVICE && never.calls == 0);
   g_fail = EMQX_OK;
+  // 4b. the commit returned but its device half failed: the batch's callers get the error
+  g_wait_fail = EMQX_EDEVICE;
+  Done dev_failed;
+  uint64_t waits0;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    waits0 = g_waits;
+  }
+  CHECK(emqx_coalescer_subscribe(c, &f, &sub, nullptr, 1, 1, &dev_failed) == EMQX_OK);
+  CHECK(emqx_coalescer_flush(c) == EMQX_EDEVICE);
+  CHECK(dev_failed.calls == 1 && dev_failed.status == EMQX_EDEVICE);
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    CHECK(g_waits == waits0 + 1);
+  }
+  g_wait_fail = EMQX_OK;
+  Done after;
+  CHECK(emqx_coalescer_subscribe(c, &f, &sub, nullptr, 1, 1, &after) == EMQX_OK);
+  CHECK(emqx_coalescer_flush(c) == EMQX_OK && after.status == EMQX_OK);
 
   // 5. destroy with changes pending: they are committed and notified
   gate_set(false);
