@@ -222,16 +222,17 @@ def shard_place(filters: Tuple[np.ndarray, np.ndarray], world: int, plan: np.nda
     return first[:n], span[:n], eng[:n]
 
 
+def shard_local_ids(filters: Tuple[np.ndarray, np.ndarray], rank: int, world: int, plan: np.ndarray):
+    """[global ids of engine A, global ids of engine B] for this rank (uint32, ascending)."""
+    first, span, eng = shard_place(filters, world, plan)
+    held = ((rank - first.astype(np.int64)) % world) < span
+    return [np.nonzero(held & (eng == e))[0].astype(np.uint32) for e in (0, 1)]
+
+
 def shard_engines(filters: Tuple[np.ndarray, np.ndarray], rank: int, world: int, plan: np.ndarray):
     """[(packed filters, global ids) of engine A, ... of engine B] for this rank."""
     from .workloads import take
-    first, span, eng = shard_place(filters, world, plan)
-    held = ((rank - first.astype(np.int64)) % world) < span
-    out = []
-    for e in (0, 1):
-        gids = np.nonzero(held & (eng == e))[0]
-        out.append((take(filters, gids), gids.astype(np.uint32)))
-    return out
+    return [(take(filters, gids), gids) for gids in shard_local_ids(filters, rank, world, plan)]
 
 
 def topic_requests(tb: torch.Tensor, to: torch.Tensor, world: int, plan: np.ndarray,
@@ -330,7 +331,12 @@ class ShardedMatcher:
     on CPU."""
 
     def __init__(self, filters: Tuple[np.ndarray, np.ndarray], group=None, device: Optional[torch.device] = None,
-                 mode: int = 0, match_fn: Optional[Callable] = None, max_piece_pm: int = MAX_PIECE_PM):
+                 mode: int = 0, match_fn: Optional[Callable] = None, max_piece_pm: int = MAX_PIECE_PM,
+                 engines: Optional[list] = None):
+        """``engines``: this rank's two engines already built ([A, B], each holding exactly the
+        filters shard_local_ids names for it, reporting global ids); they are adopted, not
+        copied (e.g. a table held whole on one GPU becomes engine A at world 1 once its P-space
+        filters are deleted from it, tests/test_gpu_c100m.py)."""
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -340,15 +346,20 @@ class ShardedMatcher:
         self.plan = shard_plan(filters, self.world, max_piece_pm)
         self.plan_dev = (torch.from_numpy(self.plan.view(np.int32).copy()).to(self.device)
                          if self.device.type == "cuda" and len(self.plan) else None)
-        self.local = shard_engines(filters, self.rank, self.world, self.plan)
+        self.local_ids = shard_local_ids(filters, self.rank, self.world, self.plan)
         self.engines = []
         self.last_local_topics = 0
-        if match_fn is None:
+        if engines is not None:
+            assert match_fn is None and len(engines) == 2
+            self.engines = list(engines)
+            match_fn = self._engine_match
+        elif match_fn is None:
             from .engine import Engine
-            for packed, gids in self.local:
+            from .workloads import take
+            for gids in self.local_ids:
                 e = Engine(self.device.index if self.device.type == "cuda" else -1)
                 if len(gids):
-                    e.insert_packed_ext(*packed, gids)
+                    e.insert_packed_ext(*take(filters, gids), gids)
                 e.commit()
                 self.engines.append(e)
             match_fn = self._engine_match
@@ -364,7 +375,7 @@ class ShardedMatcher:
 
     @property
     def n_local_filters(self) -> int:
-        return int(sum(len(g) for _, g in self.local))
+        return int(sum(len(g) for g in self.local_ids))
 
     def _engine_match(self, which: int, tb: torch.Tensor, to: torch.Tensor):
         d_off, d_ids = self._engine_csr(which, tb, to)

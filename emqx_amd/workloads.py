@@ -136,16 +136,30 @@ def take(packed: Tuple[np.ndarray, np.ndarray], idx: np.ndarray) -> Tuple[np.nda
 
 def dedupe_rows(codes: np.ndarray) -> np.ndarray:
     """Unique rows in first-occurrence order.  Rows are keyed by a 64-bit hash: a collision
-    can only drop a distinct row, which the generators replace by drawing more rows."""
-    c = codes.astype(np.uint64)
-    h = np.full(c.shape[0], 0x9E3779B97F4A7C15, dtype=np.uint64)
-    with np.errstate(over="ignore"):
-        for j in range(c.shape[1]):
-            h ^= c[:, j] + np.uint64(0x632BE59BD9B4E019) + (h << np.uint64(6)) + (h >> np.uint64(2))
-            h *= np.uint64(0xff51afd7ed558ccd)
-            h ^= h >> np.uint64(29)
-    _, first = np.unique(h, return_index=True)
-    return codes[np.sort(first)]
+    can only drop a distinct row, which the generators replace by drawing more rows.  (Hashes
+    in row chunks, first occurrences per bucket of the hash's top bits, both on the thread
+    pool: the same rows as one np.unique over all hashes.)"""
+    n = codes.shape[0]
+
+    def hashes(a):
+        c = codes[a:a + (1 << 21)].astype(np.uint64)
+        h = np.full(c.shape[0], 0x9E3779B97F4A7C15, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            for j in range(c.shape[1]):
+                h ^= c[:, j] + np.uint64(0x632BE59BD9B4E019) + (h << np.uint64(6)) + (h >> np.uint64(2))
+                h *= np.uint64(0xff51afd7ed558ccd)
+                h ^= h >> np.uint64(29)
+        return h
+    h = np.concatenate(_pmap(hashes, range(0, n, 1 << 21))) if n else np.zeros(0, np.uint64)
+    top = (h >> np.uint64(60)).astype(np.uint8)
+    keep = np.zeros(n, dtype=bool)
+
+    def bucket(b):
+        idx = np.nonzero(top == b)[0]
+        _, first = np.unique(h[idx], return_index=True)
+        keep[idx[first]] = True
+    _pmap(bucket, range(16))
+    return codes[keep]
 
 
 def _threads() -> int:
@@ -229,30 +243,37 @@ def config_a_prime(subscribers: int = 80, sub_ops: int = 1000, publishers: int =
 
 def _b_filter_codes(rng, n, vocab_sizes, samplers):
     D = len(vocab_sizes)
+    # every draw from the generator's stream first, in the original order (the table depends on
+    # it); the row-local arithmetic then runs over row chunks on the thread pool
     d = rng.integers(4, D + 1, n)  # U{4..8}
-    words = np.stack([samplers[l](n) for l in range(D)], 1).astype(np.int32)
-    lvl = np.arange(D)[None, :]
-    codes = np.where(lvl < d[:, None], words, ABSENT).astype(np.int32)
+    words = [samplers[l](n) for l in range(D)]
     cls = rng.random(n)
-    plus_cls = (cls >= 0.5) & (cls < 0.8)
-    hash_cls = cls >= 0.8
-    # '+' class: each level '+' w.p. 0.25, at least one
-    pm = (rng.random((n, D)) < 0.25) & (lvl < d[:, None])
-    none = plus_cls & ~pm.any(1)
+    pm_u = rng.random((n, D))
     force = rng.integers(0, d)  # one level in [0, d)
-    pm[np.nonzero(none)[0], force[none]] = True
-    codes = np.where(plus_cls[:, None] & pm, PLUS_CODE, codes)
-    # '#' class: keep t = U{1..d} literal levels, then '#'
     t = rng.integers(1, d + 1)
-    hrows = np.nonzero(hash_cls)[0]
-    hc = codes[hrows].copy()
-    hc[lvl.repeat(len(hrows), 0) >= t[hrows, None]] = ABSENT
+    lvl = np.arange(D)[None, :]
     codes9 = np.full((n, D + 1), ABSENT, dtype=np.int32)
-    codes9[:, :D] = codes
-    hc9 = np.full((len(hrows), D + 1), ABSENT, dtype=np.int32)
-    hc9[:, :D] = hc
-    hc9[np.arange(len(hrows)), t[hrows]] = HASH_CODE
-    codes9[hrows] = hc9
+
+    def rows(a):
+        z = slice(a, min(n, a + (1 << 20)))
+        dz, cz, tz = d[z], cls[z], t[z]
+        codes = np.where(lvl < dz[:, None], np.stack([w[z] for w in words], 1), ABSENT).astype(np.int32)
+        plus_cls = (cz >= 0.5) & (cz < 0.8)
+        hash_cls = cz >= 0.8
+        # '+' class: each level '+' w.p. 0.25, at least one
+        pm = (pm_u[z] < 0.25) & (lvl < dz[:, None])
+        none = plus_cls & ~pm.any(1)
+        pm[np.nonzero(none)[0], force[z][none]] = True
+        codes = np.where(plus_cls[:, None] & pm, PLUS_CODE, codes)
+        # '#' class: keep t = U{1..d} literal levels, then '#'
+        hrows = np.nonzero(hash_cls)[0]
+        hc = codes[hrows]
+        hc[lvl.repeat(len(hrows), 0) >= tz[hrows, None]] = ABSENT
+        codes[hrows] = hc
+        out = codes9[z]
+        out[:, :D] = codes
+        out[hrows, tz[hrows]] = HASH_CODE
+    _pmap(rows, range(0, n, 1 << 20))
     return codes9
 
 

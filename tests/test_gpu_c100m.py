@@ -1,12 +1,20 @@
-"""Config C at its real size (BASELINE configs[2]: 100M filters, generator B with vocab x4, seed
-3), ID-for-ID on a topic slice: the whole table on one GPU (replicated layout) and the same table
-through the filter-sharded device step at world 1, against the oracle (oracle/trie_oracle.cpp,
-the emqx_trie DFS + match_routes/1 union, apps/emqx/src/emqx_trie.erl:315-334) restated on the
-filters that can match the slice (oracle/pruned.py — exact for the slice).
+"""Config C at its real size (BASELINE configs[2]: 100M filters, generator B with vocab x4, seed 3),
+ID-for-ID on the first 12K topics of the C1 bench batch, in the default GPU suite:
 
-Generating and building the 100M table takes minutes, so this test runs only with
-EMQX_GPU_C100M=1 (tools/r4_c100m.sh; its log is under profiles/): the default GPU suite stays
-within a couple of minutes.  A progress line goes to gpurun_out/c100m_progress.log every 20 s.
+1. the whole table on one GPU (the replicated layout: one engine, ids = row numbers);
+2. the same table through the filter-sharded device step (emqx_shard_step_*) at world 1 over
+   RCCL.  The table is generated and built ONCE: at world 1 engine A holds every filter but the
+   P-space ones (`+/x/...`, dist.py), so leg 1's engine becomes engine A by deleting those (flag
+   flips of an incremental commit) and only engine B (the P-space filters) is built anew.
+
+Expected ids: tests/golden/c100m_slice.npz — the oracle (oracle/trie_oracle.cpp, the emqx_trie DFS
++ match_routes/1 union, apps/emqx/src/emqx_trie.erl:315-334) restated on the filters that can
+match the slice (oracle/pruned.py), made by tests/golden/make_c100m.py; the file's fingerprint
+of the generated table and batch is checked first, so a generator that drifted fails loudly
+instead of comparing against another table's answers.
+
+A progress line goes to gpurun_out/c100m_progress.log every 20 s (generation and the build take
+minutes).  EMQX_GPU_C100M=0 skips the module (iteration on other tests only).
 """
 
 import os
@@ -19,11 +27,10 @@ import pytest
 from oracle import cpp as C
 
 pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("EMQX_GPU_C100M") != "1",
-                                 reason="100M-filter table: set EMQX_GPU_C100M=1 (minutes of generation and build)")]
+              pytest.mark.skipif(os.environ.get("EMQX_GPU_C100M") == "0", reason="EMQX_GPU_C100M=0")]
 
-N_FILTERS = int(os.environ.get("EMQX_C100M_FILTERS", "100000000"))
-SLICE = 20_000
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "c100m_slice.npz")
 
 
 class _Beat:
@@ -36,8 +43,12 @@ class _Beat:
 
     def _run(self):
         while not self.stop.wait(20):
-            with open("gpurun_out/c100m_progress.log", "a") as f:
-                f.write(f"{self.what}: {time.time() - self.t0:.0f} s\n")
+            self._line(f"{self.what}: {time.time() - self.t0:.0f} s")
+
+    @staticmethod
+    def _line(s):
+        with open("gpurun_out/c100m_progress.log", "a") as f:
+            f.write(s + "\n")
 
     def __enter__(self):
         self.th.start()
@@ -45,53 +56,103 @@ class _Beat:
 
     def __exit__(self, *a):
         self.stop.set()
-        with open("gpurun_out/c100m_progress.log", "a") as f:
-            f.write(f"{self.what}: done in {time.time() - self.t0:.0f} s\n")
+        self._line(f"{self.what}: done in {time.time() - self.t0:.0f} s")
 
 
-def test_config_c_100m_slice_id_for_id():
-    import torch
-    import torch.distributed as dist
+def _fingerprint(packed):
+    import xxhash
+    buf, offs = packed
+    return [xxhash.xxh3_64_intdigest(np.ascontiguousarray(buf).data),
+            xxhash.xxh3_64_intdigest(np.ascontiguousarray(np.asarray(offs, np.uint64)).data)]
+
+
+@pytest.fixture(scope="module")
+def c100m():
+    """(workload, golden, slice) generated once for the module; the engine of leg 1 is handed to
+    leg 2 through the dict."""
     from emqx_amd import workloads as W
-    from emqx_amd.dist import ShardedMatcher
-    from emqx_amd.engine import Engine
-    from oracle import pruned
+    g = dict(np.load(GOLDEN))
     with _Beat("generate"):
-        wl = W.config_b(n_filters=N_FILTERS, n_topics=1_000_000, seed=3, vocab_scale=4)  # the C1 bench batch
-    k = SLICE
+        wl = W.config_b(n_filters=int(g["n_filters"]), n_topics=int(g["n_topics"]), seed=int(g["seed"]),
+                        vocab_scale=int(g["vocab_scale"]))
+    k = int(g["slice"])
     sl = W.take(wl.topics, np.arange(k))
-    with _Beat("oracle"):
-        off_o, ids_o, cand = pruned.slice_csr(wl.filters, wl.fcodes, sl, wl.tcodes[:k], threads=16)
-    assert int(off_o[-1]) > 0
+    assert _fingerprint(wl.filters) == [int(x) for x in g["table_fp"]], "generated table differs from the golden's"
+    assert _fingerprint(sl) == [int(x) for x in g["batch_fp"]], "generated batch differs from the golden's"
+    st = {"wl": wl, "golden": g, "slice": sl, "k": k}
+    yield st
+    e = st.pop("engine", None)
+    if e is not None:
+        e.close()
+
+
+def _dev_slice(st):
+    import torch
     dev = torch.device("cuda:0")
-    tb = torch.from_numpy(sl[0]).to(dev)
-    to = torch.from_numpy(sl[1].astype(np.int64)).to(dev)
-    # 1. the whole table on the GPU
+    sl = st["slice"]
+    return dev, torch.from_numpy(sl[0]).to(dev), torch.from_numpy(sl[1].astype(np.int64)).to(dev)
+
+
+def test_config_c_100m_replicated_id_for_id(c100m):
+    import torch
+    from emqx_amd.engine import Engine
+    st = c100m
+    g, k = st["golden"], st["k"]
+    dev, tb, to = _dev_slice(st)
     with _Beat("build replicated"):
         e = Engine(0)
-        e.insert_packed(*wl.filters)
+        e.insert_packed(*st["wl"].filters)
         e.commit()
-    cap = int(off_o[-1]) + 1024
+    st["engine"] = e
+    cap = int(g["off"][-1]) + 1024
     d_off = torch.empty(k + 1, dtype=torch.int64, device=dev)
     d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
     m = e.match_device(tb.data_ptr(), to.data_ptr(), k, d_off.data_ptr(), d_ids.data_ptr(), cap, mode=0,
                        stream=torch.cuda.current_stream(dev).cuda_stream)
-    bad = C.csr_mismatches(d_off.cpu().numpy().astype(np.uint64), d_ids[:m].cpu().numpy().view(np.uint32), off_o, ids_o)
+    assert m == int(g["off"][-1])
+    bad = C.csr_mismatches(d_off.cpu().numpy().astype(np.uint64), d_ids[:m].cpu().numpy().view(np.uint32),
+                           g["off"], g["ids"])
     assert bad.size == 0, bad[:10]
-    e.close()
-    del e
-    # 2. the same table through the sharded device step (two engines, world 1 over RCCL)
+    _Beat._line(f"replicated ok: {int(g['n_filters'])} filters, {k} topics, {m} ids ID-for-ID")
+
+
+def test_config_c_100m_sharded_step_id_for_id(c100m):
+    import torch
+    import torch.distributed as dist
+    from emqx_amd import dist as D
+    from emqx_amd.engine import Engine
+    from emqx_amd.workloads import take
+    st = c100m
+    e = st.pop("engine", None)
+    if e is None:
+        pytest.skip("the replicated leg did not build the table")
+    g, k, wl = st["golden"], st["k"], st["wl"]
+    dev, tb, to = _dev_slice(st)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = "29571"
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    eb = None
     try:
-        with _Beat("build sharded"):
-            sm = ShardedMatcher(wl.filters, device=dev)
+        with _Beat("engines A and B"):
+            plan = D.shard_plan(wl.filters, 1)
+            ids_a, ids_b = D.shard_local_ids(wl.filters, 0, 1, plan)
+            assert len(ids_a) + len(ids_b) == wl.n_filters and len(ids_b) > 0
+            e.delete(ids_b)  # leg 1's table minus the P-space filters = engine A at world 1
+            e.commit()
+            eb = Engine(0)
+            eb.insert_packed_ext(*take(wl.filters, ids_b), ids_b)
+            eb.commit()
+        sm = D.ShardedMatcher(wl.filters, device=dev, engines=[e, eb])
         off, ids = sm.match_all((tb, to))
-        bad = C.csr_mismatches(off.cpu().numpy().astype(np.uint64), ids.cpu().numpy().view(np.uint32), off_o, ids_o)
+        assert int(off[-1]) == int(g["off"][-1])
+        bad = C.csr_mismatches(off.cpu().numpy().astype(np.uint64), ids.cpu().numpy().view(np.uint32),
+                               g["off"], g["ids"])
         assert bad.size == 0, bad[:10]
+        _Beat._line(f"sharded step ok: engine A {len(ids_a)} filters, engine B {len(ids_b)}, "
+                    f"{k} topics, {int(off[-1])} ids ID-for-ID")
+        sm._step.close()
     finally:
         dist.destroy_process_group()
-    with open("gpurun_out/c100m_progress.log", "a") as f:
-        f.write(f"ok: {N_FILTERS} filters, {k} topics, {int(off_o[-1])} ids ID-for-ID (replicated and sharded), "
-                f"oracle table {len(cand)} filters\n")
+        e.close()
+        if eb is not None:
+            eb.close()
