@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "layout.h"
+
 namespace emqx {
 
 constexpr uint32_t SUB_NONE = 0xFFFFFFFFu;
@@ -137,6 +139,20 @@ constexpr uint64_t FO_SUM_F_STATE_FULL = 4;  // a pick found no room in the pick
 constexpr uint64_t FO_SUM_F_PICKS = 8;       // more round_robin / sticky picks than the pick list
                                              // holds: no ids written (rerun; the list grows)
 constexpr uint64_t FO_SUM_F_RERUN = FO_SUM_F_STATE_FULL | FO_SUM_F_PICKS;
+
+constexpr uint64_t FO_SUM_F_SMALL = 16;      // the one-launch small-batch path could not take the
+                                             // fan-out (too many entries): run the regular kernels
+// Counter-based random pick of EMQX_SHARE_RANDOM: entry i of the call, group record gidx.
+__host__ __device__ inline uint32_t fo_rand(uint32_t seed, uint64_t i, uint32_t salt) {
+  return mix32(seed ^ mix32(static_cast<uint32_t>(i) * 0x9E3779B1u ^ static_cast<uint32_t>(i >> 32) ^ salt));
+}
+// Member index of a stateless pick among n >= 2 members (emqx_shared_sub.erl:251-288): the
+// caller's phash2 key for hash_clientid / hash_topic (1 + Key rem Count, 1-based there),
+// fo_rand for random.  strategy: EMQX_SHARE_* (3, 4 hash; else random).
+__host__ __device__ inline uint32_t fo_stateless_index(uint32_t strategy, uint32_t key, uint32_t seed, uint64_t entry,
+                                                       uint32_t gidx, uint32_t n) {
+  return (strategy == 3u || strategy == 4u) ? key % n : fo_rand(seed, entry, gidx + 0x632BE5ABu) % n;
+}
 
 // True for the strategies whose picks depend on state kept per publisher.
 __host__ __device__ inline bool fo_stateful(uint32_t strategy) { return strategy == 1u || strategy == 2u; }

@@ -214,10 +214,6 @@ __global__ __launch_bounds__(FO_BLOCKS) void fanout_partials_kernel(FanoutArgs a
   }
 }
 
-__device__ __forceinline__ uint32_t fo_rand(uint32_t seed, uint64_t i, uint32_t salt) {
-  return mix32(seed ^ mix32(static_cast<uint32_t>(i) * 0x9E3779B1u ^ static_cast<uint32_t>(i >> 32) ^ salt));
-}
-
 __device__ __forceinline__ uint64_t ps_hash(uint64_t k) {
   k ^= k >> 33;
   k *= 0xff51afd7ed558ccdULL;
@@ -264,11 +260,10 @@ __device__ __forceinline__ uint32_t pick_stateless(const FanoutArgs& a, const Gr
   // pick_subscriber/6 with one member returns it without consulting the strategy
   // (emqx_shared_sub.erl:265)
   if (n == 1) return a.members[g.member_begin];
-  uint32_t idx;
-  if (a.strategy == EMQX_SHARE_HASH_CLIENTID || a.strategy == EMQX_SHARE_HASH_TOPIC)
-    idx = a.keys[t] % n;  // 1 + phash2(Key) rem Count, 1-based in the reference
-  else  // EMQX_SHARE_RANDOM (and the fallback of a stateful pick with no room for its state)
-    idx = fo_rand(a.seed, i, gidx + 0x632BE5ABu) % n;
+  // 1 + phash2(Key) rem Count for the hash strategies; random (and the fallback of a stateful
+  // pick with no room for its state): fo_rand
+  const bool hash = a.strategy == EMQX_SHARE_HASH_CLIENTID || a.strategy == EMQX_SHARE_HASH_TOPIC;
+  const uint32_t idx = fo_stateless_index(hash ? a.strategy : 0u, hash ? a.keys[t] : 0u, a.seed, i, gidx, n);
   return a.members[g.member_begin + idx];
 }
 

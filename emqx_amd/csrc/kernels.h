@@ -111,6 +111,52 @@ struct MatchArgs {
   uint64_t* partials;      // [scan_partials(n)] scan scratch (perm set)
 };
 
+// Small batches in ONE launch (the host batcher's and the publish batcher's calls, a few dozen to
+// a few hundred topics: DESIGN §3.5).  One block of SMALL_WAVES waves copies the batch from
+// pinned host memory into HBM, walks it in SMALL_WAVES tiles of ceil(n / SMALL_WAVES) topics
+// (fast_tile, the batched kernel's walk), runs the deep path over deferred topics, scans and
+// scatters the CSR, and either streams it into pinned host memory (match) or fans it out
+// (stateless $share strategies) straight into the pinned delivery buffers — no copy engine, no
+// second launch.  Anything that does not fit is flagged and rerun on the batched path.
+constexpr uint32_t SMALL_WAVES = 16;
+constexpr uint64_t SMALL_MAX_N = uint64_t(SMALL_WAVES) * TILE_TOPICS;  // 1024 topics
+constexpr uint32_t SMALL_FO_MAX_ENTRIES = 16384;                     // match entries the fan-out takes
+
+struct SmallFanout {
+  const uint4* recs;        // FilterRec per filter id (fanout.h; inline lists included)
+  uint32_t n_recs;
+  const uint32_t* plain;
+  const uint4* groups;      // GroupRec
+  const uint32_t* members;
+  uint32_t strategy;        // stateless: EMQX_SHARE_RANDOM / HASH_CLIENTID / HASH_TOPIC
+  uint32_t seed;
+  const uint32_t* h_keys;   // host-mapped per-topic keys, or null
+  uint32_t* d_keys;         // their HBM copy (the batched fan-out of a rerun reads it)
+  uint4* erec;              // [SMALL_FO_MAX_ENTRIES] scratch: each entry's record
+  uint32_t* etop;           // [SMALL_FO_MAX_ENTRIES] scratch: each entry's topic
+  const unsigned long long* ps_count;  // pick-state keys (the summary's state word), or null
+  uint64_t* h_off;          // host-mapped delivery CSR: offsets [n + 1]
+  uint32_t* h_subs;         // [cap]
+  uint32_t* h_fil;          // [cap] filter id | FANOUT_SHARED_BIT for $share picks
+  uint64_t cap;
+  uint64_t* h_sum;          // host-mapped fan-out summary [FO_SUM_WORDS]
+};
+
+struct SmallArgs {
+  MatchArgs m;              // tbytes / toffs: the HBM copy; out_off / out_ids: the CSR in HBM;
+                            // summary: host-mapped; perm / diag off
+  const uint8_t* h_tbytes;  // host-mapped batch: bytes [0, nbytes), offsets [n + 1] (from 0)
+  const uint64_t* h_toffs;
+  uint64_t nbytes;
+  uint32_t tt;              // topics per tile: ceil(n / SMALL_WAVES)
+  uint32_t has_fanout;
+  uint64_t* h_out_off;      // match only: the CSR into host-mapped buffers (null: not copied)
+  uint32_t* h_out_ids;
+  uint64_t h_cap;
+  SmallFanout f;
+};
+hipError_t launch_small_batch(const SmallArgs& a, hipStream_t s);
+
 // Deep path: waves of match_deep_kernel, slab entries each wave reserves per atomic, and the
 // padding value of a reserved entry left unused.
 constexpr uint32_t DEEP_WAVES = 512;

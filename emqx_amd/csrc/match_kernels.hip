@@ -29,6 +29,7 @@
 
 #include <algorithm>
 
+#include "fanout.h"
 #include "kernels.h"
 
 namespace emqx {
@@ -543,36 +544,31 @@ __device__ __forceinline__ uint32_t span_mask(uint32_t k, uint32_t lo, uint32_t 
 
 constexpr int ceil_log2(int v) { return v <= 1 ? 0 : 1 + ceil_log2((v + 1) / 2); }
 
-template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG>
-__global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(MatchArgs a) {
+// One wave's LDS in the fast path.
+template <int STACK_CAP, int WID_CAP>
+struct FastLds {
+  uint2 stack[STACK_CAP];  // work stack (LIFO); overflow spills its bottom half to HBM
+  uint32_t wids[WID_CAP];  // word ids of the tile's topics, topic after topic
+  uint32_t wend[64];       // per topic: end index of its word ids
+  uint32_t cnt[64];        // per topic: emitted filter ids
+};
+
+// One wave walks one tile: topics [tile * tt, tile * tt + tt) of the batch (tt <= 64; the batched
+// kernel's tiles are TILE_TOPICS wide, the small-batch kernel's narrower, so that a batch of a
+// few dozen topics spreads over many waves).  Wave-uniform returns only; no block barrier.
+template <int STACK_CAP, int WID_CAP, int K, bool DIAG>
+__device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP, WID_CAP>& L, uint64_t tile,
+                                          uint32_t tt) {
   static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
   static_assert(WID_CAP <= 1024, "item word index is 10 bits");
-  struct WaveLds {
-    uint2 stack[STACK_CAP];  // work stack (LIFO); overflow spills its bottom half to HBM
-    uint32_t wids[WID_CAP];  // word ids of the tile's topics, topic after topic
-    uint32_t wend[64];       // per topic: end index of its word ids
-    uint32_t cnt[64];        // per topic: emitted filter ids
-  };
-  __shared__ WaveLds lds_all[WAVES];
-
   const uint32_t lane = lane_id();
-  const uint32_t wv = threadIdx.x >> 6;
-  WaveLds& L = lds_all[wv];
-  // With a reordered batch (a.deal), XCD x (blocks b = x mod 8, dispatched round robin)
-  // takes one contiguous range of logical blocks: neighbouring keys share its L2.
-  uint64_t blk = blockIdx.x;
-  if (a.deal) {
-    const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, j = blockIdx.x >> 3, q = nb >> 3, r = nb & 7u;
-    blk = static_cast<uint64_t>(x) * q + min(x, r) + j;
-  }
-  const uint64_t tile = blk * WAVES + wv;
-  const uint64_t t0 = tile * TILE_TOPICS;
+  const uint64_t t0 = tile * tt;
   if (t0 >= a.n) return;  // wave-uniform; the kernel uses no block-wide barrier
   if (a.perm && (a.ctrl[CTRL_ERROR] & CTRL_ERR_ORDER_CAP)) return;  // no reordered batch: rerun
   const uint64_t clk0 = DIAG ? wall_clock64() : 0;
 
   const TableView& tv = a.tv;
-  const uint32_t tcount = static_cast<uint32_t>(min<uint64_t>(TILE_TOPICS, a.n - t0));
+  const uint32_t tcount = static_cast<uint32_t>(min<uint64_t>(tt, a.n - t0));
   const bool valid = lane < tcount;
   const uint64_t t = t0 + lane;
   uint64_t start = 0, end = 0;
@@ -993,13 +989,27 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
   }
 }
 
+template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG>
+__global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(MatchArgs a) {
+  __shared__ FastLds<STACK_CAP, WID_CAP> lds_all[WAVES];
+  const uint32_t wv = threadIdx.x >> 6;
+  // With a reordered batch (a.deal), XCD x (blocks b = x mod 8, dispatched round robin)
+  // takes one contiguous range of logical blocks: neighbouring keys share its L2.
+  uint64_t blk = blockIdx.x;
+  if (a.deal) {
+    const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, j = blockIdx.x >> 3, q = nb >> 3, r = nb & 7u;
+    blk = static_cast<uint64_t>(x) * q + min(x, r) + j;
+  }
+  fast_tile<STACK_CAP, WID_CAP, K, DIAG>(a, lds_all[wv], blk * WAVES + wv, TILE_TOPICS);
+}
+
 // ------------------------------------------------------------------------------------
 // Deep path: one wavefront per deferred topic; word ids and stack in global scratch.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
+// Wave gw of nwaves walks deferred topics gw, gw + nwaves, ... (tt: the fast path's tile width,
+// whose tile_sum the deep path adds its counts to).
+__device__ __forceinline__ void deep_walk(const MatchArgs& a, uint32_t gw, uint32_t nwaves, uint32_t tt) {
   const uint32_t lane = lane_id();
-  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (gw >= a.deep_waves) return;
   const TableView& tv = a.tv;
   const uint32_t ndef = __hip_atomic_load(&a.ctrl[CTRL_DEFERRED], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint32_t* wids = a.deep_wids + static_cast<uint64_t>(gw) * DEEP_MAX_LEVELS;
@@ -1015,7 +1025,7 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
       if (p < a.deep_slab_cap) a.deep_slab[p] = DEEP_PAD;
     ccur = cend;
   };
-  for (uint32_t j = gw; j < ndef; j += a.deep_waves) {
+  for (uint32_t j = gw; j < ndef; j += nwaves) {
     const uint32_t t = a.deferred[j];
     if (lane == 0) a.deep_rank[j] = 0;
     const uint64_t start = a.toffs[t], end = a.toffs[t + 1];
@@ -1158,12 +1168,18 @@ __global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
     const uint32_t ev = wave_sum(evals);
     if (lane == 0) {
       a.counts[t] = count;
-      if (count) atomicAdd(reinterpret_cast<unsigned long long*>(a.tile_sum + t / TILE_TOPICS),
+      if (count) atomicAdd(reinterpret_cast<unsigned long long*>(a.tile_sum + t / tt),
                            static_cast<unsigned long long>(count));
       atomicAdd(a.ctrl + CTRL_DEEP_EVALS, ev);
     }
   }
   pad_chunk();
+}
+
+__global__ __launch_bounds__(256) void match_deep_kernel(MatchArgs a) {
+  const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (gw >= a.deep_waves) return;
+  deep_walk(a, gw, a.deep_waves, TILE_TOPICS);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1320,6 +1336,8 @@ __global__ __launch_bounds__(GROUP_TILES) void group_reduce_kernel(MatchArgs a, 
 // Then its slab entries, 64 at a time: lanes holding the same topic find each other with six
 // ballots (one per bit of the topic index) and take ranks by popcount, and the same ballots
 // advance every topic's running position — no atomics.  Ids beyond out_cap are dropped.
+__device__ __forceinline__ void scatter_tile(const MatchArgs& a, uint64_t tile, uint64_t off);
+
 __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t wv = threadIdx.x >> 6;
@@ -1341,10 +1359,16 @@ __global__ __launch_bounds__(256) void scatter_fast_kernel(MatchArgs a) {
     off = before + wave_incl_scan64(c, lane) - c;
     if (t < a.n) a.out_off[t] = off;
   }
-  // Lane L keeps topic L's next output position in a register.  Per round of 64 entries the
-  // six topic-bit ballots give each entry its rank among the round's entries of its topic and
-  // each lane its topic's count in the round; positions travel by cross-lane reads.  No LDS
-  // and no fence in the loop, so the id stores never hold the next round's loads back.
+  scatter_tile(a, tile, off);
+}
+
+// Lane L keeps topic L's next output position in a register.  Per round of 64 entries the
+// six topic-bit ballots give each entry its rank among the round's entries of its topic and
+// each lane its topic's count in the round; positions travel by cross-lane reads.  No LDS
+// and no fence in the loop, so the id stores never hold the next round's loads back.
+// off: the output position of this lane's topic of the tile.
+__device__ __forceinline__ void scatter_tile(const MatchArgs& a, uint64_t tile, uint64_t off) {
+  const uint32_t lane = lane_id();
   uint64_t next = off;
   const uint32_t fill = min(a.tile_fill[tile], a.slab_cap);
   const uint64_t dmask = a.tile_defer[tile];
@@ -1482,6 +1506,216 @@ __global__ void slot_patch_kernel(EdgeSlot* edges, uint32_t* fids, const SlotPat
 }
 
 // ------------------------------------------------------------------------------------
+// Small batches in one launch (kernels.h SmallArgs)
+// ------------------------------------------------------------------------------------
+namespace {
+
+// Exclusive scan of one value per thread over a block of SMALL_WAVES waves; *total = the sum.
+__device__ __forceinline__ uint64_t small_block_scan(uint64_t v, uint64_t* total, uint64_t* wsum) {
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  const uint64_t incl = wave_incl_scan64(v, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  for (uint32_t k = 0; k < SMALL_WAVES; ++k) {
+    before += k < w ? wsum[k] : 0;
+    all += wsum[k];
+  }
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
+
+// Largest i in [0, n) with v[i] <= x (v non-decreasing, v[0] <= x).
+__device__ __forceinline__ uint32_t small_floor(const uint32_t* v, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (v[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs sa) {
+  constexpr int SC = 384, WC = 640;  // the batched kernel's shallow-table variant (FAST_K1_S384)
+  struct FoLds {
+    uint32_t D[SMALL_FO_MAX_ENTRIES + 1];  // each entry's first delivery
+    uint32_t off[SMALL_MAX_N + 1];         // each topic's first entry
+  };
+  union Lds {
+    FastLds<SC, WC> w[SMALL_WAVES];
+    FoLds f;
+  };
+  __shared__ Lds lds;
+  __shared__ uint64_t wsum[SMALL_WAVES];
+  const MatchArgs& a = sa.m;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  constexpr uint32_t NT = SMALL_WAVES * 64;
+  const uint64_t n = a.n;
+
+  // 0. the call's control words; the batch from pinned host memory into HBM (one round trip
+  //    over PCIe: every load of the copy is issued before any store)
+  if (tid < CTRL_WORDS) a.ctrl[tid] = 0;
+  {
+    uint64_t* toffs = const_cast<uint64_t*>(a.toffs);
+    uint4* tb = reinterpret_cast<uint4*>(const_cast<uint8_t*>(a.tbytes));
+    const uint4* hb = reinterpret_cast<const uint4*>(sa.h_tbytes);
+    const uint64_t nch = (sa.nbytes + 15) / 16;
+    for (uint64_t i = tid; i <= n; i += NT) toffs[i] = sa.h_toffs[i];
+    for (uint64_t i = tid; i < nch; i += NT) tb[i] = hb[i];
+    if (sa.has_fanout && sa.f.h_keys)
+      for (uint64_t i = tid; i < n; i += NT) sa.f.d_keys[i] = sa.f.h_keys[i];
+  }
+  __syncthreads();
+
+  // 1. the walk: wave w takes tile w (tt topics); 2. deferred topics on every wave
+  const uint32_t tt = sa.tt;
+  const uint64_t ntiles = (n + tt - 1) / tt;
+  if (wv < ntiles) fast_tile<SC, WC, 1, false>(a, lds.w[wv], wv, tt);
+  __syncthreads();
+  if (__hip_atomic_load(&a.ctrl[CTRL_DEFERRED], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+    deep_walk(a, wv, SMALL_WAVES, tt);
+  __syncthreads();
+
+  uint64_t* sm = a.summary;
+  const uint32_t need = a.ctrl[CTRL_NEED_SLAB], err = a.ctrl[CTRL_ERROR];
+  uint64_t flags = 0;
+  if (need > a.slab_cap || (err & (CTRL_ERR_DEEP_SLAB | CTRL_ERR_TOO_DEEP))) flags |= SUM_F_RETRY;
+  if (err & CTRL_ERR_TOO_LONG) flags |= SUM_F_ERROR;
+
+  // 3. offsets (one topic per thread), 4. the tiles' slabs and the deep slab into the CSR
+  uint64_t total = 0;
+  {
+    const uint64_t c = (tid < n && !flags) ? a.counts[tid] : 0;
+    const uint64_t ex = small_block_scan(c, &total, wsum);
+    if (tid < n) a.out_off[tid] = ex;
+    if (tid == 0) a.out_off[n] = total;
+  }
+  if (total > a.out_cap) flags |= SUM_F_OVERFLOW;
+  __syncthreads();
+  if (!(flags & (SUM_F_RETRY | SUM_F_ERROR))) {
+    if (wv < ntiles) {
+      const uint64_t t = uint64_t(wv) * tt + lane;
+      scatter_tile(a, wv, (lane < tt && t < n) ? a.out_off[t] : 0);
+    }
+    const uint32_t fill = min(a.ctrl[CTRL_DEEP_FILL], a.deep_slab_cap);
+    for (uint32_t i = tid; i < fill; i += NT) {
+      const uint64_t e = a.deep_slab[i];
+      if (e == DEEP_PAD) continue;
+      const uint32_t j = static_cast<uint32_t>(e >> 32) & 0x7FFFFFFFu;
+      const uint64_t p = a.out_off[a.deferred[j]] + atomicAdd(&a.deep_rank[j], 1u);
+      if (p < a.out_cap) a.out_ids[p] = resolve_entry(a.tv, e);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t ev = a.ctrl[CTRL_DEEP_EVALS];
+    uint32_t mx = 0;
+    for (uint64_t k = 0; k < ntiles; ++k) {
+      const uint2 st = a.tile_stats[k];
+      ev += st.x;
+      mx = max(mx, st.y);
+    }
+    sm[SUM_TOTAL] = total;
+    sm[SUM_EVALS] = ev;
+    sm[SUM_MAXSTACK] = mx;
+    sm[SUM_DEFERRED] = a.ctrl[CTRL_DEFERRED];
+    sm[SUM_NEED_SLAB] = need;
+    sm[SUM_DEEP_FILL] = a.ctrl[CTRL_DEEP_FILL];
+    sm[SUM_ERROR] = err;
+    sm[SUM_FLAGS] = flags;
+  }
+
+  // 5a. match only: the CSR into the pinned host buffers (16-B stores)
+  if (sa.h_out_off) {
+    if (flags & (SUM_F_RETRY | SUM_F_ERROR)) return;
+    const uint64_t no2 = (n + 1) / 2;
+    for (uint64_t i = tid; i < no2; i += NT)
+      reinterpret_cast<uint4*>(sa.h_out_off)[i] = reinterpret_cast<const uint4*>(a.out_off)[i];
+    if (tid == 0 && ((n + 1) & 1)) sa.h_out_off[n] = a.out_off[n];
+    const uint64_t ids = min(total, sa.h_cap), nv = ids / 4;
+    for (uint64_t i = tid; i < nv; i += NT)
+      reinterpret_cast<uint4*>(sa.h_out_ids)[i] = reinterpret_cast<const uint4*>(a.out_ids)[i];
+    if (tid < ids - 4 * nv) sa.h_out_ids[4 * nv + tid] = a.out_ids[4 * nv + tid];
+    return;
+  }
+  if (!sa.has_fanout) return;
+
+  // 5b. the fan-out (emqx_broker.erl:244-272,500-524; stateless $share picks,
+  //     emqx_shared_sub.erl:251-288), straight into the pinned delivery buffers
+  const SmallFanout& f = sa.f;
+  const uint64_t m = total;
+  if (flags || m > SMALL_FO_MAX_ENTRIES) {
+    if (tid == 0) {
+      f.h_sum[FO_SUM_FLAGS] = flags ? FO_SUM_F_MATCH : FO_SUM_F_SMALL;
+      f.h_sum[FO_SUM_TOTAL] = 0;
+      f.h_sum[FO_SUM_ENTRIES] = m;
+      f.h_sum[FO_SUM_STATE] = f.ps_count ? *f.ps_count : 0;
+    }
+    return;
+  }
+  uint32_t* D = lds.f.D;
+  uint32_t* off = lds.f.off;
+  for (uint64_t t = tid; t <= n; t += NT) off[t] = static_cast<uint32_t>(a.out_off[t]);
+  __syncthreads();
+  // pass 1: each entry's record and topic; exclusive scan of the deliveries
+  uint64_t T = 0;
+  for (uint32_t e0 = 0; e0 < m; e0 += NT) {
+    const uint32_t e = e0 + tid;
+    uint32_t c = 0;
+    if (e < m) {
+      const uint32_t fid = a.out_ids[e];
+      const uint4 r = fid < f.n_recs ? f.recs[fid] : make_uint4(0, 0, 0, 0);
+      c = fo_rec_plain(r) + fo_rec_groups(r);
+      f.erec[e] = r;
+      f.etop[e] = small_floor(off, static_cast<uint32_t>(n), e);
+    }
+    uint64_t tc;
+    const uint64_t ex = small_block_scan(c, &tc, wsum);
+    if (e < m) D[e] = static_cast<uint32_t>(T + ex);
+    T += tc;
+  }
+  if (tid == 0) D[m] = static_cast<uint32_t>(min<uint64_t>(T, 0xFFFFFFFFull));
+  __syncthreads();
+  for (uint64_t t = tid; t <= n; t += NT) f.h_off[t] = t < n ? D[off[t]] : T;
+  const bool fits = T <= f.cap;
+  // pass 2: deliveries j, lane-consecutive (coalesced stores); each finds its entry in LDS
+  if (fits) {
+    const bool hash = f.strategy == 3u || f.strategy == 4u;
+    for (uint64_t j0 = 0; j0 < T; j0 += NT) {
+      const uint32_t j = static_cast<uint32_t>(j0) + tid;
+      if (j >= T) continue;
+      const uint32_t e = small_floor(D, static_cast<uint32_t>(m), j);
+      const uint32_t r = j - D[e];
+      const uint4 rec = f.erec[e];
+      const uint32_t fid = a.out_ids[e];
+      const uint32_t np = rec.y & ~FO_INLINE_BIT;
+      uint32_t sub, fl = fid;
+      if (r < np) {
+        sub = (rec.y & FO_INLINE_BIT) ? (r == 0 ? rec.x : (r == 1 ? rec.z : rec.w)) : f.plain[rec.x + r];
+      } else {
+        const uint32_t gidx = rec.z + (r - np);
+        const uint4 g = f.groups[gidx];  // {member_begin, n_members, slot, group_id}
+        const uint32_t idx =
+            g.y <= 1 ? 0u : fo_stateless_index(f.strategy, hash ? f.d_keys[f.etop[e]] : 0u, f.seed, e, gidx, g.y);
+        sub = f.members[g.x + idx];
+        fl |= FANOUT_SHARED_BIT;
+      }
+      f.h_subs[j] = sub;
+      f.h_fil[j] = fl;
+    }
+  }
+  if (tid == 0) {
+    f.h_sum[FO_SUM_FLAGS] = fits ? 0 : FO_SUM_F_OVERFLOW;
+    f.h_sum[FO_SUM_TOTAL] = T;
+    f.h_sum[FO_SUM_ENTRIES] = m;
+    f.h_sum[FO_SUM_STATE] = f.ps_count ? *f.ps_count : 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Launch wrappers
 // ------------------------------------------------------------------------------------
 template <int W, int S, int WC, int K>
@@ -1510,6 +1744,14 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K1_S512W: launch_fast_t<4, 512, 1024, 1>(a, ntiles, s); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_small_batch(const SmallArgs& a, hipStream_t s) {
+  if (a.m.n == 0 || a.m.n > SMALL_MAX_N || a.tt == 0 || a.tt > TILE_TOPICS ||
+      (a.m.n + a.tt - 1) / a.tt > SMALL_WAVES)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(small_batch_kernel, dim3(1), dim3(SMALL_WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
 
