@@ -219,6 +219,7 @@ struct emqx_engine {
   std::atomic<uint64_t> last_ordered{0};
   std::atomic<uint64_t> order_bpt{48};  // reordered-batch bytes per topic to provision (learnt)
   std::atomic<double> last_order_ms{0};
+  std::atomic<bool> small_batch{true};  // emqx_set_tuning("small_batch", 0|1): the one-launch path
 };
 
 namespace {
@@ -526,11 +527,10 @@ FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
 // Enqueue one match call on stream s (no host synchronisation): memset of the control
 // words, fast kernel, deep kernel, tile scan (+ summary into `summary`), scatter.  A call on
 // a workspace last used from another stream first waits for that call to drain.
-int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode, const uint8_t* d_tbytes,
-                  const uint64_t* d_toffs, uint64_t n, uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap,
-                  uint64_t* summary, hipStream_t s) {
-  int rc = ensure_ws(w, n);
-  if (rc != EMQX_OK) return rc;
+// The MatchArgs of one call on workspace w (the batched and the small-batch launches).
+MatchArgs match_args(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode, const uint8_t* d_tbytes,
+                     const uint64_t* d_toffs, uint64_t n, uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap,
+                     uint64_t* summary) {
   MatchArgs a{};
   a.tv = snap.tv;
   a.tbytes = d_tbytes;
@@ -565,6 +565,15 @@ int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   a.out_ids = d_out_ids;
   a.out_cap = d_out_ids ? cap : 0;
   a.summary = summary;
+  return a;
+}
+
+int enqueue_match(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode, const uint8_t* d_tbytes,
+                  const uint64_t* d_toffs, uint64_t n, uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap,
+                  uint64_t* summary, hipStream_t s) {
+  int rc = ensure_ws(w, n);
+  if (rc != EMQX_OK) return rc;
+  MatchArgs a = match_args(e, snap, w, mode, d_tbytes, d_toffs, n, d_out_off, d_out_ids, cap, summary);
   const bool ordered = use_order(e, snap, n);
   const uint32_t sort_bits = static_cast<uint32_t>(std::min(64, std::max(1, e->order_sort_bits.load())));
   if (ordered) {
@@ -694,6 +703,45 @@ std::shared_ptr<Snapshot> current(emqx_engine* e) {
   return e->snap;
 }
 
+// A batch the one-launch small path takes (kernels.h SmallArgs): at most SMALL_MAX_N topics of a
+// table within the shallow variant's depth, no walk order, no diagnostic counters.
+bool small_ok(const emqx_engine* e, const Snapshot& snap, uint64_t n) {
+  return e->small_batch.load() && n > 0 && n <= SMALL_MAX_N && snap.max_depth <= 12 && !e->diag_on.load() &&
+         !use_order(e, snap, n);
+}
+
+// Enqueue a small batch as one kernel on s: inputs read from host-mapped pinned memory (copied to
+// d_tbytes / d_toffs on the way), the match CSR into d_out_off / d_out_ids, the summary into
+// host-mapped `summary`; then the CSR into host-mapped h_out_off / h_out_ids (match only), or the
+// fan-out f straight into its pinned buffers.
+int enqueue_small(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t mode, const uint8_t* h_tbytes,
+                  const uint64_t* h_toffs, uint64_t n, uint64_t nbytes, uint8_t* d_tbytes, uint64_t* d_toffs,
+                  uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap, uint64_t* summary, uint64_t* h_out_off,
+                  uint32_t* h_out_ids, uint64_t h_cap, const SmallFanout* f, hipStream_t s) {
+  int rc = ensure_ws(w, n);
+  if (rc != EMQX_OK) return rc;
+  SmallArgs sa{};
+  sa.m = match_args(e, snap, w, mode, d_tbytes, d_toffs, n, d_out_off, d_out_ids, cap, summary);
+  sa.m.diag = nullptr;
+  sa.h_tbytes = h_tbytes;
+  sa.h_toffs = h_toffs;
+  sa.nbytes = nbytes;
+  sa.tt = static_cast<uint32_t>((n + SMALL_WAVES - 1) / SMALL_WAVES);
+  sa.h_out_off = h_out_off;
+  sa.h_out_ids = h_out_ids;
+  sa.h_cap = h_cap;
+  if (f) {
+    sa.has_fanout = 1;
+    sa.f = *f;
+  }
+  HIP_TRY(hipStreamWaitEvent(s, w->done, 0));
+  w->last_stream = s;
+  w->ordered = false;
+  HIP_TRY(launch_small_batch(sa, s));
+  HIP_TRY(hipEventRecord(w->done, s));
+  return EMQX_OK;
+}
+
 // Device side of a pinned host batch (include/emqx_match.h, emqx_host_batch_*).
 struct HostBatchPriv {
   emqx_engine* e = nullptr;
@@ -756,11 +804,30 @@ int hb_enqueue(emqx_host_batch* b) {
   emqx_engine* e = p->e;
   const uint64_t n = b->n, nbytes = n ? b->topic_offsets[n] : 0;
   hipStream_t s = p->stream;
-  if (nbytes) HIP_TRY(hipMemcpyAsync(p->d_tbytes, b->topic_bytes, nbytes, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(p->d_toffs, b->topic_offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   uint64_t* sum_dev = nullptr;
   HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&sum_dev), p->summary, 0));
   p->snap = p->pin ? p->pin : current(e);
+  if (small_ok(e, *p->snap, n)) {  // one launch: the batch read from and the CSR written to pinned memory
+    const uint8_t* h_tb = nullptr;
+    const uint64_t* h_to = nullptr;
+    uint64_t* h_off = nullptr;
+    uint32_t* h_ids = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(const_cast<uint8_t**>(&h_tb)), b->topic_bytes, 0));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(const_cast<uint64_t**>(&h_to)), b->topic_offsets, 0));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_off), b->out_offsets, 0));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_ids), b->out_ids, 0));
+    Workspace* w = acquire_ws(e, s);
+    int rc = enqueue_small(e, *p->snap, w, p->mode, h_tb, h_to, n, nbytes, p->d_tbytes, p->d_toffs, p->d_out_off,
+                           p->d_out_ids, b->cap_ids, sum_dev, h_off, h_ids, b->cap_ids, nullptr, s);
+    if (rc == EMQX_OK) w->inflight = p->snap;
+    release_ws(e, w);
+    if (rc != EMQX_OK) return rc;
+    HIP_TRY(hipEventRecord(p->done, s));
+    p->pending = true;
+    return EMQX_OK;
+  }
+  if (nbytes) HIP_TRY(hipMemcpyAsync(p->d_tbytes, b->topic_bytes, nbytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(p->d_toffs, b->topic_offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   Workspace* w = acquire_ws(e, s);
   int rc = ensure_ws(w, n);
   if (rc == EMQX_OK)
@@ -822,6 +889,25 @@ int hb_wait(emqx_host_batch* b) {
   }
   return (flags & SUM_F_OVERFLOW) ? EMQX_EOVERFLOW : EMQX_OK;
 }
+
+}  // namespace
+
+int emqx::engine_small_batch(emqx_engine* e, uint32_t mode, const uint8_t* h_tbytes, const uint64_t* h_toffs,
+                             uint64_t n, uint64_t nbytes, uint8_t* d_tbytes, uint64_t* d_toffs, uint64_t* d_out_off,
+                             uint32_t* d_out_ids, uint64_t cap, uint64_t* h_summary, const SmallFanout& f,
+                             hipStream_t s) {
+  auto snap = current(e);
+  if (!small_ok(e, *snap, n)) return SMALL_NOT_TAKEN;
+  HIP_TRY(hipSetDevice(e->device));
+  Workspace* w = acquire_ws(e, s);
+  int rc = enqueue_small(e, *snap, w, mode, h_tbytes, h_toffs, n, nbytes, d_tbytes, d_toffs, d_out_off, d_out_ids,
+                         cap, h_summary, nullptr, nullptr, 0, &f, s);
+  if (rc == EMQX_OK) w->inflight = snap;
+  release_ws(e, w);
+  return rc;
+}
+
+namespace {
 
 bool offsets_ok(const uint64_t* offs, uint64_t n) {
   if (!offs) return n == 0;
@@ -1245,6 +1331,10 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value) {
       HIP_TRY(hipMemset(e->timeline, 0, static_cast<uint64_t>(value) * sizeof(uint4)));
       e->timeline_cap = static_cast<uint64_t>(value);
     }
+    return EMQX_OK;
+  }
+  if (std::strcmp(key, "small_batch") == 0) {  // host batches of <= SMALL_MAX_N topics in one launch
+    e->small_batch.store(value != 0);
     return EMQX_OK;
   }
   if (std::strcmp(key, "incremental") == 0) {

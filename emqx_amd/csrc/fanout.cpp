@@ -1419,6 +1419,8 @@ struct PubBatchPriv {
   uint32_t* d_ofil = nullptr;
   uint64_t* d_msum = nullptr;  // match summary (8 words) then fan-out summary (4 words)
   uint64_t* h_sums = nullptr;  // pinned copy of both
+  uint4* d_erec = nullptr;     // one-launch small path: per match entry its record and topic
+  uint32_t* d_etop = nullptr;
   uint64_t mids_per_topic = 16;  // learnt match ids per topic (sizes d_mids)
   uint64_t limit = ~0ull;        // deliveries the submission may write (<= cap_out): a call that
                                  // needs more writes no ids and consumes no pick state
@@ -1521,10 +1523,67 @@ int pb_enqueue_fanout(emqx_pub_batch* b, uint64_t m_cap, const uint64_t* msum) {
   return EMQX_OK;
 }
 
+// The one-launch small path (kernels.h SmallArgs): match and stateless fan-out in one kernel that
+// reads the pinned inputs and writes the pinned outputs and both summaries itself.  Returns
+// SMALL_NOT_TAKEN (nothing enqueued) when the batch or the strategy does not qualify.
+int pb_enqueue_small(emqx_pub_batch* b, uint64_t nbytes) {
+  auto* p = static_cast<PubBatchPriv*>(b->priv);
+  emqx_subtab* s = p->s;
+  if (fo_stateful(p->strategy) || b->n == 0 || b->n > SMALL_MAX_N) return SMALL_NOT_TAKEN;
+  hipStream_t st = p->stream;
+  if (!p->d_erec) {
+    FO_TRY(fo_alloc(p->d_erec, SMALL_FO_MAX_ENTRIES));
+    FO_TRY(fo_alloc(p->d_etop, SMALL_FO_MAX_ENTRIES));
+  }
+  const uint64_t want = p->mids_per_topic * b->n + 1024;
+  if (want > p->cap_mids) {
+    p->cap_mids = want + want / 4;
+    FO_TRY(fo_alloc(p->d_mids, p->cap_mids));
+  }
+  std::lock_guard<std::mutex> g(s->mu);
+  FoScratch* c = scratch_for(s, st);  // (its done event orders later commits after this fan-out)
+  if (!c) return EMQX_EDEVICE;
+  if (s->commit_pending) FO_TRY(hipStreamWaitEvent(st, s->commit_ev, 0));
+  SmallFanout f{};
+  f.recs = reinterpret_cast<const uint4*>(s->d_recs.p);
+  f.n_recs = s->dev_n_recs;
+  f.plain = s->d_plain.p;
+  f.groups = reinterpret_cast<const uint4*>(s->d_groups.p);
+  f.members = s->d_members.p;
+  f.strategy = p->strategy;
+  s->seed = s->seed * 1664525u + 1013904223u;
+  f.seed = s->seed;
+  f.h_keys = p->use_keys ? mapped(b->keys) : nullptr;
+  f.d_keys = p->d_keys;
+  f.erec = p->d_erec;
+  f.etop = p->d_etop;
+  f.ps_count = s->ps_count;
+  f.h_off = mapped(b->out_offsets);
+  f.h_subs = mapped(b->out_subs);
+  f.h_fil = mapped(b->out_filters);
+  f.cap = std::min(b->cap_out, p->limit);
+  f.h_sum = mapped(p->h_sums) + PB_MSUM_WORDS;
+  int rc = engine_small_batch(p->e, EMQX_MODE_ROUTES, mapped(b->topic_bytes), mapped(b->topic_offsets), b->n, nbytes,
+                              p->d_tbytes, p->d_toffs, p->d_moff, p->d_mids, p->cap_mids, mapped(p->h_sums), f, st);
+  if (rc != EMQX_OK) return rc;
+  FO_TRY(hipEventRecord(c->done, st));
+  c->used = true;
+  return EMQX_OK;
+}
+
 int pb_enqueue(emqx_pub_batch* b) {
   auto* p = static_cast<PubBatchPriv*>(b->priv);
   const uint64_t n = b->n, nbytes = n ? b->topic_offsets[n] : 0;
   hipStream_t st = p->stream;
+  {
+    const int rc = pb_enqueue_small(b, nbytes);
+    if (rc == EMQX_OK) {
+      FO_TRY(hipEventRecord(p->done, st));
+      p->pending = true;
+      return EMQX_OK;
+    }
+    if (rc != SMALL_NOT_TAKEN) return rc;
+  }
   if (nbytes) FO_TRY(hipMemcpyAsync(p->d_tbytes, b->topic_bytes, nbytes, hipMemcpyHostToDevice, st));
   FO_TRY(hipMemcpyAsync(p->d_toffs, b->topic_offsets, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   if (p->use_keys && n) FO_TRY(hipMemcpyAsync(p->d_keys, b->keys, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
@@ -1575,6 +1634,11 @@ int pb_wait(emqx_pub_batch* b) {
     p->mids_per_topic = std::max<uint64_t>(p->mids_per_topic, m / std::max<uint64_t>(b->n, 1) + 1);
   } else if (b->n) {
     p->mids_per_topic = std::max<uint64_t>(4, (ms[1] + ms[1] / 4) / b->n + 1);
+  }
+  if (fs[FO_SUM_FLAGS] & FO_SUM_F_SMALL) {  // the one-launch path's fan-out did not fit: batched kernels
+    int rc = pb_enqueue_fanout(b, p->cap_mids, nullptr);
+    if (rc != EMQX_OK) return rc;
+    FO_TRY(hipStreamSynchronize(p->stream));
   }
   // round_robin / sticky state table or pick scratch too small: nothing was consumed; grow, rerun
   for (int attempt = 0; (fs[FO_SUM_FLAGS] & FO_SUM_F_RERUN) && !(fs[FO_SUM_FLAGS] & ~FO_SUM_F_RERUN); ++attempt) {
@@ -2037,6 +2101,8 @@ int emqx_pub_batch_destroy(emqx_pub_batch* b) {
   fo_free(p->d_osubs);
   fo_free(p->d_ofil);
   fo_free(p->d_msum);
+  fo_free(p->d_erec);
+  fo_free(p->d_etop);
   {  // the subtab keeps a scratch per stream: it goes with the stream
     std::lock_guard<std::mutex> g(p->s->mu);
     auto& v = p->s->scratch;

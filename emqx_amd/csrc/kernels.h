@@ -156,6 +156,16 @@ struct SmallArgs {
   SmallFanout f;
 };
 hipError_t launch_small_batch(const SmallArgs& a, hipStream_t s);
+}  // namespace emqx
+struct emqx_engine;
+namespace emqx {
+// engine.cpp, for the publish batches (fanout.cpp): a small batch's match and stateless fan-out
+// as one launch on s.  SMALL_NOT_TAKEN (> 0): the batch does not qualify and nothing was
+// enqueued (the caller runs the batched pipeline).
+constexpr int SMALL_NOT_TAKEN = 1;
+int engine_small_batch(emqx_engine* e, uint32_t mode, const uint8_t* h_tbytes, const uint64_t* h_toffs, uint64_t n,
+                       uint64_t nbytes, uint8_t* d_tbytes, uint64_t* d_toffs, uint64_t* d_out_off, uint32_t* d_out_ids,
+                       uint64_t cap, uint64_t* h_summary, const SmallFanout& f, hipStream_t s);
 
 // Deep path: waves of match_deep_kernel, slab entries each wave reserves per atomic, and the
 // padding value of a reserved entry left unused.

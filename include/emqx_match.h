@@ -551,7 +551,9 @@ int emqx_topic_wildcard(const uint8_t* topic, uint64_t len);
  * diagnostic counters), "incremental" (0 = every commit rebuilds), "delta_max" (filters placed
  * incrementally before a rebuild, -1 = default policy), "commit_threads" (host threads of an
  * incremental commit, default min(8, cores)), "timeline" (tiles of emqx_diag_timeline to record,
- * 0 = off).  EMQX_ENOTFOUND for unknown keys. */
+ * 0 = off), "small_batch" (1 = default: host / publish batches of at most 1024 topics run as one
+ * kernel launch that reads the pinned inputs and writes the pinned outputs itself; 0 = the
+ * batched pipeline).  EMQX_ENOTFOUND for unknown keys. */
 int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value);
 /* Reads (and optionally resets) the accumulated diagnostic counters (DIAG_* order). */
 int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset);
