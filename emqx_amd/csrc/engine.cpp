@@ -264,6 +264,9 @@ int full_commit(emqx_engine* e) {
   HIP_TRY(hipMemcpy(dt->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
+  // a copy from pageable memory may return before its DMA lands, and the match streams do not
+  // follow the null stream: the tables are on the device before the snapshot is published
+  HIP_TRY(hipStreamSynchronize(nullptr));
 
   auto s = std::make_shared<Snapshot>();
   s->dt = dt;

@@ -303,6 +303,7 @@ struct emqx_subtab {
   bool bulk = false;                          // so many that the next commit rebuilds: no dirt kept
   // ---- device ----
   DevArr<FilterRec> d_recs;
+  DevArr<uint32_t> d_fcnt;  // fo_cnt_word of each device record (written with it, on the device)
   DevArr<uint32_t> d_plain, d_members;
   DevArr<GroupRec> d_groups;
   DevArr<uint32_t> d_alive;
@@ -751,6 +752,15 @@ int full_commit(emqx_subtab* s) {
     drecs[f] = FilterRec{v.x, v.y, v.z, v.w};
   }
   int rc = up(recs, drecs);
+  DevArr<uint32_t> fcnt;
+  if (rc == EMQX_OK) {
+    fcnt.cap = recs.cap;
+    if (hipMalloc(reinterpret_cast<void**>(&fcnt.p), fcnt.cap * sizeof(uint32_t)) != hipSuccess) rc = EMQX_ENOMEM;
+    if (rc == EMQX_OK && hipMemsetAsync(fcnt.p, 0, fcnt.cap * sizeof(uint32_t), s->stream) != hipSuccess)
+      rc = EMQX_EDEVICE;
+    if (rc == EMQX_OK && launch_fcnt_from_recs(recs.p, drecs.size(), fcnt.p, s->stream) != hipSuccess)
+      rc = EMQX_EDEVICE;
+  }
   if (rc == EMQX_OK) rc = up(plain, s->plain);
   if (rc == EMQX_OK) rc = up(groups, s->groups);
   if (rc == EMQX_OK) rc = up(members, s->members);
@@ -758,6 +768,7 @@ int full_commit(emqx_subtab* s) {
   if (rc == EMQX_OK && hipStreamSynchronize(s->stream) != hipSuccess) rc = EMQX_EDEVICE;
   if (rc != EMQX_OK) {
     fo_free(recs.p);
+    fo_free(fcnt.p);
     fo_free(plain.p);
     fo_free(groups.p);
     fo_free(members.p);
@@ -765,11 +776,13 @@ int full_commit(emqx_subtab* s) {
     return rc;
   }
   fo_free(s->d_recs.p);
+  fo_free(s->d_fcnt.p);
   fo_free(s->d_plain.p);
   fo_free(s->d_groups.p);
   fo_free(s->d_members.p);
   fo_free(s->d_alive.p);
   s->d_recs = recs;
+  s->d_fcnt = fcnt;
   s->d_plain = plain;
   s->d_groups = groups;
   s->d_members = members;
@@ -993,6 +1006,7 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
     s->stage_cap = rc == EMQX_OK ? cap : 0;
   }
   if (rc == EMQX_OK) rc = dev_reserve(s, s->d_recs, s->recs.size(), s->dev_n_recs, retired);
+  if (rc == EMQX_OK) rc = dev_reserve(s, s->d_fcnt, s->recs.size(), s->dev_n_recs, retired);
   if (rc == EMQX_OK) rc = dev_reserve(s, s->d_plain, s->plain.size(), s->d_plain.cap, retired);
   if (rc == EMQX_OK) rc = dev_reserve(s, s->d_members, s->members.size(), s->d_members.cap, retired);
   if (rc == EMQX_OK) rc = dev_reserve(s, s->d_groups, s->groups.size(), s->d_groups.cap, retired);
@@ -1014,7 +1028,7 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
   up(s->d_rpatch.p, s->rpatch.data(), rp_bytes);
   if (rc == EMQX_OK &&
       launch_subtab_patches(s->d_plain.p, s->d_members.p, s->d_alive.p, s->d_wpatch.p, n_plain_w, n_member_w,
-                            n_alive_w, s->d_groups.p, s->d_recs.p, s->d_rpatch.p, n_group_p, n_rec_p,
+                            n_alive_w, s->d_groups.p, s->d_recs.p, s->d_fcnt.p, s->d_rpatch.p, n_group_p, n_rec_p,
                             s->stream) != hipSuccess)
     rc = EMQX_EDEVICE;
   if (rc != EMQX_OK) {
@@ -1267,6 +1281,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   // (c->ctl is zeroed by the call's first kernel, fanout_entry_topic)
   FanoutArgs a{};
   a.recs = s->d_recs.p;
+  a.fcnt = s->d_fcnt.p;
   a.n_recs = s->dev_n_recs;
   a.plain = s->d_plain.p;
   a.groups = s->d_groups.p;
@@ -1435,6 +1450,7 @@ emqx_subtab::~emqx_subtab() {
     if (c->used) (void)hipEventSynchronize(c->done);
   for (emqx_pub_batch* b : pb_free) emqx_pub_batch_destroy(b);
   fo_free(d_recs.p);
+  fo_free(d_fcnt.p);
   fo_free(d_plain.p);
   fo_free(d_groups.p);
   fo_free(d_members.p);

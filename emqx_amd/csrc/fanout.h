@@ -38,6 +38,16 @@ constexpr uint32_t FO_INLINE_BIT = 0x80000000u;
 __host__ __device__ inline uint32_t fo_rec_plain(uint4 r) { return r.y & ~FO_INLINE_BIT; }
 __host__ __device__ inline uint32_t fo_rec_groups(uint4 r) { return (r.y & FO_INLINE_BIT) ? 0u : r.w; }
 
+// The count pass's dense per-filter word (4 B, maintained on the device from each record it
+// writes): deliveries (n_plain + n_groups) in bits 0..23 and $share groups in bits 24..31, each
+// saturated; a saturated word sends the count pass to the 16-B record.  Ten per 64-B line where
+// the records fit four, so the count pass's random reads mostly hit in L2.
+constexpr uint32_t FO_CNT_DELIV_MAX = 0xFFFFFFu, FO_CNT_GROUPS_MAX = 0xFFu;
+__host__ __device__ inline uint32_t fo_cnt_word(uint4 r) {
+  const uint32_t d = fo_rec_plain(r) + fo_rec_groups(r), g = fo_rec_groups(r);
+  return (d >= FO_CNT_DELIV_MAX || g >= FO_CNT_GROUPS_MAX) ? 0xFFFFFFFFu : (d | (g << 24));
+}
+
 // Per ($share group, filter) with members (16 B).
 struct GroupRec {
   uint32_t member_begin;  // first entry in members[] (subscription order)
@@ -71,6 +81,7 @@ __host__ __device__ inline bool fo_alive(const uint32_t* alive, uint32_t n_words
 
 struct FanoutArgs {
   const FilterRec* recs;
+  const uint32_t* fcnt;      // [n_recs] fo_cnt_word of each record (the count pass's dense copy)
   uint32_t n_recs;           // filter ids >= n_recs have no subscribers
   const uint32_t* plain;
   const GroupRec* groups;
@@ -209,8 +220,10 @@ struct WordPatch {
 // liveness bitmap alive[] (n_alive_w).
 hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, uint32_t* alive, const WordPatch* wp,
                                  uint64_t n_plain_w, uint64_t n_member_w, uint64_t n_alive_w, GroupRec* groups,
-                                 FilterRec* recs, const RecPatch* rp, uint64_t n_group_p, uint64_t n_rec_p,
-                                 hipStream_t s);
+                                 FilterRec* recs, uint32_t* fcnt, const RecPatch* rp, uint64_t n_group_p,
+                                 uint64_t n_rec_p, hipStream_t s);
+// fcnt[i] = fo_cnt_word(recs[i]) for i < n (a full upload).
+hipError_t launch_fcnt_from_recs(const FilterRec* recs, uint64_t n, uint32_t* fcnt, hipStream_t s);
 
 // Pick-state table maintenance: rehash into a larger table; drop the keys of the given
 // publishers (sorted, unique).

@@ -142,12 +142,19 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) 
       f[u] = i < hi ? a.mids[base + i] : FID_NONE;
     }
     uint64_t cs = 0, gl = 0;
+    uint32_t w[EU];
+#pragma unroll
+    for (uint32_t u = 0; u < EU; ++u) w[u] = f[u] < a.n_recs ? a.fcnt[f[u]] : 0u;
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
-      const bool in = f[u] < a.n_recs;
-      const uint4 r = *reinterpret_cast<const uint4*>(a.recs + (in ? f[u] : 0u));
-      cs += in ? fo_rec_plain(r) + fo_rec_groups(r) : 0u;
-      gl += in ? fo_rec_groups(r) : 0u;
+      if (w[u] == 0xFFFFFFFFu) {  // saturated: the record itself (a filter with 16 M deliveries)
+        const uint4 r = *reinterpret_cast<const uint4*>(a.recs + f[u]);
+        cs += fo_rec_plain(r) + fo_rec_groups(r);
+        gl += fo_rec_groups(r);
+      } else {
+        cs += w[u] & FO_CNT_DELIV_MAX;
+        gl += w[u] >> 24;
+      }
     }
     cs = fo_wave_sum(cs);
     gl = fo_wave_sum(gl);
@@ -893,14 +900,23 @@ __global__ __launch_bounds__(256) void subtab_word_patch_kernel(uint32_t* plain,
 }
 
 // Whole 16-B records (one dwordx4 store each): a reader sees a record old or new.
-__global__ __launch_bounds__(256) void subtab_rec_patch_kernel(GroupRec* groups, FilterRec* recs,
+__global__ __launch_bounds__(256) void subtab_rec_patch_kernel(GroupRec* groups, FilterRec* recs, uint32_t* fcnt,
                                                                const RecPatch* rp, uint64_t n_groups,
                                                                uint64_t n_total) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n_total; i += uint64_t(gridDim.x) * 256) {
     const RecPatch p = rp[i];
-    uint4* dst = i < n_groups ? reinterpret_cast<uint4*>(groups + p.index) : reinterpret_cast<uint4*>(recs + p.index);
-    *dst = p.value;
+    if (i < n_groups) {
+      *reinterpret_cast<uint4*>(groups + p.index) = p.value;
+    } else {
+      *reinterpret_cast<uint4*>(recs + p.index) = p.value;
+      fcnt[p.index] = fo_cnt_word(p.value);
+    }
   }
+}
+
+__global__ __launch_bounds__(256) void fcnt_from_recs_kernel(const FilterRec* recs, uint64_t n, uint32_t* fcnt) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+    fcnt[i] = fo_cnt_word(*reinterpret_cast<const uint4*>(recs + i));
 }
 
 __global__ __launch_bounds__(256) void ps_rehash_kernel(const uint64_t* old_keys, const uint32_t* old_vals,
@@ -1019,19 +1035,26 @@ hipError_t launch_share_repick(const RepickArgs& a, hipStream_t s) {
 
 hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, uint32_t* alive, const WordPatch* wp,
                                  uint64_t n_plain_w, uint64_t n_member_w, uint64_t n_alive_w, GroupRec* groups,
-                                 FilterRec* recs, const RecPatch* rp, uint64_t n_group_p, uint64_t n_rec_p,
-                                 hipStream_t s) {
+                                 FilterRec* recs, uint32_t* fcnt, const RecPatch* rp, uint64_t n_group_p,
+                                 uint64_t n_rec_p, hipStream_t s) {
   // words first (the lists), then the records that point at them
   const uint64_t nw = n_plain_w + n_member_w + n_alive_w;
   if (nw)
     hipLaunchKernelGGL(subtab_word_patch_kernel, dim3(grid_for(nw, 256)), dim3(256), 0, s, plain, members, alive, wp,
                        n_plain_w, n_plain_w + n_member_w, nw);
   if (n_group_p)
-    hipLaunchKernelGGL(subtab_rec_patch_kernel, dim3(grid_for(n_group_p, 256)), dim3(256), 0, s, groups, recs, rp,
-                       n_group_p, n_group_p);
+    hipLaunchKernelGGL(subtab_rec_patch_kernel, dim3(grid_for(n_group_p, 256)), dim3(256), 0, s, groups, recs, fcnt,
+                       rp, n_group_p, n_group_p);
   if (n_rec_p)
-    hipLaunchKernelGGL(subtab_rec_patch_kernel, dim3(grid_for(n_rec_p, 256)), dim3(256), 0, s, groups, recs,
+    hipLaunchKernelGGL(subtab_rec_patch_kernel, dim3(grid_for(n_rec_p, 256)), dim3(256), 0, s, groups, recs, fcnt,
                        rp + n_group_p, uint64_t(0), n_rec_p);
+  return hipGetLastError();
+}
+
+hipError_t launch_fcnt_from_recs(const FilterRec* recs, uint64_t n, uint32_t* fcnt, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(fcnt_from_recs_kernel, dim3(std::min<uint32_t>(grid_for(n, 256), 4096)), dim3(256), 0, s,
+                       recs, n, fcnt);
   return hipGetLastError();
 }
 

@@ -1526,6 +1526,17 @@ __device__ __forceinline__ uint64_t small_block_scan(uint64_t v, uint64_t* total
   return before + incl - v;
 }
 
+// A phase boundary of the small-batch kernel: the phases hand data to each other through global
+// memory (counts, slabs, the deferred list, control words updated by atomics in L2), so every
+// wave's writes are made visible at agent scope before the barrier, and every wave's vector L1
+// is invalidated after it — a line read before the barrier (a control word, say) must not be
+// served stale from L1 after it.
+__device__ __forceinline__ void small_phase_barrier() {
+  __threadfence();
+  __syncthreads();
+  __threadfence();
+}
+
 // Largest i in [0, n) with v[i] <= x (v non-decreasing, v[0] <= x).
 __device__ __forceinline__ uint32_t small_floor(const uint32_t* v, uint32_t n, uint32_t x) {
   uint32_t lo = 0, hi = n;
@@ -1568,19 +1579,19 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
     if (sa.has_fanout && sa.f.h_keys)
       for (uint64_t i = tid; i < n; i += NT) sa.f.d_keys[i] = sa.f.h_keys[i];
   }
-  __syncthreads();
+  small_phase_barrier();
 
   // 1. the walk: wave w takes tile w (tt topics); 2. deferred topics on every wave
   const uint32_t tt = sa.tt;
   const uint64_t ntiles = (n + tt - 1) / tt;
   if (wv < ntiles) fast_tile<SC, WC, 1, false>(a, lds.w[wv], wv, tt);
-  __syncthreads();
-  if (__hip_atomic_load(&a.ctrl[CTRL_DEFERRED], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-    deep_walk(a, wv, SMALL_WAVES, tt);
-  __syncthreads();
+  small_phase_barrier();
+  auto ctrl = [&](uint32_t k) { return __hip_atomic_load(&a.ctrl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  if (ctrl(CTRL_DEFERRED)) deep_walk(a, wv, SMALL_WAVES, tt);
+  small_phase_barrier();
 
   uint64_t* sm = a.summary;
-  const uint32_t need = a.ctrl[CTRL_NEED_SLAB], err = a.ctrl[CTRL_ERROR];
+  const uint32_t need = ctrl(CTRL_NEED_SLAB), err = ctrl(CTRL_ERROR);
   uint64_t flags = 0;
   if (need > a.slab_cap || (err & (CTRL_ERR_DEEP_SLAB | CTRL_ERR_TOO_DEEP))) flags |= SUM_F_RETRY;
   if (err & CTRL_ERR_TOO_LONG) flags |= SUM_F_ERROR;
@@ -1594,13 +1605,13 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
     if (tid == 0) a.out_off[n] = total;
   }
   if (total > a.out_cap) flags |= SUM_F_OVERFLOW;
-  __syncthreads();
+  small_phase_barrier();
   if (!(flags & (SUM_F_RETRY | SUM_F_ERROR))) {
     if (wv < ntiles) {
       const uint64_t t = uint64_t(wv) * tt + lane;
       scatter_tile(a, wv, (lane < tt && t < n) ? a.out_off[t] : 0);
     }
-    const uint32_t fill = min(a.ctrl[CTRL_DEEP_FILL], a.deep_slab_cap);
+    const uint32_t fill = min(ctrl(CTRL_DEEP_FILL), a.deep_slab_cap);
     for (uint32_t i = tid; i < fill; i += NT) {
       const uint64_t e = a.deep_slab[i];
       if (e == DEEP_PAD) continue;
@@ -1609,9 +1620,9 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
       if (p < a.out_cap) a.out_ids[p] = resolve_entry(a.tv, e);
     }
   }
-  __syncthreads();
+  small_phase_barrier();
   if (tid == 0) {
-    uint64_t ev = a.ctrl[CTRL_DEEP_EVALS];
+    uint64_t ev = ctrl(CTRL_DEEP_EVALS);
     uint32_t mx = 0;
     for (uint64_t k = 0; k < ntiles; ++k) {
       const uint2 st = a.tile_stats[k];
@@ -1621,9 +1632,9 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
     sm[SUM_TOTAL] = total;
     sm[SUM_EVALS] = ev;
     sm[SUM_MAXSTACK] = mx;
-    sm[SUM_DEFERRED] = a.ctrl[CTRL_DEFERRED];
+    sm[SUM_DEFERRED] = ctrl(CTRL_DEFERRED);
     sm[SUM_NEED_SLAB] = need;
-    sm[SUM_DEEP_FILL] = a.ctrl[CTRL_DEEP_FILL];
+    sm[SUM_DEEP_FILL] = ctrl(CTRL_DEEP_FILL);
     sm[SUM_ERROR] = err;
     sm[SUM_FLAGS] = flags;
   }
@@ -1659,7 +1670,7 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
   uint32_t* D = lds.f.D;
   uint32_t* off = lds.f.off;
   for (uint64_t t = tid; t <= n; t += NT) off[t] = static_cast<uint32_t>(a.out_off[t]);
-  __syncthreads();
+  small_phase_barrier();
   // pass 1: each entry's record and topic; exclusive scan of the deliveries
   uint64_t T = 0;
   for (uint32_t e0 = 0; e0 < m; e0 += NT) {
@@ -1678,7 +1689,7 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
     T += tc;
   }
   if (tid == 0) D[m] = static_cast<uint32_t>(min<uint64_t>(T, 0xFFFFFFFFull));
-  __syncthreads();
+  small_phase_barrier();
   for (uint64_t t = tid; t <= n; t += NT) f.h_off[t] = t < n ? D[off[t]] : T;
   const bool fits = T <= f.cap;
   // pass 2: deliveries j, lane-consecutive (coalesced stores); each finds its entry in LDS

@@ -492,6 +492,9 @@ int build_and_upload(emqx_retain* r, std::shared_ptr<RSnapshot>* out) {
     RT_TRY(hipMemcpy(sn->rank_id, rank_id.data(), rank_id.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     RT_TRY(hipMemcpy(sn->rank_exp, rank_exp.data(), rank_exp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
   }
+  // the copies' DMA has landed before the snapshot is used from another stream (pageable
+  // copies may return early; the walk streams do not follow the null stream)
+  RT_TRY(hipStreamSynchronize(nullptr));
   RetainView& rv = sn->rv;
   rv.root_ncld = nn ? nodes[0].ncld : 0u;
   rv.root_lo = nn ? nodes[0].lo : 0u;

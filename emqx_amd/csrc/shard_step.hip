@@ -488,6 +488,7 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->d_splits), std::max<uint64_t>(8ull * n_splits, 16));
   if (e == hipSuccess && n_splits)
     e = hipMemcpy(st->d_splits, splits, 8ull * n_splits, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // (the DMA has landed: steps run on other streams)
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->start), 4ull * (2 * world + 2));
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->cbase), 8ull * world);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->err), 16);
