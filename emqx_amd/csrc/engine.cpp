@@ -260,10 +260,34 @@ int full_commit(emqx_engine* e) {
   HIP_TRY(dalloc(dt->fids, 2 * dt->cap_slots));
   HIP_TRY(dalloc(dt->vocab, dt->n_vocab));
   HIP_TRY(dalloc(dt->arena, dt->cap_arena));
+  if (getenv("EMQX_TABLE_ZERO")) {  // (diagnostic: the allocations' previous contents cleared)
+    HIP_TRY(hipMemset(dt->edges, 0, dt->cap_slots * sizeof(EdgeSlot)));
+    HIP_TRY(hipMemset(dt->fids, 0, 2 * dt->cap_slots * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(dt->vocab, 0, dt->n_vocab * sizeof(VocabSlot)));
+    HIP_TRY(hipMemset(dt->arena, 0, dt->cap_arena));
+  }
+  if (getenv("EMQX_UPLOAD_KERNEL")) {  // (diagnostic: uploads by a kernel through L2, from pinned staging)
+    auto kup = [&](void* dst, const void* src, uint64_t bytes) -> hipError_t {
+      if (!bytes) return hipSuccess;
+      void* h = nullptr;
+      hipError_t r = hipHostMalloc(&h, bytes, hipHostMallocDefault);
+      if (r != hipSuccess) return r;
+      std::memcpy(h, src, bytes);
+      r = launch_copy_in(h, dst, bytes, nullptr);
+      if (r == hipSuccess) r = hipStreamSynchronize(nullptr);
+      (void)hipHostFree(h);
+      return r;
+    };
+    HIP_TRY(kup(dt->edges, ht.edges.data(), n_slots * sizeof(EdgeSlot)));
+    HIP_TRY(kup(dt->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t)));
+    HIP_TRY(kup(dt->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot)));
+    HIP_TRY(kup(dt->arena, ht.arena.data(), ht.arena.size()));
+  } else {
   HIP_TRY(hipMemcpy(dt->edges, ht.edges.data(), n_slots * sizeof(EdgeSlot), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
+  }
   // a copy from pageable memory may return before its DMA lands, and the match streams do not
   // follow the null stream: the tables are on the device before the snapshot is published
   HIP_TRY(hipStreamSynchronize(nullptr));
@@ -721,7 +745,9 @@ int enqueue_small(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
                   const uint64_t* h_toffs, uint64_t n, uint64_t nbytes, uint8_t* d_tbytes, uint64_t* d_toffs,
                   uint64_t* d_out_off, uint32_t* d_out_ids, uint64_t cap, uint64_t* summary, uint64_t* h_out_off,
                   uint32_t* h_out_ids, uint64_t h_cap, const SmallFanout* f, hipStream_t s) {
-  int rc = ensure_ws(w, n);
+  // the workspace sized for SMALL_WAVES tiles whatever n: the kernel's tiles are ceil(n / 16)
+  // topics wide, so a batch of a few topics still spans up to 16 slab tiles
+  int rc = ensure_ws(w, SMALL_MAX_N);
   if (rc != EMQX_OK) return rc;
   SmallArgs sa{};
   sa.m = match_args(e, snap, w, mode, d_tbytes, d_toffs, n, d_out_off, d_out_ids, cap, summary);
@@ -730,6 +756,7 @@ int enqueue_small(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   sa.h_toffs = h_toffs;
   sa.nbytes = nbytes;
   sa.tt = static_cast<uint32_t>((n + SMALL_WAVES - 1) / SMALL_WAVES);
+  sa.slab_tiles = static_cast<uint32_t>(std::min<uint64_t>(w->cap_slab / w->slab_per_tile, w->cap_tiles));
   sa.h_out_off = h_out_off;
   sa.h_out_ids = h_out_ids;
   sa.h_cap = h_cap;

@@ -149,6 +149,7 @@ struct SmallArgs {
   const uint64_t* h_toffs;
   uint64_t nbytes;
   uint32_t tt;              // topics per tile: ceil(n / SMALL_WAVES)
+  uint32_t slab_tiles;      // tiles the workspace's slab holds (>= the batch's tiles: checked at launch)
   uint32_t has_fanout;
   uint64_t* h_out_off;      // match only: the CSR into host-mapped buffers (null: not copied)
   uint32_t* h_out_ids;
@@ -156,6 +157,8 @@ struct SmallArgs {
   SmallFanout f;
 };
 hipError_t launch_small_batch(const SmallArgs& a, hipStream_t s);
+// bytes from host-mapped (pinned) h_src into device memory by a kernel (through L2)
+hipError_t launch_copy_in(const void* h_src, void* d_dst, uint64_t bytes, hipStream_t s);
 }  // namespace emqx
 struct emqx_engine;
 namespace emqx {

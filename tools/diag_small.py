@@ -19,6 +19,24 @@ def main():
     filters, topics = _deep_topic_batch()
     exp = [R.brute_force_routes(filters, t) for t in topics]
     runs = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    if len(sys.argv) > 2:  # the test module's earlier tests first: a 150K-filter engine, host batches
+        import numpy as np
+        from emqx_amd import workloads as W
+        from test_gpu_small_batch import _host_batch
+        wl = W.config_b(n_filters=150_000, n_topics=4096, seed=41)
+        t = Engine()
+        t.insert_packed(*wl.filters)
+        t.commit()
+        modes = {"s1": (1,), "s0": (0,), "both": (1, 0)}[sys.argv[2]]
+        sizes = (1, 3, 17, 48, 64, 65, 200, 511, 1024, 1025) if len(sys.argv) < 4 else tuple(map(int, sys.argv[3].split(",")))
+        for n in sizes:
+            for small in modes:
+                t.set_tuning("small_batch", small)
+                _host_batch(t, W.take(wl.topics, np.arange(100, 100 + n)), 0)
+        t.set_tuning("small_batch", 1)
+        if os.environ.get("DIAG_CLOSE"):
+            t.close()
+        print("prefix done", flush=True)
     for r in range(runs):
         e = Engine()
         e.insert(filters)
@@ -31,6 +49,9 @@ def main():
             line.append((small, bad[:3]))
         st = e.stats()
         print(r, line, {k: st[k] for k in ("last_evals", "last_deferred", "n_words", "n_slots")}, flush=True)
+        print("  a/b/c ->", e.match([b"a/b/c"], mode=0), "expect", [R.brute_force_routes(filters, b"a/b/c")], flush=True)
+        print("  lookup +/+/c/# ->", e.lookup(b"+/+/c/#"), "index", filters.index(b"+/+/c/#"), flush=True)
+        print("  stats", st, flush=True)
         e.close()
 
 
