@@ -234,7 +234,7 @@ struct emqx_retain {
   std::atomic<uint32_t> tile{0}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_decay{0}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
       walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP}, balance{BALANCE_QUEUE},
       queue_piece{QUEUE_PIECE}, queue_check{QUEUE_CHECK}, queue_cap{QUEUE_CAP}, queue_wait{QUEUE_MAX_WAIT},
-      queue_sleep{QUEUE_SLEEP}, queue_shards{QUEUE_SHARDS}, queue_roam{QUEUE_ROAM};
+      queue_sleep{QUEUE_SLEEP}, queue_shards{QUEUE_SHARDS}, queue_roam{QUEUE_ROAM}, queue_poll_limit{QUEUE_POLL_LIMIT};
 };
 
 namespace {
@@ -636,7 +636,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   a.queue_cap = std::min<uint32_t>(w->queue_cap, r->queue_cap.load());
   a.qpiece = std::max<uint32_t>(64, r->queue_piece.load());
   a.qcheck = r->queue_check.load();
-  a.qpoll_limit = QUEUE_POLL_LIMIT;
+  a.qpoll_limit = r->queue_poll_limit.load();
   a.qmaxwait = r->queue_wait.load();
   a.qsleep = r->queue_sleep.load();
   a.qroam = std::min<uint32_t>(r->queue_roam.load(), a.qshards - 1);
@@ -686,8 +686,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     for (uint32_t k = 0; !queue && k <= rounds; ++k) {
       RetainArgs b = a;
       b.waves = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(spill_waves, fit)));
-      const uint32_t in_word = RC_SPILL + k;
-      b.spill_word = in_word + 1;
+      const uint32_t in_word = RC_SPILL + 2 * k;
+      b.spill_word = in_word + 2;
       b.spill_out = w->spill[(k + 1) & 1];
       if (k == rounds) b.step_budget = ~0u;  // the last round finishes every stack
       else if (spill_budget) b.step_budget = std::max<uint32_t>(8u, spill_budget >> std::min<uint32_t>(k * spill_decay, 31u));
@@ -1061,6 +1061,9 @@ int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
   } else if (std::strcmp(key, "queue_cap") == 0) {
     if (v < 64 || v > QUEUE_CAP) return EMQX_EINVAL;
     r->queue_cap = v;
+  } else if (std::strcmp(key, "queue_poll_limit") == 0) {  // the safety valve (tests force it: 1)
+    if (v < 1) return EMQX_EINVAL;
+    r->queue_poll_limit = v;
   } else {
     return EMQX_ENOTFOUND;
   }

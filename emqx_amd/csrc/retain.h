@@ -151,11 +151,12 @@ enum RCtrl : uint32_t {
   RC_STAT = 64,
   RC_STAT_LINES = 16,
   RC_QABORT = 320,  // queue mode: a waiting wave gave up (poll limit); the host reruns in spill mode
-  RC_SPILL = 384,   // items spilled by the walk; RC_SPILL + 1 + k: by spill round k (each
-                    // round its own word, all zeroed with the rest at the call's start)
+  RC_SPILL = 384,   // items spilled by the walk (a u64 over words RC_SPILL, RC_SPILL + 1); RC_SPILL +
+                    // 2 (k + 1): by spill round k (each round its own u64, all zeroed with the rest at
+                    // the call's start; 64-bit so that failed reservations' overshoot cannot wrap)
   RC_WORDS = 432
 };
-constexpr uint32_t RC_MAX_ROUNDS = RC_WORDS - RC_SPILL - 2;  // budgeted spill rounds per call at most
+constexpr uint32_t RC_MAX_ROUNDS = (RC_WORDS - RC_SPILL) / 2 - 2;  // budgeted spill rounds per call at most
 
 // Queue mode: the control words of one shard (RetainArgs.qctl + shard * QS_STRIDE; all zero when
 // a call starts, zeroed again by the call's last kernel)
@@ -189,7 +190,8 @@ struct RetainArgs {
   uint32_t step_budget;    // wave steps before the rest of a stack spills (~0u: no budget)
   uint4* spill_out;        // [spill_cap] items left when the budget ran out
   uint32_t spill_cap;
-  uint32_t spill_word;     // ctrl word counting the items this launch spills (RC_SPILL + round)
+  uint32_t spill_word;     // ctrl word (even: the low half of a u64) counting the items this launch
+                           // spills (RC_SPILL + 2 * round)
   uint4* queue;            // [queue_cap] shared work (queue mode), all zero when a call starts;
                            // shard s has slots [s * cap/S, (s + 1) * cap/S)
   uint32_t queue_cap;

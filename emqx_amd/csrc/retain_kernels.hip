@@ -221,15 +221,16 @@ constexpr uint32_t RCHUNK = 256;  // ranks per big range record (one unrolled wa
 
 // Reserve n slots of the spill buffer, all or nothing (a partial reservation would leave
 // unwritten items inside the counted prefix).  Called by one lane.
-__device__ __forceinline__ bool spill_reserve(uint32_t* ctr, uint32_t n, uint32_t cap, uint32_t* base) {
+__device__ __forceinline__ bool spill_reserve(uint32_t* ctr32, uint32_t n, uint32_t cap, uint32_t* base) {
   // one fetch-add, not a compare-and-swap loop: waves of a round reach their budget together,
   // and 4096 of them retrying one CAS serialised a round for ~20 ms (budget 32).  A reservation
-  // past `cap` fails; its part below `cap` is padded with empty items by the caller
-  // (the counter is zeroed per call and one call reserves far fewer than 2^32 slots, so the
-  // failed reservations' overshoot cannot wrap it; a load before the add, tried in round 4,
-  // cost ~0.2 ms per call: 8K waves reading one word together)
-  const uint32_t old = atomicAdd(ctr, n);
-  *base = old;
+  // past `cap` fails; its part below `cap` is padded with empty items by the caller.  The
+  // counter is 64-bit (two ctrl words, zeroed per call), so the failed reservations' overshoot
+  // cannot wrap it back under `cap` (a load before the add, tried in round 4, cost ~0.2 ms per
+  // call: 8K waves reading one word together)
+  unsigned long long* ctr = reinterpret_cast<unsigned long long*>(ctr32);
+  const unsigned long long old = atomicAdd(ctr, static_cast<unsigned long long>(n));
+  *base = static_cast<uint32_t>(min(old, static_cast<unsigned long long>(cap)));
   return old <= cap && n <= cap - old;
 }
 
@@ -956,8 +957,10 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_spill_kerne
   __shared__ uint32_t s_pref[RW_WAVES][64];
   __shared__ uint4 s_item[RW_WAVES][64];
   __shared__ uint4 s_stk[RW_WAVES][RSTK];
-  const uint32_t n_in = min(__hip_atomic_load(&a.ctrl[in_word], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                            a.spill_cap);
+  const uint32_t n_in = static_cast<uint32_t>(
+      min(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.ctrl + in_word), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT),
+          static_cast<unsigned long long>(a.spill_cap)));
   if (n_in == 0) return;
   if (gw == 0 && lane == 0) {
     atomicAdd(&a.ctrl[RC_ROUNDS], 1u);

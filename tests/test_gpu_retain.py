@@ -345,6 +345,37 @@ def test_queue_full_parity(mod):
             assert g == r == tt.dispatch(f, 100), (f, cap)
 
 
+def test_queue_abort_reruns_in_spill_mode(mod):
+    """The work-sharing walk's safety valve, forced: with the poll limit at 1
+    (emqx_retain_set_tuning "queue_poll_limit") a waiting wave gives up after its second empty
+    poll (RC_QABORT), the kernel drains, and the host reruns the call in spill-round mode
+    (retain.cpp, queue_aborts counts it).  The reruns' results equal the oracle's; with the limit
+    back, calls run without aborts and give the same results."""
+    names, expiry, filters = _sharing_case(1401)
+    idx = mod.RetainIndex()
+    idx.store(names, expiry)
+    idx.commit()
+    tt = RR.TokenTrie(names, expiry)
+    idx.set_tuning("balance", 1)
+    idx.set_tuning("queue_check", 1)
+    idx.set_tuning("queue_shards", 4)
+    a0 = idx.stats()["queue_aborts"]
+    idx.set_tuning("queue_poll_limit", 1)
+    for _ in range(3):
+        got = idx.match(filters, 100)
+        for f, g in zip(filters, got):
+            assert g == tt.dispatch(f, 100), f
+    a1 = idx.stats()["queue_aborts"]
+    assert a1 > a0
+    idx.set_tuning("queue_poll_limit", 1 << 20)
+    got = idx.match(filters, 100)
+    assert idx.stats()["queue_aborts"] == a1
+    for f, g in zip(filters, got):
+        assert g == tt.dispatch(f, 100), f
+    with pytest.raises(Exception):
+        idx.set_tuning("queue_poll_limit", 0)
+
+
 @pytest.mark.parametrize("tile", [1, 5, 64])
 def test_tile_sizes_parity(mod, tile):
     """Filters per wave tile of the first walk round (emqx_retain_set_tuning "tile"): any

@@ -144,15 +144,19 @@ def _rank_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_shard_step_two_ranks_share_one_gpu():
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_shard_step_ranks_share_one_gpu(world):
+    """The device step (emqx_shard_step_*, dist.py _match_all_device) at world 2, 3 and 4 with
+    every rank a process on the one GPU (gloo for the exchanges): each rank's CSR ID-for-ID
+    against the oracle over the whole table; a rehearsal of the protocol, not a measurement."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    world, port = 2, 29565
+    port = 29565 + world
     ps = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=110) for _ in range(world)]
+    res = [q.get(timeout=200) for _ in range(world)]
     for p in ps:
         p.join(30)
     res.sort()
