@@ -154,7 +154,7 @@ enum RCtrl : uint32_t {
   RC_SPILL = 384,   // items spilled by the walk (a u64 over words RC_SPILL, RC_SPILL + 1); RC_SPILL +
                     // 2 (k + 1): by spill round k (each round its own u64, all zeroed with the rest at
                     // the call's start; 64-bit so that failed reservations' overshoot cannot wrap)
-  RC_WORDS = 432
+  RC_WORDS = 480
 };
 constexpr uint32_t RC_MAX_ROUNDS = (RC_WORDS - RC_SPILL) / 2 - 2;  // budgeted spill rounds per call at most
 
