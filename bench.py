@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--callers", type=str, default="64,512,4096",
                     help="--workload L: concurrent single-topic callers per run")
     ap.add_argument("--max-batch", type=int, default=4096, help="--workload L: batcher max_batch")
+    ap.add_argument("--small-clock", action="store_true",
+                    help="--workload L/P: per-phase clocks of the one-launch small-batch kernel in each run")
     ap.add_argument("--max-wait-us", type=str, default="200", help="--workload L: batcher max_wait_us (comma list)")
     ap.add_argument("--retained", type=int, default=1_000_000, help="--workload R: stored retained topics")
     ap.add_argument("--retain-tile", type=int, default=None, help="--workload R: filters per walk tile")
@@ -650,6 +652,7 @@ def batcher_bench(args, rank, world, dev):
     waits = [int(x) for x in str(args.max_wait_us).split(",")]
     for c, wus in [(int(x), w) for x in args.callers.split(",") for w in waits]:
         out = np.zeros(12, dtype=np.float64)
+        small_clock_start(eng, args)
         rc = L.batch_load(eng._h, args.mode, tb.ctypes.data, to.ctypes.data, wl.n_topics, c, args.max_batch,
                           wus, 500.0, 3000.0, out.ctypes.data)
         if rc != 0:
@@ -659,6 +662,9 @@ def batcher_bench(args, rank, world, dev):
                      "batches": int(out[6]), "topics_per_batch": round(out[7], 1),
                      "max_in_flight": int(out[8]), "us_per_batch_device_wait": round(out[9], 1),
                      "us_per_batch_callbacks": round(out[10], 1), "us_per_batch_submit": round(out[11], 1)})
+        clk = small_clock_read(eng, args)
+        if clk:
+            runs[-1]["small_clock"] = clk
         log(f"[rank {rank}] callers {c}: {runs[-1]}")
     best = max(runs, key=lambda r: r["topics_per_s"])
     res = {"metric": "per-PUBLISH match_routes/1 calls served/sec through the batcher (10M subs)",
@@ -671,6 +677,35 @@ def batcher_bench(args, rank, world, dev):
            "runs": runs}
     if rank == 0:
         print(json.dumps(res), flush=True)
+
+
+SMALL_CLK = ("copy_in", "walk", "deep", "scan", "scatter", "out", "fo_pass1", "fo_pass2")
+
+
+def small_clock_start(eng, args):
+    """--small-clock: the one-launch small-batch kernel accumulates its per-phase wall clocks
+    (kernels.h SMALL_CLK_*) into the engine's timeline buffer while the run lasts."""
+    if args.small_clock:
+        eng.set_tuning("timeline", 0)
+        eng.set_tuning("timeline", 5)
+
+
+def small_clock_read(eng, args):
+    """Average microseconds per launch of each small-kernel phase, and the launches counted."""
+    if not args.small_clock:
+        return None
+    import ctypes
+    from emqx_amd import _lib
+    buf = np.zeros(10, dtype=np.uint64)
+    got = ctypes.c_uint64(0)
+    _lib.check(_lib.lib().emqx_diag_timeline(eng._h, buf.ctypes.data, 5, ctypes.byref(got)), "emqx_diag_timeline")
+    eng.set_tuning("timeline", 0)
+    k = int(buf[8])
+    out = {"launches": k}
+    for i, name in enumerate(SMALL_CLK):
+        out[name + "_us"] = round(float(buf[i]) * 0.01 / max(k, 1), 2)  # 100 MHz ticks
+    out["kernel_us"] = round(float(buf[:8].sum()) * 0.01 / max(k, 1), 2)
+    return out
 
 
 def config_e_tables(args, rank, dev):
@@ -721,6 +756,7 @@ def pub_batcher_bench(args, rank, world, dev):
     waits = [int(x) for x in str(args.max_wait_us).split(",")]
     for c, wus in [(int(x), w) for x in args.callers.split(",") for w in waits]:
         out = np.zeros(13, dtype=np.float64)
+        small_clock_start(eng, args)
         rc = L.pub_load(eng._h, st.handle, strat, tb.ctypes.data, to.ctypes.data, keys.ctypes.data, fw.wl.n_topics, c,
                         args.max_batch, wus, 500.0, 3000.0, out.ctypes.data)
         if rc != 0:
@@ -731,6 +767,9 @@ def pub_batcher_bench(args, rank, world, dev):
                      "deliveries_per_message": round(out[12], 3), "max_in_flight": int(out[8]),
                      "us_per_batch_device_wait": round(out[9], 1), "us_per_batch_callbacks": round(out[10], 1),
                      "us_per_batch_submit": round(out[11], 1)})
+        clk = small_clock_read(eng, args)
+        if clk:
+            runs[-1]["small_clock"] = clk
         log(f"[rank {rank}] callers {c}: {runs[-1]}")
     best = max(runs, key=lambda r: r["messages_per_s"])
     res = {"metric": "per-PUBLISH emqx_broker:publish/1 fan-outs served/sec through the publish batcher "

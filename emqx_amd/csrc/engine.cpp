@@ -760,6 +760,8 @@ int enqueue_small(emqx_engine* e, const Snapshot& snap, Workspace* w, uint32_t m
   sa.h_out_off = h_out_off;
   sa.h_out_ids = h_out_ids;
   sa.h_cap = h_cap;
+  // the phase clock: a timeline of >= SMALL_CLK_WORDS / 2 tiles with diag off (tools/small_clock.py)
+  sa.clk = e->timeline && e->timeline_cap * 2 >= SMALL_CLK_WORDS ? reinterpret_cast<uint64_t*>(e->timeline) : nullptr;
   if (f) {
     sa.has_fanout = 1;
     sa.f = *f;

@@ -154,7 +154,14 @@ struct SmallArgs {
   uint64_t* h_out_off;      // match only: the CSR into host-mapped buffers (null: not copied)
   uint32_t* h_out_ids;
   uint64_t h_cap;
+  uint64_t* clk;            // optional (emqx_set_tuning "timeline" >= SMALL_CLK_WORDS / 2 tiles, diag off):
+                            // per-phase wall-clock ticks accumulated over launches (SMALL_CLK_*)
   SmallFanout f;
+};
+// small-batch phase clock words (100 MHz ticks summed over launches; the last word counts them)
+enum : uint32_t {
+  SMALL_CLK_COPY = 0, SMALL_CLK_WALK, SMALL_CLK_DEEP, SMALL_CLK_SCAN, SMALL_CLK_SCATTER, SMALL_CLK_OUT,
+  SMALL_CLK_FO_PASS1, SMALL_CLK_FO_PASS2, SMALL_CLK_LAUNCHES, SMALL_CLK_WORDS = 10
 };
 hipError_t launch_small_batch(const SmallArgs& a, hipStream_t s);
 // bytes from host-mapped (pinned) h_src into device memory by a kernel (through L2)

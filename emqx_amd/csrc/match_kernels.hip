@@ -1526,15 +1526,15 @@ __device__ __forceinline__ uint64_t small_block_scan(uint64_t v, uint64_t* total
   return before + incl - v;
 }
 
-// A phase boundary of the small-batch kernel: the phases hand data to each other through global
-// memory (counts, slabs, the deferred list, control words updated by atomics in L2), so every
-// wave's writes are made visible at agent scope before the barrier, and every wave's vector L1
-// is invalidated after it — a line read before the barrier (a control word, say) must not be
-// served stale from L1 after it.
+// A phase boundary of the small-batch kernel.  The phases hand data to each other through global
+// memory (counts, slabs, the deferred list), but the kernel is ONE workgroup: all its waves sit
+// on one CU and share its vector L1, so a workgroup-scope release/acquire (the barrier's own
+// s_waitcnt) is all the hand-over needs.  An agent-scope fence here would write back and
+// invalidate the XCD's whole L2 at every phase (buffer_wbl2 / buffer_inv sc1 on gfx950) and
+// every later table read would miss.  Words that atomics update in L2 (ctrl, deep_rank) are
+// read back with atomic loads, never through L1.
 __device__ __forceinline__ void small_phase_barrier() {
-  __threadfence();
   __syncthreads();
-  __threadfence();
 }
 
 // Largest i in [0, n) with v[i] <= x (v non-decreasing, v[0] <= x).
@@ -1565,6 +1565,22 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   constexpr uint32_t NT = SMALL_WAVES * 64;
   const uint64_t n = a.n;
+  // optional phase clock (thread 0; every mark follows a block barrier, so it dates the phase's end)
+  uint64_t* const clk = sa.clk;
+  uint64_t tprev = clk ? wall_clock64() : 0;
+  auto mark = [&](uint32_t k) {
+    if (clk && tid == 0) {
+      const uint64_t now = wall_clock64();
+      atomicAdd(reinterpret_cast<unsigned long long*>(clk + k), static_cast<unsigned long long>(now - tprev));
+      tprev = now;
+    }
+  };
+  auto finish = [&](uint32_t k) {  // block-uniform: the launch's last phase
+    if (!clk) return;
+    __syncthreads();
+    mark(k);
+    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(clk + SMALL_CLK_LAUNCHES), 1ull);
+  };
 
   // 0. the call's control words; the batch from pinned host memory into HBM (one round trip
   //    over PCIe: every load of the copy is issued before any store)
@@ -1580,15 +1596,18 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
       for (uint64_t i = tid; i < n; i += NT) sa.f.d_keys[i] = sa.f.h_keys[i];
   }
   small_phase_barrier();
+  mark(SMALL_CLK_COPY);
 
   // 1. the walk: wave w takes tile w (tt topics); 2. deferred topics on every wave
   const uint32_t tt = sa.tt;
   const uint64_t ntiles = (n + tt - 1) / tt;
   if (wv < ntiles) fast_tile<SC, WC, 1, false>(a, lds.w[wv], wv, tt);
   small_phase_barrier();
+  mark(SMALL_CLK_WALK);
   auto ctrl = [&](uint32_t k) { return __hip_atomic_load(&a.ctrl[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   if (ctrl(CTRL_DEFERRED)) deep_walk(a, wv, SMALL_WAVES, tt);
   small_phase_barrier();
+  mark(SMALL_CLK_DEEP);
 
   uint64_t* sm = a.summary;
   const uint32_t need = ctrl(CTRL_NEED_SLAB), err = ctrl(CTRL_ERROR);
@@ -1606,6 +1625,7 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
   }
   if (total > a.out_cap) flags |= SUM_F_OVERFLOW;
   small_phase_barrier();
+  mark(SMALL_CLK_SCAN);
   if (!(flags & (SUM_F_RETRY | SUM_F_ERROR))) {
     if (wv < ntiles) {
       const uint64_t t = uint64_t(wv) * tt + lane;
@@ -1621,6 +1641,7 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
     }
   }
   small_phase_barrier();
+  mark(SMALL_CLK_SCATTER);
   if (tid == 0) {
     uint64_t ev = ctrl(CTRL_DEEP_EVALS);
     uint32_t mx = 0;
@@ -1641,18 +1662,23 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
 
   // 5a. match only: the CSR into the pinned host buffers (16-B stores)
   if (sa.h_out_off) {
-    if (flags & (SUM_F_RETRY | SUM_F_ERROR)) return;
-    const uint64_t no2 = (n + 1) / 2;
-    for (uint64_t i = tid; i < no2; i += NT)
-      reinterpret_cast<uint4*>(sa.h_out_off)[i] = reinterpret_cast<const uint4*>(a.out_off)[i];
-    if (tid == 0 && ((n + 1) & 1)) sa.h_out_off[n] = a.out_off[n];
-    const uint64_t ids = min(total, sa.h_cap), nv = ids / 4;
-    for (uint64_t i = tid; i < nv; i += NT)
-      reinterpret_cast<uint4*>(sa.h_out_ids)[i] = reinterpret_cast<const uint4*>(a.out_ids)[i];
-    if (tid < ids - 4 * nv) sa.h_out_ids[4 * nv + tid] = a.out_ids[4 * nv + tid];
+    if (!(flags & (SUM_F_RETRY | SUM_F_ERROR))) {
+      const uint64_t no2 = (n + 1) / 2;
+      for (uint64_t i = tid; i < no2; i += NT)
+        reinterpret_cast<uint4*>(sa.h_out_off)[i] = reinterpret_cast<const uint4*>(a.out_off)[i];
+      if (tid == 0 && ((n + 1) & 1)) sa.h_out_off[n] = a.out_off[n];
+      const uint64_t ids = min(total, sa.h_cap), nv = ids / 4;
+      for (uint64_t i = tid; i < nv; i += NT)
+        reinterpret_cast<uint4*>(sa.h_out_ids)[i] = reinterpret_cast<const uint4*>(a.out_ids)[i];
+      if (tid < ids - 4 * nv) sa.h_out_ids[4 * nv + tid] = a.out_ids[4 * nv + tid];
+    }
+    finish(SMALL_CLK_OUT);
     return;
   }
-  if (!sa.has_fanout) return;
+  if (!sa.has_fanout) {
+    finish(SMALL_CLK_OUT);
+    return;
+  }
 
   // 5b. the fan-out (emqx_broker.erl:244-272,500-524; stateless $share picks,
   //     emqx_shared_sub.erl:251-288), straight into the pinned delivery buffers
@@ -1665,57 +1691,100 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
       f.h_sum[FO_SUM_ENTRIES] = m;
       f.h_sum[FO_SUM_STATE] = f.ps_count ? *f.ps_count : 0;
     }
+    finish(SMALL_CLK_OUT);
     return;
   }
   uint32_t* D = lds.f.D;
   uint32_t* off = lds.f.off;
   for (uint64_t t = tid; t <= n; t += NT) off[t] = static_cast<uint32_t>(a.out_off[t]);
   small_phase_barrier();
-  // pass 1: each entry's record and topic; exclusive scan of the deliveries
+  // pass 1: each entry's record and topic; exclusive scan of the deliveries.  A thread takes
+  // FU entries per round with every load of the round issued before any is used (the id, then
+  // the record: two dependent round trips per round, not per entry).
+  constexpr uint32_t FU = 4;
   uint64_t T = 0;
-  for (uint32_t e0 = 0; e0 < m; e0 += NT) {
-    const uint32_t e = e0 + tid;
-    uint32_t c = 0;
-    if (e < m) {
-      const uint32_t fid = a.out_ids[e];
-      const uint4 r = fid < f.n_recs ? f.recs[fid] : make_uint4(0, 0, 0, 0);
-      c = fo_rec_plain(r) + fo_rec_groups(r);
-      f.erec[e] = r;
-      f.etop[e] = small_floor(off, static_cast<uint32_t>(n), e);
+  for (uint32_t r0 = 0; r0 < m; r0 += FU * NT) {
+    uint32_t fid[FU], c[FU];
+    uint4 rec[FU];
+#pragma unroll
+    for (uint32_t u = 0; u < FU; ++u) {
+      const uint32_t e = r0 + u * NT + tid;
+      fid[u] = e < m ? a.out_ids[e] : 0xFFFFFFFFu;
     }
-    uint64_t tc;
-    const uint64_t ex = small_block_scan(c, &tc, wsum);
-    if (e < m) D[e] = static_cast<uint32_t>(T + ex);
-    T += tc;
+#pragma unroll
+    for (uint32_t u = 0; u < FU; ++u) rec[u] = fid[u] < f.n_recs ? f.recs[fid[u]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t u = 0; u < FU; ++u) {
+      const uint32_t e = r0 + u * NT + tid;
+      c[u] = e < m ? fo_rec_plain(rec[u]) + fo_rec_groups(rec[u]) : 0u;
+      if (e < m) {
+        f.erec[e] = rec[u];
+        f.etop[e] = small_floor(off, static_cast<uint32_t>(n), e);
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < FU; ++u) {
+      const uint32_t e = r0 + u * NT + tid;
+      if (r0 + u * NT >= m) break;  // block-uniform
+      uint64_t tc;
+      const uint64_t ex = small_block_scan(c[u], &tc, wsum);
+      if (e < m) D[e] = static_cast<uint32_t>(T + ex);
+      T += tc;
+    }
   }
   if (tid == 0) D[m] = static_cast<uint32_t>(min<uint64_t>(T, 0xFFFFFFFFull));
   small_phase_barrier();
+  mark(SMALL_CLK_FO_PASS1);
   for (uint64_t t = tid; t <= n; t += NT) f.h_off[t] = t < n ? D[off[t]] : T;
   const bool fits = T <= f.cap;
-  // pass 2: deliveries j, lane-consecutive (coalesced stores); each finds its entry in LDS
+  // pass 2: deliveries j, lane-consecutive (coalesced stores); each finds its entry in LDS.
+  // FU deliveries per thread per round, loads batched as in pass 1: the entry's record, then
+  // the plain subscriber or the group, then the group's member.
   if (fits) {
     const bool hash = f.strategy == 3u || f.strategy == 4u;
-    for (uint64_t j0 = 0; j0 < T; j0 += NT) {
-      const uint32_t j = static_cast<uint32_t>(j0) + tid;
-      if (j >= T) continue;
-      const uint32_t e = small_floor(D, static_cast<uint32_t>(m), j);
-      const uint32_t r = j - D[e];
-      const uint4 rec = f.erec[e];
-      const uint32_t fid = a.out_ids[e];
-      const uint32_t np = rec.y & ~FO_INLINE_BIT;
-      uint32_t sub, fl = fid;
-      if (r < np) {
-        sub = (rec.y & FO_INLINE_BIT) ? (r == 0 ? rec.x : (r == 1 ? rec.z : rec.w)) : f.plain[rec.x + r];
-      } else {
-        const uint32_t gidx = rec.z + (r - np);
-        const uint4 g = f.groups[gidx];  // {member_begin, n_members, slot, group_id}
-        const uint32_t idx =
-            g.y <= 1 ? 0u : fo_stateless_index(f.strategy, hash ? f.d_keys[f.etop[e]] : 0u, f.seed, e, gidx, g.y);
-        sub = f.members[g.x + idx];
-        fl |= FANOUT_SHARED_BIT;
+    for (uint64_t j0 = 0; j0 < T; j0 += FU * NT) {
+      uint32_t e[FU], r[FU], fid[FU], sub[FU], key[FU];
+      bool ok[FU], grp[FU];
+      uint4 rec[FU], g[FU];
+#pragma unroll
+      for (uint32_t u = 0; u < FU; ++u) {
+        const uint64_t j = j0 + u * NT + tid;
+        ok[u] = j < T;
+        e[u] = ok[u] ? small_floor(D, static_cast<uint32_t>(m), static_cast<uint32_t>(j)) : 0u;
+        r[u] = ok[u] ? static_cast<uint32_t>(j) - D[e[u]] : 0u;
       }
-      f.h_subs[j] = sub;
-      f.h_fil[j] = fl;
+#pragma unroll
+      for (uint32_t u = 0; u < FU; ++u) {
+        rec[u] = ok[u] ? f.erec[e[u]] : make_uint4(0, 0, 0, 0);
+        fid[u] = ok[u] ? a.out_ids[e[u]] : 0u;
+        key[u] = ok[u] && hash ? f.d_keys[f.etop[e[u]]] : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < FU; ++u) {
+        const uint32_t np = rec[u].y & ~FO_INLINE_BIT;
+        grp[u] = ok[u] && r[u] >= np;
+        sub[u] = 0;
+        g[u] = make_uint4(0, 0, 0, 0);
+        if (ok[u] && !grp[u])
+          sub[u] = (rec[u].y & FO_INLINE_BIT) ? (r[u] == 0 ? rec[u].x : (r[u] == 1 ? rec[u].z : rec[u].w))
+                                              : f.plain[rec[u].x + r[u]];
+        if (grp[u]) g[u] = f.groups[rec[u].z + (r[u] - np)];  // {member_begin, n_members, slot, group_id}
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < FU; ++u) {
+        if (!grp[u]) continue;
+        const uint32_t np = rec[u].y & ~FO_INLINE_BIT;
+        const uint32_t gidx = rec[u].z + (r[u] - np);
+        const uint32_t idx = g[u].y <= 1 ? 0u : fo_stateless_index(f.strategy, key[u], f.seed, e[u], gidx, g[u].y);
+        sub[u] = f.members[g[u].x + idx];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < FU; ++u) {
+        if (!ok[u]) continue;
+        const uint64_t j = j0 + u * NT + tid;
+        f.h_subs[j] = sub[u];
+        f.h_fil[j] = grp[u] ? (fid[u] | FANOUT_SHARED_BIT) : fid[u];
+      }
     }
   }
   if (tid == 0) {
@@ -1724,6 +1793,7 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
     f.h_sum[FO_SUM_ENTRIES] = m;
     f.h_sum[FO_SUM_STATE] = f.ps_count ? *f.ps_count : 0;
   }
+  finish(SMALL_CLK_FO_PASS2);
 }
 
 // ------------------------------------------------------------------------------------

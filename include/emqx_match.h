@@ -559,7 +559,10 @@ int emqx_set_tuning(emqx_engine* e, const char* key, int64_t value);
 int emqx_diag_read(emqx_engine* e, uint64_t* out, uint32_t n, int reset);
 /* Per-tile timeline of the fast kernel's last "diag" call (emqx_set_tuning "timeline" = tiles to
  * record): 4 uint32 per tile {start (100 MHz ticks, low), start high, phase-A ticks | CU id << 20,
- * end - start ticks}; *n_tiles = the recorded capacity. */
+ * end - start ticks}; *n_tiles = the recorded capacity.  With "diag" off and a timeline of at
+ * least 5 tiles, the one-launch small-batch kernel instead accumulates its per-phase wall clocks
+ * there: 10 uint64 {copy-in, walk, deep, scan, scatter, output, fan-out pass 1, pass 2 (100 MHz
+ * ticks summed over launches), launches, unused} (emqx_amd/csrc/kernels.h SMALL_CLK_*). */
 int emqx_diag_timeline(emqx_engine* e, uint32_t* out, uint64_t cap_tiles, uint64_t* n_tiles);
 
 /* Host-only self-check of the table builder (no device needed): builds the level trie of
