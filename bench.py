@@ -428,7 +428,7 @@ def sharded_bench(args, rank, world, dev):
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     with progress(f"[rank {rank}] building shard"):
         sm = ShardedMatcher(wl.filters, device=dev, mode=args.mode)
-    sts = [e.stats() for e in sm.engines]
+    sts = [e.stats() for e in sm.engines if e is not None]
     shard_bytes = sum(x["table_bytes"] for x in sts)
     log(f"[rank {rank}] shard: {sm.n_local_filters} filters, {shard_bytes / 1e9:.2f} GB, plan {len(sm.plan)} keys")
     topics = (torch.from_numpy(wl.topics[0]).to(dev), torch.from_numpy(wl.topics[1].view(np.int64)).to(dev))
@@ -493,8 +493,8 @@ def sharded_bench(args, rank, world, dev):
     dist.all_reduce(bad_rank, op=dist.ReduceOp.SUM)
     dist.all_reduce(checked, op=dist.ReduceOp.SUM)
     mism = int(bad_rank[rank].item())
-    mt = torch.tensor([float(res[0][-1].item()), float(sm.last_local_topics), 0.0, float(sm.n_local_filters)],
-                      dtype=torch.float64, device=dev)
+    mt = torch.tensor([float(res[0][-1].item()), float(sm.last_local_topics), 0.0, float(sm.n_local_filters)]
+                      + [float(x) for x in sm.last_slot_topics], dtype=torch.float64, device=dev)
     most = mt[3:4].clone()
     dist.all_reduce(mt, op=dist.ReduceOp.SUM)
     dist.all_reduce(most, op=dist.ReduceOp.MAX)
@@ -513,12 +513,16 @@ def sharded_bench(args, rank, world, dev):
                                       f"{'gloo (rehearsal)' if rehearse else 'RCCL'} all-to-all out and back"},
             "shard_filters_max_rank": int(most.item()), "shard_filters_max_frac": round(float(most.item()) / wl.n_filters, 4),
             "shard_plan_keys": len(sm.plan),
+            "shard_table_bytes_rank0": int(shard_bytes),
+            "requests_per_topic_by_slot": {k: round(float(mt[4 + i].item()) / (n * world), 4)
+                                           for i, k in enumerate(("A", "B", "AB"))},
             "matches_per_topic": round(float(mt[0].item()) / (n * world), 3),
             "parity": {"rule": parity_rule,
                        "topics_checked_per_rank": [int(x) for x in checked.cpu().tolist()],
                        "mismatching_topics_per_rank": [int(x) for x in bad_rank.cpu().tolist()]},
-            "step": "device kernels (emqx_shard_step_*: route + sort + pack, unpack, answer, merge), "
-                    "engines async with learnt capacities, two host syncs (split sizes)",
+            "step": "device kernels (emqx_shard_step_*: route + fold onto the engine slots A / B / AB + sort + "
+                    "pack, unpack, answer, merge), engines async with learnt capacities, two host syncs "
+                    "(split sizes)",
             **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
                if rehearse else {}),
         }), flush=True)

@@ -7,20 +7,29 @@
 // table past one GPU is sharded here instead, and one rank's step is
 //
 //   send    route every topic to its (rank, engine) requests (layout.h shard_route_topic),
-//           stable radix sort of the requests by destination, one chunk per destination:
-//             [u32 nA nB bytesA bytesB][u32 offsets of the nA A-requests + 1][... B + 1] pad 16
-//             [A topic bytes][B topic bytes] pad 16
-//   recv    the received chunks -> two contiguous batches (every source's A requests, then B)
-//   answer  the two engines' CSRs -> one answer chunk per source:
-//             [u32 nA nB idsA idsB][counts of the A requests][counts of B][A ids][B ids]
+//           fold them onto the rank's three engine slots (shard_fold: a topic whose requests
+//           meet on one rank, or that makes only one, asks that rank's AB engine once), stable
+//           radix sort of the requests by destination, one chunk per destination:
+//             [u32 n0 n1 n2 0 bytes0 bytes1 bytes2 0][u32 offsets of the n0 slot-0 requests + 1]
+//             [slot 1 + 1][slot 2 + 1] pad 16 [slot 0 topic bytes][slot 1][slot 2] pad 16
+//   recv    the received chunks -> three contiguous batches (every source's slot-e requests)
+//   answer  the three engines' CSRs -> one answer chunk per source:
+//             [u32 n0 n1 n2 ids0 ids1 ids2 0 0][counts of slot 0][1][2][ids 0][ids 1][ids 2]
 //   merge   the answer chunks -> the CSR of the rank's batch in batch order, each topic's
-//           engine-A ids then its engine-B ids
+//           first request's ids then its second's (engine A then engine B)
+//
+// Engine slots of a rank: 0 = A (space L + root wildcards), 1 = B (space P), 2 = AB (both, one
+// table).  A topic's two raw requests (A at rank rA, B at rank rB) become ONE request to slot 2
+// when rA == rB — AB holds exactly A_r + B_r, disjoint, so its answer is the two answers'
+// union — and a topic with one request (one level, '$', a wildcard name) asks slot 2 of its
+// rank as well (no B filter '+/x/...' can match it, and a wildcard name's filter is in AB).
+// At world 1 every request is a slot-2 request: one walk per topic over the rank's whole
+// table, as replication does; at world G a topic's two requests meet with probability ~1/G.
 //
 // Per-source / per-destination tables (chunk starts, batch bases) come from the host, which
 // holds the exchanged sizes anyway, as one kernel argument (world <= 64).  Requests are u32
 // indices (2 per topic), so a batch holds fewer than 2^31 topics.
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -36,15 +45,17 @@ namespace {
 
 constexpr uint32_t kMaxWorld = EMQX_SHARD_MAX_WORLD;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kE = EMQX_SHARD_ENGINES;  // engine slots per rank: A, B, AB
+constexpr uint32_t kHW = 8;                  // header words of a request / answer chunk
 
 struct ShardTab {
-  uint64_t base[kMaxWorld + 1];  // chunk starts (bytes: request chunks; u32 words: answer chunks)
-  uint32_t a0[kMaxWorld + 1];    // first A request of each source in the A batch (prefix of nA)
-  uint32_t b0[kMaxWorld + 1];
-  uint64_t ab0[kMaxWorld + 1];   // first A byte of each source in the A batch
-  uint64_t bb0[kMaxWorld + 1];
-  uint64_t w0[kMaxWorld + 1];    // answer chunks: prefix of (4 + nA + nB) words
+  uint64_t chunk[kMaxWorld];       // each source's received chunk (device address; a rank's own
+                                   // chunk is read in place where it was packed)
+  uint32_t q0[kE][kMaxWorld + 1];  // first slot-e request of each source in the slot-e batch
+  uint64_t y0[kE][kMaxWorld + 1];  // first slot-e byte of each source in the slot-e batch
+  uint64_t w0[kMaxWorld + 1];      // answer chunks: prefix of (kHW + n0 + n1 + n2) words
 };
+static_assert(sizeof(ShardTab) <= 3584, "kernel argument");
 
 __host__ __device__ inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 
@@ -64,10 +75,15 @@ uint32_t grid_of(uint64_t items, uint32_t per_block, uint32_t cap = 8192) {
   return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>((items + per_block - 1) / per_block, cap)));
 }
 
-uint32_t bucket_bits(uint32_t world) {  // keys 0 .. 2 * world (2 * world = no request)
-  uint32_t b = 1;
-  while ((1ull << b) < 2ull * world + 1) ++b;
-  return b;
+
+// A topic's raw requests (r[0]: rank * 2 of engine A, r[1]: rank * 2 + 1 of engine B, or kNone)
+// -> its bucket keys (rank * kE + slot; kE * world = none), see the header.
+__device__ __forceinline__ uint2 shard_fold(const uint32_t (&r)[2], uint32_t world) {
+  const uint32_t none = kE * world;
+  const bool a = r[0] != kNone, b = r[1] != kNone;
+  if (a && b && (r[0] >> 1) != (r[1] >> 1)) return make_uint2(kE * (r[0] >> 1), kE * (r[1] >> 1) + 1);
+  if (a || b) return make_uint2(kE * ((a ? r[0] : r[1]) >> 1) + 2, none);
+  return make_uint2(none, none);
 }
 
 // ---- send -------------------------------------------------------------------------------
@@ -77,82 +93,311 @@ uint32_t bucket_bits(uint32_t world) {  // keys 0 .. 2 * world (2 * world = no r
 // its end): the same summary, one load per 16 bytes instead of one per byte.
 __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb, uint64_t s, uint64_t e,
                                                  uint64_t lim, ShardTopicLevels* L) {
-  L->n_levels = 0;
-  L->wild = false;
-  L->h[0] = L->h[1] = L->h[2] = 0;
+  // (level hashes and the windows in named registers: an indexed private array would live in
+  // scratch memory; four windows are loaded before any is scanned: one round trip per 64 bytes)
+  uint32_t nl = 0, h0 = 0, h1 = 0, h2 = 0;
+  bool wild = false;
   uint32_t h = 0x811C9DC5u, len = 0, c0 = 0;
   const uintptr_t abeg = reinterpret_cast<uintptr_t>(tb + s), aend = reinterpret_cast<uintptr_t>(tb + e);
   const uintptr_t alim = reinterpret_cast<uintptr_t>(tb + lim);
-  for (uintptr_t w0 = abeg & ~static_cast<uintptr_t>(15); w0 <= aend; w0 += 16) {
-    uint4 v = make_uint4(0, 0, 0, 0);
+  auto window = [&](uintptr_t w0, uint64_t& lo, uint64_t& hi) {
+    lo = hi = 0;
+    if (w0 > aend) return;
     if (w0 + 16 <= alim) {
-      v = *reinterpret_cast<const uint4*>(w0);
+      const uint4 v = *reinterpret_cast<const uint4*>(w0);
+      lo = (static_cast<uint64_t>(v.y) << 32) | v.x;
+      hi = (static_cast<uint64_t>(v.w) << 32) | v.z;
     } else if (w0 < aend) {
-      uint32_t t4[4] = {0, 0, 0, 0};
-      for (uint32_t b = 0; b < 16 && w0 + b < alim; ++b)
-        t4[b >> 2] |= static_cast<uint32_t>(*reinterpret_cast<const uint8_t*>(w0 + b)) << (8u * (b & 3u));
-      v = make_uint4(t4[0], t4[1], t4[2], t4[3]);
+      for (uint32_t b = 0; b < 8; ++b) {
+        if (w0 + b < alim) lo |= static_cast<uint64_t>(*reinterpret_cast<const uint8_t*>(w0 + b)) << (8u * b);
+        if (w0 + 8 + b < alim) hi |= static_cast<uint64_t>(*reinterpret_cast<const uint8_t*>(w0 + 8 + b)) << (8u * b);
+      }
     }
-    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+  };
+  auto scan16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
 #pragma unroll
     for (uint32_t b = 0; b < 16; ++b) {
       const uintptr_t q = w0 + b;
       if (q < abeg || q > aend) continue;
-      const uint32_t c = q < aend ? (wd[b >> 2] >> (8u * (b & 3u))) & 0xFFu : static_cast<uint32_t>('/');
+      const uint32_t c = q < aend ? static_cast<uint32_t>(((b < 8 ? lo : hi) >> (8u * (b & 7u))) & 0xFFu)
+                                  : static_cast<uint32_t>('/');
       if (c == '/') {
-        if (L->n_levels < 3) L->h[L->n_levels] = mix32(h ^ len);
-        if (len == 1 && (c0 == '+' || c0 == '#')) L->wild = true;
-        ++L->n_levels;
+        const uint32_t v = mix32(h ^ len);
+        h0 = nl == 0 ? v : h0;
+        h1 = nl == 1 ? v : h1;
+        h2 = nl == 2 ? v : h2;
+        wild |= len == 1 && (c0 == '+' || c0 == '#');
+        ++nl;
         h = 0x811C9DC5u;
         len = 0;
       } else {
-        if (len == 0) c0 = c;
+        c0 = len == 0 ? c : c0;
         h = (h ^ c) * 0x01000193u;
         ++len;
       }
     }
+  };
+  for (uintptr_t w0 = abeg & ~static_cast<uintptr_t>(15); w0 <= aend; w0 += 64) {
+    uint64_t l0, g0, l1, g1, l2, g2, l3, g3;
+    window(w0, l0, g0);
+    window(w0 + 16, l1, g1);
+    window(w0 + 32, l2, g2);
+    window(w0 + 48, l3, g3);
+    scan16(w0, l0, g0);
+    if (w0 + 16 <= aend) scan16(w0 + 16, l1, g1);
+    if (w0 + 32 <= aend) scan16(w0 + 32, l2, g2);
+    if (w0 + 48 <= aend) scan16(w0 + 48, l3, g3);
+  }
+  L->n_levels = nl;
+  L->wild = wild;
+  L->h[0] = h0;
+  L->h[1] = h1;
+  L->h[2] = h2;
+}
+
+// The split plan in LDS when it fits (routing binary-searches it twice per topic: from global
+// memory that is ~14 dependent L2 round trips a topic).
+constexpr uint32_t kLdsSplits = 2048;
+__device__ __forceinline__ const ShardSplitE* stage_splits(const ShardSplitE* sp, uint32_t nsp, ShardSplitE* lds) {
+  if (nsp > kLdsSplits) return sp;
+  for (uint32_t i = threadIdx.x; i < nsp; i += blockDim.x) lds[i] = sp[i];
+  __syncthreads();
+  return lds;
+}
+
+// ---- the requests sorted by destination: a counting sort over the kE G + 1 buckets -------
+// Tiles of kSortTile requests (topics [tile * kSortTile / 2, ...)): the key kernel counts each
+// tile's requests and bytes per bucket, one block scans the (bucket, tile) table, and the
+// scatter kernel ranks each request inside its tile (stable: wave ballots per key, then the
+// waves and rows in order) — the sorted keys, the permutation, each request's byte length and
+// its byte offset among the sorted requests, the bucket starts.
+constexpr uint32_t kSortTile = 512;  // requests per tile (256 topics: one a thread, so the grid fills the chip)
+constexpr uint32_t kMaxBuckets = kE * kMaxWorld + 1;
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Adds the wave's requests to the block's per-bucket counts and bytes: one LDS atomic per
+// distinct key in the wave (most of a wave's requests share a bucket: same-address atomics from
+// every lane would serialise).  Lanes past the batch pass k = kNone.
+__device__ __forceinline__ void wave_count(uint32_t k, uint32_t len, uint32_t nb, uint32_t* c_cnt,
+                                           unsigned long long* c_by) {
+  const uint32_t lane = lane_id();
+  uint64_t left = __ballot(k != kNone);
+  while (left) {
+    const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(left));
+    const uint32_t kk = __shfl(k, first, 64);
+    const uint64_t mask = __ballot(k == kk);
+    uint32_t v = k == kk && kk < nb - 1 ? len : 0u;
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane == first) {
+      atomicAdd(&c_cnt[kk], static_cast<uint32_t>(__popcll(mask)));
+      if (v) atomicAdd(&c_by[kk], static_cast<unsigned long long>(v));
+    }
+    left &= ~mask;
   }
 }
 
 __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restrict__ tb,
                                                         const uint64_t* __restrict__ to, uint64_t n, uint32_t world,
-                                                        const ShardSplitE* __restrict__ sp, uint32_t nsp,
-                                                        uint32_t* __restrict__ key, uint32_t* __restrict__ idx) {
+                                                        const ShardSplitE* __restrict__ gsp, uint32_t nsp,
+                                                        uint32_t* __restrict__ key, uint32_t ntiles,
+                                                        uint32_t* __restrict__ tcnt, uint64_t* __restrict__ tbytes) {
+  __shared__ ShardSplitE lsp[kLdsSplits];
+  __shared__ uint32_t c_cnt[kMaxBuckets];
+  __shared__ unsigned long long c_by[kMaxBuckets];
+  const uint32_t nb = kE * world + 1;
+  for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
+    c_cnt[k] = 0;
+    c_by[k] = 0;
+  }
+  const ShardSplitE* sp = stage_splits(gsp, nsp, lsp);  // (its barrier covers the clearing)
   const uint64_t lim = n ? to[n] : 0;
-  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
-       t += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * (kSortTile / 2);
+  const uint64_t t1 = min<uint64_t>(n, t0 + kSortTile / 2);
+  for (uint64_t tr = t0; tr < t1; tr += blockDim.x) {  // block-uniform rows (wave_count is wave-wide)
+    const uint64_t t = tr + threadIdx.x;
+    if (t >= t1) {
+      wave_count(kNone, 0, nb, c_cnt, c_by);
+      wave_count(kNone, 0, nb, c_cnt, c_by);
+      continue;
+    }
     const uint64_t a = to[t], b = to[t + 1];
     ShardTopicLevels L;
     topic_levels_dev(tb, a, b, lim, &L);
     uint32_t r[2];
     shard_route_levels(tb + a, b - a, L, world, sp, nsp, r);
-    *reinterpret_cast<uint2*>(key + 2 * t) =
-        make_uint2(r[0] == kNone ? 2 * world : r[0], r[1] == kNone ? 2 * world : r[1]);
-    *reinterpret_cast<uint2*>(idx + 2 * t) = make_uint2(static_cast<uint32_t>(2 * t), static_cast<uint32_t>(2 * t + 1));
+    const uint2 k = shard_fold(r, world);
+    *reinterpret_cast<uint2*>(key + 2 * t) = k;
+    wave_count(k.x, static_cast<uint32_t>(b - a), nb, c_cnt, c_by);
+    wave_count(k.y, static_cast<uint32_t>(b - a), nb, c_cnt, c_by);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
+    tcnt[static_cast<uint64_t>(k) * ntiles + blockIdx.x] = c_cnt[k];
+    tbytes[static_cast<uint64_t>(k) * ntiles + blockIdx.x] = c_by[k];
   }
 }
 
-// start[b] = first position of bucket b in the sorted requests (b = 0 .. 2G + 1; start[2G] =
-// the request count, start[2G + 1] = m); len[p] = bytes of request p's topic (0 for no request).
-__global__ __launch_bounds__(256) void shard_bounds_kernel(const uint32_t* __restrict__ key_s,
-                                                           const uint32_t* __restrict__ perm,
-                                                           const uint64_t* __restrict__ to, uint64_t m,
-                                                           uint32_t world, uint32_t* __restrict__ start,
-                                                           uint32_t* __restrict__ len) {
-  const uint32_t nb = 2 * world + 1;
-  for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
-       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint32_t k = key_s[p];
-    const uint32_t lo = p ? key_s[p - 1] + 1 : 0;
-    for (uint32_t b = lo; b <= k; ++b) start[b] = static_cast<uint32_t>(p);
-    if (p == m - 1)
-      for (uint32_t b = k + 1; b <= nb; ++b) start[b] = static_cast<uint32_t>(m);
+// One block: the (bucket, tile) table -> exclusive prefixes in place (bucket-major: a bucket's
+// tiles in order, then the next bucket), start[b] for b = 0 .. nb, sc[m] = the byte total.
+__global__ __launch_bounds__(1024) void shard_sort_scan_kernel(uint32_t* __restrict__ tcnt,
+                                                               uint64_t* __restrict__ tbytes, uint32_t nb,
+                                                               uint32_t ntiles, uint64_t m,
+                                                               uint32_t* __restrict__ start, uint64_t* __restrict__ sc) {
+  __shared__ uint64_t wc[16], wb[16];
+  const uint64_t N = static_cast<uint64_t>(nb) * ntiles;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint64_t per = (N + blockDim.x - 1) / blockDim.x;
+  const uint64_t i0 = min<uint64_t>(N, tid * per), i1 = min<uint64_t>(N, i0 + per);
+  // (16 entries a round, every load of a round issued before any is used)
+  constexpr uint32_t R = 16;
+  uint64_t c = 0, by = 0;
+  for (uint64_t g = i0; g < i1; g += R) {
+    uint32_t vc[R];
+    uint64_t vb[R];
+#pragma unroll
+    for (uint32_t j = 0; j < R; ++j) {
+      vc[j] = g + j < i1 ? tcnt[g + j] : 0u;
+      vb[j] = g + j < i1 ? tbytes[g + j] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < R; ++j) {
+      c += vc[j];
+      by += vb[j];
+    }
+  }
+  uint64_t ic = c, ib = by;  // inclusive wave scans
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t xc = __shfl_up(ic, d, 64), xb = __shfl_up(ib, d, 64);
+    if (lane >= d) {
+      ic += xc;
+      ib += xb;
+    }
+  }
+  if (lane == 63) {
+    wc[w] = ic;
+    wb[w] = ib;
+  }
+  __syncthreads();
+  uint64_t bc = 0, bb = 0;
+  for (uint32_t k = 0; k < w; ++k) {
+    bc += wc[k];
+    bb += wb[k];
+  }
+  uint64_t xc = bc + ic - c, xb = bb + ib - by;  // exclusive prefix of this thread's chunk
+  for (uint64_t g = i0; g < i1; g += R) {
+    uint32_t vc[R];
+    uint64_t vb[R];
+#pragma unroll
+    for (uint32_t j = 0; j < R; ++j) {
+      vc[j] = g + j < i1 ? tcnt[g + j] : 0u;
+      vb[j] = g + j < i1 ? tbytes[g + j] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < R; ++j) {
+      const uint64_t i = g + j;
+      if (i >= i1) break;
+      if (i % ntiles == 0) start[i / ntiles] = static_cast<uint32_t>(xc);
+      tcnt[i] = static_cast<uint32_t>(xc);
+      tbytes[i] = xb;
+      xc += vc[j];
+      xb += vb[j];
+    }
+  }
+  if (tid == blockDim.x - 1) {
+    start[nb] = static_cast<uint32_t>(m);
+    sc[m] = xb;  // (the no-request bucket is last and holds no bytes)
+  }
+}
+
+// Stable scatter of one tile's requests to their sorted positions (see above).
+__global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t* __restrict__ key,
+                                                                 const uint64_t* __restrict__ to, uint64_t m,
+                                                                 uint32_t nb, uint32_t ntiles,
+                                                                 const uint32_t* __restrict__ tcnt,
+                                                                 const uint64_t* __restrict__ tbytes,
+                                                                 uint32_t* __restrict__ key_s, uint32_t* __restrict__ perm,
+                                                                 uint32_t* __restrict__ len, uint64_t* __restrict__ sc) {
+  __shared__ uint32_t run_c[kMaxBuckets];
+  __shared__ uint64_t run_b[kMaxBuckets];
+  __shared__ uint32_t w_c[4][kMaxBuckets];
+  __shared__ uint64_t w_b[4][kMaxBuckets];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  for (uint32_t k = tid; k < nb; k += 256) {
+    run_c[k] = tcnt[static_cast<uint64_t>(k) * ntiles + blockIdx.x];
+    run_b[k] = tbytes[static_cast<uint64_t>(k) * ntiles + blockIdx.x];
+    for (uint32_t j = 0; j < 4; ++j) {
+      w_c[j][k] = 0;
+      w_b[j][k] = 0;
+    }
+  }
+  __syncthreads();
+  const uint64_t p0 = static_cast<uint64_t>(blockIdx.x) * kSortTile;
+  const uint64_t p1 = min<uint64_t>(m, p0 + kSortTile);
+  for (uint64_t row = p0; row < p1; row += 256) {  // block-uniform
+    const uint64_t p = row + tid;
+    const bool ok = p < p1;
+    const uint32_t k = ok ? key[p] : 0xFFFFFFFFu;
     uint32_t l = 0;
-    if (k < 2 * world) {
-      const uint32_t t = perm[p] >> 1;
+    if (ok && k < nb - 1) {
+      const uint64_t t = p >> 1;
       l = static_cast<uint32_t>(to[t + 1] - to[t]);
     }
-    len[p] = l;
+    // rank among the wave's lanes with the same key, and the wave's totals per key
+    uint32_t rc = 0;
+    uint64_t rb = 0;
+    uint64_t left = __ballot(ok);
+    while (left) {
+      const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(left));
+      const uint32_t kk = __shfl(k, first, 64);
+      const uint64_t mask = __ballot(ok && k == kk);
+      const bool mine = ok && k == kk;
+      const uint64_t below = mask & ((1ull << lane) - 1ull);
+      // byte prefix among the key's lanes (inclusive scan of l on those lanes)
+      uint64_t v = mine ? l : 0, incl = v;
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t x = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += x;
+      }
+      if (mine) {
+        rc = static_cast<uint32_t>(__popcll(below));
+        rb = incl - v;
+      }
+      const uint64_t tot = __shfl(incl, 63, 64);
+      if (lane == first) {
+        w_c[w][kk] = static_cast<uint32_t>(__popcll(mask));
+        w_b[w][kk] = tot;
+      }
+      left &= ~mask;
+    }
+    __syncthreads();
+    if (ok) {
+      uint32_t pc = run_c[k];
+      uint64_t pb = run_b[k];
+      for (uint32_t j = 0; j < w; ++j) {
+        pc += w_c[j][k];
+        pb += w_b[j][k];
+      }
+      const uint32_t pos = pc + rc;
+      key_s[pos] = k;
+      perm[pos] = static_cast<uint32_t>(p);
+      len[pos] = l;
+      sc[pos] = pb + rb;
+    }
+    __syncthreads();
+    for (uint32_t kk = tid; kk < nb; kk += 256) {
+      uint32_t c = 0;
+      uint64_t b = 0;
+      for (uint32_t j = 0; j < 4; ++j) {
+        c += w_c[j][kk];
+        b += w_b[j][kk];
+        w_c[j][kk] = 0;
+        w_b[j][kk] = 0;
+      }
+      run_c[kk] += c;
+      run_b[kk] += b;
+    }
+    __syncthreads();
   }
 }
 
@@ -164,15 +409,21 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
                                                           uint32_t* __restrict__ err) {
   __shared__ uint64_t sz[kMaxWorld];
   const uint32_t r = threadIdx.x;
-  uint32_t nA = 0, nB = 0;
-  uint64_t bA = 0, bB = 0, size = 0;
+  uint32_t nq[kE] = {};
+  uint64_t by[kE] = {}, size = 0;
+  bool wide = false;
   if (r < world) {
-    const uint32_t s0 = start[2 * r], s1 = start[2 * r + 1], s2 = start[2 * r + 2];
-    nA = s1 - s0;
-    nB = s2 - s1;
-    bA = sc[s1] - sc[s0];
-    bB = sc[s2] - sc[s1];
-    size = 16 + al16(4ull * (nA + nB + 2)) + al16(bA + bB);
+    uint32_t nall = 0;
+    uint64_t ball = 0;
+    for (uint32_t e = 0; e < kE; ++e) {
+      const uint32_t s0 = start[kE * r + e], s1 = start[kE * r + e + 1];
+      nq[e] = s1 - s0;
+      by[e] = sc[s1] - sc[s0];
+      nall += nq[e];
+      ball += by[e];
+      wide |= by[e] > 0xFFFFFFFFull;
+    }
+    size = 4 * kHW + al16(4ull * (nall + kE)) + al16(ball);
     sz[r] = size;
   }
   __syncthreads();
@@ -182,24 +433,28 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
   uint64_t total = 0;
   for (uint32_t j = 0; j < world; ++j) total += sz[j];
   cbase[r] = base;
-  const bool over = total > cap || bA > 0xFFFFFFFFull || bB > 0xFFFFFFFFull;
-  meta[5 * r + 0] = over ? -1 : static_cast<int64_t>(size);
-  meta[5 * r + 1] = nA;
-  meta[5 * r + 2] = nB;
-  meta[5 * r + 3] = static_cast<int64_t>(bA);
-  meta[5 * r + 4] = static_cast<int64_t>(bB);
+  const bool over = total > cap || wide;
+  int64_t* m = meta + (1 + 2 * kE) * r;
+  m[0] = over ? -1 : static_cast<int64_t>(size);
+  for (uint32_t e = 0; e < kE; ++e) {
+    m[1 + e] = nq[e];
+    m[1 + kE + e] = static_cast<int64_t>(by[e]);
+  }
   if (over) {
     if (r == 0) err[0] = 1;
     return;
   }
   if (r == 0) err[0] = 0;
   uint32_t* h = reinterpret_cast<uint32_t*>(send + base);
-  h[0] = nA;
-  h[1] = nB;
-  h[2] = static_cast<uint32_t>(bA);
-  h[3] = static_cast<uint32_t>(bB);
-  h[4 + nA] = static_cast<uint32_t>(bA);           // A offsets[nA]
-  h[4 + nA + 1 + nB] = static_cast<uint32_t>(bB);  // B offsets[nB]
+  uint32_t o = kHW;
+  for (uint32_t e = 0; e < kE; ++e) {
+    h[e] = nq[e];
+    h[4 + e] = static_cast<uint32_t>(by[e]);
+    o += nq[e];
+    h[o++] = static_cast<uint32_t>(by[e]);  // slot e's offsets[n_e]
+  }
+  h[3] = 0;
+  h[7] = 0;
 }
 
 // 4 lanes per request (16 requests a wave, their loads in flight together): its offset entry
@@ -213,18 +468,19 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const uint8_t* __restri
                                                          const uint64_t* __restrict__ cbase, uint32_t world,
                                                          const uint32_t* __restrict__ err, uint8_t* __restrict__ send) {
   if (err[0]) return;
-  const uint32_t nreq = start[2 * world];
+  const uint32_t nreq = start[kE * world];
   const uint32_t sub = threadIdx.x & 3u;
   for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; p < nreq;
        p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
-    const uint32_t b = key_s[p], r = b >> 1, e = b & 1u;
-    const uint32_t s0 = start[2 * r], s1 = start[2 * r + 1], s2 = start[2 * r + 2];
-    const uint32_t nA = s1 - s0, nB = s2 - s1;
+    const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
+    const uint32_t* st = start + kE * r;
+    const uint32_t nall = st[kE] - st[0];
+    uint32_t owords = kHW;  // slot e's offsets start after the earlier slots' (n + 1 each)
+    for (uint32_t k = 0; k < e; ++k) owords += st[k + 1] - st[k] + 1;
     const uint64_t rel = sc[p] - sc[start[b]];
     uint8_t* c = send + cbase[r];
-    if (sub == 0)
-      reinterpret_cast<uint32_t*>(c)[4 + (e ? nA + 1 : 0) + (p - start[b])] = static_cast<uint32_t>(rel);
-    const uint64_t data = 16 + al16(4ull * (nA + nB + 2)) + (e ? sc[s1] - sc[s0] : 0) + rel;
+    if (sub == 0) reinterpret_cast<uint32_t*>(c)[owords + (p - start[b])] = static_cast<uint32_t>(rel);
+    const uint64_t data = 4 * kHW + al16(4ull * (nall + kE)) + (sc[start[b]] - sc[st[0]]) + rel;
     const uint32_t t = perm[p] >> 1;
     const uint64_t a = to[t], len = to[t + 1] - a;
     copy_bytes(tb + a, c + data, len, sub, 4);
@@ -234,8 +490,10 @@ __global__ __launch_bounds__(256) void shard_pack_kernel(const uint8_t* __restri
 // emqx_shard_route_device: the raw requests (req2[2t], req2[2t + 1]) with the same scanner.
 __global__ __launch_bounds__(256) void shard_route_kernel(const uint8_t* __restrict__ tb,
                                                           const uint64_t* __restrict__ to, uint64_t n, uint32_t world,
-                                                          const ShardSplitE* __restrict__ sp, uint32_t nsp,
+                                                          const ShardSplitE* __restrict__ gsp, uint32_t nsp,
                                                           uint32_t* __restrict__ req2) {
+  __shared__ ShardSplitE lsp[kLdsSplits];
+  const ShardSplitE* sp = stage_splits(gsp, nsp, lsp);
   const uint64_t lim = n ? to[n] : 0;
   for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
        t += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
@@ -251,16 +509,28 @@ __global__ __launch_bounds__(256) void shard_route_kernel(const uint8_t* __restr
 
 // ---- recv -------------------------------------------------------------------------------
 
-// grid (x, source, engine): the source's offsets rebased into the batch (its bytes are one
+// Words before slot e's offsets in a request chunk with slot sizes n[]: the header, then each
+// earlier slot's n + 1 offsets.
+__device__ __forceinline__ uint32_t offs_words(const uint32_t* n, uint32_t e) {
+  uint32_t w = kHW;
+  for (uint32_t k = 0; k < e; ++k) w += n[k] + 1;
+  return w;
+}
+
+// grid (x, source, slot): the source's offsets rebased into the slot's batch (its bytes are one
 // contiguous region each, moved by the copy engine: emqx_shard_step_recv).
-__global__ __launch_bounds__(256) void shard_unpack_kernel(const uint8_t* __restrict__ recv, ShardTab tab,
-                                                           uint64_t* __restrict__ a_off, uint64_t* __restrict__ b_off) {
+struct SlotOffsets {
+  uint64_t* p[kE];
+};
+
+__global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOffsets dst_off) {
   const uint32_t s = blockIdx.y, e = blockIdx.z;
-  const uint32_t nA = tab.a0[s + 1] - tab.a0[s], nB = tab.b0[s + 1] - tab.b0[s];
-  const uint32_t* offs = reinterpret_cast<const uint32_t*>(recv + tab.base[s]) + 4 + (e ? nA + 1 : 0);
-  const uint32_t n = e ? nB : nA;
-  const uint64_t dbase = e ? tab.bb0[s] : tab.ab0[s];
-  uint64_t* doff = (e ? b_off : a_off) + (e ? tab.b0[s] : tab.a0[s]);
+  uint32_t nq[kE];
+  for (uint32_t k = 0; k < kE; ++k) nq[k] = tab.q0[k][s + 1] - tab.q0[k][s];
+  const uint32_t* offs = reinterpret_cast<const uint32_t*>(tab.chunk[s]) + offs_words(nq, e);
+  const uint32_t n = nq[e];
+  const uint64_t dbase = tab.y0[e][s];
+  uint64_t* doff = dst_off.p[e] + tab.q0[e][s];
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k <= n; k += stride)
     doff[k] = dbase + offs[k];
@@ -268,59 +538,87 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(const uint8_t* __rest
 
 // ---- answer -----------------------------------------------------------------------------
 
-// grid (x, source): the source's answer chunk from the two CSRs.  An engine call that did not
+struct EngineCsrs {
+  const uint64_t* off[kE];
+  const uint32_t* ids[kE];
+  const uint64_t* sum[kE];  // emqx_match_batch_device_async summaries, or null
+};
+
+// grid (x, source): the source's answer chunk from the three CSRs.  An engine call that did not
 // complete (summary flags) leaves its ids unread: the step is redone.
-__global__ __launch_bounds__(256) void shard_answer_kernel(const uint64_t* __restrict__ a_off,
-                                                           const uint32_t* __restrict__ a_ids,
-                                                           const uint64_t* __restrict__ a_sum,
-                                                           const uint64_t* __restrict__ b_off,
-                                                           const uint32_t* __restrict__ b_ids,
-                                                           const uint64_t* __restrict__ b_sum, ShardTab tab,
-                                                           uint32_t* __restrict__ out, int64_t* __restrict__ ans_meta) {
+__global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardTab tab, uint32_t* __restrict__ out,
+                                                           int64_t* __restrict__ ans_meta) {
   const uint32_t s = blockIdx.y;
-  const uint32_t a0 = tab.a0[s], nA = tab.a0[s + 1] - a0, b0 = tab.b0[s], nB = tab.b0[s + 1] - b0;
-  const bool bad = (a_sum && a_sum[0]) || (b_sum && b_sum[0]);
-  const uint64_t iA0 = a_off[a0], iB0 = b_off[b0];
-  const uint64_t iA = bad ? 0 : a_off[a0 + nA] - iA0, iB = bad ? 0 : b_off[b0 + nB] - iB0;
-  const uint64_t cb = tab.w0[s] + (bad ? 0 : iA0 + iB0);
+  bool bad = false;
+  uint32_t q0[kE], nq[kE];
+  uint64_t i0[kE], ni[kE], nall = 0, iall = 0, ibefore = 0;
+  for (uint32_t e = 0; e < kE; ++e) {
+    bad |= cs.sum[e] && cs.sum[e][0];
+    q0[e] = tab.q0[e][s];
+    nq[e] = tab.q0[e][s + 1] - q0[e];
+    nall += nq[e];
+  }
+  for (uint32_t e = 0; e < kE; ++e) {
+    i0[e] = tab.q0[e][gridDim.y] ? cs.off[e][q0[e]] : 0;  // (a slot no source asked: never read)
+    ni[e] = bad || !nq[e] ? 0 : cs.off[e][q0[e] + nq[e]] - i0[e];
+    iall += ni[e];
+    ibefore += bad ? 0 : i0[e];  // this source's ids start after every earlier source's
+  }
+  const uint64_t cb = tab.w0[s] + ibefore;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    ans_meta[2 * s] = static_cast<int64_t>(4 + nA + nB + iA + iB);
+    ans_meta[2 * s] = static_cast<int64_t>(kHW + nall + iall);
     ans_meta[2 * s + 1] = bad ? 1 : 0;
   }
   if (bad) return;
   uint32_t* c = out + cb;
   const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  if (tid == 0) {
-    c[0] = nA;
-    c[1] = nB;
-    c[2] = static_cast<uint32_t>(iA);
-    c[3] = static_cast<uint32_t>(iB);
+  if (tid < kHW) {
+    uint32_t v = 0;
+    if (tid < kE) v = nq[tid];
+    else if (tid >= 3 && tid < 3 + kE) v = static_cast<uint32_t>(ni[tid - 3]);
+    c[tid] = v;
   }
-  for (uint64_t k = tid; k < nA; k += stride) c[4 + k] = static_cast<uint32_t>(a_off[a0 + k + 1] - a_off[a0 + k]);
-  for (uint64_t k = tid; k < nB; k += stride) c[4 + nA + k] = static_cast<uint32_t>(b_off[b0 + k + 1] - b_off[b0 + k]);
-  uint32_t* ids = c + 4 + nA + nB;
-  for (uint64_t j = tid; j < iA; j += stride) ids[j] = a_ids[iA0 + j];
-  for (uint64_t j = tid; j < iB; j += stride) ids[iA + j] = b_ids[iB0 + j];
+  // per request the END of its ids within the chunk's id region (the merge reads begin and end
+  // without a scan), then the ids
+  uint32_t* end = c + kHW;
+  uint32_t* ids = c + kHW + nall;
+  uint64_t before = 0;
+  for (uint32_t e = 0; e < kE; ++e) {
+    const uint64_t* off = cs.off[e] + q0[e];
+    for (uint64_t k = tid; k < nq[e]; k += stride) end[k] = static_cast<uint32_t>(before + off[k + 1] - i0[e]);
+    const uint32_t* src = cs.ids[e] + i0[e];
+    for (uint64_t j = tid; j < ni[e]; j += stride) ids[j] = src[j];
+    end += nq[e];
+    ids += ni[e];
+    before += ni[e];
+  }
 }
 
 // ---- merge ------------------------------------------------------------------------------
 
-// Per sorted request p: its answer count, and pos[request] = p (kNone for no request).
-__global__ __launch_bounds__(256) void shard_gather_counts_kernel(const uint32_t* __restrict__ back, ShardTab tab,
+// Per sorted request p: its answer count and where its ids begin in its chunk's id region, and
+// pos[request] = p (kNone for no request).
+__global__ __launch_bounds__(256) void shard_gather_counts_kernel(ShardTab tab,
                                                                   const uint32_t* __restrict__ key_s,
                                                                   const uint32_t* __restrict__ perm,
                                                                   const uint32_t* __restrict__ start, uint64_t m,
                                                                   uint32_t world, uint32_t* __restrict__ cnt,
+                                                                  uint32_t* __restrict__ beg,
                                                                   uint32_t* __restrict__ pos) {
-  const uint32_t nreq = start[2 * world];
+  const uint32_t nreq = start[kE * world];
   for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
        p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     uint32_t c = 0;
     if (p < nreq) {
-      const uint32_t b = key_s[p], r = b >> 1, e = b & 1u;
-      const uint32_t* ch = back + tab.base[r];
-      c = ch[4 + (e ? ch[0] : 0) + (p - start[b])];
+      const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
+      const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
+      uint32_t before = 0;
+      for (uint32_t k = 0; k < e; ++k) before += ch[k];
+      const uint32_t k = before + (p - start[b]);
+      const uint32_t b0 = k ? ch[kHW + k - 1] : 0u;
+      c = ch[kHW + k] - b0;
+      beg[p] = b0;
       pos[perm[p]] = static_cast<uint32_t>(p);
     } else {
       pos[perm[p]] = kNone;
@@ -341,28 +639,28 @@ __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t*
 
 // 4 lanes per request, in request (send) order: its answer's ids, read from the answer chunk
 // where they lie in that same order (coalesced), to its topic's place in the output: the
-// topic's offset, after the topic's engine-A ids for an engine-B request.
-__global__ __launch_bounds__(256) void shard_merge_kernel(const uint32_t* __restrict__ back, ShardTab tab,
+// topic's offset, after the ids of the topic's first request for its second.
+__global__ __launch_bounds__(256) void shard_merge_kernel(ShardTab tab,
                                                           const uint32_t* __restrict__ key_s,
                                                           const uint32_t* __restrict__ perm,
                                                           const uint32_t* __restrict__ start,
                                                           const uint32_t* __restrict__ cnt,
-                                                          const uint64_t* __restrict__ csc,
+                                                          const uint32_t* __restrict__ beg,
                                                           const uint32_t* __restrict__ pos, uint32_t world,
                                                           const uint64_t* __restrict__ out_off,
                                                           uint32_t* __restrict__ out_ids) {
-  const uint32_t nreq = start[2 * world];
+  const uint32_t nreq = start[kE * world];
   const uint32_t sub = threadIdx.x & 3u;
   for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; p < nreq;
        p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
     const uint32_t c = cnt[p];
     if (c == 0) continue;
-    const uint32_t q = perm[p], t = q >> 1, e = q & 1u;
-    const uint32_t b = key_s[p], r = b >> 1;
-    const uint32_t* ch = back + tab.base[r];
-    const uint64_t src = 4ull + ch[0] + ch[1] + (e ? ch[2] : 0u) + (csc[p] - csc[start[b]]);
+    const uint32_t q = perm[p], t = q >> 1, second = q & 1u;
+    const uint32_t r = key_s[p] / kE;
+    const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
+    const uint64_t src = kHW + ch[0] + ch[1] + ch[2] + beg[p];
     uint64_t dst = out_off[t];
-    if (e) {
+    if (second) {
       const uint32_t pa = pos[2 * t];
       if (pa != kNone) dst += cnt[pa];
     }
@@ -370,7 +668,6 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(const uint32_t* __rest
   }
 }
 
-using SortCfg = rocprim::default_config;
 
 }  // namespace
 
@@ -393,12 +690,10 @@ struct emqx_shard_step {
   uint32_t n_splits = 0;
   // request scratch, sized for m_cap requests
   uint64_t m_cap = 0;
-  uint32_t *key = nullptr, *idx = nullptr, *key_s = nullptr, *perm = nullptr, *len = nullptr, *pos = nullptr,
-           *tcnt = nullptr;
-  uint64_t *sc = nullptr, *partials = nullptr;
-  void* sort_temp = nullptr;
-  size_t sort_bytes = 0;
-  uint32_t* start = nullptr;  // [2G + 2]
+  uint32_t *key = nullptr, *key_s = nullptr, *perm = nullptr, *len = nullptr, *pos = nullptr, *tcnt = nullptr,
+           *beg = nullptr, *tcnt_tab = nullptr;
+  uint64_t *sc = nullptr, *partials = nullptr, *tbytes_tab = nullptr;  // (tab: the sort's (bucket, tile) table)
+  uint32_t* start = nullptr;  // [kE G + 2]
   uint64_t* cbase = nullptr;  // [G]
   uint32_t* err = nullptr;
   // the step in flight
@@ -410,16 +705,14 @@ struct emqx_shard_step {
 namespace {
 
 void free_scratch(emqx_shard_step* st) {
-  for (void* p : {static_cast<void*>(st->key), static_cast<void*>(st->idx), static_cast<void*>(st->key_s),
+  for (void* p : {static_cast<void*>(st->key), static_cast<void*>(st->tcnt_tab), static_cast<void*>(st->key_s),
                   static_cast<void*>(st->perm), static_cast<void*>(st->len), static_cast<void*>(st->pos),
                   static_cast<void*>(st->tcnt), static_cast<void*>(st->sc), static_cast<void*>(st->partials),
-                  st->sort_temp})
+                  static_cast<void*>(st->beg), static_cast<void*>(st->tbytes_tab)})
     if (p) (void)hipFree(p);
-  st->key = st->idx = st->key_s = st->perm = st->len = st->pos = st->tcnt = nullptr;
-  st->sc = st->partials = nullptr;
-  st->sort_temp = nullptr;
+  st->key = st->tcnt_tab = st->key_s = st->perm = st->len = st->pos = st->tcnt = st->beg = nullptr;
+  st->sc = st->partials = st->tbytes_tab = nullptr;
   st->m_cap = 0;
-  st->sort_bytes = 0;
 }
 
 // Scratch for m requests (grown geometrically; hipFree waits for the device, so nothing in
@@ -433,24 +726,17 @@ hipError_t ensure_scratch(emqx_shard_step* st, uint64_t m) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(p), std::max<uint64_t>(bytes, 16));
   };
   al(&st->key, 4 * cap);
-  al(&st->idx, 4 * cap);
+  const uint64_t tab = (kE * st->world + 1ull) * ((cap + kSortTile - 1) / kSortTile + 1);
+  al(&st->tcnt_tab, 4 * tab);
+  al(&st->tbytes_tab, 8 * tab);
   al(&st->key_s, 4 * cap);
   al(&st->perm, 4 * cap);
   al(&st->len, 4 * cap);
   al(&st->pos, 4 * cap);
+  al(&st->beg, 4 * cap);
   al(&st->tcnt, 4 * (cap / 2 + 1));
   al(&st->sc, 8 * (cap + 1));
   al(&st->partials, 8 * scan_partials(cap));
-  size_t tb = 0;
-  if (e == hipSuccess)
-    e = rocprim::radix_sort_pairs<SortCfg>(nullptr, tb, static_cast<const uint32_t*>(nullptr),
-                                           static_cast<uint32_t*>(nullptr), static_cast<const uint32_t*>(nullptr),
-                                           static_cast<uint32_t*>(nullptr), static_cast<size_t>(cap), 0u,
-                                           bucket_bits(st->world));
-  if (e == hipSuccess) {
-    st->sort_bytes = tb;
-    al(&st->sort_temp, tb);
-  }
   if (e != hipSuccess) {
     free_scratch(st);
     return e;
@@ -472,7 +758,7 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? EMQX_OK : (e == hipErrorOutO
 extern "C" {
 
 uint64_t emqx_shard_send_cap(uint64_t n, uint64_t batch_bytes, uint32_t world) {
-  return 48ull * std::max<uint32_t>(world, 1) + 8 * n + 2 * batch_bytes + 64;
+  return 96ull * std::max<uint32_t>(world, 1) + 8 * n + 2 * batch_bytes + 64;
 }
 
 int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* splits, uint32_t n_splits,
@@ -489,7 +775,7 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
   if (e == hipSuccess && n_splits)
     e = hipMemcpy(st->d_splits, splits, 8ull * n_splits, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // (the DMA has landed: steps run on other streams)
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->start), 4ull * (2 * world + 2));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->start), 4ull * (kE * world + 2));
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->cbase), 8ull * world);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->err), 16);
   if (e != hipSuccess) {
@@ -521,21 +807,18 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
   SS_TRY(ensure_scratch(st, m));
   const uint32_t G = st->world;
   if (m) {
-    hipLaunchKernelGGL(shard_key_kernel, dim3(grid_of(n, 256, 4096)), dim3(256), 0, s, d_bytes, d_offsets, n, G,
-                       st->d_splits, st->n_splits, st->key, st->idx);
-    size_t tb = 0;
-    SS_TRY(rocprim::radix_sort_pairs<SortCfg>(nullptr, tb, st->key, st->key_s, st->idx, st->perm,
-                                              static_cast<size_t>(m), 0u, bucket_bits(G), s));
-    if (tb > st->sort_bytes) return EMQX_EDEVICE;  // (sized for m_cap >= m)
-    tb = st->sort_bytes;
-    SS_TRY(rocprim::radix_sort_pairs<SortCfg>(st->sort_temp, tb, st->key, st->key_s, st->idx, st->perm,
-                                              static_cast<size_t>(m), 0u, bucket_bits(G), s));
-    hipLaunchKernelGGL(shard_bounds_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, st->key_s, st->perm, d_offsets, m,
-                       G, st->start, st->len);
+    const uint32_t nb = kE * G + 1;
+    const uint32_t ntiles = static_cast<uint32_t>((m + kSortTile - 1) / kSortTile);
+    hipLaunchKernelGGL(shard_key_kernel, dim3(ntiles), dim3(256), 0, s, d_bytes, d_offsets, n, G, st->d_splits,
+                       st->n_splits, st->key, ntiles, st->tcnt_tab, st->tbytes_tab);
+    hipLaunchKernelGGL(shard_sort_scan_kernel, dim3(1), dim3(1024), 0, s, st->tcnt_tab, st->tbytes_tab, nb, ntiles, m,
+                       st->start, st->sc);
+    hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_offsets, m, nb, ntiles,
+                       st->tcnt_tab, st->tbytes_tab, st->key_s, st->perm, st->len, st->sc);
   } else {
-    SS_TRY(hipMemsetAsync(st->start, 0, 4ull * (2 * G + 2), s));
+    SS_TRY(hipMemsetAsync(st->start, 0, 4ull * (kE * G + 2), s));
+    SS_TRY(hipMemsetAsync(st->sc, 0, 8, s));
   }
-  SS_TRY(launch_scan(st->len, m, st->sc, st->partials, s));
   hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->sc, G, d_send, send_cap, d_meta,
                      st->cbase, st->err);
   if (m)
@@ -548,83 +831,111 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
   return EMQX_OK;
 }
 
-int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* d_recv, const int64_t* meta_in, uint8_t* d_a_bytes,
-                         uint64_t* d_a_offsets, uint8_t* d_b_bytes, uint64_t* d_b_offsets, void* stream) {
-  if (!st || !meta_in || !d_a_offsets || !d_b_offsets) return EMQX_EINVAL;
+int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, const int64_t* meta_in,
+                         uint8_t** d_bytes, uint64_t* const* d_offsets, void* stream) {
+  if (!st || !d_chunks || !meta_in || !d_bytes || !d_offsets) return EMQX_EINVAL;
+  for (uint32_t e = 0; e < kE; ++e)
+    if (!d_offsets[e]) return EMQX_EINVAL;
   const uint32_t G = st->world;
   ShardTab& t = st->recv_tab;
   t = ShardTab{};
   uint64_t words = 0;
   for (uint32_t r = 0; r < G; ++r) {
-    const int64_t* m = meta_in + 5 * r;
-    if (m[0] < 0 || m[1] < 0 || m[2] < 0 || m[3] < 0 || m[4] < 0) return EMQX_EINVAL;
-    t.base[r + 1] = t.base[r] + static_cast<uint64_t>(m[0]);
-    t.a0[r + 1] = t.a0[r] + static_cast<uint32_t>(m[1]);
-    t.b0[r + 1] = t.b0[r] + static_cast<uint32_t>(m[2]);
-    t.ab0[r + 1] = t.ab0[r] + static_cast<uint64_t>(m[3]);
-    t.bb0[r + 1] = t.bb0[r] + static_cast<uint64_t>(m[4]);
+    const int64_t* m = meta_in + (1 + 2 * kE) * r;
+    for (uint32_t k = 0; k < 1 + 2 * kE; ++k)
+      if (m[k] < 0) return EMQX_EINVAL;
+    if (m[0] && !d_chunks[r]) return EMQX_EINVAL;
+    t.chunk[r] = reinterpret_cast<uint64_t>(d_chunks[r]);
+    uint64_t nall = 0;
+    for (uint32_t e = 0; e < kE; ++e) {
+      t.q0[e][r + 1] = t.q0[e][r] + static_cast<uint32_t>(m[1 + e]);
+      t.y0[e][r + 1] = t.y0[e][r] + static_cast<uint64_t>(m[1 + kE + e]);
+      nall += static_cast<uint64_t>(m[1 + e]);
+    }
     t.w0[r] = words;
-    words += 4 + static_cast<uint64_t>(m[1] + m[2]);
+    words += kHW + nall;
   }
   t.w0[G] = words;
-  if ((t.base[G] && !d_recv) || (t.ab0[G] && !d_a_bytes) || (t.bb0[G] && !d_b_bytes)) return EMQX_EINVAL;
+  // a slot whose requests all come from one source is read in place from that source's chunk
+  // (its offsets rebased from 0 are already relative to its byte region): no copy
+  int only[kE];
+  for (uint32_t e = 0; e < kE; ++e) {
+    only[e] = -1;
+    for (uint32_t r = 0; r < G; ++r)
+      if (t.q0[e][r + 1] != t.q0[e][r]) only[e] = only[e] == -1 ? static_cast<int>(r) : -2;
+    if (only[e] < 0 && t.y0[e][G] && !d_bytes[e]) return EMQX_EINVAL;
+  }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
-  const uint64_t per = (t.a0[G] + t.b0[G]) / (2 * G) + 1;  // offsets per (source, engine)
+  SlotOffsets so{};
+  for (uint32_t e = 0; e < kE; ++e) so.p[e] = d_offsets[e];
+  uint64_t qall = 0;
+  for (uint32_t e = 0; e < kE; ++e) qall += t.q0[e][G];
+  const uint64_t per = qall / (kE * G) + 1;  // offsets per (source, slot)
   const uint32_t x = grid_of(per, 256, std::max<uint32_t>(1, 1024 / G));
-  hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, 2), dim3(256), 0, s, d_recv, t, d_a_offsets, d_b_offsets);
+  hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, kE), dim3(256), 0, s, t, so);
   SS_TRY(hipGetLastError());
-  for (uint32_t r = 0; r < G; ++r) {  // each source's A bytes, then its B bytes: contiguous both sides
-    const uint64_t nA = t.a0[r + 1] - t.a0[r], nB = t.b0[r + 1] - t.b0[r];
-    const uint64_t bA = t.ab0[r + 1] - t.ab0[r], bB = t.bb0[r + 1] - t.bb0[r];
-    const uint8_t* data = d_recv + t.base[r] + 16 + al16(4ull * (nA + nB + 2));
-    if (bA) SS_TRY(hipMemcpyAsync(d_a_bytes + t.ab0[r], data, bA, hipMemcpyDeviceToDevice, s));
-    if (bB) SS_TRY(hipMemcpyAsync(d_b_bytes + t.bb0[r], data + bA, bB, hipMemcpyDeviceToDevice, s));
+  for (uint32_t r = 0; r < G; ++r) {  // each source's slot-0 bytes, slot 1, slot 2: contiguous both sides
+    uint64_t nall = 0;
+    for (uint32_t e = 0; e < kE; ++e) nall += t.q0[e][r + 1] - t.q0[e][r];
+    const uint8_t* data = d_chunks[r] + 4 * kHW + al16(4ull * (nall + kE));
+    for (uint32_t e = 0; e < kE; ++e) {
+      const uint64_t by = t.y0[e][r + 1] - t.y0[e][r];
+      if (only[e] == static_cast<int>(r)) d_bytes[e] = const_cast<uint8_t*>(data);
+      else if (by) SS_TRY(hipMemcpyAsync(d_bytes[e] + t.y0[e][r], data, by, hipMemcpyDeviceToDevice, s));
+      data += by;
+    }
   }
   st->have_recv = true;
   return EMQX_OK;
 }
 
-int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* d_a_offsets, const uint32_t* d_a_ids,
-                           const uint64_t* d_a_summary, const uint64_t* d_b_offsets, const uint32_t* d_b_ids,
-                           const uint64_t* d_b_summary, uint32_t* d_answer, int64_t* d_ans_meta, void* stream) {
-  if (!st || !st->have_recv || !d_a_offsets || !d_b_offsets || !d_answer || !d_ans_meta) return EMQX_EINVAL;
+int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* const* d_offsets, const uint32_t* const* d_ids,
+                           const uint64_t* const* d_summaries, uint32_t* d_answer, int64_t* d_ans_meta,
+                           void* stream) {
+  if (!st || !st->have_recv || !d_offsets || !d_ids || !d_answer || !d_ans_meta) return EMQX_EINVAL;
   const uint32_t G = st->world;
   const ShardTab& t = st->recv_tab;
+  EngineCsrs cs{};
+  uint64_t qall = 0;
+  for (uint32_t e = 0; e < kE; ++e) {
+    if (!d_offsets[e] || (t.q0[e][G] && !d_ids[e])) return EMQX_EINVAL;
+    cs.off[e] = d_offsets[e];
+    cs.ids[e] = d_ids[e];
+    cs.sum[e] = d_summaries ? d_summaries[e] : nullptr;
+    qall += t.q0[e][G];
+  }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
-  const uint32_t x = grid_of(8 * (t.a0[G] + t.b0[G]) / G + 1, 256, std::max<uint32_t>(1, 1024 / G));  // ~8 ids a request
-  hipLaunchKernelGGL(shard_answer_kernel, dim3(x, G), dim3(256), 0, s, d_a_offsets, d_a_ids, d_a_summary, d_b_offsets,
-                     d_b_ids, d_b_summary, t, d_answer, d_ans_meta);
+  const uint32_t x = grid_of(8 * qall / G + 1, 256, std::max<uint32_t>(1, 1024 / G));  // ~8 ids a request
+  hipLaunchKernelGGL(shard_answer_kernel, dim3(x, G), dim3(256), 0, s, cs, t, d_answer, d_ans_meta);
   SS_TRY(hipGetLastError());
   return EMQX_OK;
 }
 
-int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* d_back, const int64_t* ans_meta_in,
+int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, const int64_t* ans_meta_in,
                           uint64_t* d_out_offsets, uint32_t* d_out_ids, void* stream) {
-  if (!st || !st->have_send || !ans_meta_in || !d_out_offsets) return EMQX_EINVAL;
+  if (!st || !st->have_send || !d_chunks || !ans_meta_in || !d_out_offsets) return EMQX_EINVAL;
   const uint32_t G = st->world;
   ShardTab t{};
   for (uint32_t r = 0; r < G; ++r) {
-    if (ans_meta_in[2 * r] < 4 || ans_meta_in[2 * r + 1] != 0) return EMQX_EINVAL;
-    t.base[r + 1] = t.base[r] + static_cast<uint64_t>(ans_meta_in[2 * r]);
+    if (ans_meta_in[2 * r] < kHW || ans_meta_in[2 * r + 1] != 0 || !d_chunks[r]) return EMQX_EINVAL;
+    t.chunk[r] = reinterpret_cast<uint64_t>(d_chunks[r]);
   }
-  if (!d_back) return EMQX_EINVAL;
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
   const uint64_t n = st->n, m = 2 * n;
   if (m) {
-    hipLaunchKernelGGL(shard_gather_counts_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, d_back, t, st->key_s,
-                       st->perm, st->start, m, G, st->len, st->pos);
-    SS_TRY(launch_scan(st->len, m, st->sc, st->partials, s));
+    hipLaunchKernelGGL(shard_gather_counts_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, t, st->key_s,
+                       st->perm, st->start, m, G, st->len, st->beg, st->pos);
     hipLaunchKernelGGL(shard_topic_counts_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, st->len, st->pos, n,
                        st->tcnt);
   }
   SS_TRY(launch_scan(st->tcnt, n, d_out_offsets, st->partials, s));
   if (n) {
     if (!d_out_ids) return EMQX_EINVAL;
-    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, d_back, t, st->key_s, st->perm,
-                       st->start, st->len, st->sc, st->pos, G, d_out_offsets, d_out_ids);
+    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, t, st->key_s, st->perm,
+                       st->start, st->len, st->beg, st->pos, G, d_out_offsets, d_out_ids);
   }
   SS_TRY(hipGetLastError());
   return EMQX_OK;

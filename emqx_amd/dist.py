@@ -18,10 +18,13 @@ SURVEY §8(e).  Two layouts:
       of them.
   A topic l1/l2/... makes one request to its L-space rank's engine A and, if it has a second
   level and is not a '$' topic, one to its P-space rank's engine B; every filter that can match
-  it lives, once, on one of the two, so the answers concatenate (``shard_route``).  Each rank
-  partitions its batch's requests by (rank, engine), one all-to-all carries them to their
-  owners, each rank matches what it received on its two engines, and one all-to-all brings the
-  results back, where they are merged per topic in batch order.  The busiest rank holds
+  it lives, once, on one of the two, so the answers concatenate (``shard_route``).  A rank
+  holds three engines: A, B, and AB (its A and B filters in one table); a topic whose two
+  requests name the same rank, or that makes only one, asks that rank's AB engine once
+  (``fold_requests``) — at world 1 that is every topic, one walk each, as replication.  Each
+  rank partitions its batch's requests by (rank, engine slot), one all-to-all carries them to
+  their owners, each rank matches what it received on its engines, and one all-to-all brings
+  the results back, where they are merged per topic in batch order.  The busiest rank holds
   18 % of config C's filters at G = 8 (the replicated share was 29 % with the
   round-2 layout), and each rank walks ~1/G of the topics' node visits.
   Each engine is built with GLOBAL filter ids (``emqx_insert_filters_ext``).
@@ -182,7 +185,38 @@ def _a2a(out_t: torch.Tensor, in_t: torch.Tensor, out_splits: List[int], in_spli
     dist.all_to_all_single(out_t, in_t, out_splits, in_splits, group=group)
 
 
+def _exchange_chunks(send: torch.Tensor, out_sz: List[int], in_sz: List[int], recv_buf: Callable, group,
+                     rank: int) -> List[int]:
+    """Chunk r of ``send`` (sizes ``out_sz`` in rank order, contiguous) to rank r; returns the
+    device addresses of the chunks every source sent this rank.  The rank's own chunk is not
+    moved: its address is where it lies in ``send`` (an all-to-all over one rank is no call at
+    all).  RCCL: one grouped all_to_all of the other ranks' chunks.  gloo (rehearsals with
+    device tensors through host copies) has no list all-to-all: all_to_all_single, the own chunk
+    copied along and not read."""
+    G = len(out_sz)
+    out_off = np.concatenate([[0], np.cumsum(out_sz)]).astype(np.int64)
+    es = send.element_size()
+    base = send.data_ptr()
+    if G == 1:
+        return [base]
+    if dist.get_backend(group) == "gloo":
+        in_off = np.concatenate([[0], np.cumsum(in_sz)]).astype(np.int64)
+        recv = recv_buf(int(in_off[-1]))
+        _a2a(recv[: int(in_off[-1])], send[: int(out_off[-1])], in_sz, out_sz, group)
+    else:
+        in_sz = [0 if r == rank else x for r, x in enumerate(in_sz)]
+        in_off = np.concatenate([[0], np.cumsum(in_sz)]).astype(np.int64)
+        recv = recv_buf(int(in_off[-1]))
+        empty = send[:0]
+        outs = [recv[int(in_off[r]): int(in_off[r + 1])] if r != rank else empty for r in range(G)]
+        ins = [send[int(out_off[r]): int(out_off[r + 1])] if r != rank else empty for r in range(G)]
+        dist.all_to_all(outs, ins, group=group)
+    rb = recv.data_ptr()
+    return [base + es * int(out_off[r]) if r == rank else rb + es * int(in_off[r]) for r in range(G)]
+
+
 SHARD_NONE = 0xFFFFFFFF
+SHARD_ENGINES = 3  # engine slots of a rank: 0 = A, 1 = B, 2 = AB (include/emqx_match.h)
 MAX_PIECE_PM = 250  # a key is split when its filters exceed a quarter of a rank's share
 
 
@@ -223,14 +257,32 @@ def shard_place(filters: Tuple[np.ndarray, np.ndarray], world: int, plan: np.nda
 
 
 def shard_local_ids(filters: Tuple[np.ndarray, np.ndarray], rank: int, world: int, plan: np.ndarray):
-    """[global ids of engine A, global ids of engine B] for this rank (uint32, ascending)."""
+    """[global ids of engine A, of engine B, of engine AB (A and B together)] for this rank
+    (uint32, ascending)."""
     first, span, eng = shard_place(filters, world, plan)
     held = ((rank - first.astype(np.int64)) % world) < span
-    return [np.nonzero(held & (eng == e))[0].astype(np.uint32) for e in (0, 1)]
+    return [np.nonzero(held & (eng == e))[0].astype(np.uint32) for e in (0, 1)] + [
+        np.nonzero(held)[0].astype(np.uint32)]
+
+
+def fold_requests(req: torch.Tensor, world: int) -> torch.Tensor:
+    """(n, 2) raw requests (topic_requests) -> (n, 2) engine-slot keys rank * 3 + slot (3 * world
+    = none), as the device step folds them (shard_step.hip shard_fold): two requests to two
+    ranks stay A (slot 0) and B (slot 1); two to one rank, or a single one, become one request to
+    that rank's AB engine (slot 2), in the first column."""
+    E = SHARD_ENGINES
+    none = torch.full_like(req[:, 0], E * world)
+    a, b = req[:, 0] >= 0, req[:, 1] >= 0
+    ra, rb = torch.div(req[:, 0], 2, rounding_mode="floor"), torch.div(req[:, 1], 2, rounding_mode="floor")
+    split = a & b & (ra != rb)
+    k0 = torch.where(split, E * ra, torch.where(a, E * ra + 2, torch.where(b, E * rb + 2, none)))
+    k1 = torch.where(split, E * rb + 1, none)
+    return torch.stack([k0, k1], 1)
 
 
 def shard_engines(filters: Tuple[np.ndarray, np.ndarray], rank: int, world: int, plan: np.ndarray):
-    """[(packed filters, global ids) of engine A, ... of engine B] for this rank."""
+    """[(packed filters, global ids) of engine A, ... of engine B, ... of engine AB] for this
+    rank."""
     from .workloads import take
     return [(take(filters, gids), gids) for gids in shard_local_ids(filters, rank, world, plan)]
 
@@ -333,10 +385,10 @@ class ShardedMatcher:
     def __init__(self, filters: Tuple[np.ndarray, np.ndarray], group=None, device: Optional[torch.device] = None,
                  mode: int = 0, match_fn: Optional[Callable] = None, max_piece_pm: int = MAX_PIECE_PM,
                  engines: Optional[list] = None):
-        """``engines``: this rank's two engines already built ([A, B], each holding exactly the
-        filters shard_local_ids names for it, reporting global ids); they are adopted, not
-        copied (e.g. a table held whole on one GPU becomes engine A at world 1 once its P-space
-        filters are deleted from it, tests/test_gpu_c100m.py)."""
+        """``engines``: this rank's engines already built ([A, B, AB], each holding exactly the
+        filters shard_local_ids names for it, reporting global ids; A and B may be None at world
+        1, where every request is an AB request); they are adopted, not copied (e.g. a table
+        held whole on one GPU is engine AB at world 1, tests/test_gpu_c100m.py)."""
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -349,14 +401,19 @@ class ShardedMatcher:
         self.local_ids = shard_local_ids(filters, self.rank, self.world, self.plan)
         self.engines = []
         self.last_local_topics = 0
+        self.last_slot_topics = [0, 0, 0]
         if engines is not None:
-            assert match_fn is None and len(engines) == 2
+            assert match_fn is None and len(engines) == SHARD_ENGINES
+            assert self.world > 1 or engines[2] is not None
             self.engines = list(engines)
             match_fn = self._engine_match
         elif match_fn is None:
             from .engine import Engine
             from .workloads import take
-            for gids in self.local_ids:
+            for slot, gids in enumerate(self.local_ids):
+                if self.world == 1 and slot < 2:  # no request ever names A or B alone
+                    self.engines.append(None)
+                    continue
                 e = Engine(self.device.index if self.device.type == "cuda" else -1)
                 if len(gids):
                     e.insert_packed_ext(*take(filters, gids), gids)
@@ -368,30 +425,32 @@ class ShardedMatcher:
         # an injected match_fn (tests on CPU over gloo) takes the tensor path below
         self._step = _DeviceStep(self.device, self.world, self.plan) if (
             self.device.type == "cuda" and self.match_fn == self._engine_match) else None
-        self._caps = [1 << 20, 1 << 20]
+        self._caps = [1 << 20] * SHARD_ENGINES
         self._bufs = {}
         self._stream = None
         self._stream_b = None
 
     @property
     def n_local_filters(self) -> int:
-        return int(sum(len(g) for g in self.local_ids))
+        return int(len(self.local_ids[2]))
 
     def _engine_match(self, which: int, tb: torch.Tensor, to: torch.Tensor):
         d_off, d_ids = self._engine_csr(which, tb, to)
         return d_off[1:] - d_off[:-1], d_ids
 
-    def _engine_csr(self, which: int, tb: torch.Tensor, to: torch.Tensor):
-        """Synchronous match on engine `which`, growing the id buffer to the exact need."""
-        n = to.numel() - 1
+    def _engine_csr(self, which: int, tb, to: torch.Tensor, n: Optional[int] = None):
+        """Synchronous match on engine `which`, growing the id buffer to the exact need (tb: a
+        byte tensor, or a device address)."""
+        n = to.numel() - 1 if n is None else n
+        tb_addr = tb if isinstance(tb, int) else tb.data_ptr()
         d_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
-        caps = getattr(self, "_caps", [1 << 20, 1 << 20])
+        caps = getattr(self, "_caps", [1 << 20] * SHARD_ENGINES)
         cap = max(1 << 16, caps[which])
         stream = torch.cuda.current_stream(self.device).cuda_stream
         while True:
             d_ids = torch.empty(cap, dtype=torch.int32, device=self.device)
             try:
-                m = self.engines[which].match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(),
+                m = self.engines[which].match_device(tb_addr, to.data_ptr(), n, d_off.data_ptr(),
                                                      d_ids.data_ptr(), cap, mode=self.mode, stream=stream)
                 break
             except Exception as e:  # EMQX_EOVERFLOW: retry with the exact capacity
@@ -432,18 +491,21 @@ class ShardedMatcher:
         return b
 
     def _match_all_device(self, topics: Tuple[torch.Tensor, torch.Tensor]):
-        """match_all on device kernels (emqx_shard_step_*, shard_step.hip): route + stable sort
-        + pack the requests, one all-to-all of sizes and one of chunks, unpack into the two
-        engines' batches, both engines matched asynchronously into learnt capacities, the
+        """match_all on device kernels (emqx_shard_step_*, shard_step.hip): route + fold + stable
+        sort + pack the requests, one all-to-all of sizes and one of chunks, unpack into the
+        engine slots' batches, the engines matched asynchronously into learnt capacities, the
         answers packed per source, one all-to-all of sizes and one of answers, merged back in
         batch order.  The host only reads the split sizes (two syncs)."""
         from . import _lib
         L = _lib.lib()
+        E = SHARD_ENGINES
         dev, G, grp = self.device, self.world, self.group
         st = self._step.h
         stream = torch.cuda.current_stream(dev).cuda_stream
         P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        PA = lambda ts: (ctypes.c_void_p * E)(*[None if t is None else t.data_ptr() for t in ts])  # noqa: E731
         S = ctypes.c_void_p(stream)
+        MW = 1 + 2 * E  # meta words per destination
         tb, to = topics
         tb = tb.to(dev)
         to = to.to(dev).to(torch.int64)
@@ -453,119 +515,134 @@ class ShardedMatcher:
         # 1. requests -> one chunk per destination
         cap = int(L.emqx_shard_send_cap(n, tb.numel(), G))
         send = self._buf("send", cap, torch.uint8)
-        meta = torch.empty(5 * G, dtype=torch.int64, device=dev)
+        meta = torch.empty(MW * G, dtype=torch.int64, device=dev)
         _lib.check(L.emqx_shard_step_send(st, P(tb), P(to), n, P(send), send.numel(), P(meta), S),
                    "emqx_shard_step_send")
-        meta_in = torch.empty_like(meta)
-        _a2a(meta_in, meta, [5] * G, [5] * G, grp)
-        mh = torch.stack([meta, meta_in]).cpu().numpy()  # host sync 1
-        mo, mi = mh[0].reshape(G, 5), np.ascontiguousarray(mh[1].reshape(G, 5))
+        if G == 1:
+            mh = meta.cpu().numpy()  # host sync 1
+            mo = mi = np.ascontiguousarray(mh.reshape(G, MW))
+        else:
+            meta_in = torch.empty_like(meta)
+            _a2a(meta_in, meta, [MW] * G, [MW] * G, grp)
+            mh = torch.stack([meta, meta_in]).cpu().numpy()  # host sync 1
+            mo, mi = mh[0].reshape(G, MW), np.ascontiguousarray(mh[1].reshape(G, MW))
         if (mo[:, 0] < 0).any() or (mi[:, 0] < 0).any():
             raise RuntimeError("emqx_shard_step_send: chunks over the send buffer")
         out_b, in_b = mo[:, 0].tolist(), mi[:, 0].tolist()
-        recv = self._buf("recv", sum(in_b) + 16, torch.uint8)
-        _a2a(recv[: sum(in_b)], send[: sum(out_b)], in_b, out_b, grp)
-        NA, NB = int(mi[:, 1].sum()), int(mi[:, 2].sum())
-        a_bytes = self._buf("a_bytes", int(mi[:, 3].sum()) + 16, torch.uint8)
-        b_bytes = self._buf("b_bytes", int(mi[:, 4].sum()) + 16, torch.uint8)
-        a_off = self._buf("a_off", NA + 1, torch.int64)
-        b_off = self._buf("b_off", NB + 1, torch.int64)
-        _lib.check(L.emqx_shard_step_recv(st, P(recv), mi.ctypes.data, P(a_bytes), P(a_off), P(b_bytes), P(b_off), S),
+        chunks = _exchange_chunks(send, out_b, in_b, lambda k: self._buf("recv", k + 16, torch.uint8), grp,
+                                  self.rank)
+        NQ = [int(mi[:, 1 + e].sum()) for e in range(E)]
+        # a slot fed by one source only is matched in place in that source's chunk (recv
+        # replaces its byte buffer's address); the others are gathered into these buffers
+        one = [int(np.count_nonzero(mi[:, 1 + e])) <= 1 for e in range(E)]
+        qbytes = [None if one[e] else self._buf(f"q_bytes{e}", int(mi[:, 1 + E + e].sum()) + 16, torch.uint8)
+                  for e in range(E)]
+        qoff = [self._buf(f"q_off{e}", NQ[e] + 1, torch.int64) for e in range(E)]
+        qb = PA(qbytes)
+        _lib.check(L.emqx_shard_step_recv(st, (ctypes.c_void_p * G)(*chunks), mi.ctypes.data, qb, PA(qoff), S),
                    "emqx_shard_step_recv")
-        self.last_local_topics = NA + NB
-        # 2. the two engines, asynchronously, into learnt capacities; engine B on a second
-        # stream, so the two walks overlap
-        batches = [(a_bytes, a_off, NA), (b_bytes, b_off, NB)]
+        qaddr = [qb[e] for e in range(E)]
+        self.last_local_topics = sum(NQ)
+        self.last_slot_topics = NQ
+        # 2. the engines, asynchronously, into learnt capacities; each on a stream of its own
+        # after the first, so the walks overlap
+        batches = [(qaddr[e], qoff[e], NQ[e]) for e in range(E)]
         outs = []
-        summ = self._buf("summary", 16, torch.int64)
-        summ[:16].zero_()
+        summ = self._buf("summary", 8 * E, torch.int64)  # written by each engine call that runs
         cur = torch.cuda.current_stream(dev)
         if self._stream_b is None:
-            self._stream_b = torch.cuda.Stream(device=dev)
-        self._stream_b.wait_stream(cur)
+            self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E - 1)]
+        used = []
         for e, (eb, eo, ne) in enumerate(batches):
-            cap_e = max(self._caps[e], 1 << 16)
             ro = self._buf(f"off{e}", ne + 1, torch.int64)
+            if not ne:  # (a slot no source asked: the answer kernel reads nothing of it)
+                outs.append([ro, self._buf(f"ids{e}", 16, torch.int32)])
+                continue
+            cap_e = max(self._caps[e], 1 << 16)
             ri = self._buf(f"ids{e}", cap_e, torch.int32)
-            es = cur if e == 0 else self._stream_b
-            if ne:
-                self.engines[e].match_device_async(eb.data_ptr(), eo.data_ptr(), ne, ro.data_ptr(), ri.data_ptr(),
-                                                   ri.numel(), summ[8 * e:].data_ptr(), mode=self.mode,
-                                                   stream=es.cuda_stream)
-            else:
-                with torch.cuda.stream(es):
-                    ro[:1].zero_()
+            es = cur if not used else self._stream_b[len(used) - 1]
+            if es is not cur:
+                es.wait_stream(cur)
+            used.append(es)
+            self.engines[e].match_device_async(eb, eo.data_ptr(), ne, ro.data_ptr(), ri.data_ptr(),
+                                               ri.numel(), summ[8 * e:].data_ptr(), mode=self.mode,
+                                               stream=es.cuda_stream)
             outs.append([ro, ri])
-        cur.wait_stream(self._stream_b)
+        for es in used:
+            if es is not cur:
+                cur.wait_stream(es)
         # 3. answers, one chunk per source; a call that did not complete is redone before the
         # exchange (every rank learns every rank's flag from the size exchange)
         redo = False
         while True:
-            ans = self._buf("answer", 4 * G + NA + NB + outs[0][1].numel() + outs[1][1].numel(), torch.int32)
+            ans = self._buf("answer", 8 * G + sum(NQ) + sum(o[1].numel() for o in outs), torch.int32)
             ans_meta = torch.empty(2 * G, dtype=torch.int64, device=dev)
-            sp = [None if redo else P(summ[8 * e:]) for e in (0, 1)]
-            _lib.check(L.emqx_shard_step_answer(st, P(outs[0][0]), P(outs[0][1]), sp[0], P(outs[1][0]),
-                                                P(outs[1][1]), sp[1], P(ans), P(ans_meta), S), "emqx_shard_step_answer")
-            ans_in = torch.empty_like(ans_meta)
-            _a2a(ans_in, ans_meta, [2] * G, [2] * G, grp)
-            h = torch.cat([ans_meta, ans_in, summ[:16]]).cpu().numpy()  # host sync 2
-            am, ai, sm = h[: 2 * G].reshape(G, 2), np.ascontiguousarray(h[2 * G: 4 * G]), h[4 * G:].reshape(2, 8)
+            sp = None if redo else PA([summ[8 * e:] if NQ[e] else None for e in range(E)])
+            _lib.check(L.emqx_shard_step_answer(st, PA([o[0] for o in outs]), PA([o[1] for o in outs]), sp,
+                                                P(ans), P(ans_meta), S), "emqx_shard_step_answer")
+            if G == 1:
+                ans_in = ans_meta
+            else:
+                ans_in = torch.empty_like(ans_meta)
+                _a2a(ans_in, ans_meta, [2] * G, [2] * G, grp)
+            h = torch.cat([ans_meta, ans_in, summ[: 8 * E]]).cpu().numpy()  # host sync 2
+            am, ai, sm = h[: 2 * G].reshape(G, 2), np.ascontiguousarray(h[2 * G: 4 * G]), h[4 * G:].reshape(E, 8)
             if not redo:
-                for e in (0, 1):  # learn the id capacities from this call's totals
-                    if sm[e, 0] == 0:
+                for e in range(E):  # learn the id capacities from this call's totals
+                    if NQ[e] and sm[e, 0] == 0:
                         self._caps[e] = max(self._caps[e], int(sm[e, 1] * 1.25) + 4096)
             if not ai.reshape(G, 2)[:, 1].any():
                 break
             if am[0, 1]:  # this rank's call did not complete: redo it synchronously, exact size
                 for e, (eb, eo, ne) in enumerate(batches):
                     if ne and sm[e, 0]:
-                        outs[e] = list(self._engine_csr(e, eb, eo[: ne + 1]))
+                        outs[e] = list(self._engine_csr(e, eb, eo[: ne + 1], n=ne))
                         self._caps[e] = max(self._caps[e], int(outs[e][1].numel() * 1.25) + 4096)
             redo = True
         # 4. answers back to their sources, merged per topic in batch order
         out_w, in_w = am[:, 0].tolist(), ai.reshape(G, 2)[:, 0].tolist()
-        back = self._buf("back", sum(in_w) + 16, torch.int32)
-        _a2a(back[: sum(in_w)], ans[: sum(out_w)], in_w, out_w, grp)
-        total = int(sum(in_w) - 4 * G - mo[:, 1].sum() - mo[:, 2].sum())
+        back = _exchange_chunks(ans, out_w, in_w, lambda k: self._buf("back", k + 16, torch.int32), grp, self.rank)
+        total = int(sum(in_w) - 8 * G - mo[:, 1: 1 + E].sum())
         out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         out_ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
-        _lib.check(L.emqx_shard_step_merge(st, P(back), ai.ctypes.data, P(out_off), P(out_ids), S),
-                   "emqx_shard_step_merge")
+        _lib.check(L.emqx_shard_step_merge(st, (ctypes.c_void_p * G)(*back), ai.ctypes.data, P(out_off), P(out_ids),
+                                           S), "emqx_shard_step_merge")
         return out_off, out_ids[:total]
 
     def _match_all_tensors(self, topics: Tuple[torch.Tensor, torch.Tensor]):
         """match_all with torch tensor ops (an injected match_fn: the distribution logic on CPU
         over gloo in the tests)."""
         dev, G, grp = self.device, self.world, self.group
+        E = SHARD_ENGINES
         i64 = dict(dtype=torch.int64, device=dev)
         tb, to = topics
         tb, to = tb.to(dev), to.to(dev).to(torch.int64)
         n = to.numel() - 1
-        # 1. requests: (topic, rank * 2 + engine), sorted by destination bucket (stable)
-        req = topic_requests(tb, to, G, self.plan, self.plan_dev).reshape(-1)
-        bucket = torch.where(req < 0, torch.full_like(req, 2 * G), req)
+        # 1. requests: (topic, rank * 3 + slot), sorted by destination bucket (stable)
+        raw = topic_requests(tb, to, G, self.plan, self.plan_dev)
+        bucket = fold_requests(raw, G).reshape(-1)
         order = torch.sort(bucket, stable=True)[1]
-        counts = torch.bincount(bucket, minlength=2 * G + 1)[: 2 * G]  # per (rank, engine)
+        counts = torch.bincount(bucket, minlength=E * G + 1)[: E * G]  # per (rank, slot)
         req_topic = torch.div(order, 2, rounding_mode="floor")
         lens = (to[1:] - to[:-1]).to(torch.int64)
-        rank_of = torch.arange(2 * G, device=dev) // 2
-        valid_lens = lens[req_topic] * (bucket[order] < 2 * G).to(torch.int64)
-        bytes_per_bucket = torch.zeros(2 * G + 1, **i64).index_add_(0, bucket[order], valid_lens)[: 2 * G]
+        rank_of = torch.arange(E * G, device=dev) // E
+        valid_lens = lens[req_topic] * (bucket[order] < E * G).to(torch.int64)
+        bytes_per_bucket = torch.zeros(E * G + 1, **i64).index_add_(0, bucket[order], valid_lens)[: E * G]
         bytes_to = torch.zeros(G, **i64).index_add_(0, rank_of, bytes_per_bucket)
-        # 2. sizes: one all-to-all of (A requests, B requests, bytes) per destination
-        send_meta = torch.stack([counts[0::2], counts[1::2], bytes_to], 1).reshape(-1)
-        recv_meta = torch.empty(3 * G, **i64)
-        _a2a(recv_meta, send_meta, [3] * G, [3] * G, grp)
+        # 2. sizes: one all-to-all of (slot-0, slot-1, slot-2 requests, bytes) per destination
+        send_meta = torch.cat([counts.reshape(G, E), bytes_to[:, None]], 1).reshape(-1)
+        recv_meta = torch.empty((E + 1) * G, **i64)
+        _a2a(recv_meta, send_meta, [E + 1] * G, [E + 1] * G, grp)
         meta = torch.stack([send_meta, recv_meta]).cpu()  # host sync 1
-        sm, rm = meta[0].reshape(G, 3), meta[1].reshape(G, 3)
-        n_out = (sm[:, 0] + sm[:, 1]).tolist()
-        b_out = sm[:, 2].tolist()
-        nA_in, nB_in = rm[:, 0].tolist(), rm[:, 1].tolist()
-        n_in = [a + b for a, b in zip(nA_in, nB_in)]
-        b_in = rm[:, 2].tolist()
+        sm, rm = meta[0].reshape(G, E + 1), meta[1].reshape(G, E + 1)
+        n_out = sm[:, :E].sum(1).tolist()
+        b_out = sm[:, E].tolist()
+        nq_in = rm[:, :E].tolist()  # [source][slot]
+        n_in = [sum(x) for x in nq_in]
+        b_in = rm[:, E].tolist()
         n_req = sum(n_out)
         req_topic = req_topic[:n_req]
-        req_engine = (bucket[order][:n_req] % 2)
+        req_second = (bucket[order][:n_req] % E) == 1  # a B request follows its topic's A request
         # 3. the requests' topics, grouped by destination, to their owners
         bytes_p, offs_p = _gather_topics(tb, to, req_topic)
         lens_p = offs_p[1:] - offs_p[:-1]
@@ -576,13 +653,17 @@ class ShardedMatcher:
         my_offs = torch.zeros(sum(n_in) + 1, **i64)
         if sum(n_in):
             my_offs[1:] = torch.cumsum(my_lens, 0)
-        # 4. received: [src 0: A..., B...][src 1: A..., B...]...; match the A part and the B part
+        # 4. received: [src 0: slot 0..., 1..., 2...][src 1: ...]...; each slot's part on its engine
         starts = np.concatenate([[0], np.cumsum(n_in)[:-1]]).astype(np.int64)
-        idx = [torch.cat([torch.arange(int(starts[s] + (nA_in[s] if e else 0)),
-                                       int(starts[s] + nA_in[s] + (nB_in[s] if e else 0)), **i64)
-                          for s in range(G)]) for e in (0, 1)]
+        idx = []
+        for e in range(E):
+            parts = []
+            for s_ in range(G):
+                lo = int(starts[s_] + sum(nq_in[s_][:e]))
+                parts.append(torch.arange(lo, lo + int(nq_in[s_][e]), **i64))
+            idx.append(torch.cat(parts))
         cnts, idss = [], []
-        for e in (0, 1):
+        for e in range(E):
             if idx[e].numel():
                 eb, eo = _gather_topics(my_bytes, my_offs, idx[e])
                 c, i_ = self.match_fn(e, eb, eo)
@@ -605,8 +686,8 @@ class ShardedMatcher:
         _a2a(cnt_back, r_cnt, n_out, n_in, grp)
         ids_back = torch.empty(sum(ids_in), dtype=torch.int32, device=dev)
         _a2a(ids_back, r_ids, ids_in, ids_out, grp)
-        # 6. merge per topic in batch order: a topic's engine-A answer, then its engine-B answer
-        return merge_requests(cnt_back, ids_back, req_topic, req_engine, n, sum(ids_in))
+        # 6. merge per topic in batch order: a topic's first request's answer, then its second's
+        return merge_requests(cnt_back, ids_back, req_topic, req_second.to(torch.int64), n, sum(ids_in))
 
     def match(self, topics: Optional[Tuple[torch.Tensor, torch.Tensor]], src: int = 0, dst: int = 0):
         """Match a batch held by rank ``src``; rank ``dst`` gets the CSR in batch order
@@ -634,8 +715,9 @@ class ShardedMatcher:
 def merge_requests(cnt: torch.Tensor, ids: torch.Tensor, req_topic: torch.Tensor, req_engine: torch.Tensor, n: int,
                    total: int):
     """Per-request answers (counts in request order, ids request after request) -> the CSR of
-    n topics in batch order, each topic's engine-A ids before its engine-B ids.  `total` = the
-    id count (known on the host from the exchange), so no further synchronisation."""
+    n topics in batch order, each topic's first request's ids (req_engine 0: engine A or AB)
+    before its second's (req_engine 1: engine B).  `total` = the id count (known on the host
+    from the exchange), so no further synchronisation."""
     dev = cnt.device
     cnt = cnt.to(torch.int64)
     per_topic = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, req_topic, cnt)

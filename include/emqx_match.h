@@ -503,28 +503,41 @@ int emqx_csr_unpermute_device(const uint32_t* d_counts, const uint32_t* d_ids, u
  * RCCL): each call enqueues on `stream` and returns, nothing waits for the device, and the
  * step's scratch (learnt, grown with the batch) stays on the step.  One step at a time per
  * object; world <= EMQX_SHARD_MAX_WORLD; a batch holds fewer than 2^31 topics.
- *   send    routes each topic (emqx_shard_route rules), sorts its requests by destination
+ * A rank matches on EMQX_SHARD_ENGINES engine slots: 0 = A (its space-L and root-wildcard
+ * filters), 1 = B (its space-P filters), 2 = AB (both in one table).  A topic whose two
+ * emqx_shard_route requests name the same rank, or that makes only one, asks slot 2 of that
+ * rank once; otherwise slot 0 of its A rank and slot 1 of its B rank (at world 1 every request
+ * is a slot-2 request).
+ *   send    routes each topic, folds its requests onto the slots, sorts them by destination
  *           (stable) and packs one chunk per destination rank into d_send (send_cap >=
  *           emqx_shard_send_cap(n, batch bytes, world) bytes), chunk r first at the sum of the
  *           sizes before it:
- *             [u32 nA, nB, bytesA, bytesB][u32 offsets of the nA A-requests, + 1][B, + 1] pad 16
- *             [A topic bytes][B topic bytes] pad 16
- *           d_meta[5 * world] (i64, device): per destination the chunk bytes (-1: over send_cap),
- *           nA, nB, bytesA, bytesB — what the destination passes to recv.
- *   recv    meta_in[5 * world] (host) = the meta the sources sent this rank, d_recv their
- *           chunks in source order -> the engine-A batch (every source's A requests in source
- *           order: sum nA topics, sum bytesA bytes, offsets from 0) and the engine-B batch.
- *   answer  the two engines' CSRs over those batches (and their emqx_match_batch_device_async
- *           summaries, or NULL) -> one answer chunk per source in d_answer (u32 words, chunk s
- *           first at the sum of the sizes before it; room for 4 * world + NA + NB + ids):
- *             [nA, nB, idsA, idsB][counts of the A requests][counts of B][A ids][B ids]
+ *             [u32 n0, n1, n2, 0, bytes0, bytes1, bytes2, 0][offsets of the n0 slot-0 requests,
+ *             + 1][slot 1, + 1][slot 2, + 1] pad 16 [slot-0 topic bytes][slot 1][slot 2] pad 16
+ *           d_meta[7 * world] (i64, device): per destination the chunk bytes (-1: over send_cap),
+ *           n0, n1, n2, bytes0, bytes1, bytes2 — what the destination passes to recv.
+ *   recv    meta_in[7 * world] (host) = the meta the sources sent this rank, d_chunks[world]
+ *           (host array of device pointers) their chunks — the rank's own chunk where send
+ *           packed it, so it never needs to cross a link -> one batch per slot (every source's
+ *           slot-e requests in source order, offsets from 0): d_bytes[3], d_offsets[3] (host
+ *           arrays of device pointers; a slot no source asks may have a NULL byte buffer).  A
+ *           slot whose requests all come from one source is not copied: d_bytes[e] is replaced
+ *           by the address of that source's byte region (match the slot batch there).
+ *   answer  the three engines' CSRs over those batches (d_offsets[3], d_ids[3]; d_summaries[3]
+ *           their emqx_match_batch_device_async summaries, entries or the array NULL) -> one
+ *           answer chunk per source in d_answer (u32 words, chunk s first at the sum of the sizes
+ *           before it; room for 8 * world + requests + ids):
+ *             [n0, n1, n2, ids0, ids1, ids2, 0, 0][per request of slot 0, 1, 2: the end of its
+ *             ids in the chunk's id region (u32, inclusive prefix)][ids 0][ids 1][ids 2]
  *           d_ans_meta[2 * world] (i64, device): per source the chunk's words and a flag, 1 when
  *           an engine call did not complete (its summary flags): then no ids were copied and the
  *           caller redoes that match and the answer before the exchange.
- *   merge   ans_meta_in[2 * world] (host) = what the destinations sent, d_back their chunks ->
+ *   merge   ans_meta_in[2 * world] (host) = what the destinations sent, d_chunks[world] their
+ *           answer chunks (host array of device pointers; this rank's own in place) ->
  *           the CSR of the batch given to send, in batch order (d_out_offsets[n + 1], d_out_ids:
- *           each topic's engine-A ids, then its engine-B ids). */
+ *           each topic's engine-A ids, then its engine-B ids; one slot-2 answer otherwise). */
 #define EMQX_SHARD_MAX_WORLD 64
+#define EMQX_SHARD_ENGINES 3
 typedef struct emqx_shard_step emqx_shard_step;
 int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* splits, uint32_t n_splits,
                            emqx_shard_step** out);
@@ -532,12 +545,12 @@ int emqx_shard_step_destroy(emqx_shard_step* st);
 uint64_t emqx_shard_send_cap(uint64_t n, uint64_t batch_bytes, uint32_t world);
 int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
                          uint8_t* d_send, uint64_t send_cap, int64_t* d_meta, void* stream);
-int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* d_recv, const int64_t* meta_in, uint8_t* d_a_bytes,
-                         uint64_t* d_a_offsets, uint8_t* d_b_bytes, uint64_t* d_b_offsets, void* stream);
-int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* d_a_offsets, const uint32_t* d_a_ids,
-                           const uint64_t* d_a_summary, const uint64_t* d_b_offsets, const uint32_t* d_b_ids,
-                           const uint64_t* d_b_summary, uint32_t* d_answer, int64_t* d_ans_meta, void* stream);
-int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* d_back, const int64_t* ans_meta_in,
+int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, const int64_t* meta_in,
+                         uint8_t** d_bytes, uint64_t* const* d_offsets, void* stream);
+int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* const* d_offsets, const uint32_t* const* d_ids,
+                           const uint64_t* const* d_summaries, uint32_t* d_answer, int64_t* d_ans_meta,
+                           void* stream);
+int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, const int64_t* ans_meta_in,
                           uint64_t* d_out_offsets, uint32_t* d_out_ids, void* stream);
 
 /* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */

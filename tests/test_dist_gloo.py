@@ -199,13 +199,27 @@ def test_shard_layout_covers_every_match():
         assert np.all(((r // 2 - first[ids].astype(np.int64)) % world) < span[ids])
         held = np.zeros(len(first), np.int64)
         for k in range(world):
-            for e, (_, g) in enumerate(D.shard_engines(filters, k, world, plan)):
+            ga, gb, gab = D.shard_local_ids(filters, k, world, plan)
+            for e, g in enumerate((ga, gb)):
                 held[g] += 1
                 assert np.all(eng[g] == e)
+            assert np.array_equal(gab, np.union1d(ga, gb))  # the AB engine: A and B in one table
         assert np.array_equal(held, span.astype(np.int64))
         for t, rq in zip(names, req):
             if t.startswith(b"$") or b"/" not in t:
                 assert rq[1] == -1, t
+        # the folded keys (rank * 3 + slot): two requests to two ranks stay A and B; to one rank,
+        # or a single request, one AB request in the first column; at world 1 only AB
+        key = D.fold_requests(torch.from_numpy(req), world).numpy()
+        a, b = req[:, 0] >= 0, req[:, 1] >= 0
+        split = a & b & (req[:, 0] // 2 != req[:, 1] // 2)
+        assert np.array_equal(key[split, 0], 3 * (req[split, 0] // 2))
+        assert np.array_equal(key[split, 1], 3 * (req[split, 1] // 2) + 1)
+        one = ~split & (a | b)
+        assert np.all(key[one, 0] % 3 == 2) and np.all(key[one, 1] == 3 * world)
+        assert np.array_equal(key[one, 0] // 3, np.where(a[one], req[one, 0], req[one, 1]) // 2)
+        if world == 1:
+            assert np.all(key[:, 0] == 2) and not split.any()
 
 
 def W_unpack(packed):

@@ -3,9 +3,9 @@ ID-for-ID on the first 12K topics of the C1 bench batch, in the default GPU suit
 
 1. the whole table on one GPU (the replicated layout: one engine, ids = row numbers);
 2. the same table through the filter-sharded device step (emqx_shard_step_*) at world 1 over
-   RCCL.  The table is generated and built ONCE: at world 1 engine A holds every filter but the
-   P-space ones (`+/x/...`, dist.py), so leg 1's engine becomes engine A by deleting those (flag
-   flips of an incremental commit) and only engine B (the P-space filters) is built anew.
+   RCCL: route, fold, pack, the exchanges, answer and merge on the 100M table.  The table is
+   generated and built ONCE: at world 1 every request is an engine-slot AB request (dist.py
+   fold_requests) and the AB engine holds every filter, so leg 1's engine is adopted as it.
 
 Expected ids: tests/golden/c100m_slice.npz — the oracle (oracle/trie_oracle.cpp, the emqx_trie DFS
 + match_routes/1 union, apps/emqx/src/emqx_trie.erl:315-334) restated on the filters that can
@@ -120,8 +120,6 @@ def test_config_c_100m_sharded_step_id_for_id(c100m):
     import torch
     import torch.distributed as dist
     from emqx_amd import dist as D
-    from emqx_amd.engine import Engine
-    from emqx_amd.workloads import take
     st = c100m
     e = st.pop("engine", None)
     if e is None:
@@ -131,28 +129,20 @@ def test_config_c_100m_sharded_step_id_for_id(c100m):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = "29571"
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    eb = None
     try:
-        with _Beat("engines A and B"):
-            plan = D.shard_plan(wl.filters, 1)
-            ids_a, ids_b = D.shard_local_ids(wl.filters, 0, 1, plan)
-            assert len(ids_a) + len(ids_b) == wl.n_filters and len(ids_b) > 0
-            e.delete(ids_b)  # leg 1's table minus the P-space filters = engine A at world 1
-            e.commit()
-            eb = Engine(0)
-            eb.insert_packed_ext(*take(wl.filters, ids_b), ids_b)
-            eb.commit()
-        sm = D.ShardedMatcher(wl.filters, device=dev, engines=[e, eb])
+        plan = D.shard_plan(wl.filters, 1)
+        ids_a, ids_b, ids_ab = D.shard_local_ids(wl.filters, 0, 1, plan)
+        assert len(ids_a) + len(ids_b) == len(ids_ab) == wl.n_filters and len(ids_b) > 0
+        sm = D.ShardedMatcher(wl.filters, device=dev, engines=[None, None, e])
         off, ids = sm.match_all((tb, to))
+        assert sm.last_local_topics == k  # one (AB) request per topic
         assert int(off[-1]) == int(g["off"][-1])
         bad = C.csr_mismatches(off.cpu().numpy().astype(np.uint64), ids.cpu().numpy().view(np.uint32),
                                g["off"], g["ids"])
         assert bad.size == 0, bad[:10]
-        _Beat._line(f"sharded step ok: engine A {len(ids_a)} filters, engine B {len(ids_b)}, "
+        _Beat._line(f"sharded step ok: A {len(ids_a)} + B {len(ids_b)} filters on the AB engine, "
                     f"{k} topics, {int(off[-1])} ids ID-for-ID")
         sm._step.close()
     finally:
         dist.destroy_process_group()
         e.close()
-        if eb is not None:
-            eb.close()

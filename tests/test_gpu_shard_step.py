@@ -5,7 +5,7 @@ driven by emqx_amd/dist.py ShardedMatcher.match_all), ID-for-ID against the orac
 * edge batches at world 1 over RCCL: an empty batch, one-level topics (no engine-B request),
   '$' topics (no '+/x' match, emqx_topic.erl:71-74), wildcard topic names (one request, to
   their byte-identical filter), topics whose only matches are root wildcards;
-* the redo path: id capacities far too small, so both engine calls overflow and are redone
+* the redo path: id capacities far too small, so the engine call overflows and is redone
   before the answer exchange;
 * two ranks sharing the one GPU over gloo (a rehearsal of the N-rank exchange on real device
   kernels), each rank's own batch checked ID-for-ID.
@@ -89,8 +89,9 @@ def test_shard_step_edge_batches_world1():
 
 
 def test_shard_step_redo_on_small_capacities():
-    """Both engine calls overflow their (forced) tiny id buffers: the answer kernel flags them,
-    every rank learns it from the size exchange, the calls are redone, and the CSR is exact."""
+    """The engine call (world 1: every request on the AB slot) overflows its (forced) tiny id
+    buffer: the answer kernel flags it, every rank learns it from the size exchange, the call is
+    redone, and the CSR is exact."""
     import torch
     import torch.distributed as dist
     from emqx_amd import workloads as W
@@ -99,7 +100,7 @@ def test_shard_step_redo_on_small_capacities():
     _init(29563)
     try:
         sm = ShardedMatcher(wl.filters, device=torch.device("cuda:0"))
-        sm._caps = [1, 1]  # the floor of 64K ids is below this batch's ids on both engines
+        sm._caps = [1, 1, 1]  # the floor of 64K ids is below this batch's ids
         got = sm.match_all(_dev_topics(wl.topics))
         total = _check(got, wl.filters, wl.topics)
         assert total > 2 * 65536
@@ -137,9 +138,10 @@ def _rank_main(rank, world, port, q):
         else:  # the same topics on a smaller exchange: the same sets (in-topic order may differ)
             third_ok = C.csr_mismatches(third[0].cpu().numpy().astype(np.uint64),
                                         third[1].cpu().numpy().view(np.uint32), off_o, ids_o).size == 0
-        q.put((rank, int(bad.size), int(off_o[-1]), sm.last_local_topics, bool(third_ok), sm.n_local_filters))
+        q.put((rank, int(bad.size), int(off_o[-1]), sm.last_local_topics, bool(third_ok), sm.n_local_filters,
+               list(sm.last_slot_topics)))
     except Exception as e:  # reported to the parent
-        q.put((rank, -1, repr(e), 0, False, 0))
+        q.put((rank, -1, repr(e), 0, False, 0, [0, 0, 0]))
     finally:
         dist.destroy_process_group()
 
@@ -160,11 +162,14 @@ def test_shard_step_ranks_share_one_gpu(world):
     for p in ps:
         p.join(30)
     res.sort()
-    for rank, bad, ids, local, third_ok, nf in res:
+    for rank, bad, ids, local, third_ok, nf, slots in res:
         assert bad == 0, (rank, ids)
         assert ids > 0 and local > 0 and third_ok
-    # every rank holds part of the table (two key spaces), not all of it
+    # every rank holds part of the table (two key spaces), not all of it; some topics' two
+    # requests met on one rank (AB slot) and some did not (A and B slots) — both paths ran
     assert all(r[5] < 200_000 for r in res)
+    slots = np.sum([r[6] for r in res], axis=0)
+    assert slots[0] > 0 and slots[1] > 0 and slots[2] > 0, slots
 
 
 def test_device_routing_equals_host_routing():
