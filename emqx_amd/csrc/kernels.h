@@ -196,7 +196,8 @@ enum FastVariant {
   FAST_K2_S512W = 8, // 4 waves/block, stack 512 (+HBM spill), 512 word ids: 24 waves/CU
   FAST_K1_S768W = 9, // 4 waves/block, stack 768, 1024 word ids, K=1 (deep tables: 15 waves/CU)
   FAST_K1_S512W = 10,// 4 waves/block, stack 512 (+HBM spill), 1024 word ids, K=1: 18 waves/CU
-  FAST_NVARIANTS = 11
+  FAST_K1_S384R = 11,// FAST_K1_S384 with the root's edge array staged in LDS (an A/B of round 5)
+  FAST_NVARIANTS = 12
 };
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);

@@ -345,13 +345,16 @@ __device__ __forceinline__ void load6_masked(const EdgeSlot* edges, const uint32
 // before any result is consumed, so a step costs one dependent round trip (plus one more for
 // the ~1% of wide-node words displaced to their secondary bucket).  Perfect-hashed nodes
 // answer in one slot load; wide nodes load their word's 2-slot bucket (one 32-B pair).
-template <int K>
+// RL (FAST_K1_S384R): the root node's edge array is staged in LDS (rl, rsz slots from
+// root_base); a root item's three probes read it there and leave the global load group.
+template <int K, bool RL = false>
 __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, uint32_t plus_mask,
                                             const uint32_t (&base)[K],
                                             const uint32_t (&hparams)[K], const bool (&isph)[K],
                                             const bool (&cpy)[K], const bool (&needL)[K], const uint32_t (&wid)[K],
                                             const bool (&needP)[K], Slot (&lit)[K], bool (&fL)[K],
-                                            Slot (&pls)[K], bool (&fP)[K], uint32_t& extra) {
+                                            Slot (&pls)[K], bool (&fP)[K], uint32_t& extra,
+                                            const uint4* rl = nullptr, uint32_t rsz = 0, uint32_t root_base = 0) {
   Slot alt[K];
   bool wide[K], again[K];
   uint32_t sdk[K], msk[K], atp[K], atl[K];
@@ -369,7 +372,16 @@ __device__ __forceinline__ void probe_items(const EdgeSlot* __restrict__ edges, 
     atp[k] = base[k] + (needL[k] ? plus_copy(i1, cpy[k]) : 0u);
     atl[k] = base[k] + i1;
   }
-  if constexpr (K == 1) {
+  if constexpr (K == 1 && RL) {
+    const bool r = rsz != 0 && base[0] == root_base;
+    load3_masked(edges, atp[0], atl[0], atl[0] + 1, needP[0] && !r, needL[0] && !r, wide[0] && !r, pls[0], lit[0],
+                 alt[0]);
+    if (r) {  // (slots of the root's own array: inside [root_base, root_base + rsz))
+      if (needP[0]) pls[0].a = rl[atp[0] - root_base];
+      if (needL[0]) lit[0].a = rl[atl[0] - root_base];
+      if (wide[0]) alt[0].a = rl[atl[0] + 1 - root_base];
+    }
+  } else if constexpr (K == 1) {
     load3_masked(edges, atp[0], atl[0], atl[0] + 1, needP[0], needL[0], wide[0], pls[0], lit[0], alt[0]);
   } else if constexpr (K == 2) {
     load6_masked(edges, atp, atl, needP, needL, wide, pls, lit, alt);
@@ -556,9 +568,9 @@ struct FastLds {
 // One wave walks one tile: topics [tile * tt, tile * tt + tt) of the batch (tt <= 64; the batched
 // kernel's tiles are TILE_TOPICS wide, the small-batch kernel's narrower, so that a batch of a
 // few dozen topics spreads over many waves).  Wave-uniform returns only; no block barrier.
-template <int STACK_CAP, int WID_CAP, int K, bool DIAG>
+template <int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false>
 __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP, WID_CAP>& L, uint64_t tile,
-                                          uint32_t tt) {
+                                          uint32_t tt, const uint4* rl = nullptr, uint32_t rsz = 0) {
   static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
   static_assert(WID_CAP <= 1024, "item word index is 10 bits");
   const uint32_t lane = lane_id();
@@ -877,7 +889,8 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
     for (int k = 0; k < K; ++k)
       cpy[k] = plus_copies(tv.plus_mask, (it[k].y & IT_PLUS) || (droot[k] && (tv.root_meta & META_HAS_PLUS)),
                            isph[k] ? (hpar[k] & 15u) : (hpar[k] & 31u));
-    probe_items<K>(tv.edges, tv.plus_mask, ibase, hpar, isph, cpy, needL, wid, needP, lit, fL, pls, fP, dg[4]);
+    probe_items<K, RL>(tv.edges, tv.plus_mask, ibase, hpar, isph, cpy, needL, wid, needP, lit, fL, pls, fP, dg[4], rl,
+                       rsz, tv.root_base);
     if (DIAG) {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -989,10 +1002,23 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
   }
 }
 
-template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG>
+constexpr uint32_t ROOT_LDS_SLOTS = 256;  // FAST_K1_S384R: root arrays up to 4 KB staged in LDS
+
+template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false>
 __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(MatchArgs a) {
   __shared__ FastLds<STACK_CAP, WID_CAP> lds_all[WAVES];
+  __shared__ uint4 rl[RL ? ROOT_LDS_SLOTS : 1];
   const uint32_t wv = threadIdx.x >> 6;
+  uint32_t rsz = 0;
+  if constexpr (RL) {  // the root's edge array, once per block (every tile's first step probes it)
+    const TableView& tv = a.tv;
+    const uint32_t cl = (tv.root_meta & META_PH) ? (tv.root_meta & 15u) : (tv.root_meta & META_CAPLOG2_MASK);
+    const uint32_t n = (tv.root_meta & META_HAS_EDGES) ? (1u << cl) : 0u;
+    rsz = n <= ROOT_LDS_SLOTS ? n : 0u;
+    const uint4* src = reinterpret_cast<const uint4*>(tv.edges + tv.root_base);
+    for (uint32_t i = threadIdx.x; i < rsz; i += blockDim.x) rl[i] = src[i];
+    __syncthreads();
+  }
   // With a reordered batch (a.deal), XCD x (blocks b = x mod 8, dispatched round robin)
   // takes one contiguous range of logical blocks: neighbouring keys share its L2.
   uint64_t blk = blockIdx.x;
@@ -1000,7 +1026,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, j = blockIdx.x >> 3, q = nb >> 3, r = nb & 7u;
     blk = static_cast<uint64_t>(x) * q + min(x, r) + j;
   }
-  fast_tile<STACK_CAP, WID_CAP, K, DIAG>(a, lds_all[wv], blk * WAVES + wv, TILE_TOPICS);
+  fast_tile<STACK_CAP, WID_CAP, K, DIAG, RL>(a, lds_all[wv], blk * WAVES + wv, TILE_TOPICS, rl, rsz);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1799,13 +1825,15 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
 // ------------------------------------------------------------------------------------
 // Launch wrappers
 // ------------------------------------------------------------------------------------
-template <int W, int S, int WC, int K>
+template <int W, int S, int WC, int K, bool RL = false>
 static void launch_fast_t(const MatchArgs& a, uint64_t ntiles, hipStream_t s) {
   const uint64_t grid = (ntiles + W - 1) / W;
   if (a.diag)
-    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, true>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, true, RL>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0,
+                       s, a);
   else
-    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, false>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0, s, a);
+    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, false, RL>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0,
+                       s, a);
 }
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
@@ -1823,6 +1851,7 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K2_S512W: launch_fast_t<4, 512, 512, 2>(a, ntiles, s); break;
     case FAST_K1_S768W: launch_fast_t<4, 768, 1024, 1>(a, ntiles, s); break;
     case FAST_K1_S512W: launch_fast_t<4, 512, 1024, 1>(a, ntiles, s); break;
+    case FAST_K1_S384R: launch_fast_t<4, 384, 640, 1, true>(a, ntiles, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -1215,15 +1215,21 @@ __global__ __launch_bounds__(RW_WAVES * 64, QW_OCC) void retain_walk_queue_kerne
 
 // Queue mode, the call's last walk step: every shard's written slots (below its ticket and
 // reserved counts) and its control words back to zero for the next call.
+// grid (x, shard): the slots the call used, cleared by many blocks per shard (one block per
+// shard was bandwidth-starved: ~0.1 ms a call); the control words after, by
+// retain_queue_reset_kernel (every block here reads them first).
+constexpr uint32_t QCLEAR_BLOCKS = 32;
 __global__ __launch_bounds__(256) void retain_queue_clear_kernel(RetainArgs a) {
-  __shared__ uint32_t s_n;
-  uint32_t* c = a.qctl + static_cast<uint64_t>(blockIdx.x) * QS_STRIDE;
+  const uint32_t* c = a.qctl + static_cast<uint64_t>(blockIdx.y) * QS_STRIDE;
   const uint32_t cap = a.queue_cap / a.qshards;
-  if (threadIdx.x == 0) s_n = min(max(c[QS_HEAD], c[QS_TAIL]), cap);
-  __syncthreads();
-  uint4* q = a.queue + static_cast<uint64_t>(blockIdx.x) * cap;
-  for (uint32_t k = threadIdx.x; k < s_n; k += blockDim.x) q[k] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
+  const uint32_t n = min(max(c[QS_HEAD], c[QS_TAIL]), cap);
+  uint4* q = a.queue + static_cast<uint64_t>(blockIdx.y) * cap;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+    q[k] = make_uint4(0, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(64) void retain_queue_reset_kernel(RetainArgs a) {
+  uint32_t* c = a.qctl + static_cast<uint64_t>(blockIdx.x) * QS_STRIDE;
   if (threadIdx.x < 16) c[threadIdx.x] = 0;
 }
 
@@ -1434,7 +1440,8 @@ hipError_t launch_retain_walk_queue(const RetainArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(retain_walk_queue_kernel<RSEARCH_STREE>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
   else
     hipLaunchKernelGGL(retain_walk_queue_kernel<RSEARCH_FENCED>, dim3(blocks), dim3(RW_WAVES * 64), 0, s, a);
-  hipLaunchKernelGGL(retain_queue_clear_kernel, dim3(a.qshards), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(retain_queue_clear_kernel, dim3(QCLEAR_BLOCKS, a.qshards), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(retain_queue_reset_kernel, dim3(a.qshards), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -114,7 +115,9 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
       }
     }
   };
-  auto scan16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
+  // (the level hashes are finished with mix32 after the loop, not per '/'; once every lane of
+  // the wave is past its third level a window is scanned without hashing)
+  auto scan16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi, auto hash) {
 #pragma unroll
     for (uint32_t b = 0; b < 16; ++b) {
       const uintptr_t q = w0 + b;
@@ -122,20 +125,26 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
       const uint32_t c = q < aend ? static_cast<uint32_t>(((b < 8 ? lo : hi) >> (8u * (b & 7u))) & 0xFFu)
                                   : static_cast<uint32_t>('/');
       if (c == '/') {
-        const uint32_t v = mix32(h ^ len);
-        h0 = nl == 0 ? v : h0;
-        h1 = nl == 1 ? v : h1;
-        h2 = nl == 2 ? v : h2;
+        if (decltype(hash)::value) {
+          const uint32_t v = h ^ len;
+          h0 = nl == 0 ? v : h0;
+          h1 = nl == 1 ? v : h1;
+          h2 = nl == 2 ? v : h2;
+          h = 0x811C9DC5u;
+        }
         wild |= len == 1 && (c0 == '+' || c0 == '#');
         ++nl;
-        h = 0x811C9DC5u;
         len = 0;
       } else {
         c0 = len == 0 ? c : c0;
-        h = (h ^ c) * 0x01000193u;
+        if (decltype(hash)::value) h = (h ^ c) * 0x01000193u;
         ++len;
       }
     }
+  };
+  auto scan16w = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
+    if (__ballot(nl < 3)) scan16(w0, lo, hi, std::true_type{});
+    else scan16(w0, lo, hi, std::false_type{});
   };
   for (uintptr_t w0 = abeg & ~static_cast<uintptr_t>(15); w0 <= aend; w0 += 64) {
     uint64_t l0, g0, l1, g1, l2, g2, l3, g3;
@@ -143,16 +152,16 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
     window(w0 + 16, l1, g1);
     window(w0 + 32, l2, g2);
     window(w0 + 48, l3, g3);
-    scan16(w0, l0, g0);
-    if (w0 + 16 <= aend) scan16(w0 + 16, l1, g1);
-    if (w0 + 32 <= aend) scan16(w0 + 32, l2, g2);
-    if (w0 + 48 <= aend) scan16(w0 + 48, l3, g3);
+    scan16w(w0, l0, g0);
+    if (w0 + 16 <= aend) scan16w(w0 + 16, l1, g1);
+    if (w0 + 32 <= aend) scan16w(w0 + 32, l2, g2);
+    if (w0 + 48 <= aend) scan16w(w0 + 48, l3, g3);
   }
   L->n_levels = nl;
   L->wild = wild;
-  L->h[0] = h0;
-  L->h[1] = h1;
-  L->h[2] = h2;
+  L->h[0] = nl > 0 ? mix32(h0) : 0u;
+  L->h[1] = nl > 1 ? mix32(h1) : 0u;
+  L->h[2] = nl > 2 ? mix32(h2) : 0u;
 }
 
 // The split plan in LDS when it fits (routing binary-searches it twice per topic: from global
@@ -180,7 +189,7 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 // distinct key in the wave (most of a wave's requests share a bucket: same-address atomics from
 // every lane would serialise).  Lanes past the batch pass k = kNone.
 __device__ __forceinline__ void wave_count(uint32_t k, uint32_t len, uint32_t nb, uint32_t* c_cnt,
-                                           unsigned long long* c_by) {
+                                           uint32_t* c_by) {
   const uint32_t lane = lane_id();
   uint64_t left = __ballot(k != kNone);
   while (left) {
@@ -191,7 +200,7 @@ __device__ __forceinline__ void wave_count(uint32_t k, uint32_t len, uint32_t nb
     for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     if (lane == first) {
       atomicAdd(&c_cnt[kk], static_cast<uint32_t>(__popcll(mask)));
-      if (v) atomicAdd(&c_by[kk], static_cast<unsigned long long>(v));
+      if (v) atomicAdd(&c_by[kk], v);
     }
     left &= ~mask;
   }
@@ -201,10 +210,10 @@ __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ to, uint64_t n, uint32_t world,
                                                         const ShardSplitE* __restrict__ gsp, uint32_t nsp,
                                                         uint32_t* __restrict__ key, uint32_t ntiles,
-                                                        uint32_t* __restrict__ tcnt, uint64_t* __restrict__ tbytes) {
+                                                        uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tbytes) {
   __shared__ ShardSplitE lsp[kLdsSplits];
   __shared__ uint32_t c_cnt[kMaxBuckets];
-  __shared__ unsigned long long c_by[kMaxBuckets];
+  __shared__ uint32_t c_by[kMaxBuckets];  // (a tile's bytes: 512 requests of <= 64 KB topics)
   const uint32_t nb = kE * world + 1;
   for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
     c_cnt[k] = 0;
@@ -238,28 +247,48 @@ __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restric
   }
 }
 
-// One block: the (bucket, tile) table -> exclusive prefixes in place (bucket-major: a bucket's
-// tiles in order, then the next bucket), start[b] for b = 0 .. nb, sc[m] = the byte total.
-__global__ __launch_bounds__(1024) void shard_sort_scan_kernel(uint32_t* __restrict__ tcnt,
-                                                               uint64_t* __restrict__ tbytes, uint32_t nb,
-                                                               uint32_t ntiles, uint64_t m,
-                                                               uint32_t* __restrict__ start, uint64_t* __restrict__ sc) {
-  __shared__ uint64_t wc[16], wb[16];
-  const uint64_t N = static_cast<uint64_t>(nb) * ntiles;
+// One block: the (bucket, tile) table -> exclusive prefixes (bucket-major: a bucket's tiles in
+// order, then the next bucket): counts in place, bytes into pbytes (u64), start[b] for b = 0 ..
+// nb, sc[m] = the byte total.  A thread takes a chunk of consecutive entries (a multiple of 4,
+// read as 16-B vectors, every load of a round issued before any is used; the tables are padded
+// past the last chunk, the padding masked off).
+constexpr uint32_t kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void shard_sort_scan_kernel(uint32_t* __restrict__ tcnt,
+                                                                       const uint32_t* __restrict__ tbytes,
+                                                                       uint64_t* __restrict__ pbytes, uint32_t nb,
+                                                                       uint32_t ntiles, uint64_t m,
+                                                                       uint32_t* __restrict__ start,
+                                                                       uint64_t* __restrict__ sc) {
+  __shared__ uint64_t wc[kScanThreads / 64], wb[kScanThreads / 64];
+  const uint32_t N = nb * ntiles;
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const uint64_t per = (N + blockDim.x - 1) / blockDim.x;
-  const uint64_t i0 = min<uint64_t>(N, tid * per), i1 = min<uint64_t>(N, i0 + per);
-  // (16 entries a round, every load of a round issued before any is used)
-  constexpr uint32_t R = 16;
-  uint64_t c = 0, by = 0;
-  for (uint64_t g = i0; g < i1; g += R) {
-    uint32_t vc[R];
-    uint64_t vb[R];
+  const uint32_t per = ((N + kScanThreads - 1) / kScanThreads + 3) & ~3u;
+  const uint32_t i0 = min(N, tid * per), i1 = min(N, i0 + per);
+  constexpr uint32_t R = 16;  // entries a round (4 vectors of each table)
+  auto load_round = [&](uint32_t g, uint32_t (&vc)[R], uint32_t (&vb)[R]) {
+    const uint4* pc = reinterpret_cast<const uint4*>(tcnt + g);
+    const uint4* pb = reinterpret_cast<const uint4*>(tbytes + g);
+    uint4 c4[R / 4], b4[R / 4];
 #pragma unroll
-    for (uint32_t j = 0; j < R; ++j) {
-      vc[j] = g + j < i1 ? tcnt[g + j] : 0u;
-      vb[j] = g + j < i1 ? tbytes[g + j] : 0ull;
+    for (uint32_t q = 0; q < R / 4; ++q) {
+      c4[q] = pc[q];
+      b4[q] = pb[q];
     }
+#pragma unroll
+    for (uint32_t q = 0; q < R / 4; ++q) {
+      const uint32_t cc[4] = {c4[q].x, c4[q].y, c4[q].z, c4[q].w}, bb[4] = {b4[q].x, b4[q].y, b4[q].z, b4[q].w};
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        const bool in = g + 4 * q + k < i1;
+        vc[4 * q + k] = in ? cc[k] : 0u;
+        vb[4 * q + k] = in ? bb[k] : 0u;
+      }
+    }
+  };
+  uint64_t c = 0, by = 0;
+  for (uint32_t g = i0; g < i1; g += R) {
+    uint32_t vc[R], vb[R];
+    load_round(g, vc, vb);
 #pragma unroll
     for (uint32_t j = 0; j < R; ++j) {
       c += vc[j];
@@ -285,26 +314,25 @@ __global__ __launch_bounds__(1024) void shard_sort_scan_kernel(uint32_t* __restr
     bb += wb[k];
   }
   uint64_t xc = bc + ic - c, xb = bb + ib - by;  // exclusive prefix of this thread's chunk
-  for (uint64_t g = i0; g < i1; g += R) {
-    uint32_t vc[R];
-    uint64_t vb[R];
+  uint32_t nxt = (i0 + ntiles - 1) / ntiles * ntiles;  // the first bucket start at or after i0
+  for (uint32_t g = i0; g < i1; g += R) {
+    uint32_t vc[R], vb[R];
+    load_round(g, vc, vb);
 #pragma unroll
     for (uint32_t j = 0; j < R; ++j) {
-      vc[j] = g + j < i1 ? tcnt[g + j] : 0u;
-      vb[j] = g + j < i1 ? tbytes[g + j] : 0ull;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < R; ++j) {
-      const uint64_t i = g + j;
+      const uint32_t i = g + j;
       if (i >= i1) break;
-      if (i % ntiles == 0) start[i / ntiles] = static_cast<uint32_t>(xc);
+      if (i == nxt) {  // a bucket's first tile
+        start[nxt / ntiles] = static_cast<uint32_t>(xc);
+        nxt += ntiles;
+      }
       tcnt[i] = static_cast<uint32_t>(xc);
-      tbytes[i] = xb;
+      pbytes[i] = xb;
       xc += vc[j];
       xb += vb[j];
     }
   }
-  if (tid == blockDim.x - 1) {
+  if (tid == kScanThreads - 1) {
     start[nb] = static_cast<uint32_t>(m);
     sc[m] = xb;  // (the no-request bucket is last and holds no bytes)
   }
@@ -315,7 +343,7 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
                                                                  const uint64_t* __restrict__ to, uint64_t m,
                                                                  uint32_t nb, uint32_t ntiles,
                                                                  const uint32_t* __restrict__ tcnt,
-                                                                 const uint64_t* __restrict__ tbytes,
+                                                                 const uint64_t* __restrict__ tbytes,  // (prefixes)
                                                                  uint32_t* __restrict__ key_s, uint32_t* __restrict__ perm,
                                                                  uint32_t* __restrict__ len, uint64_t* __restrict__ sc) {
   __shared__ uint32_t run_c[kMaxBuckets];
@@ -691,8 +719,8 @@ struct emqx_shard_step {
   // request scratch, sized for m_cap requests
   uint64_t m_cap = 0;
   uint32_t *key = nullptr, *key_s = nullptr, *perm = nullptr, *len = nullptr, *pos = nullptr, *tcnt = nullptr,
-           *beg = nullptr, *tcnt_tab = nullptr;
-  uint64_t *sc = nullptr, *partials = nullptr, *tbytes_tab = nullptr;  // (tab: the sort's (bucket, tile) table)
+           *beg = nullptr, *tcnt_tab = nullptr, *tbytes_tab = nullptr;  // (tab: the sort's (bucket, tile) table)
+  uint64_t *sc = nullptr, *partials = nullptr, *pbytes_tab = nullptr;
   uint32_t* start = nullptr;  // [kE G + 2]
   uint64_t* cbase = nullptr;  // [G]
   uint32_t* err = nullptr;
@@ -708,10 +736,10 @@ void free_scratch(emqx_shard_step* st) {
   for (void* p : {static_cast<void*>(st->key), static_cast<void*>(st->tcnt_tab), static_cast<void*>(st->key_s),
                   static_cast<void*>(st->perm), static_cast<void*>(st->len), static_cast<void*>(st->pos),
                   static_cast<void*>(st->tcnt), static_cast<void*>(st->sc), static_cast<void*>(st->partials),
-                  static_cast<void*>(st->beg), static_cast<void*>(st->tbytes_tab)})
+                  static_cast<void*>(st->beg), static_cast<void*>(st->tbytes_tab), static_cast<void*>(st->pbytes_tab)})
     if (p) (void)hipFree(p);
-  st->key = st->tcnt_tab = st->key_s = st->perm = st->len = st->pos = st->tcnt = st->beg = nullptr;
-  st->sc = st->partials = st->tbytes_tab = nullptr;
+  st->key = st->tcnt_tab = st->key_s = st->perm = st->len = st->pos = st->tcnt = st->beg = st->tbytes_tab = nullptr;
+  st->sc = st->partials = st->pbytes_tab = nullptr;
   st->m_cap = 0;
 }
 
@@ -726,9 +754,11 @@ hipError_t ensure_scratch(emqx_shard_step* st, uint64_t m) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(p), std::max<uint64_t>(bytes, 16));
   };
   al(&st->key, 4 * cap);
-  const uint64_t tab = (kE * st->world + 1ull) * ((cap + kSortTile - 1) / kSortTile + 1);
+  // (+ one scan round of padding: shard_sort_scan_kernel reads whole 16-entry rounds)
+  const uint64_t tab = (kE * st->world + 1ull) * ((cap + kSortTile - 1) / kSortTile + 1) + 16;
   al(&st->tcnt_tab, 4 * tab);
-  al(&st->tbytes_tab, 8 * tab);
+  al(&st->tbytes_tab, 4 * tab);
+  al(&st->pbytes_tab, 8 * tab);
   al(&st->key_s, 4 * cap);
   al(&st->perm, 4 * cap);
   al(&st->len, 4 * cap);
@@ -811,10 +841,10 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
     const uint32_t ntiles = static_cast<uint32_t>((m + kSortTile - 1) / kSortTile);
     hipLaunchKernelGGL(shard_key_kernel, dim3(ntiles), dim3(256), 0, s, d_bytes, d_offsets, n, G, st->d_splits,
                        st->n_splits, st->key, ntiles, st->tcnt_tab, st->tbytes_tab);
-    hipLaunchKernelGGL(shard_sort_scan_kernel, dim3(1), dim3(1024), 0, s, st->tcnt_tab, st->tbytes_tab, nb, ntiles, m,
-                       st->start, st->sc);
+    hipLaunchKernelGGL(shard_sort_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, st->tcnt_tab, st->tbytes_tab,
+                       st->pbytes_tab, nb, ntiles, m, st->start, st->sc);
     hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_offsets, m, nb, ntiles,
-                       st->tcnt_tab, st->tbytes_tab, st->key_s, st->perm, st->len, st->sc);
+                       st->tcnt_tab, st->pbytes_tab, st->key_s, st->perm, st->len, st->sc);
   } else {
     SS_TRY(hipMemsetAsync(st->start, 0, 4ull * (kE * G + 2), s));
     SS_TRY(hipMemsetAsync(st->sc, 0, 8, s));

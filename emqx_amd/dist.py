@@ -482,6 +482,19 @@ class ShardedMatcher:
             return res
         return self._match_all_tensors(topics)
 
+    def _to_host(self, *parts: torch.Tensor) -> np.ndarray:
+        """The device tensors' values (int64) on the host: one copy into a reused pinned buffer
+        and a wait for this stream (no allocation per call)."""
+        k = sum(int(t.numel()) for t in parts)
+        hb = self._bufs.get("_host")
+        if hb is None or hb.numel() < k:
+            hb = torch.empty(max(k, 256), dtype=torch.int64, pin_memory=True)
+            self._bufs["_host"] = hb
+        dv = torch.cat([t.reshape(-1) for t in parts]) if len(parts) > 1 else parts[0].reshape(-1)
+        hb[:k].copy_(dv, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return hb[:k].numpy().copy()
+
     def _buf(self, name: str, n: int, dtype) -> torch.Tensor:
         """A reused device buffer of at least n elements (every use is ordered on one stream)."""
         b = self._bufs.get(name)
@@ -519,12 +532,12 @@ class ShardedMatcher:
         _lib.check(L.emqx_shard_step_send(st, P(tb), P(to), n, P(send), send.numel(), P(meta), S),
                    "emqx_shard_step_send")
         if G == 1:
-            mh = meta.cpu().numpy()  # host sync 1
+            mh = self._to_host(meta)  # host sync 1
             mo = mi = np.ascontiguousarray(mh.reshape(G, MW))
         else:
             meta_in = torch.empty_like(meta)
             _a2a(meta_in, meta, [MW] * G, [MW] * G, grp)
-            mh = torch.stack([meta, meta_in]).cpu().numpy()  # host sync 1
+            mh = self._to_host(meta, meta_in).reshape(2, -1)  # host sync 1
             mo, mi = mh[0].reshape(G, MW), np.ascontiguousarray(mh[1].reshape(G, MW))
         if (mo[:, 0] < 0).any() or (mi[:, 0] < 0).any():
             raise RuntimeError("emqx_shard_step_send: chunks over the send buffer")
@@ -585,7 +598,7 @@ class ShardedMatcher:
             else:
                 ans_in = torch.empty_like(ans_meta)
                 _a2a(ans_in, ans_meta, [2] * G, [2] * G, grp)
-            h = torch.cat([ans_meta, ans_in, summ[: 8 * E]]).cpu().numpy()  # host sync 2
+            h = self._to_host(ans_meta, ans_in, summ[: 8 * E])  # host sync 2
             am, ai, sm = h[: 2 * G].reshape(G, 2), np.ascontiguousarray(h[2 * G: 4 * G]), h[4 * G:].reshape(E, 8)
             if not redo:
                 for e in range(E):  # learn the id capacities from this call's totals
