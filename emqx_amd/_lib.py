@@ -256,7 +256,7 @@ def lib():
         "emqx_shard_send_cap": (u64, [u64, u64, u32]),
         "emqx_shard_step_send": (i32, [vp, vp, vp, u64, vp, u64, vp, vp]),
         "emqx_shard_step_recv": (i32, [vp, vp, vp, vp, vp, vp]),
-        "emqx_shard_step_answer": (i32, [vp, vp, vp, vp, vp, vp, vp]),
+        "emqx_shard_step_answer": (i32, [vp, vp, vp, vp, u32, vp, vp, vp]),
         "emqx_shard_step_merge": (i32, [vp, vp, vp, vp, vp, vp]),
         "emqx_batch_permute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),
         "emqx_csr_unpermute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),

@@ -573,9 +573,11 @@ struct EngineCsrs {
 };
 
 // grid (x, source): the source's answer chunk from the three CSRs.  An engine call that did not
-// complete (summary flags) leaves its ids unread: the step is redone.
-__global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardTab tab, uint32_t* __restrict__ out,
-                                                           int64_t* __restrict__ ans_meta) {
+// complete (summary flags) leaves its ids unread: the step is redone.  The chunk for this rank
+// itself (source `self`) carries no ids: the merge reads them in place from the CSRs.
+constexpr uint32_t kAnsMeta = 3;  // per source: chunk words, redo flag, ids
+__global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardTab tab, uint32_t self,
+                                                           uint32_t* __restrict__ out, int64_t* __restrict__ ans_meta) {
   const uint32_t s = blockIdx.y;
   bool bad = false;
   uint32_t q0[kE], nq[kE];
@@ -592,12 +594,19 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
     iall += ni[e];
     ibefore += bad ? 0 : i0[e];  // this source's ids start after every earlier source's
   }
+  if (!bad && self < s)  // the own chunk before this one holds no ids
+    for (uint32_t e = 0; e < kE; ++e) {
+      const uint32_t a0 = tab.q0[e][self], a1 = tab.q0[e][self + 1];
+      if (a1 > a0) ibefore -= cs.off[e][a1] - cs.off[e][a0];
+    }
   const uint64_t cb = tab.w0[s] + ibefore;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    ans_meta[2 * s] = static_cast<int64_t>(kHW + nall + iall);
-    ans_meta[2 * s + 1] = bad ? 1 : 0;
+    ans_meta[kAnsMeta * s] = static_cast<int64_t>(kHW + nall + (s == self ? 0 : iall));
+    ans_meta[kAnsMeta * s + 1] = bad ? 1 : 0;
+    ans_meta[kAnsMeta * s + 2] = static_cast<int64_t>(iall);
   }
   if (bad) return;
+  const bool copy_ids = s != self;
   uint32_t* c = out + cb;
   const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
@@ -616,7 +625,8 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
     const uint64_t* off = cs.off[e] + q0[e];
     for (uint64_t k = tid; k < nq[e]; k += stride) end[k] = static_cast<uint32_t>(before + off[k + 1] - i0[e]);
     const uint32_t* src = cs.ids[e] + i0[e];
-    for (uint64_t j = tid; j < ni[e]; j += stride) ids[j] = src[j];
+    if (copy_ids)
+      for (uint64_t j = tid; j < ni[e]; j += stride) ids[j] = src[j];
     end += nq[e];
     ids += ni[e];
     before += ni[e];
@@ -665,10 +675,20 @@ __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t*
   }
 }
 
+// This rank's own answers, read in place: per slot its engine's ids from the first id of this
+// rank's own requests (self = kNone: every answer came in a chunk).
+struct SelfIds {
+  const uint32_t* ids[kE];
+  const uint64_t* off[kE];
+  uint32_t q0[kE];
+  uint32_t self;
+};
+
 // 4 lanes per request, in request (send) order: its answer's ids, read from the answer chunk
-// where they lie in that same order (coalesced), to its topic's place in the output: the
-// topic's offset, after the ids of the topic's first request for its second.
-__global__ __launch_bounds__(256) void shard_merge_kernel(ShardTab tab,
+// where they lie in that same order (coalesced) — or, for this rank's own requests, from its
+// engines' CSRs — to its topic's place in the output: the topic's offset, after the ids of the
+// topic's first request for its second.
+__global__ __launch_bounds__(256) void shard_merge_kernel(ShardTab tab, SelfIds me,
                                                           const uint32_t* __restrict__ key_s,
                                                           const uint32_t* __restrict__ perm,
                                                           const uint32_t* __restrict__ start,
@@ -684,15 +704,23 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(ShardTab tab,
     const uint32_t c = cnt[p];
     if (c == 0) continue;
     const uint32_t q = perm[p], t = q >> 1, second = q & 1u;
-    const uint32_t r = key_s[p] / kE;
+    const uint32_t b = key_s[p], r = b / kE;
     const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
-    const uint64_t src = kHW + ch[0] + ch[1] + ch[2] + beg[p];
+    const uint32_t* from;
+    if (r == me.self) {
+      const uint32_t e = b - kE * r;
+      uint32_t before = 0;
+      for (uint32_t k = 0; k < e; ++k) before += ch[3 + k];
+      from = me.ids[e] + me.off[e][me.q0[e]] + (beg[p] - before);
+    } else {
+      from = ch + kHW + ch[0] + ch[1] + ch[2] + beg[p];
+    }
     uint64_t dst = out_off[t];
     if (second) {
       const uint32_t pa = pos[2 * t];
       if (pa != kNone) dst += cnt[pa];
     }
-    for (uint32_t j = sub; j < c; j += 4) out_ids[dst + j] = ch[src + j];
+    for (uint32_t j = sub; j < c; j += 4) out_ids[dst + j] = from[j];
   }
 }
 
@@ -727,6 +755,7 @@ struct emqx_shard_step {
   // the step in flight
   uint64_t n = 0;                       // topics of the last send
   ShardTab recv_tab{};                  // the last recv's per-source table (answer uses it)
+  SelfIds self_ids{};                   // the last answer's in-place own ids (merge uses them)
   bool have_recv = false, have_send = false;
 };
 
@@ -921,24 +950,30 @@ int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, co
 }
 
 int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* const* d_offsets, const uint32_t* const* d_ids,
-                           const uint64_t* const* d_summaries, uint32_t* d_answer, int64_t* d_ans_meta,
-                           void* stream) {
+                           const uint64_t* const* d_summaries, uint32_t self_rank, uint32_t* d_answer,
+                           int64_t* d_ans_meta, void* stream) {
   if (!st || !st->have_recv || !d_offsets || !d_ids || !d_answer || !d_ans_meta) return EMQX_EINVAL;
   const uint32_t G = st->world;
+  if (self_rank >= G && self_rank != kNone) return EMQX_EINVAL;
   const ShardTab& t = st->recv_tab;
   EngineCsrs cs{};
   uint64_t qall = 0;
+  st->self_ids = SelfIds{};
+  st->self_ids.self = self_rank;
   for (uint32_t e = 0; e < kE; ++e) {
     if (!d_offsets[e] || (t.q0[e][G] && !d_ids[e])) return EMQX_EINVAL;
     cs.off[e] = d_offsets[e];
     cs.ids[e] = d_ids[e];
     cs.sum[e] = d_summaries ? d_summaries[e] : nullptr;
     qall += t.q0[e][G];
+    st->self_ids.ids[e] = d_ids[e];
+    st->self_ids.off[e] = d_offsets[e];
+    st->self_ids.q0[e] = self_rank < G ? t.q0[e][self_rank] : 0;
   }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
   const uint32_t x = grid_of(8 * qall / G + 1, 256, std::max<uint32_t>(1, 1024 / G));  // ~8 ids a request
-  hipLaunchKernelGGL(shard_answer_kernel, dim3(x, G), dim3(256), 0, s, cs, t, d_answer, d_ans_meta);
+  hipLaunchKernelGGL(shard_answer_kernel, dim3(x, G), dim3(256), 0, s, cs, t, self_rank, d_answer, d_ans_meta);
   SS_TRY(hipGetLastError());
   return EMQX_OK;
 }
@@ -949,7 +984,7 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   const uint32_t G = st->world;
   ShardTab t{};
   for (uint32_t r = 0; r < G; ++r) {
-    if (ans_meta_in[2 * r] < kHW || ans_meta_in[2 * r + 1] != 0 || !d_chunks[r]) return EMQX_EINVAL;
+    if (ans_meta_in[kAnsMeta * r] < kHW || ans_meta_in[kAnsMeta * r + 1] != 0 || !d_chunks[r]) return EMQX_EINVAL;
     t.chunk[r] = reinterpret_cast<uint64_t>(d_chunks[r]);
   }
   const hipStream_t s = static_cast<hipStream_t>(stream);
@@ -964,7 +999,7 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   SS_TRY(launch_scan(st->tcnt, n, d_out_offsets, st->partials, s));
   if (n) {
     if (!d_out_ids) return EMQX_EINVAL;
-    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, t, st->key_s, st->perm,
+    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, t, st->self_ids, st->key_s, st->perm,
                        st->start, st->len, st->beg, st->pos, G, d_out_offsets, d_out_ids);
   }
   SS_TRY(hipGetLastError());

@@ -589,22 +589,23 @@ class ShardedMatcher:
         redo = False
         while True:
             ans = self._buf("answer", 8 * G + sum(NQ) + sum(o[1].numel() for o in outs), torch.int32)
-            ans_meta = torch.empty(2 * G, dtype=torch.int64, device=dev)
+            ans_meta = torch.empty(3 * G, dtype=torch.int64, device=dev)  # per source: words, redo, ids
             sp = None if redo else PA([summ[8 * e:] if NQ[e] else None for e in range(E)])
-            _lib.check(L.emqx_shard_step_answer(st, PA([o[0] for o in outs]), PA([o[1] for o in outs]), sp,
+            # (this rank's own answers stay in the engines' outputs: the merge reads them there)
+            _lib.check(L.emqx_shard_step_answer(st, PA([o[0] for o in outs]), PA([o[1] for o in outs]), sp, self.rank,
                                                 P(ans), P(ans_meta), S), "emqx_shard_step_answer")
             if G == 1:
                 ans_in = ans_meta
             else:
                 ans_in = torch.empty_like(ans_meta)
-                _a2a(ans_in, ans_meta, [2] * G, [2] * G, grp)
+                _a2a(ans_in, ans_meta, [3] * G, [3] * G, grp)
             h = self._to_host(ans_meta, ans_in, summ[: 8 * E])  # host sync 2
-            am, ai, sm = h[: 2 * G].reshape(G, 2), np.ascontiguousarray(h[2 * G: 4 * G]), h[4 * G:].reshape(E, 8)
+            am, ai, sm = h[: 3 * G].reshape(G, 3), np.ascontiguousarray(h[3 * G: 6 * G]), h[6 * G:].reshape(E, 8)
             if not redo:
                 for e in range(E):  # learn the id capacities from this call's totals
                     if NQ[e] and sm[e, 0] == 0:
                         self._caps[e] = max(self._caps[e], int(sm[e, 1] * 1.25) + 4096)
-            if not ai.reshape(G, 2)[:, 1].any():
+            if not ai.reshape(G, 3)[:, 1].any():
                 break
             if am[0, 1]:  # this rank's call did not complete: redo it synchronously, exact size
                 for e, (eb, eo, ne) in enumerate(batches):
@@ -613,9 +614,9 @@ class ShardedMatcher:
                         self._caps[e] = max(self._caps[e], int(outs[e][1].numel() * 1.25) + 4096)
             redo = True
         # 4. answers back to their sources, merged per topic in batch order
-        out_w, in_w = am[:, 0].tolist(), ai.reshape(G, 2)[:, 0].tolist()
+        out_w, in_w = am[:, 0].tolist(), ai.reshape(G, 3)[:, 0].tolist()
         back = _exchange_chunks(ans, out_w, in_w, lambda k: self._buf("back", k + 16, torch.int32), grp, self.rank)
-        total = int(sum(in_w) - 8 * G - mo[:, 1: 1 + E].sum())
+        total = int(ai.reshape(G, 3)[:, 2].sum())
         out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         out_ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
         _lib.check(L.emqx_shard_step_merge(st, (ctypes.c_void_p * G)(*back), ai.ctypes.data, P(out_off), P(out_ids),

@@ -529,10 +529,13 @@ int emqx_csr_unpermute_device(const uint32_t* d_counts, const uint32_t* d_ids, u
  *           before it; room for 8 * world + requests + ids):
  *             [n0, n1, n2, ids0, ids1, ids2, 0, 0][per request of slot 0, 1, 2: the end of its
  *             ids in the chunk's id region (u32, inclusive prefix)][ids 0][ids 1][ids 2]
- *           d_ans_meta[2 * world] (i64, device): per source the chunk's words and a flag, 1 when
- *           an engine call did not complete (its summary flags): then no ids were copied and the
- *           caller redoes that match and the answer before the exchange.
- *   merge   ans_meta_in[2 * world] (host) = what the destinations sent, d_chunks[world] their
+ *           except that the chunk for self_rank (this rank's own requests; UINT32_MAX: none)
+ *           carries no ids: merge reads them in place from d_ids, which must stay unchanged
+ *           until it has run.  d_ans_meta[3 * world] (i64, device): per source the chunk's
+ *           words, a flag (1 when an engine call did not complete, its summary flags: then no
+ *           ids were copied and the caller redoes that match and the answer before the
+ *           exchange), and the answer's ids.
+ *   merge   ans_meta_in[3 * world] (host) = what the destinations sent, d_chunks[world] their
  *           answer chunks (host array of device pointers; this rank's own in place) ->
  *           the CSR of the batch given to send, in batch order (d_out_offsets[n + 1], d_out_ids:
  *           each topic's engine-A ids, then its engine-B ids; one slot-2 answer otherwise). */
@@ -548,8 +551,8 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
 int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, const int64_t* meta_in,
                          uint8_t** d_bytes, uint64_t* const* d_offsets, void* stream);
 int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* const* d_offsets, const uint32_t* const* d_ids,
-                           const uint64_t* const* d_summaries, uint32_t* d_answer, int64_t* d_ans_meta,
-                           void* stream);
+                           const uint64_t* const* d_summaries, uint32_t self_rank, uint32_t* d_answer,
+                           int64_t* d_ans_meta, void* stream);
 int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, const int64_t* ans_meta_in,
                           uint64_t* d_out_offsets, uint32_t* d_out_ids, void* stream);
 
