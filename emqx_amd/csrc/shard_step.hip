@@ -60,16 +60,27 @@ static_assert(sizeof(ShardTab) <= 3584, "kernel argument");
 
 __host__ __device__ inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 
-// A topic's bytes from src to dst (any alignment: gfx950 global loads and stores take
-// unaligned addresses), `lanes` lanes of one request together (sub = this lane's index among
-// them): 16-B moves, then the tail byte by byte.
-typedef uint4 __attribute__((aligned(1))) u4u;
-__device__ __forceinline__ void copy_bytes(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t len,
-                                           uint32_t sub, uint32_t lanes) {
-  const uint64_t full = len & ~15ull;
-  for (uint64_t j = 16ull * sub; j < full; j += 16ull * lanes)
-    *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
-  for (uint64_t j = full + sub; j < len; j += lanes) dst[j] = src[j];
+typedef uint4 __attribute__((aligned(1))) u4u;  // (gfx950 global loads and stores take any alignment)
+// One thread's copy of a topic's bytes (any alignment): 16-B moves, then 8 / 4 / 2 / 1.
+__device__ __forceinline__ void copy_topic(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len) {
+  typedef uint2 __attribute__((aligned(1))) u2u;
+  typedef uint32_t __attribute__((aligned(1))) u1u;
+  typedef uint16_t __attribute__((aligned(1))) h1u;
+  uint32_t j = 0;
+  for (; j + 16 <= len; j += 16) *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
+  if (j + 8 <= len) {
+    *reinterpret_cast<u2u*>(dst + j) = *reinterpret_cast<const u2u*>(src + j);
+    j += 8;
+  }
+  if (j + 4 <= len) {
+    *reinterpret_cast<u1u*>(dst + j) = *reinterpret_cast<const u1u*>(src + j);
+    j += 4;
+  }
+  if (j + 2 <= len) {
+    *reinterpret_cast<h1u*>(dst + j) = *reinterpret_cast<const h1u*>(src + j);
+    j += 2;
+  }
+  if (j < len) dst[j] = src[j];
 }
 
 uint32_t grid_of(uint64_t items, uint32_t per_block, uint32_t cap = 8192) {
@@ -258,7 +269,7 @@ __global__ __launch_bounds__(kScanThreads) void shard_sort_scan_kernel(uint32_t*
                                                                        uint64_t* __restrict__ pbytes, uint32_t nb,
                                                                        uint32_t ntiles, uint64_t m,
                                                                        uint32_t* __restrict__ start,
-                                                                       uint64_t* __restrict__ sc) {
+                                                                       uint64_t* __restrict__ bpre) {
   __shared__ uint64_t wc[kScanThreads / 64], wb[kScanThreads / 64];
   const uint32_t N = nb * ntiles;
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
@@ -322,8 +333,9 @@ __global__ __launch_bounds__(kScanThreads) void shard_sort_scan_kernel(uint32_t*
     for (uint32_t j = 0; j < R; ++j) {
       const uint32_t i = g + j;
       if (i >= i1) break;
-      if (i == nxt) {  // a bucket's first tile
+      if (i == nxt) {  // a bucket's first tile: its first request and first byte
         start[nxt / ntiles] = static_cast<uint32_t>(xc);
+        bpre[nxt / ntiles] = xb;
         nxt += ntiles;
       }
       tcnt[i] = static_cast<uint32_t>(xc);
@@ -334,23 +346,39 @@ __global__ __launch_bounds__(kScanThreads) void shard_sort_scan_kernel(uint32_t*
   }
   if (tid == kScanThreads - 1) {
     start[nb] = static_cast<uint32_t>(m);
-    sc[m] = xb;  // (the no-request bucket is last and holds no bytes)
+    bpre[nb] = xb;  // (the no-request bucket is last and holds no bytes)
   }
 }
 
 // Stable scatter of one tile's requests to their sorted positions (see above).
+// ... and each request packed where it lands (shard_layout_kernel's bases): its offset word and
+// its topic's bytes into its destination's chunk.
 __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t* __restrict__ key,
+                                                                 const uint8_t* __restrict__ tb,
                                                                  const uint64_t* __restrict__ to, uint64_t m,
                                                                  uint32_t nb, uint32_t ntiles,
                                                                  const uint32_t* __restrict__ tcnt,
                                                                  const uint64_t* __restrict__ tbytes,  // (prefixes)
-                                                                 uint32_t* __restrict__ key_s, uint32_t* __restrict__ perm,
-                                                                 uint32_t* __restrict__ len, uint64_t* __restrict__ sc) {
+                                                                 const uint64_t* __restrict__ bpre,
+                                                                 const int64_t* __restrict__ obase,
+                                                                 const int64_t* __restrict__ dbase,
+                                                                 const uint32_t* __restrict__ err,
+                                                                 uint8_t* __restrict__ send,
+                                                                 uint32_t* __restrict__ key_s, uint32_t* __restrict__ perm) {
   __shared__ uint32_t run_c[kMaxBuckets];
   __shared__ uint64_t run_b[kMaxBuckets];
   __shared__ uint32_t w_c[4][kMaxBuckets];
   __shared__ uint64_t w_b[4][kMaxBuckets];
+  __shared__ int64_t s_ob[kMaxBuckets], s_db[kMaxWorld];
+  __shared__ uint64_t s_bp[kMaxBuckets];
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const bool pack = err[0] == 0;
+  const uint32_t world = (nb - 1) / kE;
+  for (uint32_t k = tid; k < nb - 1; k += 256) {
+    s_ob[k] = obase[k];
+    s_bp[k] = bpre[k];
+  }
+  for (uint32_t r = tid; r < world; r += 256) s_db[r] = dbase[r];
   for (uint32_t k = tid; k < nb; k += 256) {
     run_c[k] = tcnt[static_cast<uint64_t>(k) * ntiles + blockIdx.x];
     run_b[k] = tbytes[static_cast<uint64_t>(k) * ntiles + blockIdx.x];
@@ -367,9 +395,11 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
     const bool ok = p < p1;
     const uint32_t k = ok ? key[p] : 0xFFFFFFFFu;
     uint32_t l = 0;
+    uint64_t a = 0;
     if (ok && k < nb - 1) {
       const uint64_t t = p >> 1;
-      l = static_cast<uint32_t>(to[t + 1] - to[t]);
+      a = to[t];
+      l = static_cast<uint32_t>(to[t + 1] - a);
     }
     // rank among the wave's lanes with the same key, and the wave's totals per key
     uint32_t rc = 0;
@@ -409,8 +439,11 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
       const uint32_t pos = pc + rc;
       key_s[pos] = k;
       perm[pos] = static_cast<uint32_t>(p);
-      len[pos] = l;
-      sc[pos] = pb + rb;
+      if (pack && k < nb - 1) {
+        const uint64_t x = pb + rb;  // the request's first byte among the sorted requests'
+        reinterpret_cast<uint32_t*>(send)[s_ob[k] + pos] = static_cast<uint32_t>(x - s_bp[k]);
+        copy_topic(tb + a, send + (s_db[k / kE] + static_cast<int64_t>(x)), l);
+      }
     }
     __syncthreads();
     for (uint32_t kk = tid; kk < nb; kk += 256) {
@@ -429,24 +462,26 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
   }
 }
 
-// One block: per destination rank the chunk's sizes, start, header and final offsets.
+// One block: per destination rank the chunk's sizes, start, header and final offsets, and per
+// bucket where the sorted scatter puts its requests (pack fused into shard_sort_scatter_kernel):
+// obase[b] + p = the offset word of sorted request p, dbase[r] + byte prefix = its bytes.
 __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __restrict__ start,
-                                                          const uint64_t* __restrict__ sc, uint32_t world,
+                                                          const uint64_t* __restrict__ bpre, uint32_t world,
                                                           uint8_t* __restrict__ send, uint64_t cap,
                                                           int64_t* __restrict__ meta, uint64_t* __restrict__ cbase,
+                                                          int64_t* __restrict__ obase, int64_t* __restrict__ dbase,
                                                           uint32_t* __restrict__ err) {
   __shared__ uint64_t sz[kMaxWorld];
   const uint32_t r = threadIdx.x;
-  uint32_t nq[kE] = {};
+  uint32_t nq[kE] = {}, nall = 0;
   uint64_t by[kE] = {}, size = 0;
   bool wide = false;
   if (r < world) {
-    uint32_t nall = 0;
     uint64_t ball = 0;
     for (uint32_t e = 0; e < kE; ++e) {
-      const uint32_t s0 = start[kE * r + e], s1 = start[kE * r + e + 1];
-      nq[e] = s1 - s0;
-      by[e] = sc[s1] - sc[s0];
+      const uint32_t b = kE * r + e;
+      nq[e] = start[b + 1] - start[b];
+      by[e] = bpre[b + 1] - bpre[b];
       nall += nq[e];
       ball += by[e];
       wide |= by[e] > 0xFFFFFFFFull;
@@ -476,6 +511,8 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
   uint32_t* h = reinterpret_cast<uint32_t*>(send + base);
   uint32_t o = kHW;
   for (uint32_t e = 0; e < kE; ++e) {
+    const uint32_t b = kE * r + e;
+    obase[b] = static_cast<int64_t>(base / 4 + o) - static_cast<int64_t>(start[b]);
     h[e] = nq[e];
     h[4 + e] = static_cast<uint32_t>(by[e]);
     o += nq[e];
@@ -483,36 +520,7 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
   }
   h[3] = 0;
   h[7] = 0;
-}
-
-// 4 lanes per request (16 requests a wave, their loads in flight together): its offset entry
-// and its topic's bytes (16-B moves) into the destination's chunk.
-__global__ __launch_bounds__(256) void shard_pack_kernel(const uint8_t* __restrict__ tb,
-                                                         const uint64_t* __restrict__ to,
-                                                         const uint32_t* __restrict__ key_s,
-                                                         const uint32_t* __restrict__ perm,
-                                                         const uint32_t* __restrict__ start,
-                                                         const uint64_t* __restrict__ sc,
-                                                         const uint64_t* __restrict__ cbase, uint32_t world,
-                                                         const uint32_t* __restrict__ err, uint8_t* __restrict__ send) {
-  if (err[0]) return;
-  const uint32_t nreq = start[kE * world];
-  const uint32_t sub = threadIdx.x & 3u;
-  for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; p < nreq;
-       p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
-    const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
-    const uint32_t* st = start + kE * r;
-    const uint32_t nall = st[kE] - st[0];
-    uint32_t owords = kHW;  // slot e's offsets start after the earlier slots' (n + 1 each)
-    for (uint32_t k = 0; k < e; ++k) owords += st[k + 1] - st[k] + 1;
-    const uint64_t rel = sc[p] - sc[start[b]];
-    uint8_t* c = send + cbase[r];
-    if (sub == 0) reinterpret_cast<uint32_t*>(c)[owords + (p - start[b])] = static_cast<uint32_t>(rel);
-    const uint64_t data = 4 * kHW + al16(4ull * (nall + kE)) + (sc[start[b]] - sc[st[0]]) + rel;
-    const uint32_t t = perm[p] >> 1;
-    const uint64_t a = to[t], len = to[t + 1] - a;
-    copy_bytes(tb + a, c + data, len, sub, 4);
-  }
+  dbase[r] = static_cast<int64_t>(base + 4 * kHW + al16(4ull * (nall + kE))) - static_cast<int64_t>(bpre[kE * r]);
 }
 
 // emqx_shard_route_device: the raw requests (req2[2t], req2[2t + 1]) with the same scanner.
@@ -635,46 +643,6 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
 
 // ---- merge ------------------------------------------------------------------------------
 
-// Per sorted request p: its answer count and where its ids begin in its chunk's id region, and
-// pos[request] = p (kNone for no request).
-__global__ __launch_bounds__(256) void shard_gather_counts_kernel(ShardTab tab,
-                                                                  const uint32_t* __restrict__ key_s,
-                                                                  const uint32_t* __restrict__ perm,
-                                                                  const uint32_t* __restrict__ start, uint64_t m,
-                                                                  uint32_t world, uint32_t* __restrict__ cnt,
-                                                                  uint32_t* __restrict__ beg,
-                                                                  uint32_t* __restrict__ pos) {
-  const uint32_t nreq = start[kE * world];
-  for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
-       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    uint32_t c = 0;
-    if (p < nreq) {
-      const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
-      const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
-      uint32_t before = 0;
-      for (uint32_t k = 0; k < e; ++k) before += ch[k];
-      const uint32_t k = before + (p - start[b]);
-      const uint32_t b0 = k ? ch[kHW + k - 1] : 0u;
-      c = ch[kHW + k] - b0;
-      beg[p] = b0;
-      pos[perm[p]] = static_cast<uint32_t>(p);
-    } else {
-      pos[perm[p]] = kNone;
-    }
-    cnt[p] = c;
-  }
-}
-
-__global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t* __restrict__ cnt,
-                                                                 const uint32_t* __restrict__ pos, uint64_t n,
-                                                                 uint32_t* __restrict__ tcnt) {
-  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
-       t += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint2 q = *reinterpret_cast<const uint2*>(pos + 2 * t);
-    tcnt[t] = (q.x != kNone ? cnt[q.x] : 0u) + (q.y != kNone ? cnt[q.y] : 0u);
-  }
-}
-
 // This rank's own answers, read in place: per slot its engine's ids from the first id of this
 // rank's own requests (self = kNone: every answer came in a chunk).
 struct SelfIds {
@@ -684,46 +652,70 @@ struct SelfIds {
   uint32_t self;
 };
 
-// 4 lanes per request, in request (send) order: its answer's ids, read from the answer chunk
-// where they lie in that same order (coalesced) — or, for this rank's own requests, from its
-// engines' CSRs — to its topic's place in the output: the topic's offset, after the ids of the
-// topic's first request for its second.
-__global__ __launch_bounds__(256) void shard_merge_kernel(ShardTab tab, SelfIds me,
-                                                          const uint32_t* __restrict__ key_s,
-                                                          const uint32_t* __restrict__ perm,
-                                                          const uint32_t* __restrict__ start,
-                                                          const uint32_t* __restrict__ cnt,
-                                                          const uint32_t* __restrict__ beg,
-                                                          const uint32_t* __restrict__ pos, uint32_t world,
-                                                          const uint64_t* __restrict__ out_off,
-                                                          uint32_t* __restrict__ out_ids) {
+// Per sorted request p: where its answer's ids are (an answer chunk's id region, or this rank's
+// own engine output) and how many, stored at the request's own index perm[p] (2t: a topic's
+// first request, 2t + 1 its second) — the merge then reads them per topic, coalesced.
+__global__ __launch_bounds__(256) void shard_gather_kernel(ShardTab tab, SelfIds me,
+                                                           const uint32_t* __restrict__ key_s,
+                                                           const uint32_t* __restrict__ perm,
+                                                           const uint32_t* __restrict__ start, uint64_t m,
+                                                           uint32_t world, uint32_t* __restrict__ rq_cnt,
+                                                           uint64_t* __restrict__ rq_src) {
   const uint32_t nreq = start[kE * world];
-  const uint32_t sub = threadIdx.x & 3u;
-  for (uint64_t p = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; p < nreq;
-       p += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
-    const uint32_t c = cnt[p];
-    if (c == 0) continue;
-    const uint32_t q = perm[p], t = q >> 1, second = q & 1u;
-    const uint32_t b = key_s[p], r = b / kE;
+  for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
+       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t q = perm[p];
+    if (p >= nreq) {
+      rq_cnt[q] = 0;
+      continue;
+    }
+    const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
     const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
-    const uint32_t* from;
-    if (r == me.self) {
-      const uint32_t e = b - kE * r;
-      uint32_t before = 0;
-      for (uint32_t k = 0; k < e; ++k) before += ch[3 + k];
-      from = me.ids[e] + me.off[e][me.q0[e]] + (beg[p] - before);
-    } else {
-      from = ch + kHW + ch[0] + ch[1] + ch[2] + beg[p];
+    uint32_t before = 0, ibefore = 0;  // the chunk's requests / ids of the earlier slots
+    for (uint32_t k = 0; k < e; ++k) {
+      before += ch[k];
+      ibefore += ch[3 + k];
     }
-    uint64_t dst = out_off[t];
-    if (second) {
-      const uint32_t pa = pos[2 * t];
-      if (pa != kNone) dst += cnt[pa];
-    }
-    for (uint32_t j = sub; j < c; j += 4) out_ids[dst + j] = from[j];
+    const uint32_t k = before + (p - start[b]);
+    const uint32_t b0 = k ? ch[kHW + k - 1] : 0u;
+    rq_cnt[q] = ch[kHW + k] - b0;
+    const uint32_t* src = r == me.self ? me.ids[e] + me.off[e][me.q0[e]] + (b0 - ibefore)
+                                       : ch + kHW + ch[0] + ch[1] + ch[2] + b0;
+    rq_src[q] = reinterpret_cast<uint64_t>(src);
   }
 }
 
+__global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t* __restrict__ rq_cnt, uint64_t n,
+                                                                 uint32_t* __restrict__ tcnt) {
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
+       t += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint2 c = *reinterpret_cast<const uint2*>(rq_cnt + 2 * t);
+    tcnt[t] = c.x + c.y;
+  }
+}
+
+// 4 lanes per topic, in topic order: its first request's ids, then its second's, to the topic's
+// place in the output (the counts, addresses and offsets read coalesced, no dependent chain).
+__global__ __launch_bounds__(256) void shard_merge_kernel(const uint32_t* __restrict__ rq_cnt,
+                                                          const uint64_t* __restrict__ rq_src, uint64_t n,
+                                                          const uint64_t* __restrict__ out_off,
+                                                          uint32_t* __restrict__ out_ids) {
+  const uint32_t sub = threadIdx.x & 3u;
+  for (uint64_t t = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; t < n;
+       t += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
+    const uint2 c = *reinterpret_cast<const uint2*>(rq_cnt + 2 * t);
+    if ((c.x | c.y) == 0) continue;
+    const uint64_t dst = out_off[t];
+    if (c.x) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(rq_src[2 * t]);
+      for (uint32_t j = sub; j < c.x; j += 4) out_ids[dst + j] = src[j];
+    }
+    if (c.y) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(rq_src[2 * t + 1]);
+      for (uint32_t j = sub; j < c.y; j += 4) out_ids[dst + c.x + j] = src[j];
+    }
+  }
+}
 
 }  // namespace
 
@@ -746,11 +738,14 @@ struct emqx_shard_step {
   uint32_t n_splits = 0;
   // request scratch, sized for m_cap requests
   uint64_t m_cap = 0;
-  uint32_t *key = nullptr, *key_s = nullptr, *perm = nullptr, *len = nullptr, *pos = nullptr, *tcnt = nullptr,
-           *beg = nullptr, *tcnt_tab = nullptr, *tbytes_tab = nullptr;  // (tab: the sort's (bucket, tile) table)
-  uint64_t *sc = nullptr, *partials = nullptr, *pbytes_tab = nullptr;
+  uint32_t *key = nullptr, *key_s = nullptr, *perm = nullptr, *pos = nullptr, *tcnt = nullptr,
+           *tcnt_tab = nullptr, *tbytes_tab = nullptr;  // (tab: the sort's (bucket, tile) table)
+  uint64_t *partials = nullptr, *pbytes_tab = nullptr, *rq_src = nullptr;  // (pos: merge's rq_cnt)
   uint32_t* start = nullptr;  // [kE G + 2]
   uint64_t* cbase = nullptr;  // [G]
+  uint64_t* bpre = nullptr;   // [kE G + 2]: each bucket's first byte among the sorted requests'
+  int64_t* obase = nullptr;   // [kE G + 2]: offset-word base per bucket (pack)
+  int64_t* dbase = nullptr;   // [G]: byte base per destination (pack)
   uint32_t* err = nullptr;
   // the step in flight
   uint64_t n = 0;                       // topics of the last send
@@ -763,12 +758,12 @@ namespace {
 
 void free_scratch(emqx_shard_step* st) {
   for (void* p : {static_cast<void*>(st->key), static_cast<void*>(st->tcnt_tab), static_cast<void*>(st->key_s),
-                  static_cast<void*>(st->perm), static_cast<void*>(st->len), static_cast<void*>(st->pos),
-                  static_cast<void*>(st->tcnt), static_cast<void*>(st->sc), static_cast<void*>(st->partials),
-                  static_cast<void*>(st->beg), static_cast<void*>(st->tbytes_tab), static_cast<void*>(st->pbytes_tab)})
+                  static_cast<void*>(st->perm), static_cast<void*>(st->pos),
+                  static_cast<void*>(st->tcnt), static_cast<void*>(st->partials),
+                  static_cast<void*>(st->rq_src), static_cast<void*>(st->tbytes_tab), static_cast<void*>(st->pbytes_tab)})
     if (p) (void)hipFree(p);
-  st->key = st->tcnt_tab = st->key_s = st->perm = st->len = st->pos = st->tcnt = st->beg = st->tbytes_tab = nullptr;
-  st->sc = st->partials = st->pbytes_tab = nullptr;
+  st->key = st->tcnt_tab = st->key_s = st->perm = st->pos = st->tcnt = st->tbytes_tab = nullptr;
+  st->partials = st->pbytes_tab = st->rq_src = nullptr;
   st->m_cap = 0;
 }
 
@@ -790,11 +785,9 @@ hipError_t ensure_scratch(emqx_shard_step* st, uint64_t m) {
   al(&st->pbytes_tab, 8 * tab);
   al(&st->key_s, 4 * cap);
   al(&st->perm, 4 * cap);
-  al(&st->len, 4 * cap);
   al(&st->pos, 4 * cap);
-  al(&st->beg, 4 * cap);
+  al(&st->rq_src, 8 * cap);
   al(&st->tcnt, 4 * (cap / 2 + 1));
-  al(&st->sc, 8 * (cap + 1));
   al(&st->partials, 8 * scan_partials(cap));
   if (e != hipSuccess) {
     free_scratch(st);
@@ -836,6 +829,9 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
   if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // (the DMA has landed: steps run on other streams)
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->start), 4ull * (kE * world + 2));
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->cbase), 8ull * world);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->bpre), 8ull * (kE * world + 2));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->obase), 8ull * (kE * world + 2));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->dbase), 8ull * world);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->err), 16);
   if (e != hipSuccess) {
     emqx_shard_step_destroy(st);
@@ -851,6 +847,7 @@ int emqx_shard_step_destroy(emqx_shard_step* st) {
   (void)hipDeviceSynchronize();
   free_scratch(st);
   for (void* p : {static_cast<void*>(st->d_splits), static_cast<void*>(st->start), static_cast<void*>(st->cbase),
+                  static_cast<void*>(st->bpre), static_cast<void*>(st->obase), static_cast<void*>(st->dbase),
                   static_cast<void*>(st->err)})
     if (p) (void)hipFree(p);
   delete st;
@@ -871,18 +868,18 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
     hipLaunchKernelGGL(shard_key_kernel, dim3(ntiles), dim3(256), 0, s, d_bytes, d_offsets, n, G, st->d_splits,
                        st->n_splits, st->key, ntiles, st->tcnt_tab, st->tbytes_tab);
     hipLaunchKernelGGL(shard_sort_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, st->tcnt_tab, st->tbytes_tab,
-                       st->pbytes_tab, nb, ntiles, m, st->start, st->sc);
-    hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_offsets, m, nb, ntiles,
-                       st->tcnt_tab, st->pbytes_tab, st->key_s, st->perm, st->len, st->sc);
+                       st->pbytes_tab, nb, ntiles, m, st->start, st->bpre);
+    hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->bpre, G, d_send, send_cap, d_meta,
+                       st->cbase, st->obase, st->dbase, st->err);
+    hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_bytes, d_offsets, m, nb,
+                       ntiles, st->tcnt_tab, st->pbytes_tab, st->bpre, st->obase, st->dbase, st->err, d_send,
+                       st->key_s, st->perm);
   } else {
     SS_TRY(hipMemsetAsync(st->start, 0, 4ull * (kE * G + 2), s));
-    SS_TRY(hipMemsetAsync(st->sc, 0, 8, s));
+    SS_TRY(hipMemsetAsync(st->bpre, 0, 8ull * (kE * G + 2), s));
+    hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->bpre, G, d_send, send_cap, d_meta,
+                       st->cbase, st->obase, st->dbase, st->err);
   }
-  hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->sc, G, d_send, send_cap, d_meta,
-                     st->cbase, st->err);
-  if (m)
-    hipLaunchKernelGGL(shard_pack_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, d_bytes, d_offsets, st->key_s,
-                       st->perm, st->start, st->sc, st->cbase, G, st->err, d_send);
   SS_TRY(hipGetLastError());
   st->n = n;
   st->have_send = true;
@@ -991,16 +988,15 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   SS_TRY(hipSetDevice(st->device));
   const uint64_t n = st->n, m = 2 * n;
   if (m) {
-    hipLaunchKernelGGL(shard_gather_counts_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, t, st->key_s,
-                       st->perm, st->start, m, G, st->len, st->beg, st->pos);
-    hipLaunchKernelGGL(shard_topic_counts_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, st->len, st->pos, n,
-                       st->tcnt);
+    hipLaunchKernelGGL(shard_gather_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, t, st->self_ids, st->key_s,
+                       st->perm, st->start, m, G, st->pos, st->rq_src);
+    hipLaunchKernelGGL(shard_topic_counts_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, st->pos, n, st->tcnt);
   }
   SS_TRY(launch_scan(st->tcnt, n, d_out_offsets, st->partials, s));
   if (n) {
     if (!d_out_ids) return EMQX_EINVAL;
-    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(m, 64)), dim3(256), 0, s, t, st->self_ids, st->key_s, st->perm,
-                       st->start, st->len, st->beg, st->pos, G, d_out_offsets, d_out_ids);
+    hipLaunchKernelGGL(shard_merge_kernel, dim3(grid_of(n, 64)), dim3(256), 0, s, st->pos, st->rq_src, n, d_out_offsets,
+                       d_out_ids);
   }
   SS_TRY(hipGetLastError());
   return EMQX_OK;

@@ -185,6 +185,19 @@ def _a2a(out_t: torch.Tensor, in_t: torch.Tensor, out_splits: List[int], in_spli
     dist.all_to_all_single(out_t, in_t, out_splits, in_splits, group=group)
 
 
+_HIP = None
+
+
+def _hip():
+    """The HIP runtime torch already loaded (for hipHostGetDevicePointer)."""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+        _HIP.hipHostGetDevicePointer.restype = ctypes.c_int
+        _HIP.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+    return _HIP
+
+
 def _exchange_chunks(send: torch.Tensor, out_sz: List[int], in_sz: List[int], recv_buf: Callable, group,
                      rank: int) -> List[int]:
     """Chunk r of ``send`` (sizes ``out_sz`` in rank order, contiguous) to rank r; returns the
@@ -482,6 +495,20 @@ class ShardedMatcher:
             return res
         return self._match_all_tensors(topics)
 
+    def _pinned(self, name: str, n: int):
+        """A reused page-locked int64 buffer the device writes directly (its host tensor and the
+        device address it is mapped at): words the host reads after a stream sync, with no copy."""
+        got = self._bufs.get("_pin_" + name)
+        if got is None or got[0].numel() < n:
+            t = torch.zeros(max(n, 16), dtype=torch.int64, pin_memory=True)
+            d = ctypes.c_void_p()
+            rc = _hip().hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(t.data_ptr()), 0)
+            if rc != 0:
+                raise RuntimeError(f"hipHostGetDevicePointer: {rc}")
+            got = (t, d.value)
+            self._bufs["_pin_" + name] = got
+        return got
+
     def _to_host(self, *parts: torch.Tensor) -> np.ndarray:
         """The device tensors' values (int64) on the host: one copy into a reused pinned buffer
         and a wait for this stream (no allocation per call)."""
@@ -528,12 +555,15 @@ class ShardedMatcher:
         # 1. requests -> one chunk per destination
         cap = int(L.emqx_shard_send_cap(n, tb.numel(), G))
         send = self._buf("send", cap, torch.uint8)
-        meta = torch.empty(MW * G, dtype=torch.int64, device=dev)
-        _lib.check(L.emqx_shard_step_send(st, P(tb), P(to), n, P(send), send.numel(), P(meta), S),
-                   "emqx_shard_step_send")
+        # (world 1: the sizes go straight into mapped pinned memory, read after the stream sync)
+        hmeta, dmeta = self._pinned("meta", MW * G) if G == 1 else (None, None)
+        meta = None if G == 1 else torch.empty(MW * G, dtype=torch.int64, device=dev)
+        _lib.check(L.emqx_shard_step_send(st, P(tb), P(to), n, P(send), send.numel(),
+                                          ctypes.c_void_p(dmeta) if G == 1 else P(meta), S), "emqx_shard_step_send")
+        cur = torch.cuda.current_stream(dev)
         if G == 1:
-            mh = self._to_host(meta)  # host sync 1
-            mo = mi = np.ascontiguousarray(mh.reshape(G, MW))
+            cur.synchronize()  # host sync 1
+            mo = mi = hmeta[: MW * G].numpy().reshape(G, MW).copy()
         else:
             meta_in = torch.empty_like(meta)
             _a2a(meta_in, meta, [MW] * G, [MW] * G, grp)
@@ -561,8 +591,8 @@ class ShardedMatcher:
         # after the first, so the walks overlap
         batches = [(qaddr[e], qoff[e], NQ[e]) for e in range(E)]
         outs = []
-        summ = self._buf("summary", 8 * E, torch.int64)  # written by each engine call that runs
-        cur = torch.cuda.current_stream(dev)
+        hsumm, dsumm = self._pinned("summary", 8 * E)  # written by each engine call that runs
+
         if self._stream_b is None:
             self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E - 1)]
         used = []
@@ -578,7 +608,7 @@ class ShardedMatcher:
                 es.wait_stream(cur)
             used.append(es)
             self.engines[e].match_device_async(eb, eo.data_ptr(), ne, ro.data_ptr(), ri.data_ptr(),
-                                               ri.numel(), summ[8 * e:].data_ptr(), mode=self.mode,
+                                               ri.numel(), dsumm + 64 * e, mode=self.mode,
                                                stream=es.cuda_stream)
             outs.append([ro, ri])
         for es in used:
@@ -589,23 +619,28 @@ class ShardedMatcher:
         redo = False
         while True:
             ans = self._buf("answer", 8 * G + sum(NQ) + sum(o[1].numel() for o in outs), torch.int32)
-            ans_meta = torch.empty(3 * G, dtype=torch.int64, device=dev)  # per source: words, redo, ids
-            sp = None if redo else PA([summ[8 * e:] if NQ[e] else None for e in range(E)])
+            # per source: words, redo, ids (world 1: into mapped pinned memory)
+            hans, dans = self._pinned("ans_meta", 3 * G) if G == 1 else (None, None)
+            ans_meta = None if G == 1 else torch.empty(3 * G, dtype=torch.int64, device=dev)
+            sp = None if redo else (ctypes.c_void_p * E)(*[dsumm + 64 * e if NQ[e] else None for e in range(E)])
             # (this rank's own answers stay in the engines' outputs: the merge reads them there)
             _lib.check(L.emqx_shard_step_answer(st, PA([o[0] for o in outs]), PA([o[1] for o in outs]), sp, self.rank,
-                                                P(ans), P(ans_meta), S), "emqx_shard_step_answer")
+                                                P(ans), ctypes.c_void_p(dans) if G == 1 else P(ans_meta), S),
+                       "emqx_shard_step_answer")
             if G == 1:
-                ans_in = ans_meta
+                cur.synchronize()  # host sync 2
+                am = ai = hans[: 3 * G].numpy().reshape(G, 3).copy()
             else:
                 ans_in = torch.empty_like(ans_meta)
                 _a2a(ans_in, ans_meta, [3] * G, [3] * G, grp)
-            h = self._to_host(ans_meta, ans_in, summ[: 8 * E])  # host sync 2
-            am, ai, sm = h[: 3 * G].reshape(G, 3), np.ascontiguousarray(h[3 * G: 6 * G]), h[6 * G:].reshape(E, 8)
+                h = self._to_host(ans_meta, ans_in)  # host sync 2
+                am, ai = h[: 3 * G].reshape(G, 3), np.ascontiguousarray(h[3 * G: 6 * G]).reshape(G, 3)
+            sm = hsumm[: 8 * E].numpy().reshape(E, 8).copy()
             if not redo:
                 for e in range(E):  # learn the id capacities from this call's totals
                     if NQ[e] and sm[e, 0] == 0:
                         self._caps[e] = max(self._caps[e], int(sm[e, 1] * 1.25) + 4096)
-            if not ai.reshape(G, 3)[:, 1].any():
+            if not ai[:, 1].any():
                 break
             if am[0, 1]:  # this rank's call did not complete: redo it synchronously, exact size
                 for e, (eb, eo, ne) in enumerate(batches):
@@ -614,11 +649,12 @@ class ShardedMatcher:
                         self._caps[e] = max(self._caps[e], int(outs[e][1].numel() * 1.25) + 4096)
             redo = True
         # 4. answers back to their sources, merged per topic in batch order
-        out_w, in_w = am[:, 0].tolist(), ai.reshape(G, 3)[:, 0].tolist()
+        out_w, in_w = am[:, 0].tolist(), ai[:, 0].tolist()
         back = _exchange_chunks(ans, out_w, in_w, lambda k: self._buf("back", k + 16, torch.int32), grp, self.rank)
-        total = int(ai.reshape(G, 3)[:, 2].sum())
+        total = int(ai[:, 2].sum())
         out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         out_ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        ai = np.ascontiguousarray(ai, dtype=np.int64)
         _lib.check(L.emqx_shard_step_merge(st, (ctypes.c_void_p * G)(*back), ai.ctypes.data, P(out_off), P(out_ids),
                                            S), "emqx_shard_step_merge")
         return out_off, out_ids[:total]
