@@ -8,15 +8,19 @@
 //
 //   send    route every topic to its (rank, engine) requests (layout.h shard_route_topic),
 //           fold them onto the rank's three engine slots (shard_fold: a topic whose requests
-//           meet on one rank, or that makes only one, asks that rank's AB engine once), stable
-//           radix sort of the requests by destination, one chunk per destination:
+//           meet on one rank, or that makes only one, asks that rank's AB engine once), a
+//           stable counting sort of the requests by destination whose scatter packs one chunk
+//           per destination (layout first, from the sort's bucket starts and byte prefixes):
 //             [u32 n0 n1 n2 0 bytes0 bytes1 bytes2 0][u32 offsets of the n0 slot-0 requests + 1]
 //             [slot 1 + 1][slot 2 + 1] pad 16 [slot 0 topic bytes][slot 1][slot 2] pad 16
-//   recv    the received chunks -> three contiguous batches (every source's slot-e requests)
+//   recv    the received chunks (this rank's own read where it was packed) -> three batches
+//           (every source's slot-e requests; a slot with one source is matched in place)
 //   answer  the three engines' CSRs -> one answer chunk per source:
-//             [u32 n0 n1 n2 ids0 ids1 ids2 0 0][counts of slot 0][1][2][ids 0][ids 1][ids 2]
-//   merge   the answer chunks -> the CSR of the rank's batch in batch order, each topic's
-//           first request's ids then its second's (engine A then engine B)
+//             [u32 n0 n1 n2 ids0 ids1 ids2 0 0][per request the end of its ids][ids 0][1][2]
+//           (this rank's own chunk without ids: the merge reads them from the CSRs)
+//   merge   per request its ids' address and count (at the request's own index), per topic
+//           the total, a scan, then in topic order each topic's first request's ids and its
+//           second's (engine A then engine B) -> the CSR of the rank's batch in batch order
 //
 // Engine slots of a rank: 0 = A (space L + root wildcards), 1 = B (space P), 2 = AB (both, one
 // table).  A topic's two raw requests (A at rank rA, B at rank rB) become ONE request to slot 2
