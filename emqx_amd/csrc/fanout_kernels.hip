@@ -274,7 +274,8 @@ __device__ __forceinline__ uint32_t pick_stateless(const FanoutArgs& a, const Gr
   return a.members[g.member_begin + idx];
 }
 
-__global__ __launch_bounds__(FO_THREADS) void fanout_write_kernel(FanoutArgs a) {
+// (5 waves per SIMD: 96 VGPRs, no spill; the compiler's own choice, 98, rounds up to 104 and 4 waves)
+__global__ __launch_bounds__(FO_THREADS, 5) void fanout_write_kernel(FanoutArgs a) {
   struct WaveLds {
     uint32_t pre[FO_WCHUNK];  // entry's first output, relative to the chunk's first output
     uint32_t fid[FO_WCHUNK];
