@@ -1243,7 +1243,7 @@ constexpr uint32_t RUNROLL = RCHUNK / 64;
 constexpr uint32_t RGROUP = 8;                // lanes per small record
 constexpr uint32_t RPER = RBIG / RGROUP;      // ranks per lane of a small record, at most
 template <int MODE>
-__global__ __launch_bounds__(256) void retain_out_kernel(RetainArgs a) {
+__global__ __launch_bounds__(256, MODE == 1 ? 7 : 6) void retain_out_kernel(RetainArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
