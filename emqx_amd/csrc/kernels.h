@@ -197,7 +197,8 @@ enum FastVariant {
   FAST_K1_S768W = 9, // 4 waves/block, stack 768, 1024 word ids, K=1 (deep tables: 15 waves/CU)
   FAST_K1_S512W = 10,// 4 waves/block, stack 512 (+HBM spill), 1024 word ids, K=1: 18 waves/CU
   FAST_K1_S384R = 11,// FAST_K1_S384 with the root's edge array staged in LDS (an A/B of round 5)
-  FAST_NVARIANTS = 12
+  FAST_K1_S384P = 12,// FAST_K1_S384 as two kernels: phase A, then the walk (an A/B of round 5)
+  FAST_NVARIANTS = 13
 };
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);

@@ -568,11 +568,17 @@ struct FastLds {
 // One wave walks one tile: topics [tile * tt, tile * tt + tt) of the batch (tt <= 64; the batched
 // kernel's tiles are TILE_TOPICS wide, the small-batch kernel's narrower, so that a batch of a
 // few dozen topics spreads over many waves).  Wave-uniform returns only; no block barrier.
-template <int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false>
+// PA splits the tile over two kernels (FAST_K1_S384P, an A/B of round 5): 0 = one kernel,
+// 1 = phase A only, its results parked in the tile's HBM spill area (idle until phase B):
+// [0, 64) the topics' word-id ends, [64, 128) packed flags (pa_flags), [128] the tile's word
+// count, [192, 192 + words) the word ids; 2 = phase B onward, starting from that record.
+constexpr uint32_t PA_WIDS = 192;
+template <int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false, int PA = 0>
 __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP, WID_CAP>& L, uint64_t tile,
                                           uint32_t tt, const uint4* rl = nullptr, uint32_t rsz = 0) {
   static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
   static_assert(WID_CAP <= 1024, "item word index is 10 bits");
+  static_assert(PA == 0 || (!DIAG && PA_WIDS + WID_CAP <= 2 * 2048), "split tiles: no diagnostics; record fits the spill");
   const uint32_t lane = lane_id();
   const uint64_t t0 = tile * tt;
   if (t0 >= a.n) return;  // wave-uniform; the kernel uses no block-wide barrier
@@ -589,6 +595,24 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
     end = a.toffs[t + 1];
   }
 
+  uint32_t nlev = 0, wbase = 0;
+  bool wild = false, dollar = false, defer = false;
+  uint64_t defer_mask = 0;
+  if constexpr (PA == 2) {
+    const uint32_t* pa = reinterpret_cast<const uint32_t*>(a.spill + tile * a.spill_cap);
+    const uint32_t fl = pa[64 + lane];
+    L.wend[lane] = pa[lane];
+    const uint32_t nw = pa[128];
+    for (uint32_t j = lane; j < nw; j += 64) L.wids[j] = pa[PA_WIDS + j];
+    nlev = fl & 0xFFFFu;
+    defer = valid && ((fl >> 16) & 1u);
+    wild = (fl >> 17) & 1u;
+    dollar = (fl >> 18) & 1u;
+    wbase = fl >> 20;
+    defer_mask = __ballot(defer);
+    L.cnt[lane] = 0;
+    wave_sync();
+  } else {
   // ---- phase A1: tokenize ----------------------------------------------------------
   // The tile's topics are one contiguous byte range.  The wave reads it with coalesced
   // 16-B loads and writes a level map (chunk_levelmap) to the stack area, idle until
@@ -604,8 +628,7 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
   uint32_t* lmap = reinterpret_cast<uint32_t*>(L.stack);
   const uint32_t lo = static_cast<uint32_t>(start - A0), hi = static_cast<uint32_t>(end - A0);  // map path only
   Chunk64 C(a.tbytes, lim);
-  uint32_t nlev = 0;
-  bool wild = false, dollar = false, longw = false;
+  bool longw = false;
   if (use_map) {
     const uint32_t first = (valid && end > start) ? a.tbytes[start] : 0u;
     const uint32_t nch = static_cast<uint32_t>((tend - A0 + 15) >> 4);
@@ -652,10 +675,10 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
     }
     longw |= llen >= AUX_LEN_MAX;
   }
-  bool defer = valid && (nlev > static_cast<uint32_t>(WID_CAP / 8) || longw || end - A0 >= AUX_OFF_LIM);
+  defer = valid && (nlev > static_cast<uint32_t>(WID_CAP / 8) || longw || end - A0 >= AUX_OFF_LIM);
   const uint32_t need = (valid && !defer) ? nlev : 0u;
   const uint32_t incl = wave_incl_scan(need, lane);
-  const uint32_t wbase = incl - need;
+  wbase = incl - need;
   if (valid && !defer && incl > static_cast<uint32_t>(WID_CAP)) defer = true;
   L.wend[lane] = incl;  // end of the topic's word ids (= the next topic's first)
 
@@ -712,7 +735,7 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
 #pragma unroll
   for (uint32_t dd = 32; dd >= 1; dd >>= 1) nwords = max(nwords, static_cast<uint32_t>(__shfl_xor(nwords, dd, 64)));
   defer |= longw;
-  uint64_t defer_mask = __ballot(defer);
+  defer_mask = __ballot(defer);
   wave_sync();
 
   // ---- phase A2: intern every word of the tile, word-parallel ------------------------
@@ -764,6 +787,17 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
   }
   L.cnt[lane] = 0;
   wave_sync();
+  if constexpr (PA == 1) {
+    uint32_t* pa = reinterpret_cast<uint32_t*>(a.spill + tile * a.spill_cap);
+    pa[lane] = L.wend[lane];
+    // nlev and wbase matter only for topics kept on the fast path (nlev <= WID_CAP / 8, wbase < WID_CAP)
+    pa[64 + lane] = (nlev & 0xFFFFu) | (defer ? 1u << 16 : 0u) | (wild ? 1u << 17 : 0u) | (dollar ? 1u << 18 : 0u) |
+                    ((wbase & 0xFFFu) << 20);
+    if (lane == 0) pa[128] = nwords;
+    for (uint32_t j = lane; j < nwords; j += 64) pa[PA_WIDS + j] = L.wids[j];
+    return;
+  }
+  }
   const uint64_t clk1 = DIAG ? wall_clock64() : 0;
 
   // ---- phase B: pooled frontier walk ------------------------------------------------
@@ -1004,7 +1038,7 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
 
 constexpr uint32_t ROOT_LDS_SLOTS = 256;  // FAST_K1_S384R: root arrays up to 4 KB staged in LDS
 
-template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false>
+template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false, int PA = 0>
 __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(MatchArgs a) {
   __shared__ FastLds<STACK_CAP, WID_CAP> lds_all[WAVES];
   __shared__ uint4 rl[RL ? ROOT_LDS_SLOTS : 1];
@@ -1026,7 +1060,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, j = blockIdx.x >> 3, q = nb >> 3, r = nb & 7u;
     blk = static_cast<uint64_t>(x) * q + min(x, r) + j;
   }
-  fast_tile<STACK_CAP, WID_CAP, K, DIAG, RL>(a, lds_all[wv], blk * WAVES + wv, TILE_TOPICS, rl, rsz);
+  fast_tile<STACK_CAP, WID_CAP, K, DIAG, RL, PA>(a, lds_all[wv], blk * WAVES + wv, TILE_TOPICS, rl, rsz);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1852,6 +1886,16 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K1_S768W: launch_fast_t<4, 768, 1024, 1>(a, ntiles, s); break;
     case FAST_K1_S512W: launch_fast_t<4, 512, 1024, 1>(a, ntiles, s); break;
     case FAST_K1_S384R: launch_fast_t<4, 384, 640, 1, true>(a, ntiles, s); break;
+    case FAST_K1_S384P: {  // phase A and the walk as two kernels (diagnostic runs keep one)
+      if (a.diag) {
+        launch_fast_t<4, 384, 640, 1>(a, ntiles, s);
+        break;
+      }
+      const dim3 grid(static_cast<uint32_t>((ntiles + 3) / 4));
+      hipLaunchKernelGGL((match_fast_kernel<4, 384, 640, 1, false, false, 1>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((match_fast_kernel<4, 384, 640, 1, false, false, 2>), grid, dim3(256), 0, s, a);
+      break;
+    }
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
