@@ -302,7 +302,7 @@ struct emqx_subtab {
   uint64_t ops_pending = 0;                   // mutations since the last commit
   bool bulk = false;                          // so many that the next commit rebuilds: no dirt kept
   // ---- device ----
-  DevArr<FilterRec> d_recs;
+  DevArr<DevRec> d_recs;
   DevArr<uint32_t> d_fcnt;  // fo_cnt_word of each device record (written with it, on the device)
   DevArr<uint32_t> d_plain, d_members;
   DevArr<GroupRec> d_groups;
@@ -473,13 +473,15 @@ void plain_remove(emqx_subtab* s, uint32_t f, uint32_t sub) {
 
 // The device form of filter f's record (fanout.h FO_INLINE): a short plain list and no
 // groups inline, otherwise the image's record.
-uint4 dev_rec(const emqx_subtab* s, uint32_t f) {
+DevRec dev_rec(const emqx_subtab* s, uint32_t f) {
   const FilterRec& r = s->recs[f];
   if (r.n_groups == 0 && r.n_plain >= 1 && r.n_plain <= FO_INLINE) {
     const uint32_t* p = s->plain.data() + r.plain_begin;
-    return make_uint4(p[0], r.n_plain | FO_INLINE_BIT, r.n_plain > 1 ? p[1] : 0u, r.n_plain > 2 ? p[2] : 0u);
+    uint32_t v[FO_INLINE] = {};
+    for (uint32_t i = 0; i < r.n_plain; ++i) v[i] = p[i];
+    return DevRec{make_uint4(v[0], r.n_plain | FO_INLINE_BIT, v[1], v[2]), make_uint4(v[3], v[4], v[5], v[6])};
   }
-  return make_uint4(r.plain_begin, r.n_plain, r.group_begin, r.n_groups);
+  return DevRec{make_uint4(r.plain_begin, r.n_plain, r.group_begin, r.n_groups), make_uint4(0, 0, 0, 0)};
 }
 
 // EMQX_SUBTAB_PROF=1: per add/remove call and per commit, where the host time goes, on stderr
@@ -735,7 +737,7 @@ void compact_image(emqx_subtab* s) {
 int full_commit(emqx_subtab* s) {
   compact_image(s);
   // the old plain positions are indices into the lists, which compaction keeps: nothing to redo
-  DevArr<FilterRec> recs;
+  DevArr<DevRec> recs;
   DevArr<uint32_t> plain, members;
   DevArr<GroupRec> groups;
   auto up = [&](auto& d, const auto& v) -> int {
@@ -746,11 +748,8 @@ int full_commit(emqx_subtab* s) {
     return EMQX_OK;
   };
   DevArr<uint32_t> alive;
-  std::vector<FilterRec> drecs(s->recs.size());  // the device form (inline short lists)
-  for (uint64_t f = 0; f < drecs.size(); ++f) {
-    const uint4 v = dev_rec(s, static_cast<uint32_t>(f));
-    drecs[f] = FilterRec{v.x, v.y, v.z, v.w};
-  }
+  std::vector<DevRec> drecs(s->recs.size());  // the device form (inline short lists)
+  for (uint64_t f = 0; f < drecs.size(); ++f) drecs[f] = dev_rec(s, static_cast<uint32_t>(f));
   int rc = up(recs, drecs);
   DevArr<uint32_t> fcnt;
   if (rc == EMQX_OK) {
@@ -952,7 +951,8 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
     if (k + 8 < group_idx.size()) __builtin_prefetch(&s->groups[group_idx[k + 8]]);
     const uint64_t gi = group_idx[k];
     const GroupRec& g = s->groups[gi];
-    s->rpatch.push_back(RecPatch{static_cast<uint32_t>(gi), {0, 0, 0}, make_uint4(g.member_begin, g.n_members, g.slot, g.group_id)});
+    s->rpatch.push_back(RecPatch{static_cast<uint32_t>(gi), {0, 0, 0}, make_uint4(g.member_begin, g.n_members, g.slot, g.group_id),
+                                 make_uint4(0, 0, 0, 0)});
   }
   const uint64_t n_group_p = s->rpatch.size();
   mark();  // 4: group records
@@ -971,7 +971,8 @@ int live_commit(emqx_subtab* s, std::vector<void*>& retired) {
         }
         const uint32_t f = dr[i];
         s->rec_flag[f] = 0;
-        out[i] = RecPatch{f, {0, 0, 0}, dev_rec(s, f)};
+        const DevRec d = dev_rec(s, f);
+        out[i] = RecPatch{f, {0, 0, 0}, d.head, d.ext};
       }
     };
     const unsigned T = dr.size() >= PAR_MIN ? par_threads() : 1u;
@@ -1906,7 +1907,7 @@ int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4) {
   counts4[0] = s->plain_count();
   counts4[1] = s->n_members;
   counts4[2] = s->n_live_groups;
-  counts4[3] = s->d_recs.cap * sizeof(FilterRec) + s->d_plain.cap * 4 + s->d_groups.cap * sizeof(GroupRec) +
+  counts4[3] = s->d_recs.cap * sizeof(DevRec) + s->d_plain.cap * 4 + s->d_groups.cap * sizeof(GroupRec) +
                s->d_members.cap * 4 + s->ps_cap * 12;
   return EMQX_OK;
 }

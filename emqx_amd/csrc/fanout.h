@@ -30,11 +30,25 @@ struct FilterRec {
   uint32_t group_begin;  // first entry in groups[]
   uint32_t n_groups;     // $share groups with >= 1 member
 };
-// The device copy of a record whose filter has 1..FO_INLINE plain subscribers and no $share
-// group holds them inline: {s0, n_plain | FO_INLINE_BIT, s1, s2}, so its deliveries cost no
-// second random line (the host image keeps the arena form; fanout.cpp dev_rec).
-constexpr uint32_t FO_INLINE = 3;
+// The device copy of a record is 32 B (two per 64-B line): head = the record, ext unused; for a
+// filter with 1..FO_INLINE plain subscribers and no $share group the list itself,
+// head {s0, n_plain | FO_INLINE_BIT, s1, s2}, ext {s3, s4, s5, s6}, so its deliveries cost no
+// second random line (the host image keeps the arena form; fanout.cpp dev_rec).  Round 5 widened
+// it from 16 B and three subscribers: at Poisson(4.5) subscribers per filter (config E) the
+// inline share of match entries went from 34 % to 91 %.
+struct alignas(32) DevRec {
+  uint4 head;
+  uint4 ext;
+};
+constexpr uint32_t FO_INLINE = 7;
+constexpr uint32_t FO_INLINE_HEAD = 3;  // inline subscribers held in head (x, z, w); the rest in ext
 constexpr uint32_t FO_INLINE_BIT = 0x80000000u;
+// Inline subscriber r < FO_INLINE_HEAD from the head.
+__host__ __device__ inline uint32_t fo_inline_head(uint4 h, uint32_t r) { return r == 0 ? h.x : (r == 1 ? h.z : h.w); }
+// Address of inline subscriber r >= FO_INLINE_HEAD of filter f (in the record's own 32 B).
+__host__ __device__ inline const uint32_t* fo_inline_ext(const DevRec* recs, uint32_t f, uint32_t r) {
+  return reinterpret_cast<const uint32_t*>(&recs[f].ext) + (r - FO_INLINE_HEAD);
+}
 __host__ __device__ inline uint32_t fo_rec_plain(uint4 r) { return r.y & ~FO_INLINE_BIT; }
 __host__ __device__ inline uint32_t fo_rec_groups(uint4 r) { return (r.y & FO_INLINE_BIT) ? 0u : r.w; }
 
@@ -80,7 +94,7 @@ __host__ __device__ inline bool fo_alive(const uint32_t* alive, uint32_t n_words
 }
 
 struct FanoutArgs {
-  const FilterRec* recs;
+  const DevRec* recs;
   const uint32_t* fcnt;      // [n_recs] fo_cnt_word of each record (the count pass's dense copy)
   uint32_t n_recs;           // filter ids >= n_recs have no subscribers
   const uint32_t* plain;
@@ -181,7 +195,7 @@ hipError_t launch_fanout_resolve(const FanoutArgs& a, void* sort_temp, uint64_t 
 // emqx_shared_sub:dispatch/4's retry after a failed delivery (emqx_shared_sub.erl:118-130):
 // pick/6 -> do_pick/6 with FailedSubs, in request order, one wave.
 struct RepickArgs {
-  const FilterRec* recs;
+  const DevRec* recs;
   uint32_t n_recs;
   const GroupRec* groups;
   const uint32_t* members;
@@ -205,11 +219,13 @@ struct RepickArgs {
 };
 hipError_t launch_share_repick(const RepickArgs& a, hipStream_t s);
 
-// One 16-B record / one u32 word written into a device table by an incremental commit.
+// One device record (a 16-B group record, or a 32-B DevRec as value + ext) / one u32 word
+// written into a device table by an incremental commit.
 struct RecPatch {
   uint32_t index;
   uint32_t pad[3];
   uint4 value;
+  uint4 ext;
 };
 struct WordPatch {
   uint32_t index_lo, index_hi;  // element index (u64)
@@ -220,10 +236,10 @@ struct WordPatch {
 // liveness bitmap alive[] (n_alive_w).
 hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, uint32_t* alive, const WordPatch* wp,
                                  uint64_t n_plain_w, uint64_t n_member_w, uint64_t n_alive_w, GroupRec* groups,
-                                 FilterRec* recs, uint32_t* fcnt, const RecPatch* rp, uint64_t n_group_p,
+                                 DevRec* recs, uint32_t* fcnt, const RecPatch* rp, uint64_t n_group_p,
                                  uint64_t n_rec_p, hipStream_t s);
-// fcnt[i] = fo_cnt_word(recs[i]) for i < n (a full upload).
-hipError_t launch_fcnt_from_recs(const FilterRec* recs, uint64_t n, uint32_t* fcnt, hipStream_t s);
+// fcnt[i] = fo_cnt_word(recs[i].head) for i < n (a full upload).
+hipError_t launch_fcnt_from_recs(const DevRec* recs, uint64_t n, uint32_t* fcnt, hipStream_t s);
 
 // Pick-state table maintenance: rehash into a larger table; drop the keys of the given
 // publishers (sorted, unique).

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_count_kernel(FanoutArgs a) 
 #pragma unroll
     for (uint32_t u = 0; u < EU; ++u) {
       if (w[u] == 0xFFFFFFFFu) {  // saturated: the record itself (a filter with 16 M deliveries)
-        const uint4 r = *reinterpret_cast<const uint4*>(a.recs + f[u]);
+        const uint4 r = a.recs[f[u]].head;
         cs += fo_rec_plain(r) + fo_rec_groups(r);
         gl += fo_rec_groups(r);
       } else {
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(FO_THREADS, 5) void fanout_write_kernel(FanoutArgs 
 #pragma unroll
       for (uint32_t u = 0; u < EU; ++u) {
         const bool in = f[u] < a.n_recs;
-        const uint4 x = *reinterpret_cast<const uint4*>(a.recs + (in ? f[u] : 0u));
+        const uint4 x = a.recs[in ? f[u] : 0u].head;
         r[u] = in ? x : make_uint4(0, 0, 0, 0);
       }
     } else {
@@ -417,12 +417,14 @@ __global__ __launch_bounds__(FO_THREADS, 5) void fanout_write_kernel(FanoutArgs 
         const uint32_t npr = L.np[k], np = npr & ~FO_INLINE_BIT;
         const bool inl = (npr & FO_INLINE_BIT) != 0;
         shr[u] = act[u] && rr[u] >= np;
-        // the load stays unconditional (all of a round's in flight together): an inline or
-        // inactive output reads plain[0] and discards it
+        // the load stays unconditional (all of a round's in flight together): an arena output
+        // reads its plain entry, an inline one past the head its record's ext word (the line the
+        // record load just brought in), any other output plain[0], discarded
         const bool arena = act[u] && !shr[u] && !inl;
-        const uint32_t x = a.plain[arena ? L.pb[k] + rr[u] : 0u];
+        const bool ext = act[u] && !shr[u] && inl && rr[u] >= FO_INLINE_HEAD;
+        const uint32_t x = *(ext ? fo_inline_ext(a.recs, fl[u], rr[u]) : a.plain + (arena ? L.pb[k] + rr[u] : 0u));
         const uint32_t iv = rr[u] == 0 ? L.pb[k] : (rr[u] == 1 ? L.gb[k] : L.go[k]);
-        sub[u] = (act[u] && !shr[u]) ? (inl ? iv : x) : 0u;
+        sub[u] = (act[u] && !shr[u]) ? ((inl && rr[u] < FO_INLINE_HEAD) ? iv : x) : 0u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < FO_UNROLL; ++u) {
@@ -789,8 +791,9 @@ __global__ __launch_bounds__(64) void share_repick_kernel(RepickArgs a) {
     GroupRec g{0, 0, 0, 0};
     bool found = false;
     if (f < a.n_recs) {
-      const FilterRec fr = a.recs[f];
-      const uint32_t ngr = fo_rec_groups(make_uint4(fr.plain_begin, fr.n_plain, fr.group_begin, fr.n_groups));
+      const uint4 h = a.recs[f].head;
+      const FilterRec fr{h.x, h.y, h.z, h.w};
+      const uint32_t ngr = fo_rec_groups(h);
       for (uint32_t q0 = 0; q0 < ngr && !found; q0 += 64) {
         const uint32_t q = q0 + lane;
         const bool hit = q < ngr && a.groups[fr.group_begin + q].group_id == grp;
@@ -900,8 +903,9 @@ __global__ __launch_bounds__(256) void subtab_word_patch_kernel(uint32_t* plain,
   }
 }
 
-// Whole 16-B records (one dwordx4 store each): a reader sees a record old or new.
-__global__ __launch_bounds__(256) void subtab_rec_patch_kernel(GroupRec* groups, FilterRec* recs, uint32_t* fcnt,
+// Whole records (a group's one dwordx4 store, a filter's two: head and ext; no fan-out reads them
+// meanwhile, commits are ordered after the fan-outs in flight and before the next ones).
+__global__ __launch_bounds__(256) void subtab_rec_patch_kernel(GroupRec* groups, DevRec* recs, uint32_t* fcnt,
                                                                const RecPatch* rp, uint64_t n_groups,
                                                                uint64_t n_total) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n_total; i += uint64_t(gridDim.x) * 256) {
@@ -909,15 +913,16 @@ __global__ __launch_bounds__(256) void subtab_rec_patch_kernel(GroupRec* groups,
     if (i < n_groups) {
       *reinterpret_cast<uint4*>(groups + p.index) = p.value;
     } else {
-      *reinterpret_cast<uint4*>(recs + p.index) = p.value;
+      recs[p.index].head = p.value;
+      recs[p.index].ext = p.ext;
       fcnt[p.index] = fo_cnt_word(p.value);
     }
   }
 }
 
-__global__ __launch_bounds__(256) void fcnt_from_recs_kernel(const FilterRec* recs, uint64_t n, uint32_t* fcnt) {
+__global__ __launch_bounds__(256) void fcnt_from_recs_kernel(const DevRec* recs, uint64_t n, uint32_t* fcnt) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
-    fcnt[i] = fo_cnt_word(*reinterpret_cast<const uint4*>(recs + i));
+    fcnt[i] = fo_cnt_word(recs[i].head);
 }
 
 __global__ __launch_bounds__(256) void ps_rehash_kernel(const uint64_t* old_keys, const uint32_t* old_vals,
@@ -1036,7 +1041,7 @@ hipError_t launch_share_repick(const RepickArgs& a, hipStream_t s) {
 
 hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, uint32_t* alive, const WordPatch* wp,
                                  uint64_t n_plain_w, uint64_t n_member_w, uint64_t n_alive_w, GroupRec* groups,
-                                 FilterRec* recs, uint32_t* fcnt, const RecPatch* rp, uint64_t n_group_p,
+                                 DevRec* recs, uint32_t* fcnt, const RecPatch* rp, uint64_t n_group_p,
                                  uint64_t n_rec_p, hipStream_t s) {
   // words first (the lists), then the records that point at them
   const uint64_t nw = n_plain_w + n_member_w + n_alive_w;
@@ -1052,7 +1057,7 @@ hipError_t launch_subtab_patches(uint32_t* plain, uint32_t* members, uint32_t* a
   return hipGetLastError();
 }
 
-hipError_t launch_fcnt_from_recs(const FilterRec* recs, uint64_t n, uint32_t* fcnt, hipStream_t s) {
+hipError_t launch_fcnt_from_recs(const DevRec* recs, uint64_t n, uint32_t* fcnt, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(fcnt_from_recs_kernel, dim3(std::min<uint32_t>(grid_for(n, 256), 4096)), dim3(256), 0, s,
                        recs, n, fcnt);

@@ -123,7 +123,7 @@ constexpr uint64_t SMALL_MAX_N = uint64_t(SMALL_WAVES) * TILE_TOPICS;  // 1024 t
 constexpr uint32_t SMALL_FO_MAX_ENTRIES = 16384;                     // match entries the fan-out takes
 
 struct SmallFanout {
-  const uint4* recs;        // FilterRec per filter id (fanout.h; inline lists included)
+  const uint4* recs;        // DevRec per filter id (fanout.h; two uint4: head, ext with inline lists)
   uint32_t n_recs;
   const uint32_t* plain;
   const uint4* groups;      // GroupRec

@@ -1772,7 +1772,7 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
       fid[u] = e < m ? a.out_ids[e] : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (uint32_t u = 0; u < FU; ++u) rec[u] = fid[u] < f.n_recs ? f.recs[fid[u]] : make_uint4(0, 0, 0, 0);
+    for (uint32_t u = 0; u < FU; ++u) rec[u] = fid[u] < f.n_recs ? f.recs[2u * fid[u]] : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (uint32_t u = 0; u < FU; ++u) {
       const uint32_t e = r0 + u * NT + tid;
@@ -1825,9 +1825,13 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
         grp[u] = ok[u] && r[u] >= np;
         sub[u] = 0;
         g[u] = make_uint4(0, 0, 0, 0);
-        if (ok[u] && !grp[u])
-          sub[u] = (rec[u].y & FO_INLINE_BIT) ? (r[u] == 0 ? rec[u].x : (r[u] == 1 ? rec[u].z : rec[u].w))
-                                              : f.plain[rec[u].x + r[u]];
+        if (ok[u] && !grp[u]) {
+          const bool inl = (rec[u].y & FO_INLINE_BIT) != 0;
+          sub[u] = (inl && r[u] < FO_INLINE_HEAD)
+                       ? fo_inline_head(rec[u], r[u])
+                       : *(inl ? reinterpret_cast<const uint32_t*>(f.recs + 2u * fid[u] + 1u) + (r[u] - FO_INLINE_HEAD)
+                               : f.plain + rec[u].x + r[u]);
+        }
         if (grp[u]) g[u] = f.groups[rec[u].z + (r[u] - np)];  // {member_begin, n_members, slot, group_id}
       }
 #pragma unroll

@@ -81,6 +81,45 @@ def test_incremental_commits_match_oracle_every_round(F, seed):
     assert 1 in kinds[1:]  # later rounds patch in place
 
 
+@pytest.mark.parametrize("small", [1, 0])
+def test_inline_list_boundaries_every_commit(F, small):
+    """Device records hold up to FO_INLINE = 7 plain subscribers inline (fanout.h DevRec: three in
+    the head, four in ext).  Each round moves every filter's plain count to a fresh target in
+    0..11 (across the 3/4 head boundary and the 7/8 inline boundary, both ways), some filters
+    also carry a $share group (never inline); after every commit each topic's deliveries must
+    equal the oracle's, through the one-launch small path (small = 1) and the batched fan-out
+    kernels (small = 0)."""
+    rng = random.Random(7 + small)
+    filters = [b"x/%d" % i for i in range(40)] + [b"x/+", b"y/#"]
+    topics = [b"x/%d" % i for i in range(40)] + [b"y/z", b"x/none"]
+    ref = B.Broker()
+    dev = F.Broker(0, node=B.NODE, strategy="hash_clientid")
+    dev.router.engine.set_tuning("small_batch", small)
+    plain = {f: [] for f in filters}
+    for rnd in range(10):
+        for f in filters:
+            want = rng.randint(0, 11)
+            while len(plain[f]) > want:
+                s = plain[f].pop(rng.randrange(len(plain[f])))
+                ref.unsubscribe(f, s)
+                dev.unsubscribe(f, s)
+            while len(plain[f]) < want:
+                s = "s%d" % rng.randrange(500)
+                if s in plain[f]:
+                    continue
+                plain[f].append(s)
+                ref.subscribe(f, s)
+                dev.subscribe(f, s)
+            if rng.random() < 0.1:
+                s = "m%d" % rng.randrange(20)
+                ref.subscribe(f, s, b"g")
+                dev.subscribe(f, s, b"g")
+        keys = [rng.randrange(1 << 27) for _ in topics]
+        got = dev.publish_batch(topics, keys)
+        for t, k, row in zip(topics, keys, got):
+            assert canon(row) == canon(ref.publish(t, k, B.HASH_CLIENTID)), (rnd, t)
+
+
 def test_config_e_churn_equals_one_shot_build(F):
     """Config E's generator (reduced): the table built by 20 incremental commits of 4K-op churn
     (unsubscribes and resubscribes, plain and shared) gives the same deliveries per topic as a
