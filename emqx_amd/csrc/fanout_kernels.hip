@@ -401,17 +401,28 @@ __global__ __launch_bounds__(FO_THREADS, 5) void fanout_write_kernel(FanoutArgs 
     for (uint32_t j0 = 0; j0 < total; j0 += 64 * FO_UNROLL) {
       uint32_t sub[FO_UNROLL], fl[FO_UNROLL], kk[FO_UNROLL], rr[FO_UNROLL];
       bool act[FO_UNROLL], shr[FO_UNROLL];
+      // per output j, the largest k with pre[k] <= j (pre is non-decreasing, pre[0] = 0, slots
+      // past the chunk's entries hold `total`; k + step never exceeds FO_WCHUNK - 1): the
+      // FO_UNROLL searches advance step by step together, their LDS reads in flight at once
+      uint32_t jj[FO_UNROLL];
 #pragma unroll
       for (uint32_t u = 0; u < FO_UNROLL; ++u) {
-        const uint32_t j = j0 + lane + 64u * u;
-        act[u] = j < total;
-        // largest k with pre[k] <= j (pre is non-decreasing, pre[0] = 0, slots past the
-        // chunk's entries hold `total`); k + step never exceeds FO_WCHUNK - 1
-        uint32_t k = 0;
+        jj[u] = j0 + lane + 64u * u;
+        kk[u] = 0;
+      }
 #pragma unroll
-        for (uint32_t step = FO_WCHUNK / 2; step >= 1; step >>= 1)
-          if (L.pre[k + step] <= j) k += step;
-        kk[u] = k;
+      for (uint32_t step = FO_WCHUNK / 2; step >= 1; step >>= 1) {
+        uint32_t c[FO_UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < FO_UNROLL; ++u) c[u] = L.pre[kk[u] + step];
+#pragma unroll
+        for (uint32_t u = 0; u < FO_UNROLL; ++u) kk[u] += c[u] <= jj[u] ? step : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < FO_UNROLL; ++u) {
+        const uint32_t j = jj[u];
+        act[u] = j < total;
+        const uint32_t k = kk[u];
         rr[u] = j - L.pre[k];
         fl[u] = L.fid[k];
         const uint32_t npr = L.np[k], np = npr & ~FO_INLINE_BIT;
