@@ -198,7 +198,9 @@ enum FastVariant {
   FAST_K1_S512W = 10,// 4 waves/block, stack 512 (+HBM spill), 1024 word ids, K=1: 18 waves/CU
   FAST_K1_S384R = 11,// FAST_K1_S384 with the root's edge array staged in LDS (an A/B of round 5)
   FAST_K1_S384P = 12,// FAST_K1_S384 as two kernels: phase A, then the walk (an A/B of round 5)
-  FAST_NVARIANTS = 13
+  FAST_K1_S384N = 13,// FAST_K1_S384 with the next word id read after the probe loads return (the
+                     // order before round 5's hoist; kept for the A/B harness)
+  FAST_NVARIANTS = 14
 };
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);

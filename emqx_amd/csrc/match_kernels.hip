@@ -573,7 +573,10 @@ struct FastLds {
 // [0, 64) the topics' word-id ends, [64, 128) packed flags (pa_flags), [128] the tile's word
 // count, [192, 192 + words) the word ids; 2 = phase B onward, starting from that record.
 constexpr uint32_t PA_WIDS = 192;
-template <int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false, int PA = 0>
+// NH: each item's next word id is read from LDS before its probe loads are issued (in flight
+// with them), not after they return (round 5, -0.9 % on config B; FAST_K1_S384N keeps the old
+// order for the A/B harness).
+template <int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false, int PA = 0, bool NH = true>
 __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP, WID_CAP>& L, uint64_t tile,
                                           uint32_t tt, const uint4* rl = nullptr, uint32_t rsz = 0) {
   static_assert(STACK_CAP >= 4 * 64 * K && STACK_CAP % 128 == 0, "stack must hold 4 pops");
@@ -923,6 +926,11 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
     for (int k = 0; k < K; ++k)
       cpy[k] = plus_copies(tv.plus_mask, (it[k].y & IT_PLUS) || (droot[k] && (tv.root_meta & META_HAS_PLUS)),
                            isph[k] ? (hpar[k] & 15u) : (hpar[k] & 31u));
+    uint32_t nw0[K];
+    if constexpr (NH) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) nw0[k] = act[k] ? L.wids[widx[k] + 1] : WID_NONE;  // (wids[WID_CAP] is wend[0])
+    }
     probe_items<K, RL>(tv.edges, tv.plus_mask, ibase, hpar, isph, cpy, needL, wid, needP, lit, fL, pls, fP, dg[4], rl,
                        rsz, tv.root_base);
     if (DIAG) {
@@ -959,7 +967,7 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
       pP[k] = fP[k] && !leaf[k] && (pls[k].a.z & META_HAS_EDGES);
       // the topic's next word decides whether a child's literal edges can matter at all;
       // a child with nothing left to probe is not pushed
-      nwid[k] = (pL[k] || pP[k]) ? L.wids[widx[k] + 1] : WID_NONE;
+      nwid[k] = (pL[k] || pP[k]) ? (NH ? nw0[k] : L.wids[widx[k] + 1]) : WID_NONE;
       nlL[k] = nwid[k] == WID_NONE || !litf_may_contain(lit[k].a.z, lit[k].a.w, nwid[k]);
       nlP[k] = nwid[k] == WID_NONE || !litf_may_contain(pls[k].a.z, pls[k].a.w, nwid[k]);
       pL[k] = pL[k] && !(nlL[k] && !(lit[k].a.z & META_HAS_PLUS));
@@ -1038,7 +1046,7 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
 
 constexpr uint32_t ROOT_LDS_SLOTS = 256;  // FAST_K1_S384R: root arrays up to 4 KB staged in LDS
 
-template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false, int PA = 0>
+template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false, int PA = 0, bool NH = true>
 __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(MatchArgs a) {
   __shared__ FastLds<STACK_CAP, WID_CAP> lds_all[WAVES];
   __shared__ uint4 rl[RL ? ROOT_LDS_SLOTS : 1];
@@ -1060,7 +1068,7 @@ __global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(
     const uint32_t nb = gridDim.x, x = blockIdx.x & 7u, j = blockIdx.x >> 3, q = nb >> 3, r = nb & 7u;
     blk = static_cast<uint64_t>(x) * q + min(x, r) + j;
   }
-  fast_tile<STACK_CAP, WID_CAP, K, DIAG, RL, PA>(a, lds_all[wv], blk * WAVES + wv, TILE_TOPICS, rl, rsz);
+  fast_tile<STACK_CAP, WID_CAP, K, DIAG, RL, PA, NH>(a, lds_all[wv], blk * WAVES + wv, TILE_TOPICS, rl, rsz);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1863,15 +1871,15 @@ __global__ __launch_bounds__(SMALL_WAVES * 64) void small_batch_kernel(SmallArgs
 // ------------------------------------------------------------------------------------
 // Launch wrappers
 // ------------------------------------------------------------------------------------
-template <int W, int S, int WC, int K, bool RL = false>
+template <int W, int S, int WC, int K, bool RL = false, bool NH = true>
 static void launch_fast_t(const MatchArgs& a, uint64_t ntiles, hipStream_t s) {
   const uint64_t grid = (ntiles + W - 1) / W;
   if (a.diag)
-    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, true, RL>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0,
-                       s, a);
+    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, true, RL, 0, NH>), dim3(static_cast<uint32_t>(grid)),
+                       dim3(W * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, false, RL>), dim3(static_cast<uint32_t>(grid)), dim3(W * 64), 0,
-                       s, a);
+    hipLaunchKernelGGL((match_fast_kernel<W, S, WC, K, false, RL, 0, NH>), dim3(static_cast<uint32_t>(grid)),
+                       dim3(W * 64), 0, s, a);
 }
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
@@ -1890,6 +1898,7 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K1_S768W: launch_fast_t<4, 768, 1024, 1>(a, ntiles, s); break;
     case FAST_K1_S512W: launch_fast_t<4, 512, 1024, 1>(a, ntiles, s); break;
     case FAST_K1_S384R: launch_fast_t<4, 384, 640, 1, true>(a, ntiles, s); break;
+    case FAST_K1_S384N: launch_fast_t<4, 384, 640, 1, false, false>(a, ntiles, s); break;
     case FAST_K1_S384P: {  // phase A and the walk as two kernels (diagnostic runs keep one)
       if (a.diag) {
         launch_fast_t<4, 384, 640, 1>(a, ntiles, s);
