@@ -672,8 +672,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
     // reserved but unused record slots must read as empty ranges
     RT_TRY(hipMemsetAsync(w->ranges, 0, static_cast<uint64_t>(w->range_cap) * sizeof(RRange), s));
     if (r->prof_on) {
-      if (!w->prof) RT_TRY(ralloc(w->prof, 16));
-      RT_TRY(hipMemsetAsync(w->prof, 0, 16 * sizeof(uint64_t), s));
+      if (!w->prof) RT_TRY(ralloc(w->prof, 20));
+      RT_TRY(hipMemsetAsync(w->prof, 0, 20 * sizeof(uint64_t), s));
       a.prof = w->prof;
       a.ablate = r->ablate;
     }
@@ -738,7 +738,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
       std::fprintf(stderr, "RETAIN_CTRL spilled %u rounds %u spill_fail %u spill_max %u visits %u small %u big %u emitted %u\n",
                    c[RC_SPILLED], c[RC_ROUNDS], c[RC_SPILLFAIL], c[RC_SPILLMAX], visits, c[RC_RANGES], c[RC_BIG], emitted);
     if (!again && r->prof_on) {
-      uint64_t pr[16];
+      uint64_t pr[20];
       if (hipMemcpy(pr, w->prof, sizeof(pr), hipMemcpyDeviceToHost) == hipSuccess) {
         std::fprintf(stderr, "RETAIN_PROF take %llu node %llu probe %llu search %llu emitpush %llu steps %llu active %llu searching %llu\n",
                      (unsigned long long)pr[0], (unsigned long long)pr[1], (unsigned long long)pr[2],
@@ -748,6 +748,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
                      (unsigned long long)pr[8], (unsigned long long)pr[9], (unsigned long long)pr[10],
                      (unsigned long long)pr[11], (unsigned long long)pr[12], (unsigned long long)pr[13],
                      (unsigned long long)pr[14], (unsigned long long)pr[15]);
+        std::fprintf(stderr, "RETAIN_SPROF groups %llu in_ge8 %llu in_ge32 %llu\n", (unsigned long long)pr[16],
+                     (unsigned long long)pr[17], (unsigned long long)pr[18]);
       }
     }
     if (!again) {

@@ -183,7 +183,7 @@ __device__ __forceinline__ void stree_lower_bound2(const RSTree& t, uint32_t L, 
 // walk, summed into RetainArgs.prof[RPROF_SLOTS]: take (stack read + item split), node (its
 // fields + filter words), probe (edge / postings-key probes), search, emit+push; then steps,
 // active lanes, searching lanes.  Each mark waits for the wave's outstanding memory first.
-constexpr uint32_t RPROF_SLOTS = 16;  // 8..15: queue mode (retain_walk_queue_kernel)
+constexpr uint32_t RPROF_SLOTS = 20;  // 8..15: queue mode (retain_walk_queue_kernel); 16..18: search groups
 #ifdef RETAIN_PROF
 #define RPROF_MARK(slot)                                   \
   do {                                                     \
@@ -632,12 +632,14 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
     RPostKey pk{WID_NONE, 0, 0, 0};
     uint32_t bk = 0, ps = 0;
     bool nA = false, nB = false, nC = false;  // loads: node fields, edge bucket, postings key
+    uint32_t iidx = 0xFFFFFFFFu;  // (RETAIN_PROF: the lane's item in this step)
     if (act) {
       uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (pref[mid] > lane) hi = mid; else lo = mid + 1;
       }
+      iidx = lo;
       const uint32_t before = lo ? pref[lo - 1] : 0u;
       const uint4 q = itm[lo];
       lev = q.z & RITEM_LEVEL;
@@ -777,6 +779,22 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
     }
     RPROF_MARK(2);
     RPROF_ADD(7, __popcll(__ballot(skind != SK_NONE)));
+#ifdef RETAIN_PROF
+    {  // searching lanes of one item search one postings group: groups, lanes in groups of >= 8, >= 32
+      const bool srch = skind != SK_NONE && name != RNAME_ROOT;
+      uint32_t size = 0;
+      for (uint32_t d = 0; d < 64; ++d) {
+        const uint32_t v = __shfl(iidx, d, 64);
+        const uint32_t sd = __shfl(srch ? 1u : 0u, d, 64);
+        size += (srch && sd && v == iidx) ? 1u : 0u;
+      }
+      const uint32_t pi = __shfl_up(iidx, 1, 64), ps_ = __shfl_up(srch ? 1u : 0u, 1, 64);
+      const bool first = srch && (lane == 0 || !ps_ || pi != iidx);
+      RPROF_ADD(16, __popcll(__ballot(first)));
+      RPROF_ADD(17, __popcll(__ballot(srch && size >= 8)));
+      RPROF_ADD(18, __popcll(__ballot(srch && size >= 32)));
+    }
+#endif
     if (skind != SK_NONE) {
       uint32_t b = sL, e = sH;
       if (name != RNAME_ROOT) {  // the root's interval holds every rank: the whole slice
