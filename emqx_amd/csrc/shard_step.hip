@@ -104,6 +104,12 @@ __device__ __forceinline__ uint2 shard_fold(const uint32_t (&r)[2], uint32_t wor
 
 // ---- send -------------------------------------------------------------------------------
 
+// Bit k (k < 4) set iff byte k of v is zero (exact: no borrow crosses bytes).
+__device__ __forceinline__ uint32_t byte_zero4(uint32_t v) {
+  const uint32_t t = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+  return (t * 0x00204081u) >> 28;
+}
+
 // shard_topic_levels (layout.h) over the topic's bytes read as 16-B aligned windows (a window
 // holding a topic byte lies inside the batch's allocation; the batch's last window only up to
 // its end): the same summary, one load per 16 bytes instead of one per byte.
@@ -130,9 +136,14 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
       }
     }
   };
-  // (the level hashes are finished with mix32 after the loop, not per '/'; once every lane of
-  // the wave is past its third level a window is scanned without hashing)
-  auto scan16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi, auto hash) {
+  // (the level hashes are finished with mix32 after the loop, not per '/'.)  Byte by byte while
+  // some lane of the wave hashes its first three levels; after that a window is 16 bytes of
+  // byte masks: the levels are its '/' bits (the end counts as one), a wildcard level a '+' / '#'
+  // bit with a '/' (or the topic's start) before it and a '/' (or the end) after it.  carry: the
+  // byte before the window ends a level (or is the start); pend: that byte is a '+' / '#' that
+  // began its level, so a '/' first in this window makes its level a wildcard.
+  bool carry = true, pend = false;
+  auto scan16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
 #pragma unroll
     for (uint32_t b = 0; b < 16; ++b) {
       const uintptr_t q = w0 + b;
@@ -140,26 +151,46 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
       const uint32_t c = q < aend ? static_cast<uint32_t>(((b < 8 ? lo : hi) >> (8u * (b & 7u))) & 0xFFu)
                                   : static_cast<uint32_t>('/');
       if (c == '/') {
-        if (decltype(hash)::value) {
-          const uint32_t v = h ^ len;
-          h0 = nl == 0 ? v : h0;
-          h1 = nl == 1 ? v : h1;
-          h2 = nl == 2 ? v : h2;
-          h = 0x811C9DC5u;
-        }
+        const uint32_t v = h ^ len;
+        h0 = nl == 0 ? v : h0;
+        h1 = nl == 1 ? v : h1;
+        h2 = nl == 2 ? v : h2;
+        h = 0x811C9DC5u;
         wild |= len == 1 && (c0 == '+' || c0 == '#');
         ++nl;
         len = 0;
       } else {
         c0 = len == 0 ? c : c0;
-        if (decltype(hash)::value) h = (h ^ c) * 0x01000193u;
+        h = (h ^ c) * 0x01000193u;
         ++len;
       }
     }
+    carry = len == 0;
+    pend = len == 1 && (c0 == '+' || c0 == '#');
+  };
+  auto masks16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
+    const uint32_t i0 = abeg > w0 ? static_cast<uint32_t>(abeg - w0) : 0u;  // < 16
+    const uint64_t ie = aend - w0;  // the virtual '/' at the end, if < 16
+    const uint32_t real = (ie >= 16 ? 0xFFFFu : ((1u << ie) - 1u)) & ~((1u << i0) - 1u);
+    const uint32_t d[4] = {static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32), static_cast<uint32_t>(hi),
+                           static_cast<uint32_t>(hi >> 32)};
+    uint32_t sl = 0, wc = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      sl |= byte_zero4(d[k] ^ 0x2F2F2F2Fu) << (4 * k);
+      wc |= (byte_zero4(d[k] ^ 0x2B2B2B2Bu) | byte_zero4(d[k] ^ 0x23232323u)) << (4 * k);
+    }
+    const uint32_t S = (sl & real) | (ie < 16 ? 1u << ie : 0u);
+    const uint32_t P = ((S << 1) | (carry ? 1u : 0u) | (i0 ? 1u << i0 : 0u)) & 0xFFFFu;
+    const uint32_t cand = wc & real & P;
+    wild |= (cand & (S >> 1)) != 0 || (pend && (S & 1u));
+    pend = ((cand >> 15) & 1u) != 0;
+    carry = ((S >> 15) & 1u) != 0;
+    nl += static_cast<uint32_t>(__popc(S));
   };
   auto scan16w = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
-    if (__ballot(nl < 3)) scan16(w0, lo, hi, std::true_type{});
-    else scan16(w0, lo, hi, std::false_type{});
+    if (__ballot(nl < 3)) scan16(w0, lo, hi);
+    else masks16(w0, lo, hi);
   };
   for (uintptr_t w0 = abeg & ~static_cast<uintptr_t>(15); w0 <= aend; w0 += 64) {
     uint64_t l0, g0, l1, g1, l2, g2, l3, g3;

@@ -183,6 +183,15 @@ def test_device_routing_equals_host_routing():
     wl = W.config_b(n_filters=200_000, n_topics=20_000, seed=3, vocab_scale=4)
     extra = TOPICS + [b"", b"/", b"//", b"$", b"+", b"#", b"a/+/b", b"x" * 100 + b"/" + b"y" * 37,
                       b"/".join([b"l%d" % i for i in range(40)]), b"$share/g/a", b"a/b/c/"]
+    # past the third level the scanner works on 16-byte masks: wildcard levels (and near misses:
+    # '++', '+x', 'x+', '#/', '/#') at every offset against the window edges
+    for k in range(40):
+        head = b"a/b/c/" + b"x" * k
+        for tail in (b"/+", b"/#", b"/+/", b"/#/z", b"/++", b"/+x", b"/x+", b"/+/+", b"+", b"#/", b"/+x/y",
+                     b"/a+/#b"):
+            extra.append(head + tail)
+        extra.append(b"+/" * (k + 3) + b"q")
+        extra.append(b"a/b/c/" + b"/" * k + b"#")
     eb, eo = pack(extra)
     buf = np.concatenate([wl.topics[0][: int(wl.topics[1][-1])], eb])
     offs = np.concatenate([wl.topics[1].astype(np.uint64), eo[1:].astype(np.uint64) + np.uint64(wl.topics[1][-1])])
