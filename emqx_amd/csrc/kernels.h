@@ -200,7 +200,8 @@ enum FastVariant {
   FAST_K1_S384P = 12,// FAST_K1_S384 as two kernels: phase A, then the walk (an A/B of round 5)
   FAST_K1_S384N = 13,// FAST_K1_S384 with the next word id read after the probe loads return (the
                      // order before round 5's hoist; kept for the A/B harness)
-  FAST_NVARIANTS = 14
+  FAST_K1_S384W7 = 14,// 4 waves/block, stack 384, 448 word ids, K=1: 21.5 KiB per block, compiled for 7 waves/SIMD
+  FAST_NVARIANTS = 15
 };
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);

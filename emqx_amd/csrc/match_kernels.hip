@@ -1046,8 +1046,11 @@ __device__ __forceinline__ void fast_tile(const MatchArgs& a, FastLds<STACK_CAP,
 
 constexpr uint32_t ROOT_LDS_SLOTS = 256;  // FAST_K1_S384R: root arrays up to 4 KB staged in LDS
 
+// (waves per SIMD asked of the compiler: 8 for K = 1, i.e. <= 64 VGPRs, which it exceeds (73, so 6
+// waves); FAST_K1_S384W7 (448 word ids) asks for 7, which its 21.5 KiB of LDS per block allows)
+constexpr int fast_waves_hint(int K, int WC) { return K == 1 ? (WC == 448 ? 7 : 8) : 5; }
 template <int WAVES, int STACK_CAP, int WID_CAP, int K, bool DIAG, bool RL = false, int PA = 0, bool NH = true>
-__global__ __launch_bounds__(WAVES * 64, K == 1 ? 8 : 5) void match_fast_kernel(MatchArgs a) {
+__global__ __launch_bounds__(WAVES * 64, fast_waves_hint(K, WID_CAP)) void match_fast_kernel(MatchArgs a) {
   __shared__ FastLds<STACK_CAP, WID_CAP> lds_all[WAVES];
   __shared__ uint4 rl[RL ? ROOT_LDS_SLOTS : 1];
   const uint32_t wv = threadIdx.x >> 6;
@@ -1899,6 +1902,7 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K1_S512W: launch_fast_t<4, 512, 1024, 1>(a, ntiles, s); break;
     case FAST_K1_S384R: launch_fast_t<4, 384, 640, 1, true>(a, ntiles, s); break;
     case FAST_K1_S384N: launch_fast_t<4, 384, 640, 1, false, false>(a, ntiles, s); break;
+    case FAST_K1_S384W7: launch_fast_t<4, 384, 448, 1>(a, ntiles, s); break;
     case FAST_K1_S384P: {  // phase A and the walk as two kernels (diagnostic runs keep one)
       if (a.diag) {
         launch_fast_t<4, 384, 640, 1>(a, ntiles, s);
