@@ -636,6 +636,8 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   a.queue_cap = std::min<uint32_t>(w->queue_cap, r->queue_cap.load());
   a.qpiece = std::max<uint32_t>(64, r->queue_piece.load());
   a.qcheck = r->queue_check.load();
+  static const uint32_t ownmap = env_u32("EMQX_RETAIN_OWNMAP", 1);
+  a.ownmap = ownmap;
   a.qpoll_limit = r->queue_poll_limit.load();
   a.qmaxwait = r->queue_wait.load();
   a.qsleep = r->queue_sleep.load();

@@ -606,7 +606,17 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
     const uint32_t cex = wave_excl(lane < navail ? it.y : 0u, &ctot);
     pref[lane] = cex + (lane < navail ? it.y : 0u);  // inclusive
     itm[lane] = it;
+    if (a.ownmap) pref[64 + lane] = 0;
     __builtin_amdgcn_wave_barrier();
+    // ownmap: lane -> item by the items' first lanes (their exclusive prefixes; distinct among
+    // items with nodes, and the spill rounds' padding items have none) flagged in LDS with the
+    // item's index and balloted, instead of a binary search over pref per lane
+    uint64_t starts = 0;
+    if (a.ownmap) {
+      if (lane < navail && it.y && cex < 64) pref[64 + cex] = lane + 1;
+      __builtin_amdgcn_wave_barrier();
+      starts = __ballot(pref[64 + lane] != 0);
+    }
     // items fully consumed: inclusive prefix <= 64
     const uint64_t full = __ballot(lane < navail && pref[lane] <= 64);
     const uint32_t kfull = __popcll(full);  // a prefix of the lanes (counts >= 1)
@@ -635,9 +645,14 @@ __device__ __forceinline__ void walk_stack(const RetainArgs& a, uint4* ls, uint3
     uint32_t iidx = 0xFFFFFFFFu;  // (RETAIN_PROF: the lane's item in this step)
     if (act) {
       uint32_t lo = 0, hi = navail - 1;  // first j with pref[j] > lane
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pref[mid] > lane) hi = mid; else lo = mid + 1;
+      if (a.ownmap) {  // the last item start at or before this lane (lane 0 is always one)
+        const uint64_t le = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+        lo = pref[64 + 63 - static_cast<uint32_t>(__builtin_clzll(le))] - 1u;
+      } else {
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pref[mid] > lane) hi = mid; else lo = mid + 1;
+        }
       }
       iidx = lo;
       const uint32_t before = lo ? pref[lo - 1] : 0u;
@@ -899,7 +914,7 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_kernel(Reta
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * RW_WAVES + wib;
-  __shared__ uint32_t s_pref[RW_WAVES][64];
+  __shared__ uint32_t s_pref[RW_WAVES][128];  // [64, 128): the step's item-start flags
   __shared__ uint4 s_item[RW_WAVES][64];
   __shared__ uint32_t s_nlev[RW_WAVES][64];
   __shared__ uint64_t s_wb[RW_WAVES][64];
@@ -972,7 +987,7 @@ __global__ __launch_bounds__(RW_WAVES * 64, RW_OCC) void retain_walk_spill_kerne
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * RW_WAVES + wib;
-  __shared__ uint32_t s_pref[RW_WAVES][64];
+  __shared__ uint32_t s_pref[RW_WAVES][128];  // [64, 128): the step's item-start flags
   __shared__ uint4 s_item[RW_WAVES][64];
   __shared__ uint4 s_stk[RW_WAVES][RSTK];
   const uint32_t n_in = static_cast<uint32_t>(
@@ -1061,7 +1076,7 @@ __global__ __launch_bounds__(RW_WAVES * 64, QW_OCC) void retain_walk_queue_kerne
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * RW_WAVES + wib;
-  __shared__ uint32_t s_pref[RW_WAVES][64];
+  __shared__ uint32_t s_pref[RW_WAVES][128];  // [64, 128): the step's item-start flags
   __shared__ uint4 s_item[RW_WAVES][64];
   __shared__ uint32_t s_nlev[RW_WAVES][64];
   __shared__ uint64_t s_wb[RW_WAVES][64];
