@@ -33,6 +33,9 @@ SURVEY §8(e).  Two layouts:
 from __future__ import annotations
 
 import ctypes
+import os
+import sys
+import time
 from typing import Callable, List, Optional, Tuple
 
 import numpy as np
@@ -387,6 +390,36 @@ class _DeviceStep:
             pass
 
 
+# EMQX_SHARD_PROF=1 (experiments): host time between the device step's calls, averaged per
+# step and printed at exit: 0-1 send call, 1-2 host sync 1, 2-3 recv, 3-4 engine launches,
+# 4-5 answer call, 5-6 host sync 2, 6-7 merge call.
+_SHARD_PROF = os.environ.get("EMQX_SHARD_PROF") == "1"
+_PROF_SUM = [0.0] * 8
+_PROF_N = [0]
+
+
+def _host_marks():
+    t = [0.0] * 8
+
+    def mark(k):
+        t[k] = time.perf_counter()
+        if k:
+            _PROF_SUM[k] += t[k] - t[k - 1]
+        if k == 7:
+            _PROF_N[0] += 1
+    return mark
+
+
+if _SHARD_PROF:
+    import atexit
+
+    @atexit.register
+    def _print_prof():
+        n = max(_PROF_N[0], 1)
+        print("EMQX_SHARD_PROF steps %d us/step: %s" % (_PROF_N[0], " ".join(
+            "%d-%d %.1f" % (k - 1, k, 1e6 * _PROF_SUM[k] / n) for k in range(1, 8))), file=sys.stderr)
+
+
 class ShardedMatcher:
     """A filter-sharded table over the ranks of a process group (two engines per rank).
 
@@ -541,6 +574,8 @@ class ShardedMatcher:
         E = SHARD_ENGINES
         dev, G, grp = self.device, self.world, self.group
         st = self._step.h
+        mark = _host_marks() if _SHARD_PROF else (lambda k: None)
+        mark(0)
         stream = torch.cuda.current_stream(dev).cuda_stream
         P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         PA = lambda ts: (ctypes.c_void_p * E)(*[None if t is None else t.data_ptr() for t in ts])  # noqa: E731
@@ -561,6 +596,7 @@ class ShardedMatcher:
         _lib.check(L.emqx_shard_step_send(st, P(tb), P(to), n, P(send), send.numel(),
                                           ctypes.c_void_p(dmeta) if G == 1 else P(meta), S), "emqx_shard_step_send")
         cur = torch.cuda.current_stream(dev)
+        mark(1)
         if G == 1:
             cur.synchronize()  # host sync 1
             mo = mi = hmeta[: MW * G].numpy().reshape(G, MW).copy()
@@ -569,6 +605,7 @@ class ShardedMatcher:
             _a2a(meta_in, meta, [MW] * G, [MW] * G, grp)
             mh = self._to_host(meta, meta_in).reshape(2, -1)  # host sync 1
             mo, mi = mh[0].reshape(G, MW), np.ascontiguousarray(mh[1].reshape(G, MW))
+        mark(2)
         if (mo[:, 0] < 0).any() or (mi[:, 0] < 0).any():
             raise RuntimeError("emqx_shard_step_send: chunks over the send buffer")
         out_b, in_b = mo[:, 0].tolist(), mi[:, 0].tolist()
@@ -584,6 +621,7 @@ class ShardedMatcher:
         qb = PA(qbytes)
         _lib.check(L.emqx_shard_step_recv(st, (ctypes.c_void_p * G)(*chunks), mi.ctypes.data, qb, PA(qoff), S),
                    "emqx_shard_step_recv")
+        mark(3)
         qaddr = [qb[e] for e in range(E)]
         self.last_local_topics = sum(NQ)
         self.last_slot_topics = NQ
@@ -614,6 +652,7 @@ class ShardedMatcher:
         for es in used:
             if es is not cur:
                 cur.wait_stream(es)
+        mark(4)
         # 3. answers, one chunk per source; a call that did not complete is redone before the
         # exchange (every rank learns every rank's flag from the size exchange)
         redo = False
@@ -627,6 +666,7 @@ class ShardedMatcher:
             _lib.check(L.emqx_shard_step_answer(st, PA([o[0] for o in outs]), PA([o[1] for o in outs]), sp, self.rank,
                                                 P(ans), ctypes.c_void_p(dans) if G == 1 else P(ans_meta), S),
                        "emqx_shard_step_answer")
+            mark(5)
             if G == 1:
                 cur.synchronize()  # host sync 2
                 am = ai = hans[: 3 * G].numpy().reshape(G, 3).copy()
@@ -635,6 +675,7 @@ class ShardedMatcher:
                 _a2a(ans_in, ans_meta, [3] * G, [3] * G, grp)
                 h = self._to_host(ans_meta, ans_in)  # host sync 2
                 am, ai = h[: 3 * G].reshape(G, 3), np.ascontiguousarray(h[3 * G: 6 * G]).reshape(G, 3)
+            mark(6)
             sm = hsumm[: 8 * E].numpy().reshape(E, 8).copy()
             if not redo:
                 for e in range(E):  # learn the id capacities from this call's totals
@@ -657,9 +698,10 @@ class ShardedMatcher:
         ai = np.ascontiguousarray(ai, dtype=np.int64)
         _lib.check(L.emqx_shard_step_merge(st, (ctypes.c_void_p * G)(*back), ai.ctypes.data, P(out_off), P(out_ids),
                                            S), "emqx_shard_step_merge")
+        mark(7)
         return out_off, out_ids[:total]
 
-    def _match_all_tensors(self, topics: Tuple[torch.Tensor, torch.Tensor]):
+    def _match_all_tensors(self, topics: Tuple[torch.Tensor, torch.Tensor]):  # noqa: C901
         """match_all with torch tensor ops (an injected match_fn: the distribution logic on CPU
         over gloo in the tests)."""
         dev, G, grp = self.device, self.world, self.group
