@@ -210,11 +210,11 @@ def _exchange_chunks(send: torch.Tensor, out_sz: List[int], in_sz: List[int], re
     device tensors through host copies) has no list all-to-all: all_to_all_single, the own chunk
     copied along and not read."""
     G = len(out_sz)
-    out_off = np.concatenate([[0], np.cumsum(out_sz)]).astype(np.int64)
-    es = send.element_size()
     base = send.data_ptr()
     if G == 1:
         return [base]
+    out_off = np.concatenate([[0], np.cumsum(out_sz)]).astype(np.int64)
+    es = send.element_size()
     if dist.get_backend(group) == "gloo":
         in_off = np.concatenate([[0], np.cumsum(in_sz)]).astype(np.int64)
         recv = recv_buf(int(in_off[-1]))
@@ -597,30 +597,36 @@ class ShardedMatcher:
                                           ctypes.c_void_p(dmeta) if G == 1 else P(meta), S), "emqx_shard_step_send")
         cur = torch.cuda.current_stream(dev)
         mark(1)
+        # (the split sizes as Python ints: this bookkeeping sits between the host sync and the
+        # next launch, on the step's critical path, where numpy calls on a few words cost more
+        # than the arithmetic)
         if G == 1:
             cur.synchronize()  # host sync 1
-            mo = mi = hmeta[: MW * G].numpy().reshape(G, MW).copy()
+            mo_l = mi_l = hmeta[: MW * G].tolist()
+            mi_ptr = hmeta.data_ptr()  # (recv reads the words on the host, during the call)
         else:
             meta_in = torch.empty_like(meta)
             _a2a(meta_in, meta, [MW] * G, [MW] * G, grp)
             mh = self._to_host(meta, meta_in).reshape(2, -1)  # host sync 1
-            mo, mi = mh[0].reshape(G, MW), np.ascontiguousarray(mh[1].reshape(G, MW))
+            mi = np.ascontiguousarray(mh[1])
+            mo_l, mi_l, mi_ptr = mh[0].tolist(), mi.tolist(), mi.ctypes.data
         mark(2)
-        if (mo[:, 0] < 0).any() or (mi[:, 0] < 0).any():
+        out_b = mo_l[0::MW]
+        in_b = mi_l[0::MW]
+        if min(out_b) < 0 or min(in_b) < 0:
             raise RuntimeError("emqx_shard_step_send: chunks over the send buffer")
-        out_b, in_b = mo[:, 0].tolist(), mi[:, 0].tolist()
         chunks = _exchange_chunks(send, out_b, in_b, lambda k: self._buf("recv", k + 16, torch.uint8), grp,
                                   self.rank)
-        NQ = [int(mi[:, 1 + e].sum()) for e in range(E)]
+        NQ = [sum(mi_l[1 + e::MW]) for e in range(E)]
         # a slot fed by one source only is matched in place in that source's chunk (recv
         # replaces its byte buffer's address); the others are gathered into these buffers
-        one = [int(np.count_nonzero(mi[:, 1 + e])) <= 1 for e in range(E)]
-        qbytes = [None if one[e] else self._buf(f"q_bytes{e}", int(mi[:, 1 + E + e].sum()) + 16, torch.uint8)
+        one = [sum(1 for x in mi_l[1 + e::MW] if x) <= 1 for e in range(E)]
+        qbytes = [None if one[e] else self._buf(f"q_bytes{e}", sum(mi_l[1 + E + e::MW]) + 16, torch.uint8)
                   for e in range(E)]
         qoff = [self._buf(f"q_off{e}", NQ[e] + 1, torch.int64) for e in range(E)]
         qb = PA(qbytes)
-        _lib.check(L.emqx_shard_step_recv(st, (ctypes.c_void_p * G)(*chunks), mi.ctypes.data, qb, PA(qoff), S),
-                   "emqx_shard_step_recv")
+        _lib.check(L.emqx_shard_step_recv(st, (ctypes.c_void_p * G)(*chunks), ctypes.c_void_p(mi_ptr), qb, PA(qoff),
+                                          S), "emqx_shard_step_recv")
         mark(3)
         qaddr = [qb[e] for e in range(E)]
         self.last_local_topics = sum(NQ)
@@ -669,35 +675,36 @@ class ShardedMatcher:
             mark(5)
             if G == 1:
                 cur.synchronize()  # host sync 2
-                am = ai = hans[: 3 * G].numpy().reshape(G, 3).copy()
+                am_l = ai_l = hans[: 3 * G].tolist()
+                ai_ptr = hans.data_ptr()  # (merge reads the words on the host, during the call)
             else:
                 ans_in = torch.empty_like(ans_meta)
                 _a2a(ans_in, ans_meta, [3] * G, [3] * G, grp)
                 h = self._to_host(ans_meta, ans_in)  # host sync 2
-                am, ai = h[: 3 * G].reshape(G, 3), np.ascontiguousarray(h[3 * G: 6 * G]).reshape(G, 3)
+                ai = np.ascontiguousarray(h[3 * G: 6 * G], dtype=np.int64)
+                am_l, ai_l, ai_ptr = h[: 3 * G].tolist(), ai.tolist(), ai.ctypes.data
             mark(6)
-            sm = hsumm[: 8 * E].numpy().reshape(E, 8).copy()
+            sm = hsumm[: 8 * E].tolist()
             if not redo:
                 for e in range(E):  # learn the id capacities from this call's totals
-                    if NQ[e] and sm[e, 0] == 0:
-                        self._caps[e] = max(self._caps[e], int(sm[e, 1] * 1.25) + 4096)
-            if not ai[:, 1].any():
+                    if NQ[e] and sm[8 * e] == 0:
+                        self._caps[e] = max(self._caps[e], int(sm[8 * e + 1] * 1.25) + 4096)
+            if not any(ai_l[1::3]):
                 break
-            if am[0, 1]:  # this rank's call did not complete: redo it synchronously, exact size
+            if am_l[1]:  # this rank's call did not complete: redo it synchronously, exact size
                 for e, (eb, eo, ne) in enumerate(batches):
-                    if ne and sm[e, 0]:
+                    if ne and sm[8 * e]:
                         outs[e] = list(self._engine_csr(e, eb, eo[: ne + 1], n=ne))
                         self._caps[e] = max(self._caps[e], int(outs[e][1].numel() * 1.25) + 4096)
             redo = True
         # 4. answers back to their sources, merged per topic in batch order
-        out_w, in_w = am[:, 0].tolist(), ai[:, 0].tolist()
+        out_w, in_w = am_l[0::3], ai_l[0::3]
         back = _exchange_chunks(ans, out_w, in_w, lambda k: self._buf("back", k + 16, torch.int32), grp, self.rank)
-        total = int(ai[:, 2].sum())
+        total = sum(ai_l[2::3])
         out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         out_ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
-        ai = np.ascontiguousarray(ai, dtype=np.int64)
-        _lib.check(L.emqx_shard_step_merge(st, (ctypes.c_void_p * G)(*back), ai.ctypes.data, P(out_off), P(out_ids),
-                                           S), "emqx_shard_step_merge")
+        _lib.check(L.emqx_shard_step_merge(st, (ctypes.c_void_p * G)(*back), ctypes.c_void_p(ai_ptr), P(out_off),
+                                           P(out_ids), S), "emqx_shard_step_merge")
         mark(7)
         return out_off, out_ids[:total]
 
