@@ -233,7 +233,7 @@ struct emqx_retain {
   // tile 0: the balance mode's default
   std::atomic<uint32_t> tile{0}, step_budget{STEP_BUDGET}, spill_budget{SPILL_BUDGET}, spill_decay{0}, spill_per_wave{SPILL_PER_WAVE}, spill_rounds{SPILL_ROUNDS}, search{RSEARCH_STREE},
       walk_waves{MAX_WAVES}, spill_waves{SPILL_WAVES}, spill_cap{SPILL_CAP}, balance{BALANCE_QUEUE},
-      queue_piece{QUEUE_PIECE}, queue_check{QUEUE_CHECK}, queue_cap{QUEUE_CAP}, queue_wait{QUEUE_MAX_WAIT},
+      lane_map{1}, queue_piece{QUEUE_PIECE}, queue_check{QUEUE_CHECK}, queue_cap{QUEUE_CAP}, queue_wait{QUEUE_MAX_WAIT},
       queue_sleep{QUEUE_SLEEP}, queue_shards{QUEUE_SHARDS}, queue_roam{QUEUE_ROAM}, queue_poll_limit{QUEUE_POLL_LIMIT};
 };
 
@@ -636,8 +636,7 @@ int run_match(emqx_retain* r, RWork* w, const RSnapshot& sn, const uint8_t* d_fb
   a.queue_cap = std::min<uint32_t>(w->queue_cap, r->queue_cap.load());
   a.qpiece = std::max<uint32_t>(64, r->queue_piece.load());
   a.qcheck = r->queue_check.load();
-  static const uint32_t ownmap = env_u32("EMQX_RETAIN_OWNMAP", 1);
-  a.ownmap = ownmap;
+  a.ownmap = r->lane_map.load();
   a.qpoll_limit = r->queue_poll_limit.load();
   a.qmaxwait = r->queue_wait.load();
   a.qsleep = r->queue_sleep.load();
@@ -797,7 +796,8 @@ int emqx_retain_create(int32_t device, emqx_retain** out) {
   r->balance = std::min<uint32_t>(env_u32("EMQX_RETAIN_BALANCE", BALANCE_QUEUE), BALANCE_QUEUE);
   {
     const uint32_t qc = env_u32("EMQX_RETAIN_QUEUE_CHECK", QUEUE_CHECK);
-    r->queue_check = qc >= 1 && qc <= 1024 && (qc & (qc - 1)) == 0 ? qc : QUEUE_CHECK;
+    r->lane_map = env_u32("EMQX_RETAIN_LANE_MAP", 1) ? 1u : 0u;
+  r->queue_check = qc >= 1 && qc <= 1024 && (qc & (qc - 1)) == 0 ? qc : QUEUE_CHECK;
   }
   r->queue_piece = std::max<uint32_t>(64, env_u32("EMQX_RETAIN_QUEUE_PIECE", QUEUE_PIECE));
   r->queue_wait = std::max<uint32_t>(1, env_u32("EMQX_RETAIN_QUEUE_WAIT", QUEUE_MAX_WAIT));
@@ -1047,6 +1047,9 @@ int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value) {
   } else if (std::strcmp(key, "queue_piece") == 0) {
     if (v < 64 || v > (1u << 20)) return EMQX_EINVAL;
     r->queue_piece = v;
+  } else if (std::strcmp(key, "lane_map") == 0) {
+    if (v < 0 || v > 1) return EMQX_EINVAL;
+    r->lane_map = static_cast<uint32_t>(v);
   } else if (std::strcmp(key, "queue_check") == 0) {
     if (v < 1 || v > 1024 || (v & (v - 1)) != 0) return EMQX_EINVAL;
     r->queue_check = v;

@@ -200,7 +200,7 @@ struct RetainArgs {
   uint32_t qpiece;         // nodes per shared piece (queue mode)
   uint32_t qcheck;         // steps between a busy wave's looks at the waiting count (power of 2)
   uint32_t ownmap;         // 1: a step's lane -> item map from a ballot of item starts (else a binary
-                           // search of the prefix per lane; EMQX_RETAIN_OWNMAP A/B)
+                           // search of the prefix per lane; tuning key "lane_map")
   uint32_t qpoll_limit;    // polls before a waiting wave gives up (RC_QABORT; a safety valve)
   uint32_t qmaxwait;       // waves waiting on tickets of one shard at most (more return)
   uint32_t qsleep;         // s_sleep(16) (1024 clocks) per poll of a waiting wave

@@ -120,8 +120,10 @@ int emqx_retain_match_batch_device(emqx_retain* r, const uint8_t* d_filter_bytes
  * busy waves share the bottom of their stacks, no rounds; 0: the spill rounds above),
  * "queue_piece" (nodes per shared piece, 64..1M, default 256), "queue_check" (steps between a
  * busy wave's looks at the waiting count, a power of 2 up to 1024, default 8), "queue_cap"
- * (queue slots a call may use, 64..4M, default 4M; tests).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
- * _SEARCH / _WALK_WAVES / _SPILL_WAVES / _BALANCE / _QUEUE_PIECE / _QUEUE_CHECK give the initial values at create.  EMQX_ENOTFOUND for unknown keys. */
+ * (queue slots a call may use, 64..4M, default 4M; tests), "lane_map" (1: a walk step maps
+ * lanes to items by a ballot of the items' first lanes, default; 0: a binary search per lane,
+ * the round-5 A/B).  EMQX_RETAIN_TILE / _STEP_BUDGET / _SPILL_BUDGET / _SPILL_PER_WAVE / _SPILL_ROUNDS /
+ * _SEARCH / _WALK_WAVES / _SPILL_WAVES / _BALANCE / _QUEUE_PIECE / _QUEUE_CHECK / _LANE_MAP give the initial values at create.  EMQX_ENOTFOUND for unknown keys. */
 int emqx_retain_set_tuning(emqx_retain* r, const char* key, int64_t value);
 int emqx_retain_stats_get(emqx_retain* r, emqx_retain_stats* out);
 

@@ -276,6 +276,34 @@ def _sharing_case(seed):
     return names, expiry, filters
 
 
+@pytest.mark.parametrize("balance", [1, 0])
+def test_lane_map_modes_agree(mod, balance):
+    """A walk step maps its lanes to its items by a ballot of the items' first lanes (tuning
+    "lane_map" 1, the default) or by a binary search of the items' prefixes per lane (0, the
+    round-5 A/B): same results, visits and ranges, in the work-sharing walk and in the spill
+    rounds (whose padding items have no nodes and flag no lane)."""
+    names, expiry, filters = _sharing_case(4242 + balance)
+    idx = mod.RetainIndex()
+    idx.store(names, expiry)
+    idx.commit()
+    tt = RR.TokenTrie(names, expiry)
+    idx.set_tuning("balance", balance)
+    if not balance:
+        idx.set_tuning("step_budget", 2)
+        idx.set_tuning("spill_cap", 64)
+    out = {}
+    for lm in (0, 1):
+        idx.set_tuning("lane_map", lm)
+        got = idx.match(filters, 100)
+        st = idx.stats()
+        out[lm] = (got, st["last_visits"], st["last_ranges"])
+    assert out[0] == out[1]
+    for f, g in zip(filters, out[1][0]):
+        assert g == tt.dispatch(f, 100), f
+    with pytest.raises(Exception):
+        idx.set_tuning("lane_map", 2)
+
+
 @pytest.mark.parametrize("piece,check,shards,roam", [(64, 1, 1, 0), (64, 2, 4, 3), (256, 8, 64, 8), (1024, 64, 16, 15),
                                                      (512, 4, 64, 0)])
 def test_queue_sharing_parity(mod, piece, check, shards, roam):
