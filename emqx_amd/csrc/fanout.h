@@ -54,8 +54,8 @@ __host__ __device__ inline uint32_t fo_rec_groups(uint4 r) { return (r.y & FO_IN
 
 // The count pass's dense per-filter word (4 B, maintained on the device from each record it
 // writes): deliveries (n_plain + n_groups) in bits 0..23 and $share groups in bits 24..31, each
-// saturated; a saturated word sends the count pass to the 16-B record.  Ten per 64-B line where
-// the records fit four, so the count pass's random reads mostly hit in L2.
+// saturated; a saturated word sends the count pass to the record's head.  Sixteen per 64-B line where
+// the device records fit two, so the count pass's random reads mostly hit in L2.
 constexpr uint32_t FO_CNT_DELIV_MAX = 0xFFFFFFu, FO_CNT_GROUPS_MAX = 0xFFu;
 __host__ __device__ inline uint32_t fo_cnt_word(uint4 r) {
   const uint32_t d = fo_rec_plain(r) + fo_rec_groups(r), g = fo_rec_groups(r);
