@@ -548,7 +548,10 @@ FastVariant pick_variant(const emqx_engine* e, const Snapshot& snap) {
   const int fv = e->forced_variant.load();
   const int forced = fv >= 0 ? fv : env_forced;
   if (forced >= 0 && forced < FAST_NVARIANTS) return static_cast<FastVariant>(forced);
-  return snap.max_depth > 12 ? FAST_K1_S512W : FAST_K1_S384;
+  // shallow tables: FAST_K1_S384's walk in one-wave workgroups (round 5: the waves share
+  // nothing, and single-wave groups let the dispatcher refill a CU wave by wave; config B 0.5591
+  // against 0.5668 ms for 4-wave groups, profiles/r5_b1_ab_block_waves.json)
+  return snap.max_depth > 12 ? FAST_K1_S512W : FAST_K1_S384B1;
 }
 
 // Enqueue one match call on stream s (no host synchronisation): memset of the control
