@@ -200,7 +200,11 @@ constexpr uint32_t RPROF_SLOTS = 20;  // 8..15: queue mode (retain_walk_queue_ke
 #define RPROF_NOW() 0ull
 #endif
 
-constexpr int RW_WAVES = 4;
+#ifndef RW_WAVES_V
+#define RW_WAVES_V 1  // waves per block of the walk kernels: their waves share nothing, so one-wave blocks
+                      // (round 5: R call 1.045-1.054 against 1.051-1.059 ms for 4, profiles/r5_rw1_ab/)
+#endif
+constexpr int RW_WAVES = RW_WAVES_V;
 #ifndef RW_OCC
 #define RW_OCC 1  // waves per SIMD the walk kernels are compiled for (1: the compiler's choice)
 #endif
