@@ -203,7 +203,8 @@ enum FastVariant {
   FAST_K1_S384W7 = 14,// 4 waves/block, stack 384, 448 word ids, K=1: 21.5 KiB per block, compiled for 7 waves/SIMD
   FAST_K1_S384B2 = 15,// FAST_K1_S384 in blocks of 2 waves (finer dispatch at the grid's tail; an A/B)
   FAST_K1_S384B1 = 16,// ... in blocks of one wave (the default for tables up to 12 levels deep)
-  FAST_NVARIANTS = 17
+  FAST_K1_S512WB1 = 17,// FAST_K1_S512W in blocks of one wave
+  FAST_NVARIANTS = 18
 };
 
 hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s);

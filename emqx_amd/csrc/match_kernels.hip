@@ -1905,6 +1905,7 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
     case FAST_K1_S384W7: launch_fast_t<4, 384, 448, 1>(a, ntiles, s); break;
     case FAST_K1_S384B2: launch_fast_t<2, 384, 640, 1>(a, ntiles, s); break;
     case FAST_K1_S384B1: launch_fast_t<1, 384, 640, 1>(a, ntiles, s); break;
+    case FAST_K1_S512WB1: launch_fast_t<1, 512, 1024, 1>(a, ntiles, s); break;
     case FAST_K1_S384P: {  // phase A and the walk as two kernels (diagnostic runs keep one)
       if (a.diag) {
         launch_fast_t<4, 384, 640, 1>(a, ntiles, s);

@@ -13,7 +13,7 @@ from tests.test_oracle_fuzz import rand_filter, rand_topic
 
 pytestmark = pytest.mark.gpu
 
-N_VARIANTS = 17
+N_VARIANTS = 18
 
 
 @pytest.fixture(scope="module")
