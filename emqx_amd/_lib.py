@@ -39,6 +39,7 @@ EXPORTS = (
     "emqx_batcher_submit_many", "emqx_batcher_try_submit", "emqx_strerror", "emqx_version",
     "emqx_subtab_create", "emqx_subtab_destroy", "emqx_subtab_add", "emqx_subtab_remove", "emqx_subtab_commit",
     "emqx_subtab_commit_wait", "emqx_subtab_stats", "emqx_subtab_commit_stats", "emqx_subtab_forget_publishers", "emqx_subtab_set_alive",
+    "emqx_subtab_set_tuning",
     "emqx_share_repick", "emqx_coalescer_create", "emqx_coalescer_insert_filters", "emqx_coalescer_delete_filters",
     "emqx_coalescer_subscribe", "emqx_coalescer_subscribe_many", "emqx_coalescer_set_alive", "emqx_coalescer_flush", "emqx_coalescer_destroy",
     "emqx_coalescer_stats",
@@ -198,6 +199,7 @@ def lib():
         "emqx_subtab_remove": (i32, [vp, vp, vp, vp, u64]),
         "emqx_subtab_commit": (i32, [vp]),
         "emqx_subtab_commit_wait": (i32, [vp]),
+        "emqx_subtab_set_tuning": (i32, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "emqx_subtab_stats": (i32, [vp, vp]),
         "emqx_subtab_commit_stats": (i32, [vp, vp, u32]),
         "emqx_subtab_forget_publishers": (i32, [vp, vp, u64]),

@@ -260,34 +260,10 @@ int full_commit(emqx_engine* e) {
   HIP_TRY(dalloc(dt->fids, 2 * dt->cap_slots));
   HIP_TRY(dalloc(dt->vocab, dt->n_vocab));
   HIP_TRY(dalloc(dt->arena, dt->cap_arena));
-  if (getenv("EMQX_TABLE_ZERO")) {  // (diagnostic: the allocations' previous contents cleared)
-    HIP_TRY(hipMemset(dt->edges, 0, dt->cap_slots * sizeof(EdgeSlot)));
-    HIP_TRY(hipMemset(dt->fids, 0, 2 * dt->cap_slots * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(dt->vocab, 0, dt->n_vocab * sizeof(VocabSlot)));
-    HIP_TRY(hipMemset(dt->arena, 0, dt->cap_arena));
-  }
-  if (getenv("EMQX_UPLOAD_KERNEL")) {  // (diagnostic: uploads by a kernel through L2, from pinned staging)
-    auto kup = [&](void* dst, const void* src, uint64_t bytes) -> hipError_t {
-      if (!bytes) return hipSuccess;
-      void* h = nullptr;
-      hipError_t r = hipHostMalloc(&h, bytes, hipHostMallocDefault);
-      if (r != hipSuccess) return r;
-      std::memcpy(h, src, bytes);
-      r = launch_copy_in(h, dst, bytes, nullptr);
-      if (r == hipSuccess) r = hipStreamSynchronize(nullptr);
-      (void)hipHostFree(h);
-      return r;
-    };
-    HIP_TRY(kup(dt->edges, ht.edges.data(), n_slots * sizeof(EdgeSlot)));
-    HIP_TRY(kup(dt->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t)));
-    HIP_TRY(kup(dt->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot)));
-    HIP_TRY(kup(dt->arena, ht.arena.data(), ht.arena.size()));
-  } else {
   HIP_TRY(hipMemcpy(dt->edges, ht.edges.data(), n_slots * sizeof(EdgeSlot), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->fids, ht.fids.data(), ht.fids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->vocab, ht.vocab.data(), ht.vocab.size() * sizeof(VocabSlot), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(dt->arena, ht.arena.data(), ht.arena.size(), hipMemcpyHostToDevice));
-  }
   // a copy from pageable memory may return before its DMA lands, and the match streams do not
   // follow the null stream: the tables are on the device before the snapshot is published
   HIP_TRY(hipStreamSynchronize(nullptr));

@@ -271,6 +271,9 @@ struct emqx_subtab {
   std::mutex mu;   // serialises mutations, the host half of commits, and fan-out enqueues
   std::mutex cmu;  // one commit at a time (held while it drains the previous device half, which s->mu is not)
   uint8_t* h_stage = nullptr;  // pinned staging of a commit's uploads (one commit at a time)
+  // fault injection (emqx_subtab_set_tuning, tests): the next k drains report a device error,
+  // the next k full commits throw std::bad_alloc
+  uint32_t inject_drain_error = 0, inject_bad_alloc = 0;
   uint64_t stage_cap = 0;
   // ---- host store, and the image of every device array ----
   std::vector<FilterRec> recs;                // per filter id
@@ -735,6 +738,10 @@ void compact_image(emqx_subtab* s) {
 
 // Full commit: the compacted image uploaded into fresh device arrays.
 int full_commit(emqx_subtab* s) {
+  if (s->inject_bad_alloc) {
+    --s->inject_bad_alloc;
+    throw std::bad_alloc();
+  }
   compact_image(s);
   // the old plain positions are indices into the lists, which compaction keeps: nothing to redo
   DevArr<DevRec> recs;
@@ -1084,6 +1091,10 @@ int commit_enqueue(emqx_subtab* s, std::vector<void*>& retired) {
 int commit_drain(emqx_subtab* s) {
   int rc = EMQX_OK;
   if (s->commit_inflight && hipEventSynchronize(s->commit_ev) != hipSuccess) rc = EMQX_EDEVICE;
+  if (s->inject_drain_error) {
+    --s->inject_drain_error;
+    rc = EMQX_EDEVICE;
+  }
   s->commit_inflight = false;
   for (void* p : s->retired_prev) (void)hipFree(p);
   s->retired_prev.clear();
@@ -1522,7 +1533,10 @@ int pb_alloc(emqx_pub_batch* b, uint64_t cap_topics, uint64_t cap_bytes, uint64_
 
 // After the match ids of the batch are in HBM: fan-out, the delivery CSR into the pinned
 // outputs, both summaries into pinned memory (s->mu is taken here).
-int pb_enqueue_fanout(emqx_pub_batch* b, uint64_t m_cap, const uint64_t* msum) {
+// fanout_words_only: copy back only the fan-out summary (the one-launch path's fallback, whose
+// match summary the small kernel already wrote into the mapped h_sums: d_msum's match words
+// are an older call's).
+int pb_enqueue_fanout(emqx_pub_batch* b, uint64_t m_cap, const uint64_t* msum, bool fanout_words_only = false) {
   auto* p = static_cast<PubBatchPriv*>(b->priv);
   emqx_subtab* s = p->s;
   uint64_t* fsum = p->d_msum + PB_MSUM_WORDS;
@@ -1535,7 +1549,8 @@ int pb_enqueue_fanout(emqx_pub_batch* b, uint64_t m_cap, const uint64_t* msum) {
   }
   FO_TRY(launch_fanout_to_host(p->d_ooff, b->n, p->d_osubs, p->d_ofil, fsum, cap, mapped(b->out_offsets),
                                mapped(b->out_subs), mapped(b->out_filters), p->stream));
-  FO_TRY(hipMemcpyAsync(p->h_sums, p->d_msum, (PB_MSUM_WORDS + FO_SUM_WORDS) * sizeof(uint64_t),
+  const uint64_t skip = fanout_words_only ? PB_MSUM_WORDS : 0;
+  FO_TRY(hipMemcpyAsync(p->h_sums + skip, p->d_msum + skip, (PB_MSUM_WORDS + FO_SUM_WORDS - skip) * sizeof(uint64_t),
                         hipMemcpyDeviceToHost, p->stream));
   return EMQX_OK;
 }
@@ -1653,7 +1668,7 @@ int pb_wait(emqx_pub_batch* b) {
     p->mids_per_topic = std::max<uint64_t>(4, (ms[1] + ms[1] / 4) / b->n + 1);
   }
   if (fs[FO_SUM_FLAGS] & FO_SUM_F_SMALL) {  // the one-launch path's fan-out did not fit: batched kernels
-    int rc = pb_enqueue_fanout(b, p->cap_mids, nullptr);
+    int rc = pb_enqueue_fanout(b, p->cap_mids, nullptr, true);
     if (rc != EMQX_OK) return rc;
     FO_TRY(hipStreamSynchronize(p->stream));
   }
@@ -1887,18 +1902,35 @@ int emqx_subtab_commit(emqx_subtab* s) {
 
 int emqx_subtab_commit_wait(emqx_subtab* s) {
   if (!s) return EMQX_EINVAL;
+  // (guarded: the rebuild below allocates host vectors of every record, the path most likely
+  // to throw, and the coalescer calls this on every batch)
+  return subtab_guarded(s, [&] {
+    std::lock_guard<std::mutex> g(s->cmu);
+    if (hipSetDevice(s->device) != hipSuccess) return static_cast<int>(EMQX_EDEVICE);
+    int rc = commit_drain(s);
+    if (rc == EMQX_OK) return static_cast<int>(EMQX_OK);
+    // the device half failed: its tables are in an unknown state, so they are rebuilt from the
+    // host image now (a full commit), and the error goes to the callers of the failed commit
+    {
+      std::lock_guard<std::mutex> m(s->mu);
+      s->need_full = true;
+    }
+    if (commit_now(s) == EMQX_OK) (void)commit_drain(s);
+    return rc;
+  });
+}
+
+int emqx_subtab_set_tuning(emqx_subtab* s, const char* key, int64_t value) {
+  if (!s || !key || value < 0) return EMQX_EINVAL;
   std::lock_guard<std::mutex> g(s->cmu);
-  if (hipSetDevice(s->device) != hipSuccess) return EMQX_EDEVICE;
-  int rc = commit_drain(s);
-  if (rc == EMQX_OK) return EMQX_OK;
-  // the device half failed: its tables are in an unknown state, so they are rebuilt from the
-  // host image now (a full commit), and the error goes to the callers of the failed commit
-  {
-    std::lock_guard<std::mutex> m(s->mu);
-    s->need_full = true;
+  if (!std::strcmp(key, "inject_drain_error")) {
+    s->inject_drain_error = static_cast<uint32_t>(value);
+  } else if (!std::strcmp(key, "inject_bad_alloc")) {
+    s->inject_bad_alloc = static_cast<uint32_t>(value);
+  } else {
+    return EMQX_ENOTFOUND;
   }
-  if (commit_now(s) == EMQX_OK) (void)commit_drain(s);
-  return rc;
+  return EMQX_OK;
 }
 
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4) {
@@ -1908,7 +1940,7 @@ int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4) {
   counts4[1] = s->n_members;
   counts4[2] = s->n_live_groups;
   counts4[3] = s->d_recs.cap * sizeof(DevRec) + s->d_plain.cap * 4 + s->d_groups.cap * sizeof(GroupRec) +
-               s->d_members.cap * 4 + s->ps_cap * 12;
+               s->d_members.cap * 4 + s->ps_cap * 12 + s->d_fcnt.cap * sizeof(uint32_t);
   return EMQX_OK;
 }
 

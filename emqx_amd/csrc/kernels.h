@@ -164,8 +164,6 @@ enum : uint32_t {
   SMALL_CLK_FO_PASS1, SMALL_CLK_FO_PASS2, SMALL_CLK_LAUNCHES, SMALL_CLK_WORDS = 10
 };
 hipError_t launch_small_batch(const SmallArgs& a, hipStream_t s);
-// bytes from host-mapped (pinned) h_src into device memory by a kernel (through L2)
-hipError_t launch_copy_in(const void* h_src, void* d_dst, uint64_t bytes, hipStream_t s);
 }  // namespace emqx
 struct emqx_engine;
 namespace emqx {

@@ -1921,25 +1921,6 @@ hipError_t launch_match_fast(const MatchArgs& a, FastVariant v, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Uploads through the GPU's own caches: a kernel reads pinned host memory and stores into HBM
-// (16-B moves, the tail byte by byte).
-__global__ __launch_bounds__(256) void copy_in_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                      uint64_t bytes) {
-  const uint64_t n16 = bytes / 16, tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t nt = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = tid; i < n16; i += nt)
-    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-  for (uint64_t i = 16 * n16 + tid; i < bytes; i += nt) dst[i] = src[i];
-}
-
-hipError_t launch_copy_in(const void* h_src, void* d_dst, uint64_t bytes, hipStream_t s) {
-  if (!bytes) return hipSuccess;
-  const uint32_t blocks = static_cast<uint32_t>(std::min<uint64_t>((bytes / 16 + 255) / 256 + 1, 4096));
-  hipLaunchKernelGGL(copy_in_kernel, dim3(blocks), dim3(256), 0, s, static_cast<const uint8_t*>(h_src),
-                     static_cast<uint8_t*>(d_dst), bytes);
-  return hipGetLastError();
-}
-
 hipError_t launch_small_batch(const SmallArgs& a, hipStream_t s) {
   const uint64_t tiles = a.tt ? (a.m.n + a.tt - 1) / a.tt : 0;
   if (a.m.n == 0 || a.m.n > SMALL_MAX_N || a.tt == 0 || a.tt > TILE_TOPICS || tiles > SMALL_WAVES ||

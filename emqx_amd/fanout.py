@@ -96,6 +96,14 @@ class SubTable:
     def commit(self) -> None:
         check(_lib.lib().emqx_subtab_commit(self._h), "emqx_subtab_commit")
 
+    def commit_wait(self) -> int:
+        """emqx_subtab_commit_wait: the last commit's device-half status (raw rc)."""
+        return int(_lib.lib().emqx_subtab_commit_wait(self._h))
+
+    def set_tuning(self, key: str, value: int) -> None:
+        """emqx_subtab_set_tuning (fault injection for tests)."""
+        check(_lib.lib().emqx_subtab_set_tuning(self._h, key.encode(), int(value)), "emqx_subtab_set_tuning")
+
     def stats(self) -> dict:
         c = np.zeros(4, dtype=np.uint64)
         check(_lib.lib().emqx_subtab_stats(self._h, _p(c)), "emqx_subtab_stats")

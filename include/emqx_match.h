@@ -291,6 +291,10 @@ int emqx_subtab_commit(emqx_subtab* s);
  * it reaches the callers of the failed commit (the commit coalescer calls this before it runs a
  * batch's callbacks). */
 int emqx_subtab_commit_wait(emqx_subtab* s);
+/* Fault injection for tests: "inject_drain_error" = the next `value` waits for a commit's
+ * device half report EMQX_EDEVICE; "inject_bad_alloc" = the next `value` full commits fail
+ * their host allocations (the call returns EMQX_ENOMEM).  EMQX_ENOTFOUND for unknown keys. */
+int emqx_subtab_set_tuning(emqx_subtab* s, const char* key, int64_t value);
 /* counts[0..3] = live plain subscriptions, live shared memberships, groups with members,
  * device bytes */
 int emqx_subtab_stats(emqx_subtab* s, uint64_t* counts4);

@@ -377,3 +377,30 @@ def test_pub_batcher_many_threads_equals_publish_batch(F):
     for i, rows in got.items():
         assert rows == exp[i], i
     assert stats["messages"] == 64 * 200 and stats["batches"] < 64 * 200
+
+
+def test_commit_wait_rebuild_alloc_failure_is_enomem(F):
+    """emqx_subtab_commit_wait rebuilds the tables when the last commit's device half
+    failed; an allocation failure of that rebuild is EMQX_ENOMEM (no exception through the C
+    ABI), and the next commit rebuilds and serves the fan-out again."""
+    from emqx_amd import _lib
+    t = F.SubTable(0)
+    try:
+        t.add([0, 1, 1], [5, 6, 7])
+        t.commit()
+        assert t.commit_wait() == _lib.EMQX_OK
+        with pytest.raises(Exception):
+            t.set_tuning("no_such_key", 1)
+        t.set_tuning("inject_drain_error", 1)
+        t.set_tuning("inject_bad_alloc", 1)
+        assert t.commit_wait() == _lib.EMQX_ENOMEM
+        # the failed rebuild left need_full set: the next commit is a full one and succeeds
+        full0 = t.commit_stats()["full_commits"]
+        t.add([2], [8])
+        t.commit()
+        assert t.commit_wait() == _lib.EMQX_OK
+        assert t.commit_stats()["full_commits"] == full0 + 1
+        st = t.stats()
+        assert st["plain"] == 4 and st["device_bytes"] > 0
+    finally:
+        t.close()
