@@ -133,6 +133,17 @@ def main():
                          "RCCL all-to-all, matched on one shard per topic, and the results return with a "
                          "second all-to-all (strong scaling)")
     ap.add_argument("--vocab-scale", type=int, default=1, help="4 = config C's vocabulary")
+    ap.add_argument("--emulate-world", type=str, default="",
+                    help="--sharded: G ranks of the G-way plan in this one process on one GPU (dist.py "
+                         "EmulatedWorld): every rank's step timed, exchanges projected over xGMI links; a "
+                         "comma list runs each G in turn over one generated table (one JSON line each)")
+    ap.add_argument("--p-space", type=str, default="auto", choices=["auto", "sharded", "replicated"],
+                    help="--sharded: space-P layout of the plan (dist.py shard_plan): '+/x/...' filters sharded "
+                         "by x (two requests a topic) or on every rank (one request a topic)")
+    ap.add_argument("--xgmi-gbs", type=float, default=153.0,
+                    help="--emulate-world: GB/s of one xGMI link, one direction (7 links per MI355X)")
+    ap.add_argument("--a2a-us", type=float, default=30.0,
+                    help="--emulate-world: fixed cost (us) of one all-to-all call, added per exchange")
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the timed batches alternate over (pipelined calls; default 3, "
                          "see DESIGN.md §5)")
@@ -186,6 +197,8 @@ def main():
 
     t0 = time.time()
     # every rank replicates the table (seed 2); each rank draws its own topic stream (weak scaling)
+    if args.sharded and args.emulate_world:
+        return emulated_bench(args, dev)
     if args.sharded:
         return sharded_bench(args, rank, world, dev)
     if args.workload == "E":
@@ -416,6 +429,7 @@ def sharded_bench(args, rank, world, dev):
     import torch.distributed as dist
     from emqx_amd import workloads as W
     from emqx_amd.dist import ShardedMatcher
+    from emqx_amd.dist import plan_p_replicated as D_p_repl
     seed = 3 if args.vocab_scale > 1 else 2
     t0 = time.time()
     with progress(f"[rank {rank}] generating workload"):
@@ -427,7 +441,7 @@ def sharded_bench(args, rank, world, dev):
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     with progress(f"[rank {rank}] building shard"):
-        sm = ShardedMatcher(wl.filters, device=dev, mode=args.mode)
+        sm = ShardedMatcher(wl.filters, device=dev, mode=args.mode, p_space=args.p_space)
     sts = [e.stats() for e in sm.engines if e is not None]
     shard_bytes = sum(x["table_bytes"] for x in sts)
     log(f"[rank {rank}] shard: {sm.n_local_filters} filters, {shard_bytes / 1e9:.2f} GB, plan {len(sm.plan)} keys")
@@ -512,7 +526,7 @@ def sharded_bench(args, rank, world, dev):
                                       f"root '+'), hot keys split by the next level, "
                                       f"{'gloo (rehearsal)' if rehearse else 'RCCL'} all-to-all out and back"},
             "shard_filters_max_rank": int(most.item()), "shard_filters_max_frac": round(float(most.item()) / wl.n_filters, 4),
-            "shard_plan_keys": len(sm.plan),
+            "shard_plan_keys": len(sm.plan), "p_space": "replicated" if D_p_repl(sm.plan) else "sharded",
             "shard_table_bytes_rank0": int(shard_bytes),
             "requests_per_topic_by_slot": {k: round(float(mt[4 + i].item()) / (n * world), 4)
                                            for i, k in enumerate(("A", "B", "AB"))},
@@ -530,6 +544,177 @@ def sharded_bench(args, rank, world, dev):
     dist.destroy_process_group()
     if mism:
         raise SystemExit(f"rank {rank}: sharded CSR differs on {mism} topics")
+
+
+def emulated_bench(args, dev):
+    """One rank's step of the filter-sharded layout at world G, measured on ONE GPU
+    (VERDICT r5 #1): the G-way plan of the table (config C: 100M filters, vocab x4, seed 3), G
+    ranks' engines built on this GPU, G sources' batches (source s draws the stream rank s of a
+    real G-rank run would: batch 0 = the C1 batch, then topic seeds 1000 + s), and every rank's
+    step run through the product's step (dist.py ShardedMatcher._step_gen) one rank at a time,
+    chunks read in place of being moved (dist.py EmulatedWorld).  Reported per rank and phase:
+    wall time (host-inclusive) and kernel time (HIP events), the bytes each (source,
+    destination) pair exchanges, and a projection of the G-GPU step: the slowest rank per phase
+    plus each exchange's largest pair at --xgmi-gbs per link (xGMI is point to point: a pair's
+    bytes go over its own link) plus --a2a-us per all-to-all.  Parity: every source's merged CSR
+    ID-for-ID against the whole table on this GPU (the replicated layout), and source 0's first
+    12K topics against the committed oracle slice (tests/golden/c100m_slice.npz) when the table
+    is the golden's."""
+    import torch
+    from emqx_amd import workloads as W
+    from emqx_amd.dist import EmulatedWorld
+    from emqx_amd.engine import Engine
+    from oracle import cpp as C
+    worlds = [int(x) for x in str(args.emulate_world).split(",") if x.strip()]
+    G = max(worlds)
+    seed = 3 if args.vocab_scale > 1 else 2
+    n = args.batch
+    t0 = time.time()
+    with progress("generating workload"):
+        wl = W.config_b(n_filters=args.n_filters, n_topics=n, seed=seed, vocab_scale=args.vocab_scale,
+                        extra_topic_seeds=tuple(1000 + s for s in range(1, G)))
+    log(f"workload {wl.n_filters} filters, {G} batches of {n} topics ({time.time() - t0:.1f}s)")
+    srcs = [wl.topics] + list(wl.extra_topics[: G - 1])
+    batches = [(torch.from_numpy(b[0]).to(dev), torch.from_numpy(b[1].view(np.int64)).to(dev)) for b in srcs]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    # the replicated layout on this GPU: every source's expected CSR, and the 1-GPU step time
+    t0 = time.time()
+    with progress("building the whole table (replicated reference)"):
+        full = Engine(dev.index)
+        full.insert_packed(*wl.filters)
+        full.commit()
+    log(f"whole table built ({time.time() - t0:.1f}s)")
+    cap = max(64 * n, 1 << 20)
+    d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    refs, rep_ms = [], []
+    for j, (tb, to) in enumerate(batches):
+        m = full.match_device(tb.data_ptr(), to.data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(), cap,
+                              mode=args.mode, stream=stream)
+        off_r = d_off.cpu().numpy()
+        ids_r = d_ids[:m].cpu().numpy().view(np.uint32)
+        tt = np.repeat(np.arange(n, dtype=np.int64), np.diff(off_r.astype(np.int64)))
+        refs.append((off_r.astype(np.uint64), (np.sort((tt << 32) | ids_r.astype(np.int64)) & 0xFFFFFFFF).astype(np.uint32)))
+        del tt
+    for _ in range(5):
+        full.match_device(batches[0][0].data_ptr(), batches[0][1].data_ptr(), n, d_off.data_ptr(), d_ids.data_ptr(),
+                          cap, mode=args.mode, stream=stream)
+        rep_ms.append(full.stats()["last_match_ms"])
+    golden = None
+    gpath = os.path.join(ROOT, "tests", "golden", "c100m_slice.npz")
+    if os.path.exists(gpath):
+        g = dict(np.load(gpath))
+        if (int(g["n_filters"]), int(g["n_topics"]), int(g["seed"]), int(g["vocab_scale"])) == (
+                args.n_filters, n, seed, args.vocab_scale):
+            golden = g
+    full.close()
+    del full, d_ids
+    torch.cuda.empty_cache()
+    failed = []
+    for G in worlds:
+        failed += _emulated_world(args, dev, wl, batches[:G], refs, rep_ms, golden, G)
+    if failed:
+        raise SystemExit(f"emulated sharded CSR differs: {failed}")
+
+
+def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
+    """One --emulate-world line (emulated_bench) at world G; returns the parity failures."""
+    import torch
+    from emqx_amd.dist import EmulatedWorld
+    from oracle import cpp as C
+    n = args.batch
+    t0 = time.time()
+    with progress(f"building the {G} ranks' engines"):
+        ew = EmulatedWorld(wl.filters, G, dev, mode=args.mode, p_space=args.p_space,
+                           on_rank=lambda r: log(f"rank {r} built ({time.time() - t0:.0f}s)"))
+    log(f"{G} ranks built ({time.time() - t0:.1f}s): filters per rank [A, B, AB] {ew.filters_per_rank}")
+    for _ in range(max(args.warmup, 1)):
+        res = ew.step(batches)
+    torch.cuda.synchronize()
+    # the whole emulated step, back to back (all G ranks' work on one GPU, exchanges free)
+    t_all = time.perf_counter()
+    for _ in range(args.steps):
+        ew.step(batches)
+    torch.cuda.synchronize()
+    all_ms = 1e3 * (time.perf_counter() - t_all) / max(args.steps, 1)
+    phases = EmulatedWorld.PHASES if G > 1 else ("step",)  # (world 1: no exchange points)
+    per = {}
+    for mode in ("wall", "gpu"):
+        acc = np.zeros((G, len(phases)))
+        for _ in range(args.steps):
+            ew.step(batches, timing=mode)
+            t = np.array(ew.last_times, dtype=np.float64)
+            if t.shape != acc.shape:
+                raise SystemExit(f"unexpected exchange rounds {t.shape} (a redo during the timed steps)")
+            acc += t
+        per[mode] = acc / max(args.steps, 1)
+    res = ew.step(batches)
+    torch.cuda.synchronize()
+    # parity
+    bad, ids_checked = [], 0
+    for s in range(G):
+        off_g = res[s][0].cpu().numpy().astype(np.uint64)
+        ids_g = res[s][1].cpu().numpy().view(np.uint32)
+        bad.append(int(C.csr_mismatches(off_g, ids_g, *refs[s]).size))
+        ids_checked += int(off_g[-1])
+    gold = None
+    if golden is not None:
+        k = int(golden["slice"])
+        off_g = res[0][0][: k + 1].cpu().numpy().astype(np.uint64)
+        ids_g = res[0][1][: int(off_g[-1])].cpu().numpy().view(np.uint32)
+        gold = {"topics": k, "ids": int(golden["off"][-1]),
+                "mismatches": int(C.csr_mismatches(off_g, ids_g, golden["off"], golden["ids"]).size)}
+    # projection of the G-GPU step: per phase the slowest rank; per exchange the largest pair
+    link = args.xgmi_gbs * 1e9
+    bo = ew.bytes_out.copy()
+    for k in range(2):
+        np.fill_diagonal(bo[k], 0)  # (a rank's own chunk is never moved)
+    exch_ms = [float(bo[k].max()) / link * 1e3 for k in range(2)]
+    fixed_ms = 4 * args.a2a_us / 1e3 if G > 1 else 0.0  # two size exchanges + two chunk exchanges
+    proj = {}
+    for mode in ("wall", "gpu"):
+        slow = per[mode].max(axis=0)
+        step_ms = float(slow.sum()) + sum(exch_ms) + fixed_ms
+        proj[mode] = {"step_ms": round(step_ms, 4), "topics_per_s": round(G * n / step_ms * 1e3, 1),
+                      "slowest_rank_phase_ms": {p: round(float(v), 4) for p, v in zip(phases, slow)}}
+    rep = float(np.median(rep_ms))
+    rep_rate = n / rep * 1e3
+    out = {
+        "metric": f"one rank's filter-sharded step at world {G}, measured on 1xMI355X (all {G} ranks emulated), "
+                  f"and the projected {G}-GPU rate",
+        "value": proj["wall"]["topics_per_s"], "unit": "topics/s (projected)", "n_gpus": 1, "emulated_world": G,
+        "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": f"{'C' if args.vocab_scale > 1 else 'B'}-generator table of {wl.n_filters} filters, "
+                               f"{G}-way plan, every rank publishing its own {n}-topic batch per step",
+                   "parallelism": f"filter-sharded x{G} emulated on one GPU (dist.py EmulatedWorld)"},
+        "p_space": "replicated" if ew.p_replicated else "sharded",
+        "filters_per_rank_A_B_AB": ew.filters_per_rank,
+        "shard_plan_keys": int(len(ew.plan)),
+        "requests_per_rank_by_slot": [list(m.last_slot_topics) for m in ew.matchers],
+        "rank_phase_ms_wall": [[round(float(x), 4) for x in row] for row in per["wall"]],
+        "rank_phase_ms_gpu": [[round(float(x), 4) for x in row] for row in per["gpu"]],
+        "rank_step_ms_wall": [round(float(x), 4) for x in per["wall"].sum(axis=1)],
+        "rank_step_ms_gpu": [round(float(x), 4) for x in per["gpu"].sum(axis=1)],
+        "phases": list(phases),
+        "exchange_bytes_out": {"requests": bo[0].tolist(), "answers": bo[1].tolist()},
+        "exchange_max_pair_bytes": {"requests": int(bo[0].max()), "answers": int(bo[1].max())},
+        "projection": {"xgmi_gbs_per_link": args.xgmi_gbs, "a2a_fixed_us": args.a2a_us,
+                       "exchange_ms": [round(x, 4) for x in exch_ms], **proj},
+        "emulated_step_ms_all_ranks_one_gpu": round(all_ms, 4),
+        "replicated_one_gpu": {"call_ms": round(rep, 4), "topics_per_s": round(rep_rate, 1),
+                               "x_G": round(G * rep_rate, 1)},
+        "projected_vs_G_replicated": {m: round(proj[m]["topics_per_s"] / (G * rep_rate), 4) for m in proj},
+        "parity": {"rule": "every source's merged CSR vs the whole table on this GPU, ID-for-ID per topic",
+                   "topics_checked": G * n, "ids_checked": ids_checked, "mismatching_topics_per_source": bad,
+                   "golden_slice_source0": gold},
+    }
+    print(json.dumps(out), flush=True)
+    ew.close()
+    del ew, res
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return [(G, bad, gold)] if any(bad) or (gold and gold["mismatches"]) else []
 
 
 def retain_traffic(nf, n_retained):

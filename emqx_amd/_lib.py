@@ -246,7 +246,7 @@ def lib():
         "emqx_commit_stats": (i32, [vp, vp, u32]),
         "emqx_shard_owner": (i32, [vp, vp, u64, u32, u32, i32, vp]),
         "emqx_shard_owner_device": (i32, [vp, vp, u64, u32, u32, vp, vp]),
-        "emqx_shard_plan": (i32, [vp, vp, u64, u32, u32, vp, u32, ctypes.POINTER(u32)]),
+        "emqx_shard_plan": (i32, [vp, vp, u64, u32, u32, u32, vp, u32, ctypes.POINTER(u32)]),
         "emqx_shard_place": (i32, [vp, vp, u64, u32, vp, u32, vp, vp, vp]),
         "emqx_shard_route": (i32, [vp, vp, u64, u32, vp, u32, vp]),
         "emqx_shard_route_device": (i32, [vp, vp, u64, u32, vp, u32, vp, vp]),

@@ -284,6 +284,14 @@ struct ShardSplitE {
   uint32_t key, info;
 };
 
+// Space P replicated: the plan entry {SHARD_SPACE_P, SHARD_P_REPLICATED} (no real key entry has
+// that info: span 0, first rank 0xFFFF).  Then every '+/x/...' filter lives
+// on every rank with the root wildcards (engine A), and a topic makes ONE request, to its L-space
+// rank: emqx_shard_plan chooses it when space P holds at most a rank's share of the filters
+// (config C: 7 % of the table, against 12.5 % a rank at world 8), so the step carries one request
+// a topic instead of two for a larger replicated part.
+constexpr uint32_t SHARD_P_REPLICATED = 0x0000FFFFu;
+
 EMQX_HD uint32_t shard_level_hash(const uint8_t* p, uint64_t s, uint64_t e) {
   uint32_t h = 0x811C9DC5u;  // FNV-1a over the level's bytes
   for (uint64_t i = s; i < e; ++i) h = (h ^ p[i]) * 0x01000193u;
@@ -343,6 +351,10 @@ EMQX_HD void shard_place_key(uint32_t space, uint32_t hk, uint32_t next, uint32_
   *span = 1;
 }
 
+EMQX_HD bool shard_p_replicated(const ShardSplitE* sp, uint32_t nsp) {
+  return nsp && shard_split_find(sp, nsp, SHARD_SPACE_P) == SHARD_P_REPLICATED;
+}
+
 // Placement of filter p[0, n): *engine 0 (A: space L, root-wildcard) or 1 (B: space P).
 EMQX_HD void shard_place_filter(const uint8_t* p, uint64_t n, uint32_t world, const ShardSplitE* sp, uint32_t nsp,
                                 uint32_t* first, uint32_t* span, uint32_t* engine) {
@@ -351,7 +363,8 @@ EMQX_HD void shard_place_filter(const uint8_t* p, uint64_t n, uint32_t world, co
   const bool has2 = shard_level(p, n, 1, &s2, &e2);
   *engine = 0;
   if (shard_is_wild(p, s1, e1)) {
-    if (p[s1] == '#' || !has2 || shard_is_wild(p, s2, e2)) {  // '#', '+', '+/#', '+/+/...'
+    // '#', '+', '+/#', '+/+/...'; and '+/x/...' when space P is replicated
+    if (p[s1] == '#' || !has2 || shard_is_wild(p, s2, e2) || shard_p_replicated(sp, nsp)) {
       *first = 0;
       *span = world;
       return;
@@ -412,6 +425,7 @@ EMQX_HD void shard_route_levels(const uint8_t* p, uint64_t n, const ShardTopicLe
   shard_place_key(0, L.h[0], has2 ? L.h[1] : SHARD_ABSENT, world, sp, nsp, &first, &span);
   req[0] = 2 * first;
   if (!has2 || (n > 0 && p[0] == '$')) return;  // '+/x/...' never matches a '$' topic (S5)
+  if (shard_p_replicated(sp, nsp)) return;       // ... and lives on every rank
   shard_place_key(SHARD_SPACE_P, L.h[1], has3 ? L.h[2] : SHARD_ABSENT, world, sp, nsp, &first, &span);
   req[1] = 2 * first + 1;
 }

@@ -115,8 +115,10 @@ bool plan_key(const uint8_t* p, uint64_t len, uint32_t* key, uint32_t* hk, uint3
 }  // namespace
 
 extern "C" int emqx_shard_plan(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
-                               uint32_t max_piece_pm, emqx_shard_split* out, uint32_t cap, uint32_t* n_out) {
-  if ((n && !offsets) || !n_out || world == 0 || world > 65535 || max_piece_pm == 0 || (cap && !out))
+                               uint32_t max_piece_pm, uint32_t p_space, emqx_shard_split* out, uint32_t cap,
+                               uint32_t* n_out) {
+  if ((n && !offsets) || !n_out || world == 0 || world > 65535 || max_piece_pm == 0 || (cap && !out) ||
+      p_space > EMQX_SHARD_P_REPLICATED)
     return EMQX_EINVAL;
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i]) return EMQX_EINVAL;
@@ -127,12 +129,21 @@ extern "C" int emqx_shard_plan(const uint8_t* bytes, const uint64_t* offsets, ui
   };
   std::unordered_map<uint32_t, KeyLoad> per_key;
   uint32_t key, hk, next;
+  uint64_t n_p = 0;  // space P's filters
   for (uint64_t i = 0; i < n; ++i) {
     if (!plan_key(bytes + offsets[i], offsets[i + 1] - offsets[i], &key, &hk, &next)) continue;
     KeyLoad& k = per_key[key];
     ++k.all;
     k.wild_next += next == emqx::SHARD_NONE ? 1u : 0u;
+    n_p += (key & emqx::SHARD_SPACE_P) ? 1u : 0u;
   }
+  // space P replicated (layout.h SHARD_P_REPLICATED) when it holds at most a rank's share: its
+  // keys then take no part in the plan
+  const bool p_repl = world > 1 && (p_space == EMQX_SHARD_P_REPLICATED ||
+                                    (p_space == EMQX_SHARD_P_AUTO && n_p * world <= n));
+  if (p_repl)
+    for (auto it = per_key.begin(); it != per_key.end();)
+      it = (it->first & emqx::SHARD_SPACE_P) ? per_key.erase(it) : std::next(it);
   // Largest keys first onto the least-loaded ranks (LPT).  A key over max_piece_pm / 1000 of a
   // rank's share is split over the fewest consecutive ranks that bring each piece under it: its
   // wildcard-next filters go to all of them, its next-level words are placed one by one (the
@@ -205,6 +216,7 @@ extern "C" int emqx_shard_plan(const uint8_t* bytes, const uint64_t* offsets, ui
     }
     for (uint32_t k = 0; k < span; ++k) load[(best + k) % world] += (c - placed) / span;  // hashed rest
   }
+  if (p_repl) sp.push_back(emqx_shard_split{emqx::SHARD_SPACE_P, emqx::SHARD_P_REPLICATED});
   std::sort(sp.begin(), sp.end(), [](const emqx_shard_split& a, const emqx_shard_split& b) { return a.key < b.key; });
   sp.erase(std::unique(sp.begin(), sp.end(),
                        [](const emqx_shard_split& a, const emqx_shard_split& b) { return a.key == b.key; }),

@@ -236,9 +236,16 @@ SHARD_ENGINES = 3  # engine slots of a rank: 0 = A, 1 = B, 2 = AB (include/emqx_
 MAX_PIECE_PM = 250  # a key is split when its filters exceed a quarter of a rank's share
 
 
-def shard_plan(filters: Tuple[np.ndarray, np.ndarray], world: int, max_piece_pm: int = MAX_PIECE_PM) -> np.ndarray:
+P_SPACE = {"auto": 0, "sharded": 1, "replicated": 2}  # emqx_shard_plan p_space (include/emqx_match.h)
+
+
+def shard_plan(filters: Tuple[np.ndarray, np.ndarray], world: int, max_piece_pm: int = MAX_PIECE_PM,
+               p_space: str = "auto") -> np.ndarray:
     """The hot keys of a filter set (emqx_shard_plan): (k, 2) uint32 rows (key, first rank | span
-    << 16), sorted by key.  Every rank computes the same plan from the same filters."""
+    << 16), sorted by key.  Every rank computes the same plan from the same filters.  p_space:
+    "sharded" (two key spaces: a topic asks its L-space rank and its P-space rank), "replicated"
+    (the '+/x/...' filters on every rank: one request a topic), "auto" (replicated when they are
+    at most a rank's share of the filters)."""
     from . import _lib
     buf, offs = filters
     offs = np.ascontiguousarray(np.asarray(offs, dtype=np.uint64))
@@ -248,13 +255,19 @@ def shard_plan(filters: Tuple[np.ndarray, np.ndarray], world: int, max_piece_pm:
     while True:
         out = np.zeros((cap, 2), dtype=np.uint32)
         got = ctypes.c_uint32(0)
-        rc = _lib.lib().emqx_shard_plan(b.ctypes.data, offs.ctypes.data, n, world, max_piece_pm, out.ctypes.data,
-                                        cap, ctypes.byref(got))
+        rc = _lib.lib().emqx_shard_plan(b.ctypes.data, offs.ctypes.data, n, world, max_piece_pm, P_SPACE[p_space],
+                                        out.ctypes.data, cap, ctypes.byref(got))
         if rc == _lib.EMQX_EOVERFLOW:
             cap = int(got.value)
             continue
         _lib.check(rc, "emqx_shard_plan")
         return out[: got.value].copy()
+
+
+def plan_p_replicated(plan: np.ndarray) -> bool:
+    """Whether the plan replicates space P (layout.h SHARD_P_REPLICATED): every topic then makes
+    one request, to its rank's AB slot, and engines A and B are never asked."""
+    return bool(len(plan)) and bool(((plan[:, 0] == 0x80000000) & (plan[:, 1] == 0x0000FFFF)).any())
 
 
 def shard_place(filters: Tuple[np.ndarray, np.ndarray], world: int, plan: np.ndarray):
@@ -430,34 +443,45 @@ class ShardedMatcher:
 
     def __init__(self, filters: Tuple[np.ndarray, np.ndarray], group=None, device: Optional[torch.device] = None,
                  mode: int = 0, match_fn: Optional[Callable] = None, max_piece_pm: int = MAX_PIECE_PM,
-                 engines: Optional[list] = None):
+                 engines: Optional[list] = None, rank_world: Optional[Tuple[int, int]] = None,
+                 plan: Optional[np.ndarray] = None, local_ids: Optional[list] = None, p_space: str = "auto"):
         """``engines``: this rank's engines already built ([A, B, AB], each holding exactly the
         filters shard_local_ids names for it, reporting global ids; A and B may be None at world
         1, where every request is an AB request); they are adopted, not copied (e.g. a table
-        held whole on one GPU is engine AB at world 1, tests/test_gpu_c100m.py)."""
+        held whole on one GPU is engine AB at world 1, tests/test_gpu_c100m.py).
+        ``rank_world``: (rank, world) of a rank with no process group (``EmulatedWorld``: G
+        ranks in one process); ``plan`` / ``local_ids``: the plan and this rank's ids when the
+        caller computed them already (both are functions of the filters and the world).
+        ``p_space``: the plan's space-P layout (``shard_plan``)."""
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        if rank_world is not None:
+            self.rank, self.world = rank_world
+        else:
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
         self.device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
                                  else torch.device("cpu"))
         self.mode = mode
-        self.plan = shard_plan(filters, self.world, max_piece_pm)
+        self.plan = shard_plan(filters, self.world, max_piece_pm, p_space) if plan is None else plan
         self.plan_dev = (torch.from_numpy(self.plan.view(np.int32).copy()).to(self.device)
                          if self.device.type == "cuda" and len(self.plan) else None)
-        self.local_ids = shard_local_ids(filters, self.rank, self.world, self.plan)
+        self.local_ids = (shard_local_ids(filters, self.rank, self.world, self.plan) if local_ids is None
+                          else local_ids)
+        self.last_exchange_out = [None, None]
         self.engines = []
         self.last_local_topics = 0
         self.last_slot_topics = [0, 0, 0]
         if engines is not None:
             assert match_fn is None and len(engines) == SHARD_ENGINES
-            assert self.world > 1 or engines[2] is not None
+            assert (self.world > 1 and not plan_p_replicated(self.plan)) or engines[2] is not None
             self.engines = list(engines)
             match_fn = self._engine_match
         elif match_fn is None:
             from .engine import Engine
             from .workloads import take
+            one_request = self.world == 1 or plan_p_replicated(self.plan)
             for slot, gids in enumerate(self.local_ids):
-                if self.world == 1 and slot < 2:  # no request ever names A or B alone
+                if one_request and slot < 2:  # no request ever names A or B alone
                     self.engines.append(None)
                     continue
                 e = Engine(self.device.index if self.device.type == "cuda" else -1)
@@ -564,15 +588,47 @@ class ShardedMatcher:
         return b
 
     def _match_all_device(self, topics: Tuple[torch.Tensor, torch.Tensor]):
-        """match_all on device kernels (emqx_shard_step_*, shard_step.hip): route + fold + stable
-        sort + pack the requests, one all-to-all of sizes and one of chunks, unpack into the
-        engine slots' batches, the engines matched asynchronously into learnt capacities, the
-        answers packed per source, one all-to-all of sizes and one of answers, merged back in
-        batch order.  The host only reads the split sizes (two syncs)."""
+        """match_all on device kernels: the step (``_step_gen``) driven over this rank's process
+        group, one collective per exchange point."""
+        gen = self._step_gen(topics)
+        try:
+            op = next(gen)
+            while True:
+                op = gen.send(self._exchange(op))
+        except StopIteration as stop:
+            return stop.value
+
+    def _exchange(self, op):
+        """One exchange point of ``_step_gen`` over the process group (world > 1):
+        ("sizes", words, W): an all-to-all of W int64 words per rank, both sides read on the host
+        (a host sync) -> (words sent, words received, the received words as a numpy array);
+        ("chunks", buf, out sizes, in sizes, name): chunk r of buf to rank r -> the device address
+        of every source's chunk for this rank (``_exchange_chunks``)."""
+        if op[0] == "sizes":
+            _, words, W = op
+            G = self.world
+            words_in = torch.empty_like(words)
+            _a2a(words_in, words, [W] * G, [W] * G, self.group)
+            h = self._to_host(words, words_in)  # host sync
+            mi = np.ascontiguousarray(h[W * G: 2 * W * G], dtype=np.int64)
+            return h[: W * G].tolist(), mi.tolist(), mi
+        _, buf, out_sz, in_sz, name = op
+        return _exchange_chunks(buf, out_sz, in_sz, lambda k: self._buf(name, k + 16, buf.dtype), self.group,
+                                self.rank)
+
+    def _step_gen(self, topics: Tuple[torch.Tensor, torch.Tensor]):  # noqa: C901
+        """One step of match_all on device kernels (emqx_shard_step_*, shard_step.hip), as a
+        generator that yields at each exchange point and is sent its result (``_exchange`` over a
+        process group; ``EmulatedWorld`` for G ranks in one process): route + fold + stable sort
+        + pack the requests, one exchange of sizes and one of chunks, unpack into the engine
+        slots' batches, the engines matched asynchronously into learnt capacities, the answers
+        packed per source, one exchange of sizes and one of answers, merged back in batch order.
+        The host only reads the split sizes (two syncs; at world 1 from mapped pinned words, no
+        exchange).  Runs on the current stream; returns (offsets int64 (n+1,), ids int32)."""
         from . import _lib
         L = _lib.lib()
         E = SHARD_ENGINES
-        dev, G, grp = self.device, self.world, self.group
+        dev, G = self.device, self.world
         st = self._step.h
         mark = _host_marks() if _SHARD_PROF else (lambda k: None)
         mark(0)
@@ -605,18 +661,15 @@ class ShardedMatcher:
             mo_l = mi_l = hmeta[: MW * G].tolist()
             mi_ptr = hmeta.data_ptr()  # (recv reads the words on the host, during the call)
         else:
-            meta_in = torch.empty_like(meta)
-            _a2a(meta_in, meta, [MW] * G, [MW] * G, grp)
-            mh = self._to_host(meta, meta_in).reshape(2, -1)  # host sync 1
-            mi = np.ascontiguousarray(mh[1])
-            mo_l, mi_l, mi_ptr = mh[0].tolist(), mi.tolist(), mi.ctypes.data
+            mo_l, mi_l, mi = yield ("sizes", meta, MW)  # host sync 1
+            mi_ptr = mi.ctypes.data
         mark(2)
         out_b = mo_l[0::MW]
         in_b = mi_l[0::MW]
         if min(out_b) < 0 or min(in_b) < 0:
             raise RuntimeError("emqx_shard_step_send: chunks over the send buffer")
-        chunks = _exchange_chunks(send, out_b, in_b, lambda k: self._buf("recv", k + 16, torch.uint8), grp,
-                                  self.rank)
+        self.last_exchange_out = [[x for x in out_b], None]
+        chunks = [send.data_ptr()] if G == 1 else (yield ("chunks", send, out_b, in_b, "recv"))
         NQ = [sum(mi_l[1 + e::MW]) for e in range(E)]
         # a slot fed by one source only is matched in place in that source's chunk (recv
         # replaces its byte buffer's address); the others are gathered into these buffers
@@ -668,7 +721,7 @@ class ShardedMatcher:
             hans, dans = self._pinned("ans_meta", 3 * G) if G == 1 else (None, None)
             ans_meta = None if G == 1 else torch.empty(3 * G, dtype=torch.int64, device=dev)
             sp = None if redo else (ctypes.c_void_p * E)(*[dsumm + 64 * e if NQ[e] else None for e in range(E)])
-            # (this rank's own answers stay in the engines' outputs: the merge reads them there)
+            # (this rank's own answers stay in the engines' outputs: the merge reads them from there)
             _lib.check(L.emqx_shard_step_answer(st, PA([o[0] for o in outs]), PA([o[1] for o in outs]), sp, self.rank,
                                                 P(ans), ctypes.c_void_p(dans) if G == 1 else P(ans_meta), S),
                        "emqx_shard_step_answer")
@@ -678,11 +731,8 @@ class ShardedMatcher:
                 am_l = ai_l = hans[: 3 * G].tolist()
                 ai_ptr = hans.data_ptr()  # (merge reads the words on the host, during the call)
             else:
-                ans_in = torch.empty_like(ans_meta)
-                _a2a(ans_in, ans_meta, [3] * G, [3] * G, grp)
-                h = self._to_host(ans_meta, ans_in)  # host sync 2
-                ai = np.ascontiguousarray(h[3 * G: 6 * G], dtype=np.int64)
-                am_l, ai_l, ai_ptr = h[: 3 * G].tolist(), ai.tolist(), ai.ctypes.data
+                am_l, ai_l, ai = yield ("sizes", ans_meta, 3)  # host sync 2
+                ai_ptr = ai.ctypes.data
             mark(6)
             sm = hsumm[: 8 * E].tolist()
             if not redo:
@@ -699,7 +749,8 @@ class ShardedMatcher:
             redo = True
         # 4. answers back to their sources, merged per topic in batch order
         out_w, in_w = am_l[0::3], ai_l[0::3]
-        back = _exchange_chunks(ans, out_w, in_w, lambda k: self._buf("back", k + 16, torch.int32), grp, self.rank)
+        self.last_exchange_out[1] = [4 * x for x in out_w]
+        back = [ans.data_ptr()] if G == 1 else (yield ("chunks", ans, out_w, in_w, "back"))
         total = sum(ai_l[2::3])
         out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         out_ids = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
@@ -831,3 +882,124 @@ def merge_requests(cnt: torch.Tensor, ids: torch.Tensor, req_topic: torch.Tensor
         k = torch.repeat_interleave(torch.arange(cnt.numel(), device=dev), cnt, output_size=total)
         out[base[k] + (torch.arange(total, device=dev) - roff[k])] = ids.to(torch.int32)
     return offsets, out
+
+
+class EmulatedWorld:
+    """G ranks of the filter-sharded layout in ONE process on one GPU, for measuring one rank's
+    step at world G without G GPUs.  Every rank is a real ``ShardedMatcher`` with its
+    own engines (A / B / AB over exactly the filters the G-way plan gives it), its own device step
+    (emqx_shard_step_* built for world G) and its own buffers; every rank's step is the product's
+    ``_step_gen``.  Only the exchanges differ: a chunk for rank r is read where its source packed
+    it (the device address any all-to-all would have delivered it to is just another buffer on
+    the same GPU), so a step costs the ranks' own work, run one rank at a time, and the
+    exchanges' bytes are counted per (source, destination) pair for a projection over xGMI links
+    instead of being moved.
+
+    ``step(batches)`` runs one step of every rank (rank s publishing batches[s]) and returns every
+    rank's CSR.  With ``timing``: "wall" times each rank's segments between exchange points on
+    the host (device synchronised before and after: launches, host bookkeeping and kernels);
+    "gpu" times them with HIP events on the rank's stream behind a spin kernel, so the launches
+    are enqueued before the first kernel starts (kernel time only)."""
+
+    PHASES = ("send", "sizes1", "recv_match_answer", "sizes2", "merge")
+
+    def __init__(self, filters: Tuple[np.ndarray, np.ndarray], world: int, device: torch.device, mode: int = 0,
+                 max_piece_pm: int = MAX_PIECE_PM, on_rank: Optional[Callable] = None, p_space: str = "auto"):
+        self.world = world
+        self.device = device
+        self.plan = shard_plan(filters, world, max_piece_pm, p_space)
+        self.p_replicated = plan_p_replicated(self.plan)
+        first, span, eng = shard_place(filters, world, self.plan)
+        first = first.astype(np.int64)
+        self.matchers: List[ShardedMatcher] = []
+        self.filters_per_rank = []
+        for r in range(world):
+            held = ((r - first) % world) < span
+            ids = [np.nonzero(held & (eng == e))[0].astype(np.uint32) for e in (0, 1)] + [
+                np.nonzero(held)[0].astype(np.uint32)]
+            del held
+            self.filters_per_rank.append([int(len(x)) for x in ids])
+            self.matchers.append(ShardedMatcher(filters, device=device, mode=mode, rank_world=(r, world),
+                                                plan=self.plan, local_ids=ids))
+            if on_rank is not None:
+                on_rank(r)
+        self.bytes_out = np.zeros((2, world, world), dtype=np.int64)  # [requests, answers][src][dst]
+        self.last_times = None
+
+    def close(self):
+        for m in self.matchers:
+            for e in m.engines:
+                if e is not None:
+                    e.close()
+            if m._step is not None:
+                m._step.close()
+        self.matchers = []
+
+    def _run(self, r: int, gen, value, timing: Optional[str]):
+        """Advances rank r's step to its next exchange point (or its end) on the rank's stream;
+        returns (op or ("done", result), seconds or ms, or None)."""
+        m = self.matchers[r]
+        if m._stream is None:
+            m._stream = torch.cuda.Stream(device=self.device)
+        t = None
+        with torch.cuda.stream(m._stream):
+            if timing == "gpu":
+                torch.cuda.synchronize(self.device)
+                torch.cuda._sleep(2_000_000)  # (launches queue up behind it: the events time kernels)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(m._stream)
+            elif timing == "wall":
+                torch.cuda.synchronize(self.device)
+                t0 = time.perf_counter()
+            try:
+                op = next(gen) if value is None else gen.send(value)
+            except StopIteration as stop:
+                op = ("done", stop.value)
+            if timing == "gpu":
+                e1.record(m._stream)
+                e1.synchronize()
+                t = e0.elapsed_time(e1)
+            elif timing == "wall":
+                torch.cuda.synchronize(self.device)
+                t = 1e3 * (time.perf_counter() - t0)
+        return op, t
+
+    def step(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], timing: Optional[str] = None):
+        G = self.world
+        assert len(batches) == G
+        gens = [m._step_gen(b) for m, b in zip(self.matchers, batches)]
+        ops, times = [None] * G, [[] for _ in range(G)]
+        vals = [None] * G
+        rounds = 0
+        chunk_round = 0
+        while True:
+            for r in range(G):
+                ops[r], t = self._run(r, gens[r], vals[r], timing)
+                times[r].append(t)
+            kinds = {op[0] for op in ops}
+            if len(kinds) != 1:
+                raise RuntimeError(f"ranks out of step at exchange {rounds}: {kinds}")
+            kind = kinds.pop()
+            rounds += 1
+            if kind == "done":
+                break
+            torch.cuda.synchronize(self.device)
+            if kind == "sizes":
+                W = ops[0][2]
+                words = [op[1].cpu().numpy().astype(np.int64) for op in ops]
+                for r in range(G):
+                    mi = np.ascontiguousarray(np.concatenate([words[s][W * r: W * (r + 1)] for s in range(G)]))
+                    vals[r] = (words[r].tolist(), mi.tolist(), mi)
+            elif kind == "chunks":
+                # chunk r of source s lies at s's buffer + the prefix of s's sizes before r
+                offs = [np.concatenate([[0], np.cumsum(op[2])]).astype(np.int64) for op in ops]
+                for r in range(G):
+                    vals[r] = [ops[s][1].data_ptr() + ops[s][1].element_size() * int(offs[s][r]) for s in range(G)]
+                k = min(chunk_round, 1)
+                for s in range(G):
+                    self.bytes_out[k, s, :] = np.asarray(ops[s][2], dtype=np.int64) * ops[s][1].element_size()
+                chunk_round += 1
+            else:
+                raise RuntimeError(f"unknown exchange {kind}")
+        self.last_times = times if timing else None
+        return [op[1] for op in ops]

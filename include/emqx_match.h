@@ -459,6 +459,10 @@ int emqx_shard_owner_device(const uint8_t* d_bytes, const uint64_t* d_offsets, u
  * (emqx_shard_plan: more than max_piece_pm / 1000 of a rank's share) is split over `span`
  * consecutive ranks by the next level; its filters whose next level is '+' / '#' live on all of
  * them.  Each rank holds two engines: "A" (space L + root-wildcard) and "B" (space P).
+ * p_space: EMQX_SHARD_P_SHARDED as above; EMQX_SHARD_P_REPLICATED: space P lives on every rank
+ * with the root wildcards (engine A) and a topic makes one request, to its L-space rank;
+ * EMQX_SHARD_P_AUTO: replicated when space P holds at most n / world filters.  The choice is
+ * recorded in the plan (entry {0x80000000, 0x0000FFFF}), so place and route follow it.
  *   emqx_shard_plan   the hot keys of a filter set (sorted; EMQX_EOVERFLOW: *n_out = needed)
  *   emqx_shard_place  filters: ranks [first, first + span) (mod world) of engine A (0) or B (1)
  *   emqx_shard_route  topics: req2[2i] = rank * 2 of its engine-A request, req2[2i + 1] = rank * 2
@@ -472,8 +476,11 @@ typedef struct emqx_shard_split {
   uint32_t key;   /* space bit (0x80000000 = space P) | 31-bit level hash                       */
   uint32_t info;  /* first rank | span << 16                                                    */
 } emqx_shard_split;
+#define EMQX_SHARD_P_AUTO 0u
+#define EMQX_SHARD_P_SHARDED 1u
+#define EMQX_SHARD_P_REPLICATED 2u
 int emqx_shard_plan(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world, uint32_t max_piece_pm,
-                    emqx_shard_split* out, uint32_t cap, uint32_t* n_out);
+                    uint32_t p_space, emqx_shard_split* out, uint32_t cap, uint32_t* n_out);
 int emqx_shard_place(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint32_t world,
                      const emqx_shard_split* splits, uint32_t n_splits, uint32_t* first, uint32_t* span,
                      uint32_t* engine);

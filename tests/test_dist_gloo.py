@@ -47,10 +47,10 @@ def _oracle_match_fn(engines):
     return fn
 
 
-def _matcher(filters, rank, world):
+def _matcher(filters, rank, world, p_space="auto"):
     from emqx_amd import dist as D
-    plan = D.shard_plan(filters, world)
-    return D.ShardedMatcher(filters, device=torch.device("cpu"),
+    plan = D.shard_plan(filters, world, p_space=p_space)
+    return D.ShardedMatcher(filters, device=torch.device("cpu"), p_space=p_space,
                             match_fn=_oracle_match_fn(D.shard_engines(filters, rank, world, plan)))
 
 
@@ -133,14 +133,14 @@ def test_sharded_equals_single_table(world, src, dst):
     assert sum(splits) == len(_batches()[1][1]) - 1
 
 
-def _worker_all(rank, world, port, q):
+def _worker_all(rank, world, port, q, p_space):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from emqx_amd import dist as D
         filters, topics = _batches()
-        sm = _matcher(filters, rank, world)
+        sm = _matcher(filters, rank, world, p_space)
         # every rank publishes its own slice (rank 1 of 2+ an empty batch)
         part = D.split_topics(topics, rank, world)
         if rank == 1:
@@ -153,15 +153,17 @@ def _worker_all(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_match_all_sources(world):
+@pytest.mark.parametrize("world,p_space", [(2, "sharded"), (4, "sharded"), (8, "sharded"), (2, "replicated"),
+                                           (8, "replicated")])
+def test_sharded_match_all_sources(world, p_space):
     """ShardedMatcher.match_all: every rank a source of its own batch, each gets its own CSR
-    equal to the single-table oracle's for that batch."""
+    equal to the single-table oracle's for that batch; both space-P layouts (two requests a
+    topic, or space P on every rank and one request a topic)."""
     from oracle import cpp as C
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_all, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_all, args=(r, world, port, q, p_space)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=240) for _ in range(world)]
@@ -187,9 +189,11 @@ def test_shard_layout_covers_every_match():
     off, ids, _ = o.match_csr(*topics, mode=0, threads=4)
     tid = np.repeat(np.arange(len(topics[1]) - 1), np.diff(off.astype(np.int64)))
     names = W_unpack(topics)
-    for world in (1, 2, 3, 8):
-        plan = D.shard_plan(filters, world, max_piece_pm=50)  # small pieces: many split keys
+    for world, p_space in ((1, "auto"), (2, "sharded"), (3, "sharded"), (8, "sharded"), (2, "replicated"),
+                           (8, "replicated")):
+        plan = D.shard_plan(filters, world, max_piece_pm=50, p_space=p_space)  # small pieces: many split keys
         assert world == 1 or len(plan) > 0
+        assert D.plan_p_replicated(plan) == (p_space == "replicated")
         first, span, eng = D.shard_place(filters, world, plan)
         req = D.topic_requests(torch.from_numpy(topics[0]), torch.from_numpy(topics[1].astype(np.int64)), world,
                                plan).numpy()
@@ -208,6 +212,13 @@ def test_shard_layout_covers_every_match():
         for t, rq in zip(names, req):
             if t.startswith(b"$") or b"/" not in t:
                 assert rq[1] == -1, t
+        if p_space == "replicated":  # one request a topic; space P on every rank with engine A
+            assert np.all(req[:, 1] == -1) and np.all(eng == 0)
+            fnames = W_unpack(filters)
+            is_p = np.array([f.startswith(b"+/") and f[2:3] not in (b"+", b"#") for f in fnames])
+            assert is_p.any() and np.all(span[is_p] == world)
+        else:
+            assert world == 1 or (eng == 1).any()
         # the folded keys (rank * 3 + slot): two requests to two ranks stay A and B; to one rank,
         # or a single request, one AB request in the first column; at world 1 only AB
         key = D.fold_requests(torch.from_numpy(req), world).numpy()
@@ -233,13 +244,19 @@ def test_shard_plan_divides_config_c_capacity():
     from emqx_amd import dist as D
     from emqx_amd import workloads as W
     wl = W.config_b(n_filters=400_000, n_topics=10, seed=3, vocab_scale=4)
+    names = W.unpack(wl.filters)
+    p_share = sum(1 for f in names if f.startswith(b"+/") and not f[2:3] in (b"+", b"#", b"")) / wl.n_filters
     for world in (2, 4, 8):
-        plan = D.shard_plan(wl.filters, world)
-        first, span, eng = D.shard_place(wl.filters, world, plan)
-        held = np.zeros(world, np.int64)
-        for k in range(world):
-            held[k] = int(np.count_nonzero(((k - first.astype(np.int64)) % world) < span))
-        assert held.max() / wl.n_filters <= 1.5 / world, (world, held.max() / wl.n_filters)
+        for p_space in ("sharded", "auto"):
+            plan = D.shard_plan(wl.filters, world, p_space=p_space)
+            # auto: space P (~7 % of config C) replicated, at most a rank's share
+            assert D.plan_p_replicated(plan) == (p_space == "auto" and p_share * world <= 1.0)
+            first, span, eng = D.shard_place(wl.filters, world, plan)
+            held = np.zeros(world, np.int64)
+            for k in range(world):
+                held[k] = int(np.count_nonzero(((k - first.astype(np.int64)) % world) < span))
+            bound = 1.5 / world + (p_share if D.plan_p_replicated(plan) else 0.0)
+            assert held.max() / wl.n_filters <= bound, (world, p_space, held.max() / wl.n_filters)
 
 
 def test_partition_and_merge_roundtrip():

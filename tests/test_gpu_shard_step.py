@@ -111,7 +111,7 @@ def test_shard_step_redo_on_small_capacities():
         dist.destroy_process_group()
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, p_space="sharded"):
     import torch
     import torch.distributed as dist
     from emqx_amd import workloads as W
@@ -123,7 +123,7 @@ def _rank_main(rank, world, port, q):
         torch.cuda.set_device(0)
         wl = W.config_b(n_filters=200_000, n_topics=8000, seed=3, vocab_scale=4,
                         topic_seed=None if rank == 0 else 1000 + rank)
-        sm = ShardedMatcher(wl.filters, device=torch.device("cuda:0"))
+        sm = ShardedMatcher(wl.filters, device=torch.device("cuda:0"), p_space=p_space)
         assert sm._step is not None
         # two steps: the second reuses the learnt buffers; a third with an empty batch on rank 1
         sm.match_all(_dev_topics(wl.topics))
@@ -146,16 +146,17 @@ def _rank_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_shard_step_ranks_share_one_gpu(world):
+@pytest.mark.parametrize("world,p_space", [(2, "sharded"), (3, "sharded"), (4, "sharded"), (3, "replicated")])
+def test_shard_step_ranks_share_one_gpu(world, p_space):
     """The device step (emqx_shard_step_*, dist.py _match_all_device) at world 2, 3 and 4 with
     every rank a process on the one GPU (gloo for the exchanges): each rank's CSR ID-for-ID
-    against the oracle over the whole table; a rehearsal of the protocol, not a measurement."""
+    against the oracle over the whole table; a rehearsal of the protocol, not a measurement.
+    Both space-P layouts (dist.py shard_plan)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29565 + world
-    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    port = 29565 + world + (10 if p_space == "replicated" else 0)
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q, p_space)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=200) for _ in range(world)]
@@ -169,7 +170,10 @@ def test_shard_step_ranks_share_one_gpu(world):
     # requests met on one rank (AB slot) and some did not (A and B slots) — both paths ran
     assert all(r[5] < 200_000 for r in res)
     slots = np.sum([r[6] for r in res], axis=0)
-    assert slots[0] > 0 and slots[1] > 0 and slots[2] > 0, slots
+    if p_space == "sharded":
+        assert slots[0] > 0 and slots[1] > 0 and slots[2] > 0, slots
+    else:  # one request a topic, always to the AB slot
+        assert slots[0] == 0 and slots[1] == 0 and slots[2] > 0, slots
 
 
 def test_device_routing_equals_host_routing():
@@ -202,3 +206,39 @@ def test_device_routing_equals_host_routing():
         host = D.topic_requests(tb_c, to_c, world, plan)
         dev = D.topic_requests(tb_c.cuda(), to_c.cuda(), world, plan).cpu()
         assert torch.equal(host, dev), world
+
+
+@pytest.mark.parametrize("world,p_space", [(2, "sharded"), (3, "sharded"), (8, "sharded"), (2, "replicated"),
+                                           (8, "replicated")])
+def test_emulated_world_every_source_id_for_id(world, p_space):
+    """dist.py EmulatedWorld: the G ranks of the G-way plan in this one process, every rank's
+    step the product's _step_gen with chunks read in place; every source's merged CSR ID-for-ID
+    against the oracle over the whole table, in both timing modes and untimed, and the exchange
+    bytes accounted for (every request chunk is at least its header)."""
+    import torch
+    from emqx_amd import workloads as W
+    from emqx_amd.dist import EmulatedWorld
+    dev = torch.device("cuda:0")
+    wl = W.config_b(n_filters=200_000, n_topics=6000, seed=3, vocab_scale=4,
+                    extra_topic_seeds=tuple(1000 + s for s in range(1, world)))
+    srcs = [wl.topics] + list(wl.extra_topics[: world - 1])
+    ew = EmulatedWorld(wl.filters, world, dev, p_space=p_space)
+    assert ew.p_replicated == (p_space == "replicated")
+    try:
+        assert sum(x[2] for x in ew.filters_per_rank) < world * 200_000  # sharded, not replicated
+        for timing in (None, "wall", "gpu", None):
+            res = ew.step([_dev_topics(s) for s in srcs], timing=timing)
+            if timing:
+                assert len(ew.last_times) == world and all(len(t) == len(EmulatedWorld.PHASES) for t in ew.last_times)
+                assert all(x >= 0 for t in ew.last_times for x in t)
+            for s in range(world):
+                _check(res[s], wl.filters, srcs[s])
+        assert (ew.bytes_out[0] >= 32).all() and (ew.bytes_out[1] >= 32).all()
+        slots = np.sum([m.last_slot_topics for m in ew.matchers], axis=0)
+        if p_space == "sharded":
+            assert slots[0] > 0 and slots[1] > 0 and slots[2] > 0, slots
+        else:
+            assert slots[0] == 0 and slots[1] == 0 and slots[2] > 0, slots
+            assert all(m.engines[0] is None and m.engines[1] is None for m in ew.matchers)
+    finally:
+        ew.close()
