@@ -1273,6 +1273,8 @@ def fanout_bench(args, rank, world, dev):
     eng.insert_packed(*fw.wl.filters)
     eng.commit()
     st = SubTable(dev.index)
+    if args.strategy == "round_robin":  # SURVEY §8 d: config E's round_robin has its counter seeded 0
+        st.set_tuning("rr_seed0", 1)
     st.add(fw.sub_filter, fw.sub_id, fw.sub_group)
     st.commit()
     log(f"[rank {rank}] subtab {st.stats()}")
@@ -1376,11 +1378,52 @@ def fanout_bench(args, rank, world, dev):
         res["cpu_baseline"] = fanout_cpu_baseline(fw, args, gpu)
         if "parity" in res["cpu_baseline"]:
             res["parity"] = res["cpu_baseline"].pop("parity")
+        if args.strategy == "round_robin":
+            res["parity"] = round_robin_parity(fw, args, st, moff, mids, keys, ooff, osubs, ofil, ocap, stream, n)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def round_robin_parity(fw, args, st, moff, mids, keys, ooff, osubs, ofil, ocap, stream, n):
+    """Config E's round_robin pick by pick: the round_robin state of every
+    publisher forgotten on the device, then two fan-out calls over the batch's match CSR (the
+    second continues the state of the first), each against the oracle's restatement of
+    do_pick_subscriber/6 with the counter seeded 0 (oracle/fanout_oracle.cpp
+    orf_publish_list_rr; apps/emqx/src/emqx_shared_sub.erl:265-285) run over the oracle's own
+    match of the same topics: every (subscriber, filter | shared) delivery of every topic, as a
+    per-topic multiset (oracle/cpp.py pair_csr_mismatches)."""
+    from emqx_amd import workloads as W
+    from oracle import cpp as C
+    k = min(args.cpu_sample, n)
+    o = C.CppOracle(True)
+    with progress("E round_robin parity: building the oracle table"):
+        o.add_packed(*fw.wl.filters)
+        o.freeze()
+    m_off, m_ids, _ = o.match_csr(*W.take(fw.wl.topics, np.arange(k)), mode=0, threads=host_threads()[0])
+    fo = C.FanoutOracle(fw.sub_filter, fw.sub_id, fw.sub_group)
+    st.forget_publishers(np.unique(fw.keys))
+    nm = int(moff[k].item())
+    bad, checked, picks = [], 0, 0
+    for call in range(2):
+        nd = st.fanout_device("round_robin", moff.data_ptr(), mids.data_ptr(), k, keys.data_ptr(), ooff.data_ptr(),
+                              osubs.data_ptr(), ofil.data_ptr(), ocap, stream=stream)
+        off_g = ooff[: k + 1].cpu().numpy().view(np.uint64)
+        subs_g = osubs[:nd].cpu().numpy().view(np.uint32)
+        fils_g = ofil[:nd].cpu().numpy().view(np.uint32)
+        off_o, subs_o, fils_o = fo.publish_list(m_off, m_ids, fw.keys[:k], round_robin=True)
+        bad.append(int(C.pair_csr_mismatches(off_g, subs_g, fils_g, off_o, subs_o, fils_o).size))
+        checked += int(nd)
+        picks += int(np.count_nonzero(fils_o & np.uint32(0x80000000)))
+    res = {"rule": "round_robin (counter seeded 0) pick by pick: every (subscriber, filter|shared) delivery per "
+                   "topic vs oracle/fanout_oracle.cpp orf_publish_list_rr, two calls carrying the state",
+           "topics_checked": int(k), "calls": 2, "match_ids": nm, "deliveries_checked": checked,
+           "share_picks_checked": picks, "mismatches": int(sum(bad)), "mismatches_per_call": bad}
+    if sum(bad):
+        raise SystemExit(f"round_robin fan-out differs from the oracle: {bad}")
+    return res
 
 
 def fanout_roofline(fo_ms, nm, nd, n, args):

@@ -339,6 +339,7 @@ struct emqx_subtab {
   std::vector<std::unique_ptr<FoScratch>> scratch;  // one per stream that called
   uint64_t* h_total = nullptr;
   uint32_t seed = 0x2545F491u;
+  uint32_t rr_first0 = 0;  // emqx_subtab_set_tuning "rr_seed0"
   // commit statistics (emqx_subtab_commit_stats)
   uint64_t st_commits = 0, st_full = 0, st_words = 0, st_records = 0, st_moves = 0, st_last_kind = 0;
   double st_host_us = 0, st_total_us = 0;
@@ -1340,6 +1341,7 @@ int enqueue_fanout(emqx_subtab* s, uint32_t strategy, const uint64_t* d_moff, co
   a.strategy = strategy;
   s->seed = s->seed * 1664525u + 1013904223u;
   a.seed = s->seed;
+  a.rr_first0 = s->rr_first0;
   a.entry_topic = c->entry_topic;
   a.csum = c->csum;
   a.gchunk = c->gchunk;
@@ -1927,6 +1929,8 @@ int emqx_subtab_set_tuning(emqx_subtab* s, const char* key, int64_t value) {
     s->inject_drain_error = static_cast<uint32_t>(value);
   } else if (!std::strcmp(key, "inject_bad_alloc")) {
     s->inject_bad_alloc = static_cast<uint32_t>(value);
+  } else if (!std::strcmp(key, "rr_seed0")) {  // round_robin's first pick: member 0 (SURVEY §8 d)
+    s->rr_first0 = value ? 1u : 0u;
   } else {
     return EMQX_ENOTFOUND;
   }
@@ -2028,6 +2032,7 @@ int emqx_share_repick(emqx_subtab* s, uint32_t strategy, uint64_t n, const uint3
   a.strategy = strategy;
   s->seed = s->seed * 1664525u + 1013904223u;
   a.seed = s->seed;
+  a.rr_first0 = s->rr_first0;
   a.n = n;
   a.filter_ids = reinterpret_cast<const uint32_t*>(d + o_f);
   a.group_ids = reinterpret_cast<const uint32_t*>(d + o_g);

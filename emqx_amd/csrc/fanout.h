@@ -140,6 +140,8 @@ struct FanoutArgs {
   const uint32_t* keys;      // per topic: phash2 key (hash strategies) / publisher (rr, sticky), or null
   uint32_t strategy;         // EMQX_SHARE_*
   uint32_t seed;             // per-call seed of random picks
+  uint32_t rr_first0;        // round_robin's first pick of a state entry is member 0 (SURVEY §8 d's
+                             // "counter seeded 0"), not rand:uniform(N) (emqx_subtab "rr_seed0")
   uint32_t* entry_topic;     // [m] scratch: entry -> topic
   uint64_t* csum;            // [m_cap / FO_WCHUNK + 2] deliveries per chunk of FO_WCHUNK entries
   uint64_t* gchunk;          // [m_cap / FO_WCHUNK + 2] $share picks per chunk (round_robin / sticky)
@@ -207,6 +209,7 @@ struct RepickArgs {
   uint64_t ps_mask;
   uint32_t strategy;
   uint32_t seed;
+  uint32_t rr_first0;            // as FanoutArgs
   uint64_t n;
   const uint32_t* filter_ids;   // [n]
   const uint32_t* group_ids;    // [n]

@@ -557,7 +557,7 @@ __device__ __forceinline__ uint32_t rr_step(const FanoutArgs& a, const GroupRec&
                                             uint32_t ent) {
   const uint32_t n = g.n_members;
   if (n <= 1) return a.members[g.member_begin];
-  *val = *val == PS_NOVAL ? fo_rand(a.seed, pos, ent) % n : (*val + 1) % n;
+  *val = *val == PS_NOVAL ? (a.rr_first0 ? 0u : fo_rand(a.seed, pos, ent) % n) : (*val + 1) % n;
   return a.members[g.member_begin + *val];
 }
 
@@ -606,7 +606,8 @@ __global__ __launch_bounds__(FO_THREADS) void fanout_resolve_heads_kernel(Fanout
     uint32_t val = a.ps_vals[ent];
     if (!sticky) {
       const uint32_t n = g.n_members;
-      const uint32_t first = n <= 1 ? 0u : (val == PS_NOVAL ? fo_rand(a.seed, pos, ent) % n : (val + 1) % n);
+      const uint32_t first =
+          n <= 1 ? 0u : (val == PS_NOVAL ? (a.rr_first0 ? 0u : fo_rand(a.seed, pos, ent) % n) : (val + 1) % n);
       a.seg[k] = static_cast<unsigned long long>(i) | (static_cast<unsigned long long>(first) << 32);
       continue;
     }
@@ -854,7 +855,7 @@ __global__ __launch_bounds__(64) void share_repick_kernel(RepickArgs a) {
             if (lane == 0) {
               uint32_t last = PS_NOVAL;
               const uint64_t ent = rp_entry(a, skey, &last);
-              idx = last == PS_NOVAL ? fo_rand(a.seed, r, g.slot) % count : (last + 1) % count;
+              idx = last == PS_NOVAL ? (a.rr_first0 ? 0u : fo_rand(a.seed, r, g.slot) % count) : (last + 1) % count;
               if (ent != PS_EMPTY) rp_store(a, ent, idx);
             }
             idx = __shfl(idx, 0, 64);

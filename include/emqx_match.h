@@ -293,7 +293,10 @@ int emqx_subtab_commit(emqx_subtab* s);
 int emqx_subtab_commit_wait(emqx_subtab* s);
 /* Fault injection for tests: "inject_drain_error" = the next `value` waits for a commit's
  * device half report EMQX_EDEVICE; "inject_bad_alloc" = the next `value` full commits fail
- * their host allocations (the call returns EMQX_ENOMEM).  EMQX_ENOTFOUND for unknown keys. */
+ * their host allocations (the call returns EMQX_ENOMEM).  "rr_seed0" = 1: round_robin's first pick
+ * of a (group, publisher) state entry is the first member instead of rand:uniform(N) (SURVEY §8 d's
+ * config E: "round_robin with counter seeded 0"; deterministic, so checked pick by pick).
+ * EMQX_ENOTFOUND for unknown keys. */
 int emqx_subtab_set_tuning(emqx_subtab* s, const char* key, int64_t value);
 /* counts[0..3] = live plain subscriptions, live shared memberships, groups with members,
  * device bytes */

@@ -51,6 +51,8 @@ def lib():
         L.orf_publish.argtypes = [vp, u64p, u32p, ctypes.c_uint64, u32p, ctypes.c_int, u32p, u64p]
         L.orf_checksum.argtypes = [u64p, u32p, u32p, ctypes.c_uint64, u64p]
         L.orf_publish_list.argtypes = [vp, u64p, u32p, ctypes.c_uint64, u32p, ctypes.c_int, u64p, u32p, u32p]
+        L.orf_publish_list_rr.argtypes = [vp, u64p, u32p, ctypes.c_uint64, u32p, u64p, u32p, u32p]
+        L.orf_rr_reset.argtypes = [vp]
         L.orf_churn.restype = ctypes.c_uint64
         L.orf_churn.argtypes = [vp, u32p, u32p, u32p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
         L.orc_topic_match.restype = ctypes.c_int
@@ -168,9 +170,10 @@ class FanoutOracle:
                                   _p(counts), _p(sums))
         return counts[:n], sums[:n], int(total)
 
-    def publish_list(self, moff, mids, keys, threads=1):
+    def publish_list(self, moff, mids, keys, threads=1, round_robin=False):
         """Deliveries listed: (offsets[n+1], subscribers, filters | SHARED_BIT), route order per
-        topic (oracle/fanout_oracle.cpp orf_publish_list)."""
+        topic (oracle/fanout_oracle.cpp orf_publish_list; round_robin: orf_publish_list_rr, the
+        counter seeded 0, state kept over calls until ``rr_reset``)."""
         counts, _, total = self.publish(moff, mids, keys, threads)
         moff = np.ascontiguousarray(np.asarray(moff, dtype=np.uint64))
         mids = np.ascontiguousarray(np.asarray(mids, dtype=np.uint32))
@@ -180,9 +183,17 @@ class FanoutOracle:
         off[1:] = np.cumsum(counts, dtype=np.uint64)
         subs = np.zeros(max(total, 1), np.uint32)
         fils = np.zeros(max(total, 1), np.uint32)
-        lib().orf_publish_list(self.h, _p(moff), _p(mids) if mids.size else None, n, _p(keys), threads, _p(off),
-                               _p(subs), _p(fils))
+        if round_robin:
+            lib().orf_publish_list_rr(self.h, _p(moff), _p(mids) if mids.size else None, n, _p(keys), _p(off),
+                                      _p(subs), _p(fils))
+        else:
+            lib().orf_publish_list(self.h, _p(moff), _p(mids) if mids.size else None, n, _p(keys), threads, _p(off),
+                                   _p(subs), _p(fils))
         return off, subs[:total], fils[:total]
+
+    def rr_reset(self):
+        """Forgets every publisher's round_robin state (orf_rr_reset)."""
+        lib().orf_rr_reset(self.h)
 
     def churn(self, sub_filter, sub_id, sub_group, add, threads=1) -> int:
         """Subscribe (add) / unsubscribe operations as the reference's ETS bags take them

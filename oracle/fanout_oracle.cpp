@@ -9,7 +9,10 @@
 //   apps/emqx/src/emqx_shared_sub.erl:113-126,251-288  dispatch/pick: one member per $share
 //       group of a matched filter; for hash_clientid / hash_topic the member is
 //       lists:nth(1 + Key rem N, Members), Members in subscription order (ETS bag order,
-//       :287-288), Key = the caller's erlang:phash2 value (not restated).
+//       :287-288), Key = the caller's erlang:phash2 value (not restated);
+//       round_robin (:279-285) with the counter seeded 0 (SURVEY §8 d, config E): per (publisher,
+//       group, filter) the first pick is member 1, each later one (Last + 1) rem N, in message
+//       order; a one-member group is picked without touching the state (:265).
 // Per topic it reports the delivery count and an order-free checksum of its deliveries
 // (sum of mix(sub, filter | shared bit)), so a multiset comparison with the GPU's CSR needs no
 // sort.  orf_churn applies subscribe / unsubscribe operations as the reference's tables take
@@ -26,6 +29,7 @@
 #include <atomic>
 #include <cstdint>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -38,9 +42,22 @@ struct Group {
   std::vector<uint32_t> members;  // subscription order
 };
 
+struct RrKey {
+  uint64_t fil_group;  // filter << 32 | group id
+  uint32_t publisher;
+  bool operator==(const RrKey& o) const { return fil_group == o.fil_group && publisher == o.publisher; }
+};
+struct RrHash {
+  size_t operator()(const RrKey& k) const {
+    uint64_t x = k.fil_group * 0x9E3779B97F4A7C15ULL ^ (uint64_t(k.publisher) * 0xC2B2AE3D27D4EB4FULL);
+    return static_cast<size_t>(x ^ (x >> 29));
+  }
+};
+
 struct Fanout {
   std::vector<std::vector<uint32_t>> plain;  // per filter id
   std::vector<std::vector<Group>> groups;    // per filter id, groups in first-subscription order
+  std::unordered_map<RrKey, uint32_t, RrHash> rr;  // round_robin: the publisher's Last index (0-based)
 };
 
 inline uint64_t mix(uint32_t sub, uint32_t fil) {
@@ -157,6 +174,40 @@ void orf_publish_list(void* h, const uint64_t* moff, const uint32_t* mids, uint6
   }
   for (auto& x : th) x.join();
 }
+
+// round_robin with the counter seeded 0, deliveries listed as orf_publish_list (route order per
+// topic); keys[t] = the publishing process.  Message order is the batch order, so one thread; the
+// state persists over calls (orf_rr_reset clears it).
+void orf_publish_list_rr(void* h, const uint64_t* moff, const uint32_t* mids, uint64_t n, const uint32_t* keys,
+                         const uint64_t* out_off, uint32_t* out_subs, uint32_t* out_fils) {
+  Fanout* f = static_cast<Fanout*>(h);
+  for (uint64_t t = 0; t < n; ++t) {
+    uint64_t at = out_off[t];
+    for (uint64_t j = moff[t]; j < moff[t + 1]; ++j) {
+      const uint32_t fid = mids[j];
+      if (fid >= f->plain.size()) continue;
+      for (uint32_t sb : f->plain[fid]) {
+        out_subs[at] = sb;
+        out_fils[at++] = fid;
+      }
+      for (const Group& g : f->groups[fid]) {
+        const uint32_t cnt = static_cast<uint32_t>(g.members.size());
+        if (!cnt) continue;
+        uint32_t idx = 0;
+        if (cnt > 1) {
+          const RrKey k{(uint64_t(fid) << 32) | g.id, keys[t]};
+          auto it = f->rr.find(k);
+          idx = it == f->rr.end() ? 0u : (it->second + 1) % cnt;
+          f->rr[k] = idx;
+        }
+        out_subs[at] = g.members[idx];
+        out_fils[at++] = fid | SHARED_BIT;
+      }
+    }
+  }
+}
+
+void orf_rr_reset(void* h) { static_cast<Fanout*>(h)->rr.clear(); }
 
 // Subscribe (add = 1) / unsubscribe (add = 0) operations, in order per filter.  Returns the
 // operations that changed the table.

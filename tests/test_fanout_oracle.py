@@ -206,3 +206,52 @@ def test_cleanup_down_removes_memberships_and_empty_group_routes():
     assert b.shared.subscribers(b"g", b"t/+") == [] and b.shared.subscribers(b"h", b"u/#") == ["B"]
     assert b.publish(b"t/1", 0, B.HASH_CLIENTID) == []
     assert b.publish(b"u/1", 0, B.HASH_CLIENTID) == [(b"u/#", "B", True)]
+
+
+def test_cpp_round_robin_equals_shared_sub_restatement():
+    """oracle/fanout_oracle.cpp orf_publish_list_rr (bench.py's pick-exact check of config E's
+    round_robin, counter seeded 0) against broker_ref.SharedSub.pick_subscriber (the restatement
+    of emqx_shared_sub.erl:265-285) with the first draw 0: the picks of every message, over two
+    calls that carry the state, on random groups of 1-5 members and a few publishers."""
+    import numpy as np
+    from oracle import cpp as C
+    rng = np.random.default_rng(11)
+    nf, rows = 40, []
+    for f in range(nf):
+        for s in rng.choice(50, size=int(rng.integers(0, 3)), replace=False):
+            rows.append((f, int(s), 0xFFFFFFFF))
+        for g in range(int(rng.integers(0, 3))):
+            for s in rng.choice(50, size=int(rng.integers(1, 6)), replace=False):
+                rows.append((f, 100 + int(s), g))
+    filt, sub, grp = (np.array(x, np.uint32) for x in zip(*rows))
+    fo = C.FanoutOracle(filt, sub, grp)
+    ss = B.SharedSub()
+    for f, s, g in rows:
+        if g != 0xFFFFFFFF:
+            ss.subscribe(g, f, s)
+    n = 300
+    counts = rng.integers(0, 4, size=n)
+    moff = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    mids = rng.integers(0, nf, size=int(moff[-1])).astype(np.uint32)
+    keys = rng.integers(0, 3, size=n).astype(np.uint32)  # three publishers
+    for call in range(2):
+        off, subs, fils = fo.publish_list(moff, mids, keys, round_robin=True)
+        for t in range(n):
+            want = []
+            for j in range(int(moff[t]), int(moff[t + 1])):
+                f = int(mids[j])
+                want += [(s, f) for ff, s, g in rows if ff == f and g == 0xFFFFFFFF]
+                groups = []
+                for ff, s, g in rows:
+                    if ff == f and g != 0xFFFFFFFF and g not in groups:
+                        groups.append(g)
+                for g in groups:
+                    members = ss.subscribers(g, f)
+                    pick = ss.pick_subscriber(g, f, B.ROUND_ROBIN, int(keys[t]), members, lambda c: 0)
+                    want.append((pick, f | 0x80000000))
+            got = list(zip(subs[int(off[t]):int(off[t + 1])].tolist(), fils[int(off[t]):int(off[t + 1])].tolist()))
+            assert got == want, (call, t)
+    fo.rr_reset()
+    off2, subs2, _ = fo.publish_list(moff, mids, keys, round_robin=True)
+    ss.rr.clear()
+    assert subs2.size == subs.size

@@ -381,3 +381,53 @@ def test_config_e_full_size_id_for_id(F):
     bad = C.pair_csr_mismatches(oo, osubs.cpu().numpy().view(np.uint32), ofil.cpu().numpy().view(np.uint32),
                                 off_d, subs_d, fils_d)
     assert bad.size == 0, bad[:10]
+
+
+@pytest.mark.parametrize("publishers", [1, 3, 5000])
+def test_round_robin_seeded_zero_pick_exact(F, publishers):
+    """emqx_subtab "rr_seed0" (SURVEY §8 d: config E's round_robin, counter seeded 0): every pick of
+    two consecutive calls (the state carried over) equals the oracle's restatement of
+    do_pick_subscriber/6 (oracle/fanout_oracle.cpp orf_publish_list_rr, itself checked against
+    broker_ref in tests/test_fanout_oracle.py) — one publisher (one long run per group: the
+    large resolve path), a few, and many (short runs); forgetting the publishers restarts them."""
+    import torch
+    from oracle import cpp as C
+    rng = np.random.default_rng(publishers)
+    nf, rows = 3000, []
+    for f in range(nf):
+        for s in rng.choice(100_000, size=int(rng.integers(0, 4)), replace=False):
+            rows.append((f, int(s), 0xFFFFFFFF))
+        for g in range(int(rng.integers(0, 3))):
+            for s in rng.choice(100_000, size=int(rng.integers(1, 17)), replace=False):
+                rows.append((f, int(s), g))
+    filt, sub, grp = (np.array(x, np.uint32) for x in zip(*rows))
+    st = F.SubTable(0)
+    st.set_tuning("rr_seed0", 1)
+    st.add(filt, sub, grp)
+    st.commit()
+    fo = C.FanoutOracle(filt, sub, grp)
+    n = 20_000
+    counts = rng.integers(0, 6, size=n)
+    moff = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    mids = rng.integers(0, nf, size=int(moff[-1])).astype(np.uint32)
+    keys = rng.integers(0, publishers, size=n).astype(np.uint32)
+    dev = torch.device("cuda:0")
+    d_moff = torch.from_numpy(moff.view(np.int64)).to(dev)
+    d_mids = torch.from_numpy(mids.view(np.int32)).to(dev)
+    d_keys = torch.from_numpy(keys.view(np.int32)).to(dev)
+    cap = 64 * n
+    ooff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    osubs = torch.empty(cap, dtype=torch.int32, device=dev)
+    ofil = torch.empty(cap, dtype=torch.int32, device=dev)
+    for call in range(3):
+        if call == 2:  # forgotten: both sides start again from the first member
+            st.forget_publishers(np.unique(keys))
+            fo.rr_reset()
+        nd = st.fanout_device("round_robin", d_moff.data_ptr(), d_mids.data_ptr(), n, d_keys.data_ptr(),
+                              ooff.data_ptr(), osubs.data_ptr(), ofil.data_ptr(), cap)
+        off_o, subs_o, fils_o = fo.publish_list(moff, mids, keys, round_robin=True)
+        assert nd == len(subs_o)
+        bad = C.pair_csr_mismatches(ooff.cpu().numpy().view(np.uint64), osubs[:nd].cpu().numpy().view(np.uint32),
+                                    ofil[:nd].cpu().numpy().view(np.uint32), off_o, subs_o, fils_o)
+        assert bad.size == 0, (call, bad[:10])
+    st.close()
