@@ -299,6 +299,7 @@ __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restric
 // read as 16-B vectors, every load of a round issued before any is used; the tables are padded
 // past the last chunk, the padding masked off).
 constexpr uint32_t kScanThreads = 1024;
+constexpr uint32_t kOneBlockScan = 8192;  // table entries up to which one block scans it (below: 3 kernels)
 __global__ __launch_bounds__(kScanThreads) void shard_sort_scan_kernel(uint32_t* __restrict__ tcnt,
                                                                        const uint32_t* __restrict__ tbytes,
                                                                        uint64_t* __restrict__ pbytes, uint32_t nb,
@@ -382,6 +383,152 @@ __global__ __launch_bounds__(kScanThreads) void shard_sort_scan_kernel(uint32_t*
   if (tid == kScanThreads - 1) {
     start[nb] = static_cast<uint32_t>(m);
     bpre[nb] = xb;  // (the no-request bucket is last and holds no bytes)
+  }
+}
+
+// The same prefixes over many blocks (a table of kE G + 1 buckets x ntiles tiles grows with the
+// world: 98 K entries at world 8 for 1 M topics, 166 us in the one-block kernel above): segments of
+// kScanSeg entries; per segment its totals, one block scans the segment totals, then each segment
+// is scanned from its base.
+constexpr uint32_t kScanSeg = 2048;  // table entries per block: 8 per thread
+constexpr uint32_t kScanPer = kScanSeg / 256;
+
+// Block-wide exclusive scan of (c, b) pairs over 256 threads; returns this thread's prefixes and
+// the block's totals.
+__device__ __forceinline__ void block_scan2(uint64_t c, uint64_t b, uint64_t* xc, uint64_t* xb, uint64_t* tc,
+                                            uint64_t* tb) {
+  __shared__ uint64_t wc[4], wb[4];
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  uint64_t ic = c, ib = b;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t yc = __shfl_up(ic, d, 64), yb = __shfl_up(ib, d, 64);
+    if (lane >= d) {
+      ic += yc;
+      ib += yb;
+    }
+  }
+  if (lane == 63) {
+    wc[w] = ic;
+    wb[w] = ib;
+  }
+  __syncthreads();
+  uint64_t bc = 0, bb = 0, ac = 0, ab = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    if (k < w) {
+      bc += wc[k];
+      bb += wb[k];
+    }
+    ac += wc[k];
+    ab += wb[k];
+  }
+  *xc = bc + ic - c;
+  *xb = bb + ib - b;
+  *tc = ac;
+  *tb = ab;
+}
+
+// A thread's kScanPer consecutive entries from i (16-B loads; entries at or past N read as 0: the
+// tables are padded by a segment's worth past the last tile).
+__device__ __forceinline__ void load_seg(const uint32_t* __restrict__ tcnt, const uint32_t* __restrict__ tbytes,
+                                         uint32_t i, uint32_t N, uint32_t (&vc)[kScanPer], uint32_t (&vb)[kScanPer]) {
+  const uint4* pc = reinterpret_cast<const uint4*>(tcnt + i);
+  const uint4* pb = reinterpret_cast<const uint4*>(tbytes + i);
+#pragma unroll
+  for (uint32_t q = 0; q < kScanPer / 4; ++q) {
+    const uint4 c4 = pc[q], b4 = pb[q];
+    const uint32_t cc[4] = {c4.x, c4.y, c4.z, c4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const bool in = i + 4 * q + k < N;
+      vc[4 * q + k] = in ? cc[k] : 0u;
+      vb[4 * q + k] = in ? bb[k] : 0u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void shard_seg_sums_kernel(const uint32_t* __restrict__ tcnt,
+                                                             const uint32_t* __restrict__ tbytes, uint32_t N,
+                                                             uint64_t* __restrict__ seg) {
+  const uint32_t i = blockIdx.x * kScanSeg + threadIdx.x * kScanPer;
+  uint32_t vc[kScanPer], vb[kScanPer];
+  uint64_t c = 0, b = 0;
+  if (i < N) {
+    load_seg(tcnt, tbytes, i, N, vc, vb);
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; ++j) {
+      c += vc[j];
+      b += vb[j];
+    }
+  }
+  uint64_t xc, xb, tc, tb;
+  block_scan2(c, b, &xc, &xb, &tc, &tb);
+  if (threadIdx.x == 0) {
+    seg[2 * blockIdx.x] = tc;
+    seg[2 * blockIdx.x + 1] = tb;
+  }
+}
+
+// One block: the segment totals -> exclusive prefixes, in place (any number of segments).
+__global__ __launch_bounds__(256) void shard_seg_scan_kernel(uint64_t* __restrict__ seg, uint32_t nseg) {
+  const uint32_t per = (nseg + 255) / 256;
+  const uint32_t s0 = min(nseg, threadIdx.x * per), s1 = min(nseg, s0 + per);
+  uint64_t c = 0, b = 0;
+  for (uint32_t k = s0; k < s1; ++k) {
+    c += seg[2 * k];
+    b += seg[2 * k + 1];
+  }
+  uint64_t xc, xb, tc, tb;
+  block_scan2(c, b, &xc, &xb, &tc, &tb);
+  for (uint32_t k = s0; k < s1; ++k) {
+    const uint64_t vc = seg[2 * k], vb = seg[2 * k + 1];
+    seg[2 * k] = xc;
+    seg[2 * k + 1] = xb;
+    xc += vc;
+    xb += vb;
+  }
+}
+
+// Each segment from its base: counts in place, byte prefixes into pbytes, the bucket starts at
+// every multiple of ntiles, and (block of entry N - 1) start[nb] = m, bpre[nb] = the byte total.
+__global__ __launch_bounds__(256) void shard_seg_final_kernel(uint32_t* __restrict__ tcnt,
+                                                              const uint32_t* __restrict__ tbytes,
+                                                              uint64_t* __restrict__ pbytes, uint32_t N,
+                                                              uint32_t ntiles, uint32_t nb, uint64_t m,
+                                                              const uint64_t* __restrict__ seg,
+                                                              uint32_t* __restrict__ start,
+                                                              uint64_t* __restrict__ bpre) {
+  const uint32_t i = blockIdx.x * kScanSeg + threadIdx.x * kScanPer;
+  uint32_t vc[kScanPer], vb[kScanPer];
+  uint64_t c = 0, b = 0;
+  if (i < N) {
+    load_seg(tcnt, tbytes, i, N, vc, vb);
+#pragma unroll
+    for (uint32_t j = 0; j < kScanPer; ++j) {
+      c += vc[j];
+      b += vb[j];
+    }
+  }
+  uint64_t xc, xb, tc, tb;
+  block_scan2(c, b, &xc, &xb, &tc, &tb);
+  xc += seg[2 * blockIdx.x];
+  xb += seg[2 * blockIdx.x + 1];
+  if (i >= N) return;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) {
+    const uint32_t e = i + j;
+    if (e >= N) break;
+    if (e % ntiles == 0) {  // a bucket's first tile: its first request and first byte
+      start[e / ntiles] = static_cast<uint32_t>(xc);
+      bpre[e / ntiles] = xb;
+    }
+    tcnt[e] = static_cast<uint32_t>(xc);
+    pbytes[e] = xb;
+    xc += vc[j];
+    xb += vb[j];
+    if (e == N - 1) {
+      start[nb] = static_cast<uint32_t>(m);
+      bpre[nb] = xb;  // (the no-request bucket is last and holds no bytes)
+    }
   }
 }
 
@@ -588,23 +735,41 @@ __device__ __forceinline__ uint32_t offs_words(const uint32_t* n, uint32_t e) {
   return w;
 }
 
-// grid (x, source, slot): the source's offsets rebased into the slot's batch (its bytes are one
-// contiguous region each, moved by the copy engine: emqx_shard_step_recv).
+// grid (x, source, slot): the source's offsets rebased into the slot's batch, and its bytes (one
+// contiguous region per (source, slot) on both sides) moved into the slot's byte buffer — one
+// launch for every source, where one copy-engine call per source cost ~5 us each.  A slot read in
+// place (one source: bytes.p[e] null) moves no bytes.
 struct SlotOffsets {
   uint64_t* p[kE];
 };
+struct SlotBytes {
+  uint8_t* p[kE];
+};
 
-__global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOffsets dst_off) {
+__global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOffsets dst_off, SlotBytes dst_bytes) {
   const uint32_t s = blockIdx.y, e = blockIdx.z;
-  uint32_t nq[kE];
-  for (uint32_t k = 0; k < kE; ++k) nq[k] = tab.q0[k][s + 1] - tab.q0[k][s];
+  uint32_t nq[kE], nall = 0;
+  uint64_t before = 0;  // this source's bytes of the slots before e
+  for (uint32_t k = 0; k < kE; ++k) {
+    nq[k] = tab.q0[k][s + 1] - tab.q0[k][s];
+    nall += nq[k];
+    before += k < e ? tab.y0[k][s + 1] - tab.y0[k][s] : 0;
+  }
   const uint32_t* offs = reinterpret_cast<const uint32_t*>(tab.chunk[s]) + offs_words(nq, e);
   const uint32_t n = nq[e];
   const uint64_t dbase = tab.y0[e][s];
   uint64_t* doff = dst_off.p[e] + tab.q0[e][s];
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k <= n; k += stride)
-    doff[k] = dbase + offs[k];
+  for (uint64_t k = tid; k <= n; k += stride) doff[k] = dbase + offs[k];
+  if (!dst_bytes.p[e]) return;
+  const uint64_t by = tab.y0[e][s + 1] - dbase;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(tab.chunk[s]) + 4 * kHW + al16(4ull * (nall + kE)) + before;
+  uint8_t* dst = dst_bytes.p[e] + dbase;
+  for (uint64_t j = 16 * tid; j + 16 <= by; j += 16 * stride)
+    *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
+  const uint64_t tail = by & ~15ull;
+  if (tid < by - tail) dst[tail + tid] = src[tail + tid];
 }
 
 // ---- answer -----------------------------------------------------------------------------
@@ -668,8 +833,12 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
     const uint64_t* off = cs.off[e] + q0[e];
     for (uint64_t k = tid; k < nq[e]; k += stride) end[k] = static_cast<uint32_t>(before + off[k + 1] - i0[e]);
     const uint32_t* src = cs.ids[e] + i0[e];
-    if (copy_ids)
-      for (uint64_t j = tid; j < ni[e]; j += stride) ids[j] = src[j];
+    if (copy_ids) {  // 16-B moves (any 4-B alignment), then the last < 4 ids
+      for (uint64_t j = 4 * tid; j + 4 <= ni[e]; j += 4 * stride)
+        *reinterpret_cast<u4u*>(ids + j) = *reinterpret_cast<const u4u*>(src + j);
+      const uint64_t r = ni[e] & ~3ull;
+      if (tid < ni[e] - r) ids[r + tid] = src[r + tid];
+    }
     end += nq[e];
     ids += ni[e];
     before += ni[e];
@@ -729,6 +898,16 @@ __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t*
   }
 }
 
+// c ids from src to dst by the 4 lanes `sub` of a quad: 16-B moves (4 ids a lane, any 4-B
+// alignment), the last < 4 ids one by one.
+__device__ __forceinline__ void quad_copy_ids(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t c,
+                                              uint32_t sub) {
+  uint32_t j = 4 * sub;
+  for (; j + 4 <= c; j += 16) *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
+  const uint32_t r = c & ~3u;  // the ids past the last whole group of 4
+  if (sub < c - r) dst[r + sub] = src[r + sub];
+}
+
 // 4 lanes per topic, in topic order: its first request's ids, then its second's, to the topic's
 // place in the output (the counts, addresses and offsets read coalesced, no dependent chain).
 __global__ __launch_bounds__(256) void shard_merge_kernel(const uint32_t* __restrict__ rq_cnt,
@@ -741,14 +920,8 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(const uint32_t* __rest
     const uint2 c = *reinterpret_cast<const uint2*>(rq_cnt + 2 * t);
     if ((c.x | c.y) == 0) continue;
     const uint64_t dst = out_off[t];
-    if (c.x) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(rq_src[2 * t]);
-      for (uint32_t j = sub; j < c.x; j += 4) out_ids[dst + j] = src[j];
-    }
-    if (c.y) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(rq_src[2 * t + 1]);
-      for (uint32_t j = sub; j < c.y; j += 4) out_ids[dst + c.x + j] = src[j];
-    }
+    if (c.x) quad_copy_ids(reinterpret_cast<const uint32_t*>(rq_src[2 * t]), out_ids + dst, c.x, sub);
+    if (c.y) quad_copy_ids(reinterpret_cast<const uint32_t*>(rq_src[2 * t + 1]), out_ids + dst + c.x, c.y, sub);
   }
 }
 
@@ -776,6 +949,7 @@ struct emqx_shard_step {
   uint32_t *key = nullptr, *key_s = nullptr, *perm = nullptr, *pos = nullptr, *tcnt = nullptr,
            *tcnt_tab = nullptr, *tbytes_tab = nullptr;  // (tab: the sort's (bucket, tile) table)
   uint64_t *partials = nullptr, *pbytes_tab = nullptr, *rq_src = nullptr;  // (pos: merge's rq_cnt)
+  uint64_t* segsum = nullptr;  // the sort scan's segment totals (2 per kScanSeg table entries)
   uint32_t* start = nullptr;  // [kE G + 2]
   uint64_t* cbase = nullptr;  // [G]
   uint64_t* bpre = nullptr;   // [kE G + 2]: each bucket's first byte among the sorted requests'
@@ -795,10 +969,11 @@ void free_scratch(emqx_shard_step* st) {
   for (void* p : {static_cast<void*>(st->key), static_cast<void*>(st->tcnt_tab), static_cast<void*>(st->key_s),
                   static_cast<void*>(st->perm), static_cast<void*>(st->pos),
                   static_cast<void*>(st->tcnt), static_cast<void*>(st->partials),
-                  static_cast<void*>(st->rq_src), static_cast<void*>(st->tbytes_tab), static_cast<void*>(st->pbytes_tab)})
+                  static_cast<void*>(st->rq_src), static_cast<void*>(st->tbytes_tab), static_cast<void*>(st->pbytes_tab),
+                  static_cast<void*>(st->segsum)})
     if (p) (void)hipFree(p);
   st->key = st->tcnt_tab = st->key_s = st->perm = st->pos = st->tcnt = st->tbytes_tab = nullptr;
-  st->partials = st->pbytes_tab = st->rq_src = nullptr;
+  st->partials = st->pbytes_tab = st->rq_src = st->segsum = nullptr;
   st->m_cap = 0;
 }
 
@@ -813,11 +988,12 @@ hipError_t ensure_scratch(emqx_shard_step* st, uint64_t m) {
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(p), std::max<uint64_t>(bytes, 16));
   };
   al(&st->key, 4 * cap);
-  // (+ one scan round of padding: shard_sort_scan_kernel reads whole 16-entry rounds)
+  // (+ padding: the scans read whole 16-entry rounds / 8-entry thread chunks)
   const uint64_t tab = (kE * st->world + 1ull) * ((cap + kSortTile - 1) / kSortTile + 1) + 16;
   al(&st->tcnt_tab, 4 * tab);
   al(&st->tbytes_tab, 4 * tab);
   al(&st->pbytes_tab, 8 * tab);
+  al(&st->segsum, 16 * (tab / kScanSeg + 2));
   al(&st->key_s, 4 * cap);
   al(&st->perm, 4 * cap);
   al(&st->pos, 4 * cap);
@@ -902,8 +1078,18 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
     const uint32_t ntiles = static_cast<uint32_t>((m + kSortTile - 1) / kSortTile);
     hipLaunchKernelGGL(shard_key_kernel, dim3(ntiles), dim3(256), 0, s, d_bytes, d_offsets, n, G, st->d_splits,
                        st->n_splits, st->key, ntiles, st->tcnt_tab, st->tbytes_tab);
-    hipLaunchKernelGGL(shard_sort_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, st->tcnt_tab, st->tbytes_tab,
-                       st->pbytes_tab, nb, ntiles, m, st->start, st->bpre);
+    const uint32_t N = nb * ntiles;
+    if (N <= kOneBlockScan) {
+      hipLaunchKernelGGL(shard_sort_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, st->tcnt_tab, st->tbytes_tab,
+                         st->pbytes_tab, nb, ntiles, m, st->start, st->bpre);
+    } else {
+      const uint32_t nseg = (N + kScanSeg - 1) / kScanSeg;
+      hipLaunchKernelGGL(shard_seg_sums_kernel, dim3(nseg), dim3(256), 0, s, st->tcnt_tab, st->tbytes_tab, N,
+                         st->segsum);
+      hipLaunchKernelGGL(shard_seg_scan_kernel, dim3(1), dim3(256), 0, s, st->segsum, nseg);
+      hipLaunchKernelGGL(shard_seg_final_kernel, dim3(nseg), dim3(256), 0, s, st->tcnt_tab, st->tbytes_tab,
+                         st->pbytes_tab, N, ntiles, nb, m, st->segsum, st->start, st->bpre);
+    }
     hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->bpre, G, d_send, send_cap, d_meta,
                        st->cbase, st->obase, st->dbase, st->err);
     hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_bytes, d_offsets, m, nb,
@@ -962,19 +1148,22 @@ int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, co
   for (uint32_t e = 0; e < kE; ++e) so.p[e] = d_offsets[e];
   uint64_t qall = 0;
   for (uint32_t e = 0; e < kE; ++e) qall += t.q0[e][G];
-  const uint64_t per = qall / (kE * G) + 1;  // offsets per (source, slot)
+  uint64_t yall = 0;
+  for (uint32_t e = 0; e < kE; ++e) yall += t.y0[e][G];
+  // (blocks per (source, slot): its offsets, or its bytes in 16-B moves, whichever is more work)
+  const uint64_t per = std::max<uint64_t>(qall, yall / 16) / (kE * G) + 1;
   const uint32_t x = grid_of(per, 256, std::max<uint32_t>(1, 1024 / G));
-  hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, kE), dim3(256), 0, s, t, so);
+  SlotBytes sb{};
+  for (uint32_t e = 0; e < kE; ++e) sb.p[e] = only[e] >= 0 ? nullptr : d_bytes[e];
+  hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, kE), dim3(256), 0, s, t, so, sb);
   SS_TRY(hipGetLastError());
-  for (uint32_t r = 0; r < G; ++r) {  // each source's slot-0 bytes, slot 1, slot 2: contiguous both sides
+  for (uint32_t r = 0; r < G; ++r) {  // a slot with one source: matched where that source packed it
     uint64_t nall = 0;
     for (uint32_t e = 0; e < kE; ++e) nall += t.q0[e][r + 1] - t.q0[e][r];
     const uint8_t* data = d_chunks[r] + 4 * kHW + al16(4ull * (nall + kE));
     for (uint32_t e = 0; e < kE; ++e) {
-      const uint64_t by = t.y0[e][r + 1] - t.y0[e][r];
       if (only[e] == static_cast<int>(r)) d_bytes[e] = const_cast<uint8_t*>(data);
-      else if (by) SS_TRY(hipMemcpyAsync(d_bytes[e] + t.y0[e][r], data, by, hipMemcpyDeviceToDevice, s));
-      data += by;
+      data += t.y0[e][r + 1] - t.y0[e][r];
     }
   }
   st->have_recv = true;
