@@ -256,7 +256,8 @@ __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ to, uint64_t n, uint32_t world,
                                                         const ShardSplitE* __restrict__ gsp, uint32_t nsp,
                                                         uint32_t* __restrict__ key, uint32_t ntiles,
-                                                        uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tbytes) {
+                                                        uint32_t* __restrict__ tcnt, uint32_t* __restrict__ tbytes,
+                                                        uint32_t one) {
   __shared__ ShardSplitE lsp[kLdsSplits];
   __shared__ uint32_t c_cnt[kMaxBuckets];
   __shared__ uint32_t c_by[kMaxBuckets];  // (a tile's bytes: 512 requests of <= 64 KB topics)
@@ -267,13 +268,14 @@ __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restric
   }
   const ShardSplitE* sp = stage_splits(gsp, nsp, lsp);  // (its barrier covers the clearing)
   const uint64_t lim = n ? to[n] : 0;
-  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * (kSortTile / 2);
-  const uint64_t t1 = min<uint64_t>(n, t0 + kSortTile / 2);
+  const uint32_t tpt = one ? kSortTile : kSortTile / 2;  // topics a tile
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * tpt;
+  const uint64_t t1 = min<uint64_t>(n, t0 + tpt);
   for (uint64_t tr = t0; tr < t1; tr += blockDim.x) {  // block-uniform rows (wave_count is wave-wide)
     const uint64_t t = tr + threadIdx.x;
     if (t >= t1) {
       wave_count(kNone, 0, nb, c_cnt, c_by);
-      wave_count(kNone, 0, nb, c_cnt, c_by);
+      if (!one) wave_count(kNone, 0, nb, c_cnt, c_by);
       continue;
     }
     const uint64_t a = to[t], b = to[t + 1];
@@ -282,8 +284,12 @@ __global__ __launch_bounds__(256) void shard_key_kernel(const uint8_t* __restric
     uint32_t r[2];
     shard_route_levels(tb + a, b - a, L, world, sp, nsp, r);
     const uint2 k = shard_fold(r, world);
-    *reinterpret_cast<uint2*>(key + 2 * t) = k;
     wave_count(k.x, static_cast<uint32_t>(b - a), nb, c_cnt, c_by);
+    if (one) {  // (one request a topic: every request is an AB request, k.y none)
+      key[t] = k.x;
+      continue;
+    }
+    *reinterpret_cast<uint2*>(key + 2 * t) = k;
     wave_count(k.y, static_cast<uint32_t>(b - a), nb, c_cnt, c_by);
   }
   __syncthreads();
@@ -546,7 +552,8 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
                                                                  const int64_t* __restrict__ dbase,
                                                                  const uint32_t* __restrict__ err,
                                                                  uint8_t* __restrict__ send,
-                                                                 uint32_t* __restrict__ key_s, uint32_t* __restrict__ perm) {
+                                                                 uint32_t* __restrict__ key_s, uint32_t* __restrict__ perm,
+                                                                 uint32_t one) {
   __shared__ uint32_t run_c[kMaxBuckets];
   __shared__ uint64_t run_b[kMaxBuckets];
   __shared__ uint32_t w_c[4][kMaxBuckets];
@@ -579,7 +586,7 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
     uint32_t l = 0;
     uint64_t a = 0;
     if (ok && k < nb - 1) {
-      const uint64_t t = p >> 1;
+      const uint64_t t = one ? p : p >> 1;
       a = to[t];
       l = static_cast<uint32_t>(to[t + 1] - a);
     }
@@ -858,17 +865,19 @@ struct SelfIds {
 
 // Per sorted request p: where its answer's ids are (an answer chunk's id region, or this rank's
 // own engine output) and how many, stored at the request's own index perm[p] (2t: a topic's
-// first request, 2t + 1 its second) — the merge then reads them per topic, coalesced.
+// first request, 2t + 1 its second) — the merge then reads them per topic, coalesced.  With one
+// request a topic (`one`: perm[p] = the topic) it goes to 2t and 2t + 1 says none.
 __global__ __launch_bounds__(256) void shard_gather_kernel(ShardTab tab, SelfIds me,
                                                            const uint32_t* __restrict__ key_s,
                                                            const uint32_t* __restrict__ perm,
                                                            const uint32_t* __restrict__ start, uint64_t m,
                                                            uint32_t world, uint32_t* __restrict__ rq_cnt,
-                                                           uint64_t* __restrict__ rq_src) {
+                                                           uint64_t* __restrict__ rq_src, uint32_t one) {
   const uint32_t nreq = start[kE * world];
   for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
        p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint32_t q = perm[p];
+    const uint32_t q = one ? 2 * perm[p] : perm[p];
+    if (one) rq_cnt[q + 1] = 0;
     if (p >= nreq) {
       rq_cnt[q] = 0;
       continue;
@@ -957,7 +966,9 @@ struct emqx_shard_step {
   int64_t* dbase = nullptr;   // [G]: byte base per destination (pack)
   uint32_t* err = nullptr;
   // the step in flight
-  uint64_t n = 0;                       // topics of the last send
+  uint64_t n = 0, m = 0;                // topics and requests of the last send
+  uint32_t one = 0;                     // one request a topic (world 1 or space P replicated):
+                                        // m = n, request p = topic p
   ShardTab recv_tab{};                  // the last recv's per-source table (answer uses it)
   SelfIds self_ids{};                   // the last answer's in-place own ids (merge uses them)
   bool have_recv = false, have_send = false;
@@ -1033,6 +1044,7 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
   st->device = device;
   st->world = world;
   st->n_splits = n_splits;
+  st->one = world == 1 || shard_p_replicated(reinterpret_cast<const ShardSplitE*>(splits), n_splits) ? 1u : 0u;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->d_splits), std::max<uint64_t>(8ull * n_splits, 16));
   if (e == hipSuccess && n_splits)
@@ -1070,14 +1082,14 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
   if (!st || !d_send || !d_meta || (n && (!d_bytes || !d_offsets)) || n >= (1ull << 31)) return EMQX_EINVAL;
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
-  const uint64_t m = 2 * n;
-  SS_TRY(ensure_scratch(st, m));
+  const uint64_t m = st->one ? n : 2 * n;
+  SS_TRY(ensure_scratch(st, 2 * n));  // (the merge's per-topic request pairs: 2 n either way)
   const uint32_t G = st->world;
   if (m) {
     const uint32_t nb = kE * G + 1;
     const uint32_t ntiles = static_cast<uint32_t>((m + kSortTile - 1) / kSortTile);
     hipLaunchKernelGGL(shard_key_kernel, dim3(ntiles), dim3(256), 0, s, d_bytes, d_offsets, n, G, st->d_splits,
-                       st->n_splits, st->key, ntiles, st->tcnt_tab, st->tbytes_tab);
+                       st->n_splits, st->key, ntiles, st->tcnt_tab, st->tbytes_tab, st->one);
     const uint32_t N = nb * ntiles;
     if (N <= kOneBlockScan) {
       hipLaunchKernelGGL(shard_sort_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, st->tcnt_tab, st->tbytes_tab,
@@ -1094,7 +1106,7 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
                        st->cbase, st->obase, st->dbase, st->err);
     hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_bytes, d_offsets, m, nb,
                        ntiles, st->tcnt_tab, st->pbytes_tab, st->bpre, st->obase, st->dbase, st->err, d_send,
-                       st->key_s, st->perm);
+                       st->key_s, st->perm, st->one);
   } else {
     SS_TRY(hipMemsetAsync(st->start, 0, 4ull * (kE * G + 2), s));
     SS_TRY(hipMemsetAsync(st->bpre, 0, 8ull * (kE * G + 2), s));
@@ -1103,6 +1115,7 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
   }
   SS_TRY(hipGetLastError());
   st->n = n;
+  st->m = m;
   st->have_send = true;
   st->have_recv = false;
   return EMQX_OK;
@@ -1210,10 +1223,10 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
-  const uint64_t n = st->n, m = 2 * n;
+  const uint64_t n = st->n, m = st->m;
   if (m) {
     hipLaunchKernelGGL(shard_gather_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, t, st->self_ids, st->key_s,
-                       st->perm, st->start, m, G, st->pos, st->rq_src);
+                       st->perm, st->start, m, G, st->pos, st->rq_src, st->one);
     hipLaunchKernelGGL(shard_topic_counts_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, st->pos, n, st->tcnt);
   }
   SS_TRY(launch_scan(st->tcnt, n, d_out_offsets, st->partials, s));
