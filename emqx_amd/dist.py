@@ -433,6 +433,17 @@ if _SHARD_PROF:
             "%d-%d %.1f" % (k - 1, k, 1e6 * _PROF_SUM[k] / n) for k in range(1, 8))), file=sys.stderr)
 
 
+class _Lane:
+    """One step in flight of a ShardedMatcher: its device step (emqx_shard_step: the in-flight
+    step's scratch), its reused buffers and pinned words, its streams."""
+
+    def __init__(self, step: Optional[_DeviceStep]):
+        self.step = step
+        self.bufs = {}
+        self.stream = None
+        self.stream_b = None
+
+
 class ShardedMatcher:
     """A filter-sharded table over the ranks of a process group (two engines per rank).
 
@@ -493,12 +504,29 @@ class ShardedMatcher:
         self.match_fn = match_fn
         # the device step (emqx_shard_step_*) when this rank's own HIP engines do the matching;
         # an injected match_fn (tests on CPU over gloo) takes the tensor path below
-        self._step = _DeviceStep(self.device, self.world, self.plan) if (
-            self.device.type == "cuda" and self.match_fn == self._engine_match) else None
+        # a lane = the resources of one step in flight (device step object, buffers, streams);
+        # match_stream keeps two steps in flight on two lanes
+        self._lanes = [_Lane(_DeviceStep(self.device, self.world, self.plan) if (
+            self.device.type == "cuda" and self.match_fn == self._engine_match) else None)]
+        self._lane = self._lanes[0]
         self._caps = [1 << 20] * SHARD_ENGINES
-        self._bufs = {}
-        self._stream = None
-        self._stream_b = None
+
+    # (the step's resources are the current lane's)
+    _step = property(lambda self: self._lane.step)
+    _bufs = property(lambda self: self._lane.bufs)
+    _stream = property(lambda self: self._lane.stream, lambda self, v: setattr(self._lane, "stream", v))
+    _stream_b = property(lambda self: self._lane.stream_b, lambda self, v: setattr(self._lane, "stream_b", v))
+
+    def _lane_n(self, k: int) -> "_Lane":
+        while len(self._lanes) <= k:
+            self._lanes.append(_Lane(_DeviceStep(self.device, self.world, self.plan)))
+        return self._lanes[k]
+
+    def close(self):
+        """Frees the device steps (the engines stay with their owner)."""
+        for ln in self._lanes:
+            if ln.step is not None:
+                ln.step.close()
 
     @property
     def n_local_filters(self) -> int:
@@ -598,12 +626,92 @@ class ShardedMatcher:
         except StopIteration as stop:
             return stop.value
 
+    def match_stream(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], exchange: Optional[Callable] = None):
+        """match_all over a sequence of this rank's batches with two steps in flight (device
+        step only): step k + 1's send runs while step k's engines walk, and step k + 1's
+        requests are exchanged, unpacked and handed to its engines before the host waits for
+        step k's answers, so the device always has a walk queued while the host synchronises.
+        Every rank runs the same schedule, so the collectives pair up.  ``exchange``: the
+        exchange-point function (default ``_exchange``: the process group; ``EmulatedWorld``
+        passes a recorded one).  Returns every batch's (offsets, ids)."""
+        assert self._lanes[0].step is not None, "match_stream needs the device step"
+        ex = exchange or self._exchange
+        caller = torch.cuda.current_stream(self.device)
+        lanes = [self._lane_n(0), self._lane_n(1)]
+        for ln in lanes:
+            if ln.stream is None:
+                ln.stream = torch.cuda.Stream(device=self.device)
+            ln.stream.wait_stream(caller)
+        K = len(batches)
+        gens, ops, res = {}, {}, [None] * K
+
+        def on_lane(k, fn):
+            self._lane = lanes[k % 2]
+            with torch.cuda.stream(self._lane.stream):
+                return fn()
+
+        def adv(k, value):
+            def seg():
+                try:
+                    return next(gens[k]) if value is None else gens[k].send(value)
+                except StopIteration as stop:
+                    return ("done", stop.value)
+            ops[k] = on_lane(k, seg)
+
+        def start(k):  # the send
+            gens[k] = self._step_gen(batches[k])
+            adv(k, None)
+
+        def to_answer(k):  # up to the answers' sizes: recv, engines, answer enqueued
+            seen = 0
+            while ops[k][0] != "done":
+                if ops[k][0] in ("sizes", "local_sizes"):
+                    seen += 1
+                    if seen == 2:
+                        return
+                op = ops[k]
+                adv(k, on_lane(k, lambda: ex(op)))
+
+        def finish(k):  # the answers exchanged and merged
+            while ops[k][0] != "done":
+                op = ops[k]
+                adv(k, on_lane(k, lambda: ex(op)))
+            res[k] = ops.pop(k)[1]
+            del gens[k]
+
+        try:
+            if K:
+                start(0)
+                to_answer(0)
+            if K > 1:
+                start(1)
+            for k in range(K):
+                if k + 1 < K:
+                    to_answer(k + 1)
+                finish(k)
+                if k + 2 < K:
+                    start(k + 2)
+        finally:
+            self._lane = self._lanes[0]
+        for ln in lanes:
+            caller.wait_stream(ln.stream)
+        for r in res:
+            for t in r:
+                t.record_stream(caller)
+        return res
+
     def _exchange(self, op):
-        """One exchange point of ``_step_gen`` over the process group (world > 1):
+        """One exchange point of ``_step_gen`` over the process group:
+        ("local_sizes", pinned words, W) at world 1: the stream synchronised, the words read;
         ("sizes", words, W): an all-to-all of W int64 words per rank, both sides read on the host
         (a host sync) -> (words sent, words received, the received words as a numpy array);
         ("chunks", buf, out sizes, in sizes, name): chunk r of buf to rank r -> the device address
         of every source's chunk for this rank (``_exchange_chunks``)."""
+        if op[0] == "local_sizes":  # world 1: words the device wrote into mapped pinned memory
+            _, words, W = op
+            torch.cuda.current_stream(self.device).synchronize()
+            lst = words[: W * self.world].tolist()
+            return lst, lst, words
         if op[0] == "sizes":
             _, words, W = op
             G = self.world
@@ -656,13 +764,9 @@ class ShardedMatcher:
         # (the split sizes as Python ints: this bookkeeping sits between the host sync and the
         # next launch, on the step's critical path, where numpy calls on a few words cost more
         # than the arithmetic)
-        if G == 1:
-            cur.synchronize()  # host sync 1
-            mo_l = mi_l = hmeta[: MW * G].tolist()
-            mi_ptr = hmeta.data_ptr()  # (recv reads the words on the host, during the call)
-        else:
-            mo_l, mi_l, mi = yield ("sizes", meta, MW)  # host sync 1
-            mi_ptr = mi.ctypes.data
+        # host sync 1 (world 1: the stream, then the mapped words; recv reads them on the host)
+        mo_l, mi_l, mi = yield (("local_sizes", hmeta, MW) if G == 1 else ("sizes", meta, MW))
+        mi_ptr = mi.data_ptr() if G == 1 else mi.ctypes.data
         mark(2)
         out_b = mo_l[0::MW]
         in_b = mi_l[0::MW]
@@ -726,13 +830,9 @@ class ShardedMatcher:
                                                 P(ans), ctypes.c_void_p(dans) if G == 1 else P(ans_meta), S),
                        "emqx_shard_step_answer")
             mark(5)
-            if G == 1:
-                cur.synchronize()  # host sync 2
-                am_l = ai_l = hans[: 3 * G].tolist()
-                ai_ptr = hans.data_ptr()  # (merge reads the words on the host, during the call)
-            else:
-                am_l, ai_l, ai = yield ("sizes", ans_meta, 3)  # host sync 2
-                ai_ptr = ai.ctypes.data
+            # host sync 2 (world 1: the mapped words; merge reads them on the host)
+            am_l, ai_l, ai = yield (("local_sizes", hans, 3) if G == 1 else ("sizes", ans_meta, 3))
+            ai_ptr = ai.data_ptr() if G == 1 else ai.ctypes.data
             mark(6)
             sm = hsumm[: 8 * E].tolist()
             if not redo:
@@ -902,6 +1002,7 @@ class EmulatedWorld:
     are enqueued before the first kernel starts (kernel time only)."""
 
     PHASES = ("send", "sizes1", "recv_match_answer", "sizes2", "merge")
+    PHASES_1 = ("send", "recv_match_answer", "merge")  # world 1: no exchange, two host syncs
 
     def __init__(self, filters: Tuple[np.ndarray, np.ndarray], world: int, device: torch.device, mode: int = 0,
                  max_piece_pm: int = MAX_PIECE_PM, on_rank: Optional[Callable] = None, p_space: str = "auto"):
@@ -925,15 +1026,42 @@ class EmulatedWorld:
                 on_rank(r)
         self.bytes_out = np.zeros((2, world, world), dtype=np.int64)  # [requests, answers][src][dst]
         self.last_times = None
+        self.recorded = [dict() for _ in range(world)]  # per rank: what its last step's exchanges gave it
 
     def close(self):
         for m in self.matchers:
             for e in m.engines:
                 if e is not None:
                     e.close()
-            if m._step is not None:
-                m._step.close()
+            m.close()
         self.matchers = []
+
+    def rank_stream(self, r: int, batch: Tuple[torch.Tensor, torch.Tensor], steps: int):
+        """Rank r alone running ``steps`` steps of its batch with two in flight
+        (``ShardedMatcher.match_stream``), the other ranks' side replayed from the last ``step``
+        (which must have used the same batches): their size words and their chunks for r, which
+        stay where they were packed since no other rank runs; r's own chunks are its lane's.
+        This is rank r's pipelined step — the device work it does per step at world G, with the
+        collectives themselves left to the projection.  Returns (ms per step, the results)."""
+        m = self.matchers[r]
+        rec = self.recorded[r]
+
+        def replay(op):
+            if op[0] == "local_sizes":
+                return m._exchange(op)
+            if op[0] == "sizes":
+                return rec[("sizes", op[2])]
+            addrs = list(rec[("chunks", op[4])])
+            own = np.concatenate([[0], np.cumsum(op[2])]).astype(np.int64)
+            addrs[r] = op[1].data_ptr() + op[1].element_size() * int(own[r])
+            return addrs
+
+        m.match_stream([batch] * 2, exchange=replay)  # (the second lane's buffers and workspaces)
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        res = m.match_stream([batch] * steps, exchange=replay)
+        torch.cuda.synchronize(self.device)
+        return 1e3 * (time.perf_counter() - t0) / max(steps, 1), res
 
     def _run(self, r: int, gen, value, timing: Optional[str]):
         """Advances rank r's step to its next exchange point (or its end) on the rank's stream;
@@ -984,17 +1112,21 @@ class EmulatedWorld:
             if kind == "done":
                 break
             torch.cuda.synchronize(self.device)
-            if kind == "sizes":
+            if kind == "local_sizes":  # world 1
+                vals = [self.matchers[r]._exchange(ops[r]) for r in range(G)]
+            elif kind == "sizes":
                 W = ops[0][2]
                 words = [op[1].cpu().numpy().astype(np.int64) for op in ops]
                 for r in range(G):
                     mi = np.ascontiguousarray(np.concatenate([words[s][W * r: W * (r + 1)] for s in range(G)]))
                     vals[r] = (words[r].tolist(), mi.tolist(), mi)
+                    self.recorded[r][("sizes", W)] = vals[r]
             elif kind == "chunks":
                 # chunk r of source s lies at s's buffer + the prefix of s's sizes before r
                 offs = [np.concatenate([[0], np.cumsum(op[2])]).astype(np.int64) for op in ops]
                 for r in range(G):
                     vals[r] = [ops[s][1].data_ptr() + ops[s][1].element_size() * int(offs[s][r]) for s in range(G)]
+                    self.recorded[r][("chunks", ops[r][4])] = vals[r]
                 k = min(chunk_round, 1)
                 for s in range(G):
                     self.bytes_out[k, s, :] = np.asarray(ops[s][2], dtype=np.int64) * ops[s][1].element_size()

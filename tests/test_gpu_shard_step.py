@@ -84,6 +84,15 @@ def test_shard_step_edge_batches_world1():
         for batch in ([b"a/b"], [b"zz/yy/xx"] * 7, [b"$SYS"] * 3):
             t = pack(batch)
             _check(sm.match_all(_dev_topics(t)), filters, t)
+        # two steps in flight (match_stream): every batch's CSR, an empty one among them
+        seq = [topics, pack([b"a/b"]), empty, pack(TOPICS[::-1]), topics]
+        outs = sm.match_stream([_dev_topics(t) for t in seq])
+        assert len(outs) == len(seq)
+        for t, got in zip(seq, outs):
+            if len(t[1]) == 1:
+                assert got[0].cpu().tolist() == [0] and got[1].numel() == 0
+            else:
+                _check(got, filters, t)
     finally:
         dist.destroy_process_group()
 
@@ -130,9 +139,14 @@ def _rank_main(rank, world, port, q, p_space="sharded"):
         got = sm.match_all(_dev_topics(wl.topics))
         empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
         third = sm.match_all(_dev_topics(empty if rank == 1 else wl.topics))
+        # two steps in flight over the process group: the collectives of steps k and k + 1 pair up
+        streamed = sm.match_stream([_dev_topics(wl.topics)] * 3)
         off, ids = got[0].cpu().numpy(), got[1].cpu().numpy().view(np.uint32)
         off_o, ids_o = _oracle(wl.filters, wl.topics)
         bad = C.csr_mismatches(off.astype(np.uint64), ids, off_o, ids_o)
+        for st_off, st_ids in streamed:
+            bad = np.concatenate([bad, C.csr_mismatches(st_off.cpu().numpy().astype(np.uint64),
+                                                        st_ids.cpu().numpy().view(np.uint32), off_o, ids_o)])
         if rank == 1:
             third_ok = third[0].numel() == 1 and third[1].numel() == 0
         else:  # the same topics on a smaller exchange: the same sets (in-topic order may differ)
@@ -234,6 +248,11 @@ def test_emulated_world_every_source_id_for_id(world, p_space):
             for s in range(world):
                 _check(res[s], wl.filters, srcs[s])
         assert (ew.bytes_out[0] >= 32).all() and (ew.bytes_out[1] >= 32).all()
+        for r in range(world):  # each rank alone, two steps in flight, the others' side replayed
+            ms, rs = ew.rank_stream(r, _dev_topics(srcs[r]), 3)
+            assert ms > 0 and len(rs) == 3
+            for got in rs:
+                _check(got, wl.filters, srcs[r])
         slots = np.sum([m.last_slot_topics for m in ew.matchers], axis=0)
         if p_space == "sharded":
             assert slots[0] > 0 and slots[1] > 0 and slots[2] > 0, slots
