@@ -66,7 +66,7 @@ __host__ __device__ inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull;
 
 typedef uint4 __attribute__((aligned(1))) u4u;  // (gfx950 global loads and stores take any alignment)
 // One thread's copy of a topic's bytes (any alignment): 16-B moves, then 8 / 4 / 2 / 1.
-__device__ __forceinline__ void copy_topic(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len) {
+__host__ __device__ inline void copy_topic(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint32_t len) {
   typedef uint2 __attribute__((aligned(1))) u2u;
   typedef uint32_t __attribute__((aligned(1))) u1u;
   typedef uint16_t __attribute__((aligned(1))) h1u;
@@ -94,12 +94,71 @@ uint32_t grid_of(uint64_t items, uint32_t per_block, uint32_t cap = 8192) {
 
 // A topic's raw requests (r[0]: rank * 2 of engine A, r[1]: rank * 2 + 1 of engine B, or kNone)
 // -> its bucket keys (rank * kE + slot; kE * world = none), see the header.
-__device__ __forceinline__ uint2 shard_fold(const uint32_t (&r)[2], uint32_t world) {
+__host__ __device__ inline uint2 shard_fold(const uint32_t (&r)[2], uint32_t world) {
   const uint32_t none = kE * world;
   const bool a = r[0] != kNone, b = r[1] != kNone;
   if (a && b && (r[0] >> 1) != (r[1] >> 1)) return make_uint2(kE * (r[0] >> 1), kE * (r[1] >> 1) + 1);
   if (a || b) return make_uint2(kE * ((a ? r[0] : r[1]) >> 1) + 2, none);
   return make_uint2(none, none);
+}
+
+// Destination r's chunk size from the sorted buckets (its requests and bytes per slot).
+__host__ __device__ inline uint64_t dest_size(uint32_t r, const uint32_t* start, const uint64_t* bpre, bool* wide) {
+  uint64_t ball = 0, nall = 0;
+  for (uint32_t e = 0; e < kE; ++e) {
+    const uint32_t b = kE * r + e;
+    nall += start[b + 1] - start[b];
+    ball += bpre[b + 1] - bpre[b];
+    *wide |= bpre[b + 1] - bpre[b] > 0xFFFFFFFFull;
+  }
+  return 4 * kHW + al16(4ull * (nall + kE)) + al16(ball);
+}
+
+// Destination r of the send: its meta words, its chunk's header and final offsets, and per
+// bucket where the sorted scatter puts its requests (obase[b] + p = the offset word of sorted
+// request p, dbase[r] + byte prefix = its bytes); base = the chunk's start, over = the send does
+// not fit.  (shard_layout_kernel; the host step's send.)
+__host__ __device__ inline void layout_dest(uint32_t r, uint64_t size, uint64_t base, bool over,
+                                            const uint32_t* __restrict__ start, const uint64_t* __restrict__ bpre,
+                                            uint8_t* __restrict__ send, int64_t* __restrict__ meta,
+                                            int64_t* __restrict__ obase, int64_t* __restrict__ dbase) {
+  uint32_t nq[kE], nall = 0;
+  uint64_t by[kE];
+  for (uint32_t e = 0; e < kE; ++e) {
+    const uint32_t b = kE * r + e;
+    nq[e] = start[b + 1] - start[b];
+    by[e] = bpre[b + 1] - bpre[b];
+    nall += nq[e];
+  }
+  int64_t* m = meta + (1 + 2 * kE) * r;
+  m[0] = over ? -1 : static_cast<int64_t>(size);
+  for (uint32_t e = 0; e < kE; ++e) {
+    m[1 + e] = nq[e];
+    m[1 + kE + e] = static_cast<int64_t>(by[e]);
+  }
+  if (over) return;
+  uint32_t* h = reinterpret_cast<uint32_t*>(send + base);
+  uint32_t o = kHW;
+  for (uint32_t e = 0; e < kE; ++e) {
+    const uint32_t b = kE * r + e;
+    obase[b] = static_cast<int64_t>(base / 4 + o) - static_cast<int64_t>(start[b]);
+    h[e] = nq[e];
+    h[4 + e] = static_cast<uint32_t>(by[e]);
+    o += nq[e];
+    h[o++] = static_cast<uint32_t>(by[e]);  // slot e's offsets[n_e]
+  }
+  h[3] = 0;
+  h[7] = 0;
+  dbase[r] = static_cast<int64_t>(base + 4 * kHW + al16(4ull * (nall + kE))) - static_cast<int64_t>(bpre[kE * r]);
+}
+
+// Sorted request `pos` (bucket k < the no-request bucket, byte x among the sorted requests') packed
+// where it lands: its offset word and its topic's bytes into its destination's chunk.
+__host__ __device__ inline void pack_request(uint8_t* __restrict__ send, uint32_t k, uint32_t pos, uint64_t x,
+                                             const int64_t* obase, const uint64_t* bpre, const int64_t* dbase,
+                                             const uint8_t* __restrict__ topic, uint32_t len) {
+  reinterpret_cast<uint32_t*>(send)[obase[k] + pos] = static_cast<uint32_t>(x - bpre[k]);
+  copy_topic(topic, send + (dbase[k / kE] + static_cast<int64_t>(x)), len);
 }
 
 // ---- send -------------------------------------------------------------------------------
@@ -628,11 +687,7 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
       const uint32_t pos = pc + rc;
       key_s[pos] = k;
       perm[pos] = static_cast<uint32_t>(p);
-      if (pack && k < nb - 1) {
-        const uint64_t x = pb + rb;  // the request's first byte among the sorted requests'
-        reinterpret_cast<uint32_t*>(send)[s_ob[k] + pos] = static_cast<uint32_t>(x - s_bp[k]);
-        copy_topic(tb + a, send + (s_db[k / kE] + static_cast<int64_t>(x)), l);
-      }
+      if (pack && k < nb - 1) pack_request(send, k, pos, pb + rb, s_ob, s_bp, s_db, tb + a, l);
     }
     __syncthreads();
     for (uint32_t kk = tid; kk < nb; kk += 256) {
@@ -652,8 +707,7 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
 }
 
 // One block: per destination rank the chunk's sizes, start, header and final offsets, and per
-// bucket where the sorted scatter puts its requests (pack fused into shard_sort_scatter_kernel):
-// obase[b] + p = the offset word of sorted request p, dbase[r] + byte prefix = its bytes.
+// bucket where the sorted scatter puts its requests (pack fused into shard_sort_scatter_kernel).
 __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __restrict__ start,
                                                           const uint64_t* __restrict__ bpre, uint32_t world,
                                                           uint8_t* __restrict__ send, uint64_t cap,
@@ -661,22 +715,14 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
                                                           int64_t* __restrict__ obase, int64_t* __restrict__ dbase,
                                                           uint32_t* __restrict__ err) {
   __shared__ uint64_t sz[kMaxWorld];
+  __shared__ uint32_t wide_any;
   const uint32_t r = threadIdx.x;
-  uint32_t nq[kE] = {}, nall = 0;
-  uint64_t by[kE] = {}, size = 0;
+  if (r == 0) wide_any = 0;
+  __syncthreads();
   bool wide = false;
   if (r < world) {
-    uint64_t ball = 0;
-    for (uint32_t e = 0; e < kE; ++e) {
-      const uint32_t b = kE * r + e;
-      nq[e] = start[b + 1] - start[b];
-      by[e] = bpre[b + 1] - bpre[b];
-      nall += nq[e];
-      ball += by[e];
-      wide |= by[e] > 0xFFFFFFFFull;
-    }
-    size = 4 * kHW + al16(4ull * (nall + kE)) + al16(ball);
-    sz[r] = size;
+    sz[r] = dest_size(r, start, bpre, &wide);
+    if (wide) atomicOr(&wide_any, 1u);
   }
   __syncthreads();
   if (r >= world) return;
@@ -685,33 +731,10 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
   uint64_t total = 0;
   for (uint32_t j = 0; j < world; ++j) total += sz[j];
   cbase[r] = base;
-  const bool over = total > cap || wide;
-  int64_t* m = meta + (1 + 2 * kE) * r;
-  m[0] = over ? -1 : static_cast<int64_t>(size);
-  for (uint32_t e = 0; e < kE; ++e) {
-    m[1 + e] = nq[e];
-    m[1 + kE + e] = static_cast<int64_t>(by[e]);
-  }
-  if (over) {
-    if (r == 0) err[0] = 1;
-    return;
-  }
-  if (r == 0) err[0] = 0;
-  uint32_t* h = reinterpret_cast<uint32_t*>(send + base);
-  uint32_t o = kHW;
-  for (uint32_t e = 0; e < kE; ++e) {
-    const uint32_t b = kE * r + e;
-    obase[b] = static_cast<int64_t>(base / 4 + o) - static_cast<int64_t>(start[b]);
-    h[e] = nq[e];
-    h[4 + e] = static_cast<uint32_t>(by[e]);
-    o += nq[e];
-    h[o++] = static_cast<uint32_t>(by[e]);  // slot e's offsets[n_e]
-  }
-  h[3] = 0;
-  h[7] = 0;
-  dbase[r] = static_cast<int64_t>(base + 4 * kHW + al16(4ull * (nall + kE))) - static_cast<int64_t>(bpre[kE * r]);
+  const bool over = total > cap || wide_any;
+  layout_dest(r, sz[r], base, over, start, bpre, send, meta, obase, dbase);
+  if (r == 0) err[0] = over ? 1u : 0u;
 }
-
 // emqx_shard_route_device: the raw requests (req2[2t], req2[2t + 1]) with the same scanner.
 __global__ __launch_bounds__(256) void shard_route_kernel(const uint8_t* __restrict__ tb,
                                                           const uint64_t* __restrict__ to, uint64_t n, uint32_t world,
@@ -736,7 +759,7 @@ __global__ __launch_bounds__(256) void shard_route_kernel(const uint8_t* __restr
 
 // Words before slot e's offsets in a request chunk with slot sizes n[]: the header, then each
 // earlier slot's n + 1 offsets.
-__device__ __forceinline__ uint32_t offs_words(const uint32_t* n, uint32_t e) {
+__host__ __device__ inline uint32_t offs_words(const uint32_t* n, uint32_t e) {
   uint32_t w = kHW;
   for (uint32_t k = 0; k < e; ++k) w += n[k] + 1;
   return w;
@@ -753,8 +776,10 @@ struct SlotBytes {
   uint8_t* p[kE];
 };
 
-__global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOffsets dst_off, SlotBytes dst_bytes) {
-  const uint32_t s = blockIdx.y, e = blockIdx.z;
+// (source s, slot e) of the recv: items tid, tid + stride, ... (the kernel's grid-stride; the host
+// step's loop: 0, 1).
+__host__ __device__ inline void unpack_part(const ShardTab& tab, const SlotOffsets& dst_off, const SlotBytes& dst_bytes,
+                                            uint32_t s, uint32_t e, uint64_t tid, uint64_t stride) {
   uint32_t nq[kE], nall = 0;
   uint64_t before = 0;  // this source's bytes of the slots before e
   for (uint32_t k = 0; k < kE; ++k) {
@@ -766,8 +791,6 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOff
   const uint32_t n = nq[e];
   const uint64_t dbase = tab.y0[e][s];
   uint64_t* doff = dst_off.p[e] + tab.q0[e][s];
-  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t k = tid; k <= n; k += stride) doff[k] = dbase + offs[k];
   if (!dst_bytes.p[e]) return;
   const uint64_t by = tab.y0[e][s + 1] - dbase;
@@ -776,7 +799,12 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOff
   for (uint64_t j = 16 * tid; j + 16 <= by; j += 16 * stride)
     *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
   const uint64_t tail = by & ~15ull;
-  if (tid < by - tail) dst[tail + tid] = src[tail + tid];
+  for (uint64_t j = tail + tid; j < by; j += stride) dst[j] = src[j];
+}
+
+__global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOffsets dst_off, SlotBytes dst_bytes) {
+  unpack_part(tab, dst_off, dst_bytes, blockIdx.y, blockIdx.z, static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+              static_cast<uint64_t>(gridDim.x) * blockDim.x);
 }
 
 // ---- answer -----------------------------------------------------------------------------
@@ -791,9 +819,10 @@ struct EngineCsrs {
 // complete (summary flags) leaves its ids unread: the step is redone.  The chunk for this rank
 // itself (source `self`) carries no ids: the merge reads them in place from the CSRs.
 constexpr uint32_t kAnsMeta = 3;  // per source: chunk words, redo flag, ids
-__global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardTab tab, uint32_t self,
-                                                           uint32_t* __restrict__ out, int64_t* __restrict__ ans_meta) {
-  const uint32_t s = blockIdx.y;
+// Source s of G: items tid, tid + stride, ... (meta: this item writes the source's meta words).
+__host__ __device__ inline void answer_source(const EngineCsrs& cs, const ShardTab& tab, uint32_t self,
+                                              uint32_t* __restrict__ out, int64_t* __restrict__ ans_meta, uint32_t s,
+                                              uint32_t G, uint64_t tid, uint64_t stride, bool meta) {
   bool bad = false;
   uint32_t q0[kE], nq[kE];
   uint64_t i0[kE], ni[kE], nall = 0, iall = 0, ibefore = 0;
@@ -804,7 +833,7 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
     nall += nq[e];
   }
   for (uint32_t e = 0; e < kE; ++e) {
-    i0[e] = tab.q0[e][gridDim.y] ? cs.off[e][q0[e]] : 0;  // (a slot no source asked: never read)
+    i0[e] = tab.q0[e][G] ? cs.off[e][q0[e]] : 0;  // (a slot no source asked: never read)
     ni[e] = bad || !nq[e] ? 0 : cs.off[e][q0[e] + nq[e]] - i0[e];
     iall += ni[e];
     ibefore += bad ? 0 : i0[e];  // this source's ids start after every earlier source's
@@ -815,7 +844,7 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
       if (a1 > a0) ibefore -= cs.off[e][a1] - cs.off[e][a0];
     }
   const uint64_t cb = tab.w0[s] + ibefore;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (meta) {
     ans_meta[kAnsMeta * s] = static_cast<int64_t>(kHW + nall + (s == self ? 0 : iall));
     ans_meta[kAnsMeta * s + 1] = bad ? 1 : 0;
     ans_meta[kAnsMeta * s + 2] = static_cast<int64_t>(iall);
@@ -823,13 +852,11 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
   if (bad) return;
   const bool copy_ids = s != self;
   uint32_t* c = out + cb;
-  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  if (tid < kHW) {
+  for (uint64_t w = tid; w < kHW; w += stride) {
     uint32_t v = 0;
-    if (tid < kE) v = nq[tid];
-    else if (tid >= 3 && tid < 3 + kE) v = static_cast<uint32_t>(ni[tid - 3]);
-    c[tid] = v;
+    if (w < kE) v = nq[w];
+    else if (w >= 3 && w < 3 + kE) v = static_cast<uint32_t>(ni[w - 3]);
+    c[w] = v;
   }
   // per request the END of its ids within the chunk's id region (the merge reads begin and end
   // without a scan), then the ids
@@ -844,12 +871,19 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
       for (uint64_t j = 4 * tid; j + 4 <= ni[e]; j += 4 * stride)
         *reinterpret_cast<u4u*>(ids + j) = *reinterpret_cast<const u4u*>(src + j);
       const uint64_t r = ni[e] & ~3ull;
-      if (tid < ni[e] - r) ids[r + tid] = src[r + tid];
+      for (uint64_t j = r + tid; j < ni[e]; j += stride) ids[j] = src[j];
     }
     end += nq[e];
     ids += ni[e];
     before += ni[e];
   }
+}
+
+__global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardTab tab, uint32_t self,
+                                                           uint32_t* __restrict__ out, int64_t* __restrict__ ans_meta) {
+  answer_source(cs, tab, self, out, ans_meta, blockIdx.y, gridDim.y,
+                static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x, static_cast<uint64_t>(gridDim.x) * blockDim.x,
+                blockIdx.x == 0 && threadIdx.x == 0);
 }
 
 // ---- merge ------------------------------------------------------------------------------
@@ -867,20 +901,16 @@ struct SelfIds {
 // own engine output) and how many, stored at the request's own index perm[p] (2t: a topic's
 // first request, 2t + 1 its second) — the merge then reads them per topic, coalesced.  With one
 // request a topic (`one`: perm[p] = the topic) it goes to 2t and 2t + 1 says none.
-__global__ __launch_bounds__(256) void shard_gather_kernel(ShardTab tab, SelfIds me,
-                                                           const uint32_t* __restrict__ key_s,
-                                                           const uint32_t* __restrict__ perm,
-                                                           const uint32_t* __restrict__ start, uint64_t m,
-                                                           uint32_t world, uint32_t* __restrict__ rq_cnt,
-                                                           uint64_t* __restrict__ rq_src, uint32_t one) {
-  const uint32_t nreq = start[kE * world];
-  for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
-       p += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+__host__ __device__ inline void gather_request(const ShardTab& tab, const SelfIds& me, const uint32_t* __restrict__ key_s,
+                                               const uint32_t* __restrict__ perm, const uint32_t* __restrict__ start,
+                                               uint32_t nreq, uint64_t p, uint32_t* __restrict__ rq_cnt,
+                                               uint64_t* __restrict__ rq_src, uint32_t one) {
+  {
     const uint32_t q = one ? 2 * perm[p] : perm[p];
     if (one) rq_cnt[q + 1] = 0;
     if (p >= nreq) {
       rq_cnt[q] = 0;
-      continue;
+      return;
     }
     const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
     const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
@@ -898,6 +928,18 @@ __global__ __launch_bounds__(256) void shard_gather_kernel(ShardTab tab, SelfIds
   }
 }
 
+__global__ __launch_bounds__(256) void shard_gather_kernel(ShardTab tab, SelfIds me,
+                                                           const uint32_t* __restrict__ key_s,
+                                                           const uint32_t* __restrict__ perm,
+                                                           const uint32_t* __restrict__ start, uint64_t m,
+                                                           uint32_t world, uint32_t* __restrict__ rq_cnt,
+                                                           uint64_t* __restrict__ rq_src, uint32_t one) {
+  const uint32_t nreq = start[kE * world];
+  for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
+       p += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    gather_request(tab, me, key_s, perm, start, nreq, p, rq_cnt, rq_src, one);
+}
+
 __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t* __restrict__ rq_cnt, uint64_t n,
                                                                  uint32_t* __restrict__ tcnt) {
   for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
@@ -909,12 +951,24 @@ __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t*
 
 // c ids from src to dst by the 4 lanes `sub` of a quad: 16-B moves (4 ids a lane, any 4-B
 // alignment), the last < 4 ids one by one.
-__device__ __forceinline__ void quad_copy_ids(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t c,
+__host__ __device__ inline void quad_copy_ids(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t c,
                                               uint32_t sub) {
   uint32_t j = 4 * sub;
   for (; j + 4 <= c; j += 16) *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
   const uint32_t r = c & ~3u;  // the ids past the last whole group of 4
   if (sub < c - r) dst[r + sub] = src[r + sub];
+}
+
+// Topic t's ids by lane `sub` of its quad: its first request's ids, then its second's.
+__host__ __device__ inline void merge_topic(const uint32_t* __restrict__ rq_cnt, const uint64_t* __restrict__ rq_src,
+                                            uint64_t t, const uint64_t* __restrict__ out_off,
+                                            uint32_t* __restrict__ out_ids, uint32_t sub) {
+  const uint2 c = *reinterpret_cast<const uint2*>(rq_cnt + 2 * t);
+  const uint32_t cx = c.x, cy = c.y;
+  if ((cx | cy) == 0) return;
+  const uint64_t dst = out_off[t];
+  if (cx) quad_copy_ids(reinterpret_cast<const uint32_t*>(rq_src[2 * t]), out_ids + dst, cx, sub);
+  if (cy) quad_copy_ids(reinterpret_cast<const uint32_t*>(rq_src[2 * t + 1]), out_ids + dst + cx, cy, sub);
 }
 
 // 4 lanes per topic, in topic order: its first request's ids, then its second's, to the topic's
@@ -926,11 +980,7 @@ __global__ __launch_bounds__(256) void shard_merge_kernel(const uint32_t* __rest
   const uint32_t sub = threadIdx.x & 3u;
   for (uint64_t t = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; t < n;
        t += (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 2) {
-    const uint2 c = *reinterpret_cast<const uint2*>(rq_cnt + 2 * t);
-    if ((c.x | c.y) == 0) continue;
-    const uint64_t dst = out_off[t];
-    if (c.x) quad_copy_ids(reinterpret_cast<const uint32_t*>(rq_src[2 * t]), out_ids + dst, c.x, sub);
-    if (c.y) quad_copy_ids(reinterpret_cast<const uint32_t*>(rq_src[2 * t + 1]), out_ids + dst + c.x, c.y, sub);
+    merge_topic(rq_cnt, rq_src, t, out_off, out_ids, sub);
   }
 }
 
@@ -972,6 +1022,16 @@ struct emqx_shard_step {
   ShardTab recv_tab{};                  // the last recv's per-source table (answer uses it)
   SelfIds self_ids{};                   // the last answer's in-place own ids (merge uses them)
   bool have_recv = false, have_send = false;
+  // host mode (device < 0): every pointer is host memory and each call runs on the caller's
+  // thread — the kernels' per-item bodies (layout_dest, pack_request, unpack_part,
+  // answer_source, gather_request, merge_topic; routing and fold from layout.h / shard_fold) as
+  // loops, the tile sort as a stable counting sort.  The CPU rehearsal of the protocol over gloo
+  // (tests/test_dist_gloo.py drives dist.py's step with it).
+  bool host = false;
+  std::vector<ShardSplitE> h_splits;
+  std::vector<uint32_t> h_key, h_key_s, h_perm, h_pos, h_tcnt, h_start;
+  std::vector<uint64_t> h_rq_src, h_bpre, h_cbase;
+  std::vector<int64_t> h_obase, h_dbase;
 };
 
 namespace {
@@ -1021,6 +1081,91 @@ hipError_t ensure_scratch(emqx_shard_step* st, uint64_t m) {
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? EMQX_OK : (e == hipErrorOutOfMemory ? EMQX_ENOMEM : EMQX_EDEVICE); }
 
+// ---- host mode ----------------------------------------------------------------------------
+
+// The send on the host: routing and fold per topic, a stable counting sort by bucket (what the
+// tiles' counting sort computes), then the same layout and packing as the kernels.
+int host_send(emqx_shard_step* st, const uint8_t* tb, const uint64_t* to, uint64_t n, uint8_t* send, uint64_t cap,
+              int64_t* meta) {
+  const uint32_t G = st->world, nb = kE * G + 1;
+  const uint64_t m = st->one ? n : 2 * n;
+  st->h_key.assign(m, 0);
+  st->h_key_s.assign(m, 0);
+  st->h_perm.assign(m, 0);
+  for (uint64_t t = 0; t < n; ++t) {
+    ShardTopicLevels L;
+    shard_topic_levels(tb + to[t], to[t + 1] - to[t], &L);
+    uint32_t r[2];
+    shard_route_levels(tb + to[t], to[t + 1] - to[t], L, G, st->d_splits, st->n_splits, r);
+    const uint2 k = shard_fold(r, G);
+    if (st->one) {
+      st->h_key[t] = k.x;
+    } else {
+      st->h_key[2 * t] = k.x;
+      st->h_key[2 * t + 1] = k.y;
+    }
+  }
+  auto topic_of = [&](uint64_t p) { return st->one ? p : p >> 1; };
+  std::vector<uint64_t> cnt(nb, 0), byb(nb, 0);
+  for (uint64_t p = 0; p < m; ++p) {
+    const uint32_t k = st->h_key[p];
+    ++cnt[k];
+    if (k < nb - 1) byb[k] += to[topic_of(p) + 1] - to[topic_of(p)];
+  }
+  uint64_t c = 0, b = 0;
+  for (uint32_t k = 0; k < nb; ++k) {
+    st->start[k] = static_cast<uint32_t>(c);
+    st->bpre[k] = b;
+    c += cnt[k];
+    b += byb[k];
+  }
+  st->start[nb] = static_cast<uint32_t>(m);
+  st->bpre[nb] = b;
+  bool wide = false;
+  std::vector<uint64_t> sz(G);
+  uint64_t total = 0;
+  for (uint32_t r = 0; r < G; ++r) {
+    sz[r] = dest_size(r, st->start, st->bpre, &wide);
+    st->cbase[r] = total;
+    total += sz[r];
+  }
+  const bool over = total > cap || wide;
+  for (uint32_t r = 0; r < G; ++r) layout_dest(r, sz[r], st->cbase[r], over, st->start, st->bpre, send, meta, st->obase,
+                                               st->dbase);
+  std::vector<uint64_t> nextp(st->start, st->start + nb), nextx(st->bpre, st->bpre + nb);
+  for (uint64_t p = 0; p < m; ++p) {  // in request order: stable
+    const uint32_t k = st->h_key[p];
+    const uint64_t pos = nextp[k]++;
+    st->h_key_s[pos] = k;
+    st->h_perm[pos] = static_cast<uint32_t>(p);
+    if (k == nb - 1 || over) continue;
+    const uint64_t a = to[topic_of(p)];
+    const uint32_t len = static_cast<uint32_t>(to[topic_of(p) + 1] - a);
+    pack_request(send, k, static_cast<uint32_t>(pos), nextx[k], st->obase, st->bpre, st->dbase, tb + a, len);
+    nextx[k] += len;
+  }
+  st->key_s = st->h_key_s.data();
+  st->perm = st->h_perm.data();
+  return EMQX_OK;
+}
+
+// The merge on the host: gather per request, the topics' totals and offsets, then the copies.
+int host_merge(emqx_shard_step* st, const ShardTab& t, uint64_t* out_off, uint32_t* out_ids) {
+  const uint64_t n = st->n, m = st->m;
+  st->h_pos.assign(2 * n + 2, 0);
+  st->h_rq_src.assign(2 * n + 2, 0);
+  const uint32_t nreq = st->start[kE * st->world];
+  for (uint64_t p = 0; p < m; ++p)
+    gather_request(t, st->self_ids, st->key_s, st->perm, st->start, nreq, p, st->h_pos.data(), st->h_rq_src.data(),
+                   st->one);
+  out_off[0] = 0;
+  for (uint64_t q = 0; q < n; ++q) out_off[q + 1] = out_off[q] + st->h_pos[2 * q] + st->h_pos[2 * q + 1];
+  if (n && !out_ids && out_off[n]) return EMQX_EINVAL;
+  for (uint64_t q = 0; q < n; ++q)
+    for (uint32_t sub = 0; sub < 4; ++sub) merge_topic(st->h_pos.data(), st->h_rq_src.data(), q, out_off, out_ids, sub);
+  return EMQX_OK;
+}
+
 #define SS_TRY(x)                    \
   do {                               \
     hipError_t e_ = (x);             \
@@ -1045,6 +1190,29 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
   st->world = world;
   st->n_splits = n_splits;
   st->one = world == 1 || shard_p_replicated(reinterpret_cast<const ShardSplitE*>(splits), n_splits) ? 1u : 0u;
+  if (device < 0) {  // host mode
+    try {
+      st->host = true;
+      const auto* sp = reinterpret_cast<const ShardSplitE*>(splits);
+      st->h_splits.assign(sp, sp + n_splits);
+      st->d_splits = st->h_splits.data();
+      st->h_start.assign(kE * world + 2, 0);
+      st->h_bpre.assign(kE * world + 2, 0);
+      st->h_obase.assign(kE * world + 2, 0);
+      st->h_dbase.assign(world, 0);
+      st->h_cbase.assign(world, 0);
+    } catch (const std::bad_alloc&) {
+      delete st;
+      return EMQX_ENOMEM;
+    }
+    st->start = st->h_start.data();
+    st->bpre = st->h_bpre.data();
+    st->obase = st->h_obase.data();
+    st->dbase = st->h_dbase.data();
+    st->cbase = st->h_cbase.data();
+    *out = st;
+    return EMQX_OK;
+  }
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->d_splits), std::max<uint64_t>(8ull * n_splits, 16));
   if (e == hipSuccess && n_splits)
@@ -1066,6 +1234,10 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
 
 int emqx_shard_step_destroy(emqx_shard_step* st) {
   if (!st) return EMQX_EINVAL;
+  if (st->host) {
+    delete st;
+    return EMQX_OK;
+  }
   (void)hipSetDevice(st->device);
   (void)hipDeviceSynchronize();
   free_scratch(st);
@@ -1080,6 +1252,19 @@ int emqx_shard_step_destroy(emqx_shard_step* st) {
 int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
                          uint8_t* d_send, uint64_t send_cap, int64_t* d_meta, void* stream) {
   if (!st || !d_send || !d_meta || (n && (!d_bytes || !d_offsets)) || n >= (1ull << 31)) return EMQX_EINVAL;
+  if (st->host) {
+    try {
+      const int rc = host_send(st, d_bytes, d_offsets, n, d_send, send_cap, d_meta);
+      if (rc != EMQX_OK) return rc;
+    } catch (const std::bad_alloc&) {
+      return EMQX_ENOMEM;
+    }
+    st->n = n;
+    st->m = st->one ? n : 2 * n;
+    st->have_send = true;
+    st->have_recv = false;
+    return EMQX_OK;
+  }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
   const uint64_t m = st->one ? n : 2 * n;
@@ -1155,8 +1340,6 @@ int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, co
       if (t.q0[e][r + 1] != t.q0[e][r]) only[e] = only[e] == -1 ? static_cast<int>(r) : -2;
     if (only[e] < 0 && t.y0[e][G] && !d_bytes[e]) return EMQX_EINVAL;
   }
-  const hipStream_t s = static_cast<hipStream_t>(stream);
-  SS_TRY(hipSetDevice(st->device));
   SlotOffsets so{};
   for (uint32_t e = 0; e < kE; ++e) so.p[e] = d_offsets[e];
   uint64_t qall = 0;
@@ -1168,8 +1351,15 @@ int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, co
   const uint32_t x = grid_of(per, 256, std::max<uint32_t>(1, 1024 / G));
   SlotBytes sb{};
   for (uint32_t e = 0; e < kE; ++e) sb.p[e] = only[e] >= 0 ? nullptr : d_bytes[e];
-  hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, kE), dim3(256), 0, s, t, so, sb);
-  SS_TRY(hipGetLastError());
+  if (st->host) {
+    for (uint32_t r = 0; r < G; ++r)
+      for (uint32_t e = 0; e < kE; ++e) unpack_part(t, so, sb, r, e, 0, 1);
+  } else {
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    SS_TRY(hipSetDevice(st->device));
+    hipLaunchKernelGGL(shard_unpack_kernel, dim3(x, G, kE), dim3(256), 0, s, t, so, sb);
+    SS_TRY(hipGetLastError());
+  }
   for (uint32_t r = 0; r < G; ++r) {  // a slot with one source: matched where that source packed it
     uint64_t nall = 0;
     for (uint32_t e = 0; e < kE; ++e) nall += t.q0[e][r + 1] - t.q0[e][r];
@@ -1204,6 +1394,10 @@ int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* const* d_offsets
     st->self_ids.off[e] = d_offsets[e];
     st->self_ids.q0[e] = self_rank < G ? t.q0[e][self_rank] : 0;
   }
+  if (st->host) {
+    for (uint32_t r = 0; r < G; ++r) answer_source(cs, t, self_rank, d_answer, d_ans_meta, r, G, 0, 1, true);
+    return EMQX_OK;
+  }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
   const uint32_t x = grid_of(8 * qall / G + 1, 256, std::max<uint32_t>(1, 1024 / G));  // ~8 ids a request
@@ -1220,6 +1414,13 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   for (uint32_t r = 0; r < G; ++r) {
     if (ans_meta_in[kAnsMeta * r] < kHW || ans_meta_in[kAnsMeta * r + 1] != 0 || !d_chunks[r]) return EMQX_EINVAL;
     t.chunk[r] = reinterpret_cast<uint64_t>(d_chunks[r]);
+  }
+  if (st->host) {
+    try {
+      return host_merge(st, t, d_out_offsets, d_out_ids);
+    } catch (const std::bad_alloc&) {
+      return EMQX_ENOMEM;
+    }
   }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));

@@ -341,29 +341,6 @@ def topic_requests(tb: torch.Tensor, to: torch.Tensor, world: int, plan: np.ndar
     return torch.from_numpy(req[: 2 * n].view(np.int32).astype(np.int64)).reshape(n, 2)
 
 
-def _gather_topics(tb: torch.Tensor, to: torch.Tensor, idx: torch.Tensor):
-    """Topics idx[0], idx[1], ... of a packed batch as a new packed batch (bytes, offsets int64),
-    with a HIP gather for a device batch.  idx may repeat topics."""
-    dev = tb.device
-    k = idx.numel()
-    lens = (to[1:] - to[:-1]).to(torch.int64)[idx] if k else torch.zeros(0, dtype=torch.int64, device=dev)
-    offs = torch.zeros(k + 1, dtype=torch.int64, device=dev)
-    if k:
-        offs[1:] = torch.cumsum(lens, 0)
-    if tb.is_cuda and k:
-        out = torch.empty(tb.numel() * 2 + 16, dtype=torch.uint8, device=dev)  # a topic appears at most twice
-        ooffs = torch.empty(k + 1, dtype=torch.int64, device=dev)
-        _device_call("emqx_batch_permute_device", tb, to, k, idx.to(torch.int32).contiguous(), out, ooffs)
-        return out, offs
-    total = int(offs[-1]) if k else 0
-    if not total:
-        return torch.zeros(0, dtype=torch.uint8, device=dev), offs
-    starts = (to[:-1] - to[0])[idx]
-    seg = torch.repeat_interleave(torch.arange(k, device=dev), lens, output_size=total)
-    src = starts[seg] + (torch.arange(total, device=dev) - (offs[:-1])[seg])
-    return tb[int(to[0]):][src], offs
-
-
 def _p2p(t: Optional[torch.Tensor], peer: int, send: bool, group, like: Optional[torch.Tensor] = None):
     """Point-to-point copy of a tensor (host copies when a device tensor goes over gloo)."""
     gloo = dist.get_backend(group) == "gloo"
@@ -379,15 +356,16 @@ def _p2p(t: Optional[torch.Tensor], peer: int, send: bool, group, like: Optional
 
 
 class _DeviceStep:
-    """An emqx_shard_step (shard_step.hip) on this rank's device, for the rank's plan."""
+    """An emqx_shard_step (shard_step.hip) on this rank's device, for the rank's plan; on a CPU
+    device its host mode (the kernels' per-item bodies as loops over host memory)."""
 
     def __init__(self, device: torch.device, world: int, plan: np.ndarray):
         from . import _lib
         self._lib = _lib
         pl = np.ascontiguousarray(plan, dtype=np.uint32) if len(plan) else np.zeros((1, 2), np.uint32)
         h = ctypes.c_void_p()
-        _lib.check(_lib.lib().emqx_shard_step_create(device.index if device.index is not None else 0, world,
-                                                     pl.ctypes.data, len(plan), ctypes.byref(h)),
+        dev = -1 if device.type != "cuda" else (device.index if device.index is not None else 0)
+        _lib.check(_lib.lib().emqx_shard_step_create(dev, world, pl.ctypes.data, len(plan), ctypes.byref(h)),
                    "emqx_shard_step_create")
         self.h = h
 
@@ -431,6 +409,46 @@ if _SHARD_PROF:
         n = max(_PROF_N[0], 1)
         print("EMQX_SHARD_PROF steps %d us/step: %s" % (_PROF_N[0], " ".join(
             "%d-%d %.1f" % (k - 1, k, 1e6 * _PROF_SUM[k] / n) for k in range(1, 8))), file=sys.stderr)
+
+
+class _HostEngine:
+    """Engine slot `slot` of a rank on the CPU: ``match_device_async`` / ``match_device`` over host
+    memory, answered by a match function (counts, ids) = fn(slot, topic bytes, topic offsets) —
+    what the device step's host mode calls where a rank's HIP engine would run (the CPU tests
+    inject the oracle, tests/test_dist_gloo.py)."""
+
+    def __init__(self, fn: Callable, slot: int):
+        self.fn, self.slot = fn, slot
+
+    def _run(self, b_addr, o_addr, n, off_addr, ids_addr, cap):
+        offs = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(o_addr)).astype(np.int64)
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * max(int(offs[-1]), 1)).from_address(b_addr))[: int(offs[-1])]
+        cnt, ids = self.fn(self.slot, torch.from_numpy(buf.copy()), torch.from_numpy(offs - offs[0]))
+        cnt = cnt.numpy().astype(np.int64)
+        out = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(off_addr))
+        out[0] = 0
+        out[1:] = np.cumsum(cnt)
+        total = int(out[-1])
+        if total <= cap and total:
+            np.ctypeslib.as_array((ctypes.c_int32 * total).from_address(ids_addr))[:] = ids.numpy().astype(np.int32)
+        return total
+
+    def match_device_async(self, b_addr, o_addr, n, off_addr, ids_addr, cap, sum_addr, mode=0, stream=None):
+        total = self._run(b_addr, o_addr, n, off_addr, ids_addr, cap)
+        sm = np.ctypeslib.as_array((ctypes.c_int64 * 8).from_address(sum_addr))
+        sm[:] = 0
+        sm[0] = 1 if total > cap else 0  # (engine summary: word 0 = flags, 0 when complete; word 1 = total)
+        sm[1] = total
+
+    def match_device(self, b_addr, o_addr, n, off_addr, ids_addr, cap, mode=0, stream=None):
+        total = self._run(b_addr, o_addr, n, off_addr, ids_addr, cap)
+        if total > cap:
+            from .engine import EngineError
+            from . import _lib
+            err = EngineError(_lib.EMQX_EOVERFLOW, "match_device")
+            err.needed = total
+            raise err
+        return total
 
 
 class _Lane:
@@ -487,7 +505,11 @@ class ShardedMatcher:
             assert (self.world > 1 and not plan_p_replicated(self.plan)) or engines[2] is not None
             self.engines = list(engines)
             match_fn = self._engine_match
-        elif match_fn is None:
+        elif match_fn is not None:  # (tests: a per-slot match function over host memory)
+            assert self.device.type != "cuda", "an injected match_fn runs the step's host mode (CPU device)"
+            self.engines = [_HostEngine(match_fn, e) for e in range(SHARD_ENGINES)]
+            match_fn = self._engine_match
+        else:
             from .engine import Engine
             from .workloads import take
             one_request = self.world == 1 or plan_p_replicated(self.plan)
@@ -504,10 +526,11 @@ class ShardedMatcher:
         self.match_fn = match_fn
         # the device step (emqx_shard_step_*) when this rank's own HIP engines do the matching;
         # an injected match_fn (tests on CPU over gloo) takes the tensor path below
-        # a lane = the resources of one step in flight (device step object, buffers, streams);
-        # match_stream keeps two steps in flight on two lanes
-        self._lanes = [_Lane(_DeviceStep(self.device, self.world, self.plan) if (
-            self.device.type == "cuda" and self.match_fn == self._engine_match) else None)]
+        # a lane = the resources of one step in flight (step object, buffers, streams);
+        # match_stream keeps two steps in flight on two lanes.  A CPU device runs the step's host
+        # mode (the same protocol and chunk formats; the CPU tests over gloo)
+        self._lanes = [_Lane(_DeviceStep(self.device, self.world, self.plan))]
+        self._cuda = self.device.type == "cuda"
         self._lane = self._lanes[0]
         self._caps = [1 << 20] * SHARD_ENGINES
 
@@ -544,7 +567,7 @@ class ShardedMatcher:
         d_off = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         caps = getattr(self, "_caps", [1 << 20] * SHARD_ENGINES)
         cap = max(1 << 16, caps[which])
-        stream = torch.cuda.current_stream(self.device).cuda_stream
+        stream = torch.cuda.current_stream(self.device).cuda_stream if self._cuda else None
         while True:
             d_ids = torch.empty(cap, dtype=torch.int32, device=self.device)
             try:
@@ -565,6 +588,8 @@ class ShardedMatcher:
         (offsets int64 (n+1,), ids int32) in batch order — the layout's weak-scaling use, one
         publishing node per rank.  Two host synchronisations per call: the split sizes of the
         requests and of the answers (the all-to-all split lists)."""
+        if not self._cuda:
+            return self._match_all_device(topics)
         if self._step is not None:
             # on a stream of its own: the engines take a null stream handle for "their own
             # stream", so the step's kernels and the engine calls must share a real one
@@ -578,12 +603,16 @@ class ShardedMatcher:
             for t in res:
                 t.record_stream(caller)
             return res
-        return self._match_all_tensors(topics)
+        raise RuntimeError("no device step")
 
     def _pinned(self, name: str, n: int):
         """A reused page-locked int64 buffer the device writes directly (its host tensor and the
         device address it is mapped at): words the host reads after a stream sync, with no copy."""
         got = self._bufs.get("_pin_" + name)
+        if not self._cuda and (got is None or got[0].numel() < n):  # (host mode: plain memory)
+            t = torch.zeros(max(n, 16), dtype=torch.int64)
+            got = (t, t.data_ptr())
+            self._bufs["_pin_" + name] = got
         if got is None or got[0].numel() < n:
             t = torch.zeros(max(n, 16), dtype=torch.int64, pin_memory=True)
             d = ctypes.c_void_p()
@@ -598,6 +627,8 @@ class ShardedMatcher:
         """The device tensors' values (int64) on the host: one copy into a reused pinned buffer
         and a wait for this stream (no allocation per call)."""
         k = sum(int(t.numel()) for t in parts)
+        if not self._cuda:
+            return torch.cat([t.reshape(-1) for t in parts]).numpy().astype(np.int64)
         hb = self._bufs.get("_host")
         if hb is None or hb.numel() < k:
             hb = torch.empty(max(k, 256), dtype=torch.int64, pin_memory=True)
@@ -634,7 +665,7 @@ class ShardedMatcher:
         Every rank runs the same schedule, so the collectives pair up.  ``exchange``: the
         exchange-point function (default ``_exchange``: the process group; ``EmulatedWorld``
         passes a recorded one).  Returns every batch's (offsets, ids)."""
-        assert self._lanes[0].step is not None, "match_stream needs the device step"
+        assert self._cuda, "match_stream keeps steps in flight on device streams"
         ex = exchange or self._exchange
         caller = torch.cuda.current_stream(self.device)
         lanes = [self._lane_n(0), self._lane_n(1)]
@@ -709,7 +740,8 @@ class ShardedMatcher:
         of every source's chunk for this rank (``_exchange_chunks``)."""
         if op[0] == "local_sizes":  # world 1: words the device wrote into mapped pinned memory
             _, words, W = op
-            torch.cuda.current_stream(self.device).synchronize()
+            if self._cuda:
+                torch.cuda.current_stream(self.device).synchronize()
             lst = words[: W * self.world].tolist()
             return lst, lst, words
         if op[0] == "sizes":
@@ -740,7 +772,7 @@ class ShardedMatcher:
         st = self._step.h
         mark = _host_marks() if _SHARD_PROF else (lambda k: None)
         mark(0)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = torch.cuda.current_stream(dev).cuda_stream if self._cuda else None
         P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         PA = lambda ts: (ctypes.c_void_p * E)(*[None if t is None else t.data_ptr() for t in ts])  # noqa: E731
         S = ctypes.c_void_p(stream)
@@ -759,7 +791,7 @@ class ShardedMatcher:
         meta = None if G == 1 else torch.empty(MW * G, dtype=torch.int64, device=dev)
         _lib.check(L.emqx_shard_step_send(st, P(tb), P(to), n, P(send), send.numel(),
                                           ctypes.c_void_p(dmeta) if G == 1 else P(meta), S), "emqx_shard_step_send")
-        cur = torch.cuda.current_stream(dev)
+        cur = torch.cuda.current_stream(dev) if self._cuda else None
         mark(1)
         # (the split sizes as Python ints: this bookkeeping sits between the host sync and the
         # next launch, on the step's critical path, where numpy calls on a few words cost more
@@ -794,7 +826,7 @@ class ShardedMatcher:
         outs = []
         hsumm, dsumm = self._pinned("summary", 8 * E)  # written by each engine call that runs
 
-        if self._stream_b is None:
+        if self._stream_b is None and self._cuda:
             self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E - 1)]
         used = []
         for e, (eb, eo, ne) in enumerate(batches):
@@ -804,13 +836,13 @@ class ShardedMatcher:
                 continue
             cap_e = max(self._caps[e], 1 << 16)
             ri = self._buf(f"ids{e}", cap_e, torch.int32)
-            es = cur if not used else self._stream_b[len(used) - 1]
+            es = cur if not used or not self._cuda else self._stream_b[len(used) - 1]
             if es is not cur:
                 es.wait_stream(cur)
             used.append(es)
             self.engines[e].match_device_async(eb, eo.data_ptr(), ne, ro.data_ptr(), ri.data_ptr(),
                                                ri.numel(), dsumm + 64 * e, mode=self.mode,
-                                               stream=es.cuda_stream)
+                                               stream=es.cuda_stream if es is not None else None)
             outs.append([ro, ri])
         for es in used:
             if es is not cur:
@@ -859,86 +891,6 @@ class ShardedMatcher:
         mark(7)
         return out_off, out_ids[:total]
 
-    def _match_all_tensors(self, topics: Tuple[torch.Tensor, torch.Tensor]):  # noqa: C901
-        """match_all with torch tensor ops (an injected match_fn: the distribution logic on CPU
-        over gloo in the tests)."""
-        dev, G, grp = self.device, self.world, self.group
-        E = SHARD_ENGINES
-        i64 = dict(dtype=torch.int64, device=dev)
-        tb, to = topics
-        tb, to = tb.to(dev), to.to(dev).to(torch.int64)
-        n = to.numel() - 1
-        # 1. requests: (topic, rank * 3 + slot), sorted by destination bucket (stable)
-        raw = topic_requests(tb, to, G, self.plan, self.plan_dev)
-        bucket = fold_requests(raw, G).reshape(-1)
-        order = torch.sort(bucket, stable=True)[1]
-        counts = torch.bincount(bucket, minlength=E * G + 1)[: E * G]  # per (rank, slot)
-        req_topic = torch.div(order, 2, rounding_mode="floor")
-        lens = (to[1:] - to[:-1]).to(torch.int64)
-        rank_of = torch.arange(E * G, device=dev) // E
-        valid_lens = lens[req_topic] * (bucket[order] < E * G).to(torch.int64)
-        bytes_per_bucket = torch.zeros(E * G + 1, **i64).index_add_(0, bucket[order], valid_lens)[: E * G]
-        bytes_to = torch.zeros(G, **i64).index_add_(0, rank_of, bytes_per_bucket)
-        # 2. sizes: one all-to-all of (slot-0, slot-1, slot-2 requests, bytes) per destination
-        send_meta = torch.cat([counts.reshape(G, E), bytes_to[:, None]], 1).reshape(-1)
-        recv_meta = torch.empty((E + 1) * G, **i64)
-        _a2a(recv_meta, send_meta, [E + 1] * G, [E + 1] * G, grp)
-        meta = torch.stack([send_meta, recv_meta]).cpu()  # host sync 1
-        sm, rm = meta[0].reshape(G, E + 1), meta[1].reshape(G, E + 1)
-        n_out = sm[:, :E].sum(1).tolist()
-        b_out = sm[:, E].tolist()
-        nq_in = rm[:, :E].tolist()  # [source][slot]
-        n_in = [sum(x) for x in nq_in]
-        b_in = rm[:, E].tolist()
-        n_req = sum(n_out)
-        req_topic = req_topic[:n_req]
-        req_second = (bucket[order][:n_req] % E) == 1  # a B request follows its topic's A request
-        # 3. the requests' topics, grouped by destination, to their owners
-        bytes_p, offs_p = _gather_topics(tb, to, req_topic)
-        lens_p = offs_p[1:] - offs_p[:-1]
-        my_lens = torch.empty(sum(n_in), **i64)
-        _a2a(my_lens, lens_p, n_in, n_out, grp)
-        my_bytes = torch.empty(max(sum(b_in), 1), dtype=torch.uint8, device=dev)
-        _a2a(my_bytes[:sum(b_in)], bytes_p[:sum(b_out)], b_in, b_out, grp)
-        my_offs = torch.zeros(sum(n_in) + 1, **i64)
-        if sum(n_in):
-            my_offs[1:] = torch.cumsum(my_lens, 0)
-        # 4. received: [src 0: slot 0..., 1..., 2...][src 1: ...]...; each slot's part on its engine
-        starts = np.concatenate([[0], np.cumsum(n_in)[:-1]]).astype(np.int64)
-        idx = []
-        for e in range(E):
-            parts = []
-            for s_ in range(G):
-                lo = int(starts[s_] + sum(nq_in[s_][:e]))
-                parts.append(torch.arange(lo, lo + int(nq_in[s_][e]), **i64))
-            idx.append(torch.cat(parts))
-        cnts, idss = [], []
-        for e in range(E):
-            if idx[e].numel():
-                eb, eo = _gather_topics(my_bytes, my_offs, idx[e])
-                c, i_ = self.match_fn(e, eb, eo)
-            else:
-                c, i_ = torch.zeros(0, **i64), torch.zeros(0, dtype=torch.int32, device=dev)
-            cnts.append(c.to(torch.int64).to(dev))
-            idss.append(i_.to(torch.int32).to(dev))
-        self.last_local_topics = sum(n_in)
-        # back in received order (a permutation of the received positions)
-        r_off, r_ids = merge_csr(torch.cat(cnts), torch.cat(idss), torch.cat(idx))
-        r_cnt = r_off[1:] - r_off[:-1]
-        # 5. answers back to each source: counts per request, then ids (totals first)
-        bounds = torch.tensor(np.concatenate([[0], np.cumsum(n_in)]).astype(np.int64), **i64)
-        ids_out_t = r_off[bounds[1:]] - r_off[bounds[:-1]]
-        ids_in_t = torch.empty(G, **i64)
-        _a2a(ids_in_t, ids_out_t, [1] * G, [1] * G, grp)
-        tot = torch.stack([ids_out_t, ids_in_t]).cpu()  # host sync 2
-        ids_out, ids_in = tot[0].tolist(), tot[1].tolist()
-        cnt_back = torch.empty(n_req, **i64)
-        _a2a(cnt_back, r_cnt, n_out, n_in, grp)
-        ids_back = torch.empty(sum(ids_in), dtype=torch.int32, device=dev)
-        _a2a(ids_back, r_ids, ids_in, ids_out, grp)
-        # 6. merge per topic in batch order: a topic's first request's answer, then its second's
-        return merge_requests(cnt_back, ids_back, req_topic, req_second.to(torch.int64), n, sum(ids_in))
-
     def match(self, topics: Optional[Tuple[torch.Tensor, torch.Tensor]], src: int = 0, dst: int = 0):
         """Match a batch held by rank ``src``; rank ``dst`` gets the CSR in batch order
         (offsets int64 (n+1,), ids int32), the other ranks None.  Every rank takes part (the
@@ -960,28 +912,6 @@ class ShardedMatcher:
             ids = _p2p(None, src, False, self.group, like=torch.empty(int(sz[1]), dtype=torch.int32, device=dev))
             return off, ids
         return None
-
-
-def merge_requests(cnt: torch.Tensor, ids: torch.Tensor, req_topic: torch.Tensor, req_engine: torch.Tensor, n: int,
-                   total: int):
-    """Per-request answers (counts in request order, ids request after request) -> the CSR of
-    n topics in batch order, each topic's first request's ids (req_engine 0: engine A or AB)
-    before its second's (req_engine 1: engine B).  `total` = the id count (known on the host
-    from the exchange), so no further synchronisation."""
-    dev = cnt.device
-    cnt = cnt.to(torch.int64)
-    per_topic = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, req_topic, cnt)
-    a_part = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, req_topic, cnt * (req_engine == 0))
-    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    if n:
-        offsets[1:] = torch.cumsum(per_topic, 0)
-    out = torch.empty(total, dtype=torch.int32, device=dev)
-    if total:
-        base = offsets[req_topic] + a_part[req_topic] * (req_engine == 1)
-        roff = torch.cumsum(cnt, 0) - cnt
-        k = torch.repeat_interleave(torch.arange(cnt.numel(), device=dev), cnt, output_size=total)
-        out[base[k] + (torch.arange(total, device=dev) - roff[k])] = ids.to(torch.int32)
-    return offsets, out
 
 
 class EmulatedWorld:

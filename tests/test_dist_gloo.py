@@ -1,12 +1,16 @@
 """Multi-process (gloo, CPU, world sizes 2, 4 and 8) checks of the multi-GPU layouts in
 emqx_amd/dist.py.
 
-The per-shard match is injected from the oracle (test infrastructure) so that the
-distribution logic — two key spaces (first level, and second level under a root '+') with
-hot keys split by the next level, root wildcards replicated, every topic's requests to at most
-two (rank, engine) owners, the two all-to-alls and the per-topic merge back into batch order —
-is checked against a single-table oracle run.  The HIP match itself is covered by the GPU
-tests."""
+The match_all tests drive the product's step (dist.py ShardedMatcher._step_gen: the same
+protocol, exchanges, chunk formats, redo and bookkeeping as on the GPUs) with the step object in
+its host mode (emqx_shard_step_create(-1, ...): shard_step.hip's per-item bodies — routing and
+fold (layout.h), layout, pack, unpack, answer, gather, merge — as loops over host memory) and
+each rank's engines answered by the oracle (test infrastructure), over gloo; the result is
+checked against a single-table oracle run.  So the CPU rehearsal and the device step cannot
+drift apart: only the per-slot match and the tile sort's parallel form differ.  The layout
+tests check the placement (two key spaces — first level, and second level under a root '+' —
+or space P replicated; hot keys split by the next level; root wildcards on every rank) covers
+every match.  The HIP match itself is covered by the GPU tests."""
 
 import os
 import socket
@@ -175,6 +179,50 @@ def test_sharded_match_all_sources(world, p_space):
     for rank, tb, to, off, ids in got:
         off_o, ids_o, _ = o.match_csr(tb if len(tb) else np.zeros(1, np.uint8), to, mode=0, threads=2)
         assert C.csr_mismatches(off, ids, off_o, ids_o).size == 0, rank
+
+
+def _worker_redo(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from emqx_amd import workloads as W
+        wl = W.config_b(n_filters=60_000, n_topics=60_000, seed=7, topic_seed=None if rank == 0 else 70 + rank)
+        sm = _matcher(wl.filters, rank, world, "sharded")
+        sm._caps = [1, 1, 1]  # the 64 K-id floor is below a slot's ids: every engine call overflows
+        t = (torch.from_numpy(wl.topics[0].copy()), torch.from_numpy(wl.topics[1].astype(np.int64)))
+        off, ids = sm.match_all(t)
+        learnt = max(sm._caps) > 65536
+        again = sm.match_all(t)  # learnt capacities: no redo, the same CSR
+        same = torch.equal(again[0], off) and torch.equal(again[1], ids)
+        q.put((rank, wl.topics[0].copy(), wl.topics[1].copy(), off.numpy(), ids.numpy(), learnt, same, wl.filters))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_redo_on_small_capacities():
+    """The redo protocol of the step at world 2: every rank's engine calls overflow their (forced)
+    capacities, the answer chunks carry the flag, every rank redoes the answer exchange, and each
+    source's CSR equals the oracle's; the learnt capacities then need no redo."""
+    from oracle import cpp as C
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_redo, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    o = C.CppOracle(True)
+    o.add_packed(*got[0][7])
+    for rank, tb, to, off, ids, learnt, same, _ in got:
+        off_o, ids_o, _ = o.match_csr(tb, to, mode=0, threads=2)
+        assert int(off_o[-1]) > 3 * 65536
+        assert C.csr_mismatches(off, ids, off_o, ids_o).size == 0, rank
+        assert learnt and same
 
 
 def test_shard_layout_covers_every_match():

@@ -74,9 +74,16 @@ def test_shard_step_edge_batches_world1():
         topics = pack(TOPICS)
         got = sm.match_all(_dev_topics(topics))
         assert _check(got, filters, topics) > 0
-        # the same batch through the tensor path (engines as match_fn): the same CSR, in order
-        off_t, ids_t = sm._match_all_tensors(_dev_topics(topics))
-        assert torch.equal(off_t.cpu(), got[0].cpu()) and torch.equal(ids_t.cpu(), got[1].cpu())
+        # the same batch through the step's host mode (tests/test_dist_gloo.py's path: the same
+        # protocol, the kernels' bodies as loops) with this GPU's engine as the slot matcher:
+        # the same CSR, in the same order
+        def on_gpu(e, tb, to):
+            off, ids = sm._engine_csr(2, tb.cuda(), to.cuda())
+            return (off[1:] - off[:-1]).cpu(), ids.cpu()
+        host = ShardedMatcher(filters, device=torch.device("cpu"), match_fn=on_gpu)
+        off_h, ids_h = host.match_all((torch.from_numpy(topics[0].copy()), torch.from_numpy(topics[1].astype(np.int64))))
+        assert torch.equal(off_h, got[0].cpu()) and torch.equal(ids_h, got[1].cpu())
+        host.close()
         # an empty batch, a one-topic batch, and a batch of topics no filter besides roots matches
         empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
         off, ids = sm.match_all(_dev_topics(empty))
