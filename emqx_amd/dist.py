@@ -213,22 +213,33 @@ def _exchange_chunks(send: torch.Tensor, out_sz: List[int], in_sz: List[int], re
     base = send.data_ptr()
     if G == 1:
         return [base]
-    out_off = np.concatenate([[0], np.cumsum(out_sz)]).astype(np.int64)
     es = send.element_size()
-    if dist.get_backend(group) == "gloo":
-        in_off = np.concatenate([[0], np.cumsum(in_sz)]).astype(np.int64)
-        recv = recv_buf(int(in_off[-1]))
+    gloo = dist.get_backend(group) == "gloo"
+    out_off, in_off, _ = chunk_offsets(out_sz, in_sz, rank, skip_own=not gloo)
+    recv = recv_buf(int(in_off[-1]))
+    if gloo:
         _a2a(recv[: int(in_off[-1])], send[: int(out_off[-1])], in_sz, out_sz, group)
     else:
-        in_sz = [0 if r == rank else x for r, x in enumerate(in_sz)]
-        in_off = np.concatenate([[0], np.cumsum(in_sz)]).astype(np.int64)
-        recv = recv_buf(int(in_off[-1]))
         empty = send[:0]
         outs = [recv[int(in_off[r]): int(in_off[r + 1])] if r != rank else empty for r in range(G)]
         ins = [send[int(out_off[r]): int(out_off[r + 1])] if r != rank else empty for r in range(G)]
         dist.all_to_all(outs, ins, group=group)
-    rb = recv.data_ptr()
-    return [base + es * int(out_off[r]) if r == rank else rb + es * int(in_off[r]) for r in range(G)]
+    return chunk_offsets(out_sz, in_sz, rank, skip_own=not gloo, base=base, rbase=recv.data_ptr(), es=es)[2]
+
+
+def chunk_offsets(out_sz: List[int], in_sz: List[int], rank: int, skip_own: bool, base: int = 0, rbase: int = 0,
+                  es: int = 1):
+    """The chunk exchange's arithmetic (``_exchange_chunks``): (send offsets, receive offsets,
+    the address of every source's chunk for this rank).  Chunk r of the send buffer starts at the
+    prefix of out_sz; source s's chunk lands in the receive buffer at the prefix of in_sz, where
+    with ``skip_own`` (RCCL's list all_to_all: the own entry empty) the own chunk takes no room;
+    the own chunk is always read where it was packed (base + its send offset)."""
+    G = len(out_sz)
+    out_off = np.concatenate([[0], np.cumsum(out_sz)]).astype(np.int64)
+    in_eff = [0 if (skip_own and r == rank) else x for r, x in enumerate(in_sz)]
+    in_off = np.concatenate([[0], np.cumsum(in_eff)]).astype(np.int64)
+    addrs = [base + es * int(out_off[r]) if r == rank else rbase + es * int(in_off[r]) for r in range(G)]
+    return out_off, in_off, addrs
 
 
 SHARD_NONE = 0xFFFFFFFF

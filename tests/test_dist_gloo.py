@@ -324,3 +324,33 @@ def test_partition_and_merge_roundtrip():
     off, ids = D.merge_csr(rc, ri, perm)
     assert off.tolist() == [0, 1, 1, 1, 4, 6, 7]
     assert ids.tolist() == [0, 30, 31, 32, 40, 41, 50]
+
+
+@pytest.mark.parametrize("skip_own", [False, True])
+def test_chunk_exchange_addresses(skip_own):
+    """dist.py chunk_offsets, the address arithmetic of _exchange_chunks for both exchanges:
+    gloo's all_to_all_single (every chunk, the own one included, in rank order) and RCCL's list
+    all_to_all (the own entry empty; ADVICE r5: that branch has not run on several GPUs).  Both
+    collectives are simulated on host arrays from their definitions, and every source's chunk
+    is read back through the returned address."""
+    from emqx_amd import dist as D
+    rng = np.random.default_rng(3)
+    for G in (2, 3, 8):
+        sizes = rng.integers(0, 40, size=(G, G))  # sizes[s][r]: bytes source s sends rank r
+        sends = [rng.integers(0, 255, size=int(sizes[s].sum()), dtype=np.uint8) for s in range(G)]
+        for rank in range(G):
+            out_sz = sizes[rank].tolist()
+            in_sz = sizes[:, rank].tolist()
+            out_off, in_off, addrs = D.chunk_offsets(out_sz, in_sz, rank, skip_own, base=0, rbase=1 << 20)
+            recv = np.zeros(int(in_off[-1]), np.uint8)
+            for s in range(G):  # the collective: source s's chunk for `rank` at its receive offset
+                if skip_own and s == rank:
+                    continue
+                lo = int(np.sum(sizes[s][:rank]))
+                recv[int(in_off[s]): int(in_off[s + 1])] = sends[s][lo: lo + int(sizes[s][rank])]
+            for s in range(G):
+                lo = int(np.sum(sizes[s][:rank]))
+                want = sends[s][lo: lo + int(sizes[s][rank])]
+                a = addrs[s]
+                got = sends[rank][a: a + len(want)] if s == rank else recv[a - (1 << 20): a - (1 << 20) + len(want)]
+                assert np.array_equal(got, want), (G, rank, s)
