@@ -174,7 +174,8 @@ void walk(const DevImage& t, const VocabState& v, const uint8_t* p, uint64_t n, 
 // by item level and node kind, so layout ideas can be priced on the CPU before they are built.
 struct SimItem {
   uint32_t base, meta, litf, widx;
-  uint8_t topic, flags;  // flags: 1 root, 2 dollar root, 4 no literal probe, 8 chain parent
+  uint8_t topic, flags;  // flags: 1 root, 2 dollar root, 4 no literal probe, 8 chain parent,
+                         // 16 spine (reached from the root by literal edges only)
 };
 
 struct SimL2 {
@@ -211,7 +212,7 @@ enum SimOut : uint32_t {
   SO_TOPICS, SO_TILES, SO_ITEMS, SO_LOADS, SO_ACC, SO_MISS, SO_VLOADS, SO_VMISS, SO_BOTH, SO_BOTH_SPLIT,
   SO_CHAIN, SO_CHAIN_MISS, SO_MISS_L0, SO_ITEMS_L0 = SO_MISS_L0 + 8, SO_WIDE = SO_ITEMS_L0 + 8, SO_WIDE_MISS,
   SO_STEPS, SO_PLUS_MISS, SO_LIT_MISS, SO_EMITS, SO_PLUS_LOADS, SO_PH_LOADS, SO_WIDE_LOADS, SO_HITS_L0,
-  SO_N = SO_HITS_L0 + 8
+  SO_SPINE = SO_HITS_L0 + 8, SO_SPINE_LIT_MISS, SO_N
 };
 
 struct SimTile {
@@ -250,7 +251,7 @@ void sim_tile_init(const DevImage& t, const VocabState& v, const uint8_t* tb, co
     const bool dollar = n > 0 && p[0] == '$';
     const uint32_t rmeta = dollar ? (t.root_meta & ~META_HAS_PLUS) : t.root_meta;
     st.stack.push_back({t.root_base, rmeta, 0, wb, static_cast<uint8_t>(q - t0),
-                        static_cast<uint8_t>(1 | (dollar ? 2 : 0))});
+                        static_cast<uint8_t>(1 | 16 | (dollar ? 2 : 0))});
   }
 }
 
@@ -276,13 +277,16 @@ void sim_tile_step(const DevImage& t, SimTile& st, std::vector<std::pair<uint64_
     const bool wide = needL && !(it.meta & META_PH);
     // a chain item: a node whose only edge is one literal (a unique filter suffix, typically)
     const bool chain = (it.meta & META_LITF_EXACT) && !needP && !(it.flags & 1);
+    const bool spine = (it.flags & 16) != 0;
     const uint32_t cls = lvl | (wide ? 16u : 0u) | (chain ? 32u : 0u);
+    const uint32_t lcls = cls | (spine ? 128u : 0u);  // (its literal probe: class bit 7 on the spine)
     o[SO_ITEMS] += 1;
+    o[SO_SPINE] += spine ? 1 : 0;
     o[SO_ITEMS_L0 + lvl] += 1;
     o[SO_WIDE] += wide ? 1 : 0;
     o[SO_CHAIN] += chain ? 1 : 0;
     uint64_t c[2];
-    int nc = 0;
+    int nc = 0, lit_k = -1;  // (lit_k: which child came through the literal edge)
     uint64_t pa = ~0ull, la = ~0ull;
     size_t plus_at = ~size_t(0);
     if (needP) {
@@ -297,26 +301,29 @@ void sim_tile_step(const DevImage& t, SimTile& st, std::vector<std::pair<uint64_
       uint64_t f = ~0ull;
       if (it.meta & META_PH) {
         la = it.base + lit_slot(wid, sd, mask, plus_copies(t.plus_mask, it.meta & META_HAS_PLUS, caplog));
-        acc.push_back({16ull * la, cls});
+        acc.push_back({16ull * la, lcls});
         o[SO_PH_LOADS] += 1;
         if (t.edges[la].wid == wid) f = la;
       } else {
         const bool cp = plus_copies(t.plus_mask, it.meta & META_HAS_PLUS, caplog);
         la = it.base + wide_slot(wid, sd, mask, cp, false);
-        acc.push_back({16ull * la, cls});
-        acc.push_back({16ull * la + 16, cls});
+        acc.push_back({16ull * la, lcls});
+        acc.push_back({16ull * la + 16, lcls});
         o[SO_WIDE_LOADS] += 2;
         for (uint32_t k = 0; k < 2 && f == ~0ull; ++k)
           if (t.edges[la + k].wid == wid) f = la + k;
         if (f == ~0ull && (t.edges[la].meta & META_BUCKET_OVF)) {
           const uint64_t l2 = it.base + wide_slot(wid, sd, mask, cp, true);
-          acc.push_back({16ull * l2, cls});
-          acc.push_back({16ull * l2 + 16, cls});
+          acc.push_back({16ull * l2, lcls});
+          acc.push_back({16ull * l2 + 16, lcls});
           for (uint32_t k = 0; k < 2 && f == ~0ull; ++k)
             if (t.edges[l2 + k].wid == wid) f = l2 + k;
         }
       }
-      if (f != ~0ull) c[nc++] = f;
+      if (f != ~0ull) {
+        lit_k = nc;
+        c[nc++] = f;
+      }
     }
     if (plus_copies(t.plus_mask, needP, caplog) && plus_at != ~size_t(0) && la != ~0ull) {  // the copy in the literal's line
       acc[plus_at].first = 16ull * (it.base + plus_copy(static_cast<uint32_t>(la - it.base), true));
@@ -342,7 +349,8 @@ void sim_tile_step(const DevImage& t, SimTile& st, std::vector<std::pair<uint64_
       if (!(cs.meta & META_HAS_EDGES)) continue;
       const bool nl = nwid == WID_NONE || !litf_may_contain(cs.meta, cs.litf, nwid);
       if (nl && !(cs.meta & META_HAS_PLUS)) continue;
-      push.push_back({cs.child_base, cs.meta, cs.litf, it.widx + 1, it.topic, static_cast<uint8_t>(nl ? 4 : 0)});
+      push.push_back({cs.child_base, cs.meta, cs.litf, it.widx + 1, it.topic,
+                      static_cast<uint8_t>((nl ? 4 : 0) | (spine && k == lit_k ? 16 : 0))});
     }
   }
   st.stack.insert(st.stack.end(), push.begin(), push.end());
@@ -597,6 +605,7 @@ int emqx_htrie_walk_sim(emqx_htrie* h, const uint8_t* topic_bytes, const uint64_
             o[SO_WIDE_MISS] += (cls & 16u) ? 1 : 0;
             o[SO_CHAIN_MISS] += (cls & 32u) ? 1 : 0;
             o[(cls & 8u) ? SO_PLUS_MISS : SO_LIT_MISS] += 1;
+            o[SO_SPINE_LIT_MISS] += (cls & 128u) ? 1 : 0;
           }
         }
       }

@@ -23,7 +23,7 @@ NAMES = ["topics", "tiles", "items", "loads", "l2_accesses", "l2_misses", "vocab
          "items_both_probes", "both_probes_split_lines", "chain_items", "chain_misses"] + \
         ["misses_l%d" % i for i in range(8)] + ["items_l%d" % i for i in range(8)] + \
         ["wide_items", "wide_misses", "steps", "plus_misses", "literal_misses", "emits", "plus_loads", "ph_loads",
-         "wide_loads"] + ["hits_l%d" % i for i in range(8)]
+         "wide_loads"] + ["hits_l%d" % i for i in range(8)] + ["spine_items", "spine_literal_misses"]
 
 
 def main():
