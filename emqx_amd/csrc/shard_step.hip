@@ -612,7 +612,7 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
                                                                  const uint32_t* __restrict__ err,
                                                                  uint8_t* __restrict__ send,
                                                                  uint32_t* __restrict__ key_s, uint32_t* __restrict__ perm,
-                                                                 uint32_t one) {
+                                                                 uint32_t one, uint32_t* __restrict__ tpos) {
   __shared__ uint32_t run_c[kMaxBuckets];
   __shared__ uint64_t run_b[kMaxBuckets];
   __shared__ uint32_t w_c[4][kMaxBuckets];
@@ -687,6 +687,7 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
       const uint32_t pos = pc + rc;
       key_s[pos] = k;
       perm[pos] = static_cast<uint32_t>(p);
+      if (one) tpos[p] = pos;  // (request p = topic p)
       if (pack && k < nb - 1) pack_request(send, k, pos, pb + rb, s_ob, s_bp, s_db, tb + a, l);
     }
     __syncthreads();
@@ -901,6 +902,40 @@ struct SelfIds {
 // own engine output) and how many, stored at the request's own index perm[p] (2t: a topic's
 // first request, 2t + 1 its second) — the merge then reads them per topic, coalesced.  With one
 // request a topic (`one`: perm[p] = the topic) it goes to 2t and 2t + 1 says none.
+// Sorted request p's answer: its ids' count and where they are.
+__host__ __device__ inline uint32_t request_answer(const ShardTab& tab, const SelfIds& me,
+                                                   const uint32_t* __restrict__ key_s,
+                                                   const uint32_t* __restrict__ start, uint64_t p, uint64_t* src_out) {
+  const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
+  const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
+  uint32_t before = 0, ibefore = 0;  // the chunk's requests / ids of the earlier slots
+  for (uint32_t k = 0; k < e; ++k) {
+    before += ch[k];
+    ibefore += ch[3 + k];
+  }
+  const uint32_t k = before + (p - start[b]);
+  const uint32_t b0 = k ? ch[kHW + k - 1] : 0u;
+  const uint32_t* src = r == me.self ? me.ids[e] + me.off[e][me.q0[e]] + (b0 - ibefore)
+                                     : ch + kHW + ch[0] + ch[1] + ch[2] + b0;
+  *src_out = reinterpret_cast<uint64_t>(src);
+  return ch[kHW + k] - b0;
+}
+
+// One request a topic, in topic order: topic t's request sits at sorted position tpos[t]; its
+// count and address go to the topic's pair (2t; 2t + 1 says none) and its total straight to
+// tcnt — coalesced writes, and no separate topic-count pass.
+__host__ __device__ inline void gather_topic(const ShardTab& tab, const SelfIds& me, const uint32_t* __restrict__ key_s,
+                                             const uint32_t* __restrict__ tpos, const uint32_t* __restrict__ start,
+                                             uint32_t nreq, uint64_t t, uint32_t* __restrict__ rq_cnt,
+                                             uint64_t* __restrict__ rq_src, uint32_t* __restrict__ tcnt) {
+  const uint32_t p = tpos[t];
+  uint64_t src = 0;
+  const uint32_t c = p < nreq ? request_answer(tab, me, key_s, start, p, &src) : 0u;
+  *reinterpret_cast<uint2*>(rq_cnt + 2 * t) = make_uint2(c, 0u);
+  rq_src[2 * t] = src;
+  tcnt[t] = c;
+}
+
 __host__ __device__ inline void gather_request(const ShardTab& tab, const SelfIds& me, const uint32_t* __restrict__ key_s,
                                                const uint32_t* __restrict__ perm, const uint32_t* __restrict__ start,
                                                uint32_t nreq, uint64_t p, uint32_t* __restrict__ rq_cnt,
@@ -912,19 +947,9 @@ __host__ __device__ inline void gather_request(const ShardTab& tab, const SelfId
       rq_cnt[q] = 0;
       return;
     }
-    const uint32_t b = key_s[p], r = b / kE, e = b - kE * r;
-    const uint32_t* ch = reinterpret_cast<const uint32_t*>(tab.chunk[r]);
-    uint32_t before = 0, ibefore = 0;  // the chunk's requests / ids of the earlier slots
-    for (uint32_t k = 0; k < e; ++k) {
-      before += ch[k];
-      ibefore += ch[3 + k];
-    }
-    const uint32_t k = before + (p - start[b]);
-    const uint32_t b0 = k ? ch[kHW + k - 1] : 0u;
-    rq_cnt[q] = ch[kHW + k] - b0;
-    const uint32_t* src = r == me.self ? me.ids[e] + me.off[e][me.q0[e]] + (b0 - ibefore)
-                                       : ch + kHW + ch[0] + ch[1] + ch[2] + b0;
-    rq_src[q] = reinterpret_cast<uint64_t>(src);
+    uint64_t src = 0;
+    rq_cnt[q] = request_answer(tab, me, key_s, start, p, &src);
+    rq_src[q] = src;
   }
 }
 
@@ -938,6 +963,18 @@ __global__ __launch_bounds__(256) void shard_gather_kernel(ShardTab tab, SelfIds
   for (uint64_t p = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; p < m;
        p += static_cast<uint64_t>(gridDim.x) * blockDim.x)
     gather_request(tab, me, key_s, perm, start, nreq, p, rq_cnt, rq_src, one);
+}
+
+__global__ __launch_bounds__(256) void shard_gather_topic_kernel(ShardTab tab, SelfIds me,
+                                                                 const uint32_t* __restrict__ key_s,
+                                                                 const uint32_t* __restrict__ tpos,
+                                                                 const uint32_t* __restrict__ start, uint64_t n,
+                                                                 uint32_t world, uint32_t* __restrict__ rq_cnt,
+                                                                 uint64_t* __restrict__ rq_src, uint32_t* __restrict__ tcnt) {
+  const uint32_t nreq = start[kE * world];
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n;
+       t += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    gather_topic(tab, me, key_s, tpos, start, nreq, t, rq_cnt, rq_src, tcnt);
 }
 
 __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t* __restrict__ rq_cnt, uint64_t n,
@@ -1009,6 +1046,7 @@ struct emqx_shard_step {
            *tcnt_tab = nullptr, *tbytes_tab = nullptr;  // (tab: the sort's (bucket, tile) table)
   uint64_t *partials = nullptr, *pbytes_tab = nullptr, *rq_src = nullptr;  // (pos: merge's rq_cnt)
   uint64_t* segsum = nullptr;  // the sort scan's segment totals (2 per kScanSeg table entries)
+  uint32_t* tpos = nullptr;    // one request a topic: topic t's sorted position
   uint32_t* start = nullptr;  // [kE G + 2]
   uint64_t* cbase = nullptr;  // [G]
   uint64_t* bpre = nullptr;   // [kE G + 2]: each bucket's first byte among the sorted requests'
@@ -1029,7 +1067,7 @@ struct emqx_shard_step {
   // (tests/test_dist_gloo.py drives dist.py's step with it).
   bool host = false;
   std::vector<ShardSplitE> h_splits;
-  std::vector<uint32_t> h_key, h_key_s, h_perm, h_pos, h_tcnt, h_start;
+  std::vector<uint32_t> h_key, h_key_s, h_perm, h_pos, h_tcnt, h_start, h_tpos;
   std::vector<uint64_t> h_rq_src, h_bpre, h_cbase;
   std::vector<int64_t> h_obase, h_dbase;
 };
@@ -1041,9 +1079,9 @@ void free_scratch(emqx_shard_step* st) {
                   static_cast<void*>(st->perm), static_cast<void*>(st->pos),
                   static_cast<void*>(st->tcnt), static_cast<void*>(st->partials),
                   static_cast<void*>(st->rq_src), static_cast<void*>(st->tbytes_tab), static_cast<void*>(st->pbytes_tab),
-                  static_cast<void*>(st->segsum)})
+                  static_cast<void*>(st->segsum), static_cast<void*>(st->tpos)})
     if (p) (void)hipFree(p);
-  st->key = st->tcnt_tab = st->key_s = st->perm = st->pos = st->tcnt = st->tbytes_tab = nullptr;
+  st->key = st->tcnt_tab = st->key_s = st->perm = st->pos = st->tcnt = st->tbytes_tab = st->tpos = nullptr;
   st->partials = st->pbytes_tab = st->rq_src = st->segsum = nullptr;
   st->m_cap = 0;
 }
@@ -1070,6 +1108,7 @@ hipError_t ensure_scratch(emqx_shard_step* st, uint64_t m) {
   al(&st->pos, 4 * cap);
   al(&st->rq_src, 8 * cap);
   al(&st->tcnt, 4 * (cap / 2 + 1));
+  al(&st->tpos, 4 * (cap / 2 + 1));
   al(&st->partials, 8 * scan_partials(cap));
   if (e != hipSuccess) {
     free_scratch(st);
@@ -1092,6 +1131,7 @@ int host_send(emqx_shard_step* st, const uint8_t* tb, const uint64_t* to, uint64
   st->h_key.assign(m, 0);
   st->h_key_s.assign(m, 0);
   st->h_perm.assign(m, 0);
+  st->h_tpos.assign(st->one ? n : 0, 0);
   for (uint64_t t = 0; t < n; ++t) {
     ShardTopicLevels L;
     shard_topic_levels(tb + to[t], to[t + 1] - to[t], &L);
@@ -1138,6 +1178,7 @@ int host_send(emqx_shard_step* st, const uint8_t* tb, const uint64_t* to, uint64
     const uint64_t pos = nextp[k]++;
     st->h_key_s[pos] = k;
     st->h_perm[pos] = static_cast<uint32_t>(p);
+    if (st->one) st->h_tpos[p] = static_cast<uint32_t>(pos);
     if (k == nb - 1 || over) continue;
     const uint64_t a = to[topic_of(p)];
     const uint32_t len = static_cast<uint32_t>(to[topic_of(p) + 1] - a);
@@ -1146,6 +1187,7 @@ int host_send(emqx_shard_step* st, const uint8_t* tb, const uint64_t* to, uint64
   }
   st->key_s = st->h_key_s.data();
   st->perm = st->h_perm.data();
+  st->tpos = st->h_tpos.data();
   return EMQX_OK;
 }
 
@@ -1155,9 +1197,15 @@ int host_merge(emqx_shard_step* st, const ShardTab& t, uint64_t* out_off, uint32
   st->h_pos.assign(2 * n + 2, 0);
   st->h_rq_src.assign(2 * n + 2, 0);
   const uint32_t nreq = st->start[kE * st->world];
-  for (uint64_t p = 0; p < m; ++p)
-    gather_request(t, st->self_ids, st->key_s, st->perm, st->start, nreq, p, st->h_pos.data(), st->h_rq_src.data(),
-                   st->one);
+  st->h_tcnt.assign(n + 1, 0);
+  if (st->one)
+    for (uint64_t q = 0; q < n; ++q)
+      gather_topic(t, st->self_ids, st->key_s, st->tpos, st->start, nreq, q, st->h_pos.data(), st->h_rq_src.data(),
+                   st->h_tcnt.data());
+  else
+    for (uint64_t p = 0; p < m; ++p)
+      gather_request(t, st->self_ids, st->key_s, st->perm, st->start, nreq, p, st->h_pos.data(), st->h_rq_src.data(),
+                     st->one);
   out_off[0] = 0;
   for (uint64_t q = 0; q < n; ++q) out_off[q + 1] = out_off[q] + st->h_pos[2 * q] + st->h_pos[2 * q + 1];
   if (n && !out_ids && out_off[n]) return EMQX_EINVAL;
@@ -1291,7 +1339,7 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
                        st->cbase, st->obase, st->dbase, st->err);
     hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_bytes, d_offsets, m, nb,
                        ntiles, st->tcnt_tab, st->pbytes_tab, st->bpre, st->obase, st->dbase, st->err, d_send,
-                       st->key_s, st->perm, st->one);
+                       st->key_s, st->perm, st->one, st->tpos);
   } else {
     SS_TRY(hipMemsetAsync(st->start, 0, 4ull * (kE * G + 2), s));
     SS_TRY(hipMemsetAsync(st->bpre, 0, 8ull * (kE * G + 2), s));
@@ -1425,7 +1473,10 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
   const uint64_t n = st->n, m = st->m;
-  if (m) {
+  if (m && st->one) {
+    hipLaunchKernelGGL(shard_gather_topic_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, t, st->self_ids, st->key_s,
+                       st->tpos, st->start, n, G, st->pos, st->rq_src, st->tcnt);
+  } else if (m) {
     hipLaunchKernelGGL(shard_gather_kernel, dim3(grid_of(m, 256)), dim3(256), 0, s, t, st->self_ids, st->key_s,
                        st->perm, st->start, m, G, st->pos, st->rq_src, st->one);
     hipLaunchKernelGGL(shard_topic_counts_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, st->pos, n, st->tcnt);
