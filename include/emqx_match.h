@@ -552,7 +552,11 @@ int emqx_csr_unpermute_device(const uint32_t* d_counts, const uint32_t* d_ids, u
  *   merge   ans_meta_in[3 * world] (host) = what the destinations sent, d_chunks[world] their
  *           answer chunks (host array of device pointers; this rank's own in place) ->
  *           the CSR of the batch given to send, in batch order (d_out_offsets[n + 1], d_out_ids:
- *           each topic's engine-A ids, then its engine-B ids; one slot-2 answer otherwise). */
+ *           each topic's engine-A ids, then its engine-B ids; one slot-2 answer otherwise).
+ * device < 0 creates the step in host mode: every pointer above is host memory, the calls run on
+ * the caller's thread and ignore `stream` (the kernels' per-item bodies as loops; the CPU tests'
+ * rehearsal of the protocol).  With one request a topic (world 1, or a plan that replicates
+ * space P) the sort runs over n requests and every request is a slot-2 request. */
 #define EMQX_SHARD_MAX_WORLD 64
 #define EMQX_SHARD_ENGINES 3
 typedef struct emqx_shard_step emqx_shard_step;
