@@ -243,10 +243,6 @@ def chunk_offsets(out_sz: List[int], in_sz: List[int], rank: int, skip_own: bool
 
 
 SHARD_NONE = 0xFFFFFFFF
-# match_stream's scheduling: the step's own kernels on a higher-priority lane stream, the engines
-# on streams of their own (EMQX_SHARD_PRIORITY=0: one priority, engines on the lane stream)
-_ENGINE_OWN_STREAM = os.environ.get("EMQX_SHARD_PRIORITY", "1") != "0"
-_STEP_PRIORITY = -1 if _ENGINE_OWN_STREAM else 0
 SHARD_ENGINES = 3  # engine slots of a rank: 0 = A, 1 = B, 2 = AB (include/emqx_match.h)
 MAX_PIECE_PM = 250  # a key is split when its filters exceed a quarter of a rank's share
 
@@ -686,7 +682,7 @@ class ShardedMatcher:
         lanes = [self._lane_n(0), self._lane_n(1)]
         for ln in lanes:
             if ln.stream is None:
-                ln.stream = torch.cuda.Stream(device=self.device, priority=_STEP_PRIORITY)
+                ln.stream = torch.cuda.Stream(device=self.device)
             ln.stream.wait_stream(caller)
         K = len(batches)
         gens, ops, res = {}, {}, [None] * K
@@ -842,7 +838,7 @@ class ShardedMatcher:
         hsumm, dsumm = self._pinned("summary", 8 * E)  # written by each engine call that runs
 
         if self._stream_b is None and self._cuda:
-            self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E)]
+            self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E - 1)]
         used = []
         for e, (eb, eo, ne) in enumerate(batches):
             ro = self._buf(f"off{e}", ne + 1, torch.int64)
@@ -851,11 +847,7 @@ class ShardedMatcher:
                 continue
             cap_e = max(self._caps[e], 1 << 16)
             ri = self._buf(f"ids{e}", cap_e, torch.int32)
-            # (the engines on streams of their own: with two steps in flight the step's kernels,
-            # on the lane's higher-priority stream, are dispatched into the other step's walk as
-            # its blocks retire instead of queueing behind it)
-            es = self._stream_b[len(used)] if self._cuda and _ENGINE_OWN_STREAM else (
-                cur if not used or not self._cuda else self._stream_b[len(used) - 1])
+            es = cur if not used or not self._cuda else self._stream_b[len(used) - 1]
             if es is not cur:
                 es.wait_stream(cur)
             used.append(es)
