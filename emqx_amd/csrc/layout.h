@@ -292,9 +292,21 @@ struct ShardSplitE {
 // a topic instead of two for a larger replicated part.
 constexpr uint32_t SHARD_P_REPLICATED = 0x0000FFFFu;
 
+// A level's hash: its bytes as little-endian 32-bit words (the last one zero-padded), FNV-style
+// over the words, then mixed with the length — a few word steps per level where a byte-wise
+// FNV took one step a byte (the device's routing scanner, shard_step.hip, was VALU-bound on it).
+EMQX_HD uint32_t shard_word_step(uint32_t h, uint32_t w) { return (h ^ w) * 0x01000193u; }
 EMQX_HD uint32_t shard_level_hash(const uint8_t* p, uint64_t s, uint64_t e) {
-  uint32_t h = 0x811C9DC5u;  // FNV-1a over the level's bytes
-  for (uint64_t i = s; i < e; ++i) h = (h ^ p[i]) * 0x01000193u;
+  uint32_t h = 0x811C9DC5u;
+  uint64_t i = s;
+  for (; i + 4 <= e; i += 4)
+    h = shard_word_step(h, static_cast<uint32_t>(p[i]) | (static_cast<uint32_t>(p[i + 1]) << 8) |
+                               (static_cast<uint32_t>(p[i + 2]) << 16) | (static_cast<uint32_t>(p[i + 3]) << 24));
+  if (i < e) {
+    uint32_t w = 0;
+    for (uint32_t k = 0; i + k < e; ++k) w |= static_cast<uint32_t>(p[i + k]) << (8u * k);
+    h = shard_word_step(h, w);
+  }
   return mix32(h ^ static_cast<uint32_t>(e - s));
 }
 
@@ -391,21 +403,13 @@ struct ShardTopicLevels {
 EMQX_HD void shard_topic_levels(const uint8_t* p, uint64_t n, ShardTopicLevels* L) {
   L->n_levels = 0;
   L->wild = false;
-  uint32_t h = 0x811C9DC5u, len = 0;
-  uint8_t c0 = 0;
+  uint64_t s = 0;
   for (uint64_t i = 0; i <= n; ++i) {
-    const uint8_t c = i < n ? p[i] : static_cast<uint8_t>('/');
-    if (c == '/') {
-      if (L->n_levels < 3) L->h[L->n_levels] = mix32(h ^ len);
-      if (len == 1 && (c0 == '+' || c0 == '#')) L->wild = true;
-      ++L->n_levels;
-      h = 0x811C9DC5u;
-      len = 0;
-    } else {
-      if (len == 0) c0 = c;
-      h = (h ^ c) * 0x01000193u;
-      ++len;
-    }
+    if (i < n && p[i] != '/') continue;
+    if (L->n_levels < 3) L->h[L->n_levels] = shard_level_hash(p, s, i);
+    if (i - s == 1 && (p[s] == '+' || p[s] == '#')) L->wild = true;
+    ++L->n_levels;
+    s = i + 1;
   }
 }
 

@@ -171,14 +171,45 @@ __device__ __forceinline__ uint32_t byte_zero4(uint32_t v) {
 
 // shard_topic_levels (layout.h) over the topic's bytes read as 16-B aligned windows (a window
 // holding a topic byte lies inside the batch's allocation; the batch's last window only up to
-// its end): the same summary, one load per 16 bytes instead of one per byte.
+// its end): the same summary, one load per 16 bytes instead of one per byte.  Each window is
+// scanned as byte masks: its levels are its '/' bits (the end counts as one), a wildcard level a
+// '+' / '#' bit with a '/' (or the topic's start) before it and a '/' (or the end) after it; the
+// first three levels' ends are kept, and those levels are hashed a 32-bit word at a time
+// (shard_level_hash) — a byte-wise scan of the first three levels made the kernel VALU-bound
+// (~3600 VALU instructions a wave, `profiles/r6/`).
+__device__ __forceinline__ uint32_t ld_u32_any(const uint8_t* p) {
+  typedef uint32_t __attribute__((aligned(1))) u1u;
+  return *reinterpret_cast<const u1u*>(p);
+}
+
+// shard_level_hash of tb[a, b) (b <= lim, the batch's end): whole words read unaligned, the tail
+// word masked (read as a word when 4 bytes from it are inside the batch, else byte by byte).
+__device__ __forceinline__ uint32_t level_hash_dev(const uint8_t* __restrict__ tb, uint64_t a, uint64_t b,
+                                                   uint64_t lim) {
+  uint32_t h = 0x811C9DC5u;
+  uint64_t i = a;
+  for (; i + 4 <= b; i += 4) h = shard_word_step(h, ld_u32_any(tb + i));
+  if (i < b) {
+    const uint32_t r = static_cast<uint32_t>(b - i);  // 1..3
+    uint32_t w;
+    if (i + 4 <= lim) {
+      w = ld_u32_any(tb + i) & ((1u << (8u * r)) - 1u);
+    } else {
+      w = 0;
+      for (uint32_t k = 0; k < r; ++k) w |= static_cast<uint32_t>(tb[i + k]) << (8u * k);
+    }
+    h = shard_word_step(h, w);
+  }
+  return mix32(h ^ static_cast<uint32_t>(b - a));
+}
+
 __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb, uint64_t s, uint64_t e,
                                                  uint64_t lim, ShardTopicLevels* L) {
-  // (level hashes and the windows in named registers: an indexed private array would live in
-  // scratch memory; four windows are loaded before any is scanned: one round trip per 64 bytes)
-  uint32_t nl = 0, h0 = 0, h1 = 0, h2 = 0;
+  // (the windows and the three level ends in named registers: an indexed private array would
+  // live in scratch memory; four windows are loaded before any is scanned)
+  uint32_t nl = 0;
+  uint64_t c0 = e, c1 = e, c2 = e;  // the ends of levels 0, 1, 2
   bool wild = false;
-  uint32_t h = 0x811C9DC5u, len = 0, c0 = 0;
   const uintptr_t abeg = reinterpret_cast<uintptr_t>(tb + s), aend = reinterpret_cast<uintptr_t>(tb + e);
   const uintptr_t alim = reinterpret_cast<uintptr_t>(tb + lim);
   auto window = [&](uintptr_t w0, uint64_t& lo, uint64_t& hi) {
@@ -195,38 +226,9 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
       }
     }
   };
-  // (the level hashes are finished with mix32 after the loop, not per '/'.)  Byte by byte while
-  // some lane of the wave hashes its first three levels; after that a window is 16 bytes of
-  // byte masks: the levels are its '/' bits (the end counts as one), a wildcard level a '+' / '#'
-  // bit with a '/' (or the topic's start) before it and a '/' (or the end) after it.  carry: the
-  // byte before the window ends a level (or is the start); pend: that byte is a '+' / '#' that
-  // began its level, so a '/' first in this window makes its level a wildcard.
+  // carry: the byte before the window ends a level (or is the start); pend: that byte is a '+' /
+  // '#' that began its level, so a '/' first in this window makes its level a wildcard.
   bool carry = true, pend = false;
-  auto scan16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
-#pragma unroll
-    for (uint32_t b = 0; b < 16; ++b) {
-      const uintptr_t q = w0 + b;
-      if (q < abeg || q > aend) continue;
-      const uint32_t c = q < aend ? static_cast<uint32_t>(((b < 8 ? lo : hi) >> (8u * (b & 7u))) & 0xFFu)
-                                  : static_cast<uint32_t>('/');
-      if (c == '/') {
-        const uint32_t v = h ^ len;
-        h0 = nl == 0 ? v : h0;
-        h1 = nl == 1 ? v : h1;
-        h2 = nl == 2 ? v : h2;
-        h = 0x811C9DC5u;
-        wild |= len == 1 && (c0 == '+' || c0 == '#');
-        ++nl;
-        len = 0;
-      } else {
-        c0 = len == 0 ? c : c0;
-        h = (h ^ c) * 0x01000193u;
-        ++len;
-      }
-    }
-    carry = len == 0;
-    pend = len == 1 && (c0 == '+' || c0 == '#');
-  };
   auto masks16 = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
     const uint32_t i0 = abeg > w0 ? static_cast<uint32_t>(abeg - w0) : 0u;  // < 16
     const uint64_t ie = aend - w0;  // the virtual '/' at the end, if < 16
@@ -239,17 +241,21 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
       sl |= byte_zero4(d[k] ^ 0x2F2F2F2Fu) << (4 * k);
       wc |= (byte_zero4(d[k] ^ 0x2B2B2B2Bu) | byte_zero4(d[k] ^ 0x23232323u)) << (4 * k);
     }
-    const uint32_t S = (sl & real) | (ie < 16 ? 1u << ie : 0u);
+    uint32_t S = (sl & real) | (ie < 16 ? 1u << ie : 0u);
     const uint32_t P = ((S << 1) | (carry ? 1u : 0u) | (i0 ? 1u << i0 : 0u)) & 0xFFFFu;
     const uint32_t cand = wc & real & P;
     wild |= (cand & (S >> 1)) != 0 || (pend && (S & 1u));
     pend = ((cand >> 15) & 1u) != 0;
     carry = ((S >> 15) & 1u) != 0;
-    nl += static_cast<uint32_t>(__popc(S));
-  };
-  auto scan16w = [&](uintptr_t w0, uint64_t lo, uint64_t hi) {
-    if (__ballot(nl < 3)) scan16(w0, lo, hi);
-    else masks16(w0, lo, hi);
+    // the first three level ends (at most three bits of this window matter)
+    for (uint32_t k = nl; k < 3 && S; ++k) {
+      const uint64_t pos = (w0 - reinterpret_cast<uintptr_t>(tb)) + static_cast<uint32_t>(__builtin_ctz(S));
+      c0 = k == 0 ? pos : c0;
+      c1 = k == 1 ? pos : c1;
+      c2 = k == 2 ? pos : c2;
+      S &= S - 1;
+    }
+    nl += static_cast<uint32_t>(__popc((sl & real) | (ie < 16 ? 1u << ie : 0u)));
   };
   for (uintptr_t w0 = abeg & ~static_cast<uintptr_t>(15); w0 <= aend; w0 += 64) {
     uint64_t l0, g0, l1, g1, l2, g2, l3, g3;
@@ -257,16 +263,16 @@ __device__ __forceinline__ void topic_levels_dev(const uint8_t* __restrict__ tb,
     window(w0 + 16, l1, g1);
     window(w0 + 32, l2, g2);
     window(w0 + 48, l3, g3);
-    scan16w(w0, l0, g0);
-    if (w0 + 16 <= aend) scan16w(w0 + 16, l1, g1);
-    if (w0 + 32 <= aend) scan16w(w0 + 32, l2, g2);
-    if (w0 + 48 <= aend) scan16w(w0 + 48, l3, g3);
+    masks16(w0, l0, g0);
+    if (w0 + 16 <= aend) masks16(w0 + 16, l1, g1);
+    if (w0 + 32 <= aend) masks16(w0 + 32, l2, g2);
+    if (w0 + 48 <= aend) masks16(w0 + 48, l3, g3);
   }
   L->n_levels = nl;
   L->wild = wild;
-  L->h[0] = nl > 0 ? mix32(h0) : 0u;
-  L->h[1] = nl > 1 ? mix32(h1) : 0u;
-  L->h[2] = nl > 2 ? mix32(h2) : 0u;
+  L->h[0] = nl > 0 ? level_hash_dev(tb, s, c0, lim) : 0u;
+  L->h[1] = nl > 1 ? level_hash_dev(tb, c0 + 1, c1, lim) : 0u;
+  L->h[2] = nl > 2 ? level_hash_dev(tb, c1 + 1, c2, lim) : 0u;
 }
 
 // The split plan in LDS when it fits (routing binary-searches it twice per topic: from global
