@@ -625,6 +625,8 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
   __shared__ uint64_t w_b[4][kMaxBuckets];
   __shared__ int64_t s_ob[kMaxBuckets], s_db[kMaxWorld];
   __shared__ uint64_t s_bp[kMaxBuckets];
+  __shared__ uint64_t cp_src[256], cp_dst[256];  // the row's topic copies, made by 4 lanes each
+  __shared__ uint32_t cp_len[256];
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const bool pack = err[0] == 0;
   const uint32_t world = (nb - 1) / kE;
@@ -694,9 +696,27 @@ __global__ __launch_bounds__(256) void shard_sort_scatter_kernel(const uint32_t*
       key_s[pos] = k;
       perm[pos] = static_cast<uint32_t>(p);
       if (one) tpos[p] = pos;  // (request p = topic p)
-      if (pack && k < nb - 1) pack_request(send, k, pos, pb + rb, s_ob, s_bp, s_db, tb + a, l);
+      if (pack && k < nb - 1) {  // pack_request's offset word here, its bytes below
+        const uint64_t x = pb + rb;
+        reinterpret_cast<uint32_t*>(send)[s_ob[k] + pos] = static_cast<uint32_t>(x - s_bp[k]);
+        cp_src[tid] = a;
+        cp_dst[tid] = static_cast<uint64_t>(s_db[k / kE] + static_cast<int64_t>(x));
+      }
     }
+    cp_len[tid] = ok && pack && k < nb - 1 ? l : 0u;
     __syncthreads();
+    // the row's topic bytes, 4 lanes a request (16-B moves side by side: a wave's loads cover 16
+    // topics' consecutive bytes instead of 64 lanes' strided 16-B pieces)
+    for (uint32_t r = tid >> 2; r < 256; r += 64) {
+      const uint32_t len = cp_len[r];
+      if (!len) continue;
+      const uint8_t* src = tb + cp_src[r];
+      uint8_t* dst = send + cp_dst[r];
+      for (uint32_t j = 16 * (tid & 3u); j < len; j += 64) {
+        if (j + 16 <= len) *reinterpret_cast<u4u*>(dst + j) = *reinterpret_cast<const u4u*>(src + j);
+        else copy_topic(src + j, dst + j, len - j);
+      }
+    }
     for (uint32_t kk = tid; kk < nb; kk += 256) {
       uint32_t c = 0;
       uint64_t b = 0;
