@@ -394,7 +394,7 @@ def test_async_device_api(Engine):
     e2 = engine_with(Engine, pats)
     hot = pack([b"/".join(words)] * 64)
     want = len(expected(pats, [b"/".join(words)], 0)[0])
-    htb = torch.from_numpy(hot[0]).to(dev)
+    htb = torch.from_numpy(np.array(hot[0])).to(dev)
     hto = torch.from_numpy(hot[1].view(np.int64)).to(dev)
     d_off = torch.empty(65, dtype=torch.int64, device=dev)
     d_ids = torch.empty(64 * want + 16, dtype=torch.int32, device=dev)
