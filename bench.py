@@ -428,7 +428,7 @@ def sharded_bench(args, rank, world, dev):
     import torch
     import torch.distributed as dist
     from emqx_amd import workloads as W
-    from emqx_amd.dist import ShardedMatcher
+    from emqx_amd.dist import ShardedMatcher, stream_depth
     from emqx_amd.dist import plan_p_replicated as D_p_repl
     seed = 3 if args.vocab_scale > 1 else 2
     t0 = time.time()
@@ -449,11 +449,11 @@ def sharded_bench(args, rank, world, dev):
     res = None
     for _ in range(max(args.warmup, 1)):
         res = sm.match_all(topics)
-    sm.match_stream([topics] * 2)  # (the second lane's buffers and workspaces)
+    sm.match_stream([topics] * max(2, stream_depth()))  # (every lane's buffers and workspaces)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    # the timed steps: two in flight (ShardedMatcher.match_stream), every step's CSR kept
+    # the timed steps: stream_depth() in flight (ShardedMatcher.match_stream), every step's CSR kept
     t_start = time.perf_counter()
     res = sm.match_stream([topics] * args.steps)[-1] if args.steps else res
     torch.cuda.synchronize()
@@ -537,7 +537,8 @@ def sharded_bench(args, rank, world, dev):
                        "mismatching_topics_per_rank": [int(x) for x in bad_rank.cpu().tolist()]},
             "step": "device kernels (emqx_shard_step_*: route + fold onto the engine slots A / B / AB + sort + "
                     "pack, unpack, answer, merge), engines async with learnt capacities, two host syncs "
-                    "(split sizes), two steps in flight (match_stream)",
+                    f"(split sizes), {stream_depth()} steps in flight (match_stream)",
+            "steps_in_flight": stream_depth(),
             **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
                if rehearse else {}),
         }), flush=True)

@@ -250,6 +250,16 @@ MAX_PIECE_PM = 250  # a key is split when its filters exceed a quarter of a rank
 P_SPACE = {"auto": 0, "sharded": 1, "replicated": 2}  # emqx_shard_plan p_space (include/emqx_match.h)
 
 
+# (measurement probe, not a protocol: at world 1 skip the size syncs once a lane's pinned words
+# hold a step's sizes — valid only while every step repeats the same batch, as bench.py's does)
+_NOSYNC_PROBE = os.environ.get("EMQX_SHARD_NOSYNC_PROBE") == "1"
+
+
+def stream_depth() -> int:
+    """Steps in flight in ``ShardedMatcher.match_stream`` (env ``EMQX_SHARD_DEPTH``)."""
+    return int(os.environ.get("EMQX_SHARD_DEPTH", "3"))
+
+
 def shard_plan(filters: Tuple[np.ndarray, np.ndarray], world: int, max_piece_pm: int = MAX_PIECE_PM,
                p_space: str = "auto") -> np.ndarray:
     """The hot keys of a filter set (emqx_shard_plan): (k, 2) uint32 rows (key, first rank | span
@@ -668,18 +678,23 @@ class ShardedMatcher:
         except StopIteration as stop:
             return stop.value
 
-    def match_stream(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], exchange: Optional[Callable] = None):
-        """match_all over a sequence of this rank's batches with two steps in flight (device
-        step only): step k + 1's send runs while step k's engines walk, and step k + 1's
-        requests are exchanged, unpacked and handed to its engines before the host waits for
-        step k's answers, so the device always has a walk queued while the host synchronises.
-        Every rank runs the same schedule, so the collectives pair up.  ``exchange``: the
-        exchange-point function (default ``_exchange``: the process group; ``EmulatedWorld``
-        passes a recorded one).  Returns every batch's (offsets, ids)."""
+    def match_stream(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], exchange: Optional[Callable] = None,
+                     depth: Optional[int] = None):
+        """match_all over a sequence of this rank's batches with ``depth`` steps in flight (device
+        step only; default ``stream_depth()``), one lane each: step k + depth - 1's send runs
+        while the earlier steps' engines walk, and its requests are exchanged, unpacked and handed
+        to its engines before the host waits for step k's answers, so the device always has a walk
+        queued while the host synchronises.  With two lanes, step k + 2's send queues on its lane
+        behind step k's merge, which waits for step k + 1's walk to free the CUs; a third lane
+        gives that merge and send a whole walk to run under.  Every rank runs the same schedule,
+        so the collectives pair up.  ``exchange``: the exchange-point function (default
+        ``_exchange``: the process group; ``EmulatedWorld`` passes a recorded one).  Returns every
+        batch's (offsets, ids)."""
         assert self._cuda, "match_stream keeps steps in flight on device streams"
+        D = max(1, int(depth or stream_depth()))
         ex = exchange or self._exchange
         caller = torch.cuda.current_stream(self.device)
-        lanes = [self._lane_n(0), self._lane_n(1)]
+        lanes = [self._lane_n(i) for i in range(D)]
         for ln in lanes:
             if ln.stream is None:
                 ln.stream = torch.cuda.Stream(device=self.device)
@@ -688,7 +703,7 @@ class ShardedMatcher:
         gens, ops, res = {}, {}, [None] * K
 
         def on_lane(k, fn):
-            self._lane = lanes[k % 2]
+            self._lane = lanes[k % D]
             with torch.cuda.stream(self._lane.stream):
                 return fn()
 
@@ -722,17 +737,17 @@ class ShardedMatcher:
             del gens[k]
 
         try:
-            if K:
-                start(0)
-                to_answer(0)
-            if K > 1:
-                start(1)
+            for k in range(min(K, D - 1)):  # the first D - 1 steps up to their answers
+                start(k)
+                to_answer(k)
+            if K >= D:
+                start(D - 1)
             for k in range(K):
-                if k + 1 < K:
-                    to_answer(k + 1)
+                if k + D - 1 < K and D > 1:
+                    to_answer(k + D - 1)
                 finish(k)
-                if k + 2 < K:
-                    start(k + 2)
+                if k + D < K:
+                    start(k + D)
         finally:
             self._lane = self._lanes[0]
         for ln in lanes:
@@ -751,7 +766,7 @@ class ShardedMatcher:
         of every source's chunk for this rank (``_exchange_chunks``)."""
         if op[0] == "local_sizes":  # world 1: words the device wrote into mapped pinned memory
             _, words, W = op
-            if self._cuda:
+            if self._cuda and not (_NOSYNC_PROBE and int(words[0])):
                 torch.cuda.current_stream(self.device).synchronize()
             lst = words[: W * self.world].tolist()
             return lst, lst, words
@@ -997,7 +1012,7 @@ class EmulatedWorld:
             addrs[r] = op[1].data_ptr() + op[1].element_size() * int(own[r])
             return addrs
 
-        m.match_stream([batch] * 2, exchange=replay)  # (the second lane's buffers and workspaces)
+        m.match_stream([batch] * max(2, stream_depth()), exchange=replay)  # (every lane's buffers and workspaces)
         torch.cuda.synchronize(self.device)
         t0 = time.perf_counter()
         res = m.match_stream([batch] * steps, exchange=replay)
