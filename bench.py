@@ -428,7 +428,7 @@ def sharded_bench(args, rank, world, dev):
     import torch
     import torch.distributed as dist
     from emqx_amd import workloads as W
-    from emqx_amd.dist import ShardedMatcher, stream_depth
+    from emqx_amd.dist import ShardedMatcher, fixed_steps, stream_depth
     from emqx_amd.dist import plan_p_replicated as D_p_repl
     seed = 3 if args.vocab_scale > 1 else 2
     t0 = time.time()
@@ -536,9 +536,14 @@ def sharded_bench(args, rank, world, dev):
                        "topics_checked_per_rank": [int(x) for x in checked.cpu().tolist()],
                        "mismatching_topics_per_rank": [int(x) for x in bad_rank.cpu().tolist()]},
             "step": "device kernels (emqx_shard_step_*: route + fold onto the engine slots A / B / AB + sort + "
-                    "pack, unpack, answer, merge), engines async with learnt capacities, two host syncs "
-                    f"(split sizes), {stream_depth()} steps in flight (match_stream)",
+                    "pack, unpack, answer, merge), engines async with learnt capacities, "
+                    + ("fixed-capacity chunks agreed beforehand: no size exchange, no host read between steps, "
+                       "one flag word a step (a flagged step redone classically)" if fixed_steps() else
+                       "two host syncs a step (split sizes)")
+                    + f", {stream_depth()} steps in flight (match_stream)",
             "steps_in_flight": stream_depth(),
+            "fixed_capacity_steps": fixed_steps(),
+            "fixed_steps_redone": int(getattr(sm, "last_fixed_redo", 0)),
             **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
                if rehearse else {}),
         }), flush=True)

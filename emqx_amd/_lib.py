@@ -54,6 +54,8 @@ EXPORTS = (
     "emqx_shard_plan", "emqx_shard_place", "emqx_shard_route", "emqx_shard_route_device", "emqx_permute_scratch_bytes", "emqx_batch_permute_device", "emqx_owner_sort_scratch_bytes",
     "emqx_owner_sort_device", "emqx_shard_step_create", "emqx_shard_step_destroy", "emqx_shard_send_cap",
     "emqx_shard_step_send", "emqx_shard_step_recv", "emqx_shard_step_answer", "emqx_shard_step_merge",
+    "emqx_shard_step_send_fixed", "emqx_shard_step_recv_fixed", "emqx_shard_step_answer_fixed",
+    "emqx_shard_step_merge_fixed",
     "emqx_csr_unpermute_device", "emqx_htrie_create", "emqx_htrie_destroy", "emqx_htrie_insert", "emqx_htrie_delete",
     "emqx_htrie_commit", "emqx_htrie_match", "emqx_htrie_check", "emqx_htrie_walk_sim",
 )
@@ -260,6 +262,10 @@ def lib():
         "emqx_shard_step_recv": (i32, [vp, vp, vp, vp, vp, vp]),
         "emqx_shard_step_answer": (i32, [vp, vp, vp, vp, u32, vp, vp, vp]),
         "emqx_shard_step_merge": (i32, [vp, vp, vp, vp, vp, vp]),
+        "emqx_shard_step_send_fixed": (i32, [vp, vp, vp, u64, vp, u64, vp, vp]),
+        "emqx_shard_step_recv_fixed": (i32, [vp, vp, vp, vp, vp, vp, vp]),
+        "emqx_shard_step_answer_fixed": (i32, [vp, vp, vp, vp, u32, vp, u64, vp]),
+        "emqx_shard_step_merge_fixed": (i32, [vp, vp, vp, vp, vp, vp]),
         "emqx_batch_permute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),
         "emqx_csr_unpermute_device": (i32, [vp, vp, u64, vp, vp, vp, vp, vp]),
         "emqx_host_batch_create": (i32, [vp, u64, u64, u64, ctypes.POINTER(ctypes.POINTER(HostBatchStruct))]),

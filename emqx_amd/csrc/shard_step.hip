@@ -31,7 +31,11 @@
 // table, as replication does; at world G a topic's two requests meet with probability ~1/G.
 //
 // Per-source / per-destination tables (chunk starts, batch bases) come from the host, which
-// holds the exchanged sizes anyway, as one kernel argument (world <= 64).  Requests are u32
+// holds the exchanged sizes anyway, as one kernel argument (world <= 64).  The fixed-capacity
+// form (emqx_shard_step_*_fixed) has no size exchange: chunks sit at agreed capacities, the
+// tables are built on the device from the chunks' headers, the engines run fixed-size batches
+// (padding topics past the requests) and a flag word, carried in every chunk's header, marks a
+// step that did not fit (the caller redoes it with the calls above).  Requests are u32
 // indices (2 per topic), so a batch holds fewer than 2^31 topics.
 #include <hip/hip_runtime.h>
 
@@ -150,6 +154,13 @@ __host__ __device__ inline void layout_dest(uint32_t r, uint64_t size, uint64_t 
   h[3] = 0;
   h[7] = 0;
   dbase[r] = static_cast<int64_t>(base + 4 * kHW + al16(4ull * (nall + kE))) - static_cast<int64_t>(bpre[kE * r]);
+}
+
+// The fixed-capacity form's chunk of a step that does not fit: no requests, flag bit 1 in header
+// word 3 (every receiver's step then carries the flag), slot offsets 0.
+__host__ __device__ inline void flagged_chunk(uint8_t* __restrict__ chunk) {
+  uint32_t* h = reinterpret_cast<uint32_t*>(chunk);
+  for (uint32_t w = 0; w < kHW + kE; ++w) h[w] = w == 3 ? 1u : 0u;
 }
 
 // Sorted request `pos` (bucket k < the no-request bucket, byte x among the sorted requests') packed
@@ -740,7 +751,8 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
                                                           uint8_t* __restrict__ send, uint64_t cap,
                                                           int64_t* __restrict__ meta, uint64_t* __restrict__ cbase,
                                                           int64_t* __restrict__ obase, int64_t* __restrict__ dbase,
-                                                          uint32_t* __restrict__ err) {
+                                                          uint32_t* __restrict__ err, uint64_t fixed,
+                                                          uint32_t* __restrict__ flagw) {
   __shared__ uint64_t sz[kMaxWorld];
   __shared__ uint32_t wide_any;
   const uint32_t r = threadIdx.x;
@@ -749,18 +761,22 @@ __global__ __launch_bounds__(64) void shard_layout_kernel(const uint32_t* __rest
   bool wide = false;
   if (r < world) {
     sz[r] = dest_size(r, start, bpre, &wide);
-    if (wide) atomicOr(&wide_any, 1u);
+    if (wide || (fixed && sz[r] > fixed)) atomicOr(&wide_any, 1u);
   }
   __syncthreads();
   if (r >= world) return;
-  uint64_t base = 0;
+  uint64_t base = 0, total = 0;
   for (uint32_t j = 0; j < r; ++j) base += sz[j];
-  uint64_t total = 0;
   for (uint32_t j = 0; j < world; ++j) total += sz[j];
+  if (fixed) base = fixed * r;  // (fixed capacities: chunk r at r * fixed; over = one does not fit)
   cbase[r] = base;
-  const bool over = total > cap || wide_any;
+  const bool over = (!fixed && total > cap) || wide_any;
   layout_dest(r, sz[r], base, over, start, bpre, send, meta, obase, dbase);
-  if (r == 0) err[0] = over ? 1u : 0u;
+  if (fixed && over) flagged_chunk(send + base);
+  if (r == 0) {
+    err[0] = over ? 1u : 0u;
+    if (flagw) flagw[0] = over ? 1u : 0u;  // (the step's flag word starts here)
+  }
 }
 // emqx_shard_route_device: the raw requests (req2[2t], req2[2t + 1]) with the same scanner.
 __global__ __launch_bounds__(256) void shard_route_kernel(const uint8_t* __restrict__ tb,
@@ -801,6 +817,7 @@ struct SlotOffsets {
 };
 struct SlotBytes {
   uint8_t* p[kE];
+  uint32_t rel;  // (fixed form, world 1: every slot matched in place, offsets from the chunk's start)
 };
 
 // (source s, slot e) of the recv: items tid, tid + stride, ... (the kernel's grid-stride; the host
@@ -816,7 +833,7 @@ __host__ __device__ inline void unpack_part(const ShardTab& tab, const SlotOffse
   }
   const uint32_t* offs = reinterpret_cast<const uint32_t*>(tab.chunk[s]) + offs_words(nq, e);
   const uint32_t n = nq[e];
-  const uint64_t dbase = tab.y0[e][s];
+  const uint64_t dbase = dst_bytes.rel ? 4 * kHW + al16(4ull * (nall + kE)) + before : tab.y0[e][s];
   uint64_t* doff = dst_off.p[e] + tab.q0[e][s];
   for (uint64_t k = tid; k <= n; k += stride) doff[k] = dbase + offs[k];
   if (!dst_bytes.p[e]) return;
@@ -834,6 +851,80 @@ __global__ __launch_bounds__(256) void shard_unpack_kernel(ShardTab tab, SlotOff
               static_cast<uint64_t>(gridDim.x) * blockDim.x);
 }
 
+// ---- the fixed-capacity form's tables ---------------------------------------------------------
+
+// Per-slot capacities of the fixed form (requests, bytes) and the padding offset of each slot.
+struct SlotCaps {
+  uint64_t q[kE], y[kE];
+};
+
+// The recv table from the received chunks' headers (the host mode's and one device thread's
+// body): per source its slot counts and bytes, prefixes over sources; a flagged chunk, or a slot
+// over its capacity, flags the step and empties every slot batch.  pad[e]: slot e's offset after
+// its last request (the engines' padding topics are empty topics there).
+__host__ __device__ inline void recv_table(const uint64_t* chunk, uint32_t G, const SlotCaps& cap, bool rel, ShardTab* t,
+                                           uint64_t* pad, uint32_t* flagw) {
+  uint32_t f = flagw[0];
+  for (uint32_t r = 0; r < G; ++r) f |= reinterpret_cast<const uint32_t*>(chunk[r])[3];
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool empty = f != 0;
+    uint64_t words = 0;
+    for (uint32_t e = 0; e < kE; ++e) {
+      t->q0[e][0] = 0;
+      t->y0[e][0] = 0;
+    }
+    for (uint32_t r = 0; r < G; ++r) {
+      const uint32_t* h = reinterpret_cast<const uint32_t*>(chunk[r]);
+      t->chunk[r] = chunk[r];
+      uint64_t nall = 0;
+      for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t nq = empty ? 0u : h[e];
+        t->q0[e][r + 1] = t->q0[e][r] + nq;
+        t->y0[e][r + 1] = t->y0[e][r] + (empty ? 0u : h[4 + e]);
+        nall += nq;
+      }
+      t->w0[r] = words;
+      words += kHW + nall;
+    }
+    t->w0[G] = words;
+    for (uint32_t e = 0; e < kE; ++e)
+      if (t->q0[e][G] > cap.q[e] || (!rel && t->y0[e][G] > cap.y[e])) f |= 2u;
+    if (!f || empty) break;  // (over a capacity: again, every batch empty)
+  }
+  uint64_t nall0 = 0, y = 0;
+  for (uint32_t e = 0; e < kE; ++e) nall0 += t->q0[e][1];
+  for (uint32_t e = 0; e < kE; ++e) {
+    y += t->y0[e][G];
+    pad[e] = rel ? 4 * kHW + al16(4ull * (nall0 + kE)) + y : t->y0[e][G];
+  }
+  flagw[0] = f;
+}
+
+__global__ __launch_bounds__(64) void shard_recv_table_kernel(ShardTab chunks, uint32_t G, SlotCaps cap, uint32_t rel,
+                                                              ShardTab* __restrict__ t, uint64_t* __restrict__ pad,
+                                                              uint32_t* __restrict__ flagw) {
+  if (threadIdx.x == 0) recv_table(chunks.chunk, G, cap, rel != 0, t, pad, flagw);
+}
+
+__global__ __launch_bounds__(256) void shard_unpack_fixed_kernel(const ShardTab* __restrict__ tab, SlotOffsets dst_off,
+                                                                 SlotBytes dst_bytes, const uint32_t* __restrict__ flagw) {
+  if (flagw[0]) return;
+  unpack_part(*tab, dst_off, dst_bytes, blockIdx.y, blockIdx.z, static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+              static_cast<uint64_t>(gridDim.x) * blockDim.x);
+}
+
+// grid (x, slot): slot e's offsets from its request count to its capacity = pad[e].
+__host__ __device__ inline void pad_slot(const ShardTab& tab, uint32_t G, const SlotOffsets& dst_off, const SlotCaps& cap,
+                                         const uint64_t* pad, uint32_t e, uint64_t tid, uint64_t stride) {
+  for (uint64_t k = tab.q0[e][G] + tid; k <= cap.q[e]; k += stride) dst_off.p[e][k] = pad[e];
+}
+
+__global__ __launch_bounds__(256) void shard_pad_kernel(const ShardTab* __restrict__ tab, uint32_t G, SlotOffsets dst_off,
+                                                        SlotCaps cap, const uint64_t* __restrict__ pad) {
+  pad_slot(*tab, G, dst_off, cap, pad, blockIdx.y, static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+           static_cast<uint64_t>(gridDim.x) * blockDim.x);
+}
+
 // ---- answer -----------------------------------------------------------------------------
 
 struct EngineCsrs {
@@ -847,9 +938,16 @@ struct EngineCsrs {
 // itself (source `self`) carries no ids: the merge reads them in place from the CSRs.
 constexpr uint32_t kAnsMeta = 3;  // per source: chunk words, redo flag, ids
 // Source s of G: items tid, tid + stride, ... (meta: this item writes the source's meta words).
+// fixed > 0 (the fixed form): chunk s at s * fixed words, no meta; `flag` set: the chunk is a
+// header only, flag in word 7.
 __host__ __device__ inline void answer_source(const EngineCsrs& cs, const ShardTab& tab, uint32_t self,
                                               uint32_t* __restrict__ out, int64_t* __restrict__ ans_meta, uint32_t s,
-                                              uint32_t G, uint64_t tid, uint64_t stride, bool meta) {
+                                              uint32_t G, uint64_t tid, uint64_t stride, bool meta, uint64_t fixed = 0,
+                                              uint32_t flag = 0) {
+  if (fixed && flag) {
+    for (uint64_t w = tid; w < kHW; w += stride) out[fixed * s + w] = w == 7 ? flag : 0u;
+    return;
+  }
   bool bad = false;
   uint32_t q0[kE], nq[kE];
   uint64_t i0[kE], ni[kE], nall = 0, iall = 0, ibefore = 0;
@@ -870,8 +968,8 @@ __host__ __device__ inline void answer_source(const EngineCsrs& cs, const ShardT
       const uint32_t a0 = tab.q0[e][self], a1 = tab.q0[e][self + 1];
       if (a1 > a0) ibefore -= cs.off[e][a1] - cs.off[e][a0];
     }
-  const uint64_t cb = tab.w0[s] + ibefore;
-  if (meta) {
+  const uint64_t cb = fixed ? fixed * s : tab.w0[s] + ibefore;
+  if (meta && !fixed) {
     ans_meta[kAnsMeta * s] = static_cast<int64_t>(kHW + nall + (s == self ? 0 : iall));
     ans_meta[kAnsMeta * s + 1] = bad ? 1 : 0;
     ans_meta[kAnsMeta * s + 2] = static_cast<int64_t>(iall);
@@ -913,6 +1011,41 @@ __global__ __launch_bounds__(256) void shard_answer_kernel(EngineCsrs cs, ShardT
                 blockIdx.x == 0 && threadIdx.x == 0);
 }
 
+// The fixed form's answer plan (one thread): an engine call that did not complete, or an answer
+// chunk over `fixed` words, flags the step — decided for every chunk before any is written, so
+// each destination gets the same flag.
+__host__ __device__ inline void answer_plan(const EngineCsrs& cs, const ShardTab& tab, uint32_t self, uint32_t G,
+                                            uint64_t fixed, uint32_t* flagw) {
+  uint32_t f = flagw[0];
+  for (uint32_t e = 0; e < kE; ++e)
+    if (cs.sum[e] && cs.sum[e][0]) f |= 4u;
+  if (!f)
+    for (uint32_t s = 0; s < G; ++s) {
+      uint64_t nall = 0, iall = 0;
+      for (uint32_t e = 0; e < kE; ++e) {
+        const uint32_t q0 = tab.q0[e][s], nq = tab.q0[e][s + 1] - q0;
+        nall += nq;
+        if (nq) iall += cs.off[e][q0 + nq] - cs.off[e][q0];
+      }
+      if (kHW + nall + (s == self ? 0 : iall) > fixed) f |= 8u;
+    }
+  flagw[0] = f;
+}
+
+__global__ __launch_bounds__(64) void shard_answer_plan_kernel(EngineCsrs cs, const ShardTab* __restrict__ tab,
+                                                               uint32_t self, uint32_t G, uint64_t fixed,
+                                                               uint32_t* __restrict__ flagw) {
+  if (threadIdx.x == 0) answer_plan(cs, *tab, self, G, fixed, flagw);
+}
+
+__global__ __launch_bounds__(256) void shard_answer_fixed_kernel(EngineCsrs cs, const ShardTab* __restrict__ tab,
+                                                                 uint32_t self, uint32_t* __restrict__ out,
+                                                                 uint64_t fixed, const uint32_t* __restrict__ flagw) {
+  answer_source(cs, *tab, self, out, nullptr, blockIdx.y, gridDim.y,
+                static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x, static_cast<uint64_t>(gridDim.x) * blockDim.x,
+                false, fixed, flagw[0]);
+}
+
 // ---- merge ------------------------------------------------------------------------------
 
 // This rank's own answers, read in place: per slot its engine's ids from the first id of this
@@ -922,6 +1055,8 @@ struct SelfIds {
   const uint64_t* off[kE];
   uint32_t q0[kE];
   uint32_t self;
+  const ShardTab* rtab;     // (fixed form: q0 from the recv table on the device)
+  const uint32_t* flagw;    // (fixed form: the step's flag; set = no answer is read)
 };
 
 // Per sorted request p: where its answer's ids are (an answer chunk's id region, or this rank's
@@ -941,7 +1076,8 @@ __host__ __device__ inline uint32_t request_answer(const ShardTab& tab, const Se
   }
   const uint32_t k = before + (p - start[b]);
   const uint32_t b0 = k ? ch[kHW + k - 1] : 0u;
-  const uint32_t* src = r == me.self ? me.ids[e] + me.off[e][me.q0[e]] + (b0 - ibefore)
+  const uint32_t q0 = me.rtab ? me.rtab->q0[e][me.self] : me.q0[e];
+  const uint32_t* src = r == me.self ? me.ids[e] + me.off[e][q0] + (b0 - ibefore)
                                      : ch + kHW + ch[0] + ch[1] + ch[2] + b0;
   *src_out = reinterpret_cast<uint64_t>(src);
   return ch[kHW + k] - b0;
@@ -956,7 +1092,8 @@ __host__ __device__ inline void gather_topic(const ShardTab& tab, const SelfIds&
                                              uint64_t* __restrict__ rq_src, uint32_t* __restrict__ tcnt) {
   const uint32_t p = tpos[t];
   uint64_t src = 0;
-  const uint32_t c = p < nreq ? request_answer(tab, me, key_s, start, p, &src) : 0u;
+  const bool none = p >= nreq || (me.flagw && me.flagw[0]);
+  const uint32_t c = none ? 0u : request_answer(tab, me, key_s, start, p, &src);
   *reinterpret_cast<uint2*>(rq_cnt + 2 * t) = make_uint2(c, 0u);
   rq_src[2 * t] = src;
   tcnt[t] = c;
@@ -969,7 +1106,7 @@ __host__ __device__ inline void gather_request(const ShardTab& tab, const SelfId
   {
     const uint32_t q = one ? 2 * perm[p] : perm[p];
     if (one) rq_cnt[q + 1] = 0;
-    if (p >= nreq) {
+    if (p >= nreq || (me.flagw && me.flagw[0])) {
       rq_cnt[q] = 0;
       return;
     }
@@ -1010,6 +1147,20 @@ __global__ __launch_bounds__(256) void shard_topic_counts_kernel(const uint32_t*
     const uint2 c = *reinterpret_cast<const uint2*>(rq_cnt + 2 * t);
     tcnt[t] = c.x + c.y;
   }
+}
+
+// The fixed form's merge plan (one thread): the step's flag ORed with every answer chunk's (word
+// 7), the same on every rank; copied to `out` (the caller's mapped word) as well.
+__host__ __device__ inline void merge_plan(const uint64_t* chunk, uint32_t G, uint32_t* flagw, uint32_t* out) {
+  uint32_t f = flagw[0];
+  for (uint32_t r = 0; r < G; ++r) f |= reinterpret_cast<const uint32_t*>(chunk[r])[7];
+  flagw[0] = f;
+  if (out) out[0] = f;
+}
+
+__global__ __launch_bounds__(64) void shard_merge_plan_kernel(ShardTab t, uint32_t G, uint32_t* __restrict__ flagw,
+                                                              uint32_t* __restrict__ out) {
+  if (threadIdx.x == 0) merge_plan(t.chunk, G, flagw, out);
 }
 
 // c ids from src to dst by the 4 lanes `sub` of a quad: 16-B moves (4 ids a lane, any 4-B
@@ -1079,6 +1230,11 @@ struct emqx_shard_step {
   int64_t* obase = nullptr;   // [kE G + 2]: offset-word base per bucket (pack)
   int64_t* dbase = nullptr;   // [G]: byte base per destination (pack)
   uint32_t* err = nullptr;
+  // the fixed form: the recv table built on the device, the slots' padding offsets, the flag word
+  ShardTab* d_tab = nullptr;
+  uint64_t* d_pad = nullptr;
+  uint32_t* d_flagw = nullptr;
+  uint64_t fixed_q = 0;  // the last recv_fixed's request capacity (all slots)
   // the step in flight
   uint64_t n = 0, m = 0;                // topics and requests of the last send
   uint32_t one = 0;                     // one request a topic (world 1 or space P replicated):
@@ -1096,6 +1252,9 @@ struct emqx_shard_step {
   std::vector<uint32_t> h_key, h_key_s, h_perm, h_pos, h_tcnt, h_start, h_tpos;
   std::vector<uint64_t> h_rq_src, h_bpre, h_cbase;
   std::vector<int64_t> h_obase, h_dbase;
+  ShardTab h_tab{};
+  uint64_t h_pad[kE] = {};
+  uint32_t h_flagw[4] = {};
 };
 
 namespace {
@@ -1151,7 +1310,7 @@ int hip_rc(hipError_t e) { return e == hipSuccess ? EMQX_OK : (e == hipErrorOutO
 // The send on the host: routing and fold per topic, a stable counting sort by bucket (what the
 // tiles' counting sort computes), then the same layout and packing as the kernels.
 int host_send(emqx_shard_step* st, const uint8_t* tb, const uint64_t* to, uint64_t n, uint8_t* send, uint64_t cap,
-              int64_t* meta) {
+              int64_t* meta, uint64_t fixed) {
   const uint32_t G = st->world, nb = kE * G + 1;
   const uint64_t m = st->one ? n : 2 * n;
   st->h_key.assign(m, 0);
@@ -1192,12 +1351,16 @@ int host_send(emqx_shard_step* st, const uint8_t* tb, const uint64_t* to, uint64
   uint64_t total = 0;
   for (uint32_t r = 0; r < G; ++r) {
     sz[r] = dest_size(r, st->start, st->bpre, &wide);
-    st->cbase[r] = total;
+    st->cbase[r] = fixed ? fixed * r : total;
     total += sz[r];
+    wide |= fixed && sz[r] > fixed;
   }
-  const bool over = total > cap || wide;
-  for (uint32_t r = 0; r < G; ++r) layout_dest(r, sz[r], st->cbase[r], over, st->start, st->bpre, send, meta, st->obase,
-                                               st->dbase);
+  const bool over = (!fixed && total > cap) || wide;
+  for (uint32_t r = 0; r < G; ++r) {
+    layout_dest(r, sz[r], st->cbase[r], over, st->start, st->bpre, send, meta, st->obase, st->dbase);
+    if (fixed && over) flagged_chunk(send + st->cbase[r]);
+  }
+  st->h_flagw[0] = over ? 1u : 0u;
   std::vector<uint64_t> nextp(st->start, st->start + nb), nextx(st->bpre, st->bpre + nb);
   for (uint64_t p = 0; p < m; ++p) {  // in request order: stable
     const uint32_t k = st->h_key[p];
@@ -1284,6 +1447,9 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
     st->obase = st->h_obase.data();
     st->dbase = st->h_dbase.data();
     st->cbase = st->h_cbase.data();
+    st->d_tab = &st->h_tab;
+    st->d_pad = st->h_pad;
+    st->d_flagw = st->h_flagw;
     *out = st;
     return EMQX_OK;
   }
@@ -1298,6 +1464,10 @@ int emqx_shard_step_create(int device, uint32_t world, const emqx_shard_split* s
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->obase), 8ull * (kE * world + 2));
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->dbase), 8ull * world);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->err), 16);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->d_tab), sizeof(ShardTab));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->d_pad), 8 * kE);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&st->d_flagw), 16);
+  if (e == hipSuccess) e = hipMemset(st->d_flagw, 0, 16);
   if (e != hipSuccess) {
     emqx_shard_step_destroy(st);
     return hip_rc(e);
@@ -1317,18 +1487,25 @@ int emqx_shard_step_destroy(emqx_shard_step* st) {
   free_scratch(st);
   for (void* p : {static_cast<void*>(st->d_splits), static_cast<void*>(st->start), static_cast<void*>(st->cbase),
                   static_cast<void*>(st->bpre), static_cast<void*>(st->obase), static_cast<void*>(st->dbase),
-                  static_cast<void*>(st->err)})
+                  static_cast<void*>(st->err), static_cast<void*>(st->d_tab), static_cast<void*>(st->d_pad),
+                  static_cast<void*>(st->d_flagw)})
     if (p) (void)hipFree(p);
   delete st;
   return EMQX_OK;
 }
 
-int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
-                         uint8_t* d_send, uint64_t send_cap, int64_t* d_meta, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int merge_launch(emqx_shard_step* st, const ShardTab& t, uint64_t* d_out_offsets, uint32_t* d_out_ids, hipStream_t s);
+
+int send_impl(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n, uint8_t* d_send,
+              uint64_t send_cap, int64_t* d_meta, uint64_t fixed, void* stream) {
   if (!st || !d_send || !d_meta || (n && (!d_bytes || !d_offsets)) || n >= (1ull << 31)) return EMQX_EINVAL;
   if (st->host) {
     try {
-      const int rc = host_send(st, d_bytes, d_offsets, n, d_send, send_cap, d_meta);
+      const int rc = host_send(st, d_bytes, d_offsets, n, d_send, send_cap, d_meta, fixed);
       if (rc != EMQX_OK) return rc;
     } catch (const std::bad_alloc&) {
       return EMQX_ENOMEM;
@@ -1362,7 +1539,7 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
                          st->pbytes_tab, N, ntiles, nb, m, st->segsum, st->start, st->bpre);
     }
     hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->bpre, G, d_send, send_cap, d_meta,
-                       st->cbase, st->obase, st->dbase, st->err);
+                       st->cbase, st->obase, st->dbase, st->err, fixed, fixed ? st->d_flagw : nullptr);
     hipLaunchKernelGGL(shard_sort_scatter_kernel, dim3(ntiles), dim3(256), 0, s, st->key, d_bytes, d_offsets, m, nb,
                        ntiles, st->tcnt_tab, st->pbytes_tab, st->bpre, st->obase, st->dbase, st->err, d_send,
                        st->key_s, st->perm, st->one, st->tpos);
@@ -1370,7 +1547,7 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
     SS_TRY(hipMemsetAsync(st->start, 0, 4ull * (kE * G + 2), s));
     SS_TRY(hipMemsetAsync(st->bpre, 0, 8ull * (kE * G + 2), s));
     hipLaunchKernelGGL(shard_layout_kernel, dim3(1), dim3(64), 0, s, st->start, st->bpre, G, d_send, send_cap, d_meta,
-                       st->cbase, st->obase, st->dbase, st->err);
+                       st->cbase, st->obase, st->dbase, st->err, fixed, fixed ? st->d_flagw : nullptr);
   }
   SS_TRY(hipGetLastError());
   st->n = n;
@@ -1378,6 +1555,21 @@ int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint
   st->have_send = true;
   st->have_recv = false;
   return EMQX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int emqx_shard_step_send(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                         uint8_t* d_send, uint64_t send_cap, int64_t* d_meta, void* stream) {
+  return send_impl(st, d_bytes, d_offsets, n, d_send, send_cap, d_meta, 0, stream);
+}
+
+int emqx_shard_step_send_fixed(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                               uint8_t* d_send, uint64_t chunk_bytes, int64_t* d_meta, void* stream) {
+  if (!st || chunk_bytes < 4 * (kHW + kE) || chunk_bytes % 16) return EMQX_EINVAL;
+  return send_impl(st, d_bytes, d_offsets, n, d_send, chunk_bytes * st->world, d_meta, chunk_bytes, stream);
 }
 
 int emqx_shard_step_recv(emqx_shard_step* st, const uint8_t* const* d_chunks, const int64_t* meta_in,
@@ -1498,6 +1690,15 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
+  return merge_launch(st, t, d_out_offsets, d_out_ids, s);
+}
+
+}  // extern "C"
+
+namespace {
+
+int merge_launch(emqx_shard_step* st, const ShardTab& t, uint64_t* d_out_offsets, uint32_t* d_out_ids, hipStream_t s) {
+  const uint32_t G = st->world;
   const uint64_t n = st->n, m = st->m;
   if (m && st->one) {
     hipLaunchKernelGGL(shard_gather_topic_kernel, dim3(grid_of(n, 256)), dim3(256), 0, s, t, st->self_ids, st->key_s,
@@ -1515,6 +1716,124 @@ int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, 
   }
   SS_TRY(hipGetLastError());
   return EMQX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- the fixed-capacity form --------------------------------------------------------------
+
+int emqx_shard_step_recv_fixed(emqx_shard_step* st, const uint8_t* const* d_chunks, const uint64_t* cap_requests,
+                               const uint64_t* cap_bytes, uint8_t* const* d_bytes, uint64_t* const* d_offsets,
+                               void* stream) {
+  if (!st || !st->have_send || !d_chunks || !cap_requests || !cap_bytes || !d_offsets) return EMQX_EINVAL;
+  const uint32_t G = st->world;
+  bool rel = true;
+  SlotCaps cap{};
+  SlotOffsets so{};
+  SlotBytes sb{};
+  uint64_t qall = 0, yall = 0;
+  for (uint32_t e = 0; e < kE; ++e) {
+    if (!d_offsets[e] || cap_requests[e] >= (1ull << 31)) return EMQX_EINVAL;
+    cap.q[e] = cap_requests[e];
+    cap.y[e] = cap_bytes[e];
+    so.p[e] = d_offsets[e];
+    sb.p[e] = d_bytes ? d_bytes[e] : nullptr;
+    rel &= sb.p[e] == nullptr;
+    qall += cap.q[e];
+    yall += cap.y[e];
+  }
+  for (uint32_t e = 0; e < kE; ++e)
+    if (!rel && !sb.p[e] && cap.q[e]) return EMQX_EINVAL;  // (in place: every slot, and only at world 1)
+  if (rel && G != 1) return EMQX_EINVAL;
+  sb.rel = rel ? 1u : 0u;
+  ShardTab ch{};
+  for (uint32_t r = 0; r < G; ++r) {
+    if (!d_chunks[r]) return EMQX_EINVAL;
+    ch.chunk[r] = reinterpret_cast<uint64_t>(d_chunks[r]);
+  }
+  st->fixed_q = qall;
+  st->have_recv = true;
+  if (st->host) {
+    recv_table(ch.chunk, G, cap, rel, st->d_tab, st->d_pad, st->d_flagw);
+    if (!st->d_flagw[0])
+      for (uint32_t r = 0; r < G; ++r)
+        for (uint32_t e = 0; e < kE; ++e) unpack_part(*st->d_tab, so, sb, r, e, 0, 1);
+    for (uint32_t e = 0; e < kE; ++e) pad_slot(*st->d_tab, G, so, cap, st->d_pad, e, 0, 1);
+    return EMQX_OK;
+  }
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  SS_TRY(hipSetDevice(st->device));
+  hipLaunchKernelGGL(shard_recv_table_kernel, dim3(1), dim3(64), 0, s, ch, G, cap, sb.rel, st->d_tab, st->d_pad,
+                     st->d_flagw);
+  const uint64_t per = std::max<uint64_t>(qall, yall / 16) / (kE * G) + 1;
+  const uint32_t x = grid_of(per, 256, std::max<uint32_t>(1, 1024 / G));
+  hipLaunchKernelGGL(shard_unpack_fixed_kernel, dim3(x, G, kE), dim3(256), 0, s, st->d_tab, so, sb, st->d_flagw);
+  hipLaunchKernelGGL(shard_pad_kernel, dim3(grid_of(qall / kE + 1, 256, 1024), kE), dim3(256), 0, s, st->d_tab, G, so,
+                     cap, st->d_pad);
+  SS_TRY(hipGetLastError());
+  return EMQX_OK;
+}
+
+int emqx_shard_step_answer_fixed(emqx_shard_step* st, const uint64_t* const* d_offsets, const uint32_t* const* d_ids,
+                                 const uint64_t* const* d_summaries, uint32_t self_rank, uint32_t* d_answer,
+                                 uint64_t chunk_words, void* stream) {
+  if (!st || !st->have_recv || !d_offsets || !d_ids || !d_answer || chunk_words < kHW) return EMQX_EINVAL;
+  const uint32_t G = st->world;
+  if (self_rank >= G && self_rank != kNone) return EMQX_EINVAL;
+  EngineCsrs cs{};
+  st->self_ids = SelfIds{};
+  st->self_ids.self = self_rank;
+  st->self_ids.rtab = st->d_tab;
+  st->self_ids.flagw = st->d_flagw;
+  for (uint32_t e = 0; e < kE; ++e) {
+    if (!d_offsets[e] || !d_ids[e]) return EMQX_EINVAL;
+    cs.off[e] = d_offsets[e];
+    cs.ids[e] = d_ids[e];
+    cs.sum[e] = d_summaries ? d_summaries[e] : nullptr;
+    st->self_ids.ids[e] = d_ids[e];
+    st->self_ids.off[e] = d_offsets[e];
+  }
+  if (st->host) {
+    answer_plan(cs, *st->d_tab, self_rank, G, chunk_words, st->d_flagw);
+    for (uint32_t r = 0; r < G; ++r)
+      answer_source(cs, *st->d_tab, self_rank, d_answer, nullptr, r, G, 0, 1, false, chunk_words, st->d_flagw[0]);
+    return EMQX_OK;
+  }
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  SS_TRY(hipSetDevice(st->device));
+  hipLaunchKernelGGL(shard_answer_plan_kernel, dim3(1), dim3(64), 0, s, cs, st->d_tab, self_rank, G, chunk_words,
+                     st->d_flagw);
+  const uint32_t x = grid_of(8 * st->fixed_q / G + 1, 256, std::max<uint32_t>(1, 1024 / G));  // ~8 ids a request
+  hipLaunchKernelGGL(shard_answer_fixed_kernel, dim3(x, G), dim3(256), 0, s, cs, st->d_tab, self_rank, d_answer,
+                     chunk_words, st->d_flagw);
+  SS_TRY(hipGetLastError());
+  return EMQX_OK;
+}
+
+int emqx_shard_step_merge_fixed(emqx_shard_step* st, const uint32_t* const* d_chunks, uint64_t* d_out_offsets,
+                                uint32_t* d_out_ids, uint32_t* d_flag, void* stream) {
+  if (!st || !st->have_send || !st->self_ids.flagw || !d_chunks || !d_out_offsets || (st->n && !d_out_ids))
+    return EMQX_EINVAL;
+  const uint32_t G = st->world;
+  ShardTab t{};
+  for (uint32_t r = 0; r < G; ++r) {
+    if (!d_chunks[r]) return EMQX_EINVAL;
+    t.chunk[r] = reinterpret_cast<uint64_t>(d_chunks[r]);
+  }
+  if (st->host) {
+    merge_plan(t.chunk, G, st->d_flagw, d_flag);
+    try {
+      return host_merge(st, t, d_out_offsets, d_out_ids);
+    } catch (const std::bad_alloc&) {
+      return EMQX_ENOMEM;
+    }
+  }
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  SS_TRY(hipSetDevice(st->device));
+  hipLaunchKernelGGL(shard_merge_plan_kernel, dim3(1), dim3(64), 0, s, t, G, st->d_flagw, d_flag);
+  return merge_launch(st, t, d_out_offsets, d_out_ids, s);
 }
 
 }  // extern "C"

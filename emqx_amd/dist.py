@@ -32,6 +32,7 @@ SURVEY §8(e).  Two layouts:
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import sys
@@ -255,6 +256,11 @@ P_SPACE = {"auto": 0, "sharded": 1, "replicated": 2}  # emqx_shard_plan p_space 
 _NOSYNC_PROBE = os.environ.get("EMQX_SHARD_NOSYNC_PROBE") == "1"
 
 
+def fixed_steps() -> bool:
+    """``ShardedMatcher.match_stream`` in the fixed-capacity form (env ``EMQX_SHARD_FIXED``, 1)."""
+    return os.environ.get("EMQX_SHARD_FIXED", "1") != "0"
+
+
 def stream_depth() -> int:
     """Steps in flight in ``ShardedMatcher.match_stream`` (env ``EMQX_SHARD_DEPTH``)."""
     return int(os.environ.get("EMQX_SHARD_DEPTH", "3"))
@@ -443,7 +449,8 @@ class _HostEngine:
 
     def _run(self, b_addr, o_addr, n, off_addr, ids_addr, cap):
         offs = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(o_addr)).astype(np.int64)
-        buf = np.ctypeslib.as_array((ctypes.c_uint8 * max(int(offs[-1]), 1)).from_address(b_addr))[: int(offs[-1])]
+        lo, hi = int(offs[0]), int(offs[-1])  # (a batch matched in place starts past its chunk's header)
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * max(hi, 1)).from_address(b_addr))[lo:hi]
         cnt, ids = self.fn(self.slot, torch.from_numpy(buf.copy()), torch.from_numpy(offs - offs[0]))
         cnt = cnt.numpy().astype(np.int64)
         out = np.ctypeslib.as_array((ctypes.c_uint64 * (n + 1)).from_address(off_addr))
@@ -554,6 +561,9 @@ class ShardedMatcher:
         self._cuda = self.device.type == "cuda"
         self._lane = self._lanes[0]
         self._caps = [1 << 20] * SHARD_ENGINES
+        self._fixed = None        # the fixed form's agreed capacities (_learn_fixed)
+        self._last_sizes = None   # the last classic step's sizes (what _learn_fixed learns from)
+        self.last_fixed_redo = 0
 
     # (the step's resources are the current lane's)
     _step = property(lambda self: self._lane.step)
@@ -679,7 +689,7 @@ class ShardedMatcher:
             return stop.value
 
     def match_stream(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], exchange: Optional[Callable] = None,
-                     depth: Optional[int] = None):
+                     depth: Optional[int] = None, fixed: Optional[bool] = None):
         """match_all over a sequence of this rank's batches with ``depth`` steps in flight (device
         step only; default ``stream_depth()``), one lane each: step k + depth - 1's send runs
         while the earlier steps' engines walk, and its requests are exchanged, unpacked and handed
@@ -688,10 +698,16 @@ class ShardedMatcher:
         behind step k's merge, which waits for step k + 1's walk to free the CUs; a third lane
         gives that merge and send a whole walk to run under.  Every rank runs the same schedule,
         so the collectives pair up.  ``exchange``: the exchange-point function (default
-        ``_exchange``: the process group; ``EmulatedWorld`` passes a recorded one).  Returns every
+        ``_exchange``: the process group; ``EmulatedWorld`` passes a recorded one).  ``fixed``
+        (default ``fixed_steps()`` over this rank's own process group): the fixed-capacity form
+        (``_match_stream_fixed``), no host synchronisation between the steps.  Returns every
         batch's (offsets, ids)."""
-        assert self._cuda, "match_stream keeps steps in flight on device streams"
         D = max(1, int(depth or stream_depth()))
+        if fixed is None:
+            fixed = exchange is None and fixed_steps()
+        if fixed:
+            return self._match_stream_fixed(batches, D)
+        assert self._cuda, "match_stream keeps steps in flight on device streams"
         ex = exchange or self._exchange
         caller = torch.cuda.current_stream(self.device)
         lanes = [self._lane_n(i) for i in range(D)]
@@ -757,6 +773,74 @@ class ShardedMatcher:
                 t.record_stream(caller)
         return res
 
+    def _match_stream_fixed(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], D: int):
+        """match_stream in the fixed-capacity form: every step enqueued on its lane (D lanes)
+        with no host read — send, chunk exchange, recv, engines, answer, answer exchange, merge —
+        then one synchronisation for all of them: each step's flag, and each CSR cut to its
+        length.  A flagged step (some chunk, slot or engine over its capacity; the flag is the
+        same on every rank) is redone in the classic form, which also teaches larger capacities.
+        The first call learns the capacities from a classic step (its batch's result).  Runs in
+        host mode too (CPU device: the steps one after another)."""
+        K = len(batches)
+        res = [None] * K
+        if not K:
+            return res
+        first = 0
+        if self._fixed is None:
+            res[0] = self.match_all(batches[0])
+            self._learn_fixed()
+            first = 1
+        cuda = self._cuda
+        flags = torch.zeros(K, dtype=torch.int64, pin_memory=cuda)
+        if cuda:
+            d = ctypes.c_void_p()
+            rc = _hip().hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(flags.data_ptr()), 0)
+            if rc != 0:
+                raise RuntimeError(f"hipHostGetDevicePointer: {rc}")
+            faddr = d.value
+            caller = torch.cuda.current_stream(self.device)
+        else:
+            faddr = flags.data_ptr()
+        lanes = [self._lane_n(i) for i in range(D)]
+        if cuda:
+            for ln in lanes:
+                if ln.stream is None:
+                    ln.stream = torch.cuda.Stream(device=self.device)
+                ln.stream.wait_stream(caller)
+        try:
+            for k in range(first, K):
+                self._lane = lanes[k % D]
+                ctx = torch.cuda.stream(self._lane.stream) if cuda else contextlib.nullcontext()
+                with ctx:
+                    gen = self._step_gen_fixed(batches[k], faddr + 8 * k)
+                    try:
+                        op = next(gen)
+                        while True:
+                            op = gen.send(self._exchange(op))
+                    except StopIteration as stop:
+                        res[k] = stop.value
+        finally:
+            self._lane = self._lanes[0]
+        if cuda:
+            for ln in lanes:
+                caller.wait_stream(ln.stream)
+            caller.synchronize()
+        ends = torch.stack([res[k][0][-1] for k in range(first, K)]).cpu().tolist() if K > first else []
+        fl = flags.tolist()
+        self.last_fixed_redo = 0
+        for k in range(first, K):
+            if fl[k]:
+                res[k] = self.match_all(batches[k])
+                self._learn_fixed()
+                self.last_fixed_redo += 1
+            else:
+                res[k] = (res[k][0], res[k][1][: int(ends[k - first])])
+        if cuda:
+            for r in res:
+                for t in r:
+                    t.record_stream(caller)
+        return res
+
     def _exchange(self, op):
         """One exchange point of ``_step_gen`` over the process group:
         ("local_sizes", pinned words, W) at world 1: the stream synchronised, the words read;
@@ -770,6 +854,12 @@ class ShardedMatcher:
                 torch.cuda.current_stream(self.device).synchronize()
             lst = words[: W * self.world].tolist()
             return lst, lst, words
+        if op[0] == "fixed":  # equal splits of c elements: chunk r of buf to rank r
+            _, buf, c, name = op
+            G, es = self.world, buf.element_size()
+            recv = self._buf("f" + name, G * c, buf.dtype)
+            _a2a(recv[: G * c], buf[: G * c], [c] * G, [c] * G, self.group)
+            return [buf.data_ptr() + es * c * r if r == self.rank else recv.data_ptr() + es * c * r for r in range(G)]
         if op[0] == "sizes":
             _, words, W = op
             G = self.world
@@ -833,6 +923,7 @@ class ShardedMatcher:
         self.last_exchange_out = [[x for x in out_b], None]
         chunks = [send.data_ptr()] if G == 1 else (yield ("chunks", send, out_b, in_b, "recv"))
         NQ = [sum(mi_l[1 + e::MW]) for e in range(E)]
+        self._last_sizes = {"chunk": max(out_b), "q": NQ, "y": [sum(mi_l[1 + E + e::MW]) for e in range(E)]}
         # a slot fed by one source only is matched in place in that source's chunk (recv
         # replaces its byte buffer's address); the others are gathered into these buffers
         one = [sum(1 for x in mi_l[1 + e::MW] if x) <= 1 for e in range(E)]
@@ -907,6 +998,7 @@ class ShardedMatcher:
             redo = True
         # 4. answers back to their sources, merged per topic in batch order
         out_w, in_w = am_l[0::3], ai_l[0::3]
+        self._last_sizes["answer"] = max(out_w)
         self.last_exchange_out[1] = [4 * x for x in out_w]
         back = [ans.data_ptr()] if G == 1 else (yield ("chunks", ans, out_w, in_w, "back"))
         total = sum(ai_l[2::3])
@@ -916,6 +1008,99 @@ class ShardedMatcher:
                                            P(out_ids), S), "emqx_shard_step_merge")
         mark(7)
         return out_off, out_ids[:total]
+
+    def _allreduce_max(self, vals: List[int]) -> List[int]:
+        if self.world == 1 or self.group is None and not dist.is_initialized():
+            return list(vals)
+        on_dev = self._cuda and dist.get_backend(self.group) != "gloo"
+        t = torch.tensor(vals, dtype=torch.int64, device=self.device if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return [int(x) for x in t.cpu().tolist()]
+
+    def _learn_fixed(self):
+        """The fixed form's capacities from the last classic step's sizes (every rank at the same
+        point: the chunk capacities are agreed by an all-reduce of their maxima), never shrinking:
+        request chunks, answer chunks (u32 words), per slot requests and bytes (this rank's)."""
+        ls = self._last_sizes
+        old = self._fixed or {"chunk": 0, "answer": 0, "q": [0] * SHARD_ENGINES, "y": [0] * SHARD_ENGINES}
+        # (margins: a rank's requests and chunks vary by ~sqrt between batches of one stream, so
+        # 1/32 covers them; the engines walk every padding topic, so a wide margin costs walk time)
+        c1 = (ls["chunk"] + ls["chunk"] // 32 + 4096 + 15) // 16 * 16
+        c2 = ls["answer"] + ls["answer"] // 16 + 65536
+        c1, c2 = self._allreduce_max([max(c1, old["chunk"]), max(c2, old["answer"])])
+        q = [0 if self.engines[e] is None else max(old["q"][e], x + x // 32 + 1024) for e, x in enumerate(ls["q"])]
+        y = [0 if self.engines[e] is None else max(old["y"][e], x + x // 32 + 65536) for e, x in enumerate(ls["y"])]
+        self._fixed = {"chunk": c1, "answer": c2, "q": q, "y": y}
+
+    def _step_gen_fixed(self, topics: Tuple[torch.Tensor, torch.Tensor], flag_addr: int):
+        """One step in the fixed-capacity form (``emqx_shard_step_*_fixed``): the same kernels
+        with chunks at the agreed capacities (``_learn_fixed``), so the only exchange points are
+        the two chunk exchanges (equal splits; none at world 1) and nothing is read on the host.
+        The engines match each slot's fixed-size batch (padding topics past its requests) into
+        their learnt id capacities.  The step's flag (u32 at ``flag_addr``: 0 = valid) is
+        written by the merge; a flagged step is redone by the caller.  Returns (offsets int64
+        (n+1,), ids int32 with room to spare: the topics' ids end at offsets[n])."""
+        from . import _lib
+        L = _lib.lib()
+        E, fx = SHARD_ENGINES, self._fixed
+        dev, G = self.device, self.world
+        st = self._step.h
+        stream = torch.cuda.current_stream(dev).cuda_stream if self._cuda else None
+        S = ctypes.c_void_p(stream)
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        PA = lambda ts: (ctypes.c_void_p * E)(*[None if t is None else t.data_ptr() for t in ts])  # noqa: E731
+        tb, to = topics
+        tb = tb.to(dev)
+        to = to.to(dev).to(torch.int64)
+        if tb.numel() == 0:
+            tb = torch.zeros(16, dtype=torch.uint8, device=dev)
+        n = to.numel() - 1
+        c1, c2, capq, capy = fx["chunk"], fx["answer"], fx["q"], fx["y"]
+        send = self._buf("fsend", G * c1, torch.uint8)
+        meta = self._buf("fmeta", (1 + 2 * E) * G, torch.int64)
+        _lib.check(L.emqx_shard_step_send_fixed(st, P(tb), P(to), n, P(send), c1, P(meta), S),
+                   "emqx_shard_step_send_fixed")
+        chunks = [send.data_ptr()] if G == 1 else (yield ("fixed", send, c1, "recv"))
+        in_place = G == 1  # (world 1: every slot matched where send packed it)
+        qbytes = [None] * E if in_place else [self._buf(f"q_bytes{e}", capy[e] + 16, torch.uint8) for e in range(E)]
+        qoff = [self._buf(f"q_off{e}", capq[e] + 1, torch.int64) for e in range(E)]
+        _lib.check(L.emqx_shard_step_recv_fixed(st, (ctypes.c_void_p * G)(*chunks), (ctypes.c_uint64 * E)(*capq),
+                                                (ctypes.c_uint64 * E)(*capy), None if in_place else PA(qbytes),
+                                                PA(qoff), S), "emqx_shard_step_recv_fixed")
+        hsumm, dsumm = self._pinned("summary", 8 * E)
+        if self._stream_b is None and self._cuda:
+            self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E - 1)]
+        cur = torch.cuda.current_stream(dev) if self._cuda else None
+        outs, used, room = [], [], 0
+        for e in range(E):
+            ro = self._buf(f"off{e}", capq[e] + 1, torch.int64)
+            if not capq[e]:
+                outs.append([ro, self._buf(f"ids{e}", 16, torch.int32)])
+                continue
+            ri = self._buf(f"ids{e}", max(self._caps[e], 1 << 16), torch.int32)
+            room += ri.numel()
+            es = cur if not used or not self._cuda else self._stream_b[len(used) - 1]
+            if es is not cur:
+                es.wait_stream(cur)
+            used.append(es)
+            eb = send.data_ptr() if in_place else qbytes[e].data_ptr()
+            self.engines[e].match_device_async(eb, qoff[e].data_ptr(), capq[e], ro.data_ptr(), ri.data_ptr(),
+                                               ri.numel(), dsumm + 64 * e, mode=self.mode,
+                                               stream=es.cuda_stream if es is not None else None)
+            outs.append([ro, ri])
+        for es in used:
+            if es is not cur:
+                cur.wait_stream(es)
+        ans = self._buf("fanswer", G * c2, torch.int32)
+        sp = (ctypes.c_void_p * E)(*[dsumm + 64 * e if capq[e] else None for e in range(E)])
+        _lib.check(L.emqx_shard_step_answer_fixed(st, PA([o[0] for o in outs]), PA([o[1] for o in outs]), sp,
+                                                  self.rank, P(ans), c2, S), "emqx_shard_step_answer_fixed")
+        back = [ans.data_ptr()] if G == 1 else (yield ("fixed", ans, c2, "back"))
+        out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        out_ids = torch.empty(G * c2 + room + 16, dtype=torch.int32, device=dev)
+        _lib.check(L.emqx_shard_step_merge_fixed(st, (ctypes.c_void_p * G)(*back), P(out_off), P(out_ids),
+                                                 ctypes.c_void_p(flag_addr), S), "emqx_shard_step_merge_fixed")
+        return out_off, out_ids
 
     def match(self, topics: Optional[Tuple[torch.Tensor, torch.Tensor]], src: int = 0, dst: int = 0):
         """Match a batch held by rank ``src``; rank ``dst`` gets the CSR in batch order

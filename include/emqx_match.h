@@ -574,6 +574,41 @@ int emqx_shard_step_answer(emqx_shard_step* st, const uint64_t* const* d_offsets
 int emqx_shard_step_merge(emqx_shard_step* st, const uint32_t* const* d_chunks, const int64_t* ans_meta_in,
                           uint64_t* d_out_offsets, uint32_t* d_out_ids, void* stream);
 
+/* The step in fixed-capacity form: no size exchange and no host read between the calls, so a
+ * caller can enqueue steps back to back (dist.py match_stream).  The ranks agree beforehand on
+ * a request-chunk size and an answer-chunk size (each rank's chunks sit at those capacities,
+ * exchanged with equal splits); a step that does not fit anywhere is flagged, the same on every
+ * rank, and its result is invalid: the caller redoes it with the calls above (and learns larger
+ * capacities).  One step at a time per object, as above; the calls of one step in this order.
+ *   send_fixed    as send, chunk r at r * chunk_bytes of d_send (world * chunk_bytes bytes;
+ *                 chunk_bytes a multiple of 16).  A chunk over chunk_bytes empties every chunk
+ *                 and sets flag bit 1 in their header word 3.  d_meta as send's (device).
+ *   recv_fixed    d_chunks[world] the received chunks (host array of device pointers; the own
+ *                 one where send_fixed packed it) -> one fixed-size batch per slot: cap_requests[e]
+ *                 topics (host array), d_offsets[e] cap_requests[e] + 1 offsets (the slot's
+ *                 requests, then empty padding topics at the end of its bytes), bytes into d_bytes[e]
+ *                 (cap_bytes[e] bytes).  d_bytes NULL (world 1 only): every slot is matched in place,
+ *                 with its offsets from the start of d_chunks[0] (match the slot batches with bytes
+ *                 = d_chunks[0]).  A flagged chunk, or a slot over its capacity, flags the step and
+ *                 empties every batch.  The engines then match cap_requests[e] topics per slot.
+ *   answer_fixed  as answer, chunk s at s * chunk_words of d_answer (world * chunk_words u32
+ *                 words), header word 7 = the step's flag; an engine call that did not complete (its
+ *                 summary) or a chunk over chunk_words flags the step, and a flagged step sends
+ *                 header-only chunks.
+ *   merge_fixed   d_chunks[world] the answer chunks -> the CSR as merge's (d_out_ids: room for
+ *                 every answer chunk's ids and this rank's own engine ids); *d_flag (u32, device or
+ *                 mapped host memory) = the step's flag ORed over every rank's chunk: 0 = valid. */
+int emqx_shard_step_send_fixed(emqx_shard_step* st, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t n,
+                               uint8_t* d_send, uint64_t chunk_bytes, int64_t* d_meta, void* stream);
+int emqx_shard_step_recv_fixed(emqx_shard_step* st, const uint8_t* const* d_chunks, const uint64_t* cap_requests,
+                               const uint64_t* cap_bytes, uint8_t* const* d_bytes, uint64_t* const* d_offsets,
+                               void* stream);
+int emqx_shard_step_answer_fixed(emqx_shard_step* st, const uint64_t* const* d_offsets, const uint32_t* const* d_ids,
+                                 const uint64_t* const* d_summaries, uint32_t self_rank, uint32_t* d_answer,
+                                 uint64_t chunk_words, void* stream);
+int emqx_shard_step_merge_fixed(emqx_shard_step* st, const uint32_t* const* d_chunks, uint64_t* d_out_offsets,
+                                uint32_t* d_out_ids, uint32_t* d_flag, void* stream);
+
 /* emqx_topic:match/2 on raw binaries (emqx_topic.erl:68-87): 1 = match, 0 = no match. */
 int emqx_topic_match(const uint8_t* name, uint64_t name_len, const uint8_t* filter,
                      uint64_t filter_len);

@@ -225,6 +225,61 @@ def test_sharded_redo_on_small_capacities():
         assert learnt and same
 
 
+def _worker_fixed(rank, world, port, q, p_space):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from emqx_amd import dist as D
+        filters, topics = _batches()
+        sm = _matcher(filters, rank, world, p_space)
+        part = D.split_topics(topics, rank, world)
+        T = lambda b: (torch.from_numpy(b[0].copy()), torch.from_numpy(b[1].astype(np.int64)))  # noqa: E731
+        blanks = (np.zeros(0, np.uint8), np.zeros(4, np.uint64))
+        # the first batch teaches the capacities (a classic step); the whole topic set twice then
+        # overflows them (a flagged step, redone on every rank alike), the rest fit
+        nb = int(topics[1][-1])
+        big = (np.concatenate([topics[0][:nb], topics[0][:nb]]),
+               np.concatenate([topics[1].astype(np.uint64), nb + topics[1][1:].astype(np.uint64)]))
+        batches = [part, part, blanks, big, part, (np.zeros(0, np.uint8), np.zeros(1, np.uint64))]
+        res = sm.match_stream([T(b) for b in batches], fixed=True, depth=2)
+        redo = sm.last_fixed_redo
+        res2 = sm.match_stream([T(b) for b in batches[:3]], fixed=True, depth=3)  # learnt: no redo
+        q.put((rank, batches, [(o.numpy(), i.numpy()) for o, i in res + res2], redo, sm.last_fixed_redo))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,p_space", [(1, "auto"), (2, "sharded"), (3, "replicated")])
+def test_sharded_fixed_capacity_steps(world, p_space):
+    """match_stream in the fixed-capacity form (emqx_shard_step_*_fixed: chunks at agreed
+    capacities, the recv table built from the chunk headers, fixed-size engine batches with
+    padding topics, the flag carried in every chunk): every step's CSR equals the single-table
+    oracle's; a batch over the capacities is flagged on every rank and redone in the classic form,
+    after which the learnt capacities need no redo.  World 1 matches every slot in place."""
+    from oracle import cpp as C
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_fixed, args=(r, world, port, q, p_space)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    o = C.CppOracle(True)
+    o.add_packed(*_batches()[0])
+    for rank, batches, res, redo, redo2 in got:
+        assert redo == 1 and redo2 == 0, (rank, redo, redo2)
+        for k, (b, (off, ids)) in enumerate(zip(batches + batches[:3], res)):
+            tb, to = b
+            off_o, ids_o, _ = o.match_csr(tb if len(tb) else np.zeros(1, np.uint8), to.astype(np.uint64), mode=0,
+                                          threads=2)
+            assert C.csr_mismatches(off, ids, off_o, ids_o).size == 0, (rank, k)
+
+
 def test_shard_layout_covers_every_match():
     """Every filter that matches a topic is held by the rank of the topic's request to the
     filter's engine (so the two requests find every match, once); a filter is held by exactly

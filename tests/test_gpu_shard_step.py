@@ -91,15 +91,26 @@ def test_shard_step_edge_batches_world1():
         for batch in ([b"a/b"], [b"zz/yy/xx"] * 7, [b"$SYS"] * 3):
             t = pack(batch)
             _check(sm.match_all(_dev_topics(t)), filters, t)
-        # two steps in flight (match_stream): every batch's CSR, an empty one among them
-        seq = [topics, pack([b"a/b"]), empty, pack(TOPICS[::-1]), topics]
-        outs = sm.match_stream([_dev_topics(t) for t in seq])
-        assert len(outs) == len(seq)
-        for t, got in zip(seq, outs):
-            if len(t[1]) == 1:
-                assert got[0].cpu().tolist() == [0] and got[1].numel() == 0
-            else:
-                _check(got, filters, t)
+        # steps in flight (match_stream), in both forms (fixed capacities: no host read between
+        # the steps, the first call learning its capacities; classic: the size syncs): every
+        # batch's CSR, an empty one among them, and in the fixed form a batch over the learnt
+        # capacities (flagged, redone in the classic form)
+        big = pack(TOPICS * 400)
+        for fixed in (True, False):
+            seq = [topics, pack([b"a/b"]), empty, pack(TOPICS[::-1]), topics] + ([big, topics] if fixed else [])
+            outs = sm.match_stream([_dev_topics(t) for t in seq], fixed=fixed)
+            assert len(outs) == len(seq)
+            for t, got in zip(seq, outs):
+                if len(t[1]) == 1:
+                    assert got[0].cpu().tolist() == [0] and got[1].numel() == 0
+                else:
+                    _check(got, filters, t)
+            if fixed:
+                assert sm.last_fixed_redo == 1
+                outs = sm.match_stream([_dev_topics(t) for t in (big, topics, big)], fixed=True, depth=2)
+                assert sm.last_fixed_redo == 0
+                for t, got in zip((big, topics, big), outs):
+                    _check(got, filters, t)
     finally:
         dist.destroy_process_group()
 
@@ -146,8 +157,11 @@ def _rank_main(rank, world, port, q, p_space="sharded"):
         got = sm.match_all(_dev_topics(wl.topics))
         empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint64))
         third = sm.match_all(_dev_topics(empty if rank == 1 else wl.topics))
-        # two steps in flight over the process group: the collectives of steps k and k + 1 pair up
-        streamed = sm.match_stream([_dev_topics(wl.topics)] * 3)
+        # steps in flight over the process group (the fixed form, then the classic one): the
+        # collectives of the steps pair up
+        streamed = sm.match_stream([_dev_topics(wl.topics)] * 3) + sm.match_stream([_dev_topics(wl.topics)] * 3,
+                                                                                  fixed=False)
+        assert sm.last_fixed_redo == 0
         off, ids = got[0].cpu().numpy(), got[1].cpu().numpy().view(np.uint32)
         off_o, ids_o = _oracle(wl.filters, wl.topics)
         bad = C.csr_mismatches(off.astype(np.uint64), ids, off_o, ids_o)
