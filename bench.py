@@ -627,9 +627,10 @@ def emulated_bench(args, dev):
 def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
     """One --emulate-world line (emulated_bench) at world G; returns the parity failures."""
     import torch
-    from emqx_amd.dist import EmulatedWorld
+    from emqx_amd.dist import EmulatedWorld, fixed_steps
     from oracle import cpp as C
     n = args.batch
+    fx = fixed_steps()  # the fixed-capacity form (its capacities learnt from the classic warm-up)
     t0 = time.time()
     with progress(f"building the {G} ranks' engines"):
         ew = EmulatedWorld(wl.filters, G, dev, mode=args.mode, p_space=args.p_space,
@@ -637,25 +638,31 @@ def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
     log(f"{G} ranks built ({time.time() - t0:.1f}s): filters per rank [A, B, AB] {ew.filters_per_rank}")
     for _ in range(max(args.warmup, 1)):
         res = ew.step(batches)
+    if fx:
+        ew.learn_fixed()
+        res = ew.step(batches, fixed=True)
     torch.cuda.synchronize()
     # the whole emulated step, back to back (all G ranks' work on one GPU, exchanges free)
     t_all = time.perf_counter()
     for _ in range(args.steps):
-        ew.step(batches)
+        ew.step(batches, fixed=fx)
     torch.cuda.synchronize()
     all_ms = 1e3 * (time.perf_counter() - t_all) / max(args.steps, 1)
-    phases = EmulatedWorld.PHASES if G > 1 else EmulatedWorld.PHASES_1
+    if fx:
+        phases = EmulatedWorld.PHASES_FIXED if G > 1 else EmulatedWorld.PHASES_FIXED_1
+    else:
+        phases = EmulatedWorld.PHASES if G > 1 else EmulatedWorld.PHASES_1
     per = {}
     for mode in ("wall", "gpu"):
         acc = np.zeros((G, len(phases)))
         for _ in range(args.steps):
-            ew.step(batches, timing=mode)
+            ew.step(batches, timing=mode, fixed=fx)
             t = np.array(ew.last_times, dtype=np.float64)
             if t.shape != acc.shape:
                 raise SystemExit(f"unexpected exchange rounds {t.shape} (a redo during the timed steps)")
             acc += t
         per[mode] = acc / max(args.steps, 1)
-    res = ew.step(batches)
+    res = ew.step(batches, fixed=fx)
     torch.cuda.synchronize()
     # parity
     bad, ids_checked = [], 0
@@ -668,7 +675,7 @@ def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
     # side replayed from the step above), its last result checked too
     stream_ms, bad_stream = [], []
     for r in range(G):
-        ms, rs = ew.rank_stream(r, batches[r], args.steps)
+        ms, rs = ew.rank_stream(r, batches[r], args.steps, fixed=fx)
         stream_ms.append(ms)
         bad_stream.append(int(C.csr_mismatches(rs[-1][0].cpu().numpy().astype(np.uint64),
                                                rs[-1][1].cpu().numpy().view(np.uint32), *refs[r]).size))
@@ -686,7 +693,8 @@ def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
     for k in range(2):
         np.fill_diagonal(bo[k], 0)  # (a rank's own chunk is never moved)
     exch_ms = [float(bo[k].max()) / link * 1e3 for k in range(2)]
-    fixed_ms = 4 * args.a2a_us / 1e3 if G > 1 else 0.0  # two size exchanges + two chunk exchanges
+    # two size exchanges + two chunk exchanges (the fixed form: the chunk exchanges only)
+    fixed_ms = (2 if fx else 4) * args.a2a_us / 1e3 if G > 1 else 0.0
     proj = {}
     for mode in ("wall", "gpu"):
         slow = per[mode].max(axis=0)
@@ -710,6 +718,10 @@ def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
                                f"{G}-way plan, every rank publishing its own {n}-topic batch per step",
                    "parallelism": f"filter-sharded x{G} emulated on one GPU (dist.py EmulatedWorld)"},
         "p_space": "replicated" if ew.p_replicated else "sharded",
+        "fixed_capacity_steps": fx,
+        **({"fixed_capacities": {"request_chunk_bytes": ew.matchers[0]._fixed["chunk"],
+                                 "answer_chunk_words": ew.matchers[0]._fixed["answer"],
+                                 "slot_requests_rank0": ew.matchers[0]._fixed["q"]}} if fx else {}),
         "filters_per_rank_A_B_AB": ew.filters_per_rank,
         "shard_plan_keys": int(len(ew.plan)),
         "requests_per_rank_by_slot": [list(m.last_slot_topics) for m in ew.matchers],

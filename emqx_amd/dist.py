@@ -706,7 +706,7 @@ class ShardedMatcher:
         if fixed is None:
             fixed = exchange is None and fixed_steps()
         if fixed:
-            return self._match_stream_fixed(batches, D)
+            return self._match_stream_fixed(batches, D, exchange)
         assert self._cuda, "match_stream keeps steps in flight on device streams"
         ex = exchange or self._exchange
         caller = torch.cuda.current_stream(self.device)
@@ -773,20 +773,24 @@ class ShardedMatcher:
                 t.record_stream(caller)
         return res
 
-    def _match_stream_fixed(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], D: int):
+    def _match_stream_fixed(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], D: int,
+                            exchange: Optional[Callable] = None):
         """match_stream in the fixed-capacity form: every step enqueued on its lane (D lanes)
         with no host read — send, chunk exchange, recv, engines, answer, answer exchange, merge —
         then one synchronisation for all of them: each step's flag, and each CSR cut to its
         length.  A flagged step (some chunk, slot or engine over its capacity; the flag is the
         same on every rank) is redone in the classic form, which also teaches larger capacities.
         The first call learns the capacities from a classic step (its batch's result).  Runs in
-        host mode too (CPU device: the steps one after another)."""
+        host mode too (CPU device: the steps one after another).  ``exchange`` (EmulatedWorld's
+        replay): capacities learnt beforehand, and a flagged step is an error (no classic redo)."""
         K = len(batches)
         res = [None] * K
         if not K:
             return res
+        ex = exchange or self._exchange
         first = 0
         if self._fixed is None:
+            assert exchange is None, "the fixed form over a replayed exchange needs learnt capacities"
             res[0] = self.match_all(batches[0])
             self._learn_fixed()
             first = 1
@@ -816,7 +820,7 @@ class ShardedMatcher:
                     try:
                         op = next(gen)
                         while True:
-                            op = gen.send(self._exchange(op))
+                            op = gen.send(ex(op))
                     except StopIteration as stop:
                         res[k] = stop.value
         finally:
@@ -830,6 +834,8 @@ class ShardedMatcher:
         self.last_fixed_redo = 0
         for k in range(first, K):
             if fl[k]:
+                if exchange is not None:
+                    raise RuntimeError(f"fixed-capacity step {k} flagged ({fl[k]}) over a replayed exchange")
                 res[k] = self.match_all(batches[k])
                 self._learn_fixed()
                 self.last_fixed_redo += 1
@@ -1144,6 +1150,8 @@ class EmulatedWorld:
 
     PHASES = ("send", "sizes1", "recv_match_answer", "sizes2", "merge")
     PHASES_1 = ("send", "recv_match_answer", "merge")  # world 1: no exchange, two host syncs
+    PHASES_FIXED = ("send", "recv_match_answer", "merge")  # the fixed form: the two chunk exchanges
+    PHASES_FIXED_1 = ("step",)  # the fixed form at world 1: no exchange point at all
 
     def __init__(self, filters: Tuple[np.ndarray, np.ndarray], world: int, device: torch.device, mode: int = 0,
                  max_piece_pm: int = MAX_PIECE_PM, on_rank: Optional[Callable] = None, p_space: str = "auto"):
@@ -1177,7 +1185,17 @@ class EmulatedWorld:
             m.close()
         self.matchers = []
 
-    def rank_stream(self, r: int, batch: Tuple[torch.Tensor, torch.Tensor], steps: int):
+    def learn_fixed(self):
+        """The fixed form's capacities from the last (classic) ``step``: every rank's own, the
+        chunk capacities agreed as their maxima (what the ranks' all-reduce would give)."""
+        for m in self.matchers:
+            m._learn_fixed()
+        c1 = max(m._fixed["chunk"] for m in self.matchers)
+        c2 = max(m._fixed["answer"] for m in self.matchers)
+        for m in self.matchers:
+            m._fixed["chunk"], m._fixed["answer"] = c1, c2
+
+    def rank_stream(self, r: int, batch: Tuple[torch.Tensor, torch.Tensor], steps: int, fixed: bool = False):
         """Rank r alone running ``steps`` steps of its batch with two in flight
         (``ShardedMatcher.match_stream``), the other ranks' side replayed from the last ``step``
         (which must have used the same batches): their size words and their chunks for r, which
@@ -1188,6 +1206,10 @@ class EmulatedWorld:
         rec = self.recorded[r]
 
         def replay(op):
+            if op[0] == "fixed":
+                addrs = list(rec[("fixed", op[3])])
+                addrs[r] = op[1].data_ptr() + op[1].element_size() * op[2] * r
+                return addrs
             if op[0] == "local_sizes":
                 return m._exchange(op)
             if op[0] == "sizes":
@@ -1197,10 +1219,10 @@ class EmulatedWorld:
             addrs[r] = op[1].data_ptr() + op[1].element_size() * int(own[r])
             return addrs
 
-        m.match_stream([batch] * max(2, stream_depth()), exchange=replay)  # (every lane's buffers and workspaces)
+        m.match_stream([batch] * max(2, stream_depth()), exchange=replay, fixed=fixed)  # (every lane's buffers)
         torch.cuda.synchronize(self.device)
         t0 = time.perf_counter()
-        res = m.match_stream([batch] * steps, exchange=replay)
+        res = m.match_stream([batch] * steps, exchange=replay, fixed=fixed)
         torch.cuda.synchronize(self.device)
         return 1e3 * (time.perf_counter() - t0) / max(steps, 1), res
 
@@ -1233,10 +1255,21 @@ class EmulatedWorld:
                 t = 1e3 * (time.perf_counter() - t0)
         return op, t
 
-    def step(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], timing: Optional[str] = None):
+    def step(self, batches: List[Tuple[torch.Tensor, torch.Tensor]], timing: Optional[str] = None,
+             fixed: bool = False):
+        """One step of every rank (see the class); ``fixed``: the fixed-capacity form (after
+        ``learn_fixed``; a flagged step is an error here)."""
         G = self.world
         assert len(batches) == G
-        gens = [m._step_gen(b) for m, b in zip(self.matchers, batches)]
+        flags = None
+        if fixed:
+            flags = torch.zeros(G, dtype=torch.int64, pin_memory=True)
+            d = ctypes.c_void_p()
+            if _hip().hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(flags.data_ptr()), 0) != 0:
+                raise RuntimeError("hipHostGetDevicePointer")
+            gens = [m._step_gen_fixed(b, d.value + 8 * r) for r, (m, b) in enumerate(zip(self.matchers, batches))]
+        else:
+            gens = [m._step_gen(b) for m, b in zip(self.matchers, batches)]
         ops, times = [None] * G, [[] for _ in range(G)]
         vals = [None] * G
         rounds = 0
@@ -1262,6 +1295,13 @@ class EmulatedWorld:
                     mi = np.ascontiguousarray(np.concatenate([words[s][W * r: W * (r + 1)] for s in range(G)]))
                     vals[r] = (words[r].tolist(), mi.tolist(), mi)
                     self.recorded[r][("sizes", W)] = vals[r]
+            elif kind == "fixed":  # chunk r of source s at s's buffer + r * the capacity
+                c, es = ops[0][2], ops[0][1].element_size()
+                for r in range(G):
+                    vals[r] = [ops[s][1].data_ptr() + es * c * r for s in range(G)]
+                    self.recorded[r][("fixed", ops[r][3])] = vals[r]
+                self.bytes_out[min(chunk_round, 1)] = es * c
+                chunk_round += 1
             elif kind == "chunks":
                 # chunk r of source s lies at s's buffer + the prefix of s's sizes before r
                 offs = [np.concatenate([[0], np.cumsum(op[2])]).astype(np.int64) for op in ops]
@@ -1275,4 +1315,10 @@ class EmulatedWorld:
             else:
                 raise RuntimeError(f"unknown exchange {kind}")
         self.last_times = times if timing else None
-        return [op[1] for op in ops]
+        out = [op[1] for op in ops]
+        if fixed:
+            torch.cuda.synchronize(self.device)
+            if any(flags.tolist()):
+                raise RuntimeError(f"fixed-capacity step flagged: {flags.tolist()}")
+            out = [(o, i[: int(o[-1].item())]) for o, i in out]
+        return out

@@ -280,5 +280,20 @@ def test_emulated_world_every_source_id_for_id(world, p_space):
         else:
             assert slots[0] == 0 and slots[1] == 0 and slots[2] > 0, slots
             assert all(m.engines[0] is None and m.engines[1] is None for m in ew.matchers)
+        # the fixed-capacity form: capacities learnt from the classic steps above and agreed,
+        # every rank's step with no size exchange; every source ID-for-ID, pipelined too
+        ew.learn_fixed()
+        assert len({(m._fixed["chunk"], m._fixed["answer"]) for m in ew.matchers}) == 1
+        for timing in (None, "gpu"):
+            res = ew.step([_dev_topics(s) for s in srcs], timing=timing, fixed=True)
+            if timing:
+                assert all(len(t) == len(EmulatedWorld.PHASES_FIXED) for t in ew.last_times)
+            for s in range(world):
+                _check(res[s], wl.filters, srcs[s])
+        assert (ew.bytes_out[0] == ew.matchers[0]._fixed["chunk"]).all()
+        for r in range(world):
+            ms, rs = ew.rank_stream(r, _dev_topics(srcs[r]), 3, fixed=True)
+            for got in rs:
+                _check(got, wl.filters, srcs[r])
     finally:
         ew.close()
