@@ -1030,12 +1030,13 @@ class ShardedMatcher:
         ls = self._last_sizes
         old = self._fixed or {"chunk": 0, "answer": 0, "q": [0] * SHARD_ENGINES, "y": [0] * SHARD_ENGINES}
         # (margins: a rank's requests and chunks vary by ~sqrt between batches of one stream, so
-        # 1/32 covers them; the engines walk every padding topic, so a wide margin costs walk time)
-        c1 = (ls["chunk"] + ls["chunk"] // 32 + 4096 + 15) // 16 * 16
-        c2 = ls["answer"] + ls["answer"] // 16 + 65536
+        # 1/128 + 2048 requests covers them; the engines walk every padding topic, so a wide
+        # margin costs walk time, and a step over it only costs its classic redo)
+        c1 = (ls["chunk"] + ls["chunk"] // 64 + 4096 + 15) // 16 * 16
+        c2 = ls["answer"] + ls["answer"] // 32 + 16384
         c1, c2 = self._allreduce_max([max(c1, old["chunk"]), max(c2, old["answer"])])
-        q = [0 if self.engines[e] is None else max(old["q"][e], x + x // 32 + 1024) for e, x in enumerate(ls["q"])]
-        y = [0 if self.engines[e] is None else max(old["y"][e], x + x // 32 + 65536) for e, x in enumerate(ls["y"])]
+        q = [0 if self.engines[e] is None else max(old["q"][e], x + x // 128 + 2048) for e, x in enumerate(ls["q"])]
+        y = [0 if self.engines[e] is None else max(old["y"][e], x + x // 64 + 65536) for e, x in enumerate(ls["y"])]
         self._fixed = {"chunk": c1, "answer": c2, "q": q, "y": y}
 
     def _step_gen_fixed(self, topics: Tuple[torch.Tensor, torch.Tensor], flag_addr: int):
