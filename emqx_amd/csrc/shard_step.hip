@@ -900,29 +900,44 @@ __host__ __device__ inline void recv_table(const uint64_t* chunk, uint32_t G, co
   flagw[0] = f;
 }
 
-__global__ __launch_bounds__(64) void shard_recv_table_kernel(ShardTab chunks, uint32_t G, SlotCaps cap, uint32_t rel,
-                                                              ShardTab* __restrict__ t, uint64_t* __restrict__ pad,
-                                                              uint32_t* __restrict__ flagw) {
-  if (threadIdx.x == 0) recv_table(chunks.chunk, G, cap, rel != 0, t, pad, flagw);
-}
-
-__global__ __launch_bounds__(256) void shard_unpack_fixed_kernel(const ShardTab* __restrict__ tab, SlotOffsets dst_off,
-                                                                 SlotBytes dst_bytes, const uint32_t* __restrict__ flagw) {
-  if (flagw[0]) return;
-  unpack_part(*tab, dst_off, dst_bytes, blockIdx.y, blockIdx.z, static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
-              static_cast<uint64_t>(gridDim.x) * blockDim.x);
-}
-
-// grid (x, slot): slot e's offsets from its request count to its capacity = pad[e].
+// Slot e's offsets from its request count to its capacity = pad[e] (the recv kernel's padding blocks).
 __host__ __device__ inline void pad_slot(const ShardTab& tab, uint32_t G, const SlotOffsets& dst_off, const SlotCaps& cap,
                                          const uint64_t* pad, uint32_t e, uint64_t tid, uint64_t stride) {
   for (uint64_t k = tab.q0[e][G] + tid; k <= cap.q[e]; k += stride) dst_off.p[e][k] = pad[e];
 }
 
-__global__ __launch_bounds__(256) void shard_pad_kernel(const ShardTab* __restrict__ tab, uint32_t G, SlotOffsets dst_off,
-                                                        SlotCaps cap, const uint64_t* __restrict__ pad) {
-  pad_slot(*tab, G, dst_off, cap, pad, blockIdx.y, static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
-           static_cast<uint64_t>(gridDim.x) * blockDim.x);
+// The fixed form's recv in ONE launch (the table, the unpack and the padding were three, each a
+// few microseconds of latency on the path to the walk): every block builds the recv table from
+// the chunk headers in LDS (the same table in each; block (0, 0, 0) publishes it and the
+// padding offsets for the later kernels), then grid (x, source or G = padding, slot) does its
+// part.
+__global__ __launch_bounds__(256) void shard_recv_fixed_kernel(ShardTab chunks, uint32_t G, SlotCaps cap, uint32_t rel,
+                                                               SlotOffsets dst_off, SlotBytes dst_bytes,
+                                                               ShardTab* __restrict__ t_out, uint64_t* __restrict__ pad_out,
+                                                               uint32_t* __restrict__ flagw) {
+  __shared__ ShardTab t;
+  __shared__ uint64_t pad[kE];
+  __shared__ uint32_t f[1];
+  if (threadIdx.x == 0) {
+    f[0] = flagw[0];
+    recv_table(chunks.chunk, G, cap, rel != 0, &t, pad, f);
+  }
+  __syncthreads();
+  const bool first = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  if (first) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&t);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(t_out);
+    for (uint32_t w = threadIdx.x; w < sizeof(ShardTab) / 4; w += blockDim.x) dst[w] = src[w];
+    if (threadIdx.x < kE) pad_out[threadIdx.x] = pad[threadIdx.x];
+    if (threadIdx.x == 0) flagw[0] = f[0];
+  }
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  if (blockIdx.y == G) {
+    pad_slot(t, G, dst_off, cap, pad, blockIdx.z, tid, stride);
+  } else if (!f[0]) {
+    unpack_part(t, dst_off, dst_bytes, blockIdx.y, blockIdx.z, tid, stride);
+  }
 }
 
 // ---- answer -----------------------------------------------------------------------------
@@ -1032,18 +1047,21 @@ __host__ __device__ inline void answer_plan(const EngineCsrs& cs, const ShardTab
   flagw[0] = f;
 }
 
-__global__ __launch_bounds__(64) void shard_answer_plan_kernel(EngineCsrs cs, const ShardTab* __restrict__ tab,
-                                                               uint32_t self, uint32_t G, uint64_t fixed,
-                                                               uint32_t* __restrict__ flagw) {
-  if (threadIdx.x == 0) answer_plan(cs, *tab, self, G, fixed, flagw);
-}
-
+// The plan and the chunks in one launch: every block makes the (deterministic) plan itself,
+// block (0, 0) publishes the flag.
 __global__ __launch_bounds__(256) void shard_answer_fixed_kernel(EngineCsrs cs, const ShardTab* __restrict__ tab,
                                                                  uint32_t self, uint32_t* __restrict__ out,
-                                                                 uint64_t fixed, const uint32_t* __restrict__ flagw) {
+                                                                 uint64_t fixed, uint32_t* __restrict__ flagw) {
+  __shared__ uint32_t f[1];
+  if (threadIdx.x == 0) {
+    f[0] = flagw[0];
+    answer_plan(cs, *tab, self, gridDim.y, fixed, f);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) flagw[0] = f[0];
   answer_source(cs, *tab, self, out, nullptr, blockIdx.y, gridDim.y,
                 static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x, static_cast<uint64_t>(gridDim.x) * blockDim.x,
-                false, fixed, flagw[0]);
+                false, fixed, f[0]);
 }
 
 // ---- merge ------------------------------------------------------------------------------
@@ -1765,13 +1783,10 @@ int emqx_shard_step_recv_fixed(emqx_shard_step* st, const uint8_t* const* d_chun
   }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
-  hipLaunchKernelGGL(shard_recv_table_kernel, dim3(1), dim3(64), 0, s, ch, G, cap, sb.rel, st->d_tab, st->d_pad,
-                     st->d_flagw);
   const uint64_t per = std::max<uint64_t>(qall, yall / 16) / (kE * G) + 1;
   const uint32_t x = grid_of(per, 256, std::max<uint32_t>(1, 1024 / G));
-  hipLaunchKernelGGL(shard_unpack_fixed_kernel, dim3(x, G, kE), dim3(256), 0, s, st->d_tab, so, sb, st->d_flagw);
-  hipLaunchKernelGGL(shard_pad_kernel, dim3(grid_of(qall / kE + 1, 256, 1024), kE), dim3(256), 0, s, st->d_tab, G, so,
-                     cap, st->d_pad);
+  hipLaunchKernelGGL(shard_recv_fixed_kernel, dim3(x, G + 1, kE), dim3(256), 0, s, ch, G, cap, sb.rel, so, sb, st->d_tab,
+                     st->d_pad, st->d_flagw);
   SS_TRY(hipGetLastError());
   return EMQX_OK;
 }
@@ -1803,8 +1818,6 @@ int emqx_shard_step_answer_fixed(emqx_shard_step* st, const uint64_t* const* d_o
   }
   const hipStream_t s = static_cast<hipStream_t>(stream);
   SS_TRY(hipSetDevice(st->device));
-  hipLaunchKernelGGL(shard_answer_plan_kernel, dim3(1), dim3(64), 0, s, cs, st->d_tab, self_rank, G, chunk_words,
-                     st->d_flagw);
   const uint32_t x = grid_of(8 * st->fixed_q / G + 1, 256, std::max<uint32_t>(1, 1024 / G));  // ~8 ids a request
   hipLaunchKernelGGL(shard_answer_fixed_kernel, dim3(x, G), dim3(256), 0, s, cs, st->d_tab, self_rank, d_answer,
                      chunk_words, st->d_flagw);

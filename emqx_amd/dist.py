@@ -261,6 +261,11 @@ def fixed_steps() -> bool:
     return os.environ.get("EMQX_SHARD_FIXED", "1") != "0"
 
 
+def step_priority() -> bool:
+    """Fixed-form steps: the step's kernels on a high-priority stream (env ``EMQX_SHARD_PRIO``)."""
+    return os.environ.get("EMQX_SHARD_PRIO", "0") == "1"
+
+
 def stream_depth() -> int:
     """Steps in flight in ``ShardedMatcher.match_stream`` (env ``EMQX_SHARD_DEPTH``)."""
     return int(os.environ.get("EMQX_SHARD_DEPTH", "3"))
@@ -488,6 +493,8 @@ class _Lane:
         self.bufs = {}
         self.stream = None
         self.stream_b = None
+        self.stream_hi = None  # (fixed form with step_priority(): the step kernels' stream
+        self.stream_e = None   #  and the first engine's)
 
 
 class ShardedMatcher:
@@ -806,15 +813,24 @@ class ShardedMatcher:
         else:
             faddr = flags.data_ptr()
         lanes = [self._lane_n(i) for i in range(D)]
+        prio = cuda and step_priority()
         if cuda:
             for ln in lanes:
                 if ln.stream is None:
                     ln.stream = torch.cuda.Stream(device=self.device)
+                if prio and ln.stream_hi is None:
+                    # the step's own kernels on a high-priority stream, the engines on the lane's
+                    # normal ones: a send gets CUs as the other lanes' walks drain
+                    ln.stream_hi = torch.cuda.Stream(device=self.device, priority=-1)
+                    ln.stream_e = torch.cuda.Stream(device=self.device)
                 ln.stream.wait_stream(caller)
+                if prio:
+                    ln.stream_hi.wait_stream(caller)
         try:
             for k in range(first, K):
                 self._lane = lanes[k % D]
-                ctx = torch.cuda.stream(self._lane.stream) if cuda else contextlib.nullcontext()
+                ctx = (torch.cuda.stream(self._lane.stream_hi if prio else self._lane.stream) if cuda
+                       else contextlib.nullcontext())
                 with ctx:
                     gen = self._step_gen_fixed(batches[k], faddr + 8 * k)
                     try:
@@ -828,6 +844,8 @@ class ShardedMatcher:
         if cuda:
             for ln in lanes:
                 caller.wait_stream(ln.stream)
+                if prio:
+                    caller.wait_stream(ln.stream_hi)
             caller.synchronize()
         ends = torch.stack([res[k][0][-1] for k in range(first, K)]).cpu().tolist() if K > first else []
         fl = flags.tolist()
@@ -1087,6 +1105,8 @@ class ShardedMatcher:
             ri = self._buf(f"ids{e}", max(self._caps[e], 1 << 16), torch.int32)
             room += ri.numel()
             es = cur if not used or not self._cuda else self._stream_b[len(used) - 1]
+            if self._cuda and self._lane.stream_e is not None and cur is not None and cur == self._lane.stream_hi:
+                es = self._lane.stream_e if not used else self._stream_b[len(used) - 1]
             if es is not cur:
                 es.wait_stream(cur)
             used.append(es)
