@@ -862,10 +862,11 @@ struct SlotCaps {
 // body): per source its slot counts and bytes, prefixes over sources; a flagged chunk, or a slot
 // over its capacity, flags the step and empties every slot batch.  pad[e]: slot e's offset after
 // its last request (the engines' padding topics are empty topics there).
-__host__ __device__ inline void recv_table(const uint64_t* chunk, uint32_t G, const SlotCaps& cap, bool rel, ShardTab* t,
-                                           uint64_t* pad, uint32_t* flagw) {
+// (hdr[r]: where chunk r's header words are read — the chunk itself, or a copy in LDS)
+__host__ __device__ inline void recv_table(const uint64_t* chunk, const uint64_t* hdr, uint32_t G, const SlotCaps& cap,
+                                           bool rel, ShardTab* t, uint64_t* pad, uint32_t* flagw) {
   uint32_t f = flagw[0];
-  for (uint32_t r = 0; r < G; ++r) f |= reinterpret_cast<const uint32_t*>(chunk[r])[3];
+  for (uint32_t r = 0; r < G; ++r) f |= reinterpret_cast<const uint32_t*>(hdr[r])[3];
   for (int pass = 0; pass < 2; ++pass) {
     const bool empty = f != 0;
     uint64_t words = 0;
@@ -874,7 +875,7 @@ __host__ __device__ inline void recv_table(const uint64_t* chunk, uint32_t G, co
       t->y0[e][0] = 0;
     }
     for (uint32_t r = 0; r < G; ++r) {
-      const uint32_t* h = reinterpret_cast<const uint32_t*>(chunk[r]);
+      const uint32_t* h = reinterpret_cast<const uint32_t*>(hdr[r]);
       t->chunk[r] = chunk[r];
       uint64_t nall = 0;
       for (uint32_t e = 0; e < kE; ++e) {
@@ -918,9 +919,18 @@ __global__ __launch_bounds__(256) void shard_recv_fixed_kernel(ShardTab chunks, 
   __shared__ ShardTab t;
   __shared__ uint64_t pad[kE];
   __shared__ uint32_t f[1];
+  __shared__ uint4 hw[kMaxWorld][2];  // every chunk's header, loaded in parallel
+  __shared__ uint64_t hp[kMaxWorld];
+  if (threadIdx.x < G) {
+    const uint4* h = reinterpret_cast<const uint4*>(chunks.chunk[threadIdx.x]);
+    hw[threadIdx.x][0] = h[0];
+    hw[threadIdx.x][1] = h[1];
+    hp[threadIdx.x] = reinterpret_cast<uint64_t>(&hw[threadIdx.x][0]);
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     f[0] = flagw[0];
-    recv_table(chunks.chunk, G, cap, rel != 0, &t, pad, f);
+    recv_table(chunks.chunk, hp, G, cap, rel != 0, &t, pad, f);
   }
   __syncthreads();
   const bool first = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
@@ -1052,13 +1062,28 @@ __host__ __device__ inline void answer_plan(const EngineCsrs& cs, const ShardTab
 __global__ __launch_bounds__(256) void shard_answer_fixed_kernel(EngineCsrs cs, const ShardTab* __restrict__ tab,
                                                                  uint32_t self, uint32_t* __restrict__ out,
                                                                  uint64_t fixed, uint32_t* __restrict__ flagw) {
+  // (answer_plan with its G x kE terms computed by as many threads)
   __shared__ uint32_t f[1];
-  if (threadIdx.x == 0) {
-    f[0] = flagw[0];
-    answer_plan(cs, *tab, self, gridDim.y, fixed, f);
-  }
+  __shared__ unsigned long long a_n[kMaxWorld], a_i[kMaxWorld];
+  const uint32_t G = gridDim.y, j = threadIdx.x;
+  if (j < G) a_n[j] = a_i[j] = 0;
+  if (j == 0) f[0] = flagw[0];
   __syncthreads();
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) flagw[0] = f[0];
+  if (j < G * kE) {
+    const uint32_t sj = j / kE, e = j - kE * sj;
+    const uint32_t q0 = tab->q0[e][sj], nq = tab->q0[e][sj + 1] - q0;
+    if (nq) {
+      atomicAdd(&a_n[sj], static_cast<unsigned long long>(nq));
+      atomicAdd(&a_i[sj], static_cast<unsigned long long>(cs.off[e][q0 + nq] - cs.off[e][q0]));
+    }
+  }
+  if (j < kE && cs.sum[j] && cs.sum[j][0]) atomicOr(&f[0], 4u);
+  __syncthreads();
+  if (j == 0 && !f[0])
+    for (uint32_t sj = 0; sj < G; ++sj)
+      if (kHW + a_n[sj] + (sj == self ? 0 : a_i[sj]) > fixed) f[0] |= 8u;
+  __syncthreads();
+  if (blockIdx.x == 0 && blockIdx.y == 0 && j == 0) flagw[0] = f[0];
   answer_source(cs, *tab, self, out, nullptr, blockIdx.y, gridDim.y,
                 static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x, static_cast<uint64_t>(gridDim.x) * blockDim.x,
                 false, fixed, f[0]);
@@ -1178,7 +1203,15 @@ __host__ __device__ inline void merge_plan(const uint64_t* chunk, uint32_t G, ui
 
 __global__ __launch_bounds__(64) void shard_merge_plan_kernel(ShardTab t, uint32_t G, uint32_t* __restrict__ flagw,
                                                               uint32_t* __restrict__ out) {
-  if (threadIdx.x == 0) merge_plan(t.chunk, G, flagw, out);
+  __shared__ uint32_t f[1];  // (merge_plan, the chunks' words read by G threads at once)
+  if (threadIdx.x == 0) f[0] = flagw[0];
+  __syncthreads();
+  if (threadIdx.x < G) atomicOr(&f[0], reinterpret_cast<const uint32_t*>(t.chunk[threadIdx.x])[7]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    flagw[0] = f[0];
+    if (out) out[0] = f[0];
+  }
 }
 
 // c ids from src to dst by the 4 lanes `sub` of a quad: 16-B moves (4 ids a lane, any 4-B
@@ -1774,7 +1807,7 @@ int emqx_shard_step_recv_fixed(emqx_shard_step* st, const uint8_t* const* d_chun
   st->fixed_q = qall;
   st->have_recv = true;
   if (st->host) {
-    recv_table(ch.chunk, G, cap, rel, st->d_tab, st->d_pad, st->d_flagw);
+    recv_table(ch.chunk, ch.chunk, G, cap, rel, st->d_tab, st->d_pad, st->d_flagw);
     if (!st->d_flagw[0])
       for (uint32_t r = 0; r < G; ++r)
         for (uint32_t e = 0; e < kE; ++e) unpack_part(*st->d_tab, so, sb, r, e, 0, 1);
