@@ -567,6 +567,10 @@ class ShardedMatcher:
         self._lanes = [_Lane(_DeviceStep(self.device, self.world, self.plan))]
         self._cuda = self.device.type == "cuda"
         self._lane = self._lanes[0]
+        if self._cuda:  # the lanes' streams made together, so they land on different hardware queues
+            for i in range(max(2, stream_depth())):
+                ln = self._lane_n(i)
+                ln.stream = torch.cuda.Stream(device=self.device)
         self._caps = [1 << 20] * SHARD_ENGINES
         self._fixed = None        # the fixed form's agreed capacities (_learn_fixed)
         self._last_sizes = None   # the last classic step's sizes (what _learn_fixed learns from)
@@ -577,6 +581,16 @@ class ShardedMatcher:
     _bufs = property(lambda self: self._lane.bufs)
     _stream = property(lambda self: self._lane.stream, lambda self, v: setattr(self._lane, "stream", v))
     _stream_b = property(lambda self: self._lane.stream_b, lambda self, v: setattr(self._lane, "stream_b", v))
+
+    def _engine_stream(self, i: int):
+        """The lane's stream for its (i + 2)-th engine call of a step, made when first needed: a
+        process has few hardware queues (GPU_MAX_HW_QUEUES, 4 here) and streams share them in
+        creation order, so an unused stream can put two lanes on one queue."""
+        if self._stream_b is None:
+            self._stream_b = []
+        while len(self._stream_b) <= i:
+            self._stream_b.append(torch.cuda.Stream(device=self.device))
+        return self._stream_b[i]
 
     def _lane_n(self, k: int) -> "_Lane":
         while len(self._lanes) <= k:
@@ -967,8 +981,6 @@ class ShardedMatcher:
         outs = []
         hsumm, dsumm = self._pinned("summary", 8 * E)  # written by each engine call that runs
 
-        if self._stream_b is None and self._cuda:
-            self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E - 1)]
         used = []
         for e, (eb, eo, ne) in enumerate(batches):
             ro = self._buf(f"off{e}", ne + 1, torch.int64)
@@ -977,7 +989,7 @@ class ShardedMatcher:
                 continue
             cap_e = max(self._caps[e], 1 << 16)
             ri = self._buf(f"ids{e}", cap_e, torch.int32)
-            es = cur if not used or not self._cuda else self._stream_b[len(used) - 1]
+            es = cur if not used or not self._cuda else self._engine_stream(len(used) - 1)
             if es is not cur:
                 es.wait_stream(cur)
             used.append(es)
@@ -1093,8 +1105,6 @@ class ShardedMatcher:
                                                 (ctypes.c_uint64 * E)(*capy), None if in_place else PA(qbytes),
                                                 PA(qoff), S), "emqx_shard_step_recv_fixed")
         hsumm, dsumm = self._pinned("summary", 8 * E)
-        if self._stream_b is None and self._cuda:
-            self._stream_b = [torch.cuda.Stream(device=dev) for _ in range(E - 1)]
         cur = torch.cuda.current_stream(dev) if self._cuda else None
         outs, used, room = [], [], 0
         for e in range(E):
@@ -1104,9 +1114,9 @@ class ShardedMatcher:
                 continue
             ri = self._buf(f"ids{e}", max(self._caps[e], 1 << 16), torch.int32)
             room += ri.numel()
-            es = cur if not used or not self._cuda else self._stream_b[len(used) - 1]
+            es = cur if not used or not self._cuda else self._engine_stream(len(used) - 1)
             if self._cuda and self._lane.stream_e is not None and cur is not None and cur == self._lane.stream_hi:
-                es = self._lane.stream_e if not used else self._stream_b[len(used) - 1]
+                es = self._lane.stream_e if not used else self._engine_stream(len(used) - 1)
             if es is not cur:
                 es.wait_stream(cur)
             used.append(es)
