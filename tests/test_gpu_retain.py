@@ -173,7 +173,7 @@ def test_large_table_device_api(mod):
     filters = W.unpack(wl.filters)
     dev = torch.device("cuda:0")
     fb, fo = pack(filters)
-    d_fb = torch.from_numpy(fb).to(dev)
+    d_fb = torch.from_numpy(np.array(fb)).to(dev)
     d_fo = torch.from_numpy(fo.view(np.int64)).to(dev)
     d_off = torch.empty(len(filters) + 1, dtype=torch.int64, device=dev)
     cap = 4_000_000
