@@ -635,11 +635,20 @@ class ShardedMatcher:
         self._caps = caps
         return d_off, d_ids[:m]
 
-    def match_all(self, topics: Tuple[torch.Tensor, torch.Tensor]):
+    def match_all(self, topics: Tuple[torch.Tensor, torch.Tensor], fixed: Optional[bool] = None):
         """Every rank matches its own batch against the sharded table and gets its own CSR
         (offsets int64 (n+1,), ids int32) in batch order — the layout's weak-scaling use, one
-        publishing node per rank.  Two host synchronisations per call: the split sizes of the
-        requests and of the answers (the all-to-all split lists)."""
+        publishing node per rank.  The classic form has two host synchronisations per call (the
+        split sizes of the requests and of the answers); once the fixed form's capacities are
+        learnt (a ``match_stream`` call), the call runs the fixed form (``fixed``, default
+        ``fixed_steps()``): one host read at its end, the flag and the CSR's length."""
+        if fixed is None:
+            fixed = self._fixed is not None and fixed_steps()
+        if fixed:
+            return self._match_stream_fixed([topics], 1)[0]
+        return self._match_all_classic(topics)
+
+    def _match_all_classic(self, topics: Tuple[torch.Tensor, torch.Tensor]):
         if not self._cuda:
             return self._match_all_device(topics)
         if self._step is not None:
@@ -812,7 +821,7 @@ class ShardedMatcher:
         first = 0
         if self._fixed is None:
             assert exchange is None, "the fixed form over a replayed exchange needs learnt capacities"
-            res[0] = self.match_all(batches[0])
+            res[0] = self._match_all_classic(batches[0])
             self._learn_fixed()
             first = 1
         cuda = self._cuda
@@ -868,7 +877,7 @@ class ShardedMatcher:
             if fl[k]:
                 if exchange is not None:
                     raise RuntimeError(f"fixed-capacity step {k} flagged ({fl[k]}) over a replayed exchange")
-                res[k] = self.match_all(batches[k])
+                res[k] = self._match_all_classic(batches[k])
                 self._learn_fixed()
                 self.last_fixed_redo += 1
             else:

@@ -245,7 +245,11 @@ def _worker_fixed(rank, world, port, q, p_space):
         res = sm.match_stream([T(b) for b in batches], fixed=True, depth=2)
         redo = sm.last_fixed_redo
         res2 = sm.match_stream([T(b) for b in batches[:3]], fixed=True, depth=3)  # learnt: no redo
-        q.put((rank, batches, [(o.numpy(), i.numpy()) for o, i in res + res2], redo, sm.last_fixed_redo))
+        redo2 = sm.last_fixed_redo
+        # match_all once the capacities are learnt: the fixed form, then the classic one
+        res3 = [sm.match_all(T(part)), sm.match_all(T(part), fixed=False)]
+        q.put((rank, batches + batches[:3] + [part, part], [(o.numpy(), i.numpy()) for o, i in res + res2 + res3],
+               redo, redo2))
     finally:
         dist.destroy_process_group()
 
@@ -273,7 +277,8 @@ def test_sharded_fixed_capacity_steps(world, p_space):
     o.add_packed(*_batches()[0])
     for rank, batches, res, redo, redo2 in got:
         assert redo == 1 and redo2 == 0, (rank, redo, redo2)
-        for k, (b, (off, ids)) in enumerate(zip(batches + batches[:3], res)):
+        assert len(res) == len(batches)
+        for k, (b, (off, ids)) in enumerate(zip(batches, res)):
             tb, to = b
             off_o, ids_o, _ = o.match_csr(tb if len(tb) else np.zeros(1, np.uint8), to.astype(np.uint64), mode=0,
                                           threads=2)
