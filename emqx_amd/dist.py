@@ -251,11 +251,6 @@ MAX_PIECE_PM = 250  # a key is split when its filters exceed a quarter of a rank
 P_SPACE = {"auto": 0, "sharded": 1, "replicated": 2}  # emqx_shard_plan p_space (include/emqx_match.h)
 
 
-# (measurement probe, not a protocol: at world 1 skip the size syncs once a lane's pinned words
-# hold a step's sizes — valid only while every step repeats the same batch, as bench.py's does)
-_NOSYNC_PROBE = os.environ.get("EMQX_SHARD_NOSYNC_PROBE") == "1"
-
-
 def fixed_steps() -> bool:
     """``ShardedMatcher.match_stream`` in the fixed-capacity form (env ``EMQX_SHARD_FIXED``, 1)."""
     return os.environ.get("EMQX_SHARD_FIXED", "1") != "0"
@@ -897,7 +892,7 @@ class ShardedMatcher:
         of every source's chunk for this rank (``_exchange_chunks``)."""
         if op[0] == "local_sizes":  # world 1: words the device wrote into mapped pinned memory
             _, words, W = op
-            if self._cuda and not (_NOSYNC_PROBE and int(words[0])):
+            if self._cuda:
                 torch.cuda.current_stream(self.device).synchronize()
             lst = words[: W * self.world].tolist()
             return lst, lst, words
