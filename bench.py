@@ -544,6 +544,7 @@ def sharded_bench(args, rank, world, dev):
             "steps_in_flight": stream_depth(),
             "fixed_capacity_steps": fixed_steps(),
             "fixed_steps_redone": int(getattr(sm, "last_fixed_redo", 0)),
+            "fixed_host_enqueue_ms_per_step": round(float(getattr(sm, "last_fixed_enqueue_ms", 0.0)), 4),
             **({"rehearsal": "ranks sharing GPUs over gloo (EMQX_BENCH_REHEARSE): not a measurement"}
                if rehearse else {}),
         }), flush=True)
@@ -673,10 +674,11 @@ def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
         ids_checked += int(off_g[-1])
     # each rank alone with two steps in flight (ShardedMatcher.match_stream; the other ranks'
     # side replayed from the step above), its last result checked too
-    stream_ms, bad_stream, stream_ms_classic = [], [], []
+    stream_ms, bad_stream, stream_ms_classic, enq_ms = [], [], [], []
     for r in range(G):
         ms, rs = ew.rank_stream(r, batches[r], args.steps, fixed=fx)
         stream_ms.append(ms)
+        enq_ms.append(getattr(ew.matchers[r], "last_fixed_enqueue_ms", 0.0))
         if fx:  # (the classic form on the same ranks, for an A/B on one box)
             stream_ms_classic.append(ew.rank_stream(r, batches[r], args.steps, fixed=False)[0])
         bad_stream.append(int(C.csr_mismatches(rs[-1][0].cpu().numpy().astype(np.uint64),
@@ -732,7 +734,8 @@ def _emulated_world(args, dev, wl, batches, refs, rep_ms, golden, G):
         "rank_step_ms_wall": [round(float(x), 4) for x in per["wall"].sum(axis=1)],
         "rank_step_ms_gpu": [round(float(x), 4) for x in per["gpu"].sum(axis=1)],
         "rank_stream_ms": [round(float(x), 4) for x in stream_ms],
-        **({"rank_stream_ms_classic_form": [round(float(x), 4) for x in stream_ms_classic]} if fx else {}),
+        **({"rank_stream_ms_classic_form": [round(float(x), 4) for x in stream_ms_classic],
+            "rank_stream_host_enqueue_ms": [round(float(x), 4) for x in enq_ms]} if fx else {}),
         "phases": list(phases),
         "exchange_bytes_out": {"requests": bo[0].tolist(), "answers": bo[1].tolist()},
         "exchange_max_pair_bytes": {"requests": int(bo[0].max()), "answers": int(bo[1].max())},

@@ -570,6 +570,7 @@ class ShardedMatcher:
         self._fixed = None        # the fixed form's agreed capacities (_learn_fixed)
         self._last_sizes = None   # the last classic step's sizes (what _learn_fixed learns from)
         self.last_fixed_redo = 0
+        self.last_fixed_enqueue_ms = 0.0
 
     # (the step's resources are the current lane's)
     _step = property(lambda self: self._lane.step)
@@ -844,6 +845,7 @@ class ShardedMatcher:
                 ln.stream.wait_stream(caller)
                 if prio:
                     ln.stream_hi.wait_stream(caller)
+        t_enq = time.perf_counter()
         try:
             for k in range(first, K):
                 self._lane = lanes[k % D]
@@ -859,6 +861,9 @@ class ShardedMatcher:
                         res[k] = stop.value
         finally:
             self._lane = self._lanes[0]
+        # (host time to enqueue the steps, per step: the stream is host-bound when it nears the
+        # step time)
+        self.last_fixed_enqueue_ms = 1e3 * (time.perf_counter() - t_enq) / max(K - first, 1)
         if cuda:
             for ln in lanes:
                 caller.wait_stream(ln.stream)
@@ -1241,6 +1246,12 @@ class EmulatedWorld:
         collectives themselves left to the projection.  Returns (ms per step, the results)."""
         m = self.matchers[r]
         rec = self.recorded[r]
+        if m._cuda:
+            # fresh lane streams, made together: in one process the G ranks' streams share the
+            # process's few hardware queues, and a rank of a real run has them to itself
+            torch.cuda.synchronize(self.device)
+            for i in range(max(2, stream_depth())):
+                m._lane_n(i).stream = torch.cuda.Stream(device=self.device)
 
         def replay(op):
             if op[0] == "fixed":
