@@ -567,6 +567,7 @@ class ShardedMatcher:
                 ln = self._lane_n(i)
                 ln.stream = torch.cuda.Stream(device=self.device)
         self._caps = [1 << 20] * SHARD_ENGINES
+        self._ids_floor = 1 << 16  # (an engine call's id buffer is never smaller; tests lower it)
         self._fixed = None        # the fixed form's agreed capacities (_learn_fixed)
         self._last_sizes = None   # the last classic step's sizes (what _learn_fixed learns from)
         self.last_fixed_redo = 0
@@ -996,7 +997,7 @@ class ShardedMatcher:
             if not ne:  # (a slot no source asked: the answer kernel reads nothing of it)
                 outs.append([ro, self._buf(f"ids{e}", 16, torch.int32)])
                 continue
-            cap_e = max(self._caps[e], 1 << 16)
+            cap_e = max(self._caps[e], self._ids_floor)
             ri = self._buf(f"ids{e}", cap_e, torch.int32)
             es = cur if not used or not self._cuda else self._engine_stream(len(used) - 1)
             if es is not cur:
@@ -1123,7 +1124,7 @@ class ShardedMatcher:
             if not capq[e]:
                 outs.append([ro, self._buf(f"ids{e}", 16, torch.int32)])
                 continue
-            ri = self._buf(f"ids{e}", max(self._caps[e], 1 << 16), torch.int32)
+            ri = self._buf(f"ids{e}", max(self._caps[e], self._ids_floor), torch.int32)
             room += ri.numel()
             es = cur if not used or not self._cuda else self._engine_stream(len(used) - 1)
             if self._cuda and self._lane.stream_e is not None and cur is not None and cur == self._lane.stream_hi:

@@ -248,8 +248,16 @@ def _worker_fixed(rank, world, port, q, p_space):
         redo2 = sm.last_fixed_redo
         # match_all once the capacities are learnt: the fixed form, then the classic one
         res3 = [sm.match_all(T(part)), sm.match_all(T(part), fixed=False)]
-        q.put((rank, batches + batches[:3] + [part, part], [(o.numpy(), i.numpy()) for o, i in res + res2 + res3],
-               redo, redo2))
+        # engine id buffers cut to a 1 K floor: a slot over it flags its step (the engine's
+        # summary), which is redone classically on every rank
+        sm._caps, sm._ids_floor = [1, 1, 1], 1024
+        for ln in sm._lanes:
+            for e in range(3):
+                ln.bufs.pop(f"ids{e}", None)
+        res4 = sm.match_stream([T(big), T(big)], fixed=True)
+        redo4 = sm.last_fixed_redo
+        q.put((rank, batches + batches[:3] + [part, part, big, big],
+               [(o.numpy(), i.numpy()) for o, i in res + res2 + res3 + res4], redo, redo2, redo4))
     finally:
         dist.destroy_process_group()
 
@@ -275,8 +283,9 @@ def test_sharded_fixed_capacity_steps(world, p_space):
         assert p.exitcode == 0
     o = C.CppOracle(True)
     o.add_packed(*_batches()[0])
-    for rank, batches, res, redo, redo2 in got:
+    for rank, batches, res, redo, redo2, redo4 in got:
         assert redo == 1 and redo2 == 0, (rank, redo, redo2)
+        assert redo4 == 2, redo4  # (2 x 3 K topics: ~36 K ids, over every rank's 1 K buffers)
         assert len(res) == len(batches)
         for k, (b, (off, ids)) in enumerate(zip(batches, res)):
             tb, to = b
